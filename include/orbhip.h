@@ -1,0 +1,155 @@
+/*
+ * orbhip.h — C-ABI of liborbhip.so, the MI355X (gfx950) ORB front-end + BA back-end.
+ *
+ * Drop-in boundary for the hot path of EricPedley/ORB_SLAM3_ROS2.
+ * Each entry point names the reference interface it replaces:
+ *   R:src/imu_mono_realsense.cpp:337   System::TrackMonocular -> Frame(mono) -> Frame::ExtractORB
+ *   U:src/Frame.cc::Frame::ExtractORB  calls ORBextractor::operator()(im, Mat(), kps, desc, {0,1000})
+ *   U:src/ORBextractor.cc::ORBextractor::operator()          -> orbhip_extract / orbhip_extract_batch_device
+ *   U:src/ORBextractor.cc::ORBextractor::ORBextractor(...)   -> orbhip_create (orbhip_orb_params)
+ *   U:src/ORBmatcher.cc::ORBmatcher::DescriptorDistance      -> orbhip_descriptor_distance
+ *   U:src/ORBmatcher.cc  best/second + ratio + TH_LOW + rotation histogram -> orbhip_match_bf*
+ *   U:src/Optimizer.cc::Optimizer::LocalBundleAdjustment / BundleAdjustment -> orbhip_ba_solve
+ *
+ * Conventions:
+ *  - Plain pointers and sizes only; no C++ types, no exceptions cross this ABI.
+ *  - The caller owns every host buffer. A context owns its device memory, pinned
+ *    staging and one HIP stream. One context per calling thread; a context is not
+ *    re-entrant; distinct contexts are safe to use concurrently.
+ *  - Status: 0 ok, < 0 error (orbhip_status).
+ *  - Parity contract: keypoints/descriptors bit-exact with the CPU restatement in
+ *    oracle/ (the reference's own path cannot be built here: SURVEY.md §0, §8c).
+ */
+#ifndef ORBHIP_H
+#define ORBHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORBHIP_ABI_VERSION 1
+
+typedef enum {
+    ORBHIP_OK = 0,
+    ORBHIP_ERR_ARG = -1,          /* bad argument (null pointer, bad size, ...) */
+    ORBHIP_ERR_CAPACITY = -2,     /* caller buffer too small; *n_out holds the required count */
+    ORBHIP_ERR_DEVICE = -3,       /* HIP runtime failure / no device */
+    ORBHIP_ERR_NOT_PD = -4,       /* reduced camera system not positive definite */
+    ORBHIP_ERR_UNSUPPORTED = -5,  /* configuration outside the supported envelope */
+    ORBHIP_ERR_EMPTY = -6         /* empty image: ORBextractor::operator() returns -1 */
+} orbhip_status;
+
+typedef struct orbhip_ctx orbhip_ctx;
+
+/* ORBextractor ctor arguments; YAML keys ORBextractor.{nFeatures, scaleFactor, nLevels,
+ * iniThFAST, minThFAST} (R:config/Monocular/MilkV.yaml:42-55). */
+typedef struct {
+    int32_t n_features;
+    float scale_factor;
+    int32_t n_levels;
+    int32_t ini_th_fast;
+    int32_t min_th_fast;
+} orbhip_orb_params;
+
+/* cv::KeyPoint as produced by ORBextractor (class_id is always -1 there, omitted). */
+typedef struct {
+    float x, y;       /* level-0 pixel coordinates (pt *= mvScaleFactor[octave]) */
+    float size;       /* (int)(31 * mvScaleFactor[octave]) */
+    float angle;      /* IC_Angle, degrees [0, 360) */
+    float response;   /* FAST score */
+    int32_t octave;   /* pyramid level */
+} orbhip_kp;
+
+/* ---- context ------------------------------------------------------------------- */
+int orbhip_abi_version(void);
+/* device: HIP ordinal. params may be NULL -> ORB_SLAM3 defaults (1000, 1.2, 8, 20, 7). */
+int orbhip_create(orbhip_ctx** out, int device, const orbhip_orb_params* params);
+int orbhip_destroy(orbhip_ctx* ctx);
+/* Per-level tables of the ORBextractor ctor: mvScaleFactor, mnFeaturesPerLevel. */
+int orbhip_level_info(orbhip_ctx* ctx, int w, int h, int32_t* level_w, int32_t* level_h,
+                      int32_t* n_feat, float* scale);
+/* Max keypoints one frame can yield for this context at size w x h (cap for outputs). */
+int orbhip_max_keypoints(orbhip_ctx* ctx, int w, int h);
+
+/* ---- ORB extraction --------------------------------------------------------------
+ * orbhip_extract: ORBextractor::operator()(img, Mat(), kps, desc, {lap0, lap1}).
+ * Host image (CV_8UC1, row stride in bytes), host outputs (cap entries). *mono_index
+ * receives the return value of operator() (kps with lap0 <= x <= lap1 fill the array
+ * from the end, the rest from the front). Empty image -> ORBHIP_ERR_EMPTY (reference: -1). */
+int orbhip_extract(orbhip_ctx* ctx, const uint8_t* img, int w, int h, int stride, int lap0, int lap1,
+                   orbhip_kp* kps, uint8_t* desc32, int cap, int* n_out, int* mono_index);
+
+/* Batched, fully device-resident form (torch-ROCm ingest, benchmarks). d_imgs: B frames,
+ * frame f at d_imgs + f*frame_stride, rows `stride` bytes apart. Outputs per frame f:
+ * d_kps[f*cap ...], d_desc[(f*cap ...)*32], d_n[f], d_mono[f]. Asynchronous on `stream`
+ * (hipStream_t, NULL = the context's stream). */
+int orbhip_extract_batch_device(orbhip_ctx* ctx, const uint8_t* d_imgs, int B, int w, int h, int stride,
+                                int64_t frame_stride, int lap0, int lap1, orbhip_kp* d_kps, uint8_t* d_desc,
+                                int cap, int32_t* d_n, int32_t* d_mono, void* stream);
+
+/* ---- Hamming matching ------------------------------------------------------------- */
+/* ORBmatcher::DescriptorDistance (host helper, popcount of xor over 32 bytes). */
+int orbhip_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* Brute-force top-2 over the whole train set (order-free: no greedy vnMatches21 pass),
+ * accept best <= th_low && (float)best < ratio*(float)second, then (if check_orientation)
+ * the rotation-histogram filter (HISTO_LENGTH 30, ComputeThreeMaxima). best/second start at
+ * 256 (SearchByBoW). match[i] = train index or -1. Host buffers. Returns #matches >= 0. */
+int orbhip_match_bf(orbhip_ctx* ctx, const uint8_t* q_desc, const float* q_angle, int nq,
+                    const uint8_t* t_desc, const float* t_angle, int nt, int th_low, float ratio,
+                    int check_orientation, int32_t* match, int32_t* best_d, int32_t* second_d);
+
+/* Device form over extractor outputs: pairs (frame p, frame p+1) for p in [0, B-1), each
+ * frame's kps/desc at f*cap as written by orbhip_extract_batch_device. Outputs at p*cap;
+ * d_nmatch[p] = #matches. Asynchronous. */
+int orbhip_match_pairs_device(orbhip_ctx* ctx, const orbhip_kp* d_kps, const uint8_t* d_desc,
+                              const int32_t* d_n, int B, int cap, int th_low, float ratio,
+                              int check_orientation, int32_t* d_match, int32_t* d_best,
+                              int32_t* d_second, int32_t* d_nmatch, void* stream);
+
+/* ---- bundle adjustment ------------------------------------------------------------
+ * Optimizer::LocalBundleAdjustment / BundleAdjustment problem (SoA, host memory).
+ * Poses are Tcw = (q, t): q = unit quaternion (x, y, z, w), t translation, float, as
+ * Sophus::SE3f stores them. Edges are EdgeSE3ProjectXYZ mono observations. */
+typedef struct {
+    int32_t n_poses, n_points, n_edges;
+    const float* pose_q;        /* n_poses x 4 (x,y,z,w) */
+    const float* pose_t;        /* n_poses x 3 */
+    const uint8_t* pose_fixed;  /* n_poses (1 = fixed vertex) */
+    const float* points;        /* n_points x 3 (world) */
+    const int32_t* edge_pose;   /* n_edges */
+    const int32_t* edge_point;  /* n_edges */
+    const float* edge_uv;       /* n_edges x 2 (undistorted keypoint) */
+    const int32_t* edge_octave; /* n_edges */
+    const float* inv_sigma2;    /* per octave: information = I * invSigma2[octave] */
+    int32_t n_octaves;
+    float fx, fy, cx, cy;       /* Pinhole mvParameters (float) */
+    float huber_delta;          /* sqrt(5.991) for LBA; <= 0 disables the robust kernel */
+    int32_t iterations;         /* optimize(n): 10 for LBA */
+    int32_t early_stop;         /* vendored-g2o chi2 stall stop, 0 = off */
+} orbhip_ba_problem;
+
+typedef struct {
+    float* pose_q;              /* n_poses x 4 out (fixed poses copied through) */
+    float* pose_t;              /* n_poses x 3 out */
+    float* points;              /* n_points x 3 out */
+    float* edge_chi2;           /* n_edges out: e->chi2() after optimize (for the 5.991 erase) */
+    uint8_t* edge_depth_ok;     /* n_edges out: e->isDepthPositive() */
+    double initial_chi2;        /* activeRobustChi2 before iteration 0 */
+    double final_chi2;          /* activeRobustChi2 of the accepted state */
+    int32_t iterations_done;    /* SparseOptimizer::optimize return value */
+    int32_t lm_trials;          /* total Levenberg trials */
+} orbhip_ba_result;
+
+/* stop_flag: polled between LM iterations/trials (LocalMapping mbAbortBA -> g2o
+ * setForceStopFlag). May be NULL. */
+int orbhip_ba_solve(orbhip_ctx* ctx, const orbhip_ba_problem* prob, orbhip_ba_result* res,
+                    const volatile int* stop_flag);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ORBHIP_H */

@@ -1,0 +1,139 @@
+"""ctypes view of oracle/build/liborb_oracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this.
+The product (orb_slam3_ros2_amd / liborbhip.so) never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "liborb_oracle.so")
+_lib = None
+
+_u8p = np.ctypeslib.ndpointer(dtype=np.uint8, flags="C_CONTIGUOUS")
+_f32p = np.ctypeslib.ndpointer(dtype=np.float32, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(dtype=np.int32, flags="C_CONTIGUOUS")
+_f64p = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+
+
+def build() -> None:
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        c_int, c_float, c_double = ctypes.c_int, ctypes.c_float, ctypes.c_double
+        L.orc_level_info.argtypes = [c_int, c_int, c_int, c_float, c_int, _i32p, _i32p, _i32p, _f32p, _i32p]
+        L.orc_extract.argtypes = [_u8p, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_int, c_int, c_int,
+                                  _f32p, _u8p, c_int, ctypes.POINTER(c_int)]
+        L.orc_pyramid.argtypes = [_u8p, c_int, c_int, c_int, c_float, c_int, _u8p]
+        L.orc_extract_levels.argtypes = [_u8p, c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_int,
+                                         _f32p, c_int, _f32p, c_int, _i32p]
+        L.orc_blur.argtypes = [_u8p, c_int, c_int, _u8p]
+        L.orc_gaussian_kernel.argtypes = [c_int, c_double, _i32p]
+        L.orc_fast_atan2.argtypes = [c_float, c_float]
+        L.orc_fast_atan2.restype = c_float
+        L.orc_corner_score.argtypes = [_u8p, c_int]
+        L.orc_fast_window.argtypes = [_u8p, c_int, c_int, c_int, c_int, _f32p, c_int]
+        L.orc_descriptor_distance.argtypes = [_u8p, _u8p]
+        L.orc_match_bf.argtypes = [_u8p, _f32p, c_int, _u8p, _f32p, c_int, c_int, c_float, c_int,
+                                   _i32p, _i32p, _i32p]
+        L.orc_glibc_sincosf_range.argtypes = [ctypes.c_uint32, ctypes.c_uint32, _f32p, _f32p]
+        _lib = L
+    return _lib
+
+
+def level_info(w, h, nfeatures=1000, scale_factor=1.2, nlevels=8):
+    lw = np.zeros(nlevels, np.int32); lh = np.zeros(nlevels, np.int32)
+    feats = np.zeros(nlevels, np.int32); scales = np.zeros(nlevels, np.float32)
+    umax = np.zeros(16, np.int32)
+    lib().orc_level_info(w, h, nfeatures, scale_factor, nlevels, lw, lh, feats, scales, umax)
+    return dict(w=lw, h=lh, feats=feats, scales=scales, umax=umax)
+
+
+def extract(img: np.ndarray, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7,
+            lap=(0, 1000), cap=None):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    cap = cap or max(4 * nfeatures, 64)
+    kps = np.zeros((cap, 6), np.float32)
+    desc = np.zeros((cap, 32), np.uint8)
+    n = ctypes.c_int(0)
+    mono = lib().orc_extract(img, w, h, w, nfeatures, scale_factor, nlevels, ini_th, min_th, lap[0], lap[1],
+                             kps, desc, cap, ctypes.byref(n))
+    return mono, kps[: n.value].copy(), desc[: n.value].copy()
+
+
+def pyramid(img: np.ndarray, scale_factor=1.2, nlevels=8):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    info = level_info(w, h, 1000, scale_factor, nlevels)
+    total = int(np.sum(info["w"].astype(np.int64) * info["h"]))
+    out = np.zeros(total, np.uint8)
+    rc = lib().orc_pyramid(img, w, h, w, scale_factor, nlevels, out)
+    assert rc == 0
+    levels, off = [], 0
+    for l in range(nlevels):
+        n = int(info["w"][l]) * int(info["h"][l])
+        levels.append(out[off: off + n].reshape(int(info["h"][l]), int(info["w"][l])))
+        off += n
+    return levels
+
+
+def extract_levels(img, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th=20, min_th=7, cap=400000):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    h, w = img.shape
+    cand = np.zeros((cap, 6), np.float32)
+    kept = np.zeros((max(8 * nfeatures, 64), 6), np.float32)
+    counts = np.zeros(2 * nlevels, np.int32)
+    rc = lib().orc_extract_levels(img, w, h, w, nfeatures, scale_factor, nlevels, ini_th, min_th,
+                                  cand, cap, kept, kept.shape[0], counts)
+    assert rc == 0, rc
+    c, k, oc, ok = [], [], 0, 0
+    for l in range(nlevels):
+        nc, nk = int(counts[2 * l]), int(counts[2 * l + 1])
+        c.append(cand[oc: oc + nc].copy()); k.append(kept[ok: ok + nk].copy())
+        oc += nc; ok += nk
+    return c, k
+
+
+def blur(img):
+    img = np.ascontiguousarray(img, dtype=np.uint8)
+    out = np.zeros_like(img)
+    lib().orc_blur(img, img.shape[1], img.shape[0], out)
+    return out
+
+
+def gaussian_kernel(n=7, sigma=2.0):
+    out = np.zeros(n, np.int32)
+    lib().orc_gaussian_kernel(n, sigma, out)
+    return out
+
+
+def fast_atan2(y, x):
+    return lib().orc_fast_atan2(float(y), float(x))
+
+
+def match_bf(q, qa, t, ta, th_low=50, ratio=0.9, check_orientation=True):
+    q = np.ascontiguousarray(q, np.uint8); t = np.ascontiguousarray(t, np.uint8)
+    qa = np.ascontiguousarray(qa, np.float32); ta = np.ascontiguousarray(ta, np.float32)
+    nq, nt = q.shape[0], t.shape[0]
+    m = np.zeros(nq, np.int32); b = np.zeros(nq, np.int32); s = np.zeros(nq, np.int32)
+    n = lib().orc_match_bf(q, qa, nq, t, ta, nt, th_low, ratio, int(check_orientation), m, b, s)
+    return n, m, b, s
+
+
+def glibc_sincosf_range(lo_bits: int, hi_bits: int):
+    n = hi_bits - lo_bits + 1
+    c = np.empty(n, np.float32); s = np.empty(n, np.float32)
+    lib().orc_glibc_sincosf_range(lo_bits, hi_bits, c, s)
+    return c, s

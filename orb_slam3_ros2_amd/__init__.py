@@ -1,0 +1,23 @@
+"""orb_slam3_ros2_amd — MI355X-native ORB front-end + bundle-adjustment back-end.
+
+Host-side mirror of the reference's hot-path interfaces over the C-ABI of
+``liborbhip.so`` (include/orbhip.h):
+
+  ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)      U:src/ORBextractor.cc
+      __call__(image, mask, vLappingArea) -> (monoIndex, keypoints, descriptors)
+  ORBmatcher.DescriptorDistance(a, b)                                       U:src/ORBmatcher.cc
+  ORBmatcher(nnratio, checkOri).match_bf(...)                               (a12 rule)
+  Optimizer.LocalBundleAdjustment(problem)                                  U:src/Optimizer.cc
+
+The HIP library is the only compute path: importing this package on a box without the
+built extension, or calling it without a GPU, raises — there is no CPU fallback.
+"""
+from __future__ import annotations
+
+from ._lib import OrbHipError, lib, library_path  # noqa: F401
+from .extractor import KeyPoint, ORBextractor  # noqa: F401
+from .matcher import ORBmatcher  # noqa: F401
+from .optimizer import BAProblem, BAResult, Optimizer  # noqa: F401
+
+__all__ = ["ORBextractor", "KeyPoint", "ORBmatcher", "Optimizer", "BAProblem", "BAResult", "OrbHipError",
+           "lib", "library_path"]

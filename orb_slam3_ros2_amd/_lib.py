@@ -1,0 +1,138 @@
+"""ctypes binding of liborbhip.so (include/orbhip.h). Fails loudly when the library is absent."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_NAME = "liborbhip.so"
+_lib = None
+
+
+class OrbHipError(RuntimeError):
+    CODES = {-1: "ORBHIP_ERR_ARG", -2: "ORBHIP_ERR_CAPACITY", -3: "ORBHIP_ERR_DEVICE", -4: "ORBHIP_ERR_NOT_PD",
+             -5: "ORBHIP_ERR_UNSUPPORTED", -6: "ORBHIP_ERR_EMPTY"}
+
+    def __init__(self, code: int, what: str = ""):
+        self.code = code
+        super().__init__(f"{what}: {self.CODES.get(code, code)}")
+
+
+def library_path() -> str:
+    return os.path.join(_HERE, _LIB_NAME)
+
+
+class KP(ctypes.Structure):
+    _fields_ = [("x", ctypes.c_float), ("y", ctypes.c_float), ("size", ctypes.c_float), ("angle", ctypes.c_float),
+                ("response", ctypes.c_float), ("octave", ctypes.c_int32)]
+
+
+KP_DTYPE = np.dtype([("x", np.float32), ("y", np.float32), ("size", np.float32), ("angle", np.float32),
+                     ("response", np.float32), ("octave", np.int32)])
+
+
+class OrbParams(ctypes.Structure):
+    _fields_ = [("n_features", ctypes.c_int32), ("scale_factor", ctypes.c_float), ("n_levels", ctypes.c_int32),
+                ("ini_th_fast", ctypes.c_int32), ("min_th_fast", ctypes.c_int32)]
+
+
+class BAProblemC(ctypes.Structure):
+    _fields_ = [("n_poses", ctypes.c_int32), ("n_points", ctypes.c_int32), ("n_edges", ctypes.c_int32),
+                ("pose_q", ctypes.c_void_p), ("pose_t", ctypes.c_void_p), ("pose_fixed", ctypes.c_void_p),
+                ("points", ctypes.c_void_p), ("edge_pose", ctypes.c_void_p), ("edge_point", ctypes.c_void_p),
+                ("edge_uv", ctypes.c_void_p), ("edge_octave", ctypes.c_void_p), ("inv_sigma2", ctypes.c_void_p),
+                ("n_octaves", ctypes.c_int32), ("fx", ctypes.c_float), ("fy", ctypes.c_float),
+                ("cx", ctypes.c_float), ("cy", ctypes.c_float), ("huber_delta", ctypes.c_float),
+                ("iterations", ctypes.c_int32), ("early_stop", ctypes.c_int32)]
+
+
+class BAResultC(ctypes.Structure):
+    _fields_ = [("pose_q", ctypes.c_void_p), ("pose_t", ctypes.c_void_p), ("points", ctypes.c_void_p),
+                ("edge_chi2", ctypes.c_void_p), ("edge_depth_ok", ctypes.c_void_p),
+                ("initial_chi2", ctypes.c_double), ("final_chi2", ctypes.c_double),
+                ("iterations_done", ctypes.c_int32), ("lm_trials", ctypes.c_int32)]
+
+
+# every symbol include/orbhip.h declares (tests check the export table against this list)
+EXPORTED = ["orbhip_abi_version", "orbhip_create", "orbhip_destroy", "orbhip_level_info", "orbhip_max_keypoints",
+            "orbhip_extract", "orbhip_extract_batch_device", "orbhip_descriptor_distance", "orbhip_match_bf",
+            "orbhip_match_pairs_device", "orbhip_ba_solve"]
+
+
+def lib():
+    """Load liborbhip.so (raises if it was not built — there is no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = library_path()
+    # torch-ROCm bundles its own libamdhip64.so.7 (same SONAME as /opt/rocm's). Load it first
+    # so liborbhip binds to the SAME HIP runtime: device pointers from torch tensors are then
+    # valid in our kernels, and torch does not fail to initialise a second runtime.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    if not os.path.exists(path):
+        raise OrbHipError(-3, f"{path} missing — run __graft_entry__.build()")
+    L = ctypes.CDLL(path)
+    vp, i32, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+    L.orbhip_abi_version.restype = i32
+    L.orbhip_create.argtypes = [ctypes.POINTER(vp), i32, ctypes.POINTER(OrbParams)]
+    L.orbhip_destroy.argtypes = [vp]
+    L.orbhip_level_info.argtypes = [vp, i32, i32, vp, vp, vp, vp]
+    L.orbhip_max_keypoints.argtypes = [vp, i32, i32]
+    L.orbhip_extract.argtypes = [vp, vp, i32, i32, i32, i32, i32, vp, vp, i32, ctypes.POINTER(i32),
+                                 ctypes.POINTER(i32)]
+    L.orbhip_extract_batch_device.argtypes = [vp, vp, i32, i32, i32, i32, ctypes.c_int64, i32, i32, vp, vp, i32,
+                                              vp, vp, vp]
+    L.orbhip_descriptor_distance.argtypes = [vp, vp]
+    L.orbhip_match_bf.argtypes = [vp, vp, vp, i32, vp, vp, i32, i32, f32, i32, vp, vp, vp]
+    L.orbhip_match_pairs_device.argtypes = [vp, vp, vp, vp, i32, i32, i32, f32, i32, vp, vp, vp, vp, vp]
+    L.orbhip_ba_solve.argtypes = [vp, ctypes.POINTER(BAProblemC), ctypes.POINTER(BAResultC), vp]
+    L.orbhip_test_sincosf.argtypes = [vp, vp, vp, ctypes.c_int64]
+    L.orbhip_test_sincosf_sweep.argtypes = [ctypes.c_uint32, ctypes.c_uint32, vp, vp]
+    L.orbhip_test_sincosf_sweep.restype = ctypes.c_int64
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise OrbHipError(rc, what)
+    return rc
+
+
+def ptr(a) -> int | None:
+    """Data pointer of a numpy array or a torch tensor (host or device)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()
+
+
+class Context:
+    """Owns one orbhip_ctx (device memory, pinned staging, one HIP stream)."""
+
+    def __init__(self, device: int = 0, n_features=1000, scale_factor=1.2, n_levels=8, ini_th_fast=20,
+                 min_th_fast=7):
+        self._h = ctypes.c_void_p()
+        prm = OrbParams(int(n_features), float(scale_factor), int(n_levels), int(ini_th_fast), int(min_th_fast))
+        check(lib().orbhip_create(ctypes.byref(self._h), int(device), ctypes.byref(prm)), "orbhip_create")
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            lib().orbhip_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

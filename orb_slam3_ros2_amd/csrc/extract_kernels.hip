@@ -1,0 +1,709 @@
+// gfx950 kernels of the ORB front-end (ORBextractor::operator() restated for CDNA4).
+//
+//   k_resize      a3/a4  one pyramid level from the previous one (cascade), bit-exact
+//                        OpenCV 8U INTER_LINEAR fixed point (H exact, V SIMD/scalar split)
+//   k_fast_cells  a5/a6  per 35-px cell: FAST-9 strength map in LDS, window-local strict
+//                        3x3 NMS at iniThFAST, fallback to minThFAST, row-major compaction
+//   k_octree      a7     DistributeOctTree emulated with arrays: one 1024-thread workgroup
+//                        per (frame, level); list order / creation-serial tie-break exact
+//   k_desc        a8/a9  per keypoint (one wave): IC_Angle + glibc sinf/cosf + rBRIEF on
+//                        the 7x7 bit-exact Gaussian sampled from an LDS patch; final
+//                        operator() ordering (lapping area from the end)
+//
+// Everything is integer or reproduces host float rounding exactly (-ffp-contract=off).
+#include <hip/hip_runtime.h>
+
+#include "../../include/orbhip.h"
+#include "../../include/orbhip_pattern.h"
+#include "orbhip_device.h"
+#include "orbhip_kernels.h"
+#include "orbhip_plan.h"
+
+namespace orbhip {
+
+static __constant__ signed char kPattern[256 * 4] = ORBHIP_BIT_PATTERN_31_INIT;
+
+// ---------------------------------------------------------------------------
+// image addressing: level 0 is the caller's frame, levels >= 1 live in the pyramid block
+// ---------------------------------------------------------------------------
+struct ImgRef {
+    const uint8_t* p;
+    int pitch;
+};
+
+__device__ __forceinline__ ImgRef level_img(const ExtractPlan* __restrict__ P, const FrameBufs& fb, int f, int l) {
+    if (l == 0) return ImgRef{fb.in + (int64_t)f * fb.in_fstride, fb.in_stride};
+    return ImgRef{fb.pyr + (int64_t)f * P->pyr_bytes + P->lv[l].pyr_off, P->lv[l].pitch};
+}
+
+// ---------------------------------------------------------------------------
+// k_resize: OCV resizeGeneric_ 8UC1 INTER_LINEAR; block (64,4), 4 output px per thread
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_resize(const ExtractPlan* __restrict__ P, FrameBufs fb, int l,
+                                                const int* __restrict__ xofs, const int* __restrict__ xalpha,
+                                                const int* __restrict__ yofs, const int* __restrict__ ybeta) {
+    const LevelGeom& D = P->lv[l];
+    const LevelGeom& S = P->lv[l - 1];
+    const int f = blockIdx.z;
+    const int dy = blockIdx.y * 4 + threadIdx.y;
+    const int dx0 = (blockIdx.x * 64 + threadIdx.x) * 4;
+    if (dy >= D.h || dx0 >= D.w) return;
+    ImgRef src = level_img(P, fb, f, l - 1);
+    uint8_t* dst = fb.pyr + (int64_t)f * P->pyr_bytes + D.pyr_off + (int64_t)dy * D.pitch;
+    const int sy = yofs[D.ytab_off + dy];
+    const int r0 = sy < 0 ? 0 : (sy < S.h ? sy : S.h - 1);
+    const int r1 = sy + 1 < 0 ? 0 : (sy + 1 < S.h ? sy + 1 : S.h - 1);
+    const uint8_t* S0 = src.p + (int64_t)r0 * src.pitch;
+    const uint8_t* S1 = src.p + (int64_t)r1 * src.pitch;
+    const int bb = ybeta[D.ytab_off + dy];
+    const int b0 = (int)(short)(bb & 0xFFFF), b1 = (int)(short)(bb >> 16);
+    uint32_t packed = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int dx = dx0 + k;
+        if (dx >= D.w) break;
+        const int sx = xofs[D.xtab_off + dx];
+        int h0, h1;
+        if (dx < D.xmax) {
+            const int aa = xalpha[D.xtab_off + dx];
+            const int a0 = (int)(short)(aa & 0xFFFF), a1 = (int)(short)(aa >> 16);
+            h0 = S0[sx] * a0 + S0[sx + 1] * a1;
+            h1 = S1[sx] * a0 + S1[sx + 1] * a1;
+        } else {
+            h0 = S0[sx] * 2048;
+            h1 = S1[sx] * 2048;
+        }
+        int v;
+        if (dx < D.vend) {   // VResizeLinearVec_32s8u lanes (128-bit baseline)
+            int s0 = min(max(h0 >> 4, -32768), 32767);
+            int s1 = min(max(h1 >> 4, -32768), 32767);
+            int t = ((s0 * b0) >> 16) + ((s1 * b1) >> 16);
+            t = min(max(t, -32768), 32767);
+            v = (t + 2) >> 2;
+        } else {             // FixedPtCast<int, uchar, 22>
+            v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+        }
+        v = v < 0 ? 0 : (v > 255 ? 255 : v);
+        packed |= (uint32_t)v << (8 * k);
+    }
+    if (dx0 + 3 < D.w) {
+        *(uint32_t*)(dst + dx0) = packed;
+    } else {
+        for (int k = 0; k < 4 && dx0 + k < D.w; k++) dst[dx0 + k] = (uint8_t)(packed >> (8 * k));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_fast_cells: one workgroup per (cell, frame)
+// FAST strength m = max(A, B, 0): A = max over the 16 9-arcs of min(v - p), B the same for
+// (p - v). cornerScore<16> == m - 1 for every detected corner and a pixel is a corner at
+// threshold t iff m > t (derivation in DESIGN.md), so one map serves both thresholds.
+// ---------------------------------------------------------------------------
+constexpr int kWinMax = 80;
+
+__device__ __forceinline__ int fast_strength(const uint8_t* c, int w) {
+    const int o[16] = {3 * w,      3 * w + 1,  2 * w + 2,  w + 3,      3,      -w + 3, -2 * w + 2, -3 * w + 1,
+                       -3 * w,     -3 * w - 1, -2 * w - 2, -w - 3,     -3,     w - 3,  2 * w - 2,  3 * w - 1};
+    const int v = c[0];
+    int d[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) d[k] = v - (int)c[o[k]];
+    int mn2[16], mx2[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        mn2[k] = min(d[k], d[(k + 1) & 15]);
+        mx2[k] = max(d[k], d[(k + 1) & 15]);
+    }
+    int A = -256, Bm = 256;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        int mn8 = min(min(mn2[k], mn2[(k + 2) & 15]), min(mn2[(k + 4) & 15], mn2[(k + 6) & 15]));
+        int mx8 = max(max(mx2[k], mx2[(k + 2) & 15]), max(mx2[(k + 4) & 15], mx2[(k + 6) & 15]));
+        A = max(A, min(mn8, d[(k + 8) & 15]));
+        Bm = min(Bm, max(mx8, d[(k + 8) & 15]));
+    }
+    int m = max(A, -Bm);
+    return m < 0 ? 0 : m;
+}
+
+__global__ __launch_bounds__(256) void k_fast_cells(const ExtractPlan* __restrict__ P,
+                                                    const CellGeom* __restrict__ cells, FrameBufs fb,
+                                                    uint32_t* __restrict__ cand, int* __restrict__ cand_cnt) {
+    __shared__ uint8_t win[kWinMax * kWinMax];
+    __shared__ uint8_t mv[kWinMax * kWinMax];
+    __shared__ int scr[8];
+    const CellGeom cg = cells[blockIdx.x];
+    const int f = blockIdx.y;
+    const int tid = threadIdx.x;
+    const int wc = cg.wc, hc = cg.hc;
+    int* cnt_out = cand_cnt + (int64_t)f * P->n_cells_total + blockIdx.x;
+    if (wc <= 6 || hc <= 6) {
+        if (tid == 0) *cnt_out = 0;
+        return;
+    }
+    const LevelGeom& G = P->lv[cg.level];
+    ImgRef im = level_img(P, fb, f, cg.level);
+    const uint8_t* base = im.p + (int64_t)cg.y0 * im.pitch + cg.x0;
+    for (int i = tid; i < wc * hc; i += 256) {
+        const int yy = i / wc, xx = i - yy * wc;
+        win[i] = base[(int64_t)yy * im.pitch + xx];
+    }
+    __syncthreads();
+    const int dc = wc - 6, dr = hc - 6, np = dc * dr;
+    for (int p = tid; p < np; p += 256) {
+        const int py = p / dc, px = p - py * dc;
+        mv[p] = (uint8_t)fast_strength(&win[(py + 3) * wc + px + 3], wc);
+    }
+    __syncthreads();
+    auto keep = [&](int p, int t) -> bool {
+        const int m = mv[p];
+        if (m <= t) return false;
+        const int s = m - 1;
+        const int py = p / dc, px = p - py * dc;
+#pragma unroll
+        for (int yy = -1; yy <= 1; yy++)
+#pragma unroll
+            for (int xx = -1; xx <= 1; xx++) {
+                if (yy == 0 && xx == 0) continue;
+                const int qx = px + xx, qy = py + yy;
+                if (qx < 0 || qy < 0 || qx >= dc || qy >= dr) continue;
+                const int mq = mv[qy * dc + qx];
+                const int sq = mq > t ? mq - 1 : 0;
+                if (!(s > sq)) return false;
+            }
+        return true;
+    };
+    int t = P->ini_th;
+    int c = 0;
+    for (int p = tid; p < np; p += 256) c += keep(p, t) ? 1 : 0;
+    c = wave_sum_i32(c);
+    if (lane_id() == 0) scr[tid >> 6] = c;
+    __syncthreads();
+    const int total_ini = scr[0] + scr[1] + scr[2] + scr[3];
+    __syncthreads();
+    if (total_ini == 0) t = P->min_th;
+    uint32_t* out = cand + (int64_t)f * P->n_slots_total + cg.slot_off;
+    int written = 0;
+    for (int r0 = 0; r0 < np; r0 += 256) {
+        const int p = r0 + tid;
+        const int k = (p < np && keep(p, t)) ? 1 : 0;
+        int tot;
+        const int pos = block_excl_scan(k, scr, &tot);
+        if (k) {
+            const int py = p / dc, px = p - py * dc;
+            const int x = cg.x0 + 3 + px - G.min_bx, y = cg.y0 + 3 + py - G.min_by;
+            out[written + pos] = pack_cand(x, y, (int)mv[p] - 1);
+        }
+        written += tot;
+    }
+    if (tid == 0) *cnt_out = written;
+}
+
+// ---------------------------------------------------------------------------
+// k_octree: DistributeOctTree for one (level, frame). All node state in LDS; keys in LDS
+// when they fit (flat pointers otherwise point at per-level global scratch).
+// ---------------------------------------------------------------------------
+struct OctLds {
+    int* ctl;          // 64 ints: scan scratch / control words
+    uint64_t* rectA; uint32_t* cntA; uint32_t* bestA; uint32_t* serA;
+    uint64_t* rectB; uint32_t* cntB; uint32_t* bestB; uint32_t* serB;
+    uint32_t* ccount;  // node_cap*4 child counts
+    uint32_t* cbest;   // node_cap*4 child best (score<<24 | 0xFFFFFF-key)
+    uint16_t* map4;    // node_cap*4 remap old node/quadrant -> new node
+    int* tA; int* tB; int* tC; int* tD;
+    uint64_t* skey;    // sort keys (sort_cap)
+    int* cellstart;    // max_cells_level + 1
+    uint32_t* keys;    // key_cap (LDS) or null
+    uint16_t* knode;
+};
+
+__device__ __forceinline__ uint64_t mk_rect(int x0, int y0, int x1, int y1) {
+    return (uint64_t)(uint16_t)x0 | ((uint64_t)(uint16_t)y0 << 16) | ((uint64_t)(uint16_t)x1 << 32) |
+           ((uint64_t)(uint16_t)y1 << 48);
+}
+__device__ __forceinline__ int rx0(uint64_t r) { return (int)(r & 0xFFFF); }
+__device__ __forceinline__ int ry0(uint64_t r) { return (int)((r >> 16) & 0xFFFF); }
+__device__ __forceinline__ int rx1(uint64_t r) { return (int)((r >> 32) & 0xFFFF); }
+__device__ __forceinline__ int ry1(uint64_t r) { return (int)(r >> 48); }
+
+// ExtractorNode::DivideNode split: halfX = ceil((UR.x-UL.x)/2.f), halfY = ceil((BR.y-UL.y)/2.f)
+__device__ __forceinline__ void split_of(uint64_t r, int* sx, int* sy) {
+    *sx = rx0(r) + (int)ceilf((float)(rx1(r) - rx0(r)) / 2);
+    *sy = ry0(r) + (int)ceilf((float)(ry1(r) - ry0(r)) / 2);
+}
+__device__ __forceinline__ int quad_of(uint64_t r, int x, int y) {
+    int sx, sy;
+    split_of(r, &sx, &sy);
+    return (x >= sx ? 1 : 0) + (y >= sy ? 2 : 0);
+}
+__device__ __forceinline__ uint64_t child_rect(uint64_t r, int q) {
+    int sx, sy;
+    split_of(r, &sx, &sy);
+    const int x0 = rx0(r), y0 = ry0(r), x1 = rx1(r), y1 = ry1(r);
+    switch (q) {
+        case 0: return mk_rect(x0, y0, sx, sy);
+        case 1: return mk_rect(sx, y0, x1, sy);
+        case 2: return mk_rect(x0, sy, sx, y1);
+        default: return mk_rect(sx, sy, x1, y1);
+    }
+}
+__device__ __forceinline__ uint32_t pack_best(int score, int k) { return ((uint32_t)score << 24) | (0xFFFFFFu - (uint32_t)k); }
+
+// In-place exclusive scan of arr[0..n) by the whole block; returns the total. arr in LDS.
+__device__ int block_scan_array(int* arr, int n, int* ctl) {
+    const int nt = blockDim.x, tid = threadIdx.x;
+    const int per = (n + nt - 1) / nt;
+    const int b = tid * per, e = min(b + per, n);
+    int s = 0;
+    for (int i = b; i < e; i++) s += arr[i];
+    int tot;
+    int off = block_excl_scan(s, ctl, &tot);
+    for (int i = b; i < e; i++) { int v = arr[i]; arr[i] = off; off += v; }
+    __syncthreads();
+    return tot;
+}
+
+// bitonic sort of skey[0..n) descending, n power of two
+__device__ void block_sort_desc(uint64_t* a, int n) {
+    for (int k = 2; k <= n; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < n; i += blockDim.x) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint64_t x = a[i], y = a[ixj];
+                    const bool desc = (i & k) == 0;
+                    if (desc ? (x < y) : (x > y)) { a[i] = y; a[ixj] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__ P, const CellGeom* __restrict__ cells,
+                                                 const uint32_t* __restrict__ cand, const int* __restrict__ cand_cnt,
+                                                 uint32_t* __restrict__ kscratch, uint16_t* __restrict__ nscratch,
+                                                 LevelKp* __restrict__ lvl_kp, int* __restrict__ lvl_cnt,
+                                                 int* __restrict__ lvl_nlap, OctreeCfg cfg, int* __restrict__ err) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int l = blockIdx.x, f = blockIdx.y;
+    const LevelGeom& G = P->lv[l];
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const int NC = cfg.node_cap;
+    // ---- carve LDS (every offset a multiple of 16 bytes) ----
+    OctLds S;
+    size_t off = 0;
+    auto carve = [&](size_t bytes) { void* p = smem + off; off += (bytes + 15) & ~size_t(15); return p; };
+    S.ctl = (int*)carve(64 * 4);
+    S.rectA = (uint64_t*)carve(NC * 8); S.cntA = (uint32_t*)carve(NC * 4);
+    S.bestA = (uint32_t*)carve(NC * 4); S.serA = (uint32_t*)carve(NC * 4);
+    S.rectB = (uint64_t*)carve(NC * 8); S.cntB = (uint32_t*)carve(NC * 4);
+    S.bestB = (uint32_t*)carve(NC * 4); S.serB = (uint32_t*)carve(NC * 4);
+    S.ccount = (uint32_t*)carve(NC * 16); S.cbest = (uint32_t*)carve(NC * 16);
+    S.map4 = (uint16_t*)carve(NC * 8);
+    S.tA = (int*)carve(NC * 4); S.tB = (int*)carve(NC * 4); S.tC = (int*)carve(NC * 4);
+    S.tD = (int*)carve(NC * 4);
+    S.skey = (uint64_t*)carve(cfg.sort_cap * 8);
+    S.cellstart = (int*)carve((P->max_cells_level + 1) * 4);
+    uint32_t* keysL = (uint32_t*)carve(cfg.key_cap * 4);
+    uint16_t* knodeL = (uint16_t*)carve(cfg.key_cap * 2);
+    int* ctl = S.ctl;
+
+    // ---- 1. candidate count per cell -> cell-major key order ----
+    const int ncell = G.n_cells;
+    const int* cc = cand_cnt + (int64_t)f * P->n_cells_total + G.cell_base;
+    for (int i = tid; i < ncell; i += nt) S.cellstart[i] = cc[i];
+    __syncthreads();
+    const int M = block_scan_array(S.cellstart, ncell, ctl);
+    const bool keys_in_lds = M <= cfg.key_cap;
+    uint32_t* keys = keys_in_lds ? keysL : kscratch + (int64_t)f * P->n_slots_total + G.slot_base;
+    uint16_t* knode = keys_in_lds ? knodeL : nscratch + (int64_t)f * P->n_slots_total + G.slot_base;
+    const uint32_t* cbase = cand + (int64_t)f * P->n_slots_total;
+    {
+        const int wid = tid >> 6, lane = tid & 63, nw = nt >> 6;
+        for (int c = wid; c < ncell; c += nw) {
+            const int n = cc[c], st = S.cellstart[c];
+            const uint32_t* src = cbase + cells[G.cell_base + c].slot_off;
+            for (int i = lane; i < n; i += 64) keys[st + i] = src[i];
+        }
+    }
+    // ---- 2. roots (nIni <= 64 enforced by the host) ----
+    const int nIni = G.n_ini;
+    for (int i = tid; i < nIni * 4; i += nt) { S.ccount[i] = 0; S.cbest[i] = 0; }
+    __syncthreads();
+    const float hX = G.hX;
+    for (int k = tid; k < M; k += nt) {
+        const uint32_t key = keys[k];
+        int r = (int)((float)cand_x(key) / hX);
+        r = r < 0 ? 0 : (r >= nIni ? nIni - 1 : r);
+        atomicAdd(&S.ccount[r], 1u);
+        atomicMax(&S.cbest[r], pack_best(cand_s(key), k));
+        knode[k] = (uint16_t)r;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int n = 0;
+        const int H = G.max_by - G.min_by;
+        for (int r = 0; r < nIni; r++) {
+            const uint64_t rr = mk_rect((int)(hX * (float)r), 0, (int)(hX * (float)(r + 1)), H);
+            S.rectB[r] = rr;   // OLD buffer = roots (remap source)
+            if (S.ccount[r] > 0) {
+                S.rectA[n] = rr; S.cntA[n] = S.ccount[r]; S.bestA[n] = S.cbest[r]; S.serA[n] = r;
+                S.map4[r * 4 + 0] = S.map4[r * 4 + 1] = S.map4[r * 4 + 2] = S.map4[r * 4 + 3] = (uint16_t)n;
+                n++;
+            }
+        }
+        ctl[40] = n;          // list size
+        ctl[41] = nIni;       // next serial
+        ctl[42] = 0;          // mode: 0 main, 1 final
+        ctl[43] = 0;          // finished
+    }
+    __syncthreads();
+    // CUR = A, OLD = B
+    uint64_t *rectC = S.rectA, *rectO = S.rectB;
+    uint32_t *cntC = S.cntA, *bestC = S.bestA, *serC = S.serA;
+    uint32_t *cntO = S.cntB, *bestO = S.bestB, *serO = S.serB;
+    const int N = G.n_feat;
+    for (int iter = 0;; iter++) {
+        const int n = ctl[40];
+        if (iter > 64 || n > NC) {   // runaway guard: never expected
+            if (tid == 0) atomicOr(err, 1);
+            break;
+        }
+        // ---- sweep: remap keys through map4 (OLD rect split), classify into CUR children ----
+        for (int i = tid; i < n * 4; i += nt) { S.ccount[i] = 0; S.cbest[i] = 0; }
+        __syncthreads();
+        for (int k = tid; k < M; k += nt) {
+            const uint32_t key = keys[k];
+            const int x = cand_x(key), y = cand_y(key);
+            const int o = knode[k];
+            const int nd = S.map4[o * 4 + quad_of(rectO[o], x, y)];
+            knode[k] = (uint16_t)nd;
+            if (cntC[nd] > 1) {
+                const int q = quad_of(rectC[nd], x, y);
+                atomicAdd(&S.ccount[nd * 4 + q], 1u);
+                atomicMax(&S.cbest[nd * 4 + q], pack_best(cand_s(key), k));
+            }
+        }
+        __syncthreads();
+        const int mode = ctl[42];
+        const int serial0 = ctl[41];
+        int newSize;
+        if (mode == 0) {
+            // ---- MAIN pass: divide every node with > 1 key ----
+            for (int p = tid; p < n; p += nt) {
+                int c = 0, e = 0;
+                const bool div = cntC[p] > 1;
+                if (div)
+                    for (int q = 0; q < 4; q++) { c += S.ccount[p * 4 + q] > 0; e += S.ccount[p * 4 + q] > 1; }
+                S.tA[p] = c; S.tB[p] = div ? 0 : 1; S.tC[p] = e;
+            }
+            __syncthreads();
+            const int T = block_scan_array(S.tA, n, ctl);
+            const int U = block_scan_array(S.tB, n, ctl);
+            const int nToExpand = block_scan_array(S.tC, n, ctl);
+            newSize = T + U;
+            for (int p = tid; p < n; p += nt) {
+                if (cntC[p] > 1) {
+                    int c = 0;
+                    for (int q = 0; q < 4; q++) c += S.ccount[p * 4 + q] > 0;
+                    const int cb = S.tA[p];                // children created before this parent
+                    const int base = T - cb - c;          // pushed to the front: later parents first
+                    int r = 0;
+                    for (int q = 0; q < 4; q++) {
+                        const uint32_t cq = S.ccount[p * 4 + q];
+                        if (cq == 0) continue;
+                        const int pos = base + (c - 1 - r);   // n4..n1 order inside the block
+                        rectO[pos] = child_rect(rectC[p], q);
+                        cntO[pos] = cq; bestO[pos] = S.cbest[p * 4 + q]; serO[pos] = serial0 + cb + r;
+                        S.map4[p * 4 + q] = (uint16_t)pos;
+                        r++;
+                    }
+                } else {
+                    const int pos = T + S.tB[p];
+                    rectO[pos] = rectC[p]; cntO[pos] = cntC[p]; bestO[pos] = bestC[p]; serO[pos] = serC[p];
+                    S.map4[p * 4 + 0] = S.map4[p * 4 + 1] = S.map4[p * 4 + 2] = S.map4[p * 4 + 3] = (uint16_t)pos;
+                }
+            }
+            if (tid == 0) {
+                ctl[41] = serial0 + T;
+                if (newSize >= N || newSize == n) ctl[43] = 1;
+                else if (newSize + nToExpand * 3 > N) ctl[42] = 1;
+            }
+        } else {
+            // ---- FINAL phase: divide largest (size, serial) first until >= N ----
+            for (int p = tid; p < n; p += nt) S.tA[p] = cntC[p] > 1 ? 1 : 0;
+            __syncthreads();
+            const int K = block_scan_array(S.tA, n, ctl);
+            int sc = 1;
+            while (sc < K) sc <<= 1;
+            for (int i = tid; i < sc; i += nt) S.skey[i] = 0;
+            __syncthreads();
+            for (int p = tid; p < n; p += nt)
+                if (cntC[p] > 1)
+                    S.skey[S.tA[p]] = ((uint64_t)cntC[p] << 40) | ((uint64_t)serC[p] << 16) | (uint64_t)p;
+            __syncthreads();
+            block_sort_desc(S.skey, sc);
+            if (tid == 0) ctl[44] = K - 1;   // jstar: last divided index in sorted order
+            for (int j = tid; j < K; j += nt) {
+                const int p = (int)(S.skey[j] & 0xFFFF);
+                int c = 0;
+                for (int q = 0; q < 4; q++) c += S.ccount[p * 4 + q] > 0;
+                S.tB[j] = c - 1;   // list growth when dividing it
+                S.tC[j] = c;
+            }
+            for (int p = tid; p < n; p += nt) S.tD[p] = 1;
+            __syncthreads();
+            block_scan_array(S.tB, K, ctl);
+            for (int j = tid; j < K; j += nt)
+                if (n + S.tB[j] + (S.tC[j] - 1) >= N) atomicMin(&ctl[44], j);
+            __syncthreads();
+            const int jstar = ctl[44];
+            for (int j = tid; j < K; j += nt) {
+                if (j > jstar) S.tC[j] = 0;
+                else S.tD[(int)(S.skey[j] & 0xFFFF)] = 0;
+            }
+            __syncthreads();
+            for (int j = tid; j < K; j += nt) S.tB[j] = S.tC[j];
+            for (int p = tid; p < n; p += nt) S.tA[p] = S.tD[p];
+            __syncthreads();
+            const int Ctot = block_scan_array(S.tB, K, ctl);   // children created before, in division order
+            block_scan_array(S.tA, n, ctl);                    // stayers before
+            newSize = Ctot + (n - (jstar + 1));
+            for (int j = tid; j <= jstar; j += nt) {
+                const int p = (int)(S.skey[j] & 0xFFFF);
+                const int c = S.tC[j];
+                const int cb = S.tB[j];
+                const int base = Ctot - cb - c;
+                int r = 0;
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t cq = S.ccount[p * 4 + q];
+                    if (cq == 0) continue;
+                    const int pos = base + (c - 1 - r);
+                    rectO[pos] = child_rect(rectC[p], q);
+                    cntO[pos] = cq; bestO[pos] = S.cbest[p * 4 + q]; serO[pos] = serial0 + cb + r;
+                    S.map4[p * 4 + q] = (uint16_t)pos;
+                    r++;
+                }
+            }
+            for (int p = tid; p < n; p += nt) {
+                if (S.tD[p]) {
+                    const int pos = Ctot + S.tA[p];
+                    rectO[pos] = rectC[p]; cntO[pos] = cntC[p]; bestO[pos] = bestC[p]; serO[pos] = serC[p];
+                    S.map4[p * 4 + 0] = S.map4[p * 4 + 1] = S.map4[p * 4 + 2] = S.map4[p * 4 + 3] = (uint16_t)pos;
+                }
+            }
+            if (tid == 0) {
+                ctl[41] = serial0 + Ctot;
+                if (newSize >= N || newSize == n) ctl[43] = 1;
+            }
+        }
+        __syncthreads();
+        if (tid == 0) ctl[40] = newSize;
+        __syncthreads();
+        // swap: NEXT (written into the O buffers) becomes CUR, CUR becomes OLD
+        { uint64_t* t = rectC; rectC = rectO; rectO = t; }
+        { uint32_t* t = cntC; cntC = cntO; cntO = t; }
+        { uint32_t* t = bestC; bestC = bestO; bestO = t; }
+        { uint32_t* t = serC; serC = serO; serO = t; }
+        if (ctl[43]) break;
+    }
+    // ---- output in list order: retained key per node, lapping flag and rank ----
+    const int n = ctl[40];
+    LevelKp* out = lvl_kp + (int64_t)f * P->kp_slots_total + G.kp_base;
+    const int ncap = min(n, G.kp_cap);
+    for (int p = tid; p < ncap; p += nt) {
+        const int k = (int)(0xFFFFFFu - (bestC[p] & 0xFFFFFFu));
+        const uint32_t key = keys[k];
+        const int x = cand_x(key) + G.min_bx, y = cand_y(key) + G.min_by;
+        const float xs = (l == 0) ? (float)x : (float)x * G.scale;
+        const int lap = (xs >= (float)cfg.lap0 && xs <= (float)cfg.lap1) ? 1 : 0;
+        S.tA[p] = lap; S.tB[p] = 1 - lap;
+        S.tC[p] = (x & 0xFFFF) | (y << 16);
+        S.skey[p] = (uint64_t)cand_s(key);
+    }
+    __syncthreads();
+    const int nlap = block_scan_array(S.tA, ncap, ctl);
+    block_scan_array(S.tB, ncap, ctl);
+    for (int p = tid; p < ncap; p += nt) {
+        const int xy = S.tC[p];
+        const int x = xy & 0xFFFF, y = xy >> 16;
+        const int lapflag = (p + 1 < ncap ? S.tA[p + 1] : nlap) - S.tA[p];
+        const int rank = lapflag ? S.tA[p] : S.tB[p];
+        LevelKp r;
+        r.x = (int16_t)x; r.y = (int16_t)y;
+        r.srl = (uint32_t)S.skey[p] | ((uint32_t)lapflag << 8) | ((uint32_t)rank << 9);
+        out[p] = r;
+    }
+    if (tid == 0) {
+        lvl_cnt[f * P->n_levels + l] = ncap;
+        lvl_nlap[f * P->n_levels + l] = nlap;
+        if (n > G.kp_cap) atomicOr(err, 2);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_desc: one wave per kept keypoint. IC_Angle on the level, rBRIEF on the bit-exact
+// GaussianBlur(7x7, 2, REFLECT_101) of the level computed at the 512 sample points from a
+// 43x43 LDS patch (reflect-101 applied at load). Writes the final operator() slot.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P, FrameBufs fb,
+                                              const LevelKp* __restrict__ lvl_kp, const int* __restrict__ lvl_cnt,
+                                              const int* __restrict__ lvl_nlap, const int* __restrict__ disc,
+                                              orbhip_kp* __restrict__ out_kps, uint8_t* __restrict__ out_desc,
+                                              int cap, int* __restrict__ n_out, int* __restrict__ mono_out) {
+    __shared__ uint8_t patch[4][kPatchW * kPatchW + 15];
+    const int f = blockIdx.y;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int slot = blockIdx.x * 4 + wid;
+    const int L = P->n_levels;
+    // frame totals (same in every lane / wave of the frame)
+    int total = 0, nlap_tot = 0;
+    for (int l = 0; l < L; l++) { total += lvl_cnt[f * L + l]; nlap_tot += lvl_nlap[f * L + l]; }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        n_out[f] = total;
+        mono_out[f] = total - nlap_tot;
+    }
+    int l = 0, mono_base = 0, lap_base = 0;
+    while (l < L && slot >= P->lv[l].kp_cap) {
+        slot -= P->lv[l].kp_cap;
+        mono_base += lvl_cnt[f * L + l] - lvl_nlap[f * L + l];
+        lap_base += lvl_nlap[f * L + l];
+        l++;
+    }
+    const bool active = l < L && slot < lvl_cnt[f * L + l];
+    uint8_t* pt = patch[wid];
+    int cx = 0, cy = 0, lw = 0, lh = 0;
+    LevelKp kp{};
+    if (active) {
+        const LevelGeom& G = P->lv[l];
+        ImgRef im = level_img(P, fb, f, l);
+        kp = lvl_kp[(int64_t)f * P->kp_slots_total + G.kp_base + slot];
+        cx = kp.x; cy = kp.y; lw = G.w; lh = G.h;
+        for (int i = lane; i < kPatchW * kPatchW; i += 64) {
+            const int py = i / kPatchW, px = i - py * kPatchW;
+            int yy = cy - kPatchR + py, xx = cx - kPatchR + px;
+            // BORDER_REFLECT_101 (image is >= 43 px in both dims)
+            yy = yy < 0 ? -yy : (yy >= lh ? 2 * lh - 2 - yy : yy);
+            xx = xx < 0 ? -xx : (xx >= lw ? 2 * lw - 2 - xx : xx);
+            pt[i] = im.p[(int64_t)yy * im.pitch + xx];
+        }
+    }
+    __syncthreads();
+    if (!active) return;
+    const LevelGeom& G = P->lv[l];
+    // ---- IC_Angle: m10 = sum u*I, m01 = sum v*I over the umax disc ----
+    int m10 = 0, m01 = 0;
+    for (int i = lane; i < P->n_disc; i += 64) {
+        const int uv = disc[i];
+        const int u = (int)(int16_t)(uv & 0xFFFF), v = (int)(int16_t)(uv >> 16);
+        const int val = pt[(kPatchR + v) * kPatchW + kPatchR + u];
+        m10 += u * val;
+        m01 += v * val;
+    }
+    m10 = wave_sum_i32(m10);
+    m01 = wave_sum_i32(m01);
+    const float angle = fast_atan2((float)m01, (float)m10);
+    // ---- rBRIEF ----
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    const float ang = angle * factorPI;
+    const float a = glibc_cosf(ang), b = glibc_sinf(ang);
+    const int* k7 = P->blurk;
+    auto sample = [&](int idx) -> int {
+        const float px = (float)kPattern[2 * idx], py = (float)kPattern[2 * idx + 1];
+        const int oy = cv_round(px * b + py * a);
+        const int ox = cv_round(px * a - py * b);
+        const int X = kPatchR + ox, Y = kPatchR + oy;
+        uint32_t s = 0;
+#pragma unroll
+        for (int j = 0; j < 7; j++) {
+            const uint8_t* row = pt + (Y + j - 3) * kPatchW + X - 3;
+            uint32_t h = 0;
+#pragma unroll
+            for (int i = 0; i < 7; i++) h += (uint32_t)k7[i] * row[i];
+            s += (uint32_t)k7[j] * h;
+        }
+        return (int)((s + (1u << 15)) >> 16);
+    };
+    // lane handles pairs 4*lane .. 4*lane+3  (byte lane>>1, bits (lane&1)*4 ..)
+    int nib = 0;
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const int pair = 4 * lane + t;
+        const int t0 = sample(2 * pair), t1 = sample(2 * pair + 1);
+        nib |= (t0 < t1) << t;
+    }
+    const int other = __shfl_xor(nib, 1, 64);
+    const int lapflag = (kp.srl >> 8) & 1;
+    const int rank = (int)(kp.srl >> 9);
+    const int idx = lapflag ? (total - 1 - (lap_base + rank)) : (mono_base + rank);
+    if (idx >= cap) return;
+    if ((lane & 1) == 0) out_desc[((int64_t)f * cap + idx) * 32 + (lane >> 1)] = (uint8_t)(nib | (other << 4));
+    if (lane == 0) {
+        orbhip_kp o;
+        const float s = G.scale;
+        o.x = (l == 0) ? (float)cx : (float)cx * s;
+        o.y = (l == 0) ? (float)cy : (float)cy * s;
+        o.size = (float)G.patch_size;
+        o.angle = angle;
+        o.response = (float)(kp.srl & 0xFF);
+        o.octave = l;
+        out_kps[(int64_t)f * cap + idx] = o;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host-side launchers
+// ---------------------------------------------------------------------------
+void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, int B, int l,
+                   const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st) {
+    const LevelGeom& D = hP.lv[l];
+    dim3 blk(64, 4, 1);
+    dim3 grd((D.w + 255) / 256, (D.h + 3) / 4, B);
+    hipLaunchKernelGGL(k_resize, grd, blk, 0, st, dP, fb, l, xofs, xalpha, yofs, ybeta);
+}
+
+void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,
+                 uint32_t* cand, int* cand_cnt, hipStream_t st) {
+    dim3 grd(hP.n_cells_total, B, 1);
+    hipLaunchKernelGGL(k_fast_cells, grd, dim3(256), 0, st, dP, cells, fb, cand, cand_cnt);
+}
+
+size_t octree_lds_bytes(const ExtractPlan& hP, const OctreeCfg& cfg) {
+    size_t off = 0;
+    auto carve = [&](size_t bytes) { off += (bytes + 15) & ~size_t(15); };
+    const size_t NC = cfg.node_cap;
+    carve(64 * 4);
+    for (int b = 0; b < 2; b++) { carve(NC * 8); carve(NC * 4); carve(NC * 4); carve(NC * 4); }
+    carve(NC * 16); carve(NC * 16); carve(NC * 8);
+    carve(NC * 4); carve(NC * 4); carve(NC * 4); carve(NC * 4);
+    carve((size_t)cfg.sort_cap * 8);
+    carve((size_t)(hP.max_cells_level + 1) * 4);
+    carve((size_t)cfg.key_cap * 4);
+    carve((size_t)cfg.key_cap * 2);
+    return off;
+}
+
+void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const uint32_t* cand,
+                   const int* cand_cnt, uint32_t* kscratch, uint16_t* nscratch, LevelKp* lvl_kp, int* lvl_cnt,
+                   int* lvl_nlap, const OctreeCfg& cfg, int* err, int B, hipStream_t st) {
+    const size_t lds = octree_lds_bytes(hP, cfg);
+    dim3 grd(hP.n_levels, B, 1);
+    hipLaunchKernelGGL(k_octree, grd, dim3(1024), lds, st, dP, cells, cand, cand_cnt, kscratch, nscratch, lvl_kp,
+                       lvl_cnt, lvl_nlap, cfg, err);
+}
+
+void launch_desc(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, const LevelKp* lvl_kp,
+                 const int* lvl_cnt, const int* lvl_nlap, const int* disc, orbhip_kp* out_kps, uint8_t* out_desc,
+                 int cap, int* n_out, int* mono_out, int B, hipStream_t st) {
+    dim3 grd((hP.kp_slots_total + 3) / 4, B, 1);
+    hipLaunchKernelGGL(k_desc, grd, dim3(256), 0, st, dP, fb, lvl_kp, lvl_cnt, lvl_nlap, disc, out_kps, out_desc,
+                       cap, n_out, mono_out);
+}
+
+bool octree_set_lds_limit(size_t bytes) {
+    return hipFuncSetAttribute((const void*)k_octree, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) ==
+           hipSuccess;
+}
+
+}  // namespace orbhip

@@ -1,0 +1,225 @@
+// gfx950 Hamming matcher: U:src/ORBmatcher.cc DescriptorDistance + best/second + ratio +
+// TH_LOW acceptance, then the HISTO_LENGTH=30 rotation-consistency filter
+// (ComputeThreeMaxima). Order-free over the whole train set.
+//
+//   k_match_top2  grid (query blocks of 64, pairs). Train descriptors are staged in LDS in
+//                 tiles of 1024 (32 KiB); each wave owns 16 queries (descriptor in SGPRs),
+//                 lanes sweep the tile (v_xor + v_bcnt), per-lane (best, idx, second) kept
+//                 across tiles, merged across the wave with xor-shuffles.
+//   k_rot_filter  one workgroup per pair: 30-bin rotation histogram, three maxima, filter.
+#include <hip/hip_runtime.h>
+
+#include "orbhip_device.h"
+#include "orbhip_kernels.h"
+
+namespace orbhip {
+
+struct MatchView {
+    const uint8_t* qd;
+    const uint8_t* td;
+    const float* qa;
+    const float* ta;
+    int angle_stride;          // floats between consecutive angles
+    int64_t pair_desc_stride;  // bytes between pairs (query and train advance together)
+    int64_t pair_angle_stride; // floats between pairs
+    const int32_t* nq_arr;     // per pair (nullable)
+    const int32_t* nt_arr;
+    int nq, nt;
+    int64_t out_stride;        // entries between pairs in the outputs
+};
+
+constexpr int kTrainTile = 1024;
+constexpr int kQPerWave = 16;
+
+__device__ __forceinline__ void top2_merge(int& b, int& i, int& s, int b2, int i2, int s2) {
+    const int nb = (b2 < b || (b2 == b && i2 < i)) ? b2 : b;
+    const int ni = (b2 < b || (b2 == b && i2 < i)) ? i2 : i;
+    const int ns = min(max(b, b2), min(s, s2));
+    b = nb; i = ni; s = ns;
+}
+
+__global__ __launch_bounds__(256) void k_match_top2(MatchView v, int th_low, float ratio, int32_t* __restrict__ match,
+                                                     int32_t* __restrict__ best_out, int32_t* __restrict__ second_out) {
+    __shared__ __attribute__((aligned(16))) uint4 tile[kTrainTile * 2];
+    const int p = blockIdx.y;
+    const int nq = v.nq_arr ? v.nq_arr[p] : v.nq;
+    const int nt = v.nt_arr ? v.nt_arr[p] : v.nt;
+    const int q0 = blockIdx.x * (4 * kQPerWave);
+    if (q0 >= nq) return;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint8_t* qd = v.qd + (int64_t)p * v.pair_desc_stride;
+    const uint8_t* td = v.td + (int64_t)p * v.pair_desc_stride;
+    int pb[kQPerWave], pi[kQPerWave], ps[kQPerWave];
+#pragma unroll
+    for (int j = 0; j < kQPerWave; j++) { pb[j] = 256; pi[j] = 0x7fffffff; ps[j] = 256; }
+    const int qw = q0 + wid * kQPerWave;
+    for (int t0 = 0; t0 < nt; t0 += kTrainTile) {
+        const int tn = min(kTrainTile, nt - t0);
+        __syncthreads();
+        const uint4* src = (const uint4*)(td + (int64_t)t0 * 32);
+        for (int i = threadIdx.x; i < tn * 2; i += 256) tile[i] = src[i];
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kQPerWave; j++) {
+            const int q = qw + j;
+            if (q >= nq) break;   // wave-uniform
+            const uint4* qp = (const uint4*)(qd + (int64_t)q * 32);
+            const uint4 qa = qp[0], qb = qp[1];
+            int b = pb[j], bi = pi[j], s = ps[j];
+            for (int t = lane; t < tn; t += 64) {
+                const uint4 x = tile[2 * t], y = tile[2 * t + 1];
+                const int d = __popc(x.x ^ qa.x) + __popc(x.y ^ qa.y) + __popc(x.z ^ qa.z) + __popc(x.w ^ qa.w) +
+                              __popc(y.x ^ qb.x) + __popc(y.y ^ qb.y) + __popc(y.z ^ qb.z) + __popc(y.w ^ qb.w);
+                if (d < b) { s = b; b = d; bi = t0 + t; }
+                else if (d < s) s = d;
+            }
+            pb[j] = b; pi[j] = bi; ps[j] = s;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < kQPerWave; j++) {
+        const int q = qw + j;
+        if (q >= nq) break;
+        int b = pb[j], bi = pi[j], s = ps[j];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int b2 = __shfl_xor(b, o, 64), i2 = __shfl_xor(bi, o, 64), s2 = __shfl_xor(s, o, 64);
+            top2_merge(b, bi, s, b2, i2, s2);
+        }
+        if (lane == 0) {
+            const int64_t o = (int64_t)p * v.out_stride + q;
+            const bool ok = b < 256 && b <= th_low && (float)b < ratio * (float)s;
+            match[o] = ok ? bi : -1;
+            best_out[o] = b;
+            second_out[o] = s;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_rot_filter(MatchView v, int check_orientation, int32_t* __restrict__ match,
+                                                     int32_t* __restrict__ nmatch) {
+    __shared__ int hist[32];
+    __shared__ int keep[3];
+    __shared__ int cnt;
+    const int p = blockIdx.x;
+    const int nq = v.nq_arr ? v.nq_arr[p] : v.nq;
+    const float* qa = v.qa + (int64_t)p * v.pair_angle_stride;
+    const float* ta = v.ta + (int64_t)p * v.pair_angle_stride;
+    int32_t* m = match + (int64_t)p * v.out_stride;
+    const float factor = 1.0f / 30;
+    if (threadIdx.x < 32) hist[threadIdx.x] = 0;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    auto bin_of = [&](int q, int t) {
+        float rot = qa[(int64_t)q * v.angle_stride] - ta[(int64_t)t * v.angle_stride];
+        if (rot < 0.0) rot += 360.0f;
+        int bin = (int)roundf(rot * factor);
+        if (bin == 30) bin = 0;
+        return bin;
+    };
+    if (check_orientation) {
+        for (int q = threadIdx.x; q < nq; q += 256) {
+            const int t = m[q];
+            if (t >= 0) atomicAdd(&hist[bin_of(q, t)], 1);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
+            for (int i = 0; i < 30; i++) {
+                const int s = hist[i];
+                if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
+                else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
+                else if (s > max3) { max3 = s; ind3 = i; }
+            }
+            if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+            else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+            keep[0] = ind1; keep[1] = ind2; keep[2] = ind3;
+        }
+        __syncthreads();
+    }
+    int c = 0;
+    for (int q = threadIdx.x; q < nq; q += 256) {
+        const int t = m[q];
+        if (t < 0) continue;
+        if (check_orientation) {
+            const int bin = bin_of(q, t);
+            if (bin != keep[0] && bin != keep[1] && bin != keep[2]) { m[q] = -1; continue; }
+        }
+        c++;
+    }
+    c = wave_sum_i32(c);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&cnt, c);
+    __syncthreads();
+    if (threadIdx.x == 0) nmatch[p] = cnt;
+}
+
+static void run_match(const MatchView& v, int npairs, int max_q, int th_low, float ratio, int check_orientation,
+                      int32_t* match, int32_t* best, int32_t* second, int32_t* nmatch, hipStream_t st) {
+    if (npairs <= 0) return;
+    const int qblocks = (max_q + 4 * kQPerWave - 1) / (4 * kQPerWave);
+    if (qblocks > 0)
+        hipLaunchKernelGGL(k_match_top2, dim3(qblocks, npairs), dim3(256), 0, st, v, th_low, ratio, match, best,
+                           second);
+    hipLaunchKernelGGL(k_rot_filter, dim3(npairs), dim3(256), 0, st, v, check_orientation, match, nmatch);
+}
+
+void launch_match_pairs(const orbhip_kp* kps, const uint8_t* desc, const int32_t* n, int npairs, int cap,
+                        int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best,
+                        int32_t* second, int32_t* nmatch, hipStream_t st) {
+    MatchView v;
+    v.qd = desc;
+    v.td = desc + (int64_t)cap * 32;
+    v.qa = &kps[0].angle;
+    v.ta = &kps[cap].angle;
+    v.angle_stride = (int)(sizeof(orbhip_kp) / sizeof(float));
+    v.pair_desc_stride = (int64_t)cap * 32;
+    v.pair_angle_stride = (int64_t)cap * v.angle_stride;
+    v.nq_arr = n;
+    v.nt_arr = n + 1;
+    v.nq = cap;
+    v.nt = cap;
+    v.out_stride = cap;
+    run_match(v, npairs, cap, th_low, ratio, check_orientation, match, best, second, nmatch, st);
+}
+
+void launch_match_bf(const uint8_t* q, const float* qa, int nq, const uint8_t* t, const float* ta, int nt,
+                     int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best,
+                     int32_t* second, int32_t* nmatch, hipStream_t st) {
+    MatchView v;
+    v.qd = q; v.td = t; v.qa = qa; v.ta = ta;
+    v.angle_stride = 1;
+    v.pair_desc_stride = 0;
+    v.pair_angle_stride = 0;
+    v.nq_arr = nullptr; v.nt_arr = nullptr;
+    v.nq = nq; v.nt = nt;
+    v.out_stride = 0;
+    run_match(v, 1, nq, th_low, ratio, check_orientation, match, best, second, nmatch, st);
+}
+
+// ---- test hooks: device glibc sinf/cosf restatement ----
+__global__ void k_sincos_probe(const float* x, float* c, float* s, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) { c[i] = glibc_cosf(x[i]); s[i] = glibc_sinf(x[i]); }
+}
+
+void launch_sincos_probe(const float* x, float* c, float* s, int64_t n, hipStream_t st) {
+    hipLaunchKernelGGL(k_sincos_probe, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, x, c, s, n);
+}
+
+__global__ void k_sincos_sweep(uint32_t lo, uint32_t hi, const float* rc, const float* rs, unsigned long long* mism) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t u = lo + i;
+    if (u > hi) return;
+    const float x = __uint_as_float(u);
+    const bool bad = glibc_cosf(x) != rc[i] || glibc_sinf(x) != rs[i];
+    if (bad) atomicAdd(mism, 1ull);
+}
+
+void launch_sincos_sweep(uint32_t lo_bits, uint32_t hi_bits, const float* ref_c, const float* ref_s,
+                         unsigned long long* mismatches, hipStream_t st) {
+    const uint64_t n = (uint64_t)hi_bits - lo_bits + 1;
+    hipLaunchKernelGGL(k_sincos_sweep, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, lo_bits, hi_bits, ref_c,
+                       ref_s, mismatches);
+}
+
+}  // namespace orbhip

@@ -1,0 +1,623 @@
+// liborbhip.so host side: contexts, per-size extraction plans, the C-ABI of include/orbhip.h.
+//
+// Plan construction restates the table logic of the reference (it is the product's own
+// code, not the oracle's):
+//   U:src/ORBextractor.cc::ORBextractor::ORBextractor  scale / feature / umax tables
+//   U:src/ORBextractor.cc::ComputePyramid               level sizes
+//   OCV:imgproc/src/resize.cpp hal::resize              xofs/alpha/yofs/beta fixed-point tables
+//   U:src/ORBextractor.cc::ComputeKeyPointsOctTree      35-px cell grid
+//   U:src/ORBextractor.cc::DistributeOctTree            root count nIni, root width hX
+//   OCV:imgproc smooth.dispatch.cpp getGaussianKernelBitExact + fixed-point ED  (7x7, sigma 2)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "../../include/orbhip.h"
+#include "orbhip_ba.h"
+#include "orbhip_kernels.h"
+#include "orbhip_plan.h"
+
+using namespace orbhip;
+
+#define HIPOK(x)                                                                                   \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) {                                                                    \
+            std::fprintf(stderr, "orbhip: %s failed: %s (%s:%d)\n", #x, hipGetErrorString(e_),     \
+                         __FILE__, __LINE__);                                                      \
+            return ORBHIP_ERR_DEVICE;                                                              \
+        }                                                                                          \
+    } while (0)
+
+namespace {
+
+inline int round_even_f(float v) { return (int)std::nearbyintf(v); }
+inline int round_even_d(double v) { return (int)std::nearbyint(v); }
+inline int floor_f(float v) { int i = (int)v; return i - (i > v); }
+inline short sat_s16(int v) { return (short)std::min(std::max(v, -32768), 32767); }
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    hipError_t ensure(size_t count) {
+        if (count <= n && p) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; n = 0; }
+        hipError_t e = hipMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T));
+        if (e == hipSuccess) n = count;
+        return e;
+    }
+};
+
+struct Plan {
+    ExtractPlan h{};
+    std::vector<CellGeom> cells;
+    std::vector<int> xofs, xalpha, yofs, ybeta, disc;
+    OctreeCfg oct{};
+    int kp_cap_frame = 0;   // sum of level caps = max keypoints per frame
+    DevBuf<ExtractPlan> d_plan;
+    DevBuf<CellGeom> d_cells;
+    DevBuf<int> d_xofs, d_xalpha, d_yofs, d_ybeta, d_disc;
+};
+
+}  // namespace
+
+struct orbhip_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    orbhip_orb_params prm{};
+    // ORBextractor ctor tables
+    std::vector<float> scale, inv_scale;
+    std::vector<int> feat, umax;
+    int blurk[7] = {0};
+    std::map<std::pair<int, int>, std::unique_ptr<Plan>> plans;
+    // per-batch scratch (grown on demand)
+    DevBuf<uint8_t> d_in, d_pyr;
+    DevBuf<uint32_t> d_cand, d_kscratch;
+    DevBuf<uint16_t> d_nscratch;
+    DevBuf<int> d_cand_cnt, d_lvl_cnt, d_lvl_nlap, d_err;
+    DevBuf<LevelKp> d_lvl_kp;
+    DevBuf<orbhip_kp> d_kps;
+    DevBuf<uint8_t> d_desc;
+    DevBuf<int32_t> d_n, d_mono;
+    // matcher scratch
+    DevBuf<uint8_t> d_mq, d_mt;
+    DevBuf<float> d_mqa, d_mta;
+    DevBuf<int32_t> d_mm, d_mb, d_ms, d_mn;
+    BaWorkspace* ba = nullptr;
+};
+
+// ---------------------------------------------------------------------------
+// ORBextractor ctor tables
+// ---------------------------------------------------------------------------
+static void build_orb_tables(orbhip_ctx* c) {
+    const int L = c->prm.n_levels;
+    const double sf = (double)c->prm.scale_factor;
+    c->scale.assign(L, 1.f);
+    c->inv_scale.assign(L, 1.f);
+    for (int i = 1; i < L; i++) c->scale[i] = (float)(c->scale[i - 1] * sf);
+    for (int i = 0; i < L; i++) c->inv_scale[i] = 1.0f / c->scale[i];
+    c->feat.assign(L, 0);
+    const float factor = (float)(1.0f / sf);
+    float nd = c->prm.n_features * (1 - factor) / (1 - (float)std::pow((double)factor, (double)L));
+    int sum = 0;
+    for (int l = 0; l < L - 1; l++) {
+        c->feat[l] = round_even_f(nd);
+        sum += c->feat[l];
+        nd *= factor;
+    }
+    c->feat[L - 1] = std::max(c->prm.n_features - sum, 0);
+    // umax (HALF_PATCH_SIZE 15)
+    const int H = 15;
+    c->umax.assign(H + 1, 0);
+    int vmax = (int)std::floor(H * std::sqrt(2.f) / 2 + 1);
+    int vmin = (int)std::ceil(H * std::sqrt(2.f) / 2);
+    const double hp2 = H * H;
+    for (int v = 0; v <= vmax; ++v) c->umax[v] = round_even_d(std::sqrt(hp2 - v * v));
+    for (int v = H, v0 = 0; v >= vmin; --v) {
+        while (c->umax[v0] == c->umax[v0 + 1]) ++v0;
+        c->umax[v] = v0;
+        ++v0;
+    }
+    // bit-exact 7-tap Gaussian, sigma 2, 8 fractional bits, error diffusion
+    const int n = 7, n2 = 3;
+    double vals[3], s = 0, scale2X = -0.125 / (2.0 * 2.0);
+    for (int i = 0, x = 1 - n; i < n2; i++, x += 2) { vals[i] = std::exp((double)(x * x) * scale2X); s += vals[i]; }
+    s = s * 2 + 1.0;
+    const double mul1 = 1.0 / s;
+    double err = 0;
+    long tot = 0;
+    for (int i = 0; i < n2; i++) {
+        double adj = vals[i] * mul1 * 256.0 + err;
+        long v0 = round_even_d(adj);
+        err = adj - (double)v0;
+        c->blurk[i] = c->blurk[n - 1 - i] = (int)v0;
+        tot += v0;
+    }
+    c->blurk[n2] = (int)(256 - 2 * tot);
+}
+
+// ---------------------------------------------------------------------------
+// per-size plan
+// ---------------------------------------------------------------------------
+static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
+    auto key = std::make_pair(w, h);
+    auto it = c->plans.find(key);
+    if (it != c->plans.end()) { *out = it->second.get(); return ORBHIP_OK; }
+    std::unique_ptr<Plan> pl(new Plan());
+    ExtractPlan& P = pl->h;
+    const int L = c->prm.n_levels;
+    P.w = w; P.h = h; P.n_levels = L;
+    P.ini_th = std::min(std::max(c->prm.ini_th_fast, 0), 255);
+    P.min_th = std::min(std::max(c->prm.min_th_fast, 0), 255);
+    for (int i = 0; i < 7; i++) P.blurk[i] = c->blurk[i];
+    int64_t pyr_off = 0;
+    int cell_base = 0, slot_base = 0, kp_base = 0, max_cells = 0;
+    for (int l = 0; l < L; l++) {
+        LevelGeom& G = P.lv[l];
+        G.w = round_even_f((float)w * c->inv_scale[l]);
+        G.h = round_even_f((float)h * c->inv_scale[l]);
+        if (G.w < 64 || G.h < 64) return ORBHIP_ERR_UNSUPPORTED;   // every level must host 43x43 patches
+        G.pitch = l == 0 ? 0 : ((G.w + 63) / 64) * 64;
+        G.pyr_off = l == 0 ? 0 : pyr_off;
+        if (l > 0) pyr_off += (int64_t)G.pitch * G.h;
+        G.scale = c->scale[l];
+        G.n_feat = c->feat[l];
+        G.patch_size = (int)(31 * c->scale[l]);
+        // resize tables (level l from l-1)
+        G.xtab_off = (int)pl->xofs.size();
+        G.ytab_off = (int)pl->yofs.size();
+        G.xmax = G.w;
+        G.vend = 0;
+        if (l > 0) {
+            const int sw = P.lv[l - 1].w, sh = P.lv[l - 1].h, dw = G.w, dh = G.h;
+            double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
+            double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
+            int isx = round_even_d(scale_x), isy = round_even_d(scale_y);
+            if (std::abs(scale_x - isx) < DBL_EPSILON && std::abs(scale_y - isy) < DBL_EPSILON && isx == 2 && isy == 2)
+                return ORBHIP_ERR_UNSUPPORTED;   // OpenCV switches to INTER_AREA for exact 2x
+            int xmax = dw;
+            for (int dx = 0; dx < dw; dx++) {
+                float fx = (float)((dx + 0.5) * scale_x - 0.5);
+                int sx = floor_f(fx);
+                fx -= sx;
+                if (sx < 0) { fx = 0; sx = 0; }
+                if (sx + 1 >= sw) {
+                    xmax = std::min(xmax, dx);
+                    if (sx >= sw - 1) { fx = 0; sx = sw - 1; }
+                }
+                pl->xofs.push_back(sx);
+                const short a0 = sat_s16(round_even_f((1.f - fx) * 2048)), a1 = sat_s16(round_even_f(fx * 2048));
+                pl->xalpha.push_back((int)(uint16_t)a0 | ((int)(uint16_t)a1 << 16));
+            }
+            for (int dy = 0; dy < dh; dy++) {
+                float fy = (float)((dy + 0.5) * scale_y - 0.5);
+                int sy = floor_f(fy);
+                fy -= sy;
+                pl->yofs.push_back(sy);
+                const short b0 = sat_s16(round_even_f((1.f - fy) * 2048)), b1 = sat_s16(round_even_f(fy * 2048));
+                pl->ybeta.push_back((int)(uint16_t)b0 | ((int)(uint16_t)b1 << 16));
+            }
+            G.xmax = xmax;
+            int x = 0;
+            for (; x <= dw - 16; x += 16) {}
+            for (; x < dw - 8; x += 8) {}
+            G.vend = x;
+        }
+        // cells (ComputeKeyPointsOctTree)
+        const int EDGE = 19;
+        G.min_bx = EDGE - 3; G.min_by = EDGE - 3;
+        G.max_bx = G.w - EDGE + 3; G.max_by = G.h - EDGE + 3;
+        const float width = (float)(G.max_bx - G.min_bx), height = (float)(G.max_by - G.min_by);
+        G.n_cols = (int)(width / 35.f);
+        G.n_rows = (int)(height / 35.f);
+        if (G.n_cols <= 0 || G.n_rows <= 0) return ORBHIP_ERR_UNSUPPORTED;
+        G.w_cell = (int)std::ceil(width / G.n_cols);
+        G.h_cell = (int)std::ceil(height / G.n_rows);
+        G.cell_base = cell_base;
+        G.slot_base = slot_base;
+        int ncell = 0;
+        for (int i = 0; i < G.n_rows; i++) {
+            const float iniY = (float)(G.min_by + i * G.h_cell);
+            float maxY = iniY + G.h_cell + 6;
+            const bool skipY = iniY >= G.max_by - 3;
+            if (maxY > G.max_by) maxY = (float)G.max_by;
+            for (int j = 0; j < G.n_cols; j++) {
+                const float iniX = (float)(G.min_bx + j * G.w_cell);
+                float maxX = iniX + G.w_cell + 6;
+                const bool skipX = iniX >= G.max_bx - 6;
+                if (maxX > G.max_bx) maxX = (float)G.max_bx;
+                CellGeom cg{};
+                cg.level = (int16_t)l;
+                cg.x0 = (int16_t)iniX; cg.y0 = (int16_t)iniY;
+                cg.wc = (skipY || skipX) ? 0 : (int16_t)((int)maxX - (int)iniX);
+                cg.hc = (skipY || skipX) ? 0 : (int16_t)((int)maxY - (int)iniY);
+                if (cg.wc > 76 || cg.hc > 76) return ORBHIP_ERR_UNSUPPORTED;
+                cg.slot_off = slot_base;
+                const int dc = std::max(cg.wc - 6, 0), dr = std::max(cg.hc - 6, 0);
+                slot_base += ((dc + 1) / 2) * ((dr + 1) / 2);   // max strict-NMS survivors
+                pl->cells.push_back(cg);
+                ncell++;
+            }
+        }
+        G.n_cells = ncell;
+        G.n_slots = slot_base - G.slot_base;
+        cell_base += ncell;
+        max_cells = std::max(max_cells, ncell);
+        // DistributeOctTree roots
+        G.n_ini = (int)std::round((float)(G.max_bx - G.min_bx) / (G.max_by - G.min_by));
+        if (G.n_ini <= 0 || G.n_ini > 64) return ORBHIP_ERR_UNSUPPORTED;
+        G.hX = (float)(G.max_bx - G.min_bx) / G.n_ini;
+        G.kp_cap = G.n_feat + 3 + 4 * G.n_ini;
+        G.kp_base = kp_base;
+        kp_base += G.kp_cap;
+        if ((G.max_bx - G.min_bx) >= 4096 || (G.max_by - G.min_by) >= 4096) return ORBHIP_ERR_UNSUPPORTED;
+    }
+    P.n_cells_total = cell_base;
+    P.n_slots_total = slot_base;
+    P.kp_slots_total = kp_base;
+    P.pyr_bytes = ((pyr_off + 255) / 256) * 256;
+    P.max_cells_level = max_cells;
+    pl->kp_cap_frame = kp_base;
+    // IC_Angle disc offsets (u, v) packed as int16 pairs
+    for (int v = -15; v <= 15; v++) {
+        const int d = c->umax[std::abs(v)];
+        for (int u = -d; u <= d; u++) pl->disc.push_back((int)(uint16_t)(int16_t)u | ((int)(int16_t)v << 16));
+    }
+    P.n_disc = (int)pl->disc.size();
+    // octree LDS configuration
+    int max_kp_cap = 0;
+    for (int l = 0; l < L; l++) max_kp_cap = std::max(max_kp_cap, P.lv[l].kp_cap);
+    OctreeCfg& oc = pl->oct;
+    oc.node_cap = ((max_kp_cap + 63) / 64) * 64;
+    oc.sort_cap = 1;
+    while (oc.sort_cap < oc.node_cap) oc.sort_cap <<= 1;
+    oc.key_cap = 0;
+    const size_t budget = 160 * 1024;
+    const size_t base = octree_lds_bytes(P, oc);
+    if (base + 1024 > budget) return ORBHIP_ERR_UNSUPPORTED;
+    oc.key_cap = (int)std::min<size_t>(16384, ((budget - base - 64) / 6) & ~size_t(15));
+    while (octree_lds_bytes(P, oc) > budget) oc.key_cap -= 16;
+    // upload
+    HIPOK(pl->d_plan.ensure(1));
+    HIPOK(hipMemcpy(pl->d_plan.p, &P, sizeof(ExtractPlan), hipMemcpyHostToDevice));
+    HIPOK(pl->d_cells.ensure(pl->cells.size()));
+    HIPOK(hipMemcpy(pl->d_cells.p, pl->cells.data(), pl->cells.size() * sizeof(CellGeom), hipMemcpyHostToDevice));
+    auto up = [](DevBuf<int>& d, const std::vector<int>& v) -> hipError_t {
+        hipError_t e = d.ensure(v.size());
+        if (e != hipSuccess) return e;
+        if (v.empty()) return hipSuccess;
+        return hipMemcpy(d.p, v.data(), v.size() * sizeof(int), hipMemcpyHostToDevice);
+    };
+    HIPOK(up(pl->d_xofs, pl->xofs));
+    HIPOK(up(pl->d_xalpha, pl->xalpha));
+    HIPOK(up(pl->d_yofs, pl->yofs));
+    HIPOK(up(pl->d_ybeta, pl->ybeta));
+    HIPOK(up(pl->d_disc, pl->disc));
+    *out = pl.get();
+    c->plans[key] = std::move(pl);
+    return ORBHIP_OK;
+}
+
+static int ensure_batch(orbhip_ctx* c, const Plan* pl, int B) {
+    const ExtractPlan& P = pl->h;
+    HIPOK(c->d_pyr.ensure((size_t)B * P.pyr_bytes));
+    HIPOK(c->d_cand.ensure((size_t)B * P.n_slots_total));
+    HIPOK(c->d_kscratch.ensure((size_t)B * P.n_slots_total));
+    HIPOK(c->d_nscratch.ensure((size_t)B * P.n_slots_total));
+    HIPOK(c->d_cand_cnt.ensure((size_t)B * P.n_cells_total));
+    HIPOK(c->d_lvl_kp.ensure((size_t)B * P.kp_slots_total));
+    HIPOK(c->d_lvl_cnt.ensure((size_t)B * P.n_levels));
+    HIPOK(c->d_lvl_nlap.ensure((size_t)B * P.n_levels));
+    HIPOK(c->d_err.ensure(4));
+    return ORBHIP_OK;
+}
+
+static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, int stride, int64_t fstride, int lap0,
+                       int lap1, orbhip_kp* d_kps, uint8_t* d_desc, int cap, int32_t* d_n, int32_t* d_mono,
+                       hipStream_t st) {
+    const ExtractPlan& P = pl->h;
+    int rc = ensure_batch(c, pl, B);
+    if (rc) return rc;
+    FrameBufs fb;
+    fb.in = d_imgs; fb.in_stride = stride; fb.in_fstride = fstride; fb.pyr = c->d_pyr.p;
+    HIPOK(hipMemsetAsync(c->d_err.p, 0, 4 * sizeof(int), st));
+    for (int l = 1; l < P.n_levels; l++)
+        launch_resize(pl->d_plan.p, P, fb, B, l, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p, pl->d_ybeta.p, st);
+    launch_fast(pl->d_plan.p, P, pl->d_cells.p, fb, B, c->d_cand.p, c->d_cand_cnt.p, st);
+    OctreeCfg oc = pl->oct;
+    oc.lap0 = lap0; oc.lap1 = lap1;
+    launch_octree(pl->d_plan.p, P, pl->d_cells.p, c->d_cand.p, c->d_cand_cnt.p, c->d_kscratch.p, c->d_nscratch.p,
+                  c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, oc, c->d_err.p, B, st);
+    launch_desc(pl->d_plan.p, P, fb, c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, pl->d_disc.p, d_kps, d_desc, cap,
+                d_n, d_mono, B, st);
+    HIPOK(hipGetLastError());
+    return ORBHIP_OK;
+}
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+extern "C" {
+
+int orbhip_abi_version(void) { return ORBHIP_ABI_VERSION; }
+
+int orbhip_create(orbhip_ctx** out, int device, const orbhip_orb_params* params) {
+    if (!out) return ORBHIP_ERR_ARG;
+    *out = nullptr;
+    orbhip_orb_params p = {1000, 1.2f, 8, 20, 7};
+    if (params) p = *params;
+    if (p.n_features < 0 || p.n_levels < 1 || p.n_levels > kMaxLevels || !(p.scale_factor >= 1.0f))
+        return ORBHIP_ERR_ARG;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) return ORBHIP_ERR_DEVICE;
+    std::unique_ptr<orbhip_ctx> c(new orbhip_ctx());
+    c->device = device;
+    c->prm = p;
+    HIPOK(hipSetDevice(device));
+    HIPOK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if (!octree_set_lds_limit(160 * 1024)) return ORBHIP_ERR_DEVICE;
+    build_orb_tables(c.get());
+    *out = c.release();
+    return ORBHIP_OK;
+}
+
+int orbhip_destroy(orbhip_ctx* c) {
+    if (!c) return ORBHIP_ERR_ARG;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    ba_destroy(c->ba);
+    c->plans.clear();
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return ORBHIP_OK;
+}
+
+int orbhip_level_info(orbhip_ctx* c, int w, int h, int32_t* lw, int32_t* lh, int32_t* nf, float* sc) {
+    if (!c || w <= 0 || h <= 0) return ORBHIP_ERR_ARG;
+    for (int l = 0; l < c->prm.n_levels; l++) {
+        if (lw) lw[l] = round_even_f((float)w * c->inv_scale[l]);
+        if (lh) lh[l] = round_even_f((float)h * c->inv_scale[l]);
+        if (nf) nf[l] = c->feat[l];
+        if (sc) sc[l] = c->scale[l];
+    }
+    return ORBHIP_OK;
+}
+
+int orbhip_max_keypoints(orbhip_ctx* c, int w, int h) {
+    if (!c || w <= 0 || h <= 0) return ORBHIP_ERR_ARG;
+    if (hipSetDevice(c->device) != hipSuccess) return ORBHIP_ERR_DEVICE;
+    Plan* pl = nullptr;
+    int rc = build_plan(c, w, h, &pl);
+    return rc ? rc : pl->kp_cap_frame;
+}
+
+int orbhip_extract_batch_device(orbhip_ctx* c, const uint8_t* d_imgs, int B, int w, int h, int stride,
+                                int64_t frame_stride, int lap0, int lap1, orbhip_kp* d_kps, uint8_t* d_desc, int cap,
+                                int32_t* d_n, int32_t* d_mono, void* stream) {
+    if (!c || !d_imgs || B <= 0 || w <= 0 || h <= 0 || stride < w || !d_kps || !d_desc || !d_n || !d_mono || cap <= 0)
+        return ORBHIP_ERR_ARG;
+    if (B > 1 && frame_stride < (int64_t)stride * h) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    Plan* pl = nullptr;
+    int rc = build_plan(c, w, h, &pl);
+    if (rc) return rc;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return run_extract(c, pl, d_imgs, B, stride, frame_stride, lap0, lap1, d_kps, d_desc, cap, d_n, d_mono, st);
+}
+
+int orbhip_extract(orbhip_ctx* c, const uint8_t* img, int w, int h, int stride, int lap0, int lap1, orbhip_kp* kps,
+                   uint8_t* desc32, int cap, int* n_out, int* mono_index) {
+    if (!c || !n_out) return ORBHIP_ERR_ARG;
+    *n_out = 0;
+    if (mono_index) *mono_index = -1;
+    if (!img || w <= 0 || h <= 0) return ORBHIP_ERR_EMPTY;   // operator(): _image.empty() -> -1
+    if (stride < w || (cap > 0 && (!kps || !desc32))) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    Plan* pl = nullptr;
+    int rc = build_plan(c, w, h, &pl);
+    if (rc) return rc;
+    const int kcap = pl->kp_cap_frame;
+    HIPOK(c->d_in.ensure((size_t)w * h));
+    HIPOK(c->d_kps.ensure(kcap));
+    HIPOK(c->d_desc.ensure((size_t)kcap * 32));
+    HIPOK(c->d_n.ensure(1));
+    HIPOK(c->d_mono.ensure(1));
+    hipStream_t st = c->stream;
+    HIPOK(hipMemcpy2DAsync(c->d_in.p, w, img, stride, w, h, hipMemcpyHostToDevice, st));
+    rc = run_extract(c, pl, c->d_in.p, 1, w, (int64_t)w * h, lap0, lap1, c->d_kps.p, c->d_desc.p, kcap, c->d_n.p,
+                     c->d_mono.p, st);
+    if (rc) return rc;
+    int n = 0, mono = 0, err[4] = {0, 0, 0, 0};
+    HIPOK(hipMemcpyAsync(&n, c->d_n.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPOK(hipMemcpyAsync(&mono, c->d_mono.p, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPOK(hipMemcpyAsync(err, c->d_err.p, sizeof(err), hipMemcpyDeviceToHost, st));
+    HIPOK(hipStreamSynchronize(st));
+    if (err[0]) return ORBHIP_ERR_DEVICE;
+    *n_out = n;
+    if (mono_index) *mono_index = mono;
+    if (n > cap) return ORBHIP_ERR_CAPACITY;
+    if (n > 0) {
+        HIPOK(hipMemcpyAsync(kps, c->d_kps.p, (size_t)n * sizeof(orbhip_kp), hipMemcpyDeviceToHost, st));
+        HIPOK(hipMemcpyAsync(desc32, c->d_desc.p, (size_t)n * 32, hipMemcpyDeviceToHost, st));
+        HIPOK(hipStreamSynchronize(st));
+    }
+    return ORBHIP_OK;
+}
+
+int orbhip_descriptor_distance(const uint8_t* a, const uint8_t* b) {
+    if (!a || !b) return ORBHIP_ERR_ARG;
+    int d = 0;
+    for (int i = 0; i < 8; i++) {
+        uint32_t x, y;
+        std::memcpy(&x, a + 4 * i, 4);
+        std::memcpy(&y, b + 4 * i, 4);
+        d += __builtin_popcount(x ^ y);
+    }
+    return d;
+}
+
+int orbhip_match_bf(orbhip_ctx* c, const uint8_t* q, const float* qa, int nq, const uint8_t* t, const float* ta,
+                    int nt, int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best_d,
+                    int32_t* second_d) {
+    if (!c || nq < 0 || nt < 0 || (nq > 0 && (!q || !qa || !match || !best_d || !second_d)) || (nt > 0 && (!t || !ta)))
+        return ORBHIP_ERR_ARG;
+    if (nq == 0) return 0;
+    HIPOK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    HIPOK(c->d_mq.ensure((size_t)nq * 32));
+    HIPOK(c->d_mt.ensure((size_t)std::max(nt, 1) * 32));
+    HIPOK(c->d_mqa.ensure(nq));
+    HIPOK(c->d_mta.ensure(std::max(nt, 1)));
+    HIPOK(c->d_mm.ensure(nq));
+    HIPOK(c->d_mb.ensure(nq));
+    HIPOK(c->d_ms.ensure(nq));
+    HIPOK(c->d_mn.ensure(1));
+    HIPOK(hipMemcpyAsync(c->d_mq.p, q, (size_t)nq * 32, hipMemcpyHostToDevice, st));
+    HIPOK(hipMemcpyAsync(c->d_mqa.p, qa, (size_t)nq * 4, hipMemcpyHostToDevice, st));
+    if (nt > 0) {
+        HIPOK(hipMemcpyAsync(c->d_mt.p, t, (size_t)nt * 32, hipMemcpyHostToDevice, st));
+        HIPOK(hipMemcpyAsync(c->d_mta.p, ta, (size_t)nt * 4, hipMemcpyHostToDevice, st));
+    } else {
+        // no train descriptors: every query keeps best = second = 256 (no match)
+        HIPOK(hipMemsetAsync(c->d_mm.p, 0xFF, (size_t)nq * 4, st));
+    }
+    launch_match_bf(c->d_mq.p, c->d_mqa.p, nq, c->d_mt.p, c->d_mta.p, nt, th_low, ratio, check_orientation, c->d_mm.p,
+                    c->d_mb.p, c->d_ms.p, c->d_mn.p, st);
+    HIPOK(hipGetLastError());
+    int nm = 0;
+    HIPOK(hipMemcpyAsync(match, c->d_mm.p, (size_t)nq * 4, hipMemcpyDeviceToHost, st));
+    HIPOK(hipMemcpyAsync(best_d, c->d_mb.p, (size_t)nq * 4, hipMemcpyDeviceToHost, st));
+    HIPOK(hipMemcpyAsync(second_d, c->d_ms.p, (size_t)nq * 4, hipMemcpyDeviceToHost, st));
+    HIPOK(hipMemcpyAsync(&nm, c->d_mn.p, 4, hipMemcpyDeviceToHost, st));
+    HIPOK(hipStreamSynchronize(st));
+    return nm;
+}
+
+int orbhip_match_pairs_device(orbhip_ctx* c, const orbhip_kp* d_kps, const uint8_t* d_desc, const int32_t* d_n, int B,
+                              int cap, int th_low, float ratio, int check_orientation, int32_t* d_match,
+                              int32_t* d_best, int32_t* d_second, int32_t* d_nmatch, void* stream) {
+    if (!c || !d_kps || !d_desc || !d_n || B < 2 || cap <= 0 || !d_match || !d_best || !d_second || !d_nmatch)
+        return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    launch_match_pairs(d_kps, d_desc, d_n, B - 1, cap, th_low, ratio, check_orientation, d_match, d_best, d_second,
+                       d_nmatch, st);
+    HIPOK(hipGetLastError());
+    return ORBHIP_OK;
+}
+
+int orbhip_ba_solve(orbhip_ctx* c, const orbhip_ba_problem* prob, orbhip_ba_result* res, const volatile int* stop) {
+    if (!c || !prob || !res) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    if (!c->ba) c->ba = ba_create();
+    if (!c->ba) return ORBHIP_ERR_DEVICE;
+    return ba_solve(c->ba, prob, res, stop, c->stream);
+}
+
+// ---- test hooks (not part of the reference surface) ----
+int orbhip_test_sincosf(const float* x, float* cs, float* sn, int64_t n) {
+    if (!x || !cs || !sn || n <= 0) return ORBHIP_ERR_ARG;
+    float *dx = nullptr, *dc = nullptr, *ds = nullptr;
+    HIPOK(hipMalloc((void**)&dx, n * 4));
+    HIPOK(hipMalloc((void**)&dc, n * 4));
+    HIPOK(hipMalloc((void**)&ds, n * 4));
+    HIPOK(hipMemcpy(dx, x, n * 4, hipMemcpyHostToDevice));
+    launch_sincos_probe(dx, dc, ds, n, nullptr);
+    HIPOK(hipDeviceSynchronize());
+    HIPOK(hipMemcpy(cs, dc, n * 4, hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(sn, ds, n * 4, hipMemcpyDeviceToHost));
+    (void)hipFree(dx); (void)hipFree(dc); (void)hipFree(ds);
+    return ORBHIP_OK;
+}
+
+// Compare device sinf/cosf with host reference values over float bit range [lo, hi].
+int64_t orbhip_test_sincosf_sweep(uint32_t lo, uint32_t hi, const float* ref_c, const float* ref_s) {
+    if (hi < lo || !ref_c || !ref_s) return ORBHIP_ERR_ARG;
+    const size_t n = (size_t)hi - lo + 1;
+    float *dc = nullptr, *ds = nullptr;
+    unsigned long long* dm = nullptr;
+    unsigned long long hm = 0;
+    if (hipMalloc((void**)&dc, n * 4) != hipSuccess) return ORBHIP_ERR_DEVICE;
+    if (hipMalloc((void**)&ds, n * 4) != hipSuccess) return ORBHIP_ERR_DEVICE;
+    if (hipMalloc((void**)&dm, 8) != hipSuccess) return ORBHIP_ERR_DEVICE;
+    (void)hipMemset(dm, 0, 8);
+    (void)hipMemcpy(dc, ref_c, n * 4, hipMemcpyHostToDevice);
+    (void)hipMemcpy(ds, ref_s, n * 4, hipMemcpyHostToDevice);
+    launch_sincos_sweep(lo, hi, dc, ds, dm, nullptr);
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpy(&hm, dm, 8, hipMemcpyDeviceToHost);
+    (void)hipFree(dc); (void)hipFree(ds); (void)hipFree(dm);
+    return (int64_t)hm;
+}
+
+// Debug hook: run one frame and return the intermediates (pyramid levels 1.., candidates
+// per cell, octree output per level) so a mismatch can be localised offline.
+// pyr: sum_{l>=1} w_l*h_l bytes (packed, no pitch); cand: n_slots_total u32; cand_cnt:
+// n_cells_total; lvl: kp_slots_total LevelKp (8 B each); lvl_cnt/lvl_nlap: n_levels.
+int orbhip_test_extract_debug(orbhip_ctx* c, const uint8_t* img, int w, int h, int lap0, int lap1, uint8_t* pyr,
+                              uint32_t* cand, int32_t* cand_cnt, void* lvl, int32_t* lvl_cnt, int32_t* lvl_nlap,
+                              int32_t* sizes /* n_slots_total, n_cells_total, kp_slots_total, err */) {
+    if (!c || !img) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    Plan* pl = nullptr;
+    int rc = build_plan(c, w, h, &pl);
+    if (rc) return rc;
+    const ExtractPlan& P = pl->h;
+    sizes[0] = P.n_slots_total; sizes[1] = P.n_cells_total; sizes[2] = P.kp_slots_total;
+    if (!pyr) return ORBHIP_OK;   // size query
+    const int kcap = pl->kp_cap_frame;
+    HIPOK(c->d_in.ensure((size_t)w * h));
+    HIPOK(c->d_kps.ensure(kcap));
+    HIPOK(c->d_desc.ensure((size_t)kcap * 32));
+    HIPOK(c->d_n.ensure(1));
+    HIPOK(c->d_mono.ensure(1));
+    hipStream_t st = c->stream;
+    HIPOK(hipMemcpy2DAsync(c->d_in.p, w, img, w, w, h, hipMemcpyHostToDevice, st));
+    rc = run_extract(c, pl, c->d_in.p, 1, w, (int64_t)w * h, lap0, lap1, c->d_kps.p, c->d_desc.p, kcap, c->d_n.p,
+                     c->d_mono.p, st);
+    if (rc) return rc;
+    HIPOK(hipStreamSynchronize(st));
+    size_t off = 0;
+    for (int l = 1; l < P.n_levels; l++) {
+        const LevelGeom& G = P.lv[l];
+        HIPOK(hipMemcpy2D(pyr + off, G.w, c->d_pyr.p + G.pyr_off, G.pitch, G.w, G.h, hipMemcpyDeviceToHost));
+        off += (size_t)G.w * G.h;
+    }
+    HIPOK(hipMemcpy(cand, c->d_cand.p, (size_t)P.n_slots_total * 4, hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(cand_cnt, c->d_cand_cnt.p, (size_t)P.n_cells_total * 4, hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(lvl, c->d_lvl_kp.p, (size_t)P.kp_slots_total * sizeof(LevelKp), hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(lvl_cnt, c->d_lvl_cnt.p, (size_t)P.n_levels * 4, hipMemcpyDeviceToHost));
+    HIPOK(hipMemcpy(lvl_nlap, c->d_lvl_nlap.p, (size_t)P.n_levels * 4, hipMemcpyDeviceToHost));
+    int err[4];
+    HIPOK(hipMemcpy(err, c->d_err.p, sizeof(err), hipMemcpyDeviceToHost));
+    sizes[3] = err[0];
+    return ORBHIP_OK;
+}
+
+// Cell table of a plan (level, x0, y0, wc, hc, slot_off per cell) for offline checks.
+int orbhip_test_cells(orbhip_ctx* c, int w, int h, int32_t* out6, int cap) {
+    if (!c) return ORBHIP_ERR_ARG;
+    Plan* pl = nullptr;
+    int rc = build_plan(c, w, h, &pl);
+    if (rc) return rc;
+    const int n = (int)pl->cells.size();
+    if (n > cap) return n;
+    for (int i = 0; i < n; i++) {
+        const CellGeom& g = pl->cells[i];
+        out6[6 * i + 0] = g.level; out6[6 * i + 1] = g.x0; out6[6 * i + 2] = g.y0;
+        out6[6 * i + 3] = g.wc; out6[6 * i + 4] = g.hc; out6[6 * i + 5] = g.slot_off;
+    }
+    return n;
+}
+
+}  // extern "C"

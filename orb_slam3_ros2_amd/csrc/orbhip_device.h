@@ -1,0 +1,154 @@
+// Device-side numeric helpers shared by the gfx950 kernels.
+// Every routine here reproduces a host libm / OpenCV result bit-for-bit; all
+// translation units are compiled with -ffp-contract=off so no FMA is formed.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace orbhip {
+
+// cvRound(float) on x86 (cvtss2si, MXCSR round-to-nearest-even)
+__device__ __forceinline__ int cv_round(float v) { return (int)__builtin_rintf(v); }
+
+// ---------------------------------------------------------------------------
+// glibc 2.35 sinf/cosf (sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c, sincosf.h):
+// double-precision polynomial after a 2^24-prescaled quadrant reduction. This
+// restatement matches glibc bit-for-bit on every float in [0, 6.2832]
+// (exhaustive host check, tests/test_sincosf.py; device check in the gpu tests),
+// which is the whole domain the rBRIEF angle (fastAtan2 degrees * pi/180) spans.
+// The reference calls std::cos/std::sin on a float (U:src/ORBextractor.cc::
+// computeOrbDescriptor), i.e. glibc cosf/sinf.
+// ---------------------------------------------------------------------------
+struct SinCosTab {
+    double sign[4];
+    double hpi_inv, hpi, c0, c1, c2, c3, c4, s1, s2, s3;
+};
+
+static __constant__ SinCosTab kSinCosTab[2] = {
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, 0x1p0, -0x1.ffffffd0c621cp-2,
+     0x1.55553e1068f19p-5, -0x1.6c087e89a359dp-10, 0x1.99343027bf8c3p-16, -0x1.555545995a603p-3,
+     0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13},
+    {{1.0, -1.0, -1.0, 1.0}, 0x1.45F306DC9C883p+23, 0x1.921FB54442D18p0, -0x1p0, 0x1.ffffffd0c621cp-2,
+     -0x1.55553e1068f19p-5, 0x1.6c087e89a359dp-10, -0x1.99343027bf8c3p-16, -0x1.555545995a603p-3,
+     0x1.1107605230bc4p-7, -0x1.994eb3774cf24p-13}};
+
+__device__ __forceinline__ const SinCosTab& sincos_tab(int i) { return kSinCosTab[i]; }
+
+__device__ __forceinline__ uint32_t abstop12(float x) { return (__float_as_uint(x) >> 20) & 0x7ff; }
+
+__device__ __forceinline__ float sincosf_poly(double x, double x2, const SinCosTab& p, int n) {
+    if ((n & 1) == 0) {
+        double x3 = x * x2;
+        double s1 = p.s2 + x2 * p.s3;
+        double x7 = x3 * x2;
+        double s = x + x3 * p.s1;
+        return (float)(s + x7 * s1);
+    } else {
+        double x4 = x2 * x2;
+        double c2 = p.c3 + x2 * p.c4;
+        double c1 = p.c0 + x2 * p.c1;
+        double x6 = x4 * x2;
+        double c = c1 + x4 * p.c2;
+        return (float)(c + x6 * c2);
+    }
+}
+
+__device__ __forceinline__ double sincosf_reduce(double x, const SinCosTab& p, int* np) {
+    double r = x * p.hpi_inv;
+    int n = ((int32_t)r + 0x800000) >> 24;
+    *np = n;
+    return x - n * p.hpi;
+}
+
+// Valid for |y| < 120 (the range-reduction branch glibc uses up to 120.0f).
+__device__ __forceinline__ float glibc_sinf(float y) {
+    double x = y;
+    if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {
+        double s = x * x;
+        if (abstop12(y) < abstop12(0x1p-12f)) return y;
+        return sincosf_poly(x, s, sincos_tab(0), 0);
+    }
+    int n;
+    x = sincosf_reduce(x, sincos_tab(0), &n);
+    double s = sincos_tab(0).sign[n & 3];
+    return sincosf_poly(x * s, x * x, sincos_tab((n & 2) ? 1 : 0), n);
+}
+
+__device__ __forceinline__ float glibc_cosf(float y) {
+    double x = y;
+    if (abstop12(y) < abstop12(0x1.921FB6p-1f)) {
+        double x2 = x * x;
+        if (abstop12(y) < abstop12(0x1p-12f)) return 1.0f;
+        return sincosf_poly(x, x2, sincos_tab(0), 1);
+    }
+    int n;
+    x = sincosf_reduce(x, sincos_tab(0), &n);
+    double s = sincos_tab(0).sign[n & 3];
+    return sincosf_poly(x * s, x * x, sincos_tab((n & 2) ? 1 : 0), n ^ 1);
+}
+
+// OCV:core mathfuncs_core atan_f32 == cv::fastAtan2(y, x), degrees in [0, 360)
+__device__ __forceinline__ float fast_atan2(float y, float x) {
+    const float p1 = 0.9997878412794807f * 57.295780181884765625f;   // (float)(180/CV_PI)
+    const float p3 = -0.3258083974640975f * 57.295780181884765625f;
+    const float p5 = 0.1555786518463281f * 57.295780181884765625f;
+    const float p7 = -0.04432655554792128f * 57.295780181884765625f;
+    const float eps = (float)2.220446049250313e-16;                  // (float)DBL_EPSILON
+    float ax = fabsf(x), ay = fabsf(y);
+    float a, c, c2;
+    if (ax >= ay) {
+        c = ay / (ax + eps);
+        c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        c = ax / (ay + eps);
+        c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// ---------------------------------------------------------------------------
+// wave64 / block helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ int wave_sum_i32(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// inclusive prefix sum within a wave64
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+// Exclusive block scan of one int per thread. `scratch` >= blockDim/64 + 1 ints of LDS.
+// Returns the exclusive prefix; *total receives the block sum. Contains __syncthreads.
+__device__ __forceinline__ int block_excl_scan(int v, int* scratch, int* total) {
+    const int lane = lane_id(), wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+    int inc = wave_incl_scan(v);
+    if (lane == 63) scratch[wid] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int s = 0;
+        for (int i = 0; i < nw; i++) { int t = scratch[i]; scratch[i] = s; s += t; }
+        scratch[nw] = s;
+    }
+    __syncthreads();
+    int res = scratch[wid] + inc - v;
+    *total = scratch[nw];
+    __syncthreads();
+    return res;
+}
+
+}  // namespace orbhip

@@ -1,0 +1,53 @@
+// Host-visible launchers of the gfx950 kernels (one TU per kernel family, no RDC).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/orbhip.h"
+#include "orbhip_plan.h"
+
+namespace orbhip {
+
+struct FrameBufs {
+    const uint8_t* in;     // level 0: caller frames
+    int in_stride;
+    int64_t in_fstride;
+    uint8_t* pyr;          // levels >= 1
+};
+
+struct OctreeCfg {
+    int node_cap;          // LDS node capacity (>= max list size of any level)
+    int sort_cap;          // power of two >= node_cap
+    int key_cap;           // keys kept in LDS when a level has <= key_cap candidates
+    int lap0, lap1;        // vLappingArea
+};
+
+// ---- extraction ----
+void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, int B, int l,
+                   const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st);
+void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,
+                 uint32_t* cand, int* cand_cnt, hipStream_t st);
+size_t octree_lds_bytes(const ExtractPlan& hP, const OctreeCfg& cfg);
+bool octree_set_lds_limit(size_t bytes);
+void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const uint32_t* cand,
+                   const int* cand_cnt, uint32_t* kscratch, uint16_t* nscratch, LevelKp* lvl_kp, int* lvl_cnt,
+                   int* lvl_nlap, const OctreeCfg& cfg, int* err, int B, hipStream_t st);
+void launch_desc(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, const LevelKp* lvl_kp,
+                 const int* lvl_cnt, const int* lvl_nlap, const int* disc, orbhip_kp* out_kps, uint8_t* out_desc,
+                 int cap, int* n_out, int* mono_out, int B, hipStream_t st);
+
+// ---- matching ----
+void launch_match_pairs(const orbhip_kp* kps, const uint8_t* desc, const int32_t* n, int npairs, int cap,
+                        int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best,
+                        int32_t* second, int32_t* nmatch, hipStream_t st);
+void launch_match_bf(const uint8_t* q, const float* qa, int nq, const uint8_t* t, const float* ta, int nt,
+                     int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best,
+                     int32_t* second, int32_t* nmatch, hipStream_t st);
+
+// ---- test hooks ----
+void launch_sincos_probe(const float* x, float* c, float* s, int64_t n, hipStream_t st);
+void launch_sincos_sweep(uint32_t lo_bits, uint32_t hi_bits, const float* ref_c, const float* ref_s,
+                         unsigned long long* mismatches, hipStream_t st);
+
+}  // namespace orbhip

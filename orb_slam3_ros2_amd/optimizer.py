@@ -1,0 +1,99 @@
+"""Optimizer mirror (U:src/Optimizer.cc) over liborbhip.so.
+
+``Optimizer.LocalBundleAdjustment(problem)`` runs the g2o problem LocalBundleAdjustment
+builds (VertexSE3Expmap poses, marginalised VertexSBAPointXYZ points, EdgeSE3ProjectXYZ
+mono edges with Huber sqrt(5.991), BlockSolver_6_3 + Levenberg, optimize(10)) on the GPU
+and returns the optimised poses/points and the per-edge chi2 / depth flags that the
+reference uses to erase outlier observations (chi2 > 5.991 or depth <= 0).
+``Optimizer.BundleAdjustment`` is the same solver with the GBA defaults.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import BAProblemC, BAResultC, Context, check, lib, ptr
+
+TH_HUBER_MONO = float(np.sqrt(np.float32(5.991)))
+
+
+@dataclass
+class BAProblem:
+    pose_q: np.ndarray          # [P,4] float32 (x,y,z,w), Tcw rotation
+    pose_t: np.ndarray          # [P,3] float32
+    pose_fixed: np.ndarray      # [P] uint8
+    points: np.ndarray          # [M,3] float32 world
+    edge_pose: np.ndarray       # [E] int32
+    edge_point: np.ndarray      # [E] int32
+    edge_uv: np.ndarray         # [E,2] float32
+    edge_octave: np.ndarray     # [E] int32
+    inv_sigma2: np.ndarray      # [L] float32
+    fx: float
+    fy: float
+    cx: float
+    cy: float
+    huber_delta: float = TH_HUBER_MONO
+    iterations: int = 10
+    early_stop: int = 0
+
+    def normalized(self) -> "BAProblem":
+        c = lambda a, dt: np.ascontiguousarray(a, dtype=dt)  # noqa: E731
+        return BAProblem(c(self.pose_q, np.float32), c(self.pose_t, np.float32), c(self.pose_fixed, np.uint8),
+                         c(self.points, np.float32), c(self.edge_pose, np.int32), c(self.edge_point, np.int32),
+                         c(self.edge_uv, np.float32), c(self.edge_octave, np.int32), c(self.inv_sigma2, np.float32),
+                         float(self.fx), float(self.fy), float(self.cx), float(self.cy), float(self.huber_delta),
+                         int(self.iterations), int(self.early_stop))
+
+    def to_c(self) -> BAProblemC:
+        return BAProblemC(self.pose_q.shape[0], self.points.shape[0], self.edge_pose.shape[0], ptr(self.pose_q),
+                          ptr(self.pose_t), ptr(self.pose_fixed), ptr(self.points), ptr(self.edge_pose),
+                          ptr(self.edge_point), ptr(self.edge_uv), ptr(self.edge_octave), ptr(self.inv_sigma2),
+                          self.inv_sigma2.shape[0], self.fx, self.fy, self.cx, self.cy, self.huber_delta,
+                          self.iterations, self.early_stop)
+
+
+@dataclass
+class BAResult:
+    pose_q: np.ndarray
+    pose_t: np.ndarray
+    points: np.ndarray
+    edge_chi2: np.ndarray
+    edge_depth_ok: np.ndarray
+    initial_chi2: float
+    final_chi2: float
+    iterations_done: int
+    lm_trials: int
+
+    def outlier_edges(self, th: float = 5.991) -> np.ndarray:
+        """Edges LocalBundleAdjustment erases: chi2 > 5.991 || !isDepthPositive()."""
+        return np.nonzero((self.edge_chi2 > th) | (self.edge_depth_ok == 0))[0]
+
+
+class Optimizer:
+    def __init__(self, device: int = 0, ctx: Context | None = None):
+        self.ctx = ctx or Context(device)
+
+    def solve(self, prob: BAProblem, stop_flag: ctypes.c_int | None = None) -> BAResult:
+        p = prob.normalized()
+        P, M, E = p.pose_q.shape[0], p.points.shape[0], p.edge_pose.shape[0]
+        out = BAResult(np.zeros((P, 4), np.float32), np.zeros((P, 3), np.float32), np.zeros((M, 3), np.float32),
+                       np.zeros(E, np.float32), np.zeros(E, np.uint8), 0.0, 0.0, 0, 0)
+        rc = BAResultC(ptr(out.pose_q), ptr(out.pose_t), ptr(out.points), ptr(out.edge_chi2),
+                       ptr(out.edge_depth_ok), 0.0, 0.0, 0, 0)
+        pc = p.to_c()
+        sf = ctypes.addressof(stop_flag) if stop_flag is not None else None
+        check(lib().orbhip_ba_solve(self.ctx.handle, ctypes.byref(pc), ctypes.byref(rc), sf), "orbhip_ba_solve")
+        out.initial_chi2, out.final_chi2 = rc.initial_chi2, rc.final_chi2
+        out.iterations_done, out.lm_trials = rc.iterations_done, rc.lm_trials
+        return out
+
+    def LocalBundleAdjustment(self, prob: BAProblem, stop_flag=None) -> BAResult:
+        return self.solve(prob, stop_flag)
+
+    def BundleAdjustment(self, prob: BAProblem, nIterations: int = 20, bRobust: bool = True,
+                         stop_flag=None) -> BAResult:
+        p = BAProblem(**{**prob.__dict__, "iterations": nIterations,
+                         "huber_delta": float(np.sqrt(5.99)) if bRobust else 0.0})
+        return self.solve(p, stop_flag)
