@@ -47,6 +47,9 @@ def lib():
         L.orc_descriptor_distance.argtypes = [_u8p, _u8p]
         L.orc_match_bf.argtypes = [_u8p, _f32p, c_int, _u8p, _f32p, c_int, c_int, c_float, c_int,
                                    _i32p, _i32p, _i32p]
+        L.orc_ba_solve.argtypes = [c_int, c_int, c_int, _f32p, _f32p, _u8p, _f32p, _i32p, _i32p, _f32p, _i32p,
+                                   _f32p, c_float, c_float, c_float, c_float, c_float, c_int, c_int, _f32p, _f32p,
+                                   _f32p, _f32p, _u8p, _f64p]
         L.orc_glibc_sincosf_range.argtypes = [ctypes.c_uint32, ctypes.c_uint32, _f32p, _f32p]
         _lib = L
     return _lib
@@ -137,3 +140,16 @@ def glibc_sincosf_range(lo_bits: int, hi_bits: int):
     c = np.empty(n, np.float32); s = np.empty(n, np.float32)
     lib().orc_glibc_sincosf_range(lo_bits, hi_bits, c, s)
     return c, s
+
+
+def ba_solve(prob):
+    """Oracle LM/Schur solve of an orb_slam3_ros2_amd.optimizer.BAProblem. Returns a dict."""
+    p = prob.normalized()
+    P, M, E = p.pose_q.shape[0], p.points.shape[0], p.edge_pose.shape[0]
+    oq = np.zeros((P, 4), np.float32); ot = np.zeros((P, 3), np.float32); op = np.zeros((M, 3), np.float32)
+    oc = np.zeros(E, np.float32); od = np.zeros(E, np.uint8); st = np.zeros(4, np.float64)
+    lib().orc_ba_solve(P, M, E, p.pose_q, p.pose_t, p.pose_fixed, p.points, p.edge_pose, p.edge_point, p.edge_uv,
+                       p.edge_octave, p.inv_sigma2, p.fx, p.fy, p.cx, p.cy, p.huber_delta, p.iterations,
+                       p.early_stop, oq, ot, op, oc, od, st)
+    return dict(pose_q=oq, pose_t=ot, points=op, edge_chi2=oc, edge_depth_ok=od, initial_chi2=st[0],
+                final_chi2=st[1], iterations_done=int(st[2]), lm_trials=int(st[3]))

@@ -39,3 +39,120 @@ def shifted_frame(base: np.ndarray, dx: int, dy: int, seed: int, noise_sigma: fl
     img = base[ys][:, xs].astype(np.float64)
     img += rng.normal(0.0, noise_sigma, size=img.shape)
     return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+
+
+# ---------------------------------------------------------------------------
+# Bundle-adjustment problems
+# ---------------------------------------------------------------------------
+D435I = dict(fx=614.67, fy=617.63, cx=326.22, cy=245.58, w=640, h=480)   # R:config/Monocular/RealSense_D435i.yaml:16-29
+
+
+def _rodrigues(w):
+    th = np.linalg.norm(w)
+    if th < 1e-12:
+        return np.eye(3)
+    k = w / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * (K @ K)
+
+
+def _mat_to_quat(R):
+    """(x, y, z, w), w >= 0."""
+    t = np.trace(R)
+    if t > 0:
+        s = np.sqrt(t + 1.0) * 2
+        w, x, y, z = 0.25 * s, (R[2, 1] - R[1, 2]) / s, (R[0, 2] - R[2, 0]) / s, (R[1, 0] - R[0, 1]) / s
+    else:
+        i = int(np.argmax(np.diag(R)))
+        j, k = (i + 1) % 3, (i + 2) % 3
+        s = np.sqrt(R[i, i] - R[j, j] - R[k, k] + 1.0) * 2
+        q = np.zeros(3)
+        q[i] = 0.25 * s
+        w = (R[k, j] - R[j, k]) / s
+        q[j] = (R[j, i] + R[i, j]) / s
+        q[k] = (R[k, i] + R[i, k]) / s
+        x, y, z = q
+    q = np.array([x, y, z, w])
+    if q[3] < 0:
+        q = -q
+    return q / np.linalg.norm(q)
+
+
+def _look_at(c, target=np.zeros(3)):
+    """Rcw for a camera at c looking at target (camera z forward, y down)."""
+    z = target - c
+    z /= np.linalg.norm(z)
+    up = np.array([0.0, -1.0, 0.0])
+    x = np.cross(up, z)
+    x /= np.linalg.norm(x)
+    y = np.cross(z, x)
+    return np.stack([x, y, z])   # rows: camera axes in world
+
+
+def synthetic_ba_problem(n_kf=50, n_pts=2000, obs_per_pt=4, seed=7, layout="arc", window=None,
+                         rot_noise=0.01, trans_noise=0.02, pt_noise=0.05, n_levels=8, scale_factor=1.2):
+    """C4 (layout='arc'): KFs on a 2 m-radius arc looking inward, points uniform in a 1 m cube at
+    the centre, each point seen by `obs_per_pt` distinct KFs. C5 (layout='loop'): KFs around a full
+    circle, each point observed from a `window`-KF sliding window (co-visibility band).
+    Returns (BAProblem with perturbed initial state, ground-truth dict)."""
+    from .optimizer import BAProblem, TH_HUBER_MONO
+    rng = np.random.Generator(np.random.PCG64(seed))
+    cam = D435I
+    if layout == "arc":
+        ang = np.linspace(-np.pi / 3, np.pi / 3, n_kf)
+        radius = 2.0
+    else:
+        ang = np.linspace(0, 2 * np.pi, n_kf, endpoint=False)
+        radius = 4.0
+    Rs, ts = [], []
+    for a in ang:
+        c = np.array([radius * np.sin(a), 0.3 * np.sin(3 * a), -radius * np.cos(a)])
+        R = _look_at(c)
+        Rs.append(R)
+        ts.append(-R @ c)
+    Rs, ts = np.array(Rs), np.array(ts)
+    pts = rng.uniform(-0.5, 0.5, size=(n_pts, 3))
+    edges_pose, edges_pt = [], []
+    for m in range(n_pts):
+        if window is None:
+            kfs = rng.choice(n_kf, obs_per_pt, replace=False)
+        else:
+            start = int(rng.integers(0, n_kf))
+            kfs = (start + rng.choice(window, obs_per_pt, replace=False)) % n_kf
+            # place the point where that window looks (in front of its middle keyframe)
+            mid = (start + window // 2) % n_kf
+            cmid = -Rs[mid].T @ ts[mid]
+            pts[m] = cmid * 0.55 + rng.uniform(-0.4, 0.4, size=3)
+        for k in sorted(kfs.tolist()):
+            edges_pose.append(k)
+            edges_pt.append(m)
+    edges_pose = np.array(edges_pose, np.int32)
+    edges_pt = np.array(edges_pt, np.int32)
+    E = len(edges_pose)
+    octave = rng.integers(0, n_levels, size=E).astype(np.int32)
+    scales = np.ones(n_levels, np.float32)
+    for i in range(1, n_levels):
+        scales[i] = np.float32(np.float64(scales[i - 1]) * np.float64(np.float32(scale_factor)))
+    inv_sigma2 = (np.float32(1.0) / (scales * scales)).astype(np.float32)
+    Xc = np.einsum("eij,ej->ei", Rs[edges_pose], pts[edges_pt]) + ts[edges_pose]
+    uv = np.stack([cam["fx"] * Xc[:, 0] / Xc[:, 2] + cam["cx"], cam["fy"] * Xc[:, 1] / Xc[:, 2] + cam["cy"]], 1)
+    sig = np.power(np.float64(scale_factor), octave)
+    uv += rng.normal(size=uv.shape) * sig[:, None]
+    # perturbed initial state (KF0 stays at ground truth and is fixed)
+    q0, t0 = [], []
+    for k in range(n_kf):
+        if k == 0:
+            R, t = Rs[k], ts[k]
+        else:
+            R = _rodrigues(rng.normal(size=3) * rot_noise) @ Rs[k]
+            t = ts[k] + rng.normal(size=3) * trans_noise
+        q0.append(_mat_to_quat(R))
+        t0.append(t)
+    fixed = np.zeros(n_kf, np.uint8)
+    fixed[0] = 1
+    p0 = pts + rng.normal(size=pts.shape) * pt_noise
+    prob = BAProblem(np.array(q0, np.float32), np.array(t0, np.float32), fixed, p0.astype(np.float32), edges_pose,
+                     edges_pt, uv.astype(np.float32), octave, inv_sigma2, np.float32(cam["fx"]),
+                     np.float32(cam["fy"]), np.float32(cam["cx"]), np.float32(cam["cy"]), TH_HUBER_MONO, 10, 0)
+    gt = dict(R=Rs, t=ts, points=pts)
+    return prob, gt

@@ -1,0 +1,96 @@
+"""GPU parity: Hamming brute-force matcher (DescriptorDistance, best/second, TH_LOW, ratio,
+rotation histogram) vs the oracle, on extractor outputs and on the SURVEY §8(d) microbench."""
+import numpy as np
+import pytest
+
+from orb_slam3_ros2_amd.synthetic import shifted_frame, synthetic_frame
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def matcher():
+    from orb_slam3_ros2_amd import ORBmatcher
+    return ORBmatcher(0.9, True)
+
+
+def _cmp(matcher, oracle, q, qa, t, ta, th=50, ratio=0.9, ori=True):
+    matcher.mfNNratio, matcher.mbCheckOrientation = ratio, ori
+    n, m, b, s = matcher.match_bf(q, qa, t, ta, th)
+    on, om, ob, os_ = oracle.match_bf(q, qa, t, ta, th, ratio, ori)
+    assert np.array_equal(b, ob) and np.array_equal(s, os_)
+    assert np.array_equal(m, om) and n == on
+    return n
+
+
+def test_microbench_flips(matcher, oracle):
+    rng = np.random.default_rng(1234)
+    q = rng.integers(0, 256, (1000, 32), dtype=np.uint8)
+    t = q.copy()
+    for i in range(1000):
+        for bit in rng.choice(256, int(rng.integers(0, 41)), replace=False):
+            t[i, bit // 8] ^= np.uint8(1 << (bit % 8))
+    t = np.concatenate([t, rng.integers(0, 256, (1000, 32), dtype=np.uint8)])[rng.permutation(2000)]
+    qa = rng.uniform(0, 360, 1000).astype(np.float32)
+    ta = rng.uniform(0, 360, 2000).astype(np.float32)
+    for ori in (False, True):
+        _cmp(matcher, oracle, q, qa, t, ta, ori=ori)
+
+
+def test_extracted_frame_pair(matcher, oracle):
+    from orb_slam3_ros2_amd import ORBextractor
+    ext = ORBextractor(1000)
+    a = synthetic_frame(100)
+    b = shifted_frame(a, 3, -2, 101)
+    _, ka, da = ext(a)
+    _, kb, db = ext(b)
+    n = _cmp(matcher, oracle, da, ka["angle"], db, kb["angle"])
+    assert n > 300
+    _cmp(matcher, oracle, da, ka["angle"], db, kb["angle"], th=100, ratio=0.6)
+
+
+def test_ties_and_tiles(matcher, oracle):
+    """duplicate train descriptors (first index wins), > 1024 trains (multiple LDS tiles)."""
+    rng = np.random.default_rng(7)
+    base = rng.integers(0, 256, (700, 32), dtype=np.uint8)
+    t = np.concatenate([base, base, base])          # every query has 3 exact ties
+    q = base[rng.permutation(700)[:300]]
+    a = np.zeros(300, np.float32)
+    ta = np.zeros(2100, np.float32)
+    _cmp(matcher, oracle, q, a, t, ta, ratio=1.01)   # ratio > 1 so ties (d < r*d) can be accepted
+
+
+def test_empty_sets(matcher, oracle):
+    q = np.zeros((5, 32), np.uint8)
+    n, m, b, s = matcher.match_bf(q, np.zeros(5, np.float32), np.zeros((0, 32), np.uint8), np.zeros(0, np.float32))
+    assert n == 0 and np.all(m == -1)
+
+
+def test_pairs_device(oracle):
+    import torch
+    from orb_slam3_ros2_amd import ORBextractor, ORBmatcher
+    ext = ORBextractor(1000)
+    mt = ORBmatcher(0.9, True, ctx=ext.ctx)
+    B, H, W = 4, 480, 640
+    frames = [synthetic_frame(200)]
+    for i in range(1, B):
+        frames.append(shifted_frame(frames[-1], 2, 1, 200 + i))
+    frames = np.stack(frames)
+    cap = ext.max_keypoints(W, H)
+    dev = torch.device("cuda:0")
+    kps = torch.zeros((B, cap, 6), dtype=torch.float32, device=dev)
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
+    n = torch.zeros(B, dtype=torch.int32, device=dev)
+    mono = torch.zeros(B, dtype=torch.int32, device=dev)
+    ext.extract_batch_device(torch.from_numpy(frames).to(dev), kps, desc, n, mono)
+    mm = torch.zeros((B - 1, cap), dtype=torch.int32, device=dev)
+    bb = torch.zeros_like(mm); ss = torch.zeros_like(mm)
+    nm = torch.zeros(B - 1, dtype=torch.int32, device=dev)
+    mt.match_pairs_device(kps, desc, n, mm, bb, ss, nm)
+    torch.cuda.synchronize()
+    for p in range(B - 1):
+        nq, nt = int(n[p]), int(n[p + 1])
+        q = desc[p, :nq].cpu().numpy(); t = desc[p + 1, :nt].cpu().numpy()
+        qa = kps[p, :nq, 3].cpu().numpy(); ta = kps[p + 1, :nt, 3].cpu().numpy()
+        on, om, ob, os_ = oracle.match_bf(q, qa, t, ta, 50, 0.9, True)
+        assert int(nm[p]) == on and np.array_equal(mm[p, :nq].cpu().numpy(), om)
