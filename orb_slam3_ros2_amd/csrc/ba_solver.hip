@@ -343,10 +343,10 @@ constexpr int kCholNB = 16;
 __global__ __launch_bounds__(1024) void k_ba_cholesky(double* __restrict__ S, const double* __restrict__ bs,
                                                       double* __restrict__ x, int n, int* __restrict__ flag) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    double* Dg = lds;                        // 16 x 16 diagonal block
-    double* y = lds + 256;                   // n (solution vector)
+    int& bad = *(int*)lds;                   // control word (first 16 bytes)
+    double* Dg = lds + 2;                    // 16 x 16 diagonal block
+    double* y = Dg + 256;                    // n (solution vector)
     double* Pn = y + ((n + 15) & ~15);       // panel rows (n_pad x 16)
-    __shared__ int bad;
     const int tid = threadIdx.x, nt = blockDim.x;
     const int wid = tid >> 6, lane = tid & 63, nw = nt >> 6;
     if (tid == 0) bad = 0;
@@ -768,13 +768,14 @@ int ba_solve(BaWorkspace* ws, const orbhip_ba_problem* pr, orbhip_ba_result* res
     a.pt_ptr = ws->pt_ptr.p; a.pt_edges = ws->pt_edges.p; a.ps_ptr = ws->ps_ptr.p; a.ps_edges = ws->ps_edges.p;
     a.blk_i = ws->blk_i.p; a.blk_j = ws->blk_j.p; a.blk_ptr = ws->blk_ptr.p; a.blk_pairs = ws->blk_pairs.p;
     a.nblk = nblk; a.red = ws->red.p; a.flag = ws->flag.p;
-    const size_t chol_lds = sizeof(double) * (256 + ((n + 15) & ~15) + (size_t)((n + 15) & ~15) * 16);
+    const size_t chol_lds = sizeof(double) * (2 + 256 + ((n + 15) & ~15) + (size_t)((n + 15) & ~15) * 16);
     if (chol_lds > 160 * 1024) return ORBHIP_ERR_UNSUPPORTED;
     static bool lds_set = false;
     if (!lds_set) {
         BAOK(hipFuncSetAttribute((const void*)k_ba_cholesky, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         lds_set = true;
     }
+    (void)hipGetLastError();   // clear any sticky error left by an earlier, already-reported call
     auto g = [](int n_, int b_) { return dim3((unsigned)std::max(1, (n_ + b_ - 1) / b_)); };
     auto read_red = [&](int what) -> int {
         BAOK(hipMemcpyAsync(ws->h_red, ws->red.p, 4 * sizeof(double), hipMemcpyDeviceToHost, st));

@@ -326,6 +326,7 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
                        int lap1, orbhip_kp* d_kps, uint8_t* d_desc, int cap, int32_t* d_n, int32_t* d_mono,
                        hipStream_t st) {
     const ExtractPlan& P = pl->h;
+    (void)hipGetLastError();   // clear a sticky error of an earlier, already-reported call
     int rc = ensure_batch(c, pl, B);
     if (rc) return rc;
     FrameBufs fb;
@@ -491,6 +492,7 @@ int orbhip_match_bf(orbhip_ctx* c, const uint8_t* q, const float* qa, int nq, co
         // no train descriptors: every query keeps best = second = 256 (no match)
         HIPOK(hipMemsetAsync(c->d_mm.p, 0xFF, (size_t)nq * 4, st));
     }
+    (void)hipGetLastError();
     launch_match_bf(c->d_mq.p, c->d_mqa.p, nq, c->d_mt.p, c->d_mta.p, nt, th_low, ratio, check_orientation, c->d_mm.p,
                     c->d_mb.p, c->d_ms.p, c->d_mn.p, st);
     HIPOK(hipGetLastError());
@@ -510,6 +512,7 @@ int orbhip_match_pairs_device(orbhip_ctx* c, const orbhip_kp* d_kps, const uint8
         return ORBHIP_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    (void)hipGetLastError();
     launch_match_pairs(d_kps, d_desc, d_n, B - 1, cap, th_low, ratio, check_orientation, d_match, d_best, d_second,
                        d_nmatch, st);
     HIPOK(hipGetLastError());
