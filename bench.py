@@ -1,0 +1,363 @@
+#!/usr/bin/env python3
+"""bench.py — headline benchmark of the MI355X ORB front-end + BA back-end.
+
+BASELINE.json metric: "frames/sec ORB extract+match @640x480; KF/sec LocalBA (50 KF, 2k pts)".
+
+Workload of `value` (configs[1]): one step = ONE 640x480 synthetic frame (device-resident)
+through the full ORBextractor::operator() path (8 levels, 1000 features, FAST 20/7, octree,
+IC_Angle, rBRIEF) plus the brute-force Hamming match against the previous frame (TH_LOW 50,
+ratio 0.9, rotation check) — batch 1, the tracking-thread regime. value = frames/s summed over
+ranks (weak scaling: every rank streams its own frames, no collective on the data path).
+
+Extra lines in the same JSON object (rank 0): C3 (1280x720 batch 64 extract + 63-pair match),
+C4 LocalBundleAdjustment (50 KF / 2000 pts / 8000 obs, 10 LM iterations, host API incl.
+H2D/D2H) in LBA/s == KF/s, the roofline of the dominant kernel measured live with HIP events
+on its launch stream, and the CPU baseline (oracle/ restatement timed on this host's cores).
+
+Usage: python bench.py [--gpus N --steps K --warmup W]  (torchrun for N > 1)
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+STAGES = {1: "k_resize (7 levels)", 2: "k_fast_cells", 3: "k_octree", 4: "k_desc", 5: "k_match_top2",
+          6: "k_rot_filter"}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-extra", action="store_true", help="skip the C3 / LBA extra lines")
+    ap.add_argument("--c3-steps", type=int, default=10)
+    ap.add_argument("--lba-steps", type=int, default=20)
+    return ap.parse_args()
+
+
+def _dist_setup(args):
+    import torch
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return ws, rank, local
+
+
+def _barrier(ws):
+    import torch
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def _max_over_ranks(ws, v: float) -> float:
+    if ws == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _sum_over_ranks(ws, v: float) -> float:
+    if ws == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def make_stream_frames(n, w, h, seed0):
+    from orb_slam3_ros2_amd.synthetic import shifted_frame, synthetic_frame
+    fr = [synthetic_frame(seed0, w, h)]
+    for i in range(1, n):
+        fr.append(shifted_frame(fr[-1], 2 + (i % 3), 1 - (i % 2), seed0 + i))
+    return np.stack(fr)
+
+
+class Profiler:
+    def __init__(self, ctx):
+        from orb_slam3_ros2_amd._lib import lib
+        self.L, self.ctx = lib(), ctx
+
+    def select(self, stage):
+        self.L.orbhip_profile_stage(self.ctx.handle, int(stage))
+
+    def collect(self):
+        ms, n = ctypes.c_double(0), ctypes.c_int32(0)
+        self.L.orbhip_profile_collect(self.ctx.handle, ctypes.byref(ms), ctypes.byref(n))
+        return ms.value, n.value
+
+
+# ---------------------------------------------------------------------------------------
+# C2: batch-1 stream of 640x480 frames, extract + match to the previous frame
+# ---------------------------------------------------------------------------------------
+class StreamC2:
+    W, H, NF = 640, 480, 32
+
+    def __init__(self, rank):
+        import torch
+        from orb_slam3_ros2_amd import ORBextractor, ORBmatcher
+        from orb_slam3_ros2_amd._lib import lib
+        self.torch = torch
+        self.L = lib()
+        self.ext = ORBextractor(1000, 1.2, 8, 20, 7)
+        self.mt = ORBmatcher(0.9, True, ctx=self.ext.ctx)
+        self.cap = self.ext.max_keypoints(self.W, self.H)
+        dev = torch.device("cuda")
+        self.frames_np = make_stream_frames(self.NF, self.W, self.H, 1000 * rank + 1)
+        self.frames = torch.from_numpy(self.frames_np).to(dev)
+        self.kps = torch.zeros((2, self.cap, 6), dtype=torch.float32, device=dev)
+        self.desc = torch.zeros((2, self.cap, 32), dtype=torch.uint8, device=dev)
+        self.n = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.mono = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.mm = torch.zeros((3, self.cap), dtype=torch.int32, device=dev)
+        self.nm = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.stream = torch.cuda.current_stream()
+        self.st = ctypes.c_void_p(self.stream.cuda_stream)
+        self.s = 0
+
+    def step(self):
+        s, L, c = self.s, self.L, self.ext.ctx.handle
+        cur, prev = s & 1, (s + 1) & 1
+        f = self.frames[s % self.NF]
+        rc = L.orbhip_extract_batch_device(c, f.data_ptr(), 1, self.W, self.H, self.W, self.W * self.H, 0, 1000,
+                                           self.kps[cur].data_ptr(), self.desc[cur].data_ptr(), self.cap,
+                                           self.n[cur:].data_ptr(), self.mono[cur:].data_ptr(), self.st)
+        assert rc == 0, rc
+        rc = L.orbhip_match_frames_device(c, self.kps[prev].data_ptr(), self.desc[prev].data_ptr(),
+                                          self.n[prev:].data_ptr(), self.kps[cur].data_ptr(),
+                                          self.desc[cur].data_ptr(), self.n[cur:].data_ptr(), self.cap, 50,
+                                          ctypes.c_float(0.9), 1, self.mm[0].data_ptr(), self.mm[1].data_ptr(),
+                                          self.mm[2].data_ptr(), self.nm.data_ptr(), self.st)
+        assert rc == 0, rc
+        self.s += 1
+
+    def stage_bytes(self):
+        """Algorithmic HBM bytes per launch of each stage for one 640x480 frame."""
+        info = self.ext.level_info(self.W, self.H)
+        A = (info["w"].astype(np.int64) * info["h"]).tolist()
+        n_kp = float(self.n.float().mean().item()) or 1000.0
+        return {1: sum(A[:-1]) + sum(A[1:]), 2: sum(A), 3: 8.0 * 4500 + 8 * n_kp, 4: n_kp * (43 * 43 + 56),
+                5: 2 * n_kp * 32 + n_kp * 12, 6: n_kp * 12}
+
+
+class BatchC3:
+    W, H, B = 1280, 720, 64
+
+    def __init__(self, rank):
+        import torch
+        from orb_slam3_ros2_amd import ORBextractor, ORBmatcher
+        self.ext = ORBextractor(1000, 1.2, 8, 20, 7)
+        self.mt = ORBmatcher(0.9, True, ctx=self.ext.ctx)
+        self.cap = self.ext.max_keypoints(self.W, self.H)
+        dev = torch.device("cuda")
+        self.frames = torch.from_numpy(make_stream_frames(self.B, self.W, self.H, 5000 + 1000 * rank)).to(dev)
+        B, cap = self.B, self.cap
+        self.kps = torch.zeros((B, cap, 6), dtype=torch.float32, device=dev)
+        self.desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
+        self.n = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.mono = torch.zeros(B, dtype=torch.int32, device=dev)
+        self.mm = torch.zeros((3, B - 1, cap), dtype=torch.int32, device=dev)
+        self.nm = torch.zeros(B - 1, dtype=torch.int32, device=dev)
+        self.stream = torch.cuda.current_stream()
+
+    def step(self):
+        self.ext.extract_batch_device(self.frames, self.kps, self.desc, self.n, self.mono, stream=self.stream)
+        self.mt.match_pairs_device(self.kps, self.desc, self.n, self.mm[0], self.mm[1], self.mm[2], self.nm,
+                                   stream=self.stream)
+
+
+def timed(ws, fn, steps, warmup):
+    import torch
+    for _ in range(warmup):
+        fn()
+    _barrier(ws)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    _barrier(ws)
+    return _max_over_ranks(ws, time.perf_counter() - t0)
+
+
+# ---------------------------------------------------------------------------------------
+# CPU baseline: the oracle restatement on this host's cores (bounded sample)
+# ---------------------------------------------------------------------------------------
+def cpu_baseline(frames_np, budget_s=12.0):
+    """Each CPU thread streams frames exactly like a GPU step: extract frame i, match it to
+    frame i-1 (whose extraction was the previous step). frames/s = produced frames / wall."""
+    from oracle import pyoracle as O
+    O.lib()
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cores = max(1, min(cores, 16))
+    nf = len(frames_np)
+
+    def stream(start, count):
+        _, kp, dp = O.extract(frames_np[start % nf])
+        for i in range(1, count + 1):
+            _, kc, dc = O.extract(frames_np[(start + i) % nf])
+            O.match_bf(dp, kp[:, 3], dc, kc[:, 3], 50, 0.9, True)
+            kp, dp = kc, dc
+        return count
+
+    t0 = time.perf_counter()
+    n1 = 0
+    while time.perf_counter() - t0 < budget_s / 4:
+        n1 += stream(n1, 4)
+    t1 = time.perf_counter() - t0
+    single = n1 / t1
+    per_thread = max(4, int((budget_s * 0.75) * single / cores * cores / cores))
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(cores) as ex:
+        done = sum(ex.map(lambda k: stream(k * 7, per_thread), range(cores)))
+    tm = time.perf_counter() - t0
+    return dict(value=done / tm, single=single, cores=cores, frames=done + n1, wall=tm + t1)
+
+
+def cpu_lba(prob, budget_s=8.0):
+    from oracle import pyoracle as O
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cores = max(1, min(cores, 16))
+    t0 = time.perf_counter()
+    n1 = 0
+    while time.perf_counter() - t0 < budget_s / 4:
+        O.ba_solve(prob)
+        n1 += 1
+    t1 = time.perf_counter() - t0
+    total = max(cores, int(budget_s * 0.75 / (t1 / n1)))
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(cores) as ex:
+        list(ex.map(lambda i: O.ba_solve(prob), range(total)))
+    tm = time.perf_counter() - t0
+    return dict(value=total / tm, single=n1 / t1, cores=cores, solves=total + n1)
+
+
+def main():
+    args = parse()
+    import torch
+    ws, rank, local = _dist_setup(args)
+    K, W = args.steps, args.warmup
+    c2 = StreamC2(rank)
+    prof = Profiler(c2.ext.ctx)
+    # ---- find the dominant kernel of the step (short calibration, untimed) ----
+    stage_ms = {}
+    for st in (1, 2, 3, 4, 5, 6):
+        prof.select(st)
+        for _ in range(20):
+            c2.step()
+        ms, n = prof.collect()
+        stage_ms[st] = ms / max(n, 1)
+    prof.select(0)
+    dom = max(stage_ms, key=stage_ms.get)
+    # ---- timed region: K steps, the dominant stage bracketed by HIP events on its stream ----
+    for _ in range(W):
+        c2.step()
+    prof.select(dom)
+    _barrier(ws)
+    t0 = time.perf_counter()
+    for _ in range(K):
+        c2.step()
+    torch.cuda.synchronize()
+    _barrier(ws)
+    elapsed = _max_over_ranks(ws, time.perf_counter() - t0)
+    dom_ms, dom_n = prof.collect()
+    prof.select(0)
+    frames_total = _sum_over_ranks(ws, float(K))
+    value = frames_total / elapsed
+    nkp = float(c2.n.float().mean().item())
+    nmatch = int(c2.nm.item())
+    dom_avg_ms = dom_ms / max(dom_n, 1)
+    dom_bytes = c2.stage_bytes()[dom]
+    achieved = dom_bytes / (dom_avg_ms * 1e-3) / 1e9
+    out = {
+        "metric": "frames/sec ORB extract+match @640×480; KF/sec LocalBA (50 KF, 2k pts)",
+        "value": round(value, 2),
+        "unit": "frames/s",
+        "n_gpus": ws,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": round(1e3 * elapsed / K, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (SURVEY.md 8d rectangles+noise frames, translated stream, seeded)",
+        "config": {"workload": "C2: 640x480, 8-level pyramid, 1000 feat/frame, FAST 20/7, batch=1 stream; "
+                               "ORBextractor::operator() + brute-force Hamming match to the previous frame",
+                   "frames_per_step": 1, "parallelism": f"replicas x{ws} (frame streams, no collective)",
+                   "keypoints_per_frame": round(nkp, 1), "matches_last_pair": nmatch},
+        "roofline": {"kernel": STAGES[dom], "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                     "algorithmic_bytes_per_launch": int(dom_bytes), "avg_launch_ms": round(dom_avg_ms, 5),
+                     "launches_timed": dom_n,
+                     "stage_avg_ms_calibration": {STAGES[k]: round(v, 5) for k, v in stage_ms.items()}},
+    }
+    if rank == 0 and not args.no_extra:
+        extra = {}
+        c3 = BatchC3(rank)
+        t = timed(1, c3.step, args.c3_steps, 2)
+        extra["c3_1280x720_b64_extract_match_frames_per_s"] = round(c3.B * args.c3_steps / t, 1)
+        from orb_slam3_ros2_amd import Optimizer
+        from orb_slam3_ros2_amd.synthetic import synthetic_ba_problem
+        prob, _ = synthetic_ba_problem()
+        opt = Optimizer(ctx=c2.ext.ctx)
+        r = None
+        for _ in range(2):
+            r = opt.LocalBundleAdjustment(prob)
+        t0 = time.perf_counter()
+        for _ in range(args.lba_steps):
+            r = opt.LocalBundleAdjustment(prob)
+        tl = time.perf_counter() - t0
+        extra["c4_lba_kf_per_s"] = round(args.lba_steps / tl, 2)
+        extra["c4_lba_ms"] = round(1e3 * tl / args.lba_steps, 3)
+        extra["c4_lba_trials"] = r.lm_trials
+        extra["c4_lba_chi2"] = [round(r.initial_chi2, 3), round(r.final_chi2, 3)]
+        out["extra"] = extra
+    if rank == 0 and ws == 1 and not args.no_cpu:
+        cb = cpu_baseline(c2.frames_np)
+        out["cpu_baseline"] = {"value": round(cb["value"], 2), "unit": "frames/s", "cores": cb["cores"],
+                               "kind": "port",
+                               "sample": f"oracle/ C++ restatement (g++ -O3), {cb['frames']} frames of the bench's "
+                                         f"640x480 stream, each extract + match to the previous frame, "
+                                         f"{cb['cores']} threads (one frame stream per thread), {cb['wall']:.1f}s wall",
+                               "single_core_value": round(cb["single"], 2)}
+        if "extra" in out:
+            from orb_slam3_ros2_amd.synthetic import synthetic_ba_problem
+            prob, _ = synthetic_ba_problem()
+            cl = cpu_lba(prob)
+            out["cpu_baseline"]["c4_lba_kf_per_s"] = round(cl["value"], 2)
+            out["cpu_baseline"]["c4_lba_single_core_kf_per_s"] = round(cl["single"], 2)
+            out["cpu_baseline"]["c4_lba_sample"] = f"{cl['solves']} oracle LBA solves, {cl['cores']} threads"
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -110,6 +110,24 @@ int orbhip_match_pairs_device(orbhip_ctx* ctx, const orbhip_kp* d_kps, const uin
                               int check_orientation, int32_t* d_match, int32_t* d_best,
                               int32_t* d_second, int32_t* d_nmatch, void* stream);
 
+/* Device form over two arbitrary frames (e.g. frame t vs t-1 in a 2-slot ring): query
+ * set (d_q_kps/d_q_desc, count *d_nq) vs train set (d_t_kps/d_t_desc, count *d_nt), both laid
+ * out like one frame of orbhip_extract_batch_device (cap entries). Outputs (cap entries) and
+ * *d_nmatch on the device. Asynchronous; no host synchronisation. */
+int orbhip_match_frames_device(orbhip_ctx* ctx, const orbhip_kp* d_q_kps, const uint8_t* d_q_desc,
+                               const int32_t* d_nq, const orbhip_kp* d_t_kps, const uint8_t* d_t_desc,
+                               const int32_t* d_nt, int cap, int th_low, float ratio, int check_orientation,
+                               int32_t* d_match, int32_t* d_best, int32_t* d_second, int32_t* d_nmatch,
+                               void* stream);
+
+/* ---- diagnostics: live kernel timing ----------------------------------------------
+ * orbhip_profile_stage selects ONE stage whose launches are bracketed by hipEvents on the
+ * stream they run on (0 off, 1 pyramid resize, 2 FAST cells, 3 octree, 4 orientation +
+ * descriptor, 5 Hamming top-2, 6 rotation filter). orbhip_profile_collect synchronises and
+ * returns the summed duration (ms) and the number of bracketed launches, then resets. */
+int orbhip_profile_stage(orbhip_ctx* ctx, int stage);
+int orbhip_profile_collect(orbhip_ctx* ctx, double* total_ms, int32_t* count);
+
 /* ---- bundle adjustment ------------------------------------------------------------
  * Optimizer::LocalBundleAdjustment / BundleAdjustment problem (SoA, host memory).
  * Poses are Tcw = (q, t): q = unit quaternion (x, y, z, w), t translation, float, as

@@ -154,18 +154,22 @@ __global__ __launch_bounds__(256) void k_rot_filter(MatchView v, int check_orien
 }
 
 static void run_match(const MatchView& v, int npairs, int max_q, int th_low, float ratio, int check_orientation,
-                      int32_t* match, int32_t* best, int32_t* second, int32_t* nmatch, hipStream_t st) {
+                      int32_t* match, int32_t* best, int32_t* second, int32_t* nmatch, hipStream_t st,
+                      StageTimer* timer = nullptr) {
     if (npairs <= 0) return;
     const int qblocks = (max_q + 4 * kQPerWave - 1) / (4 * kQPerWave);
+    if (timer) timer->begin(5, st);
     if (qblocks > 0)
         hipLaunchKernelGGL(k_match_top2, dim3(qblocks, npairs), dim3(256), 0, st, v, th_low, ratio, match, best,
                            second);
+    if (timer) { timer->end(5, st); timer->begin(6, st); }
     hipLaunchKernelGGL(k_rot_filter, dim3(npairs), dim3(256), 0, st, v, check_orientation, match, nmatch);
+    if (timer) timer->end(6, st);
 }
 
 void launch_match_pairs(const orbhip_kp* kps, const uint8_t* desc, const int32_t* n, int npairs, int cap,
                         int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best,
-                        int32_t* second, int32_t* nmatch, hipStream_t st) {
+                        int32_t* second, int32_t* nmatch, hipStream_t st, StageTimer* timer) {
     MatchView v;
     v.qd = desc;
     v.td = desc + (int64_t)cap * 32;
@@ -179,7 +183,27 @@ void launch_match_pairs(const orbhip_kp* kps, const uint8_t* desc, const int32_t
     v.nq = cap;
     v.nt = cap;
     v.out_stride = cap;
-    run_match(v, npairs, cap, th_low, ratio, check_orientation, match, best, second, nmatch, st);
+    run_match(v, npairs, cap, th_low, ratio, check_orientation, match, best, second, nmatch, st, timer);
+}
+
+void launch_match_frames(const orbhip_kp* q_kps, const uint8_t* q_desc, const int32_t* nq, const orbhip_kp* t_kps,
+                         const uint8_t* t_desc, const int32_t* nt, int cap, int th_low, float ratio,
+                         int check_orientation, int32_t* match, int32_t* best, int32_t* second, int32_t* nmatch,
+                         hipStream_t st, StageTimer* timer) {
+    MatchView v;
+    v.qd = q_desc;
+    v.td = t_desc;
+    v.qa = &q_kps[0].angle;
+    v.ta = &t_kps[0].angle;
+    v.angle_stride = (int)(sizeof(orbhip_kp) / sizeof(float));
+    v.pair_desc_stride = 0;
+    v.pair_angle_stride = 0;
+    v.nq_arr = nq;
+    v.nt_arr = nt;
+    v.nq = cap;
+    v.nt = cap;
+    v.out_stride = 0;
+    run_match(v, 1, cap, th_low, ratio, check_orientation, match, best, second, nmatch, st, timer);
 }
 
 void launch_match_bf(const uint8_t* q, const float* qa, int nq, const uint8_t* t, const float* ta, int nt,

@@ -94,6 +94,7 @@ struct orbhip_ctx {
     DevBuf<float> d_mqa, d_mta;
     DevBuf<int32_t> d_mm, d_mb, d_ms, d_mn;
     BaWorkspace* ba = nullptr;
+    StageTimer timer;
 };
 
 // ---------------------------------------------------------------------------
@@ -332,15 +333,24 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
     FrameBufs fb;
     fb.in = d_imgs; fb.in_stride = stride; fb.in_fstride = fstride; fb.pyr = c->d_pyr.p;
     HIPOK(hipMemsetAsync(c->d_err.p, 0, 4 * sizeof(int), st));
+    StageTimer& tm = c->timer;
+    tm.begin(1, st);
     for (int l = 1; l < P.n_levels; l++)
         launch_resize(pl->d_plan.p, P, fb, B, l, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p, pl->d_ybeta.p, st);
+    tm.end(1, st);
+    tm.begin(2, st);
     launch_fast(pl->d_plan.p, P, pl->d_cells.p, fb, B, c->d_cand.p, c->d_cand_cnt.p, st);
+    tm.end(2, st);
     OctreeCfg oc = pl->oct;
     oc.lap0 = lap0; oc.lap1 = lap1;
+    tm.begin(3, st);
     launch_octree(pl->d_plan.p, P, pl->d_cells.p, c->d_cand.p, c->d_cand_cnt.p, c->d_kscratch.p, c->d_nscratch.p,
                   c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, oc, c->d_err.p, B, st);
+    tm.end(3, st);
+    tm.begin(4, st);
     launch_desc(pl->d_plan.p, P, fb, c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, pl->d_disc.p, d_kps, d_desc, cap,
                 d_n, d_mono, B, st);
+    tm.end(4, st);
     HIPOK(hipGetLastError());
     return ORBHIP_OK;
 }
@@ -376,6 +386,8 @@ int orbhip_destroy(orbhip_ctx* c) {
     if (!c) return ORBHIP_ERR_ARG;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->timer.created)
+        for (int i = 0; i < 2 * StageTimer::kCap; i++) (void)hipEventDestroy(c->timer.ev[i]);
     ba_destroy(c->ba);
     c->plans.clear();
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -514,8 +526,55 @@ int orbhip_match_pairs_device(orbhip_ctx* c, const orbhip_kp* d_kps, const uint8
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     (void)hipGetLastError();
     launch_match_pairs(d_kps, d_desc, d_n, B - 1, cap, th_low, ratio, check_orientation, d_match, d_best, d_second,
-                       d_nmatch, st);
+                       d_nmatch, st, &c->timer);
     HIPOK(hipGetLastError());
+    return ORBHIP_OK;
+}
+
+int orbhip_match_frames_device(orbhip_ctx* c, const orbhip_kp* d_q_kps, const uint8_t* d_q_desc, const int32_t* d_nq,
+                               const orbhip_kp* d_t_kps, const uint8_t* d_t_desc, const int32_t* d_nt, int cap,
+                               int th_low, float ratio, int check_orientation, int32_t* d_match, int32_t* d_best,
+                               int32_t* d_second, int32_t* d_nmatch, void* stream) {
+    if (!c || !d_q_kps || !d_q_desc || !d_nq || !d_t_kps || !d_t_desc || !d_nt || cap <= 0 || !d_match || !d_best ||
+        !d_second || !d_nmatch)
+        return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    (void)hipGetLastError();
+    launch_match_frames(d_q_kps, d_q_desc, d_nq, d_t_kps, d_t_desc, d_nt, cap, th_low, ratio, check_orientation,
+                        d_match, d_best, d_second, d_nmatch, st, &c->timer);
+    HIPOK(hipGetLastError());
+    return ORBHIP_OK;
+}
+
+int orbhip_profile_stage(orbhip_ctx* c, int stage) {
+    if (!c || stage < 0 || stage > 6) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    StageTimer& t = c->timer;
+    if (!t.created) {
+        for (int i = 0; i < 2 * StageTimer::kCap; i++) HIPOK(hipEventCreate(&t.ev[i]));
+        t.created = true;
+    }
+    HIPOK(hipDeviceSynchronize());
+    t.stage = stage;
+    t.n = 0;
+    return ORBHIP_OK;
+}
+
+int orbhip_profile_collect(orbhip_ctx* c, double* total_ms, int32_t* count) {
+    if (!c || !total_ms || !count) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    StageTimer& t = c->timer;
+    double s = 0;
+    for (int i = 0; i < t.n; i++) {
+        HIPOK(hipEventSynchronize(t.ev[2 * i + 1]));
+        float ms = 0;
+        HIPOK(hipEventElapsedTime(&ms, t.ev[2 * i], t.ev[2 * i + 1]));
+        s += ms;
+    }
+    *total_ms = s;
+    *count = t.n;
+    t.n = 0;
     return ORBHIP_OK;
 }
 

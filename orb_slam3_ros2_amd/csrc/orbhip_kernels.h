@@ -23,6 +23,17 @@ struct OctreeCfg {
     int lap0, lap1;        // vLappingArea
 };
 
+// Live timing of one pipeline stage with hipEvents on the launch stream.
+struct StageTimer {
+    int stage = 0;                    // selected stage id (0 = off)
+    int n = 0;                        // recorded pairs
+    static constexpr int kCap = 8192;
+    hipEvent_t ev[2 * kCap];
+    bool created = false;
+    void begin(int s, hipStream_t st) { if (s == stage && n < kCap) (void)hipEventRecord(ev[2 * n], st); }
+    void end(int s, hipStream_t st) { if (s == stage && n < kCap) { (void)hipEventRecord(ev[2 * n + 1], st); n++; } }
+};
+
 // ---- extraction ----
 void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, int B, int l,
                    const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st);
@@ -40,7 +51,11 @@ void launch_desc(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& 
 // ---- matching ----
 void launch_match_pairs(const orbhip_kp* kps, const uint8_t* desc, const int32_t* n, int npairs, int cap,
                         int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best,
-                        int32_t* second, int32_t* nmatch, hipStream_t st);
+                        int32_t* second, int32_t* nmatch, hipStream_t st, StageTimer* timer);
+void launch_match_frames(const orbhip_kp* q_kps, const uint8_t* q_desc, const int32_t* nq, const orbhip_kp* t_kps,
+                         const uint8_t* t_desc, const int32_t* nt, int cap, int th_low, float ratio,
+                         int check_orientation, int32_t* match, int32_t* best, int32_t* second, int32_t* nmatch,
+                         hipStream_t st, StageTimer* timer);
 void launch_match_bf(const uint8_t* q, const float* qa, int nq, const uint8_t* t, const float* ta, int nt,
                      int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best,
                      int32_t* second, int32_t* nmatch, hipStream_t st);
