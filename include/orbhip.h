@@ -167,6 +167,12 @@ typedef struct {
 int orbhip_ba_solve(orbhip_ctx* ctx, const orbhip_ba_problem* prob, orbhip_ba_result* res,
                     const volatile int* stop_flag);
 
+/* B independent problems solved together (SURVEY.md §8e replicas: concurrent maps / agents,
+ * or a batch of local windows). Each problem follows its own exact LM schedule; all share the
+ * kernel launches of a round. probs / res: arrays of B structs. */
+int orbhip_ba_solve_batch(orbhip_ctx* ctx, const orbhip_ba_problem* probs, int B, orbhip_ba_result* res,
+                          const volatile int* stop_flag);
+
 #ifdef __cplusplus
 }
 #endif

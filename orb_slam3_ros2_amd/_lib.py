@@ -59,7 +59,7 @@ class BAResultC(ctypes.Structure):
 EXPORTED = ["orbhip_abi_version", "orbhip_create", "orbhip_destroy", "orbhip_level_info", "orbhip_max_keypoints",
             "orbhip_extract", "orbhip_extract_batch_device", "orbhip_descriptor_distance", "orbhip_match_bf",
             "orbhip_match_pairs_device", "orbhip_match_frames_device", "orbhip_profile_stage",
-            "orbhip_profile_collect", "orbhip_ba_solve"]
+            "orbhip_profile_collect", "orbhip_ba_solve", "orbhip_ba_solve_batch"]
 
 
 def lib():
@@ -95,6 +95,7 @@ def lib():
     L.orbhip_profile_stage.argtypes = [vp, i32]
     L.orbhip_profile_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)]
     L.orbhip_ba_solve.argtypes = [vp, ctypes.POINTER(BAProblemC), ctypes.POINTER(BAResultC), vp]
+    L.orbhip_ba_solve_batch.argtypes = [vp, ctypes.POINTER(BAProblemC), i32, ctypes.POINTER(BAResultC), vp]
     L.orbhip_test_sincosf.argtypes = [vp, vp, vp, ctypes.c_int64]
     L.orbhip_test_sincosf_sweep.argtypes = [ctypes.c_uint32, ctypes.c_uint32, vp, vp]
     L.orbhip_test_sincosf_sweep.restype = ctypes.c_int64

@@ -2,22 +2,25 @@
 // BundleAdjustment (U:src/Optimizer.cc) solved with the Levenberg-Marquardt schedule of
 // OptimizationAlgorithmLevenberg and the Schur complement of BlockSolver<6,3>.
 //
-// The host drives the exact g2o control flow (iterations, trials, lambda schedule, push/pop,
-// termination) with ONE device->host read per trial (chi2, scale, solve flag). All
-// arithmetic is fp64 on the device:
+// Batched: every kernel runs over grid.y = the ACTIVE problems of a round (problem index from
+// act[]), so B independent problems (SURVEY.md §8e "replicas": concurrent maps / agents, or a
+// batch of local windows) share each launch. The host runs each problem's exact g2o control
+// flow (iterations, trials, lambda schedule, push/pop, termination) with ONE device->host read
+// per trial ROUND (all problems' chi2, scale, solve flag). fp64 throughout:
 //   k_ba_errors        EdgeSE3ProjectXYZ::computeError + RobustKernelHuber::robustify
-//   k_ba_lin_points    linearizeOplus + constructQuadraticForm, landmark side (Hll, b_l,
-//                      per-edge Hpl blocks)
+//   k_ba_lin_points    linearizeOplus + constructQuadraticForm, landmark side (Hll, b_l, Hpl)
 //   k_ba_lin_poses     the pose side (Hpp, b_p), one wave per pose, deterministic tree
-//   k_ba_schur_points  setLambda on Hll, Dinv (Eigen 3x3 cofactor inverse), db, W = Hpl Dinv
-//   k_ba_schur_blocks  S_ij = [i==j](Hpp_i + lambda I) - sum W_a Hpl_b^T over shared
-//                      landmarks (precomputed pair lists: deterministic gather, no atomics)
+//   k_ba_schur_points  setLambda on Hll, Dinv (Eigen 3x3 cofactor inverse), db
+//   k_ba_schur_w       W = Hpl Dinv per edge
+//   k_ba_schur_blocks  S_ij = [i==j](Hpp_i + lambda I) - sum W_a Hpl_b^T over shared landmarks
+//                      (host-built pair lists: deterministic gather, no atomics)
 //   k_ba_schur_b       b_schur = b_p - sum Hpl db
-//   k_ba_cholesky      dense LL^T of S + two triangular solves, one workgroup; the trailing
-//                      update is v_mfma_f64_16x16x4f64 on 16x16 tiles
+//   k_ba_cholesky      dense LL^T + solves, one workgroup per problem; trailing update on
+//                      v_mfma_f64_16x16x4f64
 //   k_ba_backsub       xl = Dinv (b_l - Hpl^T xp), X += xl (push: old X saved)
 //   k_ba_update_poses  T <- exp(xp) * T (SE3Quat::exp, operator*)   (push: old T saved)
-//   k_ba_reduce        activeRobustChi2 and computeScale, fixed-order reductions
+//   k_ba_reduce        activeRobustChi2, computeScale, max diag; fixed-order reductions
+//   k_ba_pop           restore the pushed state of problems whose trial was rejected
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -25,7 +28,6 @@
 #include <cstdio>
 #include <cstring>
 #include <limits>
-#include <map>
 #include <vector>
 
 #include "orbhip_ba.h"
@@ -66,7 +68,11 @@ struct BaArgs {
     int nblk;
     double* red;       // [0] chi2, [1] scale, [2] maxdiag
     int* flag;         // [0] cholesky ok
+    const double* lambda;   // current lambda of this problem (device copy)
 };
+
+#define BA_PROLOGUE                                 \
+    const BaArgs& a = args[act[blockIdx.y]];
 
 // ---------------------------------------------------------------------------
 // SE3Quat helpers (Eigen formulas)
@@ -127,10 +133,12 @@ __device__ __forceinline__ void qnormalize(DQ& q) {
 
 __device__ __forceinline__ DQ load_q(const double* p) { return DQ{p[0], p[1], p[2], p[3]}; }
 
+
 // ---------------------------------------------------------------------------
 // errors
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_ba_errors(BaArgs a) {
+__global__ __launch_bounds__(256) void k_ba_errors(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    BA_PROLOGUE
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= a.E) return;
     const double* T = a.pose + 8 * a.e_pose[e];
@@ -186,7 +194,8 @@ __device__ __forceinline__ void edge_jac(const BaArgs& a, int e, double A[6], do
 // ---------------------------------------------------------------------------
 // buildSystem
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_ba_lin_points(BaArgs a) {
+__global__ __launch_bounds__(256) void k_ba_lin_points(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    BA_PROLOGUE
     const int m = blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= a.M) return;
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};
@@ -218,7 +227,8 @@ __global__ __launch_bounds__(256) void k_ba_lin_points(BaArgs a) {
 }
 
 // one wave per optimised pose: 21 upper Hpp terms + 6 b terms, lanes over the pose's edges
-__global__ __launch_bounds__(256) void k_ba_lin_poses(BaArgs a) {
+__global__ __launch_bounds__(256) void k_ba_lin_poses(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    BA_PROLOGUE
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (i >= a.np) return;
@@ -274,9 +284,12 @@ __device__ __forceinline__ void inv3(const double m[9], double r[9]) {
     r[8] = (m[0] * m[4] - m[1] * m[3]) * id;
 }
 
-__global__ __launch_bounds__(256) void k_ba_schur_points(BaArgs a, double lambda) {
+
+__global__ __launch_bounds__(256) void k_ba_schur_points(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    BA_PROLOGUE
     const int m = blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= a.M) return;
+    const double lambda = *a.lambda;
     double D[9], Di[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) D[k] = a.Hll[9 * m + k] + (k % 4 == 0 ? lambda : 0.0);
@@ -286,217 +299,324 @@ __global__ __launch_bounds__(256) void k_ba_schur_points(BaArgs a, double lambda
     const double* bl = a.b + a.n + 3 * m;
 #pragma unroll
     for (int r = 0; r < 3; r++) a.db[3 * m + r] = Di[3 * r] * bl[0] + Di[3 * r + 1] * bl[1] + Di[3 * r + 2] * bl[2];
-    for (int k = a.pt_ptr[m]; k < a.pt_ptr[m + 1]; k++) {
-        const int e = a.pt_edges[k];
-        if (a.opt[a.e_pose[e]] < 0) continue;
-        const double* B1 = a.Hpl + 18 * e;
-        double* w = a.W + 18 * e;
+}
+
+__global__ __launch_bounds__(256) void k_ba_schur_w(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    BA_PROLOGUE
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= a.E || a.opt[a.e_pose[e]] < 0) return;
+    const double* Di = a.Dinv + 9 * a.e_pt[e];
+    double d[9];
 #pragma unroll
-        for (int r = 0; r < 6; r++)
+    for (int k = 0; k < 9; k++) d[k] = Di[k];
+    const double* B1 = a.Hpl + 18 * e;
+    double* w = a.W + 18 * e;
 #pragma unroll
-            for (int c = 0; c < 3; c++)
-                w[3 * r + c] = B1[3 * r] * Di[c] + B1[3 * r + 1] * Di[3 + c] + B1[3 * r + 2] * Di[6 + c];
+    for (int r = 0; r < 6; r++) {
+        const double h0 = B1[3 * r], h1 = B1[3 * r + 1], h2 = B1[3 * r + 2];
+#pragma unroll
+        for (int c = 0; c < 3; c++) w[3 * r + c] = h0 * d[c] + h1 * d[3 + c] + h2 * d[6 + c];
     }
 }
 
-// one wave per (i <= j) block of S; lanes 0..35 own one entry each
-__global__ __launch_bounds__(256) void k_ba_schur_blocks(BaArgs a, double lambda) {
+__global__ __launch_bounds__(256) void k_ba_zero_s(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    BA_PROLOGUE
+    const size_t nn = (size_t)a.n * a.n;
+    double2* S2 = (double2*)a.S;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nn / 2; i += (size_t)gridDim.x * blockDim.x)
+        S2[i] = make_double2(0.0, 0.0);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (nn & 1)) a.S[nn - 1] = 0.0;
+}
+
+// one wave per (i <= j) block of S; lanes 0..35 own one entry each. The block's pair list is
+// fetched 64 pairs at a time into lanes and broadcast with shuffles, so the serial loop has
+// no dependent index load.
+__global__ __launch_bounds__(256) void k_ba_schur_blocks(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    BA_PROLOGUE
     const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (blk >= a.nblk || lane >= 36) return;
+    if (blk >= a.nblk) return;
+    const double lambda = *a.lambda;
     const int i = a.blk_i[blk], j = a.blk_j[blk];
-    const int r = lane / 6, c = lane - 6 * (lane / 6);
-    double s = (i == j) ? a.Hpp[36 * i + 6 * r + c] + (r == c ? lambda : 0.0) : 0.0;
-    for (int k = a.blk_ptr[blk]; k < a.blk_ptr[blk + 1]; k++) {
-        const int ea = a.blk_pairs[2 * k], eb = a.blk_pairs[2 * k + 1];
-        const double* w = a.W + 18 * ea + 3 * r;
-        const double* h = a.Hpl + 18 * eb + 3 * c;
-        s -= w[0] * h[0] + w[1] * h[1] + w[2] * h[2];
+    const int rr = lane < 36 ? lane / 6 : 0, cc = lane < 36 ? lane - 6 * (lane / 6) : 0;
+    double s = (i == j && lane < 36) ? a.Hpp[36 * i + 6 * rr + cc] + (rr == cc ? lambda : 0.0) : 0.0;
+    const int k0 = a.blk_ptr[blk], k1 = a.blk_ptr[blk + 1];
+    for (int kb = k0; kb < k1; kb += 64) {
+        const int cnt = min(64, k1 - kb);
+        const int pa = lane < cnt ? a.blk_pairs[2 * (kb + lane)] : 0;
+        const int pb = lane < cnt ? a.blk_pairs[2 * (kb + lane) + 1] : 0;
+        int t = 0;
+        for (; t + 4 <= cnt; t += 4) {
+            double w[4][3], h[4][3];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int ea = __shfl(pa, t + u, 64), eb = __shfl(pb, t + u, 64);
+                const double* wp = a.W + 18 * ea + 3 * rr;
+                const double* hp = a.Hpl + 18 * eb + 3 * cc;
+                w[u][0] = wp[0]; w[u][1] = wp[1]; w[u][2] = wp[2];
+                h[u][0] = hp[0]; h[u][1] = hp[1]; h[u][2] = hp[2];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) s -= w[u][0] * h[u][0] + w[u][1] * h[u][1] + w[u][2] * h[u][2];
+        }
+        for (; t < cnt; t++) {
+            const int ea = __shfl(pa, t, 64), eb = __shfl(pb, t, 64);
+            const double* wp = a.W + 18 * ea + 3 * rr;
+            const double* hp = a.Hpl + 18 * eb + 3 * cc;
+            s -= wp[0] * hp[0] + wp[1] * hp[1] + wp[2] * hp[2];
+        }
     }
-    a.S[(size_t)(6 * i + r) * a.n + 6 * j + c] = s;
-    if (i != j) a.S[(size_t)(6 * j + c) * a.n + 6 * i + r] = s;
+    if (lane < 36) {
+        a.S[(size_t)(6 * i + rr) * a.n + 6 * j + cc] = s;
+        if (i != j) a.S[(size_t)(6 * j + cc) * a.n + 6 * i + rr] = s;
+    }
 }
 
-__global__ __launch_bounds__(256) void k_ba_schur_b(BaArgs a) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= a.n) return;
-    const int i = t / 6, r = t - 6 * i;
-    double s = 0;
-    for (int k = a.ps_ptr[i]; k < a.ps_ptr[i + 1]; k++) {
+__global__ __launch_bounds__(256) void k_ba_schur_b(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    BA_PROLOGUE
+    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (i >= a.np) return;
+    double acc[6] = {0, 0, 0, 0, 0, 0};
+    for (int k = a.ps_ptr[i] + lane; k < a.ps_ptr[i + 1]; k += 64) {
         const int e = a.ps_edges[k];
-        const double* h = a.Hpl + 18 * e + 3 * r;
+        const double* h = a.Hpl + 18 * e;
         const double* d = a.db + 3 * a.e_pt[e];
-        s += h[0] * d[0] + h[1] * d[1] + h[2] * d[2];
+        const double d0 = d[0], d1 = d[1], d2 = d[2];
+#pragma unroll
+        for (int r = 0; r < 6; r++) acc[r] += h[3 * r] * d0 + h[3 * r + 1] * d1 + h[3 * r + 2] * d2;
     }
-    a.bs[t] = a.b[t] - s;
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+        double v = acc[r];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (lane == 0) a.bs[6 * i + r] = a.b[6 * i + r] - v;
+    }
 }
 
 // ---------------------------------------------------------------------------
-// dense Cholesky of S (n x n, lower, in place) + solve S xp = bs; one workgroup.
-// Panel width 16; the panel below the diagonal block is staged in LDS and the trailing
-// update C -= P_I P_J^T runs as 4 x v_mfma_f64_16x16x4f64 per 16x16 tile.
+// dense Cholesky of S (n x n, lower, in place) + solve S xp = bs; one workgroup of 16 waves.
+// Right-looking, 32-column panels:
+//  (a) the 32x32 diagonal block is factored by wave 0 in REGISTERS: lane l owns column
+//      c = l & 31, rows r = 2s + (l >> 5) (s = 0..15); pivots and column values move by
+//      shuffles, no LDS round trip on the serial pivot chain. The panel's slice of the
+//      forward solve (L y = b) is done in the same pass.
+//  (b) panel rows below: L21 = A21 L11^-T, one row per thread, into LDS (stride 34 doubles:
+//      conflict-free for the MFMA operand reads) and back to S; y updated from the panel.
+//  (c) trailing update C -= P_I P_J^T on 16x16 lower tiles with v_mfma_f64_16x16x4f64
+//      (8 per tile, K = 32); the four C-tile loads of a round are issued together.
 //   f64 MFMA operand map: lane l holds A[l&15][k=l>>4], B[k=l>>4][l&15];
 //   C/D: col = l&15, row = (l>>4) + 4*reg.
+//  (d) backward solve L^T x = y panel by panel (column dot products + diagonal solve).
 // ---------------------------------------------------------------------------
-constexpr int kCholNB = 16;
+constexpr int kNB = 32;
+constexpr int kPS = 34;   // panel row stride in doubles
 
-__global__ __launch_bounds__(1024) void k_ba_cholesky(double* __restrict__ S, const double* __restrict__ bs,
-                                                      double* __restrict__ x, int n, int* __restrict__ flag) {
+__device__ __forceinline__ size_t chol_lds_bytes(int n) {
+    const int np = (n + 31) & ~31;
+    return sizeof(double) * (size_t)(2 + 32 * 33 + np + np * kPS + 64);  // + invD, dval
+}
+
+__device__ void chol_solve(double* __restrict__ S, const double* __restrict__ bs, double* __restrict__ x, int n,
+                           int* __restrict__ flag, unsigned long long* __restrict__ dbg) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
-    int& bad = *(int*)lds;                   // control word (first 16 bytes)
-    double* Dg = lds + 2;                    // 16 x 16 diagonal block
-    double* y = Dg + 256;                    // n (solution vector)
-    double* Pn = y + ((n + 15) & ~15);       // panel rows (n_pad x 16)
+    const int npad = (n + 31) & ~31;
+    int& bad = *(int*)lds;                   // control word
+    double* D = lds + 2;                     // 32 x 33 diagonal block (L11, lower)
+    double* y = D + 32 * 33;                 // npad
+    double* Pn = y + npad;                   // npad x kPS panel rows
+    double* invD = Pn + (size_t)npad * kPS;  // 32 reciprocal pivots of the current panel
+    double* dval = invD + 32;                // 32 pivots (sqrt) of the current panel
     const int tid = threadIdx.x, nt = blockDim.x;
     const int wid = tid >> 6, lane = tid & 63, nw = nt >> 6;
+    unsigned long long tprev = 0;
+    auto stamp = [&](int ph) {
+        if (dbg && tid == 0) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            if (ph >= 0) dbg[ph] += t - tprev;
+            tprev = t;
+        }
+    };
+    stamp(-1);
     if (tid == 0) bad = 0;
+    for (int i = tid; i < npad; i += nt) y[i] = i < n ? bs[i] : 0.0;
     __syncthreads();
-    for (int k0 = 0; k0 < n; k0 += kCholNB) {
-        const int kb = min(kCholNB, n - k0);
-        // (a) diagonal block
-        for (int t = tid; t < 256; t += nt) {
-            const int r = t >> 4, c = t & 15;
-            Dg[t] = (r < kb && c <= r) ? S[(size_t)(k0 + r) * n + k0 + c] : 0.0;
+    for (int k0 = 0; k0 < n; k0 += kNB) {
+        const int kb = min(kNB, n - k0);
+        // ---- (a) diagonal block in LDS, all threads: 2 barriers per pivot ----
+        for (int t = tid; t < 32 * 32; t += nt) {
+            const int r = t >> 5, cI = t & 31;
+            D[r * 33 + cI] = (r < kb && cI < kb && cI <= r) ? S[(size_t)(k0 + r) * n + k0 + cI] : (r == cI ? 1.0 : 0.0);
         }
         __syncthreads();
-        // (b) factor it (wave 0, 4 entries per lane)
-        if (wid == 0) {
-            for (int j = 0; j < kb; j++) {
-                if (lane == 0) {
-                    const double p = Dg[17 * j];
-                    if (!(p > 0.0)) bad = 1;
-                    Dg[17 * j] = sqrt(p > 0.0 ? p : 1.0);
-                }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                const double d = Dg[17 * j];
-                if (lane > j && lane < kb) Dg[16 * lane + j] /= d;
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                for (int t = lane; t < 256; t += 64) {
-                    const int r = t >> 4, c = t & 15;
-                    if (r > j && c > j && c <= r && r < kb) Dg[t] -= Dg[16 * r + j] * Dg[16 * c + j];
-                }
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        for (int j = 0; j < kb; j++) {
+            __syncthreads();   // previous step's trailing update is complete
+            const double piv = D[j * 33 + j];
+            const double d = sqrt(piv > 0.0 ? piv : 1.0);
+            const double inv = 1.0 / d;
+            if (tid < 32) {
+                if (tid == j) { invD[j] = inv; dval[j] = d; y[k0 + j] *= inv; if (!(piv > 0.0)) bad = 1; }
+                else if (tid > j) D[tid * 33 + j] *= inv;
             }
+            __syncthreads();
+            for (int t = tid; t < 32 * 32; t += nt) {
+                const int r = t >> 5, cI = t & 31;
+                if (cI > j && r >= cI) D[r * 33 + cI] -= D[r * 33 + j] * D[cI * 33 + j];
+            }
+            if (tid > j && tid < kb) y[k0 + tid] -= D[tid * 33 + j] * y[k0 + j];
         }
         __syncthreads();
-        if (bad) break;
-        for (int t = tid; t < 256; t += nt) {
-            const int r = t >> 4, c = t & 15;
-            if (r < kb && c <= r) S[(size_t)(k0 + r) * n + k0 + c] = Dg[t];
+        if (tid < kb) D[tid * 33 + tid] = dval[tid];
+        __syncthreads();
+        for (int t = tid; t < 32 * 32; t += nt) {
+            const int r = t >> 5, cI = t & 31;
+            if (r < kb && cI < kb && cI <= r) S[(size_t)(k0 + r) * n + k0 + cI] = D[r * 33 + cI];
         }
-        // (c) panel rows: L[r][0:kb] = A[r][k0:k0+kb] * Dg^{-T}
+        stamp(0);
+        if (bad) break;
+        // ---- (b) panel rows: L21 = A21 L11^-T; y_r -= L21[r] . y_panel ----
         const int r0 = k0 + kb;
         const int nr = n - r0;
         const int nr_pad = (nr + 15) & ~15;
         for (int rr = tid; rr < nr_pad; rr += nt) {
-            double v[kCholNB];
+            double v[kNB];
             const int r = r0 + rr;
+            const double* Ar = S + (size_t)r * n + k0;
 #pragma unroll
-            for (int c = 0; c < kCholNB; c++) v[c] = (rr < nr && c < kb) ? S[(size_t)r * n + k0 + c] : 0.0;
+            for (int cI = 0; cI < kNB; cI++) v[cI] = (rr < nr && cI < kb) ? Ar[cI] : 0.0;
+            double dot = 0.0;
 #pragma unroll
-            for (int c = 0; c < kCholNB; c++) {
-                if (c < kb) {
-                    double s = v[c];
-                    for (int p = 0; p < c; p++) s -= v[p] * Dg[16 * c + p];
-                    v[c] = s / Dg[17 * c];
+            for (int cI = 0; cI < kNB; cI++) {
+                double s2 = v[cI];
+#pragma unroll
+                for (int p2 = 0; p2 < cI; p2++) s2 -= v[p2] * D[cI * 33 + p2];
+                v[cI] = (cI < kb) ? s2 * invD[cI] : 0.0;
+                dot += v[cI] * y[k0 + cI];
+            }
+#pragma unroll
+            for (int cI = 0; cI < kNB; cI++) Pn[rr * kPS + cI] = v[cI];
+            if (rr < nr) {
+                double* Lr = S + (size_t)r * n + k0;
+#pragma unroll
+                for (int cI = 0; cI < kNB; cI++)
+                    if (cI < kb) Lr[cI] = v[cI];
+                y[r] -= dot;
+            }
+        }
+        __syncthreads();
+        stamp(1);
+        // ---- (c) trailing update, lower 16x16 tiles, 4 tiles per wave per round ----
+        const int T = nr_pad / 16;
+        const int ntile = T * (T + 1) / 2;
+        const int cc = lane & 15, rq = lane >> 4;
+        for (int base = wid; base < ntile; base += 4 * nw) {
+            double4_t acc[4];
+            int ti[4], tj[4];
+            bool on[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int tile = base + u * nw;
+                on[u] = tile < ntile;
+                const int tt = on[u] ? tile : 0;
+                int I = (int)((sqrtf(8.0f * (float)tt + 1.0f) - 1.0f) * 0.5f);
+                while ((I + 1) * (I + 2) / 2 <= tt) I++;
+                while (I * (I + 1) / 2 > tt) I--;
+                ti[u] = I;
+                tj[u] = tt - I * (I + 1) / 2;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int rr = r0 + 16 * ti[u] + rq + 4 * q, col = r0 + 16 * tj[u] + cc;
+                    acc[u][q] = (on[u] && rr < n && col < n) ? S[(size_t)rr * n + col] : 0.0;
                 }
             }
 #pragma unroll
-            for (int c = 0; c < kCholNB; c++) {
-                Pn[rr * 16 + c] = v[c];
-                if (rr < nr && c < kb) S[(size_t)r * n + k0 + c] = v[c];
+            for (int u = 0; u < 4; u++) {
+#pragma unroll
+                for (int kk = 0; kk < kNB / 4; kk++) {
+                    const double av = -Pn[(16 * ti[u] + cc) * kPS + 4 * kk + rq];
+                    const double bv = Pn[(16 * tj[u] + cc) * kPS + 4 * kk + rq];
+                    acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[u], 0, 0, 0);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int rr = r0 + 16 * ti[u] + rq + 4 * q, col = r0 + 16 * tj[u] + cc;
+                    if (on[u] && rr < n && col < n) S[(size_t)rr * n + col] = acc[u][q];
+                }
             }
         }
         __syncthreads();
-        // (d) trailing update, lower tiles only
-        const int T = nr_pad / 16;
-        const int ntile = T * (T + 1) / 2;
-        for (int tile = wid; tile < ntile; tile += nw) {
-            int I = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
-            while ((I + 1) * (I + 2) / 2 <= tile) I++;
-            while (I * (I + 1) / 2 > tile) I--;
-            const int J = tile - I * (I + 1) / 2;
-            const int row_base = r0 + 16 * I, col_base = r0 + 16 * J;
-            double4_t acc;
-            const int cc = lane & 15, rq = lane >> 4;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int rr = row_base + rq + 4 * q;
-                acc[q] = (rr < n && col_base + cc < n) ? S[(size_t)rr * n + col_base + cc] : 0.0;
-            }
-#pragma unroll
-            for (int kk = 0; kk < 4; kk++) {
-                const double av = -Pn[(16 * I + cc) * 16 + 4 * kk + rq];
-                const double bv = Pn[(16 * J + cc) * 16 + 4 * kk + rq];
-                acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const int rr = row_base + rq + 4 * q;
-                if (rr < n && col_base + cc < n) S[(size_t)rr * n + col_base + cc] = acc[q];
-            }
-        }
-        __syncthreads();
+        stamp(2);
     }
     if (bad) {
         if (tid == 0) flag[0] = 0;
         for (int i = tid; i < n; i += nt) x[i] = 0.0;
         return;
     }
-    // forward: L y = bs
-    for (int i = tid; i < n; i += nt) y[i] = bs[i];
-    __syncthreads();
-    for (int k0 = 0; k0 < n; k0 += 16) {
-        const int kb = min(16, n - k0);
+    // ---- (d) backward: L^T x = y, panels from the last ----
+    const int npan = (n + kNB - 1) / kNB;
+    for (int pb = npan - 1; pb >= 0; pb--) {
+        const int k0 = pb * kNB, kb = min(kNB, n - k0);
+        const int r0 = k0 + kb;
+        // y_c -= sum_{r >= r0} L[r][k0+c] x_r : 32 columns x 32 row-groups, one thread each
+        const int G = nt >> 5;
+        {
+            const int cI = tid & 31, g = tid >> 5;   // g = 0..G-1
+            double s2 = 0.0;
+            if (cI < kb)
+                for (int r = r0 + g; r < n; r += G) s2 += S[(size_t)r * n + k0 + cI] * y[r];
+            Pn[g * 33 + cI] = s2;                    // reduced over g below
+        }
+        for (int t = tid; t < 32 * 33; t += nt) {
+            const int r = t / 33, cI = t - 33 * (t / 33);
+            D[t] = (r < kb && cI < kb && cI <= r) ? S[(size_t)(k0 + r) * n + k0 + cI] : 0.0;
+        }
+        if (tid < kb) invD[tid] = 1.0 / S[(size_t)(k0 + tid) * n + k0 + tid];
+        __syncthreads();
         if (wid == 0) {
-            double v = lane < kb ? y[k0 + lane] : 0.0;
-            for (int j = 0; j < kb; j++) {
-                const double yj = __shfl(v, j, 64) / S[(size_t)(k0 + j) * n + k0 + j];
-                if (lane == j) v = yj;
-                if (lane > j && lane < kb) v -= S[(size_t)(k0 + lane) * n + k0 + j] * yj;
+            double v = 0.0;
+            if (lane < kb) {
+                double s2 = 0.0;
+                for (int g = 0; g < G; g++) s2 += Pn[g * 33 + lane];
+                v = y[k0 + lane] - s2;
             }
-            if (lane < kb) y[k0 + lane] = v;
-        }
-        __syncthreads();
-        for (int r = k0 + kb + tid; r < n; r += nt) {
-            double s = 0;
-            for (int j = 0; j < kb; j++) s += S[(size_t)r * n + k0 + j] * y[k0 + j];
-            y[r] -= s;
-        }
-        __syncthreads();
-    }
-    // backward: L^T x = y
-    const int nb = (n + 15) / 16;
-    for (int b = nb - 1; b >= 0; b--) {
-        const int k0 = 16 * b, kb = min(16, n - k0);
-        if (wid == 0) {
-            double v = lane < kb ? y[k0 + lane] : 0.0;
             for (int j = kb - 1; j >= 0; j--) {
-                const double xj = __shfl(v, j, 64) / S[(size_t)(k0 + j) * n + k0 + j];
+                const double xj = __shfl(v, j, 64) * invD[j];
                 if (lane == j) v = xj;
-                if (lane < j) v -= S[(size_t)(k0 + j) * n + k0 + lane] * xj;
+                if (lane < j) v -= D[j * 33 + lane] * xj;
             }
             if (lane < kb) y[k0 + lane] = v;
         }
         __syncthreads();
-        for (int r = tid; r < k0; r += nt) {
-            double s = 0;
-            for (int j = 0; j < kb; j++) s += S[(size_t)(k0 + j) * n + r] * y[k0 + j];
-            y[r] -= s;
-        }
-        __syncthreads();
     }
+    stamp(3);
     for (int i = tid; i < n; i += nt) x[i] = y[i];
     if (tid == 0) flag[0] = 1;
+}
+
+
+__global__ __launch_bounds__(512) void k_ba_cholesky(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    const BaArgs& a = args[act[blockIdx.x]];
+    if (a.n == 0) {
+        if (threadIdx.x == 0) a.flag[0] = 1;
+        return;
+    }
+    chol_solve(a.S, a.bs, a.x, a.n, a.flag, nullptr);
+}
+
+__global__ __launch_bounds__(512) void k_chol_test(double* S, const double* bs, double* x, int n, int* flag,
+                                                   unsigned long long* dbg) {
+    chol_solve(S, bs, x, n, flag, dbg);
 }
 
 // ---------------------------------------------------------------------------
 // back-substitution + updates (push saves the old state)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_ba_backsub(BaArgs a) {
+__global__ __launch_bounds__(256) void k_ba_backsub(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    BA_PROLOGUE
     const int m = blockIdx.x * blockDim.x + threadIdx.x;
     if (m >= a.M) return;
     const double* bl = a.b + a.n + 3 * m;
@@ -523,7 +643,8 @@ __global__ __launch_bounds__(256) void k_ba_backsub(BaArgs a) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_ba_update_poses(BaArgs a) {
+__global__ __launch_bounds__(256) void k_ba_update_poses(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    BA_PROLOGUE
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= a.P) return;
     double* T = a.pose + 8 * p;
@@ -559,7 +680,6 @@ __global__ __launch_bounds__(256) void k_ba_update_poses(BaArgs a) {
     const double tex = V[0] * u[3] + V[1] * u[4] + V[2] * u[5];
     const double tey = V[3] * u[3] + V[4] * u[4] + V[5] * u[5];
     const double tez = V[6] * u[3] + V[7] * u[4] + V[8] * u[5];
-    // exp(d) * T
     const DQ qt = load_q(T);
     double rx, ry, rz;
     qrot(qe, T[4], T[5], T[6], rx, ry, rz);
@@ -570,8 +690,25 @@ __global__ __launch_bounds__(256) void k_ba_update_poses(BaArgs a) {
     T[4] = tex + rx; T[5] = tey + ry; T[6] = tez + rz;
 }
 
+__global__ __launch_bounds__(256) void k_ba_pop(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    BA_PROLOGUE
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 8 * a.P) a.pose[i] = a.pose_bak[i];
+    if (i < 3 * a.M) a.pts[i] = a.pts_bak[i];
+}
+
+// red[0..3] + flag of the active problems packed contiguously for ONE device->host copy
+__global__ void k_ba_gather_red(const BaArgs* __restrict__ args, const int* __restrict__ act, int nact,
+                                double* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nact) return;
+    const BaArgs& a = args[act[i]];
+    for (int k = 0; k < 4; k++) out[5 * i + k] = a.red[k];
+    out[5 * i + 4] = (double)a.flag[0];
+}
+
 // ---------------------------------------------------------------------------
-// reductions (one workgroup, fixed order): [0] sum rho0, [1] computeScale, [2] max diag
+// reductions (one workgroup per problem, fixed order): [0] sum rho0, [1] scale, [2] max diag
 // ---------------------------------------------------------------------------
 __device__ double block_sum(double v, double* sh) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -585,7 +722,9 @@ __device__ double block_sum(double v, double* sh) {
     return s;
 }
 
-__global__ __launch_bounds__(1024) void k_ba_reduce(BaArgs a, double lambda, int what) {
+__global__ __launch_bounds__(1024) void k_ba_reduce(const BaArgs* __restrict__ args, const int* __restrict__ act,
+                                                    int what) {
+    const BaArgs& a = args[act[blockIdx.x]];
     __shared__ double sh[16];
     double v = 0;
     if (what & 1) {
@@ -594,6 +733,7 @@ __global__ __launch_bounds__(1024) void k_ba_reduce(BaArgs a, double lambda, int
         if (threadIdx.x == 0) a.red[0] = v;
     }
     if (what & 2) {
+        const double lambda = *a.lambda;
         v = 0;
         const int N = a.n + 3 * a.M;
         for (int j = threadIdx.x; j < N; j += blockDim.x) v += a.x[j] * (lambda * a.x[j] + a.b[j]);
@@ -618,8 +758,130 @@ __global__ __launch_bounds__(1024) void k_ba_reduce(BaArgs a, double lambda, int
 }
 
 // ---------------------------------------------------------------------------
-// host workspace
+// host side
 // ---------------------------------------------------------------------------
+#define BAOK(x)                                                                                    \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) {                                                                    \
+            std::fprintf(stderr, "orbhip ba: %s: %s\n", #x, hipGetErrorString(e_));                \
+            return ORBHIP_ERR_DEVICE;                                                              \
+        }                                                                                          \
+    } while (0)
+
+namespace {
+
+// per-problem host preparation (O(E)): index mapping, CSRs, Schur pair lists by counting sort
+struct Prep {
+    int P = 0, M = 0, E = 0, np = 0, n = 0, nblk = 0;
+    std::vector<int> opt, e_pose, e_pt, pt_ptr, pt_edges, ps_ptr, ps_edges, blk_i, blk_j, blk_ptr, blk_pairs;
+    std::vector<double> pose, pts, obs, info;
+    // offsets into the packed device buffers (elements)
+    size_t o_pose, o_pts, o_opt, o_edge, o_e2, o_e18, o_np36, o_m9, o_m3, o_b, o_S, o_n, o_ptp, o_psp, o_blk, o_blkp,
+        o_pairs, o_ps_edges;
+};
+
+inline void se3_from_float(const float* q, const float* t, double* out) {
+    double x = q[0], y = q[1], z = q[2], w = q[3];
+    if (w < 0) { x = -x; y = -y; z = -z; w = -w; }
+    const double nn = std::sqrt(x * x + y * y + z * z + w * w);
+    out[0] = x / nn; out[1] = y / nn; out[2] = z / nn; out[3] = w / nn;
+    out[4] = t[0]; out[5] = t[1]; out[6] = t[2]; out[7] = 0;
+}
+
+int prepare(const orbhip_ba_problem* pr, Prep& o) {
+    const int P = pr->n_poses, M = pr->n_points, E = pr->n_edges;
+    if (P < 0 || M < 0 || E < 0 || (P && (!pr->pose_q || !pr->pose_t || !pr->pose_fixed)) || (M && !pr->points) ||
+        (E && (!pr->edge_pose || !pr->edge_point || !pr->edge_uv || !pr->edge_octave || !pr->inv_sigma2)))
+        return ORBHIP_ERR_ARG;
+    for (int e = 0; e < E; e++)
+        if (pr->edge_pose[e] < 0 || pr->edge_pose[e] >= P || pr->edge_point[e] < 0 || pr->edge_point[e] >= M ||
+            pr->edge_octave[e] < 0 || pr->edge_octave[e] >= pr->n_octaves)
+            return ORBHIP_ERR_ARG;
+    o.P = P; o.M = M; o.E = E;
+    o.opt.assign(P, -1);
+    int np = 0;
+    for (int i = 0; i < P; i++)
+        if (!pr->pose_fixed[i]) o.opt[i] = np++;
+    o.np = np;
+    o.n = 6 * np;
+    if (o.n > 544) return ORBHIP_ERR_UNSUPPORTED;   // single-workgroup Cholesky (LDS-resident panel)
+    o.pose.resize((size_t)8 * P);
+    for (int i = 0; i < P; i++) se3_from_float(pr->pose_q + 4 * i, pr->pose_t + 3 * i, &o.pose[8 * i]);
+    o.pts.assign(pr->points, pr->points + 3 * (size_t)M);
+    o.obs.resize((size_t)2 * E);
+    o.info.resize(E);
+    o.e_pose.assign(pr->edge_pose, pr->edge_pose + E);
+    o.e_pt.assign(pr->edge_point, pr->edge_point + E);
+    for (int e = 0; e < E; e++) {
+        o.obs[2 * e] = pr->edge_uv[2 * e];
+        o.obs[2 * e + 1] = pr->edge_uv[2 * e + 1];
+        o.info[e] = (double)pr->inv_sigma2[pr->edge_octave[e]];
+    }
+    o.pt_ptr.assign(M + 1, 0);
+    o.ps_ptr.assign(np + 1, 0);
+    for (int e = 0; e < E; e++) {
+        o.pt_ptr[o.e_pt[e] + 1]++;
+        if (o.opt[o.e_pose[e]] >= 0) o.ps_ptr[o.opt[o.e_pose[e]] + 1]++;
+    }
+    for (int m = 0; m < M; m++) o.pt_ptr[m + 1] += o.pt_ptr[m];
+    for (int i = 0; i < np; i++) o.ps_ptr[i + 1] += o.ps_ptr[i];
+    o.pt_edges.resize(E);
+    o.ps_edges.resize(o.ps_ptr[np]);
+    {
+        std::vector<int> fp(o.pt_ptr.begin(), o.pt_ptr.end() - 1), fq(o.ps_ptr.begin(), o.ps_ptr.end() - 1);
+        for (int e = 0; e < E; e++) {
+            o.pt_edges[fp[o.e_pt[e]]++] = e;
+            const int oi = o.opt[o.e_pose[e]];
+            if (oi >= 0) o.ps_edges[fq[oi]++] = e;
+        }
+    }
+    // Schur pairs (a, b) of one landmark with opt(a) <= opt(b), grouped by block (i, j) with a
+    // counting sort on the dense block id i*np + j; within a block: landmark order (deterministic).
+    std::vector<int> cnt((size_t)np * np, 0);
+    for (int i = 0; i < np; i++) cnt[(size_t)i * np + i] = 0;
+    size_t npairs = 0;
+    for (int m = 0; m < M; m++)
+        for (int ka = o.pt_ptr[m]; ka < o.pt_ptr[m + 1]; ka++) {
+            const int ia = o.opt[o.e_pose[o.pt_edges[ka]]];
+            if (ia < 0) continue;
+            for (int kb = o.pt_ptr[m]; kb < o.pt_ptr[m + 1]; kb++) {
+                const int ib = o.opt[o.e_pose[o.pt_edges[kb]]];
+                if (ib < 0 || ib < ia) continue;
+                cnt[(size_t)ia * np + ib]++;
+                npairs++;
+            }
+        }
+    std::vector<int> bid((size_t)np * np, -1);
+    o.blk_ptr.assign(1, 0);
+    for (int i = 0; i < np; i++)
+        for (int j = i; j < np; j++) {
+            const size_t k = (size_t)i * np + j;
+            if (i == j || cnt[k] > 0) {
+                bid[k] = (int)o.blk_i.size();
+                o.blk_i.push_back(i);
+                o.blk_j.push_back(j);
+                o.blk_ptr.push_back(o.blk_ptr.back() + cnt[k]);
+            }
+        }
+    o.nblk = (int)o.blk_i.size();
+    o.blk_pairs.resize(2 * npairs);
+    std::vector<int> fill(o.blk_ptr.begin(), o.blk_ptr.end() - 1);
+    for (int m = 0; m < M; m++)
+        for (int ka = o.pt_ptr[m]; ka < o.pt_ptr[m + 1]; ka++) {
+            const int ea = o.pt_edges[ka], ia = o.opt[o.e_pose[ea]];
+            if (ia < 0) continue;
+            for (int kb = o.pt_ptr[m]; kb < o.pt_ptr[m + 1]; kb++) {
+                const int eb = o.pt_edges[kb], ib = o.opt[o.e_pose[eb]];
+                if (ib < 0 || ib < ia) continue;
+                const int slot = fill[bid[(size_t)ia * np + ib]]++;
+                o.blk_pairs[2 * slot] = ea;
+                o.blk_pairs[2 * slot + 1] = eb;
+            }
+        }
+    return ORBHIP_OK;
+}
+
 template <typename T>
 struct DBuf {
     T* p = nullptr;
@@ -632,259 +894,345 @@ struct DBuf {
         if (e == hipSuccess) n = c;
         return e;
     }
-    hipError_t up(const std::vector<T>& v, hipStream_t st) {
-        hipError_t e = ensure(v.size());
-        if (e != hipSuccess || v.empty()) return e;
-        return hipMemcpyAsync(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, st);
-    }
 };
+
+}  // namespace
 
 struct BaWorkspace {
-    DBuf<double> pose, pose_bak, pts, pts_bak, e_obs, e_info, e_err, e_chi2, e_rho0, e_rho1, Hpp, Hll, Hpl, b, Dinv, db,
-        W, S, bs, x, red;
-    DBuf<int> opt, e_pose, e_pt, pt_ptr, pt_edges, ps_ptr, ps_edges, blk_i, blk_j, blk_ptr, blk_pairs, flag;
-    double* h_red = nullptr;   // pinned: red[3] + flag
+    DBuf<double> dbl;      // all fp64 per-problem arrays, packed
+    DBuf<int> ints;        // all int per-problem arrays, packed
+    DBuf<BaArgs> args;
+    DBuf<int> act;         // active problem lists (several slots)
+    DBuf<double> lam;      // per-problem lambda
+    DBuf<double> gath;     // gathered red/flag of the active problems
+    double* h_gath = nullptr;  // pinned
+    double* h_lam = nullptr;   // pinned
+    double* h_red = nullptr;   // pinned: per problem red[4] + flag
+    int* h_act = nullptr;      // pinned
+    size_t h_cap = 0;
 };
 
-BaWorkspace* ba_create() {
-    BaWorkspace* w = new BaWorkspace();
-    if (hipHostMalloc((void**)&w->h_red, 64, hipHostMallocDefault) != hipSuccess) { delete w; return nullptr; }
-    return w;
-}
+BaWorkspace* ba_create() { return new BaWorkspace(); }
 
 void ba_destroy(BaWorkspace* w) {
     if (!w) return;
+    if (w->h_lam) (void)hipHostFree(w->h_lam);
     if (w->h_red) (void)hipHostFree(w->h_red);
+    if (w->h_act) (void)hipHostFree(w->h_act);
+    if (w->h_gath) (void)hipHostFree(w->h_gath);
     delete w;
 }
 
-#define BAOK(x)                                                                                    \
-    do {                                                                                           \
-        hipError_t e_ = (x);                                                                       \
-        if (e_ != hipSuccess) {                                                                    \
-            std::fprintf(stderr, "orbhip ba: %s: %s\n", #x, hipGetErrorString(e_));                \
-            return ORBHIP_ERR_DEVICE;                                                              \
-        }                                                                                          \
-    } while (0)
+struct LmState {
+    double lambda = 0, ni = 2, currentChi = 0, rho = 0;
+    int nBad = 0, it = 0, trials = 0, qmax = 0;
+    bool done = false, errors_valid = true;
+};
 
-static inline void se3_from_float(const float* q, const float* t, double out[8]) {
-    double x = q[0], y = q[1], z = q[2], w = q[3];
-    if (w < 0) { x = -x; y = -y; z = -z; w = -w; }
-    const double n = std::sqrt(x * x + y * y + z * z + w * w);
-    out[0] = x / n; out[1] = y / n; out[2] = z / n; out[3] = w / n;
-    out[4] = t[0]; out[5] = t[1]; out[6] = t[2]; out[7] = 0;
-}
-
-int ba_solve(BaWorkspace* ws, const orbhip_ba_problem* pr, orbhip_ba_result* res, const volatile int* stop,
-             hipStream_t st) {
-    const int P = pr->n_poses, M = pr->n_points, E = pr->n_edges;
-    if (P < 0 || M < 0 || E < 0 || (P && (!pr->pose_q || !pr->pose_t || !pr->pose_fixed)) || (M && !pr->points) ||
-        (E && (!pr->edge_pose || !pr->edge_point || !pr->edge_uv || !pr->edge_octave || !pr->inv_sigma2)))
-        return ORBHIP_ERR_ARG;
-    for (int e = 0; e < E; e++)
-        if (pr->edge_pose[e] < 0 || pr->edge_pose[e] >= P || pr->edge_point[e] < 0 || pr->edge_point[e] >= M ||
-            pr->edge_octave[e] < 0 || pr->edge_octave[e] >= pr->n_octaves)
-            return ORBHIP_ERR_ARG;
-    // ---- host-side structure (index mapping, CSR, Schur pair lists) ----
-    std::vector<int> opt(P, -1);
-    int np = 0;
-    for (int i = 0; i < P; i++)
-        if (!pr->pose_fixed[i]) opt[i] = np++;
-    const int n = 6 * np;
-    if (n > 1024) return ORBHIP_ERR_UNSUPPORTED;   // single-workgroup Cholesky envelope (round 1)
-    std::vector<double> pose((size_t)8 * P), pts((size_t)3 * M), obs((size_t)2 * E), info(E);
-    for (int i = 0; i < P; i++) se3_from_float(pr->pose_q + 4 * i, pr->pose_t + 3 * i, &pose[8 * i]);
-    for (int k = 0; k < 3 * M; k++) pts[k] = pr->points[k];
-    for (int e = 0; e < E; e++) {
-        obs[2 * e] = pr->edge_uv[2 * e];
-        obs[2 * e + 1] = pr->edge_uv[2 * e + 1];
-        info[e] = (double)pr->inv_sigma2[pr->edge_octave[e]];
+int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B, orbhip_ba_result* const* res,
+                   const volatile int* stop, hipStream_t st) {
+    if (B <= 0 || !probs || !res) return ORBHIP_ERR_ARG;
+    std::vector<Prep> pp(B);
+    for (int b = 0; b < B; b++) {
+        if (!probs[b] || !res[b]) return ORBHIP_ERR_ARG;
+        const int rc = prepare(probs[b], pp[b]);
+        if (rc) return rc;
     }
-    std::vector<int> pt_ptr(M + 1, 0), ps_ptr(np + 1, 0);
-    for (int e = 0; e < E; e++) {
-        pt_ptr[pr->edge_point[e] + 1]++;
-        if (opt[pr->edge_pose[e]] >= 0) ps_ptr[opt[pr->edge_pose[e]] + 1]++;
+    // ---- packed layout ----
+    size_t nd = 0, ni = 0;
+    for (auto& p : pp) {
+        const size_t P = p.P, M = p.M, E = p.E, np_ = p.np, n = p.n;
+        p.o_pose = nd; nd += 16 * P;              // pose + pose_bak
+        p.o_pts = nd; nd += 6 * M;                // pts + pts_bak
+        p.o_e2 = nd; nd += 2 * E * 2;             // e_obs, e_err
+        p.o_edge = nd; nd += 4 * E;               // e_info, e_chi2, e_rho0, e_rho1
+        p.o_e18 = nd; nd += 36 * E;               // Hpl, W
+        p.o_np36 = nd; nd += 36 * np_;            // Hpp
+        p.o_m9 = nd; nd += 18 * M;                // Hll, Dinv
+        p.o_m3 = nd; nd += 3 * M;                 // db
+        p.o_b = nd; nd += 2 * (n + 3 * M);        // b, x
+        p.o_n = nd; nd += n + 4;                  // bs, red[4]
+        nd = (nd + 1) & ~size_t(1);
+        p.o_S = nd; nd += n * n;                  // S (16-byte aligned)
+        nd = (nd + 1) & ~size_t(1);
+        p.o_opt = ni; ni += P + 4;                // opt, flag
+        p.o_ptp = ni; ni += 2 * E + (M + 1) + E;  // e_pose, e_pt, pt_ptr, pt_edges
+        p.o_psp = ni; ni += (np_ + 1);            // ps_ptr
+        p.o_ps_edges = ni; ni += p.ps_edges.size();
+        p.o_blk = ni; ni += 2 * p.nblk + (p.nblk + 1);
+        p.o_pairs = ni; ni += p.blk_pairs.size();
     }
-    for (int m = 0; m < M; m++) pt_ptr[m + 1] += pt_ptr[m];
-    for (int i = 0; i < np; i++) ps_ptr[i + 1] += ps_ptr[i];
-    std::vector<int> pt_edges(E), ps_edges(ps_ptr[np]);
-    {
-        std::vector<int> fp(pt_ptr.begin(), pt_ptr.end() - 1), fq(ps_ptr.begin(), ps_ptr.end() - 1);
-        for (int e = 0; e < E; e++) {
-            pt_edges[fp[pr->edge_point[e]]++] = e;
-            const int oi = opt[pr->edge_pose[e]];
-            if (oi >= 0) ps_edges[fq[oi]++] = e;
-        }
+    BAOK(ws->dbl.ensure(nd));
+    BAOK(ws->ints.ensure(ni));
+    BAOK(ws->args.ensure(B));
+    BAOK(ws->act.ensure(2 * (size_t)B));
+    BAOK(ws->lam.ensure(B));
+    BAOK(ws->gath.ensure(5 * (size_t)B));
+    if (ws->h_cap < (size_t)B) {
+        if (ws->h_lam) (void)hipHostFree(ws->h_lam);
+        if (ws->h_red) (void)hipHostFree(ws->h_red);
+        ws->h_red = nullptr;
+        if (ws->h_act) (void)hipHostFree(ws->h_act);
+        if (ws->h_gath) (void)hipHostFree(ws->h_gath);
+        BAOK(hipHostMalloc((void**)&ws->h_gath, sizeof(double) * 5 * B, hipHostMallocDefault));
+        BAOK(hipHostMalloc((void**)&ws->h_lam, sizeof(double) * B, hipHostMallocDefault));
+        BAOK(hipHostMalloc((void**)&ws->h_red, sizeof(double) * 5 * B, hipHostMallocDefault));
+        BAOK(hipHostMalloc((void**)&ws->h_act, sizeof(int) * 2 * B, hipHostMallocDefault));
+        ws->h_cap = B;
     }
-    // Schur pairs: for every landmark, every (a, b) of its edges with opt(a) <= opt(b)
-    std::map<std::pair<int, int>, std::vector<std::pair<int, int>>> blocks;
-    for (int i = 0; i < np; i++) blocks[{i, i}];   // diagonal blocks always present
-    for (int m = 0; m < M; m++) {
-        for (int ka = pt_ptr[m]; ka < pt_ptr[m + 1]; ka++) {
-            const int ea = pt_edges[ka], ia = opt[pr->edge_pose[ea]];
-            if (ia < 0) continue;
-            for (int kb = pt_ptr[m]; kb < pt_ptr[m + 1]; kb++) {
-                const int eb = pt_edges[kb], ib = opt[pr->edge_pose[eb]];
-                if (ib < 0 || ib < ia) continue;
-                blocks[{ia, ib}].push_back({ea, eb});
-            }
-        }
+    std::vector<double> hd(nd, 0.0);
+    std::vector<int> hi(ni, 0);
+    std::vector<BaArgs> ha(B);
+    double* D = ws->dbl.p;
+    int* I = ws->ints.p;
+    for (int b = 0; b < B; b++) {
+        Prep& p = pp[b];
+        const orbhip_ba_problem* pr = probs[b];
+        std::copy(p.pose.begin(), p.pose.end(), hd.begin() + p.o_pose);
+        std::copy(p.pts.begin(), p.pts.end(), hd.begin() + p.o_pts);
+        std::copy(p.obs.begin(), p.obs.end(), hd.begin() + p.o_e2);
+        std::copy(p.info.begin(), p.info.end(), hd.begin() + p.o_edge);
+        std::copy(p.opt.begin(), p.opt.end(), hi.begin() + p.o_opt);
+        size_t q = p.o_ptp;
+        std::copy(p.e_pose.begin(), p.e_pose.end(), hi.begin() + q); q += p.E;
+        std::copy(p.e_pt.begin(), p.e_pt.end(), hi.begin() + q); q += p.E;
+        std::copy(p.pt_ptr.begin(), p.pt_ptr.end(), hi.begin() + q); q += p.M + 1;
+        std::copy(p.pt_edges.begin(), p.pt_edges.end(), hi.begin() + q);
+        std::copy(p.ps_ptr.begin(), p.ps_ptr.end(), hi.begin() + p.o_psp);
+        std::copy(p.ps_edges.begin(), p.ps_edges.end(), hi.begin() + p.o_ps_edges);
+        q = p.o_blk;
+        std::copy(p.blk_i.begin(), p.blk_i.end(), hi.begin() + q); q += p.nblk;
+        std::copy(p.blk_j.begin(), p.blk_j.end(), hi.begin() + q); q += p.nblk;
+        std::copy(p.blk_ptr.begin(), p.blk_ptr.end(), hi.begin() + q);
+        std::copy(p.blk_pairs.begin(), p.blk_pairs.end(), hi.begin() + p.o_pairs);
+        BaArgs& a = ha[b];
+        a.P = p.P; a.M = p.M; a.E = p.E; a.np = p.np; a.n = p.n;
+        a.fx = pr->fx; a.fy = pr->fy; a.cx = pr->cx; a.cy = pr->cy; a.delta = pr->huber_delta;
+        a.pose = D + p.o_pose; a.pose_bak = a.pose + 8 * (size_t)p.P;
+        a.pts = D + p.o_pts; a.pts_bak = a.pts + 3 * (size_t)p.M;
+        a.e_obs = D + p.o_e2; a.e_err = D + p.o_e2 + 2 * (size_t)p.E;
+        a.e_info = D + p.o_edge; a.e_chi2 = D + p.o_edge + p.E; a.e_rho0 = a.e_chi2 + p.E; a.e_rho1 = a.e_rho0 + p.E;
+        a.Hpl = D + p.o_e18; a.W = a.Hpl + 18 * (size_t)p.E;
+        a.Hpp = D + p.o_np36;
+        a.Hll = D + p.o_m9; a.Dinv = a.Hll + 9 * (size_t)p.M;
+        a.db = D + p.o_m3;
+        a.b = D + p.o_b; a.x = a.b + p.n + 3 * (size_t)p.M;
+        a.bs = D + p.o_n; a.red = a.bs + p.n;
+        a.S = D + p.o_S;
+        a.opt = I + p.o_opt; a.flag = I + p.o_opt + p.P;
+        a.e_pose = I + p.o_ptp; a.e_pt = a.e_pose + p.E; a.pt_ptr = a.e_pt + p.E; a.pt_edges = a.pt_ptr + p.M + 1;
+        a.ps_ptr = I + p.o_psp; a.ps_edges = I + p.o_ps_edges;
+        a.blk_i = I + p.o_blk; a.blk_j = a.blk_i + p.nblk; a.blk_ptr = a.blk_j + p.nblk;
+        a.blk_pairs = I + p.o_pairs;
+        a.nblk = p.nblk;
+        a.lambda = ws->lam.p + b;
     }
-    std::vector<int> blk_i, blk_j, blk_ptr(1, 0), blk_pairs;
-    for (auto& kv : blocks) {
-        blk_i.push_back(kv.first.first);
-        blk_j.push_back(kv.first.second);
-        for (auto& pe : kv.second) { blk_pairs.push_back(pe.first); blk_pairs.push_back(pe.second); }
-        blk_ptr.push_back((int)blk_pairs.size() / 2);
-    }
-    const int nblk = (int)blk_i.size();
-    // ---- upload ----
-    std::vector<int> ep(pr->edge_pose, pr->edge_pose + E), em(pr->edge_point, pr->edge_point + E);
-    BAOK(ws->pose.up(pose, st)); BAOK(ws->pose_bak.ensure(pose.size()));
-    BAOK(ws->pts.up(pts, st)); BAOK(ws->pts_bak.ensure(pts.size()));
-    BAOK(ws->e_obs.up(obs, st)); BAOK(ws->e_info.up(info, st));
-    BAOK(ws->opt.up(opt, st)); BAOK(ws->e_pose.up(ep, st)); BAOK(ws->e_pt.up(em, st));
-    BAOK(ws->pt_ptr.up(pt_ptr, st)); BAOK(ws->pt_edges.up(pt_edges, st));
-    BAOK(ws->ps_ptr.up(ps_ptr, st)); BAOK(ws->ps_edges.up(ps_edges, st));
-    BAOK(ws->blk_i.up(blk_i, st)); BAOK(ws->blk_j.up(blk_j, st));
-    BAOK(ws->blk_ptr.up(blk_ptr, st)); BAOK(ws->blk_pairs.up(blk_pairs, st));
-    BAOK(ws->e_err.ensure(2 * (size_t)E)); BAOK(ws->e_chi2.ensure(E)); BAOK(ws->e_rho0.ensure(E));
-    BAOK(ws->e_rho1.ensure(E));
-    BAOK(ws->Hpp.ensure((size_t)36 * np)); BAOK(ws->Hll.ensure((size_t)9 * M));
-    BAOK(ws->Hpl.ensure((size_t)18 * E)); BAOK(ws->b.ensure((size_t)n + 3 * M));
-    BAOK(ws->Dinv.ensure((size_t)9 * M)); BAOK(ws->db.ensure((size_t)3 * M)); BAOK(ws->W.ensure((size_t)18 * E));
-    BAOK(ws->S.ensure((size_t)n * n)); BAOK(ws->bs.ensure(n)); BAOK(ws->x.ensure((size_t)n + 3 * M));
-    BAOK(ws->red.ensure(4)); BAOK(ws->flag.ensure(4));
-    BAOK(hipMemsetAsync(ws->Hpl.p, 0, sizeof(double) * 18 * std::max(E, 1), st));
-    BAOK(hipMemsetAsync(ws->W.p, 0, sizeof(double) * 18 * std::max(E, 1), st));
-    BaArgs a;
-    a.P = P; a.M = M; a.E = E; a.np = np; a.n = n;
-    a.fx = pr->fx; a.fy = pr->fy; a.cx = pr->cx; a.cy = pr->cy; a.delta = pr->huber_delta;
-    a.pose = ws->pose.p; a.pose_bak = ws->pose_bak.p; a.pts = ws->pts.p; a.pts_bak = ws->pts_bak.p;
-    a.opt = ws->opt.p; a.e_pose = ws->e_pose.p; a.e_pt = ws->e_pt.p; a.e_obs = ws->e_obs.p; a.e_info = ws->e_info.p;
-    a.e_err = ws->e_err.p; a.e_chi2 = ws->e_chi2.p; a.e_rho0 = ws->e_rho0.p; a.e_rho1 = ws->e_rho1.p;
-    a.Hpp = ws->Hpp.p; a.Hll = ws->Hll.p; a.Hpl = ws->Hpl.p; a.b = ws->b.p; a.Dinv = ws->Dinv.p; a.db = ws->db.p;
-    a.W = ws->W.p; a.S = ws->S.p; a.bs = ws->bs.p; a.x = ws->x.p;
-    a.pt_ptr = ws->pt_ptr.p; a.pt_edges = ws->pt_edges.p; a.ps_ptr = ws->ps_ptr.p; a.ps_edges = ws->ps_edges.p;
-    a.blk_i = ws->blk_i.p; a.blk_j = ws->blk_j.p; a.blk_ptr = ws->blk_ptr.p; a.blk_pairs = ws->blk_pairs.p;
-    a.nblk = nblk; a.red = ws->red.p; a.flag = ws->flag.p;
-    const size_t chol_lds = sizeof(double) * (2 + 256 + ((n + 15) & ~15) + (size_t)((n + 15) & ~15) * 16);
-    if (chol_lds > 160 * 1024) return ORBHIP_ERR_UNSUPPORTED;
+    BAOK(hipMemcpyAsync(ws->dbl.p, hd.data(), nd * sizeof(double), hipMemcpyHostToDevice, st));
+    BAOK(hipMemcpyAsync(ws->ints.p, hi.data(), ni * sizeof(int), hipMemcpyHostToDevice, st));
+    BAOK(hipMemcpyAsync(ws->args.p, ha.data(), B * sizeof(BaArgs), hipMemcpyHostToDevice, st));
     static bool lds_set = false;
     if (!lds_set) {
         BAOK(hipFuncSetAttribute((const void*)k_ba_cholesky, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         lds_set = true;
     }
-    (void)hipGetLastError();   // clear any sticky error left by an earlier, already-reported call
-    auto g = [](int n_, int b_) { return dim3((unsigned)std::max(1, (n_ + b_ - 1) / b_)); };
-    auto read_red = [&](int what) -> int {
-        BAOK(hipMemcpyAsync(ws->h_red, ws->red.p, 4 * sizeof(double), hipMemcpyDeviceToHost, st));
-        if (what) BAOK(hipMemcpyAsync(ws->h_red + 4, ws->flag.p, sizeof(int), hipMemcpyDeviceToHost, st));
-        BAOK(hipStreamSynchronize(st));
+    int maxM = 0, maxE = 0, maxP = 0, maxNp = 0, maxBlk = 0, maxN = 0;
+    for (auto& p : pp) {
+        maxM = std::max(maxM, p.M); maxE = std::max(maxE, p.E); maxP = std::max(maxP, p.P);
+        maxNp = std::max(maxNp, p.np); maxBlk = std::max(maxBlk, p.nblk); maxN = std::max(maxN, p.n);
+    }
+    const size_t chol_lds = sizeof(double) * (size_t)(2 + 32 * 33 + ((maxN + 31) & ~31) +
+                                                      (size_t)((maxN + 31) & ~31) * kPS + 64);
+    auto gx = [](int n_, int b_) { return (unsigned)std::max(1, (n_ + b_ - 1) / b_); };
+    (void)hipGetLastError();
+    int* d_act = ws->act.p;
+    int* h_act = ws->h_act;
+    auto upload_act = [&](const std::vector<int>& v) -> int {
+        for (size_t i = 0; i < v.size(); i++) h_act[i] = v[i];
+        BAOK(hipMemcpyAsync(d_act, h_act, v.size() * sizeof(int), hipMemcpyHostToDevice, st));
         return ORBHIP_OK;
     };
-    // ---- optimize(iterations) ----
-    if (E > 0) hipLaunchKernelGGL(k_ba_errors, g(E, 256), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(k_ba_reduce, dim3(1), dim3(1024), 0, st, a, 0.0, 1);
+    const BaArgs* dA = ws->args.p;
+    // per-round readback: the act list currently on the device (same order as v) is gathered
+    // into one contiguous buffer and copied with ONE transfer; h_red is indexed by problem.
+    auto read_red = [&](const std::vector<int>& v) -> int {
+        hipLaunchKernelGGL(k_ba_gather_red, dim3((unsigned)((v.size() + 63) / 64)), dim3(64), 0, st, dA, d_act,
+                           (int)v.size(), ws->gath.p);
+        BAOK(hipMemcpyAsync(ws->h_gath, ws->gath.p, 5 * v.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+        BAOK(hipStreamSynchronize(st));
+        for (size_t i = 0; i < v.size(); i++)
+            for (int k = 0; k < 5; k++) ws->h_red[5 * v[i] + k] = ws->h_gath[5 * i + k];
+        return ORBHIP_OK;
+    };
+    std::vector<LmState> L(B);
+    std::vector<int> all(B);
+    for (int b = 0; b < B; b++) all[b] = b;
+    // ---- initial errors and chi2 ----
+    if (upload_act(all)) return ORBHIP_ERR_DEVICE;
+    hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), dim3(256), 0, st, dA, d_act);
+    hipLaunchKernelGGL(k_ba_reduce, dim3(B), dim3(1024), 0, st, dA, d_act, 1);
     BAOK(hipGetLastError());
-    if (read_red(0)) return ORBHIP_ERR_DEVICE;
-    double currentChi = ws->h_red[0];
-    res->initial_chi2 = currentChi;
-    double lambda = 0, ni = 2;
-    int nBad = 0, it = 0, trials = 0;
+    if (read_red(all)) return ORBHIP_ERR_DEVICE;
+    for (int b = 0; b < B; b++) {
+        L[b].currentChi = ws->h_red[5 * b];
+        res[b]->initial_chi2 = L[b].currentChi;
+    }
+    const int maxIt = [&] { int m = 0; for (int b = 0; b < B; b++) m = std::max(m, probs[b]->iterations); return m; }();
     const double dmax = std::numeric_limits<double>::max();
-    bool errors_valid = true;
-    for (it = 0; it < pr->iterations && !(stop && *stop); it++) {
-        if (!errors_valid && E > 0) hipLaunchKernelGGL(k_ba_errors, g(E, 256), dim3(256), 0, st, a);
-        errors_valid = true;
-        if (M > 0) hipLaunchKernelGGL(k_ba_lin_points, g(M, 256), dim3(256), 0, st, a);
-        if (np > 0) hipLaunchKernelGGL(k_ba_lin_poses, g(np, 4), dim3(256), 0, st, a);
+    for (int it = 0; it < maxIt; it++) {
+        std::vector<int> act;
+        for (int b = 0; b < B; b++)
+            if (!L[b].done && it < probs[b]->iterations && !(stop && *stop)) act.push_back(b);
+            else L[b].done = true;
+        if (act.empty()) break;
+        const unsigned na = (unsigned)act.size();
+        // computeActiveErrors (only where the device copy is stale) + buildSystem
+        std::vector<int> stale;
+        for (int b : act)
+            if (!L[b].errors_valid) stale.push_back(b);
+        if (!stale.empty()) {
+            if (upload_act(stale)) return ORBHIP_ERR_DEVICE;
+            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), (unsigned)stale.size()), dim3(256), 0, st, dA, d_act);
+        }
+        if (upload_act(act)) return ORBHIP_ERR_DEVICE;
+        hipLaunchKernelGGL(k_ba_lin_points, dim3(gx(maxM, 256), na), dim3(256), 0, st, dA, d_act);
+        hipLaunchKernelGGL(k_ba_lin_poses, dim3(gx(maxNp, 4), na), dim3(256), 0, st, dA, d_act);
         if (it == 0) {
-            hipLaunchKernelGGL(k_ba_reduce, dim3(1), dim3(1024), 0, st, a, 0.0, 4);
-            if (read_red(0)) return ORBHIP_ERR_DEVICE;
-            lambda = 1e-5 * ws->h_red[2];
-            ni = 2;
-            nBad = 0;
+            hipLaunchKernelGGL(k_ba_reduce, dim3(na), dim3(1024), 0, st, dA, d_act, 4);
+            if (read_red(act)) return ORBHIP_ERR_DEVICE;
+            for (int b : act) { L[b].lambda = 1e-5 * ws->h_red[5 * b + 2]; L[b].ni = 2; L[b].nBad = 0; }
         }
-        double rho = 0, tempChi = currentChi;
-        int qmax = 0;
-        do {
-            // setLambda + Schur + solve + update (push happens inside the update kernels)
-            if (n > 0) BAOK(hipMemsetAsync(a.S, 0, sizeof(double) * (size_t)n * n, st));
-            if (M > 0) hipLaunchKernelGGL(k_ba_schur_points, g(M, 256), dim3(256), 0, st, a, lambda);
-            if (nblk > 0) hipLaunchKernelGGL(k_ba_schur_blocks, g(nblk, 4), dim3(256), 0, st, a, lambda);
-            if (n > 0) {
-                hipLaunchKernelGGL(k_ba_schur_b, g(n, 256), dim3(256), 0, st, a);
-                hipLaunchKernelGGL(k_ba_cholesky, dim3(1), dim3(1024), chol_lds, st, a.S, a.bs, a.x, n, a.flag);
-            } else {
-                BAOK(hipMemsetAsync(a.flag, 0xFF, sizeof(int), st));
-            }
-            if (M > 0) hipLaunchKernelGGL(k_ba_backsub, g(M, 256), dim3(256), 0, st, a);
-            if (P > 0) hipLaunchKernelGGL(k_ba_update_poses, g(P, 256), dim3(256), 0, st, a);
-            if (E > 0) hipLaunchKernelGGL(k_ba_errors, g(E, 256), dim3(256), 0, st, a);
-            hipLaunchKernelGGL(k_ba_reduce, dim3(1), dim3(1024), 0, st, a, lambda, 3);
+        for (int b : act) { L[b].qmax = 0; L[b].rho = 0; }
+        std::vector<int> trial = act;
+        while (!trial.empty()) {
+            const unsigned nt_ = (unsigned)trial.size();
+            for (int b : trial) ws->h_lam[b] = L[b].lambda;
+            BAOK(hipMemcpyAsync(ws->lam.p, ws->h_lam, B * sizeof(double), hipMemcpyHostToDevice, st));
+            if (upload_act(trial)) return ORBHIP_ERR_DEVICE;
+            hipLaunchKernelGGL(k_ba_zero_s, dim3(64, nt_), dim3(256), 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_schur_points, dim3(gx(maxM, 256), nt_), dim3(256), 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_schur_w, dim3(gx(maxE, 256), nt_), dim3(256), 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_schur_blocks, dim3(gx(maxBlk, 4), nt_), dim3(256), 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_schur_b, dim3(gx(maxNp, 4), nt_), dim3(256), 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_cholesky, dim3(nt_), dim3(512), chol_lds, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_backsub, dim3(gx(maxM, 256), nt_), dim3(256), 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_update_poses, dim3(gx(maxP, 256), nt_), dim3(256), 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), nt_), dim3(256), 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_reduce, dim3(nt_), dim3(1024), 0, st, dA, d_act, 3);
             BAOK(hipGetLastError());
-            if (read_red(1)) return ORBHIP_ERR_DEVICE;
-            const bool ok2 = *(int*)(ws->h_red + 4) != 0;
-            tempChi = ws->h_red[0];
-            if (!ok2) tempChi = dmax;
-            rho = currentChi - tempChi;
-            double scale = ws->h_red[1] + 1e-3;
-            rho /= scale;
-            if (rho > 0 && std::isfinite(tempChi)) {
-                double alpha = 1. - std::pow((2 * rho - 1), 3);
-                alpha = std::min(alpha, 2. / 3.);
-                lambda *= std::max(1. / 3., alpha);
-                ni = 2;
-                if (pr->early_stop) {
-                    if ((currentChi - tempChi) < 1e-3 * currentChi) nBad++;
-                    else nBad = 0;
+            if (read_red(trial)) return ORBHIP_ERR_DEVICE;
+            std::vector<int> pop, next;
+            for (int b : trial) {
+                LmState& s = L[b];
+                const bool ok2 = *(int*)(ws->h_red + 5 * b + 4) != 0;
+                double tempChi = ok2 ? ws->h_red[5 * b] : dmax;
+                double rho = s.currentChi - tempChi;
+                rho /= (ws->h_red[5 * b + 1] + 1e-3);
+                if (rho > 0 && std::isfinite(tempChi)) {
+                    double alpha = 1. - std::pow((2 * rho - 1), 3);
+                    alpha = std::min(alpha, 2. / 3.);
+                    s.lambda *= std::max(1. / 3., alpha);
+                    s.ni = 2;
+                    if (probs[b]->early_stop) {
+                        if ((s.currentChi - tempChi) < 1e-3 * s.currentChi) s.nBad++;
+                        else s.nBad = 0;
+                    }
+                    s.currentChi = tempChi;
+                } else {
+                    s.lambda *= s.ni;
+                    s.ni *= 2;
+                    pop.push_back(b);
                 }
-                currentChi = tempChi;
-            } else {
-                lambda *= ni;
-                ni *= 2;
-                // pop: restore the pre-trial state
-                BAOK(hipMemcpyAsync(a.pose, a.pose_bak, sizeof(double) * 8 * (size_t)P, hipMemcpyDeviceToDevice, st));
-                BAOK(hipMemcpyAsync(a.pts, a.pts_bak, sizeof(double) * 3 * (size_t)M, hipMemcpyDeviceToDevice, st));
+                s.rho = rho;
+                s.qmax++;
+                s.trials++;
+                if (rho < 0 && s.qmax < 10 && !(stop && *stop)) next.push_back(b);
             }
-            qmax++;
-            trials++;
-        } while (rho < 0 && qmax < 10 && !(stop && *stop));
-        // g2o recomputes the active errors at the start of every iteration; after an accepted
-        // trial the device already holds them, after a rejected one they belong to the popped
-        // trial (left stale for e->chi2(), exactly like g2o) and are refreshed below if we go on.
-        errors_valid = rho > 0;
-        if (qmax == 10 || rho == 0) { it++; break; }
-        if (pr->early_stop && nBad >= 3) { it++; break; }
-    }
-    res->final_chi2 = currentChi;
-    res->iterations_done = it;
-    res->lm_trials = trials;
-    // ---- outputs ----
-    std::vector<double> pose_o((size_t)8 * P), pts_o((size_t)3 * M), chi2_o(E);
-    if (P) BAOK(hipMemcpyAsync(pose_o.data(), a.pose, sizeof(double) * 8 * P, hipMemcpyDeviceToHost, st));
-    if (M) BAOK(hipMemcpyAsync(pts_o.data(), a.pts, sizeof(double) * 3 * M, hipMemcpyDeviceToHost, st));
-    if (E) BAOK(hipMemcpyAsync(chi2_o.data(), a.e_chi2, sizeof(double) * E, hipMemcpyDeviceToHost, st));
-    BAOK(hipStreamSynchronize(st));
-    for (int i = 0; i < P; i++) {
-        if (res->pose_q) for (int k = 0; k < 4; k++) res->pose_q[4 * i + k] = (float)pose_o[8 * i + k];
-        if (res->pose_t) for (int k = 0; k < 3; k++) res->pose_t[3 * i + k] = (float)pose_o[8 * i + 4 + k];
-    }
-    if (res->points) for (int k = 0; k < 3 * M; k++) res->points[k] = (float)pts_o[k];
-    for (int e = 0; e < E; e++) {
-        if (res->edge_chi2) res->edge_chi2[e] = (float)chi2_o[e];
-        if (res->edge_depth_ok) {   // isDepthPositive: (T.map(X)).z > 0
-            const double* T = &pose_o[8 * pr->edge_pose[e]];
-            const double* X = &pts_o[3 * pr->edge_point[e]];
-            double ux = T[1] * X[2] - T[2] * X[1], uy = T[2] * X[0] - T[0] * X[2];
-            ux += ux; uy += uy;
-            const double uz2 = 2 * (T[0] * X[1] - T[1] * X[0]);
-            const double cz = T[0] * uy - T[1] * ux;
-            const double z = X[2] + T[3] * uz2 + cz + T[6];
-            res->edge_depth_ok[e] = z > 0.0 ? 1 : 0;
+            if (!pop.empty()) {
+                // act slot 2 keeps the pop list away from the next round's upload
+                for (size_t i = 0; i < pop.size(); i++) h_act[B + i] = pop[i];
+                BAOK(hipMemcpyAsync(d_act + B, h_act + B, pop.size() * sizeof(int), hipMemcpyHostToDevice, st));
+                int maxPM = 0;
+                for (int b : pop) maxPM = std::max(maxPM, std::max(8 * pp[b].P, 3 * pp[b].M));
+                hipLaunchKernelGGL(k_ba_pop, dim3(gx(maxPM, 256), (unsigned)pop.size()), dim3(256), 0, st, dA,
+                                   d_act + B);
+            }
+            trial.swap(next);
+        }
+        for (int b : act) {
+            LmState& s = L[b];
+            s.it = it + 1;
+            s.errors_valid = s.rho > 0;   // rejected: device errors belong to the popped trial (g2o keeps them stale)
+            if (s.qmax == 10 || s.rho == 0) s.done = true;
+            if (probs[b]->early_stop && s.nBad >= 3) s.done = true;
         }
     }
+    // ---- outputs ----
+    for (int b = 0; b < B; b++) {
+        const Prep& p = pp[b];
+        orbhip_ba_result* r = res[b];
+        r->final_chi2 = L[b].currentChi;
+        r->iterations_done = L[b].it;
+        r->lm_trials = L[b].trials;
+        std::vector<double> pose_o((size_t)8 * p.P), pts_o((size_t)3 * p.M), chi2_o(p.E);
+        if (p.P) BAOK(hipMemcpyAsync(pose_o.data(), ha[b].pose, sizeof(double) * 8 * p.P, hipMemcpyDeviceToHost, st));
+        if (p.M) BAOK(hipMemcpyAsync(pts_o.data(), ha[b].pts, sizeof(double) * 3 * p.M, hipMemcpyDeviceToHost, st));
+        if (p.E) BAOK(hipMemcpyAsync(chi2_o.data(), ha[b].e_chi2, sizeof(double) * p.E, hipMemcpyDeviceToHost, st));
+        BAOK(hipStreamSynchronize(st));
+        for (int i = 0; i < p.P; i++) {
+            if (r->pose_q) for (int k = 0; k < 4; k++) r->pose_q[4 * i + k] = (float)pose_o[8 * i + k];
+            if (r->pose_t) for (int k = 0; k < 3; k++) r->pose_t[3 * i + k] = (float)pose_o[8 * i + 4 + k];
+        }
+        if (r->points) for (int k = 0; k < 3 * p.M; k++) r->points[k] = (float)pts_o[k];
+        for (int e = 0; e < p.E; e++) {
+            if (r->edge_chi2) r->edge_chi2[e] = (float)chi2_o[e];
+            if (r->edge_depth_ok) {   // isDepthPositive: (T.map(X)).z > 0
+                const double* T = &pose_o[8 * p.e_pose[e]];
+                const double* X = &pts_o[3 * p.e_pt[e]];
+                double ux = T[1] * X[2] - T[2] * X[1], uy = T[2] * X[0] - T[0] * X[2];
+                ux += ux; uy += uy;
+                const double uz2 = 2 * (T[0] * X[1] - T[1] * X[0]);
+                const double cz = T[0] * uy - T[1] * ux;
+                const double z = X[2] + T[3] * uz2 + cz + T[6];
+                r->edge_depth_ok[e] = z > 0.0 ? 1 : 0;
+            }
+        }
+    }
+    return ORBHIP_OK;
+}
+
+int ba_solve(BaWorkspace* ws, const orbhip_ba_problem* prob, orbhip_ba_result* res, const volatile int* stop,
+             hipStream_t st) {
+    const orbhip_ba_problem* pp[1] = {prob};
+    orbhip_ba_result* rr[1] = {res};
+    return ba_solve_batch(ws, pp, 1, rr, stop, st);
+}
+
+// Diagnostic: factor+solve one SPD system with per-phase cycle stamps (test hook).
+int ba_test_cholesky(const double* A, const double* b, double* x, int n, unsigned long long* phases5, float* ms) {
+    double *dS = nullptr, *db_ = nullptr, *dx = nullptr;
+    int* df = nullptr;
+    unsigned long long* dd = nullptr;
+    BAOK(hipMalloc((void**)&dS, sizeof(double) * n * n));
+    BAOK(hipMalloc((void**)&db_, sizeof(double) * n));
+    BAOK(hipMalloc((void**)&dx, sizeof(double) * n));
+    BAOK(hipMalloc((void**)&df, sizeof(int)));
+    BAOK(hipMalloc((void**)&dd, sizeof(unsigned long long) * 8));
+    BAOK(hipMemcpy(dS, A, sizeof(double) * n * n, hipMemcpyHostToDevice));
+    BAOK(hipMemcpy(db_, b, sizeof(double) * n, hipMemcpyHostToDevice));
+    BAOK(hipMemset(dd, 0, 64));
+    BAOK(hipFuncSetAttribute((const void*)k_chol_test, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    const size_t lds = sizeof(double) * (size_t)(2 + 32 * 33 + ((n + 31) & ~31) + (size_t)((n + 31) & ~31) * kPS + 64);
+    hipEvent_t e0, e1;
+    BAOK(hipEventCreate(&e0)); BAOK(hipEventCreate(&e1));
+    BAOK(hipEventRecord(e0, nullptr));
+    hipLaunchKernelGGL(k_chol_test, dim3(1), dim3(512), lds, nullptr, dS, db_, dx, n, df, dd);
+    BAOK(hipEventRecord(e1, nullptr));
+    BAOK(hipDeviceSynchronize());
+    BAOK(hipEventElapsedTime(ms, e0, e1));
+    BAOK(hipMemcpy(x, dx, sizeof(double) * n, hipMemcpyDeviceToHost));
+    BAOK(hipMemcpy(phases5, dd, sizeof(unsigned long long) * 5, hipMemcpyDeviceToHost));
+    (void)hipFree(dS); (void)hipFree(db_); (void)hipFree(dx); (void)hipFree(df); (void)hipFree(dd);
+    (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
     return ORBHIP_OK;
 }
 

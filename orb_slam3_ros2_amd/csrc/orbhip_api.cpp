@@ -586,7 +586,24 @@ int orbhip_ba_solve(orbhip_ctx* c, const orbhip_ba_problem* prob, orbhip_ba_resu
     return ba_solve(c->ba, prob, res, stop, c->stream);
 }
 
+int orbhip_ba_solve_batch(orbhip_ctx* c, const orbhip_ba_problem* probs, int B, orbhip_ba_result* res,
+                          const volatile int* stop) {
+    if (!c || !probs || !res || B <= 0) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    if (!c->ba) c->ba = ba_create();
+    if (!c->ba) return ORBHIP_ERR_DEVICE;
+    std::vector<const orbhip_ba_problem*> pp(B);
+    std::vector<orbhip_ba_result*> rr(B);
+    for (int b = 0; b < B; b++) { pp[b] = probs + b; rr[b] = res + b; }
+    return ba_solve_batch(c->ba, pp.data(), B, rr.data(), stop, c->stream);
+}
+
 // ---- test hooks (not part of the reference surface) ----
+int orbhip_test_cholesky(const double* A, const double* b, double* x, int n, unsigned long long* phases5,
+                         float* ms) {
+    if (!A || !b || !x || n <= 0 || n > 544) return ORBHIP_ERR_ARG;
+    return ba_test_cholesky(A, b, x, n, phases5, ms);
+}
 int orbhip_test_sincosf(const float* x, float* cs, float* sn, int64_t n) {
     if (!x || !cs || !sn || n <= 0) return ORBHIP_ERR_ARG;
     float *dx = nullptr, *dc = nullptr, *ds = nullptr;

@@ -89,6 +89,26 @@ class Optimizer:
         out.iterations_done, out.lm_trials = rc.iterations_done, rc.lm_trials
         return out
 
+    def solve_batch(self, probs, stop_flag: ctypes.c_int | None = None):
+        """B independent problems in one batched solve (replicas); returns a list of BAResult."""
+        ps = [p.normalized() for p in probs]
+        outs, cres = [], (BAResultC * len(ps))()
+        cprobs = (BAProblemC * len(ps))()
+        for i, p in enumerate(ps):
+            P, M, E = p.pose_q.shape[0], p.points.shape[0], p.edge_pose.shape[0]
+            o = BAResult(np.zeros((P, 4), np.float32), np.zeros((P, 3), np.float32), np.zeros((M, 3), np.float32),
+                         np.zeros(E, np.float32), np.zeros(E, np.uint8), 0.0, 0.0, 0, 0)
+            outs.append(o)
+            cres[i] = BAResultC(ptr(o.pose_q), ptr(o.pose_t), ptr(o.points), ptr(o.edge_chi2), ptr(o.edge_depth_ok),
+                                0.0, 0.0, 0, 0)
+            cprobs[i] = p.to_c()
+        sf = ctypes.addressof(stop_flag) if stop_flag is not None else None
+        check(lib().orbhip_ba_solve_batch(self.ctx.handle, cprobs, len(ps), cres, sf), "orbhip_ba_solve_batch")
+        for o, r in zip(outs, cres):
+            o.initial_chi2, o.final_chi2, o.iterations_done, o.lm_trials = (r.initial_chi2, r.final_chi2,
+                                                                              r.iterations_done, r.lm_trials)
+        return outs
+
     def LocalBundleAdjustment(self, prob: BAProblem, stop_flag=None) -> BAResult:
         return self.solve(prob, stop_flag)
 

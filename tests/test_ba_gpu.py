@@ -85,3 +85,15 @@ def test_stop_flag_aborts(opt):
     flag = ctypes.c_int(1)
     r = opt.LocalBundleAdjustment(prob, stop_flag=flag)
     assert r.iterations_done == 0
+
+
+def test_batch_matches_single(opt, oracle):
+    """orbhip_ba_solve_batch: 6 independent problems of different sizes; each equals its own
+    oracle solve (per-problem LM schedules, shared launches)."""
+    probs = [synthetic_ba_problem(n_kf=nkf, n_pts=npts, seed=s)[0]
+             for s, nkf, npts in [(21, 8, 150), (22, 30, 900), (23, 50, 2000), (24, 12, 300), (25, 40, 1500),
+                                  (26, 20, 500)]]
+    probs[3].pose_fixed[:2] = 1
+    res = opt.solve_batch(probs)
+    for p, g in zip(probs, res):
+        _compare(g, oracle.ba_solve(p), p)
