@@ -24,10 +24,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <limits>
+#include <thread>
 #include <vector>
 
 #include "orbhip_ba.h"
@@ -69,6 +73,7 @@ struct BaArgs {
     double* red;       // [0] chi2, [1] scale, [2] maxdiag
     int* flag;         // [0] cholesky ok
     const double* lambda;   // current lambda of this problem (device copy)
+    double* Lsave;     // ceil(n/32) x 1024: L11^{-1} of every Cholesky panel
 };
 
 #define BA_PROLOGUE                                 \
@@ -396,38 +401,100 @@ __global__ __launch_bounds__(256) void k_ba_schur_b(const BaArgs* __restrict__ a
 }
 
 // ---------------------------------------------------------------------------
-// dense Cholesky of S (n x n, lower, in place) + solve S xp = bs; one workgroup of 16 waves.
+// dense Cholesky of S (n x n, lower, in place) + solve S xp = bs; one workgroup (8 waves).
 // Right-looking, 32-column panels:
-//  (a) the 32x32 diagonal block is factored by wave 0 in REGISTERS: lane l owns column
-//      c = l & 31, rows r = 2s + (l >> 5) (s = 0..15); pivots and column values move by
-//      shuffles, no LDS round trip on the serial pivot chain. The panel's slice of the
-//      forward solve (L y = b) is done in the same pass.
-//  (b) panel rows below: L21 = A21 L11^-T, one row per thread, into LDS (stride 34 doubles:
-//      conflict-free for the MFMA operand reads) and back to S; y updated from the panel.
-//  (c) trailing update C -= P_I P_J^T on 16x16 lower tiles with v_mfma_f64_16x16x4f64
-//      (8 per tile, K = 32); the four C-tile loads of a round are issued together.
-//   f64 MFMA operand map: lane l holds A[l&15][k=l>>4], B[k=l>>4][l&15];
-//   C/D: col = l&15, row = (l>>4) + 4*reg.
-//  (d) backward solve L^T x = y panel by panel (column dot products + diagonal solve).
+//  (a) 32x32 diagonal block factored by ONE wavefront in registers (no block barrier per
+//      pivot): lane = column c (+ row parity), 16 rows per lane, the block kept as a full
+//      symmetric square so every cross-lane operand is one ds_bpermute. Gaussian elimination
+//      on [D | I | y] gives L_u (unit LDL^T factor), L_u^{-1} and the forward-solve slice;
+//      L11 = L_u diag(sqrt piv), L11^{-1} = diag(1/sqrt piv) L_u^{-1} at the panel end.
+//  (b) the panel L21 = A21 Linv^T and the
+//      trailing update C -= L21_I L21_J^T run on v_mfma_f64_16x16x4f64
+//      (operand map: lane l holds A[l&15][k=l>>4], B[k=l>>4][l&15]; C/D col = l&15,
+//      row = (l>>4) + 4*reg). Panel rows live in LDS (stride 34 doubles: conflict-free).
+//  (c) backward solve panel by panel: x_p = Linv^T (y_p - L21^T x_below) (Linv saved per panel).
 // ---------------------------------------------------------------------------
 constexpr int kNB = 32;
 constexpr int kPS = 34;   // panel row stride in doubles
 
-__device__ __forceinline__ size_t chol_lds_bytes(int n) {
+__host__ __device__ inline size_t chol_lds_doubles(int n) {
     const int np = (n + 31) & ~31;
-    return sizeof(double) * (size_t)(2 + 32 * 33 + np + np * kPS + 64);  // + invD, dval
+    return (size_t)(2 + 32 * 33 + np + (size_t)np * kPS + 4 * 32 + 32 * 33);
 }
 
-__device__ void chol_solve(double* __restrict__ S, const double* __restrict__ bs, double* __restrict__ x, int n,
-                           int* __restrict__ flag, unsigned long long* __restrict__ dbg) {
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, lane);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), lane);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// (a) of chol_solve: factor the 32x32 diagonal block at (k0, k0) with one wavefront.
+__device__ __forceinline__ void chol_diag_wave(double* __restrict__ S, int n, int k0, int kb, double* __restrict__ Li,
+                                            double* __restrict__ Lsave, int* bad) {
+    const int lane = threadIdx.x & 63;
+    const int c = lane & 31, h = lane >> 5;
+    double d[16], xi[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int r = 2 * k + h;
+        double v = (r == c) ? 1.0 : 0.0;
+        if (r < kb && c < kb)
+            v = r >= c ? S[(size_t)(k0 + r) * n + k0 + c] : S[(size_t)(k0 + c) * n + k0 + r];
+        d[k] = v;
+        xi[k] = (r == c) ? 1.0 : 0.0;
+    }
+    double myip = 1.0;
+    bool nonpd = false;
+#pragma unroll
+    for (int j = 0; j < 32; j++) {
+        const int jr = j >> 1, jh = 32 * (j & 1);
+        // all cross-lane operands of this step first (one LDS wait), then the FMAs
+        double colj[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            if (2 * k + 1 > j) colj[k] = __shfl(d[k], j + 32 * h, 64);   // D[r][j], r = 2k+h
+        const double rowj = __shfl(d[jr], c + jh, 64);                   // D[j][c]
+        const double xrow = __shfl(xi[jr], c + jh, 64);                  // X[j][c]
+        const double piv = readlane_f64(d[jr], j + jh);                  // uniform
+        nonpd |= !(piv > 0.0);
+        const double ip = 1.0 / (piv > 0.0 ? piv : 1.0);
+        if (c == j) myip = ip;
+        const double rs = c > j ? rowj * ip : 0.0;      // trailing columns: D[r][c] -= D[r][j] D[j][c] / piv
+        const double xs = c > j ? 0.0 : xrow * ip;      // eliminated columns: X[r][c] -= D[r][j] X[j][c] / piv
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            if (2 * k + 1 <= j) continue;                  // rows r <= j untouched
+            const double m = (2 * k == j && h == 0) ? 0.0 : colj[k];   // row r == j itself
+            d[k] = fma(-m, rs, d[k]);
+            xi[k] = fma(-m, xs, xi[k]);
+        }
+    }
+    const double dv = sqrt(1.0 / myip), idv = 1.0 / dv;
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int r = 2 * k + h;
+        const double idr = __shfl(idv, r, 64);
+        if (r < kb && c < kb && c <= r) S[(size_t)(k0 + r) * n + k0 + c] = r == c ? dv : d[k] * idv;
+        const double li = (r < kb && c < kb) ? xi[k] * idr : 0.0;
+        Li[r * 33 + c] = li;
+        if (Lsave) Lsave[(size_t)(k0 / 32) * 1024 + r * 32 + c] = li;
+    }
+    if (lane == 0 && nonpd) *bad = 1;
+}
+
+__device__ __forceinline__ void chol_solve(double* __restrict__ S, const double* __restrict__ bs, double* __restrict__ x, int n,
+                           int* __restrict__ flag, double* __restrict__ Lsave, unsigned long long* __restrict__ dbg) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int npad = (n + 31) & ~31;
     int& bad = *(int*)lds;                   // control word
-    double* D = lds + 2;                     // 32 x 33 diagonal block (L11, lower)
-    double* y = D + 32 * 33;                 // npad
+    double* Li = lds + 2;                    // 32 x 33 L11^{-1}
+    double* y = Li + 32 * 33;                // npad
     double* Pn = y + npad;                   // npad x kPS panel rows
-    double* invD = Pn + (size_t)npad * kPS;  // 32 reciprocal pivots of the current panel
-    double* dval = invD + 32;                // 32 pivots (sqrt) of the current panel
+    double* invp = Pn + (size_t)npad * kPS;  // 1/piv (raw pivot) per column of the panel
+    double* dval = invp + 32;                // sqrt(piv)
+    double* invd = dval + 32;                // 1/sqrt(piv)
+    double* red = invd + 32;                 // 32 x 33 scratch (back-solve partial sums)
     const int tid = threadIdx.x, nt = blockDim.x;
     const int wid = tid >> 6, lane = tid & 63, nw = nt >> 6;
     unsigned long long tprev = 0;
@@ -444,72 +511,65 @@ __device__ void chol_solve(double* __restrict__ S, const double* __restrict__ bs
     __syncthreads();
     for (int k0 = 0; k0 < n; k0 += kNB) {
         const int kb = min(kNB, n - k0);
-        // ---- (a) diagonal block in LDS, all threads: 2 barriers per pivot ----
-        for (int t = tid; t < 32 * 32; t += nt) {
-            const int r = t >> 5, cI = t & 31;
-            D[r * 33 + cI] = (r < kb && cI < kb && cI <= r) ? S[(size_t)(k0 + r) * n + k0 + cI] : (r == cI ? 1.0 : 0.0);
+        // ---- (a) diagonal block: wave 0, registers only ----
+        if (wid == 0) chol_diag_wave(S, n, k0, kb, Li, Lsave, &bad);
+        __syncthreads();
+        // forward-solve slice y_p = L11^{-1} y_p (elimination applied to y)
+        if (tid < 32) {
+            double s2 = 0.0;
+#pragma unroll 8
+            for (int k = 0; k < 32; k++) s2 += Li[tid * 33 + k] * (k < kb ? y[k0 + k] : 0.0);
+            invp[tid] = s2;
         }
         __syncthreads();
-        for (int j = 0; j < kb; j++) {
-            __syncthreads();   // previous step's trailing update is complete
-            const double piv = D[j * 33 + j];
-            const double d = sqrt(piv > 0.0 ? piv : 1.0);
-            const double inv = 1.0 / d;
-            if (tid < 32) {
-                if (tid == j) { invD[j] = inv; dval[j] = d; y[k0 + j] *= inv; if (!(piv > 0.0)) bad = 1; }
-                else if (tid > j) D[tid * 33 + j] *= inv;
-            }
-            __syncthreads();
-            for (int t = tid; t < 32 * 32; t += nt) {
-                const int r = t >> 5, cI = t & 31;
-                if (cI > j && r >= cI) D[r * 33 + cI] -= D[r * 33 + j] * D[cI * 33 + j];
-            }
-            if (tid > j && tid < kb) y[k0 + tid] -= D[tid * 33 + j] * y[k0 + j];
-        }
-        __syncthreads();
-        if (tid < kb) D[tid * 33 + tid] = dval[tid];
-        __syncthreads();
-        for (int t = tid; t < 32 * 32; t += nt) {
-            const int r = t >> 5, cI = t & 31;
-            if (r < kb && cI < kb && cI <= r) S[(size_t)(k0 + r) * n + k0 + cI] = D[r * 33 + cI];
-        }
+        if (tid < kb) y[k0 + tid] = invp[tid];
         stamp(0);
         if (bad) break;
-        // ---- (b) panel rows: L21 = A21 L11^-T; y_r -= L21[r] . y_panel ----
+        // ---- (b2) stage A21 rows into Pn ----
         const int r0 = k0 + kb;
         const int nr = n - r0;
         const int nr_pad = (nr + 15) & ~15;
-        for (int rr = tid; rr < nr_pad; rr += nt) {
-            double v[kNB];
-            const int r = r0 + rr;
-            const double* Ar = S + (size_t)r * n + k0;
+        for (int t = tid; t < nr_pad * 32; t += nt) {
+            const int rr = t >> 5, cI = t & 31;
+            Pn[rr * kPS + cI] = (rr < nr && cI < kb) ? S[(size_t)(r0 + rr) * n + k0 + cI] : 0.0;
+        }
+        __syncthreads();
+        // ---- (b3) L21 = A21 Linv^T on MFMA: one wave per 16-row block, both column halves ----
+        const int cc = lane & 15, rq = lane >> 4;
+        for (int R = wid; R < nr_pad / 16; R += nw) {
+            double4_t acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
 #pragma unroll
-            for (int cI = 0; cI < kNB; cI++) v[cI] = (rr < nr && cI < kb) ? Ar[cI] : 0.0;
-            double dot = 0.0;
-#pragma unroll
-            for (int cI = 0; cI < kNB; cI++) {
-                double s2 = v[cI];
-#pragma unroll
-                for (int p2 = 0; p2 < cI; p2++) s2 -= v[p2] * D[cI * 33 + p2];
-                v[cI] = (cI < kb) ? s2 * invD[cI] : 0.0;
-                dot += v[cI] * y[k0 + cI];
+            for (int kk = 0; kk < 8; kk++) {
+                const double av = Pn[(16 * R + cc) * kPS + 4 * kk + rq];
+                const double b0 = Li[cc * 33 + 4 * kk + rq];
+                const double b1 = Li[(16 + cc) * 33 + 4 * kk + rq];
+                acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b0, acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b1, acc1, 0, 0, 0);
             }
+            // all lanes' A reads of this row block are done before any write (wave-synchronous)
+            __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int cI = 0; cI < kNB; cI++) Pn[rr * kPS + cI] = v[cI];
-            if (rr < nr) {
-                double* Lr = S + (size_t)r * n + k0;
-#pragma unroll
-                for (int cI = 0; cI < kNB; cI++)
-                    if (cI < kb) Lr[cI] = v[cI];
-                y[r] -= dot;
+            for (int q = 0; q < 4; q++) {
+                const int rr = 16 * R + rq + 4 * q;
+                Pn[rr * kPS + cc] = acc0[q];
+                Pn[rr * kPS + 16 + cc] = acc1[q];
             }
         }
         __syncthreads();
+        // ---- (b4) L21 back to S (coalesced rows); y_r -= L21[r] . y_panel (half-wave per row) ----
+        for (int t = tid; t < nr * 32; t += nt) {
+            const int rr = t >> 5, cI = t & 31;
+            const double lv = Pn[rr * kPS + cI];
+            if (cI < kb) S[(size_t)(r0 + rr) * n + k0 + cI] = lv;
+            double dot = cI < kb ? lv * y[k0 + cI] : 0.0;
+#pragma unroll
+            for (int o = 16; o > 0; o >>= 1) dot += __shfl_xor(dot, o, 32);
+            if (cI == 0) y[r0 + rr] -= dot;
+        }
         stamp(1);
         // ---- (c) trailing update, lower 16x16 tiles, 4 tiles per wave per round ----
         const int T = nr_pad / 16;
         const int ntile = T * (T + 1) / 2;
-        const int cc = lane & 15, rq = lane >> 4;
         for (int base = wid; base < ntile; base += 4 * nw) {
             double4_t acc[4];
             int ti[4], tj[4];
@@ -556,39 +616,36 @@ __device__ void chol_solve(double* __restrict__ S, const double* __restrict__ bs
         for (int i = tid; i < n; i += nt) x[i] = 0.0;
         return;
     }
-    // ---- (d) backward: L^T x = y, panels from the last ----
+    // ---- (d) backward: x_p = Linv_p^T (y_p - L21_p^T x_below), panels from the last ----
     const int npan = (n + kNB - 1) / kNB;
+    const int G = nt >> 5;
     for (int pb = npan - 1; pb >= 0; pb--) {
         const int k0 = pb * kNB, kb = min(kNB, n - k0);
         const int r0 = k0 + kb;
-        // y_c -= sum_{r >= r0} L[r][k0+c] x_r : 32 columns x 32 row-groups, one thread each
-        const int G = nt >> 5;
         {
             const int cI = tid & 31, g = tid >> 5;   // g = 0..G-1
             double s2 = 0.0;
             if (cI < kb)
                 for (int r = r0 + g; r < n; r += G) s2 += S[(size_t)r * n + k0 + cI] * y[r];
-            Pn[g * 33 + cI] = s2;                    // reduced over g below
+            red[g * 33 + cI] = s2;
         }
-        for (int t = tid; t < 32 * 33; t += nt) {
-            const int r = t / 33, cI = t - 33 * (t / 33);
-            D[t] = (r < kb && cI < kb && cI <= r) ? S[(size_t)(k0 + r) * n + k0 + cI] : 0.0;
-        }
-        if (tid < kb) invD[tid] = 1.0 / S[(size_t)(k0 + tid) * n + k0 + tid];
+        for (int t = tid; t < 32 * 32; t += nt) Li[(t >> 5) * 33 + (t & 31)] = Lsave[(size_t)pb * 1024 + t];
         __syncthreads();
-        if (wid == 0) {
-            double v = 0.0;
-            if (lane < kb) {
+        if (tid < 32) {
+            double w = 0.0;
+            if (tid < kb) {
                 double s2 = 0.0;
-                for (int g = 0; g < G; g++) s2 += Pn[g * 33 + lane];
-                v = y[k0 + lane] - s2;
+                for (int g = 0; g < G; g++) s2 += red[g * 33 + tid];
+                w = y[k0 + tid] - s2;
             }
-            for (int j = kb - 1; j >= 0; j--) {
-                const double xj = __shfl(v, j, 64) * invD[j];
-                if (lane == j) v = xj;
-                if (lane < j) v -= D[j * 33 + lane] * xj;
-            }
-            if (lane < kb) y[k0 + lane] = v;
+            invp[tid] = w;                       // reuse as the 32-vector w
+        }
+        __syncthreads();
+        if (tid < kb) {
+            double s2 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 32; k++) s2 += Li[k * 33 + tid] * invp[k];
+            y[k0 + tid] = s2;
         }
         __syncthreads();
     }
@@ -597,19 +654,18 @@ __device__ void chol_solve(double* __restrict__ S, const double* __restrict__ bs
     if (tid == 0) flag[0] = 1;
 }
 
-
 __global__ __launch_bounds__(512) void k_ba_cholesky(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     const BaArgs& a = args[act[blockIdx.x]];
     if (a.n == 0) {
         if (threadIdx.x == 0) a.flag[0] = 1;
         return;
     }
-    chol_solve(a.S, a.bs, a.x, a.n, a.flag, nullptr);
+    chol_solve(a.S, a.bs, a.x, a.n, a.flag, a.Lsave, nullptr);
 }
 
 __global__ __launch_bounds__(512) void k_chol_test(double* S, const double* bs, double* x, int n, int* flag,
-                                                   unsigned long long* dbg) {
-    chol_solve(S, bs, x, n, flag, dbg);
+                                                   double* Lsave, unsigned long long* dbg) {
+    chol_solve(S, bs, x, n, flag, Lsave, dbg);
 }
 
 // ---------------------------------------------------------------------------
@@ -773,12 +829,11 @@ namespace {
 
 // per-problem host preparation (O(E)): index mapping, CSRs, Schur pair lists by counting sort
 struct Prep {
+    int rc = 0;
     int P = 0, M = 0, E = 0, np = 0, n = 0, nblk = 0;
-    std::vector<int> opt, e_pose, e_pt, pt_ptr, pt_edges, ps_ptr, ps_edges, blk_i, blk_j, blk_ptr, blk_pairs;
-    std::vector<double> pose, pts, obs, info;
-    // offsets into the packed device buffers (elements)
-    size_t o_pose, o_pts, o_opt, o_edge, o_e2, o_e18, o_np36, o_m9, o_m3, o_b, o_S, o_n, o_ptp, o_psp, o_blk, o_blkp,
-        o_pairs, o_ps_edges;
+    std::vector<int> opt, pt_ptr, pt_edges, ps_ptr, ps_edges, blk_i, blk_j, blk_ptr, blk_pairs;
+    // offsets (elements) into the packed buffers; see the segment map in ba_solve_batch
+    size_t o_chi2, o_state, o_obs, o_hw, o_scr, o_S, o_L, o_int;
 };
 
 inline void se3_from_float(const float* q, const float* t, double* out) {
@@ -805,24 +860,14 @@ int prepare(const orbhip_ba_problem* pr, Prep& o) {
         if (!pr->pose_fixed[i]) o.opt[i] = np++;
     o.np = np;
     o.n = 6 * np;
-    if (o.n > 544) return ORBHIP_ERR_UNSUPPORTED;   // single-workgroup Cholesky (LDS-resident panel)
-    o.pose.resize((size_t)8 * P);
-    for (int i = 0; i < P; i++) se3_from_float(pr->pose_q + 4 * i, pr->pose_t + 3 * i, &o.pose[8 * i]);
-    o.pts.assign(pr->points, pr->points + 3 * (size_t)M);
-    o.obs.resize((size_t)2 * E);
-    o.info.resize(E);
-    o.e_pose.assign(pr->edge_pose, pr->edge_pose + E);
-    o.e_pt.assign(pr->edge_point, pr->edge_point + E);
-    for (int e = 0; e < E; e++) {
-        o.obs[2 * e] = pr->edge_uv[2 * e];
-        o.obs[2 * e + 1] = pr->edge_uv[2 * e + 1];
-        o.info[e] = (double)pr->inv_sigma2[pr->edge_octave[e]];
-    }
+    if (o.n > 480) return ORBHIP_ERR_UNSUPPORTED;   // single-workgroup Cholesky (LDS-resident panel)
+    const int* e_pose = pr->edge_pose;
+    const int* e_pt = pr->edge_point;
     o.pt_ptr.assign(M + 1, 0);
     o.ps_ptr.assign(np + 1, 0);
     for (int e = 0; e < E; e++) {
-        o.pt_ptr[o.e_pt[e] + 1]++;
-        if (o.opt[o.e_pose[e]] >= 0) o.ps_ptr[o.opt[o.e_pose[e]] + 1]++;
+        o.pt_ptr[e_pt[e] + 1]++;
+        if (o.opt[e_pose[e]] >= 0) o.ps_ptr[o.opt[e_pose[e]] + 1]++;
     }
     for (int m = 0; m < M; m++) o.pt_ptr[m + 1] += o.pt_ptr[m];
     for (int i = 0; i < np; i++) o.ps_ptr[i + 1] += o.ps_ptr[i];
@@ -831,22 +876,21 @@ int prepare(const orbhip_ba_problem* pr, Prep& o) {
     {
         std::vector<int> fp(o.pt_ptr.begin(), o.pt_ptr.end() - 1), fq(o.ps_ptr.begin(), o.ps_ptr.end() - 1);
         for (int e = 0; e < E; e++) {
-            o.pt_edges[fp[o.e_pt[e]]++] = e;
-            const int oi = o.opt[o.e_pose[e]];
+            o.pt_edges[fp[e_pt[e]]++] = e;
+            const int oi = o.opt[e_pose[e]];
             if (oi >= 0) o.ps_edges[fq[oi]++] = e;
         }
     }
     // Schur pairs (a, b) of one landmark with opt(a) <= opt(b), grouped by block (i, j) with a
     // counting sort on the dense block id i*np + j; within a block: landmark order (deterministic).
     std::vector<int> cnt((size_t)np * np, 0);
-    for (int i = 0; i < np; i++) cnt[(size_t)i * np + i] = 0;
     size_t npairs = 0;
     for (int m = 0; m < M; m++)
         for (int ka = o.pt_ptr[m]; ka < o.pt_ptr[m + 1]; ka++) {
-            const int ia = o.opt[o.e_pose[o.pt_edges[ka]]];
+            const int ia = o.opt[e_pose[o.pt_edges[ka]]];
             if (ia < 0) continue;
             for (int kb = o.pt_ptr[m]; kb < o.pt_ptr[m + 1]; kb++) {
-                const int ib = o.opt[o.e_pose[o.pt_edges[kb]]];
+                const int ib = o.opt[e_pose[o.pt_edges[kb]]];
                 if (ib < 0 || ib < ia) continue;
                 cnt[(size_t)ia * np + ib]++;
                 npairs++;
@@ -869,10 +913,10 @@ int prepare(const orbhip_ba_problem* pr, Prep& o) {
     std::vector<int> fill(o.blk_ptr.begin(), o.blk_ptr.end() - 1);
     for (int m = 0; m < M; m++)
         for (int ka = o.pt_ptr[m]; ka < o.pt_ptr[m + 1]; ka++) {
-            const int ea = o.pt_edges[ka], ia = o.opt[o.e_pose[ea]];
+            const int ea = o.pt_edges[ka], ia = o.opt[e_pose[ea]];
             if (ia < 0) continue;
             for (int kb = o.pt_ptr[m]; kb < o.pt_ptr[m + 1]; kb++) {
-                const int eb = o.pt_edges[kb], ib = o.opt[o.e_pose[eb]];
+                const int eb = o.pt_edges[kb], ib = o.opt[e_pose[eb]];
                 if (ib < 0 || ib < ia) continue;
                 const int slot = fill[bid[(size_t)ia * np + ib]]++;
                 o.blk_pairs[2 * slot] = ea;
@@ -896,15 +940,61 @@ struct DBuf {
     }
 };
 
+template <typename T>
+struct HBuf {   // pinned host staging
+    T* p = nullptr;
+    size_t n = 0;
+    ~HBuf() { if (p) (void)hipHostFree(p); }
+    hipError_t ensure(size_t c) {
+        if (p && c <= n) return hipSuccess;
+        if (p) { (void)hipHostFree(p); p = nullptr; n = 0; }
+        c = std::max<size_t>(c + c / 4, 64);   // grow geometrically: pinning is expensive
+        hipError_t e = hipHostMalloc((void**)&p, c * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) n = c;
+        return e;
+    }
+};
+
+// fn(i) for i in [0, n) on up to `threads` host threads (problems are independent)
+template <typename F>
+void parallel_for(int n, int threads, F fn) {
+    threads = std::max(1, std::min(threads, n));
+    if (threads == 1) {
+        for (int i = 0; i < n; i++) fn(i);
+        return;
+    }
+    std::atomic<int> next{0};
+    auto work = [&] {
+        for (int i; (i = next.fetch_add(1)) < n;) fn(i);
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; t++) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+}
+
+int host_threads() {
+    static const int n = [] {
+        const char* s = std::getenv("ORBHIP_BA_THREADS");
+        if (s && std::atoi(s) > 0) return std::atoi(s);
+        const unsigned hw = std::thread::hardware_concurrency();
+        return (int)std::min<unsigned>(16, hw ? hw : 1);
+    }();
+    return n;
+}
+
 }  // namespace
 
 struct BaWorkspace {
-    DBuf<double> dbl;      // all fp64 per-problem arrays, packed
+    DBuf<double> dbl;      // all fp64 per-problem arrays, packed (segment map in ba_solve_batch)
     DBuf<int> ints;        // all int per-problem arrays, packed
     DBuf<BaArgs> args;
     DBuf<int> act;         // active problem lists (several slots)
     DBuf<double> lam;      // per-problem lambda
     DBuf<double> gath;     // gathered red/flag of the active problems
+    HBuf<double> hdbl;     // staging: [e_chi2 | pose,pts | obs,info] of every problem
+    HBuf<int> hint;
+    HBuf<BaArgs> hargs;
     double* h_gath = nullptr;  // pinned
     double* h_lam = nullptr;   // pinned
     double* h_red = nullptr;   // pinned: per problem red[4] + flag
@@ -932,42 +1022,53 @@ struct LmState {
 int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B, orbhip_ba_result* const* res,
                    const volatile int* stop, hipStream_t st) {
     if (B <= 0 || !probs || !res) return ORBHIP_ERR_ARG;
-    std::vector<Prep> pp(B);
-    for (int b = 0; b < B; b++) {
+    for (int b = 0; b < B; b++)
         if (!probs[b] || !res[b]) return ORBHIP_ERR_ARG;
-        const int rc = prepare(probs[b], pp[b]);
-        if (rc) return rc;
-    }
-    // ---- packed layout ----
-    size_t nd = 0, ni = 0;
+    static const bool timing = std::getenv("ORBHIP_BA_TIMING") != nullptr;
+    auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t_start = now();
+    const int nth = host_threads();
+    std::vector<Prep> pp(B);
+    parallel_for(B, nth, [&](int b) { pp[b].rc = prepare(probs[b], pp[b]); });
+    for (int b = 0; b < B; b++)
+        if (pp[b].rc) return pp[b].rc;
+    const double t_prep = now();
+    // ---- packed layout: fp64 segments, each contiguous over all problems ----
+    //   C  e_chi2 (E)                 downloaded with A in one transfer
+    //   A  pose (8P) + pts (3M)       uploaded, optimised in place, downloaded
+    //   U  obs (2E) + info (E)        uploaded
+    //   Z  Hpl + W (36E)              cleared with one memset (edges of fixed poses stay zero)
+    //   R  the rest (scratch), then S (n*n) and the panel inverses Lsave, 16-byte aligned
+    size_t nC = 0, nA = 0, nU = 0, nZ = 0, nR = 0, ni = 0;
     for (auto& p : pp) {
         const size_t P = p.P, M = p.M, E = p.E, np_ = p.np, n = p.n;
-        p.o_pose = nd; nd += 16 * P;              // pose + pose_bak
-        p.o_pts = nd; nd += 6 * M;                // pts + pts_bak
-        p.o_e2 = nd; nd += 2 * E * 2;             // e_obs, e_err
-        p.o_edge = nd; nd += 4 * E;               // e_info, e_chi2, e_rho0, e_rho1
-        p.o_e18 = nd; nd += 36 * E;               // Hpl, W
-        p.o_np36 = nd; nd += 36 * np_;            // Hpp
-        p.o_m9 = nd; nd += 18 * M;                // Hll, Dinv
-        p.o_m3 = nd; nd += 3 * M;                 // db
-        p.o_b = nd; nd += 2 * (n + 3 * M);        // b, x
-        p.o_n = nd; nd += n + 4;                  // bs, red[4]
-        nd = (nd + 1) & ~size_t(1);
-        p.o_S = nd; nd += n * n;                  // S (16-byte aligned)
-        nd = (nd + 1) & ~size_t(1);
-        p.o_opt = ni; ni += P + 4;                // opt, flag
-        p.o_ptp = ni; ni += 2 * E + (M + 1) + E;  // e_pose, e_pt, pt_ptr, pt_edges
-        p.o_psp = ni; ni += (np_ + 1);            // ps_ptr
-        p.o_ps_edges = ni; ni += p.ps_edges.size();
-        p.o_blk = ni; ni += 2 * p.nblk + (p.nblk + 1);
-        p.o_pairs = ni; ni += p.blk_pairs.size();
+        p.o_chi2 = nC; nC += E;
+        p.o_state = nA; nA += 8 * P + 3 * M;
+        p.o_obs = nU; nU += 3 * E;
+        p.o_hw = nZ; nZ += 36 * E;
+        p.o_scr = nR;
+        nR += 8 * P + 3 * M                          // pose_bak, pts_bak
+              + 2 * E + 3 * E                        // e_err, e_rho0, e_rho1 (+ pad)
+              + 36 * np_ + 18 * M + 3 * M            // Hpp, Hll, Dinv, db
+              + 2 * (n + 3 * M) + n + 4;             // b, x, bs, red
+        nR = (nR + 1) & ~size_t(1);
+        p.o_S = nR; nR += n * n;
+        nR = (nR + 1) & ~size_t(1);
+        p.o_L = nR; nR += 1024 * ((n + 31) / 32);
+        p.o_int = ni;
+        ni += (P + 4) + 2 * E + (M + 1) + E + (np_ + 1) + p.ps_edges.size() + 3 * p.nblk + 1 + p.blk_pairs.size();
     }
+    const size_t sC = 0, sA = nC, sU = sA + nA, sZ = (sU + nU + 1) & ~size_t(1), sR = sZ + nZ;
+    const size_t nd = sR + nR;
     BAOK(ws->dbl.ensure(nd));
     BAOK(ws->ints.ensure(ni));
     BAOK(ws->args.ensure(B));
     BAOK(ws->act.ensure(2 * (size_t)B));
     BAOK(ws->lam.ensure(B));
     BAOK(ws->gath.ensure(5 * (size_t)B));
+    BAOK(ws->hdbl.ensure(sU + nU));
+    BAOK(ws->hint.ensure(ni));
+    BAOK(ws->hargs.ensure(B));
     if (ws->h_cap < (size_t)B) {
         if (ws->h_lam) (void)hipHostFree(ws->h_lam);
         if (ws->h_red) (void)hipHostFree(ws->h_red);
@@ -980,56 +1081,71 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         BAOK(hipHostMalloc((void**)&ws->h_act, sizeof(int) * 2 * B, hipHostMallocDefault));
         ws->h_cap = B;
     }
-    std::vector<double> hd(nd, 0.0);
-    std::vector<int> hi(ni, 0);
-    std::vector<BaArgs> ha(B);
     double* D = ws->dbl.p;
     int* I = ws->ints.p;
-    for (int b = 0; b < B; b++) {
-        Prep& p = pp[b];
+    double* hd = ws->hdbl.p;
+    int* hi = ws->hint.p;
+    BaArgs* ha = ws->hargs.p;
+    parallel_for(B, nth, [&](int b) {
+        const Prep& p = pp[b];
         const orbhip_ba_problem* pr = probs[b];
-        std::copy(p.pose.begin(), p.pose.end(), hd.begin() + p.o_pose);
-        std::copy(p.pts.begin(), p.pts.end(), hd.begin() + p.o_pts);
-        std::copy(p.obs.begin(), p.obs.end(), hd.begin() + p.o_e2);
-        std::copy(p.info.begin(), p.info.end(), hd.begin() + p.o_edge);
-        std::copy(p.opt.begin(), p.opt.end(), hi.begin() + p.o_opt);
-        size_t q = p.o_ptp;
-        std::copy(p.e_pose.begin(), p.e_pose.end(), hi.begin() + q); q += p.E;
-        std::copy(p.e_pt.begin(), p.e_pt.end(), hi.begin() + q); q += p.E;
-        std::copy(p.pt_ptr.begin(), p.pt_ptr.end(), hi.begin() + q); q += p.M + 1;
-        std::copy(p.pt_edges.begin(), p.pt_edges.end(), hi.begin() + q);
-        std::copy(p.ps_ptr.begin(), p.ps_ptr.end(), hi.begin() + p.o_psp);
-        std::copy(p.ps_edges.begin(), p.ps_edges.end(), hi.begin() + p.o_ps_edges);
-        q = p.o_blk;
-        std::copy(p.blk_i.begin(), p.blk_i.end(), hi.begin() + q); q += p.nblk;
-        std::copy(p.blk_j.begin(), p.blk_j.end(), hi.begin() + q); q += p.nblk;
-        std::copy(p.blk_ptr.begin(), p.blk_ptr.end(), hi.begin() + q);
-        std::copy(p.blk_pairs.begin(), p.blk_pairs.end(), hi.begin() + p.o_pairs);
+        const size_t P = p.P, M = p.M, E = p.E;
+        double* st_ = hd + sA + p.o_state;
+        for (size_t i = 0; i < P; i++) se3_from_float(pr->pose_q + 4 * i, pr->pose_t + 3 * i, st_ + 8 * i);
+        for (size_t k = 0; k < 3 * M; k++) st_[8 * P + k] = pr->points[k];
+        double* ob = hd + sU + p.o_obs;
+        for (size_t e = 0; e < E; e++) {
+            ob[2 * e] = pr->edge_uv[2 * e];
+            ob[2 * e + 1] = pr->edge_uv[2 * e + 1];
+            ob[2 * E + e] = (double)pr->inv_sigma2[pr->edge_octave[e]];
+        }
+        int* q = hi + p.o_int;
+        auto put = [&](const int* src, size_t cnt) { int* at = q; std::memcpy(q, src, cnt * sizeof(int)); q += cnt; return at; };
         BaArgs& a = ha[b];
+        int* d0 = I + p.o_int;
+        auto dev = [&](const int* host_at) { return d0 + (host_at - (hi + p.o_int)); };
+        a.opt = dev(put(p.opt.data(), P));
+        a.flag = dev(q); q += 4;
+        a.e_pose = dev(put(pr->edge_pose, E));
+        a.e_pt = dev(put(pr->edge_point, E));
+        a.pt_ptr = dev(put(p.pt_ptr.data(), M + 1));
+        a.pt_edges = dev(put(p.pt_edges.data(), E));
+        a.ps_ptr = dev(put(p.ps_ptr.data(), p.np + 1));
+        a.ps_edges = dev(put(p.ps_edges.data(), p.ps_edges.size()));
+        a.blk_i = dev(put(p.blk_i.data(), p.nblk));
+        a.blk_j = dev(put(p.blk_j.data(), p.nblk));
+        a.blk_ptr = dev(put(p.blk_ptr.data(), p.nblk + 1));
+        a.blk_pairs = dev(put(p.blk_pairs.data(), p.blk_pairs.size()));
+        a.nblk = p.nblk;
         a.P = p.P; a.M = p.M; a.E = p.E; a.np = p.np; a.n = p.n;
         a.fx = pr->fx; a.fy = pr->fy; a.cx = pr->cx; a.cy = pr->cy; a.delta = pr->huber_delta;
-        a.pose = D + p.o_pose; a.pose_bak = a.pose + 8 * (size_t)p.P;
-        a.pts = D + p.o_pts; a.pts_bak = a.pts + 3 * (size_t)p.M;
-        a.e_obs = D + p.o_e2; a.e_err = D + p.o_e2 + 2 * (size_t)p.E;
-        a.e_info = D + p.o_edge; a.e_chi2 = D + p.o_edge + p.E; a.e_rho0 = a.e_chi2 + p.E; a.e_rho1 = a.e_rho0 + p.E;
-        a.Hpl = D + p.o_e18; a.W = a.Hpl + 18 * (size_t)p.E;
-        a.Hpp = D + p.o_np36;
-        a.Hll = D + p.o_m9; a.Dinv = a.Hll + 9 * (size_t)p.M;
-        a.db = D + p.o_m3;
-        a.b = D + p.o_b; a.x = a.b + p.n + 3 * (size_t)p.M;
-        a.bs = D + p.o_n; a.red = a.bs + p.n;
-        a.S = D + p.o_S;
-        a.opt = I + p.o_opt; a.flag = I + p.o_opt + p.P;
-        a.e_pose = I + p.o_ptp; a.e_pt = a.e_pose + p.E; a.pt_ptr = a.e_pt + p.E; a.pt_edges = a.pt_ptr + p.M + 1;
-        a.ps_ptr = I + p.o_psp; a.ps_edges = I + p.o_ps_edges;
-        a.blk_i = I + p.o_blk; a.blk_j = a.blk_i + p.nblk; a.blk_ptr = a.blk_j + p.nblk;
-        a.blk_pairs = I + p.o_pairs;
-        a.nblk = p.nblk;
+        a.e_chi2 = D + sC + p.o_chi2;
+        a.pose = D + sA + p.o_state; a.pts = a.pose + 8 * P;
+        a.e_obs = D + sU + p.o_obs; a.e_info = a.e_obs + 2 * E;
+        a.Hpl = D + sZ + p.o_hw; a.W = a.Hpl + 18 * E;
+        double* r = D + sR + p.o_scr;
+        a.pose_bak = r; r += 8 * P;
+        a.pts_bak = r; r += 3 * M;
+        a.e_err = r; r += 2 * E;
+        a.e_rho0 = r; r += E;
+        a.e_rho1 = r; r += 2 * E;
+        a.Hpp = r; r += 36 * (size_t)p.np;
+        a.Hll = r; r += 9 * M;
+        a.Dinv = r; r += 9 * M;
+        a.db = r; r += 3 * M;
+        a.b = r; r += p.n + 3 * M;
+        a.x = r; r += p.n + 3 * M;
+        a.bs = r; r += p.n;
+        a.red = r;
+        a.S = D + sR + p.o_S;
+        a.Lsave = D + sR + p.o_L;
         a.lambda = ws->lam.p + b;
-    }
-    BAOK(hipMemcpyAsync(ws->dbl.p, hd.data(), nd * sizeof(double), hipMemcpyHostToDevice, st));
-    BAOK(hipMemcpyAsync(ws->ints.p, hi.data(), ni * sizeof(int), hipMemcpyHostToDevice, st));
-    BAOK(hipMemcpyAsync(ws->args.p, ha.data(), B * sizeof(BaArgs), hipMemcpyHostToDevice, st));
+    });
+    BAOK(hipMemcpyAsync(D + sA, hd + sA, sizeof(double) * (nA + nU), hipMemcpyHostToDevice, st));
+    if (nZ) BAOK(hipMemsetAsync(D + sZ, 0, sizeof(double) * nZ, st));
+    BAOK(hipMemcpyAsync(I, hi, ni * sizeof(int), hipMemcpyHostToDevice, st));
+    BAOK(hipMemcpyAsync(ws->args.p, ha, B * sizeof(BaArgs), hipMemcpyHostToDevice, st));
+    const double t_pack = now();
     static bool lds_set = false;
     if (!lds_set) {
         BAOK(hipFuncSetAttribute((const void*)k_ba_cholesky, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -1040,8 +1156,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         maxM = std::max(maxM, p.M); maxE = std::max(maxE, p.E); maxP = std::max(maxP, p.P);
         maxNp = std::max(maxNp, p.np); maxBlk = std::max(maxBlk, p.nblk); maxN = std::max(maxN, p.n);
     }
-    const size_t chol_lds = sizeof(double) * (size_t)(2 + 32 * 33 + ((maxN + 31) & ~31) +
-                                                      (size_t)((maxN + 31) & ~31) * kPS + 64);
+    const size_t chol_lds = sizeof(double) * chol_lds_doubles(maxN);
     auto gx = [](int n_, int b_) { return (unsigned)std::max(1, (n_ + b_ - 1) / b_); };
     (void)hipGetLastError();
     int* d_act = ws->act.p;
@@ -1123,7 +1238,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             std::vector<int> pop, next;
             for (int b : trial) {
                 LmState& s = L[b];
-                const bool ok2 = *(int*)(ws->h_red + 5 * b + 4) != 0;
+                const bool ok2 = ws->h_red[5 * b + 4] != 0.0;   // gathered as a double
                 double tempChi = ok2 ? ws->h_red[5 * b] : dmax;
                 double rho = s.currentChi - tempChi;
                 rho /= (ws->h_red[5 * b + 1] + 1e-3);
@@ -1166,18 +1281,20 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             if (probs[b]->early_stop && s.nBad >= 3) s.done = true;
         }
     }
-    // ---- outputs ----
-    for (int b = 0; b < B; b++) {
+    const double t_solve = now();
+    // ---- outputs: e_chi2 of every problem + optimised poses/points, one transfer ----
+    BAOK(hipMemcpyAsync(hd, D, sizeof(double) * (nC + nA), hipMemcpyDeviceToHost, st));
+    BAOK(hipStreamSynchronize(st));
+    parallel_for(B, nth, [&](int b) {
         const Prep& p = pp[b];
+        const orbhip_ba_problem* pr = probs[b];
         orbhip_ba_result* r = res[b];
         r->final_chi2 = L[b].currentChi;
         r->iterations_done = L[b].it;
         r->lm_trials = L[b].trials;
-        std::vector<double> pose_o((size_t)8 * p.P), pts_o((size_t)3 * p.M), chi2_o(p.E);
-        if (p.P) BAOK(hipMemcpyAsync(pose_o.data(), ha[b].pose, sizeof(double) * 8 * p.P, hipMemcpyDeviceToHost, st));
-        if (p.M) BAOK(hipMemcpyAsync(pts_o.data(), ha[b].pts, sizeof(double) * 3 * p.M, hipMemcpyDeviceToHost, st));
-        if (p.E) BAOK(hipMemcpyAsync(chi2_o.data(), ha[b].e_chi2, sizeof(double) * p.E, hipMemcpyDeviceToHost, st));
-        BAOK(hipStreamSynchronize(st));
+        const double* pose_o = hd + sA + p.o_state;
+        const double* pts_o = pose_o + 8 * (size_t)p.P;
+        const double* chi2_o = hd + sC + p.o_chi2;
         for (int i = 0; i < p.P; i++) {
             if (r->pose_q) for (int k = 0; k < 4; k++) r->pose_q[4 * i + k] = (float)pose_o[8 * i + k];
             if (r->pose_t) for (int k = 0; k < 3; k++) r->pose_t[3 * i + k] = (float)pose_o[8 * i + 4 + k];
@@ -1186,8 +1303,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         for (int e = 0; e < p.E; e++) {
             if (r->edge_chi2) r->edge_chi2[e] = (float)chi2_o[e];
             if (r->edge_depth_ok) {   // isDepthPositive: (T.map(X)).z > 0
-                const double* T = &pose_o[8 * p.e_pose[e]];
-                const double* X = &pts_o[3 * p.e_pt[e]];
+                const double* T = &pose_o[8 * pr->edge_pose[e]];
+                const double* X = &pts_o[3 * pr->edge_point[e]];
                 double ux = T[1] * X[2] - T[2] * X[1], uy = T[2] * X[0] - T[0] * X[2];
                 ux += ux; uy += uy;
                 const double uz2 = 2 * (T[0] * X[1] - T[1] * X[0]);
@@ -1196,7 +1313,10 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 r->edge_depth_ok[e] = z > 0.0 ? 1 : 0;
             }
         }
-    }
+    });
+    if (timing)
+        std::fprintf(stderr, "orbhip ba timing B=%d: prep %.3f ms, pack+upload %.3f ms, solve %.3f ms, outputs %.3f ms\n",
+                     B, t_prep - t_start, t_pack - t_prep, t_solve - t_pack, now() - t_solve);
     return ORBHIP_OK;
 }
 
@@ -1221,17 +1341,20 @@ int ba_test_cholesky(const double* A, const double* b, double* x, int n, unsigne
     BAOK(hipMemcpy(db_, b, sizeof(double) * n, hipMemcpyHostToDevice));
     BAOK(hipMemset(dd, 0, 64));
     BAOK(hipFuncSetAttribute((const void*)k_chol_test, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    const size_t lds = sizeof(double) * (size_t)(2 + 32 * 33 + ((n + 31) & ~31) + (size_t)((n + 31) & ~31) * kPS + 64);
+    const size_t lds = sizeof(double) * chol_lds_doubles(n);
+    double* dL = nullptr;
+    BAOK(hipMalloc((void**)&dL, sizeof(double) * 1024 * ((n + 31) / 32)));
     hipEvent_t e0, e1;
     BAOK(hipEventCreate(&e0)); BAOK(hipEventCreate(&e1));
     BAOK(hipEventRecord(e0, nullptr));
-    hipLaunchKernelGGL(k_chol_test, dim3(1), dim3(512), lds, nullptr, dS, db_, dx, n, df, dd);
+    hipLaunchKernelGGL(k_chol_test, dim3(1), dim3(512), lds, nullptr, dS, db_, dx, n, df, dL, dd);
     BAOK(hipEventRecord(e1, nullptr));
     BAOK(hipDeviceSynchronize());
     BAOK(hipEventElapsedTime(ms, e0, e1));
     BAOK(hipMemcpy(x, dx, sizeof(double) * n, hipMemcpyDeviceToHost));
     BAOK(hipMemcpy(phases5, dd, sizeof(unsigned long long) * 5, hipMemcpyDeviceToHost));
     (void)hipFree(dS); (void)hipFree(db_); (void)hipFree(dx); (void)hipFree(df); (void)hipFree(dd);
+    (void)hipFree(dL);
     (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
     return ORBHIP_OK;
 }

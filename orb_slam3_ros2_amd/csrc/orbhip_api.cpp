@@ -601,7 +601,7 @@ int orbhip_ba_solve_batch(orbhip_ctx* c, const orbhip_ba_problem* probs, int B, 
 // ---- test hooks (not part of the reference surface) ----
 int orbhip_test_cholesky(const double* A, const double* b, double* x, int n, unsigned long long* phases5,
                          float* ms) {
-    if (!A || !b || !x || n <= 0 || n > 544) return ORBHIP_ERR_ARG;
+    if (!A || !b || !x || n <= 0 || n > 480) return ORBHIP_ERR_ARG;
     return ba_test_cholesky(A, b, x, n, phases5, ms);
 }
 int orbhip_test_sincosf(const float* x, float* cs, float* sn, int64_t n) {

@@ -11,7 +11,7 @@ from orb_slam3_ros2_amd._lib import lib  # noqa: E402
 
 L = lib()
 L.orbhip_test_cholesky.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
-for n in [int(a) for a in (sys.argv[1:] or ["294", "294", "31", "100", "540"])]:
+for n in [int(a) for a in (sys.argv[1:] or ["294", "294", "31", "100", "480"])]:
     rng = np.random.default_rng(n)
     M = rng.normal(size=(n, n))
     A = M @ M.T + n * np.eye(n)
