@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 STAGES = {1: "k_resize (7 levels)", 2: "k_fast_cells", 3: "k_octree", 4: "k_desc", 5: "k_match_top2",
           6: "k_rot_filter"}
+KERNEL_SYMBOL = {1: "k_resize", 2: "k_fast_cells", 3: "k_octree", 4: "k_desc", 5: "k_match_top2", 6: "k_rot_filter"}
 
 
 def parse():
@@ -45,6 +46,7 @@ def parse():
     ap.add_argument("--no-extra", action="store_true", help="skip the C3 / LBA extra lines")
     ap.add_argument("--c3-steps", type=int, default=10)
     ap.add_argument("--lba-steps", type=int, default=20)
+    ap.add_argument("--lba-batch", type=int, default=128)
     return ap.parse_args()
 
 
@@ -157,12 +159,32 @@ class StreamC2:
         self.s += 1
 
     def stage_bytes(self):
-        """Algorithmic HBM bytes per launch of each stage for one 640x480 frame."""
-        info = self.ext.level_info(self.W, self.H)
-        A = (info["w"].astype(np.int64) * info["h"]).tolist()
-        n_kp = float(self.n.float().mean().item()) or 1000.0
-        return {1: sum(A[:-1]) + sum(A[1:]), 2: sum(A), 3: 8.0 * 4500 + 8 * n_kp, 4: n_kp * (43 * 43 + 56),
-                5: 2 * n_kp * 32 + n_kp * 12, 6: n_kp * 12}
+        return stage_bytes(self.ext, self.W, self.H, float(self.n.float().mean().item()) or 1000.0, 1)
+
+
+def stage_bytes(ext, w, h, n_kp, frames):
+    """Algorithmic HBM bytes per launch of each stage: resize reads level l-1 and
+    writes level l (all 7 launches summed), FAST reads every level once, octree reads its packed
+    candidates (8 B) and writes kept keypoints (8 B), desc reads a 43x43 patch + writes kp/desc
+    (56 B), match reads query+train descriptors and writes 3 ints per query, rot filter 12 B/kp."""
+    info = ext.level_info(w, h)
+    A = (info["w"].astype(np.int64) * info["h"]).tolist()
+    per = {1: sum(A[:-1]) + sum(A[1:]), 2: sum(A), 3: 8.0 * 4500 + 8 * n_kp, 4: n_kp * (43 * 43 + 56),
+           5: 2 * n_kp * 32 + n_kp * 12, 6: n_kp * 12}
+    return {k: v * frames for k, v in per.items()}
+
+
+def load_traffic(kernel_name):
+    """HBM bytes per launch of `kernel_name` from the committed PMC summary (separate rocprofv3
+    --pmc FETCH_SIZE / WRITE_SIZE passes of this bench, FETCH_SIZE doubled per the gfx950
+    correction in MI355X_MICROARCH.md); None when no summary is committed."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d["kernels"][kernel_name]["hbm_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 class BatchC3:
@@ -311,7 +333,8 @@ def main():
                    "frames_per_step": 1, "parallelism": f"replicas x{ws} (frame streams, no collective)",
                    "keypoints_per_frame": round(nkp, 1), "matches_last_pair": nmatch},
         "roofline": {"kernel": STAGES[dom], "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                     "traffic": load_traffic(KERNEL_SYMBOL[dom]),
                      "algorithmic_bytes_per_launch": int(dom_bytes), "avg_launch_ms": round(dom_avg_ms, 5),
                      "launches_timed": dom_n,
                      "stage_avg_ms_calibration": {STAGES[k]: round(v, 5) for k, v in stage_ms.items()}},
@@ -321,6 +344,23 @@ def main():
         c3 = BatchC3(rank)
         t = timed(1, c3.step, args.c3_steps, 2)
         extra["c3_1280x720_b64_extract_match_frames_per_s"] = round(c3.B * args.c3_steps / t, 1)
+        # C3 roofline: the batch regime is where the extractor can approach the HBM roof
+        p3 = Profiler(c3.ext.ctx)
+        c3_ms = {}
+        for st in (1, 2, 3, 4, 5, 6):
+            p3.select(st)
+            for _ in range(3):
+                c3.step()
+            ms, n = p3.collect()
+            c3_ms[st] = ms / max(n, 1)
+        p3.select(0)
+        d3 = max(c3_ms, key=c3_ms.get)
+        b3 = stage_bytes(c3.ext, c3.W, c3.H, float(c3.n.float().mean().item()) or 1000.0, c3.B)
+        a3 = b3[d3] / (c3_ms[d3] * 1e-3) / 1e9
+        extra["c3_roofline"] = {"kernel": STAGES[d3], "bound": "hbm", "achieved": round(a3, 2),
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(a3 / HBM_PEAK_GBS, 5),
+                                "algorithmic_bytes_per_launch": int(b3[d3]), "avg_launch_ms": round(c3_ms[d3], 4),
+                                "stage_avg_ms": {STAGES[k]: round(v, 4) for k, v in c3_ms.items()}}
         from orb_slam3_ros2_amd import Optimizer
         from orb_slam3_ros2_amd.synthetic import synthetic_ba_problem
         prob, _ = synthetic_ba_problem()
@@ -336,6 +376,15 @@ def main():
         extra["c4_lba_ms"] = round(1e3 * tl / args.lba_steps, 3)
         extra["c4_lba_trials"] = r.lm_trials
         extra["c4_lba_chi2"] = [round(r.initial_chi2, 3), round(r.final_chi2, 3)]
+        # replicas: independent LBA problems (concurrent maps / agents) in one batched solve
+        probs = [synthetic_ba_problem(seed=100 + i)[0] for i in range(args.lba_batch)]
+        opt.solve_batch(probs[:2])
+        t0 = time.perf_counter()
+        rs = opt.solve_batch(probs)
+        tb = time.perf_counter() - t0
+        extra["c4_lba_batched_kf_per_s"] = round(len(probs) / tb, 1)
+        extra["c4_lba_batch"] = len(probs)
+        extra["c4_lba_batched_trials_mean"] = round(float(np.mean([x.lm_trials for x in rs])), 2)
         out["extra"] = extra
     if rank == 0 and ws == 1 and not args.no_cpu:
         cb = cpu_baseline(c2.frames_np)
