@@ -1,0 +1,193 @@
+// orbhip.hpp — C++ host mirror of the reference interfaces over the C-ABI of orbhip.h.
+//
+// Same names, argument meaning and error behaviour as the ORB_SLAM3 classes this path replaces
+// (upstream ORB_SLAM3 v1.0, the gjcliff fork's submodule; cited U:file::Symbol because the
+// submodule is empty in the reference tree):
+//   U:include/ORBextractor.h  class ORBextractor   -> orbhip::ORBextractor
+//   U:include/ORBmatcher.h    ORBmatcher::DescriptorDistance, TH_LOW / TH_HIGH / HISTO_LENGTH
+//   U:include/Optimizer.h     Optimizer::LocalBundleAdjustment / BundleAdjustment (problem form)
+// The reference types (cv::Mat, cv::KeyPoint, KeyFrame, MapPoint) stay on the adapter side
+// (INTEGRATION.md). Here images are (pointer, w, h, stride) and keypoints are orbhip::KeyPoint
+// with cv::KeyPoint's fields. Header-only: link liborbhip.so.
+#ifndef ORBHIP_HPP
+#define ORBHIP_HPP
+
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "orbhip.h"
+
+namespace orbhip {
+
+class Error : public std::runtime_error {
+public:
+    Error(int code, const std::string& what) : std::runtime_error(what + ": status " + std::to_string(code)), code_(code) {}
+    int code() const { return code_; }
+
+private:
+    int code_;
+};
+
+inline void check(int rc, const char* what) {
+    if (rc < 0) throw Error(rc, what);
+}
+
+// cv::KeyPoint's fields as ORBextractor fills them (class_id is always -1 there).
+struct KeyPoint {
+    float x, y, size, angle, response;
+    int octave;
+    int class_id = -1;
+};
+
+// U:include/ORBextractor.h::ORBextractor
+class ORBextractor {
+public:
+    ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST, int device = 0)
+        : nfeatures_(nfeatures), scaleFactor_(scaleFactor), nlevels_(nlevels) {
+        orbhip_orb_params p{nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST};
+        check(orbhip_create(&ctx_, device, &p), "orbhip_create");
+        // the ctor's tables (U:src/ORBextractor.cc): mvScaleFactor from the library (float,
+        // accumulated through the double scaleFactor), sigma2 = s*s, inverses in float
+        mvScaleFactor_.resize(nlevels);
+        check(orbhip_level_info(ctx_, 640, 480, nullptr, nullptr, nullptr, mvScaleFactor_.data()), "orbhip_level_info");
+        for (int l = 0; l < nlevels; l++) {
+            mvLevelSigma2_.push_back(mvScaleFactor_[l] * mvScaleFactor_[l]);
+            mvInvScaleFactor_.push_back(1.0f / mvScaleFactor_[l]);
+            mvInvLevelSigma2_.push_back(1.0f / mvLevelSigma2_[l]);
+        }
+    }
+    ~ORBextractor() { if (ctx_) orbhip_destroy(ctx_); }
+    ORBextractor(const ORBextractor&) = delete;
+    ORBextractor& operator=(const ORBextractor&) = delete;
+
+    // operator()(InputArray image, InputArray mask, vector<KeyPoint>&, OutputArray descriptors,
+    //            vector<int>& vLappingArea) -> monoIndex; -1 on an empty image. The mask is
+    //            ignored by the reference as well. descriptors: N rows of 32 bytes.
+    int operator()(const uint8_t* image, int w, int h, int stride, std::vector<KeyPoint>& keypoints,
+                   std::vector<uint8_t>& descriptors, const std::vector<int>& vLappingArea) {
+        keypoints.clear();
+        descriptors.clear();
+        if (!image || w <= 0 || h <= 0) return -1;
+        const int cap = orbhip_max_keypoints(ctx_, w, h);
+        check(cap, "orbhip_max_keypoints");
+        kp_.resize(cap);
+        descriptors.resize((size_t)cap * 32);
+        int n = 0, mono = 0;
+        const int lap0 = vLappingArea.size() > 0 ? vLappingArea[0] : 0;
+        const int lap1 = vLappingArea.size() > 1 ? vLappingArea[1] : 1000;
+        const int rc = orbhip_extract(ctx_, image, w, h, stride, lap0, lap1, kp_.data(), descriptors.data(), cap, &n, &mono);
+        if (rc == ORBHIP_ERR_EMPTY) return -1;
+        check(rc, "orbhip_extract");
+        keypoints.resize(n);
+        for (int i = 0; i < n; i++)
+            keypoints[i] = KeyPoint{kp_[i].x, kp_[i].y, kp_[i].size, kp_[i].angle, kp_[i].response, kp_[i].octave};
+        descriptors.resize((size_t)n * 32);
+        return mono;
+    }
+
+    int inline GetLevels() const { return nlevels_; }
+    float inline GetScaleFactor() const { return scaleFactor_; }
+    std::vector<float> inline GetScaleFactors() const { return mvScaleFactor_; }
+    std::vector<float> inline GetInverseScaleFactors() const { return mvInvScaleFactor_; }
+    std::vector<float> inline GetScaleSigmaSquares() const { return mvLevelSigma2_; }
+    std::vector<float> inline GetInverseScaleSigmaSquares() const { return mvInvLevelSigma2_; }
+    orbhip_ctx* context() const { return ctx_; }
+
+private:
+    orbhip_ctx* ctx_ = nullptr;
+    int nfeatures_;
+    float scaleFactor_;
+    int nlevels_;
+    std::vector<float> mvScaleFactor_, mvInvScaleFactor_, mvLevelSigma2_, mvInvLevelSigma2_;
+    std::vector<orbhip_kp> kp_;
+};
+
+// U:include/ORBmatcher.h — the constants and the brute-force acceptance rule (a11/a12).
+class ORBmatcher {
+public:
+    static const int TH_LOW = 50;
+    static const int TH_HIGH = 100;
+    static const int HISTO_LENGTH = 30;
+
+    ORBmatcher(float nnratio = 0.6f, bool checkOri = true) : mfNNratio(nnratio), mbCheckOrientation(checkOri) {}
+
+    static int DescriptorDistance(const uint8_t* a, const uint8_t* b) { return orbhip_descriptor_distance(a, b); }
+
+    // best/second over the whole train set; match[i] = train index or -1. Returns #matches.
+    int MatchBruteForce(orbhip_ctx* ctx, const std::vector<uint8_t>& q, const std::vector<float>& qAngle,
+                        const std::vector<uint8_t>& t, const std::vector<float>& tAngle, std::vector<int>& match,
+                        int thLow = TH_LOW) const {
+        const int nq = (int)(q.size() / 32), nt = (int)(t.size() / 32);
+        match.assign(nq, -1);
+        std::vector<int32_t> best(nq), second(nq);
+        const int rc = orbhip_match_bf(ctx, q.data(), qAngle.data(), nq, t.data(), tAngle.data(), nt, thLow, mfNNratio,
+                                       mbCheckOrientation ? 1 : 0, match.data(), best.data(), second.data());
+        check(rc, "orbhip_match_bf");
+        return rc;
+    }
+
+    float mfNNratio;
+    bool mbCheckOrientation;
+};
+
+// U:include/Optimizer.h — the g2o problem of LocalBundleAdjustment in SoA form. The adapter
+// fills it from the local KeyFrames / MapPoints and applies the result.
+struct BAProblem {
+    std::vector<float> pose_q, pose_t, points, edge_uv, inv_sigma2;
+    std::vector<uint8_t> pose_fixed;
+    std::vector<int32_t> edge_pose, edge_point, edge_octave;
+    float fx = 0, fy = 0, cx = 0, cy = 0;
+    float huber_delta = std::sqrt(5.991f);
+    int iterations = 10;
+    int early_stop = 0;
+};
+
+struct BAResult {
+    std::vector<float> pose_q, pose_t, points, edge_chi2;
+    std::vector<uint8_t> edge_depth_ok;
+    double initial_chi2 = 0, final_chi2 = 0;
+    int iterations_done = 0, lm_trials = 0;
+};
+
+class Optimizer {
+public:
+    // LocalBundleAdjustment's optimize(10) with Huber sqrt(5.991). The reference's bool*
+    // pbStopFlag (LocalMapping::mbAbortBA -> g2o setForceStopFlag) is an int here, polled by
+    // the solver between LM iterations and trials; NULL = never stop.
+    static BAResult LocalBundleAdjustment(orbhip_ctx* ctx, const BAProblem& p, const volatile int* pbStopFlag = nullptr) {
+        return solve(ctx, p, pbStopFlag);
+    }
+    // BundleAdjustment(vpKF, vpMP, nIterations, pbStopFlag, nLoopKF, bRobust): robust -> sqrt(5.99)
+    static BAResult BundleAdjustment(orbhip_ctx* ctx, BAProblem p, int nIterations = 5,
+                                     const volatile int* pbStopFlag = nullptr, bool bRobust = true) {
+        p.iterations = nIterations;
+        p.huber_delta = bRobust ? std::sqrt(5.99f) : 0.0f;
+        return solve(ctx, p, pbStopFlag);
+    }
+
+private:
+    static BAResult solve(orbhip_ctx* ctx, const BAProblem& p, const volatile int* stop) {
+        const int P = (int)p.pose_fixed.size(), M = (int)(p.points.size() / 3), E = (int)p.edge_pose.size();
+        orbhip_ba_problem c{P, M, E, p.pose_q.data(), p.pose_t.data(), p.pose_fixed.data(), p.points.data(),
+                            p.edge_pose.data(), p.edge_point.data(), p.edge_uv.data(), p.edge_octave.data(),
+                            p.inv_sigma2.data(), (int)p.inv_sigma2.size(), p.fx, p.fy, p.cx, p.cy, p.huber_delta,
+                            p.iterations, p.early_stop};
+        BAResult r;
+        r.pose_q.resize(4 * (size_t)P); r.pose_t.resize(3 * (size_t)P); r.points.resize(3 * (size_t)M);
+        r.edge_chi2.resize(E); r.edge_depth_ok.resize(E);
+        orbhip_ba_result o{r.pose_q.data(), r.pose_t.data(), r.points.data(), r.edge_chi2.data(), r.edge_depth_ok.data(),
+                           0, 0, 0, 0};
+        check(orbhip_ba_solve(ctx, &c, &o, stop), "orbhip_ba_solve");
+        r.initial_chi2 = o.initial_chi2; r.final_chi2 = o.final_chi2;
+        r.iterations_done = o.iterations_done; r.lm_trials = o.lm_trials;
+        return r;
+    }
+};
+
+}  // namespace orbhip
+
+#endif  // ORBHIP_HPP
