@@ -33,8 +33,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 STAGES = {1: "k_resize (7 levels)", 2: "k_fast_cells", 3: "k_octree", 4: "k_desc", 5: "k_match_top2",
-          6: "k_rot_filter"}
-KERNEL_SYMBOL = {1: "k_resize", 2: "k_fast_cells", 3: "k_octree", 4: "k_desc", 5: "k_match_top2", 6: "k_rot_filter"}
+          6: "k_match_finish"}
+KERNEL_SYMBOL = {1: "k_resize", 2: "k_fast_cells", 3: "k_octree", 4: "k_desc", 5: "k_match_top2", 6: "k_match_finish"}
 
 
 def parse():

@@ -90,6 +90,16 @@ int orbhip_extract_batch_device(orbhip_ctx* ctx, const uint8_t* d_imgs, int B, i
                                 int64_t frame_stride, int lap0, int lap1, orbhip_kp* d_kps, uint8_t* d_desc,
                                 int cap, int32_t* d_n, int32_t* d_mono, void* stream);
 
+/* ---- ingest (a23) -------------------------------------------------------------------
+ * cv_bridge::toCvShare(bgr8 msg, MONO8) -> cvtColor(COLOR_BGR2GRAY) (R:src/imu_mono_realsense.cpp:298)
+ * on the device, bit-exact: Y = (B*1868 + G*9617 + R*4899 + 2^13) >> 14. B frames of w x h
+ * BGR (3 bytes/px, rows `src_stride` bytes apart, frames `src_fstride` apart) -> u8 gray
+ * (rows `dst_stride`, frames `dst_fstride`), ready for orbhip_extract_batch_device.
+ * Asynchronous on `stream` (NULL = the context's stream). */
+int orbhip_bgr_to_gray_device(orbhip_ctx* ctx, const uint8_t* d_bgr, int B, int w, int h, int src_stride,
+                              int64_t src_fstride, uint8_t* d_gray, int dst_stride, int64_t dst_fstride,
+                              void* stream);
+
 /* ---- Hamming matching ------------------------------------------------------------- */
 /* ORBmatcher::DescriptorDistance (host helper, popcount of xor over 32 bytes). */
 int orbhip_descriptor_distance(const uint8_t* a, const uint8_t* b);

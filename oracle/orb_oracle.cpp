@@ -873,6 +873,18 @@ int orc_fast_window(const uint8_t* img, int step, int rows, int cols, int thresh
 
 int orc_descriptor_distance(const uint8_t* a, const uint8_t* b) { return orc::descriptor_distance(a, b); }
 
+// OCV imgproc/src/color_rgb.simd.hpp RGB2Gray<uchar> as reached by cv_bridge::toCvShare(msg,
+// MONO8) on a bgr8 message (R:src/imu_mono_realsense.cpp:298): yuv_shift = 14, coefficients
+// R2Y 4899, G2Y 9617, B2Y 1868; Y = (B*1868 + G*9617 + R*4899 + (1 << 13)) >> 14. The SIMD
+// path uses the same integer dot product, so every pixel has one exact value.
+void orc_bgr2gray(const uint8_t* bgr, int w, int h, int src_stride, uint8_t* gray, int dst_stride) {
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            const uint8_t* p = bgr + (size_t)y * src_stride + 3 * x;
+            gray[(size_t)y * dst_stride + x] = (uint8_t)((p[0] * 1868 + p[1] * 9617 + p[2] * 4899 + (1 << 13)) >> 14);
+        }
+}
+
 int orc_match_bf(const uint8_t* q, const float* q_angle, int nq, const uint8_t* t, const float* t_angle, int nt,
                  int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best_d, int32_t* second_d) {
     return orc::match_bf(q, q_angle, nq, t, t_angle, nt, th_low, ratio, check_orientation, match, best_d, second_d);

@@ -50,6 +50,7 @@ def lib():
         L.orc_ba_solve.argtypes = [c_int, c_int, c_int, _f32p, _f32p, _u8p, _f32p, _i32p, _i32p, _f32p, _i32p,
                                    _f32p, c_float, c_float, c_float, c_float, c_float, c_int, c_int, _f32p, _f32p,
                                    _f32p, _f32p, _u8p, _f64p]
+        L.orc_bgr2gray.argtypes = [_u8p, c_int, c_int, c_int, _u8p, c_int]
         L.orc_glibc_sincosf_range.argtypes = [ctypes.c_uint32, ctypes.c_uint32, _f32p, _f32p]
         _lib = L
     return _lib
@@ -133,6 +134,14 @@ def match_bf(q, qa, t, ta, th_low=50, ratio=0.9, check_orientation=True):
     m = np.zeros(nq, np.int32); b = np.zeros(nq, np.int32); s = np.zeros(nq, np.int32)
     n = lib().orc_match_bf(q, qa, nq, t, ta, nt, th_low, ratio, int(check_orientation), m, b, s)
     return n, m, b, s
+
+
+def bgr2gray(bgr: np.ndarray) -> np.ndarray:
+    bgr = np.ascontiguousarray(bgr, np.uint8)
+    h, w, _ = bgr.shape
+    out = np.empty((h, w), np.uint8)
+    lib().orc_bgr2gray(bgr, w, h, 3 * w, out, w)
+    return out
 
 
 def glibc_sincosf_range(lo_bits: int, hi_bits: int):

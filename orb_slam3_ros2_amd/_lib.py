@@ -59,7 +59,7 @@ class BAResultC(ctypes.Structure):
 EXPORTED = ["orbhip_abi_version", "orbhip_create", "orbhip_destroy", "orbhip_level_info", "orbhip_max_keypoints",
             "orbhip_extract", "orbhip_extract_batch_device", "orbhip_descriptor_distance", "orbhip_match_bf",
             "orbhip_match_pairs_device", "orbhip_match_frames_device", "orbhip_profile_stage",
-            "orbhip_profile_collect", "orbhip_ba_solve", "orbhip_ba_solve_batch"]
+            "orbhip_profile_collect", "orbhip_ba_solve", "orbhip_ba_solve_batch", "orbhip_bgr_to_gray_device"]
 
 
 def lib():
@@ -92,6 +92,7 @@ def lib():
     L.orbhip_match_bf.argtypes = [vp, vp, vp, i32, vp, vp, i32, i32, f32, i32, vp, vp, vp]
     L.orbhip_match_pairs_device.argtypes = [vp, vp, vp, vp, i32, i32, i32, f32, i32, vp, vp, vp, vp, vp]
     L.orbhip_match_frames_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, i32, vp, vp, vp, vp, vp]
+    L.orbhip_bgr_to_gray_device.argtypes = [vp, vp, i32, i32, i32, i32, ctypes.c_int64, vp, i32, ctypes.c_int64, vp]
     L.orbhip_profile_stage.argtypes = [vp, i32]
     L.orbhip_profile_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)]
     L.orbhip_ba_solve.argtypes = [vp, ctypes.POINTER(BAProblemC), ctypes.POINTER(BAResultC), vp]
@@ -101,6 +102,15 @@ def lib():
     L.orbhip_test_sincosf_sweep.restype = ctypes.c_int64
     _lib = L
     return L
+
+
+def torch_stream(stream=None):
+    """hipStream_t for a device call on torch tensors: the given torch stream, else torch's
+    CURRENT stream — so the call is ordered after the torch work that produced its inputs and
+    before torch reads its outputs (the context's own stream would race with both)."""
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
 
 
 def check(rc: int, what: str) -> int:

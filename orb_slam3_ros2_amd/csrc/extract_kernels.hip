@@ -23,6 +23,8 @@ namespace orbhip {
 
 static __constant__ signed char kPattern[256 * 4] = ORBHIP_BIT_PATTERN_31_INIT;
 
+ORBHIP_TRACE_UNIT(extract)
+
 // ---------------------------------------------------------------------------
 // image addressing: level 0 is the caller's frame, levels >= 1 live in the pyramid block
 // ---------------------------------------------------------------------------
@@ -42,6 +44,7 @@ __device__ __forceinline__ ImgRef level_img(const ExtractPlan* __restrict__ P, c
 __global__ __launch_bounds__(256) void k_resize(const ExtractPlan* __restrict__ P, FrameBufs fb, int l,
                                                 const int* __restrict__ xofs, const int* __restrict__ xalpha,
                                                 const int* __restrict__ yofs, const int* __restrict__ ybeta) {
+    TR_BEGIN()
     const LevelGeom& D = P->lv[l];
     const LevelGeom& S = P->lv[l - 1];
     const int f = blockIdx.z;
@@ -91,6 +94,7 @@ __global__ __launch_bounds__(256) void k_resize(const ExtractPlan* __restrict__ 
     } else {
         for (int k = 0; k < 4 && dx0 + k < D.w; k++) dst[dx0 + k] = (uint8_t)(packed >> (8 * k));
     }
+    if (l == 1) { TR_END(0) }
 }
 
 // ---------------------------------------------------------------------------
@@ -101,13 +105,8 @@ __global__ __launch_bounds__(256) void k_resize(const ExtractPlan* __restrict__ 
 // ---------------------------------------------------------------------------
 constexpr int kWinMax = 80;
 
-__device__ __forceinline__ int fast_strength(const uint8_t* c, int w) {
-    const int o[16] = {3 * w,      3 * w + 1,  2 * w + 2,  w + 3,      3,      -w + 3, -2 * w + 2, -3 * w + 1,
-                       -3 * w,     -3 * w - 1, -2 * w - 2, -w - 3,     -3,     w - 3,  2 * w - 2,  3 * w - 1};
-    const int v = c[0];
-    int d[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) d[k] = v - (int)c[o[k]];
+// m = max(A, B, 0) from the 16 differences d[k] = v - circle[k]
+__device__ __forceinline__ int fast_strength_d(const int* d) {
     int mn2[16], mx2[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) {
@@ -126,17 +125,36 @@ __device__ __forceinline__ int fast_strength(const uint8_t* c, int w) {
     return m < 0 ? 0 : m;
 }
 
+// quotient of i / d for 0 <= i < 2^16, 1 <= d <= 128: float reciprocal with margin >= 0.5/d
+__device__ __forceinline__ int small_div(int i, float inv_d) { return (int)(((float)i + 0.5f) * inv_d); }
+
+// Is the pixel a FAST corner candidate at threshold t? Necessary condition of a 9-arc: every
+// opposite pair (k, k+8) has at least one member beyond v +- t on the arc's side.
+__device__ __forceinline__ bool fast_pair_test(const int* d, int t) {
+    bool bright = true, dark = true;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        bright &= (d[k] < -t) | (d[k + 8] < -t);
+        dark &= (d[k] > t) | (d[k + 8] > t);
+    }
+    return bright | dark;
+}
+
 __global__ __launch_bounds__(256) void k_fast_cells(const ExtractPlan* __restrict__ P,
                                                     const CellGeom* __restrict__ cells, FrameBufs fb,
-                                                    uint32_t* __restrict__ cand, int* __restrict__ cand_cnt) {
+                                                    uint32_t* __restrict__ cand, int* __restrict__ cand_cnt,
+                                                    int* __restrict__ err) {
     __shared__ uint8_t win[kWinMax * kWinMax];
     __shared__ uint8_t mv[kWinMax * kWinMax];
-    __shared__ int scr[8];
+    __shared__ uint64_t masks[4][2][24];   // per wave, per threshold, per 64-px chunk
+    __shared__ int wcnt[2][4];
+    TR_BEGIN()
     const CellGeom cg = cells[blockIdx.x];
     const int f = blockIdx.y;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wc = cg.wc, hc = cg.hc;
     int* cnt_out = cand_cnt + (int64_t)f * P->n_cells_total + blockIdx.x;
+    if (blockIdx.x == 0 && f == 0 && tid < 4) err[tid] = 0;   // the octree (next launch) reports here
     if (wc <= 6 || hc <= 6) {
         if (tid == 0) *cnt_out = 0;
         return;
@@ -144,59 +162,108 @@ __global__ __launch_bounds__(256) void k_fast_cells(const ExtractPlan* __restric
     const LevelGeom& G = P->lv[cg.level];
     ImgRef im = level_img(P, fb, f, cg.level);
     const uint8_t* base = im.p + (int64_t)cg.y0 * im.pitch + cg.x0;
-    for (int i = tid; i < wc * hc; i += 256) {
-        const int yy = i / wc, xx = i - yy * wc;
-        win[i] = base[(int64_t)yy * im.pitch + xx];
-    }
-    __syncthreads();
-    const int dc = wc - 6, dr = hc - 6, np = dc * dr;
-    for (int p = tid; p < np; p += 256) {
-        const int py = p / dc, px = p - py * dc;
-        mv[p] = (uint8_t)fast_strength(&win[(py + 3) * wc + px + 3], wc);
-    }
-    __syncthreads();
-    auto keep = [&](int p, int t) -> bool {
-        const int m = mv[p];
-        if (m <= t) return false;
-        const int s = m - 1;
-        const int py = p / dc, px = p - py * dc;
+    // ---- window -> LDS: all loads of a thread issued back to back ----
+    {
+        const int tot = wc * hc;
+        const float inv_wc = 1.0f / (float)wc;
+        uint8_t v[kWinMax * kWinMax / 256 + 1];
 #pragma unroll
-        for (int yy = -1; yy <= 1; yy++)
-#pragma unroll
-            for (int xx = -1; xx <= 1; xx++) {
-                if (yy == 0 && xx == 0) continue;
-                const int qx = px + xx, qy = py + yy;
-                if (qx < 0 || qy < 0 || qx >= dc || qy >= dr) continue;
-                const int mq = mv[qy * dc + qx];
-                const int sq = mq > t ? mq - 1 : 0;
-                if (!(s > sq)) return false;
+        for (int u = 0; u < kWinMax * kWinMax / 256 + 1; u++) {
+            const int i = tid + 256 * u;
+            if (i < tot) {
+                const int yy = small_div(i, inv_wc), xx = i - yy * wc;
+                v[u] = base[(int64_t)yy * im.pitch + xx];
             }
-        return true;
-    };
-    int t = P->ini_th;
-    int c = 0;
-    for (int p = tid; p < np; p += 256) c += keep(p, t) ? 1 : 0;
-    c = wave_sum_i32(c);
-    if (lane_id() == 0) scr[tid >> 6] = c;
-    __syncthreads();
-    const int total_ini = scr[0] + scr[1] + scr[2] + scr[3];
-    __syncthreads();
-    if (total_ini == 0) t = P->min_th;
-    uint32_t* out = cand + (int64_t)f * P->n_slots_total + cg.slot_off;
-    int written = 0;
-    for (int r0 = 0; r0 < np; r0 += 256) {
-        const int p = r0 + tid;
-        const int k = (p < np && keep(p, t)) ? 1 : 0;
-        int tot;
-        const int pos = block_excl_scan(k, scr, &tot);
-        if (k) {
-            const int py = p / dc, px = p - py * dc;
-            const int x = cg.x0 + 3 + px - G.min_bx, y = cg.y0 + 3 + py - G.min_by;
-            out[written + pos] = pack_cand(x, y, (int)mv[p] - 1);
         }
-        written += tot;
+#pragma unroll
+        for (int u = 0; u < kWinMax * kWinMax / 256 + 1; u++) {
+            const int i = tid + 256 * u;
+            if (i < tot) win[i] = v[u];
+        }
     }
-    if (tid == 0) *cnt_out = written;
+    __syncthreads();
+    TR_PHASE(1, 0)
+    const int t_ini = P->ini_th, t_min = P->min_th;
+    const int t_lo = min(t_ini, t_min);
+    const int dc = wc - 6, dr = hc - 6, np = dc * dr;
+    const float inv_dc = 1.0f / (float)dc;
+    // ---- strength map: m if m > t_lo (a corner at some threshold in use), else 0 ----
+    for (int p = tid; p < np; p += 256) {
+        const int py = small_div(p, inv_dc), px = p - py * dc;
+        const uint8_t* c = &win[(py + 3) * wc + px + 3];
+        const int o[16] = {3 * wc,      3 * wc + 1,  2 * wc + 2,  wc + 3,      3,      -wc + 3, -2 * wc + 2, -3 * wc + 1,
+                           -3 * wc,     -3 * wc - 1, -2 * wc - 2, -wc - 3,     -3,     wc - 3,  2 * wc - 2,  3 * wc - 1};
+        const int vv = c[0];
+        int d[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) d[k] = vv - (int)c[o[k]];
+        int m = 0;
+        if (fast_pair_test(d, t_lo)) {
+            m = fast_strength_d(d);
+            if (m <= t_lo) m = 0;
+        }
+        mv[p] = (uint8_t)m;
+    }
+    __syncthreads();
+    TR_PHASE(1, 1)
+    // ---- window-local strict 3x3 NMS at both thresholds; wave w owns pixels [w*chunk, ...) ----
+    const int chunk = ((np + 255) / 256) * 64;   // multiple of 64 per wave
+    const int p0 = wid * chunk, p1 = min(np, p0 + chunk);
+    int c_ini = 0, c_min = 0;
+    for (int q0 = p0, ci = 0; q0 < p1; q0 += 64, ci++) {
+        const int p = q0 + lane;
+        bool k_ini = false, k_min = false;
+        if (p < p1) {
+            const int m = mv[p];
+            if (m > 0) {
+                const int py = small_div(p, inv_dc), px = p - py * dc;
+                int nb[8];
+                int j = 0;
+#pragma unroll
+                for (int yy = -1; yy <= 1; yy++)
+#pragma unroll
+                    for (int xx = -1; xx <= 1; xx++) {
+                        if (yy == 0 && xx == 0) continue;
+                        const int qx = px + xx, qy = py + yy;
+                        nb[j++] = (qx < 0 || qy < 0 || qx >= dc || qy >= dr) ? 0 : mv[qy * dc + qx];
+                    }
+                k_ini = m > t_ini;
+                k_min = m > t_min;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const int mq = nb[k];
+                    k_ini &= (m - 1) > (mq > t_ini ? mq - 1 : 0);
+                    k_min &= (m - 1) > (mq > t_min ? mq - 1 : 0);
+                }
+            }
+        }
+        const uint64_t bi = __ballot(k_ini), bm = __ballot(k_min);
+        if (lane == 0) { masks[wid][0][ci] = bi; masks[wid][1][ci] = bm; }
+        c_ini += __popcll(bi);
+        c_min += __popcll(bm);
+    }
+    if (lane == 0) { wcnt[0][wid] = c_ini; wcnt[1][wid] = c_min; }
+    __syncthreads();
+    TR_PHASE(1, 2)
+    const int total_ini = wcnt[0][0] + wcnt[0][1] + wcnt[0][2] + wcnt[0][3];
+    const int sel = total_ini > 0 ? 0 : 1;   // per-cell fallback iniThFAST -> minThFAST
+    int off = 0;
+    for (int w = 0; w < wid; w++) off += wcnt[sel][w];
+    uint32_t* out = cand + (int64_t)f * P->n_slots_total + cg.slot_off;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int q0 = p0, ci = 0; q0 < p1; q0 += 64, ci++) {
+        const uint64_t mk = masks[wid][sel][ci];
+        const int p = q0 + lane;
+        if ((mk >> lane) & 1ull) {
+            const int py = small_div(p, inv_dc), px = p - py * dc;
+            const int x = cg.x0 + 3 + px - G.min_bx, y = cg.y0 + 3 + py - G.min_by;
+            out[off + __popcll(mk & lt)] = pack_cand(x, y, (int)mv[p] - 1);
+        }
+        off += __popcll(mk);
+    }
+    if (tid == 0) *cnt_out = wcnt[sel][0] + wcnt[sel][1] + wcnt[sel][2] + wcnt[sel][3];
+    TR_PHASE(1, 3)
+    TR_END(1)
 }
 
 // ---------------------------------------------------------------------------
@@ -212,7 +279,9 @@ struct OctLds {
     uint16_t* map4;    // node_cap*4 remap old node/quadrant -> new node
     int* tA; int* tB; int* tC; int* tD;
     uint64_t* skey;    // sort keys (sort_cap)
+    uint64_t* skey2;   // rank-sorted keys (sort_cap)
     int* cellstart;    // max_cells_level + 1
+    int* cslot;        // max_cells_level + 1: candidate slot offset of each cell
     uint32_t* keys;    // key_cap (LDS) or null
     uint16_t* knode;
 };
@@ -262,22 +331,43 @@ __device__ int block_scan_array(int* arr, int n, int* ctl) {
     __syncthreads();
     return tot;
 }
-
-// bitonic sort of skey[0..n) descending, n power of two
-__device__ void block_sort_desc(uint64_t* a, int n) {
-    for (int k = 2; k <= n; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < n; i += blockDim.x) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const uint64_t x = a[i], y = a[ixj];
-                    const bool desc = (i & k) == 0;
-                    if (desc ? (x < y) : (x > y)) { a[i] = y; a[ixj] = x; }
-                }
-            }
-            __syncthreads();
-        }
+// Three exclusive scans in one pass (2 barriers): arrays a0..a2 of length n each; scratch =
+// ctl[0..47] (16 waves x 3). Returns the totals.
+__device__ void block_scan_array3(int* a0, int* a1, int* a2, int n, int* ctl, int* tot) {
+    const int nt = blockDim.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
+    const int per = (n + nt - 1) / nt;
+    const int b = tid * per, e = min(b + per, n);
+    int* arr[3] = {a0, a1, a2};
+    int s[3] = {0, 0, 0}, inc[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        for (int i = b; i < e; i++) s[k] += arr[k][i];
+        inc[k] = wave_incl_scan(s[k]);
+        if (lane == 63) ctl[16 * k + wid] = inc[k];
     }
+    __syncthreads();
+    int off[3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const int ws = wave_incl_scan(lane < nw ? ctl[16 * k + lane] : 0);
+        const int before = __shfl(ws, wid > 0 ? wid - 1 : 0, 64);
+        tot[k] = __shfl(ws, nw - 1, 64);
+        off[k] = (wid > 0 ? before : 0) + inc[k] - s[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++)
+        for (int i = b; i < e; i++) { const int v = arr[k][i]; arr[k][i] = off[k]; off[k] += v; }
+    __syncthreads();
+}
+// Descending sort of n unique keys by rank (no barriers inside): out[#greater] = key.
+__device__ void block_rank_sort_desc(const uint64_t* __restrict__ a, uint64_t* __restrict__ out, int n) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint64_t x = a[i];
+        int r = 0;
+        for (int j = 0; j < n; j++) r += a[j] > x ? 1 : 0;
+        out[r] = x;
+    }
+    __syncthreads();
 }
 
 __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__ P, const CellGeom* __restrict__ cells,
@@ -286,6 +376,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                                                  LevelKp* __restrict__ lvl_kp, int* __restrict__ lvl_cnt,
                                                  int* __restrict__ lvl_nlap, OctreeCfg cfg, int* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    TR_BEGIN()
     const int l = blockIdx.x, f = blockIdx.y;
     const LevelGeom& G = P->lv[l];
     const int tid = threadIdx.x, nt = blockDim.x;
@@ -304,7 +395,9 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
     S.tA = (int*)carve(NC * 4); S.tB = (int*)carve(NC * 4); S.tC = (int*)carve(NC * 4);
     S.tD = (int*)carve(NC * 4);
     S.skey = (uint64_t*)carve(cfg.sort_cap * 8);
+    S.skey2 = (uint64_t*)carve(cfg.sort_cap * 8);
     S.cellstart = (int*)carve((P->max_cells_level + 1) * 4);
+    S.cslot = (int*)carve((P->max_cells_level + 1) * 4);
     uint32_t* keysL = (uint32_t*)carve(cfg.key_cap * 4);
     uint16_t* knodeL = (uint16_t*)carve(cfg.key_cap * 2);
     int* ctl = S.ctl;
@@ -312,20 +405,27 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
     // ---- 1. candidate count per cell -> cell-major key order ----
     const int ncell = G.n_cells;
     const int* cc = cand_cnt + (int64_t)f * P->n_cells_total + G.cell_base;
-    for (int i = tid; i < ncell; i += nt) S.cellstart[i] = cc[i];
+    for (int i = tid; i < ncell; i += nt) {
+        S.cellstart[i] = cc[i];
+        S.cslot[i] = cells[G.cell_base + i].slot_off;
+    }
     __syncthreads();
     const int M = block_scan_array(S.cellstart, ncell, ctl);
+    if (tid == 0) S.cellstart[ncell] = M;
     const bool keys_in_lds = M <= cfg.key_cap;
     uint32_t* keys = keys_in_lds ? keysL : kscratch + (int64_t)f * P->n_slots_total + G.slot_base;
     uint16_t* knode = keys_in_lds ? knodeL : nscratch + (int64_t)f * P->n_slots_total + G.slot_base;
     const uint32_t* cbase = cand + (int64_t)f * P->n_slots_total;
-    {
-        const int wid = tid >> 6, lane = tid & 63, nw = nt >> 6;
-        for (int c = wid; c < ncell; c += nw) {
-            const int n = cc[c], st = S.cellstart[c];
-            const uint32_t* src = cbase + cells[G.cell_base + c].slot_off;
-            for (int i = lane; i < n; i += 64) keys[st + i] = src[i];
+    __syncthreads();
+    // flattened gather: key k belongs to the cell c with cellstart[c] <= k < cellstart[c+1]
+    // (binary search in LDS), so every global load of the level is independent
+    for (int k = tid; k < M; k += nt) {
+        int lo = 0, hi = ncell - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (S.cellstart[mid] <= k) lo = mid; else hi = mid - 1;
         }
+        keys[k] = cbase[S.cslot[lo] + (k - S.cellstart[lo])];
     }
     // ---- 2. roots (nIni <= 64 enforced by the host) ----
     const int nIni = G.n_ini;
@@ -353,19 +453,20 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                 n++;
             }
         }
-        ctl[40] = n;          // list size
-        ctl[41] = nIni;       // next serial
-        ctl[42] = 0;          // mode: 0 main, 1 final
-        ctl[43] = 0;          // finished
+        ctl[56] = n;          // list size
+        ctl[57] = nIni;       // next serial
+        ctl[58] = 0;          // mode: 0 main, 1 final
+        ctl[59] = 0;          // finished
     }
     __syncthreads();
+    TR_PHASE(2, 0)
     // CUR = A, OLD = B
     uint64_t *rectC = S.rectA, *rectO = S.rectB;
     uint32_t *cntC = S.cntA, *bestC = S.bestA, *serC = S.serA;
     uint32_t *cntO = S.cntB, *bestO = S.bestB, *serO = S.serB;
     const int N = G.n_feat;
     for (int iter = 0;; iter++) {
-        const int n = ctl[40];
+        const int n = ctl[56];
         if (iter > 64 || n > NC) {   // runaway guard: never expected
             if (tid == 0) atomicOr(err, 1);
             break;
@@ -386,8 +487,8 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
             }
         }
         __syncthreads();
-        const int mode = ctl[42];
-        const int serial0 = ctl[41];
+        const int mode = ctl[58];
+        const int serial0 = ctl[57];
         int newSize;
         if (mode == 0) {
             // ---- MAIN pass: divide every node with > 1 key ----
@@ -399,9 +500,9 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                 S.tA[p] = c; S.tB[p] = div ? 0 : 1; S.tC[p] = e;
             }
             __syncthreads();
-            const int T = block_scan_array(S.tA, n, ctl);
-            const int U = block_scan_array(S.tB, n, ctl);
-            const int nToExpand = block_scan_array(S.tC, n, ctl);
+            int tot3[3];
+            block_scan_array3(S.tA, S.tB, S.tC, n, ctl, tot3);
+            const int T = tot3[0], U = tot3[1], nToExpand = tot3[2];
             newSize = T + U;
             for (int p = tid; p < n; p += nt) {
                 if (cntC[p] > 1) {
@@ -426,25 +527,21 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                 }
             }
             if (tid == 0) {
-                ctl[41] = serial0 + T;
-                if (newSize >= N || newSize == n) ctl[43] = 1;
-                else if (newSize + nToExpand * 3 > N) ctl[42] = 1;
+                ctl[57] = serial0 + T;
+                if (newSize >= N || newSize == n) ctl[59] = 1;
+                else if (newSize + nToExpand * 3 > N) ctl[58] = 1;
             }
         } else {
             // ---- FINAL phase: divide largest (size, serial) first until >= N ----
             for (int p = tid; p < n; p += nt) S.tA[p] = cntC[p] > 1 ? 1 : 0;
             __syncthreads();
             const int K = block_scan_array(S.tA, n, ctl);
-            int sc = 1;
-            while (sc < K) sc <<= 1;
-            for (int i = tid; i < sc; i += nt) S.skey[i] = 0;
-            __syncthreads();
             for (int p = tid; p < n; p += nt)
                 if (cntC[p] > 1)
-                    S.skey[S.tA[p]] = ((uint64_t)cntC[p] << 40) | ((uint64_t)serC[p] << 16) | (uint64_t)p;
+                    S.skey2[S.tA[p]] = ((uint64_t)cntC[p] << 40) | ((uint64_t)serC[p] << 16) | (uint64_t)p;
             __syncthreads();
-            block_sort_desc(S.skey, sc);
-            if (tid == 0) ctl[44] = K - 1;   // jstar: last divided index in sorted order
+            block_rank_sort_desc(S.skey2, S.skey, K);   // keys unique: (size, serial) order
+            if (tid == 0) ctl[60] = K - 1;   // jstar: last divided index in sorted order
             for (int j = tid; j < K; j += nt) {
                 const int p = (int)(S.skey[j] & 0xFFFF);
                 int c = 0;
@@ -456,9 +553,9 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
             __syncthreads();
             block_scan_array(S.tB, K, ctl);
             for (int j = tid; j < K; j += nt)
-                if (n + S.tB[j] + (S.tC[j] - 1) >= N) atomicMin(&ctl[44], j);
+                if (n + S.tB[j] + (S.tC[j] - 1) >= N) atomicMin(&ctl[60], j);
             __syncthreads();
-            const int jstar = ctl[44];
+            const int jstar = ctl[60];
             for (int j = tid; j < K; j += nt) {
                 if (j > jstar) S.tC[j] = 0;
                 else S.tD[(int)(S.skey[j] & 0xFFFF)] = 0;
@@ -494,22 +591,23 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                 }
             }
             if (tid == 0) {
-                ctl[41] = serial0 + Ctot;
-                if (newSize >= N || newSize == n) ctl[43] = 1;
+                ctl[57] = serial0 + Ctot;
+                if (newSize >= N || newSize == n) ctl[59] = 1;
             }
         }
         __syncthreads();
-        if (tid == 0) ctl[40] = newSize;
+        if (tid == 0) ctl[56] = newSize;
         __syncthreads();
         // swap: NEXT (written into the O buffers) becomes CUR, CUR becomes OLD
         { uint64_t* t = rectC; rectC = rectO; rectO = t; }
         { uint32_t* t = cntC; cntC = cntO; cntO = t; }
         { uint32_t* t = bestC; bestC = bestO; bestO = t; }
         { uint32_t* t = serC; serC = serO; serO = t; }
-        if (ctl[43]) break;
+        TR_PHASE(2, 1 + (iter < 28 ? iter : 28) + (mode ? 32 : 0))
+        if (ctl[59]) break;
     }
     // ---- output in list order: retained key per node, lapping flag and rank ----
-    const int n = ctl[40];
+    const int n = ctl[56];
     LevelKp* out = lvl_kp + (int64_t)f * P->kp_slots_total + G.kp_base;
     const int ncap = min(n, G.kp_cap);
     for (int p = tid; p < ncap; p += nt) {
@@ -540,6 +638,8 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
         lvl_nlap[f * P->n_levels + l] = nlap;
         if (n > G.kp_cap) atomicOr(err, 2);
     }
+    TR_PHASE(2, 63)
+    TR_END(2)
 }
 
 // ---------------------------------------------------------------------------
@@ -547,12 +647,23 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
 // GaussianBlur(7x7, 2, REFLECT_101) of the level computed at the 512 sample points from a
 // 43x43 LDS patch (reflect-101 applied at load). Writes the final operator() slot.
 // ---------------------------------------------------------------------------
+// rBRIEF samples lie within +-18 px of the keypoint (max rotated pattern radius 18.38,
+// rounded): the blurred region is 37 x 37, computed from the 43 x 43 patch (+-3 blur halo).
+constexpr int kBlR = 18, kBlW = 2 * kBlR + 1;   // 37
+// GaussianBlur(7x7, sigma 2) 8-bit fixed-point taps (the host checks its table equals these)
+__device__ __forceinline__ constexpr uint32_t blur_tap(int i) {
+    return i == 0 || i == 6 ? 18u : (i == 1 || i == 5 ? 34u : (i == 2 || i == 4 ? 48u : 56u));
+}
+
 __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P, FrameBufs fb,
                                               const LevelKp* __restrict__ lvl_kp, const int* __restrict__ lvl_cnt,
                                               const int* __restrict__ lvl_nlap, const int* __restrict__ disc,
                                               orbhip_kp* __restrict__ out_kps, uint8_t* __restrict__ out_desc,
                                               int cap, int* __restrict__ n_out, int* __restrict__ mono_out) {
     __shared__ uint8_t patch[4][kPatchW * kPatchW + 15];
+    __shared__ uint16_t hrow[4][kPatchW * kBlW];     // row pass: 43 rows x 37 columns
+    __shared__ uint8_t blr[4][kBlW * kBlW + 7];       // blurred 37 x 37
+    TR_BEGIN()
     const int f = blockIdx.y;
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     int slot = blockIdx.x * 4 + wid;
@@ -571,59 +682,116 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
         lap_base += lvl_nlap[f * L + l];
         l++;
     }
-    const bool active = l < L && slot < lvl_cnt[f * L + l];
+    const bool active = l < L && slot < lvl_cnt[f * L + l];   // wave-uniform
     uint8_t* pt = patch[wid];
-    int cx = 0, cy = 0, lw = 0, lh = 0;
+    uint16_t* hr = hrow[wid];
+    uint8_t* bl = blr[wid];
+    int cx = 0, cy = 0;
     LevelKp kp{};
+    constexpr int kPU = (kPatchW * kPatchW + 63) / 64;   // 29 bytes per lane
+    constexpr float kInvPW = 1.0f / kPatchW;
     if (active) {
         const LevelGeom& G = P->lv[l];
         ImgRef im = level_img(P, fb, f, l);
         kp = lvl_kp[(int64_t)f * P->kp_slots_total + G.kp_base + slot];
-        cx = kp.x; cy = kp.y; lw = G.w; lh = G.h;
-        for (int i = lane; i < kPatchW * kPatchW; i += 64) {
-            const int py = i / kPatchW, px = i - py * kPatchW;
-            int yy = cy - kPatchR + py, xx = cx - kPatchR + px;
-            // BORDER_REFLECT_101 (image is >= 43 px in both dims)
-            yy = yy < 0 ? -yy : (yy >= lh ? 2 * lh - 2 - yy : yy);
-            xx = xx < 0 ? -xx : (xx >= lw ? 2 * lw - 2 - xx : xx);
-            pt[i] = im.p[(int64_t)yy * im.pitch + xx];
+        cx = kp.x; cy = kp.y;
+        const int lw = G.w, lh = G.h;
+        const bool inside = cx - kPatchR >= 0 && cy - kPatchR >= 0 && cx + kPatchR < lw && cy + kPatchR < lh;
+        uint8_t v[kPU];
+        if (inside) {
+            const uint8_t* src = im.p + (int64_t)(cy - kPatchR) * im.pitch + (cx - kPatchR);
+#pragma unroll
+            for (int u = 0; u < kPU; u++) {
+                const int i = lane + 64 * u;
+                const int py = (int)(((float)i + 0.5f) * kInvPW), px = i - py * kPatchW;
+                v[u] = i < kPatchW * kPatchW ? src[(int64_t)py * im.pitch + px] : 0;
+            }
+        } else {
+#pragma unroll
+            for (int u = 0; u < kPU; u++) {
+                const int i = lane + 64 * u;
+                const int py = (int)(((float)i + 0.5f) * kInvPW), px = i - py * kPatchW;
+                int yy = cy - kPatchR + py, xx = cx - kPatchR + px;
+                // BORDER_REFLECT_101 (levels are >= 43 px in both dims)
+                yy = yy < 0 ? -yy : (yy >= lh ? 2 * lh - 2 - yy : yy);
+                xx = xx < 0 ? -xx : (xx >= lw ? 2 * lw - 2 - xx : xx);
+                v[u] = i < kPatchW * kPatchW ? im.p[(int64_t)yy * im.pitch + xx] : 0;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kPU; u++) {
+            const int i = lane + 64 * u;
+            if (i < kPatchW * kPatchW) pt[i] = v[u];
         }
     }
     __syncthreads();
-    if (!active) return;
-    const LevelGeom& G = P->lv[l];
-    // ---- IC_Angle: m10 = sum u*I, m01 = sum v*I over the umax disc ----
-    int m10 = 0, m01 = 0;
-    for (int i = lane; i < P->n_disc; i += 64) {
-        const int uv = disc[i];
-        const int u = (int)(int16_t)(uv & 0xFFFF), v = (int)(int16_t)(uv >> 16);
-        const int val = pt[(kPatchR + v) * kPatchW + kPatchR + u];
-        m10 += u * val;
-        m01 += v * val;
+    TR_PHASE(3, 0)
+    // ---- IC_Angle: m10 = sum u*I, m01 = sum v*I over the umax disc (unblurred level) ----
+    float angle = 0.f;
+    if (active) {
+        int m10 = 0, m01 = 0;
+        for (int i = lane; i < P->n_disc; i += 64) {
+            const int uv = disc[i];
+            const int u = (int)(int16_t)(uv & 0xFFFF), vv = (int)(int16_t)(uv >> 16);
+            const int val = pt[(kPatchR + vv) * kPatchW + kPatchR + u];
+            m10 += u * val;
+            m01 += vv * val;
+        }
+        m10 = wave_sum_i32(m10);
+        m01 = wave_sum_i32(m01);
+        angle = fast_atan2((float)m01, (float)m10);
+        // ---- 7x7 blur, row pass: hr[r][c] = sum_i k_i pt[r][c + i], r < 43, c < 37 ----
+        // lane task = 4 consecutive columns of one row (10 byte reads for 4 outputs)
+        for (int t = lane; t < kPatchW * 10; t += 64) {
+            const int r = (int)(((float)t + 0.5f) * 0.1f), c0 = 4 * (t - 10 * r);
+            const uint8_t* row = pt + r * kPatchW + c0;
+            uint32_t x[10];
+#pragma unroll
+            for (int i = 0; i < 10; i++) x[i] = c0 + i < kPatchW ? row[i] : 0u;
+#pragma unroll
+            for (int o = 0; o < 4; o++) {
+                if (c0 + o >= kBlW) break;
+                uint32_t h = 0;
+#pragma unroll
+                for (int i = 0; i < 7; i++) h += blur_tap(i) * x[o + i];
+                hr[r * kBlW + c0 + o] = (uint16_t)h;
+            }
+        }
     }
-    m10 = wave_sum_i32(m10);
-    m01 = wave_sum_i32(m01);
-    const float angle = fast_atan2((float)m01, (float)m10);
-    // ---- rBRIEF ----
+    __syncthreads();
+    if (active) {
+        // ---- column pass: bl[r][c] = (sum_j k_j hr[r + j][c] + 2^15) >> 16, 4 rows per task ----
+        for (int t = lane; t < kBlW * 10; t += 64) {
+            const int rb = (int)(((float)t + 0.5f) * (1.0f / kBlW)), c = t - kBlW * rb, r0 = 4 * rb;
+            uint32_t y[10];
+#pragma unroll
+            for (int j = 0; j < 10; j++) y[j] = r0 + j < kPatchW ? hr[(r0 + j) * kBlW + c] : 0u;
+#pragma unroll
+            for (int o = 0; o < 4; o++) {
+                if (r0 + o >= kBlW) break;
+                uint32_t sacc = 0;
+#pragma unroll
+                for (int j = 0; j < 7; j++) sacc += blur_tap(j) * y[o + j];
+                bl[(r0 + o) * kBlW + c] = (uint8_t)((sacc + (1u << 15)) >> 16);
+            }
+        }
+    }
+    __syncthreads();
+    TR_PHASE(3, 1)
+    if (!active) {
+        TR_END(3)
+        return;
+    }
+    const LevelGeom& G = P->lv[l];
+    // ---- rBRIEF on the blurred region ----
     const float factorPI = (float)(3.14159265358979323846 / 180.f);
     const float ang = angle * factorPI;
     const float a = glibc_cosf(ang), b = glibc_sinf(ang);
-    const int* k7 = P->blurk;
     auto sample = [&](int idx) -> int {
         const float px = (float)kPattern[2 * idx], py = (float)kPattern[2 * idx + 1];
         const int oy = cv_round(px * b + py * a);
         const int ox = cv_round(px * a - py * b);
-        const int X = kPatchR + ox, Y = kPatchR + oy;
-        uint32_t s = 0;
-#pragma unroll
-        for (int j = 0; j < 7; j++) {
-            const uint8_t* row = pt + (Y + j - 3) * kPatchW + X - 3;
-            uint32_t h = 0;
-#pragma unroll
-            for (int i = 0; i < 7; i++) h += (uint32_t)k7[i] * row[i];
-            s += (uint32_t)k7[j] * h;
-        }
-        return (int)((s + (1u << 15)) >> 16);
+        return bl[(kBlR + oy) * kBlW + kBlR + ox];
     };
     // lane handles pairs 4*lane .. 4*lane+3  (byte lane>>1, bits (lane&1)*4 ..)
     int nib = 0;
@@ -634,6 +802,8 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
         nib |= (t0 < t1) << t;
     }
     const int other = __shfl_xor(nib, 1, 64);
+    TR_PHASE(3, 2)
+    TR_END(3)
     const int lapflag = (kp.srl >> 8) & 1;
     const int rank = (int)(kp.srl >> 9);
     const int idx = lapflag ? (total - 1 - (lap_base + rank)) : (mono_base + rank);
@@ -641,9 +811,9 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
     if ((lane & 1) == 0) out_desc[((int64_t)f * cap + idx) * 32 + (lane >> 1)] = (uint8_t)(nib | (other << 4));
     if (lane == 0) {
         orbhip_kp o;
-        const float s = G.scale;
-        o.x = (l == 0) ? (float)cx : (float)cx * s;
-        o.y = (l == 0) ? (float)cy : (float)cy * s;
+        const float sc = G.scale;
+        o.x = (l == 0) ? (float)cx : (float)cx * sc;
+        o.y = (l == 0) ? (float)cy : (float)cy * sc;
         o.size = (float)G.patch_size;
         o.angle = angle;
         o.response = (float)(kp.srl & 0xFF);
@@ -664,9 +834,9 @@ void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs
 }
 
 void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,
-                 uint32_t* cand, int* cand_cnt, hipStream_t st) {
+                 uint32_t* cand, int* cand_cnt, int* err, hipStream_t st) {
     dim3 grd(hP.n_cells_total, B, 1);
-    hipLaunchKernelGGL(k_fast_cells, grd, dim3(256), 0, st, dP, cells, fb, cand, cand_cnt);
+    hipLaunchKernelGGL(k_fast_cells, grd, dim3(256), 0, st, dP, cells, fb, cand, cand_cnt, err);
 }
 
 size_t octree_lds_bytes(const ExtractPlan& hP, const OctreeCfg& cfg) {
@@ -678,6 +848,8 @@ size_t octree_lds_bytes(const ExtractPlan& hP, const OctreeCfg& cfg) {
     carve(NC * 16); carve(NC * 16); carve(NC * 8);
     carve(NC * 4); carve(NC * 4); carve(NC * 4); carve(NC * 4);
     carve((size_t)cfg.sort_cap * 8);
+    carve((size_t)cfg.sort_cap * 8);
+    carve((size_t)(hP.max_cells_level + 1) * 4);
     carve((size_t)(hP.max_cells_level + 1) * 4);
     carve((size_t)cfg.key_cap * 4);
     carve((size_t)cfg.key_cap * 2);

@@ -2,17 +2,22 @@
 // TH_LOW acceptance, then the HISTO_LENGTH=30 rotation-consistency filter
 // (ComputeThreeMaxima). Order-free over the whole train set.
 //
-//   k_match_top2  grid (query blocks of 64, pairs). Train descriptors are staged in LDS in
-//                 tiles of 1024 (32 KiB); each wave owns 16 queries (descriptor in SGPRs),
-//                 lanes sweep the tile (v_xor + v_bcnt), per-lane (best, idx, second) kept
-//                 across tiles, merged across the wave with xor-shuffles.
-//   k_rot_filter  one workgroup per pair: 30-bin rotation histogram, three maxima, filter.
+//   k_match_top2    grid (64-query blocks, 256-descriptor train chunks, pairs): lane = query
+//                   (descriptor in VGPRs), the chunk is staged in LDS and read as broadcasts;
+//                   per-lane best/second/index in train order (v_xor + v_bcnt), the 4 waves'
+//                   quarter-chunks merged in order, one partial per (pair, chunk, query).
+//   k_match_finish  one workgroup per pair: merge the partials in chunk order, TH_LOW + ratio,
+//                   30-bin rotation histogram, three maxima, filter, match count.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 
 #include "orbhip_device.h"
 #include "orbhip_kernels.h"
 
 namespace orbhip {
+
+ORBHIP_TRACE_UNIT(match)
 
 struct MatchView {
     const uint8_t* qd;
@@ -28,8 +33,7 @@ struct MatchView {
     int64_t out_stride;        // entries between pairs in the outputs
 };
 
-constexpr int kTrainTile = 1024;
-constexpr int kQPerWave = 16;
+constexpr int kTC = 256;   // train descriptors per workgroup chunk (64 per wave)
 
 __device__ __forceinline__ void top2_merge(int& b, int& i, int& s, int b2, int i2, int s2) {
     const int nb = (b2 < b || (b2 == b && i2 < i)) ? b2 : b;
@@ -38,71 +42,67 @@ __device__ __forceinline__ void top2_merge(int& b, int& i, int& s, int b2, int i
     b = nb; i = ni; s = ns;
 }
 
-__global__ __launch_bounds__(256) void k_match_top2(MatchView v, int th_low, float ratio, int32_t* __restrict__ match,
-                                                     int32_t* __restrict__ best_out, int32_t* __restrict__ second_out) {
-    __shared__ __attribute__((aligned(16))) uint4 tile[kTrainTile * 2];
-    const int p = blockIdx.y;
+// Partial top-2 of 64 queries (one per lane, descriptor in VGPRs) against one 256-descriptor
+// train chunk broadcast from LDS; wave w scans train [64w, 64w+64) of the chunk in index order
+// (strict <: the first index wins), the 4 waves merge in index order. part[(pair, chunk, q)] =
+// {best | second << 16, index}.
+__global__ __launch_bounds__(256) void k_match_top2(MatchView v, uint2* __restrict__ part, int nchunk_cap,
+                                                     int part_stride) {
+    __shared__ __attribute__((aligned(16))) uint4 tile[kTC * 2];
+    __shared__ int mb[3][64], mi[3][64], ms[3][64];
+    TR_BEGIN()
+    const int p = blockIdx.z;
     const int nq = v.nq_arr ? v.nq_arr[p] : v.nq;
     const int nt = v.nt_arr ? v.nt_arr[p] : v.nt;
-    const int q0 = blockIdx.x * (4 * kQPerWave);
-    if (q0 >= nq) return;
-    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint8_t* qd = v.qd + (int64_t)p * v.pair_desc_stride;
+    const int q0 = blockIdx.x * 64, t0 = blockIdx.y * kTC;
+    if (q0 >= nq || t0 >= nt) return;   // workgroup-uniform
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+    const int tn = min(kTC, nt - t0);
     const uint8_t* td = v.td + (int64_t)p * v.pair_desc_stride;
-    int pb[kQPerWave], pi[kQPerWave], ps[kQPerWave];
-#pragma unroll
-    for (int j = 0; j < kQPerWave; j++) { pb[j] = 256; pi[j] = 0x7fffffff; ps[j] = 256; }
-    const int qw = q0 + wid * kQPerWave;
-    for (int t0 = 0; t0 < nt; t0 += kTrainTile) {
-        const int tn = min(kTrainTile, nt - t0);
-        __syncthreads();
-        const uint4* src = (const uint4*)(td + (int64_t)t0 * 32);
-        for (int i = threadIdx.x; i < tn * 2; i += 256) tile[i] = src[i];
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < kQPerWave; j++) {
-            const int q = qw + j;
-            if (q >= nq) break;   // wave-uniform
-            const uint4* qp = (const uint4*)(qd + (int64_t)q * 32);
-            const uint4 qa = qp[0], qb = qp[1];
-            int b = pb[j], bi = pi[j], s = ps[j];
-            for (int t = lane; t < tn; t += 64) {
-                const uint4 x = tile[2 * t], y = tile[2 * t + 1];
-                const int d = __popc(x.x ^ qa.x) + __popc(x.y ^ qa.y) + __popc(x.z ^ qa.z) + __popc(x.w ^ qa.w) +
-                              __popc(y.x ^ qb.x) + __popc(y.y ^ qb.y) + __popc(y.z ^ qb.z) + __popc(y.w ^ qb.w);
-                if (d < b) { s = b; b = d; bi = t0 + t; }
-                else if (d < s) s = d;
-            }
-            pb[j] = b; pi[j] = bi; ps[j] = s;
-        }
+    const uint4* src = (const uint4*)(td + (int64_t)t0 * 32);
+    for (int i = tid; i < tn * 2; i += 256) tile[i] = src[i];
+    const int q = q0 + lane;
+    uint4 qa = make_uint4(0, 0, 0, 0), qb = qa;
+    if (q < nq) {
+        const uint4* qp = (const uint4*)(v.qd + (int64_t)p * v.pair_desc_stride + (int64_t)q * 32);
+        qa = qp[0];
+        qb = qp[1];
     }
-#pragma unroll
-    for (int j = 0; j < kQPerWave; j++) {
-        const int q = qw + j;
-        if (q >= nq) break;
-        int b = pb[j], bi = pi[j], s = ps[j];
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int b2 = __shfl_xor(b, o, 64), i2 = __shfl_xor(bi, o, 64), s2 = __shfl_xor(s, o, 64);
-            top2_merge(b, bi, s, b2, i2, s2);
-        }
-        if (lane == 0) {
-            const int64_t o = (int64_t)p * v.out_stride + q;
-            const bool ok = b < 256 && b <= th_low && (float)b < ratio * (float)s;
-            match[o] = ok ? bi : -1;
-            best_out[o] = b;
-            second_out[o] = s;
-        }
+    __syncthreads();
+    int b = 256, bi = 0x7fffffff, s = 256;
+    const int w0 = wid * 64, w1 = min(tn, w0 + 64);
+    for (int t = w0; t < w1; t++) {
+        const uint4 x = tile[2 * t], y = tile[2 * t + 1];
+        const int d = __popc(x.x ^ qa.x) + __popc(x.y ^ qa.y) + __popc(x.z ^ qa.z) + __popc(x.w ^ qa.w) +
+                      __popc(y.x ^ qb.x) + __popc(y.y ^ qb.y) + __popc(y.z ^ qb.z) + __popc(y.w ^ qb.w);
+        if (d < b) { s = b; b = d; bi = t0 + t; }
+        else if (d < s) s = d;
     }
+    if (wid > 0) { mb[wid - 1][lane] = b; mi[wid - 1][lane] = bi; ms[wid - 1][lane] = s; }
+    __syncthreads();
+    if (wid == 0 && q < nq) {
+#pragma unroll
+        for (int w = 0; w < 3; w++) top2_merge(b, bi, s, mb[w][lane], mi[w][lane], ms[w][lane]);
+        part[((int64_t)p * nchunk_cap + blockIdx.y) * part_stride + q] = make_uint2((uint32_t)b | ((uint32_t)s << 16),
+                                                                                  (uint32_t)bi);
+    }
+    TR_END(4)
 }
 
-__global__ __launch_bounds__(256) void k_rot_filter(MatchView v, int check_orientation, int32_t* __restrict__ match,
-                                                     int32_t* __restrict__ nmatch) {
+// One workgroup per pair: merge the chunk partials in train order, apply best <= TH_LOW and
+// best < ratio * second, then the HISTO_LENGTH=30 rotation filter (ComputeThreeMaxima).
+__global__ __launch_bounds__(256) void k_match_finish(MatchView v, const uint2* __restrict__ part, int nchunk_cap,
+                                                       int part_stride, int th_low, float ratio, int check_orientation,
+                                                       int32_t* __restrict__ match, int32_t* __restrict__ best_out,
+                                                       int32_t* __restrict__ second_out, int32_t* __restrict__ nmatch) {
     __shared__ int hist[32];
     __shared__ int keep[3];
     __shared__ int cnt;
+    TR_BEGIN()
     const int p = blockIdx.x;
     const int nq = v.nq_arr ? v.nq_arr[p] : v.nq;
+    const int nt = v.nt_arr ? v.nt_arr[p] : v.nt;
+    const int nch = (nt + kTC - 1) / kTC;
     const float* qa = v.qa + (int64_t)p * v.pair_angle_stride;
     const float* ta = v.ta + (int64_t)p * v.pair_angle_stride;
     int32_t* m = match + (int64_t)p * v.out_stride;
@@ -117,12 +117,21 @@ __global__ __launch_bounds__(256) void k_rot_filter(MatchView v, int check_orien
         if (bin == 30) bin = 0;
         return bin;
     };
-    if (check_orientation) {
-        for (int q = threadIdx.x; q < nq; q += 256) {
-            const int t = m[q];
-            if (t >= 0) atomicAdd(&hist[bin_of(q, t)], 1);
+    for (int q = threadIdx.x; q < nq; q += 256) {
+        int b = 256, bi = 0x7fffffff, s = 256;
+        for (int c = 0; c < nch; c++) {
+            const uint2 u = part[((int64_t)p * nchunk_cap + c) * part_stride + q];
+            top2_merge(b, bi, s, (int)(u.x & 0xFFFF), (int)u.y, (int)(u.x >> 16));
         }
-        __syncthreads();
+        const bool ok = b < 256 && b <= th_low && (float)b < ratio * (float)s;
+        const int64_t o = (int64_t)p * v.out_stride + q;
+        m[q] = ok ? bi : -1;
+        best_out[o] = b;
+        second_out[o] = s;
+        if (ok && check_orientation) atomicAdd(&hist[bin_of(q, bi)], 1);
+    }
+    __syncthreads();
+    if (check_orientation) {
         if (threadIdx.x == 0) {
             int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
             for (int i = 0; i < 30; i++) {
@@ -151,25 +160,32 @@ __global__ __launch_bounds__(256) void k_rot_filter(MatchView v, int check_orien
     if ((threadIdx.x & 63) == 0) atomicAdd(&cnt, c);
     __syncthreads();
     if (threadIdx.x == 0) nmatch[p] = cnt;
+    TR_END(5)
 }
 
-static void run_match(const MatchView& v, int npairs, int max_q, int th_low, float ratio, int check_orientation,
-                      int32_t* match, int32_t* best, int32_t* second, int32_t* nmatch, hipStream_t st,
-                      StageTimer* timer = nullptr) {
+size_t match_part_entries(int npairs, int max_q, int max_t) {
+    const int nch = std::max(1, (max_t + kTC - 1) / kTC);
+    return (size_t)std::max(npairs, 1) * nch * std::max(max_q, 1);
+}
+
+static void run_match(const MatchView& v, int npairs, int max_q, int max_t, int th_low, float ratio,
+                      int check_orientation, int32_t* match, int32_t* best, int32_t* second, int32_t* nmatch,
+                      uint2* part, hipStream_t st, StageTimer* timer = nullptr) {
     if (npairs <= 0) return;
-    const int qblocks = (max_q + 4 * kQPerWave - 1) / (4 * kQPerWave);
+    const int qblocks = (max_q + 63) / 64;
+    const int nch = std::max(1, (max_t + kTC - 1) / kTC);
     if (timer) timer->begin(5, st);
-    if (qblocks > 0)
-        hipLaunchKernelGGL(k_match_top2, dim3(qblocks, npairs), dim3(256), 0, st, v, th_low, ratio, match, best,
-                           second);
+    if (qblocks > 0 && max_t > 0)
+        hipLaunchKernelGGL(k_match_top2, dim3(qblocks, nch, npairs), dim3(256), 0, st, v, part, nch, max_q);
     if (timer) { timer->end(5, st); timer->begin(6, st); }
-    hipLaunchKernelGGL(k_rot_filter, dim3(npairs), dim3(256), 0, st, v, check_orientation, match, nmatch);
+    hipLaunchKernelGGL(k_match_finish, dim3(npairs), dim3(256), 0, st, v, part, nch, max_q, th_low, ratio,
+                       check_orientation, match, best, second, nmatch);
     if (timer) timer->end(6, st);
 }
 
 void launch_match_pairs(const orbhip_kp* kps, const uint8_t* desc, const int32_t* n, int npairs, int cap,
                         int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best,
-                        int32_t* second, int32_t* nmatch, hipStream_t st, StageTimer* timer) {
+                        int32_t* second, int32_t* nmatch, void* part, hipStream_t st, StageTimer* timer) {
     MatchView v;
     v.qd = desc;
     v.td = desc + (int64_t)cap * 32;
@@ -183,13 +199,14 @@ void launch_match_pairs(const orbhip_kp* kps, const uint8_t* desc, const int32_t
     v.nq = cap;
     v.nt = cap;
     v.out_stride = cap;
-    run_match(v, npairs, cap, th_low, ratio, check_orientation, match, best, second, nmatch, st, timer);
+    run_match(v, npairs, cap, cap, th_low, ratio, check_orientation, match, best, second, nmatch, (uint2*)part, st,
+              timer);
 }
 
 void launch_match_frames(const orbhip_kp* q_kps, const uint8_t* q_desc, const int32_t* nq, const orbhip_kp* t_kps,
                          const uint8_t* t_desc, const int32_t* nt, int cap, int th_low, float ratio,
                          int check_orientation, int32_t* match, int32_t* best, int32_t* second, int32_t* nmatch,
-                         hipStream_t st, StageTimer* timer) {
+                         void* part, hipStream_t st, StageTimer* timer) {
     MatchView v;
     v.qd = q_desc;
     v.td = t_desc;
@@ -203,12 +220,12 @@ void launch_match_frames(const orbhip_kp* q_kps, const uint8_t* q_desc, const in
     v.nq = cap;
     v.nt = cap;
     v.out_stride = 0;
-    run_match(v, 1, cap, th_low, ratio, check_orientation, match, best, second, nmatch, st, timer);
+    run_match(v, 1, cap, cap, th_low, ratio, check_orientation, match, best, second, nmatch, (uint2*)part, st, timer);
 }
 
 void launch_match_bf(const uint8_t* q, const float* qa, int nq, const uint8_t* t, const float* ta, int nt,
                      int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best,
-                     int32_t* second, int32_t* nmatch, hipStream_t st) {
+                     int32_t* second, int32_t* nmatch, void* part, hipStream_t st) {
     MatchView v;
     v.qd = q; v.td = t; v.qa = qa; v.ta = ta;
     v.angle_stride = 1;
@@ -217,7 +234,7 @@ void launch_match_bf(const uint8_t* q, const float* qa, int nq, const uint8_t* t
     v.nq_arr = nullptr; v.nt_arr = nullptr;
     v.nq = nq; v.nt = nt;
     v.out_stride = 0;
-    run_match(v, 1, nq, th_low, ratio, check_orientation, match, best, second, nmatch, st);
+    run_match(v, 1, nq, nt, th_low, ratio, check_orientation, match, best, second, nmatch, (uint2*)part, st);
 }
 
 // ---- test hooks: device glibc sinf/cosf restatement ----

@@ -85,6 +85,7 @@ struct orbhip_ctx {
     DevBuf<uint32_t> d_cand, d_kscratch;
     DevBuf<uint16_t> d_nscratch;
     DevBuf<int> d_cand_cnt, d_lvl_cnt, d_lvl_nlap, d_err;
+    DevBuf<uint64_t> d_mpart;   // matcher chunk partials (match_part_entries)
     DevBuf<LevelKp> d_lvl_kp;
     DevBuf<orbhip_kp> d_kps;
     DevBuf<uint8_t> d_desc;
@@ -161,6 +162,10 @@ static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
     P.ini_th = std::min(std::max(c->prm.ini_th_fast, 0), 255);
     P.min_th = std::min(std::max(c->prm.min_th_fast, 0), 255);
     for (int i = 0; i < 7; i++) P.blurk[i] = c->blurk[i];
+    // k_desc hard-codes these taps (GaussianBlur 7x7 sigma 2 is fixed in ORBextractor)
+    static const int kTaps[7] = {18, 34, 48, 56, 48, 34, 18};
+    for (int i = 0; i < 7; i++)
+        if (P.blurk[i] != kTaps[i]) return ORBHIP_ERR_UNSUPPORTED;
     int64_t pyr_off = 0;
     int cell_base = 0, slot_base = 0, kp_base = 0, max_cells = 0;
     for (int l = 0; l < L; l++) {
@@ -332,14 +337,13 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
     if (rc) return rc;
     FrameBufs fb;
     fb.in = d_imgs; fb.in_stride = stride; fb.in_fstride = fstride; fb.pyr = c->d_pyr.p;
-    HIPOK(hipMemsetAsync(c->d_err.p, 0, 4 * sizeof(int), st));
     StageTimer& tm = c->timer;
     tm.begin(1, st);
     for (int l = 1; l < P.n_levels; l++)
         launch_resize(pl->d_plan.p, P, fb, B, l, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p, pl->d_ybeta.p, st);
     tm.end(1, st);
     tm.begin(2, st);
-    launch_fast(pl->d_plan.p, P, pl->d_cells.p, fb, B, c->d_cand.p, c->d_cand_cnt.p, st);
+    launch_fast(pl->d_plan.p, P, pl->d_cells.p, fb, B, c->d_cand.p, c->d_cand_cnt.p, c->d_err.p, st);
     tm.end(2, st);
     OctreeCfg oc = pl->oct;
     oc.lap0 = lap0; oc.lap1 = lap1;
@@ -361,6 +365,20 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
 extern "C" {
 
 int orbhip_abi_version(void) { return ORBHIP_ABI_VERSION; }
+
+int orbhip_bgr_to_gray_device(orbhip_ctx* c, const uint8_t* d_bgr, int B, int w, int h, int src_stride,
+                              int64_t src_fstride, uint8_t* d_gray, int dst_stride, int64_t dst_fstride, void* stream) {
+    if (!c || !d_bgr || !d_gray || B < 0 || w <= 0 || h <= 0 || src_stride < 3 * w || dst_stride < w ||
+        (B > 1 && (src_fstride < (int64_t)src_stride * h || dst_fstride < (int64_t)dst_stride * h)))
+        return ORBHIP_ERR_ARG;
+    if (B == 0) return ORBHIP_OK;
+    HIPOK(hipSetDevice(c->device));
+    (void)hipGetLastError();
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    launch_bgr2gray(d_bgr, B, w, h, src_stride, src_fstride, d_gray, dst_stride, dst_fstride, st);
+    HIPOK(hipGetLastError());
+    return ORBHIP_OK;
+}
 
 int orbhip_create(orbhip_ctx** out, int device, const orbhip_orb_params* params) {
     if (!out) return ORBHIP_ERR_ARG;
@@ -504,9 +522,10 @@ int orbhip_match_bf(orbhip_ctx* c, const uint8_t* q, const float* qa, int nq, co
         // no train descriptors: every query keeps best = second = 256 (no match)
         HIPOK(hipMemsetAsync(c->d_mm.p, 0xFF, (size_t)nq * 4, st));
     }
+    HIPOK(c->d_mpart.ensure(match_part_entries(1, nq, nt)));
     (void)hipGetLastError();
     launch_match_bf(c->d_mq.p, c->d_mqa.p, nq, c->d_mt.p, c->d_mta.p, nt, th_low, ratio, check_orientation, c->d_mm.p,
-                    c->d_mb.p, c->d_ms.p, c->d_mn.p, st);
+                    c->d_mb.p, c->d_ms.p, c->d_mn.p, c->d_mpart.p, st);
     HIPOK(hipGetLastError());
     int nm = 0;
     HIPOK(hipMemcpyAsync(match, c->d_mm.p, (size_t)nq * 4, hipMemcpyDeviceToHost, st));
@@ -524,9 +543,10 @@ int orbhip_match_pairs_device(orbhip_ctx* c, const orbhip_kp* d_kps, const uint8
         return ORBHIP_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    HIPOK(c->d_mpart.ensure(match_part_entries(B - 1, cap, cap)));
     (void)hipGetLastError();
     launch_match_pairs(d_kps, d_desc, d_n, B - 1, cap, th_low, ratio, check_orientation, d_match, d_best, d_second,
-                       d_nmatch, st, &c->timer);
+                       d_nmatch, c->d_mpart.p, st, &c->timer);
     HIPOK(hipGetLastError());
     return ORBHIP_OK;
 }
@@ -540,9 +560,10 @@ int orbhip_match_frames_device(orbhip_ctx* c, const orbhip_kp* d_q_kps, const ui
         return ORBHIP_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    HIPOK(c->d_mpart.ensure(match_part_entries(1, cap, cap)));
     (void)hipGetLastError();
     launch_match_frames(d_q_kps, d_q_desc, d_nq, d_t_kps, d_t_desc, d_nt, cap, th_low, ratio, check_orientation,
-                        d_match, d_best, d_second, d_nmatch, st, &c->timer);
+                        d_match, d_best, d_second, d_nmatch, c->d_mpart.p, st, &c->timer);
     HIPOK(hipGetLastError());
     return ORBHIP_OK;
 }
@@ -684,6 +705,26 @@ int orbhip_test_extract_debug(orbhip_ctx* c, const uint8_t* img, int w, int h, i
 }
 
 // Cell table of a plan (level, x0, y0, wc, hc, slot_off per cell) for offline checks.
+// Device timing trace (diagnostics; see orbhip_device.h TR_*): on != 0 allocates a zeroed
+// buffer of kTraceKernels x kTraceStride u64 and points every kernel unit at it; on == 0 copies
+// it to `out` (if non-null, kTraceKernels * kTraceStride entries) and detaches it.
+int orbhip_test_trace(int on, unsigned long long* out) {
+    static unsigned long long* buf = nullptr;
+    const size_t n = (size_t)kTraceKernels * kTraceStride;
+    if (on) {
+        if (!buf) HIPOK(hipMalloc((void**)&buf, n * sizeof(unsigned long long)));
+        HIPOK(hipMemset(buf, 0, n * sizeof(unsigned long long)));
+        trace_set_extract(buf);
+        trace_set_match(buf);
+        return ORBHIP_OK;
+    }
+    HIPOK(hipDeviceSynchronize());
+    if (buf && out) HIPOK(hipMemcpy(out, buf, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    trace_set_extract(nullptr);
+    trace_set_match(nullptr);
+    return ORBHIP_OK;
+}
+
 int orbhip_test_cells(orbhip_ctx* c, int w, int h, int32_t* out6, int cap) {
     if (!c) return ORBHIP_ERR_ARG;
     Plan* pl = nullptr;

@@ -133,22 +133,57 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
 }
 
 // Exclusive block scan of one int per thread. `scratch` >= blockDim/64 + 1 ints of LDS.
-// Returns the exclusive prefix; *total receives the block sum. Contains __syncthreads.
+// Returns the exclusive prefix; *total receives the block sum. Two barriers: every wave
+// re-scans the per-wave partials itself (no serial thread-0 pass); the trailing barrier lets
+// the caller reuse `scratch` immediately.
 __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int* total) {
     const int lane = lane_id(), wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
-    int inc = wave_incl_scan(v);
+    const int inc = wave_incl_scan(v);
     if (lane == 63) scratch[wid] = inc;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int s = 0;
-        for (int i = 0; i < nw; i++) { int t = scratch[i]; scratch[i] = s; s += t; }
-        scratch[nw] = s;
-    }
+    const int ws = wave_incl_scan(lane < nw ? scratch[lane] : 0);
+    const int before = __shfl(ws, wid > 0 ? wid - 1 : 0, 64);
+    *total = __shfl(ws, nw - 1, 64);
     __syncthreads();
-    int res = scratch[wid] + inc - v;
-    *total = scratch[nw];
-    __syncthreads();
-    return res;
+    return (wid > 0 ? before : 0) + inc - v;
 }
+
+// ---------------------------------------------------------------------------
+// Diagnostics: per-workgroup timing trace (test hooks orbhip_test_trace_*). g_trace is null
+// unless enabled, so production launches pay one scalar load and a branch. Each translation
+// unit owns its copy (no relocatable device code), set through trace_set_<unit>().
+// Layout per kernel id k (stride kTraceStride u64): [2b], [2b+1] = s_memrealtime (100 MHz)
+// at start / end of workgroup b (b < 4096); [8192 + ph] = s_memtime cycles of phase ph of
+// workgroup 0 (last launch).
+// ---------------------------------------------------------------------------
+
+#define ORBHIP_TRACE_UNIT(unit)                                                             \
+    static __device__ unsigned long long* g_trace = nullptr;                               \
+    void trace_set_##unit(unsigned long long* p) {                                         \
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &p, sizeof(p));                       \
+    }
+
+#define TR_BEGIN()                                                                          \
+    unsigned long long tr_t0 = 0, tr_tp = 0;                                                \
+    unsigned long long* const tr_buf = g_trace;                                             \
+    (void)tr_tp;                                                                            \
+    if (tr_buf && threadIdx.x == 0) {                                                       \
+        tr_t0 = __builtin_amdgcn_s_memrealtime();                                           \
+        tr_tp = __builtin_amdgcn_s_memtime();                                               \
+    }
+#define TR_PHASE(kid, ph)                                                                   \
+    if (tr_buf && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) { \
+        const unsigned long long tr_t = __builtin_amdgcn_s_memtime();                       \
+        tr_buf[(kid) * kTraceStride + 8192 + (ph)] = tr_t - tr_tp;                          \
+        tr_tp = tr_t;                                                                       \
+    }
+#define TR_END(kid)                                                                         \
+    if (tr_buf && threadIdx.x == 0) {                                                       \
+        const unsigned tr_b = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z); \
+        if (tr_b < 4096) {                                                                  \
+            tr_buf[(kid) * kTraceStride + 2 * tr_b] = tr_t0;                                \
+            tr_buf[(kid) * kTraceStride + 2 * tr_b + 1] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                                   \
+    }
 
 }  // namespace orbhip

@@ -38,7 +38,7 @@ struct StageTimer {
 void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, int B, int l,
                    const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st);
 void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,
-                 uint32_t* cand, int* cand_cnt, hipStream_t st);
+                 uint32_t* cand, int* cand_cnt, int* err, hipStream_t st);
 size_t octree_lds_bytes(const ExtractPlan& hP, const OctreeCfg& cfg);
 bool octree_set_lds_limit(size_t bytes);
 void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const uint32_t* cand,
@@ -49,18 +49,28 @@ void launch_desc(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& 
                  int cap, int* n_out, int* mono_out, int B, hipStream_t st);
 
 // ---- matching ----
+// `part`: scratch of match_part_entries(npairs, max queries, max train) x 8 bytes (chunk partials)
+size_t match_part_entries(int npairs, int max_q, int max_t);
 void launch_match_pairs(const orbhip_kp* kps, const uint8_t* desc, const int32_t* n, int npairs, int cap,
                         int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best,
-                        int32_t* second, int32_t* nmatch, hipStream_t st, StageTimer* timer);
+                        int32_t* second, int32_t* nmatch, void* part, hipStream_t st, StageTimer* timer);
 void launch_match_frames(const orbhip_kp* q_kps, const uint8_t* q_desc, const int32_t* nq, const orbhip_kp* t_kps,
                          const uint8_t* t_desc, const int32_t* nt, int cap, int th_low, float ratio,
                          int check_orientation, int32_t* match, int32_t* best, int32_t* second, int32_t* nmatch,
-                         hipStream_t st, StageTimer* timer);
+                         void* part, hipStream_t st, StageTimer* timer);
 void launch_match_bf(const uint8_t* q, const float* qa, int nq, const uint8_t* t, const float* ta, int nt,
                      int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best,
-                     int32_t* second, int32_t* nmatch, hipStream_t st);
+                     int32_t* second, int32_t* nmatch, void* part, hipStream_t st);
+
+// ---- ingest ----
+void launch_bgr2gray(const uint8_t* src, int B, int w, int h, int sstride, int64_t sfstride, uint8_t* dst, int dstride,
+                     int64_t dfstride, hipStream_t st);
 
 // ---- test hooks ----
+constexpr int kTraceStride = 16384;   // u64 per kernel id in the timing trace (orbhip_device.h)
+constexpr int kTraceKernels = 8;
+void trace_set_extract(unsigned long long* p);
+void trace_set_match(unsigned long long* p);
 void launch_sincos_probe(const float* x, float* c, float* s, int64_t n, hipStream_t st);
 void launch_sincos_sweep(uint32_t lo_bits, uint32_t hi_bits, const float* ref_c, const float* ref_s,
                          unsigned long long* mismatches, hipStream_t st);

@@ -18,7 +18,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import KP_DTYPE, Context, OrbHipError, check, lib, ptr
+from ._lib import torch_stream, KP_DTYPE, Context, OrbHipError, check, lib, ptr
 
 
 @dataclass
@@ -110,7 +110,7 @@ class ORBextractor:
         n_out / mono_out int32 [B]. Asynchronous on ``stream`` (torch stream or None)."""
         B, H, W = frames.shape
         cap = desc_out.shape[1]
-        st = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        st = torch_stream(stream)
         rc = lib().orbhip_extract_batch_device(self.ctx.handle, ptr(frames), B, W, H, frames.stride(1),
                                                frames.stride(0), int(vLappingArea[0]), int(vLappingArea[1]),
                                                ptr(kps_out), ptr(desc_out), cap, ptr(n_out), ptr(mono_out), st)

@@ -12,7 +12,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import Context, check, lib, ptr
+from ._lib import torch_stream, Context, check, lib, ptr
 
 
 class ORBmatcher:
@@ -49,7 +49,7 @@ class ORBmatcher:
         """Device tensors from ORBextractor.extract_batch_device: match frame p -> p+1."""
         B, cap = desc.shape[0], desc.shape[1]
         th = self.TH_LOW if th_low is None else int(th_low)
-        st = None if stream is None else ctypes.c_void_p(stream.cuda_stream)
+        st = torch_stream(stream)
         check(lib().orbhip_match_pairs_device(self.ctx.handle, ptr(kps), ptr(desc), ptr(n), B, cap, th,
                                               ctypes.c_float(self.mfNNratio), int(self.mbCheckOrientation),
                                               ptr(match), ptr(best), ptr(second), ptr(nmatch), st),
