@@ -14,8 +14,10 @@
  * Conventions:
  *  - Plain pointers and sizes only; no C++ types, no exceptions cross this ABI.
  *  - The caller owns every host buffer. A context owns its device memory, pinned
- *    staging and one HIP stream. One context per calling thread; a context is not
- *    re-entrant; distinct contexts are safe to use concurrently.
+ *    staging and one HIP stream (used by the host-buffer entry points). The *_device entry
+ *    points run on the caller's `stream` argument; NULL is the HIP null stream. One context
+ *    per calling thread; a context is not re-entrant; distinct contexts are safe to use
+ *    concurrently.
  *  - Status: 0 ok, < 0 error (orbhip_status).
  *  - Parity contract: keypoints/descriptors bit-exact with the CPU restatement in
  *    oracle/ (the reference's own path cannot be built here: SURVEY.md §0, §8c).
@@ -85,7 +87,7 @@ int orbhip_extract(orbhip_ctx* ctx, const uint8_t* img, int w, int h, int stride
 /* Batched, fully device-resident form (torch-ROCm ingest, benchmarks). d_imgs: B frames,
  * frame f at d_imgs + f*frame_stride, rows `stride` bytes apart. Outputs per frame f:
  * d_kps[f*cap ...], d_desc[(f*cap ...)*32], d_n[f], d_mono[f]. Asynchronous on `stream`
- * (hipStream_t, NULL = the context's stream). */
+ * (hipStream_t; NULL = the HIP null stream, as in every HIP API — torch's default stream). */
 int orbhip_extract_batch_device(orbhip_ctx* ctx, const uint8_t* d_imgs, int B, int w, int h, int stride,
                                 int64_t frame_stride, int lap0, int lap1, orbhip_kp* d_kps, uint8_t* d_desc,
                                 int cap, int32_t* d_n, int32_t* d_mono, void* stream);
@@ -95,7 +97,7 @@ int orbhip_extract_batch_device(orbhip_ctx* ctx, const uint8_t* d_imgs, int B, i
  * on the device, bit-exact: Y = (B*1868 + G*9617 + R*4899 + 2^13) >> 14. B frames of w x h
  * BGR (3 bytes/px, rows `src_stride` bytes apart, frames `src_fstride` apart) -> u8 gray
  * (rows `dst_stride`, frames `dst_fstride`), ready for orbhip_extract_batch_device.
- * Asynchronous on `stream` (NULL = the context's stream). */
+ * Asynchronous on `stream` (NULL = the HIP null stream). */
 int orbhip_bgr_to_gray_device(orbhip_ctx* ctx, const uint8_t* d_bgr, int B, int w, int h, int src_stride,
                               int64_t src_fstride, uint8_t* d_gray, int dst_stride, int64_t dst_fstride,
                               void* stream);

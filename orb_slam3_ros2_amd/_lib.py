@@ -106,8 +106,9 @@ def lib():
 
 def torch_stream(stream=None):
     """hipStream_t for a device call on torch tensors: the given torch stream, else torch's
-    CURRENT stream — so the call is ordered after the torch work that produced its inputs and
-    before torch reads its outputs (the context's own stream would race with both)."""
+    CURRENT stream (handle 0 = the HIP null stream, which the ABI takes as such) — so the call
+    is ordered after the torch work that produced its inputs and before torch reads its
+    outputs."""
     import torch
     s = stream if stream is not None else torch.cuda.current_stream()
     return ctypes.c_void_p(s.cuda_stream)

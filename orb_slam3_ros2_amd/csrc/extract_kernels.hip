@@ -474,6 +474,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
         // ---- sweep: remap keys through map4 (OLD rect split), classify into CUR children ----
         for (int i = tid; i < n * 4; i += nt) { S.ccount[i] = 0; S.cbest[i] = 0; }
         __syncthreads();
+        if (iter == 1) { TR_PHASE(2, 40) }
         for (int k = tid; k < M; k += nt) {
             const uint32_t key = keys[k];
             const int x = cand_x(key), y = cand_y(key);
@@ -487,6 +488,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
             }
         }
         __syncthreads();
+        if (iter == 1) { TR_PHASE(2, 41) }
         const int mode = ctl[58];
         const int serial0 = ctl[57];
         int newSize;
@@ -500,8 +502,10 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                 S.tA[p] = c; S.tB[p] = div ? 0 : 1; S.tC[p] = e;
             }
             __syncthreads();
+            if (iter == 1) { TR_PHASE(2, 42) }
             int tot3[3];
             block_scan_array3(S.tA, S.tB, S.tC, n, ctl, tot3);
+            if (iter == 1) { TR_PHASE(2, 43) }
             const int T = tot3[0], U = tot3[1], nToExpand = tot3[2];
             newSize = T + U;
             for (int p = tid; p < n; p += nt) {
@@ -596,6 +600,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
             }
         }
         __syncthreads();
+        if (iter == 1) { TR_PHASE(2, 44) }
         if (tid == 0) ctl[56] = newSize;
         __syncthreads();
         // swap: NEXT (written into the O buffers) becomes CUR, CUR becomes OLD

@@ -90,16 +90,21 @@ __global__ __launch_bounds__(256) void k_match_top2(MatchView v, uint2* __restri
 }
 
 // One workgroup per pair: merge the chunk partials in train order, apply best <= TH_LOW and
-// best < ratio * second, then the HISTO_LENGTH=30 rotation filter (ComputeThreeMaxima).
-__global__ __launch_bounds__(256) void k_match_finish(MatchView v, const uint2* __restrict__ part, int nchunk_cap,
-                                                       int part_stride, int th_low, float ratio, int check_orientation,
-                                                       int32_t* __restrict__ match, int32_t* __restrict__ best_out,
-                                                       int32_t* __restrict__ second_out, int32_t* __restrict__ nmatch) {
+// best < ratio * second, then the HISTO_LENGTH=30 rotation filter (ComputeThreeMaxima). The
+// per-query match and bin stay in LDS between the two passes (queries beyond kFinQ re-read).
+constexpr int kFinQ = 6144;
+__global__ __launch_bounds__(1024) void k_match_finish(MatchView v, const uint2* __restrict__ part, int nchunk_cap,
+                                                        int part_stride, int th_low, float ratio,
+                                                        int check_orientation, int32_t* __restrict__ match,
+                                                        int32_t* __restrict__ best_out, int32_t* __restrict__ second_out,
+                                                        int32_t* __restrict__ nmatch) {
     __shared__ int hist[32];
     __shared__ int keep[3];
     __shared__ int cnt;
+    __shared__ int mq[kFinQ];
+    __shared__ int8_t bq[kFinQ];
     TR_BEGIN()
-    const int p = blockIdx.x;
+    const int p = blockIdx.x, nt_ = blockDim.x;
     const int nq = v.nq_arr ? v.nq_arr[p] : v.nq;
     const int nt = v.nt_arr ? v.nt_arr[p] : v.nt;
     const int nch = (nt + kTC - 1) / kTC;
@@ -117,18 +122,24 @@ __global__ __launch_bounds__(256) void k_match_finish(MatchView v, const uint2* 
         if (bin == 30) bin = 0;
         return bin;
     };
-    for (int q = threadIdx.x; q < nq; q += 256) {
+    for (int q = threadIdx.x; q < nq; q += nt_) {
         int b = 256, bi = 0x7fffffff, s = 256;
         for (int c = 0; c < nch; c++) {
             const uint2 u = part[((int64_t)p * nchunk_cap + c) * part_stride + q];
             top2_merge(b, bi, s, (int)(u.x & 0xFFFF), (int)u.y, (int)(u.x >> 16));
         }
         const bool ok = b < 256 && b <= th_low && (float)b < ratio * (float)s;
+        const int mt = ok ? bi : -1;
         const int64_t o = (int64_t)p * v.out_stride + q;
-        m[q] = ok ? bi : -1;
         best_out[o] = b;
         second_out[o] = s;
-        if (ok && check_orientation) atomicAdd(&hist[bin_of(q, bi)], 1);
+        int bin = -1;
+        if (ok && check_orientation) {
+            bin = bin_of(q, bi);
+            atomicAdd(&hist[bin], 1);
+        }
+        if (q < kFinQ) { mq[q] = mt; bq[q] = (int8_t)bin; }
+        else m[q] = mt;
     }
     __syncthreads();
     if (check_orientation) {
@@ -147,14 +158,13 @@ __global__ __launch_bounds__(256) void k_match_finish(MatchView v, const uint2* 
         __syncthreads();
     }
     int c = 0;
-    for (int q = threadIdx.x; q < nq; q += 256) {
-        const int t = m[q];
-        if (t < 0) continue;
-        if (check_orientation) {
-            const int bin = bin_of(q, t);
-            if (bin != keep[0] && bin != keep[1] && bin != keep[2]) { m[q] = -1; continue; }
-        }
-        c++;
+    for (int q = threadIdx.x; q < nq; q += nt_) {
+        int t, bin;
+        if (q < kFinQ) { t = mq[q]; bin = bq[q]; }
+        else { t = m[q]; bin = (t >= 0 && check_orientation) ? bin_of(q, t) : -1; }
+        if (t >= 0 && check_orientation && bin != keep[0] && bin != keep[1] && bin != keep[2]) t = -1;
+        m[q] = t;
+        c += t >= 0;
     }
     c = wave_sum_i32(c);
     if ((threadIdx.x & 63) == 0) atomicAdd(&cnt, c);
@@ -178,7 +188,7 @@ static void run_match(const MatchView& v, int npairs, int max_q, int max_t, int 
     if (qblocks > 0 && max_t > 0)
         hipLaunchKernelGGL(k_match_top2, dim3(qblocks, nch, npairs), dim3(256), 0, st, v, part, nch, max_q);
     if (timer) { timer->end(5, st); timer->begin(6, st); }
-    hipLaunchKernelGGL(k_match_finish, dim3(npairs), dim3(256), 0, st, v, part, nch, max_q, th_low, ratio,
+    hipLaunchKernelGGL(k_match_finish, dim3(npairs), dim3(1024), 0, st, v, part, nch, max_q, th_low, ratio,
                        check_orientation, match, best, second, nmatch);
     if (timer) timer->end(6, st);
 }

@@ -374,7 +374,7 @@ int orbhip_bgr_to_gray_device(orbhip_ctx* c, const uint8_t* d_bgr, int B, int w,
     if (B == 0) return ORBHIP_OK;
     HIPOK(hipSetDevice(c->device));
     (void)hipGetLastError();
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the HIP null stream (HIP convention)
     launch_bgr2gray(d_bgr, B, w, h, src_stride, src_fstride, d_gray, dst_stride, dst_fstride, st);
     HIPOK(hipGetLastError());
     return ORBHIP_OK;
@@ -442,7 +442,7 @@ int orbhip_extract_batch_device(orbhip_ctx* c, const uint8_t* d_imgs, int B, int
     Plan* pl = nullptr;
     int rc = build_plan(c, w, h, &pl);
     if (rc) return rc;
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the HIP null stream (HIP convention)
     return run_extract(c, pl, d_imgs, B, stride, frame_stride, lap0, lap1, d_kps, d_desc, cap, d_n, d_mono, st);
 }
 
@@ -542,7 +542,7 @@ int orbhip_match_pairs_device(orbhip_ctx* c, const orbhip_kp* d_kps, const uint8
     if (!c || !d_kps || !d_desc || !d_n || B < 2 || cap <= 0 || !d_match || !d_best || !d_second || !d_nmatch)
         return ORBHIP_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the HIP null stream (HIP convention)
     HIPOK(c->d_mpart.ensure(match_part_entries(B - 1, cap, cap)));
     (void)hipGetLastError();
     launch_match_pairs(d_kps, d_desc, d_n, B - 1, cap, th_low, ratio, check_orientation, d_match, d_best, d_second,
@@ -559,7 +559,7 @@ int orbhip_match_frames_device(orbhip_ctx* c, const orbhip_kp* d_q_kps, const ui
         !d_second || !d_nmatch)
         return ORBHIP_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the HIP null stream (HIP convention)
     HIPOK(c->d_mpart.ensure(match_part_entries(1, cap, cap)));
     (void)hipGetLastError();
     launch_match_frames(d_q_kps, d_q_desc, d_nq, d_t_kps, d_t_desc, d_nt, cap, th_low, ratio, check_orientation,

@@ -56,7 +56,7 @@ def test_mono_ingest_end_to_end(oracle):
     bgr = _bgr(8, 640, 480)
     ing = MonoIngest(640, 480)
     kps, desc, n, mono = ing(bgr)
-    nk = int(n.item())
+    nk = int(n.item())          # no device-wide synchronize: stream ordering must suffice
     omono, ok6, od = oracle.extract(oracle.bgr2gray(bgr))
     ok = oracle_kps_to_struct(ok6)
     gk = kps[:nk].cpu().numpy().view(np.float32)
