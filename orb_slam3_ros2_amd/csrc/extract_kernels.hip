@@ -350,8 +350,8 @@ __device__ void block_scan_array3(int* a0, int* a1, int* a2, int n, int* ctl, in
 #pragma unroll
     for (int k = 0; k < 3; k++) {
         const int ws = wave_incl_scan(lane < nw ? ctl[16 * k + lane] : 0);
-        const int before = __shfl(ws, wid > 0 ? wid - 1 : 0, 64);
-        tot[k] = __shfl(ws, nw - 1, 64);
+        const int before = __builtin_amdgcn_readlane(ws, wid > 0 ? wid - 1 : 0);
+        tot[k] = __builtin_amdgcn_readlane(ws, nw - 1);
         off[k] = (wid > 0 ? before : 0) + inc[k] - s[k];
     }
 #pragma unroll
@@ -368,6 +368,22 @@ __device__ void block_rank_sort_desc(const uint64_t* __restrict__ a, uint64_t* _
         out[r] = x;
     }
     __syncthreads();
+}
+
+// cnt[tgt] += 1 for every lane with tgt != ~0u. Lanes form runs of equal tgt (keys are
+// cell-major, so neighbouring lanes mostly share a node); each run head adds the run length
+// (distance to the next head, from one ballot) with ONE LDS atomic — same-address atomics
+// would otherwise serialise lane by lane. The neighbour compare is a DPP wave_shr:1 move.
+__device__ __forceinline__ void wave_aggregate_count(uint32_t tgt, uint32_t* cnt) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp((int)~tgt, (int)tgt, 0x138, 0xF, 0xF, false);
+    const bool head = prev != tgt;   // lane 0 receives ~tgt
+    const uint64_t heads = __ballot(head);
+    if (head && tgt != 0xFFFFFFFFu) {
+        const uint64_t above = lane == 63 ? 0ull : (heads & (~0ull << (lane + 1)));
+        const int next = above ? __ffsll((unsigned long long)above) - 1 : 64;
+        atomicAdd(&cnt[tgt], (uint32_t)(next - lane));
+    }
 }
 
 __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__ P, const CellGeom* __restrict__ cells,
@@ -410,8 +426,10 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
         S.cslot[i] = cells[G.cell_base + i].slot_off;
     }
     __syncthreads();
+    TR_PHASE(2, 50)
     const int M = block_scan_array(S.cellstart, ncell, ctl);
     if (tid == 0) S.cellstart[ncell] = M;
+    TR_PHASE(2, 51)
     const bool keys_in_lds = M <= cfg.key_cap;
     uint32_t* keys = keys_in_lds ? keysL : kscratch + (int64_t)f * P->n_slots_total + G.slot_base;
     uint16_t* knode = keys_in_lds ? knodeL : nscratch + (int64_t)f * P->n_slots_total + G.slot_base;
@@ -427,20 +445,26 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
         }
         keys[k] = cbase[S.cslot[lo] + (k - S.cellstart[lo])];
     }
+    TR_PHASE(2, 52)
     // ---- 2. roots (nIni <= 64 enforced by the host) ----
     const int nIni = G.n_ini;
-    for (int i = tid; i < nIni * 4; i += nt) { S.ccount[i] = 0; S.cbest[i] = 0; }
+    for (int i = tid; i < nIni * 4; i += nt) S.ccount[i] = 0;
     __syncthreads();
     const float hX = G.hX;
-    for (int k = tid; k < M; k += nt) {
-        const uint32_t key = keys[k];
-        int r = (int)((float)cand_x(key) / hX);
-        r = r < 0 ? 0 : (r >= nIni ? nIni - 1 : r);
-        atomicAdd(&S.ccount[r], 1u);
-        atomicMax(&S.cbest[r], pack_best(cand_s(key), k));
-        knode[k] = (uint16_t)r;
+    for (int k0 = 0; k0 < M; k0 += nt) {
+        const int k = k0 + tid;
+        uint32_t tgt = 0xFFFFFFFFu;
+        if (k < M) {
+            const uint32_t key = keys[k];
+            int r = (int)((float)cand_x(key) / hX);
+            r = r < 0 ? 0 : (r >= nIni ? nIni - 1 : r);
+            tgt = (uint32_t)r;
+            knode[k] = (uint16_t)r;
+        }
+        wave_aggregate_count(tgt, S.ccount);
     }
     __syncthreads();
+    TR_PHASE(2, 53)
     if (tid == 0) {
         int n = 0;
         const int H = G.max_by - G.min_by;
@@ -448,7 +472,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
             const uint64_t rr = mk_rect((int)(hX * (float)r), 0, (int)(hX * (float)(r + 1)), H);
             S.rectB[r] = rr;   // OLD buffer = roots (remap source)
             if (S.ccount[r] > 0) {
-                S.rectA[n] = rr; S.cntA[n] = S.ccount[r]; S.bestA[n] = S.cbest[r]; S.serA[n] = r;
+                S.rectA[n] = rr; S.cntA[n] = S.ccount[r]; S.serA[n] = r;
                 S.map4[r * 4 + 0] = S.map4[r * 4 + 1] = S.map4[r * 4 + 2] = S.map4[r * 4 + 3] = (uint16_t)n;
                 n++;
             }
@@ -462,8 +486,8 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
     TR_PHASE(2, 0)
     // CUR = A, OLD = B
     uint64_t *rectC = S.rectA, *rectO = S.rectB;
-    uint32_t *cntC = S.cntA, *bestC = S.bestA, *serC = S.serA;
-    uint32_t *cntO = S.cntB, *bestO = S.bestB, *serO = S.serB;
+    uint32_t *cntC = S.cntA, *serC = S.serA;
+    uint32_t *cntO = S.cntB, *serO = S.serB;
     const int N = G.n_feat;
     for (int iter = 0;; iter++) {
         const int n = ctl[56];
@@ -472,20 +496,21 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
             break;
         }
         // ---- sweep: remap keys through map4 (OLD rect split), classify into CUR children ----
-        for (int i = tid; i < n * 4; i += nt) { S.ccount[i] = 0; S.cbest[i] = 0; }
+        for (int i = tid; i < n * 4; i += nt) S.ccount[i] = 0;
         __syncthreads();
         if (iter == 1) { TR_PHASE(2, 40) }
-        for (int k = tid; k < M; k += nt) {
-            const uint32_t key = keys[k];
-            const int x = cand_x(key), y = cand_y(key);
-            const int o = knode[k];
-            const int nd = S.map4[o * 4 + quad_of(rectO[o], x, y)];
-            knode[k] = (uint16_t)nd;
-            if (cntC[nd] > 1) {
-                const int q = quad_of(rectC[nd], x, y);
-                atomicAdd(&S.ccount[nd * 4 + q], 1u);
-                atomicMax(&S.cbest[nd * 4 + q], pack_best(cand_s(key), k));
+        for (int k0 = 0; k0 < M; k0 += nt) {
+            const int k = k0 + tid;
+            uint32_t tgt = 0xFFFFFFFFu;
+            if (k < M) {
+                const uint32_t key = keys[k];
+                const int x = cand_x(key), y = cand_y(key);
+                const int o = knode[k];
+                const int nd = S.map4[o * 4 + quad_of(rectO[o], x, y)];
+                knode[k] = (uint16_t)nd;
+                if (cntC[nd] > 1) tgt = (uint32_t)(nd * 4 + quad_of(rectC[nd], x, y));
             }
+            wave_aggregate_count(tgt, S.ccount);
         }
         __syncthreads();
         if (iter == 1) { TR_PHASE(2, 41) }
@@ -520,13 +545,13 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                         if (cq == 0) continue;
                         const int pos = base + (c - 1 - r);   // n4..n1 order inside the block
                         rectO[pos] = child_rect(rectC[p], q);
-                        cntO[pos] = cq; bestO[pos] = S.cbest[p * 4 + q]; serO[pos] = serial0 + cb + r;
+                        cntO[pos] = cq; serO[pos] = serial0 + cb + r;
                         S.map4[p * 4 + q] = (uint16_t)pos;
                         r++;
                     }
                 } else {
                     const int pos = T + S.tB[p];
-                    rectO[pos] = rectC[p]; cntO[pos] = cntC[p]; bestO[pos] = bestC[p]; serO[pos] = serC[p];
+                    rectO[pos] = rectC[p]; cntO[pos] = cntC[p]; serO[pos] = serC[p];
                     S.map4[p * 4 + 0] = S.map4[p * 4 + 1] = S.map4[p * 4 + 2] = S.map4[p * 4 + 3] = (uint16_t)pos;
                 }
             }
@@ -582,7 +607,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                     if (cq == 0) continue;
                     const int pos = base + (c - 1 - r);
                     rectO[pos] = child_rect(rectC[p], q);
-                    cntO[pos] = cq; bestO[pos] = S.cbest[p * 4 + q]; serO[pos] = serial0 + cb + r;
+                    cntO[pos] = cq; serO[pos] = serial0 + cb + r;
                     S.map4[p * 4 + q] = (uint16_t)pos;
                     r++;
                 }
@@ -590,7 +615,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
             for (int p = tid; p < n; p += nt) {
                 if (S.tD[p]) {
                     const int pos = Ctot + S.tA[p];
-                    rectO[pos] = rectC[p]; cntO[pos] = cntC[p]; bestO[pos] = bestC[p]; serO[pos] = serC[p];
+                    rectO[pos] = rectC[p]; cntO[pos] = cntC[p]; serO[pos] = serC[p];
                     S.map4[p * 4 + 0] = S.map4[p * 4 + 1] = S.map4[p * 4 + 2] = S.map4[p * 4 + 3] = (uint16_t)pos;
                 }
             }
@@ -606,17 +631,27 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
         // swap: NEXT (written into the O buffers) becomes CUR, CUR becomes OLD
         { uint64_t* t = rectC; rectC = rectO; rectO = t; }
         { uint32_t* t = cntC; cntC = cntO; cntO = t; }
-        { uint32_t* t = bestC; bestC = bestO; bestO = t; }
         { uint32_t* t = serC; serC = serO; serO = t; }
         TR_PHASE(2, 1 + (iter < 28 ? iter : 28) + (mode ? 32 : 0))
         if (ctl[59]) break;
     }
-    // ---- output in list order: retained key per node, lapping flag and rank ----
+    // ---- retained key per final node: max (response, then lowest key index) over the keys of
+    // the node; keys reach their final node through the last division's map4 ----
     const int n = ctl[56];
+    for (int i = tid; i < n; i += nt) S.cbest[i] = 0;
+    __syncthreads();
+    for (int k = tid; k < M; k += nt) {
+        const uint32_t key = keys[k];
+        const int o = knode[k];
+        const int nd = S.map4[o * 4 + quad_of(rectO[o], cand_x(key), cand_y(key))];
+        atomicMax(&S.cbest[nd], pack_best(cand_s(key), k));
+    }
+    __syncthreads();
+    // ---- output in list order: retained key per node, lapping flag and rank ----
     LevelKp* out = lvl_kp + (int64_t)f * P->kp_slots_total + G.kp_base;
     const int ncap = min(n, G.kp_cap);
     for (int p = tid; p < ncap; p += nt) {
-        const int k = (int)(0xFFFFFFu - (bestC[p] & 0xFFFFFFu));
+        const int k = (int)(0xFFFFFFu - (S.cbest[p] & 0xFFFFFFu));
         const uint32_t key = keys[k];
         const int x = cand_x(key) + G.min_bx, y = cand_y(key) + G.min_by;
         const float xs = (l == 0) ? (float)x : (float)x * G.scale;

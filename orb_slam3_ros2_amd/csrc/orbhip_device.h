@@ -115,21 +115,21 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-__device__ __forceinline__ int wave_sum_i32(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+
+// inclusive prefix sum within a wave64: DPP row_shr 1/2/4/8 inside each 16-lane row, then
+// row_bcast:15 / row_bcast:31 carry the row totals (VALU only, no LDS round trips)
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);   // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);   // row_bcast:31 -> rows 2, 3
     return v;
 }
 
-// inclusive prefix sum within a wave64
-__device__ __forceinline__ int wave_incl_scan(int v) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        int t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
-    return v;
+__device__ __forceinline__ int wave_sum_i32(int v) {
+    return __builtin_amdgcn_readlane(wave_incl_scan(v), 63);
 }
 
 // Exclusive block scan of one int per thread. `scratch` >= blockDim/64 + 1 ints of LDS.
@@ -142,8 +142,8 @@ __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int* total) 
     if (lane == 63) scratch[wid] = inc;
     __syncthreads();
     const int ws = wave_incl_scan(lane < nw ? scratch[lane] : 0);
-    const int before = __shfl(ws, wid > 0 ? wid - 1 : 0, 64);
-    *total = __shfl(ws, nw - 1, 64);
+    const int before = __builtin_amdgcn_readlane(ws, wid > 0 ? wid - 1 : 0);   // wid is wave-uniform
+    *total = __builtin_amdgcn_readlane(ws, nw - 1);
     __syncthreads();
     return (wid > 0 ? before : 0) + inc - v;
 }
