@@ -166,19 +166,26 @@ __global__ __launch_bounds__(256) void k_fast_cells(const ExtractPlan* __restric
     {
         const int tot = wc * hc;
         const float inv_wc = 1.0f / (float)wc;
-        uint8_t v[kWinMax * kWinMax / 256 + 1];
+        if (tot <= 8 * 256) {
+            // normal cells (window <= 2048 px): 8 unconditional loads from clamped addresses,
+            // straight-line so all are in flight together, then predicated stores
+            uint8_t v[8];
 #pragma unroll
-        for (int u = 0; u < kWinMax * kWinMax / 256 + 1; u++) {
-            const int i = tid + 256 * u;
-            if (i < tot) {
+            for (int u = 0; u < 8; u++) {
+                const int i = min(tid + 256 * u, tot - 1);
                 const int yy = small_div(i, inv_wc), xx = i - yy * wc;
                 v[u] = base[(int64_t)yy * im.pitch + xx];
             }
-        }
 #pragma unroll
-        for (int u = 0; u < kWinMax * kWinMax / 256 + 1; u++) {
-            const int i = tid + 256 * u;
-            if (i < tot) win[i] = v[u];
+            for (int u = 0; u < 8; u++) {
+                const int i = tid + 256 * u;
+                if (i < tot) win[i] = v[u];
+            }
+        } else {
+            for (int i = tid; i < tot; i += 256) {
+                const int yy = small_div(i, inv_wc), xx = i - yy * wc;
+                win[i] = base[(int64_t)yy * im.pitch + xx];
+            }
         }
     }
     __syncthreads();
@@ -187,7 +194,13 @@ __global__ __launch_bounds__(256) void k_fast_cells(const ExtractPlan* __restric
     const int t_lo = min(t_ini, t_min);
     const int dc = wc - 6, dr = hc - 6, np = dc * dr;
     const float inv_dc = 1.0f / (float)dc;
-    // ---- strength map: m if m > t_lo (a corner at some threshold in use), else 0 ----
+    // ---- strength map: m if m > t_lo (a corner at some threshold in use), else 0; stored with
+    // a zero border (row pitch W2 = dc + 2) so the NMS reads its 3x3 without bounds checks ----
+    const int W2 = dc + 2;
+    for (int i = tid; i < 2 * W2 + 2 * dr; i += 256) {
+        const int idx = i < W2 ? i : (i < 2 * W2 ? (dr + 1) * W2 + (i - W2) : (1 + (i - 2 * W2) / 2) * W2 + ((i & 1) ? W2 - 1 : 0));
+        mv[idx] = 0;
+    }
     for (int p = tid; p < np; p += 256) {
         const int py = small_div(p, inv_dc), px = p - py * dc;
         const uint8_t* c = &win[(py + 3) * wc + px + 3];
@@ -202,7 +215,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const ExtractPlan* __restric
             m = fast_strength_d(d);
             if (m <= t_lo) m = 0;
         }
-        mv[p] = (uint8_t)m;
+        mv[(py + 1) * W2 + px + 1] = (uint8_t)m;
     }
     __syncthreads();
     TR_PHASE(1, 1)
@@ -213,28 +226,19 @@ __global__ __launch_bounds__(256) void k_fast_cells(const ExtractPlan* __restric
     for (int q0 = p0, ci = 0; q0 < p1; q0 += 64, ci++) {
         const int p = q0 + lane;
         bool k_ini = false, k_min = false;
-        if (p < p1) {
-            const int m = mv[p];
-            if (m > 0) {
-                const int py = small_div(p, inv_dc), px = p - py * dc;
-                int nb[8];
-                int j = 0;
+        {
+            const int pc = min(p, np - 1);   // branch-free: all 9 reads in flight together
+            const int py = small_div(pc, inv_dc), px = pc - py * dc;
+            const uint8_t* c = &mv[(py + 1) * W2 + px + 1];
+            const int m = c[0];
+            const int nb[8] = {c[-W2 - 1], c[-W2], c[-W2 + 1], c[-1], c[1], c[W2 - 1], c[W2], c[W2 + 1]};
+            k_ini = p < p1 && m > t_ini;
+            k_min = p < p1 && m > t_min;
 #pragma unroll
-                for (int yy = -1; yy <= 1; yy++)
-#pragma unroll
-                    for (int xx = -1; xx <= 1; xx++) {
-                        if (yy == 0 && xx == 0) continue;
-                        const int qx = px + xx, qy = py + yy;
-                        nb[j++] = (qx < 0 || qy < 0 || qx >= dc || qy >= dr) ? 0 : mv[qy * dc + qx];
-                    }
-                k_ini = m > t_ini;
-                k_min = m > t_min;
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const int mq = nb[k];
-                    k_ini &= (m - 1) > (mq > t_ini ? mq - 1 : 0);
-                    k_min &= (m - 1) > (mq > t_min ? mq - 1 : 0);
-                }
+            for (int k = 0; k < 8; k++) {
+                const int mq = nb[k];
+                k_ini &= (m - 1) > (mq > t_ini ? mq - 1 : 0);
+                k_min &= (m - 1) > (mq > t_min ? mq - 1 : 0);
             }
         }
         const uint64_t bi = __ballot(k_ini), bm = __ballot(k_min);
@@ -257,7 +261,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const ExtractPlan* __restric
         if ((mk >> lane) & 1ull) {
             const int py = small_div(p, inv_dc), px = p - py * dc;
             const int x = cg.x0 + 3 + px - G.min_bx, y = cg.y0 + 3 + py - G.min_by;
-            out[off + __popcll(mk & lt)] = pack_cand(x, y, (int)mv[p] - 1);
+            out[off + __popcll(mk & lt)] = pack_cand(x, y, (int)mv[(py + 1) * W2 + px + 1] - 1);
         }
         off += __popcll(mk);
     }
@@ -742,20 +746,20 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
             const uint8_t* src = im.p + (int64_t)(cy - kPatchR) * im.pitch + (cx - kPatchR);
 #pragma unroll
             for (int u = 0; u < kPU; u++) {
-                const int i = lane + 64 * u;
+                const int i = min(lane + 64 * u, kPatchW * kPatchW - 1);   // branch-free loads
                 const int py = (int)(((float)i + 0.5f) * kInvPW), px = i - py * kPatchW;
-                v[u] = i < kPatchW * kPatchW ? src[(int64_t)py * im.pitch + px] : 0;
+                v[u] = src[(int64_t)py * im.pitch + px];
             }
         } else {
 #pragma unroll
             for (int u = 0; u < kPU; u++) {
-                const int i = lane + 64 * u;
+                const int i = min(lane + 64 * u, kPatchW * kPatchW - 1);
                 const int py = (int)(((float)i + 0.5f) * kInvPW), px = i - py * kPatchW;
                 int yy = cy - kPatchR + py, xx = cx - kPatchR + px;
                 // BORDER_REFLECT_101 (levels are >= 43 px in both dims)
                 yy = yy < 0 ? -yy : (yy >= lh ? 2 * lh - 2 - yy : yy);
                 xx = xx < 0 ? -xx : (xx >= lw ? 2 * lw - 2 - xx : xx);
-                v[u] = i < kPatchW * kPatchW ? im.p[(int64_t)yy * im.pitch + xx] : 0;
+                v[u] = im.p[(int64_t)yy * im.pitch + xx];
             }
         }
 #pragma unroll
