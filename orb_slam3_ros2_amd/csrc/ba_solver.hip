@@ -35,10 +35,11 @@
 #include <vector>
 
 #include "orbhip_ba.h"
+#include "ba_chol.h"
+#include "ba_chol_blocked.h"
 
 namespace orbhip {
 
-typedef double double4_t __attribute__((ext_vector_type(4)));
 
 struct BaArgs {
     int P, M, E, np, n;
@@ -74,6 +75,7 @@ struct BaArgs {
     int* flag;         // [0] cholesky ok
     const double* lambda;   // current lambda of this problem (device copy)
     double* Lsave;     // ceil(n/32) x 1024: L11^{-1} of every Cholesky panel
+    const int* row_first;   // ceil(n/32): envelope of S in 32x32 tiles (blocked solver)
 };
 
 #define BA_PROLOGUE                                 \
@@ -415,6 +417,7 @@ __global__ __launch_bounds__(256) void k_ba_schur_b(const BaArgs* __restrict__ a
 //  (c) backward solve panel by panel: x_p = Linv^T (y_p - L21^T x_below) (Linv saved per panel).
 // ---------------------------------------------------------------------------
 constexpr int kNB = 32;
+constexpr int kCholSmallN = 480;   // largest n of the single-workgroup solver (LDS envelope)
 constexpr int kPS = 34;   // panel row stride in doubles
 
 __host__ __device__ inline size_t chol_lds_doubles(int n) {
@@ -422,66 +425,6 @@ __host__ __device__ inline size_t chol_lds_doubles(int n) {
     return (size_t)(2 + 32 * 33 + np + (size_t)np * kPS + 4 * 32 + 32 * 33);
 }
 
-__device__ __forceinline__ double readlane_f64(double v, int lane) {
-    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
-    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, lane);
-    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), lane);
-    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
-}
-
-// (a) of chol_solve: factor the 32x32 diagonal block at (k0, k0) with one wavefront.
-__device__ __forceinline__ void chol_diag_wave(double* __restrict__ S, int n, int k0, int kb, double* __restrict__ Li,
-                                            double* __restrict__ Lsave, int* bad) {
-    const int lane = threadIdx.x & 63;
-    const int c = lane & 31, h = lane >> 5;
-    double d[16], xi[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int r = 2 * k + h;
-        double v = (r == c) ? 1.0 : 0.0;
-        if (r < kb && c < kb)
-            v = r >= c ? S[(size_t)(k0 + r) * n + k0 + c] : S[(size_t)(k0 + c) * n + k0 + r];
-        d[k] = v;
-        xi[k] = (r == c) ? 1.0 : 0.0;
-    }
-    double myip = 1.0;
-    bool nonpd = false;
-#pragma unroll
-    for (int j = 0; j < 32; j++) {
-        const int jr = j >> 1, jh = 32 * (j & 1);
-        // all cross-lane operands of this step first (one LDS wait), then the FMAs
-        double colj[16];
-#pragma unroll
-        for (int k = 0; k < 16; k++)
-            if (2 * k + 1 > j) colj[k] = __shfl(d[k], j + 32 * h, 64);   // D[r][j], r = 2k+h
-        const double rowj = __shfl(d[jr], c + jh, 64);                   // D[j][c]
-        const double xrow = __shfl(xi[jr], c + jh, 64);                  // X[j][c]
-        const double piv = readlane_f64(d[jr], j + jh);                  // uniform
-        nonpd |= !(piv > 0.0);
-        const double ip = 1.0 / (piv > 0.0 ? piv : 1.0);
-        if (c == j) myip = ip;
-        const double rs = c > j ? rowj * ip : 0.0;      // trailing columns: D[r][c] -= D[r][j] D[j][c] / piv
-        const double xs = c > j ? 0.0 : xrow * ip;      // eliminated columns: X[r][c] -= D[r][j] X[j][c] / piv
-#pragma unroll
-        for (int k = 0; k < 16; k++) {
-            if (2 * k + 1 <= j) continue;                  // rows r <= j untouched
-            const double m = (2 * k == j && h == 0) ? 0.0 : colj[k];   // row r == j itself
-            d[k] = fma(-m, rs, d[k]);
-            xi[k] = fma(-m, xs, xi[k]);
-        }
-    }
-    const double dv = sqrt(1.0 / myip), idv = 1.0 / dv;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        const int r = 2 * k + h;
-        const double idr = __shfl(idv, r, 64);
-        if (r < kb && c < kb && c <= r) S[(size_t)(k0 + r) * n + k0 + c] = r == c ? dv : d[k] * idv;
-        const double li = (r < kb && c < kb) ? xi[k] * idr : 0.0;
-        Li[r * 33 + c] = li;
-        if (Lsave) Lsave[(size_t)(k0 / 32) * 1024 + r * 32 + c] = li;
-    }
-    if (lane == 0 && nonpd) *bad = 1;
-}
 
 __device__ __forceinline__ void chol_solve(double* __restrict__ S, const double* __restrict__ bs, double* __restrict__ x, int n,
                            int* __restrict__ flag, double* __restrict__ Lsave, unsigned long long* __restrict__ dbg) {
@@ -832,6 +775,7 @@ struct Prep {
     int rc = 0;
     int P = 0, M = 0, E = 0, np = 0, n = 0, nblk = 0;
     std::vector<int> opt, pt_ptr, pt_edges, ps_ptr, ps_edges, blk_i, blk_j, blk_ptr, blk_pairs;
+    std::vector<int> row_first;   // blocked Cholesky structure: first 32-col tile per 32-row tile
     // offsets (elements) into the packed buffers; see the segment map in ba_solve_batch
     size_t o_chi2, o_state, o_obs, o_hw, o_scr, o_S, o_L, o_int;
 };
@@ -860,7 +804,8 @@ int prepare(const orbhip_ba_problem* pr, Prep& o) {
         if (!pr->pose_fixed[i]) o.opt[i] = np++;
     o.np = np;
     o.n = 6 * np;
-    if (o.n > 480) return ORBHIP_ERR_UNSUPPORTED;   // single-workgroup Cholesky (LDS-resident panel)
+    // n <= kCholSmallN: single-workgroup Cholesky (LDS-resident panel); larger: blocked solver
+    if (o.n > kCbMaxN) return ORBHIP_ERR_UNSUPPORTED;
     const int* e_pose = pr->edge_pose;
     const int* e_pt = pr->edge_point;
     o.pt_ptr.assign(M + 1, 0);
@@ -909,6 +854,18 @@ int prepare(const orbhip_ba_problem* pr, Prep& o) {
             }
         }
     o.nblk = (int)o.blk_i.size();
+    {   // envelope of S: first pose column coupled to each pose row (blocks are stored i <= j)
+        std::vector<int> fp(np);
+        for (int i = 0; i < np; i++) fp[i] = i;
+        for (int b = 0; b < o.nblk; b++) fp[o.blk_j[b]] = std::min(fp[o.blk_j[b]], o.blk_i[b]);
+        const int nt = (o.n + 31) / 32;
+        o.row_first.assign(nt, 0);
+        for (int R = 0; R < nt; R++) {
+            int f = R;
+            for (int r = 32 * R; r < std::min(o.n, 32 * R + 32); r++) f = std::min(f, (6 * fp[r / 6]) / 32);
+            o.row_first[R] = f;
+        }
+    }
     o.blk_pairs.resize(2 * npairs);
     std::vector<int> fill(o.blk_ptr.begin(), o.blk_ptr.end() - 1);
     for (int m = 0; m < M; m++)
@@ -1056,14 +1013,15 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         nR = (nR + 1) & ~size_t(1);
         p.o_L = nR; nR += 1024 * ((n + 31) / 32);
         p.o_int = ni;
-        ni += (P + 4) + 2 * E + (M + 1) + E + (np_ + 1) + p.ps_edges.size() + 3 * p.nblk + 1 + p.blk_pairs.size();
+        ni += (P + 4) + 2 * E + (M + 1) + E + (np_ + 1) + p.ps_edges.size() + 3 * p.nblk + 1 + p.blk_pairs.size() +
+              p.row_first.size();
     }
     const size_t sC = 0, sA = nC, sU = sA + nA, sZ = (sU + nU + 1) & ~size_t(1), sR = sZ + nZ;
     const size_t nd = sR + nR;
     BAOK(ws->dbl.ensure(nd));
     BAOK(ws->ints.ensure(ni));
     BAOK(ws->args.ensure(B));
-    BAOK(ws->act.ensure(2 * (size_t)B));
+    BAOK(ws->act.ensure(3 * (size_t)B));
     BAOK(ws->lam.ensure(B));
     BAOK(ws->gath.ensure(5 * (size_t)B));
     BAOK(ws->hdbl.ensure(sU + nU));
@@ -1078,7 +1036,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         BAOK(hipHostMalloc((void**)&ws->h_gath, sizeof(double) * 5 * B, hipHostMallocDefault));
         BAOK(hipHostMalloc((void**)&ws->h_lam, sizeof(double) * B, hipHostMallocDefault));
         BAOK(hipHostMalloc((void**)&ws->h_red, sizeof(double) * 5 * B, hipHostMallocDefault));
-        BAOK(hipHostMalloc((void**)&ws->h_act, sizeof(int) * 2 * B, hipHostMallocDefault));
+        BAOK(hipHostMalloc((void**)&ws->h_act, sizeof(int) * 3 * B, hipHostMallocDefault));
         ws->h_cap = B;
     }
     double* D = ws->dbl.p;
@@ -1116,6 +1074,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.blk_j = dev(put(p.blk_j.data(), p.nblk));
         a.blk_ptr = dev(put(p.blk_ptr.data(), p.nblk + 1));
         a.blk_pairs = dev(put(p.blk_pairs.data(), p.blk_pairs.size()));
+        a.row_first = dev(put(p.row_first.data(), p.row_first.size()));
         a.nblk = p.nblk;
         a.P = p.P; a.M = p.M; a.E = p.E; a.np = p.np; a.n = p.n;
         a.fx = pr->fx; a.fy = pr->fy; a.cx = pr->cx; a.cy = pr->cy; a.delta = pr->huber_delta;
@@ -1152,9 +1111,12 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         lds_set = true;
     }
     int maxM = 0, maxE = 0, maxP = 0, maxNp = 0, maxBlk = 0, maxN = 0;
+    bool any_large = false;
     for (auto& p : pp) {
         maxM = std::max(maxM, p.M); maxE = std::max(maxE, p.E); maxP = std::max(maxP, p.P);
-        maxNp = std::max(maxNp, p.np); maxBlk = std::max(maxBlk, p.nblk); maxN = std::max(maxN, p.n);
+        maxNp = std::max(maxNp, p.np); maxBlk = std::max(maxBlk, p.nblk);
+        if (p.n > kCholSmallN) any_large = true;
+        else maxN = std::max(maxN, p.n);
     }
     const size_t chol_lds = sizeof(double) * chol_lds_doubles(maxN);
     auto gx = [](int n_, int b_) { return (unsigned)std::max(1, (n_ + b_ - 1) / b_); };
@@ -1228,7 +1190,22 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             hipLaunchKernelGGL(k_ba_schur_w, dim3(gx(maxE, 256), nt_), dim3(256), 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_schur_blocks, dim3(gx(maxBlk, 4), nt_), dim3(256), 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_schur_b, dim3(gx(maxNp, 4), nt_), dim3(256), 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_cholesky, dim3(nt_), dim3(512), chol_lds, st, dA, d_act);
+            if (!any_large) {
+                hipLaunchKernelGGL(k_ba_cholesky, dim3(nt_), dim3(512), chol_lds, st, dA, d_act);
+            } else {
+                // small problems: one workgroup each (act slot 3); large: the blocked solver
+                int ns = 0;
+                for (int b : trial)
+                    if (pp[b].n <= kCholSmallN) h_act[2 * B + ns++] = b;
+                if (ns) {
+                    BAOK(hipMemcpyAsync(d_act + 2 * B, h_act + 2 * B, ns * sizeof(int), hipMemcpyHostToDevice, st));
+                    hipLaunchKernelGGL(k_ba_cholesky, dim3(ns), dim3(512), chol_lds, st, dA, d_act + 2 * B);
+                }
+                for (int b : trial)
+                    if (pp[b].n > kCholSmallN)
+                        chol_blocked_solve(ha[b].S, pp[b].n, ha[b].Lsave, ha[b].bs, ha[b].x, ha[b].flag,
+                                           ha[b].row_first, st);
+            }
             hipLaunchKernelGGL(k_ba_backsub, dim3(gx(maxM, 256), nt_), dim3(256), 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_update_poses, dim3(gx(maxP, 256), nt_), dim3(256), 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), nt_), dim3(256), 0, st, dA, d_act);

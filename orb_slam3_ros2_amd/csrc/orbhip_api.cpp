@@ -22,6 +22,7 @@
 
 #include "../../include/orbhip.h"
 #include "orbhip_ba.h"
+#include "ba_chol_blocked.h"
 #include "orbhip_kernels.h"
 #include "orbhip_plan.h"
 
@@ -624,6 +625,10 @@ int orbhip_test_cholesky(const double* A, const double* b, double* x, int n, uns
                          float* ms) {
     if (!A || !b || !x || n <= 0 || n > 480) return ORBHIP_ERR_ARG;
     return ba_test_cholesky(A, b, x, n, phases5, ms);
+}
+int orbhip_test_cholesky_blocked(const double* A, const double* b, double* x, int n, float* ms) {
+    if (!A || !b || !x || n <= 0 || !ms) return ORBHIP_ERR_ARG;
+    return chol_blocked_test(A, b, x, n, ms);
 }
 int orbhip_test_sincosf(const float* x, float* cs, float* sn, int64_t n) {
     if (!x || !cs || !sn || n <= 0) return ORBHIP_ERR_ARG;

@@ -98,3 +98,17 @@ def test_batch_matches_single(opt, oracle):
     for p, g in zip(probs, res):
         # small problems converge inside optimize(10): accept/reject near rho ~ 0 is rounding noise
         _compare(g, oracle.ba_solve(p), p, exact_schedule=p.points.shape[0] >= 1500)
+
+
+@pytest.mark.parametrize("n_kf,n_pts,window", [(100, 3000, 20), (90, 2500, 90)])
+def test_gba_blocked_cholesky_parity(opt, oracle, n_kf, n_pts, window):
+    """GlobalBundleAdjustment-sized reduced systems (n = 6*(n_kf-1) > 480) go through the blocked
+    multi-workgroup Cholesky: a keyframe loop with a 20-KF co-visibility window (banded S with a
+    loop-closure corner, tiles skipped by the envelope) and a fully co-visible set (dense S)."""
+    from orb_slam3_ros2_amd.optimizer import BAProblem
+    prob, _ = synthetic_ba_problem(n_kf=n_kf, n_pts=n_pts, layout="loop", window=window, seed=11)
+    p = BAProblem(**{**prob.__dict__, "iterations": 10, "huber_delta": float(np.sqrt(5.99))})
+    g = opt.BundleAdjustment(prob, nIterations=10, bRobust=True)
+    o = oracle.ba_solve(p)
+    _compare(g, o, p)
+    assert g.final_chi2 < 0.2 * g.initial_chi2
