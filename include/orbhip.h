@@ -185,6 +185,25 @@ int orbhip_ba_solve(orbhip_ctx* ctx, const orbhip_ba_problem* prob, orbhip_ba_re
 int orbhip_ba_solve_batch(orbhip_ctx* ctx, const orbhip_ba_problem* probs, int B, orbhip_ba_result* res,
                           const volatile int* stop_flag);
 
+/* ---- multi-GPU BundleAdjustment (SURVEY.md §8e, C5 GlobalBundleAdjustment) --------
+ * One process per GPU. Landmarks (with their edges) are partitioned across ranks; every rank
+ * holds all poses. Per LM trial the ranks sum their Schur contributions (the reduced camera
+ * system S, its right-hand side, Hpp, chi2 / scale terms) with RCCL all-reduces over xGMI, solve
+ * the identical S redundantly and back-substitute their own landmarks; all ranks follow one LM
+ * schedule and return identical poses.
+ *   orbhip_comm_unique_id  rank 0 only; send the 128 bytes to every rank (any transport)
+ *   orbhip_comm_init       collective over the ranks: creates the context's communicator
+ *   orbhip_ba_solve_sharded  collective: this rank's shard (all poses, its landmarks/edges);
+ *                            the stop flag is agreed on (max over ranks) at each iteration
+ *   orbhip_ba_solve_shards_local  the same decomposition with all shards in one process on one
+ *                            device (the sums run on the device): single-GPU model and test. */
+int orbhip_comm_unique_id(uint8_t* id128);
+int orbhip_comm_init(orbhip_ctx* ctx, int nranks, int rank, const uint8_t* id128);
+int orbhip_ba_solve_sharded(orbhip_ctx* ctx, const orbhip_ba_problem* shard, orbhip_ba_result* res,
+                            const volatile int* stop_flag);
+int orbhip_ba_solve_shards_local(orbhip_ctx* ctx, const orbhip_ba_problem* shards, int nshards,
+                                 orbhip_ba_result* res, const volatile int* stop_flag);
+
 #ifdef __cplusplus
 }
 #endif

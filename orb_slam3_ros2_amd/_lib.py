@@ -59,7 +59,8 @@ class BAResultC(ctypes.Structure):
 EXPORTED = ["orbhip_abi_version", "orbhip_create", "orbhip_destroy", "orbhip_level_info", "orbhip_max_keypoints",
             "orbhip_extract", "orbhip_extract_batch_device", "orbhip_descriptor_distance", "orbhip_match_bf",
             "orbhip_match_pairs_device", "orbhip_match_frames_device", "orbhip_profile_stage",
-            "orbhip_profile_collect", "orbhip_ba_solve", "orbhip_ba_solve_batch", "orbhip_bgr_to_gray_device"]
+            "orbhip_profile_collect", "orbhip_ba_solve", "orbhip_ba_solve_batch", "orbhip_bgr_to_gray_device",
+            "orbhip_comm_unique_id", "orbhip_comm_init", "orbhip_ba_solve_sharded", "orbhip_ba_solve_shards_local"]
 
 
 def lib():
@@ -92,6 +93,10 @@ def lib():
     L.orbhip_match_bf.argtypes = [vp, vp, vp, i32, vp, vp, i32, i32, f32, i32, vp, vp, vp]
     L.orbhip_match_pairs_device.argtypes = [vp, vp, vp, vp, i32, i32, i32, f32, i32, vp, vp, vp, vp, vp]
     L.orbhip_match_frames_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, i32, vp, vp, vp, vp, vp]
+    L.orbhip_comm_unique_id.argtypes = [vp]
+    L.orbhip_comm_init.argtypes = [vp, i32, i32, vp]
+    L.orbhip_ba_solve_sharded.argtypes = [vp, ctypes.POINTER(BAProblemC), ctypes.POINTER(BAResultC), vp]
+    L.orbhip_ba_solve_shards_local.argtypes = [vp, ctypes.POINTER(BAProblemC), i32, ctypes.POINTER(BAResultC), vp]
     L.orbhip_bgr_to_gray_device.argtypes = [vp, vp, i32, i32, i32, i32, ctypes.c_int64, vp, i32, ctypes.c_int64, vp]
     L.orbhip_profile_stage.argtypes = [vp, i32]
     L.orbhip_profile_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)]

@@ -22,6 +22,7 @@
 //   k_ba_reduce        activeRobustChi2, computeScale, max diag; fixed-order reductions
 //   k_ba_pop           restore the pushed state of problems whose trial was rejected
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -76,6 +77,7 @@ struct BaArgs {
     const double* lambda;   // current lambda of this problem (device copy)
     double* Lsave;     // ceil(n/32) x 1024: L11^{-1} of every Cholesky panel
     const int* row_first;   // ceil(n/32): envelope of S in 32x32 tiles (blocked solver)
+    int lead;          // sharded solve: this shard adds the pose-side Hpp + lambda terms (once)
 };
 
 #define BA_PROLOGUE                                 \
@@ -346,7 +348,7 @@ __global__ __launch_bounds__(256) void k_ba_schur_blocks(const BaArgs* __restric
     const double lambda = *a.lambda;
     const int i = a.blk_i[blk], j = a.blk_j[blk];
     const int rr = lane < 36 ? lane / 6 : 0, cc = lane < 36 ? lane - 6 * (lane / 6) : 0;
-    double s = (i == j && lane < 36) ? a.Hpp[36 * i + 6 * rr + cc] + (rr == cc ? lambda : 0.0) : 0.0;
+    double s = (i == j && lane < 36 && a.lead) ? a.Hpp[36 * i + 6 * rr + cc] + (rr == cc ? lambda : 0.0) : 0.0;
     const int k0 = a.blk_ptr[blk], k1 = a.blk_ptr[blk + 1];
     for (int kb = k0; kb < k1; kb += 64) {
         const int cnt = min(64, k1 - kb);
@@ -721,6 +723,24 @@ __device__ double block_sum(double v, double* sh) {
     return s;
 }
 
+// In-batch model of the sharded solve: problems 0..B-1 are shards of one problem (same poses,
+// disjoint landmarks); every shard's field[off .. off+count) becomes the sum (op 0) or max
+// (op 1) over the shards, in shard order (deterministic). field: 0 Hpp, 1 S, 2 bs, 3 red.
+__device__ __forceinline__ double* shard_field(const BaArgs& a, int field) {
+    return field == 0 ? a.Hpp : (field == 1 ? a.S : (field == 2 ? a.bs : a.red));
+}
+__global__ __launch_bounds__(256) void k_ba_shard_reduce(const BaArgs* __restrict__ args, int B, int field, int off,
+                                                         size_t count, int op) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x) {
+        double acc = op ? -1.0e300 : 0.0;
+        for (int b = 0; b < B; b++) {
+            const double v = shard_field(args[b], field)[off + i];
+            acc = op ? fmax(acc, v) : acc + v;
+        }
+        for (int b = 0; b < B; b++) shard_field(args[b], field)[off + i] = acc;
+    }
+}
+
 __global__ __launch_bounds__(1024) void k_ba_reduce(const BaArgs* __restrict__ args, const int* __restrict__ act,
                                                     int what) {
     const BaArgs& a = args[act[blockIdx.x]];
@@ -733,9 +753,10 @@ __global__ __launch_bounds__(1024) void k_ba_reduce(const BaArgs* __restrict__ a
     }
     if (what & 2) {
         const double lambda = *a.lambda;
+        const double lam_pose = a.lead ? lambda : 0.0;   // pose x is replicated across shards
         v = 0;
         const int N = a.n + 3 * a.M;
-        for (int j = threadIdx.x; j < N; j += blockDim.x) v += a.x[j] * (lambda * a.x[j] + a.b[j]);
+        for (int j = threadIdx.x; j < N; j += blockDim.x) v += a.x[j] * ((j < a.n ? lam_pose : lambda) * a.x[j] + a.b[j]);
         v = block_sum(v, sh);
         if (threadIdx.x == 0) a.red[1] = v;
     }
@@ -957,12 +978,19 @@ struct BaWorkspace {
     double* h_red = nullptr;   // pinned: per problem red[4] + flag
     int* h_act = nullptr;      // pinned
     size_t h_cap = 0;
+    // sharded solve over RCCL (orbhip_comm_init): landmarks partitioned, poses replicated
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+    DBuf<int> dstop;           // stop-flag consensus (all-reduce max)
+    int* h_stop = nullptr;     // pinned
 };
 
 BaWorkspace* ba_create() { return new BaWorkspace(); }
 
 void ba_destroy(BaWorkspace* w) {
     if (!w) return;
+    if (w->comm) (void)ncclCommDestroy(w->comm);
+    if (w->h_stop) (void)hipHostFree(w->h_stop);
     if (w->h_lam) (void)hipHostFree(w->h_lam);
     if (w->h_red) (void)hipHostFree(w->h_red);
     if (w->h_act) (void)hipHostFree(w->h_act);
@@ -977,8 +1005,9 @@ struct LmState {
 };
 
 int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B, orbhip_ba_result* const* res,
-                   const volatile int* stop, hipStream_t st) {
+                   const volatile int* stop, hipStream_t st, int shard_mode) {
     if (B <= 0 || !probs || !res) return ORBHIP_ERR_ARG;
+    if (shard_mode == kShardRccl && (B != 1 || !ws->comm)) return ORBHIP_ERR_ARG;
     for (int b = 0; b < B; b++)
         if (!probs[b] || !res[b]) return ORBHIP_ERR_ARG;
     static const bool timing = std::getenv("ORBHIP_BA_TIMING") != nullptr;
@@ -989,6 +1018,15 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     parallel_for(B, nth, [&](int b) { pp[b].rc = prepare(probs[b], pp[b]); });
     for (int b = 0; b < B; b++)
         if (pp[b].rc) return pp[b].rc;
+    if (shard_mode == kShardLocal) {
+        for (int b = 1; b < B; b++)
+            if (pp[b].P != pp[0].P || pp[b].np != pp[0].np) return ORBHIP_ERR_ARG;
+        // every shard factors the SUMMED S: the blocked Cholesky needs the union envelope
+        for (int b = 1; b < B; b++)
+            for (size_t R = 0; R < pp[0].row_first.size(); R++)
+                pp[0].row_first[R] = std::min(pp[0].row_first[R], pp[b].row_first[R]);
+        for (int b = 1; b < B; b++) pp[b].row_first = pp[0].row_first;
+    }
     const double t_prep = now();
     // ---- packed layout: fp64 segments, each contiguous over all problems ----
     //   C  e_chi2 (E)                 downloaded with A in one transfer
@@ -1099,11 +1137,17 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.S = D + sR + p.o_S;
         a.Lsave = D + sR + p.o_L;
         a.lambda = ws->lam.p + b;
+        a.lead = shard_mode == kShardLocal ? (b == 0) : (shard_mode == kShardRccl ? (ws->rank == 0) : 1);
     });
     BAOK(hipMemcpyAsync(D + sA, hd + sA, sizeof(double) * (nA + nU), hipMemcpyHostToDevice, st));
     if (nZ) BAOK(hipMemsetAsync(D + sZ, 0, sizeof(double) * nZ, st));
     BAOK(hipMemcpyAsync(I, hi, ni * sizeof(int), hipMemcpyHostToDevice, st));
     BAOK(hipMemcpyAsync(ws->args.p, ha, B * sizeof(BaArgs), hipMemcpyHostToDevice, st));
+    if (shard_mode == kShardRccl && !pp[0].row_first.empty()) {   // union envelope over the ranks
+        int* rf = const_cast<int*>(ha[0].row_first);
+        if (ncclAllReduce(rf, rf, pp[0].row_first.size(), ncclInt32, ncclMin, ws->comm, st) != ncclSuccess)
+            return ORBHIP_ERR_DEVICE;
+    }
     const double t_pack = now();
     static bool lds_set = false;
     if (!lds_set) {
@@ -1140,6 +1184,31 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             for (int k = 0; k < 5; k++) ws->h_red[5 * v[i] + k] = ws->h_gath[5 * i + k];
         return ORBHIP_OK;
     };
+    // ---- sharded solve: the collective steps (no-ops for independent problems) ----
+    // field: 0 Hpp, 1 S, 2 bs, 3 red; op 0 sum, 1 max
+    auto coll = [&](int field, int off, size_t count, int op) -> int {
+        if (shard_mode == kShardLocal) {
+            hipLaunchKernelGGL(k_ba_shard_reduce, dim3((unsigned)std::min<size_t>(1024, (count + 255) / 256)),
+                               dim3(256), 0, st, dA, B, field, off, count, op);
+        } else if (shard_mode == kShardRccl) {
+            const BaArgs& a0 = ha[0];
+            double* p = (field == 0 ? a0.Hpp : field == 1 ? a0.S : field == 2 ? a0.bs : a0.red) + off;
+            if (ncclAllReduce(p, p, count, ncclDouble, op ? ncclMax : ncclSum, ws->comm, st) != ncclSuccess)
+                return ORBHIP_ERR_DEVICE;
+        }
+        return ORBHIP_OK;
+    };
+    // stop flag: one consistent decision across ranks (all-reduce max) at each iteration
+    auto stop_now = [&]() -> bool {
+        const bool local = stop && *stop;
+        if (shard_mode != kShardRccl) return local;
+        *ws->h_stop = local ? 1 : 0;
+        if (hipMemcpyAsync(ws->dstop.p, ws->h_stop, sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess) return true;
+        if (ncclAllReduce(ws->dstop.p, ws->dstop.p, 1, ncclInt32, ncclMax, ws->comm, st) != ncclSuccess) return true;
+        if (hipMemcpyAsync(ws->h_stop, ws->dstop.p, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess) return true;
+        if (hipStreamSynchronize(st) != hipSuccess) return true;
+        return *ws->h_stop != 0;
+    };
     std::vector<LmState> L(B);
     std::vector<int> all(B);
     for (int b = 0; b < B; b++) all[b] = b;
@@ -1147,6 +1216,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     if (upload_act(all)) return ORBHIP_ERR_DEVICE;
     hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), dim3(256), 0, st, dA, d_act);
     hipLaunchKernelGGL(k_ba_reduce, dim3(B), dim3(1024), 0, st, dA, d_act, 1);
+    if (coll(3, 0, 1, 0)) return ORBHIP_ERR_DEVICE;
     BAOK(hipGetLastError());
     if (read_red(all)) return ORBHIP_ERR_DEVICE;
     for (int b = 0; b < B; b++) {
@@ -1157,8 +1227,9 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     const double dmax = std::numeric_limits<double>::max();
     for (int it = 0; it < maxIt; it++) {
         std::vector<int> act;
+        const bool stop_it = stop_now();
         for (int b = 0; b < B; b++)
-            if (!L[b].done && it < probs[b]->iterations && !(stop && *stop)) act.push_back(b);
+            if (!L[b].done && it < probs[b]->iterations && !stop_it) act.push_back(b);
             else L[b].done = true;
         if (act.empty()) break;
         const unsigned na = (unsigned)act.size();
@@ -1173,8 +1244,10 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         if (upload_act(act)) return ORBHIP_ERR_DEVICE;
         hipLaunchKernelGGL(k_ba_lin_points, dim3(gx(maxM, 256), na), dim3(256), 0, st, dA, d_act);
         hipLaunchKernelGGL(k_ba_lin_poses, dim3(gx(maxNp, 4), na), dim3(256), 0, st, dA, d_act);
+        if (coll(0, 0, (size_t)36 * maxNp, 0)) return ORBHIP_ERR_DEVICE;   // global Hpp on every shard
         if (it == 0) {
             hipLaunchKernelGGL(k_ba_reduce, dim3(na), dim3(1024), 0, st, dA, d_act, 4);
+            if (coll(3, 2, 1, 1)) return ORBHIP_ERR_DEVICE;
             if (read_red(act)) return ORBHIP_ERR_DEVICE;
             for (int b : act) { L[b].lambda = 1e-5 * ws->h_red[5 * b + 2]; L[b].ni = 2; L[b].nBad = 0; }
         }
@@ -1190,6 +1263,9 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             hipLaunchKernelGGL(k_ba_schur_w, dim3(gx(maxE, 256), nt_), dim3(256), 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_schur_blocks, dim3(gx(maxBlk, 4), nt_), dim3(256), 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_schur_b, dim3(gx(maxNp, 4), nt_), dim3(256), 0, st, dA, d_act);
+            if (shard_mode) {   // reduced camera system of all shards
+                if (coll(1, 0, (size_t)pp[0].n * pp[0].n, 0) || coll(2, 0, (size_t)pp[0].n, 0)) return ORBHIP_ERR_DEVICE;
+            }
             if (!any_large) {
                 hipLaunchKernelGGL(k_ba_cholesky, dim3(nt_), dim3(512), chol_lds, st, dA, d_act);
             } else {
@@ -1210,6 +1286,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             hipLaunchKernelGGL(k_ba_update_poses, dim3(gx(maxP, 256), nt_), dim3(256), 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), nt_), dim3(256), 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_reduce, dim3(nt_), dim3(1024), 0, st, dA, d_act, 3);
+            if (coll(3, 0, 2, 0)) return ORBHIP_ERR_DEVICE;
             BAOK(hipGetLastError());
             if (read_red(trial)) return ORBHIP_ERR_DEVICE;
             std::vector<int> pop, next;
@@ -1237,7 +1314,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 s.rho = rho;
                 s.qmax++;
                 s.trials++;
-                if (rho < 0 && s.qmax < 10 && !(stop && *stop)) next.push_back(b);
+                if (rho < 0 && s.qmax < 10 && !(shard_mode != kShardRccl && stop && *stop)) next.push_back(b);
             }
             if (!pop.empty()) {
                 // act slot 2 keeps the pop list away from the next round's upload
@@ -1301,7 +1378,27 @@ int ba_solve(BaWorkspace* ws, const orbhip_ba_problem* prob, orbhip_ba_result* r
              hipStream_t st) {
     const orbhip_ba_problem* pp[1] = {prob};
     orbhip_ba_result* rr[1] = {res};
-    return ba_solve_batch(ws, pp, 1, rr, stop, st);
+    return ba_solve_batch(ws, pp, 1, rr, stop, st, kShardNone);
+}
+
+int ba_comm_init(BaWorkspace* ws, int nranks, int rank, const void* id) {
+    if (nranks < 1 || rank < 0 || rank >= nranks || !id) return ORBHIP_ERR_ARG;
+    if (ws->comm) { (void)ncclCommDestroy(ws->comm); ws->comm = nullptr; }
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    if (ncclCommInitRank(&ws->comm, nranks, uid, rank) != ncclSuccess) { ws->comm = nullptr; return ORBHIP_ERR_DEVICE; }
+    ws->nranks = nranks;
+    ws->rank = rank;
+    BAOK(ws->dstop.ensure(1));
+    if (!ws->h_stop) BAOK(hipHostMalloc((void**)&ws->h_stop, sizeof(int), hipHostMallocDefault));
+    return ORBHIP_OK;
+}
+
+int ba_comm_unique_id(void* id) {
+    ncclUniqueId uid;
+    if (ncclGetUniqueId(&uid) != ncclSuccess) return ORBHIP_ERR_DEVICE;
+    std::memcpy(id, &uid, sizeof(uid));
+    return ORBHIP_OK;
 }
 
 // Diagnostic: factor+solve one SPD system with per-phase cycle stamps (test hook).

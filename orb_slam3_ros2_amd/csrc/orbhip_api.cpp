@@ -617,7 +617,41 @@ int orbhip_ba_solve_batch(orbhip_ctx* c, const orbhip_ba_problem* probs, int B, 
     std::vector<const orbhip_ba_problem*> pp(B);
     std::vector<orbhip_ba_result*> rr(B);
     for (int b = 0; b < B; b++) { pp[b] = probs + b; rr[b] = res + b; }
-    return ba_solve_batch(c->ba, pp.data(), B, rr.data(), stop, c->stream);
+    return ba_solve_batch(c->ba, pp.data(), B, rr.data(), stop, c->stream, kShardNone);
+}
+
+int orbhip_comm_unique_id(uint8_t* id) {
+    if (!id) return ORBHIP_ERR_ARG;
+    return ba_comm_unique_id(id);
+}
+
+int orbhip_comm_init(orbhip_ctx* c, int nranks, int rank, const uint8_t* id) {
+    if (!c || !id) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    if (!c->ba) c->ba = ba_create();
+    if (!c->ba) return ORBHIP_ERR_DEVICE;
+    return ba_comm_init(c->ba, nranks, rank, id);
+}
+
+int orbhip_ba_solve_sharded(orbhip_ctx* c, const orbhip_ba_problem* shard, orbhip_ba_result* res,
+                            const volatile int* stop) {
+    if (!c || !shard || !res || !c->ba) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    const orbhip_ba_problem* pp[1] = {shard};
+    orbhip_ba_result* rr[1] = {res};
+    return ba_solve_batch(c->ba, pp, 1, rr, stop, c->stream, kShardRccl);
+}
+
+int orbhip_ba_solve_shards_local(orbhip_ctx* c, const orbhip_ba_problem* shards, int nshards, orbhip_ba_result* res,
+                                 const volatile int* stop) {
+    if (!c || !shards || !res || nshards <= 0) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    if (!c->ba) c->ba = ba_create();
+    if (!c->ba) return ORBHIP_ERR_DEVICE;
+    std::vector<const orbhip_ba_problem*> pp(nshards);
+    std::vector<orbhip_ba_result*> rr(nshards);
+    for (int b = 0; b < nshards; b++) { pp[b] = shards + b; rr[b] = res + b; }
+    return ba_solve_batch(c->ba, pp.data(), nshards, rr.data(), stop, c->stream, kShardLocal);
 }
 
 // ---- test hooks (not part of the reference surface) ----

@@ -10,7 +10,13 @@ BaWorkspace* ba_create();
 void ba_destroy(BaWorkspace* ws);
 int ba_solve(BaWorkspace* ws, const orbhip_ba_problem* prob, orbhip_ba_result* res, const volatile int* stop,
              hipStream_t st);
+// shard_mode: kShardNone = B independent problems; kShardLocal = B shards of ONE problem in this
+// process (device-side sum across the batch); kShardRccl = this rank's shard (B == 1), the
+// sums are RCCL all-reduces over the communicator of ba_comm_init.
+constexpr int kShardNone = 0, kShardLocal = 1, kShardRccl = 2;
 int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B, orbhip_ba_result* const* res,
-                   const volatile int* stop, hipStream_t st);
+                   const volatile int* stop, hipStream_t st, int shard_mode);
+int ba_comm_init(BaWorkspace* ws, int nranks, int rank, const void* id);
+int ba_comm_unique_id(void* id);
 int ba_test_cholesky(const double* A, const double* b, double* x, int n, unsigned long long* phases5, float* ms);
 }  // namespace orbhip

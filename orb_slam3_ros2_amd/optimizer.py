@@ -109,6 +109,54 @@ class Optimizer:
                                                                               r.iterations_done, r.lm_trials)
         return outs
 
+    # ---- sharded BundleAdjustment ----
+    def _results_for(self, ps):
+        outs, cres = [], (BAResultC * len(ps))()
+        for i, p in enumerate(ps):
+            P, M, E = p.pose_q.shape[0], p.points.shape[0], p.edge_pose.shape[0]
+            o = BAResult(np.zeros((P, 4), np.float32), np.zeros((P, 3), np.float32), np.zeros((M, 3), np.float32),
+                         np.zeros(E, np.float32), np.zeros(E, np.uint8), 0.0, 0.0, 0, 0)
+            outs.append(o)
+            cres[i] = BAResultC(ptr(o.pose_q), ptr(o.pose_t), ptr(o.points), ptr(o.edge_chi2), ptr(o.edge_depth_ok),
+                                0.0, 0.0, 0, 0)
+        return outs, cres
+
+    @staticmethod
+    def _fill(outs, cres):
+        for o, r in zip(outs, cres):
+            o.initial_chi2, o.final_chi2, o.iterations_done, o.lm_trials = (r.initial_chi2, r.final_chi2,
+                                                                              r.iterations_done, r.lm_trials)
+        return outs
+
+    def solve_shards_local(self, shards, stop_flag: ctypes.c_int | None = None):
+        """All shards of one problem in this process, summed on the device (orbhip_ba_solve_shards_local)."""
+        ps = [p.normalized() for p in shards]
+        outs, cres = self._results_for(ps)
+        cprobs = (BAProblemC * len(ps))(*[p.to_c() for p in ps])
+        sf = ctypes.addressof(stop_flag) if stop_flag is not None else None
+        check(lib().orbhip_ba_solve_shards_local(self.ctx.handle, cprobs, len(ps), cres, sf),
+              "orbhip_ba_solve_shards_local")
+        return self._fill(outs, cres)
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = (ctypes.c_uint8 * 128)()
+        check(lib().orbhip_comm_unique_id(buf), "orbhip_comm_unique_id")
+        return bytes(buf)
+
+    def comm_init(self, nranks: int, rank: int, unique_id: bytes):
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(unique_id)
+        check(lib().orbhip_comm_init(self.ctx.handle, int(nranks), int(rank), buf), "orbhip_comm_init")
+
+    def solve_sharded(self, shard: BAProblem, stop_flag: ctypes.c_int | None = None) -> BAResult:
+        """This rank's shard of a problem solved jointly over RCCL (after comm_init)."""
+        p = shard.normalized()
+        outs, cres = self._results_for([p])
+        pc = p.to_c()
+        sf = ctypes.addressof(stop_flag) if stop_flag is not None else None
+        check(lib().orbhip_ba_solve_sharded(self.ctx.handle, ctypes.byref(pc), cres, sf), "orbhip_ba_solve_sharded")
+        return self._fill(outs, cres)[0]
+
     def LocalBundleAdjustment(self, prob: BAProblem, stop_flag=None) -> BAResult:
         return self.solve(prob, stop_flag)
 
