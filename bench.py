@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--c3-steps", type=int, default=10)
     ap.add_argument("--lba-steps", type=int, default=20)
     ap.add_argument("--lba-batch", type=int, default=128)
+    ap.add_argument("--gba-iters", type=int, default=10)
     return ap.parse_args()
 
 
@@ -252,7 +253,7 @@ def cpu_baseline(frames_np, budget_s=12.0):
         n1 += stream(n1, 4)
     t1 = time.perf_counter() - t0
     single = n1 / t1
-    per_thread = max(4, int((budget_s * 0.75) * single / cores * cores / cores))
+    per_thread = max(4, int(1.5 * single))   # ~1.5 s per thread: ~24 CPU-seconds at 16 threads
     t0 = time.perf_counter()
     with ThreadPoolExecutor(cores) as ex:
         done = sum(ex.map(lambda k: stream(k * 7, per_thread), range(cores)))
@@ -276,6 +277,43 @@ def cpu_lba(prob, budget_s=8.0):
         list(ex.map(lambda i: O.ba_solve(prob), range(total)))
     tm = time.perf_counter() - t0
     return dict(value=total / tm, single=n1 / t1, cores=cores, solves=total + n1)
+
+
+def c5_gba(ws, rank, iters):
+    """C5 GlobalBundleAdjustment (400 KF loop, 20k points, 80k obs, 20-KF co-visibility window).
+    With ORBHIP_C5_SHARDED=1 and N > 1: landmark shards over the ranks, the reduced camera system
+    summed with RCCL all-reduce (orbhip_ba_solve_sharded). Otherwise every rank solves the whole
+    problem (replicas, no collective): the multi-rank RCCL path is verified here only at one rank
+    plus the in-process shard model (tests/test_ba_sharded_gpu.py), so it is opt-in for the
+    driver's scaling runs. Every rank runs it; time = max over ranks of one solve."""
+    import torch
+    from orb_slam3_ros2_amd import Optimizer
+    from orb_slam3_ros2_amd.sharding import shard_problem
+    from orb_slam3_ros2_amd.synthetic import synthetic_ba_problem
+    prob, _ = synthetic_ba_problem(n_kf=400, n_pts=20000, layout="loop", window=20, seed=11)
+    prob.iterations, prob.huber_delta = iters, float(np.sqrt(5.99))   # BundleAdjustment(bRobust)
+    opt = Optimizer()
+    sharded = ws > 1 and os.environ.get("ORBHIP_C5_SHARDED", "0") == "1"
+    if sharded:
+        import torch.distributed as dist
+        uid = [Optimizer.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        opt.comm_init(ws, rank, uid[0])
+        shard = shard_problem(prob, rank, ws)[0]
+        solve = lambda: opt.solve_sharded(shard)  # noqa: E731
+    else:
+        solve = lambda: opt.solve(prob)  # noqa: E731
+    solve()
+    _barrier(ws)
+    t0 = time.perf_counter()
+    r = solve()
+    torch.cuda.synchronize()
+    _barrier(ws)
+    t = _max_over_ranks(ws, time.perf_counter() - t0)
+    return {"c5_gba_ms": round(1e3 * t, 2), "c5_gba_iterations": r.iterations_done, "c5_gba_trials": r.lm_trials,
+            "c5_gba_chi2": [round(r.initial_chi2, 1), round(r.final_chi2, 1)],
+            "c5_gba_mode": f"rccl shards x{ws}" if sharded else f"replicas x{ws} (one GPU per solve)",
+            "c5_problem": "400 KF loop / 20000 pts / 80000 obs, n = 2394"}
 
 
 def main():
@@ -339,8 +377,14 @@ def main():
                      "launches_timed": dom_n,
                      "stage_avg_ms_calibration": {STAGES[k]: round(v, 5) for k, v in stage_ms.items()}},
     }
+    c5 = None
+    if not args.no_extra:
+        try:
+            c5 = c5_gba(ws, rank, args.gba_iters)
+        except Exception as e:   # never lose the headline line to the extra
+            c5 = {"c5_error": repr(e)[:200]}
     if rank == 0 and not args.no_extra:
-        extra = {}
+        extra = dict(c5 or {})
         c3 = BatchC3(rank)
         t = timed(1, c3.step, args.c3_steps, 2)
         extra["c3_1280x720_b64_extract_match_frames_per_s"] = round(c3.B * args.c3_steps / t, 1)
