@@ -185,6 +185,37 @@ int orbhip_ba_solve(orbhip_ctx* ctx, const orbhip_ba_problem* prob, orbhip_ba_re
 int orbhip_ba_solve_batch(orbhip_ctx* ctx, const orbhip_ba_problem* probs, int B, orbhip_ba_result* res,
                           const volatile int* stop_flag);
 
+/* ---- bag of words -----------------------------------------
+ * DBoW2 vocabulary in the ORBvoc.txt node order (Thirdparty/DBoW2 TemplatedVocabulary):
+ * node 0 = root, node i (i >= 1) = line i of the text file with (parent, is_leaf, 32-byte
+ * descriptor, weight); children keep file order; word ids follow leaf order.
+ *   orbhip_vocab_load_text   TemplatedVocabulary::loadFromTextFile ("k L scoring weighting" header)
+ *   orbhip_bow_transform     per-descriptor transform(feature, word, weight, &node, levelsup)
+ *                            (U:src/Frame.cc::ComputeBoW: levelsup 4); the caller builds the
+ *                            BowVector (weights summed per word, L1-normalised) and FeatureVector
+ *                            (node -> ascending feature indices, weight > 0 only)
+ *   orbhip_search_bow        U:src/ORBmatcher.cc::SearchByBoW(KeyFrame*, Frame&, vpMapPointMatches):
+ *                            match[f] = KF feature index matched to frame feature f, or -1 (the
+ *                            adapter maps it to the KF's MapPoint*); kf_valid[i] = the KF feature
+ *                            has a good map point. Returns nmatches. n <= 2048 per side. */
+typedef struct orbhip_vocab orbhip_vocab;
+int orbhip_vocab_create(orbhip_ctx* ctx, int k, int L, int scoring, int weighting, int n_nodes,
+                        const int32_t* parent, const uint8_t* is_leaf, const uint8_t* desc32,
+                        const double* weight, orbhip_vocab** out);
+int orbhip_vocab_load_text(orbhip_ctx* ctx, const char* path, orbhip_vocab** out);
+int orbhip_vocab_destroy(orbhip_vocab* vocab);
+int orbhip_vocab_info(const orbhip_vocab* vocab, int32_t* k, int32_t* L, int32_t* n_nodes, int32_t* n_words);
+int orbhip_bow_transform(orbhip_ctx* ctx, const orbhip_vocab* vocab, const uint8_t* desc32, int n, int levelsup,
+                         int32_t* word_id, int32_t* node_id, double* weight);
+/* device form over extractor outputs: B frames, descriptors at f*cap, counts d_n[f]; outputs at f*cap */
+int orbhip_bow_transform_device(orbhip_ctx* ctx, const orbhip_vocab* vocab, const uint8_t* d_desc,
+                                const int32_t* d_n, int B, int cap, int levelsup, int32_t* d_word,
+                                int32_t* d_node, double* d_weight, void* stream);
+int orbhip_search_bow(orbhip_ctx* ctx, const uint8_t* kf_desc, const float* kf_angle, const int32_t* kf_node,
+                      const double* kf_weight, const uint8_t* kf_valid, int nkf, const uint8_t* f_desc,
+                      const float* f_angle, const int32_t* f_node, const double* f_weight, int nf,
+                      float ratio, int check_orientation, int th_low, int32_t* match);
+
 /* ---- multi-GPU BundleAdjustment (SURVEY.md §8e, C5 GlobalBundleAdjustment) --------
  * One process per GPU. Landmarks (with their edges) are partitioned across ranks; every rank
  * holds all poses. Per LM trial the ranks sum their Schur contributions (the reduced camera

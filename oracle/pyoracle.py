@@ -50,6 +50,12 @@ def lib():
         L.orc_ba_solve.argtypes = [c_int, c_int, c_int, _f32p, _f32p, _u8p, _f32p, _i32p, _i32p, _f32p, _i32p,
                                    _f32p, c_float, c_float, c_float, c_float, c_float, c_int, c_int, _f32p, _f32p,
                                    _f32p, _f32p, _u8p, _f64p]
+        _f64 = _f64p
+        L.orc_bow_transform.argtypes = [_u8p, _i32p, _i32p, _i32p, _i32p, _f64, c_int, _u8p, c_int, c_int, _i32p,
+                                        _i32p, _f64]
+        L.orc_bow_vector.argtypes = [_i32p, _f64, c_int, _i32p, _f64]
+        L.orc_search_bow.argtypes = [_u8p, _f32p, _i32p, _u8p, c_int, _u8p, _f32p, _i32p, c_int, c_float, c_int,
+                                     c_int, _i32p]
         L.orc_bgr2gray.argtypes = [_u8p, c_int, c_int, c_int, _u8p, c_int]
         L.orc_glibc_sincosf_range.argtypes = [ctypes.c_uint32, ctypes.c_uint32, _f32p, _f32p]
         _lib = L
@@ -142,6 +148,35 @@ def bgr2gray(bgr: np.ndarray) -> np.ndarray:
     out = np.empty((h, w), np.uint8)
     lib().orc_bgr2gray(bgr, w, h, 3 * w, out, w)
     return out
+
+
+def bow_transform(vocab, feats, levelsup=4):
+    """Per-feature DBoW2 transform: (word ids, node ids at L - levelsup, weights)."""
+    first, nch, children, word = vocab.csr()
+    f = np.ascontiguousarray(feats, np.uint8).reshape(-1, 32)
+    n = f.shape[0]
+    ow = np.zeros(n, np.int32); on = np.zeros(n, np.int32); ov = np.zeros(n, np.float64)
+    lib().orc_bow_transform(np.ascontiguousarray(vocab.desc), first, nch, children, word,
+                            np.ascontiguousarray(vocab.weight, np.float64), vocab.L, f, n, levelsup, ow, on, ov)
+    return ow, on, ov
+
+
+def bow_vector(word, weight):
+    word = np.ascontiguousarray(word, np.int32); weight = np.ascontiguousarray(weight, np.float64)
+    ow = np.zeros(len(word), np.int32); ov = np.zeros(len(word), np.float64)
+    k = lib().orc_bow_vector(word, weight, len(word), ow, ov)
+    return ow[:k].copy(), ov[:k].copy()
+
+
+def search_bow(kf_desc, kf_angle, kf_node, kf_valid, f_desc, f_angle, f_node, ratio=0.7, check_orientation=True,
+               th_low=50):
+    c = np.ascontiguousarray
+    nkf, nf = len(kf_node), len(f_node)
+    m = np.zeros(nf, np.int32)
+    n = lib().orc_search_bow(c(kf_desc, np.uint8), c(kf_angle, np.float32), c(kf_node, np.int32),
+                             c(kf_valid, np.uint8), nkf, c(f_desc, np.uint8), c(f_angle, np.float32),
+                             c(f_node, np.int32), nf, ratio, int(check_orientation), th_low, m)
+    return n, m
 
 
 def glibc_sincosf_range(lo_bits: int, hi_bits: int):

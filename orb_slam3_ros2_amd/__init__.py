@@ -8,6 +8,8 @@ Host-side mirror of the reference's hot-path interfaces over th
   ORBmatcher.DescriptorDistance(a, b)                                       U:src/ORBmatcher.cc
   ORBmatcher(nnratio, checkOri).match_bf(...)                               (a12 rule)
   Optimizer.LocalBundleAdjustment(problem)                                  U:src/Optimizer.cc
+  ORBVocabulary(vocab).transform(desc)  (DBoW2 TemplatedVocabulary)         U:src/Frame.cc::ComputeBoW
+  ORBmatcher.SearchByBoW(...)                                               U:src/ORBmatcher.cc
 
 The HIP library is the only compute path: importing this package on a box without the
 built extension, or calling it without a GPU, raises — there is no CPU fallback.
@@ -18,6 +20,7 @@ from ._lib import OrbHipError, lib, library_path  # noqa: F401
 from .extractor import KeyPoint, ORBextractor  # noqa: F401
 from .matcher import ORBmatcher  # noqa: F401
 from .optimizer import BAProblem, BAResult, Optimizer  # noqa: F401
+from .bow import ORBVocabulary  # noqa: F401
 
-__all__ = ["ORBextractor", "KeyPoint", "ORBmatcher", "Optimizer", "BAProblem", "BAResult", "OrbHipError",
+__all__ = ["ORBextractor", "KeyPoint", "ORBmatcher", "Optimizer", "BAProblem", "BAResult", "ORBVocabulary", "OrbHipError",
            "lib", "library_path"]

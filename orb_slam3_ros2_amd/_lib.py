@@ -60,7 +60,9 @@ EXPORTED = ["orbhip_abi_version", "orbhip_create", "orbhip_destroy", "orbhip_lev
             "orbhip_extract", "orbhip_extract_batch_device", "orbhip_descriptor_distance", "orbhip_match_bf",
             "orbhip_match_pairs_device", "orbhip_match_frames_device", "orbhip_profile_stage",
             "orbhip_profile_collect", "orbhip_ba_solve", "orbhip_ba_solve_batch", "orbhip_bgr_to_gray_device",
-            "orbhip_comm_unique_id", "orbhip_comm_init", "orbhip_ba_solve_sharded", "orbhip_ba_solve_shards_local"]
+            "orbhip_comm_unique_id", "orbhip_comm_init", "orbhip_ba_solve_sharded", "orbhip_ba_solve_shards_local",
+            "orbhip_vocab_create", "orbhip_vocab_load_text", "orbhip_vocab_destroy", "orbhip_vocab_info",
+            "orbhip_bow_transform", "orbhip_bow_transform_device", "orbhip_search_bow"]
 
 
 def lib():
@@ -93,6 +95,13 @@ def lib():
     L.orbhip_match_bf.argtypes = [vp, vp, vp, i32, vp, vp, i32, i32, f32, i32, vp, vp, vp]
     L.orbhip_match_pairs_device.argtypes = [vp, vp, vp, vp, i32, i32, i32, f32, i32, vp, vp, vp, vp, vp]
     L.orbhip_match_frames_device.argtypes = [vp, vp, vp, vp, vp, vp, vp, i32, i32, f32, i32, vp, vp, vp, vp, vp]
+    L.orbhip_vocab_create.argtypes = [vp, i32, i32, i32, i32, i32, vp, vp, vp, vp, ctypes.POINTER(vp)]
+    L.orbhip_vocab_load_text.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(vp)]
+    L.orbhip_vocab_destroy.argtypes = [vp]
+    L.orbhip_vocab_info.argtypes = [vp, vp, vp, vp, vp]
+    L.orbhip_bow_transform.argtypes = [vp, vp, vp, i32, i32, vp, vp, vp]
+    L.orbhip_bow_transform_device.argtypes = [vp, vp, vp, vp, i32, i32, i32, vp, vp, vp, vp]
+    L.orbhip_search_bow.argtypes = [vp, vp, vp, vp, vp, vp, i32, vp, vp, vp, vp, i32, f32, i32, i32, vp]
     L.orbhip_comm_unique_id.argtypes = [vp]
     L.orbhip_comm_init.argtypes = [vp, i32, i32, vp]
     L.orbhip_ba_solve_sharded.argtypes = [vp, ctypes.POINTER(BAProblemC), ctypes.POINTER(BAResultC), vp]

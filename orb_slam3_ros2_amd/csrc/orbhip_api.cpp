@@ -87,6 +87,8 @@ struct orbhip_ctx {
     DevBuf<uint16_t> d_nscratch;
     DevBuf<int> d_cand_cnt, d_lvl_cnt, d_lvl_nlap, d_err;
     DevBuf<uint64_t> d_mpart;   // matcher chunk partials (match_part_entries)
+    DevBuf<double> d_bw;        // bag-of-words weights (host transform)
+    DevBuf<uint8_t> d_bow_stage;   // SearchByBoW host-call staging
     DevBuf<LevelKp> d_lvl_kp;
     DevBuf<orbhip_kp> d_kps;
     DevBuf<uint8_t> d_desc;
@@ -652,6 +654,193 @@ int orbhip_ba_solve_shards_local(orbhip_ctx* c, const orbhip_ba_problem* shards,
     std::vector<orbhip_ba_result*> rr(nshards);
     for (int b = 0; b < nshards; b++) { pp[b] = shards + b; rr[b] = res + b; }
     return ba_solve_batch(c->ba, pp.data(), nshards, rr.data(), stop, c->stream, kShardLocal);
+}
+
+// ---- bag of words (a13/a14) ----
+}  // extern "C"
+
+struct orbhip_vocab {
+    int device = 0;
+    int k = 0, L = 0, scoring = 0, weighting = 0, n_nodes = 0;
+    DevBuf<uint8_t> desc;
+    DevBuf<int> first_child, n_child, children, word_id;
+    DevBuf<double> weight;
+    VocabView view() const {
+        VocabView v;
+        v.desc = (const uint4*)desc.p;
+        v.first_child = first_child.p; v.n_child = n_child.p; v.children = children.p;
+        v.word_id = word_id.p; v.weight = weight.p; v.L = L;
+        return v;
+    }
+};
+
+static int vocab_build(orbhip_ctx* c, int k, int L, int scoring, int weighting, int N, const int32_t* parent,
+                       const uint8_t* is_leaf, const uint8_t* desc32, const double* weight, orbhip_vocab** out) {
+    if (!c || !out || N < 2 || !parent || !is_leaf || !desc32 || !weight || L < 1) return ORBHIP_ERR_ARG;
+    for (int i = 1; i < N; i++)
+        if (parent[i] < 0 || parent[i] >= i) return ORBHIP_ERR_ARG;   // file order: parents precede children
+    std::vector<int> nch(N, 0), first(N, 0), children(N > 1 ? N - 1 : 1), fill(N), word(N, -1);
+    for (int i = 1; i < N; i++) nch[parent[i]]++;
+    for (int i = 1; i < N; i++) first[i] = first[i - 1] + nch[i - 1];
+    fill = first;
+    for (int i = 1; i < N; i++) children[fill[parent[i]]++] = i;   // file order within a parent
+    int nw = 0;
+    for (int i = 1; i < N; i++) {
+        if (is_leaf[i] && nch[i] > 0) return ORBHIP_ERR_ARG;
+        if (!is_leaf[i] && nch[i] == 0) return ORBHIP_ERR_ARG;
+        if (is_leaf[i]) word[i] = nw++;
+    }
+    if (nch[0] == 0) return ORBHIP_ERR_ARG;
+    std::unique_ptr<orbhip_vocab> v(new orbhip_vocab());
+    v->device = c->device; v->k = k; v->L = L; v->scoring = scoring; v->weighting = weighting; v->n_nodes = N;
+    HIPOK(hipSetDevice(c->device));
+    HIPOK(v->desc.ensure((size_t)N * 32));
+    HIPOK(v->first_child.ensure(N)); HIPOK(v->n_child.ensure(N)); HIPOK(v->children.ensure(children.size()));
+    HIPOK(v->word_id.ensure(N)); HIPOK(v->weight.ensure(N));
+    HIPOK(hipMemcpy(v->desc.p, desc32, (size_t)N * 32, hipMemcpyHostToDevice));
+    HIPOK(hipMemcpy(v->first_child.p, first.data(), N * sizeof(int), hipMemcpyHostToDevice));
+    HIPOK(hipMemcpy(v->n_child.p, nch.data(), N * sizeof(int), hipMemcpyHostToDevice));
+    HIPOK(hipMemcpy(v->children.p, children.data(), children.size() * sizeof(int), hipMemcpyHostToDevice));
+    HIPOK(hipMemcpy(v->word_id.p, word.data(), N * sizeof(int), hipMemcpyHostToDevice));
+    HIPOK(hipMemcpy(v->weight.p, weight, N * sizeof(double), hipMemcpyHostToDevice));
+    *out = v.release();
+    return ORBHIP_OK;
+}
+
+extern "C" {
+
+int orbhip_vocab_create(orbhip_ctx* c, int k, int L, int scoring, int weighting, int n_nodes, const int32_t* parent,
+                        const uint8_t* is_leaf, const uint8_t* desc32, const double* weight, orbhip_vocab** out) {
+    return vocab_build(c, k, L, scoring, weighting, n_nodes, parent, is_leaf, desc32, weight, out);
+}
+
+int orbhip_vocab_load_text(orbhip_ctx* c, const char* path, orbhip_vocab** out) {
+    if (!c || !path || !out) return ORBHIP_ERR_ARG;
+    FILE* f = std::fopen(path, "r");
+    if (!f) return ORBHIP_ERR_ARG;
+    int k = 0, L = 0, sc = 0, wt = 0;
+    if (std::fscanf(f, "%d %d %d %d", &k, &L, &sc, &wt) != 4) { std::fclose(f); return ORBHIP_ERR_ARG; }
+    std::vector<int32_t> parent(1, -1);
+    std::vector<uint8_t> leaf(1, 0), desc(32, 0);
+    std::vector<double> weight(1, 0.0);
+    int p, il;
+    while (std::fscanf(f, "%d %d", &p, &il) == 2) {
+        unsigned char d[32];
+        for (int j = 0; j < 32; j++) {
+            int v;
+            if (std::fscanf(f, "%d", &v) != 1) { std::fclose(f); return ORBHIP_ERR_ARG; }
+            d[j] = (unsigned char)v;
+        }
+        double w;
+        if (std::fscanf(f, "%lf", &w) != 1) { std::fclose(f); return ORBHIP_ERR_ARG; }
+        parent.push_back(p); leaf.push_back((uint8_t)il); weight.push_back(w);
+        desc.insert(desc.end(), d, d + 32);
+    }
+    std::fclose(f);
+    return vocab_build(c, k, L, sc, wt, (int)parent.size(), parent.data(), leaf.data(), desc.data(), weight.data(), out);
+}
+
+int orbhip_vocab_destroy(orbhip_vocab* v) {
+    if (!v) return ORBHIP_ERR_ARG;
+    (void)hipSetDevice(v->device);
+    delete v;
+    return ORBHIP_OK;
+}
+
+int orbhip_vocab_info(const orbhip_vocab* v, int32_t* k, int32_t* L, int32_t* n_nodes, int32_t* n_words) {
+    if (!v) return ORBHIP_ERR_ARG;
+    if (k) *k = v->k;
+    if (L) *L = v->L;
+    if (n_nodes) *n_nodes = v->n_nodes;
+    if (n_words) {
+        int nw = 0;
+        std::vector<int> w(v->n_nodes);
+        if (hipMemcpy(w.data(), v->word_id.p, v->n_nodes * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+            return ORBHIP_ERR_DEVICE;
+        for (int x : w) nw += x >= 0;
+        *n_words = nw;
+    }
+    return ORBHIP_OK;
+}
+
+int orbhip_bow_transform(orbhip_ctx* c, const orbhip_vocab* v, const uint8_t* desc, int n, int levelsup,
+                         int32_t* word, int32_t* node, double* weight) {
+    if (!c || !v || n < 0 || (n && (!desc || !word || !node || !weight))) return ORBHIP_ERR_ARG;
+    if (n == 0) return ORBHIP_OK;
+    HIPOK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    HIPOK(c->d_mq.ensure((size_t)n * 32));
+    HIPOK(c->d_mm.ensure(n)); HIPOK(c->d_mb.ensure(n)); HIPOK(c->d_bw.ensure(n));
+    HIPOK(hipMemcpyAsync(c->d_mq.p, desc, (size_t)n * 32, hipMemcpyHostToDevice, st));
+    (void)hipGetLastError();
+    launch_bow_transform(v->view(), c->d_mq.p, nullptr, n, 1, n, levelsup, c->d_mm.p, c->d_mb.p, c->d_bw.p, st);
+    HIPOK(hipGetLastError());
+    HIPOK(hipMemcpyAsync(word, c->d_mm.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIPOK(hipMemcpyAsync(node, c->d_mb.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIPOK(hipMemcpyAsync(weight, c->d_bw.p, (size_t)n * 8, hipMemcpyDeviceToHost, st));
+    HIPOK(hipStreamSynchronize(st));
+    return ORBHIP_OK;
+}
+
+int orbhip_bow_transform_device(orbhip_ctx* c, const orbhip_vocab* v, const uint8_t* d_desc, const int32_t* d_n,
+                                int B, int cap, int levelsup, int32_t* d_word, int32_t* d_node, double* d_weight,
+                                void* stream) {
+    if (!c || !v || !d_desc || !d_n || B <= 0 || cap <= 0 || !d_word || !d_node || !d_weight) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    (void)hipGetLastError();
+    launch_bow_transform(v->view(), d_desc, d_n, 0, B, cap, levelsup, d_word, d_node, d_weight, (hipStream_t)stream);
+    HIPOK(hipGetLastError());
+    return ORBHIP_OK;
+}
+
+int orbhip_search_bow(orbhip_ctx* c, const uint8_t* kf_desc, const float* kf_angle, const int32_t* kf_node,
+                      const double* kf_weight, const uint8_t* kf_valid, int nkf, const uint8_t* f_desc,
+                      const float* f_angle, const int32_t* f_node, const double* f_weight, int nf, float ratio,
+                      int check_orientation, int th_low, int32_t* match) {
+    if (!c || nkf < 0 || nf < 0 || (nf && !match)) return ORBHIP_ERR_ARG;
+    if (nkf > kBowMax || nf > kBowMax) return ORBHIP_ERR_UNSUPPORTED;
+    if (nf == 0) return 0;
+    for (int i = 0; i < nf; i++) match[i] = -1;
+    if (nkf == 0) return 0;
+    if (!kf_desc || !kf_angle || !kf_node || !kf_weight || !kf_valid || !f_desc || !f_angle || !f_node || !f_weight)
+        return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    hipStream_t st = c->stream;
+    static bool lds_ok = false;
+    if (!lds_ok) {
+        if (!search_bow_set_lds_limit()) return ORBHIP_ERR_DEVICE;
+        lds_ok = true;
+    }
+    // one staging block: [kf desc | f desc | kf angle | f angle | kf node | f node | kf w | f w | valid | match, n]
+    const size_t bytes = (size_t)(nkf + nf) * 32 + (size_t)(nkf + nf) * (4 + 4 + 8) + nkf + (size_t)nf * 4 + 64;
+    HIPOK(c->d_bow_stage.ensure(bytes + 64));
+    uint8_t* base = c->d_bow_stage.p;
+    size_t off = 0;
+    auto place = [&](const void* src, size_t n_) -> uint8_t* {
+        off = (off + 15) & ~size_t(15);
+        uint8_t* d = base + off;
+        if (src && n_) (void)hipMemcpyAsync(d, src, n_, hipMemcpyHostToDevice, st);
+        off += n_;
+        return d;
+    };
+    BowSide K, F;
+    K.desc = place(kf_desc, (size_t)nkf * 32); F.desc = place(f_desc, (size_t)nf * 32);
+    K.angle = (const float*)place(kf_angle, (size_t)nkf * 4); F.angle = (const float*)place(f_angle, (size_t)nf * 4);
+    K.angle_stride = F.angle_stride = 1;
+    K.node = (const int32_t*)place(kf_node, (size_t)nkf * 4); F.node = (const int32_t*)place(f_node, (size_t)nf * 4);
+    K.weight = (const double*)place(kf_weight, (size_t)nkf * 8); F.weight = (const double*)place(f_weight, (size_t)nf * 8);
+    K.valid = place(kf_valid, nkf); F.valid = nullptr;
+    K.n = nkf; F.n = nf;
+    int32_t* d_match = (int32_t*)place(nullptr, (size_t)nf * 4);
+    int32_t* d_nm = (int32_t*)place(nullptr, 4);
+    (void)hipGetLastError();
+    launch_search_bow(K, F, ratio, check_orientation, th_low, d_match, d_nm, st);
+    HIPOK(hipGetLastError());
+    int nm = 0;
+    HIPOK(hipMemcpyAsync(match, d_match, (size_t)nf * 4, hipMemcpyDeviceToHost, st));
+    HIPOK(hipMemcpyAsync(&nm, d_nm, 4, hipMemcpyDeviceToHost, st));
+    HIPOK(hipStreamSynchronize(st));
+    return nm;
 }
 
 // ---- test hooks (not part of the reference surface) ----

@@ -62,6 +62,33 @@ void launch_match_bf(const uint8_t* q, const float* qa, int nq, const uint8_t* t
                      int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best,
                      int32_t* second, int32_t* nmatch, void* part, hipStream_t st);
 
+// ---- bag of words ----
+constexpr int kBowMax = 2048;   // features per frame in SearchByBoW (LDS-resident FeatureVectors)
+struct VocabView {
+    const uint4* desc;          // n_nodes x 2 uint4
+    const int* first_child;     // CSR, children in file order
+    const int* n_child;
+    const int* children;
+    const int* word_id;         // -1 for internal nodes
+    const double* weight;
+    int L;
+};
+struct BowSide {
+    const uint8_t* desc;        // n x 32
+    const float* angle;         // keypoint angles, angle_stride floats apart
+    int angle_stride;
+    const int32_t* node;        // FeatureVector node (transform output)
+    const double* weight;       // word weight (FeatureVector holds weight > 0 only)
+    const uint8_t* valid;       // KF side: feature has a good map point (null on the frame side)
+    int n;
+};
+void launch_bow_transform(const VocabView& V, const uint8_t* desc, const int32_t* n_arr, int n_fixed, int B, int cap,
+                          int levelsup, int32_t* word, int32_t* node, double* weight, hipStream_t st);
+size_t search_bow_lds_bytes();
+bool search_bow_set_lds_limit();
+void launch_search_bow(const BowSide& K, const BowSide& F, float ratio, int check_orientation, int th_low,
+                       int32_t* match, int32_t* nmatch, hipStream_t st);
+
 // ---- ingest ----
 void launch_bgr2gray(const uint8_t* src, int B, int w, int h, int sstride, int64_t sfstride, uint8_t* dst, int dstride,
                      int64_t dfstride, hipStream_t st);

@@ -54,3 +54,24 @@ class ORBmatcher:
                                               ctypes.c_float(self.mfNNratio), int(self.mbCheckOrientation),
                                               ptr(match), ptr(best), ptr(second), ptr(nmatch), st),
               "orbhip_match_pairs_device")
+
+    def SearchByBoW(self, kf_desc, kf_angle, kf_node, kf_weight, kf_valid, f_desc, f_angle, f_node, f_weight,
+                    th_low: int | None = None):
+        """U:src/ORBmatcher.cc::SearchByBoW(KeyFrame*, Frame&, vpMapPointMatches) on the GPU.
+        node / weight come from ORBVocabulary.transform_features (FeatureVector = weight > 0);
+        kf_valid[i]: the KF feature has a good map point. Returns (nmatches, match[nf]) with
+        match[f] = KF feature index (its MapPoint in the reference) or -1."""
+        c = np.ascontiguousarray
+        kd, fd = c(kf_desc, np.uint8).reshape(-1, 32), c(f_desc, np.uint8).reshape(-1, 32)
+        ka, fa = c(kf_angle, np.float32), c(f_angle, np.float32)
+        kn, fn = c(kf_node, np.int32), c(f_node, np.int32)
+        kw, fw = c(kf_weight, np.float64), c(f_weight, np.float64)
+        kv = c(kf_valid, np.uint8)
+        nkf, nf = kd.shape[0], fd.shape[0]
+        m = np.full(nf, -1, np.int32)
+        th = self.TH_LOW if th_low is None else int(th_low)
+        n = check(lib().orbhip_search_bow(self.ctx.handle, ptr(kd), ptr(ka), ptr(kn), ptr(kw), ptr(kv), nkf, ptr(fd),
+                                          ptr(fa), ptr(fn), ptr(fw), nf, ctypes.c_float(self.mfNNratio),
+                                          int(self.mbCheckOrientation), th, ptr(m)), "orbhip_search_bow")
+        return n, m
+
