@@ -1,0 +1,45 @@
+// Per-problem argument record of the batched bundle-adjustment kernels (ba_solver.hip) and the
+// register-resident Cholesky (ba_chol_reg.hip). Device pointers into the packed workspace.
+#pragma once
+
+namespace orbhip {
+
+struct BaArgs {
+    int P, M, E, np, n;
+    double fx, fy, cx, cy, delta;
+    double* pose;      // P*8: qx qy qz qw tx ty tz pad
+    double* pose_bak;
+    double* pts;       // M*3
+    double* pts_bak;
+    const int* opt;    // P
+    const int* e_pose;
+    const int* e_pt;
+    const double* e_obs;   // E*2
+    const double* e_info;  // E
+    double* e_err;     // E*2
+    double* e_chi2;    // E
+    double* e_rho0;    // E
+    double* e_rho1;    // E
+    double* Hpp;       // np*36
+    double* Hll;       // M*9
+    double* Hpl;       // E*18 (zero for edges of fixed poses)
+    double* b;         // n + 3M
+    double* Dinv;      // M*9
+    double* db;        // M*3
+    double* W;         // E*18
+    double* S;         // n*n
+    double* bs;        // n
+    double* x;         // n + 3M
+    const int* pt_ptr; const int* pt_edges;     // CSR point -> edges (all edges)
+    const int* ps_ptr; const int* ps_edges;     // CSR optimised pose -> edges
+    const int* blk_i; const int* blk_j; const int* blk_ptr; const int* blk_pairs;  // Schur pair lists
+    int nblk;
+    double* red;       // [0] chi2, [1] scale, [2] maxdiag
+    int* flag;         // [0] cholesky ok
+    const double* lambda;   // current lambda of this problem (device copy)
+    double* Lsave;     // ceil(n/32) x 1024: L11^{-1} of every Cholesky panel
+    const int* row_first;   // ceil(n/32): envelope of S in 32x32 tiles (blocked solver)
+    int lead;          // sharded solve: this shard adds the pose-side Hpp + lambda terms (once)
+};
+
+}  // namespace orbhip

@@ -38,47 +38,14 @@
 #include "orbhip_ba.h"
 #include "ba_chol.h"
 #include "ba_chol_blocked.h"
+#include "ba_args.h"
+#include "ba_chol_reg.h"
 
 namespace orbhip {
 
 
-struct BaArgs {
-    int P, M, E, np, n;
-    double fx, fy, cx, cy, delta;
-    double* pose;      // P*8: qx qy qz qw tx ty tz pad
-    double* pose_bak;
-    double* pts;       // M*3
-    double* pts_bak;
-    const int* opt;    // P
-    const int* e_pose;
-    const int* e_pt;
-    const double* e_obs;   // E*2
-    const double* e_info;  // E
-    double* e_err;     // E*2
-    double* e_chi2;    // E
-    double* e_rho0;    // E
-    double* e_rho1;    // E
-    double* Hpp;       // np*36
-    double* Hll;       // M*9
-    double* Hpl;       // E*18 (zero for edges of fixed poses)
-    double* b;         // n + 3M
-    double* Dinv;      // M*9
-    double* db;        // M*3
-    double* W;         // E*18
-    double* S;         // n*n
-    double* bs;        // n
-    double* x;         // n + 3M
-    const int* pt_ptr; const int* pt_edges;     // CSR point -> edges (all edges)
-    const int* ps_ptr; const int* ps_edges;     // CSR optimised pose -> edges
-    const int* blk_i; const int* blk_j; const int* blk_ptr; const int* blk_pairs;  // Schur pair lists
-    int nblk;
-    double* red;       // [0] chi2, [1] scale, [2] maxdiag
-    int* flag;         // [0] cholesky ok
-    const double* lambda;   // current lambda of this problem (device copy)
-    double* Lsave;     // ceil(n/32) x 1024: L11^{-1} of every Cholesky panel
-    const int* row_first;   // ceil(n/32): envelope of S in 32x32 tiles (blocked solver)
-    int lead;          // sharded solve: this shard adds the pose-side Hpp + lambda terms (once)
-};
+// struct BaArgs: ba_args.h
+
 
 #define BA_PROLOGUE                                 \
     const BaArgs& a = args[act[blockIdx.y]];
@@ -1267,7 +1234,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 if (coll(1, 0, (size_t)pp[0].n * pp[0].n, 0) || coll(2, 0, (size_t)pp[0].n, 0)) return ORBHIP_ERR_DEVICE;
             }
             if (!any_large) {
-                hipLaunchKernelGGL(k_ba_cholesky, dim3(nt_), dim3(512), chol_lds, st, dA, d_act);
+                if (maxN <= kCholRegMaxN) BAOK(chol_reg_launch(maxN, (int)nt_, dA, d_act, st));
+                else hipLaunchKernelGGL(k_ba_cholesky, dim3(nt_), dim3(512), chol_lds, st, dA, d_act);
             } else {
                 // small problems: one workgroup each (act slot 3); large: the blocked solver
                 int ns = 0;
@@ -1275,7 +1243,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                     if (pp[b].n <= kCholSmallN) h_act[2 * B + ns++] = b;
                 if (ns) {
                     BAOK(hipMemcpyAsync(d_act + 2 * B, h_act + 2 * B, ns * sizeof(int), hipMemcpyHostToDevice, st));
-                    hipLaunchKernelGGL(k_ba_cholesky, dim3(ns), dim3(512), chol_lds, st, dA, d_act + 2 * B);
+                    if (maxN <= kCholRegMaxN) BAOK(chol_reg_launch(maxN, ns, dA, d_act + 2 * B, st));
+                    else hipLaunchKernelGGL(k_ba_cholesky, dim3(ns), dim3(512), chol_lds, st, dA, d_act + 2 * B);
                 }
                 for (int b : trial)
                     if (pp[b].n > kCholSmallN)
@@ -1402,6 +1371,52 @@ int ba_comm_unique_id(void* id) {
 }
 
 // Diagnostic: factor+solve one SPD system with per-phase cycle stamps (test hook).
+// Diagnostic: the register-resident solver on one SPD system (test hook); reps launches timed.
+int ba_test_cholesky_reg(const double* A, const double* b, double* x, int n, int reps, float* ms,
+                         unsigned long long* phases5) {
+    if (n <= 0 || n > kCholRegMaxN || reps < 1) return ORBHIP_ERR_ARG;
+    double *dS = nullptr, *db_ = nullptr, *dx = nullptr;
+    int *df = nullptr, *dact = nullptr;
+    BaArgs* dargs = nullptr;
+    BAOK(hipMalloc((void**)&dS, sizeof(double) * n * n));
+    BAOK(hipMalloc((void**)&db_, sizeof(double) * n));
+    BAOK(hipMalloc((void**)&dx, sizeof(double) * n));
+    BAOK(hipMalloc((void**)&df, sizeof(int)));
+    BAOK(hipMalloc((void**)&dact, sizeof(int)));
+    BAOK(hipMalloc((void**)&dargs, sizeof(BaArgs)));
+    BAOK(hipMemcpy(dS, A, sizeof(double) * n * n, hipMemcpyHostToDevice));
+    BAOK(hipMemcpy(db_, b, sizeof(double) * n, hipMemcpyHostToDevice));
+    BaArgs h{};
+    h.n = n; h.S = dS; h.bs = db_; h.x = dx; h.flag = df;
+    const int zero = 0;
+    BAOK(hipMemcpy(dargs, &h, sizeof(BaArgs), hipMemcpyHostToDevice));
+    BAOK(hipMemcpy(dact, &zero, sizeof(int), hipMemcpyHostToDevice));
+    BAOK(chol_reg_launch(n, 1, dargs, dact, nullptr));   // warm-up (S is read-only)
+    hipEvent_t e0, e1;
+    BAOK(hipEventCreate(&e0)); BAOK(hipEventCreate(&e1));
+    BAOK(hipEventRecord(e0, nullptr));
+    for (int r = 0; r < reps; r++) BAOK(chol_reg_launch(n, 1, dargs, dact, nullptr));
+    BAOK(hipEventRecord(e1, nullptr));
+    BAOK(hipDeviceSynchronize());
+    BAOK(hipEventElapsedTime(ms, e0, e1));
+    *ms /= reps;
+    if (phases5) {
+        unsigned long long* dd = nullptr;
+        BAOK(hipMalloc((void**)&dd, sizeof(unsigned long long) * 48));
+        BAOK(hipMemset(dd, 0, 48 * 8));
+        BAOK(chol_reg_probe(n, dargs, dd, nullptr));
+        BAOK(hipMemcpy(phases5, dd, sizeof(unsigned long long) * 48, hipMemcpyDeviceToHost));
+        (void)hipFree(dd);
+    }
+    int fl = 0;
+    BAOK(hipMemcpy(&fl, df, sizeof(int), hipMemcpyDeviceToHost));
+    BAOK(hipMemcpy(x, dx, sizeof(double) * n, hipMemcpyDeviceToHost));
+    (void)hipFree(dS); (void)hipFree(db_); (void)hipFree(dx); (void)hipFree(df); (void)hipFree(dact);
+    (void)hipFree(dargs);
+    (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
+    return fl ? ORBHIP_OK : ORBHIP_ERR_NOT_PD;
+}
+
 int ba_test_cholesky(const double* A, const double* b, double* x, int n, unsigned long long* phases5, float* ms) {
     double *dS = nullptr, *db_ = nullptr, *dx = nullptr;
     int* df = nullptr;

@@ -849,6 +849,11 @@ int orbhip_test_cholesky(const double* A, const double* b, double* x, int n, uns
     if (!A || !b || !x || n <= 0 || n > 480) return ORBHIP_ERR_ARG;
     return ba_test_cholesky(A, b, x, n, phases5, ms);
 }
+int orbhip_test_cholesky_reg(const double* A, const double* b, double* x, int n, int reps, float* ms,
+                             unsigned long long* phases5) {
+    if (!A || !b || !x || !ms) return ORBHIP_ERR_ARG;
+    return ba_test_cholesky_reg(A, b, x, n, reps, ms, phases5);
+}
 int orbhip_test_cholesky_blocked(const double* A, const double* b, double* x, int n, float* ms) {
     if (!A || !b || !x || n <= 0 || !ms) return ORBHIP_ERR_ARG;
     return chol_blocked_test(A, b, x, n, ms);

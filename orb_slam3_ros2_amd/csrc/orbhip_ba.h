@@ -18,5 +18,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                    const volatile int* stop, hipStream_t st, int shard_mode);
 int ba_comm_init(BaWorkspace* ws, int nranks, int rank, const void* id);
 int ba_comm_unique_id(void* id);
+int ba_test_cholesky_reg(const double* A, const double* b, double* x, int n, int reps, float* ms,
+                         unsigned long long* phases5);
 int ba_test_cholesky(const double* A, const double* b, double* x, int n, unsigned long long* phases5, float* ms);
 }  // namespace orbhip
