@@ -40,6 +40,13 @@ struct BaArgs {
     double* Lsave;     // ceil(n/32) x 1024: L11^{-1} of every Cholesky panel
     const int* row_first;   // ceil(n/32): envelope of S in 32x32 tiles (blocked solver)
     int lead;          // sharded solve: this shard adds the pose-side Hpp + lambda terms (once)
+    // Schur work items (k_ba_schur_items): {k0, k1, blk, slot} over blk_pairs, at most kSchurChunk
+    // pairs each; slot -1 = the block's only item (written to S directly), else its partial sum
+    // goes to Spart[36 slot] and k_ba_schur_fin adds the block's partials (+ Hpp + lambda on the
+    // diagonal) in order. fin: {blk, first slot, count} per such block.
+    const int* items; int nitems;
+    const int* fin; int nfin;
+    double* Spart;
 };
 
 }  // namespace orbhip

@@ -10,10 +10,10 @@
 //   k_ba_errors        EdgeSE3ProjectXYZ::computeError + RobustKernelHuber::robustify
 //   k_ba_lin_points    linearizeOplus + constructQuadraticForm, landmark side (Hll, b_l, Hpl)
 //   k_ba_lin_poses     the pose side (Hpp, b_p), one wave per pose, deterministic tree
-//   k_ba_schur_points  setLambda on Hll, Dinv (Eigen 3x3 cofactor inverse), db
-//   k_ba_schur_w       W = Hpl Dinv per edge
-//   k_ba_schur_blocks  S_ij = [i==j](Hpp_i + lambda I) - sum W_a Hpl_b^T over shared landmarks
-//                      (host-built pair lists: deterministic gather, no atomics)
+//   k_ba_schur_points  setLambda on Hll, Dinv (Eigen 3x3 cofactor inverse), db, W = Hpl Dinv
+//   k_ba_schur_items   S_ij = [i==j](Hpp_i + lambda I) - sum W_a Hpl_b^T over shared landmarks:
+//   k_ba_schur_fin     one lane per chunk of a block's (host-built) pair list, chunk partials summed
+//                      in order by the finisher (deterministic gather, no atomics)
 //   k_ba_schur_b       b_schur = b_p - sum Hpl db
 //   k_ba_cholesky      dense LL^T + solves, one workgroup per problem; trailing update on
 //                      v_mfma_f64_16x16x4f64
@@ -47,8 +47,28 @@ namespace orbhip {
 // struct BaArgs: ba_args.h
 
 
+// Grid (X work-groups per problem, Y problems). Work-groups are dispatched round-robin over the
+// 8 XCDs in linear order, so the plain (blockIdx.x, blockIdx.y) spreads every problem over all
+// XCDs and each XCD's L2 streams every problem's arrays. Remapped, the X work-groups of problem p
+// run on XCD p % 8 (for the first 8 floor(Y / 8) problems; the tail keeps the plain order), so a
+// problem's Hpl / W / S stay in one L2. Speed only: correctness never depends on the placement.
+__device__ __forceinline__ void ba_xcd_map(int& bx, int& by) {
+    const int X = gridDim.x, Y = gridDim.y;
+    const int id = blockIdx.x + X * blockIdx.y;
+    const int Yf = Y & ~7;
+    if (id < X * Yf) {
+        const int k = id & 7, s = id >> 3;
+        by = 8 * (s / X) + k;
+        bx = s - (s / X) * X;
+    } else {
+        by = id / X;
+        bx = id - by * X;
+    }
+}
 #define BA_PROLOGUE                                 \
-    const BaArgs& a = args[act[blockIdx.y]];
+    int bx_, by_;                                   \
+    ba_xcd_map(bx_, by_);                           \
+    const BaArgs& a = args[act[by_]];
 
 // ---------------------------------------------------------------------------
 // SE3Quat helpers (Eigen formulas)
@@ -115,7 +135,7 @@ __device__ __forceinline__ DQ load_q(const double* p) { return DQ{p[0], p[1], p[
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_ba_errors(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    const int e = bx_ * blockDim.x + threadIdx.x;
     if (e >= a.E) return;
     const double* T = a.pose + 8 * a.e_pose[e];
     const double* X = a.pts + 3 * a.e_pt[e];
@@ -172,7 +192,7 @@ __device__ __forceinline__ void edge_jac(const BaArgs& a, int e, double A[6], do
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_ba_lin_points(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
-    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    const int m = bx_ * blockDim.x + threadIdx.x;
     if (m >= a.M) return;
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};
     for (int k = a.pt_ptr[m]; k < a.pt_ptr[m + 1]; k++) {
@@ -205,7 +225,7 @@ __global__ __launch_bounds__(256) void k_ba_lin_points(const BaArgs* __restrict_
 // one wave per optimised pose: 21 upper Hpp terms + 6 b terms, lanes over the pose's edges
 __global__ __launch_bounds__(256) void k_ba_lin_poses(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
-    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int i = bx_ * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (i >= a.np) return;
     double acc[27];
@@ -261,9 +281,11 @@ __device__ __forceinline__ void inv3(const double m[9], double r[9]) {
 }
 
 
+// one thread per landmark: setLambda on Hll, Dinv (Eigen 3x3 cofactor inverse), db = Dinv b_l,
+// and W = Hpl Dinv for the landmark's edges (edges of fixed poses keep W = 0)
 __global__ __launch_bounds__(256) void k_ba_schur_points(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
-    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    const int m = bx_ * blockDim.x + threadIdx.x;
     if (m >= a.M) return;
     const double lambda = *a.lambda;
     double D[9], Di[9];
@@ -275,23 +297,21 @@ __global__ __launch_bounds__(256) void k_ba_schur_points(const BaArgs* __restric
     const double* bl = a.b + a.n + 3 * m;
 #pragma unroll
     for (int r = 0; r < 3; r++) a.db[3 * m + r] = Di[3 * r] * bl[0] + Di[3 * r + 1] * bl[1] + Di[3 * r + 2] * bl[2];
-}
-
-__global__ __launch_bounds__(256) void k_ba_schur_w(const BaArgs* __restrict__ args, const int* __restrict__ act) {
-    BA_PROLOGUE
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= a.E || a.opt[a.e_pose[e]] < 0) return;
-    const double* Di = a.Dinv + 9 * a.e_pt[e];
-    double d[9];
+    for (int k = a.pt_ptr[m]; k < a.pt_ptr[m + 1]; k++) {
+        const int e = a.pt_edges[k];
+        if (a.opt[a.e_pose[e]] < 0) continue;
+        const double2* B2 = (const double2*)(a.Hpl + 18 * e);
+        double h[18];
 #pragma unroll
-    for (int k = 0; k < 9; k++) d[k] = Di[k];
-    const double* B1 = a.Hpl + 18 * e;
-    double* w = a.W + 18 * e;
+        for (int i = 0; i < 9; i++) { const double2 v = B2[i]; h[2 * i] = v.x; h[2 * i + 1] = v.y; }
+        double w[18];
 #pragma unroll
-    for (int r = 0; r < 6; r++) {
-        const double h0 = B1[3 * r], h1 = B1[3 * r + 1], h2 = B1[3 * r + 2];
+        for (int r = 0; r < 6; r++)
 #pragma unroll
-        for (int c = 0; c < 3; c++) w[3 * r + c] = h0 * d[c] + h1 * d[3 + c] + h2 * d[6 + c];
+            for (int c = 0; c < 3; c++) w[3 * r + c] = h[3 * r] * Di[c] + h[3 * r + 1] * Di[3 + c] + h[3 * r + 2] * Di[6 + c];
+        double2* W2 = (double2*)(a.W + 18 * e);
+#pragma unroll
+        for (int i = 0; i < 9; i++) W2[i] = make_double2(w[2 * i], w[2 * i + 1]);
     }
 }
 
@@ -299,58 +319,75 @@ __global__ __launch_bounds__(256) void k_ba_zero_s(const BaArgs* __restrict__ ar
     BA_PROLOGUE
     const size_t nn = (size_t)a.n * a.n;
     double2* S2 = (double2*)a.S;
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < nn / 2; i += (size_t)gridDim.x * blockDim.x)
+    for (size_t i = (size_t)bx_ * blockDim.x + threadIdx.x; i < nn / 2; i += (size_t)gridDim.x * blockDim.x)
         S2[i] = make_double2(0.0, 0.0);
-    if (blockIdx.x == 0 && threadIdx.x == 0 && (nn & 1)) a.S[nn - 1] = 0.0;
+    if (bx_ == 0 && threadIdx.x == 0 && (nn & 1)) a.S[nn - 1] = 0.0;
 }
 
-// one wave per (i <= j) block of S; lanes 0..35 own one entry each. The block's pair list is
-// fetched 64 pairs at a time into lanes and broadcast with shuffles, so the serial loop has
-// no dependent index load.
-__global__ __launch_bounds__(256) void k_ba_schur_blocks(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+// One LANE per Schur work item (a chunk of at most kSchurChunk pairs of one 6x6 block): the 36
+// sums live in the lane's registers and each pair's W_a / Hpl_b rows (18 + 18 doubles, 16-byte
+// loads) are read exactly once, so the L1/L2 traffic is the operands themselves (the previous
+// wave-per-block form re-read every row once per output lane). S_ij -= sum W_a Hpl_b^T.
+__global__ __launch_bounds__(256) void k_ba_schur_items(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
-    const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (blk >= a.nblk) return;
-    const double lambda = *a.lambda;
-    const int i = a.blk_i[blk], j = a.blk_j[blk];
-    const int rr = lane < 36 ? lane / 6 : 0, cc = lane < 36 ? lane - 6 * (lane / 6) : 0;
-    double s = (i == j && lane < 36 && a.lead) ? a.Hpp[36 * i + 6 * rr + cc] + (rr == cc ? lambda : 0.0) : 0.0;
-    const int k0 = a.blk_ptr[blk], k1 = a.blk_ptr[blk + 1];
-    for (int kb = k0; kb < k1; kb += 64) {
-        const int cnt = min(64, k1 - kb);
-        const int pa = lane < cnt ? a.blk_pairs[2 * (kb + lane)] : 0;
-        const int pb = lane < cnt ? a.blk_pairs[2 * (kb + lane) + 1] : 0;
-        int t = 0;
-        for (; t + 4 <= cnt; t += 4) {
-            double w[4][3], h[4][3];
+    const int it = bx_ * blockDim.x + threadIdx.x;
+    if (it >= a.nitems) return;
+    const int4 wi = ((const int4*)a.items)[it];
+    double s[36];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int ea = __shfl(pa, t + u, 64), eb = __shfl(pb, t + u, 64);
-                const double* wp = a.W + 18 * ea + 3 * rr;
-                const double* hp = a.Hpl + 18 * eb + 3 * cc;
-                w[u][0] = wp[0]; w[u][1] = wp[1]; w[u][2] = wp[2];
-                h[u][0] = hp[0]; h[u][1] = hp[1]; h[u][2] = hp[2];
+    for (int k = 0; k < 36; k++) s[k] = 0.0;
+    for (int k = wi.x; k < wi.y; k++) {
+        const int2 pr = ((const int2*)a.blk_pairs)[k];
+        const double2* W2 = (const double2*)(a.W + 18 * pr.x);
+        const double2* H2 = (const double2*)(a.Hpl + 18 * pr.y);
+        double w[18], h[18];
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            const double2 u = W2[i], v = H2[i];
+            w[2 * i] = u.x; w[2 * i + 1] = u.y;
+            h[2 * i] = v.x; h[2 * i + 1] = v.y;
+        }
+#pragma unroll
+        for (int rr = 0; rr < 6; rr++)
+#pragma unroll
+            for (int cc = 0; cc < 6; cc++)
+                s[6 * rr + cc] -= w[3 * rr] * h[3 * cc] + w[3 * rr + 1] * h[3 * cc + 1] + w[3 * rr + 2] * h[3 * cc + 2];
+    }
+    if (wi.w < 0) {   // the block's only item: straight into S (both triangles)
+        const int i = a.blk_i[wi.z], j = a.blk_j[wi.z];
+#pragma unroll
+        for (int rr = 0; rr < 6; rr++)
+#pragma unroll
+            for (int cc = 0; cc < 6; cc++) {
+                a.S[(size_t)(6 * i + rr) * a.n + 6 * j + cc] = s[6 * rr + cc];
+                a.S[(size_t)(6 * j + cc) * a.n + 6 * i + rr] = s[6 * rr + cc];
             }
+    } else {
+        double2* dst = (double2*)(a.Spart + 36 * (size_t)wi.w);
 #pragma unroll
-            for (int u = 0; u < 4; u++) s -= w[u][0] * h[u][0] + w[u][1] * h[u][1] + w[u][2] * h[u][2];
-        }
-        for (; t < cnt; t++) {
-            const int ea = __shfl(pa, t, 64), eb = __shfl(pb, t, 64);
-            const double* wp = a.W + 18 * ea + 3 * rr;
-            const double* hp = a.Hpl + 18 * eb + 3 * cc;
-            s -= wp[0] * hp[0] + wp[1] * hp[1] + wp[2] * hp[2];
-        }
+        for (int k = 0; k < 18; k++) dst[k] = make_double2(s[2 * k], s[2 * k + 1]);
     }
-    if (lane < 36) {
-        a.S[(size_t)(6 * i + rr) * a.n + 6 * j + cc] = s;
-        if (i != j) a.S[(size_t)(6 * j + cc) * a.n + 6 * i + rr] = s;
-    }
+}
+
+// one wave per block with several items or on the diagonal: [i==j](Hpp_i + lambda I) + its partial
+// sums in item order (fixed order: deterministic)
+__global__ __launch_bounds__(256) void k_ba_schur_fin(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    BA_PROLOGUE
+    const int f = bx_ * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (f >= a.nfin || lane >= 36) return;
+    const int blk = a.fin[3 * f], slot0 = a.fin[3 * f + 1], nch = a.fin[3 * f + 2];
+    const int i = a.blk_i[blk], j = a.blk_j[blk];
+    const int rr = lane / 6, cc = lane - 6 * rr;
+    double s = (i == j && a.lead) ? a.Hpp[36 * i + 6 * rr + cc] + (rr == cc ? *a.lambda : 0.0) : 0.0;
+    for (int c = 0; c < nch; c++) s += a.Spart[36 * (size_t)(slot0 + c) + lane];
+    a.S[(size_t)(6 * i + rr) * a.n + 6 * j + cc] = s;
+    if (i != j) a.S[(size_t)(6 * j + cc) * a.n + 6 * i + rr] = s;
 }
 
 __global__ __launch_bounds__(256) void k_ba_schur_b(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
-    const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int i = bx_ * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (i >= a.np) return;
     double acc[6] = {0, 0, 0, 0, 0, 0};
@@ -386,6 +423,7 @@ __global__ __launch_bounds__(256) void k_ba_schur_b(const BaArgs* __restrict__ a
 //  (c) backward solve panel by panel: x_p = Linv^T (y_p - L21^T x_below) (Linv saved per panel).
 // ---------------------------------------------------------------------------
 constexpr int kNB = 32;
+constexpr int kSchurChunk = 16;    // pairs per Schur work item (one lane)
 constexpr int kCholSmallN = 480;   // largest n of the single-workgroup solver (LDS envelope)
 constexpr int kPS = 34;   // panel row stride in doubles
 
@@ -585,7 +623,7 @@ __global__ __launch_bounds__(512) void k_chol_test(double* S, const double* bs, 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_ba_backsub(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
-    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    const int m = bx_ * blockDim.x + threadIdx.x;
     if (m >= a.M) return;
     const double* bl = a.b + a.n + 3 * m;
     double c[3] = {bl[0], bl[1], bl[2]};
@@ -613,7 +651,7 @@ __global__ __launch_bounds__(256) void k_ba_backsub(const BaArgs* __restrict__ a
 
 __global__ __launch_bounds__(256) void k_ba_update_poses(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int p = bx_ * blockDim.x + threadIdx.x;
     if (p >= a.P) return;
     double* T = a.pose + 8 * p;
 #pragma unroll
@@ -660,7 +698,7 @@ __global__ __launch_bounds__(256) void k_ba_update_poses(const BaArgs* __restric
 
 __global__ __launch_bounds__(256) void k_ba_pop(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = bx_ * blockDim.x + threadIdx.x;
     if (i < 8 * a.P) a.pose[i] = a.pose_bak[i];
     if (i < 3 * a.M) a.pts[i] = a.pts_bak[i];
 }
@@ -764,8 +802,10 @@ struct Prep {
     int P = 0, M = 0, E = 0, np = 0, n = 0, nblk = 0;
     std::vector<int> opt, pt_ptr, pt_edges, ps_ptr, ps_edges, blk_i, blk_j, blk_ptr, blk_pairs;
     std::vector<int> row_first;   // blocked Cholesky structure: first 32-col tile per 32-row tile
+    std::vector<int> items, fin;  // Schur work items {k0, k1, blk, slot} and finisher blocks {blk, slot0, n}
+    int nslot = 0;
     // offsets (elements) into the packed buffers; see the segment map in ba_solve_batch
-    size_t o_chi2, o_state, o_obs, o_hw, o_scr, o_S, o_L, o_int;
+    size_t o_chi2, o_state, o_obs, o_hw, o_scr, o_S, o_L, o_part, o_int;
 };
 
 inline void se3_from_float(const float* q, const float* t, double* out) {
@@ -853,6 +893,21 @@ int prepare(const orbhip_ba_problem* pr, Prep& o) {
             for (int r = 32 * R; r < std::min(o.n, 32 * R + 32); r++) f = std::min(f, (6 * fp[r / 6]) / 32);
             o.row_first[R] = f;
         }
+    }
+    // Schur work items: chunks of at most kSchurChunk pairs; a block with one off-diagonal chunk
+    // is written by its item, the others (and every diagonal block) through the finisher
+    for (int b = 0; b < o.nblk; b++) {
+        const int k0 = o.blk_ptr[b], k1 = o.blk_ptr[b + 1];
+        const bool diag = o.blk_i[b] == o.blk_j[b];
+        if (!diag && k1 - k0 <= kSchurChunk) {
+            o.items.insert(o.items.end(), {k0, k1, b, -1});
+            continue;
+        }
+        const int nch = std::max(1, (k1 - k0 + kSchurChunk - 1) / kSchurChunk);
+        o.fin.insert(o.fin.end(), {b, o.nslot, nch});
+        for (int c = 0; c < nch; c++)
+            o.items.insert(o.items.end(), {k0 + c * kSchurChunk, std::min(k1, k0 + (c + 1) * kSchurChunk), b, o.nslot + c});
+        o.nslot += nch;
     }
     o.blk_pairs.resize(2 * npairs);
     std::vector<int> fill(o.blk_ptr.begin(), o.blk_ptr.end() - 1);
@@ -1017,9 +1072,11 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         p.o_S = nR; nR += n * n;
         nR = (nR + 1) & ~size_t(1);
         p.o_L = nR; nR += 1024 * ((n + 31) / 32);
+        nR = (nR + 1) & ~size_t(1);
+        p.o_part = nR; nR += 36 * (size_t)p.nslot;
         p.o_int = ni;
         ni += (P + 4) + 2 * E + (M + 1) + E + (np_ + 1) + p.ps_edges.size() + 3 * p.nblk + 1 + p.blk_pairs.size() +
-              p.row_first.size();
+              p.row_first.size() + p.items.size() + p.fin.size() + 8;
     }
     const size_t sC = 0, sA = nC, sU = sA + nA, sZ = (sU + nU + 1) & ~size_t(1), sR = sZ + nZ;
     const size_t nd = sR + nR;
@@ -1078,7 +1135,13 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.blk_i = dev(put(p.blk_i.data(), p.nblk));
         a.blk_j = dev(put(p.blk_j.data(), p.nblk));
         a.blk_ptr = dev(put(p.blk_ptr.data(), p.nblk + 1));
+        if ((q - hi) & 1) q++;   // int2 alignment of the pair list
         a.blk_pairs = dev(put(p.blk_pairs.data(), p.blk_pairs.size()));
+        while ((q - hi) & 3) q++;   // int4 alignment of the items
+        a.items = dev(put(p.items.data(), p.items.size()));
+        a.nitems = (int)(p.items.size() / 4);
+        a.fin = dev(put(p.fin.data(), p.fin.size()));
+        a.nfin = (int)(p.fin.size() / 3);
         a.row_first = dev(put(p.row_first.data(), p.row_first.size()));
         a.nblk = p.nblk;
         a.P = p.P; a.M = p.M; a.E = p.E; a.np = p.np; a.n = p.n;
@@ -1103,6 +1166,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.red = r;
         a.S = D + sR + p.o_S;
         a.Lsave = D + sR + p.o_L;
+        a.Spart = D + sR + p.o_part;
         a.lambda = ws->lam.p + b;
         a.lead = shard_mode == kShardLocal ? (b == 0) : (shard_mode == kShardRccl ? (ws->rank == 0) : 1);
     });
@@ -1121,15 +1185,19 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         BAOK(hipFuncSetAttribute((const void*)k_ba_cholesky, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         lds_set = true;
     }
-    int maxM = 0, maxE = 0, maxP = 0, maxNp = 0, maxBlk = 0, maxN = 0;
+    int maxM = 0, maxE = 0, maxP = 0, maxNp = 0, maxBlk = 0, maxN = 0, maxItems = 0, maxFin = 0;
     bool any_large = false;
     for (auto& p : pp) {
         maxM = std::max(maxM, p.M); maxE = std::max(maxE, p.E); maxP = std::max(maxP, p.P);
         maxNp = std::max(maxNp, p.np); maxBlk = std::max(maxBlk, p.nblk);
+        maxItems = std::max(maxItems, (int)(p.items.size() / 4)); maxFin = std::max(maxFin, (int)(p.fin.size() / 3));
         if (p.n > kCholSmallN) any_large = true;
         else maxN = std::max(maxN, p.n);
     }
     const size_t chol_lds = sizeof(double) * chol_lds_doubles(maxN);
+    // every problem on the register-resident Cholesky (reads S, never writes it), no shard sums
+    const bool s_readonly = !any_large && maxN <= kCholRegMaxN && shard_mode == kShardNone;
+    bool s_clean = false;
     auto gx = [](int n_, int b_) { return (unsigned)std::max(1, (n_ + b_ - 1) / b_); };
     (void)hipGetLastError();
     int* d_act = ws->act.p;
@@ -1225,10 +1293,13 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             for (int b : trial) ws->h_lam[b] = L[b].lambda;
             BAOK(hipMemcpyAsync(ws->lam.p, ws->h_lam, B * sizeof(double), hipMemcpyHostToDevice, st));
             if (upload_act(trial)) return ORBHIP_ERR_DEVICE;
-            hipLaunchKernelGGL(k_ba_zero_s, dim3(64, nt_), dim3(256), 0, st, dA, d_act);
+            // S outside the block structure stays zero; it only needs clearing again when a solver
+            // factors S in place (or the shards' sums overwrite it)
+            if (!s_clean) hipLaunchKernelGGL(k_ba_zero_s, dim3(64, nt_), dim3(256), 0, st, dA, d_act);
+            s_clean = s_readonly;
             hipLaunchKernelGGL(k_ba_schur_points, dim3(gx(maxM, 256), nt_), dim3(256), 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_schur_w, dim3(gx(maxE, 256), nt_), dim3(256), 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_schur_blocks, dim3(gx(maxBlk, 4), nt_), dim3(256), 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_schur_items, dim3(gx(maxItems, 256), nt_), dim3(256), 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_schur_fin, dim3(gx(maxFin, 4), nt_), dim3(256), 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_schur_b, dim3(gx(maxNp, 4), nt_), dim3(256), 0, st, dA, d_act);
             if (shard_mode) {   // reduced camera system of all shards
                 if (coll(1, 0, (size_t)pp[0].n * pp[0].n, 0) || coll(2, 0, (size_t)pp[0].n, 0)) return ORBHIP_ERR_DEVICE;
