@@ -185,6 +185,40 @@ int orbhip_ba_solve(orbhip_ctx* ctx, const orbhip_ba_problem* prob, orbhip_ba_re
 int orbhip_ba_solve_batch(orbhip_ctx* ctx, const orbhip_ba_problem* probs, int B, orbhip_ba_result* res,
                           const volatile int* stop_flag);
 
+/* ---- motion-only bundle adjustment -------------------------
+ * U:src/Optimizer.cc::Optimizer::PoseOptimization(Frame* pFrame), monocular observations:
+ * one VertexSE3Expmap (Tcw), EdgeSE3ProjectXYZOnlyPose per matched MapPoint (information
+ * I * mvInvLevelSigma2[octave], Huber sqrt(5.991)), 4 rounds of Levenberg optimize(10) each
+ * from the frame's initial pose, chi2 > 5.991 -> outlier after every round, robust kernel
+ * dropped after round 2, early stop after round 0 for < 10 edges. The adapter fills one
+ * problem per Frame from its mvpMapPoints (non-NULL entries, mvuRight < 0) and writes back
+ * SetPose(result) and mvbOutlier[i] = outlier[k]. Returns nInitialCorrespondences - nBad
+ * (0, pose untouched, when < 3 correspondences). */
+typedef struct {
+    int32_t n;                  /* correspondences */
+    const float* pose_q;        /* 4: initial Tcw rotation (x, y, z, w) = pFrame->GetPose() */
+    const float* pose_t;        /* 3 */
+    const float* points;        /* n x 3: MapPoint::GetWorldPos() */
+    const float* uv;            /* n x 2: mvKeysUn[i].pt */
+    const int32_t* octave;      /* n: mvKeysUn[i].octave */
+    const float* inv_sigma2;    /* per octave: mvInvLevelSigma2 */
+    int32_t n_octaves;
+    float fx, fy, cx, cy;       /* Pinhole mvParameters */
+} orbhip_pose_problem;
+
+typedef struct {
+    float pose_q[4];            /* optimised Tcw */
+    float pose_t[3];
+    uint8_t* outlier;           /* n out (caller-owned, may be NULL): mvbOutlier */
+    int32_t n_inliers;          /* PoseOptimization return value */
+    int32_t lm_trials;          /* total Levenberg trials over the 4 rounds */
+} orbhip_pose_result;
+
+int orbhip_pose_optimization(orbhip_ctx* ctx, const orbhip_pose_problem* prob, orbhip_pose_result* res);
+/* B frames (e.g. every camera of a rig, or a batch of agents) in one launch, one wavefront each. */
+int orbhip_pose_optimization_batch(orbhip_ctx* ctx, const orbhip_pose_problem* probs, int B,
+                                   orbhip_pose_result* res);
+
 /* ---- bag of words -----------------------------------------
  * DBoW2 vocabulary in the ORBvoc.txt node order (Thirdparty/DBoW2 TemplatedVocabulary):
  * node 0 = root, node i (i >= 1) = line i of the text file with (parent, is_leaf, 32-byte

@@ -420,6 +420,154 @@ static int solve(Problem& pr, int iterations, int early_stop, Result& res, const
     return 0;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// U:src/Optimizer.cc::Optimizer::PoseOptimization(Frame*), monocular edges (recalled upstream):
+// one VertexSE3Expmap (Tcw) and EdgeSE3ProjectXYZOnlyPose per matched MapPoint
+// (U:src/OptimizableTypes.cpp: error obs - project(T.map(Xw)), Jacobian -projectJac(Xc) *
+// [[0,z,-y,1,0,0],[-z,0,x,0,1,0],[y,-x,0,0,0,1]]), information I*invSigma2[octave], Huber
+// deltaMono = (float)sqrt(5.991); BlockSolver_6_3 + LinearSolverDense + Levenberg. Four rounds
+// of optimize(10) (its[4] = {10,10,10,10}); EVERY round starts from the frame's initial pose (the
+// reference re-reads pFrame->GetPose(), which is only written after the last round). After a
+// round each edge is classified with chi2() (an outlier's error recomputed at the current
+// estimate, an inlier's as left by the last trial) against chi2Mono = 5.991f: outliers go to
+// level 1 (inactive next round), inliers back to level 0; after round 2 the robust kernel is
+// removed from every edge; the loop stops after a round if the frame has < 10 edges. Returns
+// nInitialCorrespondences - nBad (0 and the pose untouched when < 3 correspondences).
+// ---------------------------------------------------------------------------------------------
+struct PoseEdge { V3 Xw; double u, v, info; };
+
+static inline void pose_edge_error(const SE3& T, const PoseEdge& pe, double fx, double fy, double cx, double cy,
+                                   double& e0, double& e1, double& chi2) {
+    const V3 Xc = se3_map(T, pe.Xw);
+    e0 = pe.u - (fx * Xc.x / Xc.z + cx);
+    e1 = pe.v - (fy * Xc.y / Xc.z + cy);
+    chi2 = pe.info * (e0 * e0 + e1 * e1);
+}
+
+static inline void robustify(double chi2, double delta, bool robust, double& rho0, double& rho1) {
+    if (!robust || delta <= 0) { rho0 = chi2; rho1 = 1.0; return; }
+    const double dsqr = delta * delta;
+    if (chi2 <= dsqr) { rho0 = chi2; rho1 = 1.0; }
+    else { const double sq = std::sqrt(chi2); rho0 = 2 * sq * delta - dsqr; rho1 = delta / sq; }
+}
+
+// g2o optimize(iterations) on the active (level 0) edges; chi2_last[e] = chi2 of the last
+// computeActiveErrors (stale after a rejected final trial, as in g2o)
+static void pose_optimize(SE3& T, const std::vector<PoseEdge>& ed, const std::vector<uint8_t>& level,
+                          bool robust, double delta, double fx, double fy, double cx, double cy, int iterations,
+                          std::vector<double>& chi2_last, int& trials_out) {
+    const int N = (int)ed.size();
+    int nact = 0;
+    for (int e = 0; e < N; e++) nact += level[e] == 0;
+    if (nact == 0) return;   // no active vertex: optimize() does nothing
+    auto errors = [&](const SE3& Tc) {
+        double chi = 0;
+        for (int e = 0; e < N; e++) {
+            if (level[e]) continue;
+            double e0, e1, c2, r0, r1;
+            pose_edge_error(Tc, ed[e], fx, fy, cx, cy, e0, e1, c2);
+            robustify(c2, delta, robust, r0, r1);
+            chi2_last[e] = c2;
+            chi += r0;
+        }
+        return chi;
+    };
+    double lambda = 0, ni = 2;
+    for (int it = 0; it < iterations; it++) {
+        double currentChi = errors(T);
+        // buildSystem: H = sum rho' B^T Omega B, b = -sum rho' B^T Omega e
+        double H[36] = {0}, b[6] = {0};
+        for (int e = 0; e < N; e++) {
+            if (level[e]) continue;
+            double e0, e1, c2, r0, r1;
+            pose_edge_error(T, ed[e], fx, fy, cx, cy, e0, e1, c2);
+            robustify(c2, delta, robust, r0, r1);
+            const V3 Xc = se3_map(T, ed[e].Xw);
+            const double x = Xc.x, y = Xc.y, z = Xc.z;
+            double J[6];
+            J[0] = -(fx / z); J[1] = -0.0; J[2] = -(-fx * x / (z * z));
+            J[3] = -0.0; J[4] = -(fy / z); J[5] = -(-fy * y / (z * z));
+            const double D[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
+            double B[12];
+            for (int r = 0; r < 2; r++)
+                for (int c = 0; c < 6; c++)
+                    B[6 * r + c] = J[3 * r] * D[c] + J[3 * r + 1] * D[6 + c] + J[3 * r + 2] * D[12 + c];
+            const double w = r1 * ed[e].info;
+            const double om0 = -ed[e].info * e0 * r1, om1 = -ed[e].info * e1 * r1;
+            for (int r = 0; r < 6; r++) {
+                b[r] += B[r] * om0 + B[6 + r] * om1;
+                for (int c = 0; c < 6; c++) H[6 * r + c] += w * (B[r] * B[c] + B[6 + r] * B[6 + c]);
+            }
+        }
+        if (it == 0) {
+            double md = 0;
+            for (int j = 0; j < 6; j++) md = std::max(md, std::fabs(H[7 * j]));
+            lambda = 1e-5 * md;
+            ni = 2;
+        }
+        double rho = 0;
+        int qmax = 0;
+        do {
+            const SE3 Tbak = T;
+            std::vector<double> S(36), xv(6), bv(b, b + 6);
+            for (int k = 0; k < 36; k++) S[k] = H[k] + (k % 7 == 0 ? lambda : 0.0);
+            const bool ok2 = ldlt_solve(S, 6, bv, xv);
+            if (!ok2) std::fill(xv.begin(), xv.end(), 0.0);
+            T = se3_mul(se3_exp(xv.data()), T);
+            double tempChi = errors(T);
+            if (!ok2) tempChi = std::numeric_limits<double>::max();
+            double scale = 1e-3;
+            for (int j = 0; j < 6; j++) scale += xv[j] * (lambda * xv[j] + b[j]);
+            rho = (currentChi - tempChi) / scale;
+            if (rho > 0 && std::isfinite(tempChi)) {
+                double alpha = 1. - std::pow((2 * rho - 1), 3);
+                alpha = std::min(alpha, 2. / 3.);
+                lambda *= std::max(1. / 3., alpha);
+                ni = 2;
+                currentChi = tempChi;
+            } else {
+                lambda *= ni;
+                ni *= 2;
+                T = Tbak;   // pop
+            }
+            qmax++;
+            trials_out++;
+        } while (rho < 0 && qmax < 10);
+        if (qmax == 10 || rho == 0) break;
+    }
+}
+
+static int pose_optimization(SE3& Tout, const SE3& Tinit, const std::vector<PoseEdge>& ed, double delta,
+                             double fx, double fy, double cx, double cy, std::vector<uint8_t>& outlier, int& trials) {
+    const int N = (int)ed.size();
+    outlier.assign(N, 0);
+    Tout = Tinit;
+    if (N < 3) return 0;
+    const float chi2Mono[4] = {5.991f, 5.991f, 5.991f, 5.991f};
+    std::vector<uint8_t> level(N, 0);
+    std::vector<double> chi2_last(N, 0.0);
+    bool robust = true;
+    int nBad = 0;
+    SE3 T = Tinit;
+    for (int it = 0; it < 4; it++) {
+        T = Tinit;   // vSE3->setEstimate(pFrame->GetPose())
+        pose_optimize(T, ed, level, robust, delta, fx, fy, cx, cy, 10, chi2_last, trials);
+        nBad = 0;
+        for (int e = 0; e < N; e++) {
+            if (outlier[e]) {   // level-1 edge: e->computeError() at the current estimate
+                double e0, e1;
+                pose_edge_error(T, ed[e], fx, fy, cx, cy, e0, e1, chi2_last[e]);
+            }
+            if (chi2_last[e] > chi2Mono[it]) { outlier[e] = 1; level[e] = 1; nBad++; }
+            else { outlier[e] = 0; level[e] = 0; }
+        }
+        if (it == 2) robust = false;   // e->setRobustKernel(0)
+        if (N < 10) break;             // optimizer.edges().size() < 10
+    }
+    Tout = T;
+    return N - nBad;
+}
 }  // namespace bao
 
 extern "C" {
@@ -474,5 +622,29 @@ int orc_ba_solve(int P, int M, int E, const float* pose_q, const float* pose_t, 
     out_stats[2] = res.iters;
     out_stats[3] = res.trials;
     return 0;
+}
+
+// Optimizer::PoseOptimization(Frame*) on N monocular correspondences (see pose_optimization).
+// Returns the inlier count; out_stats = {trials}.
+int orc_pose_optimization(int N, const float* pose_q, const float* pose_t, const float* points, const float* uv,
+                          const int32_t* octave, const float* inv_sigma2, float fx, float fy, float cx, float cy,
+                          float huber_delta, float* out_q, float* out_t, uint8_t* out_outlier, double* out_stats) {
+    bao::SE3 T0;
+    T0.q = bao::Q{pose_q[0], pose_q[1], pose_q[2], pose_q[3]};
+    bao::normalize_rotation(T0.q);
+    T0.t = bao::V3{pose_t[0], pose_t[1], pose_t[2]};
+    std::vector<bao::PoseEdge> ed(N);
+    for (int e = 0; e < N; e++)
+        ed[e] = bao::PoseEdge{bao::V3{points[3 * e], points[3 * e + 1], points[3 * e + 2]}, (double)uv[2 * e],
+                              (double)uv[2 * e + 1], (double)inv_sigma2[octave[e]]};
+    bao::SE3 T;
+    std::vector<uint8_t> outl;
+    int trials = 0;
+    const int nin = bao::pose_optimization(T, T0, ed, huber_delta, fx, fy, cx, cy, outl, trials);
+    out_q[0] = (float)T.q.x; out_q[1] = (float)T.q.y; out_q[2] = (float)T.q.z; out_q[3] = (float)T.q.w;
+    out_t[0] = (float)T.t.x; out_t[1] = (float)T.t.y; out_t[2] = (float)T.t.z;
+    for (int e = 0; e < N; e++) out_outlier[e] = outl[e];
+    if (out_stats) out_stats[0] = trials;
+    return nin;
 }
 }

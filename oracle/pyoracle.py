@@ -56,6 +56,8 @@ def lib():
         L.orc_bow_vector.argtypes = [_i32p, _f64, c_int, _i32p, _f64]
         L.orc_search_bow.argtypes = [_u8p, _f32p, _i32p, _u8p, c_int, _u8p, _f32p, _i32p, c_int, c_float, c_int,
                                      c_int, _i32p]
+        L.orc_pose_optimization.argtypes = [c_int, _f32p, _f32p, _f32p, _f32p, _i32p, _f32p, c_float, c_float,
+                                            c_float, c_float, c_float, _f32p, _f32p, _u8p, _f64]
         L.orc_bgr2gray.argtypes = [_u8p, c_int, c_int, c_int, _u8p, c_int]
         L.orc_glibc_sincosf_range.argtypes = [ctypes.c_uint32, ctypes.c_uint32, _f32p, _f32p]
         _lib = L
@@ -197,3 +199,14 @@ def ba_solve(prob):
                        p.early_stop, oq, ot, op, oc, od, st)
     return dict(pose_q=oq, pose_t=ot, points=op, edge_chi2=oc, edge_depth_ok=od, initial_chi2=st[0],
                 final_chi2=st[1], iterations_done=int(st[2]), lm_trials=int(st[3]))
+
+
+def pose_optimization(prob):
+    """Oracle Optimizer::PoseOptimization of an orb_slam3_ros2_amd.optimizer.PoseProblem."""
+    p = prob.normalized()
+    n = p.points.shape[0]
+    oq = np.zeros(4, np.float32); ot = np.zeros(3, np.float32); ol = np.zeros(n, np.uint8)
+    st = np.zeros(1, np.float64)
+    nin = lib().orc_pose_optimization(n, p.pose_q, p.pose_t, p.points, p.uv, p.octave, p.inv_sigma2, p.fx, p.fy,
+                                      p.cx, p.cy, float(np.float32(np.sqrt(5.991))), oq, ot, ol, st)
+    return dict(pose_q=oq, pose_t=ot, outlier=ol, n_inliers=int(nin), lm_trials=int(st[0]))

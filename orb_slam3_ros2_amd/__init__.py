@@ -8,6 +8,7 @@ Host-side mirror of the reference's hot-path interfaces over th
   ORBmatcher.DescriptorDistance(a, b)                                       U:src/ORBmatcher.cc
   ORBmatcher(nnratio, checkOri).match_bf(...)                               (a12 rule)
   Optimizer.LocalBundleAdjustment(problem)                                  U:src/Optimizer.cc
+  Optimizer.PoseOptimization(frame_problem)                                 U:src/Optimizer.cc
   ORBVocabulary(vocab).transform(desc)  (DBoW2 TemplatedVocabulary)         U:src/Frame.cc::ComputeBoW
   ORBmatcher.SearchByBoW(...)                                               U:src/ORBmatcher.cc
 
@@ -19,8 +20,8 @@ from __future__ import annotations
 from ._lib import OrbHipError, lib, library_path  # noqa: F401
 from .extractor import KeyPoint, ORBextractor  # noqa: F401
 from .matcher import ORBmatcher  # noqa: F401
-from .optimizer import BAProblem, BAResult, Optimizer  # noqa: F401
+from .optimizer import BAProblem, BAResult, Optimizer, PoseProblem, PoseResult  # noqa: F401
 from .bow import ORBVocabulary  # noqa: F401
 
-__all__ = ["ORBextractor", "KeyPoint", "ORBmatcher", "Optimizer", "BAProblem", "BAResult", "ORBVocabulary", "OrbHipError",
+__all__ = ["ORBextractor", "KeyPoint", "ORBmatcher", "Optimizer", "BAProblem", "BAResult", "PoseProblem", "PoseResult", "ORBVocabulary", "OrbHipError",
            "lib", "library_path"]

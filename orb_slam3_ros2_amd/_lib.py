@@ -55,6 +55,18 @@ class BAResultC(ctypes.Structure):
                 ("iterations_done", ctypes.c_int32), ("lm_trials", ctypes.c_int32)]
 
 
+class PoseProblemC(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("pose_q", ctypes.c_void_p), ("pose_t", ctypes.c_void_p),
+                ("points", ctypes.c_void_p), ("uv", ctypes.c_void_p), ("octave", ctypes.c_void_p),
+                ("inv_sigma2", ctypes.c_void_p), ("n_octaves", ctypes.c_int32), ("fx", ctypes.c_float),
+                ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float)]
+
+
+class PoseResultC(ctypes.Structure):
+    _fields_ = [("pose_q", ctypes.c_float * 4), ("pose_t", ctypes.c_float * 3), ("outlier", ctypes.c_void_p),
+                ("n_inliers", ctypes.c_int32), ("lm_trials", ctypes.c_int32)]
+
+
 # every symbol include/orbhip.h declares (tests check the export table against this list)
 EXPORTED = ["orbhip_abi_version", "orbhip_create", "orbhip_destroy", "orbhip_level_info", "orbhip_max_keypoints",
             "orbhip_extract", "orbhip_extract_batch_device", "orbhip_descriptor_distance", "orbhip_match_bf",
@@ -62,7 +74,8 @@ EXPORTED = ["orbhip_abi_version", "orbhip_create", "orbhip_destroy", "orbhip_lev
             "orbhip_profile_collect", "orbhip_ba_solve", "orbhip_ba_solve_batch", "orbhip_bgr_to_gray_device",
             "orbhip_comm_unique_id", "orbhip_comm_init", "orbhip_ba_solve_sharded", "orbhip_ba_solve_shards_local",
             "orbhip_vocab_create", "orbhip_vocab_load_text", "orbhip_vocab_destroy", "orbhip_vocab_info",
-            "orbhip_bow_transform", "orbhip_bow_transform_device", "orbhip_search_bow"]
+            "orbhip_bow_transform", "orbhip_bow_transform_device", "orbhip_search_bow",
+            "orbhip_pose_optimization", "orbhip_pose_optimization_batch"]
 
 
 def lib():
@@ -111,6 +124,8 @@ def lib():
     L.orbhip_profile_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)]
     L.orbhip_ba_solve.argtypes = [vp, ctypes.POINTER(BAProblemC), ctypes.POINTER(BAResultC), vp]
     L.orbhip_ba_solve_batch.argtypes = [vp, ctypes.POINTER(BAProblemC), i32, ctypes.POINTER(BAResultC), vp]
+    L.orbhip_pose_optimization.argtypes = [vp, ctypes.POINTER(PoseProblemC), ctypes.POINTER(PoseResultC)]
+    L.orbhip_pose_optimization_batch.argtypes = [vp, ctypes.POINTER(PoseProblemC), i32, ctypes.POINTER(PoseResultC)]
     L.orbhip_test_sincosf.argtypes = [vp, vp, vp, ctypes.c_int64]
     L.orbhip_test_sincosf_sweep.argtypes = [ctypes.c_uint32, ctypes.c_uint32, vp, vp]
     L.orbhip_test_sincosf_sweep.restype = ctypes.c_int64

@@ -40,6 +40,7 @@
 #include "ba_chol_blocked.h"
 #include "ba_args.h"
 #include "ba_chol_reg.h"
+#include "ba_se3.h"
 
 namespace orbhip {
 
@@ -69,66 +70,6 @@ __device__ __forceinline__ void ba_xcd_map(int& bx, int& by) {
     int bx_, by_;                                   \
     ba_xcd_map(bx_, by_);                           \
     const BaArgs& a = args[act[by_]];
-
-// ---------------------------------------------------------------------------
-// SE3Quat helpers (Eigen formulas)
-// ---------------------------------------------------------------------------
-struct DQ { double x, y, z, w; };
-
-__device__ __forceinline__ void qrot(const DQ& q, double vx, double vy, double vz, double& ox, double& oy, double& oz) {
-    double ux = q.y * vz - q.z * vy, uy = q.z * vx - q.x * vz, uz = q.x * vy - q.y * vx;
-    ux += ux; uy += uy; uz += uz;
-    const double cx = q.y * uz - q.z * uy, cy = q.z * ux - q.x * uz, cz = q.x * uy - q.y * ux;
-    ox = vx + q.w * ux + cx;
-    oy = vy + q.w * uy + cy;
-    oz = vz + q.w * uz + cz;
-}
-
-__device__ __forceinline__ void qtomat(const DQ& q, double R[9]) {
-    const double tx = 2 * q.x, ty = 2 * q.y, tz = 2 * q.z;
-    const double twx = tx * q.w, twy = ty * q.w, twz = tz * q.w;
-    const double txx = tx * q.x, txy = ty * q.x, txz = tz * q.x;
-    const double tyy = ty * q.y, tyz = tz * q.y, tzz = tz * q.z;
-    R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
-    R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
-    R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
-}
-
-__device__ __forceinline__ DQ mattoq(const double m[9]) {
-    DQ q;
-    double t = m[0] + m[4] + m[8];
-    if (t > 0) {
-        t = sqrt(t + 1.0);
-        q.w = 0.5 * t;
-        t = 0.5 / t;
-        q.x = (m[7] - m[5]) * t;
-        q.y = (m[2] - m[6]) * t;
-        q.z = (m[3] - m[1]) * t;
-    } else {
-        int i = 0;
-        if (m[4] > m[0]) i = 1;
-        if (m[8] > m[3 * i + i]) i = 2;
-        const int j = (i + 1) % 3, k = (j + 1) % 3;
-        t = sqrt(m[3 * i + i] - m[3 * j + j] - m[3 * k + k] + 1.0);
-        double c[3];
-        c[i] = 0.5 * t;
-        t = 0.5 / t;
-        q.w = (m[3 * k + j] - m[3 * j + k]) * t;
-        c[j] = (m[3 * j + i] + m[3 * i + j]) * t;
-        c[k] = (m[3 * k + i] + m[3 * i + k]) * t;
-        q.x = c[0]; q.y = c[1]; q.z = c[2];
-    }
-    return q;
-}
-
-__device__ __forceinline__ void qnormalize(DQ& q) {
-    if (q.w < 0) { q.x = -q.x; q.y = -q.y; q.z = -q.z; q.w = -q.w; }
-    const double n = sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
-    q.x /= n; q.y /= n; q.z /= n; q.w /= n;
-}
-
-__device__ __forceinline__ DQ load_q(const double* p) { return DQ{p[0], p[1], p[2], p[3]}; }
-
 
 // ---------------------------------------------------------------------------
 // errors
@@ -658,42 +599,7 @@ __global__ __launch_bounds__(256) void k_ba_update_poses(const BaArgs* __restric
     for (int k = 0; k < 8; k++) a.pose_bak[8 * p + k] = T[k];
     const int oi = a.opt[p];
     if (oi < 0) return;
-    const double* u = a.x + 6 * oi;
-    // SE3Quat::exp
-    const double ox = u[0], oy = u[1], oz = u[2];
-    const double theta = sqrt(ox * ox + oy * oy + oz * oz);
-    const double O[9] = {0, -oz, oy, oz, 0, -ox, -oy, ox, 0};
-    double O2[9];
-#pragma unroll
-    for (int r = 0; r < 3; r++)
-#pragma unroll
-        for (int c = 0; c < 3; c++) O2[3 * r + c] = O[3 * r] * O[c] + O[3 * r + 1] * O[3 + c] + O[3 * r + 2] * O[6 + c];
-    double R[9], V[9];
-    if (theta < 0.00001) {
-#pragma unroll
-        for (int i = 0; i < 9; i++) { R[i] = (i % 4 == 0 ? 1.0 : 0.0) + O[i] + O2[i]; V[i] = R[i]; }
-    } else {
-        const double sa = sin(theta) / theta, cb = (1 - cos(theta)) / (theta * theta);
-        const double cc = (theta - sin(theta)) / (theta * theta * theta);
-#pragma unroll
-        for (int i = 0; i < 9; i++) {
-            R[i] = (i % 4 == 0 ? 1.0 : 0.0) + sa * O[i] + cb * O2[i];
-            V[i] = (i % 4 == 0 ? 1.0 : 0.0) + cb * O[i] + cc * O2[i];
-        }
-    }
-    DQ qe = mattoq(R);
-    qnormalize(qe);
-    const double tex = V[0] * u[3] + V[1] * u[4] + V[2] * u[5];
-    const double tey = V[3] * u[3] + V[4] * u[4] + V[5] * u[5];
-    const double tez = V[6] * u[3] + V[7] * u[4] + V[8] * u[5];
-    const DQ qt = load_q(T);
-    double rx, ry, rz;
-    qrot(qe, T[4], T[5], T[6], rx, ry, rz);
-    DQ q{qe.w * qt.x + qe.x * qt.w + qe.y * qt.z - qe.z * qt.y, qe.w * qt.y + qe.y * qt.w + qe.z * qt.x - qe.x * qt.z,
-         qe.w * qt.z + qe.z * qt.w + qe.x * qt.y - qe.y * qt.x, qe.w * qt.w - qe.x * qt.x - qe.y * qt.y - qe.z * qt.z};
-    qnormalize(q);
-    T[0] = q.x; T[1] = q.y; T[2] = q.z; T[3] = q.w;
-    T[4] = tex + rx; T[5] = tey + ry; T[6] = tez + rz;
+    se3_update(a.x + 6 * oi, T);
 }
 
 __global__ __launch_bounds__(256) void k_ba_pop(const BaArgs* __restrict__ args, const int* __restrict__ act) {

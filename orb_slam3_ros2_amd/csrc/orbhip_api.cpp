@@ -22,6 +22,7 @@
 
 #include "../../include/orbhip.h"
 #include "orbhip_ba.h"
+#include "pose_opt.h"
 #include "ba_chol_blocked.h"
 #include "orbhip_kernels.h"
 #include "orbhip_plan.h"
@@ -98,6 +99,7 @@ struct orbhip_ctx {
     DevBuf<float> d_mqa, d_mta;
     DevBuf<int32_t> d_mm, d_mb, d_ms, d_mn;
     BaWorkspace* ba = nullptr;
+    PoseWorkspace* pose = nullptr;
     StageTimer timer;
 };
 
@@ -410,6 +412,7 @@ int orbhip_destroy(orbhip_ctx* c) {
     if (c->timer.created)
         for (int i = 0; i < 2 * StageTimer::kCap; i++) (void)hipEventDestroy(c->timer.ev[i]);
     ba_destroy(c->ba);
+    pose_ws_destroy(c->pose);
     c->plans.clear();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -620,6 +623,20 @@ int orbhip_ba_solve_batch(orbhip_ctx* c, const orbhip_ba_problem* probs, int B, 
     std::vector<orbhip_ba_result*> rr(B);
     for (int b = 0; b < B; b++) { pp[b] = probs + b; rr[b] = res + b; }
     return ba_solve_batch(c->ba, pp.data(), B, rr.data(), stop, c->stream, kShardNone);
+}
+
+int orbhip_pose_optimization_batch(orbhip_ctx* c, const orbhip_pose_problem* probs, int B,
+                                   orbhip_pose_result* res) {
+    if (!c || !probs || !res || B <= 0) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    if (!c->pose) c->pose = pose_ws_create();
+    if (!c->pose) return ORBHIP_ERR_DEVICE;
+    return pose_opt_batch(c->pose, probs, B, res, c->stream);
+}
+
+int orbhip_pose_optimization(orbhip_ctx* c, const orbhip_pose_problem* prob, orbhip_pose_result* res) {
+    const int rc = orbhip_pose_optimization_batch(c, prob, 1, res);
+    return rc < 0 ? rc : res->n_inliers;
 }
 
 int orbhip_comm_unique_id(uint8_t* id) {

@@ -14,7 +14,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import BAProblemC, BAResultC, Context, check, lib, ptr
+from ._lib import BAProblemC, BAResultC, Context, PoseProblemC, PoseResultC, check, lib, ptr
 
 TH_HUBER_MONO = float(np.sqrt(np.float32(5.991)))
 
@@ -69,6 +69,43 @@ class BAResult:
     def outlier_edges(self, th: float = 5.991) -> np.ndarray:
         """Edges LocalBundleAdjustment erases: chi2 > 5.991 || !isDepthPositive()."""
         return np.nonzero((self.edge_chi2 > th) | (self.edge_depth_ok == 0))[0]
+
+
+@dataclass
+class PoseProblem:
+    """The g2o problem Optimizer::PoseOptimization(Frame*) builds for one monocular Frame: the
+    initial Tcw and, per matched MapPoint, its world position and the undistorted keypoint."""
+    pose_q: np.ndarray          # [4] float32 (x,y,z,w), pFrame->GetPose() rotation
+    pose_t: np.ndarray          # [3] float32
+    points: np.ndarray          # [N,3] float32 MapPoint::GetWorldPos
+    uv: np.ndarray              # [N,2] float32 mvKeysUn[i].pt
+    octave: np.ndarray          # [N] int32 mvKeysUn[i].octave
+    inv_sigma2: np.ndarray      # [L] float32 mvInvLevelSigma2
+    fx: float
+    fy: float
+    cx: float
+    cy: float
+
+    def normalized(self) -> "PoseProblem":
+        c = lambda a, dt: np.ascontiguousarray(a, dtype=dt)  # noqa: E731
+        return PoseProblem(c(self.pose_q, np.float32).reshape(4), c(self.pose_t, np.float32).reshape(3),
+                           c(self.points, np.float32).reshape(-1, 3), c(self.uv, np.float32).reshape(-1, 2),
+                           c(self.octave, np.int32).reshape(-1), c(self.inv_sigma2, np.float32),
+                           float(self.fx), float(self.fy), float(self.cx), float(self.cy))
+
+    def to_c(self) -> PoseProblemC:
+        return PoseProblemC(self.points.shape[0], ptr(self.pose_q), ptr(self.pose_t), ptr(self.points), ptr(self.uv),
+                            ptr(self.octave), ptr(self.inv_sigma2), self.inv_sigma2.shape[0], self.fx, self.fy,
+                            self.cx, self.cy)
+
+
+@dataclass
+class PoseResult:
+    pose_q: np.ndarray          # optimised Tcw
+    pose_t: np.ndarray
+    outlier: np.ndarray         # [N] uint8: mvbOutlier
+    n_inliers: int              # PoseOptimization return value
+    lm_trials: int
 
 
 class Optimizer:
@@ -165,3 +202,21 @@ class Optimizer:
         p = BAProblem(**{**prob.__dict__, "iterations": nIterations,
                          "huber_delta": float(np.sqrt(5.99)) if bRobust else 0.0})
         return self.solve(p, stop_flag)
+
+    # ---- motion-only BA ----
+    def PoseOptimization(self, prob: PoseProblem) -> PoseResult:
+        """U:src/Optimizer.cc::Optimizer::PoseOptimization(Frame*) for one frame."""
+        return self.PoseOptimization_batch([prob])[0]
+
+    def PoseOptimization_batch(self, probs) -> list:
+        """Several frames in one launch (one wavefront per frame)."""
+        ps = [p.normalized() for p in probs]
+        outl = [np.zeros(p.points.shape[0], np.uint8) for p in ps]
+        cprobs = (PoseProblemC * len(ps))(*[p.to_c() for p in ps])
+        cres = (PoseResultC * len(ps))()
+        for i, o in enumerate(outl):
+            cres[i].outlier = ptr(o)
+        check(lib().orbhip_pose_optimization_batch(self.ctx.handle, cprobs, len(ps), cres),
+              "orbhip_pose_optimization_batch")
+        return [PoseResult(np.array(r.pose_q[:], np.float32), np.array(r.pose_t[:], np.float32), o, r.n_inliers,
+                           r.lm_trials) for r, o in zip(cres, outl)]

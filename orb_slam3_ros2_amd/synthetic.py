@@ -156,3 +156,35 @@ def synthetic_ba_problem(n_kf=50, n_pts=2000, obs_per_pt=4, seed=7, layout="arc"
                      np.float32(cam["fy"]), np.float32(cam["cx"]), np.float32(cam["cy"]), TH_HUBER_MONO, 10, 0)
     gt = dict(R=Rs, t=ts, points=pts)
     return prob, gt
+
+
+def synthetic_pose_problem(n=600, outlier_frac=0.15, seed=3, rot_noise=0.02, trans_noise=0.05, n_levels=8,
+                           scale_factor=1.2):
+    """A tracked monocular Frame for PoseOptimization: a camera looking at map points 2-6 m away,
+    keypoints = projections + 1.2^octave px noise, a fraction replaced by gross mismatches
+    (uniform in the image), initial pose perturbed like a constant-velocity prediction.
+    Returns (PoseProblem, ground truth dict)."""
+    from .optimizer import PoseProblem
+    rng = np.random.Generator(np.random.PCG64(seed))
+    cam = D435I
+    R = _rodrigues(rng.normal(size=3) * 0.3)
+    t = rng.normal(size=3) * 0.5
+    # points in front of the camera, inside the image
+    z = rng.uniform(2.0, 6.0, size=n)
+    u = rng.uniform(20, 620, size=n)
+    v = rng.uniform(20, 460, size=n)
+    Xc = np.stack([(u - cam["cx"]) / cam["fx"] * z, (v - cam["cy"]) / cam["fy"] * z, z], 1)
+    Xw = (Xc - t) @ R          # R^T (Xc - t)
+    octave = rng.integers(0, n_levels, size=n).astype(np.int32)
+    scales = np.ones(n_levels, np.float32)
+    for i in range(1, n_levels):
+        scales[i] = np.float32(np.float64(scales[i - 1]) * np.float64(np.float32(scale_factor)))
+    inv_sigma2 = (np.float32(1.0) / (scales * scales)).astype(np.float32)
+    uv = np.stack([u, v], 1) + rng.normal(size=(n, 2)) * np.power(np.float64(scale_factor), octave)[:, None]
+    bad = rng.random(n) < outlier_frac
+    uv[bad] = np.stack([rng.uniform(0, 640, bad.sum()), rng.uniform(0, 480, bad.sum())], 1)
+    R0 = _rodrigues(rng.normal(size=3) * rot_noise) @ R
+    t0 = t + rng.normal(size=3) * trans_noise
+    prob = PoseProblem(_mat_to_quat(R0).astype(np.float32), t0.astype(np.float32), Xw.astype(np.float32),
+                       uv.astype(np.float32), octave, inv_sigma2, cam["fx"], cam["fy"], cam["cx"], cam["cy"])
+    return prob, dict(R=R, t=t, bad=bad)
