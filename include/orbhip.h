@@ -185,6 +185,60 @@ int orbhip_ba_solve(orbhip_ctx* ctx, const orbhip_ba_problem* prob, orbhip_ba_re
 int orbhip_ba_solve_batch(orbhip_ctx* ctx, const orbhip_ba_problem* probs, int B, orbhip_ba_result* res,
                           const volatile int* stop_flag);
 
+/* ---- projection-guided matching ---------------------------
+ * The current Frame as U:src/Frame.cc holds it after extraction: keypoints mvKeysUn (= mvKeys,
+ * distortion k1 == 0), descriptors, image bounds mnMinX..mnMaxY (ComputeImageBounds), the
+ * 64 x 48 grid implied by them (AssignFeaturesToGrid / PosInGrid / GetFeaturesInArea), the
+ * scale tables and the pose Tcw. claimed[k] = mvpMapPoints[k] set (with observations) before
+ * the call (NULL: none). At most 65535 keypoints. */
+typedef struct {
+    int32_t n;
+    const orbhip_kp* kps;       /* n: mvKeysUn */
+    const uint8_t* desc;        /* n x 32: mDescriptors */
+    const uint8_t* claimed;     /* n or NULL */
+    float min_x, max_x, min_y, max_y;
+    const float* scale_factors; /* mvScaleFactors */
+    int32_t n_levels;
+    float log_scale_factor;     /* mfLogScaleFactor */
+    float fx, fy, cx, cy;       /* Pinhole mvParameters */
+    float pose_q[4];            /* Tcw rotation (x, y, z, w) */
+    float pose_t[3];
+} orbhip_frame;
+
+/* U:src/ORBmatcher.cc::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th,
+ * bMono = true) (TrackWithMotionModel). Queries: LastFrame entries i with a MapPoint that is
+ * not an outlier, in index order: world position, pMP->GetDescriptor(), LastFrame keypoint
+ * octave and angle. match[q] = CurrentFrame keypoint assigned to query q (the adapter sets
+ * CurrentFrame.mvpMapPoints[match[q]] = pMP) or -1. Returns nmatches. */
+typedef struct {
+    int32_t n;
+    const float* points;        /* n x 3 */
+    const uint8_t* desc;        /* n x 32 */
+    const int32_t* octave;      /* n */
+    const float* angle;         /* n: LastFrame.mvKeysUn[i].angle */
+} orbhip_proj_last;
+int orbhip_search_by_projection_last(orbhip_ctx* ctx, const orbhip_frame* cur, const orbhip_proj_last* last,
+                                     float th, int check_orientation, int32_t* match);
+
+/* U:src/Tracking.cc::SearchLocalPoints: Frame::isInFrustum(pMP, view_cos_limit = 0.5) for every
+ * local MapPoint not skipped, then U:src/ORBmatcher.cc::SearchByProjection(F, vpMapPoints, th,
+ * bFarPoints, thFarPoints) in vpMapPoints order. Per point: GetWorldPos, GetNormal,
+ * mfMinDistance, mfMaxDistance, GetDescriptor; skip[m] = bad / already matched in this frame.
+ * Outputs: in_view[m] = mbTrackInView, level[m] = mnTrackScaleLevel, match[m] = F keypoint or -1.
+ * Returns nmatches. */
+typedef struct {
+    int32_t n;
+    const float* points;        /* n x 3 */
+    const float* normals;       /* n x 3 */
+    const float* min_dist;      /* n: mfMinDistance */
+    const float* max_dist;      /* n: mfMaxDistance */
+    const uint8_t* desc;        /* n x 32 */
+    const uint8_t* skip;        /* n or NULL */
+} orbhip_local_points;
+int orbhip_search_local_points(orbhip_ctx* ctx, const orbhip_frame* frame, const orbhip_local_points* mps,
+                               float view_cos_limit, float th, float nnratio, int far_points, float th_far,
+                               uint8_t* in_view, int32_t* level, int32_t* match);
+
 /* ---- motion-only bundle adjustment -------------------------
  * U:src/Optimizer.cc::Optimizer::PoseOptimization(Frame* pFrame), monocular observations:
  * one VertexSE3Expmap (Tcw), EdgeSE3ProjectXYZOnlyPose per matched MapPoint (information

@@ -1,0 +1,273 @@
+// ============================================================================
+// ORACLE — TEST INFRASTRUCTURE ONLY (see orb_oracle.cpp header for the rules).
+//
+// CPU restatement of the projection-guided matchers, float semantics as
+// the reference computes them (recalled upstream; the ORB_SLAM3 submodule is empty here):
+//   U:src/Frame.cc::Frame::AssignFeaturesToGrid / PosInGrid   FRAME_GRID_COLS 64 x ROWS 48,
+//       mfGridElementWidthInv = 64.f / (mnMaxX - mnMinX), cell = round((pt - min) * inv)
+//   U:src/Frame.cc::Frame::GetFeaturesInArea(x, y, r, minLevel, maxLevel)   cells ix (outer),
+//       iy, then cell order; |dx| < r && |dy| < r
+//   U:src/Frame.cc::Frame::isInFrustum(pMP, viewingCosLimit)   Pc = mRcw P + mtcw, project,
+//       bounds, 0.8 minDist / 1.2 maxDist, viewCos, MapPoint::PredictScale (ceil(log(ratio) /
+//       mfLogScaleFactor), clamped)
+//   U:src/ORBmatcher.cc::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, th,
+//       bMono = true)   window th * scale[lastOctave], levels lastOctave-1 .. lastOctave+1, best
+//       Hamming (strict <, first wins) <= TH_HIGH = 100, greedy claims in LastFrame index order,
+//       30-bin rotation histogram + ComputeThreeMaxima
+//   U:src/ORBmatcher.cc::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoints, th,
+//       bFarPoints, thFarPoints)   RadiusByViewingCos (2.5 if viewCos > 0.998, else 4.0; x th
+//       when th != 1), levels predicted-1 .. predicted, best/second with levels, ratio test only
+//       when both lie on the same level; greedy claims in vpMapPoints order
+// Pose arithmetic: Sophus SE3f * p = q._transformVector(p) + t (Eigen, float); mRcw =
+// q.toRotationMatrix(); mOw = Twc.translation() = conj(q)._transformVector(-t). No FMA
+// contraction (-ffp-contract=off). Undistortion is the identity (mDistCoef k1 == 0, the
+// RealSense_D435i.yaml case): mvKeysUn = mvKeys, bounds [0, cols] x [0, rows].
+// PARITY UNPINNED by the reference (no fixtures upstream).
+// ============================================================================
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+namespace proj {
+
+constexpr int kCols = 64, kRows = 48, TH_HIGH = 100, HISTO_LENGTH = 30;
+
+struct Kp { float x, y, size, angle, response; int32_t octave; };   // orbhip_kp layout
+
+struct Frame {
+    int n;
+    const Kp* kps;
+    const uint8_t* desc;
+    float minx, maxx, miny, maxy, invw, invh;
+    std::vector<int> grid[kCols][kRows];
+    void build() {
+        invw = (float)kCols / (maxx - minx);
+        invh = (float)kRows / (maxy - miny);
+        for (int i = 0; i < n; i++) {
+            const int px = (int)std::round((kps[i].x - minx) * invw);
+            const int py = (int)std::round((kps[i].y - miny) * invh);
+            if (px < 0 || px >= kCols || py < 0 || py >= kRows) continue;
+            grid[px][py].push_back(i);
+        }
+    }
+    void features_in_area(float x, float y, float r, int minLevel, int maxLevel, std::vector<int>& out) const {
+        out.clear();
+        const int nMinCellX = std::max(0, (int)std::floor((x - minx - r) * invw));
+        if (nMinCellX >= kCols) return;
+        const int nMaxCellX = std::min(kCols - 1, (int)std::ceil((x - minx + r) * invw));
+        if (nMaxCellX < 0) return;
+        const int nMinCellY = std::max(0, (int)std::floor((y - miny - r) * invh));
+        if (nMinCellY >= kRows) return;
+        const int nMaxCellY = std::min(kRows - 1, (int)std::ceil((y - miny + r) * invh));
+        if (nMaxCellY < 0) return;
+        const bool bCheckLevels = (minLevel > 0) || (maxLevel >= 0);
+        for (int ix = nMinCellX; ix <= nMaxCellX; ix++)
+            for (int iy = nMinCellY; iy <= nMaxCellY; iy++)
+                for (int j : grid[ix][iy]) {
+                    const Kp& k = kps[j];
+                    if (bCheckLevels) {
+                        if (k.octave < minLevel) continue;
+                        if (maxLevel >= 0 && k.octave > maxLevel) continue;
+                    }
+                    const float dx = k.x - x, dy = k.y - y;
+                    if (std::fabs(dx) < r && std::fabs(dy) < r) out.push_back(j);
+                }
+    }
+};
+
+static inline int hamming(const uint8_t* a, const uint8_t* b) {
+    int d = 0;
+    for (int i = 0; i < 32; i++) d += __builtin_popcount((unsigned)(a[i] ^ b[i]));
+    return d;
+}
+
+// Eigen QuaternionBase::_transformVector, float
+static inline void qrot(const float q[4], const float v[3], float o[3]) {
+    float uv[3] = {q[1] * v[2] - q[2] * v[1], q[2] * v[0] - q[0] * v[2], q[0] * v[1] - q[1] * v[0]};
+    uv[0] += uv[0]; uv[1] += uv[1]; uv[2] += uv[2];
+    const float c[3] = {q[1] * uv[2] - q[2] * uv[1], q[2] * uv[0] - q[0] * uv[2], q[0] * uv[1] - q[1] * uv[0]};
+    o[0] = v[0] + q[3] * uv[0] + c[0];
+    o[1] = v[1] + q[3] * uv[1] + c[1];
+    o[2] = v[2] + q[3] * uv[2] + c[2];
+}
+
+static inline void qtomat(const float q[4], float R[9]) {   // Eigen toRotationMatrix, float
+    const float tx = 2 * q[0], ty = 2 * q[1], tz = 2 * q[2];
+    const float twx = tx * q[3], twy = ty * q[3], twz = tz * q[3];
+    const float txx = tx * q[0], txy = ty * q[0], txz = tz * q[0];
+    const float tyy = ty * q[1], tyz = tz * q[1], tzz = tz * q[2];
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz; R[2] = txz + twy;
+    R[3] = txy + twz; R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy; R[7] = tyz + twx; R[8] = 1 - (txx + tyy);
+}
+
+static void three_maxima(const int* h, int& i1, int& i2, int& i3) {
+    int m1 = 0, m2 = 0, m3 = 0;
+    i1 = i2 = i3 = -1;
+    for (int i = 0; i < HISTO_LENGTH; i++) {
+        const int s = h[i];
+        if (s > m1) { m3 = m2; m2 = m1; m1 = s; i3 = i2; i2 = i1; i1 = i; }
+        else if (s > m2) { m3 = m2; m2 = s; i3 = i2; i2 = i; }
+        else if (s > m3) { m3 = s; i3 = i; }
+    }
+    if (m2 < 0.1f * (float)m1) { i2 = -1; i3 = -1; }
+    else if (m3 < 0.1f * (float)m1) { i3 = -1; }
+}
+
+}  // namespace proj
+
+extern "C" {
+
+// SearchByProjection(CurrentFrame, LastFrame, th, bMono = true). Queries: the LastFrame entries
+// with a non-outlier MapPoint, in index order (world position, MapPoint descriptor, last-frame
+// keypoint octave and angle). claimed[k]: CurrentFrame.mvpMapPoints[k] already set (with
+// observations) before the call. match[i] = current keypoint or -1. Returns nmatches.
+int orc_search_by_projection_last(int n_cur, const void* cur_kps, const uint8_t* cur_desc, const uint8_t* claimed,
+                                  float minx, float maxx, float miny, float maxy, const float* scale_factors,
+                                  const float* q, const float* t, float fx, float fy, float cx, float cy, int n_last,
+                                  const float* pts, const uint8_t* mp_desc, const int32_t* last_octave,
+                                  const float* last_angle, float th, int check_orientation, int32_t* match) {
+    proj::Frame F;
+    F.n = n_cur; F.kps = (const proj::Kp*)cur_kps; F.desc = cur_desc;
+    F.minx = minx; F.maxx = maxx; F.miny = miny; F.maxy = maxy;
+    F.build();
+    std::vector<uint8_t> taken(n_cur, 0);
+    if (claimed) for (int k = 0; k < n_cur; k++) taken[k] = claimed[k];
+    std::vector<int> cand, bin(n_last, -1);
+    int hist[proj::HISTO_LENGTH] = {0};
+    const float factor = 1.0f / proj::HISTO_LENGTH;
+    int nmatches = 0;
+    for (int i = 0; i < n_last; i++) {
+        match[i] = -1;
+        float Xc[3];
+        proj::qrot(q, &pts[3 * i], Xc);
+        Xc[0] += t[0]; Xc[1] += t[1]; Xc[2] += t[2];
+        const float invzc = 1.0 / Xc[2];
+        if (invzc < 0) continue;
+        const float u = fx * Xc[0] / Xc[2] + cx, v = fy * Xc[1] / Xc[2] + cy;
+        if (u < minx || u > maxx || v < miny || v > maxy) continue;
+        const int lo = last_octave[i];
+        const float radius = th * scale_factors[lo];
+        F.features_in_area(u, v, radius, lo - 1, lo + 1, cand);
+        if (cand.empty()) continue;
+        int bestDist = 256, bestIdx2 = -1;
+        for (int i2 : cand) {
+            if (taken[i2]) continue;
+            const int dist = proj::hamming(&mp_desc[32 * i], &cur_desc[32 * i2]);
+            if (dist < bestDist) { bestDist = dist; bestIdx2 = i2; }
+        }
+        if (bestDist <= proj::TH_HIGH) {
+            taken[bestIdx2] = 1;
+            match[i] = bestIdx2;
+            nmatches++;
+            if (check_orientation) {
+                float rot = last_angle[i] - F.kps[bestIdx2].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int b = (int)std::round(rot * factor);
+                if (b == proj::HISTO_LENGTH) b = 0;
+                bin[i] = b;
+                hist[b]++;
+            }
+        }
+    }
+    if (check_orientation) {
+        int i1, i2, i3;
+        proj::three_maxima(hist, i1, i2, i3);
+        for (int i = 0; i < n_last; i++)
+            if (match[i] >= 0 && bin[i] != i1 && bin[i] != i2 && bin[i] != i3) { match[i] = -1; nmatches--; }
+    }
+    return nmatches;
+}
+
+// Frame::isInFrustum(pMP, view_cos_limit) for every local MapPoint not skipped, then
+// SearchByProjection(F, vpMapPoints, th, bFarPoints, thFarPoints). Per point: world position,
+// normal, mfMinDistance, mfMaxDistance, descriptor; skip[m] = already matched in this frame /
+// bad (mbTrackInView stays false). Outputs in_view (mbTrackInView), level (mnTrackScaleLevel),
+// match (frame keypoint or -1). Returns nmatches.
+int orc_search_local_points(int n_cur, const void* cur_kps, const uint8_t* cur_desc, const uint8_t* claimed,
+                            float minx, float maxx, float miny, float maxy, const float* scale_factors, int n_levels,
+                            float log_scale_factor, const float* q, const float* t, float fx, float fy, float cx,
+                            float cy, int n_mp, const float* pts, const float* normals, const float* min_dist,
+                            const float* max_dist, const uint8_t* mp_desc, const uint8_t* skip, float view_cos_limit,
+                            float th, float nnratio, int far_points, float th_far, uint8_t* in_view, int32_t* level,
+                            int32_t* match) {
+    proj::Frame F;
+    F.n = n_cur; F.kps = (const proj::Kp*)cur_kps; F.desc = cur_desc;
+    F.minx = minx; F.maxx = maxx; F.miny = miny; F.maxy = maxy;
+    F.build();
+    std::vector<uint8_t> taken(n_cur, 0);
+    if (claimed) for (int k = 0; k < n_cur; k++) taken[k] = claimed[k];
+    float R[9];
+    proj::qtomat(q, R);
+    const float qc[4] = {-q[0], -q[1], -q[2], q[3]};
+    const float mt[3] = {t[0] * -1.0f, t[1] * -1.0f, t[2] * -1.0f};
+    float Ow[3];
+    proj::qrot(qc, mt, Ow);
+    std::vector<float> projx(n_mp), projy(n_mp), vcos(n_mp), depth(n_mp);
+    // ---- isInFrustum ----
+    for (int m = 0; m < n_mp; m++) {
+        in_view[m] = 0; level[m] = -1; match[m] = -1;
+        if (skip && skip[m]) continue;
+        const float* P = &pts[3 * m];
+        const float Pc[3] = {R[0] * P[0] + R[1] * P[1] + R[2] * P[2] + t[0],
+                             R[3] * P[0] + R[4] * P[1] + R[5] * P[2] + t[1],
+                             R[6] * P[0] + R[7] * P[1] + R[8] * P[2] + t[2]};
+        const float Pc_dist = std::sqrt(Pc[0] * Pc[0] + Pc[1] * Pc[1] + Pc[2] * Pc[2]);
+        if (Pc[2] < 0.0f) continue;
+        const float u = fx * Pc[0] / Pc[2] + cx, v = fy * Pc[1] / Pc[2] + cy;
+        if (u < minx || u > maxx) continue;
+        if (v < miny || v > maxy) continue;
+        const float PO[3] = {P[0] - Ow[0], P[1] - Ow[1], P[2] - Ow[2]};
+        const float dist = std::sqrt(PO[0] * PO[0] + PO[1] * PO[1] + PO[2] * PO[2]);
+        const float maxDistance = 1.2f * max_dist[m], minDistance = 0.8f * min_dist[m];
+        if (dist < minDistance || dist > maxDistance) continue;
+        const float* Pn = &normals[3 * m];
+        const float viewCos = (PO[0] * Pn[0] + PO[1] * Pn[1] + PO[2] * Pn[2]) / dist;
+        if (viewCos < view_cos_limit) continue;
+        const float ratio = max_dist[m] / dist;
+        int nScale = (int)std::ceil(std::log(ratio) / log_scale_factor);
+        if (nScale < 0) nScale = 0;
+        else if (nScale >= n_levels) nScale = n_levels - 1;
+        in_view[m] = 1; level[m] = nScale;
+        projx[m] = u; projy[m] = v; vcos[m] = viewCos; depth[m] = Pc_dist;
+    }
+    // ---- SearchByProjection ----
+    const bool bFactor = th != 1.0;
+    std::vector<int> cand;
+    int nmatches = 0;
+    for (int m = 0; m < n_mp; m++) {
+        if (!in_view[m]) continue;
+        if (far_points && depth[m] > th_far) continue;
+        const int nPredictedLevel = level[m];
+        float r = vcos[m] > 0.998 ? 2.5 : 4.0;   // RadiusByViewingCos
+        if (bFactor) r *= th;
+        F.features_in_area(projx[m], projy[m], r * scale_factors[nPredictedLevel], nPredictedLevel - 1,
+                           nPredictedLevel, cand);
+        if (cand.empty()) continue;
+        int bestDist = 256, bestLevel = -1, bestDist2 = 256, bestLevel2 = -1, bestIdx = -1;
+        for (int idx : cand) {
+            if (taken[idx]) continue;
+            const int dist = proj::hamming(&mp_desc[32 * m], &cur_desc[32 * idx]);
+            if (dist < bestDist) {
+                bestDist2 = bestDist; bestDist = dist;
+                bestLevel2 = bestLevel; bestLevel = F.kps[idx].octave;
+                bestIdx = idx;
+            } else if (dist < bestDist2) {
+                bestLevel2 = F.kps[idx].octave;
+                bestDist2 = dist;
+            }
+        }
+        if (bestDist <= proj::TH_HIGH) {
+            if (bestLevel == bestLevel2 && bestDist > nnratio * bestDist2) continue;
+            if (bestLevel != bestLevel2 || bestDist <= nnratio * bestDist2) {
+                taken[bestIdx] = 1;
+                match[m] = bestIdx;
+                nmatches++;
+            }
+        }
+    }
+    return nmatches;
+}
+
+}  // extern "C"

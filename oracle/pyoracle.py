@@ -58,6 +58,14 @@ def lib():
                                      c_int, _i32p]
         L.orc_pose_optimization.argtypes = [c_int, _f32p, _f32p, _f32p, _f32p, _i32p, _f32p, c_float, c_float,
                                             c_float, c_float, c_float, _f32p, _f32p, _u8p, _f64]
+        vp = ctypes.c_void_p
+        L.orc_search_by_projection_last.argtypes = [c_int, vp, _u8p, vp, c_float, c_float, c_float, c_float, _f32p,
+                                                    _f32p, _f32p, c_float, c_float, c_float, c_float, c_int, _f32p,
+                                                    _u8p, _i32p, _f32p, c_float, c_int, _i32p]
+        L.orc_search_local_points.argtypes = [c_int, vp, _u8p, vp, c_float, c_float, c_float, c_float, _f32p, c_int,
+                                              c_float, _f32p, _f32p, c_float, c_float, c_float, c_float, c_int,
+                                              _f32p, _f32p, _f32p, _f32p, _u8p, vp, c_float, c_float, c_float, c_int,
+                                              c_float, _u8p, _i32p, _i32p]
         L.orc_bgr2gray.argtypes = [_u8p, c_int, c_int, c_int, _u8p, c_int]
         L.orc_glibc_sincosf_range.argtypes = [ctypes.c_uint32, ctypes.c_uint32, _f32p, _f32p]
         _lib = L
@@ -210,3 +218,36 @@ def pose_optimization(prob):
     nin = lib().orc_pose_optimization(n, p.pose_q, p.pose_t, p.points, p.uv, p.octave, p.inv_sigma2, p.fx, p.fy,
                                       p.cx, p.cy, float(np.float32(np.sqrt(5.991))), oq, ot, ol, st)
     return dict(pose_q=oq, pose_t=ot, outlier=ol, n_inliers=int(nin), lm_trials=int(st[0]))
+
+
+def _vp(a):
+    return None if a is None else a.ctypes.data
+
+
+def search_by_projection_last(frame, points, mp_desc, last_octave, last_angle, th=15.0, check_orientation=True):
+    """Oracle SearchByProjection(CurrentFrame, LastFrame, th, bMono) on a matcher.ProjFrame."""
+    pts = np.ascontiguousarray(points, np.float32).reshape(-1, 3)
+    match = np.full(pts.shape[0], -1, np.int32)
+    n = lib().orc_search_by_projection_last(
+        frame.kps.shape[0], _vp(frame.kps), frame.desc, _vp(frame.claimed), *frame.bounds, frame.scale_factors,
+        frame.pose_q, frame.pose_t, frame.fx, frame.fy, frame.cx, frame.cy, pts.shape[0], pts,
+        np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32), np.ascontiguousarray(last_octave, np.int32),
+        np.ascontiguousarray(last_angle, np.float32), th, int(check_orientation), match)
+    return n, match
+
+
+def search_local_points(frame, points, normals, min_dist, max_dist, mp_desc, skip=None, th=1.0, nnratio=0.8,
+                        view_cos_limit=0.5, far_points=False, th_far=0.0):
+    """Oracle isInFrustum + SearchByProjection(F, vpMapPoints, th, bFarPoints, thFarPoints)."""
+    pts = np.ascontiguousarray(points, np.float32).reshape(-1, 3)
+    m = pts.shape[0]
+    match = np.full(m, -1, np.int32); in_view = np.zeros(m, np.uint8); level = np.full(m, -1, np.int32)
+    sk = None if skip is None else np.ascontiguousarray(skip, np.uint8)
+    n = lib().orc_search_local_points(
+        frame.kps.shape[0], _vp(frame.kps), frame.desc, _vp(frame.claimed), *frame.bounds, frame.scale_factors,
+        len(frame.scale_factors), frame.log_scale_factor, frame.pose_q, frame.pose_t, frame.fx, frame.fy, frame.cx,
+        frame.cy, m, pts, np.ascontiguousarray(normals, np.float32).reshape(-1, 3),
+        np.ascontiguousarray(min_dist, np.float32), np.ascontiguousarray(max_dist, np.float32),
+        np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32), _vp(sk), view_cos_limit, th, nnratio,
+        int(far_points), th_far, in_view, level, match)
+    return n, match, in_view, level

@@ -67,6 +67,25 @@ class PoseResultC(ctypes.Structure):
                 ("n_inliers", ctypes.c_int32), ("lm_trials", ctypes.c_int32)]
 
 
+class FrameC(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("kps", ctypes.c_void_p), ("desc", ctypes.c_void_p), ("claimed", ctypes.c_void_p),
+                ("min_x", ctypes.c_float), ("max_x", ctypes.c_float), ("min_y", ctypes.c_float), ("max_y", ctypes.c_float),
+                ("scale_factors", ctypes.c_void_p), ("n_levels", ctypes.c_int32), ("log_scale_factor", ctypes.c_float),
+                ("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
+                ("pose_q", ctypes.c_float * 4), ("pose_t", ctypes.c_float * 3)]
+
+
+class ProjLastC(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("points", ctypes.c_void_p), ("desc", ctypes.c_void_p),
+                ("octave", ctypes.c_void_p), ("angle", ctypes.c_void_p)]
+
+
+class LocalPointsC(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("points", ctypes.c_void_p), ("normals", ctypes.c_void_p),
+                ("min_dist", ctypes.c_void_p), ("max_dist", ctypes.c_void_p), ("desc", ctypes.c_void_p),
+                ("skip", ctypes.c_void_p)]
+
+
 # every symbol include/orbhip.h declares (tests check the export table against this list)
 EXPORTED = ["orbhip_abi_version", "orbhip_create", "orbhip_destroy", "orbhip_level_info", "orbhip_max_keypoints",
             "orbhip_extract", "orbhip_extract_batch_device", "orbhip_descriptor_distance", "orbhip_match_bf",
@@ -75,7 +94,8 @@ EXPORTED = ["orbhip_abi_version", "orbhip_create", "orbhip_destroy", "orbhip_lev
             "orbhip_comm_unique_id", "orbhip_comm_init", "orbhip_ba_solve_sharded", "orbhip_ba_solve_shards_local",
             "orbhip_vocab_create", "orbhip_vocab_load_text", "orbhip_vocab_destroy", "orbhip_vocab_info",
             "orbhip_bow_transform", "orbhip_bow_transform_device", "orbhip_search_bow",
-            "orbhip_pose_optimization", "orbhip_pose_optimization_batch"]
+            "orbhip_pose_optimization", "orbhip_pose_optimization_batch", "orbhip_search_by_projection_last",
+            "orbhip_search_local_points"]
 
 
 def lib():
@@ -126,6 +146,10 @@ def lib():
     L.orbhip_ba_solve_batch.argtypes = [vp, ctypes.POINTER(BAProblemC), i32, ctypes.POINTER(BAResultC), vp]
     L.orbhip_pose_optimization.argtypes = [vp, ctypes.POINTER(PoseProblemC), ctypes.POINTER(PoseResultC)]
     L.orbhip_pose_optimization_batch.argtypes = [vp, ctypes.POINTER(PoseProblemC), i32, ctypes.POINTER(PoseResultC)]
+    L.orbhip_search_by_projection_last.argtypes = [vp, ctypes.POINTER(FrameC), ctypes.POINTER(ProjLastC), f32, i32,
+                                                   vp]
+    L.orbhip_search_local_points.argtypes = [vp, ctypes.POINTER(FrameC), ctypes.POINTER(LocalPointsC), f32, f32, f32,
+                                             i32, f32, vp, vp, vp]
     L.orbhip_test_sincosf.argtypes = [vp, vp, vp, ctypes.c_int64]
     L.orbhip_test_sincosf_sweep.argtypes = [ctypes.c_uint32, ctypes.c_uint32, vp, vp]
     L.orbhip_test_sincosf_sweep.restype = ctypes.c_int64

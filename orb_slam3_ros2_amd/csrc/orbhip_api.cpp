@@ -23,6 +23,7 @@
 #include "../../include/orbhip.h"
 #include "orbhip_ba.h"
 #include "pose_opt.h"
+#include "proj.h"
 #include "ba_chol_blocked.h"
 #include "orbhip_kernels.h"
 #include "orbhip_plan.h"
@@ -100,6 +101,7 @@ struct orbhip_ctx {
     DevBuf<int32_t> d_mm, d_mb, d_ms, d_mn;
     BaWorkspace* ba = nullptr;
     PoseWorkspace* pose = nullptr;
+    ProjWorkspace* proj = nullptr;
     StageTimer timer;
 };
 
@@ -413,6 +415,7 @@ int orbhip_destroy(orbhip_ctx* c) {
         for (int i = 0; i < 2 * StageTimer::kCap; i++) (void)hipEventDestroy(c->timer.ev[i]);
     ba_destroy(c->ba);
     pose_ws_destroy(c->pose);
+    proj_ws_destroy(c->proj);
     c->plans.clear();
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -637,6 +640,24 @@ int orbhip_pose_optimization_batch(orbhip_ctx* c, const orbhip_pose_problem* pro
 int orbhip_pose_optimization(orbhip_ctx* c, const orbhip_pose_problem* prob, orbhip_pose_result* res) {
     const int rc = orbhip_pose_optimization_batch(c, prob, 1, res);
     return rc < 0 ? rc : res->n_inliers;
+}
+
+int orbhip_search_by_projection_last(orbhip_ctx* c, const orbhip_frame* cur, const orbhip_proj_last* last,
+                                     float th, int check_orientation, int32_t* match) {
+    if (!c) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    if (!c->proj) c->proj = proj_ws_create();
+    return proj_search_last(c->proj, cur, last, th, check_orientation, match, nullptr, c->stream);
+}
+
+int orbhip_search_local_points(orbhip_ctx* c, const orbhip_frame* frame, const orbhip_local_points* mps,
+                               float view_cos_limit, float th, float nnratio, int far_points, float th_far,
+                               uint8_t* in_view, int32_t* level, int32_t* match) {
+    if (!c) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    if (!c->proj) c->proj = proj_ws_create();
+    return proj_search_local(c->proj, frame, mps, view_cos_limit, th, nnratio, far_points, th_far, in_view, level,
+                             match, nullptr, c->stream);
 }
 
 int orbhip_comm_unique_id(uint8_t* id) {

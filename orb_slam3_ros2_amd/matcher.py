@@ -12,7 +12,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import torch_stream, Context, check, lib, ptr
+from ._lib import (KP_DTYPE, FrameC, LocalPointsC, ProjLastC, torch_stream, Context, check, lib, ptr)
 
 
 class ORBmatcher:
@@ -75,3 +75,76 @@ class ORBmatcher:
                                           int(self.mbCheckOrientation), th, ptr(m)), "orbhip_search_bow")
         return n, m
 
+    # ---- projection-guided matching ----
+    def SearchByProjectionLastFrame(self, frame: "ProjFrame", points, mp_desc, last_octave, last_angle,
+                                    th: float = 15.0):
+        """U:src/ORBmatcher.cc::SearchByProjection(CurrentFrame, LastFrame, th, bMono=true).
+        Queries = LastFrame entries with a non-outlier MapPoint (index order). Returns
+        (nmatches, match[q] = CurrentFrame keypoint or -1)."""
+        pts = np.ascontiguousarray(points, np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
+        oc = np.ascontiguousarray(last_octave, np.int32)
+        an = np.ascontiguousarray(last_angle, np.float32)
+        match = np.full(pts.shape[0], -1, np.int32)
+        fc = frame.to_c()
+        lc = ProjLastC(pts.shape[0], ptr(pts), ptr(d), ptr(oc), ptr(an))
+        n = check(lib().orbhip_search_by_projection_last(self.ctx.handle, ctypes.byref(fc), ctypes.byref(lc),
+                                                         float(th), int(self.mbCheckOrientation), ptr(match)),
+                  "orbhip_search_by_projection_last")
+        return n, match
+
+    def SearchLocalPoints(self, frame: "ProjFrame", points, normals, min_dist, max_dist, mp_desc, skip=None,
+                          th: float = 1.0, view_cos_limit: float = 0.5, far_points: bool = False,
+                          th_far: float = 0.0):
+        """Tracking::SearchLocalPoints: Frame::isInFrustum + SearchByProjection(F, vpMapPoints, th,
+        bFarPoints, thFarPoints) with this matcher's nnratio. Returns (nmatches, match, in_view, level)."""
+        pts = np.ascontiguousarray(points, np.float32).reshape(-1, 3)
+        nrm = np.ascontiguousarray(normals, np.float32).reshape(-1, 3)
+        mn = np.ascontiguousarray(min_dist, np.float32)
+        mx = np.ascontiguousarray(max_dist, np.float32)
+        d = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
+        sk = None if skip is None else np.ascontiguousarray(skip, np.uint8)
+        m = pts.shape[0]
+        match = np.full(m, -1, np.int32)
+        in_view = np.zeros(m, np.uint8)
+        level = np.full(m, -1, np.int32)
+        fc = frame.to_c()
+        lc = LocalPointsC(m, ptr(pts), ptr(nrm), ptr(mn), ptr(mx), ptr(d), ptr(sk))
+        n = check(lib().orbhip_search_local_points(self.ctx.handle, ctypes.byref(fc), ctypes.byref(lc),
+                                                   float(view_cos_limit), float(th), float(self.mfNNratio),
+                                                   int(far_points), float(th_far), ptr(in_view), ptr(level),
+                                                   ptr(match)), "orbhip_search_local_points")
+        return n, match, in_view, level
+
+
+class ProjFrame:
+    """The current Frame for projection matching (U:src/Frame.cc): keypoints (orbhip_kp records,
+    mvKeysUn = mvKeys for zero distortion), descriptors, claimed mask, image bounds, scale tables,
+    intrinsics and Tcw."""
+
+    def __init__(self, kps, desc, pose_q, pose_t, fx, fy, cx, cy, width=640, height=480, scale_factor=1.2,
+                 n_levels=8, claimed=None):
+        self.kps = np.ascontiguousarray(kps, KP_DTYPE)
+        self.desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+        self.claimed = None if claimed is None else np.ascontiguousarray(claimed, np.uint8)
+        self.pose_q = np.asarray(pose_q, np.float32).reshape(4)
+        self.pose_t = np.asarray(pose_t, np.float32).reshape(3)
+        self.fx, self.fy, self.cx, self.cy = float(fx), float(fy), float(cx), float(cy)
+        self.bounds = (0.0, float(width), 0.0, float(height))
+        sf = np.ones(n_levels, np.float32)
+        for i in range(1, n_levels):
+            sf[i] = np.float32(np.float64(sf[i - 1]) * np.float64(np.float32(scale_factor)))
+        self.scale_factors = sf
+        self.log_scale_factor = float(np.log(np.float32(scale_factor)).astype(np.float32))
+
+    def to_c(self) -> FrameC:
+        c = FrameC()
+        c.n = self.kps.shape[0]
+        c.kps, c.desc, c.claimed = ptr(self.kps), ptr(self.desc), ptr(self.claimed)
+        c.min_x, c.max_x, c.min_y, c.max_y = self.bounds
+        c.scale_factors, c.n_levels, c.log_scale_factor = ptr(self.scale_factors), len(self.scale_factors), \
+            self.log_scale_factor
+        c.fx, c.fy, c.cx, c.cy = self.fx, self.fy, self.cx, self.cy
+        c.pose_q[:] = [float(v) for v in self.pose_q]
+        c.pose_t[:] = [float(v) for v in self.pose_t]
+        return c

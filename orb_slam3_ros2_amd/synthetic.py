@@ -188,3 +188,66 @@ def synthetic_pose_problem(n=600, outlier_frac=0.15, seed=3, rot_noise=0.02, tra
     prob = PoseProblem(_mat_to_quat(R0).astype(np.float32), t0.astype(np.float32), Xw.astype(np.float32),
                        uv.astype(np.float32), octave, inv_sigma2, cam["fx"], cam["fy"], cam["cx"], cam["cy"])
     return prob, dict(R=R, t=t, bad=bad)
+
+
+def synthetic_projection_scene(n_kp=1000, n_mp=900, seed=5, dup_frac=0.15, distractor_frac=0.15,
+                               claimed_frac=0.05, width=640, height=480, n_levels=8):
+    """A tracked Frame plus MapPoints for the projection matchers.
+    Keypoints uniform over the image (some on the far right / bottom edge, outside PosInGrid),
+    random descriptors; MapPoints back-projected from keypoints at 1-8 m (pixel jitter ~ the
+    keypoint scale, 0-40 flipped descriptor bits, rotation +12 deg), near-duplicates of the same
+    keypoint (greedy conflicts) and random distractors. Returns a dict of arrays."""
+    from ._lib import KP_DTYPE
+    rng = np.random.Generator(np.random.PCG64(seed))
+    cam = D435I
+    kps = np.zeros(n_kp, KP_DTYPE)
+    kps["x"] = rng.uniform(0, width, n_kp).astype(np.float32)
+    kps["y"] = rng.uniform(0, height, n_kp).astype(np.float32)
+    edge = rng.random(n_kp) < 0.03
+    kps["x"][edge] = rng.uniform(width - 6, width, edge.sum()).astype(np.float32)
+    kps["octave"] = rng.integers(0, n_levels, n_kp)
+    kps["angle"] = rng.uniform(0, 360, n_kp).astype(np.float32)
+    kps["size"] = 31.0
+    kps["response"] = rng.uniform(20, 80, n_kp).astype(np.float32)
+    desc = rng.integers(0, 256, (n_kp, 32), dtype=np.uint8)
+    R = _rodrigues(rng.normal(size=3) * 0.4)
+    t = rng.normal(size=3)
+    q = _mat_to_quat(R).astype(np.float32)
+    Rf = R.astype(np.float32)
+    Ow = (-Rf.T @ t.astype(np.float32)).astype(np.float64)
+    src = rng.choice(n_kp, n_mp, replace=False) if (dup_frac == 0 and n_mp <= n_kp) else \
+        rng.integers(0, max(n_kp, 1), n_mp)
+    ndup = int(dup_frac * n_mp)
+    src[:ndup] = rng.integers(0, max(1, n_kp // 20), ndup)          # many points on few keypoints
+    rng.shuffle(src)
+    sc = np.power(1.2, kps["octave"][src])
+    z = rng.uniform(1.0, 8.0, n_mp)
+    u = kps["x"][src] + rng.normal(size=n_mp) * sc
+    v = kps["y"][src] + rng.normal(size=n_mp) * sc
+    Xc = np.stack([(u - cam["cx"]) / cam["fx"] * z, (v - cam["cy"]) / cam["fy"] * z, z], 1)
+    pts = (Xc - t) @ R
+    mdesc = desc[src].copy()
+    for m in range(n_mp):
+        nb = int(rng.integers(0, 41))
+        bits = rng.choice(256, nb, replace=False)
+        for b in bits:
+            mdesc[m, b >> 3] ^= np.uint8(1 << (b & 7))
+    dis = rng.random(n_mp) < distractor_frac
+    mdesc[dis] = rng.integers(0, 256, (dis.sum(), 32), dtype=np.uint8)
+    octave = np.clip(kps["octave"][src] + rng.integers(-1, 2, n_mp), 0, n_levels - 1).astype(np.int32)
+    angle = ((kps["angle"][src] + 12.0 + rng.normal(size=n_mp) * 3.0) % 360.0).astype(np.float32)
+    # MapPoint geometry for isInFrustum
+    PO = pts - Ow
+    dist = np.linalg.norm(PO, axis=1)
+    normals = PO / dist[:, None] + rng.normal(size=(n_mp, 3)) * 0.05
+    normals /= np.linalg.norm(normals, axis=1)[:, None]
+    back = rng.random(n_mp) < 0.05
+    normals[back] *= -1
+    max_dist = dist * rng.uniform(0.75, 1.4, n_mp)
+    min_dist = max_dist / np.float64(1.2) ** (n_levels - 1)
+    claimed = (rng.random(n_kp) < claimed_frac).astype(np.uint8)
+    skip = (rng.random(n_mp) < 0.05).astype(np.uint8)
+    return dict(kps=kps, desc=desc, pose_q=q, pose_t=t.astype(np.float32), fx=cam["fx"], fy=cam["fy"], cx=cam["cx"],
+                cy=cam["cy"], points=pts.astype(np.float32), mp_desc=mdesc, last_octave=octave, last_angle=angle,
+                normals=normals.astype(np.float32), min_dist=min_dist.astype(np.float32),
+                max_dist=max_dist.astype(np.float32), claimed=claimed, skip=skip, src=src)
