@@ -98,6 +98,111 @@ __global__ __launch_bounds__(256) void k_resize(const ExtractPlan* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
+// k_pyr_cone: the whole cascade (levels 1..L-1) in ONE launch. Each workgroup owns a tile of
+// the last level and the matching slice of every level (a partition per level); it recomputes
+// in LDS the cone of each level its slices need (bit-exact: the same per-pixel INTER_LINEAR as
+// k_resize, from the level below held in LDS, level 0 staged from the frame) and writes only its
+// owned pixels. The redundant cone overlap (~1.3x the pyramid) costs far less than the 6
+// dependent launch gaps of the per-level cascade at batch 1. Tables: ConeRect per (tile, level).
+// ---------------------------------------------------------------------------
+// LDS: [level 0 stage | level 1 .. L-1 cones] bytes, then per level the column table
+// (xofs, xalpha) of its need columns and the row table (clamped r0, r1, ybeta) of its rows: one
+// global round trip loads every table entry and the level-0 cone, then the levels follow from LDS.
+__global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict__ P, FrameBufs fb,
+                                                   const ConeRect* __restrict__ rects, const int* __restrict__ xofs,
+                                                   const int* __restrict__ xalpha, const int* __restrict__ yofs,
+                                                   const int* __restrict__ ybeta) {
+    TR_BEGIN()
+    extern __shared__ __attribute__((aligned(16))) uint8_t cone[];
+    const int tile = blockIdx.x, f = blockIdx.y, L = P->n_levels, tid = threadIdx.x, nt = blockDim.x;
+    const ConeRect* R = rects + (size_t)tile * kMaxLevels;
+    int boff[kMaxLevels], toff[kMaxLevels];
+    int tot = 0;
+    for (int l = 0; l < L; l++) {
+        boff[l] = tot;
+        tot += ((R[l].nx1 - R[l].nx0) * (R[l].ny1 - R[l].ny0) + 15) & ~15;
+    }
+    int* tab = (int*)(cone + tot);
+    int ttot = 0;
+    for (int l = 1; l < L; l++) {
+        toff[l] = ttot;
+        ttot += 2 * (R[l].nx1 - R[l].nx0) + 3 * (R[l].ny1 - R[l].ny0);
+    }
+    // ---- one round trip: tables of every level + the level-0 cone ----
+    for (int l = 1; l < L; l++) {
+        const LevelGeom& D = P->lv[l];
+        const LevelGeom& S = P->lv[l - 1];
+        const ConeRect r = R[l];
+        const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0;
+        int* t = tab + toff[l];
+        for (int i = tid; i < nw + nh; i += nt) {
+            if (i < nw) {
+                t[i] = xofs[D.xtab_off + r.nx0 + i];
+                t[nw + i] = xalpha[D.xtab_off + r.nx0 + i];
+            } else {
+                const int j = i - nw;
+                const int sy = yofs[D.ytab_off + r.ny0 + j];
+                t[2 * nw + 3 * j] = sy < 0 ? 0 : (sy < S.h ? sy : S.h - 1);
+                t[2 * nw + 3 * j + 1] = sy + 1 < 0 ? 0 : (sy + 1 < S.h ? sy + 1 : S.h - 1);
+                t[2 * nw + 3 * j + 2] = ybeta[D.ytab_off + r.ny0 + j];
+            }
+        }
+    }
+    {
+        const ImgRef in0 = level_img(P, fb, f, 0);
+        const ConeRect r = R[0];
+        const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0;
+        for (int i = tid; i < nw * nh; i += nt) {
+            const int y = i / nw, x = i - y * nw;
+            cone[boff[0] + i] = in0.p[(int64_t)(r.ny0 + y) * in0.pitch + r.nx0 + x];
+        }
+    }
+    __syncthreads();
+    for (int l = 1; l < L; l++) {
+        const LevelGeom& D = P->lv[l];
+        const ConeRect r = R[l], rp = R[l - 1];
+        const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0, nwp = rp.nx1 - rp.nx0;
+        const int* t = tab + toff[l];
+        const uint8_t* src = cone + boff[l - 1];
+        uint8_t* dst = fb.pyr + (int64_t)f * P->pyr_bytes + D.pyr_off;
+        for (int i = tid; i < nw * nh; i += nt) {
+            const int yy = i / nw, xx = i - yy * nw;
+            const int x = r.nx0 + xx, y = r.ny0 + yy;
+            const int sx = t[xx] - rp.nx0;
+            const uint8_t* S0 = src + (t[2 * nw + 3 * yy] - rp.ny0) * nwp;
+            const uint8_t* S1 = src + (t[2 * nw + 3 * yy + 1] - rp.ny0) * nwp;
+            int h0, h1;
+            if (x < D.xmax) {
+                const int aa = t[nw + xx];
+                const int a0 = (int)(short)(aa & 0xFFFF), a1 = (int)(short)(aa >> 16);
+                h0 = S0[sx] * a0 + S0[sx + 1] * a1;
+                h1 = S1[sx] * a0 + S1[sx + 1] * a1;
+            } else {
+                h0 = S0[sx] * 2048;
+                h1 = S1[sx] * 2048;
+            }
+            const int bb = t[2 * nw + 3 * yy + 2];
+            const int b0 = (int)(short)(bb & 0xFFFF), b1 = (int)(short)(bb >> 16);
+            int v;
+            if (x < D.vend) {   // VResizeLinearVec_32s8u lanes (128-bit baseline)
+                int s0 = min(max(h0 >> 4, -32768), 32767);
+                int s1 = min(max(h1 >> 4, -32768), 32767);
+                int tt = ((s0 * b0) >> 16) + ((s1 * b1) >> 16);
+                tt = min(max(tt, -32768), 32767);
+                v = (tt + 2) >> 2;
+            } else {            // FixedPtCast<int, uchar, 22>
+                v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+            }
+            const uint8_t u = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
+            cone[boff[l] + i] = u;
+            if (x >= r.ox0 && x < r.ox1 && y >= r.oy0 && y < r.oy1) dst[(int64_t)y * D.pitch + x] = u;
+        }
+        __syncthreads();
+    }
+    TR_END(0)
+}
+
+// ---------------------------------------------------------------------------
 // k_fast_cells: one workgroup per (cell, frame)
 // FAST strength m = max(A, B, 0): A = max over the 16 9-arcs of min(v - p), B the same for
 // (p - v). cornerScore<16> == m - 1 for every detected corner and a pixel is a corner at
@@ -875,6 +980,16 @@ void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs
     dim3 blk(64, 4, 1);
     dim3 grd((D.w + 255) / 256, (D.h + 3) / 4, B);
     hipLaunchKernelGGL(k_resize, grd, blk, 0, st, dP, fb, l, xofs, xalpha, yofs, ybeta);
+}
+
+void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameBufs& fb, int B, const ConeRect* rects,
+                     const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_pyr_cone, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+        attr = true;
+    }
+    hipLaunchKernelGGL(k_pyr_cone, dim3(ntiles, B), dim3(1024), lds, st, dP, fb, rects, xofs, xalpha, yofs, ybeta);
 }
 
 void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,

@@ -65,6 +65,10 @@ struct Plan {
     ExtractPlan h{};
     std::vector<CellGeom> cells;
     std::vector<int> xofs, xalpha, yofs, ybeta, disc;
+    std::vector<ConeRect> cone;   // k_pyr_cone tables (empty: per-level k_resize cascade)
+    int cone_tiles = 0;
+    size_t cone_lds = 0;
+    DevBuf<ConeRect> d_cone;
     OctreeCfg oct{};
     int kp_cap_frame = 0;   // sum of level caps = max keypoints per frame
     DevBuf<ExtractPlan> d_plan;
@@ -281,6 +285,58 @@ static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
     P.pyr_bytes = ((pyr_off + 255) / 256) * 256;
     P.max_cells_level = max_cells;
     pl->kp_cap_frame = kp_base;
+    // cone pyramid tables: tiles of ~16x16 on the last level, an even partition of every level
+    if (L > 1) {
+        const LevelGeom& T = P.lv[L - 1];
+        const int ntx = (T.w + 15) / 16, nty = (T.h + 15) / 16;
+        size_t lds_max = 0;
+        std::vector<ConeRect> rects((size_t)ntx * nty * kMaxLevels);
+        for (int ti = 0; ti < nty; ti++)
+            for (int tj = 0; tj < ntx; tj++) {
+                ConeRect* R = &rects[((size_t)ti * ntx + tj) * kMaxLevels];
+                int nx0 = 0, nx1 = 0, ny0 = 0, ny1 = 0;   // need of the level above (l + 1)
+                for (int l = L - 1; l >= 1; l--) {
+                    const LevelGeom& G = P.lv[l];
+                    const int ox0 = (int)((int64_t)tj * G.w / ntx), ox1 = (int)((int64_t)(tj + 1) * G.w / ntx);
+                    const int oy0 = (int)((int64_t)ti * G.h / nty), oy1 = (int)((int64_t)(ti + 1) * G.h / nty);
+                    int a0 = ox0, a1 = ox1, b0 = oy0, b1 = oy1;
+                    if (l < L - 1 && nx1 > nx0 && ny1 > ny0) {   // inputs of the level-(l+1) need
+                        const LevelGeom& U = P.lv[l + 1];
+                        const int lo = pl->xofs[U.xtab_off + nx0];
+                        const int hi = pl->xofs[U.xtab_off + nx1 - 1] + ((nx1 - 1) < U.xmax ? 1 : 0);
+                        auto clampr = [&](int r) { return r < 0 ? 0 : (r < G.h ? r : G.h - 1); };
+                        const int r0 = clampr(pl->yofs[U.ytab_off + ny0]), r1 = clampr(pl->yofs[U.ytab_off + ny1 - 1] + 1);
+                        a0 = std::min(a0, lo); a1 = std::max(a1, hi + 1);
+                        b0 = std::min(b0, r0); b1 = std::max(b1, r1 + 1);
+                        if (ox1 <= ox0 || oy1 <= oy0) { a0 = lo; a1 = hi + 1; b0 = r0; b1 = r1 + 1; }
+                    }
+                    R[l] = ConeRect{(int16_t)a0, (int16_t)a1, (int16_t)b0, (int16_t)b1,
+                                    (int16_t)ox0, (int16_t)ox1, (int16_t)oy0, (int16_t)oy1};
+                    nx0 = a0; nx1 = a1; ny0 = b0; ny1 = b1;
+                }
+                {   // level-0 inputs of the level-1 need (staged in LDS)
+                    const LevelGeom& U = P.lv[1];
+                    const LevelGeom& G = P.lv[0];
+                    const int lo = pl->xofs[U.xtab_off + nx0];
+                    const int hi = pl->xofs[U.xtab_off + nx1 - 1] + ((nx1 - 1) < U.xmax ? 1 : 0);
+                    auto clampr = [&](int r) { return r < 0 ? 0 : (r < G.h ? r : G.h - 1); };
+                    const int r0 = clampr(pl->yofs[U.ytab_off + ny0]), r1 = clampr(pl->yofs[U.ytab_off + ny1 - 1] + 1);
+                    R[0] = ConeRect{(int16_t)lo, (int16_t)(hi + 1), (int16_t)r0, (int16_t)(r1 + 1), 0, 0, 0, 0};
+                }
+                size_t tot = 0, ttot = 0;
+                for (int l = 0; l < L; l++)
+                    tot += ((size_t)(R[l].nx1 - R[l].nx0) * (R[l].ny1 - R[l].ny0) + 15) & ~size_t(15);
+                for (int l = 1; l < L; l++)
+                    ttot += 4 * (2 * (size_t)(R[l].nx1 - R[l].nx0) + 3 * (size_t)(R[l].ny1 - R[l].ny0));
+                tot += ttot;
+                lds_max = std::max(lds_max, tot);
+            }
+        if (lds_max <= 60 * 1024) {
+            pl->cone.swap(rects);
+            pl->cone_tiles = ntx * nty;
+            pl->cone_lds = lds_max;
+        }
+    }
     // IC_Angle disc offsets (u, v) packed as int16 pairs
     for (int v = -15; v <= 15; v++) {
         const int d = c->umax[std::abs(v)];
@@ -316,6 +372,10 @@ static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
     HIPOK(up(pl->d_yofs, pl->yofs));
     HIPOK(up(pl->d_ybeta, pl->ybeta));
     HIPOK(up(pl->d_disc, pl->disc));
+    if (!pl->cone.empty()) {
+        HIPOK(pl->d_cone.ensure(pl->cone.size()));
+        HIPOK(hipMemcpy(pl->d_cone.p, pl->cone.data(), pl->cone.size() * sizeof(ConeRect), hipMemcpyHostToDevice));
+    }
     *out = pl.get();
     c->plans[key] = std::move(pl);
     return ORBHIP_OK;
@@ -346,8 +406,13 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
     fb.in = d_imgs; fb.in_stride = stride; fb.in_fstride = fstride; fb.pyr = c->d_pyr.p;
     StageTimer& tm = c->timer;
     tm.begin(1, st);
-    for (int l = 1; l < P.n_levels; l++)
-        launch_resize(pl->d_plan.p, P, fb, B, l, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p, pl->d_ybeta.p, st);
+    static const bool no_cone = std::getenv("ORBHIP_NO_CONE") != nullptr;   // A/B switch for the cascade
+    if (pl->cone_tiles && !no_cone)
+        launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_xofs.p, pl->d_xalpha.p,
+                        pl->d_yofs.p, pl->d_ybeta.p, st);
+    else
+        for (int l = 1; l < P.n_levels; l++)
+            launch_resize(pl->d_plan.p, P, fb, B, l, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p, pl->d_ybeta.p, st);
     tm.end(1, st);
     tm.begin(2, st);
     launch_fast(pl->d_plan.p, P, pl->d_cells.p, fb, B, c->d_cand.p, c->d_cand_cnt.p, c->d_err.p, st);

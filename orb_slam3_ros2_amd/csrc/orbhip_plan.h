@@ -46,6 +46,13 @@ struct ExtractPlan {
     LevelGeom lv[kMaxLevels];
 };
 
+// Cone pyramid (k_pyr_cone): per (last-level tile, level) the rectangle the tile computes in LDS
+// (need, the cone of the levels above) and the part it owns and writes (own). Half-open.
+struct ConeRect {
+    int16_t nx0, nx1, ny0, ny1;
+    int16_t ox0, ox1, oy0, oy1;
+};
+
 // Candidate packing: x_rel 12 bits | y_rel 12 bits | score 8 bits (coordinates relative
 // to the level's min border, as in vToDistributeKeys).
 __host__ __device__ inline uint32_t pack_cand(int x, int y, int score) {
