@@ -3,6 +3,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 namespace orbhip {
 
 struct DQ { double x, y, z, w; };
@@ -40,15 +42,21 @@ __device__ __forceinline__ DQ mattoq(const double m[9]) {
         int i = 0;
         if (m[4] > m[0]) i = 1;
         if (m[8] > m[3 * i + i]) i = 2;
-        const int j = (i + 1) % 3, k = (j + 1) % 3;
-        t = sqrt(m[3 * i + i] - m[3 * j + j] - m[3 * k + k] + 1.0);
-        double c[3];
-        c[i] = 0.5 * t;
-        t = 0.5 / t;
-        q.w = (m[3 * k + j] - m[3 * j + k]) * t;
-        c[j] = (m[3 * j + i] + m[3 * i + j]) * t;
-        c[k] = (m[3 * k + i] + m[3 * i + k]) * t;
-        q.x = c[0]; q.y = c[1]; q.z = c[2];
+        // the three cases with static indices (a runtime-indexed c[3] / m[] goes to scratch)
+        auto branch = [&](auto I) {
+            constexpr int ii = decltype(I)::value, j = (ii + 1) % 3, k = (j + 1) % 3;
+            double s = sqrt(m[3 * ii + ii] - m[3 * j + j] - m[3 * k + k] + 1.0);
+            double c[3];
+            c[ii] = 0.5 * s;
+            s = 0.5 / s;
+            q.w = (m[3 * k + j] - m[3 * j + k]) * s;
+            c[j] = (m[3 * j + ii] + m[3 * ii + j]) * s;
+            c[k] = (m[3 * k + ii] + m[3 * ii + k]) * s;
+            q.x = c[0]; q.y = c[1]; q.z = c[2];
+        };
+        if (i == 0) branch(std::integral_constant<int, 0>{});
+        else if (i == 1) branch(std::integral_constant<int, 1>{});
+        else branch(std::integral_constant<int, 2>{});
     }
     return q;
 }

@@ -9,13 +9,15 @@
 // J = -projectJac(Xc) [[0,z,-y,1,0,0],[-z,0,x,0,1,0],[y,-x,0,0,0,1]], Omega = I invSigma2[oct],
 // Huber deltaMono = (float)sqrt(5.991). The 6x6 system (H + lambda I) x = b is tiny: every lane
 // solves it redundantly (dense LDL^T), so the lanes never exchange anything but the edge sums.
-// Edge sums are wave butterfly reductions (the same bits in every lane, deterministic).
+// Edge sums are fixed-order LDS reductions (partials -> strip sums -> totals) with the same bits in
+// every lane, the per-trial chi2 a DPP/permlane wave sum then the W wave sums in order.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <vector>
@@ -23,6 +25,7 @@
 #include "../../include/orbhip.h"
 #include "ba_se3.h"
 #include "pose_opt.h"
+#include "wave_f64.h"
 
 namespace orbhip {
 
@@ -41,16 +44,62 @@ struct PoseEdgeIn {          // float inputs as the reference holds them
 
 namespace {
 
-__device__ __forceinline__ double wsum(double v) {
+constexpr int kAcc = 28;   // 21 upper-triangle H + 6 b + chi2
+
+// The W wavefronts that run one frame, and their LDS: partial table [kAcc][RS], strip sums
+// [kAcc][S], totals [32], wave sums [2][W] (double-buffered: consecutive sum1 calls need no
+// trailing barrier).
+template <int W>
+struct FrameGroup {
+    static constexpr int T = 64 * W;
+    static constexpr int S = W == 1 ? 2 : 8;
+    static constexpr int RS = T + S;   // row stride: the S-lane groups of the strip pass hit distinct banks
+    static constexpr int kDoubles = kAcc * RS + kAcc * S + 32 + 2 * W;
+    double* L;
+    int tid, par = 0;
+    __device__ __forceinline__ void sync() const {
+        if constexpr (W == 1) wave_lds_sync();
+        else __syncthreads();
+    }
+    // acc[k] <- sum over the group's threads, same bits everywhere
+    __device__ __forceinline__ void sum_acc(double* acc) {
+        double* L2 = L + kAcc * RS;
+        double* L3 = L2 + kAcc * S;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-__device__ __forceinline__ double wmax(double v) {
+        for (int k = 0; k < kAcc; k++) L[k * RS + tid] = acc[k];
+        sync();
+        if (tid < kAcc * S) {
+            const int k = tid / S, s = tid - k * S;
+            const double* row = L + k * RS;
+            double p0 = 0, p1 = 0;
+#pragma unroll 4
+            for (int j = s; j < T; j += 2 * S) { p0 += row[j]; p1 += row[j + S]; }
+            L2[tid] = p0 + p1;
+        }
+        sync();
+        if (tid < kAcc) {
+            double p = 0;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    return v;
-}
+            for (int s = 0; s < S; s++) p += L2[tid * S + s];
+            L3[tid] = p;
+        }
+        sync();
+#pragma unroll
+        for (int k = 0; k < kAcc; k++) acc[k] = L3[k];
+    }
+    __device__ __forceinline__ double sum1(double v) {
+        v = col4_sum(row16_sum(v));
+        if constexpr (W == 1) return v;
+        double* Lw = L + kAcc * RS + kAcc * S + 32 + par * W;
+        if ((tid & 63) == 0) Lw[tid >> 6] = v;
+        sync();
+        double s = 0;
+#pragma unroll
+        for (int w = 0; w < W; w++) s += Lw[w];
+        par ^= 1;
+        return s;
+    }
+};
 
 // e = obs - project(T.map(Xw)); chi2 = info |e|^2
 __device__ __forceinline__ void edge_err(const double* T, const PoseEdgeIn& ed, const PoseHdr& h, double& e0,
@@ -110,20 +159,22 @@ __device__ __forceinline__ bool ldlt6(double S[36], const double b[6], double x[
 
 // g2o optimize(10) over the level-0 edges of one frame (one wave). chi2_last[e] = the chi2 of
 // the last computeActiveErrors that saw edge e (stale after a rejected final trial, as g2o).
-__device__ void pose_optimize(double* T, const PoseHdr& h, const PoseEdgeIn* __restrict__ ed,
+template <int W>
+__device__ void pose_optimize(FrameGroup<W>& g, double* T, const PoseHdr& h, const PoseEdgeIn* __restrict__ ed,
                               const uint8_t* __restrict__ level, double* __restrict__ chi2_last, bool robust,
                               int& trials) {
-    const int lane = threadIdx.x & 63, n = h.n;
+    constexpr int NT = FrameGroup<W>::T;
+    const int tid = g.tid, n = h.n;
     int na = 0;
-    for (int e = lane; e < n; e += 64) na += level[e] == 0;
-    if (wsum((double)na) == 0.0) return;   // no active vertex: optimize() does nothing
+    for (int e = tid; e < n; e += NT) na += level[e] == 0;
+    if (g.sum1((double)na) == 0.0) return;   // no active vertex: optimize() does nothing
     double lambda = 0, ni = 2;
     for (int it = 0; it < 10; it++) {
         // computeActiveErrors + buildSystem
-        double acc[28];
+        double acc[kAcc];
 #pragma unroll
-        for (int k = 0; k < 28; k++) acc[k] = 0.0;
-        for (int e = lane; e < n; e += 64) {
+        for (int k = 0; k < kAcc; k++) acc[k] = 0.0;
+        for (int e = tid; e < n; e += NT) {
             if (level[e]) continue;
             const PoseEdgeIn E = ed[e];
             double e0, e1, c2, x, y, z, r0, r1;
@@ -151,8 +202,7 @@ __device__ void pose_optimize(double* T, const PoseHdr& h, const PoseEdgeIn* __r
 #pragma unroll
             for (int r = 0; r < 6; r++) acc[21 + r] += B[r] * om0 + B[6 + r] * om1;
         }
-#pragma unroll
-        for (int k = 0; k < 28; k++) acc[k] = wsum(acc[k]);
+        g.sum_acc(acc);
         double H[36], b[6];
         {
             int t = 0;
@@ -187,7 +237,7 @@ __device__ void pose_optimize(double* T, const PoseHdr& h, const PoseEdgeIn* __r
             for (int k = 0; k < 8; k++) Tn[k] = T[k];
             se3_update(x, Tn);
             double tc = 0;
-            for (int e = lane; e < n; e += 64) {
+            for (int e = tid; e < n; e += NT) {
                 if (level[e]) continue;
                 double e0, e1, c2, px, py, pz, r0, r1;
                 edge_err(Tn, ed[e], h, e0, e1, c2, px, py, pz);
@@ -195,7 +245,7 @@ __device__ void pose_optimize(double* T, const PoseHdr& h, const PoseEdgeIn* __r
                 chi2_last[e] = c2;
                 tc += r0;
             }
-            double tempChi = wsum(tc);
+            double tempChi = g.sum1(tc);
             if (!ok) tempChi = DBL_MAX;
             double scale = 1e-3;
 #pragma unroll
@@ -223,13 +273,20 @@ __device__ void pose_optimize(double* T, const PoseHdr& h, const PoseEdgeIn* __r
 
 }  // namespace
 
-// one wave per frame, 4 frames per 256-thread work-group
+// W wavefronts per frame, 4 / W frames per 256-thread work-group
+template <int W>
 __global__ __launch_bounds__(256) void k_pose_opt(const PoseHdr* __restrict__ hdr, const PoseEdgeIn* __restrict__ edges,
                                                    uint8_t* __restrict__ level, uint8_t* __restrict__ outlier,
                                                    double* __restrict__ chi2_last, PoseOut* __restrict__ out, int B) {
-    const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (f >= B) return;
+    constexpr int FPB = 4 / W, NT = FrameGroup<W>::T;
+    __shared__ double sm[FPB * FrameGroup<W>::kDoubles];
+    const int grp = threadIdx.x / NT;
+    const int f = blockIdx.x * FPB + grp;
+    if (f >= B) return;   // W == 1 only (the grid is exact for W > 1): a whole wave leaves
+    FrameGroup<W> g;
+    g.L = sm + grp * FrameGroup<W>::kDoubles;
+    g.tid = threadIdx.x - grp * NT;
+    const int tid = g.tid;
     const PoseHdr h = hdr[f];
     const PoseEdgeIn* ed = edges + h.off;
     uint8_t* lv = level + h.off;
@@ -238,17 +295,16 @@ __global__ __launch_bounds__(256) void k_pose_opt(const PoseHdr* __restrict__ hd
     double T[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) T[k] = h.T0[k];
-    for (int e = lane; e < h.n; e += 64) { lv[e] = 0; ol[e] = 0; c2[e] = 0.0; }
+    for (int e = tid; e < h.n; e += NT) { lv[e] = 0; ol[e] = 0; c2[e] = 0.0; }
     int trials = 0, nbad = 0;
     if (h.n >= 3) {
         bool robust = true;
         for (int round = 0; round < 4; round++) {
 #pragma unroll
             for (int k = 0; k < 8; k++) T[k] = h.T0[k];   // vSE3->setEstimate(pFrame->GetPose())
-            __builtin_amdgcn_wave_barrier();
-            pose_optimize(T, h, ed, lv, c2, robust, trials);
+            pose_optimize<W>(g, T, h, ed, lv, c2, robust, trials);
             int nb = 0;
-            for (int e = lane; e < h.n; e += 64) {
+            for (int e = tid; e < h.n; e += NT) {   // each thread only touches its own edges
                 double chi = c2[e];
                 if (ol[e]) {   // level-1 edge: e->computeError() at the current estimate
                     double e0, e1, x, y, z;
@@ -257,13 +313,12 @@ __global__ __launch_bounds__(256) void k_pose_opt(const PoseHdr* __restrict__ hd
                 const bool bad = chi > (double)5.991f;
                 ol[e] = bad; lv[e] = bad; nb += bad;
             }
-            nbad = (int)wsum((double)nb);
+            nbad = (int)g.sum1((double)nb);
             if (round == 2) robust = false;   // e->setRobustKernel(0)
             if (h.n < 10) break;              // optimizer.edges().size() < 10
-            __builtin_amdgcn_wave_barrier();
         }
     }
-    if (lane == 0) {
+    if (tid == 0) {
         PoseOut& o = out[f];
 #pragma unroll
         for (int k = 0; k < 8; k++) o.T[k] = T[k];
@@ -310,11 +365,11 @@ int pose_opt_batch(PoseWorkspace* ws, const orbhip_pose_problem* probs, int B, o
             if (p.octave[e] < 0 || p.octave[e] >= p.n_octaves) return ORBHIP_ERR_ARG;
         E += p.n;
     }
-    // packed: [hdr B][out B][edges E][chi2 E][level E][outlier E] (16-byte aligned segments)
+    // packed: [hdr B][edges E] (one upload) [out B][outlier E] (one download) [chi2 E][level E]
     auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-    const size_t o_hdr = 0, o_out = al(sizeof(PoseHdr) * B), o_edge = o_out + al(sizeof(PoseOut) * B);
-    const size_t o_c2 = o_edge + al(sizeof(PoseEdgeIn) * E), o_lv = o_c2 + al(sizeof(double) * E);
-    const size_t o_ol = o_lv + al(E), total = o_ol + al(E);
+    const size_t o_hdr = 0, o_edge = al(sizeof(PoseHdr) * B), o_out = o_edge + al(sizeof(PoseEdgeIn) * E);
+    const size_t o_ol = o_out + al(sizeof(PoseOut) * B), o_c2 = o_ol + al(E);
+    const size_t o_lv = o_c2 + al(sizeof(double) * E), total = o_lv + al(E);
     if (ws->dcap < total) {
         if (ws->d) (void)hipFree(ws->d);
         ws->d = nullptr;
@@ -354,14 +409,23 @@ int pose_opt_batch(PoseWorkspace* ws, const orbhip_pose_problem* probs, int B, o
         }
         off += p.n;
     }
-    PSOK(hipMemcpyAsync(D, H, o_out, hipMemcpyHostToDevice, st));
-    if (E) PSOK(hipMemcpyAsync(D + o_edge, H + o_edge, sizeof(PoseEdgeIn) * E, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(k_pose_opt, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, (const PoseHdr*)(D + o_hdr),
-                       (const PoseEdgeIn*)(D + o_edge), (uint8_t*)(D + o_lv), (uint8_t*)(D + o_ol),
-                       (double*)(D + o_c2), (PoseOut*)(D + o_out), B);
+    PSOK(hipMemcpyAsync(D, H, o_edge + sizeof(PoseEdgeIn) * E, hipMemcpyHostToDevice, st));
+    // W = 4 wavefronts per frame while that still fills the chip's SIMDs twice over, else one
+    int W = B <= 512 ? 4 : 1;
+    if (const char* s = std::getenv("ORBHIP_POSE_WAVES")) W = std::atoi(s) == 1 ? 1 : 4;
+    const PoseHdr* dh = (const PoseHdr*)(D + o_hdr);
+    const PoseEdgeIn* de = (const PoseEdgeIn*)(D + o_edge);
+    uint8_t* dlv = (uint8_t*)(D + o_lv);
+    uint8_t* dol = (uint8_t*)(D + o_ol);
+    double* dc2 = (double*)(D + o_c2);
+    PoseOut* dout = (PoseOut*)(D + o_out);
+    if (W == 4)
+        hipLaunchKernelGGL(k_pose_opt<4>, dim3((unsigned)B), dim3(256), 0, st, dh, de, dlv, dol, dc2, dout, B);
+    else
+        hipLaunchKernelGGL(k_pose_opt<1>, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, dh, de, dlv, dol, dc2,
+                           dout, B);
     PSOK(hipGetLastError());
-    PSOK(hipMemcpyAsync(H + o_out, D + o_out, sizeof(PoseOut) * B, hipMemcpyDeviceToHost, st));
-    if (E) PSOK(hipMemcpyAsync(H + o_ol, D + o_ol, E, hipMemcpyDeviceToHost, st));
+    PSOK(hipMemcpyAsync(H + o_out, D + o_out, o_ol - o_out + E, hipMemcpyDeviceToHost, st));
     PSOK(hipStreamSynchronize(st));
     const PoseOut* ho = (const PoseOut*)(H + o_out);
     const uint8_t* hol = (const uint8_t*)(H + o_ol);

@@ -62,7 +62,10 @@ def _check(g, o, tol=1e-4):
 
 
 @pytest.mark.gpu
-def test_pose_optimization_matches_oracle(oracle):
+@pytest.mark.parametrize("waves", ["1", "4"])
+def test_pose_optimization_matches_oracle(oracle, monkeypatch, waves):
+    # ORBHIP_POSE_WAVES forces the frame-group width (1 = batched layout, 4 = latency layout)
+    monkeypatch.setenv("ORBHIP_POSE_WAVES", waves)
     from orb_slam3_ros2_amd import Optimizer
     opt = Optimizer()
     for seed, n, frac in [(21, 600, 0.15), (22, 1000, 0.3), (23, 150, 0.05), (24, 9, 0.0), (25, 64, 0.5)]:
@@ -71,7 +74,9 @@ def test_pose_optimization_matches_oracle(oracle):
 
 
 @pytest.mark.gpu
-def test_pose_optimization_batch_and_edge_cases(oracle):
+@pytest.mark.parametrize("waves", ["1", "4"])
+def test_pose_optimization_batch_and_edge_cases(oracle, monkeypatch, waves):
+    monkeypatch.setenv("ORBHIP_POSE_WAVES", waves)
     from orb_slam3_ros2_amd import Optimizer
     opt = Optimizer()
     probs = [synthetic_pose_problem(n=int(n), outlier_frac=0.2, seed=100 + i)[0]

@@ -18,14 +18,18 @@ t = time.perf_counter()
 for _ in range(20):
     opt.PoseOptimization(probs[0])
 dt1 = (time.perf_counter() - t) / 20
-opt.PoseOptimization_batch(probs)
-t = time.perf_counter()
-rs = opt.PoseOptimization_batch(probs)
-dtb = time.perf_counter() - t
+rates = {}
+for w in ("1", "4"):
+    os.environ["ORBHIP_POSE_WAVES"] = w
+    opt.PoseOptimization_batch(probs)
+    t = time.perf_counter()
+    rs = opt.PoseOptimization_batch(probs)
+    rates[w] = B / (time.perf_counter() - t)
+os.environ.pop("ORBHIP_POSE_WAVES")
 t = time.perf_counter()
 k = 0
 while time.perf_counter() - t < 2.0:
     O.pose_optimization(probs[k % B]); k += 1
 dto = (time.perf_counter() - t) / k
-print(f"PoseOptimization n={n}: single {dt1*1e3:.3f} ms; batch of {B}: {dtb*1e3:.2f} ms = {B/dtb:.0f} frames/s; "
+print(f"PoseOptimization n={n}: single {dt1*1e3:.3f} ms; batch of {B}: W=1 {rates['1']:.0f}, W=4 {rates['4']:.0f} frames/s; "
       f"oracle 1 core {dto*1e3:.3f} ms/frame; trials mean {sum(r.lm_trials for r in rs)/B:.1f}")
