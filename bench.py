@@ -316,6 +316,57 @@ def c5_gba(ws, rank, iters):
             "c5_problem": "400 KF loop / 20000 pts / 80000 obs, n = 2394"}
 
 
+def _f8_inputs():
+    from orb_slam3_ros2_amd.matcher import ProjFrame
+    from orb_slam3_ros2_amd.synthetic import synthetic_pose_problem, synthetic_projection_scene
+    probs = [synthetic_pose_problem(n=600, outlier_frac=0.15, seed=1000 + i)[0] for i in range(1024)]
+    s = synthetic_projection_scene(n_kp=1250, n_mp=1000, seed=77)
+    f = ProjFrame(s["kps"], s["desc"], s["pose_q"], s["pose_t"], s["fx"], s["fy"], s["cx"], s["cy"],
+                  claimed=s["claimed"])
+    return probs, s, f
+
+
+def _ms(fn, reps):
+    fn()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    return 1e3 * (time.perf_counter() - t0) / reps
+
+
+def f8_tracking(ctx):
+    """SURVEY.md 8f rows on the device (host buffers in and out, PCIe-inclusive): PoseOptimization
+    (600 edges, 15% mismatches) single-frame latency and 1024-frame batch rate; the two
+    projection-guided searches (1250 keypoints x 1000 map points) per call."""
+    from orb_slam3_ros2_amd import ORBmatcher, Optimizer
+    probs, s, f = _f8_inputs()
+    opt = Optimizer(ctx=ctx)
+    out = {"f8_pose_opt_single_ms": round(_ms(lambda: opt.PoseOptimization(probs[0]), 50), 4)}
+    opt.PoseOptimization_batch(probs)
+    t0 = time.perf_counter()
+    opt.PoseOptimization_batch(probs)
+    out["f8_pose_opt_batch1024_frames_per_s"] = round(len(probs) / (time.perf_counter() - t0), 1)
+    m1, m2 = ORBmatcher(0.9, True), ORBmatcher(0.8, False)
+    out["f8_search_by_projection_last_ms"] = round(_ms(lambda: m1.SearchByProjectionLastFrame(
+        f, s["points"], s["mp_desc"], s["last_octave"], s["last_angle"]), 50), 4)
+    out["f8_search_local_points_ms"] = round(_ms(lambda: m2.SearchLocalPoints(
+        f, s["points"], s["normals"], s["min_dist"], s["max_dist"], s["mp_desc"], s["skip"], th=1.0), 50), 4)
+    out["f8_inputs"] = "PoseOptimization 600 edges/frame; projection 1250 keypoints x 1000 map points"
+    return out
+
+
+def cpu_f8_tracking():
+    """The oracle on one core for the same 8f inputs (ms per frame / per call)."""
+    from oracle import pyoracle as O
+    probs, s, f = _f8_inputs()
+    return {"f8_pose_opt_single_core_ms": round(_ms(lambda: O.pose_optimization(probs[0]), 20), 4),
+            "f8_search_by_projection_last_single_core_ms": round(_ms(lambda: O.search_by_projection_last(
+                f, s["points"], s["mp_desc"], s["last_octave"], s["last_angle"]), 20), 4),
+            "f8_search_local_points_single_core_ms": round(_ms(lambda: O.search_local_points(
+                f, s["points"], s["normals"], s["min_dist"], s["max_dist"], s["mp_desc"], s["skip"], th=1.0,
+                nnratio=0.8), 20), 4)}
+
+
 def main():
     args = parse()
     import torch
@@ -429,6 +480,7 @@ def main():
         extra["c4_lba_batched_kf_per_s"] = round(len(probs) / tb, 1)
         extra["c4_lba_batch"] = len(probs)
         extra["c4_lba_batched_trials_mean"] = round(float(np.mean([x.lm_trials for x in rs])), 2)
+        extra.update(f8_tracking(c2.ext.ctx))
         out["extra"] = extra
     if rank == 0 and ws == 1 and not args.no_cpu:
         cb = cpu_baseline(c2.frames_np)
@@ -445,6 +497,7 @@ def main():
             out["cpu_baseline"]["c4_lba_kf_per_s"] = round(cl["value"], 2)
             out["cpu_baseline"]["c4_lba_single_core_kf_per_s"] = round(cl["single"], 2)
             out["cpu_baseline"]["c4_lba_sample"] = f"{cl['solves']} oracle LBA solves, {cl['cores']} threads"
+            out["cpu_baseline"].update(cpu_f8_tracking())
     if rank == 0:
         print(json.dumps(out), flush=True)
     if ws > 1:
