@@ -407,7 +407,9 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
     StageTimer& tm = c->timer;
     tm.begin(1, st);
     static const bool no_cone = std::getenv("ORBHIP_NO_CONE") != nullptr;   // A/B switch for the cascade
-    if (pl->cone_tiles && !no_cone)
+    // the cone recomputes each tile's halo on every level: it pays only while the per-level cascade
+    // is launch-latency bound (a few work-groups per CU); big batches keep the cascade
+    if (pl->cone_tiles && !no_cone && (size_t)B * pl->cone_tiles <= 1024)
         launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_xofs.p, pl->d_xalpha.p,
                         pl->d_yofs.p, pl->d_ybeta.p, st);
     else

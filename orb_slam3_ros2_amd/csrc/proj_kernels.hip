@@ -141,14 +141,24 @@ __device__ __forceinline__ void top2_add(Top2& a, int d, int k, int l) {
     else if (lt(d, k, a.d2, a.k2)) { a.d2 = d; a.k2 = k; a.l2 = l; }
 }
 
-// One wave per query. mode 0: LastFrame (best <= TH_HIGH); mode 1: local points (best/second,
-// ratio test when both on the same level). owner[k] < i excludes keypoints claimed earlier.
-__global__ __launch_bounds__(256) void k_proj_round(ProjFrame f, int nq, int mode, float nnratio,
+// Round r of the fixed point, one wave per query. mode 0: LastFrame (best <= TH_HIGH); mode 1:
+// local points (best/second, ratio test when both on the same level). owner[k] < i excludes
+// keypoints claimed earlier. The owner table rotates through three buffers: round r reads
+// own[r % 3] (built from round r-1's picks), builds own[(r+1) % 3] by atomicMin, and clears
+// own[(r+2) % 3] for round r+1, so a round is one launch. chg[r] = some pick changed in round r;
+// a round whose predecessor changed nothing exits at once (the host launches rounds ahead).
+__global__ __launch_bounds__(256) void k_proj_round(ProjFrame f, int nq, int mode, float nnratio, int r,
                                                     const Query* __restrict__ qs, const orbhip_kp* __restrict__ kps,
                                                     const uint8_t* __restrict__ kdesc, const int* __restrict__ cell,
-                                                    const uint8_t* __restrict__ claimed, const int* __restrict__ owner,
+                                                    const uint8_t* __restrict__ claimed, int* __restrict__ own3,
                                                     const uint8_t* __restrict__ qdesc, int* __restrict__ pick,
-                                                    int* __restrict__ changed) {
+                                                    int* __restrict__ chg) {
+    if (r > 0 && chg[r - 1] == 0) return;   // converged: uniform over the grid
+    const int n = f.n;
+    const int* __restrict__ owner = own3 + (size_t)(r % 3) * n;
+    int* own_next = own3 + (size_t)((r + 1) % 3) * n;
+    int* own_clear = own3 + (size_t)((r + 2) % 3) * n;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) own_clear[k] = INT_MAX;
     const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (i >= nq) return;
@@ -204,19 +214,10 @@ __global__ __launch_bounds__(256) void k_proj_round(ProjFrame f, int nq, int mod
         }
     }
     if (lane == 0) {
-        if (pick[i] != p) *changed = 1;
+        if (pick[i] != p) chg[r] = 1;
         pick[i] = p;
+        if (p >= 0) atomicMin(&own_next[p], i);   // owner[k] = the first query whose pick is k
     }
-}
-
-// owner[k] = the first query whose current pick is k (INT_MAX if none)
-__global__ __launch_bounds__(1024) void k_proj_owner(int n, int nq, const int* __restrict__ pick,
-                                                     int* __restrict__ owner, int* __restrict__ changed) {
-    for (int k = threadIdx.x; k < n; k += blockDim.x) owner[k] = INT_MAX;
-    __syncthreads();
-    for (int i = threadIdx.x; i < nq; i += blockDim.x)
-        if (pick[i] >= 0) atomicMin(&owner[pick[i]], i);
-    if (threadIdx.x == 0) *changed = 0;
 }
 
 // the rotation-consistency filter of SearchByProjection(CurrentFrame, LastFrame) and the count
@@ -278,6 +279,7 @@ struct ProjWorkspace {
     size_t dcap = 0;
     void* h = nullptr;
     size_t hcap = 0;
+    int ahead = 4;   // rounds launched per host sync (adapts to the last search)
     ~ProjWorkspace() {
         if (d) (void)hipFree(d);
         if (h) (void)hipHostFree(h);
@@ -350,26 +352,42 @@ int ensure(ProjWorkspace* ws, size_t total) {
     return ORBHIP_OK;
 }
 
-// the fixed-point rounds; returns the number of rounds run (< 0 on error)
-int run_rounds(const ProjFrame& f, int nq, int mode, float nnratio, char* D, size_t o_q, size_t o_kps, size_t o_kd,
-               size_t o_cell, const uint8_t* claimed, size_t o_own, size_t o_qd, size_t o_pick, size_t o_flag,
-               char* H, hipStream_t st) {
+// The fixed-point rounds, launched `ws->ahead` at a time with the finishing work (`tail`: the
+// finish kernel and the result downloads) behind them and ONE host sync per batch: rounds after
+// convergence exit on the device, so the common case is a single round trip. Returns the number
+// of rounds that did work (< 0 on error).
+template <typename Tail>
+int run_rounds(ProjWorkspace* ws, const ProjFrame& f, int nq, int mode, float nnratio, char* D, size_t o_q,
+               size_t o_kps, size_t o_kd, size_t o_cell, const uint8_t* claimed, size_t o_own, size_t o_qd,
+               size_t o_pick, size_t o_chg, char* H, hipStream_t st, Tail&& tail) {
     const dim3 gq((unsigned)std::max(1, (nq + 3) / 4));
-    int rounds = 0;
+    const int cap = nq + 2;   // a fixed point is reached within nq + 1 rounds
+    int* chg = (int*)(D + o_chg);
+    const int* hchg = (const int*)(H + o_chg);
+    PJOK(hipMemsetAsync(D + o_own, 0x7F, 3 * sizeof(int) * (size_t)std::max(f.n, 1), st));   // > any query
+    PJOK(hipMemsetAsync(chg, 0, sizeof(int) * (size_t)cap, st));
+    int r = 0;
     for (;;) {
-        hipLaunchKernelGGL(k_proj_owner, dim3(1), dim3(1024), 0, st, f.n, nq, (const int*)(D + o_pick),
-                           (int*)(D + o_own), (int*)(D + o_flag));
-        hipLaunchKernelGGL(k_proj_round, gq, dim3(256), 0, st, f, nq, mode, nnratio, (const Query*)(D + o_q),
-                           (const orbhip_kp*)(D + o_kps), (const uint8_t*)(D + o_kd), (const int*)(D + o_cell),
-                           claimed, (const int*)(D + o_own), (const uint8_t*)(D + o_qd), (int*)(D + o_pick),
-                           (int*)(D + o_flag));
+        const int R = std::min(ws->ahead, cap - r);
+        for (int j = 0; j < R; j++)
+            hipLaunchKernelGGL(k_proj_round, gq, dim3(256), 0, st, f, nq, mode, nnratio, r + j,
+                               (const Query*)(D + o_q), (const orbhip_kp*)(D + o_kps), (const uint8_t*)(D + o_kd),
+                               (const int*)(D + o_cell), claimed, (int*)(D + o_own), (const uint8_t*)(D + o_qd),
+                               (int*)(D + o_pick), chg);
         PJOK(hipGetLastError());
-        rounds++;
-        PJOK(hipMemcpyAsync(H + o_flag, D + o_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+        if (int rc = tail()) return rc;
+        PJOK(hipMemcpyAsync(H + o_chg + sizeof(int) * r, chg + r, sizeof(int) * R, hipMemcpyDeviceToHost, st));
         PJOK(hipStreamSynchronize(st));
-        if (*(int*)(H + o_flag) == 0 || rounds > nq + 1) break;
+        for (int j = 0; j < R; j++)
+            if (hchg[r + j] == 0) {
+                const int rounds = r + j + 1;
+                ws->ahead = std::min(16, std::max(2, rounds + 1));
+                return rounds;
+            }
+        r += R;
+        if (r >= cap) return r;
+        ws->ahead = std::min(16, 2 * ws->ahead);
     }
-    return rounds;
 }
 
 }  // namespace
@@ -388,7 +406,8 @@ int proj_search_last(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_proj
     const size_t o_scale = lay.add(sizeof(float) * F->n_levels);
     const size_t o_pts = lay.add(12 * (size_t)nq), o_qd = lay.add(32 * (size_t)nq), o_oct = lay.add(4 * (size_t)nq);
     const size_t o_ang = lay.add(4 * (size_t)nq), o_in_end = lay.off;
-    const size_t o_cell = lay.add(4 * (size_t)n), o_own = lay.add(4 * (size_t)n), o_q = lay.add(sizeof(Query) * nq);
+    const size_t o_cell = lay.add(4 * (size_t)n), o_own = lay.add(12 * (size_t)std::max(n, 1));
+    const size_t o_q = lay.add(sizeof(Query) * nq), o_chg = lay.add(4 * ((size_t)nq + 2));
     const size_t o_pick = lay.add(4 * (size_t)nq), o_match = lay.add(4 * (size_t)nq), o_flag = lay.add(8);
     if (int rc = ensure(ws, lay.off)) return rc;
     char* H = (char*)ws->h;
@@ -409,16 +428,18 @@ int proj_search_last(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_proj
     hipLaunchKernelGGL(k_proj_prep_last, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, f, nq,
                        (const float*)(D + o_pts), (const int*)(D + o_oct), (const float*)(D + o_scale), th,
                        (Query*)(D + o_q));
-    const int rounds = run_rounds(f, nq, 0, 0.f, D, o_q, o_kps, o_kd, o_cell,
-                                  F->claimed ? (const uint8_t*)(D + o_cl) : nullptr, o_own, o_qd, o_pick, o_flag, H,
-                                  st);
+    auto tail = [&]() -> int {
+        hipLaunchKernelGGL(k_proj_finish, dim3(1), dim3(1024), 0, st, nq, check_orientation,
+                           (const float*)(D + o_ang), (const orbhip_kp*)(D + o_kps), (const int*)(D + o_pick),
+                           (int*)(D + o_match), (int*)(D + o_flag));
+        PJOK(hipMemcpyAsync(H + o_match, D + o_match, 4 * (size_t)nq, hipMemcpyDeviceToHost, st));
+        PJOK(hipMemcpyAsync(H + o_flag, D + o_flag, 4, hipMemcpyDeviceToHost, st));
+        return 0;
+    };
+    const int rounds = run_rounds(ws, f, nq, 0, 0.f, D, o_q, o_kps, o_kd, o_cell,
+                                  F->claimed ? (const uint8_t*)(D + o_cl) : nullptr, o_own, o_qd, o_pick, o_chg, H,
+                                  st, tail);
     if (rounds < 0) return rounds;
-    hipLaunchKernelGGL(k_proj_finish, dim3(1), dim3(1024), 0, st, nq, check_orientation, (const float*)(D + o_ang),
-                       (const orbhip_kp*)(D + o_kps), (const int*)(D + o_pick), (int*)(D + o_match),
-                       (int*)(D + o_flag));
-    PJOK(hipMemcpyAsync(H + o_match, D + o_match, 4 * (size_t)nq, hipMemcpyDeviceToHost, st));
-    PJOK(hipMemcpyAsync(H + o_flag, D + o_flag, 4, hipMemcpyDeviceToHost, st));
-    PJOK(hipStreamSynchronize(st));
     std::memcpy(match, H + o_match, 4 * (size_t)nq);
     if (rounds_out) *rounds_out = rounds;
     return *(int*)(H + o_flag);
@@ -439,7 +460,8 @@ int proj_search_local(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_loc
     const size_t o_pts = lay.add(12 * (size_t)nq), o_nrm = lay.add(12 * (size_t)nq), o_mind = lay.add(4 * (size_t)nq);
     const size_t o_maxd = lay.add(4 * (size_t)nq), o_qd = lay.add(32 * (size_t)nq), o_skip = lay.add(nq);
     const size_t o_in_end = lay.off;
-    const size_t o_cell = lay.add(4 * (size_t)n), o_own = lay.add(4 * (size_t)n), o_q = lay.add(sizeof(Query) * nq);
+    const size_t o_cell = lay.add(4 * (size_t)n), o_own = lay.add(12 * (size_t)std::max(n, 1));
+    const size_t o_q = lay.add(sizeof(Query) * nq), o_chg = lay.add(4 * ((size_t)nq + 2));
     const size_t o_pick = lay.add(4 * (size_t)nq), o_lvl = lay.add(4 * (size_t)nq), o_iv = lay.add(nq);
     const size_t o_match = lay.add(4 * (size_t)nq), o_flag = lay.add(8);
     if (int rc = ensure(ws, lay.off)) return rc;
@@ -465,18 +487,20 @@ int proj_search_local(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_loc
                        (const float*)(D + o_maxd), M->skip ? (const uint8_t*)(D + o_skip) : nullptr,
                        (const float*)(D + o_scale), F->n_levels, F->log_scale_factor, view_cos_limit, th, far_points,
                        th_far, (Query*)(D + o_q), (uint8_t*)(D + o_iv), (int*)(D + o_lvl));
-    const int rounds = run_rounds(f, nq, 1, nnratio, D, o_q, o_kps, o_kd, o_cell,
-                                  F->claimed ? (const uint8_t*)(D + o_cl) : nullptr, o_own, o_qd, o_pick, o_flag, H,
-                                  st);
+    auto tail = [&]() -> int {
+        hipLaunchKernelGGL(k_proj_finish, dim3(1), dim3(1024), 0, st, nq, 0, (const float*)nullptr,
+                           (const orbhip_kp*)(D + o_kps), (const int*)(D + o_pick), (int*)(D + o_match),
+                           (int*)(D + o_flag));
+        PJOK(hipMemcpyAsync(H + o_match, D + o_match, 4 * (size_t)nq, hipMemcpyDeviceToHost, st));
+        PJOK(hipMemcpyAsync(H + o_lvl, D + o_lvl, 4 * (size_t)nq, hipMemcpyDeviceToHost, st));
+        PJOK(hipMemcpyAsync(H + o_iv, D + o_iv, nq, hipMemcpyDeviceToHost, st));
+        PJOK(hipMemcpyAsync(H + o_flag, D + o_flag, 4, hipMemcpyDeviceToHost, st));
+        return 0;
+    };
+    const int rounds = run_rounds(ws, f, nq, 1, nnratio, D, o_q, o_kps, o_kd, o_cell,
+                                  F->claimed ? (const uint8_t*)(D + o_cl) : nullptr, o_own, o_qd, o_pick, o_chg, H,
+                                  st, tail);
     if (rounds < 0) return rounds;
-    hipLaunchKernelGGL(k_proj_finish, dim3(1), dim3(1024), 0, st, nq, 0, (const float*)nullptr,
-                       (const orbhip_kp*)(D + o_kps), (const int*)(D + o_pick), (int*)(D + o_match),
-                       (int*)(D + o_flag));
-    PJOK(hipMemcpyAsync(H + o_match, D + o_match, 4 * (size_t)nq, hipMemcpyDeviceToHost, st));
-    PJOK(hipMemcpyAsync(H + o_lvl, D + o_lvl, 4 * (size_t)nq, hipMemcpyDeviceToHost, st));
-    PJOK(hipMemcpyAsync(H + o_iv, D + o_iv, nq, hipMemcpyDeviceToHost, st));
-    PJOK(hipMemcpyAsync(H + o_flag, D + o_flag, 4, hipMemcpyDeviceToHost, st));
-    PJOK(hipStreamSynchronize(st));
     std::memcpy(match, H + o_match, 4 * (size_t)nq);
     std::memcpy(level, H + o_lvl, 4 * (size_t)nq);
     std::memcpy(in_view, H + o_iv, nq);
