@@ -63,8 +63,8 @@ __device__ __forceinline__ DQ mattoq(const double m[9]) {
 
 __device__ __forceinline__ void qnormalize(DQ& q) {
     if (q.w < 0) { q.x = -q.x; q.y = -q.y; q.z = -q.z; q.w = -q.w; }
-    const double n = sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
-    q.x /= n; q.y /= n; q.z /= n; q.w /= n;
+    const double in = 1.0 / sqrt(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
+    q.x *= in; q.y *= in; q.z *= in; q.w *= in;
 }
 
 __device__ __forceinline__ DQ load_q(const double* p) { return DQ{p[0], p[1], p[2], p[3]}; }
@@ -86,8 +86,10 @@ __device__ __forceinline__ void se3_update(const double* u, double* T) {
 #pragma unroll
         for (int i = 0; i < 9; i++) { R[i] = (i % 4 == 0 ? 1.0 : 0.0) + O[i] + O2[i]; V[i] = R[i]; }
     } else {
-        const double sa = sin(theta) / theta, cb = (1 - cos(theta)) / (theta * theta);
-        const double cc = (theta - sin(theta)) / (theta * theta * theta);
+        double st, ct;
+        sincos(theta, &st, &ct);
+        const double it = 1.0 / theta, it2 = it * it;
+        const double sa = st * it, cb = (1 - ct) * it2, cc = (theta - st) * it2 * it;
 #pragma unroll
         for (int i = 0; i < 9; i++) {
             R[i] = (i % 4 == 0 ? 1.0 : 0.0) + sa * O[i] + cb * O2[i];

@@ -107,8 +107,9 @@ __device__ __forceinline__ void edge_err(const double* T, const PoseEdgeIn& ed, 
     const DQ q = load_q(T);
     qrot(q, (double)ed.X[0], (double)ed.X[1], (double)ed.X[2], x, y, z);
     x += T[4]; y += T[5]; z += T[6];
-    e0 = (double)ed.u - (h.fx * x / z + h.cx);
-    e1 = (double)ed.v - (h.fy * y / z + h.cy);
+    const double iz = 1.0 / z;
+    e0 = (double)ed.u - (h.fx * x * iz + h.cx);
+    e1 = (double)ed.v - (h.fy * y * iz + h.cy);
     chi2 = (double)ed.info * (e0 * e0 + e1 * e1);
 }
 
@@ -126,7 +127,7 @@ __device__ __forceinline__ void huber(double chi2, double delta, bool robust, do
 
 // dense LDL^T without pivoting (the oracle's ldlt_solve), uniform in every lane
 __device__ __forceinline__ bool ldlt6(double S[36], const double b[6], double x[6]) {
-    double d[6];
+    double d[6], id[6];   // pivots and their reciprocals (one division per pivot)
 #pragma unroll
     for (int j = 0; j < 6; j++) {
         double dj = S[6 * j + j];
@@ -134,12 +135,13 @@ __device__ __forceinline__ bool ldlt6(double S[36], const double b[6], double x[
         for (int k = 0; k < j; k++) dj -= S[6 * j + k] * S[6 * j + k] * d[k];
         if (dj == 0.0 || !isfinite(dj)) return false;
         d[j] = dj;
+        id[j] = 1.0 / dj;
 #pragma unroll
         for (int i = j + 1; i < 6; i++) {
             double s = S[6 * i + j];
 #pragma unroll
             for (int k = 0; k < j; k++) s -= S[6 * i + k] * S[6 * j + k] * d[k];
-            S[6 * i + j] = s / dj;
+            S[6 * i + j] = s * id[j];
         }
     }
 #pragma unroll
@@ -149,7 +151,7 @@ __device__ __forceinline__ bool ldlt6(double S[36], const double b[6], double x[
 #pragma unroll
         for (int k = 0; k < i; k++) x[i] -= S[6 * i + k] * x[k];
 #pragma unroll
-    for (int i = 0; i < 6; i++) x[i] /= d[i];
+    for (int i = 0; i < 6; i++) x[i] *= id[i];
 #pragma unroll
     for (int i = 5; i >= 0; i--)
 #pragma unroll
@@ -164,9 +166,23 @@ __device__ void pose_optimize(FrameGroup<W>& g, double* T, const PoseHdr& h, con
                               const uint8_t* __restrict__ level, double* __restrict__ chi2_last, bool robust,
                               int& trials) {
     constexpr int NT = FrameGroup<W>::T;
+    // the first EC edges of every thread stay in registers for all trials (their level is fixed
+    // during optimize(): a bit mask); the rest are re-read each pass
+    constexpr int EC = W == 1 ? 2 : 4;
     const int tid = g.tid, n = h.n;
+    PoseEdgeIn ec[EC];
+    unsigned act = 0;
     int na = 0;
-    for (int e = tid; e < n; e += NT) na += level[e] == 0;
+#pragma unroll
+    for (int c = 0; c < EC; c++) {
+        const int e = tid + c * NT;
+        if (e < n) {
+            ec[c] = ed[e];
+            if (!level[e]) act |= 1u << c;
+        }
+    }
+    na = __builtin_popcount(act);
+    for (int e = tid + EC * NT; e < n; e += NT) na += level[e] == 0;
     if (g.sum1((double)na) == 0.0) return;   // no active vertex: optimize() does nothing
     double lambda = 0, ni = 2;
     for (int it = 0; it < 10; it++) {
@@ -174,17 +190,16 @@ __device__ void pose_optimize(FrameGroup<W>& g, double* T, const PoseHdr& h, con
         double acc[kAcc];
 #pragma unroll
         for (int k = 0; k < kAcc; k++) acc[k] = 0.0;
-        for (int e = tid; e < n; e += NT) {
-            if (level[e]) continue;
-            const PoseEdgeIn E = ed[e];
+        auto build = [&](const PoseEdgeIn& E, int e) {
             double e0, e1, c2, x, y, z, r0, r1;
             edge_err(T, E, h, e0, e1, c2, x, y, z);
             huber(c2, h.delta, robust, r0, r1);
             chi2_last[e] = c2;
             acc[27] += r0;
             double J[6];
-            J[0] = -(h.fx / z); J[1] = -0.0; J[2] = -(-h.fx * x / (z * z));
-            J[3] = -0.0; J[4] = -(h.fy / z); J[5] = -(-h.fy * y / (z * z));
+            const double iz = 1.0 / z, iz2 = iz * iz;
+            J[0] = -(h.fx * iz); J[1] = -0.0; J[2] = h.fx * x * iz2;
+            J[3] = -0.0; J[4] = -(h.fy * iz); J[5] = h.fy * y * iz2;
             const double D[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
             double B[12];
 #pragma unroll
@@ -201,7 +216,12 @@ __device__ void pose_optimize(FrameGroup<W>& g, double* T, const PoseHdr& h, con
                 for (int c = r; c < 6; c++) acc[t++] += w * (B[r] * B[c] + B[6 + r] * B[6 + c]);
 #pragma unroll
             for (int r = 0; r < 6; r++) acc[21 + r] += B[r] * om0 + B[6 + r] * om1;
-        }
+        };
+#pragma unroll
+        for (int c = 0; c < EC; c++)
+            if (act >> c & 1) build(ec[c], tid + c * NT);
+        for (int e = tid + EC * NT; e < n; e += NT)
+            if (!level[e]) build(ed[e], e);
         g.sum_acc(acc);
         double H[36], b[6];
         {
@@ -237,14 +257,18 @@ __device__ void pose_optimize(FrameGroup<W>& g, double* T, const PoseHdr& h, con
             for (int k = 0; k < 8; k++) Tn[k] = T[k];
             se3_update(x, Tn);
             double tc = 0;
-            for (int e = tid; e < n; e += NT) {
-                if (level[e]) continue;
+            auto chi = [&](const PoseEdgeIn& E, int e) {
                 double e0, e1, c2, px, py, pz, r0, r1;
-                edge_err(Tn, ed[e], h, e0, e1, c2, px, py, pz);
+                edge_err(Tn, E, h, e0, e1, c2, px, py, pz);
                 huber(c2, h.delta, robust, r0, r1);
                 chi2_last[e] = c2;
                 tc += r0;
-            }
+            };
+#pragma unroll
+            for (int c = 0; c < EC; c++)
+                if (act >> c & 1) chi(ec[c], tid + c * NT);
+            for (int e = tid + EC * NT; e < n; e += NT)
+                if (!level[e]) chi(ed[e], e);
             double tempChi = g.sum1(tc);
             if (!ok) tempChi = DBL_MAX;
             double scale = 1e-3;
