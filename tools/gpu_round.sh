@@ -11,6 +11,7 @@ if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
 timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu > gpurun_out/prof.log 2>&1 && \
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c2 -o run -- python3 bench.py --no-cpu --no-extra > gpurun_out/prof_c2.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 100 --warmup 10 --no-cpu --no-extra > gpurun_out/pmc_fetch.log 2>&1 && \
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 100 --warmup 10 --no-cpu --no-extra > gpurun_out/pmc_write.log 2>&1
 rc=$?; echo "rc=$rc"; tail -2 gpurun_out/bench.log; exit $rc
