@@ -318,12 +318,12 @@ def c5_gba(ws, rank, iters):
 
 def _f8_inputs():
     from orb_slam3_ros2_amd.matcher import ProjFrame
-    from orb_slam3_ros2_amd.synthetic import synthetic_pose_problem, synthetic_projection_scene
+    from orb_slam3_ros2_amd.synthetic import synthetic_init_pair, synthetic_pose_problem, synthetic_projection_scene
     probs = [synthetic_pose_problem(n=600, outlier_frac=0.15, seed=1000 + i)[0] for i in range(1024)]
     s = synthetic_projection_scene(n_kp=1250, n_mp=1000, seed=77)
     f = ProjFrame(s["kps"], s["desc"], s["pose_q"], s["pose_t"], s["fx"], s["fy"], s["cx"], s["cy"],
                   claimed=s["claimed"])
-    return probs, s, f
+    return probs, s, f, synthetic_init_pair(n1=1800, seed=31)
 
 
 def _ms(fn, reps):
@@ -339,7 +339,7 @@ def f8_tracking(ctx):
     (600 edges, 15% mismatches) single-frame latency and 1024-frame batch rate; the two
     projection-guided searches (1250 keypoints x 1000 map points) per call."""
     from orb_slam3_ros2_amd import ORBmatcher, Optimizer
-    probs, s, f = _f8_inputs()
+    probs, s, f, ini = _f8_inputs()
     opt = Optimizer(ctx=ctx)
     out = {"f8_pose_opt_single_ms": round(_ms(lambda: opt.PoseOptimization(probs[0]), 50), 4)}
     opt.PoseOptimization_batch(probs)
@@ -351,15 +351,20 @@ def f8_tracking(ctx):
         f, s["points"], s["mp_desc"], s["last_octave"], s["last_angle"]), 50), 4)
     out["f8_search_local_points_ms"] = round(_ms(lambda: m2.SearchLocalPoints(
         f, s["points"], s["normals"], s["min_dist"], s["max_dist"], s["mp_desc"], s["skip"], th=1.0), 50), 4)
-    out["f8_inputs"] = "PoseOptimization 600 edges/frame; projection 1250 keypoints x 1000 map points"
+    mi = ORBmatcher(0.9, True, ctx=ctx)
+    out["a12_search_for_initialization_ms"] = round(_ms(lambda: mi.SearchForInitialization(*ini, 100), 20), 4)
+    out["f8_inputs"] = ("PoseOptimization 600 edges/frame; projection 1250 keypoints x 1000 map points; "
+                        "SearchForInitialization 1114 octave-0 queries x 1128 F2 keypoints, window 100")
     return out
 
 
 def cpu_f8_tracking():
     """The oracle on one core for the same 8f inputs (ms per frame / per call)."""
     from oracle import pyoracle as O
-    probs, s, f = _f8_inputs()
-    return {"f8_pose_opt_single_core_ms": round(_ms(lambda: O.pose_optimization(probs[0]), 20), 4),
+    probs, s, f, ini = _f8_inputs()
+    return {"a12_search_for_initialization_single_core_ms": round(_ms(
+                lambda: O.search_for_initialization(*ini, 100, 0.9, True), 20), 4),
+            "f8_pose_opt_single_core_ms": round(_ms(lambda: O.pose_optimization(probs[0]), 20), 4),
             "f8_search_by_projection_last_single_core_ms": round(_ms(lambda: O.search_by_projection_last(
                 f, s["points"], s["mp_desc"], s["last_octave"], s["last_angle"]), 20), 4),
             "f8_search_local_points_single_core_ms": round(_ms(lambda: O.search_local_points(

@@ -239,6 +239,27 @@ int orbhip_search_local_points(orbhip_ctx* ctx, const orbhip_frame* frame, const
                                float view_cos_limit, float th, float nnratio, int far_points, float th_far,
                                uint8_t* in_view, int32_t* level, int32_t* match);
 
+/* ---- monocular initialisation matching -------------------------------------------
+ * U:src/ORBmatcher.cc::SearchForInitialization(Frame& F1, Frame& F2, vector<cv::Point2f>&
+ * vbPrevMatched, vector<int>& vnMatches12, int windowSize), called by
+ * U:src/Tracking.cc::MonocularInitialization as ORBmatcher(0.9, true) with windowSize 100.
+ * Exact greedy semantics: F1 keypoints of octave 0 in index order, F2.GetFeaturesInArea(
+ * vbPrevMatched[i1], windowSize, 0, 0) on F2's 64 x 48 grid (bounds min_x..max_y), candidates
+ * with vMatchedDistance <= dist skipped, TH_LOW = 50 and the nnratio test, later better matches
+ * steal the F2 keypoint, rotation histogram over all pushes (ComputeThreeMaxima).
+ * prev_matched (n1 x 2 floats) is updated in place for the surviving matches; matches12[n1]
+ * receives vnMatches12. Returns nmatches. Octaves must be >= 0. Envelope: 4 * (F2 octave-0
+ * keypoints) + 4 * (F1 octave-0 keypoints) <= 150 KiB (ORBHIP_ERR_UNSUPPORTED beyond). */
+typedef struct {
+    int32_t n;
+    const orbhip_kp* kps;       /* n: mvKeysUn */
+    const uint8_t* desc;        /* n x 32 */
+    float min_x, max_x, min_y, max_y;   /* mnMinX, mnMaxX, mnMinY, mnMaxY (grid of F2) */
+} orbhip_init_frame;
+int orbhip_search_for_initialization(orbhip_ctx* ctx, const orbhip_init_frame* f1, const orbhip_init_frame* f2,
+                                     float* prev_matched, int window_size, float nnratio, int check_orientation,
+                                     int32_t* matches12);
+
 /* ---- motion-only bundle adjustment -------------------------
  * U:src/Optimizer.cc::Optimizer::PoseOptimization(Frame* pFrame), monocular observations:
  * one VertexSE3Expmap (Tcw), EdgeSE3ProjectXYZOnlyPose per matched MapPoint (information

@@ -130,6 +130,23 @@ public:
         return rc;
     }
 
+    // U:src/ORBmatcher.cc::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize):
+    // keypoints/descriptors of both frames, F2's image bounds, vbPrevMatched as (x, y) pairs
+    // (updated in place). Returns nmatches.
+    int SearchForInitialization(orbhip_ctx* ctx, const std::vector<orbhip_kp>& kps1, const std::vector<uint8_t>& desc1,
+                                const std::vector<orbhip_kp>& kps2, const std::vector<uint8_t>& desc2,
+                                const float bounds2[4], std::vector<float>& vbPrevMatched,
+                                std::vector<int>& vnMatches12, int windowSize = 10) const {
+        vnMatches12.assign(kps1.size(), -1);
+        const orbhip_init_frame f1{(int32_t)kps1.size(), kps1.data(), desc1.data(), 0.f, 1.f, 0.f, 1.f};
+        const orbhip_init_frame f2{(int32_t)kps2.size(), kps2.data(), desc2.data(), bounds2[0], bounds2[1],
+                                   bounds2[2], bounds2[3]};
+        const int rc = orbhip_search_for_initialization(ctx, &f1, &f2, vbPrevMatched.data(), windowSize, mfNNratio,
+                                                        mbCheckOrientation ? 1 : 0, vnMatches12.data());
+        check(rc, "orbhip_search_for_initialization");
+        return rc;
+    }
+
     float mfNNratio;
     bool mbCheckOrientation;
 };

@@ -18,12 +18,19 @@
 //       bFarPoints, thFarPoints)   RadiusByViewingCos (2.5 if viewCos > 0.998, else 4.0; x th
 //       when th != 1), levels predicted-1 .. predicted, best/second with levels, ratio test only
 //       when both lie on the same level; greedy claims in vpMapPoints order
+//   U:src/ORBmatcher.cc::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)
+//       F1 keypoints of octave 0 in index order; F2.GetFeaturesInArea(prev, windowSize, 0, 0);
+//       candidates with vMatchedDistance[i2] <= dist skipped; best/second (strict <);
+//       bestDist <= TH_LOW = 50 && bestDist < (float)bestDist2 * mfNNratio; a better later match
+//       steals i2 (the earlier vnMatches12 entry is reset, its rotHist entry stays); rotation
+//       histogram of pushes + ComputeThreeMaxima; vbPrevMatched updated for the survivors
 // Pose arithmetic: Sophus SE3f * p = q._transformVector(p) + t (Eigen, float); mRcw =
 // q.toRotationMatrix(); mOw = Twc.translation() = conj(q)._transformVector(-t). No FMA
 // contraction (-ffp-contract=off). Undistortion is the identity (mDistCoef k1 == 0, the
 // RealSense_D435i.yaml case): mvKeysUn = mvKeys, bounds [0, cols] x [0, rows].
 // PARITY UNPINNED by the reference (no fixtures upstream).
 // ============================================================================
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -267,6 +274,68 @@ int orc_search_local_points(int n_cur, const void* cur_kps, const uint8_t* cur_d
             }
         }
     }
+    return nmatches;
+}
+
+// SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize) with the matcher's
+// mfNNratio / mbCheckOrientation. F2's grid uses its own image bounds. prev: n1 x 2, in/out.
+int orc_search_for_initialization(int n1, const void* kps1, const uint8_t* desc1, int n2, const void* kps2,
+                                  const uint8_t* desc2, float minx, float maxx, float miny, float maxy, float* prev,
+                                  int window, float nnratio, int check_orientation, int32_t* matches12) {
+    proj::Frame F2;
+    F2.n = n2; F2.kps = (const proj::Kp*)kps2; F2.desc = desc2;
+    F2.minx = minx; F2.maxx = maxx; F2.miny = miny; F2.maxy = maxy;
+    F2.build();
+    const proj::Kp* K1 = (const proj::Kp*)kps1;
+    constexpr int TH_LOW = 50;
+    int nmatches = 0;
+    for (int i = 0; i < n1; i++) matches12[i] = -1;
+    std::vector<int> rotHist[proj::HISTO_LENGTH];
+    const float factor = 1.0f / proj::HISTO_LENGTH;
+    std::vector<int> vMatchedDistance(n2, INT_MAX), vnMatches21(n2, -1), cand;
+    for (int i1 = 0; i1 < n1; i1++) {
+        const int level1 = K1[i1].octave;
+        if (level1 > 0) continue;
+        F2.features_in_area(prev[2 * i1], prev[2 * i1 + 1], (float)window, level1, level1, cand);
+        if (cand.empty()) continue;
+        int bestDist = INT_MAX, bestDist2 = INT_MAX, bestIdx2 = -1;
+        for (int i2 : cand) {
+            const int dist = proj::hamming(&desc1[32 * i1], &desc2[32 * i2]);
+            if (vMatchedDistance[i2] <= dist) continue;
+            if (dist < bestDist) { bestDist2 = bestDist; bestDist = dist; bestIdx2 = i2; }
+            else if (dist < bestDist2) bestDist2 = dist;
+        }
+        if (bestDist <= TH_LOW && bestDist < (float)bestDist2 * nnratio) {
+            if (vnMatches21[bestIdx2] >= 0) { matches12[vnMatches21[bestIdx2]] = -1; nmatches--; }
+            matches12[i1] = bestIdx2;
+            vnMatches21[bestIdx2] = i1;
+            vMatchedDistance[bestIdx2] = bestDist;
+            nmatches++;
+            if (check_orientation) {
+                float rot = K1[i1].angle - F2.kps[bestIdx2].angle;
+                if (rot < 0.0) rot += 360.0f;
+                int b = (int)std::round(rot * factor);
+                if (b == proj::HISTO_LENGTH) b = 0;
+                rotHist[b].push_back(i1);
+            }
+        }
+    }
+    if (check_orientation) {
+        int h[proj::HISTO_LENGTH];
+        for (int b = 0; b < proj::HISTO_LENGTH; b++) h[b] = (int)rotHist[b].size();
+        int ind1, ind2, ind3;
+        proj::three_maxima(h, ind1, ind2, ind3);
+        for (int b = 0; b < proj::HISTO_LENGTH; b++) {
+            if (b == ind1 || b == ind2 || b == ind3) continue;
+            for (int idx1 : rotHist[b])
+                if (matches12[idx1] >= 0) { matches12[idx1] = -1; nmatches--; }
+        }
+    }
+    for (int i1 = 0; i1 < n1; i1++)
+        if (matches12[i1] >= 0) {
+            prev[2 * i1] = F2.kps[matches12[i1]].x;
+            prev[2 * i1 + 1] = F2.kps[matches12[i1]].y;
+        }
     return nmatches;
 }
 

@@ -66,6 +66,8 @@ def lib():
                                               c_float, _f32p, _f32p, c_float, c_float, c_float, c_float, c_int,
                                               _f32p, _f32p, _f32p, _f32p, _u8p, vp, c_float, c_float, c_float, c_int,
                                               c_float, _u8p, _i32p, _i32p]
+        L.orc_search_for_initialization.argtypes = [c_int, vp, _u8p, c_int, vp, _u8p, c_float, c_float, c_float,
+                                                    c_float, _f32p, c_int, c_float, c_int, _i32p]
         L.orc_bgr2gray.argtypes = [_u8p, c_int, c_int, c_int, _u8p, c_int]
         L.orc_glibc_sincosf_range.argtypes = [ctypes.c_uint32, ctypes.c_uint32, _f32p, _f32p]
         _lib = L
@@ -251,3 +253,18 @@ def search_local_points(frame, points, normals, min_dist, max_dist, mp_desc, ski
         np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32), _vp(sk), view_cos_limit, th, nnratio,
         int(far_points), th_far, in_view, level, match)
     return n, match, in_view, level
+
+
+def search_for_initialization(kps1, desc1, kps2, desc2, prev_matched, window=100, nnratio=0.9,
+                              check_orientation=True, bounds=(0.0, 640.0, 0.0, 480.0)):
+    """Oracle SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize).
+    kps: orbhip_kp records (matcher.KP_DTYPE). Returns (nmatches, matches12, prev_matched')."""
+    from orb_slam3_ros2_amd._lib import KP_DTYPE
+    k1 = np.ascontiguousarray(kps1, KP_DTYPE); k2 = np.ascontiguousarray(kps2, KP_DTYPE)
+    prev = np.ascontiguousarray(prev_matched, np.float32).reshape(-1, 2).copy()
+    m = np.full(k1.shape[0], -1, np.int32)
+    n = lib().orc_search_for_initialization(
+        k1.shape[0], _vp(k1), np.ascontiguousarray(desc1, np.uint8).reshape(-1, 32), k2.shape[0], _vp(k2),
+        np.ascontiguousarray(desc2, np.uint8).reshape(-1, 32), *[float(b) for b in bounds], prev, int(window),
+        float(nnratio), int(check_orientation), m)
+    return n, m, prev

@@ -80,6 +80,11 @@ class ProjLastC(ctypes.Structure):
                 ("octave", ctypes.c_void_p), ("angle", ctypes.c_void_p)]
 
 
+class InitFrameC(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int32), ("kps", ctypes.c_void_p), ("desc", ctypes.c_void_p), ("min_x", ctypes.c_float),
+                ("max_x", ctypes.c_float), ("min_y", ctypes.c_float), ("max_y", ctypes.c_float)]
+
+
 class LocalPointsC(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int32), ("points", ctypes.c_void_p), ("normals", ctypes.c_void_p),
                 ("min_dist", ctypes.c_void_p), ("max_dist", ctypes.c_void_p), ("desc", ctypes.c_void_p),
@@ -95,7 +100,7 @@ EXPORTED = ["orbhip_abi_version", "orbhip_create", "orbhip_destroy", "orbhip_lev
             "orbhip_vocab_create", "orbhip_vocab_load_text", "orbhip_vocab_destroy", "orbhip_vocab_info",
             "orbhip_bow_transform", "orbhip_bow_transform_device", "orbhip_search_bow",
             "orbhip_pose_optimization", "orbhip_pose_optimization_batch", "orbhip_search_by_projection_last",
-            "orbhip_search_local_points"]
+            "orbhip_search_local_points", "orbhip_search_for_initialization"]
 
 
 def lib():
@@ -150,6 +155,8 @@ def lib():
                                                    vp]
     L.orbhip_search_local_points.argtypes = [vp, ctypes.POINTER(FrameC), ctypes.POINTER(LocalPointsC), f32, f32, f32,
                                              i32, f32, vp, vp, vp]
+    L.orbhip_search_for_initialization.argtypes = [vp, ctypes.POINTER(InitFrameC), ctypes.POINTER(InitFrameC), vp,
+                                                   i32, f32, i32, vp]
     L.orbhip_test_sincosf.argtypes = [vp, vp, vp, ctypes.c_int64]
     L.orbhip_test_sincosf_sweep.argtypes = [ctypes.c_uint32, ctypes.c_uint32, vp, vp]
     L.orbhip_test_sincosf_sweep.restype = ctypes.c_int64

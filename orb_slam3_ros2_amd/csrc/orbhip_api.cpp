@@ -727,6 +727,15 @@ int orbhip_search_local_points(orbhip_ctx* c, const orbhip_frame* frame, const o
                              match, nullptr, c->stream);
 }
 
+int orbhip_search_for_initialization(orbhip_ctx* c, const orbhip_init_frame* f1, const orbhip_init_frame* f2,
+                                     float* prev_matched, int window_size, float nnratio, int check_orientation,
+                                     int32_t* matches12) {
+    if (!c) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    if (!c->proj) c->proj = proj_ws_create();
+    return init_search(c->proj, f1, f2, prev_matched, window_size, nnratio, check_orientation, matches12, c->stream);
+}
+
 int orbhip_comm_unique_id(uint8_t* id) {
     if (!id) return ORBHIP_ERR_ARG;
     return ba_comm_unique_id(id);

@@ -13,4 +13,6 @@ int proj_search_last(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_proj
 int proj_search_local(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_local_points* M, float view_cos_limit,
                       float th, float nnratio, int far_points, float th_far, uint8_t* in_view, int32_t* level,
                       int32_t* match, int* rounds_out, hipStream_t st);
+int init_search(ProjWorkspace* ws, const orbhip_init_frame* F1, const orbhip_init_frame* F2, float* prev_matched,
+                int window_size, float nnratio, int check_orientation, int32_t* matches12, hipStream_t st);
 }  // namespace orbhip

@@ -23,10 +23,12 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
 #include "../../include/orbhip.h"
+#include "orbhip_device.h"
 #include "proj.h"
 
 namespace orbhip {
@@ -269,6 +271,375 @@ __global__ __launch_bounds__(1024) void k_proj_finish(int nq, int check_orientat
     if (threadIdx.x == 0) *nmatch = cnt;
 }
 
+
+// ---------------------------------------------------------------------------
+// SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)
+//   (U:src/ORBmatcher.cc; monocular initialisation, Tracking::MonocularInitialization)
+//
+// The reference walks the F1 keypoints of octave 0 in index order; each reads and writes the
+// per-F2-keypoint state (vMatchedDistance, vnMatches21), so query i depends on every earlier
+// query. The device splits that into the state-free part and the chain:
+//   k_init_prep     one WG: F2 octave-0 keypoints with a grid cell, ranked in walk order
+//                   (cell = px * 48 + py, then index); F1 octave-0 keypoints -> query slots
+//   k_init_cands    one wave per query: GetFeaturesInArea(prev, windowSize, 0, 0) as a
+//                   rectangle/level/|d| < r test over the ranked F2 keypoints, Hamming distance,
+//                   ballot-compacted list of (dist << 21 | rank << 5 | rotation bin), and the
+//                   list's 16 smallest entries (per-lane sorted top-4, 16 wave-min extractions)
+//   k_init_greedy   one WG: wave 0 runs the chain with the state in LDS. Per query: the
+//                   eligible entries (dist < vMatchedDistance[rank]) among its 16 smallest by one
+//                   ballot; the first two set bits are the reference's best and second best
+//                   whenever two are eligible or the list has <= 16 entries (else the whole list
+//                   is scanned, a DPP/permlane top-2 butterfly); TH_LOW / ratio test; the steal
+//                   update. Four queries share a 64-lane register, blocks of four are in flight.
+//                   Then the whole WG applies the rotation histogram (ComputeThreeMaxima over the
+//                   pushes, stale ones included) and writes vnMatches12 / vbPrevMatched.
+// (dist, rank) order is the walk order tie-break of "dist < bestDist", and the second-best
+// distance is the second element of the multiset, so the chain is exact. The bin of the pair
+// (the rotHist push) rides in the low bits, so the chain never touches the keypoints.
+// ---------------------------------------------------------------------------
+constexpr int kInitCells = kGridCols * kGridRows;   // 3072
+constexpr int kThLow = 50;
+constexpr int kInitK = 16;   // smallest list entries per query handed to the chain
+constexpr int kInitR = 4;    // ring of 4-query blocks in flight in the chain
+
+// min over the wave, every lane gets it
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true));    // quad_perm [1,0,3,2]
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true));    // quad_perm [2,3,0,1]
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true));   // row_half_mirror
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true));   // row_mirror
+    const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = min(a[0], a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return min(b[0], b[1]);
+}
+
+struct InitGeom {
+    int n1, n2;
+    float minx, maxx, miny, maxy, invw, invh, r;
+    int list_cap;    // entries per query list (>= number of ranked F2 keypoints, multiple of 64)
+};
+
+__device__ __forceinline__ int init_cell(const InitGeom& g, float x, float y) {   // PosInGrid
+    const int px = (int)roundf((x - g.minx) * g.invw);
+    const int py = (int)roundf((y - g.miny) * g.invh);
+    return (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? -1 : px * kGridRows + py;
+}
+
+// counts[0] = queries (F1 octave 0), counts[1] = ranked F2 keypoints, counts[2] = nmatches
+__global__ __launch_bounds__(1024) void k_init_prep(InitGeom g, const orbhip_kp* __restrict__ kps1,
+                                                    const orbhip_kp* __restrict__ kps2, int* __restrict__ slot,
+                                                    int* __restrict__ qlist, int* __restrict__ counts) {
+    __shared__ int cnt[kInitCells], start[kInitCells], scratch[20], tot;
+    const int tid = threadIdx.x, nt = blockDim.x;
+    for (int c = tid; c < kInitCells; c += nt) cnt[c] = 0;
+    __syncthreads();
+    for (int k = tid; k < g.n2; k += nt) {
+        const orbhip_kp kp = kps2[k];
+        const int c = kp.octave == 0 ? init_cell(g, kp.x, kp.y) : -1;
+        if (c >= 0) atomicAdd(&cnt[c], 1);
+    }
+    __syncthreads();
+    // exclusive scan of the 3072 cell counts (3 per thread, in order)
+    {
+        int v[3], s = 0;
+        for (int j = 0; j < 3; j++) { const int c = tid * 3 + j; v[j] = c < kInitCells ? cnt[c] : 0; s += v[j]; }
+        int total;
+        int base = block_excl_scan(s, scratch, &total);
+        for (int j = 0; j < 3; j++) { const int c = tid * 3 + j; if (c < kInitCells) start[c] = base; base += v[j]; }
+        if (tid == 0) tot = total;
+    }
+    __syncthreads();
+    for (int c = tid; c < kInitCells; c += nt) cnt[c] = 0;
+    __syncthreads();
+    for (int k = tid; k < g.n2; k += nt) {
+        const orbhip_kp kp = kps2[k];
+        const int c = kp.octave == 0 ? init_cell(g, kp.x, kp.y) : -1;
+        if (c >= 0) slot[start[c] + atomicAdd(&cnt[c], 1)] = k;
+    }
+    __syncthreads();
+    // index order inside each cell (cells hold a handful of keypoints)
+    for (int c = tid; c < kInitCells; c += nt) {
+        int* a = slot + start[c];
+        const int m = cnt[c];
+        for (int i = 1; i < m; i++) {
+            const int v = a[i];
+            int j = i - 1;
+            while (j >= 0 && a[j] > v) { a[j + 1] = a[j]; j--; }
+            a[j + 1] = v;
+        }
+    }
+    // F1 octave-0 keypoints in index order
+    int run = 0;
+    for (int k0 = 0; k0 < g.n1; k0 += nt) {
+        const int k = k0 + tid;
+        const int f = (k < g.n1 && kps1[k].octave == 0) ? 1 : 0;   // level1 > 0 -> skipped
+        int total;
+        const int pos = block_excl_scan(f, scratch, &total);
+        if (f) qlist[run + pos] = k;
+        run += total;
+    }
+    if (tid == 0) { counts[0] = run; counts[1] = tot; }
+}
+
+// one wave per query slot: the candidate list of GetFeaturesInArea(prev[i1], r, 0, 0)
+__global__ __launch_bounds__(256) void k_init_cands(InitGeom g, const orbhip_kp* __restrict__ kps1,
+                                                    const uint8_t* __restrict__ desc1,
+                                                    const orbhip_kp* __restrict__ kps2,
+                                                    const uint8_t* __restrict__ desc2, const float* __restrict__ prev,
+                                                    const int* __restrict__ slot, const int* __restrict__ qlist,
+                                                    const int* __restrict__ counts, uint32_t* __restrict__ lists,
+                                                    int* __restrict__ lens, uint32_t* __restrict__ topk,
+                                                    int* __restrict__ need) {
+    const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int nq = counts[0], nr = counts[1];
+    if (q >= nq) return;
+    const int i1 = qlist[q];
+    const float x = prev[2 * i1], y = prev[2 * i1 + 1], r = g.r;
+    const int nMinCellX = max(0, (int)floorf((x - g.minx - r) * g.invw));
+    const int nMaxCellX = min(kGridCols - 1, (int)ceilf((x - g.minx + r) * g.invw));
+    const int nMinCellY = max(0, (int)floorf((y - g.miny - r) * g.invh));
+    const int nMaxCellY = min(kGridRows - 1, (int)ceilf((y - g.miny + r) * g.invh));
+    const bool any = nMinCellX < kGridCols && nMaxCellX >= 0 && nMinCellY < kGridRows && nMaxCellY >= 0;
+    uint32_t* out = lists + (size_t)q * g.list_cap;
+    const float a1 = kps1[i1].angle, factor = 1.0f / kHisto;
+    int n = 0, seen = 0;
+    uint32_t t0 = ~0u, t1 = ~0u, t2 = ~0u, t3 = ~0u;
+    if (any) {
+        const uint4* qd4 = (const uint4*)(desc1 + 32 * (size_t)i1);
+        const uint4 qa = qd4[0], qb = qd4[1];
+        for (int b = 0; b < nr; b += 64) {
+            const int rk = b + lane;
+            bool ok = false;
+            uint32_t v = 0;
+            if (rk < nr) {
+                const int k = slot[rk];
+                const orbhip_kp kp = kps2[k];
+                const int c = init_cell(g, kp.x, kp.y);
+                const int px = c / kGridRows, py = c - px * kGridRows;
+                if (px >= nMinCellX && px <= nMaxCellX && py >= nMinCellY && py <= nMaxCellY &&
+                    fabsf(kp.x - x) < r && fabsf(kp.y - y) < r) {
+                    const uint4* kd4 = (const uint4*)(desc2 + 32 * (size_t)k);
+                    const uint4 ka = kd4[0], kb = kd4[1];
+                    const int d = __popc(qa.x ^ ka.x) + __popc(qa.y ^ ka.y) + __popc(qa.z ^ ka.z) +
+                                  __popc(qa.w ^ ka.w) + __popc(qb.x ^ kb.x) + __popc(qb.y ^ kb.y) +
+                                  __popc(qb.z ^ kb.z) + __popc(qb.w ^ kb.w);
+                    float rot = a1 - kp.angle;
+                    if (rot < 0.0) rot += 360.0f;
+                    int bin = (int)roundf(rot * factor);
+                    if (bin == kHisto) bin = 0;
+                    v = ((uint32_t)d << 21) | ((uint32_t)rk << 5) | (uint32_t)bin;
+                    ok = true;
+                }
+            }
+            const uint64_t m = __ballot(ok);
+            if (ok) out[n + __popcll(m & ((1ull << lane) - 1ull))] = v;
+            n += __popcll(m);
+            // per-lane sorted top-4 (branch-free insert)
+            const uint32_t w = ok ? v : ~0u;
+            t3 = min(t3, max(t2, w)); t2 = min(t2, max(t1, w)); t1 = min(t1, max(t0, w)); t0 = min(t0, w);
+            seen += ok;
+        }
+    }
+    // the list's 16 smallest entries: 16 rounds of wave-min over the lane heads, the winning lane
+    // pops. A lane that pops all 4 of its kept entries while it had more may have lost one of
+    // the 16: then the chain scans the whole list (need = 2).
+    uint32_t mine = ~0u;
+    int popped = 0;
+#pragma unroll
+    for (int j = 0; j < kInitK; j++) {
+        const uint32_t mn = wave_min_u32(t0);
+        if (lane == j) mine = mn;
+        if (t0 == mn && mn != ~0u) { t0 = t1; t1 = t2; t2 = t3; t3 = ~0u; popped++; }
+    }
+    const bool lost = __ballot(popped == 4 && seen > 4) != 0;
+    if (lane < kInitK) topk[(size_t)q * kInitK + lane] = mine;
+    if (lane == 0) {
+        lens[q] = n;
+        need[q] = lost ? 2 : (n > kInitK ? 1 : 0);
+    }
+}
+
+// (m1, m2) = the two smallest values of the multiset union of two disjoint lane sets
+__device__ __forceinline__ void top2_merge(uint32_t& m1, uint32_t& m2, uint32_t o1, uint32_t o2) {
+    const uint32_t hi = max(m1, o1);
+    m1 = min(m1, o1);
+    m2 = min(hi, min(m2, o2));
+}
+template <int CTRL>
+__device__ __forceinline__ void top2_dpp(uint32_t& m1, uint32_t& m2) {
+    const uint32_t o1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)m1, CTRL, 0xF, 0xF, true);
+    const uint32_t o2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)m2, CTRL, 0xF, 0xF, true);
+    top2_merge(m1, m2, o1, o2);
+}
+// butterfly over the wave: xor 1, xor 2, half-row mirror, row mirror (each pairs lanes whose
+// sets are disjoint), then rows 0<->1, 2<->3 and halves by permlane swaps; every lane ends with
+// the wave's top-2
+__device__ __forceinline__ void wave_top2(uint32_t& m1, uint32_t& m2) {
+    top2_dpp<0xB1>(m1, m2);
+    top2_dpp<0x4E>(m1, m2);
+    top2_dpp<0x141>(m1, m2);
+    top2_dpp<0x140>(m1, m2);
+    {
+        const auto a = __builtin_amdgcn_permlane16_swap(m1, m1, false, false);
+        const auto b = __builtin_amdgcn_permlane16_swap(m2, m2, false, false);
+        m1 = a[0]; m2 = b[0];
+        top2_merge(m1, m2, a[1], b[1]);
+    }
+    {
+        const auto a = __builtin_amdgcn_permlane32_swap(m1, m1, false, false);
+        const auto b = __builtin_amdgcn_permlane32_swap(m2, m2, false, false);
+        m1 = a[0]; m2 = b[0];
+        top2_merge(m1, m2, a[1], b[1]);
+    }
+}
+
+
+// LDS: ST u32[nr] = vMatchedDistance (low 16 bits, 0xFFFF = INT_MAX) | vnMatches21 as a query
+// slot (high 16, 0xFFFF none); CL u32[nq] = the rank query q claimed | its rotHist push bin << 16
+// (~0u none). vnMatches12 is implied: the claim of q survives iff ST[rank].hi == q at the end (a
+// steal only ever replaces it), so the chain never reads a match back.
+__global__ __launch_bounds__(256) void k_init_greedy(InitGeom g, float nnratio, int check_orientation,
+                                                     const orbhip_kp* __restrict__ kps2, const int* __restrict__ slot,
+                                                     const int* __restrict__ qlist, const int* __restrict__ counts,
+                                                     const uint32_t* __restrict__ lists, const int* __restrict__ lens,
+                                                     const uint32_t* __restrict__ topk, const int* __restrict__ need,
+                                                     int32_t* __restrict__ matches12, float* __restrict__ prev,
+                                                     int* __restrict__ nmatch) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ int hist[32], keep[3], cnt;
+    const int nq = counts[0], nr = counts[1];
+    uint32_t* ST = (uint32_t*)smem;
+    uint32_t* CL = ST + nr;
+    const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
+    for (int k = tid; k < nr; k += nt) ST[k] = ~0u;
+    for (int q = tid; q < nq; q += nt) CL[q] = ~0u;
+    for (int i = tid; i < g.n1; i += nt) matches12[i] = -1;
+    if (tid < 32) hist[tid] = 0;
+    if (tid == 0) cnt = 0;
+    __syncthreads();
+    if (tid < 64 && nq > 0) {
+        // blocks of 4 queries: lane 16j + e holds entry e of query 4b + j's top-16 (one 256-byte
+        // row per block), and lane j < 4 its `need`. A ring of kInitR blocks is in flight; the
+        // loads are unconditional (clamped block) so the waits count only the oldest block.
+        // vMatchedDistance of a block's entries is read from LDS one block ahead (mdv) and kept
+        // current by forwarding (the chain is the only writer, one rank per accepted query): a
+        // block's own updates go into its mdv at once and into the next block's at its start.
+        const int nb = (nq + 3) >> 2;
+        uint32_t tk[kInitR];
+        int nd[kInitR], mdv[kInitR];
+        auto load = [&](int b, int r) {
+            const int bb = min(b, nb - 1);
+            tk[r] = topk[(size_t)bb * 64 + lane];
+            nd[r] = need[min(4 * bb + (lane & 3), nq - 1)];
+        };
+        auto rank_of = [&](uint32_t v) { return v == ~0u ? 0 : (int)((v >> 5) & 0xFFFF); };
+#pragma unroll
+        for (int r = 0; r < kInitR; r++) load(r, r);
+        mdv[0] = (int)(ST[rank_of(tk[0])] & 0xFFFF);
+        for (int b0 = 0; b0 < nb; b0 += kInitR) {
+#pragma unroll
+            for (int r = 0; r < kInitR; r++) {
+                const int b = b0 + r;
+                const int rn = (r + 1) % kInitR;
+                mdv[rn] = (int)(ST[rank_of(tk[rn])] & 0xFFFF);   // next block, before this block's writes
+                const int rk_c = rank_of(tk[r]), rk_n = rank_of(tk[rn]);
+                int upd_rk[4] = {-1, -1, -1, -1}, upd_d[4] = {0, 0, 0, 0};
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int q = 4 * b + j;
+                    if (q < nq) {
+                        const uint32_t v = tk[r];
+                        const bool elig = v != ~0u && (int)(v >> 21) < mdv[r];
+                        const uint32_t mask = (uint32_t)(__ballot(elig) >> (16 * j)) & 0xFFFFu;
+                        const int nq_need = __builtin_amdgcn_readlane(nd[r], j);
+                        uint32_t m1 = ~0u, m2 = ~0u;
+                        if (nq_need == 0 || (nq_need == 1 && __popc(mask) >= 2)) {
+                            // the two smallest eligible entries are among the list's 16 smallest
+                            if (mask) m1 = (uint32_t)__builtin_amdgcn_readlane((int)v, 16 * j + __ffs(mask) - 1);
+                            const uint32_t rest = mask & (mask - 1);
+                            if (rest) m2 = (uint32_t)__builtin_amdgcn_readlane((int)v, 16 * j + __ffs(rest) - 1);
+                        } else {
+                            // whole-list scan (fewer than two eligible among the 16, or a lost entry)
+                            const int lc = lens[q];
+                            const uint32_t* lq = lists + (size_t)q * g.list_cap;
+                            for (int e = lane; e < lc; e += 64) {
+                                const uint32_t w0 = lq[e];
+                                const uint32_t w = (w0 >> 21) < (ST[(w0 >> 5) & 0xFFFF] & 0xFFFF) ? w0 : ~0u;
+                                m2 = min(m2, max(m1, w));
+                                m1 = min(m1, w);
+                            }
+                            wave_top2(m1, m2);
+                            m1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)m1);
+                            m2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)m2);
+                        }
+                        if (m1 != ~0u) {
+                            const int d1 = (int)(m1 >> 21);
+                            const int d2 = m2 == ~0u ? INT_MAX : (int)(m2 >> 21);
+                            if (d1 <= kThLow && (float)d1 < (float)d2 * nnratio) {
+                                const int rk = (int)((m1 >> 5) & 0xFFFF);
+                                if (lane == 0) {
+                                    CL[q] = (uint32_t)rk | ((m1 & 31) << 16);
+                                    ST[rk] = (uint32_t)d1 | ((uint32_t)q << 16);
+                                }
+                                // forward into this block's registers now, the next block's later
+                                mdv[r] = rk_c == rk ? d1 : mdv[r];
+                                upd_rk[j] = rk;
+                                upd_d[j] = d1;
+                                // a wave's LDS operations complete in order: only keep the compiler
+                                // from moving later MD reads above these writes
+                                asm volatile("" ::: "memory");
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < 4; j++) mdv[rn] = rk_n == upd_rk[j] ? upd_d[j] : mdv[rn];
+                load(b + kInitR, r);
+            }
+        }
+    }
+    __syncthreads();
+    if (check_orientation) {
+        for (int q = tid; q < nq; q += nt)
+            if (CL[q] != ~0u) atomicAdd(&hist[CL[q] >> 16], 1);   // every push, stolen ones included
+        __syncthreads();
+        if (tid == 0) {   // ComputeThreeMaxima
+            int m1 = 0, m2 = 0, m3 = 0, i1 = -1, i2 = -1, i3 = -1;
+            for (int b = 0; b < kHisto; b++) {
+                const int s = hist[b];
+                if (s > m1) { m3 = m2; m2 = m1; m1 = s; i3 = i2; i2 = i1; i1 = b; }
+                else if (s > m2) { m3 = m2; m2 = s; i3 = i2; i2 = b; }
+                else if (s > m3) { m3 = s; i3 = b; }
+            }
+            if (m2 < 0.1f * (float)m1) { i2 = -1; i3 = -1; }
+            else if (m3 < 0.1f * (float)m1) { i3 = -1; }
+            keep[0] = i1; keep[1] = i2; keep[2] = i3;
+        }
+        __syncthreads();
+    }
+    int c = 0;
+    for (int q = tid; q < nq; q += nt) {
+        int rk = CL[q] == ~0u ? -1 : (int)(CL[q] & 0xFFFF);
+        if (rk >= 0 && (int)(ST[rk] >> 16) != q) rk = -1;   // stolen by a later query
+        if (rk >= 0 && check_orientation) {
+            const int b = (int)(CL[q] >> 16);
+            if (b != keep[0] && b != keep[1] && b != keep[2]) rk = -1;
+        }
+        if (rk >= 0) {
+            const int i1 = qlist[q], k = slot[rk];
+            matches12[i1] = k;
+            prev[2 * i1] = kps2[k].x;
+            prev[2 * i1 + 1] = kps2[k].y;
+            c++;
+        }
+    }
+    atomicAdd(&cnt, c);
+    __syncthreads();
+    if (tid == 0) *nmatch = cnt;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -506,6 +877,79 @@ int proj_search_local(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_loc
     std::memcpy(in_view, H + o_iv, nq);
     if (rounds_out) *rounds_out = rounds;
     return *(int*)(H + o_flag);
+}
+
+int init_search(ProjWorkspace* ws, const orbhip_init_frame* F1, const orbhip_init_frame* F2, float* prev_matched,
+                int window_size, float nnratio, int check_orientation, int32_t* matches12, hipStream_t st) {
+    if (!ws || !F1 || !F2 || !prev_matched || !matches12 || F1->n < 0 || F2->n < 0 || F1->n > 65535 ||
+        F2->n > 65535 || (F1->n && (!F1->kps || !F1->desc)) || (F2->n && (!F2->kps || !F2->desc)) ||
+        !(F2->max_x > F2->min_x) || !(F2->max_y > F2->min_y))
+        return ORBHIP_ERR_ARG;
+    const int n1 = F1->n, n2 = F2->n;
+    for (int i = 0; i < n1; i++) matches12[i] = -1;
+    if (n1 == 0) return 0;
+    // capacity from the octave-0 counts (bounds of the device-side queries / ranks)
+    // (octaves are >= 0: ORBextractor levels; a negative octave would disable the level check)
+    int nq0 = 0, nr0 = 0;
+    for (int i = 0; i < n1; i++) {
+        if (F1->kps[i].octave < 0) return ORBHIP_ERR_ARG;
+        nq0 += F1->kps[i].octave == 0;
+    }
+    for (int k = 0; k < n2; k++) nr0 += F2->kps[k].octave == 0;
+    const size_t lds = 4 * (size_t)nr0 + 4 * (size_t)nq0 + 16;
+    if (lds > 150 * 1024) return ORBHIP_ERR_UNSUPPORTED;
+    const int list_cap = std::max(64, (nr0 + 63) & ~63);
+    if ((size_t)std::max(nq0, 1) * list_cap > ((size_t)1 << 28)) return ORBHIP_ERR_UNSUPPORTED;
+    // the kernel's static LDS (histogram) comes on top of the dynamic 150 KiB envelope
+    static const hipError_t attr = hipFuncSetAttribute((const void*)k_init_greedy,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024);
+    PJOK(attr);
+    Layout lay;
+    const size_t o_k1 = lay.add(sizeof(orbhip_kp) * n1), o_d1 = lay.add(32 * (size_t)n1);
+    const size_t o_k2 = lay.add(sizeof(orbhip_kp) * std::max(n2, 1)), o_d2 = lay.add(32 * (size_t)std::max(n2, 1));
+    const size_t o_prev = lay.add(8 * (size_t)n1), o_in_end = lay.off;
+    const size_t o_match = lay.add(4 * (size_t)n1), o_cnt = lay.add(16), o_out_end = lay.off;
+    const size_t o_slot = lay.add(4 * (size_t)std::max(n2, 1)), o_ql = lay.add(4 * (size_t)n1);
+    const size_t o_len = lay.add(4 * ((size_t)n1 + 1)), o_list = lay.add(4 * (size_t)std::max(nq0, 1) * list_cap);
+    const size_t o_topk = lay.add(4 * (size_t)kInitK * (((size_t)std::max(nq0, 1) + 3) & ~size_t(3)));
+    const size_t o_need = lay.add(4 * (size_t)std::max(nq0, 1));
+    if (int rc = ensure(ws, lay.off)) return rc;
+    char* H = (char*)ws->h;
+    char* D = (char*)ws->d;
+    std::memcpy(H + o_k1, F1->kps, sizeof(orbhip_kp) * n1);
+    std::memcpy(H + o_d1, F1->desc, 32 * (size_t)n1);
+    if (n2) {
+        std::memcpy(H + o_k2, F2->kps, sizeof(orbhip_kp) * n2);
+        std::memcpy(H + o_d2, F2->desc, 32 * (size_t)n2);
+    }
+    std::memcpy(H + o_prev, prev_matched, 8 * (size_t)n1);
+    PJOK(hipMemcpyAsync(D, H, o_in_end, hipMemcpyHostToDevice, st));
+    InitGeom g{};
+    g.n1 = n1; g.n2 = n2;
+    g.minx = F2->min_x; g.maxx = F2->max_x; g.miny = F2->min_y; g.maxy = F2->max_y;
+    g.invw = (float)kGridCols / (g.maxx - g.minx);
+    g.invh = (float)kGridRows / (g.maxy - g.miny);
+    g.r = (float)window_size;
+    g.list_cap = list_cap;
+    const orbhip_kp* dk1 = (const orbhip_kp*)(D + o_k1);
+    const orbhip_kp* dk2 = (const orbhip_kp*)(D + o_k2);
+    int* counts = (int*)(D + o_cnt);
+    hipLaunchKernelGGL(k_init_prep, dim3(1), dim3(1024), 0, st, g, dk1, dk2, (int*)(D + o_slot), (int*)(D + o_ql),
+                       counts);
+    hipLaunchKernelGGL(k_init_cands, dim3((unsigned)std::max(1, (nq0 + 3) / 4)), dim3(256), 0, st, g, dk1,
+                       (const uint8_t*)(D + o_d1), dk2, (const uint8_t*)(D + o_d2), (const float*)(D + o_prev),
+                       (const int*)(D + o_slot), (const int*)(D + o_ql), (const int*)counts, (uint32_t*)(D + o_list),
+                       (int*)(D + o_len), (uint32_t*)(D + o_topk), (int*)(D + o_need));
+    hipLaunchKernelGGL(k_init_greedy, dim3(1), dim3(256), lds, st, g, nnratio, check_orientation, dk2,
+                       (const int*)(D + o_slot), (const int*)(D + o_ql), (const int*)counts,
+                       (const uint32_t*)(D + o_list), (const int*)(D + o_len), (const uint32_t*)(D + o_topk),
+                       (const int*)(D + o_need), (int32_t*)(D + o_match), (float*)(D + o_prev), counts + 2);
+    PJOK(hipGetLastError());
+    PJOK(hipMemcpyAsync(H + o_prev, D + o_prev, o_out_end - o_prev, hipMemcpyDeviceToHost, st));
+    PJOK(hipStreamSynchronize(st));
+    std::memcpy(matches12, H + o_match, 4 * (size_t)n1);
+    std::memcpy(prev_matched, H + o_prev, 8 * (size_t)n1);
+    return ((int*)(H + o_cnt))[2];
 }
 
 }  // namespace orbhip

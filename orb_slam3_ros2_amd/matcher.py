@@ -4,7 +4,8 @@
 acceptance rule shared by SearchByBoW / SearchForInitialization — best/second over the
 train set, ``best <= TH_LOW`` and ``best < mfNNratio * second``, then the 30-bin rotation
 histogram (ComputeThreeMaxima) when ``mbCheckOrientation`` — order-free over the whole
-train set (the greedy one-to-one pass of those functions is not applied).
+train set (the C3 brute-force matcher). ``SearchForInitialization`` is the reference function
+itself, with its windowed, greedy (stealing) one-to-one semantics.
 """
 from __future__ import annotations
 
@@ -12,7 +13,7 @@ import ctypes
 
 import numpy as np
 
-from ._lib import (KP_DTYPE, FrameC, LocalPointsC, ProjLastC, torch_stream, Context, check, lib, ptr)
+from ._lib import (KP_DTYPE, FrameC, InitFrameC, LocalPointsC, ProjLastC, torch_stream, Context, check, lib, ptr)
 
 
 class ORBmatcher:
@@ -74,6 +75,25 @@ class ORBmatcher:
                                           ptr(fa), ptr(fn), ptr(fw), nf, ctypes.c_float(self.mfNNratio),
                                           int(self.mbCheckOrientation), th, ptr(m)), "orbhip_search_bow")
         return n, m
+
+    def SearchForInitialization(self, kps1, desc1, kps2, desc2, vbPrevMatched, windowSize: int = 10,
+                                bounds2=(0.0, 640.0, 0.0, 480.0)):
+        """U:src/ORBmatcher.cc::SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)
+        with the exact greedy semantics (Tracking::MonocularInitialization uses ORBmatcher(0.9, true)
+        and windowSize 100). kps: orbhip_kp records; bounds2 = F2's (mnMinX, mnMaxX, mnMinY, mnMaxY).
+        Returns (nmatches, vnMatches12, vbPrevMatched updated for the matches)."""
+        k1 = np.ascontiguousarray(kps1, KP_DTYPE); k2 = np.ascontiguousarray(kps2, KP_DTYPE)
+        d1 = np.ascontiguousarray(desc1, np.uint8).reshape(-1, 32)
+        d2 = np.ascontiguousarray(desc2, np.uint8).reshape(-1, 32)
+        prev = np.ascontiguousarray(vbPrevMatched, np.float32).reshape(-1, 2).copy()
+        m = np.full(k1.shape[0], -1, np.int32)
+        f1 = InitFrameC(k1.shape[0], ptr(k1), ptr(d1), 0.0, 1.0, 0.0, 1.0)
+        f2 = InitFrameC(k2.shape[0], ptr(k2), ptr(d2), *[float(b) for b in bounds2])
+        n = check(lib().orbhip_search_for_initialization(self.ctx.handle, ctypes.byref(f1), ctypes.byref(f2),
+                                                         ptr(prev), int(windowSize), ctypes.c_float(self.mfNNratio),
+                                                         int(self.mbCheckOrientation), ptr(m)),
+                  "orbhip_search_for_initialization")
+        return n, m, prev
 
     # ---- projection-guided matching (SURVEY.md §8f rank 1) ----
     def SearchByProjectionLastFrame(self, frame: "ProjFrame", points, mp_desc, last_octave, last_angle,

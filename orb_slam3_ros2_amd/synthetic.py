@@ -251,3 +251,67 @@ def synthetic_projection_scene(n_kp=1000, n_mp=900, seed=5, dup_frac=0.15, distr
                 cy=cam["cy"], points=pts.astype(np.float32), mp_desc=mdesc, last_octave=octave, last_angle=angle,
                 normals=normals.astype(np.float32), min_dist=min_dist.astype(np.float32),
                 max_dist=max_dist.astype(np.float32), claimed=claimed, skip=skip, src=src)
+
+
+def _flip_bits(rng, d, nb):
+    d = d.copy()
+    for b in rng.choice(256, nb, replace=False):
+        d[b >> 3] ^= np.uint8(1 << (b & 7))
+    return d
+
+
+def synthetic_init_pair(n1=1500, seed=9, width=640, height=480, n_levels=8, level0_frac=0.6, steal_frac=0.15,
+                        distractor_frac=0.3, rot_deg=10.0, shift=(14.0, -6.0)):
+    """Two frames for monocular initialisation (U:src/ORBmatcher.cc::SearchForInitialization):
+    F1 keypoints (level0_frac on octave 0), F2 = F1 moved by `shift` px + jitter with 0-30
+    flipped descriptor bits and a rotation of ~rot_deg (some random, for the histogram filter),
+    some on octave 1 (level filter), plus distractors; `steal_frac` of the F1 level-0 keypoints get
+    a later F1 twin near them whose descriptor is closer to the same F2 keypoint (the greedy
+    steal path). F2 is shuffled. Returns (kps1, desc1, kps2, desc2, prev_matched)."""
+    from ._lib import KP_DTYPE
+    rng = np.random.Generator(np.random.PCG64(seed))
+    k1 = np.zeros(n1, KP_DTYPE)
+    k1["x"] = rng.uniform(0, width, n1).astype(np.float32)
+    k1["y"] = rng.uniform(0, height, n1).astype(np.float32)
+    k1["octave"] = np.where(rng.random(n1) < level0_frac, 0, rng.integers(1, n_levels, n1))
+    k1["angle"] = rng.uniform(0, 360, n1).astype(np.float32)
+    k1["size"] = 31.0
+    k1["response"] = rng.uniform(20, 80, n1).astype(np.float32)
+    d1 = rng.integers(0, 256, (n1, 32), dtype=np.uint8)
+    k2, d2 = [], []
+    for i in range(n1):
+        if k1["octave"][i] != 0 or rng.random() < 0.2:
+            continue
+        r = np.zeros(1, KP_DTYPE)[0]
+        r["x"] = np.float32(k1["x"][i] + shift[0] + rng.normal() * 3)
+        r["y"] = np.float32(k1["y"][i] + shift[1] + rng.normal() * 3)
+        r["octave"] = 0 if rng.random() > 0.05 else 1
+        rot = rot_deg + rng.normal() * 2 if rng.random() > 0.1 else rng.uniform(0, 360)
+        r["angle"] = np.float32((k1["angle"][i] - rot) % 360.0)
+        r["size"] = 31.0
+        r["response"] = np.float32(50)
+        k2.append(r)
+        d2.append(_flip_bits(rng, d1[i], int(rng.integers(0, 31))))
+    # steals: a later F1 keypoint near i whose descriptor is closer to i's F2 partner
+    n2m = len(k2)
+    for j in rng.choice(n2m, int(steal_frac * n2m), replace=False):
+        t = rng.integers(0, n1)
+        k1["octave"][t] = 0
+        k1["x"][t] = np.float32(k2[j]["x"] - shift[0] + rng.normal() * 5)
+        k1["y"][t] = np.float32(k2[j]["y"] - shift[1] + rng.normal() * 5)
+        k1["angle"][t] = np.float32((k2[j]["angle"] + rot_deg) % 360.0)
+        d1[t] = _flip_bits(rng, d2[j], int(rng.integers(0, 12)))
+    nd = int(distractor_frac * n2m)
+    for _ in range(nd):
+        r = np.zeros(1, KP_DTYPE)[0]
+        r["x"] = np.float32(rng.uniform(0, width)); r["y"] = np.float32(rng.uniform(0, height))
+        r["octave"] = 0; r["angle"] = np.float32(rng.uniform(0, 360)); r["size"] = 31.0; r["response"] = 40.0
+        k2.append(r)
+        # near-copies of a random F1 descriptor: second-best competition for the ratio test
+        d2.append(_flip_bits(rng, d1[rng.integers(0, n1)], int(rng.integers(5, 40))))
+    k2 = np.array(k2, KP_DTYPE)
+    d2 = np.stack(d2).astype(np.uint8)
+    perm = rng.permutation(k2.shape[0])
+    k2, d2 = k2[perm], d2[perm]
+    prev = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
+    return k1, d1, k2, d2, prev
