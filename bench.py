@@ -32,9 +32,16 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-STAGES = {1: "k_resize (7 levels)", 2: "k_fast_cells", 3: "k_octree", 4: "k_desc", 5: "k_match_top2",
-          6: "k_match_finish"}
-KERNEL_SYMBOL = {1: "k_resize", 2: "k_fast_cells", 3: "k_octree", 4: "k_desc", 5: "k_match_top2", 6: "k_match_finish"}
+STAGES = {1: "pyramid (k_pyr_cone | 7x k_resize)", 2: "k_fast_cells", 3: "k_octree", 4: "rBRIEF (k_desc_kp | k_desc)",
+          5: "k_match_top2", 6: "k_match_finish"}
+
+
+def kernel_symbol(stage, batch):
+    """The kernel a stage launches at this batch size (liborbhip picks the small-batch variants
+    while B x tiles / keypoints leave the chip idle: orbhip_api.cpp run_extract, launch_desc)."""
+    small = batch <= 4
+    return {1: "k_pyr_cone" if small else "k_resize", 2: "k_fast_cells", 3: "k_octree",
+            4: "k_desc_kp" if small else "k_desc", 5: "k_match_top2", 6: "k_match_finish"}[stage]
 
 
 def parse():
@@ -428,7 +435,8 @@ def main():
                    "keypoints_per_frame": round(nkp, 1), "matches_last_pair": nmatch},
         "roofline": {"kernel": STAGES[dom], "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                     "traffic": load_traffic(KERNEL_SYMBOL[dom]),
+                     "kernel_symbol": kernel_symbol(dom, 1),
+                     "traffic": load_traffic(kernel_symbol(dom, 1)),
                      "algorithmic_bytes_per_launch": int(dom_bytes), "avg_launch_ms": round(dom_avg_ms, 5),
                      "launches_timed": dom_n,
                      "stage_avg_ms_calibration": {STAGES[k]: round(v, 5) for k, v in stage_ms.items()}},

@@ -12,6 +12,7 @@
 //
 // Everything is integer or reproduces host float rounding exactly (-ffp-contract=off).
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include "../../include/orbhip.h"
 #include "../../include/orbhip_pattern.h"
@@ -97,6 +98,10 @@ __global__ __launch_bounds__(256) void k_resize(const ExtractPlan* __restrict__ 
     if (l == 1) { TR_END(0) }
 }
 
+// quotient of i / d for 0 <= i < 2^16, d >= 1: the float reciprocal's error stays below the
+// 0.5/d margin of (i + 0.5)/d to the next integer
+__device__ __forceinline__ int small_div(int i, float inv_d) { return (int)(((float)i + 0.5f) * inv_d); }
+
 // ---------------------------------------------------------------------------
 // k_pyr_cone: the whole cascade (levels 1..L-1) in ONE launch. Each workgroup owns a tile of
 // the last level and the matching slice of every level (a partition per level); it recomputes
@@ -109,9 +114,8 @@ __global__ __launch_bounds__(256) void k_resize(const ExtractPlan* __restrict__ 
 // (xofs, xalpha) of its need columns and the row table (clamped r0, r1, ybeta) of its rows: one
 // global round trip loads every table entry and the level-0 cone, then the levels follow from LDS.
 __global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict__ P, FrameBufs fb,
-                                                   const ConeRect* __restrict__ rects, const int* __restrict__ xofs,
-                                                   const int* __restrict__ xalpha, const int* __restrict__ yofs,
-                                                   const int* __restrict__ ybeta) {
+                                                   const ConeRect* __restrict__ rects, const int* __restrict__ ctab,
+                                                   int tab_stride) {
     TR_BEGIN()
     extern __shared__ __attribute__((aligned(16))) uint8_t cone[];
     const int tile = blockIdx.x, f = blockIdx.y, L = P->n_levels, tid = threadIdx.x, nt = blockDim.x;
@@ -128,36 +132,43 @@ __global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict
         toff[l] = ttot;
         ttot += 2 * (R[l].nx1 - R[l].nx0) + 3 * (R[l].ny1 - R[l].ny0);
     }
-    // ---- one round trip: tables of every level + the level-0 cone ----
-    for (int l = 1; l < L; l++) {
-        const LevelGeom& D = P->lv[l];
-        const LevelGeom& S = P->lv[l - 1];
-        const ConeRect r = R[l];
-        const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0;
-        int* t = tab + toff[l];
-        for (int i = tid; i < nw + nh; i += nt) {
-            if (i < nw) {
-                t[i] = xofs[D.xtab_off + r.nx0 + i];
-                t[nw + i] = xalpha[D.xtab_off + r.nx0 + i];
-            } else {
-                const int j = i - nw;
-                const int sy = yofs[D.ytab_off + r.ny0 + j];
-                t[2 * nw + 3 * j] = sy < 0 ? 0 : (sy < S.h ? sy : S.h - 1);
-                t[2 * nw + 3 * j + 1] = sy + 1 < 0 ? 0 : (sy + 1 < S.h ? sy + 1 : S.h - 1);
-                t[2 * nw + 3 * j + 2] = ybeta[D.ytab_off + r.ny0 + j];
-            }
-        }
-    }
+    // ---- one round trip: the tile's tables of every level (prebuilt by the host in LDS layout)
+    // and its level-0 cone, all loads issued before any store ----
     {
         const ImgRef in0 = level_img(P, fb, f, 0);
         const ConeRect r = R[0];
         const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0;
-        for (int i = tid; i < nw * nh; i += nt) {
-            const int y = i / nw, x = i - y * nw;
-            cone[boff[0] + i] = in0.p[(int64_t)(r.ny0 + y) * in0.pitch + r.nx0 + x];
+        const int tot0 = nw * nh;
+        const float inv_nw = 1.0f / (float)nw;
+        const uint8_t* src0 = in0.p + (int64_t)r.ny0 * in0.pitch + r.nx0;
+        const int* gt = ctab + (size_t)tile * tab_stride;
+        if (tot0 <= 4 * 1024 && ttot <= 2 * 1024 && nt == 1024) {
+            uint8_t v[4];
+            int tv[2];
+#pragma unroll
+            for (int u = 0; u < 2; u++) tv[u] = gt[min(tid + 1024 * u, ttot - 1)];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = min(tid + 1024 * u, tot0 - 1);
+                const int y = small_div(i, inv_nw), x = i - y * nw;
+                v[u] = src0[(int64_t)y * in0.pitch + x];
+            }
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+                if (tid + 1024 * u < ttot) tab[tid + 1024 * u] = tv[u];
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (tid + 1024 * u < tot0) cone[boff[0] + tid + 1024 * u] = v[u];
+        } else {
+            for (int i = tid; i < ttot; i += nt) tab[i] = gt[i];
+            for (int i = tid; i < tot0; i += nt) {
+                const int y = small_div(i, inv_nw), x = i - y * nw;
+                cone[boff[0] + i] = src0[(int64_t)y * in0.pitch + x];
+            }
         }
     }
     __syncthreads();
+    TR_PHASE(0, 0)
     for (int l = 1; l < L; l++) {
         const LevelGeom& D = P->lv[l];
         const ConeRect r = R[l], rp = R[l - 1];
@@ -165,8 +176,9 @@ __global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict
         const int* t = tab + toff[l];
         const uint8_t* src = cone + boff[l - 1];
         uint8_t* dst = fb.pyr + (int64_t)f * P->pyr_bytes + D.pyr_off;
+        const float inv_nw = 1.0f / (float)nw;
         for (int i = tid; i < nw * nh; i += nt) {
-            const int yy = i / nw, xx = i - yy * nw;
+            const int yy = small_div(i, inv_nw), xx = i - yy * nw;
             const int x = r.nx0 + xx, y = r.ny0 + yy;
             const int sx = t[xx] - rp.nx0;
             const uint8_t* S0 = src + (t[2 * nw + 3 * yy] - rp.ny0) * nwp;
@@ -198,6 +210,7 @@ __global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict
             if (x >= r.ox0 && x < r.ox1 && y >= r.oy0 && y < r.oy1) dst[(int64_t)y * D.pitch + x] = u;
         }
         __syncthreads();
+        TR_PHASE(0, l)
     }
     TR_END(0)
 }
@@ -230,8 +243,6 @@ __device__ __forceinline__ int fast_strength_d(const int* d) {
     return m < 0 ? 0 : m;
 }
 
-// quotient of i / d for 0 <= i < 2^16, 1 <= d <= 128: float reciprocal with margin >= 0.5/d
-__device__ __forceinline__ int small_div(int i, float inv_d) { return (int)(((float)i + 0.5f) * inv_d); }
 
 // Is the pixel a FAST corner candidate at threshold t? Necessary condition of a 9-arc: every
 // opposite pair (k, k+8) has at least one member beyond v +- t on the arc's side.
@@ -245,14 +256,16 @@ __device__ __forceinline__ bool fast_pair_test(const int* d, int t) {
     return bright | dark;
 }
 
-__global__ __launch_bounds__(256) void k_fast_cells(const ExtractPlan* __restrict__ P,
+template <int NT>
+__global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict__ P,
                                                     const CellGeom* __restrict__ cells, FrameBufs fb,
                                                     uint32_t* __restrict__ cand, int* __restrict__ cand_cnt,
                                                     int* __restrict__ err) {
     __shared__ uint8_t win[kWinMax * kWinMax];
     __shared__ uint8_t mv[kWinMax * kWinMax];
-    __shared__ uint64_t masks[4][2][24];   // per wave, per threshold, per 64-px chunk
-    __shared__ int wcnt[2][4];
+    constexpr int NW = NT / 64, NCH = 96 / NW;   // windows up to 6144 px
+    __shared__ uint64_t masks[NW][2][NCH];   // per wave, per threshold, per 64-px chunk
+    __shared__ int wcnt[2][NW];
     TR_BEGIN()
     const CellGeom cg = cells[blockIdx.x];
     const int f = blockIdx.y;
@@ -271,23 +284,24 @@ __global__ __launch_bounds__(256) void k_fast_cells(const ExtractPlan* __restric
     {
         const int tot = wc * hc;
         const float inv_wc = 1.0f / (float)wc;
-        if (tot <= 8 * 256) {
-            // normal cells (window <= 2048 px): 8 unconditional loads from clamped addresses,
+        constexpr int NU = 2048 / NT;
+        if (tot <= NU * NT) {
+            // normal cells (window <= 2048 px): unconditional loads from clamped addresses,
             // straight-line so all are in flight together, then predicated stores
-            uint8_t v[8];
+            uint8_t v[NU];
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int i = min(tid + 256 * u, tot - 1);
+            for (int u = 0; u < NU; u++) {
+                const int i = min(tid + NT * u, tot - 1);
                 const int yy = small_div(i, inv_wc), xx = i - yy * wc;
                 v[u] = base[(int64_t)yy * im.pitch + xx];
             }
 #pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int i = tid + 256 * u;
+            for (int u = 0; u < NU; u++) {
+                const int i = tid + NT * u;
                 if (i < tot) win[i] = v[u];
             }
         } else {
-            for (int i = tid; i < tot; i += 256) {
+            for (int i = tid; i < tot; i += NT) {
                 const int yy = small_div(i, inv_wc), xx = i - yy * wc;
                 win[i] = base[(int64_t)yy * im.pitch + xx];
             }
@@ -302,11 +316,11 @@ __global__ __launch_bounds__(256) void k_fast_cells(const ExtractPlan* __restric
     // ---- strength map: m if m > t_lo (a corner at some threshold in use), else 0; stored with
     // a zero border (row pitch W2 = dc + 2) so the NMS reads its 3x3 without bounds checks ----
     const int W2 = dc + 2;
-    for (int i = tid; i < 2 * W2 + 2 * dr; i += 256) {
+    for (int i = tid; i < 2 * W2 + 2 * dr; i += NT) {
         const int idx = i < W2 ? i : (i < 2 * W2 ? (dr + 1) * W2 + (i - W2) : (1 + (i - 2 * W2) / 2) * W2 + ((i & 1) ? W2 - 1 : 0));
         mv[idx] = 0;
     }
-    for (int p = tid; p < np; p += 256) {
+    for (int p = tid; p < np; p += NT) {
         const int py = small_div(p, inv_dc), px = p - py * dc;
         const uint8_t* c = &win[(py + 3) * wc + px + 3];
         const int o[16] = {3 * wc,      3 * wc + 1,  2 * wc + 2,  wc + 3,      3,      -wc + 3, -2 * wc + 2, -3 * wc + 1,
@@ -325,7 +339,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(const ExtractPlan* __restric
     __syncthreads();
     TR_PHASE(1, 1)
     // ---- window-local strict 3x3 NMS at both thresholds; wave w owns pixels [w*chunk, ...) ----
-    const int chunk = ((np + 255) / 256) * 64;   // multiple of 64 per wave
+    const int chunk = ((np + NT - 1) / NT) * 64;   // multiple of 64 per wave
     const int p0 = wid * chunk, p1 = min(np, p0 + chunk);
     int c_ini = 0, c_min = 0;
     for (int q0 = p0, ci = 0; q0 < p1; q0 += 64, ci++) {
@@ -354,7 +368,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(const ExtractPlan* __restric
     if (lane == 0) { wcnt[0][wid] = c_ini; wcnt[1][wid] = c_min; }
     __syncthreads();
     TR_PHASE(1, 2)
-    const int total_ini = wcnt[0][0] + wcnt[0][1] + wcnt[0][2] + wcnt[0][3];
+    int total_ini = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) total_ini += wcnt[0][w];
     const int sel = total_ini > 0 ? 0 : 1;   // per-cell fallback iniThFAST -> minThFAST
     int off = 0;
     for (int w = 0; w < wid; w++) off += wcnt[sel][w];
@@ -370,7 +386,12 @@ __global__ __launch_bounds__(256) void k_fast_cells(const ExtractPlan* __restric
         }
         off += __popcll(mk);
     }
-    if (tid == 0) *cnt_out = wcnt[sel][0] + wcnt[sel][1] + wcnt[sel][2] + wcnt[sel][3];
+    if (tid == 0) {
+        int c = 0;
+#pragma unroll
+        for (int w = 0; w < NW; w++) c += wcnt[sel][w];
+        *cnt_out = c;
+    }
     TR_PHASE(1, 3)
     TR_END(1)
 }
@@ -971,6 +992,152 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
     }
 }
 
+// k_desc_kp: the same computation with ONE KEYPOINT PER WORK-GROUP (4 waves). At small batches
+// (C2: ~1000 keypoints, one frame) k_desc's single wave per keypoint is issue-bound on its own
+// instruction stream while most of the chip idles; here the patch load, the IC_Angle disc, both
+// blur passes and the 256 rBRIEF pairs are spread over 256 threads, and each wave's 64 pair bits
+// leave as one ballot (bytes 8w..8w+7 of the descriptor).
+__global__ __launch_bounds__(256) void k_desc_kp(const ExtractPlan* __restrict__ P, FrameBufs fb,
+                                                 const LevelKp* __restrict__ lvl_kp, const int* __restrict__ lvl_cnt,
+                                                 const int* __restrict__ lvl_nlap, const int* __restrict__ disc,
+                                                 orbhip_kp* __restrict__ out_kps, uint8_t* __restrict__ out_desc,
+                                                 int cap, int* __restrict__ n_out, int* __restrict__ mono_out) {
+    __shared__ uint8_t pt[kPatchW * kPatchW + 15];
+    __shared__ uint16_t hr[kPatchW * kBlW];
+    __shared__ uint8_t bl[kBlW * kBlW + 7];
+    __shared__ int msum[2][4];
+    TR_BEGIN()
+    const int f = blockIdx.y;
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+    int slot = blockIdx.x;
+    const int L = P->n_levels;
+    int total = 0, nlap_tot = 0;
+    for (int l = 0; l < L; l++) { total += lvl_cnt[f * L + l]; nlap_tot += lvl_nlap[f * L + l]; }
+    if (blockIdx.x == 0 && tid == 0) {
+        n_out[f] = total;
+        mono_out[f] = total - nlap_tot;
+    }
+    int l = 0, mono_base = 0, lap_base = 0;
+    while (l < L && slot >= P->lv[l].kp_cap) {
+        slot -= P->lv[l].kp_cap;
+        mono_base += lvl_cnt[f * L + l] - lvl_nlap[f * L + l];
+        lap_base += lvl_nlap[f * L + l];
+        l++;
+    }
+    if (!(l < L && slot < lvl_cnt[f * L + l])) return;   // block-uniform
+    const LevelGeom& G = P->lv[l];
+    const LevelKp kp = lvl_kp[(int64_t)f * P->kp_slots_total + G.kp_base + slot];
+    const int cx = kp.x, cy = kp.y;
+    {
+        ImgRef im = level_img(P, fb, f, l);
+        const int lw = G.w, lh = G.h;
+        const bool inside = cx - kPatchR >= 0 && cy - kPatchR >= 0 && cx + kPatchR < lw && cy + kPatchR < lh;
+        constexpr int kPU = (kPatchW * kPatchW + 255) / 256;   // 8 bytes per thread
+        constexpr float kInvPW = 1.0f / kPatchW;
+        uint8_t v[kPU];
+#pragma unroll
+        for (int u = 0; u < kPU; u++) {
+            const int i = min(tid + 256 * u, kPatchW * kPatchW - 1);   // branch-free loads
+            const int py = (int)(((float)i + 0.5f) * kInvPW), px = i - py * kPatchW;
+            int yy = cy - kPatchR + py, xx = cx - kPatchR + px;
+            if (!inside) {   // BORDER_REFLECT_101 (levels are >= 43 px in both dims)
+                yy = yy < 0 ? -yy : (yy >= lh ? 2 * lh - 2 - yy : yy);
+                xx = xx < 0 ? -xx : (xx >= lw ? 2 * lw - 2 - xx : xx);
+            }
+            v[u] = im.p[(int64_t)yy * im.pitch + xx];
+        }
+#pragma unroll
+        for (int u = 0; u < kPU; u++) {
+            const int i = tid + 256 * u;
+            if (i < kPatchW * kPatchW) pt[i] = v[u];
+        }
+    }
+    __syncthreads();
+    TR_PHASE(3, 0)
+    // ---- IC_Angle partial moments over the umax disc (unblurred level) + blur row pass ----
+    {
+        int m10 = 0, m01 = 0;
+        for (int i = tid; i < P->n_disc; i += 256) {
+            const int uv = disc[i];
+            const int u = (int)(int16_t)(uv & 0xFFFF), vv = (int)(int16_t)(uv >> 16);
+            const int val = pt[(kPatchR + vv) * kPatchW + kPatchR + u];
+            m10 += u * val;
+            m01 += vv * val;
+        }
+        m10 = wave_sum_i32(m10);
+        m01 = wave_sum_i32(m01);
+        if (lane == 0) { msum[0][wid] = m10; msum[1][wid] = m01; }
+        for (int t = tid; t < kPatchW * 10; t += 256) {
+            const int r = (int)(((float)t + 0.5f) * 0.1f), c0 = 4 * (t - 10 * r);
+            const uint8_t* row = pt + r * kPatchW + c0;
+            uint32_t x[10];
+#pragma unroll
+            for (int i = 0; i < 10; i++) x[i] = c0 + i < kPatchW ? row[i] : 0u;
+#pragma unroll
+            for (int o = 0; o < 4; o++) {
+                if (c0 + o >= kBlW) break;
+                uint32_t h = 0;
+#pragma unroll
+                for (int i = 0; i < 7; i++) h += blur_tap(i) * x[o + i];
+                hr[r * kBlW + c0 + o] = (uint16_t)h;
+            }
+        }
+    }
+    __syncthreads();
+    // ---- column pass: bl[r][c] = (sum_j k_j hr[r + j][c] + 2^15) >> 16, 4 rows per task ----
+    for (int t = tid; t < kBlW * 10; t += 256) {
+        const int rb = (int)(((float)t + 0.5f) * (1.0f / kBlW)), c = t - kBlW * rb, r0 = 4 * rb;
+        uint32_t y[10];
+#pragma unroll
+        for (int j = 0; j < 10; j++) y[j] = r0 + j < kPatchW ? hr[(r0 + j) * kBlW + c] : 0u;
+#pragma unroll
+        for (int o = 0; o < 4; o++) {
+            if (r0 + o >= kBlW) break;
+            uint32_t sacc = 0;
+#pragma unroll
+            for (int j = 0; j < 7; j++) sacc += blur_tap(j) * y[o + j];
+            bl[(r0 + o) * kBlW + c] = (uint8_t)((sacc + (1u << 15)) >> 16);
+        }
+    }
+    __syncthreads();
+    TR_PHASE(3, 1)
+    // the moments in the reference's summation order do not matter (integers)
+    const int m10 = msum[0][0] + msum[0][1] + msum[0][2] + msum[0][3];
+    const int m01 = msum[1][0] + msum[1][1] + msum[1][2] + msum[1][3];
+    const float angle = fast_atan2((float)m01, (float)m10);
+    const float factorPI = (float)(3.14159265358979323846 / 180.f);
+    const float ang = angle * factorPI;
+    const float a = glibc_cosf(ang), b = glibc_sinf(ang);
+    // pair tid: bit (tid & 7) of byte tid >> 3
+    int bit;
+    {
+        const float px0 = (float)kPattern[4 * tid], py0 = (float)kPattern[4 * tid + 1];
+        const float px1 = (float)kPattern[4 * tid + 2], py1 = (float)kPattern[4 * tid + 3];
+        const int t0 = bl[(kBlR + cv_round(px0 * b + py0 * a)) * kBlW + kBlR + cv_round(px0 * a - py0 * b)];
+        const int t1 = bl[(kBlR + cv_round(px1 * b + py1 * a)) * kBlW + kBlR + cv_round(px1 * a - py1 * b)];
+        bit = t0 < t1;
+    }
+    const uint64_t word = __ballot(bit);
+    TR_PHASE(3, 2)
+    TR_END(3)
+    const int lapflag = (kp.srl >> 8) & 1;
+    const int rank = (int)(kp.srl >> 9);
+    const int idx = lapflag ? (total - 1 - (lap_base + rank)) : (mono_base + rank);
+    if (idx >= cap) return;
+    if (lane == 0) *(uint64_t*)(out_desc + ((int64_t)f * cap + idx) * 32 + 8 * wid) = word;
+    if (tid == 0) {
+        orbhip_kp o;
+        const float sc = G.scale;
+        o.x = (l == 0) ? (float)cx : (float)cx * sc;
+        o.y = (l == 0) ? (float)cy : (float)cy * sc;
+        o.size = (float)G.patch_size;
+        o.angle = angle;
+        o.response = (float)(kp.srl & 0xFF);
+        o.octave = l;
+        out_kps[(int64_t)f * cap + idx] = o;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // host-side launchers
 // ---------------------------------------------------------------------------
@@ -983,19 +1150,30 @@ void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs
 }
 
 void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameBufs& fb, int B, const ConeRect* rects,
-                     const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st) {
+                     const int* ctab, int tab_stride, hipStream_t st) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_pyr_cone, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL(k_pyr_cone, dim3(ntiles, B), dim3(1024), lds, st, dP, fb, rects, xofs, xalpha, yofs, ybeta);
+    hipLaunchKernelGGL(k_pyr_cone, dim3(ntiles, B), dim3(1024), lds, st, dP, fb, rects, ctab, tab_stride);
 }
 
 void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,
                  uint32_t* cand, int* cand_cnt, int* err, hipStream_t st) {
+    // more threads per cell while the cells alone cannot fill the chip (one frame: ~600 cells on
+    // 256 CUs), as many as keep every work-group resident at once (8192 wave slots); 256 once
+    // the batch fills the chip
+    static const int nt_env = getenv("ORBHIP_FAST_NT") ? atoi(getenv("ORBHIP_FAST_NT")) : 0;
+    const int ncell = B * hP.n_cells_total;
+    const int nt = nt_env ? nt_env : (ncell <= 512 ? 1024 : (ncell <= 1024 ? 512 : 256));
     dim3 grd(hP.n_cells_total, B, 1);
-    hipLaunchKernelGGL(k_fast_cells, grd, dim3(256), 0, st, dP, cells, fb, cand, cand_cnt, err);
+    if (nt == 1024)
+        hipLaunchKernelGGL(k_fast_cells<1024>, grd, dim3(1024), 0, st, dP, cells, fb, cand, cand_cnt, err);
+    else if (nt == 512)
+        hipLaunchKernelGGL(k_fast_cells<512>, grd, dim3(512), 0, st, dP, cells, fb, cand, cand_cnt, err);
+    else
+        hipLaunchKernelGGL(k_fast_cells<256>, grd, dim3(256), 0, st, dP, cells, fb, cand, cand_cnt, err);
 }
 
 size_t octree_lds_bytes(const ExtractPlan& hP, const OctreeCfg& cfg) {
@@ -1024,9 +1202,20 @@ void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom*
                        lvl_cnt, lvl_nlap, cfg, err);
 }
 
+constexpr int kDescKpMaxSlots = 16384;
+
 void launch_desc(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, const LevelKp* lvl_kp,
                  const int* lvl_cnt, const int* lvl_nlap, const int* disc, orbhip_kp* out_kps, uint8_t* out_desc,
                  int cap, int* n_out, int* mono_out, int B, hipStream_t st) {
+    // a keypoint per work-group while the batch leaves the chip mostly idle; a keypoint per wave
+    // (4 per work-group) once there are enough keypoints to fill it
+    static const int mode = getenv("ORBHIP_DESC_MODE") ? atoi(getenv("ORBHIP_DESC_MODE")) : -1;
+    const bool per_wg = mode >= 0 ? mode == 1 : B * hP.kp_slots_total <= kDescKpMaxSlots;
+    if (per_wg) {
+        hipLaunchKernelGGL(k_desc_kp, dim3(hP.kp_slots_total, B, 1), dim3(256), 0, st, dP, fb, lvl_kp, lvl_cnt,
+                           lvl_nlap, disc, out_kps, out_desc, cap, n_out, mono_out);
+        return;
+    }
     dim3 grd((hP.kp_slots_total + 3) / 4, B, 1);
     hipLaunchKernelGGL(k_desc, grd, dim3(256), 0, st, dP, fb, lvl_kp, lvl_cnt, lvl_nlap, disc, out_kps, out_desc,
                        cap, n_out, mono_out);

@@ -66,9 +66,12 @@ struct Plan {
     std::vector<CellGeom> cells;
     std::vector<int> xofs, xalpha, yofs, ybeta, disc;
     std::vector<ConeRect> cone;   // k_pyr_cone tables (empty: per-level k_resize cascade)
+    std::vector<int> cone_tab;    // per tile: every level's resize tables in the kernel's LDS layout
+    int cone_tab_stride = 0;
     int cone_tiles = 0;
     size_t cone_lds = 0;
     DevBuf<ConeRect> d_cone;
+    DevBuf<int> d_cone_tab;
     OctreeCfg oct{};
     int kp_cap_frame = 0;   // sum of level caps = max keypoints per frame
     DevBuf<ExtractPlan> d_plan;
@@ -285,10 +288,13 @@ static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
     P.pyr_bytes = ((pyr_off + 255) / 256) * 256;
     P.max_cells_level = max_cells;
     pl->kp_cap_frame = kp_base;
-    // cone pyramid tables: tiles of ~16x16 on the last level, an even partition of every level
+    // cone pyramid tables: tiles of ~10x10 on the last level (252 at 640x480: the per-tile cascade
+    // is latency bound, so smaller cones finish sooner), an even partition of every level
     if (L > 1) {
         const LevelGeom& T = P.lv[L - 1];
-        const int ntx = (T.w + 15) / 16, nty = (T.h + 15) / 16;
+        static const int ts_env = std::getenv("ORBHIP_CONE_TILE") ? std::atoi(std::getenv("ORBHIP_CONE_TILE")) : 0;
+        const int ts = ts_env > 0 ? ts_env : 10;
+        const int ntx = (T.w + ts - 1) / ts, nty = (T.h + ts - 1) / ts;
         size_t lds_max = 0;
         std::vector<ConeRect> rects((size_t)ntx * nty * kMaxLevels);
         for (int ti = 0; ti < nty; ti++)
@@ -331,7 +337,40 @@ static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
                 tot += ttot;
                 lds_max = std::max(lds_max, tot);
             }
+        // the tables of each tile, in the kernel's LDS layout (row indices clamped to the source)
+        size_t tab_max = 0;
+        for (int t = 0; t < ntx * nty; t++) {
+            size_t tt = 0;
+            for (int l = 1; l < L; l++)
+                tt += 2 * (size_t)(rects[(size_t)t * kMaxLevels + l].nx1 - rects[(size_t)t * kMaxLevels + l].nx0) +
+                      3 * (size_t)(rects[(size_t)t * kMaxLevels + l].ny1 - rects[(size_t)t * kMaxLevels + l].ny0);
+            tab_max = std::max(tab_max, tt);
+        }
+        std::vector<int> ctab((size_t)ntx * nty * tab_max, 0);
+        for (int t = 0; t < ntx * nty; t++) {
+            int* o = ctab.data() + (size_t)t * tab_max;
+            for (int l = 1; l < L; l++) {
+                const LevelGeom& D = P.lv[l];
+                const LevelGeom& S = P.lv[l - 1];
+                const ConeRect r = rects[(size_t)t * kMaxLevels + l];
+                const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0;
+                for (int i = 0; i < nw; i++) {
+                    o[i] = pl->xofs[D.xtab_off + r.nx0 + i];
+                    o[nw + i] = pl->xalpha[D.xtab_off + r.nx0 + i];
+                }
+                auto clampr = [&](int v) { return v < 0 ? 0 : (v < S.h ? v : S.h - 1); };
+                for (int j = 0; j < nh; j++) {
+                    const int sy = pl->yofs[D.ytab_off + r.ny0 + j];
+                    o[2 * nw + 3 * j] = clampr(sy);
+                    o[2 * nw + 3 * j + 1] = clampr(sy + 1);
+                    o[2 * nw + 3 * j + 2] = pl->ybeta[D.ytab_off + r.ny0 + j];
+                }
+                o += 2 * nw + 3 * nh;
+            }
+        }
         if (lds_max <= 60 * 1024) {
+            pl->cone_tab.swap(ctab);
+            pl->cone_tab_stride = (int)tab_max;
             pl->cone.swap(rects);
             pl->cone_tiles = ntx * nty;
             pl->cone_lds = lds_max;
@@ -375,6 +414,7 @@ static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
     if (!pl->cone.empty()) {
         HIPOK(pl->d_cone.ensure(pl->cone.size()));
         HIPOK(hipMemcpy(pl->d_cone.p, pl->cone.data(), pl->cone.size() * sizeof(ConeRect), hipMemcpyHostToDevice));
+        HIPOK(up(pl->d_cone_tab, pl->cone_tab));
     }
     *out = pl.get();
     c->plans[key] = std::move(pl);
@@ -410,8 +450,8 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
     // the cone recomputes each tile's halo on every level: it pays only while the per-level cascade
     // is launch-latency bound (a few work-groups per CU); big batches keep the cascade
     if (pl->cone_tiles && !no_cone && (size_t)B * pl->cone_tiles <= 1024)
-        launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_xofs.p, pl->d_xalpha.p,
-                        pl->d_yofs.p, pl->d_ybeta.p, st);
+        launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_cone_tab.p,
+                        pl->cone_tab_stride, st);
     else
         for (int l = 1; l < P.n_levels; l++)
             launch_resize(pl->d_plan.p, P, fb, B, l, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p, pl->d_ybeta.p, st);

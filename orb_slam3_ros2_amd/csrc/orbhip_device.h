@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 namespace orbhip {
 
 // cvRound(float) on x86 (cvtss2si, MXCSR round-to-nearest-even)
@@ -159,8 +161,12 @@ __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int* total) 
 
 #define ORBHIP_TRACE_UNIT(unit)                                                             \
     static __device__ unsigned long long* g_trace = nullptr;                               \
+    static __device__ int g_trace_blk = 0;                                                 \
     void trace_set_##unit(unsigned long long* p) {                                         \
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &p, sizeof(p));                       \
+        const char* e = std::getenv("ORBHIP_TRACE_BLOCK");                                 \
+        const int b = e ? std::atoi(e) : 0;                                                \
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_trace_blk), &b, sizeof(b));                   \
     }
 
 #define TR_BEGIN()                                                                          \
@@ -172,7 +178,7 @@ __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int* total) 
         tr_tp = __builtin_amdgcn_s_memtime();                                               \
     }
 #define TR_PHASE(kid, ph)                                                                   \
-    if (tr_buf && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) { \
+    if (tr_buf && threadIdx.x == 0 && blockIdx.x == g_trace_blk && blockIdx.y == 0 && blockIdx.z == 0) { \
         const unsigned long long tr_t = __builtin_amdgcn_s_memtime();                       \
         tr_buf[(kid) * kTraceStride + 8192 + (ph)] = tr_t - tr_tp;                          \
         tr_tp = tr_t;                                                                       \

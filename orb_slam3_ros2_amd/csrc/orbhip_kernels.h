@@ -36,7 +36,7 @@ struct StageTimer {
 
 // ---- extraction ----
 void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameBufs& fb, int B, const ConeRect* rects,
-                     const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st);
+                     const int* ctab, int tab_stride, hipStream_t st);
 void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, int B, int l,
                    const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st);
 void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,
