@@ -516,6 +516,33 @@ __device__ __forceinline__ void wave_aggregate_count(uint32_t tgt, uint32_t* cnt
     }
 }
 
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// In-place exclusive scan of arr[0..n) in LDS by ONE wave (a contiguous range per lane, DPP wave
+// scan of the range sums). Returns the total (uniform). No block barrier.
+__device__ int wave_scan_lds(int* arr, int n) {
+    const int lane = threadIdx.x & 63;
+    const int per = (n + 63) >> 6;
+    const int b = min(lane * per, n), e = min(b + per, n);
+    int s = 0;
+    for (int i = b; i < e; i++) s += arr[i];
+    const int inc = wave_incl_scan(s);
+    const int tot = __builtin_amdgcn_readlane(inc, 63);
+    int off = inc - s;
+    for (int i = b; i < e; i++) { const int v = arr[i]; arr[i] = off; off += v; }
+    wave_lds_fence();
+    return tot;
+}
+
+__device__ __forceinline__ int nonempty4(const uint32_t* c) { return (c[0] > 0) + (c[1] > 0) + (c[2] > 0) + (c[3] > 0); }
+__device__ __forceinline__ int multi4(const uint32_t* c) { return (c[0] > 1) + (c[1] > 1) + (c[2] > 1) + (c[3] > 1); }
+
+// The node list work of one division pass runs in wave 0 alone (nodes <= node_cap, a few per
+// lane; DPP scans, no block barriers); the key sweeps use the whole work-group. A MAIN round is
+// then 2 block barriers, a FINAL round 4.
 __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__ P, const CellGeom* __restrict__ cells,
                                                  const uint32_t* __restrict__ cand, const int* __restrict__ cand_cnt,
                                                  uint32_t* __restrict__ kscratch, uint16_t* __restrict__ nscratch,
@@ -525,7 +552,8 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
     TR_BEGIN()
     const int l = blockIdx.x, f = blockIdx.y;
     const LevelGeom& G = P->lv[l];
-    const int tid = threadIdx.x, nt = blockDim.x;
+    const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
+    const bool w0 = tid < 64;
     const int NC = cfg.node_cap;
     // ---- carve LDS (every offset a multiple of 16 bytes) ----
     OctLds S;
@@ -548,69 +576,81 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
     uint16_t* knodeL = (uint16_t*)carve(cfg.key_cap * 2);
     int* ctl = S.ctl;
 
-    // ---- 1. candidate count per cell -> cell-major key order ----
+    // ---- 1. candidate count per cell -> cell-major key order (wave 0 scans the cells) ----
     const int ncell = G.n_cells;
     const int* cc = cand_cnt + (int64_t)f * P->n_cells_total + G.cell_base;
-    for (int i = tid; i < ncell; i += nt) {
-        S.cellstart[i] = cc[i];
-        S.cslot[i] = cells[G.cell_base + i].slot_off;
+    const int nIni = G.n_ini;
+    if (w0) {
+        for (int i = lane; i < ncell; i += 64) {
+            S.cellstart[i] = cc[i];
+            S.cslot[i] = cells[G.cell_base + i].slot_off;
+        }
+        wave_lds_fence();
+        const int M0 = wave_scan_lds(S.cellstart, ncell);
+        if (lane == 0) { S.cellstart[ncell] = M0; ctl[55] = M0; }
+        for (int i = lane; i < nIni * 4; i += 64) S.ccount[i] = 0;
     }
     __syncthreads();
     TR_PHASE(2, 50)
-    const int M = block_scan_array(S.cellstart, ncell, ctl);
-    if (tid == 0) S.cellstart[ncell] = M;
-    TR_PHASE(2, 51)
+    const int M = ctl[55];
     const bool keys_in_lds = M <= cfg.key_cap;
     uint32_t* keys = keys_in_lds ? keysL : kscratch + (int64_t)f * P->n_slots_total + G.slot_base;
     uint16_t* knode = keys_in_lds ? knodeL : nscratch + (int64_t)f * P->n_slots_total + G.slot_base;
     const uint32_t* cbase = cand + (int64_t)f * P->n_slots_total;
-    __syncthreads();
-    // flattened gather: key k belongs to the cell c with cellstart[c] <= k < cellstart[c+1]
-    // (binary search in LDS), so every global load of the level is independent
-    for (int k = tid; k < M; k += nt) {
-        int lo = 0, hi = ncell - 1;
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (S.cellstart[mid] <= k) lo = mid; else hi = mid - 1;
-        }
-        keys[k] = cbase[S.cslot[lo] + (k - S.cellstart[lo])];
-    }
-    TR_PHASE(2, 52)
-    // ---- 2. roots (nIni <= 64 enforced by the host) ----
-    const int nIni = G.n_ini;
-    for (int i = tid; i < nIni * 4; i += nt) S.ccount[i] = 0;
-    __syncthreads();
     const float hX = G.hX;
-    for (int k0 = 0; k0 < M; k0 += nt) {
-        const int k = k0 + tid;
-        uint32_t tgt = 0xFFFFFFFFu;
-        if (k < M) {
-            const uint32_t key = keys[k];
-            int r = (int)((float)cand_x(key) / hX);
-            r = r < 0 ? 0 : (r >= nIni ? nIni - 1 : r);
-            tgt = (uint32_t)r;
-            knode[k] = (uint16_t)r;
+    // flattened gather + root classification: key k belongs to the cell c with cellstart[c] <= k <
+    // cellstart[c+1] (binary search in LDS); up to 4 keys per thread with their loads in flight
+    // together
+    for (int k0 = 0; k0 < M; k0 += 4 * nt) {
+        uint32_t kv[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = min(k0 + tid + u * nt, M - 1);
+            int lo = 0, hi = ncell - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (S.cellstart[mid] <= k) lo = mid; else hi = mid - 1;
+            }
+            kv[u] = cbase[S.cslot[lo] + (k - S.cellstart[lo])];
         }
-        wave_aggregate_count(tgt, S.ccount);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = k0 + tid + u * nt;
+            uint32_t tgt = 0xFFFFFFFFu;
+            if (k < M) {
+                keys[k] = kv[u];
+                int r = (int)((float)cand_x(kv[u]) / hX);
+                r = r < 0 ? 0 : (r >= nIni ? nIni - 1 : r);
+                tgt = (uint32_t)r;
+                knode[k] = (uint16_t)r;
+            }
+            wave_aggregate_count(tgt, S.ccount);
+        }
     }
     __syncthreads();
     TR_PHASE(2, 53)
-    if (tid == 0) {
-        int n = 0;
-        const int H = G.max_by - G.min_by;
-        for (int r = 0; r < nIni; r++) {
-            const uint64_t rr = mk_rect((int)(hX * (float)r), 0, (int)(hX * (float)(r + 1)), H);
-            S.rectB[r] = rr;   // OLD buffer = roots (remap source)
-            if (S.ccount[r] > 0) {
-                S.rectA[n] = rr; S.cntA[n] = S.ccount[r]; S.serA[n] = r;
-                S.map4[r * 4 + 0] = S.map4[r * 4 + 1] = S.map4[r * 4 + 2] = S.map4[r * 4 + 3] = (uint16_t)n;
-                n++;
+    // ---- 2. roots (nIni <= 64 enforced by the host) ----
+    if (w0) {
+        if (lane == 0) {
+            int n = 0;
+            const int H = G.max_by - G.min_by;
+            for (int r = 0; r < nIni; r++) {
+                const uint64_t rr = mk_rect((int)(hX * (float)r), 0, (int)(hX * (float)(r + 1)), H);
+                S.rectB[r] = rr;   // OLD buffer = roots (remap source)
+                if (S.ccount[r] > 0) {
+                    S.rectA[n] = rr; S.cntA[n] = S.ccount[r]; S.serA[n] = r;
+                    S.map4[r * 4 + 0] = S.map4[r * 4 + 1] = S.map4[r * 4 + 2] = S.map4[r * 4 + 3] = (uint16_t)n;
+                    n++;
+                }
             }
+            ctl[56] = n;          // list size
+            ctl[57] = nIni;       // next serial
+            ctl[58] = 0;          // mode: 0 main, 1 final
+            ctl[59] = 0;          // finished
         }
-        ctl[56] = n;          // list size
-        ctl[57] = nIni;       // next serial
-        ctl[58] = 0;          // mode: 0 main, 1 final
-        ctl[59] = 0;          // finished
+        wave_lds_fence();
+        const int n = ctl[56];
+        for (int i = lane; i < n * 4; i += 64) S.ccount[i] = 0;
     }
     __syncthreads();
     TR_PHASE(2, 0)
@@ -620,15 +660,14 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
     uint32_t *cntO = S.cntB, *serO = S.serB;
     const int N = G.n_feat;
     for (int iter = 0;; iter++) {
+        // read before the sweep barrier: wave 0 rewrites the control words in its node pass
         const int n = ctl[56];
+        const int mode = ctl[58];
         if (iter > 64 || n > NC) {   // runaway guard: never expected
             if (tid == 0) atomicOr(err, 1);
             break;
         }
         // ---- sweep: remap keys through map4 (OLD rect split), classify into CUR children ----
-        for (int i = tid; i < n * 4; i += nt) S.ccount[i] = 0;
-        __syncthreads();
-        if (iter == 1) { TR_PHASE(2, 40) }
         for (int k0 = 0; k0 < M; k0 += nt) {
             const int k = k0 + tid;
             uint32_t tgt = 0xFFFFFFFFu;
@@ -644,120 +683,139 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
         }
         __syncthreads();
         if (iter == 1) { TR_PHASE(2, 41) }
-        const int mode = ctl[58];
-        const int serial0 = ctl[57];
-        int newSize;
         if (mode == 0) {
-            // ---- MAIN pass: divide every node with > 1 key ----
-            for (int p = tid; p < n; p += nt) {
-                int c = 0, e = 0;
-                const bool div = cntC[p] > 1;
-                if (div)
-                    for (int q = 0; q < 4; q++) { c += S.ccount[p * 4 + q] > 0; e += S.ccount[p * 4 + q] > 1; }
-                S.tA[p] = c; S.tB[p] = div ? 0 : 1; S.tC[p] = e;
+            // ---- MAIN pass (wave 0): divide every node with > 1 key ----
+            if (w0) {
+                const int serial0 = ctl[57];
+                const int per = (n + 63) >> 6;
+                const int b = min(lane * per, n), e = min(b + per, n);
+                int sc = 0, su = 0, se = 0;
+                for (int p = b; p < e; p++) {
+                    if (cntC[p] > 1) { sc += nonempty4(S.ccount + 4 * p); se += multi4(S.ccount + 4 * p); }
+                    else su += 1;
+                }
+                const int ic = wave_incl_scan(sc), iu = wave_incl_scan(su), ie = wave_incl_scan(se);
+                const int T = __builtin_amdgcn_readlane(ic, 63), U = __builtin_amdgcn_readlane(iu, 63);
+                const int nToExpand = __builtin_amdgcn_readlane(ie, 63);
+                int cb = ic - sc, ub = iu - su;
+                for (int p = b; p < e; p++) {
+                    if (cntC[p] > 1) {
+                        const int c = nonempty4(S.ccount + 4 * p);
+                        const int base = T - cb - c;          // pushed to the front: later parents first
+                        int r = 0;
+                        for (int q = 0; q < 4; q++) {
+                            const uint32_t cq = S.ccount[p * 4 + q];
+                            if (cq == 0) continue;
+                            const int pos = base + (c - 1 - r);   // n4..n1 order inside the block
+                            rectO[pos] = child_rect(rectC[p], q);
+                            cntO[pos] = cq; serO[pos] = serial0 + cb + r;
+                            S.map4[p * 4 + q] = (uint16_t)pos;
+                            r++;
+                        }
+                        cb += c;
+                    } else {
+                        const int pos = T + ub;
+                        rectO[pos] = rectC[p]; cntO[pos] = cntC[p]; serO[pos] = serC[p];
+                        S.map4[p * 4 + 0] = S.map4[p * 4 + 1] = S.map4[p * 4 + 2] = S.map4[p * 4 + 3] = (uint16_t)pos;
+                        ub++;
+                    }
+                }
+                const int newSize = T + U;
+                wave_lds_fence();
+                for (int i = lane; i < min(newSize, NC) * 4; i += 64) S.ccount[i] = 0;
+                if (lane == 0) {
+                    ctl[57] = serial0 + T;
+                    ctl[56] = newSize;
+                    if (newSize >= N || newSize == n) ctl[59] = 1;
+                    else if (newSize + nToExpand * 3 > N) ctl[58] = 1;
+                }
+            }
+        } else {
+            // ---- FINAL phase: divide largest (size, serial) first until >= N ----
+            if (w0) {
+                const int per = (n + 63) >> 6;
+                const int b = min(lane * per, n), e = min(b + per, n);
+                int s = 0;
+                for (int p = b; p < e; p++) s += cntC[p] > 1;
+                const int inc = wave_incl_scan(s);
+                int pos = inc - s;
+                for (int p = b; p < e; p++)
+                    if (cntC[p] > 1)
+                        S.skey2[pos++] = ((uint64_t)cntC[p] << 40) | ((uint64_t)serC[p] << 16) | (uint64_t)p;
+                if (lane == 0) ctl[60] = __builtin_amdgcn_readlane(inc, 63);
             }
             __syncthreads();
-            if (iter == 1) { TR_PHASE(2, 42) }
-            int tot3[3];
-            block_scan_array3(S.tA, S.tB, S.tC, n, ctl, tot3);
-            if (iter == 1) { TR_PHASE(2, 43) }
-            const int T = tot3[0], U = tot3[1], nToExpand = tot3[2];
-            newSize = T + U;
-            for (int p = tid; p < n; p += nt) {
-                if (cntC[p] > 1) {
-                    int c = 0;
-                    for (int q = 0; q < 4; q++) c += S.ccount[p * 4 + q] > 0;
-                    const int cb = S.tA[p];                // children created before this parent
-                    const int base = T - cb - c;          // pushed to the front: later parents first
+            const int K = ctl[60];
+            block_rank_sort_desc(S.skey2, S.skey, K);   // keys unique: (size, serial) order; ends in a barrier
+            if (w0) {
+                const int serial0 = ctl[57];
+                const int per = (K + 63) >> 6;
+                const int b = min(lane * per, K), e = min(b + per, K);
+                // jstar: the first division (sorted order) after which the list holds >= N nodes
+                int g = 0;
+                for (int j = b; j < e; j++) g += nonempty4(S.ccount + 4 * (int)(S.skey[j] & 0xFFFF)) - 1;
+                const int ig = wave_incl_scan(g);
+                int run = n + ig - g, cand_j = K - 1;
+                for (int j = b; j < e; j++) {
+                    run += nonempty4(S.ccount + 4 * (int)(S.skey[j] & 0xFFFF)) - 1;
+                    if (run >= N) { cand_j = j; break; }
+                }
+                int jstar = cand_j;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) jstar = min(jstar, __shfl_xor(jstar, o, 64));
+                // children of the divisions 0..jstar, pushed to the front in division order
+                int sc = 0;
+                for (int j = b; j < min(e, jstar + 1); j++) sc += nonempty4(S.ccount + 4 * (int)(S.skey[j] & 0xFFFF));
+                const int ic = wave_incl_scan(sc);
+                const int Ctot = __builtin_amdgcn_readlane(ic, 63);
+                for (int p = lane; p < n; p += 64) S.tD[p] = 1;
+                wave_lds_fence();
+                int cb = ic - sc;
+                for (int j = b; j < min(e, jstar + 1); j++) {
+                    const int p = (int)(S.skey[j] & 0xFFFF);
+                    const int c = nonempty4(S.ccount + 4 * p);
+                    const int base = Ctot - cb - c;
                     int r = 0;
                     for (int q = 0; q < 4; q++) {
                         const uint32_t cq = S.ccount[p * 4 + q];
                         if (cq == 0) continue;
-                        const int pos = base + (c - 1 - r);   // n4..n1 order inside the block
-                        rectO[pos] = child_rect(rectC[p], q);
-                        cntO[pos] = cq; serO[pos] = serial0 + cb + r;
-                        S.map4[p * 4 + q] = (uint16_t)pos;
+                        const int ps = base + (c - 1 - r);
+                        rectO[ps] = child_rect(rectC[p], q);
+                        cntO[ps] = cq; serO[ps] = serial0 + cb + r;
+                        S.map4[p * 4 + q] = (uint16_t)ps;
                         r++;
                     }
-                } else {
-                    const int pos = T + S.tB[p];
-                    rectO[pos] = rectC[p]; cntO[pos] = cntC[p]; serO[pos] = serC[p];
-                    S.map4[p * 4 + 0] = S.map4[p * 4 + 1] = S.map4[p * 4 + 2] = S.map4[p * 4 + 3] = (uint16_t)pos;
+                    S.tD[p] = 0;
+                    cb += c;
                 }
-            }
-            if (tid == 0) {
-                ctl[57] = serial0 + T;
-                if (newSize >= N || newSize == n) ctl[59] = 1;
-                else if (newSize + nToExpand * 3 > N) ctl[58] = 1;
-            }
-        } else {
-            // ---- FINAL phase: divide largest (size, serial) first until >= N ----
-            for (int p = tid; p < n; p += nt) S.tA[p] = cntC[p] > 1 ? 1 : 0;
-            __syncthreads();
-            const int K = block_scan_array(S.tA, n, ctl);
-            for (int p = tid; p < n; p += nt)
-                if (cntC[p] > 1)
-                    S.skey2[S.tA[p]] = ((uint64_t)cntC[p] << 40) | ((uint64_t)serC[p] << 16) | (uint64_t)p;
-            __syncthreads();
-            block_rank_sort_desc(S.skey2, S.skey, K);   // keys unique: (size, serial) order
-            if (tid == 0) ctl[60] = K - 1;   // jstar: last divided index in sorted order
-            for (int j = tid; j < K; j += nt) {
-                const int p = (int)(S.skey[j] & 0xFFFF);
-                int c = 0;
-                for (int q = 0; q < 4; q++) c += S.ccount[p * 4 + q] > 0;
-                S.tB[j] = c - 1;   // list growth when dividing it
-                S.tC[j] = c;
-            }
-            for (int p = tid; p < n; p += nt) S.tD[p] = 1;
-            __syncthreads();
-            block_scan_array(S.tB, K, ctl);
-            for (int j = tid; j < K; j += nt)
-                if (n + S.tB[j] + (S.tC[j] - 1) >= N) atomicMin(&ctl[60], j);
-            __syncthreads();
-            const int jstar = ctl[60];
-            for (int j = tid; j < K; j += nt) {
-                if (j > jstar) S.tC[j] = 0;
-                else S.tD[(int)(S.skey[j] & 0xFFFF)] = 0;
-            }
-            __syncthreads();
-            for (int j = tid; j < K; j += nt) S.tB[j] = S.tC[j];
-            for (int p = tid; p < n; p += nt) S.tA[p] = S.tD[p];
-            __syncthreads();
-            const int Ctot = block_scan_array(S.tB, K, ctl);   // children created before, in division order
-            block_scan_array(S.tA, n, ctl);                    // stayers before
-            newSize = Ctot + (n - (jstar + 1));
-            for (int j = tid; j <= jstar; j += nt) {
-                const int p = (int)(S.skey[j] & 0xFFFF);
-                const int c = S.tC[j];
-                const int cb = S.tB[j];
-                const int base = Ctot - cb - c;
-                int r = 0;
-                for (int q = 0; q < 4; q++) {
-                    const uint32_t cq = S.ccount[p * 4 + q];
-                    if (cq == 0) continue;
-                    const int pos = base + (c - 1 - r);
-                    rectO[pos] = child_rect(rectC[p], q);
-                    cntO[pos] = cq; serO[pos] = serial0 + cb + r;
-                    S.map4[p * 4 + q] = (uint16_t)pos;
-                    r++;
+                wave_lds_fence();
+                // the other nodes keep their order behind the children
+                const int pn = (n + 63) >> 6;
+                const int bn = min(lane * pn, n), en = min(bn + pn, n);
+                int st = 0;
+                for (int p = bn; p < en; p++) st += S.tD[p];
+                const int is = wave_incl_scan(st);
+                int sb = is - st;
+                for (int p = bn; p < en; p++) {
+                    if (S.tD[p]) {
+                        const int ps = Ctot + sb;
+                        rectO[ps] = rectC[p]; cntO[ps] = cntC[p]; serO[ps] = serC[p];
+                        S.map4[p * 4 + 0] = S.map4[p * 4 + 1] = S.map4[p * 4 + 2] = S.map4[p * 4 + 3] = (uint16_t)ps;
+                        sb++;
+                    }
                 }
-            }
-            for (int p = tid; p < n; p += nt) {
-                if (S.tD[p]) {
-                    const int pos = Ctot + S.tA[p];
-                    rectO[pos] = rectC[p]; cntO[pos] = cntC[p]; serO[pos] = serC[p];
-                    S.map4[p * 4 + 0] = S.map4[p * 4 + 1] = S.map4[p * 4 + 2] = S.map4[p * 4 + 3] = (uint16_t)pos;
+                const int newSize = Ctot + (n - (jstar + 1));
+                wave_lds_fence();
+                for (int i = lane; i < min(newSize, NC) * 4; i += 64) S.ccount[i] = 0;
+                if (lane == 0) {
+                    ctl[57] = serial0 + Ctot;
+                    ctl[56] = newSize;
+                    if (newSize >= N || newSize == n) ctl[59] = 1;
                 }
-            }
-            if (tid == 0) {
-                ctl[57] = serial0 + Ctot;
-                if (newSize >= N || newSize == n) ctl[59] = 1;
             }
         }
         __syncthreads();
         if (iter == 1) { TR_PHASE(2, 44) }
-        if (tid == 0) ctl[56] = newSize;
-        __syncthreads();
         // swap: NEXT (written into the O buffers) becomes CUR, CUR becomes OLD
         { uint64_t* t = rectC; rectC = rectO; rectO = t; }
         { uint32_t* t = cntC; cntC = cntO; cntO = t; }
@@ -777,36 +835,38 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
         atomicMax(&S.cbest[nd], pack_best(cand_s(key), k));
     }
     __syncthreads();
-    // ---- output in list order: retained key per node, lapping flag and rank ----
-    LevelKp* out = lvl_kp + (int64_t)f * P->kp_slots_total + G.kp_base;
-    const int ncap = min(n, G.kp_cap);
-    for (int p = tid; p < ncap; p += nt) {
-        const int k = (int)(0xFFFFFFu - (S.cbest[p] & 0xFFFFFFu));
-        const uint32_t key = keys[k];
-        const int x = cand_x(key) + G.min_bx, y = cand_y(key) + G.min_by;
-        const float xs = (l == 0) ? (float)x : (float)x * G.scale;
-        const int lap = (xs >= (float)cfg.lap0 && xs <= (float)cfg.lap1) ? 1 : 0;
-        S.tA[p] = lap; S.tB[p] = 1 - lap;
-        S.tC[p] = (x & 0xFFFF) | (y << 16);
-        S.skey[p] = (uint64_t)cand_s(key);
-    }
-    __syncthreads();
-    const int nlap = block_scan_array(S.tA, ncap, ctl);
-    block_scan_array(S.tB, ncap, ctl);
-    for (int p = tid; p < ncap; p += nt) {
-        const int xy = S.tC[p];
-        const int x = xy & 0xFFFF, y = xy >> 16;
-        const int lapflag = (p + 1 < ncap ? S.tA[p + 1] : nlap) - S.tA[p];
-        const int rank = lapflag ? S.tA[p] : S.tB[p];
-        LevelKp r;
-        r.x = (int16_t)x; r.y = (int16_t)y;
-        r.srl = (uint32_t)S.skey[p] | ((uint32_t)lapflag << 8) | ((uint32_t)rank << 9);
-        out[p] = r;
-    }
-    if (tid == 0) {
-        lvl_cnt[f * P->n_levels + l] = ncap;
-        lvl_nlap[f * P->n_levels + l] = nlap;
-        if (n > G.kp_cap) atomicOr(err, 2);
+    // ---- output in list order (wave 0): retained key per node, lapping flag and rank ----
+    if (w0) {
+        LevelKp* out = lvl_kp + (int64_t)f * P->kp_slots_total + G.kp_base;
+        const int ncap = min(n, G.kp_cap);
+        for (int p = lane; p < ncap; p += 64) {
+            const int k = (int)(0xFFFFFFu - (S.cbest[p] & 0xFFFFFFu));
+            const uint32_t key = keys[k];
+            const int x = cand_x(key) + G.min_bx, y = cand_y(key) + G.min_by;
+            const float xs = (l == 0) ? (float)x : (float)x * G.scale;
+            const int lap = (xs >= (float)cfg.lap0 && xs <= (float)cfg.lap1) ? 1 : 0;
+            S.tA[p] = lap; S.tB[p] = 1 - lap;
+            S.tC[p] = (x & 0xFFFF) | (y << 16);
+            S.skey[p] = (uint64_t)cand_s(key);
+        }
+        wave_lds_fence();
+        const int nlap = wave_scan_lds(S.tA, ncap);
+        wave_scan_lds(S.tB, ncap);
+        for (int p = lane; p < ncap; p += 64) {
+            const int xy = S.tC[p];
+            const int x = xy & 0xFFFF, y = xy >> 16;
+            const int lapflag = (p + 1 < ncap ? S.tA[p + 1] : nlap) - S.tA[p];
+            const int rank = lapflag ? S.tA[p] : S.tB[p];
+            LevelKp r;
+            r.x = (int16_t)x; r.y = (int16_t)y;
+            r.srl = (uint32_t)S.skey[p] | ((uint32_t)lapflag << 8) | ((uint32_t)rank << 9);
+            out[p] = r;
+        }
+        if (lane == 0) {
+            lvl_cnt[f * P->n_levels + l] = ncap;
+            lvl_nlap[f * P->n_levels + l] = nlap;
+            if (n > G.kp_cap) atomicOr(err, 2);
+        }
     }
     TR_PHASE(2, 63)
     TR_END(2)

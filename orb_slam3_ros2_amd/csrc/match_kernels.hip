@@ -2,12 +2,15 @@
 // TH_LOW acceptance, then the HISTO_LENGTH=30 rotation-consistency filter
 // (ComputeThreeMaxima). Order-free over the whole train set.
 //
-//   k_match_top2    grid (64-query blocks, 256-descriptor train chunks, pairs): lane = query
+//   k_match_top2    grid (64-query blocks, 256- (64- for one pair) descriptor train chunks, pairs): lane = query
 //                   (descriptor in VGPRs), the chunk is staged in LDS and read as broadcasts;
 //                   per-lane best/second/index in train order (v_xor + v_bcnt), the 4 waves'
 //                   quarter-chunks merged in order, one partial per (pair, chunk, query).
-//   k_match_finish  one workgroup per pair: merge the partials in chunk order, TH_LOW + ratio,
-//                   30-bin rotation histogram, three maxima, filter, match count.
+//                   (A 64-bit atomicCAS merge into one record per query was tried: the
+//                   cross-XCD atomics cost more than the finish saves.)
+//   k_match_finish  one workgroup per pair: merge the partials (lexicographic (best, index),
+//                   multiset second), TH_LOW + ratio, 30-bin rotation histogram, three maxima
+//                   (one wave), filter, match count.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -33,7 +36,8 @@ struct MatchView {
     int64_t out_stride;        // entries between pairs in the outputs
 };
 
-constexpr int kTC = 256;   // train descriptors per workgroup chunk (64 per wave)
+constexpr int kTC = 256;     // train descriptors per workgroup chunk (64 per wave): batches
+constexpr int kTCSmall = 64; // 16 per wave: one pair (C2), where 256-chunks leave the chip idle
 
 __device__ __forceinline__ void top2_merge(int& b, int& i, int& s, int b2, int i2, int s2) {
     const int nb = (b2 < b || (b2 == b && i2 < i)) ? b2 : b;
@@ -42,22 +46,23 @@ __device__ __forceinline__ void top2_merge(int& b, int& i, int& s, int b2, int i
     b = nb; i = ni; s = ns;
 }
 
-// Partial top-2 of 64 queries (one per lane, descriptor in VGPRs) against one 256-descriptor
-// train chunk broadcast from LDS; wave w scans train [64w, 64w+64) of the chunk in index order
-// (strict <: the first index wins), the 4 waves merge in index order. part[(pair, chunk, q)] =
+// Partial top-2 of 64 queries (one per lane, descriptor in VGPRs) against one TC-descriptor
+// train chunk broadcast from LDS; wave w scans its quarter of the chunk in index order (strict <:
+// the first index wins), the 4 waves merge in index order. part[(pair, chunk, q)] =
 // {best | second << 16, index}.
+template <int TC>
 __global__ __launch_bounds__(256) void k_match_top2(MatchView v, uint2* __restrict__ part, int nchunk_cap,
                                                      int part_stride) {
-    __shared__ __attribute__((aligned(16))) uint4 tile[kTC * 2];
+    __shared__ __attribute__((aligned(16))) uint4 tile[TC * 2];
     __shared__ int mb[3][64], mi[3][64], ms[3][64];
     TR_BEGIN()
     const int p = blockIdx.z;
     const int nq = v.nq_arr ? v.nq_arr[p] : v.nq;
     const int nt = v.nt_arr ? v.nt_arr[p] : v.nt;
-    const int q0 = blockIdx.x * 64, t0 = blockIdx.y * kTC;
+    const int q0 = blockIdx.x * 64, t0 = blockIdx.y * TC;
     if (q0 >= nq || t0 >= nt) return;   // workgroup-uniform
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-    const int tn = min(kTC, nt - t0);
+    const int tn = min(TC, nt - t0);
     const uint8_t* td = v.td + (int64_t)p * v.pair_desc_stride;
     const uint4* src = (const uint4*)(td + (int64_t)t0 * 32);
     for (int i = tid; i < tn * 2; i += 256) tile[i] = src[i];
@@ -70,7 +75,7 @@ __global__ __launch_bounds__(256) void k_match_top2(MatchView v, uint2* __restri
     }
     __syncthreads();
     int b = 256, bi = 0x7fffffff, s = 256;
-    const int w0 = wid * 64, w1 = min(tn, w0 + 64);
+    const int w0 = wid * (TC / 4), w1 = min(tn, w0 + TC / 4);
     for (int t = w0; t < w1; t++) {
         const uint4 x = tile[2 * t], y = tile[2 * t + 1];
         const int d = __popc(x.x ^ qa.x) + __popc(x.y ^ qa.y) + __popc(x.z ^ qa.z) + __popc(x.w ^ qa.w) +
@@ -89,12 +94,46 @@ __global__ __launch_bounds__(256) void k_match_top2(MatchView v, uint2* __restri
     TR_END(4)
 }
 
-// One workgroup per pair: merge the chunk partials in train order, apply best <= TH_LOW and
-// best < ratio * second, then the HISTO_LENGTH=30 rotation filter (ComputeThreeMaxima). The
-// per-query match and bin stay in LDS between the two passes (queries beyond kFinQ re-read).
+// ComputeThreeMaxima over a 30-bin LDS histogram by one wave. The reference inserts bins in
+// index order with strict '>' into a top-3 that starts at 0, so its order is value descending,
+// ties by lower index, positive values only: three wave max-reductions of (value << 8 | 255 - i).
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true));    // quad_perm [1,0,3,2]
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true));    // quad_perm [2,3,0,1]
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true));   // row_half_mirror
+    v = max(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true));   // row_mirror
+    const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = max(a[0], a[1]);
+    const auto b = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return max(b[0], b[1]);
+}
+__device__ __forceinline__ void three_maxima_wave(const int* hist, int* keep) {
+    const int lane = threadIdx.x & 63;
+    const int h = lane < 30 ? hist[lane] : 0;
+    uint32_t key = h > 0 ? ((uint32_t)h << 8) | (uint32_t)(255 - lane) : 0u;
+    uint32_t k[3];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        k[j] = wave_max_u32(key);
+        if (key == k[j]) key = 0u;
+    }
+    const int max1 = (int)(k[0] >> 8), max2 = (int)(k[1] >> 8), max3 = (int)(k[2] >> 8);
+    int ind1 = k[0] ? 255 - (int)(k[0] & 0xFF) : -1;
+    int ind2 = k[1] ? 255 - (int)(k[1] & 0xFF) : -1;
+    int ind3 = k[2] ? 255 - (int)(k[2] & 0xFF) : -1;
+    if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
+    else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
+    if (lane == 0) { keep[0] = ind1; keep[1] = ind2; keep[2] = ind3; }
+}
+
+// One workgroup per pair: merge the chunk partials, apply best <= TH_LOW and best < ratio *
+// second, then the HISTO_LENGTH=30 rotation filter (ComputeThreeMaxima). The per-query match and
+// bin stay in LDS between the two passes (queries beyond kFinQ re-read). The train angles are
+// staged in LDS while the first query's partials and angle are already in flight: one global
+// round trip before the merge in the common case (nq <= 1024, <= 16 chunks).
 constexpr int kFinQ = 6144;
 __global__ __launch_bounds__(1024) void k_match_finish(MatchView v, const uint2* __restrict__ part, int nchunk_cap,
-                                                        int part_stride, int th_low, float ratio,
+                                                        int part_stride, int tc, int th_low, float ratio,
                                                         int check_orientation, int32_t* __restrict__ match,
                                                         int32_t* __restrict__ best_out, int32_t* __restrict__ second_out,
                                                         int32_t* __restrict__ nmatch) {
@@ -103,30 +142,50 @@ __global__ __launch_bounds__(1024) void k_match_finish(MatchView v, const uint2*
     __shared__ int cnt;
     __shared__ int mq[kFinQ];
     __shared__ int8_t bq[kFinQ];
+    __shared__ float tang[kFinQ];
     TR_BEGIN()
-    const int p = blockIdx.x, nt_ = blockDim.x;
+    const int p = blockIdx.x, nt_ = blockDim.x, tid = threadIdx.x;
     const int nq = v.nq_arr ? v.nq_arr[p] : v.nq;
     const int nt = v.nt_arr ? v.nt_arr[p] : v.nt;
-    const int nch = (nt + kTC - 1) / kTC;
+    const int nch = (nt + tc - 1) / tc;
     const float* qa = v.qa + (int64_t)p * v.pair_angle_stride;
     const float* ta = v.ta + (int64_t)p * v.pair_angle_stride;
     int32_t* m = match + (int64_t)p * v.out_stride;
     const float factor = 1.0f / 30;
-    if (threadIdx.x < 32) hist[threadIdx.x] = 0;
-    if (threadIdx.x == 0) cnt = 0;
+    const bool tang_lds = nt <= kFinQ;
+    uint2 u0[16];
+    float qa0 = 0.f;
+    if (tid < nq) {
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+            u0[j] = part[((int64_t)p * nchunk_cap + min(j, max(nch - 1, 0))) * part_stride + tid];
+        qa0 = qa[(int64_t)tid * v.angle_stride];
+    }
+    if (tang_lds)
+        for (int t = tid; t < nt; t += nt_) tang[t] = ta[(int64_t)t * v.angle_stride];
+    if (tid < 32) hist[tid] = 0;
+    if (tid == 0) cnt = 0;
     __syncthreads();
-    auto bin_of = [&](int q, int t) {
-        float rot = qa[(int64_t)q * v.angle_stride] - ta[(int64_t)t * v.angle_stride];
-        if (rot < 0.0) rot += 360.0f;
-        int bin = (int)roundf(rot * factor);
-        if (bin == 30) bin = 0;
-        return bin;
-    };
-    for (int q = threadIdx.x; q < nq; q += nt_) {
+    auto tangle = [&](int t) { return tang_lds ? tang[t] : ta[(int64_t)t * v.angle_stride]; };
+    for (int q = tid; q < nq; q += nt_) {
         int b = 256, bi = 0x7fffffff, s = 256;
-        for (int c = 0; c < nch; c++) {
-            const uint2 u = part[((int64_t)p * nchunk_cap + c) * part_stride + q];
-            top2_merge(b, bi, s, (int)(u.x & 0xFFFF), (int)u.y, (int)(u.x >> 16));
+        float aq;
+        if (q == tid) {
+#pragma unroll
+            for (int j = 0; j < 16; j++)
+                if (j < nch) top2_merge(b, bi, s, (int)(u0[j].x & 0xFFFF), (int)u0[j].y, (int)(u0[j].x >> 16));
+            aq = qa0;
+        } else {
+            aq = qa[(int64_t)q * v.angle_stride];
+        }
+        for (int c0 = (q == tid ? 16 : 0); c0 < nch; c0 += 16) {
+            uint2 u[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++)
+                u[j] = part[((int64_t)p * nchunk_cap + min(c0 + j, nch - 1)) * part_stride + q];
+#pragma unroll
+            for (int j = 0; j < 16; j++)
+                if (c0 + j < nch) top2_merge(b, bi, s, (int)(u[j].x & 0xFFFF), (int)u[j].y, (int)(u[j].x >> 16));
         }
         const bool ok = b < 256 && b <= th_low && (float)b < ratio * (float)s;
         const int mt = ok ? bi : -1;
@@ -135,46 +194,61 @@ __global__ __launch_bounds__(1024) void k_match_finish(MatchView v, const uint2*
         second_out[o] = s;
         int bin = -1;
         if (ok && check_orientation) {
-            bin = bin_of(q, bi);
-            atomicAdd(&hist[bin], 1);
+            float rot = aq - tangle(bi);
+            if (rot < 0.0) rot += 360.0f;
+            bin = (int)roundf(rot * factor);
+            if (bin == 30) bin = 0;
+        }
+        // one LDS atomic per distinct bin of the wave (matches crowd into 1-3 bins, and
+        // same-address atomics would serialise lane by lane)
+        {
+            uint64_t todo = __ballot(bin >= 0);
+            while (todo) {
+                const int b0 = __builtin_amdgcn_readlane(bin, __ffsll((unsigned long long)todo) - 1);
+                const uint64_t same = __ballot(bin == b0) & todo;
+                if ((tid & 63) == __ffsll((unsigned long long)same) - 1) atomicAdd(&hist[b0], __popcll(same));
+                todo &= ~same;
+            }
         }
         if (q < kFinQ) { mq[q] = mt; bq[q] = (int8_t)bin; }
         else m[q] = mt;
     }
+    TR_PHASE(5, 0)
     __syncthreads();
+    TR_PHASE(5, 1)
     if (check_orientation) {
-        if (threadIdx.x == 0) {
-            int max1 = 0, max2 = 0, max3 = 0, ind1 = -1, ind2 = -1, ind3 = -1;
-            for (int i = 0; i < 30; i++) {
-                const int s = hist[i];
-                if (s > max1) { max3 = max2; max2 = max1; max1 = s; ind3 = ind2; ind2 = ind1; ind1 = i; }
-                else if (s > max2) { max3 = max2; max2 = s; ind3 = ind2; ind2 = i; }
-                else if (s > max3) { max3 = s; ind3 = i; }
-            }
-            if (max2 < 0.1f * (float)max1) { ind2 = -1; ind3 = -1; }
-            else if (max3 < 0.1f * (float)max1) { ind3 = -1; }
-            keep[0] = ind1; keep[1] = ind2; keep[2] = ind3;
-        }
+        if (tid < 64) three_maxima_wave(hist, keep);
         __syncthreads();
     }
+    TR_PHASE(5, 2)
     int c = 0;
-    for (int q = threadIdx.x; q < nq; q += nt_) {
+    for (int q = tid; q < nq; q += nt_) {
         int t, bin;
         if (q < kFinQ) { t = mq[q]; bin = bq[q]; }
-        else { t = m[q]; bin = (t >= 0 && check_orientation) ? bin_of(q, t) : -1; }
+        else {
+            t = m[q];
+            bin = -1;
+            if (t >= 0 && check_orientation) {
+                float rot = qa[(int64_t)q * v.angle_stride] - tangle(t);
+                if (rot < 0.0) rot += 360.0f;
+                bin = (int)roundf(rot * factor);
+                if (bin == 30) bin = 0;
+            }
+        }
         if (t >= 0 && check_orientation && bin != keep[0] && bin != keep[1] && bin != keep[2]) t = -1;
         m[q] = t;
         c += t >= 0;
     }
     c = wave_sum_i32(c);
-    if ((threadIdx.x & 63) == 0) atomicAdd(&cnt, c);
+    if ((tid & 63) == 0) atomicAdd(&cnt, c);
     __syncthreads();
-    if (threadIdx.x == 0) nmatch[p] = cnt;
+    if (tid == 0) nmatch[p] = cnt;
+    TR_PHASE(5, 3)
     TR_END(5)
 }
 
 size_t match_part_entries(int npairs, int max_q, int max_t) {
-    const int nch = std::max(1, (max_t + kTC - 1) / kTC);
+    const int nch = std::max(1, (max_t + kTCSmall - 1) / kTCSmall);
     return (size_t)std::max(npairs, 1) * nch * std::max(max_q, 1);
 }
 
@@ -183,12 +257,20 @@ static void run_match(const MatchView& v, int npairs, int max_q, int max_t, int 
                       uint2* part, hipStream_t st, StageTimer* timer = nullptr) {
     if (npairs <= 0) return;
     const int qblocks = (max_q + 63) / 64;
-    const int nch = std::max(1, (max_t + kTC - 1) / kTC);
+    // 16 trains per wave while 64 per wave would leave most of the chip idle (one pair)
+    const bool small = (int64_t)npairs * qblocks * ((max_t + kTC - 1) / kTC) < 512;
+    const int tc = small ? kTCSmall : kTC;
+    const int nch = std::max(1, (max_t + tc - 1) / tc);
     if (timer) timer->begin(5, st);
-    if (qblocks > 0 && max_t > 0)
-        hipLaunchKernelGGL(k_match_top2, dim3(qblocks, nch, npairs), dim3(256), 0, st, v, part, nch, max_q);
+    if (qblocks > 0 && max_t > 0) {
+        if (small)
+            hipLaunchKernelGGL(k_match_top2<kTCSmall>, dim3(qblocks, nch, npairs), dim3(256), 0, st, v, part, nch,
+                               max_q);
+        else
+            hipLaunchKernelGGL(k_match_top2<kTC>, dim3(qblocks, nch, npairs), dim3(256), 0, st, v, part, nch, max_q);
+    }
     if (timer) { timer->end(5, st); timer->begin(6, st); }
-    hipLaunchKernelGGL(k_match_finish, dim3(npairs), dim3(1024), 0, st, v, part, nch, max_q, th_low, ratio,
+    hipLaunchKernelGGL(k_match_finish, dim3(npairs), dim3(1024), 0, st, v, part, nch, max_q, tc, th_low, ratio,
                        check_orientation, match, best, second, nmatch);
     if (timer) timer->end(6, st);
 }
