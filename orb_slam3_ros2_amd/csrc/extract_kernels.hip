@@ -222,6 +222,8 @@ __global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict
 // threshold t iff m > t (derivation in DESIGN.md), so one map serves both thresholds.
 // ---------------------------------------------------------------------------
 constexpr int kWinMax = 80;
+constexpr int kWinP = kWinMax;   // LDS row pitch of the FAST window and strength maps
+static_assert(kWinP % 4 == 0, "dword window rows");
 
 // m = max(A, B, 0) from the 16 differences d[k] = v - circle[k]
 __device__ __forceinline__ int fast_strength_d(const int* d) {
@@ -261,11 +263,14 @@ __global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict
                                                     const CellGeom* __restrict__ cells, FrameBufs fb,
                                                     uint32_t* __restrict__ cand, int* __restrict__ cand_cnt,
                                                     int* __restrict__ err) {
-    __shared__ uint8_t win[kWinMax * kWinMax];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kWinMax * kWinMax];
     __shared__ uint8_t mv[kWinMax * kWinMax];
-    constexpr int NW = NT / 64, NCH = 96 / NW;   // windows up to 6144 px
-    __shared__ uint64_t masks[NW][2][NCH];   // per wave, per threshold, per 64-px chunk
-    __shared__ int wcnt[2][NW];
+    constexpr int NW = NT / 64;
+    __shared__ unsigned long long bmask[2][96];   // NMS survivors per threshold, raster order (<= 6144 px)
+    __shared__ int woff[96];                      // output offset of each 64-px word
+    __shared__ int wsel, wtot;
+    __shared__ uint16_t clist[kWinMax * kWinMax];   // pair-test survivors (strength to compute)
+    __shared__ int ncand;
     TR_BEGIN()
     const CellGeom cg = cells[blockIdx.x];
     const int f = blockIdx.y;
@@ -280,33 +285,50 @@ __global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict
     const LevelGeom& G = P->lv[cg.level];
     ImgRef im = level_img(P, fb, f, cg.level);
     const uint8_t* base = im.p + (int64_t)cg.y0 * im.pitch + cg.x0;
-    // ---- window -> LDS: all loads of a thread issued back to back ----
+    // ---- window -> LDS: all loads of a thread issued back to back. When the rows are 4-byte
+    // aligned (pyramid levels always; the caller's frame when its pointer and stride are), the
+    // window moves as aligned dwords into LDS rows of kWinP bytes, shifted by sh = base & 3 ----
+    int sh = 0;
     {
-        const int tot = wc * hc;
-        const float inv_wc = 1.0f / (float)wc;
-        constexpr int NU = 2048 / NT;
-        if (tot <= NU * NT) {
-            // normal cells (window <= 2048 px): unconditional loads from clamped addresses,
-            // straight-line so all are in flight together, then predicated stores
-            uint8_t v[NU];
+        const bool dw = ((im.pitch & 3) == 0) && ((((uintptr_t)im.p) & 3) == 0);
+        if (dw) {
+            sh = (int)(((uintptr_t)base) & 3);
+            const uint32_t* b4 = (const uint32_t*)(base - sh);
+            const int nwd = (wc + sh + 3) >> 2;   // <= kWinP / 4
+            const int tot = nwd * hc, p4 = im.pitch >> 2;
+            const float inv_n = 1.0f / (float)nwd;
+            uint32_t* w4 = (uint32_t*)win;
+            constexpr int NU = (NT >= 512) ? 1 : 2;
+            if (tot <= NU * NT) {
+                uint32_t v[NU];
+                int li[NU];
 #pragma unroll
-            for (int u = 0; u < NU; u++) {
-                const int i = min(tid + NT * u, tot - 1);
-                const int yy = small_div(i, inv_wc), xx = i - yy * wc;
-                v[u] = base[(int64_t)yy * im.pitch + xx];
-            }
+                for (int u = 0; u < NU; u++) {
+                    const int i = min(tid + NT * u, tot - 1);
+                    const int yy = small_div(i, inv_n), xx = i - yy * nwd;
+                    v[u] = b4[(int64_t)yy * p4 + xx];
+                    li[u] = yy * (kWinP / 4) + xx;
+                }
 #pragma unroll
-            for (int u = 0; u < NU; u++) {
-                const int i = tid + NT * u;
-                if (i < tot) win[i] = v[u];
+                for (int u = 0; u < NU; u++)
+                    if (tid + NT * u < tot) w4[li[u]] = v[u];
+            } else {
+                for (int i = tid; i < tot; i += NT) {
+                    const int yy = small_div(i, inv_n), xx = i - yy * nwd;
+                    w4[yy * (kWinP / 4) + xx] = b4[(int64_t)yy * p4 + xx];
+                }
             }
         } else {
+            const int tot = wc * hc;
+            const float inv_wc = 1.0f / (float)wc;
             for (int i = tid; i < tot; i += NT) {
                 const int yy = small_div(i, inv_wc), xx = i - yy * wc;
-                win[i] = base[(int64_t)yy * im.pitch + xx];
+                win[yy * kWinP + xx] = base[(int64_t)yy * im.pitch + xx];
             }
         }
     }
+    if (tid == 0) ncand = 0;
+    if (tid < 192) bmask[tid / 96][tid % 96] = 0ull;
     __syncthreads();
     TR_PHASE(1, 0)
     const int t_ini = P->ini_th, t_min = P->min_th;
@@ -315,83 +337,104 @@ __global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict
     const float inv_dc = 1.0f / (float)dc;
     // ---- strength map: m if m > t_lo (a corner at some threshold in use), else 0; stored with
     // a zero border (row pitch W2 = dc + 2) so the NMS reads its 3x3 without bounds checks ----
-    const int W2 = dc + 2;
-    for (int i = tid; i < 2 * W2 + 2 * dr; i += NT) {
-        const int idx = i < W2 ? i : (i < 2 * W2 ? (dr + 1) * W2 + (i - W2) : (1 + (i - 2 * W2) / 2) * W2 + ((i & 1) ? W2 - 1 : 0));
+    // both LDS maps use the fixed pitch kWinP: every neighbour offset is an immediate
+    constexpr int W2 = kWinP;
+    const int Wz = dc + 2;   // zero border: rows 0 and dr + 1, columns 0 and dc + 1
+    for (int i = tid; i < 2 * Wz + 2 * dr; i += NT) {
+        const int idx = i < Wz ? i : (i < 2 * Wz ? (dr + 1) * W2 + (i - Wz) : (1 + (i - 2 * Wz) / 2) * W2 + ((i & 1) ? Wz - 1 : 0));
         mv[idx] = 0;
     }
-    for (int p = tid; p < np; p += NT) {
+    // every pixel runs the cheap opposite-pair test; the ~5-10% that pass are compacted into
+    // clist, and the strength (the expensive part) runs on the dense list, so no wave spends its
+    // issue slots on masked-off lanes
+    auto diffs = [&](int p, int* d) {
         const int py = small_div(p, inv_dc), px = p - py * dc;
-        const uint8_t* c = &win[(py + 3) * wc + px + 3];
-        const int o[16] = {3 * wc,      3 * wc + 1,  2 * wc + 2,  wc + 3,      3,      -wc + 3, -2 * wc + 2, -3 * wc + 1,
-                           -3 * wc,     -3 * wc - 1, -2 * wc - 2, -wc - 3,     -3,     wc - 3,  2 * wc - 2,  3 * wc - 1};
+        const uint8_t* c = &win[(py + 3) * kWinP + px + 3 + sh];
+        constexpr int P = kWinP;
+        constexpr int o[16] = {3 * P,      3 * P + 1,  2 * P + 2,  P + 3,      3,      -P + 3, -2 * P + 2, -3 * P + 1,
+                               -3 * P,     -3 * P - 1, -2 * P - 2, -P - 3,     -3,     P - 3,  2 * P - 2,  3 * P - 1};
         const int vv = c[0];
-        int d[16];
 #pragma unroll
         for (int k = 0; k < 16; k++) d[k] = vv - (int)c[o[k]];
-        int m = 0;
-        if (fast_pair_test(d, t_lo)) {
-            m = fast_strength_d(d);
-            if (m <= t_lo) m = 0;
+        return (py + 1) * W2 + px + 1;
+    };
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int p0 = 0; p0 < np; p0 += NT) {
+        const int p = p0 + tid;
+        bool pass = false;
+        if (p < np) {
+            int d[16];
+            const int mi = diffs(p, d);
+            pass = fast_pair_test(d, t_lo);
+            mv[mi] = 0;
         }
-        mv[(py + 1) * W2 + px + 1] = (uint8_t)m;
+        const uint64_t bal = __ballot(pass);
+        int base = 0;
+        if (lane == 0 && bal) base = atomicAdd(&ncand, __popcll(bal));
+        base = __shfl(base, 0, 64);
+        if (pass) clist[base + __popcll(bal & lt)] = (uint16_t)p;
+    }
+    __syncthreads();
+    const int nc = ncand;
+    for (int i = tid; i < nc; i += NT) {
+        int d[16];
+        const int mi = diffs(clist[i], d);
+        int m = fast_strength_d(d);
+        if (m <= t_lo) m = 0;
+        mv[mi] = (uint8_t)m;
     }
     __syncthreads();
     TR_PHASE(1, 1)
-    // ---- window-local strict 3x3 NMS at both thresholds; wave w owns pixels [w*chunk, ...) ----
-    const int chunk = ((np + NT - 1) / NT) * 64;   // multiple of 64 per wave
-    const int p0 = wid * chunk, p1 = min(np, p0 + chunk);
-    int c_ini = 0, c_min = 0;
-    for (int q0 = p0, ci = 0; q0 < p1; q0 += 64, ci++) {
-        const int p = q0 + lane;
-        bool k_ini = false, k_min = false;
-        {
-            const int pc = min(p, np - 1);   // branch-free: all 9 reads in flight together
-            const int py = small_div(pc, inv_dc), px = pc - py * dc;
-            const uint8_t* c = &mv[(py + 1) * W2 + px + 1];
-            const int m = c[0];
-            const int nb[8] = {c[-W2 - 1], c[-W2], c[-W2 + 1], c[-1], c[1], c[W2 - 1], c[W2], c[W2 + 1]};
-            k_ini = p < p1 && m > t_ini;
-            k_min = p < p1 && m > t_min;
+    // ---- window-local strict 3x3 NMS at both thresholds, on the surviving pixels only; the
+    // results are bits of a raster-order mask per threshold ----
+    for (int i = tid; i < nc; i += NT) {
+        const int p = clist[i];
+        const int py = small_div(p, inv_dc), px = p - py * dc;
+        const uint8_t* c = &mv[(py + 1) * W2 + px + 1];
+        const int m = c[0];
+        if (m == 0) continue;
+        const int nb[8] = {c[-W2 - 1], c[-W2], c[-W2 + 1], c[-1], c[1], c[W2 - 1], c[W2], c[W2 + 1]};
+        bool k_ini = m > t_ini, k_min = m > t_min;
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const int mq = nb[k];
-                k_ini &= (m - 1) > (mq > t_ini ? mq - 1 : 0);
-                k_min &= (m - 1) > (mq > t_min ? mq - 1 : 0);
-            }
+        for (int k = 0; k < 8; k++) {
+            const int mq = nb[k];
+            k_ini &= (m - 1) > (mq > t_ini ? mq - 1 : 0);
+            k_min &= (m - 1) > (mq > t_min ? mq - 1 : 0);
         }
-        const uint64_t bi = __ballot(k_ini), bm = __ballot(k_min);
-        if (lane == 0) { masks[wid][0][ci] = bi; masks[wid][1][ci] = bm; }
-        c_ini += __popcll(bi);
-        c_min += __popcll(bm);
+        const unsigned long long bit = 1ull << (p & 63);
+        if (k_ini) atomicOr(&bmask[0][p >> 6], bit);
+        if (k_min) atomicOr(&bmask[1][p >> 6], bit);
     }
-    if (lane == 0) { wcnt[0][wid] = c_ini; wcnt[1][wid] = c_min; }
     __syncthreads();
     TR_PHASE(1, 2)
-    int total_ini = 0;
-#pragma unroll
-    for (int w = 0; w < NW; w++) total_ini += wcnt[0][w];
-    const int sel = total_ini > 0 ? 0 : 1;   // per-cell fallback iniThFAST -> minThFAST
-    int off = 0;
-    for (int w = 0; w < wid; w++) off += wcnt[sel][w];
+    // ---- per-cell fallback iniThFAST -> minThFAST, then the ordered compaction ----
+    const int nwd = (np + 63) >> 6;
+    if (wid == 0) {
+        int ci = 0;
+        for (int w = lane; w < nwd; w += 64) ci += __popcll(bmask[0][w]);
+        const int tot_ini = wave_sum_i32(ci);
+        const int sel = tot_ini > 0 ? 0 : 1;
+        // exclusive scan of the selected mask's word popcounts (2 words per lane: nwd <= 96)
+        const int w0 = 2 * lane, w1 = 2 * lane + 1;
+        const int c0 = w0 < nwd ? __popcll(bmask[sel][w0]) : 0, c1 = w1 < nwd ? __popcll(bmask[sel][w1]) : 0;
+        const int inc = wave_incl_scan(c0 + c1);
+        if (w0 < nwd) woff[w0] = inc - c0 - c1;
+        if (w1 < nwd) woff[w1] = inc - c1;
+        if (lane == 63) { wsel = sel; wtot = inc; }
+    }
+    __syncthreads();
+    const int sel = wsel;
     uint32_t* out = cand + (int64_t)f * P->n_slots_total + cg.slot_off;
-    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int q0 = p0, ci = 0; q0 < p1; q0 += 64, ci++) {
-        const uint64_t mk = masks[wid][sel][ci];
-        const int p = q0 + lane;
+    for (int w = wid; w < nwd; w += NW) {
+        const uint64_t mk = bmask[sel][w];
+        const int p = 64 * w + lane;
         if ((mk >> lane) & 1ull) {
             const int py = small_div(p, inv_dc), px = p - py * dc;
             const int x = cg.x0 + 3 + px - G.min_bx, y = cg.y0 + 3 + py - G.min_by;
-            out[off + __popcll(mk & lt)] = pack_cand(x, y, (int)mv[(py + 1) * W2 + px + 1] - 1);
+            out[woff[w] + __popcll(mk & lt)] = pack_cand(x, y, (int)mv[(py + 1) * W2 + px + 1] - 1);
         }
-        off += __popcll(mk);
     }
-    if (tid == 0) {
-        int c = 0;
-#pragma unroll
-        for (int w = 0; w < NW; w++) c += wcnt[sel][w];
-        *cnt_out = c;
-    }
+    if (tid == 0) *cnt_out = wtot;
     TR_PHASE(1, 3)
     TR_END(1)
 }
