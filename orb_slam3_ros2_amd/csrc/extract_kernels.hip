@@ -532,13 +532,25 @@ __device__ void block_scan_array3(int* a0, int* a1, int* a2, int n, int* ctl, in
         for (int i = b; i < e; i++) { const int v = arr[k][i]; arr[k][i] = off[k]; off[k] += v; }
     __syncthreads();
 }
-// Descending sort of n unique keys by rank (no barriers inside): out[#greater] = key.
+// Descending sort of n unique keys by rank: out[#greater] = key. Four threads per key (a quad)
+// each count a quarter of the keys, two ds_read_b128 per step; the quad sums by DPP.
 __device__ void block_rank_sort_desc(const uint64_t* __restrict__ a, uint64_t* __restrict__ out, int n) {
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        const uint64_t x = a[i];
+    const int q = threadIdx.x & 3, nq = blockDim.x >> 2;
+    const int per = (((n + 3) >> 2) + 1) & ~1;   // even: pairs of keys per 16-byte read
+    const int j0 = min(q * per, n), j1 = min(j0 + per, n);
+    for (int i0 = 0; i0 < n; i0 += nq) {
+        const int i = i0 + (threadIdx.x >> 2);
+        const uint64_t x = i < n ? a[i] : ~0ull;
         int r = 0;
-        for (int j = 0; j < n; j++) r += a[j] > x ? 1 : 0;
-        out[r] = x;
+        int j = j0;
+        for (; j + 1 < j1; j += 2) {
+            const ulonglong2 v = *(const ulonglong2*)(a + j);
+            r += (v.x > x ? 1 : 0) + (v.y > x ? 1 : 0);
+        }
+        if (j < j1) r += a[j] > x ? 1 : 0;
+        r += __builtin_amdgcn_update_dpp(0, r, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+        r += __builtin_amdgcn_update_dpp(0, r, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+        if (q == 0 && i < n) out[r] = x;
     }
     __syncthreads();
 }
@@ -644,6 +656,12 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
     // flattened gather + root classification: key k belongs to the cell c with cellstart[c] <= k <
     // cellstart[c+1] (binary search in LDS); up to 4 keys per thread with their loads in flight
     // together
+    // With M <= 4 * nt (every C2/C3 level) each thread keeps its keys k = tid + u * nt and their
+    // current nodes in registers for the whole division (kreg/nreg): the sweeps then read no key
+    // state from LDS, and the 4 keys' lookup chains interleave.
+    const bool kr = M <= 4 * nt;
+    uint32_t kreg[4] = {0u, 0u, 0u, 0u};
+    int nreg[4] = {0, 0, 0, 0};
     for (int k0 = 0; k0 < M; k0 += 4 * nt) {
         uint32_t kv[4];
 #pragma unroll
@@ -665,7 +683,8 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                 int r = (int)((float)cand_x(kv[u]) / hX);
                 r = r < 0 ? 0 : (r >= nIni ? nIni - 1 : r);
                 tgt = (uint32_t)r;
-                knode[k] = (uint16_t)r;
+                if (kr) { kreg[u] = kv[u]; nreg[u] = r; }
+                else knode[k] = (uint16_t)r;
             }
             wave_aggregate_count(tgt, S.ccount);
         }
@@ -711,18 +730,42 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
             break;
         }
         // ---- sweep: remap keys through map4 (OLD rect split), classify into CUR children ----
-        for (int k0 = 0; k0 < M; k0 += nt) {
-            const int k = k0 + tid;
-            uint32_t tgt = 0xFFFFFFFFu;
-            if (k < M) {
-                const uint32_t key = keys[k];
-                const int x = cand_x(key), y = cand_y(key);
-                const int o = knode[k];
-                const int nd = S.map4[o * 4 + quad_of(rectO[o], x, y)];
-                knode[k] = (uint16_t)nd;
-                if (cntC[nd] > 1) tgt = (uint32_t)(nd * 4 + quad_of(rectC[nd], x, y));
+        if (kr) {
+            uint32_t tg[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int k = tid + u * nt;
+                tg[u] = 0xFFFFFFFFu;
+                if (k < M) {
+                    const int x = cand_x(kreg[u]), y = cand_y(kreg[u]);
+                    const int o = nreg[u];
+                    nreg[u] = S.map4[o * 4 + quad_of(rectO[o], x, y)];
+                }
             }
-            wave_aggregate_count(tgt, S.ccount);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int k = tid + u * nt;
+                if (k < M) {
+                    const int nd = nreg[u];
+                    if (cntC[nd] > 1) tg[u] = (uint32_t)(nd * 4 + quad_of(rectC[nd], cand_x(kreg[u]), cand_y(kreg[u])));
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) wave_aggregate_count(tg[u], S.ccount);
+        } else {
+            for (int k0 = 0; k0 < M; k0 += nt) {
+                const int k = k0 + tid;
+                uint32_t tgt = 0xFFFFFFFFu;
+                if (k < M) {
+                    const uint32_t key = keys[k];
+                    const int x = cand_x(key), y = cand_y(key);
+                    const int o = knode[k];
+                    const int nd = S.map4[o * 4 + quad_of(rectO[o], x, y)];
+                    knode[k] = (uint16_t)nd;
+                    if (cntC[nd] > 1) tgt = (uint32_t)(nd * 4 + quad_of(rectC[nd], x, y));
+                }
+                wave_aggregate_count(tgt, S.ccount);
+            }
         }
         __syncthreads();
         if (iter == 1) { TR_PHASE(2, 41) }
@@ -775,6 +818,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
             }
         } else {
             // ---- FINAL phase: divide largest (size, serial) first until >= N ----
+            TR_PHASE(2, 48)
             if (w0) {
                 const int per = (n + 63) >> 6;
                 const int b = min(lane * per, n), e = min(b + per, n);
@@ -787,9 +831,12 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                         S.skey2[pos++] = ((uint64_t)cntC[p] << 40) | ((uint64_t)serC[p] << 16) | (uint64_t)p;
                 if (lane == 0) ctl[60] = __builtin_amdgcn_readlane(inc, 63);
             }
+            TR_PHASE(2, 45)
             __syncthreads();
+            TR_PHASE(2, 46)
             const int K = ctl[60];
             block_rank_sort_desc(S.skey2, S.skey, K);   // keys unique: (size, serial) order; ends in a barrier
+            TR_PHASE(2, 47)
             if (w0) {
                 const int serial0 = ctl[57];
                 const int per = (K + 63) >> 6;
@@ -871,45 +918,59 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
     const int n = ctl[56];
     for (int i = tid; i < n; i += nt) S.cbest[i] = 0;
     __syncthreads();
-    for (int k = tid; k < M; k += nt) {
-        const uint32_t key = keys[k];
-        const int o = knode[k];
-        const int nd = S.map4[o * 4 + quad_of(rectO[o], cand_x(key), cand_y(key))];
-        atomicMax(&S.cbest[nd], pack_best(cand_s(key), k));
+    TR_PHASE(2, 60)
+    if (kr) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int k = tid + u * nt;
+            if (k < M) {
+                const uint32_t key = kreg[u];
+                const int o = nreg[u];
+                const int nd = S.map4[o * 4 + quad_of(rectO[o], cand_x(key), cand_y(key))];
+                atomicMax(&S.cbest[nd], pack_best(cand_s(key), k));
+            }
+        }
+    } else {
+        for (int k = tid; k < M; k += nt) {
+            const uint32_t key = keys[k];
+            const int o = knode[k];
+            const int nd = S.map4[o * 4 + quad_of(rectO[o], cand_x(key), cand_y(key))];
+            atomicMax(&S.cbest[nd], pack_best(cand_s(key), k));
+        }
     }
     __syncthreads();
-    // ---- output in list order (wave 0): retained key per node, lapping flag and rank ----
-    if (w0) {
-        LevelKp* out = lvl_kp + (int64_t)f * P->kp_slots_total + G.kp_base;
-        const int ncap = min(n, G.kp_cap);
-        for (int p = lane; p < ncap; p += 64) {
+    TR_PHASE(2, 61)
+    // ---- output in list order: retained key per node, lapping flag, and its rank among the
+    // same-flag nodes from one block scan per 1024 nodes ----
+    const int ncap = min(n, G.kp_cap);
+    LevelKp* out = lvl_kp + (int64_t)f * P->kp_slots_total + G.kp_base;
+    int lap_run = 0;
+    for (int p0 = 0; p0 < ncap; p0 += nt) {
+        const int p = p0 + tid;
+        int lap = 0, x = 0, y = 0, sc = 0;
+        if (p < ncap) {
             const int k = (int)(0xFFFFFFu - (S.cbest[p] & 0xFFFFFFu));
             const uint32_t key = keys[k];
-            const int x = cand_x(key) + G.min_bx, y = cand_y(key) + G.min_by;
+            x = cand_x(key) + G.min_bx; y = cand_y(key) + G.min_by;
+            sc = cand_s(key);
             const float xs = (l == 0) ? (float)x : (float)x * G.scale;
-            const int lap = (xs >= (float)cfg.lap0 && xs <= (float)cfg.lap1) ? 1 : 0;
-            S.tA[p] = lap; S.tB[p] = 1 - lap;
-            S.tC[p] = (x & 0xFFFF) | (y << 16);
-            S.skey[p] = (uint64_t)cand_s(key);
+            lap = (xs >= (float)cfg.lap0 && xs <= (float)cfg.lap1) ? 1 : 0;
         }
-        wave_lds_fence();
-        const int nlap = wave_scan_lds(S.tA, ncap);
-        wave_scan_lds(S.tB, ncap);
-        for (int p = lane; p < ncap; p += 64) {
-            const int xy = S.tC[p];
-            const int x = xy & 0xFFFF, y = xy >> 16;
-            const int lapflag = (p + 1 < ncap ? S.tA[p + 1] : nlap) - S.tA[p];
-            const int rank = lapflag ? S.tA[p] : S.tB[p];
+        int tot;
+        const int before = lap_run + block_excl_scan(lap, ctl, &tot);   // same-flag nodes before p
+        if (p < ncap) {
+            const int rank = lap ? before : p - before;
             LevelKp r;
             r.x = (int16_t)x; r.y = (int16_t)y;
-            r.srl = (uint32_t)S.skey[p] | ((uint32_t)lapflag << 8) | ((uint32_t)rank << 9);
+            r.srl = (uint32_t)sc | ((uint32_t)lap << 8) | ((uint32_t)rank << 9);
             out[p] = r;
         }
-        if (lane == 0) {
-            lvl_cnt[f * P->n_levels + l] = ncap;
-            lvl_nlap[f * P->n_levels + l] = nlap;
-            if (n > G.kp_cap) atomicOr(err, 2);
-        }
+        lap_run += tot;
+    }
+    if (tid == 0) {
+        lvl_cnt[f * P->n_levels + l] = ncap;
+        lvl_nlap[f * P->n_levels + l] = lap_run;
+        if (n > G.kp_cap) atomicOr(err, 2);
     }
     TR_PHASE(2, 63)
     TR_END(2)
