@@ -333,6 +333,15 @@ def _f8_inputs():
     return probs, s, f, synthetic_init_pair(n1=1800, seed=31)
 
 
+def _kfdb_inputs():
+    from orb_slam3_ros2_amd.synthetic import synthetic_kfdb_scene, synthetic_query_bow
+    sc = synthetic_kfdb_scene(n_kf=1000, seed=21)
+    qbow = synthetic_query_bow(sc, [120, 480, 900], seed=5, keep=0.5)
+    con = np.zeros(1000, np.uint8)
+    con[sc["covis"][120][sc["covis"][120] >= 0]] = 1
+    return sc, qbow, con
+
+
 def _ms(fn, reps):
     fn()
     t0 = time.perf_counter()
@@ -360,8 +369,20 @@ def f8_tracking(ctx):
         f, s["points"], s["normals"], s["min_dist"], s["max_dist"], s["mp_desc"], s["skip"], th=1.0), 50), 4)
     mi = ORBmatcher(0.9, True, ctx=ctx)
     out["a12_search_for_initialization_ms"] = round(_ms(lambda: mi.SearchForInitialization(*ini, 100), 20), 4)
+    from orb_slam3_ros2_amd import KeyFrameDatabase
+    sc, qbow, con = _kfdb_inputs()
+    db = KeyFrameDatabase(len(sc["bows"]), ctx=ctx)
+    for i, b in enumerate(sc["bows"]):
+        db.add(i, b)
+    qid = iter(range(1, 1 << 30))
+    out["f8_kfdb_relocalization_ms"] = round(_ms(lambda: db.DetectRelocalizationCandidates(
+        next(qid), qbow, sc["covis"]), 20), 4)
+    out["f8_kfdb_nbest_ms"] = round(_ms(lambda: db.DetectNBestCandidates(
+        next(qid), qbow, sc["covis"], con, 3, sc["kf_map"], 0), 20), 4)
+    db.close()
     out["f8_inputs"] = ("PoseOptimization 600 edges/frame; projection 1250 keypoints x 1000 map points; "
-                        "SearchForInitialization 1114 octave-0 queries x 1128 F2 keypoints, window 100")
+                        "SearchForInitialization 1114 octave-0 queries x 1128 F2 keypoints, window 100; "
+                        "KeyFrameDatabase 1000 keyframes (~600 words each), query of 3 places")
     return out
 
 
@@ -369,7 +390,16 @@ def cpu_f8_tracking():
     """The oracle on one core for the same 8f inputs (ms per frame / per call)."""
     from oracle import pyoracle as O
     probs, s, f, ini = _f8_inputs()
-    return {"a12_search_for_initialization_single_core_ms": round(_ms(
+    sc, qbow, con = _kfdb_inputs()
+    db = O.KeyFrameDatabase(len(sc["bows"]), 20000)
+    for i, b in enumerate(sc["bows"]):
+        db.add(i, b)
+    qid = iter(range(1, 1 << 30))
+    kf = {"f8_kfdb_relocalization_single_core_ms": round(_ms(lambda: db.DetectRelocalizationCandidates(
+              next(qid), qbow, sc["covis"]), 20), 4),
+          "f8_kfdb_nbest_single_core_ms": round(_ms(lambda: db.DetectNBestCandidates(
+              next(qid), qbow, sc["covis"], con, 3, sc["kf_map"], 0), 20), 4)}
+    return {**kf, "a12_search_for_initialization_single_core_ms": round(_ms(
                 lambda: O.search_for_initialization(*ini, 100, 0.9, True), 20), 4),
             "f8_pose_opt_single_core_ms": round(_ms(lambda: O.pose_optimization(probs[0]), 20), 4),
             "f8_search_by_projection_last_single_core_ms": round(_ms(lambda: O.search_by_projection_last(

@@ -260,6 +260,37 @@ int orbhip_search_for_initialization(orbhip_ctx* ctx, const orbhip_init_frame* f
                                      float* prev_matched, int window_size, float nnratio, int check_orientation,
                                      int32_t* matches12);
 
+/* ---- KeyFrameDatabase place recognition ---------------------
+ * U:src/KeyFrameDatabase.cc. The database lives on the device: add/erase mirror
+ * KeyFrameDatabase::add(pKF) / erase(pKF) with the KF's BowVector (ascending word ids, L1
+ * values; slot = the adapter's KeyFrame index, < max_kf). The KeyFrame members the queries use
+ * (mnRelocQuery/Words, mRelocScore, mnPlaceRecognitionQuery/Words/Score) persist in the
+ * database between queries, as on the KeyFrames. Per query the adapter passes the query
+ * BowVector (<= 3072 words), a unique query id (Frame / KeyFrame mnId), covis = max_kf x 10
+ * slots of KeyFrame::GetBestCovisibilityKeyFrames(10) (-1 padded), and optionally the map id of
+ * every slot (GetMap()) with the query's map, and flags (bit 0 isBad(), bit 1 GetMap()->IsBad()). */
+typedef struct orbhip_kfdb orbhip_kfdb;
+typedef struct {
+    int64_t query_id;
+    const int32_t* words;
+    const double* values;
+    int32_t n;
+    const int32_t* covis;       /* max_kf x 10 */
+    const int32_t* kf_map;      /* max_kf or NULL (one map) */
+    int32_t query_map;
+    const uint8_t* kf_flags;    /* max_kf or NULL */
+} orbhip_kfdb_query;
+int orbhip_kfdb_create(orbhip_ctx* ctx, int max_kf, orbhip_kfdb** out);
+int orbhip_kfdb_destroy(orbhip_kfdb* db);
+int orbhip_kfdb_add(orbhip_kfdb* db, int kf, const int32_t* words, const double* values, int n);
+int orbhip_kfdb_erase(orbhip_kfdb* db, int kf);
+/* DetectRelocalizationCandidates(F, pMap): writes up to cap slots, returns the full count. */
+int orbhip_kfdb_detect_relocalization(orbhip_kfdb* db, const orbhip_kfdb_query* q, int32_t* out, int cap);
+/* DetectNBestCandidates(pKF, vpLoopCand, vpMergeCand, n): connected = max_kf flags of
+ * pKF->GetConnectedKeyFrames() (or NULL); n <= 32. Returns n_loop + n_merge. */
+int orbhip_kfdb_detect_nbest(orbhip_kfdb* db, const orbhip_kfdb_query* q, const uint8_t* connected, int n,
+                             int32_t* loop_out, int32_t* n_loop, int32_t* merge_out, int32_t* n_merge);
+
 /* ---- motion-only bundle adjustment -------------------------
  * U:src/Optimizer.cc::Optimizer::PoseOptimization(Frame* pFrame), monocular observations:
  * one VertexSE3Expmap (Tcw), EdgeSE3ProjectXYZOnlyPose per matched MapPoint (information

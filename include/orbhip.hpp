@@ -12,6 +12,7 @@
 #ifndef ORBHIP_HPP
 #define ORBHIP_HPP
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -149,6 +150,38 @@ public:
 
     float mfNNratio;
     bool mbCheckOrientation;
+};
+
+// U:include/KeyFrameDatabase.h — the device database; slots stand for KeyFrames.
+class KeyFrameDatabase {
+public:
+    KeyFrameDatabase(orbhip_ctx* ctx, int maxKF) : maxKF_(maxKF) { check(orbhip_kfdb_create(ctx, maxKF, &db_), "orbhip_kfdb_create"); }
+    ~KeyFrameDatabase() { if (db_) orbhip_kfdb_destroy(db_); }
+    KeyFrameDatabase(const KeyFrameDatabase&) = delete;
+    KeyFrameDatabase& operator=(const KeyFrameDatabase&) = delete;
+    void add(int kf, const std::vector<int32_t>& words, const std::vector<double>& values) {
+        check(orbhip_kfdb_add(db_, kf, words.data(), values.data(), (int)words.size()), "orbhip_kfdb_add");
+    }
+    void erase(int kf) { check(orbhip_kfdb_erase(db_, kf), "orbhip_kfdb_erase"); }
+    std::vector<int> DetectRelocalizationCandidates(const orbhip_kfdb_query& q) {
+        std::vector<int32_t> out(maxKF_);
+        const int n = orbhip_kfdb_detect_relocalization(db_, &q, out.data(), maxKF_);
+        check(n, "orbhip_kfdb_detect_relocalization");
+        return std::vector<int>(out.begin(), out.begin() + std::min(n, maxKF_));
+    }
+    void DetectNBestCandidates(const orbhip_kfdb_query& q, const std::vector<uint8_t>& connected, int n,
+                               std::vector<int>& loopCand, std::vector<int>& mergeCand) {
+        std::vector<int32_t> lo(n > 0 ? n : 1), me(n > 0 ? n : 1);
+        int32_t nl = 0, nm = 0;
+        check(orbhip_kfdb_detect_nbest(db_, &q, connected.empty() ? nullptr : connected.data(), n, lo.data(), &nl,
+                                       me.data(), &nm), "orbhip_kfdb_detect_nbest");
+        loopCand.assign(lo.begin(), lo.begin() + nl);
+        mergeCand.assign(me.begin(), me.begin() + nm);
+    }
+
+private:
+    orbhip_kfdb* db_ = nullptr;
+    int maxKF_;
 };
 
 // U:include/Optimizer.h — the g2o problem of LocalBundleAdjustment in SoA form. The adapter

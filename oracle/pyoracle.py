@@ -68,6 +68,15 @@ def lib():
                                               c_float, _u8p, _i32p, _i32p]
         L.orc_search_for_initialization.argtypes = [c_int, vp, _u8p, c_int, vp, _u8p, c_float, c_float, c_float,
                                                     c_float, _f32p, c_int, c_float, c_int, _i32p]
+        L.orc_kfdb_create.argtypes = [c_int, c_int]
+        L.orc_kfdb_create.restype = vp
+        L.orc_kfdb_destroy.argtypes = [vp]
+        L.orc_kfdb_add.argtypes = [vp, c_int, _i32p, _f64p, c_int]
+        L.orc_kfdb_erase.argtypes = [vp, c_int]
+        L.orc_kfdb_detect_relocalization.argtypes = [vp, ctypes.c_longlong, _i32p, _f64p, c_int, _i32p, vp, c_int,
+                                                     _i32p]
+        L.orc_kfdb_detect_nbest.argtypes = [vp, ctypes.c_longlong, _i32p, _f64p, c_int, _i32p, vp, vp, c_int, vp,
+                                            c_int, _i32p, _i32p, _i32p, _i32p]
         L.orc_bgr2gray.argtypes = [_u8p, c_int, c_int, c_int, _u8p, c_int]
         L.orc_glibc_sincosf_range.argtypes = [ctypes.c_uint32, ctypes.c_uint32, _f32p, _f32p]
         _lib = L
@@ -268,3 +277,46 @@ def search_for_initialization(kps1, desc1, kps2, desc2, prev_matched, window=100
         np.ascontiguousarray(desc2, np.uint8).reshape(-1, 32), *[float(b) for b in bounds], prev, int(window),
         float(nnratio), int(check_orientation), m)
     return n, m, prev
+
+
+class KeyFrameDatabase:
+    """Oracle KeyFrameDatabase (persistent KeyFrame members, inverted file in insertion order)."""
+
+    def __init__(self, max_kf, n_words):
+        self.max_kf = max_kf
+        self._h = lib().orc_kfdb_create(int(max_kf), int(n_words))
+
+    def add(self, kf, bow):
+        w = np.ascontiguousarray(bow[0], np.int32); v = np.ascontiguousarray(bow[1], np.float64)
+        lib().orc_kfdb_add(self._h, int(kf), w, v, w.shape[0])
+
+    def erase(self, kf):
+        lib().orc_kfdb_erase(self._h, int(kf))
+
+    def DetectRelocalizationCandidates(self, query_id, bow, covis, kf_map=None, query_map=0):
+        w = np.ascontiguousarray(bow[0], np.int32); v = np.ascontiguousarray(bow[1], np.float64)
+        cv = np.ascontiguousarray(covis, np.int32).reshape(-1)
+        km = None if kf_map is None else np.ascontiguousarray(kf_map, np.int32)
+        out = np.zeros(self.max_kf, np.int32)
+        n = lib().orc_kfdb_detect_relocalization(self._h, int(query_id), w, v, w.shape[0], cv, _vp(km),
+                                                 int(query_map), out)
+        return out[:n].copy()
+
+    def DetectNBestCandidates(self, query_id, bow, covis, connected=None, n=3, kf_map=None, query_map=0,
+                              flags=None):
+        w = np.ascontiguousarray(bow[0], np.int32); v = np.ascontiguousarray(bow[1], np.float64)
+        cv = np.ascontiguousarray(covis, np.int32).reshape(-1)
+        con = None if connected is None else np.ascontiguousarray(connected, np.uint8)
+        km = None if kf_map is None else np.ascontiguousarray(kf_map, np.int32)
+        fl = None if flags is None else np.ascontiguousarray(flags, np.uint8)
+        lo = np.zeros(max(n, 1), np.int32); me = np.zeros(max(n, 1), np.int32)
+        nl = np.zeros(1, np.int32); nm = np.zeros(1, np.int32)
+        lib().orc_kfdb_detect_nbest(self._h, int(query_id), w, v, w.shape[0], cv, _vp(con), _vp(km), int(query_map),
+                                    _vp(fl), int(n), lo, nl, me, nm)
+        return lo[: nl[0]].copy(), me[: nm[0]].copy()
+
+    def __del__(self):
+        try:
+            lib().orc_kfdb_destroy(self._h)
+        except Exception:
+            pass

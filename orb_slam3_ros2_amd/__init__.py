@@ -11,6 +11,10 @@ Host-side mirror of the reference's hot-path interfaces over th
   Optimizer.PoseOptimization(frame_problem)                                 U:src/Optimizer.cc
   ORBVocabulary(vocab).transform(desc)  (DBoW2 TemplatedVocabulary)         U:src/Frame.cc::ComputeBoW
   ORBmatcher.SearchByBoW(...)                                               U:src/ORBmatcher.cc
+  ORBmatcher.SearchForInitialization(...)                                   U:src/ORBmatcher.cc
+  ORBmatcher.SearchByProjectionLastFrame / SearchLocalPoints(...)           U:src/ORBmatcher.cc
+  KeyFrameDatabase(max_kf).DetectRelocalizationCandidates / DetectNBestCandidates
+                                                                            U:src/KeyFrameDatabase.cc
 
 The HIP library is the only compute path: importing this package on a box without the
 built extension, or calling it without a GPU, raises — there is no CPU fallback.
@@ -22,6 +26,7 @@ from .extractor import KeyPoint, ORBextractor  # noqa: F401
 from .matcher import ORBmatcher  # noqa: F401
 from .optimizer import BAProblem, BAResult, Optimizer, PoseProblem, PoseResult  # noqa: F401
 from .bow import ORBVocabulary  # noqa: F401
+from .kfdb import KeyFrameDatabase  # noqa: F401
 
-__all__ = ["ORBextractor", "KeyPoint", "ORBmatcher", "Optimizer", "BAProblem", "BAResult", "PoseProblem", "PoseResult", "ORBVocabulary", "OrbHipError",
+__all__ = ["ORBextractor", "KeyPoint", "ORBmatcher", "Optimizer", "BAProblem", "BAResult", "PoseProblem", "PoseResult", "ORBVocabulary", "KeyFrameDatabase", "OrbHipError",
            "lib", "library_path"]

@@ -85,6 +85,12 @@ class InitFrameC(ctypes.Structure):
                 ("max_x", ctypes.c_float), ("min_y", ctypes.c_float), ("max_y", ctypes.c_float)]
 
 
+class KfdbQueryC(ctypes.Structure):
+    _fields_ = [("query_id", ctypes.c_int64), ("words", ctypes.c_void_p), ("values", ctypes.c_void_p),
+                ("n", ctypes.c_int32), ("covis", ctypes.c_void_p), ("kf_map", ctypes.c_void_p),
+                ("query_map", ctypes.c_int32), ("kf_flags", ctypes.c_void_p)]
+
+
 class LocalPointsC(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int32), ("points", ctypes.c_void_p), ("normals", ctypes.c_void_p),
                 ("min_dist", ctypes.c_void_p), ("max_dist", ctypes.c_void_p), ("desc", ctypes.c_void_p),
@@ -100,7 +106,9 @@ EXPORTED = ["orbhip_abi_version", "orbhip_create", "orbhip_destroy", "orbhip_lev
             "orbhip_vocab_create", "orbhip_vocab_load_text", "orbhip_vocab_destroy", "orbhip_vocab_info",
             "orbhip_bow_transform", "orbhip_bow_transform_device", "orbhip_search_bow",
             "orbhip_pose_optimization", "orbhip_pose_optimization_batch", "orbhip_search_by_projection_last",
-            "orbhip_search_local_points", "orbhip_search_for_initialization"]
+            "orbhip_search_local_points", "orbhip_search_for_initialization",
+            "orbhip_kfdb_create", "orbhip_kfdb_destroy", "orbhip_kfdb_add", "orbhip_kfdb_erase",
+            "orbhip_kfdb_detect_relocalization", "orbhip_kfdb_detect_nbest"]
 
 
 def lib():
@@ -157,6 +165,12 @@ def lib():
                                              i32, f32, vp, vp, vp]
     L.orbhip_search_for_initialization.argtypes = [vp, ctypes.POINTER(InitFrameC), ctypes.POINTER(InitFrameC), vp,
                                                    i32, f32, i32, vp]
+    L.orbhip_kfdb_create.argtypes = [vp, i32, ctypes.POINTER(vp)]
+    L.orbhip_kfdb_destroy.argtypes = [vp]
+    L.orbhip_kfdb_add.argtypes = [vp, i32, vp, vp, i32]
+    L.orbhip_kfdb_erase.argtypes = [vp, i32]
+    L.orbhip_kfdb_detect_relocalization.argtypes = [vp, ctypes.POINTER(KfdbQueryC), vp, i32]
+    L.orbhip_kfdb_detect_nbest.argtypes = [vp, ctypes.POINTER(KfdbQueryC), vp, i32, vp, vp, vp, vp]
     L.orbhip_test_sincosf.argtypes = [vp, vp, vp, ctypes.c_int64]
     L.orbhip_test_sincosf_sweep.argtypes = [ctypes.c_uint32, ctypes.c_uint32, vp, vp]
     L.orbhip_test_sincosf_sweep.restype = ctypes.c_int64

@@ -24,6 +24,7 @@
 #include "orbhip_ba.h"
 #include "pose_opt.h"
 #include "proj.h"
+#include "kfdb.h"
 #include "ba_chol_blocked.h"
 #include "orbhip_kernels.h"
 #include "orbhip_plan.h"
@@ -774,6 +775,55 @@ int orbhip_search_for_initialization(orbhip_ctx* c, const orbhip_init_frame* f1,
     HIPOK(hipSetDevice(c->device));
     if (!c->proj) c->proj = proj_ws_create();
     return init_search(c->proj, f1, f2, prev_matched, window_size, nnratio, check_orientation, matches12, c->stream);
+}
+
+struct orbhip_kfdb {
+    orbhip::KfDb* d = nullptr;
+    int device = 0;
+};
+
+int orbhip_kfdb_create(orbhip_ctx* c, int max_kf, orbhip_kfdb** out) {
+    if (!c || !out) return ORBHIP_ERR_ARG;
+    *out = nullptr;
+    HIPOK(hipSetDevice(c->device));
+    int rc = ORBHIP_OK;
+    KfDb* d = kfdb_create(max_kf, c->stream, &rc);
+    if (!d) return rc;
+    *out = new orbhip_kfdb{d, c->device};
+    return ORBHIP_OK;
+}
+
+int orbhip_kfdb_destroy(orbhip_kfdb* db) {
+    if (!db) return ORBHIP_ERR_ARG;
+    (void)hipSetDevice(db->device);
+    kfdb_destroy(db->d);
+    delete db;
+    return ORBHIP_OK;
+}
+
+int orbhip_kfdb_add(orbhip_kfdb* db, int kf, const int32_t* words, const double* values, int n) {
+    if (!db) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(db->device));
+    return kfdb_add(db->d, kf, words, values, n);
+}
+
+int orbhip_kfdb_erase(orbhip_kfdb* db, int kf) {
+    if (!db) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(db->device));
+    return kfdb_erase(db->d, kf);
+}
+
+int orbhip_kfdb_detect_relocalization(orbhip_kfdb* db, const orbhip_kfdb_query* q, int32_t* out, int cap) {
+    if (!db) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(db->device));
+    return kfdb_detect_relocalization(db->d, q, out, cap);
+}
+
+int orbhip_kfdb_detect_nbest(orbhip_kfdb* db, const orbhip_kfdb_query* q, const uint8_t* connected, int n,
+                             int32_t* loop_out, int32_t* n_loop, int32_t* merge_out, int32_t* n_merge) {
+    if (!db) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(db->device));
+    return kfdb_detect_nbest(db->d, q, connected, n, loop_out, n_loop, merge_out, n_merge);
 }
 
 int orbhip_comm_unique_id(uint8_t* id) {

@@ -315,3 +315,52 @@ def synthetic_init_pair(n1=1500, seed=9, width=640, height=480, n_levels=8, leve
     k2, d2 = k2[perm], d2[perm]
     prev = np.stack([k1["x"], k1["y"]], 1).astype(np.float32)
     return k1, d1, k2, d2, prev
+
+
+def synthetic_kfdb_scene(n_kf=200, n_words=20000, words_per_place=400, seed=13, n_maps=2, common_pool=0,
+                         common_frac=0.3):
+    """A keyframe trajectory for KeyFrameDatabase queries. KF i sees the
+    words of places i-2..i+2 (a sliding window, so neighbours share many words) plus random
+    words; values positive, L1-normalised (DBoW2 BowVector). covis[i] = the 10 nearest KFs by
+    index (GetBestCovisibilityKeyFrames order: most shared first), maps split the trajectory.
+    A few KFs revisit an early place (loop closures). common_pool > 0 adds a pool of words every KF
+    sees a fraction of (repetitive texture: many KFs pass the 0.8 x max common-words cut and the
+    scores crowd). Returns dict(bows, covis, kf_map, place)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    n_places = n_kf + 4
+    place_words = [rng.choice(n_words, words_per_place, replace=False) for _ in range(n_places)]
+    place = np.arange(n_kf)
+    loops = rng.choice(np.arange(n_kf // 2, n_kf), max(1, n_kf // 20), replace=False)
+    place[loops] = rng.integers(0, n_kf // 4, loops.shape[0])
+    pool = rng.choice(n_words, common_pool, replace=False) if common_pool else None
+    bows = []
+    for i in range(n_kf):
+        ws = [] if pool is None else [pool[rng.random(common_pool) < common_frac]]
+        for d in range(-2, 3):
+            p = min(max(place[i] + d, 0), n_places - 1)
+            pw = place_words[p]
+            ws.append(pw[rng.random(pw.shape[0]) < 0.35])
+        ws.append(rng.choice(n_words, 60, replace=False))
+        w = np.unique(np.concatenate(ws)).astype(np.int32)
+        v = rng.gamma(2.0, 1.0, w.shape[0])
+        bows.append((w, v / v.sum()))
+    covis = np.full((n_kf, 10), -1, np.int32)
+    for i in range(n_kf):
+        nb = sorted((j for j in range(max(0, i - 8), min(n_kf, i + 9)) if j != i), key=lambda j: (abs(i - j), j))
+        covis[i, : min(10, len(nb))] = nb[:10]
+    kf_map = (np.arange(n_kf) * n_maps // n_kf).astype(np.int32)
+    return dict(bows=bows, covis=covis, kf_map=kf_map, place=place)
+
+
+def synthetic_query_bow(scene, kf, seed, n_words=20000, keep=0.6, noise=80):
+    """A frame near keyframe `kf` (or seeing several places: a list of KFs): a subset of their
+    words plus noise words, L1-normalised."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    kfs = [kf] if np.isscalar(kf) else list(kf)
+    parts = []
+    for k in kfs:
+        w0, _ = scene["bows"][int(k)]
+        parts.append(w0[rng.random(w0.shape[0]) < keep])
+    w = np.unique(np.concatenate(parts + [rng.choice(n_words, noise, replace=False)])).astype(np.int32)
+    v = rng.gamma(2.0, 1.0, w.shape[0])
+    return w, v / v.sum()
