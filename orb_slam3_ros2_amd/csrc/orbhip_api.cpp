@@ -194,7 +194,9 @@ static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
         G.scale = c->scale[l];
         G.n_feat = c->feat[l];
         G.patch_size = (int)(31 * c->scale[l]);
-        // resize tables (level l from l-1)
+        // resize tables (level l from l-1); each level's column table starts 16-byte aligned and
+        // is padded, so k_resize reads 4 consecutive entries as one int4
+        while (pl->xofs.size() % 4) { pl->xofs.push_back(0); pl->xalpha.push_back(0); }
         G.xtab_off = (int)pl->xofs.size();
         G.ytab_off = (int)pl->yofs.size();
         G.xmax = G.w;
@@ -407,6 +409,7 @@ static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
         if (v.empty()) return hipSuccess;
         return hipMemcpy(d.p, v.data(), v.size() * sizeof(int), hipMemcpyHostToDevice);
     };
+    for (int i = 0; i < 4; i++) { pl->xofs.push_back(0); pl->xalpha.push_back(0); }   // int4 tail reads
     HIPOK(up(pl->d_xofs, pl->xofs));
     HIPOK(up(pl->d_xalpha, pl->xalpha));
     HIPOK(up(pl->d_yofs, pl->yofs));
@@ -450,7 +453,9 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
     static const bool no_cone = std::getenv("ORBHIP_NO_CONE") != nullptr;   // A/B switch for the cascade
     // the cone recomputes each tile's halo on every level: it pays only while the per-level cascade
     // is launch-latency bound (a few work-groups per CU); big batches keep the cascade
-    if (pl->cone_tiles && !no_cone && (size_t)B * pl->cone_tiles <= 1024)
+    static const size_t cone_max = std::getenv("ORBHIP_CONE_MAX_WG") ? (size_t)std::atol(std::getenv("ORBHIP_CONE_MAX_WG"))
+                                                                      : (size_t)1024;
+    if (pl->cone_tiles && !no_cone && (size_t)B * pl->cone_tiles <= cone_max)
         launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_cone_tab.p,
                         pl->cone_tab_stride, st);
     else

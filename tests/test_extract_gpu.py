@@ -120,3 +120,27 @@ def test_device_sincosf_matches_glibc_exhaustive(oracle):
         assert bad >= 0
         total_bad += bad
     assert total_bad == 0
+
+
+def test_large_batch_paths_match_oracle(ext1000, oracle):
+    """B = 16: the batch launch shapes (per-level k_resize cascade, 256-thread FAST cells, a
+    keypoint per wave in k_desc) against the oracle, frame by frame."""
+    import torch
+    B, H, W = 16, 480, 640
+    frames = np.stack([synthetic_frame(60 + i, W, H) for i in range(B)])
+    cap = ext1000.max_keypoints(W, H)
+    dev = torch.device("cuda:0")
+    tf = torch.from_numpy(frames).to(dev)
+    kps = torch.zeros((B, cap, 6), dtype=torch.float32, device=dev)
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
+    n = torch.zeros(B, dtype=torch.int32, device=dev)
+    mono = torch.zeros(B, dtype=torch.int32, device=dev)
+    ext1000.extract_batch_device(tf, kps, desc, n, mono)
+    torch.cuda.synchronize()
+    for i in range(B):
+        om, ok, od = oracle.extract(frames[i])
+        assert int(n[i]) == len(ok) and int(mono[i]) == om, i
+        kk = kps[i, : len(ok)].cpu().numpy()
+        assert np.array_equal(kk[:, :5], ok[:, :5]), i
+        assert np.array_equal(kk[:, 5].view(np.int32), ok[:, 5].astype(np.int32)), i
+        assert np.array_equal(desc[i, : len(ok)].cpu().numpy(), od), i
