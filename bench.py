@@ -101,11 +101,10 @@ def _sum_over_ranks(ws, v: float) -> float:
 
 
 def make_stream_frames(n, w, h, seed0):
-    from orb_slam3_ros2_amd.synthetic import shifted_frame, synthetic_frame
-    fr = [synthetic_frame(seed0, w, h)]
-    for i in range(1, n):
-        fr.append(shifted_frame(fr[-1], 2 + (i % 3), 1 - (i % 2), seed0 + i))
-    return np.stack(fr)
+    """A panning camera over one static scene, SURVEY.md 8d image statistics at every frame
+    (synthetic.synthetic_stream)."""
+    from orb_slam3_ros2_amd.synthetic import synthetic_stream
+    return synthetic_stream(n, w, h, seed0)
 
 
 class Profiler:
@@ -458,7 +457,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (SURVEY.md 8d rectangles+noise frames, translated stream, seeded)",
+        "data": "synthetic (SURVEY.md 8d rectangles + sigma-4 noise; a camera panning over one static scene, seeded)",
         "config": {"workload": "C2: 640x480, 8-level pyramid, 1000 feat/frame, FAST 20/7, batch=1 stream; "
                                "ORBextractor::operator() + brute-force Hamming match to the previous frame",
                    "frames_per_step": 1, "parallelism": f"replicas x{ws} (frame streams, no collective)",

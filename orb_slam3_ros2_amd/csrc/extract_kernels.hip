@@ -604,6 +604,8 @@ __device__ __forceinline__ void wave_aggregate_count(uint32_t tgt, uint32_t* cnt
     }
 }
 
+constexpr int kOctKR = 8;    // keys per thread kept in registers through the division (M <= 8 x 1024)
+
 __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -638,7 +640,8 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                                                  int* __restrict__ lvl_nlap, OctreeCfg cfg, int* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     TR_BEGIN()
-    const int l = blockIdx.x, f = blockIdx.y;
+    // grid (frame, level): the level-0 work-groups (the longest) of every frame dispatch first
+    const int f = blockIdx.x, l = blockIdx.y;
     const LevelGeom& G = P->lv[l];
     const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
     const bool w0 = tid < 64;
@@ -692,11 +695,12 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
     // With M <= 4 * nt (every C2/C3 level) each thread keeps its keys k = tid + u * nt and their
     // current nodes in registers for the whole division (kreg/nreg): the sweeps then read no key
     // state from LDS, and the 4 keys' lookup chains interleave.
-    const bool kr = M <= 4 * nt;
-    uint32_t kreg[4] = {0u, 0u, 0u, 0u};
-    int nreg[4] = {0, 0, 0, 0};
-    for (int k0 = 0; k0 < M; k0 += 4 * nt) {
-        uint32_t kv[4];
+    const bool kr = M <= kOctKR * nt;
+    uint32_t kreg[kOctKR];
+    int nreg[kOctKR];
+#pragma unroll
+    for (int u = 0; u < kOctKR; u++) { kreg[u] = 0u; nreg[u] = 0; }
+    auto gather4 = [&](int k0, uint32_t* kv) {
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int k = min(k0 + tid + u * nt, M - 1);
@@ -707,6 +711,8 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
             }
             kv[u] = cbase[S.cslot[lo] + (k - S.cellstart[lo])];
         }
+    };
+    auto root4 = [&](int k0, const uint32_t* kv, uint32_t* kr4, int* nr4) {
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int k = k0 + tid + u * nt;
@@ -716,10 +722,27 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                 int r = (int)((float)cand_x(kv[u]) / hX);
                 r = r < 0 ? 0 : (r >= nIni ? nIni - 1 : r);
                 tgt = (uint32_t)r;
-                if (kr) { kreg[u] = kv[u]; nreg[u] = r; }
+                if (kr4) { kr4[u] = kv[u]; nr4[u] = r; }
                 else knode[k] = (uint16_t)r;
             }
             wave_aggregate_count(tgt, S.ccount);
+        }
+    };
+    if (kr) {
+        // compile-time register slots: group g holds keys k = (4g + u) * nt + tid
+#pragma unroll
+        for (int g = 0; g < kOctKR / 4; g++) {
+            if (4 * g * nt < M) {   // block-uniform
+                uint32_t kv[4];
+                gather4(4 * g * nt, kv);
+                root4(4 * g * nt, kv, kreg + 4 * g, nreg + 4 * g);
+            }
+        }
+    } else {
+        for (int k0 = 0; k0 < M; k0 += 4 * nt) {
+            uint32_t kv[4];
+            gather4(k0, kv);
+            root4(k0, kv, nullptr, nullptr);
         }
     }
     __syncthreads();
@@ -764,27 +787,34 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
         }
         // ---- sweep: remap keys through map4 (OLD rect split), classify into CUR children ----
         if (kr) {
-            uint32_t tg[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int k = tid + u * nt;
-                tg[u] = 0xFFFFFFFFu;
-                if (k < M) {
-                    const int x = cand_x(kreg[u]), y = cand_y(kreg[u]);
-                    const int o = nreg[u];
-                    nreg[u] = S.map4[o * 4 + quad_of(rectO[o], x, y)];
+            for (int g = 0; g < kOctKR / 4; g++) {
+                if (4 * g * nt >= M) continue;   // block-uniform
+                uint32_t tg[4];
+#pragma unroll
+                for (int v = 0; v < 4; v++) {
+                    const int u = 4 * g + v;
+                    const int k = tid + u * nt;
+                    tg[v] = 0xFFFFFFFFu;
+                    if (k < M) {
+                        const int x = cand_x(kreg[u]), y = cand_y(kreg[u]);
+                        const int o = nreg[u];
+                        nreg[u] = S.map4[o * 4 + quad_of(rectO[o], x, y)];
+                    }
                 }
-            }
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int k = tid + u * nt;
-                if (k < M) {
-                    const int nd = nreg[u];
-                    if (cntC[nd] > 1) tg[u] = (uint32_t)(nd * 4 + quad_of(rectC[nd], cand_x(kreg[u]), cand_y(kreg[u])));
+                for (int v = 0; v < 4; v++) {
+                    const int u = 4 * g + v;
+                    const int k = tid + u * nt;
+                    if (k < M) {
+                        const int nd = nreg[u];
+                        if (cntC[nd] > 1)
+                            tg[v] = (uint32_t)(nd * 4 + quad_of(rectC[nd], cand_x(kreg[u]), cand_y(kreg[u])));
+                    }
                 }
-            }
 #pragma unroll
-            for (int u = 0; u < 4; u++) wave_aggregate_count(tg[u], S.ccount);
+                for (int v = 0; v < 4; v++) wave_aggregate_count(tg[v], S.ccount);
+            }
         } else {
             for (int k0 = 0; k0 < M; k0 += nt) {
                 const int k = k0 + tid;
@@ -954,7 +984,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
     TR_PHASE(2, 60)
     if (kr) {
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kOctKR; u++) {
             const int k = tid + u * nt;
             if (k < M) {
                 const uint32_t key = kreg[u];
@@ -1394,7 +1424,7 @@ void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom*
                    const int* cand_cnt, uint32_t* kscratch, uint16_t* nscratch, LevelKp* lvl_kp, int* lvl_cnt,
                    int* lvl_nlap, const OctreeCfg& cfg, int* err, int B, hipStream_t st) {
     const size_t lds = octree_lds_bytes(hP, cfg);
-    dim3 grd(hP.n_levels, B, 1);
+    dim3 grd(B, hP.n_levels, 1);
     hipLaunchKernelGGL(k_octree, grd, dim3(1024), lds, st, dP, cells, cand, cand_cnt, kscratch, nscratch, lvl_kp,
                        lvl_cnt, lvl_nlap, cfg, err);
 }

@@ -41,6 +41,32 @@ def shifted_frame(base: np.ndarray, dx: int, dy: int, seed: int, noise_sigma: fl
     return np.clip(np.rint(img), 0, 255).astype(np.uint8)
 
 
+def synthetic_stream(n: int, width: int, height: int, seed0: int, noise_sigma: float = 4.0,
+                     margin=(256, 128)) -> np.ndarray:
+    """A camera panning over one static scene (SURVEY.md 8d image spec at every frame): the scene
+    is a (width + mx) x (height + my) image with the 640x480 rectangle density (300 per 640x480),
+    frame i the crop at a smooth offset (2-4 px right, 0-1 px down per frame, bouncing inside the
+    margin) plus fresh N(0, noise_sigma) noise. Consecutive frames share most corners, and every
+    frame has the same statistics (noise does not accumulate along the stream)."""
+    mx, my = margin
+    W, H = width + mx, height + my
+    n_rect = int(round(300 * (W * H) / (640 * 480)))
+    world = synthetic_frame(seed0, W, H, n_rect=n_rect, noise_sigma=0.0).astype(np.float64)
+    rng = np.random.Generator(np.random.PCG64(seed0 + 1))
+    out = np.empty((n, height, width), np.uint8)
+    ox = oy = 0
+    for i in range(n):
+        img = world[oy:oy + height, ox:ox + width] + rng.normal(0.0, noise_sigma, size=(height, width))
+        out[i] = np.clip(np.rint(img), 0, 255).astype(np.uint8)
+        ox += 2 + (i % 3)
+        oy += i % 2
+        if ox > mx:
+            ox = ox % (mx + 1)
+        if oy > my:
+            oy = oy % (my + 1)
+    return out
+
+
 # ---------------------------------------------------------------------------
 # Bundle-adjustment problems (SURVEY.md §8(d) C4 / C5)
 # ---------------------------------------------------------------------------
