@@ -301,6 +301,7 @@ constexpr int kInitCells = kGridCols * kGridRows;   // 3072
 constexpr int kThLow = 50;
 constexpr int kInitK = 16;   // smallest list entries per query handed to the chain
 constexpr int kInitR = 4;    // ring of 4-query blocks in flight in the chain
+constexpr int kInitMaxRounds = 64;   // parallel rounds before the chain takes over
 
 // min over the wave, every lane gets it
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
@@ -329,7 +330,8 @@ __device__ __forceinline__ int init_cell(const InitGeom& g, float x, float y) { 
 // counts[0] = queries (F1 octave 0), counts[1] = ranked F2 keypoints, counts[2] = nmatches
 __global__ __launch_bounds__(1024) void k_init_prep(InitGeom g, const orbhip_kp* __restrict__ kps1,
                                                     const orbhip_kp* __restrict__ kps2, int* __restrict__ slot,
-                                                    int* __restrict__ qlist, int* __restrict__ counts) {
+                                                    int* __restrict__ qlist, int* __restrict__ counts,
+                                                    int* __restrict__ cnt3, int* __restrict__ flags, int nflags) {
     __shared__ int cnt[kInitCells], start[kInitCells], scratch[20], tot;
     const int tid = threadIdx.x, nt = blockDim.x;
     for (int c = tid; c < kInitCells; c += nt) cnt[c] = 0;
@@ -380,6 +382,9 @@ __global__ __launch_bounds__(1024) void k_init_prep(InitGeom g, const orbhip_kp*
         run += total;
     }
     if (tid == 0) { counts[0] = run; counts[1] = tot; }
+    // the parallel rounds' first two claim tables and flags start empty
+    for (int k = tid; k < 2 * tot; k += nt) cnt3[k] = 0;
+    for (int k = tid; k < nflags; k += nt) flags[k] = 0;
 }
 
 // one wave per query slot: the candidate list of GetFeaturesInArea(prev[i1], r, 0, 0)
@@ -640,6 +645,162 @@ __global__ __launch_bounds__(256) void k_init_greedy(InitGeom g, float nnratio, 
     if (tid == 0) *nmatch = cnt;
 }
 
+// ---------------------------------------------------------------------------
+// The same greedy pass as a parallel fixed point. Round r recomputes every query's pick from the
+// picks of round r - 1: query q's vMatchedDistance of rank k is the smallest distance among the
+// earlier queries (j < q) that picked k in round r - 1 (in the sequential pass each later claimant
+// is strictly closer, so the last write is the minimum). Query 0 is right in round 0, and a query
+// is right once every earlier one was right a round before, so a round that changes nothing ends
+// at the sequential result. The claims of a round go to a per-rank table (kInitC slots of
+// q << 9 | dist); three tables rotate (read r, fill r + 1, clear r + 2), as in k_proj_round. A
+// rank with more than kInitC claimants in one round sets the overflow flag and the host runs the
+// chain kernel instead. The 16-lane row of a query holds its 16 smallest entries; the selection
+// is the chain's (first two eligible bits, or the whole-list scan reduced within the row).
+// flags[0] = overflow, flags[1 + r] = "round r changed a pick".
+// ---------------------------------------------------------------------------
+constexpr int kInitC = 8;
+
+__device__ __forceinline__ int init_md(const int* __restrict__ cnt, const uint32_t* __restrict__ ent, int rk, int q) {
+    const int c = min(cnt[rk], kInitC);
+    int md = INT_MAX;
+    for (int t = 0; t < c; t++) {
+        const uint32_t e = ent[(size_t)rk * kInitC + t];
+        md = (int)(e >> 9) < q ? min(md, (int)(e & 511)) : md;
+    }
+    return md;
+}
+
+__global__ __launch_bounds__(256) void k_init_round(InitGeom g, float nnratio, int r, const int* __restrict__ counts,
+                                                    const uint32_t* __restrict__ lists, const int* __restrict__ lens,
+                                                    const uint32_t* __restrict__ topk, const int* __restrict__ need,
+                                                    int* __restrict__ cnt3, uint32_t* __restrict__ ent3,
+                                                    uint32_t* __restrict__ pick, int* __restrict__ flags) {
+    if (flags[0] || (r > 0 && flags[r] == 0)) return;   // overflow, or converged a round ago
+    const int nq = counts[0], nr = counts[1];
+    const int* cc = cnt3 + (size_t)(r % 3) * nr;
+    const uint32_t* ec = ent3 + (size_t)(r % 3) * nr * kInitC;
+    int* cn = cnt3 + (size_t)((r + 1) % 3) * nr;
+    uint32_t* en = ent3 + (size_t)((r + 1) % 3) * nr * kInitC;
+    int* cz = cnt3 + (size_t)((r + 2) % 3) * nr;
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nr; k += gridDim.x * blockDim.x) cz[k] = 0;
+
+    const int lane = threadIdx.x & 63, row = lane >> 4, e = lane & 15;
+    const int q = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 + row;
+    const bool qv = q < nq;
+    const uint32_t v = qv ? topk[(size_t)q * kInitK + e] : ~0u;
+    const int nd = qv ? need[q] : 0;
+    const int md = v != ~0u ? init_md(cc, ec, (int)((v >> 5) & 0xFFFF), q) : INT_MAX;
+    const bool elig = v != ~0u && (int)(v >> 21) < md;
+    const uint32_t mask = (uint32_t)(__ballot(elig) >> (16 * row)) & 0xFFFFu;
+    const uint32_t rest = mask & (mask - 1);
+    // first two eligible entries of the row (all lanes shuffle, so no source lane is inactive)
+    const uint32_t a = (uint32_t)__shfl((int)v, 16 * row + (mask ? __ffs(mask) - 1 : 0));
+    const uint32_t b = (uint32_t)__shfl((int)v, 16 * row + (rest ? __ffs(rest) - 1 : 0));
+    const bool full = qv && (nd == 2 || (nd == 1 && __popc(mask) < 2));
+    uint32_t f1 = ~0u, f2 = ~0u;
+    if (full) {   // whole list, 16 lanes of the row
+        const int lc = lens[q];
+        const uint32_t* lq = lists + (size_t)q * g.list_cap;
+        for (int t = e; t < lc; t += 16) {
+            const uint32_t w0 = lq[t];
+            const uint32_t w = (int)(w0 >> 21) < init_md(cc, ec, (int)((w0 >> 5) & 0xFFFF), q) ? w0 : ~0u;
+            f2 = min(f2, max(f1, w));
+            f1 = min(f1, w);
+        }
+    }
+    // top-2 within each 16-lane row (rows that did not scan reduce ~0u)
+    top2_dpp<0xB1>(f1, f2);
+    top2_dpp<0x4E>(f1, f2);
+    top2_dpp<0x141>(f1, f2);
+    top2_dpp<0x140>(f1, f2);
+    const uint32_t m1 = full ? f1 : (mask ? a : ~0u);
+    const uint32_t m2 = full ? f2 : (rest ? b : ~0u);
+    uint32_t np = ~0u;
+    if (m1 != ~0u) {
+        const int d1 = (int)(m1 >> 21);
+        const int d2 = m2 == ~0u ? INT_MAX : (int)(m2 >> 21);
+        if (d1 <= kThLow && (float)d1 < (float)d2 * nnratio) np = m1;
+    }
+    if (qv && e == 0) {
+        const uint32_t was = r == 0 ? ~0u : pick[q];   // round 0 starts from "no picks"
+        if (r == 0 || was != np) pick[q] = np;
+        if (was != np) flags[1 + r] = 1;
+        if (np != ~0u) {
+            const int rk = (int)((np >> 5) & 0xFFFF);
+            const int s = atomicAdd(&cn[rk], 1);
+            if (s < kInitC) en[(size_t)rk * kInitC + s] = ((uint32_t)q << 9) | (np >> 21);
+            else flags[0] = 1;
+        }
+    }
+}
+
+// Applies converged picks: the last claimant of each rank keeps it (the steals), the rotation
+// histogram counts every pick, as k_init_greedy. Writes matches12 and prev_out for all of F1 (so
+// a finish over a not yet converged round, which the host discards, leaves nothing behind).
+__global__ __launch_bounds__(1024) void k_init_finish(InitGeom g, int check_orientation, const orbhip_kp* __restrict__ kps2,
+                                                      const int* __restrict__ slot, const int* __restrict__ qlist,
+                                                      const int* __restrict__ counts, const uint32_t* __restrict__ pick,
+                                                      const float* __restrict__ prev_in, int32_t* __restrict__ matches12,
+                                                      float* __restrict__ prev_out, int* __restrict__ nmatch) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ int hist[32], keep[3], cnt;
+    int* owner = (int*)smem;
+    const int nq = counts[0], nr = counts[1];
+    const int tid = threadIdx.x, nt = blockDim.x;
+    for (int k = tid; k < nr; k += nt) owner[k] = -1;
+    for (int i = tid; i < g.n1; i += nt) {
+        matches12[i] = -1;
+        prev_out[2 * i] = prev_in[2 * i];
+        prev_out[2 * i + 1] = prev_in[2 * i + 1];
+    }
+    if (tid < 32) hist[tid] = 0;
+    if (tid == 0) cnt = 0;
+    __syncthreads();
+    for (int q = tid; q < nq; q += nt) {
+        const uint32_t p = pick[q];
+        if (p != ~0u) {
+            atomicMax(&owner[(p >> 5) & 0xFFFF], q);
+            if (check_orientation) atomicAdd(&hist[p & 31], 1);
+        }
+    }
+    __syncthreads();
+    if (check_orientation) {
+        if (tid == 0) {   // ComputeThreeMaxima
+            int m1 = 0, m2 = 0, m3 = 0, i1 = -1, i2 = -1, i3 = -1;
+            for (int b = 0; b < kHisto; b++) {
+                const int s = hist[b];
+                if (s > m1) { m3 = m2; m2 = m1; m1 = s; i3 = i2; i2 = i1; i1 = b; }
+                else if (s > m2) { m3 = m2; m2 = s; i3 = i2; i2 = b; }
+                else if (s > m3) { m3 = s; i3 = b; }
+            }
+            if (m2 < 0.1f * (float)m1) { i2 = -1; i3 = -1; }
+            else if (m3 < 0.1f * (float)m1) { i3 = -1; }
+            keep[0] = i1; keep[1] = i2; keep[2] = i3;
+        }
+        __syncthreads();
+    }
+    int c = 0;
+    for (int q = tid; q < nq; q += nt) {
+        const uint32_t p = pick[q];
+        int rk = p == ~0u ? -1 : (int)((p >> 5) & 0xFFFF);
+        if (rk >= 0 && owner[rk] != q) rk = -1;   // stolen by a later query
+        if (rk >= 0 && check_orientation) {
+            const int b = (int)(p & 31);
+            if (b != keep[0] && b != keep[1] && b != keep[2]) rk = -1;
+        }
+        if (rk >= 0) {
+            const int i1 = qlist[q], k = slot[rk];
+            matches12[i1] = k;
+            prev_out[2 * i1] = kps2[k].x;
+            prev_out[2 * i1 + 1] = kps2[k].y;
+            c++;
+        }
+    }
+    atomicAdd(&cnt, c);
+    __syncthreads();
+    if (tid == 0) *nmatch = cnt;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -651,6 +812,7 @@ struct ProjWorkspace {
     void* h = nullptr;
     size_t hcap = 0;
     int ahead = 4;   // rounds launched per host sync (adapts to the last search)
+    int init_ahead = 6;   // the same for SearchForInitialization's rounds
     ~ProjWorkspace() {
         if (d) (void)hipFree(d);
         if (h) (void)hipHostFree(h);
@@ -904,6 +1066,9 @@ int init_search(ProjWorkspace* ws, const orbhip_init_frame* F1, const orbhip_ini
     static const hipError_t attr = hipFuncSetAttribute((const void*)k_init_greedy,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024);
     PJOK(attr);
+    static const hipError_t attr_f = hipFuncSetAttribute((const void*)k_init_finish,
+                                                         hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024);
+    PJOK(attr_f);
     Layout lay;
     const size_t o_k1 = lay.add(sizeof(orbhip_kp) * n1), o_d1 = lay.add(32 * (size_t)n1);
     const size_t o_k2 = lay.add(sizeof(orbhip_kp) * std::max(n2, 1)), o_d2 = lay.add(32 * (size_t)std::max(n2, 1));
@@ -913,6 +1078,12 @@ int init_search(ProjWorkspace* ws, const orbhip_init_frame* F1, const orbhip_ini
     const size_t o_len = lay.add(4 * ((size_t)n1 + 1)), o_list = lay.add(4 * (size_t)std::max(nq0, 1) * list_cap);
     const size_t o_topk = lay.add(4 * (size_t)kInitK * (((size_t)std::max(nq0, 1) + 3) & ~size_t(3)));
     const size_t o_need = lay.add(4 * (size_t)std::max(nq0, 1));
+    const int cap = std::min(kInitMaxRounds, nq0 + 2);
+    const size_t o_cnt3 = lay.add(4 * 3 * (size_t)std::max(nr0, 1));
+    const size_t o_ent3 = lay.add(4 * 3 * (size_t)std::max(nr0, 1) * kInitC);
+    const size_t o_pick = lay.add(4 * (size_t)std::max(nq0, 1));
+    const size_t o_pout = lay.add(8 * (size_t)n1);
+    const size_t o_flags = lay.add(4 * ((size_t)cap + 1));
     if (int rc = ensure(ws, lay.off)) return rc;
     char* H = (char*)ws->h;
     char* D = (char*)ws->d;
@@ -934,12 +1105,48 @@ int init_search(ProjWorkspace* ws, const orbhip_init_frame* F1, const orbhip_ini
     const orbhip_kp* dk1 = (const orbhip_kp*)(D + o_k1);
     const orbhip_kp* dk2 = (const orbhip_kp*)(D + o_k2);
     int* counts = (int*)(D + o_cnt);
+    int* flags = (int*)(D + o_flags);
     hipLaunchKernelGGL(k_init_prep, dim3(1), dim3(1024), 0, st, g, dk1, dk2, (int*)(D + o_slot), (int*)(D + o_ql),
-                       counts);
+                       counts, (int*)(D + o_cnt3), flags, cap + 1);
     hipLaunchKernelGGL(k_init_cands, dim3((unsigned)std::max(1, (nq0 + 3) / 4)), dim3(256), 0, st, g, dk1,
                        (const uint8_t*)(D + o_d1), dk2, (const uint8_t*)(D + o_d2), (const float*)(D + o_prev),
                        (const int*)(D + o_slot), (const int*)(D + o_ql), (const int*)counts, (uint32_t*)(D + o_list),
                        (int*)(D + o_len), (uint32_t*)(D + o_topk), (int*)(D + o_need));
+    PJOK(hipGetLastError());
+    // parallel rounds, launched init_ahead at a time with the finish and the read-back behind them
+    const int* hflags = (const int*)(H + o_flags);
+    const dim3 gq((unsigned)std::max(1, (nq0 + 15) / 16));
+    bool done = false;
+    for (int r = 0; r < cap && !done && std::getenv("ORBHIP_INIT_CHAIN") == nullptr;) {
+        const int R = std::min(ws->init_ahead, cap - r);
+        for (int j = 0; j < R; j++)
+            hipLaunchKernelGGL(k_init_round, gq, dim3(256), 0, st, g, nnratio, r + j, (const int*)counts,
+                               (const uint32_t*)(D + o_list), (const int*)(D + o_len),
+                               (const uint32_t*)(D + o_topk), (const int*)(D + o_need), (int*)(D + o_cnt3),
+                               (uint32_t*)(D + o_ent3), (uint32_t*)(D + o_pick), flags);
+        hipLaunchKernelGGL(k_init_finish, dim3(1), dim3(1024), 4 * (size_t)std::max(nr0, 1), st, g,
+                           check_orientation, dk2, (const int*)(D + o_slot), (const int*)(D + o_ql),
+                           (const int*)counts, (const uint32_t*)(D + o_pick), (const float*)(D + o_prev),
+                           (int32_t*)(D + o_match), (float*)(D + o_pout), counts + 2);
+        PJOK(hipGetLastError());
+        PJOK(hipMemcpyAsync(H + o_match, D + o_match, o_out_end - o_match, hipMemcpyDeviceToHost, st));
+        PJOK(hipMemcpyAsync(H + o_pout, D + o_pout, 8 * (size_t)n1, hipMemcpyDeviceToHost, st));
+        PJOK(hipMemcpyAsync(H + o_flags, flags, 4 * ((size_t)cap + 1), hipMemcpyDeviceToHost, st));
+        PJOK(hipStreamSynchronize(st));
+        if (hflags[0]) break;   // a rank overflowed its claim slots: the chain decides
+        for (int j = 0; j < R && !done; j++)
+            if (hflags[1 + r + j] == 0) {
+                done = true;
+                ws->init_ahead = std::min(16, std::max(3, r + j + 2));
+            }
+        r += R;
+        if (!done) ws->init_ahead = std::min(16, 2 * ws->init_ahead);
+    }
+    if (done) {
+        std::memcpy(matches12, H + o_match, 4 * (size_t)n1);
+        std::memcpy(prev_matched, H + o_pout, 8 * (size_t)n1);
+        return ((int*)(H + o_cnt))[2];
+    }
     hipLaunchKernelGGL(k_init_greedy, dim3(1), dim3(256), lds, st, g, nnratio, check_orientation, dk2,
                        (const int*)(D + o_slot), (const int*)(D + o_ql), (const int*)counts,
                        (const uint32_t*)(D + o_list), (const int*)(D + o_len), (const uint32_t*)(D + o_topk),

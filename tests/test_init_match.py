@@ -127,8 +127,13 @@ def test_oracle_identical_frames_match_themselves(oracle):
 
 
 @pytest.mark.gpu
-def test_search_for_initialization_matches_oracle(oracle):
+@pytest.mark.parametrize("path", ["rounds", "chain"])
+def test_search_for_initialization_matches_oracle(oracle, monkeypatch, path):
+    """Both device formulations: the parallel fixed-point rounds (default) and the one-wave chain
+    (ORBHIP_INIT_CHAIN, also the fallback when a rank overflows its claim slots)."""
     from orb_slam3_ros2_amd import ORBmatcher
+    if path == "chain":
+        monkeypatch.setenv("ORBHIP_INIT_CHAIN", "1")
     for seed in range(6):
         k1, d1, k2, d2, prev = synthetic_init_pair(n1=1500 + 500 * seed, seed=20 + seed)
         for window, ratio, ori in [(100, 0.9, True), (100, 0.9, False), (50, 0.7, True), (200, 0.9, True)]:
@@ -164,6 +169,35 @@ def test_search_for_initialization_extracted_frames(oracle):
         on, om, oprev = oracle.search_for_initialization(ks[0], ds[0], ks[j], ds[j], oprev, 100, 0.9, True)
         assert n == on and np.array_equal(m, om) and np.array_equal(prev, oprev), j
         assert n > 100
+
+
+@pytest.mark.gpu
+def test_search_for_initialization_crowded_rank(oracle):
+    """Many queries around one F2 keypoint: round 0 puts them all on one rank (more claimants
+    than the claim slots, so the chain decides), with equal distances (no steal: only the first
+    keeps it) and with strictly decreasing distances (every query steals from the previous)."""
+    from orb_slam3_ros2_amd import ORBmatcher
+    k1, d1, k2, d2, prev = synthetic_init_pair(n1=300, seed=6)
+    k2 = k2[k2["octave"] == 0][:1].copy()
+    d2 = np.zeros((1, 32), np.uint8) + 0x5A
+    assert len(k2) == 1
+    q = np.repeat(k2, 24)
+    q["angle"] = np.linspace(0, 40, 24, dtype=np.float32)
+    p = np.stack([q["x"], q["y"]], 1).astype(np.float32) + 3.0
+    for steal in (False, True):
+        dq = np.repeat(d2, 24, 0)
+        if steal:
+            for i in range(24):      # 30 - i differing bits: each later query is strictly closer
+                bits = np.unpackbits(dq[i])
+                bits[: 30 - i] ^= 1
+                dq[i] = np.packbits(bits)
+        else:
+            dq[:, 0] ^= 0x0F          # distance 4 for everybody
+        mt = ORBmatcher(0.9, True)
+        n, m, pp = mt.SearchForInitialization(q, dq, k2, d2, p, 100)
+        on, om, op = oracle.search_for_initialization(q, dq, k2, d2, p, 100, 0.9, True)
+        assert n == on and np.array_equal(m, om) and np.array_equal(pp, op), steal
+        assert on == 1 and om[-1 if steal else 0] == 0
 
 
 @pytest.mark.gpu
