@@ -140,6 +140,14 @@ int orbhip_match_frames_device(orbhip_ctx* ctx, const orbhip_kp* d_q_kps, const 
 int orbhip_profile_stage(orbhip_ctx* ctx, int stage);
 int orbhip_profile_collect(orbhip_ctx* ctx, double* total_ms, int32_t* count);
 
+/* With ORBHIP_GRAPH=1 in the environment, repeated calls of orbhip_extract_batch_device /
+ * orbhip_match_*_device with identical arguments on a non-NULL stream are replayed from a
+ * captured hipGraph (from the second such call on: one hipGraphLaunch instead of the kernel
+ * launches). Same kernels, same results. Off by default (the replay adds device time on this
+ * runtime); always direct while a profile stage is selected or on a capturing stream.
+ * Returns the number of launch graphs the context holds. */
+int orbhip_launch_graphs(orbhip_ctx* ctx);
+
 /* ---- bundle adjustment ------------------------------------------------------------
  * Optimizer::LocalBundleAdjustment / BundleAdjustment problem (SoA, host memory).
  * Poses are Tcw = (q, t): q = unit quaternion (x, y, z, w), t translation, float, as

@@ -101,7 +101,7 @@ class LocalPointsC(ctypes.Structure):
 EXPORTED = ["orbhip_abi_version", "orbhip_create", "orbhip_destroy", "orbhip_level_info", "orbhip_max_keypoints",
             "orbhip_extract", "orbhip_extract_batch_device", "orbhip_descriptor_distance", "orbhip_match_bf",
             "orbhip_match_pairs_device", "orbhip_match_frames_device", "orbhip_profile_stage",
-            "orbhip_profile_collect", "orbhip_ba_solve", "orbhip_ba_solve_batch", "orbhip_bgr_to_gray_device",
+            "orbhip_profile_collect", "orbhip_launch_graphs", "orbhip_ba_solve", "orbhip_ba_solve_batch", "orbhip_bgr_to_gray_device",
             "orbhip_comm_unique_id", "orbhip_comm_init", "orbhip_ba_solve_sharded", "orbhip_ba_solve_shards_local",
             "orbhip_vocab_create", "orbhip_vocab_load_text", "orbhip_vocab_destroy", "orbhip_vocab_info",
             "orbhip_bow_transform", "orbhip_bow_transform_device", "orbhip_search_bow",
@@ -155,6 +155,7 @@ def lib():
     L.orbhip_bgr_to_gray_device.argtypes = [vp, vp, i32, i32, i32, i32, ctypes.c_int64, vp, i32, ctypes.c_int64, vp]
     L.orbhip_profile_stage.argtypes = [vp, i32]
     L.orbhip_profile_collect.argtypes = [vp, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)]
+    L.orbhip_launch_graphs.argtypes = [vp]
     L.orbhip_ba_solve.argtypes = [vp, ctypes.POINTER(BAProblemC), ctypes.POINTER(BAResultC), vp]
     L.orbhip_ba_solve_batch.argtypes = [vp, ctypes.POINTER(BAProblemC), i32, ctypes.POINTER(BAResultC), vp]
     L.orbhip_pose_optimization.argtypes = [vp, ctypes.POINTER(PoseProblemC), ctypes.POINTER(PoseResultC)]

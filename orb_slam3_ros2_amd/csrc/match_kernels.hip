@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "orbhip_device.h"
 #include "orbhip_kernels.h"
@@ -38,6 +39,7 @@ struct MatchView {
 
 constexpr int kTC = 256;     // train descriptors per workgroup chunk (64 per wave): batches
 constexpr int kTCSmall = 64; // 16 per wave: one pair (C2), where 256-chunks leave the chip idle
+constexpr int kFusedMaxPairs = 4;   // k_match_fused up to this many pairs (the sync scratch holds 64 ints each)
 
 __device__ __forceinline__ void top2_merge(int& b, int& i, int& s, int b2, int i2, int s2) {
     const int nb = (b2 < b || (b2 == b && i2 < i)) ? b2 : b;
@@ -247,6 +249,179 @@ __global__ __launch_bounds__(1024) void k_match_finish(MatchView v, const uint2*
     TR_END(5)
 }
 
+// ---------------------------------------------------------------------------
+// k_match_fused: the whole matcher in one launch, for a few pairs (C2: one frame pair). A
+// workgroup takes 16 queries against the pair's whole train set: lane (query = tid & 15,
+// slice = tid >> 4) scans trains slice, slice + 64, ... of each 1024-descriptor LDS chunk in
+// index order (strict <), the 64 slices merge lexicographically (shuffles inside the wave, then
+// 16 wave partials in LDS), so every query's (best, index, second) is final inside its workgroup
+// and no chunk partials travel between workgroups. TH_LOW + ratio and the rotation bin follow
+// at once (train angles staged in LDS with the first chunk). The last workgroup of the pair
+// takes ComputeThreeMaxima of the pair's histogram, filters every query and writes the count.
+//
+// Cross-workgroup hand-off without an agent-scope fence: on gfx950 a release fence at agent
+// scope is a buffer_wbl2 of the whole XCD L2 (~14 us measured here, the L2 still holds the
+// pyramid), so everything another workgroup reads goes through device-coherent atomics instead
+// (tentative matches by atomicExch, histogram and count by atomicAdd), a vmcnt(0) wait orders
+// them before the done-counter increment, and the last workgroup reads them back by atomics.
+// sync: 64 ints per pair, zero before the first launch: [0] done counter, [1..30] histogram,
+// [31] match count; the last workgroup resets them.
+// ---------------------------------------------------------------------------
+constexpr int kFQ = 16, kFChunk = 1024;
+
+__device__ __forceinline__ void wait_vm_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__global__ __launch_bounds__(1024) void k_match_fused(MatchView v, int th_low, float ratio, int check_orientation,
+                                                       int32_t* __restrict__ match, int32_t* __restrict__ best_out,
+                                                       int32_t* __restrict__ second_out, int32_t* __restrict__ nmatch,
+                                                       int* __restrict__ sync) {
+    __shared__ __attribute__((aligned(16))) uint4 tile[kFChunk * 2];
+    __shared__ float tang[kFChunk];
+    __shared__ int rb[16][kFQ], ri[16][kFQ], rs[16][kFQ];
+    __shared__ int hist[32], keep[3], cnt, last;
+    TR_BEGIN()
+    const int p = blockIdx.y;
+    const int nq = v.nq_arr ? v.nq_arr[p] : v.nq;
+    const int nt = v.nt_arr ? v.nt_arr[p] : v.nt;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int active = (nq + kFQ - 1) / kFQ;
+    int* ps = sync + 64 * p;
+    if (nq <= 0) {
+        if (blockIdx.x == 0 && tid == 0) nmatch[p] = 0;
+        return;
+    }
+    if ((int)blockIdx.x >= active) return;   // workgroup-uniform
+    const int ql = tid & (kFQ - 1), slice = tid >> 4;
+    const int q = blockIdx.x * kFQ + ql;
+    const float* qa_p = v.qa + (int64_t)p * v.pair_angle_stride;
+    const float* ta_p = v.ta + (int64_t)p * v.pair_angle_stride;
+    const uint4* src = (const uint4*)(v.td + (int64_t)p * v.pair_desc_stride);
+    const bool tang_lds = nt <= kFChunk;
+    // every global read of the prologue in flight at once (the descriptors were written by other
+    // XCDs a kernel ago: one memory round trip, not four)
+    const int tn0 = min(kFChunk, nt);
+    uint4 t0 = make_uint4(0, 0, 0, 0), t1 = t0;
+    if (tid < tn0 * 2) t0 = src[tid];
+    if (tid + 1024 < tn0 * 2) t1 = src[tid + 1024];
+    uint4 qa = make_uint4(0, 0, 0, 0), qb = qa;
+    float aq = 0.f, at = 0.f;
+    if (q < nq) {
+        const uint4* qp = (const uint4*)(v.qd + (int64_t)p * v.pair_desc_stride + (int64_t)q * 32);
+        qa = qp[0];
+        qb = qp[1];
+        if (tid < kFQ) aq = qa_p[(int64_t)q * v.angle_stride];
+    }
+    if (tang_lds && tid < nt) at = ta_p[(int64_t)tid * v.angle_stride];
+    if (tid < 32) hist[tid] = 0;
+    if (tid == 0) cnt = 0;
+    if (tid < tn0 * 2) tile[tid] = t0;
+    if (tid + 1024 < tn0 * 2) tile[tid + 1024] = t1;
+    if (tang_lds && tid < nt) tang[tid] = at;
+    int b = 256, bi = 0x7fffffff, s = 256;
+    TR_PHASE(5, 6)
+    for (int c0 = 0; c0 < nt; c0 += kFChunk) {
+        const int tn = min(kFChunk, nt - c0);
+        if (c0) {
+            __syncthreads();   // the previous chunk is read
+            for (int i = tid; i < tn * 2; i += 1024) tile[i] = src[(int64_t)c0 * 2 + i];
+        }
+        __syncthreads();
+        for (int t = slice; t < tn; t += 64) {
+            const uint4 x = tile[2 * t], y = tile[2 * t + 1];
+            const int d = __popc(x.x ^ qa.x) + __popc(x.y ^ qa.y) + __popc(x.z ^ qa.z) + __popc(x.w ^ qa.w) +
+                          __popc(y.x ^ qb.x) + __popc(y.y ^ qb.y) + __popc(y.z ^ qb.z) + __popc(y.w ^ qb.w);
+            if (d < b) { s = b; b = d; bi = c0 + t; }
+            else if (d < s) s = d;
+        }
+    }
+    TR_PHASE(5, 2)
+    // slices 4w .. 4w+3 of a query sit in lanes ql, ql+16, ql+32, ql+48 of wave w
+#pragma unroll
+    for (int o = 16; o <= 32; o <<= 1) {
+        const int b2 = __shfl_xor(b, o, 64), i2 = __shfl_xor(bi, o, 64), s2 = __shfl_xor(s, o, 64);
+        top2_merge(b, bi, s, b2, i2, s2);
+    }
+    if (lane < kFQ) { rb[wid][lane] = b; ri[wid][lane] = bi; rs[wid][lane] = s; }
+    __syncthreads();
+    if (tid < 64) {
+        // wave 0: lane ql + 16k merges waves k, k+4, k+8, k+12; then the four lanes of a query
+        const int k = lane >> 4;
+        b = rb[k][ql]; bi = ri[k][ql]; s = rs[k][ql];
+#pragma unroll
+        for (int w = k + 4; w < 16; w += 4) top2_merge(b, bi, s, rb[w][ql], ri[w][ql], rs[w][ql]);
+#pragma unroll
+        for (int o = 16; o <= 32; o <<= 1) {
+            const int b2 = __shfl_xor(b, o, 64), i2 = __shfl_xor(bi, o, 64), s2 = __shfl_xor(s, o, 64);
+            top2_merge(b, bi, s, b2, i2, s2);
+        }
+    }
+    if (tid < kFQ) {
+        if (q < nq) {
+            const bool ok = b < 256 && b <= th_low && (float)b < ratio * (float)s;
+            const int64_t o = (int64_t)p * v.out_stride + q;
+            best_out[o] = b;
+            second_out[o] = s;
+            int mt = ok ? bi : -1;
+            if (ok && check_orientation) {
+                float rot = aq - (tang_lds ? tang[bi] : ta_p[(int64_t)bi * v.angle_stride]);
+                if (rot < 0.0) rot += 360.0f;
+                int bin = (int)roundf(rot * (1.0f / 30));
+                if (bin == 30) bin = 0;
+                atomicAdd(&hist[bin], 1);
+                mt |= bin << 24;   // tentative: the last workgroup filters
+                (void)atomicExch(&match[o], mt);
+            } else {
+                match[o] = mt;     // final (no filter reads it)
+            }
+            if (ok) atomicAdd(&cnt, 1);
+        }
+    }
+    __syncthreads();
+    TR_PHASE(5, 3)
+    if (tid < 30 && hist[tid]) atomicAdd(&ps[1 + tid], hist[tid]);
+    if (tid == 0 && cnt) atomicAdd(&ps[31], cnt);
+    wait_vm_all();      // this thread's device atomics are performed
+    __syncthreads();    // ... for every thread of the workgroup
+    if (tid == 0) last = atomicAdd(&ps[0], 1) == active - 1;
+    __syncthreads();
+    TR_PHASE(5, 0)
+    if (!last) {
+        TR_END(5)
+        return;
+    }
+    if (!check_orientation) {
+        if (tid == 0) {
+            nmatch[p] = atomicExch(&ps[31], 0);
+            (void)atomicExch(&ps[0], 0);
+        }
+        return;
+    }
+    if (tid < 30) hist[tid] = atomicAdd(&ps[1 + tid], 0);
+    if (tid == 0) cnt = 0;
+    __syncthreads();
+    if (tid < 64) three_maxima_wave(hist, keep);
+    __syncthreads();
+    int c = 0;
+    for (int qq = tid; qq < nq; qq += 1024) {
+        const int64_t o = (int64_t)p * v.out_stride + qq;
+        int mt = atomicAdd(&match[o], 0);
+        if (mt >= 0) {
+            const int bin = mt >> 24;
+            mt &= 0xFFFFFF;
+            if (bin != keep[0] && bin != keep[1] && bin != keep[2]) mt = -1;
+            match[o] = mt;
+            c += mt >= 0;
+        }
+    }
+    c = wave_sum_i32(c);
+    if (lane == 0 && c) atomicAdd(&cnt, c);
+    if (tid < 32) (void)atomicExch(&ps[tid], 0);   // counter + histogram + count for the next launch
+    __syncthreads();
+    if (tid == 0) nmatch[p] = cnt;
+    TR_PHASE(5, 1)
+    TR_END(5)
+}
+
 size_t match_part_entries(int npairs, int max_q, int max_t) {
     const int nch = std::max(1, (max_t + kTCSmall - 1) / kTCSmall);
     return (size_t)std::max(npairs, 1) * nch * std::max(max_q, 1);
@@ -254,8 +429,16 @@ size_t match_part_entries(int npairs, int max_q, int max_t) {
 
 static void run_match(const MatchView& v, int npairs, int max_q, int max_t, int th_low, float ratio,
                       int check_orientation, int32_t* match, int32_t* best, int32_t* second, int32_t* nmatch,
-                      uint2* part, hipStream_t st, StageTimer* timer = nullptr) {
+                      uint2* part, hipStream_t st, StageTimer* timer = nullptr, int* sync = nullptr) {
     if (npairs <= 0) return;
+    const char* unf = std::getenv("ORBHIP_MATCH_UNFUSED");   // A/B switch (read per call: tests flip it)
+    if (sync && npairs <= kFusedMaxPairs && !(unf && unf[0] && unf[0] != '0')) {
+        if (timer) timer->begin(5, st);
+        hipLaunchKernelGGL(k_match_fused, dim3((unsigned)std::max(1, (max_q + kFQ - 1) / kFQ), npairs), dim3(1024),
+                           0, st, v, th_low, ratio, check_orientation, match, best, second, nmatch, sync);
+        if (timer) timer->end(5, st);
+        return;
+    }
     const int qblocks = (max_q + 63) / 64;
     // 16 trains per wave while 64 per wave would leave most of the chip idle (one pair)
     const bool small = (int64_t)npairs * qblocks * ((max_t + kTC - 1) / kTC) < 512;
@@ -277,7 +460,8 @@ static void run_match(const MatchView& v, int npairs, int max_q, int max_t, int 
 
 void launch_match_pairs(const orbhip_kp* kps, const uint8_t* desc, const int32_t* n, int npairs, int cap,
                         int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best,
-                        int32_t* second, int32_t* nmatch, void* part, hipStream_t st, StageTimer* timer) {
+                        int32_t* second, int32_t* nmatch, void* part, hipStream_t st, StageTimer* timer,
+                        int* sync) {
     MatchView v;
     v.qd = desc;
     v.td = desc + (int64_t)cap * 32;
@@ -292,13 +476,13 @@ void launch_match_pairs(const orbhip_kp* kps, const uint8_t* desc, const int32_t
     v.nt = cap;
     v.out_stride = cap;
     run_match(v, npairs, cap, cap, th_low, ratio, check_orientation, match, best, second, nmatch, (uint2*)part, st,
-              timer);
+              timer, sync);
 }
 
 void launch_match_frames(const orbhip_kp* q_kps, const uint8_t* q_desc, const int32_t* nq, const orbhip_kp* t_kps,
                          const uint8_t* t_desc, const int32_t* nt, int cap, int th_low, float ratio,
                          int check_orientation, int32_t* match, int32_t* best, int32_t* second, int32_t* nmatch,
-                         void* part, hipStream_t st, StageTimer* timer) {
+                         void* part, hipStream_t st, StageTimer* timer, int* sync) {
     MatchView v;
     v.qd = q_desc;
     v.td = t_desc;
@@ -312,12 +496,13 @@ void launch_match_frames(const orbhip_kp* q_kps, const uint8_t* q_desc, const in
     v.nq = cap;
     v.nt = cap;
     v.out_stride = 0;
-    run_match(v, 1, cap, cap, th_low, ratio, check_orientation, match, best, second, nmatch, (uint2*)part, st, timer);
+    run_match(v, 1, cap, cap, th_low, ratio, check_orientation, match, best, second, nmatch, (uint2*)part, st, timer,
+              sync);
 }
 
 void launch_match_bf(const uint8_t* q, const float* qa, int nq, const uint8_t* t, const float* ta, int nt,
                      int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best,
-                     int32_t* second, int32_t* nmatch, void* part, hipStream_t st) {
+                     int32_t* second, int32_t* nmatch, void* part, hipStream_t st, int* sync) {
     MatchView v;
     v.qd = q; v.td = t; v.qa = qa; v.ta = ta;
     v.angle_stride = 1;
@@ -326,7 +511,8 @@ void launch_match_bf(const uint8_t* q, const float* qa, int nq, const uint8_t* t
     v.nq_arr = nullptr; v.nt_arr = nullptr;
     v.nq = nq; v.nt = nt;
     v.out_stride = 0;
-    run_match(v, 1, nq, nt, th_low, ratio, check_orientation, match, best, second, nmatch, (uint2*)part, st);
+    run_match(v, 1, nq, nt, th_low, ratio, check_orientation, match, best, second, nmatch, (uint2*)part, st, nullptr,
+              sync);
 }
 
 // ---- test hooks: device glibc sinf/cosf restatement ----

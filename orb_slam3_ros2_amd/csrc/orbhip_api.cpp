@@ -28,6 +28,7 @@
 #include "ba_chol_blocked.h"
 #include "orbhip_kernels.h"
 #include "orbhip_plan.h"
+#include "graph_cache.h"
 
 using namespace orbhip;
 
@@ -97,6 +98,7 @@ struct orbhip_ctx {
     DevBuf<uint16_t> d_nscratch;
     DevBuf<int> d_cand_cnt, d_lvl_cnt, d_lvl_nlap, d_err;
     DevBuf<uint64_t> d_mpart;   // matcher chunk partials (match_part_entries)
+    DevBuf<int> d_msync;        // one-launch matcher counters (zeroed once, reset by every launch)
     DevBuf<double> d_bw;        // bag-of-words weights (host transform)
     DevBuf<uint8_t> d_bow_stage;   // SearchByBoW host-call staging
     DevBuf<LevelKp> d_lvl_kp;
@@ -111,6 +113,7 @@ struct orbhip_ctx {
     PoseWorkspace* pose = nullptr;
     ProjWorkspace* proj = nullptr;
     StageTimer timer;
+    GraphCache graphs;   // replays of repeated per-frame launch sequences (graph_cache.h)
 };
 
 // ---------------------------------------------------------------------------
@@ -446,37 +449,46 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
     (void)hipGetLastError();   // clear a sticky error of an earlier, already-reported call
     int rc = ensure_batch(c, pl, B);
     if (rc) return rc;
-    FrameBufs fb;
-    fb.in = d_imgs; fb.in_stride = stride; fb.in_fstride = fstride; fb.pyr = c->d_pyr.p;
-    StageTimer& tm = c->timer;
-    tm.begin(1, st);
-    static const bool no_cone = std::getenv("ORBHIP_NO_CONE") != nullptr;   // A/B switch for the cascade
-    // the cone recomputes each tile's halo on every level: it pays only while the per-level cascade
-    // is launch-latency bound (a few work-groups per CU); big batches keep the cascade
-    static const size_t cone_max = std::getenv("ORBHIP_CONE_MAX_WG") ? (size_t)std::atol(std::getenv("ORBHIP_CONE_MAX_WG"))
-                                                                      : (size_t)1024;
-    if (pl->cone_tiles && !no_cone && (size_t)B * pl->cone_tiles <= cone_max)
-        launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_cone_tab.p,
-                        pl->cone_tab_stride, st);
-    else
-        for (int l = 1; l < P.n_levels; l++)
-            launch_resize(pl->d_plan.p, P, fb, B, l, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p, pl->d_ybeta.p, st);
-    tm.end(1, st);
-    tm.begin(2, st);
-    launch_fast(pl->d_plan.p, P, pl->d_cells.p, fb, B, c->d_cand.p, c->d_cand_cnt.p, c->d_err.p, st);
-    tm.end(2, st);
-    OctreeCfg oc = pl->oct;
-    oc.lap0 = lap0; oc.lap1 = lap1;
-    tm.begin(3, st);
-    launch_octree(pl->d_plan.p, P, pl->d_cells.p, c->d_cand.p, c->d_cand_cnt.p, c->d_kscratch.p, c->d_nscratch.p,
-                  c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, oc, c->d_err.p, B, st);
-    tm.end(3, st);
-    tm.begin(4, st);
-    launch_desc(pl->d_plan.p, P, fb, c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, pl->d_disc.p, d_kps, d_desc, cap,
-                d_n, d_mono, B, st);
-    tm.end(4, st);
-    HIPOK(hipGetLastError());
-    return ORBHIP_OK;
+    GraphKey key;
+    key.add(1).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
+        .add((uint64_t)lap1).ptr(d_kps).ptr(d_desc).add((uint64_t)cap).ptr(d_n).ptr(d_mono).ptr(st).ptr(c->d_pyr.p)
+        .ptr(c->d_cand.p).ptr(c->d_kscratch.p).ptr(c->d_nscratch.p).ptr(c->d_cand_cnt.p).ptr(c->d_lvl_kp.p)
+        .ptr(c->d_lvl_cnt.p).ptr(c->d_lvl_nlap.p).ptr(c->d_err.p);
+    return c->graphs.run(key, st, c->timer.stage != 0, [&](hipStream_t st) -> int {
+        FrameBufs fb;
+        fb.in = d_imgs; fb.in_stride = stride; fb.in_fstride = fstride; fb.pyr = c->d_pyr.p;
+        StageTimer& tm = c->timer;
+        tm.begin(1, st);
+        static const bool no_cone = std::getenv("ORBHIP_NO_CONE") != nullptr;   // A/B switch for the cascade
+        // the cone recomputes each tile's halo on every level: it pays only while the per-level
+        // cascade is launch-latency bound (a few work-groups per CU); big batches keep the cascade
+        static const size_t cone_max = std::getenv("ORBHIP_CONE_MAX_WG")
+                                           ? (size_t)std::atol(std::getenv("ORBHIP_CONE_MAX_WG"))
+                                           : (size_t)1024;
+        if (pl->cone_tiles && !no_cone && (size_t)B * pl->cone_tiles <= cone_max)
+            launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_cone_tab.p,
+                            pl->cone_tab_stride, st);
+        else
+            for (int l = 1; l < P.n_levels; l++)
+                launch_resize(pl->d_plan.p, P, fb, B, l, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p, pl->d_ybeta.p,
+                              st);
+        tm.end(1, st);
+        tm.begin(2, st);
+        launch_fast(pl->d_plan.p, P, pl->d_cells.p, fb, B, c->d_cand.p, c->d_cand_cnt.p, c->d_err.p, st);
+        tm.end(2, st);
+        OctreeCfg oc = pl->oct;
+        oc.lap0 = lap0; oc.lap1 = lap1;
+        tm.begin(3, st);
+        launch_octree(pl->d_plan.p, P, pl->d_cells.p, c->d_cand.p, c->d_cand_cnt.p, c->d_kscratch.p, c->d_nscratch.p,
+                      c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, oc, c->d_err.p, B, st);
+        tm.end(3, st);
+        tm.begin(4, st);
+        launch_desc(pl->d_plan.p, P, fb, c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, pl->d_disc.p, d_kps, d_desc,
+                    cap, d_n, d_mono, B, st);
+        tm.end(4, st);
+        HIPOK(hipGetLastError());
+        return ORBHIP_OK;
+    });
 }
 
 // ===========================================================================
@@ -524,6 +536,8 @@ int orbhip_destroy(orbhip_ctx* c) {
     if (!c) return ORBHIP_ERR_ARG;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->graphs.graphs()) (void)hipDeviceSynchronize();   // replays may run on caller streams
+    c->graphs.clear();
     if (c->timer.created)
         for (int i = 0; i < 2 * StageTimer::kCap; i++) (void)hipEventDestroy(c->timer.ev[i]);
     ba_destroy(c->ba);
@@ -619,6 +633,14 @@ int orbhip_descriptor_distance(const uint8_t* a, const uint8_t* b) {
     return d;
 }
 
+// the one-launch matcher's counters: zeroed on the call's stream before their first use
+static int ensure_msync(orbhip_ctx* c, hipStream_t st) {
+    if (c->d_msync.p) return ORBHIP_OK;
+    HIPOK(c->d_msync.ensure(kMatchSyncInts));
+    HIPOK(hipMemsetAsync(c->d_msync.p, 0, sizeof(int) * kMatchSyncInts, st));
+    return ORBHIP_OK;
+}
+
 int orbhip_match_bf(orbhip_ctx* c, const uint8_t* q, const float* qa, int nq, const uint8_t* t, const float* ta,
                     int nt, int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best_d,
                     int32_t* second_d) {
@@ -645,9 +667,10 @@ int orbhip_match_bf(orbhip_ctx* c, const uint8_t* q, const float* qa, int nq, co
         HIPOK(hipMemsetAsync(c->d_mm.p, 0xFF, (size_t)nq * 4, st));
     }
     HIPOK(c->d_mpart.ensure(match_part_entries(1, nq, nt)));
+    if (int rc = ensure_msync(c, st)) return rc;
     (void)hipGetLastError();
     launch_match_bf(c->d_mq.p, c->d_mqa.p, nq, c->d_mt.p, c->d_mta.p, nt, th_low, ratio, check_orientation, c->d_mm.p,
-                    c->d_mb.p, c->d_ms.p, c->d_mn.p, c->d_mpart.p, st);
+                    c->d_mb.p, c->d_ms.p, c->d_mn.p, c->d_mpart.p, st, c->d_msync.p);
     HIPOK(hipGetLastError());
     int nm = 0;
     HIPOK(hipMemcpyAsync(match, c->d_mm.p, (size_t)nq * 4, hipMemcpyDeviceToHost, st));
@@ -666,11 +689,18 @@ int orbhip_match_pairs_device(orbhip_ctx* c, const orbhip_kp* d_kps, const uint8
     HIPOK(hipSetDevice(c->device));
     hipStream_t st = (hipStream_t)stream;   // NULL = the HIP null stream (HIP convention)
     HIPOK(c->d_mpart.ensure(match_part_entries(B - 1, cap, cap)));
+    if (int rc = ensure_msync(c, st)) return rc;
     (void)hipGetLastError();
-    launch_match_pairs(d_kps, d_desc, d_n, B - 1, cap, th_low, ratio, check_orientation, d_match, d_best, d_second,
-                       d_nmatch, c->d_mpart.p, st, &c->timer);
-    HIPOK(hipGetLastError());
-    return ORBHIP_OK;
+    GraphKey key;
+    key.add(3).ptr(d_kps).ptr(d_desc).ptr(d_n).add((uint64_t)B).add((uint64_t)cap).add((uint64_t)th_low).f32(ratio)
+        .add((uint64_t)check_orientation).ptr(d_match).ptr(d_best).ptr(d_second).ptr(d_nmatch).ptr(st)
+        .ptr(c->d_mpart.p).ptr(c->d_msync.p);
+    return c->graphs.run(key, st, c->timer.stage != 0, [&](hipStream_t st) -> int {
+        launch_match_pairs(d_kps, d_desc, d_n, B - 1, cap, th_low, ratio, check_orientation, d_match, d_best,
+                           d_second, d_nmatch, c->d_mpart.p, st, &c->timer, c->d_msync.p);
+        HIPOK(hipGetLastError());
+        return ORBHIP_OK;
+    });
 }
 
 int orbhip_match_frames_device(orbhip_ctx* c, const orbhip_kp* d_q_kps, const uint8_t* d_q_desc, const int32_t* d_nq,
@@ -683,11 +713,23 @@ int orbhip_match_frames_device(orbhip_ctx* c, const orbhip_kp* d_q_kps, const ui
     HIPOK(hipSetDevice(c->device));
     hipStream_t st = (hipStream_t)stream;   // NULL = the HIP null stream (HIP convention)
     HIPOK(c->d_mpart.ensure(match_part_entries(1, cap, cap)));
+    if (int rc = ensure_msync(c, st)) return rc;
     (void)hipGetLastError();
-    launch_match_frames(d_q_kps, d_q_desc, d_nq, d_t_kps, d_t_desc, d_nt, cap, th_low, ratio, check_orientation,
-                        d_match, d_best, d_second, d_nmatch, c->d_mpart.p, st, &c->timer);
-    HIPOK(hipGetLastError());
-    return ORBHIP_OK;
+    GraphKey key;
+    key.add(2).ptr(d_q_kps).ptr(d_q_desc).ptr(d_nq).ptr(d_t_kps).ptr(d_t_desc).ptr(d_nt).add((uint64_t)cap)
+        .add((uint64_t)th_low).f32(ratio).add((uint64_t)check_orientation).ptr(d_match).ptr(d_best).ptr(d_second)
+        .ptr(d_nmatch).ptr(st).ptr(c->d_mpart.p).ptr(c->d_msync.p);
+    return c->graphs.run(key, st, c->timer.stage != 0, [&](hipStream_t st) -> int {
+        launch_match_frames(d_q_kps, d_q_desc, d_nq, d_t_kps, d_t_desc, d_nt, cap, th_low, ratio, check_orientation,
+                            d_match, d_best, d_second, d_nmatch, c->d_mpart.p, st, &c->timer, c->d_msync.p);
+        HIPOK(hipGetLastError());
+        return ORBHIP_OK;
+    });
+}
+
+int orbhip_launch_graphs(orbhip_ctx* c) {
+    if (!c) return ORBHIP_ERR_ARG;
+    return c->graphs.graphs();
 }
 
 int orbhip_profile_stage(orbhip_ctx* c, int stage) {

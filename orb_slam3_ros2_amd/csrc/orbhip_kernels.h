@@ -52,17 +52,22 @@ void launch_desc(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& 
 
 // ---- matching ----
 // `part`: scratch of match_part_entries(npairs, max queries, max train) x 8 bytes (chunk partials)
+// `sync`: kMatchSyncInts zero-initialised ints kept by the caller across launches (the one-launch
+// matcher's counters, reset by each launch); null = the two-kernel path
+constexpr int kMatchSyncInts = 64 * 4;
 size_t match_part_entries(int npairs, int max_q, int max_t);
 void launch_match_pairs(const orbhip_kp* kps, const uint8_t* desc, const int32_t* n, int npairs, int cap,
                         int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best,
-                        int32_t* second, int32_t* nmatch, void* part, hipStream_t st, StageTimer* timer);
+                        int32_t* second, int32_t* nmatch, void* part, hipStream_t st, StageTimer* timer,
+                        int* sync);
 void launch_match_frames(const orbhip_kp* q_kps, const uint8_t* q_desc, const int32_t* nq, const orbhip_kp* t_kps,
                          const uint8_t* t_desc, const int32_t* nt, int cap, int th_low, float ratio,
                          int check_orientation, int32_t* match, int32_t* best, int32_t* second, int32_t* nmatch,
-                         void* part, hipStream_t st, StageTimer* timer);
+                         void* part, hipStream_t st, StageTimer* timer, int* sync);
 void launch_match_bf(const uint8_t* q, const float* qa, int nq, const uint8_t* t, const float* ta, int nt,
                      int th_low, float ratio, int check_orientation, int32_t* match, int32_t* best,
-                     int32_t* second, int32_t* nmatch, void* part, hipStream_t st);
+                     int32_t* second, int32_t* nmatch, void* part, hipStream_t st,
+                     int* sync);
 
 // ---- bag of words ----
 constexpr int kBowMax = 2048;   // features per frame in SearchByBoW (LDS-resident FeatureVectors)

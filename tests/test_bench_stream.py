@@ -1,15 +1,19 @@
 """The bench's pipelined C2 stream (frames of one camera stream in flight on several contexts /
-streams with event hand-offs) produces exactly the sequential per-frame results."""
+streams with event hand-offs) produces exactly the sequential per-frame results. The stream
+cycles through 32 frames, so from frame 32 on every call repeats an earlier one and, with
+ORBHIP_GRAPH=1, runs as a launch-graph replay; the reference runs on the HIP null stream with
+every kernel launched directly."""
 import numpy as np
 import pytest
 
 
 @pytest.mark.gpu
-def test_pipelined_stream_matches_sequential():
+@pytest.mark.parametrize("graphs", [False, True])
+def test_pipelined_stream_matches_sequential(monkeypatch, graphs):
     import torch
     import bench
-    K = 23
-    seq = bench.StreamC2(0, 1)
+    K = 75
+    seq = bench.StreamC2(0, 1, null_stream=True)   # built before the switch: direct launches
     ref = []
     for _ in range(K):
         seq.step()
@@ -17,11 +21,14 @@ def test_pipelined_stream_matches_sequential():
         cur = (seq.s - 1) % seq.ns
         ref.append((int(seq.n[cur]), seq.kps[cur].clone(), seq.desc[cur].clone(), int(seq.nm[cur]),
                     seq.mm[cur].clone()))
-    for S in (2, 4):
+    if graphs:
+        monkeypatch.setenv("ORBHIP_GRAPH", "1")
+    for S in (1, 2, 4):
         pip = bench.StreamC2(0, S)
         for _ in range(K):
             pip.step()
         torch.cuda.synchronize()
+        assert all((pip.L.orbhip_launch_graphs(h) > 0) == graphs for h in pip.handles), S
         for k in range(K - pip.ns, K):   # the frames still held in the slots
             slot = k % pip.ns
             n, kps, desc, nm, mm = ref[k]

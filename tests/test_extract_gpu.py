@@ -144,3 +144,52 @@ def test_large_batch_paths_match_oracle(ext1000, oracle):
         assert np.array_equal(kk[:, :5], ok[:, :5]), i
         assert np.array_equal(kk[:, 5].view(np.int32), ok[:, 5].astype(np.int32)), i
         assert np.array_equal(desc[i, : len(ok)].cpu().numpy(), od), i
+
+
+def test_graph_replay_recomputes_from_current_inputs(monkeypatch):
+    """With ORBHIP_GRAPH=1, repeated device calls with identical arguments on a stream replay a
+    captured launch graph (graph_cache.h). A replay must read the buffers' CURRENT contents: the same input
+    buffer is refilled with different frames between calls, and every extraction and match must
+    equal the direct launches on the HIP null stream."""
+    import torch
+    from orb_slam3_ros2_amd import ORBextractor, ORBmatcher
+    from orb_slam3_ros2_amd._lib import lib
+    monkeypatch.setenv("ORBHIP_GRAPH", "1")
+    ext = ORBextractor(1000, 1.2, 8, 20, 7)
+    mt = ORBmatcher(0.9, True, ctx=ext.ctx)
+    H, W = 480, 640
+    cap = ext.max_keypoints(W, H)
+    dev = torch.device("cuda:0")
+    imgs = [torch.from_numpy(synthetic_frame(60 + i, W, H)).to(dev) for i in range(5)]
+
+    def bufs():
+        return (torch.zeros((2, cap, 6), dtype=torch.float32, device=dev),
+                torch.zeros((2, cap, 32), dtype=torch.uint8, device=dev),
+                torch.zeros(2, dtype=torch.int32, device=dev), torch.zeros(2, dtype=torch.int32, device=dev),
+                torch.zeros((3, cap), dtype=torch.int32, device=dev), torch.zeros(1, dtype=torch.int32, device=dev))
+
+    def run(frame_buf, b, stream):
+        kps, desc, n, mono, mm, nm = b
+        ext.extract_batch_device(frame_buf, kps, desc, n, mono, stream=stream)
+        mt.match_pairs_device(kps, desc, n, mm[0:1], mm[1:2], mm[2:3], nm, stream=stream)
+
+    st = torch.cuda.Stream()
+    fb = torch.empty((2, H, W), dtype=torch.uint8, device=dev)
+    got, ref = bufs(), bufs()
+    for i in range(4):
+        pair = torch.stack([imgs[i], imgs[i + 1]])
+        fb.copy_(pair)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(st):
+            run(fb, got, st)
+        st.synchronize()
+        run(pair.contiguous(), ref, None)   # null stream: direct
+        torch.cuda.synchronize()
+        kps, desc, n, mono, mm, nm = got
+        rk, rd, rn, rmono, rmm, rnm = ref
+        assert torch.equal(n, rn) and torch.equal(mono, rmono) and torch.equal(nm, rnm), i
+        for f in range(2):
+            c = int(rn[f])
+            assert torch.equal(kps[f, :c], rk[f, :c]) and torch.equal(desc[f, :c], rd[f, :c]), (i, f)
+        assert torch.equal(mm[:, : int(rn[0])], rmm[:, : int(rn[0])]), i
+    assert lib().orbhip_launch_graphs(ext.ctx.handle) >= 2   # extract + match replayed

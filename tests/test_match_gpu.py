@@ -1,11 +1,22 @@
 """GPU parity: Hamming brute-force matcher (DescriptorDistance, best/second, TH_LOW, ratio,
-rotation histogram) vs the oracle, on extractor outputs and on the SURVEY §8(d) microbench."""
+rotation histogram) vs the oracle, on extractor outputs and on the SURVEY §8(d) microbench,
+through both device formulations (one launch with a last-workgroup filter; top-2 partials +
+finish kernel)."""
 import numpy as np
 import pytest
 
 from orb_slam3_ros2_amd.synthetic import shifted_frame, synthetic_frame
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(params=["fused", "two-kernel"], autouse=True)
+def match_path(request, monkeypatch):
+    """Every test runs on both device matchers: the one-launch k_match_fused (<= 4 pairs, the
+    default) and the k_match_top2 + k_match_finish pair (larger batches; forced here)."""
+    if request.param == "two-kernel":
+        monkeypatch.setenv("ORBHIP_MATCH_UNFUSED", "1")
+    return request.param
 
 
 @pytest.fixture(scope="module")
