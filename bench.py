@@ -55,7 +55,7 @@ def parse():
     ap.add_argument("--lba-steps", type=int, default=20)
     ap.add_argument("--lba-batch", type=int, default=256)
     ap.add_argument("--gba-iters", type=int, default=10)
-    ap.add_argument("--inflight", type=int, default=4,
+    ap.add_argument("--inflight", type=int, default=8,
                     help="frames of the C2 stream in flight (pipelined batch-1 frames; 1 = strictly sequential)")
     return ap.parse_args()
 
@@ -148,7 +148,10 @@ class StreamC2:
         dev = torch.device("cuda")
         self.frames_np = make_stream_frames(self.NF, self.W, self.H, 1000 * rank + 1)
         self.frames = torch.from_numpy(self.frames_np).to(dev)
-        ns = max(2, S)   # output slots (two suffice for one stream)
+        # output slots: two suffice for one stream; with S streams, 2S slots put a slot's last
+        # cross-stream reader 2S - 1 frames back, so its event is normally complete by reuse
+        # time and the host skips the stream wait (a hipStreamWaitEvent costs ~4 us of host time)
+        ns = 2 if S == 1 else 2 * S
         self.ns = ns
         self.kps = torch.zeros((ns, self.cap, 6), dtype=torch.float32, device=dev)
         self.desc = torch.zeros((ns, self.cap, 32), dtype=torch.uint8, device=dev)
@@ -187,8 +190,10 @@ class StreamC2:
         j = k % self.S
         cur, prev = k % self.ns, (k - 1) % self.ns
         c, sp = self.handles[j], self.sts[j]
-        if self.S > 1 and k >= self.ns:
-            # slot `cur` was last read (as `prev`) by the match of frame k - ns + 1
+        if self.S > 1 and k >= self.ns and not self.ev_m[cur].query():
+            # slot `cur` was last read (as `prev`) by the match of frame k - ns + 1, on another
+            # stream, and that match has not finished yet (its reader as `cur`, frame k - ns,
+            # ran on this stream: ordered already)
             self.streams[j].wait_event(self.ev_m[cur])
         rc = self.extract(c, self.p_frames[k % self.NF], 1, self.W, self.H, self.W, self.W * self.H, 0, 1000,
                           self.p_kps[cur], self.p_desc[cur], self.cap, self.p_n[cur], self.p_mono[cur], sp)

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 
 __global__ void k_empty(int* p, int v) {
     if (threadIdx.x == 0 && blockIdx.x == 0 && v < 0) p[0] = v;
@@ -43,6 +44,29 @@ int main() {
         std::printf("graph(6 nodes): host %.2f us/graph, drain %.2f us/graph\n",
                     std::chrono::duration<double, std::micro>(t1 - t0).count() / n,
                     std::chrono::duration<double, std::micro>(t2 - t0).count() / n);
+    }
+    {
+        const int n = 100000;
+        auto t0 = now();
+        int hits = 0;
+        for (int i = 0; i < n; i++) hits += std::getenv("ORBHIP_GRAPH") != nullptr;
+        auto t1 = now();
+        std::printf("getenv: %.3f us/call (%d hits)\n", std::chrono::duration<double, std::micro>(t1 - t0).count() / n,
+                    hits);
+        hipEvent_t ev;
+        (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        hipStream_t s2;
+        (void)hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
+        const int m = 2000;
+        t0 = now();
+        for (int i = 0; i < m; i++) (void)hipEventRecord(ev, s);
+        t1 = now();
+        std::printf("hipEventRecord (no timing): %.2f us\n", std::chrono::duration<double, std::micro>(t1 - t0).count() / m);
+        t0 = now();
+        for (int i = 0; i < m; i++) (void)hipStreamWaitEvent(s2, ev, 0);
+        t1 = now();
+        std::printf("hipStreamWaitEvent: %.2f us\n", std::chrono::duration<double, std::micro>(t1 - t0).count() / m);
+        (void)hipStreamSynchronize(s2);
     }
     return 0;
 }
