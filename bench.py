@@ -217,6 +217,49 @@ class StreamC2:
         return stage_bytes(self.ext, self.W, self.H, float(self.n.float().mean().item()) or 1000.0, 1)
 
 
+class FrontendC2:
+    """The same camera stream through the library's front-end (FrameStream, include/orbhip.h
+    orbhip_frontend_*): frame k extracted at batch 1 on context k % inflight, matched to frame
+    k - 1 with the same event hand-offs as StreamC2, the bookkeeping in C (one C call per frame).
+    The headline path; StreamC2 is its Python-side twin for the parity tests."""
+    W, H, NF = 640, 480, 32
+
+    def __init__(self, rank, inflight=8):
+        import torch
+        from orb_slam3_ros2_amd import ORBextractor
+        from orb_slam3_ros2_amd.frontend import FrameStream
+        self.S = max(1, int(inflight))
+        self.fs = FrameStream(self.W, self.H, self.S, 1000, 1.2, 8, 20, 7, 50, 0.9, True)
+        self.ext = ORBextractor(1000, 1.2, 8, 20, 7)   # level tables for the roofline bytes only
+        self.frames_np = make_stream_frames(self.NF, self.W, self.H, 1000 * rank + 1)
+        self.frames = torch.from_numpy(self.frames_np).to("cuda")
+        self.p_frames = [self.frames[i].data_ptr() for i in range(self.NF)]
+        self.push = self.fs.push_ptr
+        self.ctx0 = self.fs.context(0)
+        self.s, self.last = 0, -1
+        torch.cuda.synchronize()
+
+    def step(self):
+        slot = self.push(self.p_frames[self.s % self.NF], self.W)
+        if slot < 0:
+            raise RuntimeError(f"orbhip_frontend_push: {slot}")
+        self.last = slot
+        self.s += 1
+
+    def last_matches(self):
+        self.fs.wait(self.last)
+        return int(self.fs.view(self.last)["nmatch"].item())
+
+    def mean_keypoints(self):
+        import torch
+        torch.cuda.synchronize()
+        ns = [int(self.fs.view(i)["n"].item()) for i in range(min(self.fs.slots, self.s))]
+        return float(np.mean(ns)) if ns else 0.0
+
+    def stage_bytes(self):
+        return stage_bytes(self.ext, self.W, self.H, self.mean_keypoints() or 1000.0, 1)
+
+
 def stage_bytes(ext, w, h, n_kp, frames):
     """Algorithmic HBM bytes per launch of each stage: resize reads level l-1 and
     writes level l (all 7 launches summed), FAST reads every level once, octree reads its packed
@@ -461,8 +504,8 @@ def main():
     import torch
     ws, rank, local = _dist_setup(args)
     K, W = args.steps, args.warmup
-    c2 = StreamC2(rank, args.inflight)
-    prof = Profiler(c2.ext.ctx)   # the stage timers of context 0 (frames k % inflight == 0)
+    c2 = FrontendC2(rank, args.inflight)
+    prof = Profiler(c2.ctx0)   # the stage timers of context 0 (frames k % inflight == 0)
     # ---- find the dominant kernel of the step (short calibration, untimed) ----
     stage_ms = {}
     for st in (1, 2, 3, 4, 5, 6):
@@ -489,10 +532,10 @@ def main():
     prof.select(0)
     frames_total = _sum_over_ranks(ws, float(K))
     value = frames_total / elapsed
-    nkp = float(c2.n.float().mean().item())
+    nkp = c2.mean_keypoints()
     nmatch = c2.last_matches()
     # the same stream strictly one frame at a time (no overlap): per-frame latency
-    seq = StreamC2(rank, 1) if c2.S > 1 else c2
+    seq = FrontendC2(rank, 1) if c2.S > 1 else c2
     if seq is not c2:
         for _ in range(W):
             seq.step()

@@ -132,6 +132,42 @@ int orbhip_match_frames_device(orbhip_ctx* ctx, const orbhip_kp* d_q_kps, const 
                                int32_t* d_match, int32_t* d_best, int32_t* d_second, int32_t* d_nmatch,
                                void* stream);
 
+/* ---- camera front-end stream -------------------------------------------------------
+ * One camera's frames, as Tracking receives them (Frame ctor -> ExtractORB, then matching
+ * against the last frame), pipelined on the device: frame k is extracted at batch 1 on
+ * context k % frames_in_flight (each context = its own HIP stream / hardware queue) into
+ * output slot k % slots (slots = 2 * frames_in_flight, 2 for 1), then the previous frame
+ * (queries) is matched to it (train) as orbhip_match_frames_device does with (th_low, ratio,
+ * check_orientation). Cross-frame hand-offs are device events; push never blocks the host.
+ * Same kernels and results as the one-frame calls. Frame 0 has no match (*nmatch = -1).
+ *   push: d_img = device u8 frame (w x h, rows `stride` bytes apart), vLappingArea
+ *         {lap0, lap1}; returns the slot index (>= 0) or an error (< 0). The caller keeps
+ *         d_img unchanged until the frame completes.
+ *   view: device pointers of a slot's outputs (valid until the slot is reused, `slots`
+ *         pushes later); frame = number of the frame held (-1 none).
+ *   wait: the frame in `slot` complete: host-blocking (stream NULL) or stream-ordered.
+ *   context: context j (0 <= j < frames_in_flight), e.g. for orbhip_profile_stage. */
+typedef struct orbhip_frontend orbhip_frontend;
+typedef struct {
+    int64_t frame;
+    int32_t cap, slots;
+    orbhip_kp* kps;          /* cap entries */
+    uint8_t* desc;           /* cap x 32 */
+    int32_t* n;              /* 1 */
+    int32_t* mono;           /* 1: operator()'s return value */
+    int32_t* match;          /* cap: previous frame's keypoint i -> this frame's index or -1 */
+    int32_t* best;           /* cap */
+    int32_t* second;         /* cap */
+    int32_t* nmatch;         /* 1 */
+} orbhip_frontend_slot;
+int orbhip_frontend_create(orbhip_frontend** out, int device, const orbhip_orb_params* params, int w, int h,
+                           int frames_in_flight, int th_low, float ratio, int check_orientation);
+int orbhip_frontend_destroy(orbhip_frontend* fe);
+int orbhip_frontend_push(orbhip_frontend* fe, const uint8_t* d_img, int stride, int lap0, int lap1);
+int orbhip_frontend_view(orbhip_frontend* fe, int slot, orbhip_frontend_slot* out);
+int orbhip_frontend_wait(orbhip_frontend* fe, int slot, void* stream);
+int orbhip_frontend_context(orbhip_frontend* fe, int j, orbhip_ctx** out);
+
 /* ---- diagnostics: live kernel timing ----------------------------------------------
  * orbhip_profile_stage selects ONE stage whose launches are bracketed by hipEvents on the
  * stream they run on (0 off, 1 pyramid resize, 2 FAST cells, 3 octree, 4 orientation +

@@ -15,6 +15,8 @@ Host-side mirror of the reference's hot-path interfaces over th
   ORBmatcher.SearchByProjectionLastFrame / SearchLocalPoints(...)           U:src/ORBmatcher.cc
   KeyFrameDatabase(max_kf).DetectRelocalizationCandidates / DetectNBestCandidates
                                                                             U:src/KeyFrameDatabase.cc
+  FrameStream(w, h, frames_in_flight).push(frame)   Frame ctor -> ExtractORB + match to the last
+                                                    frame, pipelined on the device
 
 The HIP library is the only compute path: importing this package on a box without the
 built extension, or calling it without a GPU, raises — there is no CPU fallback.
@@ -27,6 +29,8 @@ from .matcher import ORBmatcher  # noqa: F401
 from .optimizer import BAProblem, BAResult, Optimizer, PoseProblem, PoseResult  # noqa: F401
 from .bow import ORBVocabulary  # noqa: F401
 from .kfdb import KeyFrameDatabase  # noqa: F401
+from .frontend import FrameStream  # noqa: F401
 
-__all__ = ["ORBextractor", "KeyPoint", "ORBmatcher", "Optimizer", "BAProblem", "BAResult", "PoseProblem", "PoseResult", "ORBVocabulary", "KeyFrameDatabase", "OrbHipError",
+__all__ = ["ORBextractor", "KeyPoint", "ORBmatcher", "Optimizer", "BAProblem", "BAResult", "PoseProblem", "PoseResult", "ORBVocabulary", "KeyFrameDatabase", "FrameStream",
+           "OrbHipError",
            "lib", "library_path"]

@@ -108,7 +108,9 @@ EXPORTED = ["orbhip_abi_version", "orbhip_create", "orbhip_destroy", "orbhip_lev
             "orbhip_pose_optimization", "orbhip_pose_optimization_batch", "orbhip_search_by_projection_last",
             "orbhip_search_local_points", "orbhip_search_for_initialization",
             "orbhip_kfdb_create", "orbhip_kfdb_destroy", "orbhip_kfdb_add", "orbhip_kfdb_erase",
-            "orbhip_kfdb_detect_relocalization", "orbhip_kfdb_detect_nbest"]
+            "orbhip_kfdb_detect_relocalization", "orbhip_kfdb_detect_nbest",
+            "orbhip_frontend_create", "orbhip_frontend_destroy", "orbhip_frontend_push", "orbhip_frontend_view",
+            "orbhip_frontend_wait", "orbhip_frontend_context"]
 
 
 def lib():
@@ -172,6 +174,13 @@ def lib():
     L.orbhip_kfdb_erase.argtypes = [vp, i32]
     L.orbhip_kfdb_detect_relocalization.argtypes = [vp, ctypes.POINTER(KfdbQueryC), vp, i32]
     L.orbhip_kfdb_detect_nbest.argtypes = [vp, ctypes.POINTER(KfdbQueryC), vp, i32, vp, vp, vp, vp]
+    L.orbhip_frontend_create.argtypes = [ctypes.POINTER(vp), i32, ctypes.POINTER(OrbParams), i32, i32, i32, i32, f32,
+                                         i32]
+    L.orbhip_frontend_destroy.argtypes = [vp]
+    L.orbhip_frontend_push.argtypes = [vp, vp, i32, i32, i32]
+    L.orbhip_frontend_view.argtypes = [vp, i32, vp]
+    L.orbhip_frontend_wait.argtypes = [vp, i32, vp]
+    L.orbhip_frontend_context.argtypes = [vp, i32, ctypes.POINTER(vp)]
     L.orbhip_test_sincosf.argtypes = [vp, vp, vp, ctypes.c_int64]
     L.orbhip_test_sincosf_sweep.argtypes = [ctypes.c_uint32, ctypes.c_uint32, vp, vp]
     L.orbhip_test_sincosf_sweep.restype = ctypes.c_int64

@@ -1225,3 +1225,156 @@ int orbhip_test_cells(orbhip_ctx* c, int w, int h, int32_t* out6, int cap) {
 }
 
 }  // extern "C"
+
+// ===========================================================================
+// Camera front-end stream (orbhip_frontend_*): one camera's frames, each extracted at batch 1
+// and matched to the previous frame, pipelined over S contexts (the contexts' own HIP streams,
+// created back to back so they land on distinct hardware queues). Frame k runs on context
+// k % S into output slot k % ns (ns = 2S; 2 for S = 1). Per frame the host issues: a wait for
+// the slot's last cross-stream reader only if it has not finished (hipEventQuery; it is 2S - 1
+// frames back, so normally done), the extraction, the extraction event, a wait on the previous
+// frame's extraction event, the match (previous frame = queries, this frame = train, as the C2
+// bench) and one event that also marks the frame complete. Same kernels and results as the
+// one-frame calls; the host work per frame is one C call instead of the caller's bookkeeping.
+// ===========================================================================
+struct orbhip_frontend {
+    int device = 0, w = 0, h = 0, S = 0, ns = 0, cap = 0;
+    int th_low = 50, check_orientation = 1;
+    float ratio = 0.9f;
+    int64_t k = 0;   // frames pushed
+    std::vector<orbhip_ctx*> ctx;
+    orbhip_kp* kps = nullptr;
+    uint8_t* desc = nullptr;
+    int32_t *n = nullptr, *mono = nullptr, *mm = nullptr, *nm = nullptr;
+    std::vector<hipEvent_t> ev_x, ev_m;   // slot's extraction done / the match that read the slot as prev done
+    std::vector<int64_t> frame_of;        // frame number held by each slot (-1 none)
+};
+
+static void frontend_free(orbhip_frontend* f) {
+    if (!f) return;
+    for (orbhip_ctx* c : f->ctx)
+        if (c) (void)hipStreamSynchronize(c->stream);
+    for (hipEvent_t e : f->ev_x)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : f->ev_m)
+        if (e) (void)hipEventDestroy(e);
+    if (f->kps) (void)hipFree(f->kps);
+    if (f->desc) (void)hipFree(f->desc);
+    if (f->n) (void)hipFree(f->n);
+    if (f->mono) (void)hipFree(f->mono);
+    if (f->mm) (void)hipFree(f->mm);
+    if (f->nm) (void)hipFree(f->nm);
+    for (orbhip_ctx* c : f->ctx)
+        if (c) (void)orbhip_destroy(c);
+    delete f;
+}
+
+extern "C" {
+
+int orbhip_frontend_create(orbhip_frontend** out, int device, const orbhip_orb_params* params, int w, int h,
+                           int frames_in_flight, int th_low, float ratio, int check_orientation) {
+    if (!out || w <= 0 || h <= 0 || frames_in_flight < 1 || frames_in_flight > 32) return ORBHIP_ERR_ARG;
+    *out = nullptr;
+    std::unique_ptr<orbhip_frontend, void (*)(orbhip_frontend*)> f(new orbhip_frontend(), frontend_free);
+    f->device = device; f->w = w; f->h = h;
+    f->S = frames_in_flight;
+    f->ns = frames_in_flight == 1 ? 2 : 2 * frames_in_flight;
+    f->th_low = th_low; f->ratio = ratio; f->check_orientation = check_orientation;
+    f->ctx.assign(f->S, nullptr);
+    for (int j = 0; j < f->S; j++)
+        if (int rc = orbhip_create(&f->ctx[j], device, params)) return rc;
+    const int cap = orbhip_max_keypoints(f->ctx[0], w, h);
+    if (cap <= 0) return cap < 0 ? cap : ORBHIP_ERR_UNSUPPORTED;
+    f->cap = cap;
+    const size_t ns = (size_t)f->ns;
+    HIPOK(hipMalloc((void**)&f->kps, sizeof(orbhip_kp) * cap * ns));
+    HIPOK(hipMalloc((void**)&f->desc, 32 * (size_t)cap * ns));
+    HIPOK(hipMalloc((void**)&f->n, 4 * ns));
+    HIPOK(hipMalloc((void**)&f->mono, 4 * ns));
+    HIPOK(hipMalloc((void**)&f->mm, 12 * (size_t)cap * ns));
+    HIPOK(hipMalloc((void**)&f->nm, 4 * ns));
+    f->ev_x.assign(ns, nullptr);
+    f->ev_m.assign(ns, nullptr);
+    f->frame_of.assign(ns, -1);
+    for (size_t i = 0; i < ns; i++) {
+        HIPOK(hipEventCreateWithFlags(&f->ev_x[i], hipEventDisableTiming));
+        HIPOK(hipEventCreateWithFlags(&f->ev_m[i], hipEventDisableTiming));
+    }
+    *out = f.release();
+    return ORBHIP_OK;
+}
+
+int orbhip_frontend_destroy(orbhip_frontend* f) {
+    if (!f) return ORBHIP_ERR_ARG;
+    (void)hipSetDevice(f->device);
+    frontend_free(f);
+    return ORBHIP_OK;
+}
+
+int orbhip_frontend_push(orbhip_frontend* f, const uint8_t* d_img, int stride, int lap0, int lap1) {
+    if (!f || !d_img || stride < f->w) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(f->device));
+    const int64_t k = f->k;
+    const int S = f->S, ns = f->ns, cap = f->cap;
+    const int j = (int)(k % S), cur = (int)(k % ns), prev = (int)((k + ns - 1) % ns);
+    orbhip_ctx* c = f->ctx[j];
+    hipStream_t st = c->stream;
+    // slot `cur` was last read as `prev` by the match of frame k - ns + 1 (on another stream when
+    // S > 1); its reader as `cur`, frame k - ns, ran on this stream
+    if (S > 1 && k >= ns && hipEventQuery(f->ev_m[cur]) != hipSuccess) HIPOK(hipStreamWaitEvent(st, f->ev_m[cur], 0));
+    orbhip_kp* kc = f->kps + (size_t)cur * cap;
+    uint8_t* dc = f->desc + (size_t)cur * cap * 32;
+    if (int rc = orbhip_extract_batch_device(c, d_img, 1, f->w, f->h, stride, (int64_t)stride * f->h, lap0, lap1, kc,
+                                             dc, cap, f->n + cur, f->mono + cur, st))
+        return rc;
+    if (S > 1) HIPOK(hipEventRecord(f->ev_x[cur], st));   // the next frame's match (another stream) waits on it
+    int32_t* m = f->mm + (size_t)cur * 3 * cap;
+    if (k == 0) {
+        HIPOK(hipMemsetAsync(f->nm + cur, 0xFF, 4, st));   // no previous frame: nmatch = -1
+    } else {
+        if (S > 1) HIPOK(hipStreamWaitEvent(st, f->ev_x[prev], 0));
+        if (int rc = orbhip_match_frames_device(c, f->kps + (size_t)prev * cap, f->desc + (size_t)prev * cap * 32,
+                                                f->n + prev, kc, dc, f->n + cur, cap, f->th_low, f->ratio,
+                                                f->check_orientation, m, m + cap, m + 2 * cap, f->nm + cur, st))
+            return rc;
+    }
+    HIPOK(hipEventRecord(f->ev_m[prev], st));   // the match read `prev`; and frame k is complete
+    f->frame_of[cur] = k;
+    f->k = k + 1;
+    return cur;
+}
+
+int orbhip_frontend_view(orbhip_frontend* f, int slot, orbhip_frontend_slot* v) {
+    if (!f || !v || slot < 0 || slot >= f->ns) return ORBHIP_ERR_ARG;
+    const size_t cap = (size_t)f->cap;
+    v->frame = f->frame_of[slot];
+    v->cap = f->cap;
+    v->slots = f->ns;
+    v->kps = f->kps + slot * cap;
+    v->desc = f->desc + slot * cap * 32;
+    v->n = f->n + slot;
+    v->mono = f->mono + slot;
+    v->match = f->mm + (size_t)slot * 3 * cap;
+    v->best = v->match + cap;
+    v->second = v->match + 2 * cap;
+    v->nmatch = f->nm + slot;
+    return ORBHIP_OK;
+}
+
+int orbhip_frontend_wait(orbhip_frontend* f, int slot, void* stream) {
+    if (!f || slot < 0 || slot >= f->ns || f->frame_of[slot] < 0) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(f->device));
+    // frame k completes with the event its push recorded on ev_m[(k - 1) mod ns]
+    hipEvent_t e = f->ev_m[(slot + f->ns - 1) % f->ns];
+    if (stream) HIPOK(hipStreamWaitEvent((hipStream_t)stream, e, 0));
+    else HIPOK(hipEventSynchronize(e));
+    return ORBHIP_OK;
+}
+
+int orbhip_frontend_context(orbhip_frontend* f, int j, orbhip_ctx** out) {
+    if (!f || !out || j < 0 || j >= f->S) return ORBHIP_ERR_ARG;
+    *out = f->ctx[j];
+    return ORBHIP_OK;
+}
+
+}  // extern "C"
