@@ -146,12 +146,18 @@ __device__ __forceinline__ int small_div(int i, float inv_d) { return (int)(((fl
 // LDS: [level 0 stage | level 1 .. L-1 cones] bytes, then per level the column table
 // (xofs, xalpha) of its need columns and the row table (clamped r0, r1, ybeta) of its rows: one
 // global round trip loads every table entry and the level-0 cone, then the levels follow from LDS.
-__global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict__ P, FrameBufs fb,
-                                                   const ConeRect* __restrict__ rects, const int* __restrict__ ctab,
-                                                   int tab_stride) {
+__device__ __forceinline__ void wait_vm_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// SYNC (k_pyr_fast): the owned pixels of each level leave from LDS as device-coherent (sc1,
+// write-through) dword stores, and the tile is counted in lvl_done[f * L] once all of them are
+// performed, for the FAST work-groups of the same launch that wait on it.
+template <bool SYNC>
+__device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P, const FrameBufs& fb,
+                                              const ConeRect* __restrict__ rects, const int* __restrict__ ctab,
+                                              int tab_stride, uint8_t* __restrict__ cone, int tile,
+                                              int* __restrict__ lvl_done) {
     TR_BEGIN()
-    extern __shared__ __attribute__((aligned(16))) uint8_t cone[];
-    const int tile = blockIdx.x, f = blockIdx.y, L = P->n_levels, tid = threadIdx.x, nt = blockDim.x;
+    const int f = blockIdx.y, L = P->n_levels, tid = threadIdx.x, nt = blockDim.x;
     const ConeRect* R = rects + (size_t)tile * kMaxLevels;
     int boff[kMaxLevels], toff[kMaxLevels];
     int tot = 0;
@@ -240,12 +246,53 @@ __global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict
             }
             const uint8_t u = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
             cone[boff[l] + i] = u;
-            if (x >= r.ox0 && x < r.ox1 && y >= r.oy0 && y < r.oy1) dst[(int64_t)y * D.pitch + x] = u;
+            if constexpr (!SYNC) {
+                if (x >= r.ox0 && x < r.ox1 && y >= r.oy0 && y < r.oy1) dst[(int64_t)y * D.pitch + x] = u;
+            }
         }
         __syncthreads();
+        if constexpr (SYNC) {
+            // the owned pixels leave from LDS as device-coherent stores: aligned dwords in the
+            // interior of each row, bytes at its ends; not waited for until after the last level
+            const int xa = (r.ox0 + 3) & ~3, xb = r.ox1 & ~3, oh = r.oy1 - r.oy0;
+            const int nlead = max(0, min(xa, r.ox1) - r.ox0);
+            const int nmid = max(0, xb - xa) >> 2;
+            const int ntail = max(0, r.ox1 - max(xa, xb));
+            const int per = nlead + nmid + ntail;
+            if (per > 0 && oh > 0) {
+                const float inv_per = 1.0f / (float)per;
+                for (int i = tid; i < per * oh; i += nt) {
+                    const int yy = small_div(i, inv_per), k = i - yy * per;
+                    const int y = r.oy0 + yy;
+                    const uint8_t* srow = cone + boff[l] + (y - r.ny0) * nw - r.nx0;   // indexed by x
+                    uint8_t* drow = dst + (int64_t)y * D.pitch;
+                    if (k >= nlead && k < nlead + nmid) {
+                        const int x = xa + 4 * (k - nlead);
+                        const uint32_t v = (uint32_t)srow[x] | ((uint32_t)srow[x + 1] << 8) |
+                                           ((uint32_t)srow[x + 2] << 16) | ((uint32_t)srow[x + 3] << 24);
+                        __hip_atomic_store((uint32_t*)(drow + x), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    } else {
+                        const int x = k < nlead ? r.ox0 + k : max(xa, xb) + (k - nlead - nmid);
+                        __hip_atomic_store(drow + x, srow[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+            }
+        }
         TR_PHASE(0, l)
     }
+    if constexpr (SYNC) {
+        wait_vm_all();      // this thread's pyramid stores are performed
+        __syncthreads();
+        if (tid == 0) atomicAdd(&lvl_done[f * L], 1);   // one more tile done (every level)
+    }
     TR_END(0)
+}
+
+__global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict__ P, FrameBufs fb,
+                                                   const ConeRect* __restrict__ rects, const int* __restrict__ ctab,
+                                                   int tab_stride) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t cone[];
+    pyr_cone_body<false>(P, fb, rects, ctab, tab_stride, cone, blockIdx.x, nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -291,26 +338,43 @@ __device__ __forceinline__ bool fast_pair_test(const int* d, int t) {
     return bright | dark;
 }
 
-template <int NT>
-__global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict__ P,
-                                                    const CellGeom* __restrict__ cells, FrameBufs fb,
-                                                    uint32_t* __restrict__ cand, int* __restrict__ cand_cnt,
-                                                    int* __restrict__ err) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[kWinMax * kWinMax];
-    __shared__ uint8_t mv[kWinMax * kWinMax];
+// LDS of one FAST cell (static in k_fast_cells, carved from the dynamic buffer in k_pyr_fast)
+struct FastLds {
+    uint8_t* win;                   // kWinMax^2 window
+    uint8_t* mv;                    // kWinMax^2 strength map
+    unsigned long long (*bmask)[96];   // [2][96] NMS survivors per threshold, raster order (<= 6144 px)
+    int* woff;                      // [96] output offset of each 64-px word
+    int* wsel;
+    int* wtot;
+    uint16_t* clist;                // kWinMax^2 pair-test survivors (strength to compute)
+    int* ncand;
+};
+constexpr size_t kFastLdsBytes = 2 * kWinMax * kWinMax + 2 * 96 * 8 + 96 * 4 + 16 + 2 * kWinMax * kWinMax + 16;
+
+// SYNC (k_pyr_fast): a cell of level l > 0 first waits until every cone tile of the launch is
+// done, then reads its window device-coherent (sc1 loads: the tiles wrote it
+// through other XCDs' L2s a moment ago). A bounded wait: the error flag instead of a hang.
+template <int NT, bool SYNC>
+__device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P, const CellGeom* __restrict__ cells,
+                                               const FrameBufs& fb, uint32_t* __restrict__ cand,
+                                               int* __restrict__ cand_cnt, int* __restrict__ err, int cell,
+                                               const FastLds& LS, const int* __restrict__ lvl_done, int ntiles) {
+    uint8_t* const win = LS.win;
+    uint8_t* const mv = LS.mv;
+    unsigned long long (*const bmask)[96] = LS.bmask;
+    int* const woff = LS.woff;
+    int& wsel = *LS.wsel;
+    int& wtot = *LS.wtot;
+    uint16_t* const clist = LS.clist;
+    int& ncand = *LS.ncand;
     constexpr int NW = NT / 64;
-    __shared__ unsigned long long bmask[2][96];   // NMS survivors per threshold, raster order (<= 6144 px)
-    __shared__ int woff[96];                      // output offset of each 64-px word
-    __shared__ int wsel, wtot;
-    __shared__ uint16_t clist[kWinMax * kWinMax];   // pair-test survivors (strength to compute)
-    __shared__ int ncand;
     TR_BEGIN()
-    const CellGeom cg = cells[blockIdx.x];
+    const CellGeom cg = cells[cell];
     const int f = blockIdx.y;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wc = cg.wc, hc = cg.hc;
-    int* cnt_out = cand_cnt + (int64_t)f * P->n_cells_total + blockIdx.x;
-    if (blockIdx.x == 0 && f == 0 && tid < 4) err[tid] = 0;   // the octree (next launch) reports here
+    int* cnt_out = cand_cnt + (int64_t)f * P->n_cells_total + cell;
+    if (cell == 0 && f == 0 && tid < 4) err[tid] = 0;   // the octree (next launch) reports here
     if (wc <= 6 || hc <= 6) {
         if (tid == 0) *cnt_out = 0;
         return;
@@ -318,6 +382,23 @@ __global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict
     const LevelGeom& G = P->lv[cg.level];
     ImgRef im = level_img(P, fb, f, cg.level);
     const uint8_t* base = im.p + (int64_t)cg.y0 * im.pitch + cg.x0;
+    const bool coherent = SYNC && cg.level > 0;
+    if (coherent) {
+        if (tid == 0) {
+            const int* d = lvl_done + f * P->n_levels;   // tiles done
+            for (int it = 0; __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ntiles; it++) {
+                if (it > (1 << 22)) {   // ~0.1 s: never expected
+                    atomicOr(err, 4);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        __syncthreads();
+    }
+    auto ld4 = [&](const uint32_t* q) -> uint32_t {
+        return coherent ? __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *q;
+    };
     // ---- window -> LDS: all loads of a thread issued back to back. When the rows are 4-byte
     // aligned (pyramid levels always; the caller's frame when its pointer and stride are), the
     // window moves as aligned dwords into LDS rows of kWinP bytes, shifted by sh = base & 3 ----
@@ -339,7 +420,7 @@ __global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict
                 for (int u = 0; u < NU; u++) {
                     const int i = min(tid + NT * u, tot - 1);
                     const int yy = small_div(i, inv_n), xx = i - yy * nwd;
-                    v[u] = b4[(int64_t)yy * p4 + xx];
+                    v[u] = ld4(&b4[(int64_t)yy * p4 + xx]);
                     li[u] = yy * (kWinP / 4) + xx;
                 }
 #pragma unroll
@@ -348,7 +429,7 @@ __global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict
             } else {
                 for (int i = tid; i < tot; i += NT) {
                     const int yy = small_div(i, inv_n), xx = i - yy * nwd;
-                    w4[yy * (kWinP / 4) + xx] = b4[(int64_t)yy * p4 + xx];
+                    w4[yy * (kWinP / 4) + xx] = ld4(&b4[(int64_t)yy * p4 + xx]);
                 }
             }
         } else {
@@ -470,6 +551,50 @@ __global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict
     if (tid == 0) *cnt_out = wtot;
     TR_PHASE(1, 3)
     TR_END(1)
+}
+
+template <int NT>
+__global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict__ P,
+                                                    const CellGeom* __restrict__ cells, FrameBufs fb,
+                                                    uint32_t* __restrict__ cand, int* __restrict__ cand_cnt,
+                                                    int* __restrict__ err) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[kWinMax * kWinMax];
+    __shared__ uint8_t mv[kWinMax * kWinMax];
+    __shared__ unsigned long long bmask[2][96];
+    __shared__ int woff[96];
+    __shared__ int wsel, wtot;
+    __shared__ uint16_t clist[kWinMax * kWinMax];
+    __shared__ int ncand;
+    const FastLds LS{win, mv, bmask, woff, &wsel, &wtot, clist, &ncand};
+    fast_cell_body<NT, false>(P, cells, fb, cand, cand_cnt, err, blockIdx.x, LS, nullptr, 0);
+}
+
+// ---------------------------------------------------------------------------
+// k_pyr_fast: k_pyr_cone and k_fast_cells in ONE launch (the cone path, small batches). Work-
+// groups [0, ntiles) are the cone tiles, the rest FAST cells. Work-groups are dispatched in
+// index order, so every tile is resident or done before any cell waits on it: level-0 cells
+// (the frame itself) start at once, next to the tiles; the cells of the other levels start when
+// every tile is done. The counters are reset by k_octree (the next launch on the stream).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_pyr_fast(const ExtractPlan* __restrict__ P, FrameBufs fb,
+                                                   const ConeRect* __restrict__ rects, const int* __restrict__ ctab,
+                                                   int tab_stride, int ntiles, const CellGeom* __restrict__ cells,
+                                                   uint32_t* __restrict__ cand, int* __restrict__ cand_cnt,
+                                                   int* __restrict__ err, int* __restrict__ lvl_done) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t cone[];
+    if ((int)blockIdx.x < ntiles) {
+        pyr_cone_body<true>(P, fb, rects, ctab, tab_stride, cone, blockIdx.x, lvl_done);
+        return;
+    }
+    uint8_t* b = cone;
+    FastLds LS;
+    LS.win = b; b += kWinMax * kWinMax;
+    LS.mv = b; b += kWinMax * kWinMax;
+    LS.bmask = (unsigned long long (*)[96])b; b += 2 * 96 * 8;
+    LS.woff = (int*)b; b += 96 * 4;
+    LS.wsel = (int*)b; LS.wtot = (int*)b + 1; LS.ncand = (int*)b + 2; b += 16;
+    LS.clist = (uint16_t*)b;
+    fast_cell_body<1024, true>(P, cells, fb, cand, cand_cnt, err, (int)blockIdx.x - ntiles, LS, lvl_done, ntiles);
 }
 
 // ---------------------------------------------------------------------------
@@ -637,11 +762,13 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                                                  const uint32_t* __restrict__ cand, const int* __restrict__ cand_cnt,
                                                  uint32_t* __restrict__ kscratch, uint16_t* __restrict__ nscratch,
                                                  LevelKp* __restrict__ lvl_kp, int* __restrict__ lvl_cnt,
-                                                 int* __restrict__ lvl_nlap, OctreeCfg cfg, int* __restrict__ err) {
+                                                 int* __restrict__ lvl_nlap, OctreeCfg cfg, int* __restrict__ err,
+                                                 int* __restrict__ lvl_done) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     TR_BEGIN()
     // grid (frame, level): the level-0 work-groups (the longest) of every frame dispatch first
     const int f = blockIdx.x, l = blockIdx.y;
+    if (threadIdx.x == 0) lvl_done[f * P->n_levels + l] = 0;   // k_pyr_fast's counters, for the next frame
     const LevelGeom& G = P->lv[l];
     const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
     const bool w0 = tid < 64;
@@ -1386,6 +1513,19 @@ void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameB
     hipLaunchKernelGGL(k_pyr_cone, dim3(ntiles, B), dim3(1024), lds, st, dP, fb, rects, ctab, tab_stride);
 }
 
+void launch_pyr_fast(const ExtractPlan* dP, const ExtractPlan& hP, int ntiles, size_t cone_lds, const FrameBufs& fb,
+                     int B, const ConeRect* rects, const int* ctab, int tab_stride, const CellGeom* cells,
+                     uint32_t* cand, int* cand_cnt, int* err, int* lvl_done, hipStream_t st) {
+    static bool attr = false;
+    if (!attr) {
+        (void)hipFuncSetAttribute((const void*)k_pyr_fast, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+        attr = true;
+    }
+    const size_t lds = std::max(cone_lds, kFastLdsBytes);
+    hipLaunchKernelGGL(k_pyr_fast, dim3(ntiles + hP.n_cells_total, B), dim3(1024), lds, st, dP, fb, rects, ctab,
+                       tab_stride, ntiles, cells, cand, cand_cnt, err, lvl_done);
+}
+
 void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,
                  uint32_t* cand, int* cand_cnt, int* err, hipStream_t st) {
     // more threads per cell while the cells alone cannot fill the chip (one frame: ~600 cells on
@@ -1422,11 +1562,11 @@ size_t octree_lds_bytes(const ExtractPlan& hP, const OctreeCfg& cfg) {
 
 void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const uint32_t* cand,
                    const int* cand_cnt, uint32_t* kscratch, uint16_t* nscratch, LevelKp* lvl_kp, int* lvl_cnt,
-                   int* lvl_nlap, const OctreeCfg& cfg, int* err, int B, hipStream_t st) {
+                   int* lvl_nlap, const OctreeCfg& cfg, int* err, int* lvl_done, int B, hipStream_t st) {
     const size_t lds = octree_lds_bytes(hP, cfg);
     dim3 grd(B, hP.n_levels, 1);
     hipLaunchKernelGGL(k_octree, grd, dim3(1024), lds, st, dP, cells, cand, cand_cnt, kscratch, nscratch, lvl_kp,
-                       lvl_cnt, lvl_nlap, cfg, err);
+                       lvl_cnt, lvl_nlap, cfg, err, lvl_done);
 }
 
 constexpr int kDescKpMaxSlots = 16384;

@@ -97,6 +97,7 @@ struct orbhip_ctx {
     DevBuf<uint32_t> d_cand, d_kscratch;
     DevBuf<uint16_t> d_nscratch;
     DevBuf<int> d_cand_cnt, d_lvl_cnt, d_lvl_nlap, d_err;
+    DevBuf<int> d_lvl_done;     // k_pyr_fast level counters (zeroed on allocation, reset by k_octree)
     DevBuf<uint64_t> d_mpart;   // matcher chunk partials (match_part_entries)
     DevBuf<int> d_msync;        // one-launch matcher counters (zeroed once, reset by every launch)
     DevBuf<double> d_bw;        // bag-of-words weights (host transform)
@@ -449,11 +450,17 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
     (void)hipGetLastError();   // clear a sticky error of an earlier, already-reported call
     int rc = ensure_batch(c, pl, B);
     if (rc) return rc;
+    {
+        const int* before = c->d_lvl_done.p;
+        HIPOK(c->d_lvl_done.ensure((size_t)B * P.n_levels));
+        if (c->d_lvl_done.p != before)
+            HIPOK(hipMemsetAsync(c->d_lvl_done.p, 0, sizeof(int) * (size_t)B * P.n_levels, st));
+    }
     GraphKey key;
     key.add(1).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
         .add((uint64_t)lap1).ptr(d_kps).ptr(d_desc).add((uint64_t)cap).ptr(d_n).ptr(d_mono).ptr(st).ptr(c->d_pyr.p)
         .ptr(c->d_cand.p).ptr(c->d_kscratch.p).ptr(c->d_nscratch.p).ptr(c->d_cand_cnt.p).ptr(c->d_lvl_kp.p)
-        .ptr(c->d_lvl_cnt.p).ptr(c->d_lvl_nlap.p).ptr(c->d_err.p);
+        .ptr(c->d_lvl_cnt.p).ptr(c->d_lvl_nlap.p).ptr(c->d_err.p).ptr(c->d_lvl_done.p);
     return c->graphs.run(key, st, c->timer.stage != 0, [&](hipStream_t st) -> int {
         FrameBufs fb;
         fb.in = d_imgs; fb.in_stride = stride; fb.in_fstride = fstride; fb.pyr = c->d_pyr.p;
@@ -465,22 +472,33 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
         static const size_t cone_max = std::getenv("ORBHIP_CONE_MAX_WG")
                                            ? (size_t)std::atol(std::getenv("ORBHIP_CONE_MAX_WG"))
                                            : (size_t)1024;
-        if (pl->cone_tiles && !no_cone && (size_t)B * pl->cone_tiles <= cone_max)
-            launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_cone_tab.p,
-                            pl->cone_tab_stride, st);
-        else
-            for (int l = 1; l < P.n_levels; l++)
-                launch_resize(pl->d_plan.p, P, fb, B, l, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p, pl->d_ybeta.p,
-                              st);
-        tm.end(1, st);
-        tm.begin(2, st);
-        launch_fast(pl->d_plan.p, P, pl->d_cells.p, fb, B, c->d_cand.p, c->d_cand_cnt.p, c->d_err.p, st);
-        tm.end(2, st);
+        // the cone and FAST in one launch (k_pyr_fast) only with ORBHIP_PYR_FAST=1: measured slower
+        // than the two launches ("k_pyr_fast")
+        const char* pf = std::getenv("ORBHIP_PYR_FAST");
+        const bool cone_path = pl->cone_tiles && !no_cone && (size_t)B * pl->cone_tiles <= cone_max;
+        if (cone_path && pf && pf[0] == '1') {
+            launch_pyr_fast(pl->d_plan.p, P, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_cone_tab.p,
+                            pl->cone_tab_stride, pl->d_cells.p, c->d_cand.p, c->d_cand_cnt.p, c->d_err.p,
+                            c->d_lvl_done.p, st);
+            tm.end(1, st);
+        } else {
+            if (cone_path)
+                launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_cone_tab.p,
+                                pl->cone_tab_stride, st);
+            else
+                for (int l = 1; l < P.n_levels; l++)
+                    launch_resize(pl->d_plan.p, P, fb, B, l, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p,
+                                  pl->d_ybeta.p, st);
+            tm.end(1, st);
+            tm.begin(2, st);
+            launch_fast(pl->d_plan.p, P, pl->d_cells.p, fb, B, c->d_cand.p, c->d_cand_cnt.p, c->d_err.p, st);
+            tm.end(2, st);
+        }
         OctreeCfg oc = pl->oct;
         oc.lap0 = lap0; oc.lap1 = lap1;
         tm.begin(3, st);
         launch_octree(pl->d_plan.p, P, pl->d_cells.p, c->d_cand.p, c->d_cand_cnt.p, c->d_kscratch.p, c->d_nscratch.p,
-                      c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, oc, c->d_err.p, B, st);
+                      c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, oc, c->d_err.p, c->d_lvl_done.p, B, st);
         tm.end(3, st);
         tm.begin(4, st);
         launch_desc(pl->d_plan.p, P, fb, c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, pl->d_disc.p, d_kps, d_desc,
