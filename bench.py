@@ -33,7 +33,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 STAGES = {1: "pyramid (k_pyr_cone | 7x k_resize)", 2: "k_fast_cells", 3: "k_octree", 4: "rBRIEF (k_desc_kp | k_desc)",
-          5: "k_match_top2", 6: "k_match_finish"}
+          5: "match (k_match_fused | k_match_top2)", 6: "k_match_finish"}
 
 
 def kernel_symbol(stage, batch):
@@ -41,7 +41,8 @@ def kernel_symbol(stage, batch):
     while B x tiles / keypoints leave the chip idle: orbhip_api.cpp run_extract, launch_desc)."""
     small = batch <= 4
     return {1: "k_pyr_cone" if small else "k_resize", 2: "k_fast_cells", 3: "k_octree",
-            4: "k_desc_kp" if small else "k_desc", 5: "k_match_top2", 6: "k_match_finish"}[stage]
+            4: "k_desc_kp" if small else "k_desc", 5: "k_match_fused" if small else "k_match_top2",
+            6: "k_match_finish"}[stage]
 
 
 def parse():
