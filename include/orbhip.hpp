@@ -238,6 +238,37 @@ private:
     }
 };
 
+// Camera front-end stream (orbhip_frontend_*): push device frames, read slots when needed.
+class FrameStream {
+public:
+    FrameStream(int w, int h, int frames_in_flight = 8, int device = 0, orbhip_orb_params prm = {1000, 1.2f, 8, 20, 7},
+                int th_low = 50, float nnratio = 0.9f, bool check_orientation = true) {
+        check(orbhip_frontend_create(&fe_, device, &prm, w, h, frames_in_flight, th_low, nnratio,
+                                     check_orientation ? 1 : 0),
+              "orbhip_frontend_create");
+    }
+    ~FrameStream() {
+        if (fe_) orbhip_frontend_destroy(fe_);
+    }
+    FrameStream(const FrameStream&) = delete;
+    FrameStream& operator=(const FrameStream&) = delete;
+    // returns the slot that will hold this frame's keypoints and its match to the previous frame
+    int push(const uint8_t* d_gray, int stride, int lap0 = 0, int lap1 = 1000) {
+        const int slot = orbhip_frontend_push(fe_, d_gray, stride, lap0, lap1);
+        check(slot, "orbhip_frontend_push");
+        return slot;
+    }
+    orbhip_frontend_slot view(int slot) const {
+        orbhip_frontend_slot v{};
+        check(orbhip_frontend_view(fe_, slot, &v), "orbhip_frontend_view");
+        return v;
+    }
+    void wait(int slot, void* stream = nullptr) const { check(orbhip_frontend_wait(fe_, slot, stream), "orbhip_frontend_wait"); }
+
+private:
+    orbhip_frontend* fe_ = nullptr;
+};
+
 }  // namespace orbhip
 
 #endif  // ORBHIP_HPP
