@@ -56,8 +56,10 @@ def parse():
     ap.add_argument("--lba-steps", type=int, default=20)
     ap.add_argument("--lba-batch", type=int, default=256)
     ap.add_argument("--gba-iters", type=int, default=10)
+    ap.add_argument("--cameras", type=int, default=1,
+                    help="independent C2 camera streams per GPU (the CPU baseline runs 16 frame streams)")
     ap.add_argument("--inflight", type=int, default=8,
-                    help="frames of the C2 stream in flight (pipelined batch-1 frames; 1 = strictly sequential)")
+                    help="frames in flight per camera (pipelined batch-1 frames; 1 = frame by frame)")
     return ap.parse_args()
 
 
@@ -219,42 +221,48 @@ class StreamC2:
 
 
 class FrontendC2:
-    """The same camera stream through the library's front-end (FrameStream, include/orbhip.h
-    orbhip_frontend_*): frame k extracted at batch 1 on context k % inflight, matched to frame
-    k - 1 with the same event hand-offs as StreamC2, the bookkeeping in C (one C call per frame).
-    The headline path; StreamC2 is its Python-side twin for the parity tests."""
+    """C2 through the library's front-end (FrameStream, include/orbhip.h orbhip_frontend_*):
+    `cameras` independent camera streams, the CPU baseline's layout (one frame stream per
+    thread), each a FrameStream with `inflight` frames in flight (1: frame by frame, no event
+    hand-offs), frames pushed round-robin from this host thread. Every frame: batch-1
+    ORBextractor::operator() + brute-force match to the same camera's previous frame, one C call.
+    The cameras replay the bench's 32-frame stream at different phases."""
     W, H, NF = 640, 480, 32
 
-    def __init__(self, rank, inflight=8):
+    def __init__(self, rank, inflight=1, cameras=1):
         import torch
         from orb_slam3_ros2_amd import ORBextractor
         from orb_slam3_ros2_amd.frontend import FrameStream
-        self.S = max(1, int(inflight))
-        self.fs = FrameStream(self.W, self.H, self.S, 1000, 1.2, 8, 20, 7, 50, 0.9, True)
+        self.S, self.C = max(1, int(inflight)), max(1, int(cameras))
+        self.fss = [FrameStream(self.W, self.H, self.S, 1000, 1.2, 8, 20, 7, 50, 0.9, True) for _ in range(self.C)]
         self.ext = ORBextractor(1000, 1.2, 8, 20, 7)   # level tables for the roofline bytes only
         self.frames_np = make_stream_frames(self.NF, self.W, self.H, 1000 * rank + 1)
         self.frames = torch.from_numpy(self.frames_np).to("cuda")
-        self.p_frames = [self.frames[i].data_ptr() for i in range(self.NF)]
-        self.push = self.fs.push_ptr
-        self.ctx0 = self.fs.context(0)
-        self.s, self.last = 0, -1
+        p = [self.frames[i].data_ptr() for i in range(self.NF)]
+        self.p_frames = [[p[(k + 5 * c) % self.NF] for k in range(self.NF)] for c in range(self.C)]
+        self.pushes = [fs.push_ptr for fs in self.fss]
+        self.ctx0 = self.fss[0].context(0)
+        self.s, self.last = 0, (0, -1)
         torch.cuda.synchronize()
 
     def step(self):
-        slot = self.push(self.p_frames[self.s % self.NF], self.W)
+        c, k = self.s % self.C, self.s // self.C
+        slot = self.pushes[c](self.p_frames[c][k % self.NF], self.W)
         if slot < 0:
             raise RuntimeError(f"orbhip_frontend_push: {slot}")
-        self.last = slot
+        self.last = (c, slot)
         self.s += 1
 
     def last_matches(self):
-        self.fs.wait(self.last)
-        return int(self.fs.view(self.last)["nmatch"].item())
+        c, slot = self.last
+        self.fss[c].wait(slot)
+        return int(self.fss[c].view(slot)["nmatch"].item())
 
     def mean_keypoints(self):
         import torch
         torch.cuda.synchronize()
-        ns = [int(self.fs.view(i)["n"].item()) for i in range(min(self.fs.slots, self.s))]
+        fs = self.fss[0]
+        ns = [int(fs.view(i)["n"].item()) for i in range(min(fs.slots, -(-self.s // self.C)))]
         return float(np.mean(ns)) if ns else 0.0
 
     def stage_bytes(self):
@@ -505,10 +513,10 @@ def main():
     import torch
     ws, rank, local = _dist_setup(args)
     K, W = args.steps, args.warmup
-    c2 = FrontendC2(rank, args.inflight)
-    prof = Profiler(c2.ctx0)   # the stage timers of context 0 (frames k % inflight == 0)
-    # the same stream one frame at a time: per-frame latency, and the kernels' own durations
-    seq = FrontendC2(rank, 1) if c2.S > 1 else c2
+    c2 = FrontendC2(rank, args.inflight, args.cameras)
+    prof = Profiler(c2.ctx0)   # the stage timers of camera 0's context 0
+    # one camera, one frame at a time: per-frame latency, and the kernels' own durations
+    seq = FrontendC2(rank, 1, 1) if (c2.S > 1 or c2.C > 1) else c2
     # ---- find the dominant kernel of the step (short calibration on the one-frame stream, where
     # an event pair around a kernel holds that kernel only; untimed) ----
     prof_s = Profiler(seq.ctx0)
@@ -549,6 +557,17 @@ def main():
         seq.step()
     torch.cuda.synchronize()
     seq_ms = 1e3 * (time.perf_counter() - t1) / K
+    # the CPU baseline's layout: 16 independent cameras, frame by frame each (no event hand-offs)
+    multi = FrontendC2(rank, 1, 16)
+    for _ in range(W):
+        multi.step()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    for _ in range(K):
+        multi.step()
+    torch.cuda.synchronize()
+    multi_fps = K / (time.perf_counter() - t2)
+    del multi
     # the dominant kernel's duration: with frames in flight an event pair around it also holds
     # the wait for a dispatch slot among the other queues' work, so the roofline takes it from
     # HIP events on the one-frame-at-a-time stream (what rocprofv3's kernel trace reports); the
@@ -577,12 +596,14 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (SURVEY.md 8d rectangles + sigma-4 noise; a camera panning over one static scene, seeded)",
-        "config": {"workload": "C2: 640x480, 8-level pyramid, 1000 feat/frame, FAST 20/7, batch=1 stream; "
-                               "ORBextractor::operator() + brute-force Hamming match to the previous frame",
-                   "frames_per_step": 1, "parallelism": f"replicas x{ws} (frame streams, no collective)",
-                   "frames_in_flight": c2.S,
+        "config": {"workload": "C2: 640x480, 8-level pyramid, 1000 feat/frame, FAST 20/7, batch=1 camera streams; "
+                               "ORBextractor::operator() + brute-force Hamming match to the camera's previous frame",
+                   "frames_per_step": 1,
+                   "parallelism": f"replicas x{ws} (no collective); {c2.C} camera streams per GPU, batch 1 each",
+                   "cameras": c2.C, "frames_in_flight_per_camera": c2.S,
                    "sequential_frame_latency_ms": round(seq_ms, 4),
                    "sequential_frames_per_s": round(1e3 / seq_ms, 1),
+                   "sixteen_cameras_frame_by_frame_frames_per_s": round(multi_fps, 1),
                    "host_submit_ms_per_frame": round(1e3 * t_enq / K, 4),
                    "keypoints_per_frame": round(nkp, 1), "matches_last_pair": nmatch},
         "roofline": {"kernel": STAGES[dom], "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,

@@ -115,6 +115,7 @@ struct orbhip_ctx {
     ProjWorkspace* proj = nullptr;
     StageTimer timer;
     GraphCache graphs;   // replays of repeated per-frame launch sequences (graph_cache.h)
+    int cone_tile = 0;   // k_pyr_cone tile edge in last-level pixels (0: 10, the one-frame latency optimum)
 };
 
 // ---------------------------------------------------------------------------
@@ -300,7 +301,7 @@ static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
     if (L > 1) {
         const LevelGeom& T = P.lv[L - 1];
         static const int ts_env = std::getenv("ORBHIP_CONE_TILE") ? std::atoi(std::getenv("ORBHIP_CONE_TILE")) : 0;
-        const int ts = ts_env > 0 ? ts_env : 10;
+        const int ts = ts_env > 0 ? ts_env : (c->cone_tile > 0 ? c->cone_tile : 10);
         const int ntx = (T.w + ts - 1) / ts, nty = (T.h + ts - 1) / ts;
         size_t lds_max = 0;
         std::vector<ConeRect> rects((size_t)ntx * nty * kMaxLevels);
@@ -1255,6 +1256,8 @@ int orbhip_test_cells(orbhip_ctx* c, int w, int h, int32_t* out6, int cap) {
 // bench) and one event that also marks the frame complete. Same kernels and results as the
 // one-frame calls; the host work per frame is one C call instead of the caller's bookkeeping.
 // ===========================================================================
+constexpr int kFrontendConeTile = 14;
+
 struct orbhip_frontend {
     int device = 0, w = 0, h = 0, S = 0, ns = 0, cap = 0;
     int th_low = 50, check_orientation = 1;
@@ -1299,8 +1302,12 @@ int orbhip_frontend_create(orbhip_frontend** out, int device, const orbhip_orb_p
     f->ns = frames_in_flight == 1 ? 2 : 2 * frames_in_flight;
     f->th_low = th_low; f->ratio = ratio; f->check_orientation = check_orientation;
     f->ctx.assign(f->S, nullptr);
-    for (int j = 0; j < f->S; j++)
+    for (int j = 0; j < f->S; j++) {
         if (int rc = orbhip_create(&f->ctx[j], device, params)) return rc;
+        // throughput plan: 14-pixel cone tiles (130 instead of 252 work-groups at 640x480) leave
+        // room for more frames on the chip at once, for ~4% more one-frame latency
+        f->ctx[j]->cone_tile = kFrontendConeTile;
+    }
     const int cap = orbhip_max_keypoints(f->ctx[0], w, h);
     if (cap <= 0) return cap < 0 ? cap : ORBHIP_ERR_UNSUPPORTED;
     f->cap = cap;
