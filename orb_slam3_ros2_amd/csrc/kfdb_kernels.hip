@@ -141,7 +141,8 @@ __device__ __forceinline__ float block_max_f32(float v, float* scratch) {
     return r;
 }
 
-// ordered compaction of flag[i] (i < n) into out (global), returns the count (block-uniform)
+// ordered compaction of flag[i] (i < n) into out (global), returns the count (block-uniform).
+// Ends in a barrier: the callers read entries other threads wrote.
 template <typename F>
 __device__ int block_compact(int n, F&& pred, int32_t* __restrict__ out, int* scratch) {
     int run = 0;
@@ -153,6 +154,7 @@ __device__ int block_compact(int n, F&& pred, int32_t* __restrict__ out, int* sc
         if (f) out[run + pos] = i;
         run += tot;
     }
+    __syncthreads();
     return run;
 }
 
