@@ -346,10 +346,10 @@ struct FastLds {
     int* woff;                      // [96] output offset of each 64-px word
     int* wsel;
     int* wtot;
-    uint16_t* clist;                // kWinMax^2 pair-test survivors (strength to compute)
+    uint16_t* clist;                // kClistCap pair-test survivors (strength to compute)
     int* ncand;
 };
-constexpr size_t kFastLdsBytes = 2 * kWinMax * kWinMax + 2 * 96 * 8 + 96 * 4 + 16 + 2 * kWinMax * kWinMax + 16;
+constexpr size_t kFastLdsBytes = 2 * kWinMax * kWinMax + 2 * 96 * 8 + 96 * 4 + 16 + 2 * kClistCap + 16;
 
 // SYNC (k_pyr_fast): a cell of level l > 0 first waits until every cone tile of the launch is
 // done, then reads its window device-coherent (sc1 loads: the tiles wrote it
@@ -486,13 +486,18 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
         int base = 0;
         if (lane == 0 && bal) base = atomicAdd(&ncand, __popcll(bal));
         base = __shfl(base, 0, 64);
-        if (pass) clist[base + __popcll(bal & lt)] = (uint16_t)p;
+        const int ci = base + __popcll(bal & lt);
+        if (pass && ci < P->clist_cap) clist[ci] = (uint16_t)p;
     }
     __syncthreads();
-    const int nc = ncand;
+    // dense: the list overflowed, so the strength and NMS passes walk every pixel instead (the
+    // pair test repeated; pixels that failed it hold m = 0 and are skipped by the NMS)
+    const bool dense = ncand > P->clist_cap;
+    const int nc = dense ? np : ncand;
     for (int i = tid; i < nc; i += NT) {
         int d[16];
-        const int mi = diffs(clist[i], d);
+        const int mi = diffs(dense ? i : clist[i], d);
+        if (dense && !fast_pair_test(d, t_lo)) continue;
         int m = fast_strength_d(d);
         if (m <= t_lo) m = 0;
         mv[mi] = (uint8_t)m;
@@ -502,7 +507,7 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     // ---- window-local strict 3x3 NMS at both thresholds, on the surviving pixels only; the
     // results are bits of a raster-order mask per threshold ----
     for (int i = tid; i < nc; i += NT) {
-        const int p = clist[i];
+        const int p = dense ? i : clist[i];
         const int py = small_div(p, inv_dc), px = p - py * dc;
         const uint8_t* c = &mv[(py + 1) * W2 + px + 1];
         const int m = c[0];
@@ -563,7 +568,7 @@ __global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict
     __shared__ unsigned long long bmask[2][96];
     __shared__ int woff[96];
     __shared__ int wsel, wtot;
-    __shared__ uint16_t clist[kWinMax * kWinMax];
+    __shared__ uint16_t clist[kClistCap];
     __shared__ int ncand;
     const FastLds LS{win, mv, bmask, woff, &wsel, &wtot, clist, &ncand};
     fast_cell_body<NT, false>(P, cells, fb, cand, cand_cnt, err, blockIdx.x, LS, nullptr, 0);

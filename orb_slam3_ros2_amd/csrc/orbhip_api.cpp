@@ -181,6 +181,9 @@ static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
     P.w = w; P.h = h; P.n_levels = L;
     P.ini_th = std::min(std::max(c->prm.ini_th_fast, 0), 255);
     P.min_th = std::min(std::max(c->prm.min_th_fast, 0), 255);
+    // ORBHIP_FAST_CLIST_CAP lowers the survivor list (tests force the dense FAST pass with 0)
+    const char* cap_env = getenv("ORBHIP_FAST_CLIST_CAP");   // read per plan (once per ctx and size)
+    P.clist_cap = cap_env ? std::min(std::max(atoi(cap_env), 0), kClistCap) : kClistCap;
     for (int i = 0; i < 7; i++) P.blurk[i] = c->blurk[i];
     // k_desc hard-codes these taps (GaussianBlur 7x7 sigma 2 is fixed in ORBextractor)
     static const int kTaps[7] = {18, 34, 48, 56, 48, 34, 18};

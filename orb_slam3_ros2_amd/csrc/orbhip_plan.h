@@ -34,6 +34,11 @@ struct CellGeom {
     int32_t slot_off;         // first candidate slot (per frame)
 };
 
+// k_fast_cells: pair-test survivors kept in LDS per cell. Typically 5-10% of a cell's <= 74 x 74
+// pixels pass; a cell with more (noise-like texture) takes the dense path. The cap keeps the
+// work-group at ~19 KB of LDS: 8 work-groups (32 waves) per CU at 256 threads, not 5
+constexpr int kClistCap = 2048;
+
 struct ExtractPlan {
     int w, h, n_levels;
     int n_cells_total, n_slots_total;   // per frame
@@ -43,6 +48,7 @@ struct ExtractPlan {
     int n_disc;
     int blurk[7];                       // bit-exact 7x7 sigma=2 taps, 8 fractional bits
     int max_cells_level;                // max cells of any level (octree LDS carve)
+    int clist_cap;                      // FAST survivors listed per cell (<= kClistCap; more -> dense pass)
     LevelGeom lv[kMaxLevels];
 };
 

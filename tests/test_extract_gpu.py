@@ -89,6 +89,20 @@ def test_uniform_noise(ext1000, oracle):
     _check(ext1000, oracle, rng.integers(0, 256, size=(480, 640), dtype=np.uint8))
 
 
+@pytest.mark.parametrize("cap", [0, 64])
+def test_fast_dense_pass(oracle, monkeypatch, cap):
+    """k_fast_cells keeps at most kClistCap pair-test survivors per cell in LDS; a cell with more
+    walks every pixel instead. A lowered cap (0: every cell, 64: the textured ones) forces that
+    dense pass on frames whose survivors fit the default list."""
+    monkeypatch.setenv("ORBHIP_FAST_CLIST_CAP", str(cap))
+    from orb_slam3_ros2_amd import ORBextractor
+    ext = ORBextractor(1000, 1.2, 8, 20, 7)   # a fresh context: the plan reads the cap
+    rng = np.random.default_rng(9)
+    for img in (synthetic_frame(3, 640, 480), rng.integers(0, 256, size=(480, 640), dtype=np.uint8),
+                (128 + rng.integers(-9, 10, size=(480, 640))).astype(np.uint8)):
+        assert _check(ext, oracle, img) > 0
+
+
 def test_low_contrast_uses_min_threshold(ext1000, oracle):
     """Cells with no corner at iniThFAST=20 fall back to minThFAST=7."""
     rng = np.random.default_rng(6)
