@@ -327,15 +327,17 @@ __device__ __forceinline__ int fast_strength_d(const int* d) {
 
 
 // Is the pixel a FAST corner candidate at threshold t? Necessary condition of a 9-arc: every
-// opposite pair (k, k+8) has at least one member beyond v +- t on the arc's side.
+// opposite pair (k, k+8) has at least one member beyond v +- t on the arc's side, i.e.
+// max_k min(d[k], d[k+8]) < -t (bright circle) or min_k max(d[k], d[k+8]) > t (dark). As
+// min/max chains (v_min3/v_max3) instead of 32 compares and their boolean reduction.
 __device__ __forceinline__ bool fast_pair_test(const int* d, int t) {
-    bool bright = true, dark = true;
+    int bright = -256, dark = 256;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        bright &= (d[k] < -t) | (d[k + 8] < -t);
-        dark &= (d[k] > t) | (d[k + 8] > t);
+        bright = max(bright, min(d[k], d[k + 8]));
+        dark = min(dark, max(d[k], d[k + 8]));
     }
-    return bright | dark;
+    return (bright < -t) | (dark > t);
 }
 
 // LDS of one FAST cell (static in k_fast_cells, carved from the dynamic buffer in k_pyr_fast)
