@@ -444,7 +444,7 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
         }
     }
     if (tid == 0) ncand = 0;
-    if (tid < 192) bmask[tid / 96][tid % 96] = 0ull;
+    for (int i = tid; i < 192; i += NT) bmask[i / 96][i % 96] = 0ull;
     __syncthreads();
     TR_PHASE(1, 0)
     const int t_ini = P->ini_th, t_min = P->min_th;
@@ -1546,6 +1546,8 @@ void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* c
         hipLaunchKernelGGL(k_fast_cells<1024>, grd, dim3(1024), 0, st, dP, cells, fb, cand, cand_cnt, err);
     else if (nt == 512)
         hipLaunchKernelGGL(k_fast_cells<512>, grd, dim3(512), 0, st, dP, cells, fb, cand, cand_cnt, err);
+    else if (nt == 128)   // A/B only (ORBHIP_FAST_NT=128)
+        hipLaunchKernelGGL(k_fast_cells<128>, grd, dim3(128), 0, st, dP, cells, fb, cand, cand_cnt, err);
     else
         hipLaunchKernelGGL(k_fast_cells<256>, grd, dim3(256), 0, st, dP, cells, fb, cand, cand_cnt, err);
 }
