@@ -376,7 +376,9 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wc = cg.wc, hc = cg.hc;
     int* cnt_out = cand_cnt + (int64_t)f * P->n_cells_total + cell;
-    if (cell == 0 && f == 0 && tid < 4) err[tid] = 0;   // the octree (next launch) reports here
+    // the octree (next launch) reports here; an agent-scope store, so that the reset cannot land
+    // after (and erase) a timeout bit another XCD's cell sets with atomicOr in the SYNC form
+    if (cell == 0 && f == 0 && tid < 4) __hip_atomic_store(&err[tid], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (wc <= 6 || hc <= 6) {
         if (tid == 0) *cnt_out = 0;
         return;

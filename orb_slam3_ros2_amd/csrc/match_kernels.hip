@@ -261,9 +261,13 @@ __global__ __launch_bounds__(1024) void k_match_finish(MatchView v, const uint2*
 //
 // Cross-workgroup hand-off without an agent-scope fence: on gfx950 a release fence at agent
 // scope is a buffer_wbl2 of the whole XCD L2 (~14 us measured here, the L2 still holds the
-// pyramid), so everything another workgroup reads goes through device-coherent atomics instead
-// (tentative matches by atomicExch, histogram and count by atomicAdd), a vmcnt(0) wait orders
-// them before the done-counter increment, and the last workgroup reads them back by atomics.
+// pyramid), so everything another workgroup reads goes through device-coherent forms instead
+// (every match[o] as an sc1 write-through store, histogram and count by atomicAdd), a vmcnt(0)
+// wait orders them before the done-counter increment, and the last workgroup reads them back
+// with sc1 loads (MI355X_MICROARCH.md, inter-workgroup visibility, "Valid forms": every store
+// of the handed-off words sc1 and drained before the counter, every load of them sc1). r01
+// stored the non-tentative match[o] plainly; the last workgroup then read stale words (the
+// previous frame's indices, or zeros) as bin-0 tentative matches.
 // sync: 64 ints per pair, zero before the first launch: [0] done counter, [1..30] histogram,
 // [31] match count; the last workgroup resets them.
 // ---------------------------------------------------------------------------
@@ -369,10 +373,16 @@ __global__ __launch_bounds__(1024) void k_match_fused(MatchView v, int th_low, f
                 if (bin == 30) bin = 0;
                 atomicAdd(&hist[bin], 1);
                 mt |= bin << 24;   // tentative: the last workgroup filters
-                (void)atomicExch(&match[o], mt);
-            } else {
-                match[o] = mt;     // final (no filter reads it)
             }
+            // With the rotation filter on, the last workgroup reads back EVERY match[o] of the
+            // pair, so every one of them (tentative, rejected -1 and all) leaves as an sc1
+            // write-through store: a plain store could still sit dirty in this XCD's L2 while the
+            // last workgroup, on another XCD, reads the buffer's previous contents. Without the
+            // filter nobody in this launch reads match[], and a plain store is enough.
+            if (check_orientation)
+                __hip_atomic_store(&match[o], mt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                match[o] = mt;
             if (ok) atomicAdd(&cnt, 1);
         }
     }
@@ -404,7 +414,7 @@ __global__ __launch_bounds__(1024) void k_match_fused(MatchView v, int th_low, f
     int c = 0;
     for (int qq = tid; qq < nq; qq += 1024) {
         const int64_t o = (int64_t)p * v.out_stride + qq;
-        int mt = atomicAdd(&match[o], 0);
+        int mt = __hip_atomic_load(&match[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1: written sc1 above
         if (mt >= 0) {
             const int bin = mt >> 24;
             mt &= 0xFFFFFF;

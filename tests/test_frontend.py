@@ -1,9 +1,12 @@
 """The camera front-end stream (include/orbhip.h orbhip_frontend_*, FrameStream): frames pushed
-through the pipelined device stream give exactly the per-frame results of the one-frame calls
-(batch extraction of the pair + the pair match, direct launches on the HIP null stream), for
-1, 3 and 8 frames in flight; frame 0 has no match; misuse is rejected."""
+through the pipelined device stream give exactly the oracle's per-frame results (extraction of
+the frame, brute-force match against the previous frame), and the same as the one-frame device
+calls, for 1, 3 and 8 frames in flight; frame 0 has no match; misuse is rejected."""
 import numpy as np
 import pytest
+
+from tests.helpers import diff_report, oracle_kps_to_struct
+from orb_slam3_ros2_amd._lib import KP_DTYPE
 
 pytestmark = pytest.mark.gpu
 
@@ -24,7 +27,7 @@ def _direct(ext, mt, frames, k, cap):
 
 
 @pytest.mark.parametrize("S", [1, 3, 8])
-def test_frontend_matches_one_frame_calls(S):
+def test_frontend_matches_oracle_and_one_frame_calls(S, oracle):
     import torch
     from orb_slam3_ros2_amd import FrameStream, ORBextractor, ORBmatcher
     from orb_slam3_ros2_amd.synthetic import synthetic_stream
@@ -39,6 +42,10 @@ def test_frontend_matches_one_frame_calls(S):
     ext = ORBextractor(1000, 1.2, 8, 20, 7)
     mt = ORBmatcher(0.9, True, ctx=ext.ctx)
     cap = fs.cap
+    host = frames.cpu().numpy()
+    okp = {}
+    for k in range(K - fs.slots - 1, K):
+        okp[k] = oracle.extract(host[k])
     for k in range(K - fs.slots, K):
         v = fs.view(slots[k])
         assert v["frame"] == k
@@ -49,6 +56,18 @@ def test_frontend_matches_one_frame_calls(S):
         assert int(v["nmatch"][0]) == int(nm[0]) and int(nm[0]) > 100, k
         for j, name in enumerate(("match", "best", "second")):
             assert torch.equal(v[name][:cq], mm[j, :cq]), (k, name)
+        # the oracle: this frame's extraction and its match against the previous frame
+        omono, ok6, od = okp[k]
+        gk = np.frombuffer(v["kps"][:c].cpu().numpy().tobytes(), KP_DTYPE)
+        gd = v["desc"][:c].cpu().numpy()
+        ok = oracle_kps_to_struct(ok6)
+        assert int(v["mono"][0]) == omono and np.array_equal(gk, ok) and np.array_equal(gd, od), \
+            (k, diff_report(gk, gd, ok, od))
+        _, pk6, pd = okp[k - 1]
+        on, om, ob, os_ = oracle.match_bf(pd, pk6[:, 3].astype(np.float32), od, ok6[:, 3].astype(np.float32),
+                                          50, 0.9, True)
+        assert int(v["nmatch"][0]) == on, k
+        assert np.array_equal(v["match"][:cq].cpu().numpy(), om), k
 
 
 def test_frontend_first_frame_and_misuse():

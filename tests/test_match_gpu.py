@@ -105,3 +105,87 @@ def test_pairs_device(oracle):
         qa = kps[p, :nq, 3].cpu().numpy(); ta = kps[p + 1, :nt, 3].cpu().numpy()
         on, om, ob, os_ = oracle.match_bf(q, qa, t, ta, 50, 0.9, True)
         assert int(nm[p]) == on and np.array_equal(mm[p, :nq].cpu().numpy(), om)
+
+
+def _extract_stream(B, seed):
+    import torch
+    from orb_slam3_ros2_amd import ORBextractor
+    from orb_slam3_ros2_amd.synthetic import synthetic_stream
+    ext = ORBextractor(1000)
+    frames = torch.from_numpy(synthetic_stream(B, 640, 480, seed)).to("cuda:0")
+    cap = ext.max_keypoints(640, 480)
+    dev = frames.device
+    kps = torch.zeros((B, cap, 6), dtype=torch.float32, device=dev)
+    desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
+    n = torch.zeros(B, dtype=torch.int32, device=dev)
+    mono = torch.zeros(B, dtype=torch.int32, device=dev)
+    ext.extract_batch_device(frames, kps, desc, n, mono)
+    torch.cuda.synchronize()
+    return ext, kps, desc, n, cap
+
+
+@pytest.mark.parametrize("fill", ["zeros", "bin0_indices", "previous_results", "word_ids"])
+def test_stale_output_buffers_vs_oracle(oracle, fill):
+    """Adversarial stale contents in the match/best/second outputs: the one-launch
+    matcher's last workgroup reads match[] back, so anything a plain store left behind in another
+    XCD's L2 would surface here as a bin-0 tentative match. Every pair is checked against the
+    oracle, never against another device path."""
+    import torch
+    from orb_slam3_ros2_amd import ORBmatcher
+    B = 6
+    ext, kps, desc, n, cap = _extract_stream(B, 4242)
+    mt = ORBmatcher(0.9, True, ctx=ext.ctx)
+    dev = kps.device
+    refs = []
+    for p in range(B - 1):
+        nq, nt = int(n[p]), int(n[p + 1])
+        q = desc[p, :nq].cpu().numpy(); t = desc[p + 1, :nt].cpu().numpy()
+        qa = kps[p, :nq, 3].cpu().numpy(); ta = kps[p + 1, :nt, 3].cpu().numpy()
+        refs.append(oracle.match_bf(q, qa, t, ta, 50, 0.9, True))
+    rng = np.random.default_rng(5)
+    for rep in range(3):
+        if fill == "zeros":
+            mm = torch.zeros((B - 1, cap), dtype=torch.int32, device=dev)
+        elif fill == "bin0_indices":   # non-negative indices with bits 24+ clear = bin-0 tentative matches
+            mm = torch.arange(cap, dtype=torch.int32, device=dev).repeat(B - 1, 1)
+        elif fill == "previous_results":   # the oracle's answer for a DIFFERENT pair
+            prev = np.full((B - 1, cap), -1, np.int32)
+            for p in range(B - 1):
+                om = refs[(p + 1 + rep) % (B - 1)][1]
+                prev[p, :len(om)] = om
+            mm = torch.from_numpy(prev).to(dev)
+        else:                          # random word ids (what bow_transform leaves in the ctx scratch)
+            mm = torch.from_numpy(rng.integers(0, 1 << 20, (B - 1, cap), dtype=np.int32)).to(dev)
+        bb = torch.full_like(mm, 7); ss = torch.full_like(mm, 3)
+        nm = torch.full((B - 1,), 12345, dtype=torch.int32, device=dev)
+        # one pair per launch (the C2 fused shape) and all pairs in one launch
+        for p in range(B - 1):
+            mt.match_pairs_device(kps[p:p + 2], desc[p:p + 2], n[p:p + 2], mm[p:p + 1], bb[p:p + 1], ss[p:p + 1],
+                                  nm[p:p + 1])
+        torch.cuda.synchronize()
+        for p in range(B - 1):
+            on, om, ob, os_ = refs[p]
+            nq = len(om)
+            assert int(nm[p]) == on, (fill, rep, p)
+            assert np.array_equal(mm[p, :nq].cpu().numpy(), om), (fill, rep, p)
+            assert np.array_equal(bb[p, :nq].cpu().numpy(), ob) and np.array_equal(ss[p, :nq].cpu().numpy(), os_)
+
+
+def test_match_bf_sequence_vs_oracle(oracle):
+    """The host match_bf reuses the context's device scratch for its outputs: a sequence of calls
+    over different pairs (each leaving its results behind for the next) and a DBoW2 transform in
+    between, every call against the oracle."""
+    from orb_slam3_ros2_amd import ORBextractor, ORBmatcher
+    from orb_slam3_ros2_amd.synthetic import synthetic_stream
+    ext = ORBextractor(1000)
+    mt = ORBmatcher(0.9, True, ctx=ext.ctx)
+    frames = synthetic_stream(8, 640, 480, 99)
+    out = [ext(f) for f in frames]
+    for k in range(1, len(out)):
+        _, ka, da = out[k - 1]
+        _, kb, db = out[k]
+        for ori in (True, False):
+            mt.mbCheckOrientation = ori
+            n, m, b, s = mt.match_bf(da, ka["angle"], db, kb["angle"])
+            on, om, ob, os_ = oracle.match_bf(da, ka["angle"], db, kb["angle"], 50, 0.9, ori)
+            assert n == on and np.array_equal(m, om) and np.array_equal(b, ob), (k, ori)
