@@ -48,8 +48,8 @@ def kernel_symbol(stage, batch):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--steps", type=int, default=200, help="timed steps (one frame per camera each)")
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-extra", action="store_true", help="skip the C3 / LBA extra lines")
     ap.add_argument("--c3-steps", type=int, default=10)
@@ -60,6 +60,8 @@ def parse():
                     help="independent C2 camera streams per GPU (the CPU baseline runs 16 frame streams)")
     ap.add_argument("--inflight", type=int, default=1,
                     help="frames in flight per camera (pipelined batch-1 frames; 1 = frame by frame)")
+    ap.add_argument("--extra-timeout", type=float, default=240.0,
+                    help="seconds for the extras (C3/C4/C5/8f) before the watchdog prints the headline")
     return ap.parse_args()
 
 
@@ -224,9 +226,11 @@ class FrontendC2:
     """C2 through the library's front-end (FrameStream, include/orbhip.h orbhip_frontend_*):
     `cameras` independent camera streams, the CPU baseline's layout (one frame stream per
     thread), each a FrameStream with `inflight` frames in flight (1: frame by frame, no event
-    hand-offs), frames pushed round-robin from this host thread. Every frame: batch-1
-    ORBextractor::operator() + brute-force match to the same camera's previous frame, one C call.
-    The cameras replay the bench's 32-frame stream at different phases."""
+    hand-offs). One step pushes ONE frame into EVERY camera (round-robin from this host thread),
+    so a step is `cameras` frames and a short timed region still runs the pipeline in steady
+    state. Every frame: batch-1 ORBextractor::operator() + brute-force match to the same
+    camera's previous frame, one C call. The cameras replay the bench's 32-frame stream at
+    different phases."""
     W, H, NF = 640, 480, 32
 
     def __init__(self, rank, inflight=1, cameras=1):
@@ -242,16 +246,24 @@ class FrontendC2:
         self.p_frames = [[p[(k + 5 * c) % self.NF] for k in range(self.NF)] for c in range(self.C)]
         self.pushes = [fs.push_ptr for fs in self.fss]
         self.ctx0 = self.fss[0].context(0)
-        self.s, self.last = 0, (0, -1)
+        self.k, self.last = 0, (0, -1)
         torch.cuda.synchronize()
 
-    def step(self):
-        c, k = self.s % self.C, self.s // self.C
-        slot = self.pushes[c](self.p_frames[c][k % self.NF], self.W)
+    @property
+    def frames_per_step(self):
+        return self.C
+
+    def push_one(self, c):
+        slot = self.pushes[c](self.p_frames[c][self.k % self.NF], self.W)
         if slot < 0:
             raise RuntimeError(f"orbhip_frontend_push: {slot}")
         self.last = (c, slot)
-        self.s += 1
+
+    def step(self):
+        """One frame into every camera."""
+        for c in range(self.C):
+            self.push_one(c)
+        self.k += 1
 
     def last_matches(self):
         c, slot = self.last
@@ -262,7 +274,7 @@ class FrontendC2:
         import torch
         torch.cuda.synchronize()
         fs = self.fss[0]
-        ns = [int(fs.view(i)["n"].item()) for i in range(min(fs.slots, -(-self.s // self.C)))]
+        ns = [int(fs.view(i)["n"].item()) for i in range(min(fs.slots, self.k))]
         return float(np.mean(ns)) if ns else 0.0
 
     def stage_bytes(self):
@@ -281,11 +293,12 @@ def stage_bytes(ext, w, h, n_kp, frames):
     return {k: v * frames for k, v in per.items()}
 
 
-def load_traffic(kernel_name):
-    """HBM bytes per launch of `kernel_name` from the committed PMC summary (separate rocprofv3
-    --pmc FETCH_SIZE / WRITE_SIZE passes of this bench, FETCH_SIZE doubled per the gfx950
-    correction in MI355X_MICROARCH.md); None when no summary is committed."""
-    path = os.path.join(ROOT, "profiles", "traffic.json")
+def load_traffic(kernel_name, regime="c2"):
+    """HBM bytes per launch of `kernel_name` from the committed PMC summary of the regime
+    (profiles/traffic_<regime>.json: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of
+    this bench's C2 stream or C3 batch, FETCH_SIZE doubled per the gfx950 correction in
+    MI355X_MICROARCH.md); None when no summary is committed."""
+    path = os.path.join(ROOT, "profiles", f"traffic_{regime}.json")
     try:
         with open(path) as f:
             d = json.load(f)
@@ -295,29 +308,41 @@ def load_traffic(kernel_name):
 
 
 class BatchC3:
+    """C3: 1280x720, a batch of B = 64 consecutive frames of one stream, extracted in one batched
+    call and matched pair by pair (i, i+1). With N ranks the batch is cut into contiguous slices
+    with a one-frame halo (sharding.frame_slice_with_halo): rank r extracts frames
+    [lo, hi_ext) and matches its own pairs; no collective. Every rank holds the same 64 frames."""
     W, H, B = 1280, 720, 64
 
-    def __init__(self, rank):
+    def __init__(self, rank=0, ws=1):
         import torch
         from orb_slam3_ros2_amd import ORBextractor, ORBmatcher
+        from orb_slam3_ros2_amd.sharding import frame_slice_with_halo
         self.ext = ORBextractor(1000, 1.2, 8, 20, 7)
         self.mt = ORBmatcher(0.9, True, ctx=self.ext.ctx)
         self.cap = self.ext.max_keypoints(self.W, self.H)
+        self.lo, self.hi, self.plo, self.phi = frame_slice_with_halo(self.B, rank, ws)
+        self.nb = self.hi - self.lo           # frames this rank extracts (halo included)
+        self.npairs = self.phi - self.plo      # pairs this rank owns (= nb - 1)
         dev = torch.device("cuda")
-        self.frames = torch.from_numpy(make_stream_frames(self.B, self.W, self.H, 5000 + 1000 * rank)).to(dev)
-        B, cap = self.B, self.cap
+        allf = make_stream_frames(self.B, self.W, self.H, 5000)
+        self.frames = torch.from_numpy(np.ascontiguousarray(allf[self.lo:self.hi])).to(dev)
+        B, cap = max(self.nb, 1), self.cap
         self.kps = torch.zeros((B, cap, 6), dtype=torch.float32, device=dev)
         self.desc = torch.zeros((B, cap, 32), dtype=torch.uint8, device=dev)
         self.n = torch.zeros(B, dtype=torch.int32, device=dev)
         self.mono = torch.zeros(B, dtype=torch.int32, device=dev)
-        self.mm = torch.zeros((3, B - 1, cap), dtype=torch.int32, device=dev)
-        self.nm = torch.zeros(B - 1, dtype=torch.int32, device=dev)
+        self.mm = torch.zeros((3, max(B - 1, 1), cap), dtype=torch.int32, device=dev)
+        self.nm = torch.zeros(max(B - 1, 1), dtype=torch.int32, device=dev)
         self.stream = torch.cuda.current_stream()
 
     def step(self):
+        if self.nb <= 0:
+            return
         self.ext.extract_batch_device(self.frames, self.kps, self.desc, self.n, self.mono, stream=self.stream)
-        self.mt.match_pairs_device(self.kps, self.desc, self.n, self.mm[0], self.mm[1], self.mm[2], self.nm,
-                                   stream=self.stream)
+        if self.nb > 1:
+            self.mt.match_pairs_device(self.kps, self.desc, self.n, self.mm[0], self.mm[1], self.mm[2], self.nm,
+                                       stream=self.stream)
 
 
 def timed(ws, fn, steps, warmup):
@@ -336,13 +361,38 @@ def timed(ws, fn, steps, warmup):
 # ---------------------------------------------------------------------------------------
 # CPU baseline: the oracle restatement on this host's cores (bounded sample)
 # ---------------------------------------------------------------------------------------
+def host_cpus():
+    """The host's CPUs: nproc (affinity), the cgroup CPU quota (cpu.max), the CPU model. The
+    baseline runs one thread per CPU this process may actually use = min(affinity, quota): on
+    the GPU box the container sees 256 hardware threads but its cgroup quota is 16 CPUs, so more
+    threads would only be throttled to the same 16 CPUs of time."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"usable": max(1, min(aff, quota or aff)), "nproc": aff, "cgroup_quota_cpus": quota, "model": model}
+
+
 def cpu_baseline(frames_np, budget_s=12.0):
     """Each CPU thread streams frames exactly like a GPU step: extract frame i, match it to
     frame i-1 (whose extraction was the previous step). frames/s = produced frames / wall."""
     from oracle import pyoracle as O
     O.lib()
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    cores = max(1, min(cores, 16))
+    cores = host_cpus()["usable"]
     nf = len(frames_np)
 
     def stream(start, count):
@@ -369,8 +419,7 @@ def cpu_baseline(frames_np, budget_s=12.0):
 
 def cpu_lba(prob, budget_s=8.0):
     from oracle import pyoracle as O
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    cores = max(1, min(cores, 16))
+    cores = host_cpus()["usable"]
     t0 = time.perf_counter()
     n1 = 0
     while time.perf_counter() - t0 < budget_s / 4:
@@ -387,11 +436,9 @@ def cpu_lba(prob, budget_s=8.0):
 
 def c5_gba(ws, rank, iters):
     """C5 GlobalBundleAdjustment (400 KF loop, 20k points, 80k obs, 20-KF co-visibility window).
-    With ORBHIP_C5_SHARDED=1 and N > 1: landmark shards over the ranks, the reduced camera system
-    summed with RCCL all-reduce (orbhip_ba_solve_sharded). Otherwise every rank solves the whole
-    problem (replicas, no collective): the multi-rank RCCL path is verified here only at one rank
-    plus the in-process shard model (tests/test_ba_sharded_gpu.py), so it is opt-in for the
-    driver's scaling runs. Every rank runs it; time = max over ranks of one solve."""
+    With N > 1: landmark shards over the ranks, the reduced camera system summed with an RCCL
+    all-reduce per LM trial (orbhip_ba_solve_sharded); ORBHIP_C5_SHARDED=0 runs
+    replicas instead (every rank the whole problem). Time = max over ranks of one solve."""
     import torch
     from orb_slam3_ros2_amd import Optimizer
     from orb_slam3_ros2_amd.sharding import shard_problem
@@ -399,7 +446,7 @@ def c5_gba(ws, rank, iters):
     prob, _ = synthetic_ba_problem(n_kf=400, n_pts=20000, layout="loop", window=20, seed=11)
     prob.iterations, prob.huber_delta = iters, float(np.sqrt(5.99))   # BundleAdjustment(bRobust)
     opt = Optimizer()
-    sharded = ws > 1 and os.environ.get("ORBHIP_C5_SHARDED", "0") == "1"
+    sharded = ws > 1 and os.environ.get("ORBHIP_C5_SHARDED", "1") != "0"
     if sharded:
         import torch.distributed as dist
         uid = [Optimizer.comm_unique_id() if rank == 0 else None]
@@ -508,17 +555,70 @@ def cpu_f8_tracking():
                 nnratio=0.8), 20), 4)}
 
 
-def main():
-    args = parse()
+def load_counters(kernel_name, regime):
+    """Instruction-mix counters of `kernel_name` from the committed PMC summary
+    (profiles/counters.json, written by tools/prof_summary.py counters from separate rocprofv3
+    --pmc passes of this bench): VALU / LDS / MFMA activity per launch and the fraction of the
+    chip's issue capacity they used over the kernel's duration; None when not committed."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "counters.json")) as f:
+            return json.load(f)["regimes"][regime].get(kernel_name)
+    except (OSError, KeyError, ValueError):
+        return None
+
+
+def _spawn_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: start N rank processes through torch.distributed.run
+    (one per GPU, 127.0.0.1 rendezvous) as CHILD processes and return their exit code. Runs
+    before anything touches the GPU (no exec from a GPU-initialised process)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+class Watchdog:
+    """Extras (C3/C4/C5/8f) run after the headline is measured. If one of them hangs (an RCCL
+    collective across ranks, say), the watchdog prints the line measured so far with the stage
+    that timed out and ends the process, so the driver never loses the headline."""
+
+    def __init__(self, out, rank, limit_s):
+        import threading
+        self.out, self.rank, self.stage, self.done = out, rank, "", False
+        self.t = threading.Timer(limit_s, self._fire)
+        self.t.daemon = True
+        self.t.start()
+
+    def _fire(self):
+        if self.done:
+            return
+        if self.rank == 0:
+            self.out.setdefault("extra", {})["timeout_in"] = self.stage
+            print(json.dumps(self.out), flush=True)
+        os._exit(0)
+
+    def disarm(self):
+        self.done = True
+        self.t.cancel()
+
+
+def c2_headline(args, ws, rank):
+    """C2 camera streams: K timed steps of one frame per camera, the dominant stage bracketed by
+    HIP events on its launch stream; then the strict batch-1 figure (one camera, one frame at a
+    time) and one camera with 8 frames in flight."""
     import torch
-    ws, rank, local = _dist_setup(args)
     K, W = args.steps, args.warmup
     c2 = FrontendC2(rank, args.inflight, args.cameras)
     prof = Profiler(c2.ctx0)   # the stage timers of camera 0's context 0
-    # one camera, one frame at a time: per-frame latency, and the kernels' own durations
-    seq = FrontendC2(rank, 1, 1) if (c2.S > 1 or c2.C > 1) else c2
-    # ---- find the dominant kernel of the step (short calibration on the one-frame stream, where
-    # an event pair around a kernel holds that kernel only; untimed) ----
+    seq = FrontendC2(rank, 1, 1)
+    # ---- the dominant kernel of the step (short calibration on the one-frame stream, where an
+    # event pair around a kernel holds that kernel only; untimed) ----
     prof_s = Profiler(seq.ctx0)
     stage_ms = {}
     for st in (1, 2, 3, 4, 5, 6):
@@ -529,7 +629,7 @@ def main():
         stage_ms[st] = ms / max(n, 1)
     prof_s.select(0)
     dom = max(stage_ms, key=stage_ms.get)
-    # ---- timed region: K steps, the dominant stage bracketed by HIP events on its stream ----
+    # ---- timed region ----
     for _ in range(W):
         c2.step()
     prof.select(dom)
@@ -537,95 +637,63 @@ def main():
     t0 = time.perf_counter()
     for _ in range(K):
         c2.step()
-    t_enq = time.perf_counter() - t0   # host time to submit the K frames (no blocking call inside)
+    t_enq = time.perf_counter() - t0   # host time to submit the frames (no blocking call inside)
     torch.cuda.synchronize()
     _barrier(ws)
     elapsed = _max_over_ranks(ws, time.perf_counter() - t0)
-    dom_ms, dom_n = prof.collect()
+    dom_ms_if, dom_n_if = prof.collect()
     prof.select(0)
-    frames_total = _sum_over_ranks(ws, float(K))
-    value = frames_total / elapsed
-    nkp = c2.mean_keypoints()
-    nmatch = c2.last_matches()
-    # the same stream strictly one frame at a time (no overlap): per-frame latency
-    if seq is not c2:
-        for _ in range(W):
-            seq.step()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    for _ in range(K):
+    frames_total = _sum_over_ranks(ws, float(K * c2.frames_per_step))
+    r = {"value": frames_total / elapsed, "elapsed": elapsed, "frames_per_step": c2.frames_per_step,
+         "cameras": c2.C, "inflight": c2.S, "host_submit_ms_per_frame": 1e3 * t_enq / (K * c2.frames_per_step),
+         "keypoints": c2.mean_keypoints(), "nmatch": c2.last_matches(), "stage_ms": stage_ms, "dom": dom}
+    # ---- strict batch 1: one camera, one frame at a time on one stream ----
+    K1 = max(K, 200)
+    for _ in range(W):
         seq.step()
     torch.cuda.synchronize()
-    seq_ms = 1e3 * (time.perf_counter() - t1) / K
-    # one camera with 8 frames in flight (event hand-offs between its contexts)
+    t1 = time.perf_counter()
+    for _ in range(K1):
+        seq.step()
+    torch.cuda.synchronize()
+    r["batch1_ms"] = 1e3 * (time.perf_counter() - t1) / K1
+    # ---- one camera, 8 frames in flight (event hand-offs between its contexts) ----
     one = FrontendC2(rank, 8, 1)
-    for _ in range(W):
+    for _ in range(max(W, 16)):
         one.step()
     torch.cuda.synchronize()
     t2 = time.perf_counter()
-    for _ in range(K):
+    for _ in range(K1):
         one.step()
     torch.cuda.synchronize()
-    one_fps = K / (time.perf_counter() - t2)
+    r["one_camera_inflight_fps"] = K1 / (time.perf_counter() - t2)
     del one
-    # the dominant kernel's duration: with frames in flight an event pair around it also holds
-    # the wait for a dispatch slot among the other queues' work, so the roofline takes it from
-    # HIP events on the one-frame-at-a-time stream (what rocprofv3's kernel trace reports); the
-    # in-flight figure is kept beside it
-    dom_avg_inflight_ms = dom_ms / max(dom_n, 1)
-    if seq is not c2:
-        prof_s.select(dom)
-        for _ in range(min(K, 300)):
-            seq.step()
-        torch.cuda.synchronize()
-        dom_ms, dom_n = prof_s.collect()
-        prof_s.select(0)
-    dom_avg_ms = dom_ms / max(dom_n, 1)
-    dom_bytes = c2.stage_bytes()[dom]
-    achieved = dom_bytes / (dom_avg_ms * 1e-3) / 1e9
-    out = {
-        "metric": "frames/sec ORB extract+match @640×480; KF/sec LocalBA (50 KF, 2k pts)",
-        "value": round(value, 2),
-        "unit": "frames/s",
-        "n_gpus": ws,
-        "steps": K,
-        "warmup": W,
-        "ms_per_step": round(1e3 * elapsed / K, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (SURVEY.md 8d rectangles + sigma-4 noise; a camera panning over one static scene, seeded)",
-        "config": {"workload": "C2: 640x480, 8-level pyramid, 1000 feat/frame, FAST 20/7, batch=1 camera streams; "
-                               "ORBextractor::operator() + brute-force Hamming match to the camera's previous frame",
-                   "frames_per_step": 1,
-                   "parallelism": f"replicas x{ws} (no collective); {c2.C} camera streams per GPU, batch 1 each",
-                   "cameras": c2.C, "frames_in_flight_per_camera": c2.S,
-                   "sequential_frame_latency_ms": round(seq_ms, 4),
-                   "sequential_frames_per_s": round(1e3 / seq_ms, 1),
-                   "one_camera_8_in_flight_frames_per_s": round(one_fps, 1),
-                   "host_submit_ms_per_frame": round(1e3 * t_enq / K, 4),
-                   "keypoints_per_frame": round(nkp, 1), "matches_last_pair": nmatch},
-        "roofline": {"kernel": STAGES[dom], "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                     "kernel_symbol": kernel_symbol(dom, 1),
-                     "traffic": load_traffic(kernel_symbol(dom, 1)),
-                     "algorithmic_bytes_per_launch": int(dom_bytes), "avg_launch_ms": round(dom_avg_ms, 5),
-                     "launches_timed": dom_n, "avg_launch_ms_in_flight": round(dom_avg_inflight_ms, 5),
-                     "stage_avg_ms_calibration": {STAGES[k]: round(v, 5) for k, v in stage_ms.items()}},
-    }
-    c5 = None
-    if not args.no_extra:
-        try:
-            c5 = c5_gba(ws, rank, args.gba_iters)
-        except Exception as e:   # never lose the headline line to the extra
-            c5 = {"c5_error": repr(e)[:200]}
-    if rank == 0 and not args.no_extra:
-        extra = dict(c5 or {})
-        c3 = BatchC3(rank)
-        t = timed(1, c3.step, args.c3_steps, 2)
-        extra["c3_1280x720_b64_extract_match_frames_per_s"] = round(c3.B * args.c3_steps / t, 1)
-        # C3 roofline: the batch regime is where the extractor can approach the HBM roof
+    # ---- the dominant kernel's duration on the one-frame stream (what rocprofv3's kernel trace
+    # reports); with frames in flight an event pair also holds the wait for a dispatch slot ----
+    prof_s.select(dom)
+    for _ in range(300):
+        seq.step()
+    torch.cuda.synchronize()
+    dom_ms, dom_n = prof_s.collect()
+    prof_s.select(0)
+    r["dom_avg_ms"] = dom_ms / max(dom_n, 1)
+    r["dom_n"] = dom_n
+    r["dom_avg_ms_in_flight"] = dom_ms_if / max(dom_n_if, 1)
+    r["dom_bytes"] = c2.stage_bytes()[dom]
+    r["frames_np"] = c2.frames_np
+    r["ctx"] = c2.ext.ctx
+    return r
+
+
+def c3_batch(args, ws, rank):
+    """C3 1280x720 B=64 extract + 63 pair matches; N > 1: halo slices (strong scaling of the
+    batch). frames/s = 64 x steps / max-over-ranks time."""
+    c3 = BatchC3(rank, ws)
+    t = timed(ws, c3.step, args.c3_steps, 2)
+    out = {"c3_1280x720_b64_extract_match_frames_per_s": round(c3.B * args.c3_steps / t, 1),
+           "c3_partition": f"{ws} contiguous slice(s) + 1-frame halo; rank {rank}: frames [{c3.lo},{c3.hi}), "
+                           f"pairs [{c3.plo},{c3.phi})"}
+    if rank == 0:
         p3 = Profiler(c3.ext.ctx)
         c3_ms = {}
         for st in (1, 2, 3, 4, 5, 6):
@@ -636,16 +704,56 @@ def main():
             c3_ms[st] = ms / max(n, 1)
         p3.select(0)
         d3 = max(c3_ms, key=c3_ms.get)
-        b3 = stage_bytes(c3.ext, c3.W, c3.H, float(c3.n.float().mean().item()) or 1000.0, c3.B)
+        b3 = stage_bytes(c3.ext, c3.W, c3.H, float(c3.n.float().mean().item()) or 1000.0, c3.nb)
         a3 = b3[d3] / (c3_ms[d3] * 1e-3) / 1e9
-        extra["c3_roofline"] = {"kernel": STAGES[d3], "bound": "hbm", "achieved": round(a3, 2),
-                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(a3 / HBM_PEAK_GBS, 5),
-                                "algorithmic_bytes_per_launch": int(b3[d3]), "avg_launch_ms": round(c3_ms[d3], 4),
-                                "stage_avg_ms": {STAGES[k]: round(v, 4) for k, v in c3_ms.items()}}
-        from orb_slam3_ros2_amd import Optimizer
-        from orb_slam3_ros2_amd.synthetic import synthetic_ba_problem
+        ks = kernel_symbol(d3, c3.nb)
+        out["c3_roofline"] = {"kernel": ks, "bound": "hbm", "achieved": round(a3, 2), "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": round(a3 / HBM_PEAK_GBS, 5),
+                              "traffic": load_traffic(ks, "c3"), "counters": load_counters(ks, "c3"),
+                              "algorithmic_bytes_per_launch": int(b3[d3]), "avg_launch_ms": round(c3_ms[d3], 4),
+                              "stage_avg_ms": {STAGES[k]: round(v, 4) for k, v in c3_ms.items()}}
+    return out
+
+
+FP64_MFMA_PEAK_TFS = 78.6   # MI355X FP64 matrix peak (AMD spec; the guide lists no fp64 row)
+
+
+def ba_cholesky_roofline(n, blocked):
+    """Live fp64 MFMA roofline of the dense Cholesky solve (n^3/3 + 2n^2 flops per LM
+    trial): a C4 / C5-sized SPD reduced camera system factored and solved by the same kernels the
+    LM loop launches, timed with HIP events around back-to-back launches."""
+    from orb_slam3_ros2_amd._lib import lib
+    rng = np.random.default_rng(3)
+    A = rng.standard_normal((n, n))
+    S = A @ A.T / n + np.eye(n) * 2.0
+    b = rng.standard_normal(n)
+    x = np.zeros(n)
+    ms = ctypes.c_float(0)
+    L = lib()
+    if blocked:
+        rc = L.orbhip_test_cholesky_blocked(S.ctypes.data, b.ctypes.data, x.ctypes.data, n, ctypes.byref(ms))
+        kern = "k_cb_diag + k_cb_panel + k_cb_update + k_cb_solve (dense S)"
+    else:
+        rc = L.orbhip_test_cholesky_reg(S.ctypes.data, b.ctypes.data, x.ctypes.data, n, 20, ctypes.byref(ms), None)
+        kern = "k_ba_chol_reg"
+    if rc != 0:
+        return {"error": rc}
+    err = float(np.abs(S @ x - b).max() / np.abs(b).max())
+    flops = n ** 3 / 3 + 2 * n * n
+    ach = flops / (ms.value * 1e-3) / 1e12
+    return {"kernel": kern, "bound": "mfma", "achieved": round(ach, 4), "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+            "frac": round(ach / FP64_MFMA_PEAK_TFS, 6), "n": n, "flops_per_launch": int(flops),
+            "avg_launch_ms": round(ms.value, 4), "residual": err,
+            "counters": load_counters(kern.split()[0], "c5" if blocked else "c4")}
+
+
+def c4_lba(args, ws, rank, ctx):
+    from orb_slam3_ros2_amd import Optimizer
+    from orb_slam3_ros2_amd.synthetic import synthetic_ba_problem
+    out = {}
+    opt = Optimizer(ctx=ctx)
+    if rank == 0:
         prob, _ = synthetic_ba_problem()
-        opt = Optimizer(ctx=c2.ext.ctx)
         r = None
         for _ in range(2):
             r = opt.LocalBundleAdjustment(prob)
@@ -653,28 +761,92 @@ def main():
         for _ in range(args.lba_steps):
             r = opt.LocalBundleAdjustment(prob)
         tl = time.perf_counter() - t0
-        extra["c4_lba_kf_per_s"] = round(args.lba_steps / tl, 2)
-        extra["c4_lba_ms"] = round(1e3 * tl / args.lba_steps, 3)
-        extra["c4_lba_trials"] = r.lm_trials
-        extra["c4_lba_chi2"] = [round(r.initial_chi2, 3), round(r.final_chi2, 3)]
-        # replicas: independent LBA problems (concurrent maps / agents) in one batched solve
-        probs = [synthetic_ba_problem(seed=100 + i)[0] for i in range(args.lba_batch)]
-        opt.solve_batch(probs)   # warm-up at full size (pinned staging grows once)
-        t0 = time.perf_counter()
-        rs = opt.solve_batch(probs)
-        tb = time.perf_counter() - t0
-        extra["c4_lba_batched_kf_per_s"] = round(len(probs) / tb, 1)
-        extra["c4_lba_batch"] = len(probs)
-        extra["c4_lba_batched_trials_mean"] = round(float(np.mean([x.lm_trials for x in rs])), 2)
-        extra.update(f8_tracking(c2.ext.ctx))
-        out["extra"] = extra
+        out.update({"c4_lba_kf_per_s": round(args.lba_steps / tl, 2), "c4_lba_ms": round(1e3 * tl / args.lba_steps, 3),
+                    "c4_lba_trials": r.lm_trials, "c4_lba_chi2": [round(r.initial_chi2, 3), round(r.final_chi2, 3)]})
+    # replicas: independent LBA problems (concurrent maps / agents) in one batched solve per rank
+    probs = [synthetic_ba_problem(seed=100 + 1000 * rank + i)[0] for i in range(args.lba_batch)]
+    opt.solve_batch(probs)   # warm-up at full size (pinned staging grows once)
+    _barrier(ws)
+    t0 = time.perf_counter()
+    rs = opt.solve_batch(probs)
+    _barrier(ws)
+    tb = _max_over_ranks(ws, time.perf_counter() - t0)
+    out["c4_lba_batched_kf_per_s"] = round(_sum_over_ranks(ws, float(len(probs))) / tb, 1)
+    out["c4_lba_batch_per_gpu"] = len(probs)
+    out["c4_lba_batched_trials_mean"] = round(float(np.mean([x.lm_trials for x in rs])), 2)
+    if rank == 0:
+        out["c4_roofline"] = ba_cholesky_roofline(294, blocked=False)
+        out["c5_roofline"] = ba_cholesky_roofline(2394, blocked=True)
+    return out
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_spawn_ranks(args))
+    ws, rank, local = _dist_setup(args)
+    if ws != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={ws}")
+    r = c2_headline(args, ws, rank)
+    K, W, dom = args.steps, args.warmup, r["dom"]
+    achieved = r["dom_bytes"] / (r["dom_avg_ms"] * 1e-3) / 1e9
+    ks = kernel_symbol(dom, 1)
+    host = host_cpus()
+    out = {
+        "metric": "frames/sec ORB extract+match @640×480; KF/sec LocalBA (50 KF, 2k pts)",
+        "value": round(r["value"], 2),
+        "unit": "frames/s",
+        "n_gpus": ws,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": round(1e3 * r["elapsed"] / K, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (SURVEY.md 8d rectangles + sigma-4 noise; a camera panning over one static scene, seeded)",
+        "batch1_frames_per_s": round(1e3 / r["batch1_ms"], 1),
+        "batch1_latency_ms": round(r["batch1_ms"], 4),
+        "config": {"workload": "C2: 640x480, 8-level pyramid, 1000 feat/frame, FAST 20/7, batch=1 per camera stream; "
+                               "ORBextractor::operator() + brute-force Hamming match to the camera's previous frame",
+                   "step": f"one frame on each of {r['cameras']} independent camera streams",
+                   "frames_per_step": r["frames_per_step"],
+                   "parallelism": f"replicas x{ws} (no collective); {r['cameras']} camera streams per GPU, batch 1 each",
+                   "cameras": r["cameras"], "frames_in_flight_per_camera": r["inflight"],
+                   "batch1_latency_ms": round(r["batch1_ms"], 4),
+                   "batch1_frames_per_s": round(1e3 / r["batch1_ms"], 1),
+                   "one_camera_8_in_flight_frames_per_s": round(r["one_camera_inflight_fps"], 1),
+                   "host_submit_ms_per_frame": round(r["host_submit_ms_per_frame"], 4),
+                   "keypoints_per_frame": round(r["keypoints"], 1), "matches_last_pair": r["nmatch"]},
+        "roofline": {"kernel": ks, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                     "traffic": load_traffic(ks, "c2"), "counters": load_counters(ks, "c2"),
+                     "algorithmic_bytes_per_launch": int(r["dom_bytes"]), "avg_launch_ms": round(r["dom_avg_ms"], 5),
+                     "launches_timed": r["dom_n"], "avg_launch_ms_in_flight": round(r["dom_avg_ms_in_flight"], 5),
+                     "stage_avg_ms_calibration": {STAGES[k]: round(v, 5) for k, v in r["stage_ms"].items()}},
+    }
+    if not args.no_extra:
+        wd = Watchdog(out, rank, args.extra_timeout)
+        extra = {}
+        for name, fn in (("c5", lambda: c5_gba(ws, rank, args.gba_iters)),
+                         ("c3", lambda: c3_batch(args, ws, rank)),
+                         ("c4", lambda: c4_lba(args, ws, rank, r["ctx"])),
+                         ("f8", lambda: f8_tracking(r["ctx"]) if rank == 0 else {})):
+            wd.stage = name
+            try:
+                extra.update(fn())
+            except Exception as e:   # never lose the headline line to an extra
+                extra[f"{name}_error"] = repr(e)[:200]
+            out["extra"] = extra
+        wd.disarm()
     if rank == 0 and ws == 1 and not args.no_cpu:
-        cb = cpu_baseline(c2.frames_np)
+        cb = cpu_baseline(r["frames_np"])
         out["cpu_baseline"] = {"value": round(cb["value"], 2), "unit": "frames/s", "cores": cb["cores"],
                                "kind": "port",
                                "sample": f"oracle/ C++ restatement (g++ -O3), {cb['frames']} frames of the bench's "
                                          f"640x480 stream, each extract + match to the previous frame, "
                                          f"{cb['cores']} threads (one frame stream per thread), {cb['wall']:.1f}s wall",
+                               "host": host,
                                "single_core_value": round(cb["single"], 2)}
         if "extra" in out:
             from orb_slam3_ros2_amd.synthetic import synthetic_ba_problem

@@ -184,6 +184,9 @@ def lib():
     L.orbhip_test_sincosf.argtypes = [vp, vp, vp, ctypes.c_int64]
     L.orbhip_test_sincosf_sweep.argtypes = [ctypes.c_uint32, ctypes.c_uint32, vp, vp]
     L.orbhip_test_sincosf_sweep.restype = ctypes.c_int64
+    # measurement hooks of the dense Cholesky (HIP events around back-to-back launches)
+    L.orbhip_test_cholesky_reg.argtypes = [vp, vp, vp, i32, i32, ctypes.POINTER(f32), vp]
+    L.orbhip_test_cholesky_blocked.argtypes = [vp, vp, vp, i32, ctypes.POINTER(f32)]
     _lib = L
     return L
 

@@ -52,3 +52,36 @@ def merge_results(prob, shard_results, bounds, edge_sets):
     r0 = shard_results[0]
     return BAResult(r0.pose_q, r0.pose_t, pts, chi2, dok, r0.initial_chi2, r0.final_chi2, r0.iterations_done,
                     r0.lm_trials)
+
+
+# ---------------------------------------------------------------------------------------------
+# Batched front-end (C3) over ranks: SURVEY.md §8e "Extract: contiguous batch slices, B/N per GPU;
+# Match: frame pairs (i, i+1) partitioned, each GPU also loads the first frame of the next slice".
+# ---------------------------------------------------------------------------------------------
+def frame_slices(B: int, nranks: int):
+    """Contiguous frame ranges [lo_r, hi_r) covering 0..B-1, sizes differing by at most one."""
+    if B < 0 or nranks < 1:
+        raise ValueError("frame_slices: B >= 0 and nranks >= 1")
+    base, extra = divmod(B, nranks)
+    lo, out = 0, []
+    for r in range(nranks):
+        hi = lo + base + (1 if r < extra else 0)
+        out.append((lo, hi))
+        lo = hi
+    return out
+
+
+def frame_slice_with_halo(B: int, rank: int, nranks: int):
+    """The rank's work for a B-frame extract + consecutive-pair match batch.
+
+    Returns (lo, hi_ext, pair_lo, pair_hi): the rank extracts frames [lo, hi_ext) — its own slice
+    plus a one-frame halo (the first frame of the next non-empty slice) — and owns the match pairs
+    (i, i+1) for i in [pair_lo, pair_hi). Every pair 0..B-2 is owned by exactly one rank and every
+    frame is extracted by its owner (halo frames a second time, by the previous rank). No
+    collective is needed: pairs never cross a slice boundary without the halo frame at hand.
+    """
+    lo, hi = frame_slices(B, nranks)[rank]
+    if hi <= lo:
+        return lo, lo, lo, lo
+    hi_ext = min(hi + 1, B)
+    return lo, hi_ext, lo, hi_ext - 1

@@ -6,10 +6,13 @@ every kernel launched directly."""
 import numpy as np
 import pytest
 
+from tests.helpers import oracle_kps_to_struct
+from orb_slam3_ros2_amd._lib import KP_DTYPE
+
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("graphs", [False, True])
-def test_pipelined_stream_matches_sequential(monkeypatch, graphs):
+def test_pipelined_stream_matches_sequential(monkeypatch, graphs, oracle):
     import torch
     import bench
     K = 75
@@ -21,6 +24,19 @@ def test_pipelined_stream_matches_sequential(monkeypatch, graphs):
         cur = (seq.s - 1) % seq.ns
         ref.append((int(seq.n[cur]), seq.kps[cur].clone(), seq.desc[cur].clone(), int(seq.nm[cur]),
                     seq.mm[cur].clone()))
+    # the sequential reference itself against the oracle (every stream frame of the last cycle)
+    okp = {}
+    for k in range(K - 9, K):
+        okp[k] = oracle.extract(seq.frames_np[k % seq.NF])
+    for k in range(K - 8, K):
+        n, kps, desc, nm, mm = ref[k]
+        _, ok6, od = okp[k]
+        gk = np.frombuffer(kps[:n].cpu().numpy().tobytes(), KP_DTYPE)
+        assert np.array_equal(gk, oracle_kps_to_struct(ok6)) and np.array_equal(desc[:n].cpu().numpy(), od), k
+        _, pk6, pd = okp[k - 1]
+        on, om, ob, os_ = oracle.match_bf(pd, pk6[:, 3].astype(np.float32), od, ok6[:, 3].astype(np.float32),
+                                          50, 0.9, True)
+        assert nm == on and np.array_equal(mm[0, :len(om)].cpu().numpy(), om), k
     if graphs:
         monkeypatch.setenv("ORBHIP_GRAPH", "1")
     for S in (1, 2, 4):

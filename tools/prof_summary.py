@@ -40,10 +40,10 @@ def per_kernel(src, counter):
     return acc
 
 
-def traffic(fetch_src, write_src, dst):
+def traffic(fetch_src, write_src, dst, regime="c2"):
     fe, wr = per_kernel(fetch_src, "FETCH_SIZE"), per_kernel(write_src, "WRITE_SIZE")
-    out = {"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes of "
-                     "`python3 bench.py --steps 100 --warmup 10 --no-cpu --no-extra`",
+    out = {"source": "rocprofv3 --kernel-trace --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate passes of "
+                     f"`python3 tools/pmc_workload.py {regime}` (tools/gpu_pmc.sh)",
            "correction": "FETCH_SIZE (KB) x 2 (gfx950 wide-read undercount) + WRITE_SIZE (KB); x1024 -> bytes",
            "kernels": {}}
     for k in sorted(set(fe) | set(wr)):
@@ -55,8 +55,83 @@ def traffic(fetch_src, write_src, dst):
     json.dump(out, open(dst, "w"), indent=1)
 
 
+def durations(trace_csv):
+    acc = defaultdict(list)
+    for r in csv.DictReader(open(trace_csv)):
+        acc[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
+    return acc
+
+
+SIMDS, CUS = 1024, 256
+FP64_MFMA_PEAK_TFS = 78.6
+
+
+def counters(pmc_dir, dst, regimes):
+    """VALU / LDS / MFMA activity per launch from the p1 / p2 passes of each regime.
+
+    Units (MI355X_MICROARCH.md, PMC slots and cycle constants): SQ_INSTS_* count wave-instructions;
+    SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count quad-cycles summed over waves;
+    GRBM_GUI_ACTIVE is the dispatch's GPU-busy cycles summed over the 8 XCDs (so / 8 = cycles).
+    Derived, chip-wide over the kernel's busy cycles C = GRBM_GUI_ACTIVE / 8:
+      valu_issue_frac = SQ_INSTS_VALU / (1024 SIMDs x C / 2)   a wave64 VALU op holds a SIMD-32 2 cycles
+      lds_issue_frac  = SQ_INSTS_LDS / (256 CUs x C)           one LDS instruction per CU per cycle
+      f64 MFMA TF/s   = SQ_INSTS_VALU_MFMA_MOPS_F64 x 512 / duration, against the 78.6 TF fp64 peak
+      stall split     = SQ_WAIT_ANY, SQ_WAIT_INST_ANY, SQ_ACTIVE_INST_ANY over SQ_WAVE_CYCLES
+    """
+    import glob
+    out = {"source": "rocprofv3 --kernel-trace --pmc, two SQ passes per regime (tools/gpu_pmc.sh); "
+                     "per-launch means over every dispatch of the kernel in the pass",
+           "definitions": counters.__doc__, "regimes": {}}
+    for rg in regimes:
+        res = {}
+        data = {}
+        for ps in ("p1", "p2"):
+            src = glob.glob(f"{pmc_dir}/{rg}_{ps}/**/*counter_collection.csv", recursive=True)
+            tr = glob.glob(f"{pmc_dir}/{rg}_{ps}/**/*kernel_trace.csv", recursive=True)
+            if not src:
+                continue
+            names = set(r["Counter_Name"] for r in csv.DictReader(open(src[0])))
+            for c in names:
+                for k, v in per_kernel(src[0], c).items():
+                    data.setdefault(k, {})[c] = sum(v) / len(v)
+            if tr and ps == "p1":
+                for k, v in durations(tr[0]).items():
+                    data.setdefault(k, {})["dur_s"] = sum(v) / len(v)
+        for k, d in data.items():
+            g = d.get("GRBM_GUI_ACTIVE", 0.0)
+            cyc = g / 8.0
+            e = {"duration_us": round(1e6 * d.get("dur_s", 0.0), 3), "busy_cycles": round(cyc, 1)}
+            for c in ("SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_SALU", "SQ_INSTS_VMEM", "SQ_INSTS_MFMA",
+                      "SQ_LDS_BANK_CONFLICT", "SQ_ACTIVE_INST_LDS", "SQ_INSTS_VALU_MFMA_MOPS_F64",
+                      "SQ_VALU_MFMA_BUSY_CYCLES"):
+                if c in d:
+                    e[c] = round(d[c], 1)
+            if cyc > 0:
+                if "SQ_INSTS_VALU" in d:
+                    e["valu_issue_frac"] = round(d["SQ_INSTS_VALU"] / (SIMDS * cyc / 2), 5)
+                if "SQ_INSTS_LDS" in d:
+                    e["lds_issue_frac"] = round(d["SQ_INSTS_LDS"] / (CUS * cyc), 5)
+            if d.get("SQ_ACTIVE_INST_LDS"):
+                e["lds_bank_conflict_per_active_lds_cycle"] = round(d.get("SQ_LDS_BANK_CONFLICT", 0) /
+                                                                     d["SQ_ACTIVE_INST_LDS"], 4)
+            if d.get("SQ_WAVE_CYCLES"):
+                wc = d["SQ_WAVE_CYCLES"]
+                e["wave_time_split"] = {"waiting": round(d.get("SQ_WAIT_ANY", 0) / wc, 4),
+                                        "issue_stalled": round(d.get("SQ_WAIT_INST_ANY", 0) / wc, 4),
+                                        "issuing": round(d.get("SQ_ACTIVE_INST_ANY", 0) / wc, 4)}
+            if d.get("SQ_INSTS_VALU_MFMA_MOPS_F64") and d.get("dur_s"):
+                tf = d["SQ_INSTS_VALU_MFMA_MOPS_F64"] * 512 / d["dur_s"] / 1e12
+                e["f64_mfma_tflops"] = round(tf, 4)
+                e["f64_mfma_frac_of_peak"] = round(tf / FP64_MFMA_PEAK_TFS, 6)
+            res[k] = e
+        out["regimes"][rg] = res
+    json.dump(out, open(dst, "w"), indent=1)
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3], *(sys.argv[4:5] or ["kernel stats"]))
+    elif sys.argv[1] == "counters":
+        counters(sys.argv[2], sys.argv[3], sys.argv[4:])
     else:
-        traffic(sys.argv[2], sys.argv[3], sys.argv[4])
+        traffic(sys.argv[2], sys.argv[3], sys.argv[4], *(sys.argv[5:6] or ["c2"]))
