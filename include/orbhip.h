@@ -92,6 +92,29 @@ int orbhip_extract_batch_device(orbhip_ctx* ctx, const uint8_t* d_imgs, int B, i
                                 int64_t frame_stride, int lap0, int lap1, orbhip_kp* d_kps, uint8_t* d_desc,
                                 int cap, int32_t* d_n, int32_t* d_mono, void* stream);
 
+/* ---- distorted pinhole camera -----------------------------------
+ * U:src/CameraModels/Pinhole (fx fy cx cy) + U:src/Frame.cc mDistCoef (k1 k2 p1 p2 [k3]), as the
+ * node's camera file gives them (R:config/Monocular/MilkV.yaml:10-25). k1 == 0 means no
+ * distortion (the reference's test: mDistCoef.at<float>(0) == 0). */
+typedef struct orbhip_pinhole {
+    float fx, fy, cx, cy;
+    float k1, k2, p1, p2, k3;
+} orbhip_pinhole;
+
+/* U:src/Frame.cc::Frame::UndistortKeyPoints: mvKeysUn from mvKeys through cv::undistortPoints
+ * (OpenCV 4.5.4, 5 fixed-point rounds, fp64), bit-exact. Host buffers; out may alias kps.
+ * k1 == 0: out = kps. Replaces the cv::undistortPoints call inside Frame(mono) after ExtractORB. */
+int orbhip_undistort_keypoints(orbhip_ctx* ctx, const orbhip_pinhole* cam, const orbhip_kp* kps, int n,
+                               orbhip_kp* out);
+/* The same on the device over an extraction batch: d_kps[b*cap + i] for i < d_n[b] -> d_out
+ * (may alias). Asynchronous on `stream` (NULL = the HIP null stream). */
+int orbhip_undistort_keypoints_device(orbhip_ctx* ctx, const orbhip_pinhole* cam, const orbhip_kp* d_kps,
+                                      const int32_t* d_n, int B, int cap, orbhip_kp* d_out, void* stream);
+/* U:src/Frame.cc::Frame::ComputeImageBounds: bounds = {mnMinX, mnMaxX, mnMinY, mnMaxY} from the
+ * undistorted image corners ({0, cols, 0, rows} when k1 == 0). These bounds define the 64 x 48
+ * frame grid the projection / initialisation searches use (orbhip_frame.min_x ...). */
+int orbhip_image_bounds(orbhip_ctx* ctx, const orbhip_pinhole* cam, int cols, int rows, float bounds[4]);
+
 /* ---- ingest (a23) -------------------------------------------------------------------
  * cv_bridge::toCvShare(bgr8 msg, MONO8) -> cvtColor(COLOR_BGR2GRAY) (R:src/imu_mono_realsense.cpp:298)
  * on the device, bit-exact: Y = (B*1868 + G*9617 + R*4899 + 2^13) >> 14. B frames of w x h

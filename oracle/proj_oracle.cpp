@@ -26,10 +26,12 @@
 //       histogram of pushes + ComputeThreeMaxima; vbPrevMatched updated for the survivors
 // Pose arithmetic: Sophus SE3f * p = q._transformVector(p) + t (Eigen, float); mRcw =
 // q.toRotationMatrix(); mOw = Twc.translation() = conj(q)._transformVector(-t). No FMA
-// contraction (-ffp-contract=off). Undistortion is the identity (mDistCoef k1 == 0, the
-// RealSense_D435i.yaml case): mvKeysUn = mvKeys, bounds [0, cols] x [0, rows].
+// contraction (-ffp-contract=off). The searches take mvKeysUn and the image bounds as given:
+// orc_undistort_keypoints / orc_image_bounds (end of file) compute them for a distorted pinhole
+// (R:config/Monocular/MilkV.yaml:22-25); with k1 == 0 they are mvKeys and [0, cols] x [0, rows].
 // PARITY UNPINNED by the reference (no fixtures upstream).
 // ============================================================================
+#include <algorithm>
 #include <climits>
 #include <cmath>
 #include <cstdint>
@@ -337,6 +339,74 @@ int orc_search_for_initialization(int n1, const void* kps1, const uint8_t* desc1
             prev[2 * i1 + 1] = F2.kps[matches12[i1]].y;
         }
     return nmatches;
+}
+
+// ---- distorted pinhole cameras (UndistortKeyPoints + image bounds) ----
+// U:src/Frame.cc::Frame::UndistortKeyPoints: if mDistCoef.at<float>(0) == 0, mvKeysUn = mvKeys;
+// else cv::undistortPoints(mat(N x 1, CV_32FC2), mat, K (float), mDistCoef (float k1 k2 p1 p2
+// [k3]), cv::Mat(), mK). OCV 4.5.4 imgproc/src/undistort.dispatch.cpp: undistortPoints(src, dst,
+// K, D, R, P) = the TermCriteria(MAX_ITER, 5, 0.01) overload -> cvUndistortPointsInternal, all in
+// double: x = (u - cx) * (1 / fx), 5 fixed-point rounds of
+//   r2 = x*x + y*y
+//   icdist = (1 + ((k7*r2 + k6)*r2 + k5)*r2) / (1 + ((k4*r2 + k1)*r2 + k0)*r2)   (icdist < 0: restart, stop)
+//   deltaX = 2*k2*x*y + k3*(r2 + 2*x*x) + k8*r2 + k9*r2*r2
+//   deltaY = k2*(r2 + 2*y*y) + 2*k3*x*y + k10*r2 + k11*r2*r2
+//   x = (x0 - deltaX) * icdist,  y = (y0 - deltaY) * icdist
+// then RR = P * I = K: u' = (fx*x + 0*y) + cx, v' = (0*x + fy*y) + cy, w = 1 / ((0*x + 0*y) + 1),
+// stored as float. The tilt matrices are the identity (k12 = k13 = 0) and drop out exactly.
+// Frame::ComputeImageBounds: the 4 corners (0,0), (cols,0), (0,rows), (cols,rows) undistorted;
+// mnMinX = min(x0, x2), mnMaxX = max(x1, x3), mnMinY = min(y0, y1), mnMaxY = max(y2, y3).
+static void undistort_one(float u_f, float v_f, const float cam[4], const float dist[5], float& xo, float& yo) {
+    double k[14] = {0};
+    for (int i = 0; i < 5; i++) k[i == 4 ? 4 : i] = (double)dist[i];   // k1 k2 p1 p2 k3 -> k[0..4]
+    const double fx = cam[0], fy = cam[1], cx = cam[2], cy = cam[3];
+    const double ifx = 1. / fx, ify = 1. / fy;
+    const double u = u_f, v = v_f;
+    double x = (u - cx) * ifx, y = (v - cy) * ify;
+    const double x0 = x, y0 = y;
+    for (int j = 0; j < 5; j++) {
+        const double r2 = x * x + y * y;
+        const double icdist = (1 + ((k[7] * r2 + k[6]) * r2 + k[5]) * r2) / (1 + ((k[4] * r2 + k[1]) * r2 + k[0]) * r2);
+        if (icdist < 0) {
+            x = (u - cx) * ifx;
+            y = (v - cy) * ify;
+            break;
+        }
+        const double deltaX = 2 * k[2] * x * y + k[3] * (r2 + 2 * x * x) + k[8] * r2 + k[9] * r2 * r2;
+        const double deltaY = k[2] * (r2 + 2 * y * y) + 2 * k[3] * x * y + k[10] * r2 + k[11] * r2 * r2;
+        x = (x0 - deltaX) * icdist;
+        y = (y0 - deltaY) * icdist;
+    }
+    const double xx = fx * x + 0.0 * y + cx;
+    const double yy = 0.0 * x + fy * y + cy;
+    const double ww = 1. / (0.0 * x + 0.0 * y + 1.0);
+    xo = (float)(xx * ww);
+    yo = (float)(yy * ww);
+}
+
+// cam = {fx, fy, cx, cy}; dist = {k1, k2, p1, p2, k3}. in/out: orbhip_kp records (out may alias in).
+void orc_undistort_keypoints(const void* in_kps, int n, const float* cam, const float* dist, void* out_kps) {
+    const proj::Kp* in = (const proj::Kp*)in_kps;
+    proj::Kp* out = (proj::Kp*)out_kps;
+    for (int i = 0; i < n; i++) {
+        proj::Kp k = in[i];
+        if (dist[0] != 0.0f) undistort_one(in[i].x, in[i].y, cam, dist, k.x, k.y);
+        out[i] = k;
+    }
+}
+
+void orc_image_bounds(int cols, int rows, const float* cam, const float* dist, float* bounds) {
+    if (dist[0] == 0.0f) {
+        bounds[0] = 0.0f; bounds[1] = (float)cols; bounds[2] = 0.0f; bounds[3] = (float)rows;
+        return;
+    }
+    float x[4], y[4];
+    const float cu[4] = {0.0f, (float)cols, 0.0f, (float)cols}, cv_[4] = {0.0f, 0.0f, (float)rows, (float)rows};
+    for (int i = 0; i < 4; i++) undistort_one(cu[i], cv_[i], cam, dist, x[i], y[i]);
+    bounds[0] = std::min(x[0], x[2]);
+    bounds[1] = std::max(x[1], x[3]);
+    bounds[2] = std::min(y[0], y[1]);
+    bounds[3] = std::max(y[2], y[3]);
 }
 
 }  // extern "C"

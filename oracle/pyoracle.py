@@ -68,6 +68,8 @@ def lib():
                                               c_float, _u8p, _i32p, _i32p]
         L.orc_search_for_initialization.argtypes = [c_int, vp, _u8p, c_int, vp, _u8p, c_float, c_float, c_float,
                                                     c_float, _f32p, c_int, c_float, c_int, _i32p]
+        L.orc_undistort_keypoints.argtypes = [vp, c_int, _f32p, _f32p, vp]
+        L.orc_image_bounds.argtypes = [c_int, c_int, _f32p, _f32p, _f32p]
         L.orc_kfdb_create.argtypes = [c_int, c_int]
         L.orc_kfdb_create.restype = vp
         L.orc_kfdb_destroy.argtypes = [vp]
@@ -277,6 +279,29 @@ def search_for_initialization(kps1, desc1, kps2, desc2, prev_matched, window=100
         np.ascontiguousarray(desc2, np.uint8).reshape(-1, 32), *[float(b) for b in bounds], prev, int(window),
         float(nnratio), int(check_orientation), m)
     return n, m, prev
+
+
+def _cam(camera):
+    """(fx, fy, cx, cy, k1, k2, p1, p2[, k3]) -> float32 cam[4], dist[5]."""
+    c = [float(v) for v in camera] + [0.0] * (9 - len(camera))
+    return np.array(c[:4], np.float32), np.array(c[4:9], np.float32)
+
+
+def undistort_keypoints(kps, camera):
+    """Frame::UndistortKeyPoints (cv::undistortPoints, 5 iterations): orbhip_kp records -> mvKeysUn."""
+    k = np.ascontiguousarray(kps).copy()
+    cam, dist = _cam(camera)
+    out = k.copy()
+    lib().orc_undistort_keypoints(_vp(k), k.shape[0], cam, dist, _vp(out))
+    return out
+
+
+def image_bounds(cols, rows, camera):
+    """Frame::ComputeImageBounds -> (mnMinX, mnMaxX, mnMinY, mnMaxY)."""
+    cam, dist = _cam(camera)
+    b = np.zeros(4, np.float32)
+    lib().orc_image_bounds(int(cols), int(rows), cam, dist, b)
+    return tuple(float(v) for v in b)
 
 
 class KeyFrameDatabase:

@@ -30,7 +30,8 @@ from .optimizer import BAProblem, BAResult, Optimizer, PoseProblem, PoseResult  
 from .bow import ORBVocabulary  # noqa: F401
 from .kfdb import KeyFrameDatabase  # noqa: F401
 from .frontend import FrameStream  # noqa: F401
+from .camera import PinholeCamera  # noqa: F401
 
-__all__ = ["ORBextractor", "KeyPoint", "ORBmatcher", "Optimizer", "BAProblem", "BAResult", "PoseProblem", "PoseResult", "ORBVocabulary", "KeyFrameDatabase", "FrameStream",
+__all__ = ["ORBextractor", "KeyPoint", "ORBmatcher", "Optimizer", "BAProblem", "BAResult", "PoseProblem", "PoseResult", "ORBVocabulary", "KeyFrameDatabase", "FrameStream", "PinholeCamera",
            "OrbHipError",
            "lib", "library_path"]

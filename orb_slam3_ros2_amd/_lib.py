@@ -67,6 +67,12 @@ class PoseResultC(ctypes.Structure):
                 ("n_inliers", ctypes.c_int32), ("lm_trials", ctypes.c_int32)]
 
 
+class PinholeC(ctypes.Structure):
+    _fields_ = [("fx", ctypes.c_float), ("fy", ctypes.c_float), ("cx", ctypes.c_float), ("cy", ctypes.c_float),
+                ("k1", ctypes.c_float), ("k2", ctypes.c_float), ("p1", ctypes.c_float), ("p2", ctypes.c_float),
+                ("k3", ctypes.c_float)]
+
+
 class FrameC(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int32), ("kps", ctypes.c_void_p), ("desc", ctypes.c_void_p), ("claimed", ctypes.c_void_p),
                 ("min_x", ctypes.c_float), ("max_x", ctypes.c_float), ("min_y", ctypes.c_float), ("max_y", ctypes.c_float),
@@ -110,7 +116,8 @@ EXPORTED = ["orbhip_abi_version", "orbhip_create", "orbhip_destroy", "orbhip_lev
             "orbhip_kfdb_create", "orbhip_kfdb_destroy", "orbhip_kfdb_add", "orbhip_kfdb_erase",
             "orbhip_kfdb_detect_relocalization", "orbhip_kfdb_detect_nbest",
             "orbhip_frontend_create", "orbhip_frontend_destroy", "orbhip_frontend_push", "orbhip_frontend_view",
-            "orbhip_frontend_wait", "orbhip_frontend_context"]
+            "orbhip_frontend_wait", "orbhip_frontend_context", "orbhip_undistort_keypoints",
+            "orbhip_undistort_keypoints_device", "orbhip_image_bounds"]
 
 
 def lib():
@@ -181,6 +188,9 @@ def lib():
     L.orbhip_frontend_view.argtypes = [vp, i32, vp]
     L.orbhip_frontend_wait.argtypes = [vp, i32, vp]
     L.orbhip_frontend_context.argtypes = [vp, i32, ctypes.POINTER(vp)]
+    L.orbhip_undistort_keypoints.argtypes = [vp, ctypes.POINTER(PinholeC), vp, i32, vp]
+    L.orbhip_undistort_keypoints_device.argtypes = [vp, ctypes.POINTER(PinholeC), vp, vp, i32, i32, vp, vp]
+    L.orbhip_image_bounds.argtypes = [vp, ctypes.POINTER(PinholeC), i32, i32, vp]
     L.orbhip_test_sincosf.argtypes = [vp, vp, vp, ctypes.c_int64]
     L.orbhip_test_sincosf_sweep.argtypes = [ctypes.c_uint32, ctypes.c_uint32, vp, vp]
     L.orbhip_test_sincosf_sweep.restype = ctypes.c_int64

@@ -534,6 +534,57 @@ int orbhip_bgr_to_gray_device(orbhip_ctx* c, const uint8_t* d_bgr, int B, int w,
     return ORBHIP_OK;
 }
 
+static bool valid_cam(const orbhip_pinhole* c) {
+    return c && c->fx != 0.0f && c->fy != 0.0f && std::isfinite(c->fx) && std::isfinite(c->fy);
+}
+
+int orbhip_undistort_keypoints(orbhip_ctx* c, const orbhip_pinhole* cam, const orbhip_kp* kps, int n, orbhip_kp* out) {
+    if (!c || !valid_cam(cam) || n < 0 || (n > 0 && (!kps || !out))) return ORBHIP_ERR_ARG;
+    if (n == 0) return ORBHIP_OK;
+    if (cam->k1 == 0.0f) {   // mvKeysUn = mvKeys
+        if (out != kps) std::memmove(out, kps, sizeof(orbhip_kp) * (size_t)n);
+        return ORBHIP_OK;
+    }
+    HIPOK(hipSetDevice(c->device));
+    HIPOK(c->d_kps.ensure((size_t)n));
+    hipStream_t st = c->stream;
+    HIPOK(hipMemcpyAsync(c->d_kps.p, kps, sizeof(orbhip_kp) * (size_t)n, hipMemcpyHostToDevice, st));
+    (void)hipGetLastError();
+    launch_undistort_kps(c->d_kps.p, nullptr, n, 1, n, *cam, c->d_kps.p, st);
+    HIPOK(hipGetLastError());
+    HIPOK(hipMemcpyAsync(out, c->d_kps.p, sizeof(orbhip_kp) * (size_t)n, hipMemcpyDeviceToHost, st));
+    HIPOK(hipStreamSynchronize(st));
+    return ORBHIP_OK;
+}
+
+int orbhip_undistort_keypoints_device(orbhip_ctx* c, const orbhip_pinhole* cam, const orbhip_kp* d_kps,
+                                      const int32_t* d_n, int B, int cap, orbhip_kp* d_out, void* stream) {
+    if (!c || !valid_cam(cam) || B < 0 || cap < 0 || (B > 0 && (!d_kps || !d_n || !d_out))) return ORBHIP_ERR_ARG;
+    if (B == 0 || cap == 0) return ORBHIP_OK;
+    HIPOK(hipSetDevice(c->device));
+    (void)hipGetLastError();
+    launch_undistort_kps(d_kps, d_n, 0, B, cap, *cam, d_out, (hipStream_t)stream);   // k1 == 0: a copy
+    HIPOK(hipGetLastError());
+    return ORBHIP_OK;
+}
+
+int orbhip_image_bounds(orbhip_ctx* c, const orbhip_pinhole* cam, int cols, int rows, float bounds[4]) {
+    if (!c || !valid_cam(cam) || cols <= 0 || rows <= 0 || !bounds) return ORBHIP_ERR_ARG;
+    if (cam->k1 == 0.0f) {
+        bounds[0] = 0.0f; bounds[1] = (float)cols; bounds[2] = 0.0f; bounds[3] = (float)rows;
+        return ORBHIP_OK;
+    }
+    HIPOK(hipSetDevice(c->device));
+    HIPOK(c->d_kps.ensure(4));   // 4 floats of scratch
+    hipStream_t st = c->stream;
+    (void)hipGetLastError();
+    launch_image_bounds(cols, rows, *cam, (float*)c->d_kps.p, st);
+    HIPOK(hipGetLastError());
+    HIPOK(hipMemcpyAsync(bounds, c->d_kps.p, 4 * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIPOK(hipStreamSynchronize(st));
+    return ORBHIP_OK;
+}
+
 int orbhip_create(orbhip_ctx** out, int device, const orbhip_orb_params* params) {
     if (!out) return ORBHIP_ERR_ARG;
     *out = nullptr;

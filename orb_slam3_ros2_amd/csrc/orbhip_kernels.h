@@ -104,6 +104,11 @@ void launch_search_bow(const BowSide& K, const BowSide& F, float ratio, int chec
 void launch_bgr2gray(const uint8_t* src, int B, int w, int h, int sstride, int64_t sfstride, uint8_t* dst, int dstride,
                      int64_t dfstride, hipStream_t st);
 
+// ---- distorted pinhole camera (Frame::UndistortKeyPoints / ComputeImageBounds) ----
+void launch_undistort_kps(const orbhip_kp* kps, const int32_t* n_arr, int n_fixed, int B, int cap,
+                          const orbhip_pinhole& cam, orbhip_kp* out, hipStream_t st);
+void launch_image_bounds(int cols, int rows, const orbhip_pinhole& cam, float* bounds, hipStream_t st);
+
 // ---- test hooks ----
 constexpr int kTraceStride = 16384;   // u64 per kernel id in the timing trace (orbhip_device.h)
 constexpr int kTraceKernels = 8;

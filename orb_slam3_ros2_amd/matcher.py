@@ -138,19 +138,21 @@ class ORBmatcher:
 
 
 class ProjFrame:
-    """The current Frame for projection matching (U:src/Frame.cc): keypoints (orbhip_kp records,
-    mvKeysUn = mvKeys for zero distortion), descriptors, claimed mask, image bounds, scale tables,
+    """The current Frame for projection matching (U:src/Frame.cc): keypoints (orbhip_kp records:
+    mvKeysUn — PinholeCamera.UndistortKeyPoints for a distorted camera, mvKeys otherwise),
+    descriptors, claimed mask, image bounds (Frame::ComputeImageBounds: PinholeCamera
+    .ComputeImageBounds, or [0, width] x [0, height] without distortion), scale tables,
     intrinsics and Tcw."""
 
     def __init__(self, kps, desc, pose_q, pose_t, fx, fy, cx, cy, width=640, height=480, scale_factor=1.2,
-                 n_levels=8, claimed=None):
+                 n_levels=8, claimed=None, bounds=None):
         self.kps = np.ascontiguousarray(kps, KP_DTYPE)
         self.desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
         self.claimed = None if claimed is None else np.ascontiguousarray(claimed, np.uint8)
         self.pose_q = np.asarray(pose_q, np.float32).reshape(4)
         self.pose_t = np.asarray(pose_t, np.float32).reshape(3)
         self.fx, self.fy, self.cx, self.cy = float(fx), float(fy), float(cx), float(cy)
-        self.bounds = (0.0, float(width), 0.0, float(height))
+        self.bounds = (0.0, float(width), 0.0, float(height)) if bounds is None else tuple(float(b) for b in bounds)
         sf = np.ones(n_levels, np.float32)
         for i in range(1, n_levels):
             sf[i] = np.float32(np.float64(sf[i - 1]) * np.float64(np.float32(scale_factor)))
