@@ -77,16 +77,17 @@ __device__ __forceinline__ double bcast64(double v) {
 // One 2x2-block Gaussian-elimination step on [D | X] (C layout: lane (cc, rg) holds D[rg + 4q][cc]
 // and X[rg + 4q][cc]), pivots J0 = 2P and J1 = 2P + 1: with the pivot block B = D[J0..J1][J0..J1],
 // rows r > J1 get [D | X][r] -= [D[r][J0] D[r][J1]] B^-1 [D | X][J0..J1]. Half the sequential steps
-// of scalar pivoting, same Schur complements. Rows J0, J1 cross lanes through the LDS scratch sc
-// (lane cc reads its 4 values with two 16-byte loads); columns J0, J1 come by DPP row_newbcast;
-// the block by readlane. The D entries left of / above the trailing block are not masked: they only
-// feed other such entries, never a later pivot or X. prm[3P..3P+2] receives the block's Cholesky
-// inverse [[s0, 0], [s1, s2]]; *ok is cleared on a non-positive-definite block.
+// of scalar pivoting, same Schur complements. Rows J0, J1 cross lanes through LDS (abd + 24, two
+// alternating 64-double buffers); columns J0, J1 come by DPP row_newbcast; the block by readlane. The D entries left of /
+// above the trailing block are not masked: they only feed other such entries, never a later pivot
+// or X. abd[3P..3P+2] receives the block's (a, b, det) for block_params; *ok is cleared on a
+// non-positive-definite block.
 template <int P>
-__device__ __forceinline__ void elim_block(double4_t& d, double4_t& xv, int rg, int cc, double* sc, double* prm,
-                                           bool& ok) {
+__device__ __forceinline__ void elim_block(double4_t& d, double4_t& xv, int rg, int cc, double* abd, bool& ok) {
     constexpr int J0 = 2 * P, J1 = 2 * P + 1, jq = J0 >> 2, r0 = J0 & 3, r1 = J1 & 3;
-    double* buf = sc + 64 * (P & 1);
+    // rows J0, J1 of [D | X] cross lanes through LDS (lane cc reads its 4 values with two 16-byte
+    // loads); measured faster than permlane16/32 broadcasts here (n = 294: 180 vs 198 us)
+    double* buf = abd + 24 + 64 * (P & 1);
     if (rg == r0) { buf[cc * 4 + 0] = d[jq]; buf[cc * 4 + 1] = xv[jq]; }
     if (rg == r1) { buf[cc * 4 + 2] = d[jq]; buf[cc * 4 + 3] = xv[jq]; }
     double u0[4], u1[4];
@@ -114,27 +115,39 @@ __device__ __forceinline__ void elim_block(double4_t& d, double4_t& xv, int rg, 
         xv[q] = fma(-m1, x1, fma(-m0, x0, xv[q]));
     }
     ok = ok && a > 0.0 && det > 0.0;
-    // s0 = 1/sqrt(a), s2 = 1/sqrt(det/a) = sqrt(a) sqrt(1/det): rsq + 2 Newton steps (no IEEE
-    // div/sqrt sequences on this single-wave chain)
-    double s0 = __builtin_amdgcn_rsq(a);
-    s0 = s0 * fma(-0.5 * a * s0, s0, 1.5);
-    s0 = s0 * fma(-0.5 * a * s0, s0, 1.5);
-    const double sc2 = det * s0 * s0;              // det / a
-    double s2 = __builtin_amdgcn_rsq(sc2);
-    s2 = s2 * fma(-0.5 * sc2 * s2, s2, 1.5);
-    s2 = s2 * fma(-0.5 * sc2 * s2, s2, 1.5);
+    // the block's Cholesky-inverse parameters are computed for all 8 blocks together after the
+    // elimination (block_params): only (a, b, det) leave the chain here
     if ((threadIdx.x & 63) == 0) {
-        prm[3 * P] = s0;
-        prm[3 * P + 1] = -b * s0 * s0 * s2;
-        prm[3 * P + 2] = s2;
+        abd[3 * P] = a;
+        abd[3 * P + 1] = b;
+        abd[3 * P + 2] = det;
     }
     __builtin_amdgcn_sched_barrier(0);   // keep each step's live range local (register budget)
 }
 
+// prm[3P..3P+2] = Cholesky inverse [[s0, 0], [s1, s2]] of pivot block P from its (a, b, det):
+// s0 = 1/sqrt(a), s2 = 1/sqrt(det/a), s1 = -b s0^2 s2; rsq + 2 Newton steps, one lane per block
+__device__ __forceinline__ void block_params(const double* abd, double* prm) {
+    const int lane = threadIdx.x & 63;
+    if (lane < 8) {
+        const double a = abd[3 * lane], b = abd[3 * lane + 1], det = abd[3 * lane + 2];
+        double s0 = __builtin_amdgcn_rsq(a);
+        s0 = s0 * fma(-0.5 * a * s0, s0, 1.5);
+        s0 = s0 * fma(-0.5 * a * s0, s0, 1.5);
+        const double sc2 = det * s0 * s0;              // det / a
+        double s2 = __builtin_amdgcn_rsq(sc2);
+        s2 = s2 * fma(-0.5 * sc2 * s2, s2, 1.5);
+        s2 = s2 * fma(-0.5 * sc2 * s2, s2, 1.5);
+        prm[3 * lane] = s0;
+        prm[3 * lane + 1] = -b * s0 * s0 * s2;
+        prm[3 * lane + 2] = s2;
+    }
+}
+
 template <int... P>
-__device__ __forceinline__ void elim_all(double4_t& d, double4_t& xv, int rg, int cc, double* sc, double* prm,
-                                         bool& ok, std::integer_sequence<int, P...>) {
-    (elim_block<P>(d, xv, rg, cc, sc, prm, ok), ...);
+__device__ __forceinline__ void elim_all(double4_t& d, double4_t& xv, int rg, int cc, double* abd, bool& ok,
+                                         std::integer_sequence<int, P...>) {
+    (elim_block<P>(d, xv, rg, cc, abd, ok), ...);
 }
 
 // Factor the diagonal tile held in d (C layout) with LDS scratch sc (128 doubles) and prm (24).
@@ -142,16 +155,19 @@ __device__ __forceinline__ void elim_all(double4_t& d, double4_t& xv, int rg, in
 // operand order (element (r, c) at ((r + 16 (c & 3)) * 4 + (c >> 2))), applies y_k <- Linv_k y_k,
 // and sets *bad on a non-positive-definite pivot block.
 __device__ __forceinline__ void diag_tile(double4_t d, double* __restrict__ Linv_k, double* __restrict__ yk,
-                                          double* __restrict__ sc, double* __restrict__ prm, int* bad) {
+                                          double* __restrict__ sc, double* __restrict__ prm, int* bad,
+                                          unsigned long long* tel = nullptr) {
     const int lane = threadIdx.x & 63, cc = lane & 15, rg = lane >> 4;
+    const unsigned long long te0 = tel ? __builtin_amdgcn_s_memtime() : 0;
     double4_t xv;
 #pragma unroll
     for (int q = 0; q < 4; q++) xv[q] = (rg + 4 * q == cc) ? 1.0 : 0.0;
     bool ok = true;
-    elim_all(d, xv, rg, cc, sc, prm, ok, std::make_integer_sequence<int, 8>{});
+    elim_all(d, xv, rg, cc, sc, ok, std::make_integer_sequence<int, 8>{});
+    if (tel) tel[0] += __builtin_amdgcn_s_memtime() - te0;
     wave_lds_sync();
-    const double ycc = yk[cc];
-    double yo[4];
+    block_params(sc, prm);
+    wave_lds_sync();
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         // row r = rg + 4q is row J0 (rg even) or J1 (rg odd) of block r / 2; an odd row needs X of
@@ -162,16 +178,25 @@ __device__ __forceinline__ void diag_tile(double4_t d, double* __restrict__ Linv
         const double xprev = mk64(sl[0], sh[0]);
         const double l = (rg & 1) ? fma(xv[q], prm[3 * P + 2], xprev * prm[3 * P + 1]) : xv[q] * prm[3 * P];
         Linv_k[(rg + 4 * q + 16 * (cc & 3)) * 4 + (cc >> 2)] = l;
-        yo[q] = row16_sum(l * ycc);   // (Linv_k y_k)[rg + 4q]
-        __builtin_amdgcn_sched_barrier(0);
     }
     wave_lds_sync();
-    if (cc == 0) {
+    // y_k <- Linv_k y_k: lane (r, h) sums columns 4h..4h+3 of row r from LDS, then two DPP levels
+    {
+        const int r = lane >> 2, h = lane & 3;
+        double sv = 0.0;
 #pragma unroll
-        for (int q = 0; q < 4; q++) yk[rg + 4 * q] = yo[q];
+        for (int j = 0; j < 4; j++) {
+            const int c = 4 * h + j;
+            sv = fma(Linv_k[(r + 16 * (c & 3)) * 4 + (c >> 2)], yk[c], sv);
+        }
+        sv += dpp64<0xB1>(sv);   // quad_perm [1,0,3,2]
+        sv += dpp64<0x4E>(sv);   // quad_perm [2,3,0,1]
+        wave_lds_sync();
+        if (h == 0) yk[r] = sv;
     }
     if (lane == 0 && !ok) *bad = 1;
     wave_lds_sync();
+    if (tel) tel[1] += __builtin_amdgcn_s_memtime() - te0;
 }
 
 // x_k <- Linv_k^T y_k in place (one wave)
@@ -193,7 +218,7 @@ __device__ __forceinline__ void apply_linv_t(const double* __restrict__ Linv_k, 
 
 size_t chol_reg_lds_bytes(int n) {
     const int T = (n + 15) / 16;
-    return sizeof(double) * (3 * (size_t)T * 256 + 16 * (size_t)T + 160 + 8);
+    return sizeof(double) * (3 * (size_t)T * 256 + 16 * (size_t)T + 176 + 8);
 }
 
 template <int MAXT>
@@ -202,7 +227,7 @@ __device__ __forceinline__ void chol_reg_solve(const double* __restrict__ S, con
                                                unsigned long long* __restrict__ dbg = nullptr) {
     // dbg (diagnostics): [0] load+diag0, [1] panels, [2] trailing, [3] backward, [4] diagonal
     // factorizations (summed over waves); accumulated in registers, written once at the end
-    unsigned long long tprev = 0, ph_acc[5] = {0, 0, 0, 0, 0};
+    unsigned long long tprev = 0, ph_acc[5] = {0, 0, 0, 0, 0}, tel[3] = {0, 0, 0};
     auto stamp = [&](int ph) {
         if (dbg) {
             const unsigned long long t = __builtin_amdgcn_s_memtime();
@@ -221,8 +246,8 @@ __device__ __forceinline__ void chol_reg_solve(const double* __restrict__ S, con
     double* Linv = Lpan + (size_t)T * 256;     // T x 256: Linv_k in operand order
     double* Dt = Linv + (size_t)T * 256;       // T x 256: diagonal tiles C_JJ (C layout, lane-contiguous)
     double* y = Dt + (size_t)T * 256;          // 16 T: y, then x in place
-    double* dsc = y + 16 * T;                  // diagonal-factorization scratch (128) + block params (24)
-    int* bad = (int*)(dsc + 160);
+    double* dsc = y + 16 * T;                  // diagonal-factorization scratch (24 + 128) + block params (24)
+    int* bad = (int*)(dsc + 176);
     // Off-diagonal tile (I > J), column-major index g, lives in slot g / 8 of wave g % 8. (I, J)
     // are walked incrementally in scalar registers: +8 rows, wrapping into the next columns
     // (column J holds rows J+1 .. T-1).
@@ -315,7 +340,8 @@ __device__ __forceinline__ void chol_reg_solve(const double* __restrict__ S, con
                 y_update(d1, k);
                 wave_lds_sync();
             }
-            diag_tile(dt, Linv + (size_t)d1 * 256, y + 16 * d1, dsc, dsc + 128, bad);
+            if (dbg) tel[2] += __builtin_amdgcn_s_memtime() - t0;
+            diag_tile(dt, Linv + (size_t)d1 * 256, y + 16 * d1, dsc, dsc + 152, bad, dbg ? tel : nullptr);
             if (dbg) ph_acc[4] += __builtin_amdgcn_s_memtime() - t0;
         }
         if (k >= 0) {
@@ -379,6 +405,9 @@ __device__ __forceinline__ void chol_reg_solve(const double* __restrict__ S, con
         if (wid == 0)
             for (int i = 0; i < 4; i++) dbg[i] = ph_acc[i];
         atomicAdd(&dbg[4], ph_acc[4]);
+        atomicAdd(&dbg[5], tel[2]);   // diag wave: tile update + y update before the factorization
+        atomicAdd(&dbg[6], tel[0]);   // elimination
+        atomicAdd(&dbg[7], tel[1] - tel[0]);   // parameters + Linv + y epilogue
         for (int i = 0; i < 5; i++) dbg[8 + 5 * wid + i] = ph_acc[i];
     }
     const int nb = *bad;

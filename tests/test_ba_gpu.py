@@ -141,3 +141,27 @@ def test_gba_c5_eight_landmark_shards_parity(opt, c5_case):
     res = opt.solve_shards_local([q[0] for q in parts])
     merged = merge_results(p, res, shard_bounds(p, 8), [q[3] for q in parts])
     _compare(merged, o, p)
+
+
+@pytest.mark.parametrize("n", [6, 30, 96, 150, 294, 304])
+def test_register_cholesky_solves_spd(n):
+    """The register-resident LL^T (ba_chol_reg.hip, the C4 solver) on random SPD systems, well and
+    badly conditioned (eigenvalues over 8 decades, like S + lambda I late in an LM run), against
+    numpy's fp64 solve: relative residual at rounding level."""
+    import ctypes
+    from orb_slam3_ros2_amd._lib import lib
+    L = lib()
+    rng = np.random.default_rng(n)
+    for cond in (1e2, 1e8):
+        Q, _ = np.linalg.qr(rng.normal(size=(n, n)))
+        ev = np.geomspace(1.0, cond, n) * 1e3
+        A = (Q * ev) @ Q.T
+        A = 0.5 * (A + A.T)
+        b = rng.normal(size=n)
+        x = np.zeros(n)
+        ms = ctypes.c_float(0)
+        rc = L.orbhip_test_cholesky_reg(A.ctypes.data, b.ctypes.data, x.ctypes.data, n, 1, ctypes.byref(ms), None)
+        assert rc == 0
+        ref = np.linalg.solve(A, b)
+        assert np.abs(A @ x - b).max() <= 1e-9 * np.abs(b).max() * cond / 1e2 + 1e-12
+        assert np.abs(x - ref).max() <= 1e-13 * cond * np.abs(ref).max()

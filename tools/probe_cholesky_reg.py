@@ -10,7 +10,7 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from orb_slam3_ros2_amd._lib import lib  # noqa: E402
 
-L = lib()
+L = ctypes.CDLL(os.environ["ORBHIP_PROBE_LIB"]) if os.environ.get("ORBHIP_PROBE_LIB") else lib()
 L.orbhip_test_cholesky_reg.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
 L.orbhip_test_cholesky.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
 for n in [int(a) for a in (sys.argv[1:] or ["6", "31", "100", "160", "240", "294", "304"])]:
@@ -30,6 +30,6 @@ for n in [int(a) for a in (sys.argv[1:] or ["6", "31", "100", "160", "240", "294
     ms2 = ctypes.c_float(0)
     L.orbhip_test_cholesky(A.ctypes.data, b.ctypes.data, x2.ctypes.data, n, ph.ctypes.data, ctypes.byref(ms2))
     print(f"n={n} rc={rc} reg {ms.value*1e3:.1f} us relerr={err:.2e} | lds-panel {ms2.value*1e3:.1f} us | reg cycles: load+diag0={phr[0]} panels={phr[1]} "
-          f"trailing={phr[2]} back={phr[3]} diag-sum={phr[4]} [elim={phr[6]} epilogue={phr[7]}]", flush=True)
+          f"trailing={phr[2]} back={phr[3]} diag-sum={phr[4]} [pre={phr[5]} elim={phr[6]} epilogue={phr[7]}]", flush=True)
     pw = phr[8:48].reshape(8, 5)
     print("   per wave [load, panel, trailing(+own diag), back, diag]:", pw.tolist(), flush=True)
