@@ -4,6 +4,16 @@
 
 namespace orbhip {
 
+// Per-problem Levenberg-Marquardt state of the device-driven solve (k_ba_ctl_*): the exact g2o
+// OptimizationAlgorithmLevenberg control flow, advanced one trial per slot on the device.
+enum : int { kPhBuild = 0, kPhTrial = 1, kPhDone = 2 };
+struct LmCtl {
+    double ni, currentChi, rho, initChi;
+    int phase, it, trials, qmax;
+    int nBad, errors_valid, pop, stop;
+    int iterations, early_stop, pad0, pad1;
+};
+
 struct BaArgs {
     int P, M, E, np, n;
     double fx, fy, cx, cy, delta;
@@ -22,11 +32,11 @@ struct BaArgs {
     double* e_rho1;    // E
     double* Hpp;       // np*36
     double* Hll;       // M*9
-    double* Hpl;       // E*18 (zero for edges of fixed poses)
+    double* e_lin;     // E*4: linearisation per edge: camera-frame point (x y z), robust weight w
+    double* R_lin;     // np*9: rotation of each optimised pose at the linearisation (row-major)
     double* b;         // n + 3M
     double* Dinv;      // M*9
     double* db;        // M*3
-    double* W;         // E*18
     double* S;         // n*n
     double* bs;        // n
     double* x;         // n + 3M
@@ -47,6 +57,7 @@ struct BaArgs {
     const int* items; int nitems;
     const int* fin; int nfin;
     double* Spart;
+    LmCtl* ctl;        // device-driven solve: this problem's LM state (nullptr: host-driven rounds)
 };
 
 }  // namespace orbhip

@@ -11,8 +11,9 @@ constexpr int kCbMaxN = 4096;   // largest n (6 x optimised keyframes) of the bl
 // S (n x n, row-major, lower triangle read, factor written in place), Lsave (1024 x ceil(n/32)
 // doubles), row_first (ceil(n/32) ints: first 32-column tile with a structural non-zero in each
 // 32-row tile). flag[0] = 1 on success, 0 on a non-positive pivot (x = 0). Asynchronous on st.
+// gate (device int, optional): every kernel returns unless *gate == kPhTrial (ba_args.h).
 void chol_blocked_solve(double* S, int n, double* Lsave, const double* bs, double* x, int* flag,
-                        const int* row_first, hipStream_t st);
+                        const int* row_first, hipStream_t st, const int* gate = nullptr);
 
 int chol_blocked_test(const double* A, const double* b, double* x, int n, float* ms);
 

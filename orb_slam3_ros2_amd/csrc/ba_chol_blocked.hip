@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "ba_chol.h"
+#include "ba_args.h"
 #include "ba_chol_blocked.h"
 #include "wave_f64.h"
 
@@ -50,15 +51,22 @@ __device__ __forceinline__ void cb_diag_forward(double* __restrict__ S, int n, i
     if (lane == 0 && bad) flag[0] = 0;
 }
 
+// gate: the device-driven LM rounds (ba_solver.hip) run a problem's solve only in its trial phase
+// (the phase word of its LmCtl); nullptr = always
+#define CB_GATE \
+    if (gate && *gate != kPhTrial) return;
+
 __global__ __launch_bounds__(64) void k_cb_diag(double* __restrict__ S, int n, int k0, double* __restrict__ Lsave,
-                                                double* __restrict__ x, int* __restrict__ flag) {
+                                                double* __restrict__ x, int* __restrict__ flag, const int* __restrict__ gate) {
+    CB_GATE
     __shared__ double Li[32 * 33 + 32];
     cb_diag_forward(S, n, k0, Li, Li + 32 * 33, Lsave, x, flag);
 }
 
 // x = bs (the forward substitution runs in x), flag = 1
 __global__ __launch_bounds__(256) void k_cb_init(const double* __restrict__ bs, double* __restrict__ x, int n,
-                                                 int* __restrict__ flag) {
+                                                 int* __restrict__ flag, const int* __restrict__ gate) {
+    CB_GATE
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < n) x[i] = bs[i];
     if (i == 0) flag[0] = 1;
@@ -66,7 +74,8 @@ __global__ __launch_bounds__(256) void k_cb_init(const double* __restrict__ bs, 
 
 __global__ __launch_bounds__(256) void k_cb_panel(double* __restrict__ S, int n, int k0,
                                                   const double* __restrict__ Lsave, const int* __restrict__ row_first,
-                                                  double* __restrict__ x) {
+                                                  double* __restrict__ x, const int* __restrict__ gate) {
+    CB_GATE
     __shared__ double Li[32 * 33];
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
     const double* Lp = Lsave + (size_t)(k0 / kCT) * 1024;
@@ -147,7 +156,9 @@ __device__ __forceinline__ void update_tile(double* __restrict__ S, int n, int k
 // 16w..16w+15 of the tile against all 64 columns (4 MFMA accumulators, K = 32)
 __global__ __launch_bounds__(256) void k_cb_update(double* __restrict__ S, int n, int k0,
                                                    const int* __restrict__ row_first, double* __restrict__ Lsave,
-                                                   double* __restrict__ x, int* __restrict__ flag) {
+                                                   double* __restrict__ x, int* __restrict__ flag,
+                                                   const int* __restrict__ gate) {
+    CB_GATE
     __shared__ double Bt[kUT * 34];   // the J rows of the panel; then the next diagonal block's scratch
     const int t0 = k0 + kCT;
     int tt = blockIdx.x;
@@ -182,7 +193,9 @@ __global__ __launch_bounds__(256) void k_cb_update(double* __restrict__ S, int n
 constexpr int kBackPre = 12;
 __global__ __launch_bounds__(1024) void k_cb_back(const double* __restrict__ S, int n,
                                                   const double* __restrict__ Lsave, double* __restrict__ x,
-                                                  const int* __restrict__ flag, const int* __restrict__ row_first) {
+                                                  const int* __restrict__ flag, const int* __restrict__ row_first,
+                                                  const int* __restrict__ gate) {
+    CB_GATE
     __shared__ double y[kCbMaxN];
     __shared__ double red[16 * 32];
     __shared__ double Lt[32 * 33];
@@ -258,20 +271,20 @@ __global__ __launch_bounds__(1024) void k_cb_back(const double* __restrict__ S, 
 }
 
 void chol_blocked_solve(double* S, int n, double* Lsave, const double* bs, double* x, int* flag,
-                        const int* row_first, hipStream_t st) {
-    hipLaunchKernelGGL(k_cb_init, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, bs, x, n, flag);
-    hipLaunchKernelGGL(k_cb_diag, dim3(1), dim3(64), 0, st, S, n, 0, Lsave, x, flag);
+                        const int* row_first, hipStream_t st, const int* gate) {
+    hipLaunchKernelGGL(k_cb_init, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, bs, x, n, flag, gate);
+    hipLaunchKernelGGL(k_cb_diag, dim3(1), dim3(64), 0, st, S, n, 0, Lsave, x, flag, gate);
     const int np_ = (n + kCT - 1) / kCT;
     for (int p = 0; p < np_; p++) {
         const int k0 = p * kCT, rest = n - (k0 + kCT);
         if (rest <= 0) break;
         hipLaunchKernelGGL(k_cb_panel, dim3((unsigned)((rest + 63) / 64)), dim3(256), 0, st, S, n, k0, Lsave,
-                           row_first, x);
+                           row_first, x, gate);
         const int T = (rest + kUT - 1) / kUT;
         hipLaunchKernelGGL(k_cb_update, dim3((unsigned)(T * (T + 1) / 2)), dim3(256), 0, st, S, n, k0, row_first,
-                           Lsave, x, flag);   // + the diagonal block of panel p + 1
+                           Lsave, x, flag, gate);   // + the diagonal block of panel p + 1
     }
-    hipLaunchKernelGGL(k_cb_back, dim3(1), dim3(1024), 0, st, S, n, Lsave, x, flag, row_first);
+    hipLaunchKernelGGL(k_cb_back, dim3(1), dim3(1024), 0, st, S, n, Lsave, x, flag, row_first, gate);
 }
 
 // test hook: solve A x = b (A dense SPD, n <= kCbMaxN) through the blocked path; ms = device time

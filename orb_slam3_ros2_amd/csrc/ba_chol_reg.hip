@@ -418,6 +418,7 @@ __device__ __forceinline__ void chol_reg_solve(const double* __restrict__ S, con
 template <int MT>
 __global__ __launch_bounds__(512) void k_ba_chol_reg(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     const BaArgs& a = args[act[blockIdx.x]];
+    if (a.ctl && a.ctl->phase != kPhTrial) return;   // device-driven rounds: not in a trial
     if (a.n == 0) {
         if (threadIdx.x == 0) a.flag[0] = 1;
         return;

@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cfloat>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -71,11 +72,21 @@ __device__ __forceinline__ void ba_xcd_map(int& bx, int& by) {
     ba_xcd_map(bx_, by_);                           \
     const BaArgs& a = args[act[by_]];
 
+// Device-driven rounds: a kernel runs for a problem only in the phase it belongs to (build:
+// linearisation; trial: Schur / solve / update / errors). Host-driven rounds (a.ctl == nullptr)
+// select problems through act[] alone.
+__device__ __forceinline__ bool in_phase(const BaArgs& a, int ph) { return !a.ctl || a.ctl->phase == ph; }
+#define BA_PHASE(ph) \
+    if (!in_phase(a, ph)) return;
+
 // ---------------------------------------------------------------------------
-// errors
+// errors (when: 0 always, 1 the build's stale-error refresh, 2 a trial's new state)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_ba_errors(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+__global__ __launch_bounds__(256) void k_ba_errors(const BaArgs* __restrict__ args, const int* __restrict__ act,
+                                                   int when) {
     BA_PROLOGUE
+    if (when == 1 && !(in_phase(a, kPhBuild) && (!a.ctl || !a.ctl->errors_valid))) return;
+    if (when == 2 && !in_phase(a, kPhTrial)) return;
     const int e = bx_ * blockDim.x + threadIdx.x;
     if (e >= a.E) return;
     const double* T = a.pose + 8 * a.e_pose[e];
@@ -102,44 +113,70 @@ __global__ __launch_bounds__(256) void k_ba_errors(const BaArgs* __restrict__ ar
     a.e_rho1[e] = r1;
 }
 
-// Jacobians of the error for edge e: A (2x3, point), B (2x6, pose [omega, upsilon])
-__device__ __forceinline__ void edge_jac(const BaArgs& a, int e, double A[6], double B[12]) {
+// Jacobians of EdgeSE3ProjectXYZ at the camera-frame point (x, y, z) of a pose with rotation R
+// (row-major). The (negated) projection Jacobian J has rows (j00, 0, j02) and (0, j11, j12):
+//   j00 = -fx / z, j02 = fx x / z^2, j11 = -fy / z, j12 = fy y / z^2
+// A (2x3, landmark) = J R, B (2x6, pose [omega, upsilon]) = J [ -[Pc]x | I ]:
+//   B = [[j02 y, j00 z - j02 x, -j00 y, j00, 0, j02], [j12 y - j11 z, -j12 x, j11 x, 0, j11, j12]].
+// The linearisation stores (x, y, z, w) per edge; every consumer (Schur, back-substitution)
+// rebuilds J, A and B from that record and the pose's R_lin, so Hpl_e = w B^T A (18 doubles per
+// edge) is never stored. These consumers are bound by L2 traffic, not flops: storing J too (64
+// instead of 32 bytes per edge) measured 20% slower at B = 256.
+__device__ __forceinline__ void proj_jac(double fx, double fy, double x, double y, double z, double j[4]) {
+    j[0] = -(fx / z);
+    j[1] = fx * x / (z * z);
+    j[2] = -(fy / z);
+    j[3] = fy * y / (z * z);
+}
+__device__ __forceinline__ void jac_ab(const double j[4], double x, double y, double z, const double R[9],
+                                       double A[6], double B[12]) {
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        A[c] = j[0] * R[c] + j[1] * R[6 + c];
+        A[3 + c] = j[2] * R[3 + c] + j[3] * R[6 + c];
+    }
+    B[0] = j[1] * y; B[1] = j[0] * z - j[1] * x; B[2] = -j[0] * y; B[3] = j[0]; B[4] = 0.0; B[5] = j[1];
+    B[6] = j[3] * y - j[2] * z; B[7] = -j[3] * x; B[8] = j[2] * x; B[9] = 0.0; B[10] = j[2]; B[11] = j[3];
+}
+
+// camera-frame point of edge e at the current state + the pose's rotation matrix
+__device__ __forceinline__ void edge_pc(const BaArgs& a, int e, double& x, double& y, double& z, double R[9]) {
     const double* T = a.pose + 8 * a.e_pose[e];
     const double* X = a.pts + 3 * a.e_pt[e];
     const DQ q = load_q(T);
-    double x, y, z;
     qrot(q, X[0], X[1], X[2], x, y, z);
     x += T[4]; y += T[5]; z += T[6];
-    double J[6];
-    J[0] = -(a.fx / z); J[1] = -0.0; J[2] = -(-a.fx * x / (z * z));
-    J[3] = -0.0; J[4] = -(a.fy / z); J[5] = -(-a.fy * y / (z * z));
-    double R[9];
     qtomat(q, R);
+}
+
+// A, B of edge e from its stored linearisation (e_lin) and its pose's R_lin (optimised poses only)
+__device__ __forceinline__ double lin_ab(const BaArgs& a, int e, int oi, double A[6], double B[12]) {
+    const double4 l = ((const double4*)a.e_lin)[e];
+    double j[4];
+    proj_jac(a.fx, a.fy, l.x, l.y, l.z, j);
+    double R[9];
 #pragma unroll
-    for (int r = 0; r < 2; r++)
-#pragma unroll
-        for (int c = 0; c < 3; c++)
-            A[3 * r + c] = J[3 * r] * R[c] + J[3 * r + 1] * R[3 + c] + J[3 * r + 2] * R[6 + c];
-    const double D[18] = {0, z, -y, 1, 0, 0, -z, 0, x, 0, 1, 0, y, -x, 0, 0, 0, 1};
-#pragma unroll
-    for (int r = 0; r < 2; r++)
-#pragma unroll
-        for (int c = 0; c < 6; c++)
-            B[6 * r + c] = J[3 * r] * D[c] + J[3 * r + 1] * D[6 + c] + J[3 * r + 2] * D[12 + c];
+    for (int k = 0; k < 9; k++) R[k] = a.R_lin[9 * oi + k];
+    jac_ab(j, l.x, l.y, l.z, R, A, B);
+    return l.w;
 }
 
 // ---------------------------------------------------------------------------
 // buildSystem
 // ---------------------------------------------------------------------------
+// one thread per landmark: Hll, b_l over all its edges; stores each edge's linearisation (Pc, w)
 __global__ __launch_bounds__(256) void k_ba_lin_points(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
+    BA_PHASE(kPhBuild)
     const int m = bx_ * blockDim.x + threadIdx.x;
     if (m >= a.M) return;
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};
     for (int k = a.pt_ptr[m]; k < a.pt_ptr[m + 1]; k++) {
         const int e = a.pt_edges[k];
-        double A[6], B[12];
-        edge_jac(a, e, A, B);
+        double x, y, z, R[9], j[4], A[6], B[12];
+        edge_pc(a, e, x, y, z, R);
+        proj_jac(a.fx, a.fy, x, y, z, j);
+        jac_ab(j, x, y, z, R, A, B);
         const double r1 = a.e_rho1[e], info = a.e_info[e];
         const double w = r1 * info;
         const double om0 = -info * a.e_err[2 * e] * r1, om1 = -info * a.e_err[2 * e + 1] * r1;
@@ -149,13 +186,7 @@ __global__ __launch_bounds__(256) void k_ba_lin_points(const BaArgs* __restrict_
 #pragma unroll
             for (int c = 0; c < 3; c++) H[3 * r + c] += w * (A[r] * A[c] + A[3 + r] * A[3 + c]);
         }
-        double* hp = a.Hpl + 18 * e;
-        if (a.opt[a.e_pose[e]] >= 0) {
-#pragma unroll
-            for (int r = 0; r < 6; r++)
-#pragma unroll
-                for (int c = 0; c < 3; c++) hp[3 * r + c] = w * (B[r] * A[c] + B[6 + r] * A[3 + c]);
-        }
+        ((double4*)a.e_lin)[e] = make_double4(x, y, z, w);
     }
 #pragma unroll
     for (int i = 0; i < 9; i++) a.Hll[9 * m + i] = H[i];
@@ -163,9 +194,11 @@ __global__ __launch_bounds__(256) void k_ba_lin_points(const BaArgs* __restrict_
     for (int r = 0; r < 3; r++) a.b[a.n + 3 * m + r] = bl[r];
 }
 
-// one wave per optimised pose: 21 upper Hpp terms + 6 b terms, lanes over the pose's edges
+// one wave per optimised pose: 21 upper Hpp terms + 6 b terms, lanes over the pose's edges; lane 0
+// keeps the pose's rotation at the linearisation (R_lin)
 __global__ __launch_bounds__(256) void k_ba_lin_poses(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
+    BA_PHASE(kPhBuild)
     const int i = bx_ * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (i >= a.np) return;
@@ -174,8 +207,10 @@ __global__ __launch_bounds__(256) void k_ba_lin_poses(const BaArgs* __restrict__
     for (int k = 0; k < 27; k++) acc[k] = 0;
     for (int k = a.ps_ptr[i] + lane; k < a.ps_ptr[i + 1]; k += 64) {
         const int e = a.ps_edges[k];
-        double A[6], B[12];
-        edge_jac(a, e, A, B);
+        double x, y, z, R[9], j[4], A[6], B[12];
+        edge_pc(a, e, x, y, z, R);
+        proj_jac(a.fx, a.fy, x, y, z, j);
+        jac_ab(j, x, y, z, R, A, B);
         const double r1 = a.e_rho1[e], info = a.e_info[e];
         const double w = r1 * info;
         const double om0 = -info * a.e_err[2 * e] * r1, om1 = -info * a.e_err[2 * e + 1] * r1;
@@ -201,6 +236,17 @@ __global__ __launch_bounds__(256) void k_ba_lin_poses(const BaArgs* __restrict__
             for (int c = r; c < 6; c++) { H[6 * r + c] = acc[t]; H[6 * c + r] = acc[t]; t++; }
         for (int r = 0; r < 6; r++) a.b[6 * i + r] = acc[21 + r];
     }
+    if (lane < 9 && a.ps_ptr[i] < a.ps_ptr[i + 1]) {   // the pose's rotation, as its edges used it
+        {
+            const int p = a.e_pose[a.ps_edges[a.ps_ptr[i]]];
+            double R[9];
+            qtomat(load_q(a.pose + 8 * p), R);
+            double r = R[0];
+#pragma unroll
+            for (int k = 1; k < 9; k++) r = lane == k ? R[k] : r;
+            a.R_lin[9 * i + lane] = r;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -221,11 +267,10 @@ __device__ __forceinline__ void inv3(const double m[9], double r[9]) {
     r[8] = (m[0] * m[4] - m[1] * m[3]) * id;
 }
 
-
-// one thread per landmark: setLambda on Hll, Dinv (Eigen 3x3 cofactor inverse), db = Dinv b_l,
-// and W = Hpl Dinv for the landmark's edges (edges of fixed poses keep W = 0)
+// one thread per landmark: setLambda on Hll, Dinv (Eigen 3x3 cofactor inverse), db = Dinv b_l
 __global__ __launch_bounds__(256) void k_ba_schur_points(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
+    BA_PHASE(kPhTrial)
     const int m = bx_ * blockDim.x + threadIdx.x;
     if (m >= a.M) return;
     const double lambda = *a.lambda;
@@ -238,26 +283,12 @@ __global__ __launch_bounds__(256) void k_ba_schur_points(const BaArgs* __restric
     const double* bl = a.b + a.n + 3 * m;
 #pragma unroll
     for (int r = 0; r < 3; r++) a.db[3 * m + r] = Di[3 * r] * bl[0] + Di[3 * r + 1] * bl[1] + Di[3 * r + 2] * bl[2];
-    for (int k = a.pt_ptr[m]; k < a.pt_ptr[m + 1]; k++) {
-        const int e = a.pt_edges[k];
-        if (a.opt[a.e_pose[e]] < 0) continue;
-        const double2* B2 = (const double2*)(a.Hpl + 18 * e);
-        double h[18];
-#pragma unroll
-        for (int i = 0; i < 9; i++) { const double2 v = B2[i]; h[2 * i] = v.x; h[2 * i + 1] = v.y; }
-        double w[18];
-#pragma unroll
-        for (int r = 0; r < 6; r++)
-#pragma unroll
-            for (int c = 0; c < 3; c++) w[3 * r + c] = h[3 * r] * Di[c] + h[3 * r + 1] * Di[3 + c] + h[3 * r + 2] * Di[6 + c];
-        double2* W2 = (double2*)(a.W + 18 * e);
-#pragma unroll
-        for (int i = 0; i < 9; i++) W2[i] = make_double2(w[2 * i], w[2 * i + 1]);
-    }
 }
 
-__global__ __launch_bounds__(256) void k_ba_zero_s(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+__global__ __launch_bounds__(256) void k_ba_zero_s(const BaArgs* __restrict__ args, const int* __restrict__ act,
+                                                   int always) {
     BA_PROLOGUE
+    if (!always) BA_PHASE(kPhTrial)
     const size_t nn = (size_t)a.n * a.n;
     double2* S2 = (double2*)a.S;
     for (size_t i = (size_t)bx_ * blockDim.x + threadIdx.x; i < nn / 2; i += (size_t)gridDim.x * blockDim.x)
@@ -265,48 +296,97 @@ __global__ __launch_bounds__(256) void k_ba_zero_s(const BaArgs* __restrict__ ar
     if (bx_ == 0 && threadIdx.x == 0 && (nn & 1)) a.S[nn - 1] = 0.0;
 }
 
-// One LANE per Schur work item (a chunk of at most kSchurChunk pairs of one 6x6 block): the 36
-// sums live in the lane's registers and each pair's W_a / Hpl_b rows (18 + 18 doubles, 16-byte
-// loads) are read exactly once, so the L1/L2 traffic is the operands themselves (the previous
-// wave-per-block form re-read every row once per output lane). S_ij -= sum W_a Hpl_b^T.
+// Two LANES per Schur work item (a chunk of pairs of one 6x6 block (i, j)): lane half h owns rows
+// 3h..3h+2 of the block, 18 sums in registers (the pair prologue is computed by both lanes: the
+// register budget, not the flops, bounds this kernel). Matrix-free: for a pair (a, b) of edges of
+// landmark m,
+//   W_a Hpl_b^T = Hpl_a Dinv_m Hpl_b^T = w_a w_b B_a^T (A_a Dinv_m A_b^T) B_b
+// with A, B rebuilt from the edges' stored (Pc, w) and the poses' R_lin: 17 doubles read per pair
+// (edge records + Dinv) instead of the 36 of stored W / Hpl blocks, and no W written per trial.
 __global__ __launch_bounds__(256) void k_ba_schur_items(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
-    const int it = bx_ * blockDim.x + threadIdx.x;
+    BA_PHASE(kPhTrial)
+    const int gt = bx_ * blockDim.x + threadIdx.x;
+    const int it = gt >> 1, h = gt & 1;
     if (it >= a.nitems) return;
     const int4 wi = ((const int4*)a.items)[it];
-    double s[36];
+    const int bi = a.blk_i[wi.z], bj = a.blk_j[wi.z];
+    double Ri[9], Rj[9];
 #pragma unroll
-    for (int k = 0; k < 36; k++) s[k] = 0.0;
+    for (int k = 0; k < 9; k++) { Ri[k] = a.R_lin[9 * bi + k]; Rj[k] = a.R_lin[9 * bj + k]; }
+    double s[18];
+#pragma unroll
+    for (int k = 0; k < 18; k++) s[k] = 0.0;
+    const double fx = a.fx, fy = a.fy;
     for (int k = wi.x; k < wi.y; k++) {
         const int2 pr = ((const int2*)a.blk_pairs)[k];
-        const double2* W2 = (const double2*)(a.W + 18 * pr.x);
-        const double2* H2 = (const double2*)(a.Hpl + 18 * pr.y);
-        double w[18], h[18];
+        const double4 la = ((const double4*)a.e_lin)[pr.x], lb = ((const double4*)a.e_lin)[pr.y];
+        const double* Di = a.Dinv + 9 * a.e_pt[pr.x];
+        // the projection Jacobians of both edges (proj_jac); A and B are used through their structure
+        double ja[4], jb[4];
+        proj_jac(fx, fy, la.x, la.y, la.z, ja);
+        proj_jac(fx, fy, lb.x, lb.y, lb.z, jb);
+        const double a00 = ja[0], a02 = ja[1], a11 = ja[2], a12 = ja[3];
+        const double b00 = jb[0], b02 = jb[1], b11 = jb[2], b12 = jb[3];
+        double T[6];   // A_a Dinv (2x3), A_a = [a00 Ri0 + a02 Ri2; a11 Ri1 + a12 Ri2]
 #pragma unroll
-        for (int i = 0; i < 9; i++) {
-            const double2 u = W2[i], v = H2[i];
-            w[2 * i] = u.x; w[2 * i + 1] = u.y;
-            h[2 * i] = v.x; h[2 * i + 1] = v.y;
+        for (int c = 0; c < 3; c++) {
+            const double d0 = Di[c], d1 = Di[3 + c], d2 = Di[6 + c];
+            const double r0 = Ri[0] * d0 + Ri[1] * d1 + Ri[2] * d2;
+            const double r1 = Ri[3] * d0 + Ri[4] * d1 + Ri[5] * d2;
+            const double r2 = Ri[6] * d0 + Ri[7] * d1 + Ri[8] * d2;
+            T[c] = a00 * r0 + a02 * r2;
+            T[3 + c] = a11 * r1 + a12 * r2;
+        }
+        const double ww = la.w * lb.w;
+        double C[4];   // w_a w_b A_a Dinv A_b^T (2x2)
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            const double jb0 = c == 0 ? b00 : b11, jb2 = c == 0 ? b02 : b12;
+            double ab[3];
+#pragma unroll
+            for (int q = 0; q < 3; q++) ab[q] = jb0 * Rj[3 * c + q] + jb2 * Rj[6 + q];
+#pragma unroll
+            for (int r = 0; r < 2; r++) C[2 * r + c] = ww * (T[3 * r] * ab[0] + T[3 * r + 1] * ab[1] + T[3 * r + 2] * ab[2]);
+        }
+        // B_b rows: [b02 y, b00 z - b02 x, -b00 y, b00, 0, b02], [b12 y - b11 z, -b12 x, b11 x, 0, b11, b12]
+        const double Bb0[6] = {b02 * lb.y, b00 * lb.z - b02 * lb.x, -b00 * lb.y, b00, 0.0, b02};
+        const double Bb1[6] = {b12 * lb.y - b11 * lb.z, -b12 * lb.x, b11 * lb.x, 0.0, b11, b12};
+        double CB0[6], CB1[6];   // C B_b (2x6)
+#pragma unroll
+        for (int c = 0; c < 6; c++) {
+            CB0[c] = C[0] * Bb0[c] + C[1] * Bb1[c];
+            CB1[c] = C[2] * Bb0[c] + C[3] * Bb1[c];
+        }
+        // this lane's rows of B_a^T: rows 3h..3h+2 of [a02 y, a00 z - a02 x, -a00 y, a00, 0, a02] and
+        // [a12 y - a11 z, -a12 x, a11 x, 0, a11, a12]
+        double u0[3], u1[3];
+        if (h == 0) {
+            u0[0] = a02 * la.y; u0[1] = a00 * la.z - a02 * la.x; u0[2] = -a00 * la.y;
+            u1[0] = a12 * la.y - a11 * la.z; u1[1] = -a12 * la.x; u1[2] = a11 * la.x;
+        } else {
+            u0[0] = a00; u0[1] = 0.0; u0[2] = a02;
+            u1[0] = 0.0; u1[1] = a11; u1[2] = a12;
         }
 #pragma unroll
-        for (int rr = 0; rr < 6; rr++)
+        for (int rr = 0; rr < 3; rr++)
 #pragma unroll
-            for (int cc = 0; cc < 6; cc++)
-                s[6 * rr + cc] -= w[3 * rr] * h[3 * cc] + w[3 * rr + 1] * h[3 * cc + 1] + w[3 * rr + 2] * h[3 * cc + 2];
+            for (int cc = 0; cc < 6; cc++) s[6 * rr + cc] -= u0[rr] * CB0[cc] + u1[rr] * CB1[cc];
     }
     if (wi.w < 0) {   // the block's only item: straight into S (both triangles)
-        const int i = a.blk_i[wi.z], j = a.blk_j[wi.z];
 #pragma unroll
-        for (int rr = 0; rr < 6; rr++)
+        for (int r = 0; r < 3; r++) {
+            const int rr = 3 * h + r;
 #pragma unroll
             for (int cc = 0; cc < 6; cc++) {
-                a.S[(size_t)(6 * i + rr) * a.n + 6 * j + cc] = s[6 * rr + cc];
-                a.S[(size_t)(6 * j + cc) * a.n + 6 * i + rr] = s[6 * rr + cc];
+                a.S[(size_t)(6 * bi + rr) * a.n + 6 * bj + cc] = s[6 * r + cc];
+                a.S[(size_t)(6 * bj + cc) * a.n + 6 * bi + rr] = s[6 * r + cc];
             }
+        }
     } else {
-        double2* dst = (double2*)(a.Spart + 36 * (size_t)wi.w);
+        double2* dst = (double2*)(a.Spart + 36 * (size_t)wi.w + 18 * h);
 #pragma unroll
-        for (int k = 0; k < 18; k++) dst[k] = make_double2(s[2 * k], s[2 * k + 1]);
+        for (int k = 0; k < 9; k++) dst[k] = make_double2(s[2 * k], s[2 * k + 1]);
     }
 }
 
@@ -314,6 +394,7 @@ __global__ __launch_bounds__(256) void k_ba_schur_items(const BaArgs* __restrict
 // sums in item order (fixed order: deterministic)
 __global__ __launch_bounds__(256) void k_ba_schur_fin(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
+    BA_PHASE(kPhTrial)
     const int f = bx_ * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (f >= a.nfin || lane >= 36) return;
@@ -326,19 +407,23 @@ __global__ __launch_bounds__(256) void k_ba_schur_fin(const BaArgs* __restrict__
     if (i != j) a.S[(size_t)(6 * j + cc) * a.n + 6 * i + rr] = s;
 }
 
+// one wave per optimised pose: b_schur = b_p - sum_e Hpl_e db, Hpl_e db = w B^T (A db)
 __global__ __launch_bounds__(256) void k_ba_schur_b(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
+    BA_PHASE(kPhTrial)
     const int i = bx_ * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (i >= a.np) return;
     double acc[6] = {0, 0, 0, 0, 0, 0};
     for (int k = a.ps_ptr[i] + lane; k < a.ps_ptr[i + 1]; k += 64) {
         const int e = a.ps_edges[k];
-        const double* h = a.Hpl + 18 * e;
+        double A[6], B[12];
+        const double w = lin_ab(a, e, i, A, B);
         const double* d = a.db + 3 * a.e_pt[e];
         const double d0 = d[0], d1 = d[1], d2 = d[2];
+        const double v0 = w * (A[0] * d0 + A[1] * d1 + A[2] * d2), v1 = w * (A[3] * d0 + A[4] * d1 + A[5] * d2);
 #pragma unroll
-        for (int r = 0; r < 6; r++) acc[r] += h[3 * r] * d0 + h[3 * r + 1] * d1 + h[3 * r + 2] * d2;
+        for (int r = 0; r < 6; r++) acc[r] += B[r] * v0 + B[6 + r] * v1;
     }
 #pragma unroll
     for (int r = 0; r < 6; r++) {
@@ -547,6 +632,7 @@ __device__ __forceinline__ void chol_solve(double* __restrict__ S, const double*
 
 __global__ __launch_bounds__(512) void k_ba_cholesky(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     const BaArgs& a = args[act[blockIdx.x]];
+    BA_PHASE(kPhTrial)
     if (a.n == 0) {
         if (threadIdx.x == 0) a.flag[0] = 1;
         return;
@@ -564,6 +650,7 @@ __global__ __launch_bounds__(512) void k_chol_test(double* S, const double* bs, 
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_ba_backsub(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
+    BA_PHASE(kPhTrial)
     const int m = bx_ * blockDim.x + threadIdx.x;
     if (m >= a.M) return;
     const double* bl = a.b + a.n + 3 * m;
@@ -572,12 +659,15 @@ __global__ __launch_bounds__(256) void k_ba_backsub(const BaArgs* __restrict__ a
         const int e = a.pt_edges[k];
         const int oi = a.opt[a.e_pose[e]];
         if (oi < 0) continue;
-        const double* h = a.Hpl + 18 * e;
+        double A[6], B[12];
+        const double w = lin_ab(a, e, oi, A, B);   // Hpl_e^T xp = w A^T (B xp)
         const double* xp = a.x + 6 * oi;
+        double u0 = 0.0, u1 = 0.0;
 #pragma unroll
-        for (int cc = 0; cc < 3; cc++)
+        for (int r = 0; r < 6; r++) { u0 += B[r] * xp[r]; u1 += B[6 + r] * xp[r]; }
+        u0 *= w; u1 *= w;
 #pragma unroll
-            for (int r = 0; r < 6; r++) c[cc] -= h[3 * r + cc] * xp[r];
+        for (int cc = 0; cc < 3; cc++) c[cc] -= A[cc] * u0 + A[3 + cc] * u1;
     }
     const double* Di = a.Dinv + 9 * m;
     double* X = a.pts + 3 * m;
@@ -592,6 +682,7 @@ __global__ __launch_bounds__(256) void k_ba_backsub(const BaArgs* __restrict__ a
 
 __global__ __launch_bounds__(256) void k_ba_update_poses(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
+    BA_PHASE(kPhTrial)
     const int p = bx_ * blockDim.x + threadIdx.x;
     if (p >= a.P) return;
     double* T = a.pose + 8 * p;
@@ -602,8 +693,11 @@ __global__ __launch_bounds__(256) void k_ba_update_poses(const BaArgs* __restric
     se3_update(a.x + 6 * oi, T);
 }
 
+// restore the pushed state: host-driven rounds list the rejected problems in act[]; device-driven
+// rounds restore every problem whose controller flagged its trial rejected (ctl->pop)
 __global__ __launch_bounds__(256) void k_ba_pop(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
+    if (a.ctl && !a.ctl->pop) return;
     const int i = bx_ * blockDim.x + threadIdx.x;
     if (i < 8 * a.P) a.pose[i] = a.pose_bak[i];
     if (i < 3 * a.M) a.pts[i] = a.pts_bak[i];
@@ -652,10 +746,7 @@ __global__ __launch_bounds__(256) void k_ba_shard_reduce(const BaArgs* __restric
     }
 }
 
-__global__ __launch_bounds__(1024) void k_ba_reduce(const BaArgs* __restrict__ args, const int* __restrict__ act,
-                                                    int what) {
-    const BaArgs& a = args[act[blockIdx.x]];
-    __shared__ double sh[16];
+__device__ void ba_reduce_body(const BaArgs& a, int what, double* sh) {
     double v = 0;
     if (what & 1) {
         for (int e = threadIdx.x; e < a.E; e += blockDim.x) v += a.e_rho0[e];
@@ -688,6 +779,105 @@ __global__ __launch_bounds__(1024) void k_ba_reduce(const BaArgs* __restrict__ a
     }
 }
 
+__global__ __launch_bounds__(1024) void k_ba_reduce(const BaArgs* __restrict__ args, const int* __restrict__ act,
+                                                    int what) {
+    __shared__ double sh[16];
+    ba_reduce_body(args[act[blockIdx.x]], what, sh);
+}
+
+// ---------------------------------------------------------------------------
+// device-driven Levenberg-Marquardt control: one slot = [pre] build kernels [begin] trial kernels
+// [end] pop. The rules are those of the host-driven rounds in ba_solve_batch (g2o
+// OptimizationAlgorithmLevenberg::solve + SparseOptimizer::optimize, U:Thirdparty/g2o), applied
+// per problem on the device so that a whole solve needs no host round trip per trial.
+// ---------------------------------------------------------------------------
+// initial activeRobustChi2 (errors computed by the preceding k_ba_errors)
+__global__ __launch_bounds__(1024) void k_ba_ctl_init(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    __shared__ double sh[16];
+    const BaArgs& a = args[act[blockIdx.x]];
+    ba_reduce_body(a, 1, sh);
+    if (threadIdx.x == 0) {
+        LmCtl& c = *a.ctl;
+        c.currentChi = a.red[0];
+        c.initChi = a.red[0];
+    }
+}
+
+// start of a slot: clear the pop request of the previous slot; at an iteration start, stop on the
+// iteration budget or the (host-relayed) stop flag
+__global__ void k_ba_ctl_pre(LmCtl* __restrict__ ctl, int B) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    LmCtl& c = ctl[b];
+    c.pop = 0;
+    if (c.phase == kPhBuild && (c.stop || c.it >= c.iterations)) c.phase = kPhDone;
+}
+
+__global__ void k_ba_ctl_stop(LmCtl* __restrict__ ctl, int B) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b < B) ctl[b].stop = 1;
+}
+
+// after the build: lambda initialisation on the first iteration (1e-5 max diagonal), then trials
+__global__ __launch_bounds__(1024) void k_ba_ctl_begin(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    __shared__ double sh[16];
+    const BaArgs& a = args[act[blockIdx.x]];
+    LmCtl& c = *a.ctl;
+    if (c.phase != kPhBuild) return;   // uniform
+    if (c.it == 0) ba_reduce_body(a, 4, sh);
+    if (threadIdx.x == 0) {
+        if (c.it == 0) {
+            *const_cast<double*>(a.lambda) = 1e-5 * a.red[2];
+            c.ni = 2;
+            c.nBad = 0;
+        }
+        c.qmax = 0;
+        c.rho = 0;
+        c.phase = kPhTrial;
+    }
+}
+
+// after a trial: chi2 and scale, rho, accept (lambda shrink) or reject (lambda *= ni, pop), and
+// the end-of-iteration rules
+__global__ __launch_bounds__(1024) void k_ba_ctl_end(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    __shared__ double sh[16];
+    const BaArgs& a = args[act[blockIdx.x]];
+    LmCtl& c = *a.ctl;
+    if (c.phase != kPhTrial) return;   // uniform
+    ba_reduce_body(a, 3, sh);
+    if (threadIdx.x != 0) return;
+    double* lambda = const_cast<double*>(a.lambda);
+    const bool ok2 = a.flag[0] != 0;
+    const double tempChi = ok2 ? a.red[0] : DBL_MAX;
+    double rho = c.currentChi - tempChi;
+    rho /= (a.red[1] + 1e-3);
+    if (rho > 0 && isfinite(tempChi)) {
+        double alpha = 1. - pow((2 * rho - 1), 3.0);
+        alpha = fmin(alpha, 2. / 3.);
+        *lambda *= fmax(1. / 3., alpha);
+        c.ni = 2;
+        if (c.early_stop) {
+            if ((c.currentChi - tempChi) < 1e-3 * c.currentChi) c.nBad++;
+            else c.nBad = 0;
+        }
+        c.currentChi = tempChi;
+    } else {
+        *lambda *= c.ni;
+        c.ni *= 2;
+        c.pop = 1;
+    }
+    c.rho = rho;
+    c.qmax++;
+    c.trials++;
+    if (rho < 0 && c.qmax < 10 && !c.stop) return;   // another trial of this iteration
+    c.it++;
+    c.errors_valid = rho > 0;   // rejected: the device errors belong to the popped trial
+    bool done = (c.qmax == 10 || rho == 0);
+    if (c.early_stop && c.nBad >= 3) done = true;
+    if (c.it >= c.iterations) done = true;   // the budget (checked by ctl_pre too), no idle slot
+    c.phase = done ? kPhDone : kPhBuild;
+}
+
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
@@ -711,7 +901,7 @@ struct Prep {
     std::vector<int> items, fin;  // Schur work items {k0, k1, blk, slot} and finisher blocks {blk, slot0, n}
     int nslot = 0;
     // offsets (elements) into the packed buffers; see the segment map in ba_solve_batch
-    size_t o_chi2, o_state, o_obs, o_hw, o_scr, o_S, o_L, o_part, o_int;
+    size_t o_chi2, o_state, o_obs, o_scr, o_lin, o_S, o_L, o_part, o_int;
 };
 
 inline void se3_from_float(const float* q, const float* t, double* out) {
@@ -722,7 +912,7 @@ inline void se3_from_float(const float* q, const float* t, double* out) {
     out[4] = t[0]; out[5] = t[1]; out[6] = t[2]; out[7] = 0;
 }
 
-int prepare(const orbhip_ba_problem* pr, Prep& o) {
+int prepare(const orbhip_ba_problem* pr, Prep& o, int chunk) {
     const int P = pr->n_poses, M = pr->n_points, E = pr->n_edges;
     if (P < 0 || M < 0 || E < 0 || (P && (!pr->pose_q || !pr->pose_t || !pr->pose_fixed)) || (M && !pr->points) ||
         (E && (!pr->edge_pose || !pr->edge_point || !pr->edge_uv || !pr->edge_octave || !pr->inv_sigma2)))
@@ -805,14 +995,14 @@ int prepare(const orbhip_ba_problem* pr, Prep& o) {
     for (int b = 0; b < o.nblk; b++) {
         const int k0 = o.blk_ptr[b], k1 = o.blk_ptr[b + 1];
         const bool diag = o.blk_i[b] == o.blk_j[b];
-        if (!diag && k1 - k0 <= kSchurChunk) {
+        if (!diag && k1 - k0 <= chunk) {
             o.items.insert(o.items.end(), {k0, k1, b, -1});
             continue;
         }
-        const int nch = std::max(1, (k1 - k0 + kSchurChunk - 1) / kSchurChunk);
+        const int nch = std::max(1, (k1 - k0 + chunk - 1) / chunk);
         o.fin.insert(o.fin.end(), {b, o.nslot, nch});
         for (int c = 0; c < nch; c++)
-            o.items.insert(o.items.end(), {k0 + c * kSchurChunk, std::min(k1, k0 + (c + 1) * kSchurChunk), b, o.nslot + c});
+            o.items.insert(o.items.end(), {k0 + c * chunk, std::min(k1, k0 + (c + 1) * chunk), b, o.nslot + c});
         o.nslot += nch;
     }
     o.blk_pairs.resize(2 * npairs);
@@ -898,6 +1088,8 @@ struct BaWorkspace {
     DBuf<int> act;         // active problem lists (several slots)
     DBuf<double> lam;      // per-problem lambda
     DBuf<double> gath;     // gathered red/flag of the active problems
+    DBuf<LmCtl> ctl;       // device-driven rounds: per-problem LM state
+    HBuf<LmCtl> hctl;      // its pinned staging (initial state up, final state down)
     HBuf<double> hdbl;     // staging: [e_chi2 | pose,pts | obs,info] of every problem
     HBuf<int> hint;
     HBuf<BaArgs> hargs;
@@ -943,7 +1135,10 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     const double t_start = now();
     const int nth = host_threads();
     std::vector<Prep> pp(B);
-    parallel_for(B, nth, [&](int b) { pp[b].rc = prepare(probs[b], pp[b]); });
+    // Schur work-item size: a batch fills the chip with 16 pairs per lane; a few problems alone
+    // would leave it mostly idle, so their items are cut to 4 pairs (4x the lanes)
+    const int chunk = B >= 32 ? kSchurChunk : 4;
+    parallel_for(B, nth, [&](int b) { pp[b].rc = prepare(probs[b], pp[b], chunk); });
     for (int b = 0; b < B; b++)
         if (pp[b].rc) return pp[b].rc;
     if (shard_mode == kShardLocal) {
@@ -960,21 +1155,21 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     //   C  e_chi2 (E)                 downloaded with A in one transfer
     //   A  pose (8P) + pts (3M)       uploaded, optimised in place, downloaded
     //   U  obs (2E) + info (E)        uploaded
-    //   Z  Hpl + W (36E)              cleared with one memset (edges of fixed poses stay zero)
-    //   R  the rest (scratch), then S (n*n) and the panel inverses Lsave, 16-byte aligned
-    size_t nC = 0, nA = 0, nU = 0, nZ = 0, nR = 0, ni = 0;
+    //   R  the rest (scratch), then the edge linearisations e_lin (32-byte aligned), S (n*n) and
+    //      the panel inverses Lsave, 16-byte aligned
+    size_t nC = 0, nA = 0, nU = 0, nR = 0, ni = 0;
     for (auto& p : pp) {
         const size_t P = p.P, M = p.M, E = p.E, np_ = p.np, n = p.n;
         p.o_chi2 = nC; nC += E;
         p.o_state = nA; nA += 8 * P + 3 * M;
         p.o_obs = nU; nU += 3 * E;
-        p.o_hw = nZ; nZ += 36 * E;
         p.o_scr = nR;
         nR += 8 * P + 3 * M                          // pose_bak, pts_bak
               + 2 * E + 3 * E                        // e_err, e_rho0, e_rho1 (+ pad)
-              + 36 * np_ + 18 * M + 3 * M            // Hpp, Hll, Dinv, db
+              + 36 * np_ + 9 * np_ + 18 * M + 3 * M  // Hpp, R_lin, Hll, Dinv, db
               + 2 * (n + 3 * M) + n + 4;             // b, x, bs, red
-        nR = (nR + 1) & ~size_t(1);
+        nR = (nR + 3) & ~size_t(3);
+        p.o_lin = nR; nR += 4 * E;
         p.o_S = nR; nR += n * n;
         nR = (nR + 1) & ~size_t(1);
         p.o_L = nR; nR += 1024 * ((n + 31) / 32);
@@ -984,7 +1179,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         ni += (P + 4) + 2 * E + (M + 1) + E + (np_ + 1) + p.ps_edges.size() + 3 * p.nblk + 1 + p.blk_pairs.size() +
               p.row_first.size() + p.items.size() + p.fin.size() + 8;
     }
-    const size_t sC = 0, sA = nC, sU = sA + nA, sZ = (sU + nU + 1) & ~size_t(1), sR = sZ + nZ;
+    const size_t sC = 0, sA = nC, sU = sA + nA, sR = (sU + nU + 3) & ~size_t(3);
     const size_t nd = sR + nR;
     BAOK(ws->dbl.ensure(nd));
     BAOK(ws->ints.ensure(ni));
@@ -992,6 +1187,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     BAOK(ws->act.ensure(3 * (size_t)B));
     BAOK(ws->lam.ensure(B));
     BAOK(ws->gath.ensure(5 * (size_t)B));
+    BAOK(ws->ctl.ensure(B));
+    BAOK(ws->hctl.ensure(B));
     BAOK(ws->hdbl.ensure(sU + nU));
     BAOK(ws->hint.ensure(ni));
     BAOK(ws->hargs.ensure(B));
@@ -1055,7 +1252,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.e_chi2 = D + sC + p.o_chi2;
         a.pose = D + sA + p.o_state; a.pts = a.pose + 8 * P;
         a.e_obs = D + sU + p.o_obs; a.e_info = a.e_obs + 2 * E;
-        a.Hpl = D + sZ + p.o_hw; a.W = a.Hpl + 18 * E;
+        a.e_lin = D + sR + p.o_lin;
         double* r = D + sR + p.o_scr;
         a.pose_bak = r; r += 8 * P;
         a.pts_bak = r; r += 3 * M;
@@ -1063,6 +1260,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.e_rho0 = r; r += E;
         a.e_rho1 = r; r += 2 * E;
         a.Hpp = r; r += 36 * (size_t)p.np;
+        a.R_lin = r; r += 9 * (size_t)p.np;
         a.Hll = r; r += 9 * M;
         a.Dinv = r; r += 9 * M;
         a.db = r; r += 3 * M;
@@ -1075,9 +1273,9 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.Spart = D + sR + p.o_part;
         a.lambda = ws->lam.p + b;
         a.lead = shard_mode == kShardLocal ? (b == 0) : (shard_mode == kShardRccl ? (ws->rank == 0) : 1);
+        a.ctl = shard_mode == kShardNone ? ws->ctl.p + b : nullptr;
     });
     BAOK(hipMemcpyAsync(D + sA, hd + sA, sizeof(double) * (nA + nU), hipMemcpyHostToDevice, st));
-    if (nZ) BAOK(hipMemsetAsync(D + sZ, 0, sizeof(double) * nZ, st));
     BAOK(hipMemcpyAsync(I, hi, ni * sizeof(int), hipMemcpyHostToDevice, st));
     BAOK(hipMemcpyAsync(ws->args.p, ha, B * sizeof(BaArgs), hipMemcpyHostToDevice, st));
     if (shard_mode == kShardRccl && !pp[0].row_first.empty()) {   // union envelope over the ranks
@@ -1153,9 +1351,108 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     std::vector<LmState> L(B);
     std::vector<int> all(B);
     for (int b = 0; b < B; b++) all[b] = b;
-    // ---- initial errors and chi2 ----
     if (upload_act(all)) return ORBHIP_ERR_DEVICE;
-    hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), dim3(256), 0, st, dA, d_act);
+    if (shard_mode == kShardNone) {
+        // ---- device-driven rounds: each slot advances every problem by one LM trial (with the
+        // iteration's linearisation in front when it starts one); the k_ba_ctl_* kernels apply
+        // the g2o rules per problem, so the host only enqueues slots and reads the state back once
+        // per batch of slots ----
+        LmCtl* dctl = ws->ctl.p;
+        for (int b = 0; b < B; b++) {
+            LmCtl& c = ws->hctl.p[b];
+            c = LmCtl{};
+            c.ni = 2;
+            c.phase = kPhBuild;
+            c.errors_valid = 1;
+            c.iterations = probs[b]->iterations;
+            c.early_stop = probs[b]->early_stop;
+        }
+        BAOK(hipMemcpyAsync(dctl, ws->hctl.p, B * sizeof(LmCtl), hipMemcpyHostToDevice, st));
+        int ns = 0;   // problems on the single-workgroup solvers (act slot 3)
+        for (int b = 0; b < B; b++)
+            if (pp[b].n <= kCholSmallN) h_act[2 * B + ns++] = b;
+        if (ns) BAOK(hipMemcpyAsync(d_act + 2 * B, h_act + 2 * B, ns * sizeof(int), hipMemcpyHostToDevice, st));
+        if (s_readonly) hipLaunchKernelGGL(k_ba_zero_s, dim3(64, B), dim3(256), 0, st, dA, d_act, 1);
+        hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), dim3(256), 0, st, dA, d_act, 0);
+        hipLaunchKernelGGL(k_ba_ctl_init, dim3(B), dim3(1024), 0, st, dA, d_act);
+        const dim3 gB((unsigned)((B + 255) / 256)), b256(256);
+        auto slot = [&]() -> int {
+            hipLaunchKernelGGL(k_ba_ctl_pre, gB, b256, 0, st, dctl, B);
+            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 1);
+            hipLaunchKernelGGL(k_ba_lin_points, dim3(gx(maxM, 256), B), b256, 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_lin_poses, dim3(gx(maxNp, 4), B), b256, 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_ctl_begin, dim3(B), dim3(1024), 0, st, dA, d_act);
+            if (!s_readonly) hipLaunchKernelGGL(k_ba_zero_s, dim3(64, B), b256, 0, st, dA, d_act, 0);
+            hipLaunchKernelGGL(k_ba_schur_points, dim3(gx(maxM, 256), B), b256, 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_schur_items, dim3(gx(2 * maxItems, 256), B), b256, 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_schur_fin, dim3(gx(maxFin, 4), B), b256, 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_schur_b, dim3(gx(maxNp, 4), B), b256, 0, st, dA, d_act);
+            if (ns) {
+                if (maxN <= kCholRegMaxN) BAOK(chol_reg_launch(maxN, ns, dA, d_act + 2 * B, st));
+                else hipLaunchKernelGGL(k_ba_cholesky, dim3(ns), dim3(512), chol_lds, st, dA, d_act + 2 * B);
+            }
+            for (int b = 0; b < B; b++)
+                if (pp[b].n > kCholSmallN)
+                    chol_blocked_solve(ha[b].S, pp[b].n, ha[b].Lsave, ha[b].bs, ha[b].x, ha[b].flag, ha[b].row_first,
+                                       st, &dctl[b].phase);
+            hipLaunchKernelGGL(k_ba_backsub, dim3(gx(maxM, 256), B), b256, 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_update_poses, dim3(gx(maxP, 256), B), b256, 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 2);
+            hipLaunchKernelGGL(k_ba_ctl_end, dim3(B), dim3(1024), 0, st, dA, d_act);
+            int maxPM = 0;
+            for (auto& p : pp) maxPM = std::max(maxPM, std::max(8 * p.P, 3 * p.M));
+            hipLaunchKernelGGL(k_ba_pop, dim3(gx(maxPM, 256), B), b256, 0, st, dA, d_act);
+            BAOK(hipGetLastError());
+            return ORBHIP_OK;
+        };
+        // Pacing: at most two slots in flight, so a stop request reaches the device within about
+        // two trials (g2o checks its force-stop flag once per iteration).
+        hipEvent_t ev[2];
+        BAOK(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+        BAOK(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+        int rc = ORBHIP_OK;
+        bool stop_sent = false;
+        int remaining = 0;   // slots every unfinished problem still needs at least
+        for (int b = 0; b < B; b++) remaining = std::max(remaining, probs[b]->iterations);
+        int nslot = 0;
+        while (remaining > 0 && rc == ORBHIP_OK) {
+            for (int k = 0; k < remaining && rc == ORBHIP_OK; k++, nslot++) {
+                if (!stop_sent && stop && *stop) {
+                    hipLaunchKernelGGL(k_ba_ctl_stop, gB, b256, 0, st, dctl, B);
+                    stop_sent = true;
+                }
+                rc = slot();
+                if (rc == ORBHIP_OK && hipEventRecord(ev[nslot & 1], st) != hipSuccess) rc = ORBHIP_ERR_DEVICE;
+                if (rc == ORBHIP_OK && nslot >= 1 && hipEventSynchronize(ev[(nslot - 1) & 1]) != hipSuccess)
+                    rc = ORBHIP_ERR_DEVICE;
+            }
+            if (rc != ORBHIP_OK) break;
+            if (hipMemcpyAsync(ws->hctl.p, dctl, B * sizeof(LmCtl), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess) {
+                rc = ORBHIP_ERR_DEVICE;
+                break;
+            }
+            remaining = 0;
+            for (int b = 0; b < B; b++) {
+                const LmCtl& c = ws->hctl.p[b];
+                if (c.phase == kPhDone) continue;
+                remaining = std::max(remaining, stop_sent ? 1 : std::max(1, c.iterations - c.it));
+            }
+        }
+        (void)hipEventDestroy(ev[0]);
+        (void)hipEventDestroy(ev[1]);
+        if (rc != ORBHIP_OK) return rc;
+        for (int b = 0; b < B; b++) {
+            const LmCtl& c = ws->hctl.p[b];
+            L[b].currentChi = c.currentChi;
+            L[b].it = c.it;
+            L[b].trials = c.trials;
+            res[b]->initial_chi2 = c.initChi;
+        }
+    } else {
+    // ---- host-driven rounds (sharded solves: collectives and the stop-flag consensus) ----
+    // ---- initial errors and chi2 ----
+    hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), dim3(256), 0, st, dA, d_act, 0);
     hipLaunchKernelGGL(k_ba_reduce, dim3(B), dim3(1024), 0, st, dA, d_act, 1);
     if (coll(3, 0, 1, 0)) return ORBHIP_ERR_DEVICE;
     BAOK(hipGetLastError());
@@ -1180,7 +1477,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             if (!L[b].errors_valid) stale.push_back(b);
         if (!stale.empty()) {
             if (upload_act(stale)) return ORBHIP_ERR_DEVICE;
-            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), (unsigned)stale.size()), dim3(256), 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), (unsigned)stale.size()), dim3(256), 0, st, dA, d_act, 0);
         }
         if (upload_act(act)) return ORBHIP_ERR_DEVICE;
         hipLaunchKernelGGL(k_ba_lin_points, dim3(gx(maxM, 256), na), dim3(256), 0, st, dA, d_act);
@@ -1201,10 +1498,10 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             if (upload_act(trial)) return ORBHIP_ERR_DEVICE;
             // S outside the block structure stays zero; it only needs clearing again when a solver
             // factors S in place (or the shards' sums overwrite it)
-            if (!s_clean) hipLaunchKernelGGL(k_ba_zero_s, dim3(64, nt_), dim3(256), 0, st, dA, d_act);
+            if (!s_clean) hipLaunchKernelGGL(k_ba_zero_s, dim3(64, nt_), dim3(256), 0, st, dA, d_act, 1);
             s_clean = s_readonly;
             hipLaunchKernelGGL(k_ba_schur_points, dim3(gx(maxM, 256), nt_), dim3(256), 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_schur_items, dim3(gx(maxItems, 256), nt_), dim3(256), 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_schur_items, dim3(gx(2 * maxItems, 256), nt_), dim3(256), 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_schur_fin, dim3(gx(maxFin, 4), nt_), dim3(256), 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_schur_b, dim3(gx(maxNp, 4), nt_), dim3(256), 0, st, dA, d_act);
             if (shard_mode) {   // reduced camera system of all shards
@@ -1230,7 +1527,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             }
             hipLaunchKernelGGL(k_ba_backsub, dim3(gx(maxM, 256), nt_), dim3(256), 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_update_poses, dim3(gx(maxP, 256), nt_), dim3(256), 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), nt_), dim3(256), 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), nt_), dim3(256), 0, st, dA, d_act, 0);
             hipLaunchKernelGGL(k_ba_reduce, dim3(nt_), dim3(1024), 0, st, dA, d_act, 3);
             if (coll(3, 0, 2, 0)) return ORBHIP_ERR_DEVICE;
             BAOK(hipGetLastError());
@@ -1281,6 +1578,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             if (probs[b]->early_stop && s.nBad >= 3) s.done = true;
         }
     }
+    }   // host-driven rounds
     const double t_solve = now();
     // ---- outputs: e_chi2 of every problem + optimised poses/points, one transfer ----
     BAOK(hipMemcpyAsync(hd, D, sizeof(double) * (nC + nA), hipMemcpyDeviceToHost, st));

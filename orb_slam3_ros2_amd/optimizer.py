@@ -108,6 +108,15 @@ class PoseResult:
     lm_trials: int
 
 
+@dataclass
+class BABatch:
+    """A batch of problems in C-ABI form (Optimizer.prepare_batch); run_batch solves it in place."""
+    problems: list
+    outs: list
+    cprobs: object
+    cres: object
+
+
 class Optimizer:
     def __init__(self, device: int = 0, ctx: Context | None = None):
         self.ctx = ctx or Context(device)
@@ -128,23 +137,22 @@ class Optimizer:
 
     def solve_batch(self, probs, stop_flag: ctypes.c_int | None = None):
         """B independent problems in one batched solve (replicas); returns a list of BAResult."""
+        return self.run_batch(self.prepare_batch(probs), stop_flag)
+
+    def prepare_batch(self, probs) -> "BABatch":
+        """The C-ABI view of a batch (orbhip_ba_problem / orbhip_ba_result arrays over the
+        problems' own arrays and freshly allocated outputs), as a C++ host adapter holds it: the
+        Python marshalling is done once here, run_batch is the orbhip_ba_solve_batch call alone."""
         ps = [p.normalized() for p in probs]
-        outs, cres = [], (BAResultC * len(ps))()
-        cprobs = (BAProblemC * len(ps))()
-        for i, p in enumerate(ps):
-            P, M, E = p.pose_q.shape[0], p.points.shape[0], p.edge_pose.shape[0]
-            o = BAResult(np.zeros((P, 4), np.float32), np.zeros((P, 3), np.float32), np.zeros((M, 3), np.float32),
-                         np.zeros(E, np.float32), np.zeros(E, np.uint8), 0.0, 0.0, 0, 0)
-            outs.append(o)
-            cres[i] = BAResultC(ptr(o.pose_q), ptr(o.pose_t), ptr(o.points), ptr(o.edge_chi2), ptr(o.edge_depth_ok),
-                                0.0, 0.0, 0, 0)
-            cprobs[i] = p.to_c()
+        outs, cres = self._results_for(ps)
+        cprobs = (BAProblemC * len(ps))(*[p.to_c() for p in ps])
+        return BABatch(ps, outs, cprobs, cres)
+
+    def run_batch(self, batch: "BABatch", stop_flag: ctypes.c_int | None = None):
         sf = ctypes.addressof(stop_flag) if stop_flag is not None else None
-        check(lib().orbhip_ba_solve_batch(self.ctx.handle, cprobs, len(ps), cres, sf), "orbhip_ba_solve_batch")
-        for o, r in zip(outs, cres):
-            o.initial_chi2, o.final_chi2, o.iterations_done, o.lm_trials = (r.initial_chi2, r.final_chi2,
-                                                                              r.iterations_done, r.lm_trials)
-        return outs
+        check(lib().orbhip_ba_solve_batch(self.ctx.handle, batch.cprobs, len(batch.problems), batch.cres, sf),
+              "orbhip_ba_solve_batch")
+        return self._fill(batch.outs, batch.cres)
 
     # ---- sharded BundleAdjustment (SURVEY.md §8e) ----
     def _results_for(self, ps):

