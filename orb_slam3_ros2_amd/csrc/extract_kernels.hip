@@ -807,7 +807,16 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
     const int ncell = G.n_cells;
     const int* cc = cand_cnt + (int64_t)f * P->n_cells_total + G.cell_base;
     const int nIni = G.n_ini;
-    if (w0) {
+    if (ncell <= nt) {
+        // one cell per thread: every count / slot load in flight at once, one block scan
+        const int c = tid < ncell ? cc[tid] : 0;
+        if (tid < ncell) S.cslot[tid] = cells[G.cell_base + tid].slot_off;
+        int M0;
+        const int ex = block_excl_scan(c, ctl, &M0);
+        if (tid < ncell) S.cellstart[tid] = ex;
+        if (tid == 0) { S.cellstart[ncell] = M0; ctl[55] = M0; }
+        for (int i = tid; i < nIni * 4; i += nt) S.ccount[i] = 0;
+    } else if (w0) {
         for (int i = lane; i < ncell; i += 64) {
             S.cellstart[i] = cc[i];
             S.cslot[i] = cells[G.cell_base + i].slot_off;
