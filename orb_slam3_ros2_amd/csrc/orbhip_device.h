@@ -130,6 +130,21 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
     return v;
 }
 
+// Work-groups are dealt round-robin over the 8 XCDs (dispatch index b -> XCD b % 8; observed,
+// speed only, never correctness). xcd_runs maps dispatch index b of a grid of n onto a logical
+// index such that each XCD receives runs of g consecutive logical indices, the runs dealt
+// round-robin: neighbouring tiles / cells / keypoints, whose image windows overlap, then share one
+// XCD's L2 (fewer lines fetched by several L2s), while every XCD still gets a spread of the grid
+// (balance: level-0 cells cost more than the others). Identity on the tail past the last full
+// round of 8 runs, so a bijection on [0, n) for any n; g == 0 is the identity.
+__device__ __forceinline__ int xcd_runs(int b, int n, int g) {
+    if (g <= 0) return b;
+    const int full = (n / (8 * g)) * (8 * g);
+    if (b >= full) return b;
+    const int k = b & 7, i = b >> 3;
+    return ((i / g) * 8 + k) * g + (i % g);
+}
+
 __device__ __forceinline__ int wave_sum_i32(int v) {
     return __builtin_amdgcn_readlane(wave_incl_scan(v), 63);
 }
