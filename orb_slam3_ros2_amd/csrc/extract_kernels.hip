@@ -292,7 +292,7 @@ __global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict
                                                    const ConeRect* __restrict__ rects, const int* __restrict__ ctab,
                                                    int tab_stride, int xrun) {
     extern __shared__ __attribute__((aligned(16))) uint8_t cone[];
-    const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun);
+    const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
     pyr_cone_body<false>(P, fb, rects, ctab, tab_stride, cone, lg % X, lg / X, nullptr);
 }
 
@@ -575,7 +575,7 @@ __global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict
     __shared__ uint16_t clist[kClistCap];
     __shared__ int ncand;
     const FastLds LS{win, mv, bmask, woff, &wsel, &wtot, clist, &ncand};
-    const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun);
+    const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
     fast_cell_body<NT, false>(P, cells, fb, cand, cand_cnt, err, lg % X, lg / X, LS, nullptr, 0);
 }
 
@@ -1203,19 +1203,20 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
                                               const LevelKp* __restrict__ lvl_kp, const int* __restrict__ lvl_cnt,
                                               const int* __restrict__ lvl_nlap, const int* __restrict__ disc,
                                               orbhip_kp* __restrict__ out_kps, uint8_t* __restrict__ out_desc,
-                                              int cap, int* __restrict__ n_out, int* __restrict__ mono_out) {
+                                              int cap, int* __restrict__ n_out, int* __restrict__ mono_out, int xrun) {
     __shared__ uint8_t patch[4][kPatchW * kPatchW + 15];
     __shared__ uint16_t hrow[4][kPatchW * kBlW];     // row pass: 43 rows x 37 columns
     __shared__ uint8_t blr[4][kBlW * kBlW + 7];       // blurred 37 x 37
     TR_BEGIN()
-    const int f = blockIdx.y;
+    const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
+    const int f = lg / X;
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int slot = blockIdx.x * 4 + wid;
+    int slot = (lg % X) * 4 + wid;
     const int L = P->n_levels;
     // frame totals (same in every lane / wave of the frame)
     int total = 0, nlap_tot = 0;
     for (int l = 0; l < L; l++) { total += lvl_cnt[f * L + l]; nlap_tot += lvl_nlap[f * L + l]; }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (lg % X == 0 && threadIdx.x == 0) {
         n_out[f] = total;
         mono_out[f] = total - nlap_tot;
     }
@@ -1381,7 +1382,7 @@ __global__ __launch_bounds__(256) void k_desc_kp(const ExtractPlan* __restrict__
     __shared__ uint8_t bl[kBlW * kBlW + 7];
     __shared__ int msum[2][4];
     TR_BEGIN()
-    const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun);
+    const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
     const int f = lg / X;
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
     int slot = lg % X;
@@ -1517,13 +1518,14 @@ __global__ __launch_bounds__(256) void k_desc_kp(const ExtractPlan* __restrict__
 // host-side launchers
 // ---------------------------------------------------------------------------
 // Run length of the XCD-aware work-group order (xcd_runs) of the cone / FAST / rBRIEF launches.
-// Batches: runs of 16 neighbouring tiles / cells / keypoints per XCD cut the cross-XCD re-fetch
-// of the frames (C3 k_fast_cells 835 -> 183 MB of HBM traffic per launch, time unchanged: it is
-// VALU-bound). One frame: the plain round-robin order, since grouping neighbours onto one XCD
-// made the latency-bound one-frame stream slower with frames in flight (30k -> 24k frames/s).
+// Batches of 8+ frames: -1 = one frame's whole grid row per run, so every frame's tiles / cells /
+// keypoints land on ONE XCD and its L2 fetches the frame once (C3 k_fast_cells 835 -> ~183 MB of
+// HBM traffic per launch, against 183 MB algorithmic; the time is unchanged, the kernel is
+// VALU-bound). Smaller batches: runs of 16. One frame: the plain round-robin order (grouping
+// neighbours onto one XCD measured ~1% below it on the 16-camera C2 stream).
 static int xcd_run_for(int B) {
-    static const int env = getenv("ORBHIP_XCD_RUN") ? atoi(getenv("ORBHIP_XCD_RUN")) : -1;
-    return env >= 0 ? env : (B > 1 ? 16 : 0);
+    static const int env = getenv("ORBHIP_XCD_RUN") ? atoi(getenv("ORBHIP_XCD_RUN")) : -2;
+    return env >= -1 ? env : (B >= 8 ? -1 : (B > 1 ? 16 : 0));
 }
 
 void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, int B, int l,
@@ -1620,7 +1622,7 @@ void launch_desc(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& 
     }
     dim3 grd((hP.kp_slots_total + 3) / 4, B, 1);
     hipLaunchKernelGGL(k_desc, grd, dim3(256), 0, st, dP, fb, lvl_kp, lvl_cnt, lvl_nlap, disc, out_kps, out_desc,
-                       cap, n_out, mono_out);
+                       cap, n_out, mono_out, xcd_run_for(B));
 }
 
 bool octree_set_lds_limit(size_t bytes) {
