@@ -165,3 +165,49 @@ def test_register_cholesky_solves_spd(n):
         ref = np.linalg.solve(A, b)
         assert np.abs(A @ x - b).max() <= 1e-9 * np.abs(b).max() * cond / 1e2 + 1e-12
         assert np.abs(x - ref).max() <= 1e-13 * cond * np.abs(ref).max()
+
+
+def test_device_lm_rejections_and_pops(opt, oracle):
+    """Runs past convergence (60 iterations): trials get rejected (rho <= 0: lambda grows, the
+    pushed state is popped on the device) and the runs stop on rho == 0 at different iterations;
+    one batched solve holds problems that finish after different numbers of slots."""
+    probs = []
+    for seed in (1, 2, 3, 4):
+        p, _ = synthetic_ba_problem(n_kf=10, n_pts=300, seed=seed)
+        p.iterations = 60
+        probs.append(p)
+    outs = [oracle.ba_solve(p) for p in probs]
+    assert any(o["lm_trials"] > o["iterations_done"] for o in outs)   # rejections happen
+    gs = [opt.solve(p) for p in probs]
+    # where a run stops (rho == 0 vs a rejected rho < 0 at convergence) is rounding noise, so the
+    # rejections are asserted over the set, the results per problem
+    assert any(g.lm_trials > g.iterations_done for g in gs)
+    for p, o, g in zip(probs, outs, gs):
+        _compare(g, o, p, exact_schedule=False)
+    for p, o, g in zip(probs, outs, opt.solve_batch(probs)):
+        _compare(g, o, p, exact_schedule=False)
+
+
+def test_zero_iterations_and_mixed_budgets(opt, oracle):
+    """iterations = 0 leaves the state untouched (final chi2 = initial); a batch mixing budgets
+    0 / 3 / 10 runs each problem for its own budget."""
+    probs = []
+    for seed, it in ((31, 0), (32, 3), (33, 10)):
+        p, _ = synthetic_ba_problem(n_kf=12, n_pts=400, seed=seed)
+        p.iterations = it
+        probs.append(p)
+    res = opt.solve_batch(probs)
+    assert res[0].iterations_done == 0 and res[0].lm_trials == 0
+    assert res[0].final_chi2 == res[0].initial_chi2
+    for p, g in zip(probs, res):
+        o = oracle.ba_solve(p)
+        assert g.iterations_done == o["iterations_done"] and g.lm_trials == o["lm_trials"]
+        _compare(g, o, p, exact_schedule=p.iterations <= 10)
+
+
+def test_batch_stop_flag_aborts(opt):
+    import ctypes
+    probs = [synthetic_ba_problem(n_kf=10, n_pts=200, seed=40 + i)[0] for i in range(3)]
+    flag = ctypes.c_int(1)
+    for r in opt.solve_batch(probs, stop_flag=flag):
+        assert r.iterations_done == 0 and r.final_chi2 == r.initial_chi2
