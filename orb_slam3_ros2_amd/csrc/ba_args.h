@@ -49,6 +49,7 @@ struct BaArgs {
     const double* lambda;   // current lambda of this problem (device copy)
     double* Lsave;     // ceil(n/32) x 1024: L11^{-1} of every Cholesky panel
     const int* row_first;   // ceil(n/32): envelope of S in 32x32 tiles (blocked solver)
+    const int* cb_tiles;    // blocked solver: each panel's trailing-update tiles inside the envelope
     int lead;          // sharded solve: this shard adds the pose-side Hpp + lambda terms (once)
     // Schur work items (k_ba_schur_items): {k0, k1, blk, slot} over blk_pairs, at most kSchurChunk
     // pairs each; slot -1 = the block's only item (written to S directly), else its partial sum

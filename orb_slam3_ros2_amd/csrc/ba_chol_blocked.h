@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <vector>
 
 namespace orbhip {
 
@@ -13,7 +14,12 @@ constexpr int kCbMaxN = 4096;   // largest n (6 x optimised keyframes) of the bl
 // 32-row tile). flag[0] = 1 on success, 0 on a non-positive pivot (x = 0). Asynchronous on st.
 // gate (device int, optional): every kernel returns unless *gate == kPhTrial (ba_args.h).
 void chol_blocked_solve(double* S, int n, double* Lsave, const double* bs, double* x, int* flag,
-                        const int* row_first, hipStream_t st, const int* gate = nullptr);
+                        const int* row_first, hipStream_t st, const int* gate = nullptr,
+                        const int* tiles = nullptr, const int* tile_off = nullptr);
+// tiles / tile_off (optional): the per-panel trailing-update tiles inside the envelope
+// (cb_envelope_tiles; tiles on the device, tile_off on the host); nullptr = every lower tile,
+// skipped in the kernel when outside the envelope.
+void cb_envelope_tiles(const int* row_first, int n, std::vector<int>& tiles, std::vector<int>& off);
 
 int chol_blocked_test(const double* A, const double* b, double* x, int n, float* ms);
 

@@ -157,15 +157,21 @@ __device__ __forceinline__ void update_tile(double* __restrict__ S, int n, int k
 __global__ __launch_bounds__(256) void k_cb_update(double* __restrict__ S, int n, int k0,
                                                    const int* __restrict__ row_first, double* __restrict__ Lsave,
                                                    double* __restrict__ x, int* __restrict__ flag,
-                                                   const int* __restrict__ gate) {
+                                                   const int* __restrict__ gate, const int* __restrict__ tiles) {
     CB_GATE
     __shared__ double Bt[kUT * 34];   // the J rows of the panel; then the next diagonal block's scratch
     const int t0 = k0 + kCT;
-    int tt = blockIdx.x;
-    int I = (int)((sqrtf(8.0f * (float)tt + 1.0f) - 1.0f) * 0.5f);
-    while ((I + 1) * (I + 2) / 2 <= tt) I++;
-    while (I * (I + 1) / 2 > tt) I--;
-    const int J = tt - I * (I + 1) / 2;
+    const int tt = blockIdx.x;
+    int I, J;
+    if (tiles) {   // this panel's envelope tiles (host-built, tile (0, 0) first): I << 16 | J
+        I = tiles[tt] >> 16;
+        J = tiles[tt] & 0xFFFF;
+    } else {       // every lower tile of the trailing matrix, triangular index
+        I = (int)((sqrtf(8.0f * (float)tt + 1.0f) - 1.0f) * 0.5f);
+        while ((I + 1) * (I + 2) / 2 <= tt) I++;
+        while (I * (I + 1) / 2 > tt) I--;
+        J = tt - I * (I + 1) / 2;
+    }
     const int ri = t0 + kUT * I, rj = t0 + kUT * J;
     const int kt = k0 / kCT;
     // structure: the 64-row tile is non-zero in this panel if either 32-row half is
@@ -271,7 +277,8 @@ __global__ __launch_bounds__(1024) void k_cb_back(const double* __restrict__ S, 
 }
 
 void chol_blocked_solve(double* S, int n, double* Lsave, const double* bs, double* x, int* flag,
-                        const int* row_first, hipStream_t st, const int* gate) {
+                        const int* row_first, hipStream_t st, const int* gate, const int* tiles,
+                        const int* tile_off) {
     hipLaunchKernelGGL(k_cb_init, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, bs, x, n, flag, gate);
     hipLaunchKernelGGL(k_cb_diag, dim3(1), dim3(64), 0, st, S, n, 0, Lsave, x, flag, gate);
     const int np_ = (n + kCT - 1) / kCT;
@@ -281,10 +288,42 @@ void chol_blocked_solve(double* S, int n, double* Lsave, const double* bs, doubl
         hipLaunchKernelGGL(k_cb_panel, dim3((unsigned)((rest + 63) / 64)), dim3(256), 0, st, S, n, k0, Lsave,
                            row_first, x, gate);
         const int T = (rest + kUT - 1) / kUT;
-        hipLaunchKernelGGL(k_cb_update, dim3((unsigned)(T * (T + 1) / 2)), dim3(256), 0, st, S, n, k0, row_first,
-                           Lsave, x, flag, gate);   // + the diagonal block of panel p + 1
+        // + the diagonal block of panel p + 1 (tile (0, 0)'s work-group)
+        if (tiles && tile_off)
+            hipLaunchKernelGGL(k_cb_update, dim3((unsigned)(tile_off[p + 1] - tile_off[p])), dim3(256), 0, st, S, n,
+                               k0, row_first, Lsave, x, flag, gate, tiles + tile_off[p]);
+        else
+            hipLaunchKernelGGL(k_cb_update, dim3((unsigned)(T * (T + 1) / 2)), dim3(256), 0, st, S, n, k0, row_first,
+                               Lsave, x, flag, gate, nullptr);
     }
     hipLaunchKernelGGL(k_cb_back, dim3(1), dim3(1024), 0, st, S, n, Lsave, x, flag, row_first, gate);
+}
+
+// host: the 64x64 trailing-update tiles of every panel inside the envelope (the ones k_cb_update
+// would not skip), tile (0, 0) first in each panel (its work-group factors the next diagonal
+// block). tiles = I << 16 | J, offsets per panel (np + 1 entries, panels with no trailing matrix
+// empty). At C5 (n = 2394, a loop with a 20-KF window) 865 of the 18278 lower tiles.
+void cb_envelope_tiles(const int* row_first, int n, std::vector<int>& tiles, std::vector<int>& off) {
+    const int np_ = (n + kCT - 1) / kCT;
+    tiles.clear();
+    off.assign(np_ + 1, 0);
+    auto rf = [&](int r) { return row_first[r / kCT]; };
+    for (int p = 0; p < np_; p++) {
+        off[p] = (int)tiles.size();
+        const int k0 = p * kCT, t0 = k0 + kCT, rest = n - t0;
+        if (rest <= 0) continue;
+        const int T = (rest + kUT - 1) / kUT;
+        tiles.push_back(0);   // (0, 0)
+        for (int I = 0; I < T; I++)
+            for (int J = 0; J <= I; J++) {
+                if (I == 0 && J == 0) continue;
+                const int ri = t0 + kUT * I, rj = t0 + kUT * J;
+                const int fi = std::min(rf(ri), ri + kCT < n ? rf(ri + kCT) : 1 << 30);
+                const int fj = std::min(rf(rj), rj + kCT < n ? rf(rj + kCT) : 1 << 30);
+                if (fi <= p && fj <= p) tiles.push_back((I << 16) | J);
+            }
+    }
+    off[np_] = (int)tiles.size();
 }
 
 // test hook: solve A x = b (A dense SPD, n <= kCbMaxN) through the blocked path; ms = device time
@@ -294,7 +333,9 @@ int chol_blocked_test(const double* A, const double* b, double* x, int n, float*
     std::vector<int> rf(nt);
     row_first_from_dense(A, n, rf.data());
     double *dS = nullptr, *db = nullptr, *dx = nullptr, *dL = nullptr;
-    int *df = nullptr, *drf = nullptr;
+    int *df = nullptr, *drf = nullptr, *dtl = nullptr;
+    std::vector<int> tl, toff;
+    cb_envelope_tiles(rf.data(), n, tl, toff);
     int rc = 0;
     auto ok = [&](hipError_t e) { if (e != hipSuccess && rc == 0) rc = -3; return e == hipSuccess; };
     ok(hipMalloc((void**)&dS, sizeof(double) * n * n));
@@ -303,14 +344,16 @@ int chol_blocked_test(const double* A, const double* b, double* x, int n, float*
     ok(hipMalloc((void**)&dL, sizeof(double) * 1024 * nt));
     ok(hipMalloc((void**)&df, sizeof(int)));
     ok(hipMalloc((void**)&drf, sizeof(int) * nt));
+    ok(hipMalloc((void**)&dtl, sizeof(int) * std::max<size_t>(1, tl.size())));
     if (rc == 0) {
+        if (!tl.empty()) ok(hipMemcpy(dtl, tl.data(), sizeof(int) * tl.size(), hipMemcpyHostToDevice));
         ok(hipMemcpy(dS, A, sizeof(double) * n * n, hipMemcpyHostToDevice));
         ok(hipMemcpy(db, b, sizeof(double) * n, hipMemcpyHostToDevice));
         ok(hipMemcpy(drf, rf.data(), sizeof(int) * nt, hipMemcpyHostToDevice));
         hipEvent_t e0, e1;
         ok(hipEventCreate(&e0)); ok(hipEventCreate(&e1));
         ok(hipEventRecord(e0, nullptr));
-        chol_blocked_solve(dS, n, dL, db, dx, df, drf, nullptr);
+        chol_blocked_solve(dS, n, dL, db, dx, df, drf, nullptr, nullptr, dtl, toff.data());
         ok(hipEventRecord(e1, nullptr));
         ok(hipDeviceSynchronize());
         ok(hipGetLastError());
@@ -322,6 +365,7 @@ int chol_blocked_test(const double* A, const double* b, double* x, int n, float*
         (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
     }
     (void)hipFree(dS); (void)hipFree(db); (void)hipFree(dx); (void)hipFree(dL); (void)hipFree(df); (void)hipFree(drf);
+    (void)hipFree(dtl);
     return rc;
 }
 

@@ -898,6 +898,7 @@ struct Prep {
     int P = 0, M = 0, E = 0, np = 0, n = 0, nblk = 0;
     std::vector<int> opt, pt_ptr, pt_edges, ps_ptr, ps_edges, blk_i, blk_j, blk_ptr, blk_pairs;
     std::vector<int> row_first;   // blocked Cholesky structure: first 32-col tile per 32-row tile
+    std::vector<int> cb_tiles, cb_off;   // blocked Cholesky: envelope tiles per panel (cb_envelope_tiles)
     std::vector<int> items, fin;  // Schur work items {k0, k1, blk, slot} and finisher blocks {blk, slot0, n}
     int nslot = 0;
     // offsets (elements) into the packed buffers; see the segment map in ba_solve_batch
@@ -1150,6 +1151,12 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 pp[0].row_first[R] = std::min(pp[0].row_first[R], pp[b].row_first[R]);
         for (int b = 1; b < B; b++) pp[b].row_first = pp[0].row_first;
     }
+    // the blocked solver's per-panel tile lists (not for RCCL shards: their envelope is the union
+    // over the ranks, known on the device only)
+    if (shard_mode != kShardRccl)
+        parallel_for(B, nth, [&](int b) {
+            if (pp[b].n > kCholSmallN) cb_envelope_tiles(pp[b].row_first.data(), pp[b].n, pp[b].cb_tiles, pp[b].cb_off);
+        });
     const double t_prep = now();
     // ---- packed layout: fp64 segments, each contiguous over all problems ----
     //   C  e_chi2 (E)                 downloaded with A in one transfer
@@ -1177,7 +1184,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         p.o_part = nR; nR += 36 * (size_t)p.nslot;
         p.o_int = ni;
         ni += (P + 4) + 2 * E + (M + 1) + E + (np_ + 1) + p.ps_edges.size() + 3 * p.nblk + 1 + p.blk_pairs.size() +
-              p.row_first.size() + p.items.size() + p.fin.size() + 8;
+              p.row_first.size() + p.items.size() + p.fin.size() + p.cb_tiles.size() + 8;
     }
     const size_t sC = 0, sA = nC, sU = sA + nA, sR = (sU + nU + 3) & ~size_t(3);
     const size_t nd = sR + nR;
@@ -1246,6 +1253,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.fin = dev(put(p.fin.data(), p.fin.size()));
         a.nfin = (int)(p.fin.size() / 3);
         a.row_first = dev(put(p.row_first.data(), p.row_first.size()));
+        a.cb_tiles = p.cb_tiles.empty() ? nullptr : dev(put(p.cb_tiles.data(), p.cb_tiles.size()));
         a.nblk = p.nblk;
         a.P = p.P; a.M = p.M; a.E = p.E; a.np = p.np; a.n = p.n;
         a.fx = pr->fx; a.fy = pr->fy; a.cx = pr->cx; a.cy = pr->cy; a.delta = pr->huber_delta;
@@ -1394,7 +1402,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             for (int b = 0; b < B; b++)
                 if (pp[b].n > kCholSmallN)
                     chol_blocked_solve(ha[b].S, pp[b].n, ha[b].Lsave, ha[b].bs, ha[b].x, ha[b].flag, ha[b].row_first,
-                                       st, &dctl[b].phase);
+                                       st, &dctl[b].phase, ha[b].cb_tiles,
+                                       pp[b].cb_off.empty() ? nullptr : pp[b].cb_off.data());
             hipLaunchKernelGGL(k_ba_backsub, dim3(gx(maxM, 256), B), b256, 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_update_poses, dim3(gx(maxP, 256), B), b256, 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 2);
@@ -1523,7 +1532,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 for (int b : trial)
                     if (pp[b].n > kCholSmallN)
                         chol_blocked_solve(ha[b].S, pp[b].n, ha[b].Lsave, ha[b].bs, ha[b].x, ha[b].flag,
-                                           ha[b].row_first, st);
+                                           ha[b].row_first, st, nullptr, ha[b].cb_tiles,
+                                           pp[b].cb_off.empty() ? nullptr : pp[b].cb_off.data());
             }
             hipLaunchKernelGGL(k_ba_backsub, dim3(gx(maxM, 256), nt_), dim3(256), 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_update_poses, dim3(gx(maxP, 256), nt_), dim3(256), 0, st, dA, d_act);

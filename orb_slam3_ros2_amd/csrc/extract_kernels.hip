@@ -1565,16 +1565,15 @@ void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* c
     // more threads per cell while the cells alone cannot fill the chip (one frame: ~600 cells on
     // 256 CUs), as many as keep every work-group resident at once (8192 wave slots); 256 once
     // the batch fills the chip
-    static const int nt_env = getenv("ORBHIP_FAST_NT") ? atoi(getenv("ORBHIP_FAST_NT")) : 0;
     const int ncell = B * hP.n_cells_total;
-    const int nt = nt_env ? nt_env : (ncell <= 512 ? 1024 : (ncell <= 1024 ? 512 : 256));
+    const int nt = hP.fast_nt ? hP.fast_nt : (ncell <= 512 ? 1024 : (ncell <= 1024 ? 512 : 256));
     dim3 grd(hP.n_cells_total, B, 1);
     const int xr = xcd_run_for(B);
     if (nt == 1024)
         hipLaunchKernelGGL(k_fast_cells<1024>, grd, dim3(1024), 0, st, dP, cells, fb, cand, cand_cnt, err, xr);
     else if (nt == 512)
         hipLaunchKernelGGL(k_fast_cells<512>, grd, dim3(512), 0, st, dP, cells, fb, cand, cand_cnt, err, xr);
-    else if (nt == 128)   // A/B only (ORBHIP_FAST_NT=128)
+    else if (nt == 128)   // A/B and tests only (ORBHIP_FAST_NT=128)
         hipLaunchKernelGGL(k_fast_cells<128>, grd, dim3(128), 0, st, dP, cells, fb, cand, cand_cnt, err, xr);
     else
         hipLaunchKernelGGL(k_fast_cells<256>, grd, dim3(256), 0, st, dP, cells, fb, cand, cand_cnt, err, xr);

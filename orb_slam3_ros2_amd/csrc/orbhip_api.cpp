@@ -184,6 +184,14 @@ static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
     // ORBHIP_FAST_CLIST_CAP lowers the survivor list (tests force the dense FAST pass with 0)
     const char* cap_env = getenv("ORBHIP_FAST_CLIST_CAP");   // read per plan (once per ctx and size)
     P.clist_cap = cap_env ? std::min(std::max(atoi(cap_env), 0), kClistCap) : kClistCap;
+    // ORBHIP_FAST_NT pins k_fast_cells' threads per cell (A/B and tests; read per plan like the cap):
+    // 128, 256, 512 or 1024; any other value is rejected loudly and the batch-size choice stays
+    P.fast_nt = 0;
+    if (const char* nt_env = getenv("ORBHIP_FAST_NT")) {
+        const int v = atoi(nt_env);
+        if (v == 128 || v == 256 || v == 512 || v == 1024) P.fast_nt = v;
+        else std::fprintf(stderr, "orbhip: ORBHIP_FAST_NT=%s ignored (128, 256, 512 or 1024)\n", nt_env);
+    }
     for (int i = 0; i < 7; i++) P.blurk[i] = c->blurk[i];
     // k_desc hard-codes these taps (GaussianBlur 7x7 sigma 2 is fixed in ORBextractor)
     static const int kTaps[7] = {18, 34, 48, 56, 48, 34, 18};

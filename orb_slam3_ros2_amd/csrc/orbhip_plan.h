@@ -49,6 +49,7 @@ struct ExtractPlan {
     int blurk[7];                       // bit-exact 7x7 sigma=2 taps, 8 fractional bits
     int max_cells_level;                // max cells of any level (octree LDS carve)
     int clist_cap;                      // FAST survivors listed per cell (<= kClistCap; more -> dense pass)
+    int fast_nt;                        // k_fast_cells threads per cell: 0 = by batch size, else 128/256/512/1024
     LevelGeom lv[kMaxLevels];
 };
 

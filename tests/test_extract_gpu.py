@@ -103,6 +103,39 @@ def test_fast_dense_pass(oracle, monkeypatch, cap):
         assert _check(ext, oracle, img) > 0
 
 
+@pytest.mark.parametrize("nt", [128, 256, 512, 1024])
+@pytest.mark.parametrize("cap", [0, 2048])
+def test_fast_threads_per_cell_batched(oracle, monkeypatch, nt, cap):
+    """Every k_fast_cells variant (threads per cell pinned per plan by ORBHIP_FAST_NT) on a batch
+    of 3 frames through the device path, with the survivor list (cap 2048, the default) and the
+    dense pass forced (cap 0): each frame equals the oracle."""
+    import torch
+    monkeypatch.setenv("ORBHIP_FAST_NT", str(nt))
+    monkeypatch.setenv("ORBHIP_FAST_CLIST_CAP", str(cap))
+    from orb_slam3_ros2_amd import ORBextractor
+    ext = ORBextractor(1000, 1.2, 8, 20, 7)   # a fresh context: the plan reads both variables
+    rng = np.random.default_rng(nt + cap)
+    B, H, W = 3, 480, 640
+    frames = np.stack([synthetic_frame(70 + nt % 7, W, H), rng.integers(0, 256, size=(H, W), dtype=np.uint8),
+                       (128 + rng.integers(-9, 10, size=(H, W))).astype(np.uint8)])
+    kcap = ext.max_keypoints(W, H)
+    dev = torch.device("cuda:0")
+    kps = torch.zeros((B, kcap, 6), dtype=torch.float32, device=dev)
+    desc = torch.zeros((B, kcap, 32), dtype=torch.uint8, device=dev)
+    n = torch.zeros(B, dtype=torch.int32, device=dev)
+    mono = torch.zeros(B, dtype=torch.int32, device=dev)
+    ext.extract_batch_device(torch.from_numpy(frames).to(dev), kps, desc, n, mono)
+    torch.cuda.synchronize()
+    for i in range(B):
+        omono, ok6, od = oracle.extract(frames[i], 1000, 1.2, 8, 20, 7, (0, 1000))
+        ok = oracle_kps_to_struct(ok6)
+        assert int(n[i]) == len(ok) and int(mono[i]) == omono
+        kk = kps[i, : len(ok)].cpu().numpy()
+        assert np.array_equal(kk[:, 0], ok["x"]) and np.array_equal(kk[:, 1], ok["y"])
+        assert np.array_equal(kk[:, 3], ok["angle"]) and np.array_equal(kk[:, 5].view(np.int32), ok["octave"])
+        assert np.array_equal(desc[i, : len(ok)].cpu().numpy(), od)
+
+
 def test_low_contrast_uses_min_threshold(ext1000, oracle):
     """Cells with no corner at iniThFAST=20 fall back to minThFAST=7."""
     rng = np.random.default_rng(6)
