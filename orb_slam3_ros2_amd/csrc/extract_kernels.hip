@@ -13,6 +13,7 @@
 // Everything is integer or reproduces host float rounding exactly (-ffp-contract=off).
 #include <hip/hip_runtime.h>
 #include <cstdlib>
+#include <type_traits>
 
 #include "../../include/orbhip.h"
 #include "../../include/orbhip_pattern.h"
@@ -766,9 +767,21 @@ __device__ int wave_scan_lds(int* arr, int n) {
 __device__ __forceinline__ int nonempty4(const uint32_t* c) { return (c[0] > 0) + (c[1] > 0) + (c[2] > 0) + (c[3] > 0); }
 __device__ __forceinline__ int multi4(const uint32_t* c) { return (c[0] > 1) + (c[1] > 1) + (c[2] > 1) + (c[3] > 1); }
 
-// The node list work of one division pass runs in wave 0 alone (nodes <= node_cap, a few per
-// lane; DPP scans, no block barriers); the key sweeps use the whole work-group. A MAIN round is
-// then 2 block barriers, a FINAL round 4.
+// Two division engines, one node list logic (MAIN / FINAL passes in wave 0, the block rank sort):
+//  - pyramid path (cfg.fast, tried first): every key's quadrant path is fixed by geometry alone (a
+//    node's split lines depend only on its rectangle), so one pass over the keys histograms their
+//    depth-Dh cells (count + max (response, -key index, key)) and a reduction builds the counts and
+//    retained keys of every shallower cell. A node is (depth, path) and its children's counts are
+//    pyramid reads, so a division round touches no key: no sweep and one block barrier. A node
+//    with > 1 key at depth Dh (its children are deeper than the pyramid) sends the level to
+//    the sweep path, from scratch.
+//  - sweep path: nodes are rectangles, each round remaps every key to its node and counts the
+//    children (run-aggregated LDS atomics), then wave 0 runs the node pass. A MAIN round is 2
+//    block barriers, a FINAL round 4.
+// Node pass work (children counts, positions, serials, the largest-first selection of the FINAL
+// pass) runs in wave 0 alone with DPP wave scans over a few nodes per lane.
+constexpr int kOctMaxDh = 6;
+
 __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__ P, const CellGeom* __restrict__ cells,
                                                  const uint32_t* __restrict__ cand, const int* __restrict__ cand_cnt,
                                                  uint32_t* __restrict__ kscratch, uint16_t* __restrict__ nscratch,
@@ -804,15 +817,43 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
     uint32_t* keysL = (uint32_t*)carve(cfg.key_cap * 4);
     uint16_t* knodeL = (uint16_t*)carve(cfg.key_cap * 2);
     int* ctl = S.ctl;
+    const int nIni = G.n_ini;
+
+    // ---- pyramid (fast path) in the sweep path's key region: depth d holds nIni * 4^d cells at
+    // poff(d); pbest = (response << 56 | (0xFFFFFF - key index) << 32 | key), the retained key ----
+    const size_t preg_bytes = (((size_t)cfg.key_cap * 4 + 15) & ~size_t(15)) + (((size_t)cfg.key_cap * 2 + 15) & ~size_t(15));
+    // level d starts at poff(d), a multiple of 4 cells (16-byte vector reads of 4 siblings)
+    const int nIni4 = (nIni + 3) & ~3;
+    auto poff = [&](int d) { return d == 0 ? 0 : nIni4 + nIni * ((1 << (2 * d)) - 4) / 3; };
+    int Dh = 0;
+    if (cfg.fast)
+        for (int d = min(cfg.max_dh, kOctMaxDh); d >= 1; d--)
+            if ((size_t)poff(d + 1) * 12 <= preg_bytes) { Dh = d; break; }
+    unsigned long long* pbest = (unsigned long long*)keysL;
+    uint32_t* pcnt = (uint32_t*)(pbest + (Dh ? poff(Dh + 1) : 0));
 
     // ---- 1. candidate count per cell -> cell-major key order (wave 0 scans the cells) ----
     const int ncell = G.n_cells;
     const int* cc = cand_cnt + (int64_t)f * P->n_cells_total + G.cell_base;
-    const int nIni = G.n_ini;
+    // the pyramid's deepest level starts at zero (16-byte stores while the count loads fly)
+    auto zero_pyramid = [&]() {
+        if (Dh) {
+            ulonglong2* b2 = (ulonglong2*)(pbest + poff(Dh));
+            uint4* c4 = (uint4*)(pcnt + poff(Dh));
+            const int n4 = (poff(Dh + 1) - poff(Dh)) >> 2;
+            for (int i = tid; i < n4; i += nt) {
+                b2[2 * i] = ulonglong2{0ull, 0ull};
+                b2[2 * i + 1] = ulonglong2{0ull, 0ull};
+                c4[i] = uint4{0u, 0u, 0u, 0u};
+            }
+        }
+    };
     if (ncell <= nt) {
         // one cell per thread: every count / slot load in flight at once, one block scan
         const int c = tid < ncell ? cc[tid] : 0;
-        if (tid < ncell) S.cslot[tid] = cells[G.cell_base + tid].slot_off;
+        const int so = tid < ncell ? cells[G.cell_base + tid].slot_off : 0;
+        zero_pyramid();
+        if (tid < ncell) S.cslot[tid] = so;
         int M0;
         const int ex = block_excl_scan(c, ctl, &M0);
         if (tid < ncell) S.cellstart[tid] = ex;
@@ -828,360 +869,497 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
         if (lane == 0) { S.cellstart[ncell] = M0; ctl[55] = M0; }
         for (int i = lane; i < nIni * 4; i += 64) S.ccount[i] = 0;
     }
+    if (ncell > nt) zero_pyramid();
     __syncthreads();
     TR_PHASE(2, 50)
     const int M = ctl[55];
-    const bool keys_in_lds = M <= cfg.key_cap;
-    uint32_t* keys = keys_in_lds ? keysL : kscratch + (int64_t)f * P->n_slots_total + G.slot_base;
-    uint16_t* knode = keys_in_lds ? knodeL : nscratch + (int64_t)f * P->n_slots_total + G.slot_base;
     const uint32_t* cbase = cand + (int64_t)f * P->n_slots_total;
     const float hX = G.hX;
-    // flattened gather + root classification: key k belongs to the cell c with cellstart[c] <= k <
-    // cellstart[c+1] (binary search in LDS); up to 4 keys per thread with their loads in flight
-    // together
-    // With M <= 4 * nt (every C2/C3 level) each thread keeps its keys k = tid + u * nt and their
-    // current nodes in registers for the whole division (kreg/nreg): the sweeps then read no key
-    // state from LDS, and the 4 keys' lookup chains interleave.
-    const bool kr = M <= kOctKR * nt;
-    uint32_t kreg[kOctKR];
-    int nreg[kOctKR];
-#pragma unroll
-    for (int u = 0; u < kOctKR; u++) { kreg[u] = 0u; nreg[u] = 0; }
-    auto gather4 = [&](int k0, uint32_t* kv) {
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int k = min(k0 + tid + u * nt, M - 1);
-            int lo = 0, hi = ncell - 1;
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (S.cellstart[mid] <= k) lo = mid; else hi = mid - 1;
-            }
-            kv[u] = cbase[S.cslot[lo] + (k - S.cellstart[lo])];
-        }
-    };
-    auto root4 = [&](int k0, const uint32_t* kv, uint32_t* kr4, int* nr4) {
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int k = k0 + tid + u * nt;
-            uint32_t tgt = 0xFFFFFFFFu;
-            if (k < M) {
-                keys[k] = kv[u];
-                int r = (int)((float)cand_x(kv[u]) / hX);
-                r = r < 0 ? 0 : (r >= nIni ? nIni - 1 : r);
-                tgt = (uint32_t)r;
-                if (kr4) { kr4[u] = kv[u]; nr4[u] = r; }
-                else knode[k] = (uint16_t)r;
-            }
-            wave_aggregate_count(tgt, S.ccount);
-        }
-    };
-    if (kr) {
-        // compile-time register slots: group g holds keys k = (4g + u) * nt + tid
-#pragma unroll
-        for (int g = 0; g < kOctKR / 4; g++) {
-            if (4 * g * nt < M) {   // block-uniform
-                uint32_t kv[4];
-                gather4(4 * g * nt, kv);
-                root4(4 * g * nt, kv, kreg + 4 * g, nreg + 4 * g);
-            }
-        }
-    } else {
-        for (int k0 = 0; k0 < M; k0 += 4 * nt) {
-            uint32_t kv[4];
-            gather4(k0, kv);
-            root4(k0, kv, nullptr, nullptr);
-        }
-    }
-    __syncthreads();
-    TR_PHASE(2, 53)
-    // ---- 2. roots (nIni <= 64 enforced by the host) ----
-    if (w0) {
-        if (lane == 0) {
-            int n = 0;
-            const int H = G.max_by - G.min_by;
-            for (int r = 0; r < nIni; r++) {
-                const uint64_t rr = mk_rect((int)(hX * (float)r), 0, (int)(hX * (float)(r + 1)), H);
-                S.rectB[r] = rr;   // OLD buffer = roots (remap source)
-                if (S.ccount[r] > 0) {
-                    S.rectA[n] = rr; S.cntA[n] = S.ccount[r]; S.serA[n] = r;
-                    S.map4[r * 4 + 0] = S.map4[r * 4 + 1] = S.map4[r * 4 + 2] = S.map4[r * 4 + 3] = (uint16_t)n;
-                    n++;
-                }
-            }
-            ctl[56] = n;          // list size
-            ctl[57] = nIni;       // next serial
-            ctl[58] = 0;          // mode: 0 main, 1 final
-            ctl[59] = 0;          // finished
-        }
-        wave_lds_fence();
-        const int n = ctl[56];
-        for (int i = lane; i < n * 4; i += 64) S.ccount[i] = 0;
-    }
-    __syncthreads();
-    TR_PHASE(2, 0)
-    // CUR = A, OLD = B
-    uint64_t *rectC = S.rectA, *rectO = S.rectB;
-    uint32_t *cntC = S.cntA, *serC = S.serA;
-    uint32_t *cntO = S.cntB, *serO = S.serB;
+    const int Hroot = G.max_by - G.min_by;
     const int N = G.n_feat;
-    for (int iter = 0;; iter++) {
-        // read before the sweep barrier: wave 0 rewrites the control words in its node pass
-        const int n = ctl[56];
-        const int mode = ctl[58];
-        if (iter > 64 || n > NC) {   // runaway guard: never expected
-            if (tid == 0) atomicOr(err, 1);
-            break;
-        }
-        // ---- sweep: remap keys through map4 (OLD rect split), classify into CUR children ----
-        if (kr) {
+
+    auto run = [&](auto fastc) -> bool {
+        constexpr bool FAST = decltype(fastc)::value;
+        const bool keys_in_lds = M <= cfg.key_cap;
+        uint32_t* keys = keys_in_lds ? keysL : kscratch + (int64_t)f * P->n_slots_total + G.slot_base;
+        uint16_t* knode = keys_in_lds ? knodeL : nscratch + (int64_t)f * P->n_slots_total + G.slot_base;
+        // flattened gather: key k belongs to the cell c with cellstart[c] <= k < cellstart[c+1]
+        // (binary search in LDS); 4 keys per thread with their loads in flight together
+        auto gather4 = [&](int k0, uint32_t* kv) {
 #pragma unroll
-            for (int g = 0; g < kOctKR / 4; g++) {
-                if (4 * g * nt >= M) continue;   // block-uniform
-                uint32_t tg[4];
+            for (int u = 0; u < 4; u++) {
+                const int k = min(k0 + tid + u * nt, M - 1);
+                int lo = 0, hi = ncell - 1;
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) >> 1;
+                    if (S.cellstart[mid] <= k) lo = mid; else hi = mid - 1;
+                }
+                kv[u] = cbase[S.cslot[lo] + (k - S.cellstart[lo])];
+            }
+        };
+        auto root_of = [&](uint32_t key) {
+            const int r = (int)((float)cand_x(key) / hX);
+            return r < 0 ? 0 : (r >= nIni ? nIni - 1 : r);
+        };
+        auto root_rect = [&](int r) { return mk_rect((int)(hX * (float)r), 0, (int)(hX * (float)(r + 1)), Hroot); };
+        // node of the division: a rectangle (sweep) or (depth << 32 | path) (pyramid)
+        auto kid = [&](uint64_t r, int q) -> uint64_t {
+            if constexpr (FAST) return ((r + (1ull << 32)) & 0xFFFFFFFF00000000ull) | (uint64_t)((uint32_t)r * 4u + (uint32_t)q);
+            else return child_rect(r, q);
+        };
+        // With M <= kOctKR * nt (every C2/C3 level) the sweep path keeps each thread's keys
+        // k = tid + u * nt and their current nodes in registers for the whole division (kreg/nreg)
+        const bool kr = !FAST && M <= kOctKR * nt;
+        uint32_t kreg[kOctKR];
+        int nreg[kOctKR];
 #pragma unroll
-                for (int v = 0; v < 4; v++) {
-                    const int u = 4 * g + v;
-                    const int k = tid + u * nt;
-                    tg[v] = 0xFFFFFFFFu;
+        for (int u = 0; u < kOctKR; u++) { kreg[u] = 0u; nreg[u] = 0; }
+        if constexpr (FAST) {
+            // ---- 2. histogram of the depth-Dh cells, then the pyramid (two levels per barrier) ----
+            const int ob = poff(Dh);
+            for (int k0 = 0; k0 < M; k0 += 4 * nt) {
+                uint32_t kv[4];
+                gather4(k0, kv);
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int k = k0 + tid + u * nt;
                     if (k < M) {
-                        const int x = cand_x(kreg[u]), y = cand_y(kreg[u]);
-                        const int o = nreg[u];
-                        nreg[u] = S.map4[o * 4 + quad_of(rectO[o], x, y)];
+                        const int x = cand_x(kv[u]), y = cand_y(kv[u]);
+                        const int r = root_of(kv[u]);
+                        // DivideNode's ceil((x1 - x0) / 2.f) == (x1 - x0 + 1) >> 1 on these widths
+                        int x0 = (int)(hX * (float)r), x1 = (int)(hX * (float)(r + 1)), y0 = 0, y1 = Hroot;
+                        uint32_t path = (uint32_t)r;
+#pragma unroll
+                        for (int d = 0; d < kOctMaxDh; d++) {
+                            if (d < Dh) {
+                                const int sx = x0 + ((x1 - x0 + 1) >> 1), sy = y0 + ((y1 - y0 + 1) >> 1);
+                                const bool bx = x >= sx, by = y >= sy;
+                                x0 = bx ? sx : x0; x1 = bx ? x1 : sx;
+                                y0 = by ? sy : y0; y1 = by ? y1 : sy;
+                                path = path * 4u + (bx ? 1u : 0u) + (by ? 2u : 0u);
+                            }
+                        }
+                        atomicAdd(&pcnt[ob + (int)path], 1u);
+                        atomicMax(&pbest[ob + (int)path], ((unsigned long long)cand_s(kv[u]) << 56) |
+                                                              ((unsigned long long)(0xFFFFFFu - (uint32_t)k) << 32) | kv[u]);
                     }
                 }
+            }
+            __syncthreads();
+            TR_PHASE(2, 53)
+            // the two deepest levels below Dh by the block (a thread per depth-(Dh-2) cell), the
+            // rest by wave 0 level by level (no block barriers); the root counts feed the roots
+            int d = Dh;
+            if (d >= 2) {
+                const int o0 = poff(d), o1 = poff(d - 1), o2 = poff(d - 2);
+                for (int i = tid; i < (nIni << (2 * (d - 2))); i += nt) {
+                    uint32_t c2 = 0;
+                    unsigned long long b2 = 0;
 #pragma unroll
-                for (int v = 0; v < 4; v++) {
-                    const int u = 4 * g + v;
-                    const int k = tid + u * nt;
-                    if (k < M) {
-                        const int nd = nreg[u];
-                        if (cntC[nd] > 1)
-                            tg[v] = (uint32_t)(nd * 4 + quad_of(rectC[nd], cand_x(kreg[u]), cand_y(kreg[u])));
+                    for (int j = 0; j < 4; j++) {
+                        const int i1 = 4 * i + j;
+                        const uint4 c4 = *(const uint4*)&pcnt[o0 + 4 * i1];
+                        const ulonglong2 ba = *(const ulonglong2*)&pbest[o0 + 4 * i1];
+                        const ulonglong2 bb = *(const ulonglong2*)&pbest[o0 + 4 * i1 + 2];
+                        const uint32_t c1 = c4.x + c4.y + c4.z + c4.w;
+                        const unsigned long long b1 = max(max(ba.x, ba.y), max(bb.x, bb.y));
+                        pcnt[o1 + i1] = c1;
+                        pbest[o1 + i1] = b1;
+                        c2 += c1;
+                        b2 = max(b2, b1);
                     }
+                    pcnt[o2 + i] = c2;
+                    pbest[o2 + i] = b2;
                 }
-#pragma unroll
-                for (int v = 0; v < 4; v++) wave_aggregate_count(tg[v], S.ccount);
+                d -= 2;
+                __syncthreads();
+            }
+            if (w0) {
+                for (d = d - 1; d >= 0; d--) {
+                    const int o0 = poff(d + 1), o1 = poff(d);
+                    for (int i = lane; i < (nIni << (2 * d)); i += 64) {
+                        const uint4 c4 = *(const uint4*)&pcnt[o0 + 4 * i];
+                        const ulonglong2 ba = *(const ulonglong2*)&pbest[o0 + 4 * i];
+                        const ulonglong2 bb = *(const ulonglong2*)&pbest[o0 + 4 * i + 2];
+                        pcnt[o1 + i] = c4.x + c4.y + c4.z + c4.w;
+                        pbest[o1 + i] = max(max(ba.x, ba.y), max(bb.x, bb.y));
+                    }
+                    wave_lds_fence();
+                }
+                for (int i = lane; i < nIni; i += 64) S.ccount[i] = pcnt[i];   // root counts (poff(0) = 0)
             }
         } else {
-            for (int k0 = 0; k0 < M; k0 += nt) {
-                const int k = k0 + tid;
-                uint32_t tgt = 0xFFFFFFFFu;
-                if (k < M) {
-                    const uint32_t key = keys[k];
-                    const int x = cand_x(key), y = cand_y(key);
-                    const int o = knode[k];
-                    const int nd = S.map4[o * 4 + quad_of(rectO[o], x, y)];
-                    knode[k] = (uint16_t)nd;
-                    if (cntC[nd] > 1) tgt = (uint32_t)(nd * 4 + quad_of(rectC[nd], x, y));
+            // ---- 2. gather + root classification (run-aggregated counts per root) ----
+            auto root4 = [&](int k0, const uint32_t* kv, uint32_t* kr4, int* nr4) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int k = k0 + tid + u * nt;
+                    uint32_t tgt = 0xFFFFFFFFu;
+                    if (k < M) {
+                        keys[k] = kv[u];
+                        const int r = root_of(kv[u]);
+                        tgt = (uint32_t)r;
+                        if (kr4) { kr4[u] = kv[u]; nr4[u] = r; }
+                        else knode[k] = (uint16_t)r;
+                    }
+                    wave_aggregate_count(tgt, S.ccount);
                 }
-                wave_aggregate_count(tgt, S.ccount);
+            };
+            if (kr) {
+                // compile-time register slots: group g holds keys k = (4g + u) * nt + tid
+#pragma unroll
+                for (int g = 0; g < kOctKR / 4; g++) {
+                    if (4 * g * nt < M) {   // block-uniform
+                        uint32_t kv[4];
+                        gather4(4 * g * nt, kv);
+                        root4(4 * g * nt, kv, kreg + 4 * g, nreg + 4 * g);
+                    }
+                }
+            } else {
+                for (int k0 = 0; k0 < M; k0 += 4 * nt) {
+                    uint32_t kv[4];
+                    gather4(k0, kv);
+                    root4(k0, kv, nullptr, nullptr);
+                }
             }
         }
         __syncthreads();
-        if (iter == 1) { TR_PHASE(2, 41) }
-        if (mode == 0) {
-            // ---- MAIN pass (wave 0): divide every node with > 1 key ----
-            if (w0) {
-                const int serial0 = ctl[57];
-                const int per = (n + 63) >> 6;
-                const int b = min(lane * per, n), e = min(b + per, n);
-                int sc = 0, su = 0, se = 0;
-                for (int p = b; p < e; p++) {
-                    if (cntC[p] > 1) { sc += nonempty4(S.ccount + 4 * p); se += multi4(S.ccount + 4 * p); }
-                    else su += 1;
+        TR_PHASE(2, 54)
+        // ---- 3. roots (nIni <= 64 enforced by the host) ----
+        if (w0) {
+            if (lane == 0) {
+                int n = 0;
+                for (int r = 0; r < nIni; r++) {
+                    const uint64_t rr = FAST ? (uint64_t)r : root_rect(r);
+                    S.rectB[r] = rr;   // OLD buffer = roots (remap source)
+                    if (S.ccount[r] > 0) {
+                        S.rectA[n] = rr; S.cntA[n] = S.ccount[r]; S.serA[n] = r;
+                        S.map4[r * 4 + 0] = S.map4[r * 4 + 1] = S.map4[r * 4 + 2] = S.map4[r * 4 + 3] = (uint16_t)n;
+                        n++;
+                    }
                 }
-                const int ic = wave_incl_scan(sc), iu = wave_incl_scan(su), ie = wave_incl_scan(se);
-                const int T = __builtin_amdgcn_readlane(ic, 63), U = __builtin_amdgcn_readlane(iu, 63);
-                const int nToExpand = __builtin_amdgcn_readlane(ie, 63);
-                int cb = ic - sc, ub = iu - su;
-                for (int p = b; p < e; p++) {
-                    if (cntC[p] > 1) {
+                ctl[56] = n;          // list size
+                ctl[57] = nIni;       // next serial
+                ctl[58] = 0;          // mode: 0 main, 1 final
+                ctl[59] = 0;          // finished
+                ctl[62] = 0;          // pyramid too shallow: back to the sweep path
+            }
+            wave_lds_fence();
+            const int n = ctl[56];
+            for (int i = lane; i < n * 4; i += 64) S.ccount[i] = 0;
+        }
+        __syncthreads();
+        TR_PHASE(2, 0)
+        // CUR = A, OLD = B
+        uint64_t *rectC = S.rectA, *rectO = S.rectB;
+        uint32_t *cntC = S.cntA, *serC = S.serA;
+        uint32_t *cntO = S.cntB, *serO = S.serB;
+        for (int iter = 0;; iter++) {
+            // read before the round's barrier: wave 0 rewrites the control words in its node pass
+            const int n = ctl[56];
+            const int mode = ctl[58];
+            if (iter > 64 || n > NC) {   // runaway guard: never expected
+                if (tid == 0) atomicOr(err, 1);
+                break;
+            }
+            if constexpr (FAST) {
+                // ---- children counts of every node to divide, from the pyramid (wave 0) ----
+                if (w0) {
+                    bool deep = false;
+                    for (int p = lane; p < n; p += 64) {
+                        if (cntC[p] > 1) {
+                            const uint64_t cd = rectC[p];
+                            const int d = (int)(cd >> 32);
+                            if (d >= Dh) {
+                                deep = true;
+                            } else {
+                                const uint4 c4 = *(const uint4*)&pcnt[poff(d + 1) + 4 * (int)(uint32_t)cd];
+                                *(uint4*)&S.ccount[4 * p] = c4;
+                            }
+                        }
+                    }
+                    if (__ballot(deep) && lane == 0) ctl[62] = 1;
+                    wave_lds_fence();
+                }
+            } else {
+                // ---- sweep: remap keys through map4 (OLD rect split), classify into CUR children ----
+                if (kr) {
+#pragma unroll
+                    for (int g = 0; g < kOctKR / 4; g++) {
+                        if (4 * g * nt >= M) continue;   // block-uniform
+                        uint32_t tg[4];
+#pragma unroll
+                        for (int v = 0; v < 4; v++) {
+                            const int u = 4 * g + v;
+                            const int k = tid + u * nt;
+                            tg[v] = 0xFFFFFFFFu;
+                            if (k < M) {
+                                const int x = cand_x(kreg[u]), y = cand_y(kreg[u]);
+                                const int o = nreg[u];
+                                nreg[u] = S.map4[o * 4 + quad_of(rectO[o], x, y)];
+                            }
+                        }
+#pragma unroll
+                        for (int v = 0; v < 4; v++) {
+                            const int u = 4 * g + v;
+                            const int k = tid + u * nt;
+                            if (k < M) {
+                                const int nd = nreg[u];
+                                if (cntC[nd] > 1)
+                                    tg[v] = (uint32_t)(nd * 4 + quad_of(rectC[nd], cand_x(kreg[u]), cand_y(kreg[u])));
+                            }
+                        }
+#pragma unroll
+                        for (int v = 0; v < 4; v++) wave_aggregate_count(tg[v], S.ccount);
+                    }
+                } else {
+                    for (int k0 = 0; k0 < M; k0 += nt) {
+                        const int k = k0 + tid;
+                        uint32_t tgt = 0xFFFFFFFFu;
+                        if (k < M) {
+                            const uint32_t key = keys[k];
+                            const int x = cand_x(key), y = cand_y(key);
+                            const int o = knode[k];
+                            const int nd = S.map4[o * 4 + quad_of(rectO[o], x, y)];
+                            knode[k] = (uint16_t)nd;
+                            if (cntC[nd] > 1) tgt = (uint32_t)(nd * 4 + quad_of(rectC[nd], x, y));
+                        }
+                        wave_aggregate_count(tgt, S.ccount);
+                    }
+                }
+                __syncthreads();
+            }
+            if (iter == 1) { TR_PHASE(2, 41) }
+            // wave 0 only: after the fill, ctl[62] is final for this round
+            const bool stop = FAST && w0 && ctl[62];
+            if (mode == 0) {
+                // ---- MAIN pass (wave 0): divide every node with > 1 key ----
+                if (w0 && !stop) {
+                    const int serial0 = ctl[57];
+                    const int per = (n + 63) >> 6;
+                    const int b = min(lane * per, n), e = min(b + per, n);
+                    int sc = 0, su = 0, se = 0;
+                    for (int p = b; p < e; p++) {
+                        if (cntC[p] > 1) { sc += nonempty4(S.ccount + 4 * p); se += multi4(S.ccount + 4 * p); }
+                        else su += 1;
+                    }
+                    const int ic = wave_incl_scan(sc), iu = wave_incl_scan(su), ie = wave_incl_scan(se);
+                    const int T = __builtin_amdgcn_readlane(ic, 63), U = __builtin_amdgcn_readlane(iu, 63);
+                    const int nToExpand = __builtin_amdgcn_readlane(ie, 63);
+                    int cb = ic - sc, ub = iu - su;
+                    for (int p = b; p < e; p++) {
+                        if (cntC[p] > 1) {
+                            const int c = nonempty4(S.ccount + 4 * p);
+                            const int base = T - cb - c;          // pushed to the front: later parents first
+                            int r = 0;
+                            for (int q = 0; q < 4; q++) {
+                                const uint32_t cq = S.ccount[p * 4 + q];
+                                if (cq == 0) continue;
+                                const int pos = base + (c - 1 - r);   // n4..n1 order inside the block
+                                rectO[pos] = kid(rectC[p], q);
+                                cntO[pos] = cq; serO[pos] = serial0 + cb + r;
+                                S.map4[p * 4 + q] = (uint16_t)pos;
+                                r++;
+                            }
+                            cb += c;
+                        } else {
+                            const int pos = T + ub;
+                            rectO[pos] = rectC[p]; cntO[pos] = cntC[p]; serO[pos] = serC[p];
+                            S.map4[p * 4 + 0] = S.map4[p * 4 + 1] = S.map4[p * 4 + 2] = S.map4[p * 4 + 3] = (uint16_t)pos;
+                            ub++;
+                        }
+                    }
+                    const int newSize = T + U;
+                    wave_lds_fence();
+                    if constexpr (!FAST)
+                        for (int i = lane; i < min(newSize, NC) * 4; i += 64) S.ccount[i] = 0;
+                    if (lane == 0) {
+                        ctl[57] = serial0 + T;
+                        ctl[56] = newSize;
+                        if (newSize >= N || newSize == n) ctl[59] = 1;
+                        else if (newSize + nToExpand * 3 > N) ctl[58] = 1;
+                    }
+                }
+            } else {
+                // ---- FINAL phase: divide largest (size, serial) first until >= N ----
+                TR_PHASE(2, 48)
+                if (w0) {
+                    const int per = (n + 63) >> 6;
+                    const int b = min(lane * per, n), e = min(b + per, n);
+                    int s = 0;
+                    for (int p = b; p < e; p++) s += cntC[p] > 1;
+                    const int inc = wave_incl_scan(s);
+                    int pos = inc - s;
+                    for (int p = b; p < e; p++)
+                        if (cntC[p] > 1)
+                            S.skey2[pos++] = ((uint64_t)cntC[p] << 40) | ((uint64_t)serC[p] << 16) | (uint64_t)p;
+                    if (lane == 0) ctl[60] = __builtin_amdgcn_readlane(inc, 63);
+                }
+                TR_PHASE(2, 45)
+                __syncthreads();
+                TR_PHASE(2, 46)
+                const int K = ctl[60];
+                block_rank_sort_desc(S.skey2, S.skey, K);   // keys unique: (size, serial) order; ends in a barrier
+                TR_PHASE(2, 47)
+                if (w0 && !stop) {
+                    const int serial0 = ctl[57];
+                    const int per = (K + 63) >> 6;
+                    const int b = min(lane * per, K), e = min(b + per, K);
+                    // jstar: the first division (sorted order) after which the list holds >= N nodes
+                    int g = 0;
+                    for (int j = b; j < e; j++) g += nonempty4(S.ccount + 4 * (int)(S.skey[j] & 0xFFFF)) - 1;
+                    const int ig = wave_incl_scan(g);
+                    int run = n + ig - g, cand_j = K - 1;
+                    for (int j = b; j < e; j++) {
+                        run += nonempty4(S.ccount + 4 * (int)(S.skey[j] & 0xFFFF)) - 1;
+                        if (run >= N) { cand_j = j; break; }
+                    }
+                    int jstar = cand_j;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) jstar = min(jstar, __shfl_xor(jstar, o, 64));
+                    // children of the divisions 0..jstar, pushed to the front in division order
+                    int sc = 0;
+                    for (int j = b; j < min(e, jstar + 1); j++) sc += nonempty4(S.ccount + 4 * (int)(S.skey[j] & 0xFFFF));
+                    const int ic = wave_incl_scan(sc);
+                    const int Ctot = __builtin_amdgcn_readlane(ic, 63);
+                    for (int p = lane; p < n; p += 64) S.tD[p] = 1;
+                    wave_lds_fence();
+                    int cb = ic - sc;
+                    for (int j = b; j < min(e, jstar + 1); j++) {
+                        const int p = (int)(S.skey[j] & 0xFFFF);
                         const int c = nonempty4(S.ccount + 4 * p);
-                        const int base = T - cb - c;          // pushed to the front: later parents first
+                        const int base = Ctot - cb - c;
                         int r = 0;
                         for (int q = 0; q < 4; q++) {
                             const uint32_t cq = S.ccount[p * 4 + q];
                             if (cq == 0) continue;
-                            const int pos = base + (c - 1 - r);   // n4..n1 order inside the block
-                            rectO[pos] = child_rect(rectC[p], q);
-                            cntO[pos] = cq; serO[pos] = serial0 + cb + r;
-                            S.map4[p * 4 + q] = (uint16_t)pos;
+                            const int ps = base + (c - 1 - r);
+                            rectO[ps] = kid(rectC[p], q);
+                            cntO[ps] = cq; serO[ps] = serial0 + cb + r;
+                            S.map4[p * 4 + q] = (uint16_t)ps;
                             r++;
                         }
+                        S.tD[p] = 0;
                         cb += c;
-                    } else {
-                        const int pos = T + ub;
-                        rectO[pos] = rectC[p]; cntO[pos] = cntC[p]; serO[pos] = serC[p];
-                        S.map4[p * 4 + 0] = S.map4[p * 4 + 1] = S.map4[p * 4 + 2] = S.map4[p * 4 + 3] = (uint16_t)pos;
-                        ub++;
+                    }
+                    wave_lds_fence();
+                    // the other nodes keep their order behind the children
+                    const int pn = (n + 63) >> 6;
+                    const int bn = min(lane * pn, n), en = min(bn + pn, n);
+                    int st = 0;
+                    for (int p = bn; p < en; p++) st += S.tD[p];
+                    const int is = wave_incl_scan(st);
+                    int sb = is - st;
+                    for (int p = bn; p < en; p++) {
+                        if (S.tD[p]) {
+                            const int ps = Ctot + sb;
+                            rectO[ps] = rectC[p]; cntO[ps] = cntC[p]; serO[ps] = serC[p];
+                            S.map4[p * 4 + 0] = S.map4[p * 4 + 1] = S.map4[p * 4 + 2] = S.map4[p * 4 + 3] = (uint16_t)ps;
+                            sb++;
+                        }
+                    }
+                    const int newSize = Ctot + (n - (jstar + 1));
+                    wave_lds_fence();
+                    if constexpr (!FAST)
+                        for (int i = lane; i < min(newSize, NC) * 4; i += 64) S.ccount[i] = 0;
+                    if (lane == 0) {
+                        ctl[57] = serial0 + Ctot;
+                        ctl[56] = newSize;
+                        if (newSize >= N || newSize == n) ctl[59] = 1;
                     }
                 }
-                const int newSize = T + U;
-                wave_lds_fence();
-                for (int i = lane; i < min(newSize, NC) * 4; i += 64) S.ccount[i] = 0;
-                if (lane == 0) {
-                    ctl[57] = serial0 + T;
-                    ctl[56] = newSize;
-                    if (newSize >= N || newSize == n) ctl[59] = 1;
-                    else if (newSize + nToExpand * 3 > N) ctl[58] = 1;
-                }
             }
-        } else {
-            // ---- FINAL phase: divide largest (size, serial) first until >= N ----
-            TR_PHASE(2, 48)
-            if (w0) {
-                const int per = (n + 63) >> 6;
-                const int b = min(lane * per, n), e = min(b + per, n);
-                int s = 0;
-                for (int p = b; p < e; p++) s += cntC[p] > 1;
-                const int inc = wave_incl_scan(s);
-                int pos = inc - s;
-                for (int p = b; p < e; p++)
-                    if (cntC[p] > 1)
-                        S.skey2[pos++] = ((uint64_t)cntC[p] << 40) | ((uint64_t)serC[p] << 16) | (uint64_t)p;
-                if (lane == 0) ctl[60] = __builtin_amdgcn_readlane(inc, 63);
-            }
-            TR_PHASE(2, 45)
             __syncthreads();
-            TR_PHASE(2, 46)
-            const int K = ctl[60];
-            block_rank_sort_desc(S.skey2, S.skey, K);   // keys unique: (size, serial) order; ends in a barrier
-            TR_PHASE(2, 47)
-            if (w0) {
-                const int serial0 = ctl[57];
-                const int per = (K + 63) >> 6;
-                const int b = min(lane * per, K), e = min(b + per, K);
-                // jstar: the first division (sorted order) after which the list holds >= N nodes
-                int g = 0;
-                for (int j = b; j < e; j++) g += nonempty4(S.ccount + 4 * (int)(S.skey[j] & 0xFFFF)) - 1;
-                const int ig = wave_incl_scan(g);
-                int run = n + ig - g, cand_j = K - 1;
-                for (int j = b; j < e; j++) {
-                    run += nonempty4(S.ccount + 4 * (int)(S.skey[j] & 0xFFFF)) - 1;
-                    if (run >= N) { cand_j = j; break; }
-                }
-                int jstar = cand_j;
+            if (iter == 1) { TR_PHASE(2, 44) }
+            if constexpr (FAST) {
+                if (ctl[62]) return false;   // every thread, after the barrier: the level goes to the sweep path
+            }
+            // swap: NEXT (written into the O buffers) becomes CUR, CUR becomes OLD
+            { uint64_t* t = rectC; rectC = rectO; rectO = t; }
+            { uint32_t* t = cntC; cntC = cntO; cntO = t; }
+            { uint32_t* t = serC; serC = serO; serO = t; }
+            TR_PHASE(2, 1 + (iter < 28 ? iter : 28) + (mode ? 32 : 0))
+            if (ctl[59]) break;
+        }
+        const int n = ctl[56];
+        if constexpr (!FAST) {
+            // ---- retained key per final node: max (response, then lowest key index) over the
+            // keys of the node; keys reach their final node through the last division's map4 ----
+            for (int i = tid; i < n; i += nt) S.cbest[i] = 0;
+            __syncthreads();
+            TR_PHASE(2, 60)
+            if (kr) {
 #pragma unroll
-                for (int o = 1; o < 64; o <<= 1) jstar = min(jstar, __shfl_xor(jstar, o, 64));
-                // children of the divisions 0..jstar, pushed to the front in division order
-                int sc = 0;
-                for (int j = b; j < min(e, jstar + 1); j++) sc += nonempty4(S.ccount + 4 * (int)(S.skey[j] & 0xFFFF));
-                const int ic = wave_incl_scan(sc);
-                const int Ctot = __builtin_amdgcn_readlane(ic, 63);
-                for (int p = lane; p < n; p += 64) S.tD[p] = 1;
-                wave_lds_fence();
-                int cb = ic - sc;
-                for (int j = b; j < min(e, jstar + 1); j++) {
-                    const int p = (int)(S.skey[j] & 0xFFFF);
-                    const int c = nonempty4(S.ccount + 4 * p);
-                    const int base = Ctot - cb - c;
-                    int r = 0;
-                    for (int q = 0; q < 4; q++) {
-                        const uint32_t cq = S.ccount[p * 4 + q];
-                        if (cq == 0) continue;
-                        const int ps = base + (c - 1 - r);
-                        rectO[ps] = child_rect(rectC[p], q);
-                        cntO[ps] = cq; serO[ps] = serial0 + cb + r;
-                        S.map4[p * 4 + q] = (uint16_t)ps;
-                        r++;
-                    }
-                    S.tD[p] = 0;
-                    cb += c;
-                }
-                wave_lds_fence();
-                // the other nodes keep their order behind the children
-                const int pn = (n + 63) >> 6;
-                const int bn = min(lane * pn, n), en = min(bn + pn, n);
-                int st = 0;
-                for (int p = bn; p < en; p++) st += S.tD[p];
-                const int is = wave_incl_scan(st);
-                int sb = is - st;
-                for (int p = bn; p < en; p++) {
-                    if (S.tD[p]) {
-                        const int ps = Ctot + sb;
-                        rectO[ps] = rectC[p]; cntO[ps] = cntC[p]; serO[ps] = serC[p];
-                        S.map4[p * 4 + 0] = S.map4[p * 4 + 1] = S.map4[p * 4 + 2] = S.map4[p * 4 + 3] = (uint16_t)ps;
-                        sb++;
+                for (int u = 0; u < kOctKR; u++) {
+                    const int k = tid + u * nt;
+                    if (k < M) {
+                        const uint32_t key = kreg[u];
+                        const int o = nreg[u];
+                        const int nd = S.map4[o * 4 + quad_of(rectO[o], cand_x(key), cand_y(key))];
+                        atomicMax(&S.cbest[nd], pack_best(cand_s(key), k));
                     }
                 }
-                const int newSize = Ctot + (n - (jstar + 1));
-                wave_lds_fence();
-                for (int i = lane; i < min(newSize, NC) * 4; i += 64) S.ccount[i] = 0;
-                if (lane == 0) {
-                    ctl[57] = serial0 + Ctot;
-                    ctl[56] = newSize;
-                    if (newSize >= N || newSize == n) ctl[59] = 1;
+            } else {
+                for (int k = tid; k < M; k += nt) {
+                    const uint32_t key = keys[k];
+                    const int o = knode[k];
+                    const int nd = S.map4[o * 4 + quad_of(rectO[o], cand_x(key), cand_y(key))];
+                    atomicMax(&S.cbest[nd], pack_best(cand_s(key), k));
                 }
             }
+            __syncthreads();
         }
+        TR_PHASE(2, 61)
+        // ---- output in list order: retained key per node, lapping flag, and its rank among the
+        // same-flag nodes from one block scan per 1024 nodes ----
+        const int ncap = min(n, G.kp_cap);
+        LevelKp* out = lvl_kp + (int64_t)f * P->kp_slots_total + G.kp_base;
+        int lap_run = 0;
+        for (int p0 = 0; p0 < ncap; p0 += nt) {
+            const int p = p0 + tid;
+            int lap = 0, x = 0, y = 0, sc = 0;
+            if (p < ncap) {
+                uint32_t key;
+                if constexpr (FAST) {
+                    const uint64_t cd = rectC[p];
+                    key = (uint32_t)pbest[poff((int)(cd >> 32)) + (int)(uint32_t)cd];
+                } else {
+                    key = keys[(int)(0xFFFFFFu - (S.cbest[p] & 0xFFFFFFu))];
+                }
+                x = cand_x(key) + G.min_bx; y = cand_y(key) + G.min_by;
+                sc = cand_s(key);
+                const float xs = (l == 0) ? (float)x : (float)x * G.scale;
+                lap = (xs >= (float)cfg.lap0 && xs <= (float)cfg.lap1) ? 1 : 0;
+            }
+            int tot;
+            const int before = lap_run + block_excl_scan(lap, ctl, &tot);   // same-flag nodes before p
+            if (p < ncap) {
+                const int rank = lap ? before : p - before;
+                LevelKp r;
+                r.x = (int16_t)x; r.y = (int16_t)y;
+                r.srl = (uint32_t)sc | ((uint32_t)lap << 8) | ((uint32_t)rank << 9);
+                out[p] = r;
+            }
+            lap_run += tot;
+        }
+        if (tid == 0) {
+            lvl_cnt[f * P->n_levels + l] = ncap;
+            lvl_nlap[f * P->n_levels + l] = lap_run;
+            if (n > G.kp_cap) atomicOr(err, 2);
+        }
+        return true;
+    };
+    if (Dh) {
+        if (run(std::true_type{})) {
+            TR_PHASE(2, 63)
+            TR_END(2)
+            return;
+        }
+        // a node too deep for the pyramid: the sweep path from the gather on
+        for (int i = tid; i < nIni * 4; i += nt) S.ccount[i] = 0;
         __syncthreads();
-        if (iter == 1) { TR_PHASE(2, 44) }
-        // swap: NEXT (written into the O buffers) becomes CUR, CUR becomes OLD
-        { uint64_t* t = rectC; rectC = rectO; rectO = t; }
-        { uint32_t* t = cntC; cntC = cntO; cntO = t; }
-        { uint32_t* t = serC; serC = serO; serO = t; }
-        TR_PHASE(2, 1 + (iter < 28 ? iter : 28) + (mode ? 32 : 0))
-        if (ctl[59]) break;
     }
-    // ---- retained key per final node: max (response, then lowest key index) over the keys of
-    // the node; keys reach their final node through the last division's map4 ----
-    const int n = ctl[56];
-    for (int i = tid; i < n; i += nt) S.cbest[i] = 0;
-    __syncthreads();
-    TR_PHASE(2, 60)
-    if (kr) {
-#pragma unroll
-        for (int u = 0; u < kOctKR; u++) {
-            const int k = tid + u * nt;
-            if (k < M) {
-                const uint32_t key = kreg[u];
-                const int o = nreg[u];
-                const int nd = S.map4[o * 4 + quad_of(rectO[o], cand_x(key), cand_y(key))];
-                atomicMax(&S.cbest[nd], pack_best(cand_s(key), k));
-            }
-        }
-    } else {
-        for (int k = tid; k < M; k += nt) {
-            const uint32_t key = keys[k];
-            const int o = knode[k];
-            const int nd = S.map4[o * 4 + quad_of(rectO[o], cand_x(key), cand_y(key))];
-            atomicMax(&S.cbest[nd], pack_best(cand_s(key), k));
-        }
-    }
-    __syncthreads();
-    TR_PHASE(2, 61)
-    // ---- output in list order: retained key per node, lapping flag, and its rank among the
-    // same-flag nodes from one block scan per 1024 nodes ----
-    const int ncap = min(n, G.kp_cap);
-    LevelKp* out = lvl_kp + (int64_t)f * P->kp_slots_total + G.kp_base;
-    int lap_run = 0;
-    for (int p0 = 0; p0 < ncap; p0 += nt) {
-        const int p = p0 + tid;
-        int lap = 0, x = 0, y = 0, sc = 0;
-        if (p < ncap) {
-            const int k = (int)(0xFFFFFFu - (S.cbest[p] & 0xFFFFFFu));
-            const uint32_t key = keys[k];
-            x = cand_x(key) + G.min_bx; y = cand_y(key) + G.min_by;
-            sc = cand_s(key);
-            const float xs = (l == 0) ? (float)x : (float)x * G.scale;
-            lap = (xs >= (float)cfg.lap0 && xs <= (float)cfg.lap1) ? 1 : 0;
-        }
-        int tot;
-        const int before = lap_run + block_excl_scan(lap, ctl, &tot);   // same-flag nodes before p
-        if (p < ncap) {
-            const int rank = lap ? before : p - before;
-            LevelKp r;
-            r.x = (int16_t)x; r.y = (int16_t)y;
-            r.srl = (uint32_t)sc | ((uint32_t)lap << 8) | ((uint32_t)rank << 9);
-            out[p] = r;
-        }
-        lap_run += tot;
-    }
-    if (tid == 0) {
-        lvl_cnt[f * P->n_levels + l] = ncap;
-        lvl_nlap[f * P->n_levels + l] = lap_run;
-        if (n > G.kp_cap) atomicOr(err, 2);
-    }
+    run(std::false_type{});
     TR_PHASE(2, 63)
     TR_END(2)
 }

@@ -468,8 +468,15 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
         if (c->d_lvl_done.p != before)
             HIPOK(hipMemsetAsync(c->d_lvl_done.p, 0, sizeof(int) * (size_t)B * P.n_levels, st));
     }
+    // octree division engine (read per call so that tests can switch it): ORBHIP_OCTREE_SWEEP=1 runs
+    // the sweep path only, ORBHIP_OCTREE_DH=d caps the pyramid depth (a shallow cap forces the
+    // pyramid path's fallback to the sweep path)
+    const char* e_sw = std::getenv("ORBHIP_OCTREE_SWEEP");
+    const char* e_dh = std::getenv("ORBHIP_OCTREE_DH");
+    const int oct_fast = (e_sw && e_sw[0] == '1') ? 0 : 1;
+    const int oct_max_dh = e_dh ? std::max(1, std::min(6, std::atoi(e_dh))) : 6;
     GraphKey key;
-    key.add(1).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
+    key.add(1).add((uint64_t)oct_fast).add((uint64_t)oct_max_dh).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
         .add((uint64_t)lap1).ptr(d_kps).ptr(d_desc).add((uint64_t)cap).ptr(d_n).ptr(d_mono).ptr(st).ptr(c->d_pyr.p)
         .ptr(c->d_cand.p).ptr(c->d_kscratch.p).ptr(c->d_nscratch.p).ptr(c->d_cand_cnt.p).ptr(c->d_lvl_kp.p)
         .ptr(c->d_lvl_cnt.p).ptr(c->d_lvl_nlap.p).ptr(c->d_err.p).ptr(c->d_lvl_done.p);
@@ -508,6 +515,8 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
         }
         OctreeCfg oc = pl->oct;
         oc.lap0 = lap0; oc.lap1 = lap1;
+        oc.fast = oct_fast;
+        oc.max_dh = oct_max_dh;
         tm.begin(3, st);
         launch_octree(pl->d_plan.p, P, pl->d_cells.p, c->d_cand.p, c->d_cand_cnt.p, c->d_kscratch.p, c->d_nscratch.p,
                       c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, oc, c->d_err.p, c->d_lvl_done.p, B, st);

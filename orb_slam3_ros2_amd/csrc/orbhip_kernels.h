@@ -21,6 +21,8 @@ struct OctreeCfg {
     int sort_cap;          // power of two >= node_cap
     int key_cap;           // keys kept in LDS when a level has <= key_cap candidates
     int lap0, lap1;        // vLappingArea
+    int fast;              // 1: pyramid division first (sweep path as its fallback); 0: sweep path only
+    int max_dh;            // deepest pyramid level allowed (<= 6; tests lower it to force the fallback)
 };
 
 // Live timing of one pipeline stage with hipEvents on the launch stream.

@@ -257,3 +257,34 @@ def test_graph_replay_recomputes_from_current_inputs(monkeypatch):
             assert torch.equal(kps[f, :c], rk[f, :c]) and torch.equal(desc[f, :c], rd[f, :c]), (i, f)
         assert torch.equal(mm[:, : int(rn[0])], rmm[:, : int(rn[0])]), i
     assert lib().orbhip_launch_graphs(ext.ctx.handle) >= 2   # extract + match replayed
+
+
+def _clustered_frame(seed, w=640, h=480):
+    """A flat frame with one small, dense, high-contrast patch: thousands of FAST candidates in
+    a few cells, so DistributeOctTree divides deep (far below the pyramid depth) around it."""
+    rng = np.random.default_rng(seed)
+    img = np.full((h, w), 128, np.uint8)
+    y0, x0 = h // 3, w // 2
+    img[y0:y0 + 40, x0:x0 + 48] = rng.integers(0, 256, size=(40, 48), dtype=np.uint8)
+    return img
+
+
+@pytest.mark.parametrize("engine", ["pyramid", "sweep", "dh1", "dh2", "dh3"])
+def test_octree_engines(oracle, monkeypatch, engine):
+    """k_octree divides with the pyramid (counts of every depth-d cell, no key sweeps) and falls
+    back to the key-sweep path when a node to divide sits at the pyramid's deepest level. Each
+    engine, and the fallback forced by shallow pyramids (ORBHIP_OCTREE_DH), bit-exact against the
+    oracle on C2 / C3-sized frames, 5000 features, noise and clustered keys."""
+    from orb_slam3_ros2_amd import ORBextractor
+    if engine == "sweep":
+        monkeypatch.setenv("ORBHIP_OCTREE_SWEEP", "1")
+    elif engine != "pyramid":
+        monkeypatch.setenv("ORBHIP_OCTREE_DH", engine[2:])
+    rng = np.random.default_rng(17)
+    e1000 = ORBextractor(1000, 1.2, 8, 20, 7)
+    for img in (synthetic_frame(40, 640, 480), synthetic_frame(41, 1280, 720), _clustered_frame(42),
+                rng.integers(0, 256, size=(480, 640), dtype=np.uint8), _clustered_frame(43, 1280, 720)):
+        _check(e1000, oracle, img)
+    e5000 = ORBextractor(5000, 1.2, 8, 20, 7)
+    for img in (synthetic_frame(44, 640, 480), _clustered_frame(45)):
+        _check(e5000, oracle, img, nfeatures=5000)
