@@ -149,14 +149,9 @@ __device__ __forceinline__ int small_div(int i, float inv_d) { return (int)(((fl
 // global round trip loads every table entry and the level-0 cone, then the levels follow from LDS.
 __device__ __forceinline__ void wait_vm_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// SYNC (k_pyr_fast): the owned pixels of each level leave from LDS as device-coherent (sc1,
-// write-through) dword stores, and the tile is counted in lvl_done[f * L] once all of them are
-// performed, for the FAST work-groups of the same launch that wait on it.
-template <bool SYNC>
 __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P, const FrameBufs& fb,
                                               const ConeRect* __restrict__ rects, const int* __restrict__ ctab,
-                                              int tab_stride, uint8_t* __restrict__ cone, int tile, int f,
-                                              int* __restrict__ lvl_done) {
+                                              int tab_stride, uint8_t* __restrict__ cone, int tile, int f) {
     TR_BEGIN()
     const int L = P->n_levels, tid = threadIdx.x, nt = blockDim.x;
     const ConeRect* R = rects + (size_t)tile * kMaxLevels;
@@ -247,44 +242,10 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
             }
             const uint8_t u = (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v));
             cone[boff[l] + i] = u;
-            if constexpr (!SYNC) {
-                if (x >= r.ox0 && x < r.ox1 && y >= r.oy0 && y < r.oy1) dst[(int64_t)y * D.pitch + x] = u;
-            }
+            if (x >= r.ox0 && x < r.ox1 && y >= r.oy0 && y < r.oy1) dst[(int64_t)y * D.pitch + x] = u;
         }
         __syncthreads();
-        if constexpr (SYNC) {
-            // the owned pixels leave from LDS as device-coherent stores: aligned dwords in the
-            // interior of each row, bytes at its ends; not waited for until after the last level
-            const int xa = (r.ox0 + 3) & ~3, xb = r.ox1 & ~3, oh = r.oy1 - r.oy0;
-            const int nlead = max(0, min(xa, r.ox1) - r.ox0);
-            const int nmid = max(0, xb - xa) >> 2;
-            const int ntail = max(0, r.ox1 - max(xa, xb));
-            const int per = nlead + nmid + ntail;
-            if (per > 0 && oh > 0) {
-                const float inv_per = 1.0f / (float)per;
-                for (int i = tid; i < per * oh; i += nt) {
-                    const int yy = small_div(i, inv_per), k = i - yy * per;
-                    const int y = r.oy0 + yy;
-                    const uint8_t* srow = cone + boff[l] + (y - r.ny0) * nw - r.nx0;   // indexed by x
-                    uint8_t* drow = dst + (int64_t)y * D.pitch;
-                    if (k >= nlead && k < nlead + nmid) {
-                        const int x = xa + 4 * (k - nlead);
-                        const uint32_t v = (uint32_t)srow[x] | ((uint32_t)srow[x + 1] << 8) |
-                                           ((uint32_t)srow[x + 2] << 16) | ((uint32_t)srow[x + 3] << 24);
-                        __hip_atomic_store((uint32_t*)(drow + x), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    } else {
-                        const int x = k < nlead ? r.ox0 + k : max(xa, xb) + (k - nlead - nmid);
-                        __hip_atomic_store(drow + x, srow[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                }
-            }
-        }
         TR_PHASE(0, l)
-    }
-    if constexpr (SYNC) {
-        wait_vm_all();      // this thread's pyramid stores are performed
-        __syncthreads();
-        if (tid == 0) atomicAdd(&lvl_done[f * L], 1);   // one more tile done (every level)
     }
     TR_END(0)
 }
@@ -294,7 +255,7 @@ __global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict
                                                    int tab_stride, int xrun) {
     extern __shared__ __attribute__((aligned(16))) uint8_t cone[];
     const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
-    pyr_cone_body<false>(P, fb, rects, ctab, tab_stride, cone, lg % X, lg / X, nullptr);
+    pyr_cone_body(P, fb, rects, ctab, tab_stride, cone, lg % X, lg / X);
 }
 
 // ---------------------------------------------------------------------------
@@ -342,7 +303,7 @@ __device__ __forceinline__ bool fast_pair_test(const int* d, int t) {
     return (bright < -t) | (dark > t);
 }
 
-// LDS of one FAST cell (static in k_fast_cells, carved from the dynamic buffer in k_pyr_fast)
+// LDS of one FAST cell (static in k_fast_cells)
 struct FastLds {
     uint8_t* win;                   // kWinMax^2 window
     uint8_t* mv;                    // kWinMax^2 strength map
@@ -353,16 +314,12 @@ struct FastLds {
     uint16_t* clist;                // kClistCap pair-test survivors (strength to compute)
     int* ncand;
 };
-constexpr size_t kFastLdsBytes = 2 * kWinMax * kWinMax + 2 * 96 * 8 + 96 * 4 + 16 + 2 * kClistCap + 16;
 
-// SYNC (k_pyr_fast): a cell of level l > 0 first waits until every cone tile of the launch is
-// done, then reads its window device-coherent (sc1 loads: the tiles wrote it
-// through other XCDs' L2s a moment ago). A bounded wait: the error flag instead of a hang.
-template <int NT, bool SYNC>
+template <int NT>
 __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P, const CellGeom* __restrict__ cells,
                                                const FrameBufs& fb, uint32_t* __restrict__ cand,
                                                int* __restrict__ cand_cnt, int* __restrict__ err, int cell, int f,
-                                               const FastLds& LS, const int* __restrict__ lvl_done, int ntiles) {
+                                               const FastLds& LS) {
     uint8_t* const win = LS.win;
     uint8_t* const mv = LS.mv;
     unsigned long long (*const bmask)[96] = LS.bmask;
@@ -377,8 +334,7 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int wc = cg.wc, hc = cg.hc;
     int* cnt_out = cand_cnt + (int64_t)f * P->n_cells_total + cell;
-    // the octree (next launch) reports here; an agent-scope store, so that the reset cannot land
-    // after (and erase) a timeout bit another XCD's cell sets with atomicOr in the SYNC form
+    // the error words of the extraction: cleared here, set by the octree (next launch)
     if (cell == 0 && f == 0 && tid < 4) __hip_atomic_store(&err[tid], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (wc <= 6 || hc <= 6) {
         if (tid == 0) *cnt_out = 0;
@@ -387,23 +343,6 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     const LevelGeom& G = P->lv[cg.level];
     ImgRef im = level_img(P, fb, f, cg.level);
     const uint8_t* base = im.p + (int64_t)cg.y0 * im.pitch + cg.x0;
-    const bool coherent = SYNC && cg.level > 0;
-    if (coherent) {
-        if (tid == 0) {
-            const int* d = lvl_done + f * P->n_levels;   // tiles done
-            for (int it = 0; __hip_atomic_load(d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ntiles; it++) {
-                if (it > (1 << 22)) {   // ~0.1 s: never expected
-                    atomicOr(err, 4);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-        }
-        __syncthreads();
-    }
-    auto ld4 = [&](const uint32_t* q) -> uint32_t {
-        return coherent ? __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *q;
-    };
     // ---- window -> LDS: all loads of a thread issued back to back. When the rows are 4-byte
     // aligned (pyramid levels always; the caller's frame when its pointer and stride are), the
     // window moves as aligned dwords into LDS rows of kWinP bytes, shifted by sh = base & 3 ----
@@ -425,7 +364,7 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
                 for (int u = 0; u < NU; u++) {
                     const int i = min(tid + NT * u, tot - 1);
                     const int yy = small_div(i, inv_n), xx = i - yy * nwd;
-                    v[u] = ld4(&b4[(int64_t)yy * p4 + xx]);
+                    v[u] = b4[(int64_t)yy * p4 + xx];
                     li[u] = yy * (kWinP / 4) + xx;
                 }
 #pragma unroll
@@ -434,7 +373,7 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
             } else {
                 for (int i = tid; i < tot; i += NT) {
                     const int yy = small_div(i, inv_n), xx = i - yy * nwd;
-                    w4[yy * (kWinP / 4) + xx] = ld4(&b4[(int64_t)yy * p4 + xx]);
+                    w4[yy * (kWinP / 4) + xx] = b4[(int64_t)yy * p4 + xx];
                 }
             }
         } else {
@@ -577,36 +516,7 @@ __global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict
     __shared__ int ncand;
     const FastLds LS{win, mv, bmask, woff, &wsel, &wtot, clist, &ncand};
     const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
-    fast_cell_body<NT, false>(P, cells, fb, cand, cand_cnt, err, lg % X, lg / X, LS, nullptr, 0);
-}
-
-// ---------------------------------------------------------------------------
-// k_pyr_fast: k_pyr_cone and k_fast_cells in ONE launch (the cone path, small batches). Work-
-// groups [0, ntiles) are the cone tiles, the rest FAST cells. Work-groups are dispatched in
-// index order, so every tile is resident or done before any cell waits on it: level-0 cells
-// (the frame itself) start at once, next to the tiles; the cells of the other levels start when
-// every tile is done. The counters are reset by k_octree (the next launch on the stream).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_pyr_fast(const ExtractPlan* __restrict__ P, FrameBufs fb,
-                                                   const ConeRect* __restrict__ rects, const int* __restrict__ ctab,
-                                                   int tab_stride, int ntiles, const CellGeom* __restrict__ cells,
-                                                   uint32_t* __restrict__ cand, int* __restrict__ cand_cnt,
-                                                   int* __restrict__ err, int* __restrict__ lvl_done) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t cone[];
-    if ((int)blockIdx.x < ntiles) {
-        pyr_cone_body<true>(P, fb, rects, ctab, tab_stride, cone, blockIdx.x, blockIdx.y, lvl_done);
-        return;
-    }
-    uint8_t* b = cone;
-    FastLds LS;
-    LS.win = b; b += kWinMax * kWinMax;
-    LS.mv = b; b += kWinMax * kWinMax;
-    LS.bmask = (unsigned long long (*)[96])b; b += 2 * 96 * 8;
-    LS.woff = (int*)b; b += 96 * 4;
-    LS.wsel = (int*)b; LS.wtot = (int*)b + 1; LS.ncand = (int*)b + 2; b += 16;
-    LS.clist = (uint16_t*)b;
-    fast_cell_body<1024, true>(P, cells, fb, cand, cand_cnt, err, (int)blockIdx.x - ntiles, blockIdx.y, LS, lvl_done,
-                               ntiles);
+    fast_cell_body<NT>(P, cells, fb, cand, cand_cnt, err, lg % X, lg / X, LS);
 }
 
 // ---------------------------------------------------------------------------
@@ -783,16 +693,14 @@ __device__ __forceinline__ int multi4(const uint32_t* c) { return (c[0] > 1) + (
 constexpr int kOctMaxDh = 6;
 
 __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__ P, const CellGeom* __restrict__ cells,
-                                                 const uint32_t* __restrict__ cand, const int* __restrict__ cand_cnt,
+                                                 const uint16_t* __restrict__ otab, const uint32_t* __restrict__ cand, const int* __restrict__ cand_cnt,
                                                  uint32_t* __restrict__ kscratch, uint16_t* __restrict__ nscratch,
                                                  LevelKp* __restrict__ lvl_kp, int* __restrict__ lvl_cnt,
-                                                 int* __restrict__ lvl_nlap, OctreeCfg cfg, int* __restrict__ err,
-                                                 int* __restrict__ lvl_done) {
+                                                 int* __restrict__ lvl_nlap, OctreeCfg cfg, int* __restrict__ err) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     TR_BEGIN()
     // grid (frame, level): the level-0 work-groups (the longest) of every frame dispatch first
     const int f = blockIdx.x, l = blockIdx.y;
-    if (threadIdx.x == 0) lvl_done[f * P->n_levels + l] = 0;   // k_pyr_fast's counters, for the next frame
     const LevelGeom& G = P->lv[l];
     const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63;
     const bool w0 = tid < 64;
@@ -825,13 +733,37 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
     // level d starts at poff(d), a multiple of 4 cells (16-byte vector reads of 4 siblings)
     const int nIni4 = (nIni + 3) & ~3;
     auto poff = [&](int d) { return d == 0 ? 0 : nIni4 + nIni * ((1 << (2 * d)) - 4) / 3; };
+    // behind the pyramid: the depth-Dh x interval of every level column (root << 8 | x path bits)
+    // and y interval of every row, so that a key's cell is two table reads
+    const int Wlev = G.max_bx - G.min_bx, Hroot = G.max_by - G.min_by;
+    const size_t tab_bytes = 2 * (size_t)Wlev + (size_t)Hroot + 32;
+    // depth: one level below the first with >= N cells (ceil(log4(N / nIni)) + 1), where the
+    // final divisions of a typical level stop; a deeper division takes the sweep path
     int Dh = 0;
-    if (cfg.fast)
-        for (int d = min(cfg.max_dh, kOctMaxDh); d >= 1; d--)
-            if ((size_t)poff(d + 1) * 12 <= preg_bytes) { Dh = d; break; }
+    if (cfg.fast) {
+        int want = 1;
+        while (want < kOctMaxDh && (nIni << (2 * want)) < G.n_feat) want++;
+        want = min(want + 1, min(cfg.max_dh, kOctMaxDh));
+        for (int d = want; d >= 1; d--)
+            if ((size_t)poff(d + 1) * 12 + tab_bytes <= preg_bytes) { Dh = d; break; }
+    }
     unsigned long long* pbest = (unsigned long long*)keysL;
     uint32_t* pcnt = (uint32_t*)(pbest + (Dh ? poff(Dh + 1) : 0));
-
+    uint16_t* xtab = (uint16_t*)(pcnt + (Dh ? poff(Dh + 1) : 0));
+    uint8_t* ytab = (uint8_t*)(xtab + Wlev);
+    const float hX = G.hX;
+    auto root_of_x = [&](int x) {
+        const int r = (int)((float)x / hX);
+        return r < 0 ? 0 : (r >= nIni ? nIni - 1 : r);
+    };
+    // the plan's interval tables (6 split levels) cut to Dh levels, copied to LDS; entries
+    // tid and tid + nt are loaded with the cell counts, the rest (wide levels) on the way
+    const int ntab = Dh ? Wlev + Hroot : 0;
+    const uint16_t* otl = otab + G.oct_tab_off;
+    auto tab_put = [&](int i, uint32_t v) {
+        if (i < Wlev) xtab[i] = (uint16_t)((v & 0xFF00u) | ((v & 0xFFu) >> (kOctMaxDh - Dh)));
+        else ytab[i - Wlev] = (uint8_t)(v >> (kOctMaxDh - Dh));
+    };
     // ---- 1. candidate count per cell -> cell-major key order (wave 0 scans the cells) ----
     const int ncell = G.n_cells;
     const int* cc = cand_cnt + (int64_t)f * P->n_cells_total + G.cell_base;
@@ -848,10 +780,12 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
             }
         }
     };
+    const uint32_t* cbase = cand + (int64_t)f * P->n_slots_total;
     if (ncell <= nt) {
         // one cell per thread: every count / slot load in flight at once, one block scan
         const int c = tid < ncell ? cc[tid] : 0;
         const int so = tid < ncell ? cells[G.cell_base + tid].slot_off : 0;
+        const uint32_t t0 = tid < ntab ? otl[tid] : 0u, t1 = tid + nt < ntab ? otl[tid + nt] : 0u;
         zero_pyramid();
         if (tid < ncell) S.cslot[tid] = so;
         int M0;
@@ -859,6 +793,9 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
         if (tid < ncell) S.cellstart[tid] = ex;
         if (tid == 0) { S.cellstart[ncell] = M0; ctl[55] = M0; }
         for (int i = tid; i < nIni * 4; i += nt) S.ccount[i] = 0;
+        if (tid < ntab) tab_put(tid, t0);
+        if (tid + nt < ntab) tab_put(tid + nt, t1);
+        for (int i = tid + 2 * nt; i < ntab; i += nt) tab_put(i, otl[i]);
     } else if (w0) {
         for (int i = lane; i < ncell; i += 64) {
             S.cellstart[i] = cc[i];
@@ -869,13 +806,13 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
         if (lane == 0) { S.cellstart[ncell] = M0; ctl[55] = M0; }
         for (int i = lane; i < nIni * 4; i += 64) S.ccount[i] = 0;
     }
-    if (ncell > nt) zero_pyramid();
+    if (ncell > nt) {
+        zero_pyramid();
+        for (int i = tid; i < ntab; i += nt) tab_put(i, otl[i]);
+    }
     __syncthreads();
     TR_PHASE(2, 50)
     const int M = ctl[55];
-    const uint32_t* cbase = cand + (int64_t)f * P->n_slots_total;
-    const float hX = G.hX;
-    const int Hroot = G.max_by - G.min_by;
     const int N = G.n_feat;
 
     auto run = [&](auto fastc) -> bool {
@@ -885,22 +822,24 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
         uint16_t* knode = keys_in_lds ? knodeL : nscratch + (int64_t)f * P->n_slots_total + G.slot_base;
         // flattened gather: key k belongs to the cell c with cellstart[c] <= k < cellstart[c+1]
         // (binary search in LDS); 4 keys per thread with their loads in flight together
+        // the 4 searches step together (a uniform trip count), so their LDS reads overlap
+        int top = 1;
+        while (2 * top < ncell) top *= 2;
         auto gather4 = [&](int k0, uint32_t* kv) {
+            int k[4], lo[4] = {0, 0, 0, 0};
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int k = min(k0 + tid + u * nt, M - 1);
-                int lo = 0, hi = ncell - 1;
-                while (lo < hi) {
-                    const int mid = (lo + hi + 1) >> 1;
-                    if (S.cellstart[mid] <= k) lo = mid; else hi = mid - 1;
+            for (int u = 0; u < 4; u++) k[u] = min(k0 + tid + u * nt, M - 1);
+            for (int step = top; step > 0; step >>= 1) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int c = lo[u] + step;
+                    if (c < ncell && S.cellstart[c] <= k[u]) lo[u] = c;
                 }
-                kv[u] = cbase[S.cslot[lo] + (k - S.cellstart[lo])];
             }
+#pragma unroll
+            for (int u = 0; u < 4; u++) kv[u] = cbase[S.cslot[lo[u]] + (k[u] - S.cellstart[lo[u]])];
         };
-        auto root_of = [&](uint32_t key) {
-            const int r = (int)((float)cand_x(key) / hX);
-            return r < 0 ? 0 : (r >= nIni ? nIni - 1 : r);
-        };
+        auto root_of = [&](uint32_t key) { return root_of_x(cand_x(key)); };
         auto root_rect = [&](int r) { return mk_rect((int)(hX * (float)r), 0, (int)(hX * (float)(r + 1)), Hroot); };
         // node of the division: a rectangle (sweep) or (depth << 32 | path) (pyramid)
         auto kid = [&](uint64_t r, int q) -> uint64_t {
@@ -916,35 +855,49 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
         for (int u = 0; u < kOctKR; u++) { kreg[u] = 0u; nreg[u] = 0; }
         if constexpr (FAST) {
             // ---- 2. histogram of the depth-Dh cells, then the pyramid (two levels per barrier) ----
+            // key -> cell without a search: each cell writes its index over its key range into
+            // cellof (u16), which borrows the node-pass scratch (ccount .. skey2: untouched until
+            // the roots); a level with more keys than it holds searches instead
+            uint16_t* cellof = (uint16_t*)S.ccount;
+            const bool direct = M <= (int)(((unsigned char*)(S.skey2 + cfg.sort_cap) - (unsigned char*)S.ccount) / 2);
+            if (direct) {
+                for (int c = tid; c < ncell; c += nt)
+                    for (int j = S.cellstart[c]; j < S.cellstart[c + 1]; j++) cellof[j] = (uint16_t)c;
+                __syncthreads();
+            }
             const int ob = poff(Dh);
             for (int k0 = 0; k0 < M; k0 += 4 * nt) {
                 uint32_t kv[4];
-                gather4(k0, kv);
+                if (direct) {
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int k = min(k0 + tid + u * nt, M - 1);
+                        const int c = cellof[k];
+                        kv[u] = cbase[S.cslot[c] + (k - S.cellstart[c])];
+                    }
+                } else {
+                    gather4(k0, kv);
+                }
+                if (k0 == 0) { TR_PHASE(2, 55) }
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     const int k = k0 + tid + u * nt;
                     if (k < M) {
-                        const int x = cand_x(kv[u]), y = cand_y(kv[u]);
-                        const int r = root_of(kv[u]);
-                        // DivideNode's ceil((x1 - x0) / 2.f) == (x1 - x0 + 1) >> 1 on these widths
-                        int x0 = (int)(hX * (float)r), x1 = (int)(hX * (float)(r + 1)), y0 = 0, y1 = Hroot;
-                        uint32_t path = (uint32_t)r;
-#pragma unroll
-                        for (int d = 0; d < kOctMaxDh; d++) {
-                            if (d < Dh) {
-                                const int sx = x0 + ((x1 - x0 + 1) >> 1), sy = y0 + ((y1 - y0 + 1) >> 1);
-                                const bool bx = x >= sx, by = y >= sy;
-                                x0 = bx ? sx : x0; x1 = bx ? x1 : sx;
-                                y0 = by ? sy : y0; y1 = by ? y1 : sy;
-                                path = path * 4u + (bx ? 1u : 0u) + (by ? 2u : 0u);
-                            }
-                        }
+                        const uint32_t xb = xtab[cand_x(kv[u])], yb = ytab[cand_y(kv[u])];
+                        // Morton interleave: quadrant digit d = x bit d + 2 * y bit d
+                        auto spread = [](uint32_t v) {
+                            v = (v | (v << 4)) & 0x0F0Fu;
+                            v = (v | (v << 2)) & 0x3333u;
+                            return (v | (v << 1)) & 0x5555u;
+                        };
+                        const uint32_t path = ((xb >> 8) << (2 * Dh)) | spread(xb & 0xFFu) | (spread(yb) << 1);
                         atomicAdd(&pcnt[ob + (int)path], 1u);
                         atomicMax(&pbest[ob + (int)path], ((unsigned long long)cand_s(kv[u]) << 56) |
                                                               ((unsigned long long)(0xFFFFFFu - (uint32_t)k) << 32) | kv[u]);
                     }
                 }
             }
+            TR_PHASE(2, 56)
             __syncthreads();
             TR_PHASE(2, 53)
             // the two deepest levels below Dh by the block (a thread per depth-(Dh-2) cell), the
@@ -1725,19 +1678,6 @@ void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameB
                        xcd_run_for(B));
 }
 
-void launch_pyr_fast(const ExtractPlan* dP, const ExtractPlan& hP, int ntiles, size_t cone_lds, const FrameBufs& fb,
-                     int B, const ConeRect* rects, const int* ctab, int tab_stride, const CellGeom* cells,
-                     uint32_t* cand, int* cand_cnt, int* err, int* lvl_done, hipStream_t st) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_pyr_fast, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
-        attr = true;
-    }
-    const size_t lds = std::max(cone_lds, kFastLdsBytes);
-    hipLaunchKernelGGL(k_pyr_fast, dim3(ntiles + hP.n_cells_total, B), dim3(1024), lds, st, dP, fb, rects, ctab,
-                       tab_stride, ntiles, cells, cand, cand_cnt, err, lvl_done);
-}
-
 void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,
                  uint32_t* cand, int* cand_cnt, int* err, hipStream_t st) {
     // more threads per cell while the cells alone cannot fill the chip (one frame: ~600 cells on
@@ -1774,13 +1714,14 @@ size_t octree_lds_bytes(const ExtractPlan& hP, const OctreeCfg& cfg) {
     return off;
 }
 
-void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const uint32_t* cand,
+void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const uint16_t* otab,
+                   const uint32_t* cand,
                    const int* cand_cnt, uint32_t* kscratch, uint16_t* nscratch, LevelKp* lvl_kp, int* lvl_cnt,
-                   int* lvl_nlap, const OctreeCfg& cfg, int* err, int* lvl_done, int B, hipStream_t st) {
+                   int* lvl_nlap, const OctreeCfg& cfg, int* err, int B, hipStream_t st) {
     const size_t lds = octree_lds_bytes(hP, cfg);
     dim3 grd(B, hP.n_levels, 1);
-    hipLaunchKernelGGL(k_octree, grd, dim3(1024), lds, st, dP, cells, cand, cand_cnt, kscratch, nscratch, lvl_kp,
-                       lvl_cnt, lvl_nlap, cfg, err, lvl_done);
+    hipLaunchKernelGGL(k_octree, grd, dim3(1024), lds, st, dP, cells, otab, cand, cand_cnt, kscratch, nscratch, lvl_kp,
+                       lvl_cnt, lvl_nlap, cfg, err);
 }
 
 constexpr int kDescKpMaxSlots = 16384;

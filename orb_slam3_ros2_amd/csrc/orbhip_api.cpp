@@ -79,6 +79,8 @@ struct Plan {
     DevBuf<ExtractPlan> d_plan;
     DevBuf<CellGeom> d_cells;
     DevBuf<int> d_xofs, d_xalpha, d_yofs, d_ybeta, d_disc;
+    std::vector<uint16_t> otab;   // k_octree interval tables (LevelGeom::oct_tab_off)
+    DevBuf<uint16_t> d_otab;
 };
 
 }  // namespace
@@ -97,7 +99,6 @@ struct orbhip_ctx {
     DevBuf<uint32_t> d_cand, d_kscratch;
     DevBuf<uint16_t> d_nscratch;
     DevBuf<int> d_cand_cnt, d_lvl_cnt, d_lvl_nlap, d_err;
-    DevBuf<int> d_lvl_done;     // k_pyr_fast level counters (zeroed on allocation, reset by k_octree)
     DevBuf<uint64_t> d_mpart;   // matcher chunk partials (match_part_entries)
     DevBuf<int> d_msync;        // one-launch matcher counters (zeroed once, reset by every launch)
     DevBuf<double> d_bw;        // bag-of-words weights (host transform)
@@ -300,6 +301,29 @@ static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
         G.kp_base = kp_base;
         kp_base += G.kp_cap;
         if ((G.max_bx - G.min_bx) >= 4096 || (G.max_by - G.min_by) >= 4096) return ORBHIP_ERR_UNSUPPORTED;
+        // k_octree interval tables: the first 6 quadrant splits of DistributeOctTree's root
+        // rectangles (DivideNode: halfX = ceil((UR.x - UL.x) / 2.f)) are fixed by geometry, so a
+        // column's root and x-side choices (and a row's y-side choices) are tabulated once
+        {
+            auto bits6 = [](int v, int a0, int a1) {
+                int b = 0;
+                for (int d = 0; d < 6; d++) {
+                    const int sv = a0 + (int)std::ceil((float)(a1 - a0) / 2);
+                    const bool hi = v >= sv;
+                    (hi ? a0 : a1) = sv;
+                    b = 2 * b + (hi ? 1 : 0);
+                }
+                return b;
+            };
+            const int Wl = G.max_bx - G.min_bx, Hl = G.max_by - G.min_by;
+            G.oct_tab_off = (int)pl->otab.size();
+            for (int x = 0; x < Wl; x++) {
+                int r = (int)((float)x / G.hX);
+                r = r < 0 ? 0 : (r >= G.n_ini ? G.n_ini - 1 : r);
+                pl->otab.push_back((uint16_t)((r << 8) | bits6(x, (int)(G.hX * (float)r), (int)(G.hX * (float)(r + 1)))));
+            }
+            for (int y = 0; y < Hl; y++) pl->otab.push_back((uint16_t)bits6(y, 0, Hl));
+        }
     }
     P.n_cells_total = cell_base;
     P.n_slots_total = slot_base;
@@ -431,6 +455,8 @@ static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
     HIPOK(up(pl->d_yofs, pl->yofs));
     HIPOK(up(pl->d_ybeta, pl->ybeta));
     HIPOK(up(pl->d_disc, pl->disc));
+    HIPOK(pl->d_otab.ensure(pl->otab.size()));
+    HIPOK(hipMemcpy(pl->d_otab.p, pl->otab.data(), pl->otab.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     if (!pl->cone.empty()) {
         HIPOK(pl->d_cone.ensure(pl->cone.size()));
         HIPOK(hipMemcpy(pl->d_cone.p, pl->cone.data(), pl->cone.size() * sizeof(ConeRect), hipMemcpyHostToDevice));
@@ -462,12 +488,6 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
     (void)hipGetLastError();   // clear a sticky error of an earlier, already-reported call
     int rc = ensure_batch(c, pl, B);
     if (rc) return rc;
-    {
-        const int* before = c->d_lvl_done.p;
-        HIPOK(c->d_lvl_done.ensure((size_t)B * P.n_levels));
-        if (c->d_lvl_done.p != before)
-            HIPOK(hipMemsetAsync(c->d_lvl_done.p, 0, sizeof(int) * (size_t)B * P.n_levels, st));
-    }
     // octree division engine (read per call so that tests can switch it): ORBHIP_OCTREE_SWEEP=1 runs
     // the sweep path only, ORBHIP_OCTREE_DH=d caps the pyramid depth (a shallow cap forces the
     // pyramid path's fallback to the sweep path)
@@ -479,7 +499,7 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
     key.add(1).add((uint64_t)oct_fast).add((uint64_t)oct_max_dh).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
         .add((uint64_t)lap1).ptr(d_kps).ptr(d_desc).add((uint64_t)cap).ptr(d_n).ptr(d_mono).ptr(st).ptr(c->d_pyr.p)
         .ptr(c->d_cand.p).ptr(c->d_kscratch.p).ptr(c->d_nscratch.p).ptr(c->d_cand_cnt.p).ptr(c->d_lvl_kp.p)
-        .ptr(c->d_lvl_cnt.p).ptr(c->d_lvl_nlap.p).ptr(c->d_err.p).ptr(c->d_lvl_done.p);
+        .ptr(c->d_lvl_cnt.p).ptr(c->d_lvl_nlap.p).ptr(c->d_err.p);
     return c->graphs.run(key, st, c->timer.stage != 0, [&](hipStream_t st) -> int {
         FrameBufs fb;
         fb.in = d_imgs; fb.in_stride = stride; fb.in_fstride = fstride; fb.pyr = c->d_pyr.p;
@@ -491,35 +511,25 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
         static const size_t cone_max = std::getenv("ORBHIP_CONE_MAX_WG")
                                            ? (size_t)std::atol(std::getenv("ORBHIP_CONE_MAX_WG"))
                                            : (size_t)1024;
-        // the cone and FAST in one launch (k_pyr_fast) only with ORBHIP_PYR_FAST=1: measured slower
-        // than the two launches ("k_pyr_fast")
-        const char* pf = std::getenv("ORBHIP_PYR_FAST");
         const bool cone_path = pl->cone_tiles && !no_cone && (size_t)B * pl->cone_tiles <= cone_max;
-        if (cone_path && pf && pf[0] == '1') {
-            launch_pyr_fast(pl->d_plan.p, P, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_cone_tab.p,
-                            pl->cone_tab_stride, pl->d_cells.p, c->d_cand.p, c->d_cand_cnt.p, c->d_err.p,
-                            c->d_lvl_done.p, st);
-            tm.end(1, st);
-        } else {
-            if (cone_path)
-                launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_cone_tab.p,
-                                pl->cone_tab_stride, st);
-            else
-                for (int l = 1; l < P.n_levels; l++)
-                    launch_resize(pl->d_plan.p, P, fb, B, l, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p,
-                                  pl->d_ybeta.p, st);
-            tm.end(1, st);
-            tm.begin(2, st);
-            launch_fast(pl->d_plan.p, P, pl->d_cells.p, fb, B, c->d_cand.p, c->d_cand_cnt.p, c->d_err.p, st);
-            tm.end(2, st);
-        }
+        if (cone_path)
+            launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_cone_tab.p,
+                            pl->cone_tab_stride, st);
+        else
+            for (int l = 1; l < P.n_levels; l++)
+                launch_resize(pl->d_plan.p, P, fb, B, l, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p, pl->d_ybeta.p,
+                              st);
+        tm.end(1, st);
+        tm.begin(2, st);
+        launch_fast(pl->d_plan.p, P, pl->d_cells.p, fb, B, c->d_cand.p, c->d_cand_cnt.p, c->d_err.p, st);
+        tm.end(2, st);
         OctreeCfg oc = pl->oct;
         oc.lap0 = lap0; oc.lap1 = lap1;
         oc.fast = oct_fast;
         oc.max_dh = oct_max_dh;
         tm.begin(3, st);
-        launch_octree(pl->d_plan.p, P, pl->d_cells.p, c->d_cand.p, c->d_cand_cnt.p, c->d_kscratch.p, c->d_nscratch.p,
-                      c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, oc, c->d_err.p, c->d_lvl_done.p, B, st);
+        launch_octree(pl->d_plan.p, P, pl->d_cells.p, pl->d_otab.p, c->d_cand.p, c->d_cand_cnt.p, c->d_kscratch.p, c->d_nscratch.p,
+                      c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, oc, c->d_err.p, B, st);
         tm.end(3, st);
         tm.begin(4, st);
         launch_desc(pl->d_plan.p, P, fb, c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, pl->d_disc.p, d_kps, d_desc,

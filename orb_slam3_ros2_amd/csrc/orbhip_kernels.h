@@ -41,17 +41,14 @@ void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameB
                      const int* ctab, int tab_stride, hipStream_t st);
 void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, int B, int l,
                    const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st);
-// the cone and FAST in one launch; lvl_done: B * n_levels ints, zero (k_octree resets them)
-void launch_pyr_fast(const ExtractPlan* dP, const ExtractPlan& hP, int ntiles, size_t cone_lds, const FrameBufs& fb,
-                     int B, const ConeRect* rects, const int* ctab, int tab_stride, const CellGeom* cells,
-                     uint32_t* cand, int* cand_cnt, int* err, int* lvl_done, hipStream_t st);
 void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,
                  uint32_t* cand, int* cand_cnt, int* err, hipStream_t st);
 size_t octree_lds_bytes(const ExtractPlan& hP, const OctreeCfg& cfg);
 bool octree_set_lds_limit(size_t bytes);
-void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const uint32_t* cand,
+void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const uint16_t* otab,
+                   const uint32_t* cand,
                    const int* cand_cnt, uint32_t* kscratch, uint16_t* nscratch, LevelKp* lvl_kp, int* lvl_cnt,
-                   int* lvl_nlap, const OctreeCfg& cfg, int* err, int* lvl_done, int B, hipStream_t st);
+                   int* lvl_nlap, const OctreeCfg& cfg, int* err, int B, hipStream_t st);
 void launch_desc(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, const LevelKp* lvl_kp,
                  const int* lvl_cnt, const int* lvl_nlap, const int* disc, orbhip_kp* out_kps, uint8_t* out_desc,
                  int cap, int* n_out, int* mono_out, int B, hipStream_t st);

@@ -22,6 +22,8 @@ struct LevelGeom {
     int n_ini;                // DistributeOctTree root count
     float hX;                 // root width
     int kp_cap, kp_base;      // octree output capacity / offset (per frame)
+    int oct_tab_off;          // octree interval table of the level (u16): max_bx - min_bx column
+                              // entries (root << 8 | 6 x-split bits), then max_by - min_by row entries
     int patch_size;           // (int)(31 * scale)
     // resize tables (level l from l-1), offsets into xtab/ytab arrays
     int xtab_off, ytab_off, xmax, vend;

@@ -30,32 +30,15 @@ def _check(ext, oracle, img, nfeatures=1000, lap=(0, 1000), scale=1.2, nlevels=8
     return len(gk)
 
 
-@pytest.fixture(params=["split", "pyr_fast"])
-def pyr_path(request, monkeypatch):
-    """The pyramid cone and FAST as two launches (default), and as one (k_pyr_fast, a tile counter
-    between the work-groups; opt-in ORBHIP_PYR_FAST=1)."""
-    if request.param == "pyr_fast":
-        monkeypatch.setenv("ORBHIP_PYR_FAST", "1")
-    return request.param
-
-
 @pytest.mark.parametrize("seed", [0, 1, 2, 3])
-def test_c2_640x480_bit_exact(ext1000, oracle, pyr_path, seed):
+def test_c2_640x480_bit_exact(ext1000, oracle, seed):
     n = _check(ext1000, oracle, synthetic_frame(seed, 640, 480))
     assert n > 900
 
 
 @pytest.mark.parametrize("w,h,seed", [(1280, 720, 10), (752, 480, 11), (641, 479, 12), (320, 240, 13)])
-def test_sizes_bit_exact(ext1000, oracle, pyr_path, w, h, seed):
+def test_sizes_bit_exact(ext1000, oracle, w, h, seed):
     _check(ext1000, oracle, synthetic_frame(seed, w, h))
-
-
-def test_pyr_fast_repeated_frames(ext1000, oracle, monkeypatch):
-    """The fused launch over a run of different frames in one context (the tile counter is
-    reset by each frame's octree): every frame bit-exact."""
-    monkeypatch.setenv("ORBHIP_PYR_FAST", "1")
-    for seed in range(20, 32):
-        _check(ext1000, oracle, synthetic_frame(seed, 640, 480))
 
 
 def test_milkv_1250_features(oracle):
