@@ -746,6 +746,24 @@ __global__ __launch_bounds__(256) void k_ba_shard_reduce(const BaArgs* __restric
     }
 }
 
+// Envelope packing of S for the sharded all-reduce: 32-row tile R keeps columns [32 rf[R],
+// 32 R + 32) (the lower envelope, which is all any Cholesky here reads; outside it every shard's
+// S is zero), packed row-major per tile at toff[R]. pack (dir 0) S -> buf, unpack (dir 1) buf -> S.
+__global__ __launch_bounds__(256) void k_ba_env_pack(double* __restrict__ S, int n, const int* __restrict__ rf,
+                                                     const long long* __restrict__ toff, double* __restrict__ buf,
+                                                     int dir) {
+    const int R = blockIdx.y;
+    const int c0 = 32 * rf[R], c1 = min(32 * R + 32, n), w = c1 - c0;
+    const int rows = min(32, n - 32 * R);
+    double* tb = buf + toff[R];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < rows * w; i += gridDim.x * blockDim.x) {
+        const int r = i / w, c = i - r * w;
+        double* e = S + (size_t)(32 * R + r) * n + c0 + c;
+        if (dir == 0) tb[i] = *e;
+        else *e = tb[i];
+    }
+}
+
 __device__ void ba_reduce_body(const BaArgs& a, int what, double* sh) {
     double v = 0;
     if (what & 1) {
@@ -1103,6 +1121,8 @@ struct BaWorkspace {
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     DBuf<int> dstop;           // stop-flag consensus (all-reduce max)
+    DBuf<double> envbuf;       // S's union envelope, packed for the all-reduce (k_ba_env_pack)
+    DBuf<long long> envoff;    // its per-32-row-tile offsets
     int* h_stop = nullptr;     // pinned
 };
 
@@ -1286,10 +1306,27 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     BAOK(hipMemcpyAsync(D + sA, hd + sA, sizeof(double) * (nA + nU), hipMemcpyHostToDevice, st));
     BAOK(hipMemcpyAsync(I, hi, ni * sizeof(int), hipMemcpyHostToDevice, st));
     BAOK(hipMemcpyAsync(ws->args.p, ha, B * sizeof(BaArgs), hipMemcpyHostToDevice, st));
+    // RCCL shards solved by the blocked Cholesky (which reads only the lower triangle inside the
+    // envelope; the one-workgroup solvers also read the mirrored upper triangle) all-reduce S
+    // over its union envelope only: ~5 MB instead of n^2 doubles (46 MB) at C5
+    size_t env_total = 0;
     if (shard_mode == kShardRccl && !pp[0].row_first.empty()) {   // union envelope over the ranks
         int* rf = const_cast<int*>(ha[0].row_first);
         if (ncclAllReduce(rf, rf, pp[0].row_first.size(), ncclInt32, ncclMin, ws->comm, st) != ncclSuccess)
             return ORBHIP_ERR_DEVICE;
+        const int nt = (int)pp[0].row_first.size(), n = pp[0].n;
+        if (n > kCholSmallN && !std::getenv("ORBHIP_SHARD_FULL_S")) {
+        std::vector<int> urf(nt);
+        BAOK(hipMemcpyAsync(urf.data(), rf, nt * sizeof(int), hipMemcpyDeviceToHost, st));
+        BAOK(hipStreamSynchronize(st));
+        std::vector<long long> off(nt + 1, 0);
+        for (int R = 0; R < nt; R++)
+            off[R + 1] = off[R] + (long long)std::min(32, n - 32 * R) * (std::min(32 * R + 32, n) - 32 * urf[R]);
+        env_total = (size_t)off[nt];
+        BAOK(ws->envbuf.ensure(env_total));
+        BAOK(ws->envoff.ensure(nt + 1));
+        BAOK(hipMemcpyAsync(ws->envoff.p, off.data(), (nt + 1) * sizeof(long long), hipMemcpyHostToDevice, st));
+        }
     }
     const double t_pack = now();
     static bool lds_set = false;
@@ -1339,6 +1376,17 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                                dim3(256), 0, st, dA, B, field, off, count, op);
         } else if (shard_mode == kShardRccl) {
             const BaArgs& a0 = ha[0];
+            if (field == 1 && off == 0 && env_total) {   // S: its union envelope, packed
+                const int nt = (int)pp[0].row_first.size();
+                const dim3 g(8, (unsigned)nt);
+                hipLaunchKernelGGL(k_ba_env_pack, g, dim3(256), 0, st, a0.S, a0.n, a0.row_first, ws->envoff.p,
+                                   ws->envbuf.p, 0);
+                if (ncclAllReduce(ws->envbuf.p, ws->envbuf.p, env_total, ncclDouble, ncclSum, ws->comm, st) != ncclSuccess)
+                    return ORBHIP_ERR_DEVICE;
+                hipLaunchKernelGGL(k_ba_env_pack, g, dim3(256), 0, st, a0.S, a0.n, a0.row_first, ws->envoff.p,
+                                   ws->envbuf.p, 1);
+                return ORBHIP_OK;
+            }
             double* p = (field == 0 ? a0.Hpp : field == 1 ? a0.S : field == 2 ? a0.bs : a0.red) + off;
             if (ncclAllReduce(p, p, count, ncclDouble, op ? ncclMax : ncclSum, ws->comm, st) != ncclSuccess)
                 return ORBHIP_ERR_DEVICE;

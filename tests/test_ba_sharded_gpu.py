@@ -44,3 +44,15 @@ def test_rccl_single_rank_matches_unsharded():
     full = opt.solve(prob)
     opt.comm_init(1, 0, Optimizer.comm_unique_id())
     _close(full, opt.solve_sharded(prob))
+
+
+def test_rccl_envelope_allreduce_matches_unsharded():
+    """The blocked-solver sizes all-reduce S over its union envelope only (k_ba_env_pack: pack,
+    ncclAllReduce, unpack). One rank: the packed round trip must leave the solve identical to the
+    unsharded one (a loop of 100 KFs with a 20-KF window: n = 594 > the one-workgroup solvers)."""
+    from orb_slam3_ros2_amd import Optimizer
+    prob, _ = synthetic_ba_problem(n_kf=100, n_pts=3000, layout="loop", window=20, seed=34)
+    opt = Optimizer()
+    full = opt.solve(prob)
+    opt.comm_init(1, 0, Optimizer.comm_unique_id())
+    _close(full, opt.solve_sharded(prob))

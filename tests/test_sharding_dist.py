@@ -1,6 +1,7 @@
 """N > 1 path on the CPU (gloo, world size 2): landmark shards partition the problem, and the
 shards' partial reduced camera systems sum (all_reduce) to the full system — the identity the
-RCCL all-reduce of orbhip_ba_solve_sharded relies on."""
+RCCL all-reduce of orbhip_ba_solve_sharded relies on — also when only their
+union envelope is packed and summed (the blocked-solver sizes)."""
 import os
 
 import numpy as np
@@ -39,7 +40,36 @@ def _worker(rank, port, q):
         dist.all_reduce(bt)
         Sf, bf = reduced_system(prob)
         scale = np.abs(Sf).max()
-        q.put((rank, float(np.abs(St.numpy() - Sf).max() / scale), float(np.abs(bt.numpy() - bf).max() / np.abs(bf).max())))
+        # 3. the envelope-packed all-reduce of orbhip_ba_solve_sharded (k_ba_env_pack): per
+        # 32-row tile R the columns [32 rf[R], 32 R + 32) of each shard's S, rf the union (min
+        # over the shards) of their envelopes, summed packed and unpacked, equal the full
+        # system's lower triangle; outside the union envelope every entry is zero
+        n = S.shape[0]
+        nt = (n + 31) // 32
+        rf = np.arange(nt)
+        for r in range(n):
+            nz = np.nonzero(S[r, :r + 1])[0]
+            if nz.size:
+                rf[r // 32] = min(rf[r // 32], nz[0] // 32)
+        rft = torch.from_numpy(rf.astype(np.int64))
+        dist.all_reduce(rft, op=dist.ReduceOp.MIN)
+        rf = rft.numpy()
+        spans = [(32 * R, min(32 * R + 32, n), 32 * rf[R], min(32 * R + 32, n)) for R in range(nt)]
+        packed = torch.from_numpy(np.concatenate([S[r0:r1, c0:c1].ravel() for r0, r1, c0, c1 in spans]))
+        dist.all_reduce(packed)
+        Senv = np.zeros_like(S)
+        o = 0
+        for r0, r1, c0, c1 in spans:
+            k = (r1 - r0) * (c1 - c0)
+            Senv[r0:r1, c0:c1] = packed.numpy()[o:o + k].reshape(r1 - r0, c1 - c0)
+            o += k
+        rows, cols = np.indices(S.shape)
+        lower = cols <= rows
+        env = lower & (cols >= 32 * rf[rows // 32])
+        assert not np.any(Sf[lower & ~env]), "a non-zero of the summed S outside the union envelope"
+        d_env = float(np.abs(Senv - Sf)[env].max() / scale)
+        q.put((rank, max(float(np.abs(St.numpy() - Sf).max() / scale), d_env),
+               float(np.abs(bt.numpy() - bf).max() / np.abs(bf).max())))
     finally:
         dist.destroy_process_group()
 
