@@ -77,3 +77,25 @@ def test_c3_halo_slices_reproduce_batch(c3, N):
             assert nm2[j] == nm[p] and np.array_equal(mm2[:, j, :n[p]], mm[:, p, :n[p]]), (N, r, p)
         seen += list(range(plo, phi))
     assert sorted(seen) == list(range(B - 1))
+
+
+def test_c3_pipelined_batches_match_single(c3):
+    """bench.PipelinedC3 (two 64-frame batches in flight, each slot its own context and stream):
+    after several alternating batches, every slot holds exactly the one-batch results (the
+    oracle-checked ones above)."""
+    import torch
+    import bench
+    frames, (kps, desc, n, mono, mm, nm) = c3
+    pc = bench.PipelinedC3(0, 1, 2)
+    for _ in range(5):
+        pc.step()
+    torch.cuda.synchronize()
+    for sl in pc.slots:
+        assert np.array_equal(sl.n.cpu().numpy(), n) and np.array_equal(sl.mono.cpu().numpy(), mono)
+        for f in range(B):
+            assert np.array_equal(sl.kps[f, :n[f]].cpu().numpy(), kps[f, :n[f]])
+            assert np.array_equal(sl.desc[f, :n[f]].cpu().numpy(), desc[f, :n[f]])
+        assert np.array_equal(sl.nm.cpu().numpy(), nm)
+        for p in range(B - 1):
+            c = nm[p]
+            assert np.array_equal(sl.mm[0, p].cpu().numpy()[: n[p]], mm[0, p][: n[p]]), p
