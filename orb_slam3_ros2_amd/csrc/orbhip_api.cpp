@@ -93,7 +93,7 @@ struct orbhip_ctx {
     std::vector<float> scale, inv_scale;
     std::vector<int> feat, umax;
     int blurk[7] = {0};
-    std::map<std::pair<int, int>, std::unique_ptr<Plan>> plans;
+    std::map<std::pair<int, int>, std::shared_ptr<Plan>> plans;   // shared with other contexts (plan_cache)
     // per-batch scratch (grown on demand)
     DevBuf<uint8_t> d_in, d_pyr;
     DevBuf<uint32_t> d_cand, d_kscratch;
@@ -172,10 +172,50 @@ static void build_orb_tables(orbhip_ctx* c) {
 // ---------------------------------------------------------------------------
 // per-size plan
 // ---------------------------------------------------------------------------
+// A plan depends only on the device, the frame size, the ORBextractor parameters, the cone tile
+// and the test switches read while building it, never on a context's buffers: contexts with the
+// same key (e.g. the 16 camera streams of the C2 bench) share one, so its tables (the cone's
+// per-tile resize tables are ~0.5 MB at 640x480) stay L2-resident once instead of once per
+// context. The cache holds weak references: a plan dies with the last context using it.
+struct PlanKey {
+    int device, w, h, nfeat, nlev, ini, mn, cone_tile, clist_cap, fast_nt;
+    float scale;
+    bool operator<(const PlanKey& o) const {
+        return std::memcmp(this, &o, sizeof(PlanKey)) < 0;
+    }
+};
+static std::mutex g_plan_m;
+static std::map<PlanKey, std::weak_ptr<Plan>>& plan_cache() {
+    static auto* m = new std::map<PlanKey, std::weak_ptr<Plan>>();   // never destroyed (exit order)
+    return *m;
+}
+static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& out);
+
 static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
     auto key = std::make_pair(w, h);
     auto it = c->plans.find(key);
     if (it != c->plans.end()) { *out = it->second.get(); return ORBHIP_OK; }
+    PlanKey k;
+    std::memset(&k, 0, sizeof(k));
+    k.device = c->device; k.w = w; k.h = h; k.nfeat = c->prm.n_features; k.nlev = c->prm.n_levels;
+    k.ini = c->prm.ini_th_fast; k.mn = c->prm.min_th_fast; k.scale = c->prm.scale_factor;
+    k.cone_tile = c->cone_tile;
+    const char* cap_env = getenv("ORBHIP_FAST_CLIST_CAP");
+    k.clist_cap = cap_env ? atoi(cap_env) : -1;
+    const char* nt_env = getenv("ORBHIP_FAST_NT");
+    k.fast_nt = nt_env ? atoi(nt_env) : -1;
+    std::lock_guard<std::mutex> g(g_plan_m);
+    std::shared_ptr<Plan> sp = plan_cache()[k].lock();
+    if (!sp) {
+        if (int rc = build_plan_new(c, w, h, sp)) return rc;
+        plan_cache()[k] = sp;
+    }
+    *out = sp.get();
+    c->plans[key] = sp;
+    return ORBHIP_OK;
+}
+
+static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& out) {
     std::unique_ptr<Plan> pl(new Plan());
     ExtractPlan& P = pl->h;
     const int L = c->prm.n_levels;
@@ -462,8 +502,7 @@ static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
         HIPOK(hipMemcpy(pl->d_cone.p, pl->cone.data(), pl->cone.size() * sizeof(ConeRect), hipMemcpyHostToDevice));
         HIPOK(up(pl->d_cone_tab, pl->cone_tab));
     }
-    *out = pl.get();
-    c->plans[key] = std::move(pl);
+    out = std::shared_ptr<Plan>(pl.release());
     return ORBHIP_OK;
 }
 
