@@ -757,7 +757,7 @@ def ba_cholesky_roofline(n, blocked):
     L = lib()
     if blocked:
         rc = L.orbhip_test_cholesky_blocked(S.ctypes.data, b.ctypes.data, x.ctypes.data, n, ctypes.byref(ms))
-        kern = "k_cb_diag + k_cb_panel + k_cb_update + k_cb_solve (dense S)"
+        kern = "k_cb_diag + k_cb_update + k_cb_back (dense S)"
     else:
         rc = L.orbhip_test_cholesky_reg(S.ctypes.data, b.ctypes.data, x.ctypes.data, n, 20, ctypes.byref(ms), None)
         kern = "k_ba_chol_reg"

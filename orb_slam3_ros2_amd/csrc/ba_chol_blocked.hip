@@ -1,23 +1,27 @@
 // Multi-workgroup dense Cholesky + solve of the reduced camera system S xp = bs for large
 // problems (GlobalBundleAdjustment / BundleAdjustment, SURVEY.md §8 a20/a22: n = 6 * #optimised
-// KFs, up to 4096), right-looking with 32-column panels:
-//   k_cb_diag    one wavefront factors the 32x32 diagonal block in registers (chol_diag_wave):
-//                L11 into S, L11^{-1} into Lsave (the backward solve reuses it), and applies
-//                y_p = L11^{-1} x_p (the forward substitution rides on the factorization: x holds
-//                bs, and each panel subtracts L21 y_p from the rows below it)
-//   k_cb_panel   L21 = A21 L11^{-T} on v_mfma_f64_16x16x4f64, one wave per 16-row block, and
-//                x_r -= L21[r] y_p for its rows
-//   k_cb_update  C -= L21_I L21_J^T over 64x64 lower tiles of the trailing matrix (MFMA); the
-//                work-group of tile (0, 0) then factors the next diagonal block (no k_cb_diag
-//                launch after the first panel)
+// KFs, up to 4096), right-looking with 32-column panels, ONE launch per panel:
+//   k_cb_diag    one wavefront factors the first 32x32 diagonal block in registers
+//                (chol_diag_wave): L11 into S, L11^{-1} into Lsave (the backward solve reuses it),
+//                and applies y_p = L11^{-1} x_p (the forward substitution rides on the
+//                factorization: x holds bs)
+//   k_cb_update  per 64x64 lower tile (I, J) of the trailing matrix: the work-group computes the
+//                panel rows it needs, L21_I = A21_I L11^{-T} and L21_J (v_mfma_f64_16x16x4f64,
+//                from the raw panel column and Lsave), then C -= L21_I L21_J^T (MFMA). The
+//                work-group of each diagonal tile (I, I) also stores L21_I, transposed, into
+//                S's upper triangle (rows of the panel, columns below it: nothing reads that
+//                region during the factorization, while the panel column itself is still read
+//                by the other work-groups) and applies x_r -= L21[r] y_p to its rows. The
+//                work-group of tile (0, 0) then factors the next diagonal block.
 //   k_cb_back    backward substitution, one 1024-thread workgroup, x in LDS: per panel the 32x32
-//                factor tiles below it (its envelope), loaded one panel ahead into registers
+//                factor tiles below it (its envelope, read from the upper triangle), loaded one
+//                panel ahead into registers
 // Structure: row_first[R] = first 32-column tile with a structural non-zero in 32-row tile R of
 // S. The envelope (profile) of a symmetric matrix is preserved by its Cholesky factor, so every
-// tile left of row_first stays zero: the panel, update and solve kernels skip it. A banded or
+// tile left of row_first stays zero: the update and solve kernels skip it. A banded or
 // arrow-shaped S (a loop of keyframes with a co-visibility window) costs O(n b^2), not O(n^3).
-// Only the lower triangle of S is read; the update writes lower tiles (diagonal tiles in full,
-// their upper half is never read).
+// The lower triangle of S is the input; the factor ends as L11 blocks on the diagonal (lower)
+// and L21 panels transposed in the upper triangle.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -72,57 +76,39 @@ __global__ __launch_bounds__(256) void k_cb_init(const double* __restrict__ bs, 
     if (i == 0) flag[0] = 1;
 }
 
-__global__ __launch_bounds__(256) void k_cb_panel(double* __restrict__ S, int n, int k0,
-                                                  const double* __restrict__ Lsave, const int* __restrict__ row_first,
-                                                  double* __restrict__ x, const int* __restrict__ gate) {
-    CB_GATE
-    __shared__ double Li[32 * 33];
-    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-    const double* Lp = Lsave + (size_t)(k0 / kCT) * 1024;
-    for (int t = tid; t < 1024; t += 256) Li[(t >> 5) * 33 + (t & 31)] = Lp[t];
-    __syncthreads();
-    const int r0 = k0 + kCT + 16 * (blockIdx.x * 4 + wid);
-    if (r0 >= n || row_first[r0 / kCT] > k0 / kCT) return;   // wave-uniform
-    const int cc = lane & 15, rq = lane >> 4;
+// L21 rows [r0, r0 + 64) of the panel at k0 into LDS Lt (64 x 34): L21 = A21 Li^T, Li = L11^{-1}
+// (LDS, 32 x 33), A21 the panel column of S (final: every earlier panel's update is done). Wave w
+// computes rows 16w..16w+15 on MFMA (lane (cc, rq): A row cc, k = 4kk + rq; C rows rq + 4q).
+__device__ __forceinline__ void panel_rows(const double* __restrict__ S, int n, int k0, int r0,
+                                           const double* __restrict__ Li, double* __restrict__ Lt) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, cc = lane & 15, rq = lane >> 4;
+    const int rb = r0 + 16 * wid;
     double4_t acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
-    const bool rin = r0 + cc < n;
+    const bool rin = rb + cc < n;
+    double av[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; kk++) av[kk] = rin ? S[(size_t)(rb + cc) * n + k0 + 4 * kk + rq] : 0.0;
 #pragma unroll
     for (int kk = 0; kk < 8; kk++) {
-        const double av = rin ? S[(size_t)(r0 + cc) * n + k0 + 4 * kk + rq] : 0.0;
-        const double b0 = Li[cc * 33 + 4 * kk + rq];
-        const double b1 = Li[(16 + cc) * 33 + 4 * kk + rq];
-        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b0, acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, b1, acc1, 0, 0, 0);
+        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kk], Li[cc * 33 + 4 * kk + rq], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kk], Li[(16 + cc) * 33 + 4 * kk + rq], acc1, 0, 0, 0);
     }
-    // forward substitution: x_row -= L21[row] y_p (y_p = x[k0, k0 + 32), final since its diagonal
-    // block; every row belongs to one wave)
-    const double y0 = x[k0 + cc], y1 = x[k0 + 16 + cc];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        const int row = r0 + rq + 4 * q;
-        const double part = row16_sum(fma(acc0[q], y0, acc1[q] * y1));
-        if (row < n) {
-            S[(size_t)row * n + k0 + cc] = acc0[q];
-            S[(size_t)row * n + k0 + 16 + cc] = acc1[q];
-            if (cc == 0) x[row] -= part;
-        }
+        Lt[(16 * wid + rq + 4 * q) * 34 + cc] = acc0[q];
+        Lt[(16 * wid + rq + 4 * q) * 34 + 16 + cc] = acc1[q];
     }
 }
 
-// C -= L21_I L21_J^T on the 64x64 lower tile (ri, rj) of the trailing matrix
-__device__ __forceinline__ void update_tile(double* __restrict__ S, int n, int k0, int ri, int rj, bool diag,
-                                            double* __restrict__ Bt) {
-    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-    for (int t = tid; t < kUT * kCT; t += 256) {
-        const int r = t >> 5, c = t & 31;
-        Bt[r * 34 + c] = rj + r < n ? S[(size_t)(rj + r) * n + k0 + c] : 0.0;
-    }
+// C -= L21_I L21_J^T on the 64x64 lower tile (ri, rj) of the trailing matrix; LI / LJ: the panel
+// rows of both (LDS, 64 x 34); wave w owns rows 16w..16w+15 against all 64 columns
+__device__ __forceinline__ void update_tile(double* __restrict__ S, int n, int ri, int rj, bool diag,
+                                            const double* __restrict__ LI, const double* __restrict__ LJ) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int cc = lane & 15, rq = lane >> 4;
-    const int rowA = ri + 16 * wid + cc;
     double av[8];
 #pragma unroll
-    for (int kk = 0; kk < 8; kk++) av[kk] = rowA < n ? -S[(size_t)rowA * n + k0 + 4 * kk + rq] : 0.0;
-    __syncthreads();
+    for (int kk = 0; kk < 8; kk++) av[kk] = -LI[(16 * wid + cc) * 34 + 4 * kk + rq];
     double4_t acc[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
@@ -137,7 +123,7 @@ __device__ __forceinline__ void update_tile(double* __restrict__ S, int n, int k
         if (diag && u > wid) continue;   // strictly-upper 16x16 blocks of a diagonal tile
 #pragma unroll
         for (int kk = 0; kk < 8; kk++) {
-            const double bv = Bt[(16 * u + cc) * 34 + 4 * kk + rq];
+            const double bv = LJ[(16 * u + cc) * 34 + 4 * kk + rq];
             acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kk], bv, acc[u], 0, 0, 0);
         }
     }
@@ -152,16 +138,17 @@ __device__ __forceinline__ void update_tile(double* __restrict__ S, int n, int k
     }
 }
 
-// lower 64x64 tile (I, J), I >= J, of the trailing matrix starting at t0; wave w owns rows
-// 16w..16w+15 of the tile against all 64 columns (4 MFMA accumulators, K = 32)
+// lower 64x64 tile (I, J), I >= J, of the trailing matrix starting at t0
 __global__ __launch_bounds__(256) void k_cb_update(double* __restrict__ S, int n, int k0,
                                                    const int* __restrict__ row_first, double* __restrict__ Lsave,
                                                    double* __restrict__ x, int* __restrict__ flag,
                                                    const int* __restrict__ gate, const int* __restrict__ tiles) {
     CB_GATE
-    __shared__ double Bt[kUT * 34];   // the J rows of the panel; then the next diagonal block's scratch
+    __shared__ double Li[32 * 33];          // L11^{-1} of the panel
+    __shared__ double LI[kUT * 34], LJ[kUT * 34];   // panel rows of tiles I and J; LI then the next
+                                                    // diagonal block's scratch
     const int t0 = k0 + kCT;
-    const int tt = blockIdx.x;
+    const int tt = blockIdx.x, tid = threadIdx.x;
     int I, J;
     if (tiles) {   // this panel's envelope tiles (host-built, tile (0, 0) first): I << 16 | J
         I = tiles[tt] >> 16;
@@ -177,25 +164,46 @@ __global__ __launch_bounds__(256) void k_cb_update(double* __restrict__ S, int n
     // structure: the 64-row tile is non-zero in this panel if either 32-row half is
     const int fi = min(row_first[ri / kCT], ri + kCT < n ? row_first[ri / kCT + 1] : 1 << 30);
     const int fj = min(row_first[rj / kCT], rj + kCT < n ? row_first[rj / kCT + 1] : 1 << 30);
-    const int wid = threadIdx.x >> 6;
+    const int wid = tid >> 6;
     if (fi <= kt && fj <= kt) {   // workgroup-uniform: the tile is inside the envelope
-        update_tile(S, n, k0, ri, rj, I == J, Bt);
+        const double* Lp = Lsave + (size_t)kt * 1024;
+        for (int t = tid; t < 1024; t += 256) Li[(t >> 5) * 33 + (t & 31)] = Lp[t];
+        __syncthreads();
+        panel_rows(S, n, k0, ri, Li, LI);
+        if (I != J) panel_rows(S, n, k0, rj, Li, LJ);
+        __syncthreads();
+        update_tile(S, n, ri, rj, I == J, LI, I == J ? LI : LJ);
+        if (I == J) {
+            // the factor's panel rows, transposed into the upper triangle (rows k0.., columns ri..)
+            for (int i = tid; i < kUT * kCT; i += 256) {
+                const int r = i & 63, c = i >> 6;
+                if (ri + r < n) S[(size_t)(k0 + c) * n + ri + r] = LI[r * 34 + c];
+            }
+            // forward substitution: x_r -= L21[r] y_p (y_p = x[k0, k0 + 32), final)
+            if (tid < kUT && ri + tid < n) {
+                double s = 0.0;
+#pragma unroll 8
+                for (int c = 0; c < kCT; c++) s = fma(LI[tid * 34 + c], x[k0 + c], s);
+                x[ri + tid] -= s;
+            }
+        }
     }
     // tile (0, 0) holds the next diagonal block, now final: factor it here (its own stores, so a
     // workgroup barrier is the only ordering needed)
     if (tt == 0 && t0 < n) {
         __syncthreads();
-        if (wid == 0) cb_diag_forward(S, n, t0, Bt, Bt + 32 * 33, Lsave, x, flag);
+        if (wid == 0) cb_diag_forward(S, n, t0, LI, LI + 32 * 33, Lsave, x, flag);
     }
 }
 
-// Backward substitution L^T x = y (y: the forward result in x; the factor in the lower triangle of
-// S, the panel inverses in Lsave); flag[0] == 0 (a non-positive pivot) -> x = 0. One 1024-thread
-// workgroup, x in LDS (n <= kCbMaxN). Panel p: s = sum over the factor tiles R > p of its envelope
-// (row_first[R] <= p) of L_Rp^T x_R, then x_p = L11^{-T} (y_p - s). Thread t owns element
-// (t >> 5, t & 31) of every 32x32 tile; the next panel's tiles (up to kBackPre) and its L11^{-1}
-// are loaded into registers before this panel's reductions, so the panel chain waits on LDS and
-// barriers, not on HBM.
+// Backward substitution L^T x = y (y: the forward result in x; the factor's panels transposed in
+// the upper triangle of S, the panel inverses in Lsave); flag[0] == 0 (a non-positive pivot) ->
+// x = 0. One 1024-thread workgroup, x in LDS (n <= kCbMaxN). Panel p: s = sum over the factor
+// tiles R > p of its envelope (row_first[R] <= p) of L_Rp^T x_R, then x_p = L11^{-T} (y_p - s).
+// Thread t owns element (row t & 31, column t >> 5) of every 32x32 tile, read from the transposed
+// panel (S[column][row]: consecutive threads, consecutive addresses); the next panel's tiles (up
+// to kBackPre) and its L11^{-1} are loaded into registers before this panel's reductions, so the
+// panel chain waits on LDS and barriers, not on HBM.
 constexpr int kBackPre = 12;
 __global__ __launch_bounds__(1024) void k_cb_back(const double* __restrict__ S, int n,
                                                   const double* __restrict__ Lsave, double* __restrict__ x,
@@ -222,7 +230,7 @@ __global__ __launch_bounds__(1024) void k_cb_back(const double* __restrict__ S, 
         cnt[tid] = m;
     }
     __syncthreads();
-    const int ti = tid >> 5, tc = tid & 31;
+    const int ti = tid & 31, tc = tid >> 5;   // row and column inside a 32x32 tile
     double cur[kBackPre], nxt[kBackPre];
     double lcur, lnxt = 0.0;
     auto load = [&](int p, double (&buf)[kBackPre], double& l) {
@@ -232,7 +240,7 @@ __global__ __launch_bounds__(1024) void k_cb_back(const double* __restrict__ S, 
             double v = 0.0;
             if (j < m) {
                 const int r = kCT * lst[128 * p + j] + ti;
-                if (r < n && col < n) v = S[(size_t)r * n + col];
+                if (r < n && col < n) v = S[(size_t)col * n + r];   // L[r][col], transposed
             }
             buf[j] = v;
         }
@@ -248,19 +256,16 @@ __global__ __launch_bounds__(1024) void k_cb_back(const double* __restrict__ S, 
             if (j < m) s = fma(cur[j], y[kCT * lst[128 * p + j] + ti], s);   // x of tiles R > p: final
         for (int j = kBackPre; j < m; j++) {                                 // wide envelopes only
             const int r = kCT * lst[128 * p + j] + ti;
-            if (r < n && k0 + tc < n) s = fma(S[(size_t)r * n + k0 + tc], y[r], s);
+            if (r < n && k0 + tc < n) s = fma(S[(size_t)(k0 + tc) * n + r], y[r], s);
         }
-        Lt[ti * 33 + tc] = lcur;   // L11^{-1}[ti][tc]
-        s += __shfl_xor(s, 32);    // rows 2w and 2w + 1 of the wave
-        if (lane < 32) red[wid * 32 + lane] = s;
+        Lt[(tid >> 5) * 33 + (tid & 31)] = lcur;   // L11^{-1} (Lsave is row-major 32 x 32)
+        // column tc's sum over the 32 rows: the 32 lanes of this half-wave
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o);
+        if ((lane & 31) == 0) red[tc] = s;
         __syncthreads();
         if (wid == 0) {
-            if (lane < kCT) {
-                double t = 0.0;
-#pragma unroll
-                for (int g = 0; g < 16; g++) t += red[g * 32 + lane];
-                w[lane] = k0 + lane < n ? y[k0 + lane] - t : 0.0;
-            }
+            if (lane < kCT) w[lane] = k0 + lane < n ? y[k0 + lane] - red[lane] : 0.0;
             wave_lds_sync();
             if (lane < kCT && k0 + lane < n) {
                 double xj = 0.0;
@@ -285,8 +290,6 @@ void chol_blocked_solve(double* S, int n, double* Lsave, const double* bs, doubl
     for (int p = 0; p < np_; p++) {
         const int k0 = p * kCT, rest = n - (k0 + kCT);
         if (rest <= 0) break;
-        hipLaunchKernelGGL(k_cb_panel, dim3((unsigned)((rest + 63) / 64)), dim3(256), 0, st, S, n, k0, Lsave,
-                           row_first, x, gate);
         const int T = (rest + kUT - 1) / kUT;
         // + the diagonal block of panel p + 1 (tile (0, 0)'s work-group)
         if (tiles && tile_off)
