@@ -205,6 +205,13 @@ __global__ __launch_bounds__(256) void k_cb_update(double* __restrict__ S, int n
 // to kBackPre) and its L11^{-1} are loaded into registers before this panel's reductions, so the
 // panel chain waits on LDS and barriers, not on HBM.
 constexpr int kBackPre = 12;
+// workgroup barrier ordering LDS only: __syncthreads() is a workgroup fence, which on gfx950 also
+// drains vmcnt, i.e. would wait for the next panel's prefetch loads at every panel
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
 __global__ __launch_bounds__(1024) void k_cb_back(const double* __restrict__ S, int n,
                                                   const double* __restrict__ Lsave, double* __restrict__ x,
                                                   const int* __restrict__ flag, const int* __restrict__ row_first,
@@ -231,8 +238,6 @@ __global__ __launch_bounds__(1024) void k_cb_back(const double* __restrict__ S, 
     }
     __syncthreads();
     const int ti = tid & 31, tc = tid >> 5;   // row and column inside a 32x32 tile
-    double cur[kBackPre], nxt[kBackPre];
-    double lcur, lnxt = 0.0;
     auto load = [&](int p, double (&buf)[kBackPre], double& l) {
         const int m = cnt[p], col = kCT * p + tc;
 #pragma unroll
@@ -246,10 +251,11 @@ __global__ __launch_bounds__(1024) void k_cb_back(const double* __restrict__ S, 
         }
         l = Lsave[(size_t)p * 1024 + tid];
     };
-    load(np_ - 1, cur, lcur);
-    for (int p = np_ - 1; p >= 0; p--) {
+    // panel p with its tiles in `cur` while panel p - 1's load into `nxt` is in flight; the two
+    // register sets swap roles by unrolling (a copy would wait for the loads)
+    auto panel = [&](int p, const double (&cur)[kBackPre], double lcur, double (&nxt)[kBackPre], double& lnxt) {
         const int k0 = p * kCT, m = cnt[p];
-        if (p > 0) load(p - 1, nxt, lnxt);
+        Lt[(tid >> 5) * 33 + (tid & 31)] = lcur;   // L11^{-1} (Lsave is row-major 32 x 32)
         double s = 0.0;
 #pragma unroll
         for (int j = 0; j < kBackPre; j++)
@@ -258,12 +264,14 @@ __global__ __launch_bounds__(1024) void k_cb_back(const double* __restrict__ S, 
             const int r = kCT * lst[128 * p + j] + ti;
             if (r < n && k0 + tc < n) s = fma(S[(size_t)(k0 + tc) * n + r], y[r], s);
         }
-        Lt[(tid >> 5) * 33 + (tid & 31)] = lcur;   // L11^{-1} (Lsave is row-major 32 x 32)
+        // the next panel's loads go out once this panel's tiles are consumed: they stay in
+        // flight through the reductions and barriers below (which order LDS only)
+        if (p > 0) load(p - 1, nxt, lnxt);
         // column tc's sum over the 32 rows: the 32 lanes of this half-wave
 #pragma unroll
         for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o);
         if ((lane & 31) == 0) red[tc] = s;
-        __syncthreads();
+        lds_barrier();
         if (wid == 0) {
             if (lane < kCT) w[lane] = k0 + lane < n ? y[k0 + lane] - red[lane] : 0.0;
             wave_lds_sync();
@@ -273,10 +281,13 @@ __global__ __launch_bounds__(1024) void k_cb_back(const double* __restrict__ S, 
                 y[k0 + lane] = xj;
             }
         }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < kBackPre; j++) cur[j] = nxt[j];
-        lcur = lnxt;
+        lds_barrier();
+    };
+    double bufA[kBackPre], bufB[kBackPre], lA = 0.0, lB = 0.0;
+    load(np_ - 1, bufA, lA);
+    for (int p = np_ - 1; p >= 0; p -= 2) {
+        panel(p, bufA, lA, bufB, lB);
+        if (p >= 1) panel(p - 1, bufB, lB, bufA, lA);
     }
     for (int i = tid; i < n; i += 1024) x[i] = y[i];
 }
