@@ -79,15 +79,18 @@ __global__ __launch_bounds__(256) void k_cb_init(const double* __restrict__ bs, 
 // L21 rows [r0, r0 + 64) of the panel at k0 into LDS Lt (64 x 34): L21 = A21 Li^T, Li = L11^{-1}
 // (LDS, 32 x 33), A21 the panel column of S (final: every earlier panel's update is done). Wave w
 // computes rows 16w..16w+15 on MFMA (lane (cc, rq): A row cc, k = 4kk + rq; C rows rq + 4q).
-__device__ __forceinline__ void panel_rows(const double* __restrict__ S, int n, int k0, int r0,
-                                           const double* __restrict__ Li, double* __restrict__ Lt) {
+// Split in a load (av: issued with the tile's other loads) and the MFMA part.
+__device__ __forceinline__ void panel_rows_load(const double* __restrict__ S, int n, int k0, int r0, double* av) {
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, cc = lane & 15, rq = lane >> 4;
     const int rb = r0 + 16 * wid;
-    double4_t acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
     const bool rin = rb + cc < n;
-    double av[8];
 #pragma unroll
     for (int kk = 0; kk < 8; kk++) av[kk] = rin ? S[(size_t)(rb + cc) * n + k0 + 4 * kk + rq] : 0.0;
+}
+__device__ __forceinline__ void panel_rows_mfma(const double* av, const double* __restrict__ Li,
+                                                double* __restrict__ Lt) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, cc = lane & 15, rq = lane >> 4;
+    double4_t acc0 = {0, 0, 0, 0}, acc1 = {0, 0, 0, 0};
 #pragma unroll
     for (int kk = 0; kk < 8; kk++) {
         acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av[kk], Li[cc * 33 + 4 * kk + rq], acc0, 0, 0, 0);
@@ -100,16 +103,11 @@ __device__ __forceinline__ void panel_rows(const double* __restrict__ S, int n, 
     }
 }
 
-// C -= L21_I L21_J^T on the 64x64 lower tile (ri, rj) of the trailing matrix; LI / LJ: the panel
-// rows of both (LDS, 64 x 34); wave w owns rows 16w..16w+15 against all 64 columns
-__device__ __forceinline__ void update_tile(double* __restrict__ S, int n, int ri, int rj, bool diag,
-                                            const double* __restrict__ LI, const double* __restrict__ LJ) {
+// the 64x64 lower tile (ri, rj) of the trailing matrix: wave w holds rows 16w..16w+15 against all
+// 64 columns (4 MFMA accumulators in C layout)
+__device__ __forceinline__ void tile_load(const double* __restrict__ S, int n, int ri, int rj, double4_t* acc) {
     const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int cc = lane & 15, rq = lane >> 4;
-    double av[8];
-#pragma unroll
-    for (int kk = 0; kk < 8; kk++) av[kk] = -LI[(16 * wid + cc) * 34 + 4 * kk + rq];
-    double4_t acc[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
 #pragma unroll
@@ -118,6 +116,16 @@ __device__ __forceinline__ void update_tile(double* __restrict__ S, int n, int r
             acc[u][q] = (row < n && col < n) ? S[(size_t)row * n + col] : 0.0;
         }
     }
+}
+
+// C -= L21_I L21_J^T on the loaded tile; LI / LJ: the panel rows of both (LDS, 64 x 34)
+__device__ __forceinline__ void update_tile(double* __restrict__ S, int n, int ri, int rj, bool diag, double4_t* acc,
+                                            const double* __restrict__ LI, const double* __restrict__ LJ) {
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int cc = lane & 15, rq = lane >> 4;
+    double av[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; kk++) av[kk] = -LI[(16 * wid + cc) * 34 + 4 * kk + rq];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
         if (diag && u > wid) continue;   // strictly-upper 16x16 blocks of a diagonal tile
@@ -166,13 +174,26 @@ __global__ __launch_bounds__(256) void k_cb_update(double* __restrict__ S, int n
     const int fj = min(row_first[rj / kCT], rj + kCT < n ? row_first[rj / kCT + 1] : 1 << 30);
     const int wid = tid >> 6;
     if (fi <= kt && fj <= kt) {   // workgroup-uniform: the tile is inside the envelope
+        // every global load of the tile in one round trip: L11^{-1}, both panel row blocks, C
         const double* Lp = Lsave + (size_t)kt * 1024;
-        for (int t = tid; t < 1024; t += 256) Li[(t >> 5) * 33 + (t & 31)] = Lp[t];
+        double lv[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) lv[u] = Lp[tid + 256 * u];
+        double avI[8], avJ[8];
+        panel_rows_load(S, n, k0, ri, avI);
+        if (I != J) panel_rows_load(S, n, k0, rj, avJ);
+        double4_t acc[4];
+        tile_load(S, n, ri, rj, acc);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int t = tid + 256 * u;
+            Li[(t >> 5) * 33 + (t & 31)] = lv[u];
+        }
         __syncthreads();
-        panel_rows(S, n, k0, ri, Li, LI);
-        if (I != J) panel_rows(S, n, k0, rj, Li, LJ);
+        panel_rows_mfma(avI, Li, LI);
+        if (I != J) panel_rows_mfma(avJ, Li, LJ);
         __syncthreads();
-        update_tile(S, n, ri, rj, I == J, LI, I == J ? LI : LJ);
+        update_tile(S, n, ri, rj, I == J, acc, LI, I == J ? LI : LJ);
         if (I == J) {
             // the factor's panel rows, transposed into the upper triangle (rows k0.., columns ri..)
             for (int i = tid; i < kUT * kCT; i += 256) {
