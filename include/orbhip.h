@@ -168,7 +168,9 @@ int orbhip_match_frames_device(orbhip_ctx* ctx, const orbhip_kp* d_q_kps, const 
  *         d_img unchanged until the frame completes.
  *   view: device pointers of a slot's outputs (valid until the slot is reused, `slots`
  *         pushes later); frame = number of the frame held (-1 none).
- *   wait: the frame in `slot` complete: host-blocking (stream NULL) or stream-ordered.
+ *   wait: the frame in `slot` complete: host-blocking (stream NULL) or stream-ordered. With
+ *         one frame in flight the stream is one in-order HIP stream and push records no event:
+ *         the first wait that needs one records it then (covering every frame pushed so far).
  *   context: context j (0 <= j < frames_in_flight), e.g. for orbhip_profile_stage. */
 typedef struct orbhip_frontend orbhip_frontend;
 typedef struct {

@@ -1389,6 +1389,10 @@ struct orbhip_frontend {
     int32_t *n = nullptr, *mono = nullptr, *mm = nullptr, *nm = nullptr;
     std::vector<hipEvent_t> ev_x, ev_m;   // slot's extraction done / the match that read the slot as prev done
     std::vector<int64_t> frame_of;        // frame number held by each slot (-1 none)
+    // one frame in flight (S = 1): completion is recorded on demand by wait (ev_done covers the
+    // frames up to done_upto), not per push (an event per frame costs ~3% of the 16-camera rate)
+    hipEvent_t ev_done = nullptr;
+    int64_t done_upto = -1;
 };
 
 static void frontend_free(orbhip_frontend* f) {
@@ -1399,6 +1403,7 @@ static void frontend_free(orbhip_frontend* f) {
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : f->ev_m)
         if (e) (void)hipEventDestroy(e);
+    if (f->ev_done) (void)hipEventDestroy(f->ev_done);
     if (f->kps) (void)hipFree(f->kps);
     if (f->desc) (void)hipFree(f->desc);
     if (f->n) (void)hipFree(f->n);
@@ -1445,6 +1450,7 @@ int orbhip_frontend_create(orbhip_frontend** out, int device, const orbhip_orb_p
         HIPOK(hipEventCreateWithFlags(&f->ev_x[i], hipEventDisableTiming));
         HIPOK(hipEventCreateWithFlags(&f->ev_m[i], hipEventDisableTiming));
     }
+    HIPOK(hipEventCreateWithFlags(&f->ev_done, hipEventDisableTiming));
     *out = f.release();
     return ORBHIP_OK;
 }
@@ -1483,7 +1489,8 @@ int orbhip_frontend_push(orbhip_frontend* f, const uint8_t* d_img, int stride, i
                                                 f->check_orientation, m, m + cap, m + 2 * cap, f->nm + cur, st))
             return rc;
     }
-    HIPOK(hipEventRecord(f->ev_m[prev], st));   // the match read `prev`; and frame k is complete
+    // the match read `prev`, and frame k is complete (S = 1: recorded on demand by wait)
+    if (S > 1) HIPOK(hipEventRecord(f->ev_m[prev], st));
     f->frame_of[cur] = k;
     f->k = k + 1;
     return cur;
@@ -1509,8 +1516,17 @@ int orbhip_frontend_view(orbhip_frontend* f, int slot, orbhip_frontend_slot* v) 
 int orbhip_frontend_wait(orbhip_frontend* f, int slot, void* stream) {
     if (!f || slot < 0 || slot >= f->ns || f->frame_of[slot] < 0) return ORBHIP_ERR_ARG;
     HIPOK(hipSetDevice(f->device));
-    // frame k completes with the event its push recorded on ev_m[(k - 1) mod ns]
+    // frame k completes with the event its push recorded on ev_m[(k - 1) mod ns]; with S = 1
+    // every frame runs on context 0's stream in order: record ev_done there if no record covers
+    // this frame yet
     hipEvent_t e = f->ev_m[(slot + f->ns - 1) % f->ns];
+    if (f->S == 1) {
+        if (f->done_upto < f->frame_of[slot]) {
+            HIPOK(hipEventRecord(f->ev_done, f->ctx[0]->stream));
+            f->done_upto = f->k - 1;
+        }
+        e = f->ev_done;
+    }
     if (stream) HIPOK(hipStreamWaitEvent((hipStream_t)stream, e, 0));
     else HIPOK(hipEventSynchronize(e));
     return ORBHIP_OK;
