@@ -9,7 +9,8 @@ namespace orbhip {
 
 constexpr int kCbMaxN = 4096;   // largest n (6 x optimised keyframes) of the blocked solver
 
-// S (n x n, row-major, lower triangle read, factor written in place), Lsave (1024 x ceil(n/32)
+// S (n x n, row-major, lower triangle read; the factor is written in place: its 32x32 diagonal
+// blocks in the lower triangle, its panels below them transposed into the upper triangle), Lsave (1024 x ceil(n/32)
 // doubles), row_first (ceil(n/32) ints: first 32-column tile with a structural non-zero in each
 // 32-row tile). flag[0] = 1 on success, 0 on a non-positive pivot (x = 0). Asynchronous on st.
 // gate (device int, optional): every kernel returns unless *gate == kPhTrial (ba_args.h).

@@ -239,7 +239,7 @@ __global__ __launch_bounds__(1024) void k_cb_back(const double* __restrict__ S, 
                                                   const int* __restrict__ gate) {
     CB_GATE
     __shared__ double y[kCbMaxN];
-    __shared__ double red[16 * 32];
+    __shared__ double red[32];
     __shared__ double Lt[32 * 33];
     __shared__ double w[32];
     __shared__ unsigned char lst[128 * 128];   // factor tiles below panel p: lst[128 p + j]
