@@ -268,21 +268,20 @@ constexpr int kWinMax = 80;
 constexpr int kWinP = kWinMax;   // LDS row pitch of the FAST window and strength maps
 static_assert(kWinP % 4 == 0, "dword window rows");
 
-// m = max(A, B, 0) from the 16 differences d[k] = v - circle[k]
+// m = max(A, B, 0) from the 16 differences d[k] = v - circle[k]. The 9-arcs are folded from
+// 4-arcs (pairs of neighbouring pair-minima, built one arc start at a time) instead of holding
+// all 16 pair minima and maxima live: 32 fewer VGPRs, so k_fast_cells keeps 8 waves per SIMD.
 __device__ __forceinline__ int fast_strength_d(const int* d) {
-    int mn2[16], mx2[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        mn2[k] = min(d[k], d[(k + 1) & 15]);
-        mx2[k] = max(d[k], d[(k + 1) & 15]);
-    }
     int A = -256, Bm = 256;
 #pragma unroll
     for (int k = 0; k < 16; k++) {
-        int mn8 = min(min(mn2[k], mn2[(k + 2) & 15]), min(mn2[(k + 4) & 15], mn2[(k + 6) & 15]));
-        int mx8 = max(max(mx2[k], mx2[(k + 2) & 15]), max(mx2[(k + 4) & 15], mx2[(k + 6) & 15]));
-        A = max(A, min(mn8, d[(k + 8) & 15]));
-        Bm = min(Bm, max(mx8, d[(k + 8) & 15]));
+        // arc k .. k+8: min / max over 9 consecutive d
+        const int m4a = min(min(d[k], d[(k + 1) & 15]), min(d[(k + 2) & 15], d[(k + 3) & 15]));
+        const int m4b = min(min(d[(k + 4) & 15], d[(k + 5) & 15]), min(d[(k + 6) & 15], d[(k + 7) & 15]));
+        const int x4a = max(max(d[k], d[(k + 1) & 15]), max(d[(k + 2) & 15], d[(k + 3) & 15]));
+        const int x4b = max(max(d[(k + 4) & 15], d[(k + 5) & 15]), max(d[(k + 6) & 15], d[(k + 7) & 15]));
+        A = max(A, min(min(m4a, m4b), d[(k + 8) & 15]));
+        Bm = min(Bm, max(max(x4a, x4b), d[(k + 8) & 15]));
     }
     int m = max(A, -Bm);
     return m < 0 ? 0 : m;
