@@ -41,93 +41,142 @@ __device__ __forceinline__ ImgRef level_img(const ExtractPlan* __restrict__ P, c
 }
 
 // ---------------------------------------------------------------------------
-// k_resize: OCV resizeGeneric_ 8UC1 INTER_LINEAR; block (64,4), 4 output px per thread
+// k_resize: OCV resizeGeneric_ 8UC1 INTER_LINEAR; block (64,4), 4 output px x kRzRows output rows
+// per thread. Latency-bound at one round trip per dependent load, so each thread keeps
+// kRzRows x 4 output bytes in flight: after the column and row tables, every source row its
+// output rows read (a 1.2x downscale: kRzRows + 2 rows) is loaded at once as 3 aligned dwords.
 // ---------------------------------------------------------------------------
+constexpr int kRzRows = 4;
+constexpr int kRzSrc = kRzRows + 2;   // source rows held (more: the per-row path)
+
+// one output pixel from its two source rows' byte pairs (p0x: row sy, p1x: row sy + 1)
+__device__ __forceinline__ int rz_px(int p00, int p01, int p10, int p11, int aa, int b0, int b1,
+                                     bool inx, bool vecy) {
+    int h0, h1;
+    if (inx) {
+        const int a0 = (int)(short)(aa & 0xFFFF), a1 = (int)(short)(aa >> 16);
+        h0 = p00 * a0 + p01 * a1;
+        h1 = p10 * a0 + p11 * a1;
+    } else {
+        h0 = p00 * 2048;
+        h1 = p10 * 2048;
+    }
+    int v;
+    if (vecy) {   // VResizeLinearVec_32s8u lanes (128-bit baseline)
+        const int s0 = min(max(h0 >> 4, -32768), 32767);
+        const int s1 = min(max(h1 >> 4, -32768), 32767);
+        int t = ((s0 * b0) >> 16) + ((s1 * b1) >> 16);
+        t = min(max(t, -32768), 32767);
+        v = (t + 2) >> 2;
+    } else {      // FixedPtCast<int, uchar, 22>
+        v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
+    }
+    return v < 0 ? 0 : (v > 255 ? 255 : v);
+}
+
 __global__ __launch_bounds__(256) void k_resize(const ExtractPlan* __restrict__ P, FrameBufs fb, int l,
                                                 const int* __restrict__ xofs, const int* __restrict__ xalpha,
                                                 const int* __restrict__ yofs, const int* __restrict__ ybeta) {
     TR_BEGIN()
-    const LevelGeom& D = P->lv[l];
-    const LevelGeom& S = P->lv[l - 1];
+    // geometry copied to registers (the byte stores below may alias the plan for the compiler)
+    const int Dw = P->lv[l].w, Dh = P->lv[l].h, Dpitch = P->lv[l].pitch;
+    const int xmax = P->lv[l].xmax, vend = P->lv[l].vend;
+    const int xtab = P->lv[l].xtab_off, ytab = P->lv[l].ytab_off;
+    const int Sw = P->lv[l - 1].w, Sh = P->lv[l - 1].h;
     const int f = blockIdx.z;
-    const int dy = blockIdx.y * 4 + threadIdx.y;
+    const int dyb = (blockIdx.y * 4 + threadIdx.y) * kRzRows;   // wave-uniform
     const int dx0 = (blockIdx.x * 64 + threadIdx.x) * 4;
-    if (dy >= D.h || dx0 >= D.w) return;
-    ImgRef src = level_img(P, fb, f, l - 1);
-    uint8_t* dst = fb.pyr + (int64_t)f * P->pyr_bytes + D.pyr_off + (int64_t)dy * D.pitch;
-    const int sy = yofs[D.ytab_off + dy];
-    const int r0 = sy < 0 ? 0 : (sy < S.h ? sy : S.h - 1);
-    const int r1 = sy + 1 < 0 ? 0 : (sy + 1 < S.h ? sy + 1 : S.h - 1);
-    const uint8_t* S0 = src.p + (int64_t)r0 * src.pitch;
-    const uint8_t* S1 = src.p + (int64_t)r1 * src.pitch;
-    const int bb = ybeta[D.ytab_off + dy];
-    const int b0 = (int)(short)(bb & 0xFFFF), b1 = (int)(short)(bb >> 16);
-    // the 4 columns' tables as one int4 each (16-byte aligned per level), and the source bytes
-    // of both rows as 3 aligned dwords when the rows are dword aligned and the span stays
-    // inside the row: 8 loads instead of 24
-    const int4 xo4 = *(const int4*)(xofs + D.xtab_off + dx0);
-    const int4 xa4 = *(const int4*)(xalpha + D.xtab_off + dx0);
+    if (dyb >= Dh || dx0 >= Dw) return;
+    const ImgRef src = level_img(P, fb, f, l - 1);
+    uint8_t* const dst0 = fb.pyr + (int64_t)f * P->pyr_bytes + P->lv[l].pyr_off;
+    // the 4 columns' tables as one int4 each (16-byte aligned per level), the rows' tables
+    const int4 xo4 = *(const int4*)(xofs + xtab + dx0);
+    const int4 xa4 = *(const int4*)(xalpha + xtab + dx0);
+    const int nrow = min(kRzRows, Dh - dyb);
+    int sy[kRzRows], bbv[kRzRows];
+#pragma unroll
+    for (int j = 0; j < kRzRows; j++) {
+        const int dy = dyb + min(j, nrow - 1);
+        sy[j] = __builtin_amdgcn_readfirstlane(yofs[ytab + dy]);   // dy is wave-uniform
+        bbv[j] = __builtin_amdgcn_readfirstlane(ybeta[ytab + dy]);
+    }
     const int sxa[4] = {xo4.x, xo4.y, xo4.z, xo4.w}, axa[4] = {xa4.x, xa4.y, xa4.z, xa4.w};
     const int base = sxa[0] & ~3;
-    const bool vec = ((src.pitch & 3) == 0) && ((((uintptr_t)src.p) & 3) == 0) && base + 12 <= S.w &&
-                     dx0 + 3 < D.w;
-    uint32_t w0[3] = {0u, 0u, 0u}, w1[3] = {0u, 0u, 0u};
-    if (vec) {
-        const uint32_t* p0 = (const uint32_t*)(S0 + base);
-        const uint32_t* p1 = (const uint32_t*)(S1 + base);
+    auto clampr = [&](int r) { return r < 0 ? 0 : (r < Sh ? r : Sh - 1); };
+    const int rbase = clampr(sy[0]);
+    // interior lanes: 4 full columns inside xmax / vend, the source span as 3 aligned dwords of
+    // each row, every row the outputs read within kRzSrc rows of rbase
+    const bool interior = ((src.pitch & 3) == 0) && ((((uintptr_t)src.p) & 3) == 0) && base + 12 <= Sw &&
+                          sxa[3] - base <= 10 &&
+                          dx0 + 3 < xmax && dx0 + 3 < vend && nrow == kRzRows &&
+                          clampr(sy[kRzRows - 1] + 1) - rbase < kRzSrc;
+    if (interior) {
+        uint32_t W[kRzSrc][3];
 #pragma unroll
-        for (int i = 0; i < 3; i++) { w0[i] = p0[i]; w1[i] = p1[i]; }
-    }
-    // bytes o and o + 1 (o = sx - base < 10) of a 12-byte row span
-    auto pair_at = [](const uint32_t* w, int o, int& a, int& b) {
-        const uint32_t lo = o < 4 ? w[0] : (o < 8 ? w[1] : w[2]);
-        const uint32_t hi = o < 4 ? w[1] : (o < 8 ? w[2] : 0u);
-        const uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(o & 3));
-        a = (int)(v & 0xFF);
-        b = (int)((v >> 8) & 0xFF);
-    };
-    uint32_t packed = 0;
+        for (int i = 0; i < kRzSrc; i++) {
+            const uint32_t* p = (const uint32_t*)(src.p + (int64_t)min(rbase + i, Sh - 1) * src.pitch + base);
+            W[i][0] = p[0]; W[i][1] = p[1]; W[i][2] = p[2];
+        }
+        // horizontal pass once per source row: bytes o, o + 1 (o = sx - base <= 10) of the 12-byte
+        // span picked by one v_perm into 16-bit halves, times the (a0, a1) pair by one dot2
+        int H[4][kRzSrc];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int dx = dx0 + k;
-        if (dx >= D.w) break;
-        const int sx = sxa[k];
-        int p00, p01, p10, p11;
-        if (vec) {
-            pair_at(w0, sx - base, p00, p01);
-            pair_at(w1, sx - base, p10, p11);
-        } else {
-            p00 = S0[sx]; p10 = S1[sx];
-            p01 = dx < D.xmax ? S0[sx + 1] : 0;
-            p11 = dx < D.xmax ? S1[sx + 1] : 0;
+        for (int k = 0; k < 4; k++) {
+            const int o = sxa[k] - base;
+            const uint32_t sel = 0x0C000C00u | (uint32_t)(o & 3) | ((uint32_t)((o & 3) + 1) << 16);
+            typedef short short2v __attribute__((ext_vector_type(2)));
+            const short2v av = __builtin_bit_cast(short2v, axa[k]);
+            // lane masks for the dword choice (a plain ?: over W lets the compiler turn the choice
+            // into an indexed scratch load)
+            const uint64_t m4 = __builtin_amdgcn_ballot_w64(o < 4), m8 = __builtin_amdgcn_ballot_w64(o < 8);
+            auto pick = [](uint32_t f, uint32_t t, uint64_t m) {
+                uint32_t r;
+                asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+                return r;
+            };
+#pragma unroll
+            for (int i = 0; i < kRzSrc; i++) {
+                const uint32_t lo = pick(pick(W[i][2], W[i][1], m8), W[i][0], m4);
+                const uint32_t hi = pick(W[i][2], W[i][1], m4);
+                const uint32_t pp = __builtin_amdgcn_perm(hi, lo, sel);   // (p0, p1) as u16 halves
+                H[k][i] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, pp), av, 0, false);
+            }
         }
-        int h0, h1;
-        if (dx < D.xmax) {
-            const int aa = axa[k];
-            const int a0 = (int)(short)(aa & 0xFFFF), a1 = (int)(short)(aa >> 16);
-            h0 = p00 * a0 + p01 * a1;
-            h1 = p10 * a0 + p11 * a1;
-        } else {
-            h0 = p00 * 2048;
-            h1 = p10 * 2048;
+#pragma unroll
+        for (int j = 0; j < kRzRows; j++) {
+            const int i0 = clampr(sy[j]) - rbase, i1 = clampr(sy[j] + 1) - rbase;   // wave-uniform
+            const int b0 = (int)(short)(bbv[j] & 0xFFFF), b1 = (int)(short)(bbv[j] >> 16);
+            uint32_t packed = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {   // VResizeLinearVec_32s8u lanes (128-bit baseline)
+                const int s0 = min(max(H[k][i0] >> 4, -32768), 32767);
+                const int s1 = min(max(H[k][i1] >> 4, -32768), 32767);
+                int t = ((s0 * b0) >> 16) + ((s1 * b1) >> 16);
+                t = min(max(t, -32768), 32767);
+                int v = (t + 2) >> 2;
+                v = v < 0 ? 0 : (v > 255 ? 255 : v);
+                packed |= (uint32_t)v << (8 * k);
+            }
+            *(uint32_t*)(dst0 + (int64_t)(dyb + j) * Dpitch + dx0) = packed;
         }
-        int v;
-        if (dx < D.vend) {   // VResizeLinearVec_32s8u lanes (128-bit baseline)
-            int s0 = min(max(h0 >> 4, -32768), 32767);
-            int s1 = min(max(h1 >> 4, -32768), 32767);
-            int t = ((s0 * b0) >> 16) + ((s1 * b1) >> 16);
-            t = min(max(t, -32768), 32767);
-            v = (t + 2) >> 2;
-        } else {             // FixedPtCast<int, uchar, 22>
-            v = (h0 * b0 + h1 * b1 + (1 << 21)) >> 22;
-        }
-        v = v < 0 ? 0 : (v > 255 ? 255 : v);
-        packed |= (uint32_t)v << (8 * k);
-    }
-    if (dx0 + 3 < D.w) {
-        *(uint32_t*)(dst + dx0) = packed;
     } else {
-        for (int k = 0; k < 4 && dx0 + k < D.w; k++) dst[dx0 + k] = (uint8_t)(packed >> (8 * k));
+        for (int j = 0; j < nrow; j++) {
+            const int dy = dyb + j;
+            uint8_t* dst = dst0 + (int64_t)dy * Dpitch;
+            const uint8_t* S0 = src.p + (int64_t)clampr(sy[j]) * src.pitch;
+            const uint8_t* S1 = src.p + (int64_t)clampr(sy[j] + 1) * src.pitch;
+            const int b0 = (int)(short)(bbv[j] & 0xFFFF), b1 = (int)(short)(bbv[j] >> 16);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int dx = dx0 + k;
+                if (dx >= Dw) break;
+                const int sx = sxa[k];
+                const bool inx = dx < xmax;
+                const int p00 = S0[sx], p10 = S1[sx];
+                const int p01 = inx ? S0[sx + 1] : 0, p11 = inx ? S1[sx + 1] : 0;
+                dst[dx] = (uint8_t)rz_px(p00, p01, p10, p11, axa[k], b0, b1, inx, dx < vend);
+            }
+        }
     }
     if (l == 1) { TR_END(0) }
 }
@@ -1662,7 +1711,7 @@ void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs
                    const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st) {
     const LevelGeom& D = hP.lv[l];
     dim3 blk(64, 4, 1);
-    dim3 grd((D.w + 255) / 256, (D.h + 3) / 4, B);
+    dim3 grd((D.w + 255) / 256, (D.h + 4 * kRzRows - 1) / (4 * kRzRows), B);
     hipLaunchKernelGGL(k_resize, grd, blk, 0, st, dP, fb, l, xofs, xalpha, yofs, ybeta);
 }
 

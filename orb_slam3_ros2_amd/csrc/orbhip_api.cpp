@@ -534,8 +534,10 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
     const char* e_dh = std::getenv("ORBHIP_OCTREE_DH");
     const int oct_fast = (e_sw && e_sw[0] == '1') ? 0 : 1;
     const int oct_max_dh = e_dh ? std::max(1, std::min(6, std::atoi(e_dh))) : 6;
+    // pyramid engine, also per call: ORBHIP_NO_CONE=1 forces the k_resize cascade
+    const bool no_cone = std::getenv("ORBHIP_NO_CONE") != nullptr;
     GraphKey key;
-    key.add(1).add((uint64_t)oct_fast).add((uint64_t)oct_max_dh).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
+    key.add(1).add((uint64_t)oct_fast).add((uint64_t)oct_max_dh).add((uint64_t)no_cone).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
         .add((uint64_t)lap1).ptr(d_kps).ptr(d_desc).add((uint64_t)cap).ptr(d_n).ptr(d_mono).ptr(st).ptr(c->d_pyr.p)
         .ptr(c->d_cand.p).ptr(c->d_kscratch.p).ptr(c->d_nscratch.p).ptr(c->d_cand_cnt.p).ptr(c->d_lvl_kp.p)
         .ptr(c->d_lvl_cnt.p).ptr(c->d_lvl_nlap.p).ptr(c->d_err.p);
@@ -544,7 +546,6 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
         fb.in = d_imgs; fb.in_stride = stride; fb.in_fstride = fstride; fb.pyr = c->d_pyr.p;
         StageTimer& tm = c->timer;
         tm.begin(1, st);
-        static const bool no_cone = std::getenv("ORBHIP_NO_CONE") != nullptr;   // A/B switch for the cascade
         // the cone recomputes each tile's halo on every level: it pays only while the per-level
         // cascade is launch-latency bound (a few work-groups per CU); big batches keep the cascade
         static const size_t cone_max = std::getenv("ORBHIP_CONE_MAX_WG")

@@ -41,6 +41,19 @@ def test_sizes_bit_exact(ext1000, oracle, w, h, seed):
     _check(ext1000, oracle, synthetic_frame(seed, w, h))
 
 
+@pytest.mark.parametrize("w,h,scale,nlev,seed", [(1280, 720, 1.2, 8, 30), (641, 479, 1.2, 8, 31),
+                                                 (641, 481, 1.5, 5, 32), (801, 601, 1.9, 4, 33),
+                                                 (1001, 751, 2.5, 3, 34)])
+def test_resize_cascade_bit_exact(oracle, monkeypatch, w, h, scale, nlev, seed):
+    """The per-level k_resize cascade (the batch engine) forced on single frames: odd sizes take
+    its edge lanes, scale factors above 1.2 its per-row path (a 4-row group reads more than 6
+    source rows), all bit-exact against the oracle's cv::resize restatement."""
+    from orb_slam3_ros2_amd import ORBextractor
+    monkeypatch.setenv("ORBHIP_NO_CONE", "1")
+    ext = ORBextractor(1000, scale, nlev, 20, 7)
+    _check(ext, oracle, synthetic_frame(seed, w, h), scale=scale, nlevels=nlev)
+
+
 def test_milkv_1250_features(oracle):
     """R:config/Monocular/MilkV.yaml:42-55 (1250 features) at its 640x360 camera size."""
     from orb_slam3_ros2_amd import ORBextractor
