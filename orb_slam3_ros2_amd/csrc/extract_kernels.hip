@@ -84,8 +84,10 @@ __global__ __launch_bounds__(256) void k_resize(const ExtractPlan* __restrict__ 
     const int xtab = P->lv[l].xtab_off, ytab = P->lv[l].ytab_off;
     const int Sw = P->lv[l - 1].w, Sh = P->lv[l - 1].h;
     const int f = blockIdx.z;
-    const int dyb = (blockIdx.y * 4 + threadIdx.y) * kRzRows;   // wave-uniform
-    const int dx0 = (blockIdx.x * 64 + threadIdx.x) * 4;
+    // row groups on blockIdx.x: consecutive work-groups (dealt round-robin to the XCDs) walk down
+    // a column strip, so every XCD gets the same share of the light right-edge strip
+    const int dyb = (blockIdx.x * 4 + threadIdx.y) * kRzRows;   // wave-uniform
+    const int dx0 = (blockIdx.y * 64 + threadIdx.x) * 4;
     if (dyb >= Dh || dx0 >= Dw) return;
     const ImgRef src = level_img(P, fb, f, l - 1);
     uint8_t* const dst0 = fb.pyr + (int64_t)f * P->pyr_bytes + P->lv[l].pyr_off;
@@ -118,44 +120,64 @@ __global__ __launch_bounds__(256) void k_resize(const ExtractPlan* __restrict__ 
             W[i][0] = p[0]; W[i][1] = p[1]; W[i][2] = p[2];
         }
         // horizontal pass once per source row: bytes o, o + 1 (o = sx - base <= 10) of the 12-byte
-        // span picked by one v_perm into 16-bit halves, times the (a0, a1) pair by one dot2
+        // span picked by one v_perm from the dword pair (w1:w0) (o <= 6) or (w2:w1) into 16-bit
+        // halves, times the (a0, a1) pair by one dot2. A column whose lanes all have o <= 6 (every
+        // column but the last at 1.2x) needs no pair choice.
+        typedef short short2v __attribute__((ext_vector_type(2)));
         int H[4][kRzSrc];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const int o = sxa[k] - base;
-            const uint32_t sel = 0x0C000C00u | (uint32_t)(o & 3) | ((uint32_t)((o & 3) + 1) << 16);
-            typedef short short2v __attribute__((ext_vector_type(2)));
+            const int oo = o > 6 ? o - 4 : o;
+            const uint32_t sel = 0x0C000C00u | (uint32_t)oo | ((uint32_t)(oo + 1) << 16);
             const short2v av = __builtin_bit_cast(short2v, axa[k]);
-            // lane masks for the dword choice (a plain ?: over W lets the compiler turn the choice
-            // into an indexed scratch load)
-            const uint64_t m4 = __builtin_amdgcn_ballot_w64(o < 4), m8 = __builtin_amdgcn_ballot_w64(o < 8);
-            auto pick = [](uint32_t f, uint32_t t, uint64_t m) {
-                uint32_t r;
-                asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
-                return r;
-            };
+            const uint64_t m = __builtin_amdgcn_ballot_w64(o > 6);
+            if (m == 0) {
 #pragma unroll
-            for (int i = 0; i < kRzSrc; i++) {
-                const uint32_t lo = pick(pick(W[i][2], W[i][1], m8), W[i][0], m4);
-                const uint32_t hi = pick(W[i][2], W[i][1], m4);
-                const uint32_t pp = __builtin_amdgcn_perm(hi, lo, sel);   // (p0, p1) as u16 halves
-                H[k][i] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, pp), av, 0, false);
+                for (int i = 0; i < kRzSrc; i++) {
+                    const uint32_t pp = __builtin_amdgcn_perm(W[i][1], W[i][0], sel);
+                    H[k][i] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, pp), av, 0, false);
+                }
+            } else {
+                // lane-mask choice (a plain ?: over W lets the compiler turn it into an indexed
+                // scratch load)
+                auto pick = [](uint32_t f, uint32_t t, uint64_t mm) {
+                    uint32_t r;
+                    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(mm));
+                    return r;
+                };
+#pragma unroll
+                for (int i = 0; i < kRzSrc; i++) {
+                    const uint32_t pp = __builtin_amdgcn_perm(pick(W[i][1], W[i][2], m), pick(W[i][0], W[i][1], m), sel);
+                    H[k][i] = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2v, pp), av, 0, false);
+                }
             }
         }
+        // vertical pass (VResizeLinearVec_32s8u lanes, 128-bit baseline); with taps checked on the
+        // host (rz_noclamp) its saturations cannot bind and are left out
+        const bool noclamp = P->lv[l].rz_noclamp != 0;
 #pragma unroll
         for (int j = 0; j < kRzRows; j++) {
             const int i0 = clampr(sy[j]) - rbase, i1 = clampr(sy[j] + 1) - rbase;   // wave-uniform
             const int b0 = (int)(short)(bbv[j] & 0xFFFF), b1 = (int)(short)(bbv[j] >> 16);
             uint32_t packed = 0;
+            if (noclamp) {
 #pragma unroll
-            for (int k = 0; k < 4; k++) {   // VResizeLinearVec_32s8u lanes (128-bit baseline)
-                const int s0 = min(max(H[k][i0] >> 4, -32768), 32767);
-                const int s1 = min(max(H[k][i1] >> 4, -32768), 32767);
-                int t = ((s0 * b0) >> 16) + ((s1 * b1) >> 16);
-                t = min(max(t, -32768), 32767);
-                int v = (t + 2) >> 2;
-                v = v < 0 ? 0 : (v > 255 ? 255 : v);
-                packed |= (uint32_t)v << (8 * k);
+                for (int k = 0; k < 4; k++) {
+                    const int t = (__mul24(H[k][i0] >> 4, b0) >> 16) + (__mul24(H[k][i1] >> 4, b1) >> 16);
+                    packed |= (uint32_t)((t + 2) >> 2) << (8 * k);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const int s0 = min(max(H[k][i0] >> 4, -32768), 32767);
+                    const int s1 = min(max(H[k][i1] >> 4, -32768), 32767);
+                    int t = ((s0 * b0) >> 16) + ((s1 * b1) >> 16);
+                    t = min(max(t, -32768), 32767);
+                    int v = (t + 2) >> 2;
+                    v = v < 0 ? 0 : (v > 255 ? 255 : v);
+                    packed |= (uint32_t)v << (8 * k);
+                }
             }
             *(uint32_t*)(dst0 + (int64_t)(dyb + j) * Dpitch + dx0) = packed;
         }
@@ -1711,7 +1733,7 @@ void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs
                    const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st) {
     const LevelGeom& D = hP.lv[l];
     dim3 blk(64, 4, 1);
-    dim3 grd((D.w + 255) / 256, (D.h + 4 * kRzRows - 1) / (4 * kRzRows), B);
+    dim3 grd((D.h + 4 * kRzRows - 1) / (4 * kRzRows), (D.w + 255) / 256, B);
     hipLaunchKernelGGL(k_resize, grd, blk, 0, st, dP, fb, l, xofs, xalpha, yofs, ybeta);
 }
 

@@ -258,6 +258,14 @@ static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& ou
         G.ytab_off = (int)pl->yofs.size();
         G.xmax = G.w;
         G.vend = 0;
+        G.rz_noclamp = 1;
+        // |p| <= 255 and taps a0, a1, b0, b1 >= 0 with a0 + a1, b0 + b1 <= 2049 keep every
+        // intermediate of the vertical pass in range: (255 * 2049) >> 4 < 32768, and the rounded
+        // sum (t + 2) >> 2 <= 255
+        auto taps_ok = [](int packed) {
+            const int t0 = (int)(short)(packed & 0xFFFF), t1 = (int)(short)(packed >> 16);
+            return t0 >= 0 && t1 >= 0 && t0 + t1 <= 2049;
+        };
         if (l > 0) {
             const int sw = P.lv[l - 1].w, sh = P.lv[l - 1].h, dw = G.w, dh = G.h;
             double inv_sx = (double)dw / sw, inv_sy = (double)dh / sh;
@@ -278,6 +286,7 @@ static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& ou
                 pl->xofs.push_back(sx);
                 const short a0 = sat_s16(round_even_f((1.f - fx) * 2048)), a1 = sat_s16(round_even_f(fx * 2048));
                 pl->xalpha.push_back((int)(uint16_t)a0 | ((int)(uint16_t)a1 << 16));
+                if (!taps_ok(pl->xalpha.back())) G.rz_noclamp = 0;
             }
             for (int dy = 0; dy < dh; dy++) {
                 float fy = (float)((dy + 0.5) * scale_y - 0.5);
@@ -286,6 +295,7 @@ static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& ou
                 pl->yofs.push_back(sy);
                 const short b0 = sat_s16(round_even_f((1.f - fy) * 2048)), b1 = sat_s16(round_even_f(fy * 2048));
                 pl->ybeta.push_back((int)(uint16_t)b0 | ((int)(uint16_t)b1 << 16));
+                if (!taps_ok(pl->ybeta.back())) G.rz_noclamp = 0;
             }
             G.xmax = xmax;
             int x = 0;

@@ -22,6 +22,7 @@ struct LevelGeom {
     int n_ini;                // DistributeOctTree root count
     float hX;                 // root width
     int kp_cap, kp_base;      // octree output capacity / offset (per frame)
+    int rz_noclamp;           // resize taps in [0, 2049] summing to <= 2049: k_resize's saturations are no-ops
     int oct_tab_off;          // octree interval table of the level (u16): max_bx - min_bx column
                               // entries (root << 8 | 6 x-split bits), then max_by - min_by row entries
     int patch_size;           // (int)(31 * scale)
