@@ -487,21 +487,50 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
         return (py + 1) * W2 + px + 1;
     };
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int p0 = 0; p0 < np; p0 += NT) {
-        const int p = p0 + tid;
-        bool pass = false;
-        if (p < np) {
-            int d[16];
-            const int mi = diffs(p, d);
-            pass = fast_pair_test(d, t_lo);
-            mv[mi] = 0;
+    const int clist_cap = P->clist_cap;
+    // the pair test runs on two pixels per lane (q and q + half) as 16-bit halves: the circle
+    // bytes land in the halves straight from LDS (d16 / d16_hi loads), and the min / max chains
+    // and threshold compares are packed ops. In circle values c (d = v - c): bright iff
+    // min_k max(c_k, c_k+8) > v + t, dark iff v > max_k min(c_k, c_k+8) + t.
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const int half = (np + 1) >> 1;
+    const u16x2 tv = {(unsigned short)t_lo, (unsigned short)t_lo};
+    for (int q0 = 0; q0 < half; q0 += NT) {
+        const int q = q0 + tid;
+        bool pass0 = false, pass1 = false;
+        if (q < half) {
+            const bool two = q + half < np;
+            const int pa = q, pb = two ? q + half : q;
+            const int ya = small_div(pa, inv_dc), xa = pa - ya * dc;
+            const int yb = small_div(pb, inv_dc), xb = pb - yb * dc;
+            const uint8_t* ca = &win[(ya + 3) * kWinP + xa + 3 + sh];
+            const uint8_t* cb = &win[(yb + 3) * kWinP + xb + 3 + sh];
+            constexpr int P = kWinP;
+            constexpr int o[16] = {3 * P,      3 * P + 1,  2 * P + 2,  P + 3,      3,      -P + 3, -2 * P + 2, -3 * P + 1,
+                                   -3 * P,     -3 * P - 1, -2 * P - 2, -P - 3,     -3,     P - 3,  2 * P - 2,  3 * P - 1};
+            u16x2 c[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) c[k] = u16x2{(unsigned short)ca[o[k]], (unsigned short)cb[o[k]]};
+            const u16x2 v = {(unsigned short)ca[0], (unsigned short)cb[0]};
+            u16x2 M1 = __builtin_elementwise_max(c[0], c[8]), M2 = __builtin_elementwise_min(c[0], c[8]);
+#pragma unroll
+            for (int k = 1; k < 8; k++) {
+                M1 = __builtin_elementwise_min(M1, __builtin_elementwise_max(c[k], c[k + 8]));
+                M2 = __builtin_elementwise_max(M2, __builtin_elementwise_min(c[k], c[k + 8]));
+            }
+            const u16x2 X = v + tv, Y = M2 + tv;
+            pass0 = (M1.x > X.x) | (v.x > Y.x);
+            pass1 = two & ((M1.y > X.y) | (v.y > Y.y));
+            mv[(ya + 1) * W2 + xa + 1] = 0;
+            mv[(yb + 1) * W2 + xb + 1] = 0;
         }
-        const uint64_t bal = __ballot(pass);
+        const uint64_t b0 = __ballot(pass0), b1 = __ballot(pass1);
         int base = 0;
-        if (lane == 0 && bal) base = atomicAdd(&ncand, __popcll(bal));
+        if (lane == 0 && (b0 | b1)) base = atomicAdd(&ncand, __popcll(b0) + __popcll(b1));
         base = __shfl(base, 0, 64);
-        const int ci = base + __popcll(bal & lt);
-        if (pass && ci < P->clist_cap) clist[ci] = (uint16_t)p;
+        const int ci0 = base + __popcll(b0 & lt), ci1 = base + __popcll(b0) + __popcll(b1 & lt);
+        if (pass0 && ci0 < clist_cap) clist[ci0] = (uint16_t)q;
+        if (pass1 && ci1 < clist_cap) clist[ci1] = (uint16_t)(q + half);
     }
     __syncthreads();
     // dense: the list overflowed, so the strength and NMS passes walk every pixel instead (the
