@@ -373,26 +373,38 @@ __device__ __forceinline__ bool fast_pair_test(const int* d, int t) {
     return (bright < -t) | (dark > t);
 }
 
-// LDS of one FAST cell (static in k_fast_cells)
+// LDS of one FAST cell: static arrays in k_fast_cells, sized for windows of up to WR rows (80:
+// any cell; 56: the compact variant, rows of 64 bytes, ~9.6 KB, which keeps 16 work-groups of
+// 128 threads per CU)
+template <int WR>
+struct FastShape {
+    static constexpr bool full = WR >= kWinMax;
+    static constexpr int wp = full ? kWinP : 64;                     // window / map row pitch
+    static constexpr int nw = ((WR - 6) * (wp - 6) + 63) / 64;       // mask words of the largest cell
+    static constexpr int cap = full ? kClistCap : 768;               // survivor list entries
+};
 struct FastLds {
-    uint8_t* win;                   // kWinMax^2 window
-    uint8_t* mv;                    // kWinMax^2 strength map
-    unsigned long long (*bmask)[96];   // [2][96] NMS survivors per threshold, raster order (<= 6144 px)
-    int* woff;                      // [96] output offset of each 64-px word
+    uint8_t* win;                   // window, rows of kWinP bytes
+    uint8_t* mv;                    // strength map, rows of kWinP bytes
+    unsigned long long* bmask;      // [2][nw] NMS survivors per threshold, raster order
+    int nw;
+    int* woff;                      // [nw] output offset of each 64-px word
     int* wsel;
     int* wtot;
-    uint16_t* clist;                // kClistCap pair-test survivors (strength to compute)
+    uint16_t* clist;                // pair-test survivors (strength to compute)
     int* ncand;
+    int cap;                        // clist entries in use: min(plan's clist_cap, the variant's)
 };
 
-template <int NT>
+template <int NT, int WP>
 __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P, const CellGeom* __restrict__ cells,
                                                const FrameBufs& fb, uint32_t* __restrict__ cand,
                                                int* __restrict__ cand_cnt, int* __restrict__ err, int cell, int f,
                                                const FastLds& LS) {
     uint8_t* const win = LS.win;
     uint8_t* const mv = LS.mv;
-    unsigned long long (*const bmask)[96] = LS.bmask;
+    unsigned long long* const bm0 = LS.bmask;
+    unsigned long long* const bm1 = LS.bmask + LS.nw;
     int* const woff = LS.woff;
     int& wsel = *LS.wsel;
     int& wtot = *LS.wtot;
@@ -415,14 +427,14 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     const uint8_t* base = im.p + (int64_t)cg.y0 * im.pitch + cg.x0;
     // ---- window -> LDS: all loads of a thread issued back to back. When the rows are 4-byte
     // aligned (pyramid levels always; the caller's frame when its pointer and stride are), the
-    // window moves as aligned dwords into LDS rows of kWinP bytes, shifted by sh = base & 3 ----
+    // window moves as aligned dwords into LDS rows of WP bytes, shifted by sh = base & 3 ----
     int sh = 0;
     {
         const bool dw = ((im.pitch & 3) == 0) && ((((uintptr_t)im.p) & 3) == 0);
         if (dw) {
             sh = (int)(((uintptr_t)base) & 3);
             const uint32_t* b4 = (const uint32_t*)(base - sh);
-            const int nwd = (wc + sh + 3) >> 2;   // <= kWinP / 4
+            const int nwd = (wc + sh + 3) >> 2;   // <= WP / 4
             const int tot = nwd * hc, p4 = im.pitch >> 2;
             const float inv_n = 1.0f / (float)nwd;
             uint32_t* w4 = (uint32_t*)win;
@@ -435,7 +447,7 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
                     const int i = min(tid + NT * u, tot - 1);
                     const int yy = small_div(i, inv_n), xx = i - yy * nwd;
                     v[u] = b4[(int64_t)yy * p4 + xx];
-                    li[u] = yy * (kWinP / 4) + xx;
+                    li[u] = yy * (WP / 4) + xx;
                 }
 #pragma unroll
                 for (int u = 0; u < NU; u++)
@@ -443,7 +455,7 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
             } else {
                 for (int i = tid; i < tot; i += NT) {
                     const int yy = small_div(i, inv_n), xx = i - yy * nwd;
-                    w4[yy * (kWinP / 4) + xx] = b4[(int64_t)yy * p4 + xx];
+                    w4[yy * (WP / 4) + xx] = b4[(int64_t)yy * p4 + xx];
                 }
             }
         } else {
@@ -451,12 +463,12 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
             const float inv_wc = 1.0f / (float)wc;
             for (int i = tid; i < tot; i += NT) {
                 const int yy = small_div(i, inv_wc), xx = i - yy * wc;
-                win[yy * kWinP + xx] = base[(int64_t)yy * im.pitch + xx];
+                win[yy * WP + xx] = base[(int64_t)yy * im.pitch + xx];
             }
         }
     }
     if (tid == 0) ncand = 0;
-    for (int i = tid; i < 192; i += NT) bmask[i / 96][i % 96] = 0ull;
+    for (int i = tid; i < 2 * LS.nw; i += NT) LS.bmask[i] = 0ull;
     __syncthreads();
     TR_PHASE(1, 0)
     const int t_ini = P->ini_th, t_min = P->min_th;
@@ -465,8 +477,8 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     const float inv_dc = 1.0f / (float)dc;
     // ---- strength map: m if m > t_lo (a corner at some threshold in use), else 0; stored with
     // a zero border (row pitch W2 = dc + 2) so the NMS reads its 3x3 without bounds checks ----
-    // both LDS maps use the fixed pitch kWinP: every neighbour offset is an immediate
-    constexpr int W2 = kWinP;
+    // both LDS maps use the fixed pitch WP: every neighbour offset is an immediate
+    constexpr int W2 = WP;
     const int Wz = dc + 2;   // zero border: rows 0 and dr + 1, columns 0 and dc + 1
     for (int i = tid; i < 2 * Wz + 2 * dr; i += NT) {
         const int idx = i < Wz ? i : (i < 2 * Wz ? (dr + 1) * W2 + (i - Wz) : (1 + (i - 2 * Wz) / 2) * W2 + ((i & 1) ? Wz - 1 : 0));
@@ -477,8 +489,8 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     // issue slots on masked-off lanes
     auto diffs = [&](int p, int* d) {
         const int py = small_div(p, inv_dc), px = p - py * dc;
-        const uint8_t* c = &win[(py + 3) * kWinP + px + 3 + sh];
-        constexpr int P = kWinP;
+        const uint8_t* c = &win[(py + 3) * WP + px + 3 + sh];
+        constexpr int P = WP;
         constexpr int o[16] = {3 * P,      3 * P + 1,  2 * P + 2,  P + 3,      3,      -P + 3, -2 * P + 2, -3 * P + 1,
                                -3 * P,     -3 * P - 1, -2 * P - 2, -P - 3,     -3,     P - 3,  2 * P - 2,  3 * P - 1};
         const int vv = c[0];
@@ -487,7 +499,7 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
         return (py + 1) * W2 + px + 1;
     };
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const int clist_cap = P->clist_cap;
+    const int clist_cap = LS.cap;
     // the pair test runs on two pixels per lane (q and q + half) as 16-bit halves: the circle
     // bytes land in the halves straight from LDS (d16 / d16_hi loads), and the min / max chains
     // and threshold compares are packed ops. In circle values c (d = v - c): bright iff
@@ -503,9 +515,9 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
             const int pa = q, pb = two ? q + half : q;
             const int ya = small_div(pa, inv_dc), xa = pa - ya * dc;
             const int yb = small_div(pb, inv_dc), xb = pb - yb * dc;
-            const uint8_t* ca = &win[(ya + 3) * kWinP + xa + 3 + sh];
-            const uint8_t* cb = &win[(yb + 3) * kWinP + xb + 3 + sh];
-            constexpr int P = kWinP;
+            const uint8_t* ca = &win[(ya + 3) * WP + xa + 3 + sh];
+            const uint8_t* cb = &win[(yb + 3) * WP + xb + 3 + sh];
+            constexpr int P = WP;
             constexpr int o[16] = {3 * P,      3 * P + 1,  2 * P + 2,  P + 3,      3,      -P + 3, -2 * P + 2, -3 * P + 1,
                                    -3 * P,     -3 * P - 1, -2 * P - 2, -P - 3,     -3,     P - 3,  2 * P - 2,  3 * P - 1};
             u16x2 c[16];
@@ -535,7 +547,7 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     __syncthreads();
     // dense: the list overflowed, so the strength and NMS passes walk every pixel instead (the
     // pair test repeated; pixels that failed it hold m = 0 and are skipped by the NMS)
-    const bool dense = ncand > P->clist_cap;
+    const bool dense = ncand > clist_cap;
     const int nc = dense ? np : ncand;
     for (int i = tid; i < nc; i += NT) {
         int d[16];
@@ -564,8 +576,8 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
             k_min &= (m - 1) > (mq > t_min ? mq - 1 : 0);
         }
         const unsigned long long bit = 1ull << (p & 63);
-        if (k_ini) atomicOr(&bmask[0][p >> 6], bit);
-        if (k_min) atomicOr(&bmask[1][p >> 6], bit);
+        if (k_ini) atomicOr(&bm0[p >> 6], bit);
+        if (k_min) atomicOr(&bm1[p >> 6], bit);
     }
     __syncthreads();
     TR_PHASE(1, 2)
@@ -573,12 +585,13 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     const int nwd = (np + 63) >> 6;
     if (wid == 0) {
         int ci = 0;
-        for (int w = lane; w < nwd; w += 64) ci += __popcll(bmask[0][w]);
+        for (int w = lane; w < nwd; w += 64) ci += __popcll(bm0[w]);
         const int tot_ini = wave_sum_i32(ci);
         const int sel = tot_ini > 0 ? 0 : 1;
-        // exclusive scan of the selected mask's word popcounts (2 words per lane: nwd <= 96)
+        const unsigned long long* bs = sel ? bm1 : bm0;
+        // exclusive scan of the selected mask's word popcounts (2 words per lane: nwd <= 128)
         const int w0 = 2 * lane, w1 = 2 * lane + 1;
-        const int c0 = w0 < nwd ? __popcll(bmask[sel][w0]) : 0, c1 = w1 < nwd ? __popcll(bmask[sel][w1]) : 0;
+        const int c0 = w0 < nwd ? __popcll(bs[w0]) : 0, c1 = w1 < nwd ? __popcll(bs[w1]) : 0;
         const int inc = wave_incl_scan(c0 + c1);
         if (w0 < nwd) woff[w0] = inc - c0 - c1;
         if (w1 < nwd) woff[w1] = inc - c1;
@@ -588,7 +601,7 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     const int sel = wsel;
     uint32_t* out = cand + (int64_t)f * P->n_slots_total + cg.slot_off;
     for (int w = wid; w < nwd; w += NW) {
-        const uint64_t mk = bmask[sel][w];
+        const uint64_t mk = (sel ? bm1 : bm0)[w];
         const int p = 64 * w + lane;
         if ((mk >> lane) & 1ull) {
             const int py = small_div(p, inv_dc), px = p - py * dc;
@@ -601,21 +614,22 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     TR_END(1)
 }
 
-template <int NT>
+template <int NT, int WR>
 __global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict__ P,
                                                     const CellGeom* __restrict__ cells, FrameBufs fb,
                                                     uint32_t* __restrict__ cand, int* __restrict__ cand_cnt,
                                                     int* __restrict__ err, int xrun) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[kWinMax * kWinMax];
-    __shared__ uint8_t mv[kWinMax * kWinMax];
-    __shared__ unsigned long long bmask[2][96];
-    __shared__ int woff[96];
+    using SH = FastShape<WR>;
+    __shared__ __attribute__((aligned(16))) uint8_t win[WR * SH::wp];
+    __shared__ uint8_t mv[WR * SH::wp];
+    __shared__ unsigned long long bmask[2 * SH::nw];
+    __shared__ int woff[SH::nw];
     __shared__ int wsel, wtot;
-    __shared__ uint16_t clist[kClistCap];
+    __shared__ uint16_t clist[SH::cap];
     __shared__ int ncand;
-    const FastLds LS{win, mv, bmask, woff, &wsel, &wtot, clist, &ncand};
+    const FastLds LS{win, mv, bmask, SH::nw, woff, &wsel, &wtot, clist, &ncand, min(P->clist_cap, SH::cap)};
     const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
-    fast_cell_body<NT>(P, cells, fb, cand, cand_cnt, err, lg % X, lg / X, LS);
+    fast_cell_body<NT, SH::wp>(P, cells, fb, cand, cand_cnt, err, lg % X, lg / X, LS);
 }
 
 // ---------------------------------------------------------------------------
@@ -1781,19 +1795,29 @@ void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* c
                  uint32_t* cand, int* cand_cnt, int* err, hipStream_t st) {
     // more threads per cell while the cells alone cannot fill the chip (one frame: ~600 cells on
     // 256 CUs), as many as keep every work-group resident at once (8192 wave slots); 256 once
-    // the batch fills the chip
+    // the batch fills the chip; 128 for big batches (C3: 127k cells), where fewer waves per cell
+    // idle less at the phase barriers and the compact LDS variant keeps 16 work-groups per CU
     const int ncell = B * hP.n_cells_total;
-    const int nt = hP.fast_nt ? hP.fast_nt : (ncell <= 512 ? 1024 : (ncell <= 1024 ? 512 : 256));
+    const int nt = hP.fast_nt ? hP.fast_nt
+                              : (ncell <= 512 ? 1024 : (ncell <= 1024 ? 512 : (ncell <= 32768 ? 256 : 128)));
     dim3 grd(hP.n_cells_total, B, 1);
     const int xr = xcd_run_for(B);
+    const bool compact = hP.fast_win_rows <= 56 && hP.fast_win_cols + 3 <= 64;   // window dwords (sh <= 3) fit a row
+#define ORBHIP_FAST_LAUNCH(NTV, WRV) \
+    hipLaunchKernelGGL((k_fast_cells<NTV, WRV>), grd, dim3(NTV), 0, st, dP, cells, fb, cand, cand_cnt, err, xr)
     if (nt == 1024)
-        hipLaunchKernelGGL(k_fast_cells<1024>, grd, dim3(1024), 0, st, dP, cells, fb, cand, cand_cnt, err, xr);
+        ORBHIP_FAST_LAUNCH(1024, kWinMax);
     else if (nt == 512)
-        hipLaunchKernelGGL(k_fast_cells<512>, grd, dim3(512), 0, st, dP, cells, fb, cand, cand_cnt, err, xr);
-    else if (nt == 128)   // A/B and tests only (ORBHIP_FAST_NT=128)
-        hipLaunchKernelGGL(k_fast_cells<128>, grd, dim3(128), 0, st, dP, cells, fb, cand, cand_cnt, err, xr);
+        ORBHIP_FAST_LAUNCH(512, kWinMax);
+    else if (nt == 128 && compact)
+        ORBHIP_FAST_LAUNCH(128, 56);
+    else if (nt == 128)
+        ORBHIP_FAST_LAUNCH(128, kWinMax);
+    else if (compact)
+        ORBHIP_FAST_LAUNCH(256, 56);
     else
-        hipLaunchKernelGGL(k_fast_cells<256>, grd, dim3(256), 0, st, dP, cells, fb, cand, cand_cnt, err, xr);
+        ORBHIP_FAST_LAUNCH(256, kWinMax);
+#undef ORBHIP_FAST_LAUNCH
 }
 
 size_t octree_lds_bytes(const ExtractPlan& hP, const OctreeCfg& cfg) {

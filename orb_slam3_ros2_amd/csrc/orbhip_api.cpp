@@ -239,7 +239,7 @@ static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& ou
     for (int i = 0; i < 7; i++)
         if (P.blurk[i] != kTaps[i]) return ORBHIP_ERR_UNSUPPORTED;
     int64_t pyr_off = 0;
-    int cell_base = 0, slot_base = 0, kp_base = 0, max_cells = 0;
+    int cell_base = 0, slot_base = 0, kp_base = 0, max_cells = 0, hc_max = 7, wc_max = 7;
     for (int l = 0; l < L; l++) {
         LevelGeom& G = P.lv[l];
         G.w = round_even_f((float)w * c->inv_scale[l]);
@@ -335,6 +335,10 @@ static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& ou
                 cg.slot_off = slot_base;
                 const int dc = std::max(cg.wc - 6, 0), dr = std::max(cg.hc - 6, 0);
                 slot_base += ((dc + 1) / 2) * ((dr + 1) / 2);   // max strict-NMS survivors
+                if (cg.wc > 6 && cg.hc > 6) {   // cells k_fast_cells works on
+                    hc_max = std::max(hc_max, (int)cg.hc);
+                    wc_max = std::max(wc_max, (int)cg.wc);
+                }
                 pl->cells.push_back(cg);
                 ncell++;
             }
@@ -381,6 +385,8 @@ static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& ou
     P.pyr_bytes = ((pyr_off + 255) / 256) * 256;
     P.max_cells_level = max_cells;
     pl->kp_cap_frame = kp_base;
+    P.fast_win_rows = hc_max;   // k_fast_cells' LDS variant
+    P.fast_win_cols = wc_max;
     // cone pyramid tables: tiles of ~10x10 on the last level (252 at 640x480: the per-tile cascade
     // is latency bound, so smaller cones finish sooner), an even partition of every level
     if (L > 1) {

@@ -101,17 +101,20 @@ def test_fast_dense_pass(oracle, monkeypatch, cap):
 
 @pytest.mark.parametrize("nt", [128, 256, 512, 1024])
 @pytest.mark.parametrize("cap", [0, 2048])
-def test_fast_threads_per_cell_batched(oracle, monkeypatch, nt, cap):
+@pytest.mark.parametrize("size", [(640, 480), (320, 240)])
+def test_fast_threads_per_cell_batched(oracle, monkeypatch, nt, cap, size):
     """Every k_fast_cells variant (threads per cell pinned per plan by ORBHIP_FAST_NT) on a batch
-    of 3 frames through the device path, with the survivor list (cap 2048, the default) and the
-    dense pass forced (cap 0): each frame equals the oracle."""
+    of 3 frames through the device path, with the survivor list (cap 2048, the default; the
+    compact LDS variant lists 768) and the dense pass forced (cap 0): each frame equals the
+    oracle. 640x480 cells fit the compact LDS variant (128 / 256 threads); 320x240 has one-row
+    levels whose cells (up to 75 rows) take the full one."""
     import torch
     monkeypatch.setenv("ORBHIP_FAST_NT", str(nt))
     monkeypatch.setenv("ORBHIP_FAST_CLIST_CAP", str(cap))
     from orb_slam3_ros2_amd import ORBextractor
     ext = ORBextractor(1000, 1.2, 8, 20, 7)   # a fresh context: the plan reads both variables
     rng = np.random.default_rng(nt + cap)
-    B, H, W = 3, 480, 640
+    B, (W, H) = 3, size
     frames = np.stack([synthetic_frame(70 + nt % 7, W, H), rng.integers(0, 256, size=(H, W), dtype=np.uint8),
                        (128 + rng.integers(-9, 10, size=(H, W))).astype(np.uint8)])
     kcap = ext.max_keypoints(W, H)
