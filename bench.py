@@ -737,6 +737,12 @@ def c3_batch(args, ws, rank):
                               "traffic": load_traffic(ks, "c3"), "counters": load_counters(ks, "c3"),
                               "algorithmic_bytes_per_launch": int(b3[d3]), "avg_launch_ms": round(c3_ms[d3], 4),
                               "stage_avg_ms": {STAGES[k]: round(v, 4) for k, v in c3_ms.items()}}
+        # the extractor's streaming stage against the HBM roof: the 7-level k_resize cascade
+        # (level l-1 read, level l written, per frame), timed as one stage (launch gaps included)
+        ah = b3[1] / (c3_ms[1] * 1e-3) / 1e9
+        out["c3_hbm_stage"] = {"kernel": kernel_symbol(1, c3.nb), "bound": "hbm", "achieved": round(ah, 1),
+                               "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ah / HBM_PEAK_GBS, 4),
+                               "algorithmic_bytes_per_stage": int(b3[1]), "stage_ms": round(c3_ms[1], 4)}
     return out
 
 
@@ -884,6 +890,15 @@ def main():
             out["cpu_baseline"]["c4_lba_single_core_kf_per_s"] = round(cl["single"], 2)
             out["cpu_baseline"]["c4_lba_sample"] = f"{cl['solves']} oracle LBA solves, {cl['cores']} threads"
             out["cpu_baseline"].update(cpu_f8_tracking())
+            # C3's workload on the CPU: 1280x720 frames of the same generator, each extracted and
+            # matched to the previous one, one frame stream per thread (bounded sample)
+            c3f = make_stream_frames(16, BatchC3.W, BatchC3.H, 5000)
+            c3c = cpu_baseline(c3f, budget_s=8.0)
+            out["cpu_baseline"]["c3_frames_per_s"] = round(c3c["value"], 2)
+            out["cpu_baseline"]["c3_single_core_frames_per_s"] = round(c3c["single"], 2)
+            out["cpu_baseline"]["c3_sample"] = (f"{c3c['frames']} 1280x720 frames (16-frame stream, seed 5000), each "
+                                                f"extract + match to the previous frame, {c3c['cores']} threads, "
+                                                f"{c3c['wall']:.1f}s wall")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if ws > 1:
