@@ -438,7 +438,7 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
             const int tot = nwd * hc, p4 = im.pitch >> 2;
             const float inv_n = 1.0f / (float)nwd;
             uint32_t* w4 = (uint32_t*)win;
-            constexpr int NU = (NT >= 512) ? 1 : 2;
+            constexpr int NU = (NT >= 512) ? 1 : 512 / NT;   // a 44 x 43 window (473 dwords) in one round
             if (tot <= NU * NT) {
                 uint32_t v[NU];
                 int li[NU];
