@@ -336,6 +336,7 @@ __global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict
 // threshold t iff m > t (derivation in DESIGN.md), so one map serves both thresholds.
 // ---------------------------------------------------------------------------
 constexpr int kWinMax = 80;
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));   // two pixels, one per 16-bit half
 constexpr int kWinP = kWinMax;   // LDS row pitch of the FAST window and strength maps
 static_assert(kWinP % 4 == 0, "dword window rows");
 
@@ -504,7 +505,6 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     // bytes land in the halves straight from LDS (d16 / d16_hi loads), and the min / max chains
     // and threshold compares are packed ops. In circle values c (d = v - c): bright iff
     // min_k max(c_k, c_k+8) > v + t, dark iff v > max_k min(c_k, c_k+8) + t.
-    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
     const int half = (np + 1) >> 1;
     const u16x2 tv = {(unsigned short)t_lo, (unsigned short)t_lo};
     for (int q0 = 0; q0 < half; q0 += NT) {
@@ -549,13 +549,65 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     // pair test repeated; pixels that failed it hold m = 0 and are skipped by the NMS)
     const bool dense = ncand > clist_cap;
     const int nc = dense ? np : ncand;
-    for (int i = tid; i < nc; i += NT) {
-        int d[16];
-        const int mi = diffs(dense ? i : clist[i], d);
-        if (dense && !fast_pair_test(d, t_lo)) continue;
-        int m = fast_strength_d(d);
-        if (m <= t_lo) m = 0;
-        mv[mi] = (uint8_t)m;
+    if (dense) {
+        for (int i = tid; i < nc; i += NT) {
+            int d[16];
+            const int mi = diffs(i, d);
+            if (!fast_pair_test(d, t_lo)) continue;
+            int m = fast_strength_d(d);
+            if (m <= t_lo) m = 0;
+            mv[mi] = (uint8_t)m;
+        }
+    } else {
+        // listed survivors two per lane (i and i + hn) as 16-bit halves, in circle values:
+        // m = max(v - min over 9-arcs of the arc max, max over 9-arcs of the arc min - v, 0), the
+        // arc extrema built by doubling (2-, 4-, 8-arcs, then the 9th value)
+        const int hn = (nc + 1) >> 1;
+        for (int i = tid; i < hn; i += NT) {
+            const bool two = i + hn < nc;
+            const int pa = clist[i], pb = two ? clist[i + hn] : pa;
+            const int ya = small_div(pa, inv_dc), xa = pa - ya * dc;
+            const int yb = small_div(pb, inv_dc), xb = pb - yb * dc;
+            const uint8_t* ca = &win[(ya + 3) * WP + xa + 3 + sh];
+            const uint8_t* cb = &win[(yb + 3) * WP + xb + 3 + sh];
+            constexpr int P = WP;
+            constexpr int o[16] = {3 * P,      3 * P + 1,  2 * P + 2,  P + 3,      3,      -P + 3, -2 * P + 2, -3 * P + 1,
+                                   -3 * P,     -3 * P - 1, -2 * P - 2, -P - 3,     -3,     P - 3,  2 * P - 2,  3 * P - 1};
+            u16x2 c[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) c[k] = u16x2{(unsigned short)ca[o[k]], (unsigned short)cb[o[k]]};
+            const u16x2 v = {(unsigned short)ca[0], (unsigned short)cb[0]};
+            // one network at a time (mins, then maxes): 16 arc registers live instead of 32
+            auto arc9 = [&](auto op, auto fold, u16x2 init) {
+                u16x2 t[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) t[k] = op(c[k], c[(k + 1) & 15]);   // 2-arcs k, k+1
+#pragma unroll
+                for (int sp = 2; sp <= 4; sp *= 2) {   // 4-arcs, then 8-arcs
+                    u16x2 h[4];
+#pragma unroll
+                    for (int k = 0; k < 4; k++) h[k] = t[k];
+#pragma unroll
+                    for (int k = 0; k < 16; k++) {
+                        const int j = (k + sp) & 15;
+                        t[k] = op(t[k], j < 4 ? h[j] : t[j]);
+                    }
+                }
+                u16x2 r = init;
+#pragma unroll
+                for (int k = 0; k < 16; k++) r = fold(r, op(t[k], c[(k + 8) & 15]));   // 9-arcs k .. k+8
+                return r;
+            };
+            auto vmin = [](u16x2 p, u16x2 q) { return __builtin_elementwise_min(p, q); };
+            auto vmax = [](u16x2 p, u16x2 q) { return __builtin_elementwise_max(p, q); };
+            const u16x2 Mm = arc9(vmin, vmax, u16x2{0, 0});       // max over arcs of the arc min
+            const u16x2 MM = arc9(vmax, vmin, u16x2{255, 255});   // min over arcs of the arc max
+            const u16x2 m2 = __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, MM),
+                                                       __builtin_elementwise_sub_sat(Mm, v));
+            const int ma = m2.x > t_lo ? (int)m2.x : 0, mb = m2.y > t_lo ? (int)m2.y : 0;
+            mv[(ya + 1) * W2 + xa + 1] = (uint8_t)ma;
+            if (two) mv[(yb + 1) * W2 + xb + 1] = (uint8_t)mb;
+        }
     }
     __syncthreads();
     TR_PHASE(1, 1)
