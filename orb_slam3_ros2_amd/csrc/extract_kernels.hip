@@ -1490,6 +1490,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
 // rBRIEF samples lie within +-18 px of the keypoint (max rotated pattern radius 18.38,
 // rounded): the blurred region is 37 x 37, computed from the 43 x 43 patch (+-3 blur halo).
 constexpr int kBlR = 18, kBlW = 2 * kBlR + 1;   // 37
+constexpr int kDpP = 48;                         // k_desc patch row pitch (12 dwords)
 // GaussianBlur(7x7, sigma 2) 8-bit fixed-point taps (the host checks its table equals these)
 __device__ __forceinline__ constexpr uint32_t blur_tap(int i) {
     return i == 0 || i == 6 ? 18u : (i == 1 || i == 5 ? 34u : (i == 2 || i == 4 ? 48u : 56u));
@@ -1500,7 +1501,9 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
                                               const int* __restrict__ lvl_nlap, const int* __restrict__ disc,
                                               orbhip_kp* __restrict__ out_kps, uint8_t* __restrict__ out_desc,
                                               int cap, int* __restrict__ n_out, int* __restrict__ mono_out, int xrun) {
-    __shared__ uint8_t patch[4][kPatchW * kPatchW + 15];
+    // patch rows of kDpP bytes: a pixel at byte sh + x of its row (sh = the patch origin's byte
+    // misalignment when the rows were copied as aligned dwords, 0 on the reflected border path)
+    __shared__ __attribute__((aligned(16))) uint8_t patch[4][kPatchW * kDpP + 16];
     __shared__ uint16_t hrow[4][kPatchW * kBlW];     // row pass: 43 rows x 37 columns
     __shared__ uint8_t blr[4][kBlW * kBlW + 7];       // blurred 37 x 37
     TR_BEGIN()
@@ -1527,10 +1530,8 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
     uint8_t* pt = patch[wid];
     uint16_t* hr = hrow[wid];
     uint8_t* bl = blr[wid];
-    int cx = 0, cy = 0;
+    int cx = 0, cy = 0, sh = 0;
     LevelKp kp{};
-    constexpr int kPU = (kPatchW * kPatchW + 63) / 64;   // 29 bytes per lane
-    constexpr float kInvPW = 1.0f / kPatchW;
     if (active) {
         const LevelGeom& G = P->lv[l];
         ImgRef im = level_img(P, fb, f, l);
@@ -1538,31 +1539,50 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
         cx = kp.x; cy = kp.y;
         const int lw = G.w, lh = G.h;
         const bool inside = cx - kPatchR >= 0 && cy - kPatchR >= 0 && cx + kPatchR < lw && cy + kPatchR < lh;
-        uint8_t v[kPU];
-        if (inside) {
+        const bool dw = inside && ((im.pitch & 3) == 0) && ((((uintptr_t)im.p) & 3) == 0);
+        if (dw) {
+            // 43 rows x 12 aligned dwords (the 43 + sh <= 46 patch bytes of a row), 9 per lane
             const uint8_t* src = im.p + (int64_t)(cy - kPatchR) * im.pitch + (cx - kPatchR);
+            sh = (int)(((uintptr_t)src) & 3);
+            const uint32_t* s4 = (const uint32_t*)(src - sh);
+            const int p4 = im.pitch >> 2;
+            constexpr int kND = kPatchW * (kDpP / 4), kDU = (kND + 63) / 64;
+            uint32_t v[kDU];
 #pragma unroll
-            for (int u = 0; u < kPU; u++) {
-                const int i = min(lane + 64 * u, kPatchW * kPatchW - 1);   // branch-free loads
-                const int py = (int)(((float)i + 0.5f) * kInvPW), px = i - py * kPatchW;
-                v[u] = src[(int64_t)py * im.pitch + px];
+            for (int u = 0; u < kDU; u++) {
+                const int i = min(lane + 64 * u, kND - 1);   // branch-free loads
+                const int r = (i * 43691) >> 19, k = i - 12 * r;   // i / 12 for i < 98304
+                v[u] = s4[(int64_t)r * p4 + k];
+            }
+            uint32_t* d4 = (uint32_t*)pt;
+#pragma unroll
+            for (int u = 0; u < kDU; u++) {
+                const int i = lane + 64 * u;
+                if (i < kND) d4[i] = v[u];
             }
         } else {
+            // reflected border: byte loads in rounds of 8 (few keypoints; bounded registers)
+            constexpr int kPU = (kPatchW * kPatchW + 63) / 64;   // 29 bytes per lane
+            constexpr float kInvPW = 1.0f / kPatchW;
+#pragma unroll 1
+            for (int u0 = 0; u0 < kPU; u0 += 8) {
+                uint8_t v[8];
+                int li[8];
 #pragma unroll
-            for (int u = 0; u < kPU; u++) {
-                const int i = min(lane + 64 * u, kPatchW * kPatchW - 1);
-                const int py = (int)(((float)i + 0.5f) * kInvPW), px = i - py * kPatchW;
-                int yy = cy - kPatchR + py, xx = cx - kPatchR + px;
-                // BORDER_REFLECT_101 (levels are >= 43 px in both dims)
-                yy = yy < 0 ? -yy : (yy >= lh ? 2 * lh - 2 - yy : yy);
-                xx = xx < 0 ? -xx : (xx >= lw ? 2 * lw - 2 - xx : xx);
-                v[u] = im.p[(int64_t)yy * im.pitch + xx];
+                for (int u = 0; u < 8; u++) {
+                    const int i = min(lane + 64 * (u0 + u), kPatchW * kPatchW - 1);
+                    const int py = (int)(((float)i + 0.5f) * kInvPW), px = i - py * kPatchW;
+                    int yy = cy - kPatchR + py, xx = cx - kPatchR + px;
+                    // BORDER_REFLECT_101 (levels are >= 43 px in both dims)
+                    yy = yy < 0 ? -yy : (yy >= lh ? 2 * lh - 2 - yy : yy);
+                    xx = xx < 0 ? -xx : (xx >= lw ? 2 * lw - 2 - xx : xx);
+                    v[u] = (u0 + u < kPU) ? im.p[(int64_t)yy * im.pitch + xx] : 0;
+                    li[u] = py * kDpP + px;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (u0 + u < kPU && lane + 64 * (u0 + u) < kPatchW * kPatchW) pt[li[u]] = v[u];
             }
-        }
-#pragma unroll
-        for (int u = 0; u < kPU; u++) {
-            const int i = lane + 64 * u;
-            if (i < kPatchW * kPatchW) pt[i] = v[u];
         }
     }
     __syncthreads();
@@ -1574,7 +1594,7 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
         for (int i = lane; i < P->n_disc; i += 64) {
             const int uv = disc[i];
             const int u = (int)(int16_t)(uv & 0xFFFF), vv = (int)(int16_t)(uv >> 16);
-            const int val = pt[(kPatchR + vv) * kPatchW + kPatchR + u];
+            const int val = pt[(kPatchR + vv) * kDpP + sh + kPatchR + u];
             m10 += u * val;
             m01 += vv * val;
         }
@@ -1582,19 +1602,24 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
         m01 = wave_sum_i32(m01);
         angle = fast_atan2((float)m01, (float)m10);
         // ---- 7x7 blur, row pass: hr[r][c] = sum_i k_i pt[r][c + i], r < 43, c < 37 ----
-        // lane task = 4 consecutive columns of one row (10 byte reads for 4 outputs)
+        // lane task = 4 consecutive columns of one row: 4 dword reads, realigned by sh, and two
+        // v_dot4_u32_u8 per output (taps 18 34 48 56 | 48 34 18 0 against bytes c..c+3 | c+4..c+7)
+        const uint32_t K0 = 18u | 34u << 8 | 48u << 16 | 56u << 24, K1 = 48u | 34u << 8 | 18u << 16;
+        const uint32_t* p4 = (const uint32_t*)pt;
+#pragma unroll 1
         for (int t = lane; t < kPatchW * 10; t += 64) {
-            const int r = (int)(((float)t + 0.5f) * 0.1f), c0 = 4 * (t - 10 * r);
-            const uint8_t* row = pt + r * kPatchW + c0;
-            uint32_t x[10];
-#pragma unroll
-            for (int i = 0; i < 10; i++) x[i] = c0 + i < kPatchW ? row[i] : 0u;
+            const int r = (t * 6554) >> 16, c0 = 4 * (t - 10 * r);   // t / 10 for t < 16384
+            const uint32_t* w = p4 + r * (kDpP / 4) + (c0 >> 2);
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+            const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, sh);   // pixels c0 .. c0+3
+            const uint32_t x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);   // c0+4 .. c0+7
+            const uint32_t x2 = __builtin_amdgcn_alignbyte(w3, w2, sh);   // c0+8 .. c0+11
 #pragma unroll
             for (int o = 0; o < 4; o++) {
                 if (c0 + o >= kBlW) break;
-                uint32_t h = 0;
-#pragma unroll
-                for (int i = 0; i < 7; i++) h += blur_tap(i) * x[o + i];
+                const uint32_t a = o == 0 ? x0 : __builtin_amdgcn_alignbyte(x1, x0, o);
+                const uint32_t bq = o == 0 ? x1 : __builtin_amdgcn_alignbyte(x2, x1, o);
+                const uint32_t h = __builtin_amdgcn_udot4(bq, K1, __builtin_amdgcn_udot4(a, K0, 0u, false), false);
                 hr[r * kBlW + c0 + o] = (uint16_t)h;
             }
         }
