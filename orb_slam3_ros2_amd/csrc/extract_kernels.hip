@@ -1491,6 +1491,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
 // rounded): the blurred region is 37 x 37, computed from the 43 x 43 patch (+-3 blur halo).
 constexpr int kBlR = 18, kBlW = 2 * kBlR + 1;   // 37
 constexpr int kDpP = 48;                         // k_desc patch row pitch (12 dwords)
+constexpr int kHrP = 48;                         // k_desc transposed row-pass pitch (rows 0..42, read to 45)
 // GaussianBlur(7x7, sigma 2) 8-bit fixed-point taps (the host checks its table equals these)
 __device__ __forceinline__ constexpr uint32_t blur_tap(int i) {
     return i == 0 || i == 6 ? 18u : (i == 1 || i == 5 ? 34u : (i == 2 || i == 4 ? 48u : 56u));
@@ -1504,8 +1505,8 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
     // patch rows of kDpP bytes: a pixel at byte sh + x of its row (sh = the patch origin's byte
     // misalignment when the rows were copied as aligned dwords, 0 on the reflected border path)
     __shared__ __attribute__((aligned(16))) uint8_t patch[4][kPatchW * kDpP + 16];
-    __shared__ uint16_t hrow[4][kPatchW * kBlW];     // row pass: 43 rows x 37 columns
-    __shared__ uint8_t blr[4][kBlW * kBlW + 7];       // blurred 37 x 37
+    // row pass output TRANSPOSED (column c at c * kHrP): the column pass reads row pairs as dwords
+    __shared__ __attribute__((aligned(16))) uint16_t hrow[4][kBlW * kHrP];
     TR_BEGIN()
     const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
     const int f = lg / X;
@@ -1529,7 +1530,8 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
     const bool active = l < L && slot < lvl_cnt[f * L + l];   // wave-uniform
     uint8_t* pt = patch[wid];
     uint16_t* hr = hrow[wid];
-    uint8_t* bl = blr[wid];
+    uint8_t* bl = patch[wid];   // blurred 37 x 37: the patch is dead once the row pass has run
+    static_assert(kBlW * kBlW <= kPatchW * kDpP, "blurred region fits the patch");
     int cx = 0, cy = 0, sh = 0;
     LevelKp kp{};
     if (active) {
@@ -1620,25 +1622,33 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
                 const uint32_t a = o == 0 ? x0 : __builtin_amdgcn_alignbyte(x1, x0, o);
                 const uint32_t bq = o == 0 ? x1 : __builtin_amdgcn_alignbyte(x2, x1, o);
                 const uint32_t h = __builtin_amdgcn_udot4(bq, K1, __builtin_amdgcn_udot4(a, K0, 0u, false), false);
-                hr[r * kBlW + c0 + o] = (uint16_t)h;
+                hr[(c0 + o) * kHrP + r] = (uint16_t)h;
             }
         }
     }
     __syncthreads();
     if (active) {
-        // ---- column pass: bl[r][c] = (sum_j k_j hr[r + j][c] + 2^15) >> 16, 4 rows per task ----
+        // ---- column pass: bl[r][c] = (sum_j k_j hr[r + j][c] + 2^15) >> 16, 4 rows per task:
+        // rows r0 .. r0+9 of column c as 5 dwords of row pairs, 4 v_dot2_u32_u16 per output
+        // (even outputs against taps (k0,k1)(k2,k3)(k4,k5)(k6,0), odd ones (0,k0)(k1,k2)(k3,k4)(k5,k6)) ----
+        const u16x2 E0 = {18, 34}, E1 = {48, 56}, E2 = {48, 34}, E3 = {18, 0};
+        const u16x2 O0 = {0, 18}, O1 = {34, 48}, O2 = {56, 48}, O3 = {34, 18};
+        auto d2 = [](uint32_t d, u16x2 k, uint32_t acc) {
+            return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, d), k, acc, false);
+        };
         for (int t = lane; t < kBlW * 10; t += 64) {
             const int rb = (int)(((float)t + 0.5f) * (1.0f / kBlW)), c = t - kBlW * rb, r0 = 4 * rb;
-            uint32_t y[10];
-#pragma unroll
-            for (int j = 0; j < 10; j++) y[j] = r0 + j < kPatchW ? hr[(r0 + j) * kBlW + c] : 0u;
+            const uint32_t* y2 = (const uint32_t*)(hr + c * kHrP + r0);
+            const uint32_t q0 = y2[0], q1 = y2[1], q2 = y2[2], q3 = y2[3], q4 = y2[4];
+            const uint32_t s0 = d2(q3, E3, d2(q2, E2, d2(q1, E1, d2(q0, E0, 0u))));
+            const uint32_t s1 = d2(q3, O3, d2(q2, O2, d2(q1, O1, d2(q0, O0, 0u))));
+            const uint32_t s2 = d2(q4, E3, d2(q3, E2, d2(q2, E1, d2(q1, E0, 0u))));
+            const uint32_t s3 = d2(q4, O3, d2(q3, O2, d2(q2, O1, d2(q1, O0, 0u))));
+            const uint32_t sv[4] = {s0, s1, s2, s3};
 #pragma unroll
             for (int o = 0; o < 4; o++) {
                 if (r0 + o >= kBlW) break;
-                uint32_t sacc = 0;
-#pragma unroll
-                for (int j = 0; j < 7; j++) sacc += blur_tap(j) * y[o + j];
-                bl[(r0 + o) * kBlW + c] = (uint8_t)((sacc + (1u << 15)) >> 16);
+                bl[(r0 + o) * kBlW + c] = (uint8_t)((sv[o] + (1u << 15)) >> 16);
             }
         }
     }
