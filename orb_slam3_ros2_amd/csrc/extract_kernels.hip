@@ -1708,9 +1708,11 @@ __global__ __launch_bounds__(256) void k_desc_kp(const ExtractPlan* __restrict__
                                                  const int* __restrict__ lvl_nlap, const int* __restrict__ disc,
                                                  orbhip_kp* __restrict__ out_kps, uint8_t* __restrict__ out_desc,
                                                  int cap, int* __restrict__ n_out, int* __restrict__ mono_out, int xrun) {
-    __shared__ uint8_t pt[kPatchW * kPatchW + 15];
-    __shared__ uint16_t hr[kPatchW * kBlW];
-    __shared__ uint8_t bl[kBlW * kBlW + 7];
+    // the k_desc layouts: patch rows of kDpP bytes offset by sh, row-pass sums transposed, the
+    // blurred region over the dead patch
+    __shared__ __attribute__((aligned(16))) uint8_t pt[kPatchW * kDpP + 16];
+    __shared__ __attribute__((aligned(16))) uint16_t hr[kBlW * kHrP];
+    uint8_t* const bl = pt;
     __shared__ int msum[2][4];
     TR_BEGIN()
     const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
@@ -1735,28 +1737,47 @@ __global__ __launch_bounds__(256) void k_desc_kp(const ExtractPlan* __restrict__
     const LevelGeom& G = P->lv[l];
     const LevelKp kp = lvl_kp[(int64_t)f * P->kp_slots_total + G.kp_base + slot];
     const int cx = kp.x, cy = kp.y;
+    int sh = 0;
     {
         ImgRef im = level_img(P, fb, f, l);
         const int lw = G.w, lh = G.h;
         const bool inside = cx - kPatchR >= 0 && cy - kPatchR >= 0 && cx + kPatchR < lw && cy + kPatchR < lh;
-        constexpr int kPU = (kPatchW * kPatchW + 255) / 256;   // 8 bytes per thread
-        constexpr float kInvPW = 1.0f / kPatchW;
-        uint8_t v[kPU];
+        if (inside && ((im.pitch & 3) == 0) && ((((uintptr_t)im.p) & 3) == 0)) {
+            // 43 rows x 12 aligned dwords, 3 per thread
+            const uint8_t* src = im.p + (int64_t)(cy - kPatchR) * im.pitch + (cx - kPatchR);
+            sh = (int)(((uintptr_t)src) & 3);
+            const uint32_t* s4 = (const uint32_t*)(src - sh);
+            const int p4 = im.pitch >> 2;
+            constexpr int kND = kPatchW * (kDpP / 4), kDU = (kND + 255) / 256;
+            uint32_t v[kDU];
 #pragma unroll
-        for (int u = 0; u < kPU; u++) {
-            const int i = min(tid + 256 * u, kPatchW * kPatchW - 1);   // branch-free loads
-            const int py = (int)(((float)i + 0.5f) * kInvPW), px = i - py * kPatchW;
-            int yy = cy - kPatchR + py, xx = cx - kPatchR + px;
-            if (!inside) {   // BORDER_REFLECT_101 (levels are >= 43 px in both dims)
+            for (int u = 0; u < kDU; u++) {
+                const int i = min(tid + 256 * u, kND - 1);
+                const int r = (i * 43691) >> 19, k = i - 12 * r;   // i / 12 for i < 98304
+                v[u] = s4[(int64_t)r * p4 + k];
+            }
+#pragma unroll
+            for (int u = 0; u < kDU; u++)
+                if (tid + 256 * u < kND) ((uint32_t*)pt)[tid + 256 * u] = v[u];
+        } else {
+            constexpr int kPU = (kPatchW * kPatchW + 255) / 256;   // 8 bytes per thread
+            constexpr float kInvPW = 1.0f / kPatchW;
+            uint8_t v[kPU];
+            int li[kPU];
+#pragma unroll
+            for (int u = 0; u < kPU; u++) {
+                const int i = min(tid + 256 * u, kPatchW * kPatchW - 1);   // branch-free loads
+                const int py = (int)(((float)i + 0.5f) * kInvPW), px = i - py * kPatchW;
+                int yy = cy - kPatchR + py, xx = cx - kPatchR + px;
+                // BORDER_REFLECT_101 (levels are >= 43 px in both dims)
                 yy = yy < 0 ? -yy : (yy >= lh ? 2 * lh - 2 - yy : yy);
                 xx = xx < 0 ? -xx : (xx >= lw ? 2 * lw - 2 - xx : xx);
+                v[u] = im.p[(int64_t)yy * im.pitch + xx];
+                li[u] = py * kDpP + px;
             }
-            v[u] = im.p[(int64_t)yy * im.pitch + xx];
-        }
 #pragma unroll
-        for (int u = 0; u < kPU; u++) {
-            const int i = tid + 256 * u;
-            if (i < kPatchW * kPatchW) pt[i] = v[u];
+            for (int u = 0; u < kPU; u++)
+                if (tid + 256 * u < kPatchW * kPatchW) pt[li[u]] = v[u];
         }
     }
     __syncthreads();
@@ -1767,43 +1788,55 @@ __global__ __launch_bounds__(256) void k_desc_kp(const ExtractPlan* __restrict__
         for (int i = tid; i < P->n_disc; i += 256) {
             const int uv = disc[i];
             const int u = (int)(int16_t)(uv & 0xFFFF), vv = (int)(int16_t)(uv >> 16);
-            const int val = pt[(kPatchR + vv) * kPatchW + kPatchR + u];
+            const int val = pt[(kPatchR + vv) * kDpP + sh + kPatchR + u];
             m10 += u * val;
             m01 += vv * val;
         }
         m10 = wave_sum_i32(m10);
         m01 = wave_sum_i32(m01);
         if (lane == 0) { msum[0][wid] = m10; msum[1][wid] = m01; }
+        // row pass as in k_desc: realigned dwords, two v_dot4_u32_u8 per output, stored transposed
+        const uint32_t K0 = 18u | 34u << 8 | 48u << 16 | 56u << 24, K1 = 48u | 34u << 8 | 18u << 16;
+        const uint32_t* p4 = (const uint32_t*)pt;
         for (int t = tid; t < kPatchW * 10; t += 256) {
-            const int r = (int)(((float)t + 0.5f) * 0.1f), c0 = 4 * (t - 10 * r);
-            const uint8_t* row = pt + r * kPatchW + c0;
-            uint32_t x[10];
-#pragma unroll
-            for (int i = 0; i < 10; i++) x[i] = c0 + i < kPatchW ? row[i] : 0u;
+            const int r = (t * 6554) >> 16, c0 = 4 * (t - 10 * r);   // t / 10 for t < 16384
+            const uint32_t* w = p4 + r * (kDpP / 4) + (c0 >> 2);
+            const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3];
+            const uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            const uint32_t x1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+            const uint32_t x2 = __builtin_amdgcn_alignbyte(w3, w2, sh);
 #pragma unroll
             for (int o = 0; o < 4; o++) {
                 if (c0 + o >= kBlW) break;
-                uint32_t h = 0;
-#pragma unroll
-                for (int i = 0; i < 7; i++) h += blur_tap(i) * x[o + i];
-                hr[r * kBlW + c0 + o] = (uint16_t)h;
+                const uint32_t aq = o == 0 ? x0 : __builtin_amdgcn_alignbyte(x1, x0, o);
+                const uint32_t bq = o == 0 ? x1 : __builtin_amdgcn_alignbyte(x2, x1, o);
+                const uint32_t h = __builtin_amdgcn_udot4(bq, K1, __builtin_amdgcn_udot4(aq, K0, 0u, false), false);
+                hr[(c0 + o) * kHrP + r] = (uint16_t)h;
             }
         }
     }
     __syncthreads();
-    // ---- column pass: bl[r][c] = (sum_j k_j hr[r + j][c] + 2^15) >> 16, 4 rows per task ----
-    for (int t = tid; t < kBlW * 10; t += 256) {
-        const int rb = (int)(((float)t + 0.5f) * (1.0f / kBlW)), c = t - kBlW * rb, r0 = 4 * rb;
-        uint32_t y[10];
+    // ---- column pass: bl[r][c] = (sum_j k_j hr[r + j][c] + 2^15) >> 16, 4 rows per task, as
+    // in k_desc (row pairs as dwords, 4 v_dot2_u32_u16 per output) ----
+    {
+        const u16x2 E0 = {18, 34}, E1 = {48, 56}, E2 = {48, 34}, E3 = {18, 0};
+        const u16x2 O0 = {0, 18}, O1 = {34, 48}, O2 = {56, 48}, O3 = {34, 18};
+        auto d2 = [](uint32_t d, u16x2 k, uint32_t acc) {
+            return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, d), k, acc, false);
+        };
+        for (int t = tid; t < kBlW * 10; t += 256) {
+            const int rb = (int)(((float)t + 0.5f) * (1.0f / kBlW)), c = t - kBlW * rb, r0 = 4 * rb;
+            const uint32_t* y2 = (const uint32_t*)(hr + c * kHrP + r0);
+            const uint32_t q0 = y2[0], q1 = y2[1], q2 = y2[2], q3 = y2[3], q4 = y2[4];
+            const uint32_t sv[4] = {d2(q3, E3, d2(q2, E2, d2(q1, E1, d2(q0, E0, 0u)))),
+                                    d2(q3, O3, d2(q2, O2, d2(q1, O1, d2(q0, O0, 0u)))),
+                                    d2(q4, E3, d2(q3, E2, d2(q2, E1, d2(q1, E0, 0u)))),
+                                    d2(q4, O3, d2(q3, O2, d2(q2, O1, d2(q1, O0, 0u))))};
 #pragma unroll
-        for (int j = 0; j < 10; j++) y[j] = r0 + j < kPatchW ? hr[(r0 + j) * kBlW + c] : 0u;
-#pragma unroll
-        for (int o = 0; o < 4; o++) {
-            if (r0 + o >= kBlW) break;
-            uint32_t sacc = 0;
-#pragma unroll
-            for (int j = 0; j < 7; j++) sacc += blur_tap(j) * y[o + j];
-            bl[(r0 + o) * kBlW + c] = (uint8_t)((sacc + (1u << 15)) >> 16);
+            for (int o = 0; o < 4; o++) {
+                if (r0 + o >= kBlW) break;
+                bl[(r0 + o) * kBlW + c] = (uint8_t)((sv[o] + (1u << 15)) >> 16);
+            }
         }
     }
     __syncthreads();
