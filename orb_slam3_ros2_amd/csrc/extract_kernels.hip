@@ -228,10 +228,14 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
     const ConeRect* R = rects + (size_t)tile * kMaxLevels;
     int boff[kMaxLevels], toff[kMaxLevels];
     int tot = 0;
+    // level 0 is staged as aligned dwords: rows of P0 = round_up(width + 3, 4) bytes, the region
+    // starting at byte sh0 of its row (sh0: the frame address misalignment, 0 on the byte path)
+    const int P0 = (R[0].nx1 - R[0].nx0 + 6) & ~3;
     for (int l = 0; l < L; l++) {
         boff[l] = tot;
-        tot += ((R[l].nx1 - R[l].nx0) * (R[l].ny1 - R[l].ny0) + 15) & ~15;
+        tot += ((l == 0 ? P0 : (R[l].nx1 - R[l].nx0)) * (R[l].ny1 - R[l].ny0) + 15) & ~15;
     }
+    int sh0 = 0;
     int* tab = (int*)(cone + tot);
     int ttot = 0;
     for (int l = 1; l < L; l++) {
@@ -244,32 +248,40 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
         const ImgRef in0 = level_img(P, fb, f, 0);
         const ConeRect r = R[0];
         const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0;
-        const int tot0 = nw * nh;
-        const float inv_nw = 1.0f / (float)nw;
         const uint8_t* src0 = in0.p + (int64_t)r.ny0 * in0.pitch + r.nx0;
         const int* gt = ctab + (size_t)tile * tab_stride;
-        if (tot0 <= 4 * 1024 && ttot <= 2 * 1024 && nt == 1024) {
-            uint8_t v[4];
+        const bool dw = ((in0.pitch & 3) == 0) && ((((uintptr_t)in0.p) & 3) == 0);
+        if (dw) sh0 = (int)(((uintptr_t)src0) & 3);
+        const int nwd = dw ? (nw + sh0 + 3) >> 2 : 0;   // dwords per row (<= P0 / 4)
+        const int tot0 = dw ? nwd * nh : nw * nh;
+        const float inv_n = 1.0f / (float)(dw ? nwd : nw);
+        uint8_t* lv0 = cone + boff[0];
+        if (dw && tot0 <= 1024 && ttot <= 2 * 1024 && nt == 1024) {
+            const uint32_t* s4 = (const uint32_t*)(src0 - sh0);
+            const int p4 = in0.pitch >> 2;
             int tv[2];
 #pragma unroll
             for (int u = 0; u < 2; u++) tv[u] = gt[min(tid + 1024 * u, ttot - 1)];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int i = min(tid + 1024 * u, tot0 - 1);
-                const int y = small_div(i, inv_nw), x = i - y * nw;
-                v[u] = src0[(int64_t)y * in0.pitch + x];
-            }
+            const int i = min(tid, tot0 - 1);
+            const int y = small_div(i, inv_n), x = i - y * nwd;
+            const uint32_t v = s4[(int64_t)y * p4 + x];
 #pragma unroll
             for (int u = 0; u < 2; u++)
                 if (tid + 1024 * u < ttot) tab[tid + 1024 * u] = tv[u];
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                if (tid + 1024 * u < tot0) cone[boff[0] + tid + 1024 * u] = v[u];
+            if (tid < tot0) ((uint32_t*)lv0)[y * (P0 >> 2) + x] = v;
+        } else if (dw) {
+            const uint32_t* s4 = (const uint32_t*)(src0 - sh0);
+            const int p4 = in0.pitch >> 2;
+            for (int i = tid; i < ttot; i += nt) tab[i] = gt[i];
+            for (int i = tid; i < tot0; i += nt) {
+                const int y = small_div(i, inv_n), x = i - y * nwd;
+                ((uint32_t*)lv0)[y * (P0 >> 2) + x] = s4[(int64_t)y * p4 + x];
+            }
         } else {
             for (int i = tid; i < ttot; i += nt) tab[i] = gt[i];
             for (int i = tid; i < tot0; i += nt) {
-                const int y = small_div(i, inv_nw), x = i - y * nw;
-                cone[boff[0] + i] = src0[(int64_t)y * in0.pitch + x];
+                const int y = small_div(i, inv_n), x = i - y * nw;
+                lv0[y * P0 + x] = src0[(int64_t)y * in0.pitch + x];
             }
         }
     }
@@ -278,9 +290,9 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
     for (int l = 1; l < L; l++) {
         const LevelGeom& D = P->lv[l];
         const ConeRect r = R[l], rp = R[l - 1];
-        const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0, nwp = rp.nx1 - rp.nx0;
+        const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0, nwp = l == 1 ? P0 : rp.nx1 - rp.nx0;
         const int* t = tab + toff[l];
-        const uint8_t* src = cone + boff[l - 1];
+        const uint8_t* src = cone + boff[l - 1] + (l == 1 ? sh0 : 0);
         uint8_t* dst = fb.pyr + (int64_t)f * P->pyr_bytes + D.pyr_off;
         const float inv_nw = 1.0f / (float)nw;
         for (int i = tid; i < nw * nh; i += nt) {

@@ -429,8 +429,10 @@ static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& ou
                     R[0] = ConeRect{(int16_t)lo, (int16_t)(hi + 1), (int16_t)r0, (int16_t)(r1 + 1), 0, 0, 0, 0};
                 }
                 size_t tot = 0, ttot = 0;
-                for (int l = 0; l < L; l++)
-                    tot += ((size_t)(R[l].nx1 - R[l].nx0) * (R[l].ny1 - R[l].ny0) + 15) & ~size_t(15);
+                for (int l = 0; l < L; l++) {   // level 0: rows of round_up(width + 3, 4) (k_pyr_cone dword staging)
+                    const size_t wl = l == 0 ? (size_t)((R[0].nx1 - R[0].nx0 + 6) & ~3) : (size_t)(R[l].nx1 - R[l].nx0);
+                    tot += (wl * (R[l].ny1 - R[l].ny0) + 15) & ~size_t(15);
+                }
                 for (int l = 1; l < L; l++)
                     ttot += 4 * (2 * (size_t)(R[l].nx1 - R[l].nx0) + 3 * (size_t)(R[l].ny1 - R[l].ny0));
                 tot += ttot;
