@@ -295,6 +295,7 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
         const uint8_t* src = cone + boff[l - 1] + (l == 1 ? sh0 : 0);
         uint8_t* dst = fb.pyr + (int64_t)f * P->pyr_bytes + D.pyr_off;
         const float inv_nw = 1.0f / (float)nw;
+        const bool noclamp = D.rz_noclamp != 0;
         for (int i = tid; i < nw * nh; i += nt) {
             const int yy = small_div(i, inv_nw), xx = i - yy * nw;
             const int x = r.nx0 + xx, y = r.ny0 + yy;
@@ -314,7 +315,9 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
             const int bb = t[2 * nw + 3 * yy + 2];
             const int b0 = (int)(short)(bb & 0xFFFF), b1 = (int)(short)(bb >> 16);
             int v;
-            if (x < D.vend) {   // VResizeLinearVec_32s8u lanes (128-bit baseline)
+            if (x < D.vend && noclamp) {   // as below; taps checked on the host (k_resize notes)
+                v = ((__mul24(h0 >> 4, b0) >> 16) + (__mul24(h1 >> 4, b1) >> 16) + 2) >> 2;
+            } else if (x < D.vend) {   // VResizeLinearVec_32s8u lanes (128-bit baseline)
                 int s0 = min(max(h0 >> 4, -32768), 32767);
                 int s1 = min(max(h1 >> 4, -32768), 32767);
                 int tt = ((s0 * b0) >> 16) + ((s1 * b1) >> 16);
