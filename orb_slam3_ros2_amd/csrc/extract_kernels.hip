@@ -1733,6 +1733,12 @@ __global__ __launch_bounds__(256) void k_desc_kp(const ExtractPlan* __restrict__
     const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
     const int f = lg / X;
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
+    // the IC_Angle disc offsets (n_disc <= 31 x 31 < 4 x 256), loaded first so that they arrive
+    // with the keypoint and the patch; entries past n_disc are (0, 0) and add nothing
+    constexpr int kDiscU = 4;
+    int dv[kDiscU];
+#pragma unroll
+    for (int u = 0; u < kDiscU; u++) dv[u] = tid + 256 * u < P->n_disc ? disc[tid + 256 * u] : 0;
     int slot = lg % X;
     const int L = P->n_levels;
     int total = 0, nlap_tot = 0;
@@ -1800,8 +1806,9 @@ __global__ __launch_bounds__(256) void k_desc_kp(const ExtractPlan* __restrict__
     // ---- IC_Angle partial moments over the umax disc (unblurred level) + blur row pass ----
     {
         int m10 = 0, m01 = 0;
-        for (int i = tid; i < P->n_disc; i += 256) {
-            const int uv = disc[i];
+#pragma unroll
+        for (int q = 0; q < kDiscU; q++) {
+            const int uv = dv[q];
             const int u = (int)(int16_t)(uv & 0xFFFF), vv = (int)(int16_t)(uv >> 16);
             const int val = pt[(kPatchR + vv) * kDpP + sh + kPatchR + u];
             m10 += u * val;

@@ -482,7 +482,7 @@ static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& ou
         const int d = c->umax[std::abs(v)];
         for (int u = -d; u <= d; u++) pl->disc.push_back((int)(uint16_t)(int16_t)u | ((int)(int16_t)v << 16));
     }
-    P.n_disc = (int)pl->disc.size();
+    P.n_disc = (int)pl->disc.size();   // <= 31 x 31 (k_desc_kp holds 4 entries per thread)
     // octree LDS configuration
     int max_kp_cap = 0;
     for (int l = 0; l < L; l++) max_kp_cap = std::max(max_kp_cap, P.lv[l].kp_cap);
