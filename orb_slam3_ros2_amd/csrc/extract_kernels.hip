@@ -1947,8 +1947,12 @@ void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* c
     const bool compact = hP.fast_win_rows <= 56 && hP.fast_win_cols + 3 <= 64;   // window dwords (sh <= 3) fit a row
 #define ORBHIP_FAST_LAUNCH(NTV, WRV) \
     hipLaunchKernelGGL((k_fast_cells<NTV, WRV>), grd, dim3(NTV), 0, st, dP, cells, fb, cand, cand_cnt, err, xr)
-    if (nt == 1024)
+    if (nt == 1024 && compact)
+        ORBHIP_FAST_LAUNCH(1024, 56);
+    else if (nt == 1024)
         ORBHIP_FAST_LAUNCH(1024, kWinMax);
+    else if (nt == 512 && compact)
+        ORBHIP_FAST_LAUNCH(512, 56);
     else if (nt == 512)
         ORBHIP_FAST_LAUNCH(512, kWinMax);
     else if (nt == 128 && compact)
