@@ -370,30 +370,38 @@ __device__ __forceinline__ void chol_reg_solve(const double* __restrict__ S, con
     // ---- backward: x_{T-1} = Linv^T y_{T-1}; then per k: y_J -= L_kJ^T x_k (J < k), and the
     // owner of (k, k-1) (its update of y_{k-1} is the last one) finishes x_{k-1} ----
     if (wid == (T - 1) % kRegWaves) apply_linv_t(Linv + (size_t)(T - 1) * 256, y + 16 * (T - 1));
+    // the (I, J) of every slot, walked once (wave-uniform: scalar registers), so that a backward
+    // step tests each slot with one compare instead of re-walking the column-major order
+    int rIJ[MAXT];   // I | J << 8 (I = 255: no tile)
+    {
+        int I = I0, J = J0;
+#pragma unroll
+        for (int t = 0; t < MAXT; t++) {
+            rIJ[t] = (t < nslots ? I : 255) | J << 8;
+            I += kRegWaves;
+            while (I >= T && J < T - 1) { I = I - T + J + 2; J++; }
+        }
+    }
     __syncthreads();
     for (int k = T - 1; k >= 1; k--) {
         const double xk = y[16 * k + cc];
         bool own = false;
-        // tiles (k, J), J < k: walk this wave's slots with (I, J) in scalar registers
-        {
-            int I = I0, J = J0;
-            run_slots<MAXT>(0, nslots, [&](auto tc) {
-                constexpr int t = decltype(tc)::value;
-                if (I == k) {
-                    // lane holds L_kJ[cc][rg + 4q]: (L_kJ^T x_k)[rg + 4q] = sum over cc
-                    double sq[4];
+        // tiles (k, J), J < k
+        run_slots<MAXT>(0, nslots, [&](auto tc) {
+            constexpr int t = decltype(tc)::value;
+            if ((rIJ[t] & 0xFF) == k) {
+                const int J = rIJ[t] >> 8;
+                // lane holds L_kJ[cc][rg + 4q]: (L_kJ^T x_k)[rg + 4q] = sum over cc
+                double sq[4];
 #pragma unroll
-                    for (int q = 0; q < 4; q++) sq[q] = row16_sum(acc[t][q] * xk);
-                    if (cc == 0) {
+                for (int q = 0; q < 4; q++) sq[q] = row16_sum(acc[t][q] * xk);
+                if (cc == 0) {
 #pragma unroll
-                        for (int q = 0; q < 4; q++) y[16 * J + rg + 4 * q] -= sq[q];
-                    }
-                    own |= (J == k - 1);
+                    for (int q = 0; q < 4; q++) y[16 * J + rg + 4 * q] -= sq[q];
                 }
-                I += kRegWaves;
-                while (I >= T && J < T - 1) { I = I - T + J + 2; J++; }
-            });
-        }
+                own |= (J == k - 1);
+            }
+        });
         if (own) {
             wave_lds_sync();
             apply_linv_t(Linv + (size_t)(k - 1) * 256, y + 16 * (k - 1));
