@@ -309,6 +309,19 @@ __device__ __forceinline__ void chol_reg_solve(const double* __restrict__ S, con
         if (rg == 0) y[16 * I + cc] -= sv;
     };
 
+    // the (I, J) of every slot, walked once (wave-uniform: scalar registers), so that the trailing
+    // updates and the backward steps read a slot's tile coordinates instead of re-walking the
+    // column-major order
+    int rIJ[MAXT];   // I | J << 8 (I = 255: no tile)
+    {
+        int I = I0, J = J0;
+#pragma unroll
+        for (int t = 0; t < MAXT; t++) {
+            rIJ[t] = (t < nslots ? I : 255) | J << 8;
+            I += kRegWaves;
+            while (I >= T && J < T - 1) { I = I - T + J + 2; J++; }
+        }
+    }
     // step k = -1 .. T-2: [panel k] barrier [diag k+1 | diagonal-tile and y updates | trailing k]
     // barrier. The look-ahead wave (k+1) % 8 finishes tile (k+1, k+1) and factors it first.
     for (int k = -1; k < T - 1; k++) {
@@ -354,14 +367,9 @@ __device__ __forceinline__ void chol_reg_solve(const double* __restrict__ S, con
             }
             // slots of columns > k: a suffix of this wave's slots, walked from its first tile
             const int tb = slot_at(off(k + 1));
-            int J = k + 1;
-            const int gb = wid + kRegWaves * tb;
-            while (J < T - 1 && gb >= off(J + 1)) J++;
-            int I = J + 1 + (gb - off(J));
             run_slots<MAXT>(tb, nslots, [&](auto tc) {
-                tile_update(acc[decltype(tc)::value], I, J);
-                I += kRegWaves;
-                while (I >= T && J < T - 1) { I = I - T + J + 2; J++; }
+                constexpr int t = decltype(tc)::value;
+                tile_update(acc[t], rIJ[t] & 0xFF, rIJ[t] >> 8);
             });
         }
         __syncthreads();
@@ -370,18 +378,6 @@ __device__ __forceinline__ void chol_reg_solve(const double* __restrict__ S, con
     // ---- backward: x_{T-1} = Linv^T y_{T-1}; then per k: y_J -= L_kJ^T x_k (J < k), and the
     // owner of (k, k-1) (its update of y_{k-1} is the last one) finishes x_{k-1} ----
     if (wid == (T - 1) % kRegWaves) apply_linv_t(Linv + (size_t)(T - 1) * 256, y + 16 * (T - 1));
-    // the (I, J) of every slot, walked once (wave-uniform: scalar registers), so that a backward
-    // step tests each slot with one compare instead of re-walking the column-major order
-    int rIJ[MAXT];   // I | J << 8 (I = 255: no tile)
-    {
-        int I = I0, J = J0;
-#pragma unroll
-        for (int t = 0; t < MAXT; t++) {
-            rIJ[t] = (t < nslots ? I : 255) | J << 8;
-            I += kRegWaves;
-            while (I >= T && J < T - 1) { I = I - T + J + 2; J++; }
-        }
-    }
     __syncthreads();
     for (int k = T - 1; k >= 1; k--) {
         const double xk = y[16 * k + cc];
