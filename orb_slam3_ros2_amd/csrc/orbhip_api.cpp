@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -18,6 +19,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <tuple>
 #include <vector>
 
 #include "../../include/orbhip.h"
@@ -93,7 +95,7 @@ struct orbhip_ctx {
     std::vector<float> scale, inv_scale;
     std::vector<int> feat, umax;
     int blurk[7] = {0};
-    std::map<std::pair<int, int>, std::shared_ptr<Plan>> plans;   // shared with other contexts (plan_cache)
+    std::map<std::tuple<int, int, int>, std::shared_ptr<Plan>> plans;   // (w, h, cone tile); shared with other contexts (plan_cache)
     // per-batch scratch (grown on demand)
     DevBuf<uint8_t> d_in, d_pyr;
     DevBuf<uint32_t> d_cand, d_kscratch;
@@ -191,15 +193,24 @@ static std::map<PlanKey, std::weak_ptr<Plan>>& plan_cache() {
 }
 static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& out);
 
+// k_pyr_cone tile edge of a plan: ORBHIP_CONE_TILE (read per plan lookup, A/B and tests), else
+// the context's choice, else 10 (the one-frame latency optimum)
+static int cone_tile_of(const orbhip_ctx* c) {
+    const char* e = std::getenv("ORBHIP_CONE_TILE");
+    const int ts_env = e ? std::atoi(e) : 0;
+    return ts_env > 0 ? ts_env : (c->cone_tile > 0 ? c->cone_tile : 10);
+}
+
 static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
-    auto key = std::make_pair(w, h);
+    const int ts = cone_tile_of(c);
+    auto key = std::make_tuple(w, h, ts);
     auto it = c->plans.find(key);
     if (it != c->plans.end()) { *out = it->second.get(); return ORBHIP_OK; }
     PlanKey k;
     std::memset(&k, 0, sizeof(k));
     k.device = c->device; k.w = w; k.h = h; k.nfeat = c->prm.n_features; k.nlev = c->prm.n_levels;
     k.ini = c->prm.ini_th_fast; k.mn = c->prm.min_th_fast; k.scale = c->prm.scale_factor;
-    k.cone_tile = c->cone_tile;
+    k.cone_tile = ts;
     const char* cap_env = getenv("ORBHIP_FAST_CLIST_CAP");
     k.clist_cap = cap_env ? atoi(cap_env) : -1;
     const char* nt_env = getenv("ORBHIP_FAST_NT");
@@ -391,8 +402,7 @@ static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& ou
     // is latency bound, so smaller cones finish sooner), an even partition of every level
     if (L > 1) {
         const LevelGeom& T = P.lv[L - 1];
-        static const int ts_env = std::getenv("ORBHIP_CONE_TILE") ? std::atoi(std::getenv("ORBHIP_CONE_TILE")) : 0;
-        const int ts = ts_env > 0 ? ts_env : (c->cone_tile > 0 ? c->cone_tile : 10);
+        const int ts = cone_tile_of(c);
         const int ntx = (T.w + ts - 1) / ts, nty = (T.h + ts - 1) / ts;
         size_t lds_max = 0;
         std::vector<ConeRect> rects((size_t)ntx * nty * kMaxLevels);
@@ -1395,7 +1405,16 @@ int orbhip_test_cells(orbhip_ctx* c, int w, int h, int32_t* out6, int cap) {
 // bench) and one event that also marks the frame complete. Same kernels and results as the
 // one-frame calls; the host work per frame is one C call instead of the caller's bookkeeping.
 // ===========================================================================
-constexpr int kFrontendConeTile = 14;
+// Cone tile of the front-end's frames by the number of live front-ends (camera streams) in the
+// process: one stream is latency-bound (10-pixel tiles, 252 work-groups at 640x480: 15.7k
+// frames/s one frame at a time against 15.0k at 14), many streams share the chip and want less
+// halo recompute per frame (16 cameras: 39.6k frames/s at 16-pixel tiles against 38.3k at 14;
+// tools/gpu_cone_tile.sh). Both tilings give the same pyramid (every tile writes what it owns).
+static std::atomic<int> g_live_frontends{0};
+static int frontend_cone_tile() {
+    const int n = g_live_frontends.load(std::memory_order_relaxed);
+    return n >= 8 ? 16 : (n >= 2 ? 14 : 10);
+}
 
 struct orbhip_frontend {
     int device = 0, w = 0, h = 0, S = 0, ns = 0, cap = 0;
@@ -1412,6 +1431,7 @@ struct orbhip_frontend {
     // frames up to done_upto), not per push (an event per frame costs ~3% of the 16-camera rate)
     hipEvent_t ev_done = nullptr;
     int64_t done_upto = -1;
+    bool live = false;   // counted in g_live_frontends
 };
 
 static void frontend_free(orbhip_frontend* f) {
@@ -1431,6 +1451,7 @@ static void frontend_free(orbhip_frontend* f) {
     if (f->nm) (void)hipFree(f->nm);
     for (orbhip_ctx* c : f->ctx)
         if (c) (void)orbhip_destroy(c);
+    if (f->live) g_live_frontends.fetch_sub(1, std::memory_order_relaxed);
     delete f;
 }
 
@@ -1448,10 +1469,10 @@ int orbhip_frontend_create(orbhip_frontend** out, int device, const orbhip_orb_p
     f->ctx.assign(f->S, nullptr);
     for (int j = 0; j < f->S; j++) {
         if (int rc = orbhip_create(&f->ctx[j], device, params)) return rc;
-        // throughput plan: 14-pixel cone tiles (130 instead of 252 work-groups at 640x480) leave
-        // room for more frames on the chip at once, for ~4% more one-frame latency
-        f->ctx[j]->cone_tile = kFrontendConeTile;
+        f->ctx[j]->cone_tile = 10;   // set per push (frontend_cone_tile)
     }
+    g_live_frontends.fetch_add(1, std::memory_order_relaxed);
+    f->live = true;
     const int cap = orbhip_max_keypoints(f->ctx[0], w, h);
     if (cap <= 0) return cap < 0 ? cap : ORBHIP_ERR_UNSUPPORTED;
     f->cap = cap;
@@ -1488,6 +1509,7 @@ int orbhip_frontend_push(orbhip_frontend* f, const uint8_t* d_img, int stride, i
     const int S = f->S, ns = f->ns, cap = f->cap;
     const int j = (int)(k % S), cur = (int)(k % ns), prev = (int)((k + ns - 1) % ns);
     orbhip_ctx* c = f->ctx[j];
+    c->cone_tile = frontend_cone_tile();
     hipStream_t st = c->stream;
     // slot `cur` was last read as `prev` by the match of frame k - ns + 1 (on another stream when
     // S > 1); its reader as `cur`, frame k - ns, ran on this stream

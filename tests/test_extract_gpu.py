@@ -54,6 +54,17 @@ def test_resize_cascade_bit_exact(oracle, monkeypatch, w, h, scale, nlev, seed):
     _check(ext, oracle, synthetic_frame(seed, w, h), scale=scale, nlevels=nlev)
 
 
+@pytest.mark.parametrize("tile", [12, 14, 16, 20])
+def test_cone_tiles_bit_exact(oracle, monkeypatch, tile):
+    """k_pyr_cone at the tile edges the front-end picks by camera count (10 / 14 / 16) and
+    others (ORBHIP_CONE_TILE, read per plan lookup): every tiling writes the same pyramid."""
+    from orb_slam3_ros2_amd import ORBextractor
+    monkeypatch.setenv("ORBHIP_CONE_TILE", str(tile))
+    ext = ORBextractor(1000, 1.2, 8, 20, 7)
+    _check(ext, oracle, synthetic_frame(40 + tile, 640, 480))
+    _check(ext, oracle, synthetic_frame(41 + tile, 752, 480))
+
+
 def test_milkv_1250_features(oracle):
     """R:config/Monocular/MilkV.yaml:42-55 (1250 features) at its 640x360 camera size."""
     from orb_slam3_ros2_amd import ORBextractor
