@@ -1934,14 +1934,16 @@ void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameB
 }
 
 void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,
-                 uint32_t* cand, int* cand_cnt, int* err, hipStream_t st) {
+                 uint32_t* cand, int* cand_cnt, int* err, hipStream_t st, int nt_hint) {
     // more threads per cell while the cells alone cannot fill the chip (one frame: ~600 cells on
     // 256 CUs), as many as keep every work-group resident at once (8192 wave slots); 256 once
     // the batch fills the chip; 128 for big batches (C3: 127k cells), where fewer waves per cell
     // idle less at the phase barriers and the compact LDS variant keeps 16 work-groups per CU
     const int ncell = B * hP.n_cells_total;
+    // (ORBHIP_FAST_NT pins it per plan; a caller's hint, e.g. the front-end with many cameras, next)
     const int nt = hP.fast_nt ? hP.fast_nt
-                              : (ncell <= 512 ? 1024 : (ncell <= 1024 ? 512 : (ncell <= 32768 ? 256 : 128)));
+                              : (nt_hint ? nt_hint
+                                         : (ncell <= 512 ? 1024 : (ncell <= 1024 ? 512 : (ncell <= 32768 ? 256 : 128))));
     dim3 grd(hP.n_cells_total, B, 1);
     const int xr = xcd_run_for(B);
     const bool compact = hP.fast_win_rows <= 56 && hP.fast_win_cols + 3 <= 64;   // window dwords (sh <= 3) fit a row

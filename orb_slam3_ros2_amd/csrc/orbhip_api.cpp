@@ -119,6 +119,7 @@ struct orbhip_ctx {
     StageTimer timer;
     GraphCache graphs;   // replays of repeated per-frame launch sequences (graph_cache.h)
     int cone_tile = 0;   // k_pyr_cone tile edge in last-level pixels (0: 10, the one-frame latency optimum)
+    int fast_nt = 0;     // k_fast_cells threads per cell hint (0: by batch size; 128/256/512/1024)
 };
 
 // ---------------------------------------------------------------------------
@@ -565,7 +566,7 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
     // pyramid engine, also per call: ORBHIP_NO_CONE=1 forces the k_resize cascade
     const bool no_cone = std::getenv("ORBHIP_NO_CONE") != nullptr;
     GraphKey key;
-    key.add(1).add((uint64_t)oct_fast).add((uint64_t)oct_max_dh).add((uint64_t)no_cone).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
+    key.add(1).add((uint64_t)oct_fast).add((uint64_t)oct_max_dh).add((uint64_t)no_cone).add((uint64_t)c->fast_nt).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
         .add((uint64_t)lap1).ptr(d_kps).ptr(d_desc).add((uint64_t)cap).ptr(d_n).ptr(d_mono).ptr(st).ptr(c->d_pyr.p)
         .ptr(c->d_cand.p).ptr(c->d_kscratch.p).ptr(c->d_nscratch.p).ptr(c->d_cand_cnt.p).ptr(c->d_lvl_kp.p)
         .ptr(c->d_lvl_cnt.p).ptr(c->d_lvl_nlap.p).ptr(c->d_err.p);
@@ -589,7 +590,7 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
                               st);
         tm.end(1, st);
         tm.begin(2, st);
-        launch_fast(pl->d_plan.p, P, pl->d_cells.p, fb, B, c->d_cand.p, c->d_cand_cnt.p, c->d_err.p, st);
+        launch_fast(pl->d_plan.p, P, pl->d_cells.p, fb, B, c->d_cand.p, c->d_cand_cnt.p, c->d_err.p, st, c->fast_nt);
         tm.end(2, st);
         OctreeCfg oc = pl->oct;
         oc.lap0 = lap0; oc.lap1 = lap1;
@@ -1415,6 +1416,12 @@ static int frontend_cone_tile() {
     const int n = g_live_frontends.load(std::memory_order_relaxed);
     return n >= 8 ? 16 : (n >= 2 ? 14 : 10);
 }
+// FAST threads per cell the same way: one camera keeps the one-frame rule (512 at 640x480, 15.8k
+// frames/s against 15.4k at 256); 8+ cameras take 256 (16 cameras: 40.5k against 39.6k at 512,
+// 35.6k at 1024; tools/gpu_c2_fastnt.sh)
+static int frontend_fast_nt() {
+    return g_live_frontends.load(std::memory_order_relaxed) >= 8 ? 256 : 0;
+}
 
 struct orbhip_frontend {
     int device = 0, w = 0, h = 0, S = 0, ns = 0, cap = 0;
@@ -1510,6 +1517,7 @@ int orbhip_frontend_push(orbhip_frontend* f, const uint8_t* d_img, int stride, i
     const int j = (int)(k % S), cur = (int)(k % ns), prev = (int)((k + ns - 1) % ns);
     orbhip_ctx* c = f->ctx[j];
     c->cone_tile = frontend_cone_tile();
+    c->fast_nt = frontend_fast_nt();
     hipStream_t st = c->stream;
     // slot `cur` was last read as `prev` by the match of frame k - ns + 1 (on another stream when
     // S > 1); its reader as `cur`, frame k - ns, ran on this stream

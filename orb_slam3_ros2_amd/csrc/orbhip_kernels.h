@@ -42,7 +42,7 @@ void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameB
 void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, int B, int l,
                    const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st);
 void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,
-                 uint32_t* cand, int* cand_cnt, int* err, hipStream_t st);
+                 uint32_t* cand, int* cand_cnt, int* err, hipStream_t st, int nt_hint = 0);
 size_t octree_lds_bytes(const ExtractPlan& hP, const OctreeCfg& cfg);
 bool octree_set_lds_limit(size_t bytes);
 void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const uint16_t* otab,
