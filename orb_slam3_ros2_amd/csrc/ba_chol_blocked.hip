@@ -13,9 +13,9 @@
 //                region during the factorization, while the panel column itself is still read
 //                by the other work-groups) and applies x_r -= L21[r] y_p to its rows. The
 //                work-group of tile (0, 0) then factors the next diagonal block.
-//   k_cb_back    backward substitution, one 1024-thread workgroup, x in LDS: per panel the 32x32
-//                factor tiles below it (its envelope, read from the upper triangle), loaded one
-//                panel ahead into registers
+//   k_cb_back_last / k_cb_back_step  backward substitution by super-blocks of 8 panels: the
+//                tiles left of each diagonal super-block applied by one workgroup per panel, the
+//                diagonal super-block solved by the last of them (details at cb_back_block)
 // Structure: row_first[R] = first 32-column tile with a structural non-zero in 32-row tile R of
 // S. The envelope (profile) of a symmetric matrix is preserved by its Cholesky factor, so every
 // tile left of row_first stays zero: the update and solve kernels skip it. A banded or
@@ -30,6 +30,7 @@
 #include "ba_chol.h"
 #include "ba_args.h"
 #include "ba_chol_blocked.h"
+#include "ba_diag16.h"
 #include "wave_f64.h"
 
 namespace orbhip {
@@ -37,14 +38,24 @@ namespace orbhip {
 constexpr int kCT = 32;    // panel width / structure tile
 constexpr int kUT = 64;    // trailing-update tile
 
-// factor the diagonal block at k0 (one wave) and apply the forward step y_p = L11^{-1} x_p in place;
-// Li: 32 x 33 doubles of LDS, xs: 32
+// factor the diagonal block at k0 (one wave, diag32_linv: two 16x16 tiles with 4x4 pivot blocks on
+// MFMA) and apply the forward step y_p = L11^{-1} x_p in place; Li: 32 x 33 doubles of LDS, xs: 32,
+// then 512 doubles of factorization scratch. Only L11^{-1} is kept (Lsave + Li): every later use
+// of the diagonal block (the panel rows, both triangular solves) needs the inverse, not L11.
 __device__ __forceinline__ void cb_diag_forward(double* __restrict__ S, int n, int k0, double* __restrict__ Li,
                                                 double* __restrict__ xs, double* __restrict__ Lsave,
                                                 double* __restrict__ x, int* __restrict__ flag) {
     const int lane = threadIdx.x & 63, kb = min(kCT, n - k0);
-    int bad = 0;
-    chol_diag_wave(S, n, k0, kb, Li, Lsave, &bad);
+    double* Ls = Lsave + (size_t)(k0 / kCT) * 1024;
+    const bool ok = diag32_linv(
+        [&](int r, int c) {   // r >= c; identity outside the matrix
+            return (r < kb && c < kb) ? S[(size_t)(k0 + r) * n + k0 + c] : (r == c ? 1.0 : 0.0);
+        },
+        xs + kCT,
+        [&](int r, int c, double v) {
+            Li[r * 33 + c] = v;
+            Ls[r * 32 + c] = v;
+        });
     if (lane < kCT) xs[lane] = lane < kb ? x[k0 + lane] : 0.0;
     wave_lds_sync();
     if (lane < kb) {
@@ -52,7 +63,7 @@ __device__ __forceinline__ void cb_diag_forward(double* __restrict__ S, int n, i
         for (int c = 0; c <= lane; c++) s += Li[lane * 33 + c] * xs[c];
         x[k0 + lane] = s;
     }
-    if (lane == 0 && bad) flag[0] = 0;
+    if (lane == 0 && !ok) flag[0] = 0;
 }
 
 // gate: the device-driven LM rounds (ba_solver.hip) run a problem's solve only in its trial phase
@@ -63,7 +74,7 @@ __device__ __forceinline__ void cb_diag_forward(double* __restrict__ S, int n, i
 __global__ __launch_bounds__(64) void k_cb_diag(double* __restrict__ S, int n, int k0, double* __restrict__ Lsave,
                                                 double* __restrict__ x, int* __restrict__ flag, const int* __restrict__ gate) {
     CB_GATE
-    __shared__ double Li[32 * 33 + 32];
+    __shared__ double Li[32 * 33 + 32 + 512];
     cb_diag_forward(S, n, k0, Li, Li + 32 * 33, Lsave, x, flag);
 }
 
@@ -218,14 +229,21 @@ __global__ __launch_bounds__(256) void k_cb_update(double* __restrict__ S, int n
 }
 
 // Backward substitution L^T x = y (y: the forward result in x; the factor's panels transposed in
-// the upper triangle of S, the panel inverses in Lsave); flag[0] == 0 (a non-positive pivot) ->
-// x = 0. One 1024-thread workgroup, x in LDS (n <= kCbMaxN). Panel p: s = sum over the factor
-// tiles R > p of its envelope (row_first[R] <= p) of L_Rp^T x_R, then x_p = L11^{-T} (y_p - s).
-// Thread t owns element (row t & 31, column t >> 5) of every 32x32 tile, read from the transposed
-// panel (S[column][row]: consecutive threads, consecutive addresses); the next panel's tiles (up
-// to kBackPre) and its L11^{-1} are loaded into registers before this panel's reductions, so the
-// panel chain waits on LDS and barriers, not on HBM.
-constexpr int kBackPre = 12;
+// the upper triangle of S, the panel inverses in Lsave) in SUPER-BLOCKS of kSB panels (256 rows),
+// last to first. For super-block b:
+//   diagonal solve  x_p = L11^{-T} (y_p - sum over R > p inside b of L_Rp^T x_R), p descending
+//                   (one 1024-thread workgroup, y of the super-block in LDS);
+//   step            y_i -= sum over R in b of L_Ri^T x_R for every panel i left of b (one
+//                   workgroup per panel, envelope tiles only), then the LAST workgroup to finish
+//                   runs the diagonal solve of super-block b - 1.
+// So the chain is ceil(np / 8) launches, the tiles left of the diagonal blocks are read by many
+// workgroups at once, and no workgroup ever waits for another: the step workgroups publish their
+// y_i with sc1 (write-through) stores, drain them (vmcnt(0)), and count themselves in flag[1] by
+// an agent-scope atomic; the workgroup whose add comes last reads the super-block's y back with
+// sc1 loads (MI355X_MICROARCH.md, inter-workgroup visibility, the table's first row). flag[0] == 0
+// (a non-positive pivot) -> x = 0.
+constexpr int kSB = 8;        // panels per super-block
+constexpr int kBackPre = kSB - 1;
 // workgroup barrier ordering LDS only: __syncthreads() is a workgroup fence, which on gfx950 also
 // drains vmcnt, i.e. would wait for the next panel's prefetch loads at every panel
 __device__ __forceinline__ void lds_barrier() {
@@ -233,84 +251,124 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 }
-__global__ __launch_bounds__(1024) void k_cb_back(const double* __restrict__ S, int n,
-                                                  const double* __restrict__ Lsave, double* __restrict__ x,
-                                                  const int* __restrict__ flag, const int* __restrict__ row_first,
-                                                  const int* __restrict__ gate) {
-    CB_GATE
-    __shared__ double y[kCbMaxN];
+__device__ __forceinline__ void wait_vm_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// diagonal solve of super-block sb (panels [p0, p1)), 1024 threads; sc1: read y with sc1 loads
+// (it was published by other workgroups of this launch)
+__device__ __forceinline__ void cb_back_block(const double* __restrict__ S, int n, const double* __restrict__ Lsave,
+                                              double* __restrict__ x, const int* __restrict__ row_first, int sb,
+                                              bool sc1) {
+    __shared__ double y[kSB * kCT];
     __shared__ double red[32];
     __shared__ double Lt[32 * 33];
     __shared__ double w[32];
-    __shared__ unsigned char lst[128 * 128];   // factor tiles below panel p: lst[128 p + j]
-    __shared__ int cnt[128];
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    if (flag[0] == 0) {
-        for (int i = tid; i < n; i += 1024) x[i] = 0.0;
-        return;
-    }
+    __shared__ unsigned char lst[kSB * kSB];   // factor tiles below panel p inside the super-block
+    __shared__ int cnt[kSB];
     const int np_ = (n + kCT - 1) / kCT;
-    for (int i = tid; i < n; i += 1024) y[i] = x[i];
-    if (tid < np_) {
+    const int p0 = sb * kSB, p1 = min(np_, p0 + kSB), r0 = p0 * kCT;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (tid < kSB * kCT)   // rows past n (or past the super-block) read as 0: their tiles are 0
+        y[tid] = (tid < (p1 - p0) * kCT && r0 + tid < n)
+                     ? (sc1 ? __hip_atomic_load(&x[r0 + tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : x[r0 + tid])
+                     : 0.0;
+    if (tid < p1 - p0) {
+        const int p = p0 + tid;
         int m = 0;
-        for (int R = tid + 1; R < np_; R++)
-            if (row_first[R] <= tid) lst[128 * tid + m++] = (unsigned char)R;
+        for (int R = p + 1; R < p1; R++)
+            if (row_first[R] <= p) lst[kSB * tid + m++] = (unsigned char)(R - p0);
         cnt[tid] = m;
     }
     __syncthreads();
     const int ti = tid & 31, tc = tid >> 5;   // row and column inside a 32x32 tile
     auto load = [&](int p, double (&buf)[kBackPre], double& l) {
-        const int m = cnt[p], col = kCT * p + tc;
+        const int m = cnt[p - p0], col = kCT * p + tc;
 #pragma unroll
         for (int j = 0; j < kBackPre; j++) {
             double v = 0.0;
             if (j < m) {
-                const int r = kCT * lst[128 * p + j] + ti;
+                const int r = r0 + kCT * lst[kSB * (p - p0) + j] + ti;
                 if (r < n && col < n) v = S[(size_t)col * n + r];   // L[r][col], transposed
             }
             buf[j] = v;
         }
         l = Lsave[(size_t)p * 1024 + tid];
     };
-    // panel p with its tiles in `cur` while panel p - 1's load into `nxt` is in flight; the two
-    // register sets swap roles by unrolling (a copy would wait for the loads)
     auto panel = [&](int p, const double (&cur)[kBackPre], double lcur, double (&nxt)[kBackPre], double& lnxt) {
-        const int k0 = p * kCT, m = cnt[p];
+        const int k0 = p * kCT, m = cnt[p - p0];
         Lt[(tid >> 5) * 33 + (tid & 31)] = lcur;   // L11^{-1} (Lsave is row-major 32 x 32)
         double s = 0.0;
 #pragma unroll
         for (int j = 0; j < kBackPre; j++)
-            if (j < m) s = fma(cur[j], y[kCT * lst[128 * p + j] + ti], s);   // x of tiles R > p: final
-        for (int j = kBackPre; j < m; j++) {                                 // wide envelopes only
-            const int r = kCT * lst[128 * p + j] + ti;
-            if (r < n && k0 + tc < n) s = fma(S[(size_t)(k0 + tc) * n + r], y[r], s);
-        }
-        // the next panel's loads go out once this panel's tiles are consumed: they stay in
-        // flight through the reductions and barriers below (which order LDS only)
-        if (p > 0) load(p - 1, nxt, lnxt);
-        // column tc's sum over the 32 rows: the 32 lanes of this half-wave
+            if (j < m) s = fma(cur[j], y[kCT * lst[kSB * (p - p0) + j] + ti], s);   // x of tiles R > p: final
+        if (p > p0) load(p - 1, nxt, lnxt);   // in flight through the reductions and barriers below
 #pragma unroll
         for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o);
         if ((lane & 31) == 0) red[tc] = s;
         lds_barrier();
         if (wid == 0) {
-            if (lane < kCT) w[lane] = k0 + lane < n ? y[k0 + lane] - red[lane] : 0.0;
+            if (lane < kCT) w[lane] = k0 + lane < n ? y[k0 - r0 + lane] - red[lane] : 0.0;
             wave_lds_sync();
             if (lane < kCT && k0 + lane < n) {
                 double xj = 0.0;
                 for (int c = lane; c < kCT; c++) xj = fma(Lt[c * 33 + lane], w[c], xj);   // (L11^{-T} w)_j
-                y[k0 + lane] = xj;
+                y[k0 - r0 + lane] = xj;
             }
         }
         lds_barrier();
     };
     double bufA[kBackPre], bufB[kBackPre], lA = 0.0, lB = 0.0;
-    load(np_ - 1, bufA, lA);
-    for (int p = np_ - 1; p >= 0; p -= 2) {
+    load(p1 - 1, bufA, lA);
+    for (int p = p1 - 1; p >= p0; p -= 2) {
         panel(p, bufA, lA, bufB, lB);
-        if (p >= 1) panel(p - 1, bufB, lB, bufA, lA);
+        if (p - 1 >= p0) panel(p - 1, bufB, lB, bufA, lA);
     }
-    for (int i = tid; i < n; i += 1024) x[i] = y[i];
+    if (tid < (p1 - p0) * kCT && r0 + tid < n) x[r0 + tid] = y[tid];
+}
+
+// the last super-block's diagonal solve (or x = 0 after a non-positive pivot)
+__global__ __launch_bounds__(1024) void k_cb_back_last(const double* __restrict__ S, int n,
+                                                       const double* __restrict__ Lsave, double* __restrict__ x,
+                                                       const int* __restrict__ flag, const int* __restrict__ row_first,
+                                                       const int* __restrict__ gate) {
+    CB_GATE
+    if (flag[0] == 0) {
+        for (int i = threadIdx.x; i < n; i += 1024) x[i] = 0.0;
+        return;
+    }
+    const int np_ = (n + kCT - 1) / kCT;
+    cb_back_block(S, n, Lsave, x, row_first, (np_ - 1) / kSB, false);
+}
+
+// step of super-block sb: workgroup = panel i (panels[blockIdx.x], or blockIdx.x without a list)
+__global__ __launch_bounds__(1024) void k_cb_back_step(const double* __restrict__ S, int n,
+                                                       const double* __restrict__ Lsave, double* __restrict__ x,
+                                                       int* __restrict__ flag, const int* __restrict__ row_first,
+                                                       const int* __restrict__ gate, int sb,
+                                                       const int* __restrict__ panels) {
+    CB_GATE
+    if (flag[0] == 0) return;   // x = 0 already
+    __shared__ int last;
+    const int np_ = (n + kCT - 1) / kCT;
+    const int i = panels ? panels[blockIdx.x] : blockIdx.x;
+    const int tid = threadIdx.x, ti = tid & 31, tc = tid >> 5, col = kCT * i + tc;
+    const int R0 = sb * kSB, R1 = min(np_, R0 + kSB);
+    double s = 0.0;
+    for (int R = R0; R < R1; R++) {
+        if (row_first[R] > i) continue;   // uniform
+        const int r = kCT * R + ti;
+        if (r < n && col < n) s = fma(S[(size_t)col * n + r], x[r], s);   // L[r][col] x_R[r]
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (ti == 0 && col < n)
+        __hip_atomic_store(&x[col], x[col] - s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1
+    wait_vm_all();
+    __syncthreads();
+    if (tid == 0) last = atomicAdd(&flag[1], 1) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    if (tid == 0) (void)atomicExch(&flag[1], 0);
+    cb_back_block(S, n, Lsave, x, row_first, sb - 1, true);
 }
 
 void chol_blocked_solve(double* S, int n, double* Lsave, const double* bs, double* x, int* flag,
@@ -331,7 +389,18 @@ void chol_blocked_solve(double* S, int n, double* Lsave, const double* bs, doubl
             hipLaunchKernelGGL(k_cb_update, dim3((unsigned)(T * (T + 1) / 2)), dim3(256), 0, st, S, n, k0, row_first,
                                Lsave, x, flag, gate, nullptr);
     }
-    hipLaunchKernelGGL(k_cb_back, dim3(1), dim3(1024), 0, st, S, n, Lsave, x, flag, row_first, gate);
+    hipLaunchKernelGGL(k_cb_back_last, dim3(1), dim3(1024), 0, st, S, n, Lsave, x, flag, row_first, gate);
+    const int nsb = (np_ + kSB - 1) / kSB;
+    for (int sb = nsb - 1; sb >= 1; sb--) {
+        if (tiles && tile_off) {   // this super-block's step panels (cb_envelope_tiles)
+            const int o0 = tile_off[np_ + (nsb - 1 - sb)], o1 = tile_off[np_ + 1 + (nsb - 1 - sb)];
+            hipLaunchKernelGGL(k_cb_back_step, dim3((unsigned)(o1 - o0)), dim3(1024), 0, st, S, n, Lsave, x, flag,
+                               row_first, gate, sb, tiles + o0);
+        } else {
+            hipLaunchKernelGGL(k_cb_back_step, dim3((unsigned)(sb * kSB)), dim3(1024), 0, st, S, n, Lsave, x, flag,
+                               row_first, gate, sb, nullptr);
+        }
+    }
 }
 
 // host: the 64x64 trailing-update tiles of every panel inside the envelope (the ones k_cb_update
@@ -359,6 +428,19 @@ void cb_envelope_tiles(const int* row_first, int n, std::vector<int>& tiles, std
             }
     }
     off[np_] = (int)tiles.size();
+    // backward steps, super-block sb = nsb-1 .. 1: the panels i < kSB sb with an envelope tile in
+    // the super-block, and every panel of super-block sb - 1 (their last workgroup solves it)
+    const int nsb = (np_ + kSB - 1) / kSB;
+    off.resize(np_ + nsb);
+    for (int sb = nsb - 1; sb >= 1; sb--) {
+        const int R0 = sb * kSB, R1 = std::min(np_, R0 + kSB);
+        for (int i = 0; i < R0; i++) {
+            bool any = i >= R0 - kSB;
+            for (int R = R0; R < R1 && !any; R++) any = row_first[R] <= i;
+            if (any) tiles.push_back(i);
+        }
+        off[np_ + 1 + (nsb - 1 - sb)] = (int)tiles.size();
+    }
 }
 
 // test hook: solve A x = b (A dense SPD, n <= kCbMaxN) through the blocked path; ms = device time
@@ -377,7 +459,8 @@ int chol_blocked_test(const double* A, const double* b, double* x, int n, float*
     ok(hipMalloc((void**)&db, sizeof(double) * n));
     ok(hipMalloc((void**)&dx, sizeof(double) * n));
     ok(hipMalloc((void**)&dL, sizeof(double) * 1024 * nt));
-    ok(hipMalloc((void**)&df, sizeof(int)));
+    ok(hipMalloc((void**)&df, 4 * sizeof(int)));
+    ok(hipMemset(df, 0, 4 * sizeof(int)));
     ok(hipMalloc((void**)&drf, sizeof(int) * nt));
     ok(hipMalloc((void**)&dtl, sizeof(int) * std::max<size_t>(1, tl.size())));
     if (rc == 0) {

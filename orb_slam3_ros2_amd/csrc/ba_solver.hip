@@ -823,12 +823,17 @@ __global__ __launch_bounds__(1024) void k_ba_ctl_init(const BaArgs* __restrict__
 
 // start of a slot: clear the pop request of the previous slot; at an iteration start, stop on the
 // iteration budget or the (host-relayed) stop flag
-__global__ void k_ba_ctl_pre(LmCtl* __restrict__ ctl, int B) {
+// done[b] (host-mapped, optional): set when problem b reaches kPhDone, so the host stops queueing
+// slots once every problem has finished
+__global__ void k_ba_ctl_pre(LmCtl* __restrict__ ctl, int B, int* done) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     LmCtl& c = ctl[b];
     c.pop = 0;
-    if (c.phase == kPhBuild && (c.stop || c.it >= c.iterations)) c.phase = kPhDone;
+    if (c.phase == kPhBuild && (c.stop || c.it >= c.iterations)) {
+        c.phase = kPhDone;
+        if (done) __hip_atomic_store(done + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 __global__ void k_ba_ctl_stop(LmCtl* __restrict__ ctl, int B) {
@@ -857,7 +862,8 @@ __global__ __launch_bounds__(1024) void k_ba_ctl_begin(const BaArgs* __restrict_
 
 // after a trial: chi2 and scale, rho, accept (lambda shrink) or reject (lambda *= ni, pop), and
 // the end-of-iteration rules
-__global__ __launch_bounds__(1024) void k_ba_ctl_end(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+__global__ __launch_bounds__(1024) void k_ba_ctl_end(const BaArgs* __restrict__ args, const int* __restrict__ act,
+                                                     int* done_flags) {
     __shared__ double sh[16];
     const BaArgs& a = args[act[blockIdx.x]];
     LmCtl& c = *a.ctl;
@@ -894,6 +900,7 @@ __global__ __launch_bounds__(1024) void k_ba_ctl_end(const BaArgs* __restrict__ 
     if (c.early_stop && c.nBad >= 3) done = true;
     if (c.it >= c.iterations) done = true;   // the budget (checked by ctl_pre too), no idle slot
     c.phase = done ? kPhDone : kPhBuild;
+    if (done && done_flags) __hip_atomic_store(done_flags + act[blockIdx.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------
@@ -1124,6 +1131,9 @@ struct BaWorkspace {
     DBuf<double> envbuf;       // S's union envelope, packed for the all-reduce (k_ba_env_pack)
     DBuf<long long> envoff;    // its per-32-row-tile offsets
     int* h_stop = nullptr;     // pinned
+    int* h_done = nullptr;     // pinned, mapped: per problem, set by the device when its LM run ends
+    int* d_done = nullptr;     // its device address
+    size_t done_cap = 0;
 };
 
 BaWorkspace* ba_create() { return new BaWorkspace(); }
@@ -1132,6 +1142,7 @@ void ba_destroy(BaWorkspace* w) {
     if (!w) return;
     if (w->comm) (void)ncclCommDestroy(w->comm);
     if (w->h_stop) (void)hipHostFree(w->h_stop);
+    if (w->h_done) (void)hipHostFree(w->h_done);
     if (w->h_lam) (void)hipHostFree(w->h_lam);
     if (w->h_red) (void)hipHostFree(w->h_red);
     if (w->h_act) (void)hipHostFree(w->h_act);
@@ -1255,7 +1266,9 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         int* d0 = I + p.o_int;
         auto dev = [&](const int* host_at) { return d0 + (host_at - (hi + p.o_int)); };
         a.opt = dev(put(p.opt.data(), P));
-        a.flag = dev(q); q += 4;
+        a.flag = dev(q);   // [0] Cholesky ok, [1] blocked backward arrival counter (zero between uses)
+        std::memset(q, 0, 4 * sizeof(int));
+        q += 4;
         a.e_pose = dev(put(pr->edge_pose, E));
         a.e_pt = dev(put(pr->edge_point, E));
         a.pt_ptr = dev(put(p.pt_ptr.data(), M + 1));
@@ -1433,7 +1446,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         hipLaunchKernelGGL(k_ba_ctl_init, dim3(B), dim3(1024), 0, st, dA, d_act);
         const dim3 gB((unsigned)((B + 255) / 256)), b256(256);
         auto slot = [&]() -> int {
-            hipLaunchKernelGGL(k_ba_ctl_pre, gB, b256, 0, st, dctl, B);
+            hipLaunchKernelGGL(k_ba_ctl_pre, gB, b256, 0, st, dctl, B, ws->d_done);
             hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 1);
             hipLaunchKernelGGL(k_ba_lin_points, dim3(gx(maxM, 256), B), b256, 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_lin_poses, dim3(gx(maxNp, 4), B), b256, 0, st, dA, d_act);
@@ -1455,7 +1468,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             hipLaunchKernelGGL(k_ba_backsub, dim3(gx(maxM, 256), B), b256, 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_update_poses, dim3(gx(maxP, 256), B), b256, 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 2);
-            hipLaunchKernelGGL(k_ba_ctl_end, dim3(B), dim3(1024), 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_ctl_end, dim3(B), dim3(1024), 0, st, dA, d_act, ws->d_done);
             int maxPM = 0;
             for (auto& p : pp) maxPM = std::max(maxPM, std::max(8 * p.P, 3 * p.M));
             hipLaunchKernelGGL(k_ba_pop, dim3(gx(maxPM, 256), B), b256, 0, st, dA, d_act);
@@ -1469,6 +1482,21 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         BAOK(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
         int rc = ORBHIP_OK;
         bool stop_sent = false;
+        // done flags: a problem that ends early (rho == 0, 10 trials, _nBad) leaves the later
+        // slots empty; once every flag is set the host queues no further slot
+        if (ws->done_cap < (size_t)B) {
+            if (ws->h_done) (void)hipHostFree(ws->h_done);
+            ws->h_done = nullptr; ws->d_done = nullptr; ws->done_cap = 0;
+            BAOK(hipHostMalloc((void**)&ws->h_done, sizeof(int) * B, hipHostMallocMapped | hipHostMallocCoherent));
+            BAOK(hipHostGetDevicePointer((void**)&ws->d_done, ws->h_done, 0));
+            ws->done_cap = B;
+        }
+        for (int b = 0; b < B; b++) __atomic_store_n(ws->h_done + b, 0, __ATOMIC_RELAXED);
+        auto all_done = [&] {
+            for (int b = 0; b < B; b++)
+                if (!__atomic_load_n(ws->h_done + b, __ATOMIC_RELAXED)) return false;
+            return true;
+        };
         int remaining = 0;   // slots every unfinished problem still needs at least
         for (int b = 0; b < B; b++) remaining = std::max(remaining, probs[b]->iterations);
         int nslot = 0;
@@ -1482,6 +1510,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 if (rc == ORBHIP_OK && hipEventRecord(ev[nslot & 1], st) != hipSuccess) rc = ORBHIP_ERR_DEVICE;
                 if (rc == ORBHIP_OK && nslot >= 1 && hipEventSynchronize(ev[(nslot - 1) & 1]) != hipSuccess)
                     rc = ORBHIP_ERR_DEVICE;
+                if (rc == ORBHIP_OK && nslot >= 1 && all_done()) { nslot++; break; }
             }
             if (rc != ORBHIP_OK) break;
             if (hipMemcpyAsync(ws->hctl.p, dctl, B * sizeof(LmCtl), hipMemcpyDeviceToHost, st) != hipSuccess ||

@@ -45,8 +45,9 @@ __device__ __forceinline__ void undistort_point(float u_f, float v_f, const orbh
     yo = (float)(yy * ww);
 }
 
-// kps[b][cap] -> out[b][cap] for the first n[b] records (n_arr) or n_fixed; out may alias kps
-__global__ __launch_bounds__(256) void k_undistort_kps(const orbhip_kp* __restrict__ kps, const int32_t* __restrict__ n_arr,
+// kps[b][cap] -> out[b][cap] for the first n[b] records (n_arr) or n_fixed; out may alias kps (so
+// neither is __restrict__)
+__global__ __launch_bounds__(256) void k_undistort_kps(const orbhip_kp* kps, const int32_t* __restrict__ n_arr,
                                                        int n_fixed, int cap, orbhip_pinhole cam, orbhip_kp* out) {
     const int b = blockIdx.y;
     const int i = blockIdx.x * 256 + threadIdx.x;

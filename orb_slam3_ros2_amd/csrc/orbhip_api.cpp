@@ -95,7 +95,7 @@ struct orbhip_ctx {
     std::vector<float> scale, inv_scale;
     std::vector<int> feat, umax;
     int blurk[7] = {0};
-    std::map<std::tuple<int, int, int>, std::shared_ptr<Plan>> plans;   // (w, h, cone tile); shared with other contexts (plan_cache)
+    std::map<std::tuple<int, int, int, int, int>, std::shared_ptr<Plan>> plans;   // (w, h, cone tile, FAST clist cap, FAST threads); shared with other contexts (plan_cache)
     // per-batch scratch (grown on demand)
     DevBuf<uint8_t> d_in, d_pyr;
     DevBuf<uint32_t> d_cand, d_kscratch;
@@ -204,7 +204,13 @@ static int cone_tile_of(const orbhip_ctx* c) {
 
 static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
     const int ts = cone_tile_of(c);
-    auto key = std::make_tuple(w, h, ts);
+    // every setting the shared PlanKey holds is part of the context's key too, so an env switch
+    // (ORBHIP_FAST_CLIST_CAP / ORBHIP_FAST_NT) takes effect on an existing context
+    const char* cap_env = getenv("ORBHIP_FAST_CLIST_CAP");
+    const int clist_cap = cap_env ? atoi(cap_env) : -1;
+    const char* nt_env = getenv("ORBHIP_FAST_NT");
+    const int fast_nt = nt_env ? atoi(nt_env) : -1;
+    auto key = std::make_tuple(w, h, ts, clist_cap, fast_nt);
     auto it = c->plans.find(key);
     if (it != c->plans.end()) { *out = it->second.get(); return ORBHIP_OK; }
     PlanKey k;
@@ -212,10 +218,8 @@ static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
     k.device = c->device; k.w = w; k.h = h; k.nfeat = c->prm.n_features; k.nlev = c->prm.n_levels;
     k.ini = c->prm.ini_th_fast; k.mn = c->prm.min_th_fast; k.scale = c->prm.scale_factor;
     k.cone_tile = ts;
-    const char* cap_env = getenv("ORBHIP_FAST_CLIST_CAP");
-    k.clist_cap = cap_env ? atoi(cap_env) : -1;
-    const char* nt_env = getenv("ORBHIP_FAST_NT");
-    k.fast_nt = nt_env ? atoi(nt_env) : -1;
+    k.clist_cap = clist_cap;
+    k.fast_nt = fast_nt;
     std::lock_guard<std::mutex> g(g_plan_m);
     std::shared_ptr<Plan> sp = plan_cache()[k].lock();
     if (!sp) {
@@ -1411,16 +1415,19 @@ int orbhip_test_cells(orbhip_ctx* c, int w, int h, int32_t* out6, int cap) {
 // frames/s one frame at a time against 15.0k at 14), many streams share the chip and want less
 // halo recompute per frame (16 cameras: 39.6k frames/s at 16-pixel tiles against 38.3k at 14;
 // tools/gpu_cone_tile.sh). Both tilings give the same pyramid (every tile writes what it owns).
-static std::atomic<int> g_live_frontends{0};
-static int frontend_cone_tile() {
-    const int n = g_live_frontends.load(std::memory_order_relaxed);
+// Counted per device: a process driving one camera per GPU keeps every GPU at the one-camera choice.
+constexpr int kMaxDevices = 64;
+static std::atomic<int> g_live_frontends[kMaxDevices];
+static std::atomic<int>& live_frontends(int device) { return g_live_frontends[device & (kMaxDevices - 1)]; }
+static int frontend_cone_tile(int device) {
+    const int n = live_frontends(device).load(std::memory_order_relaxed);
     return n >= 8 ? 16 : (n >= 2 ? 14 : 10);
 }
 // FAST threads per cell the same way: one camera keeps the one-frame rule (512 at 640x480, 15.8k
 // frames/s against 15.4k at 256); 8+ cameras take 256 (16 cameras: 40.5k against 39.6k at 512,
 // 35.6k at 1024; tools/gpu_c2_fastnt.sh)
-static int frontend_fast_nt() {
-    return g_live_frontends.load(std::memory_order_relaxed) >= 8 ? 256 : 0;
+static int frontend_fast_nt(int device) {
+    return live_frontends(device).load(std::memory_order_relaxed) >= 8 ? 256 : 0;
 }
 
 struct orbhip_frontend {
@@ -1438,7 +1445,7 @@ struct orbhip_frontend {
     // frames up to done_upto), not per push (an event per frame costs ~3% of the 16-camera rate)
     hipEvent_t ev_done = nullptr;
     int64_t done_upto = -1;
-    bool live = false;   // counted in g_live_frontends
+    bool live = false;   // counted in live_frontends(device)
 };
 
 static void frontend_free(orbhip_frontend* f) {
@@ -1458,7 +1465,7 @@ static void frontend_free(orbhip_frontend* f) {
     if (f->nm) (void)hipFree(f->nm);
     for (orbhip_ctx* c : f->ctx)
         if (c) (void)orbhip_destroy(c);
-    if (f->live) g_live_frontends.fetch_sub(1, std::memory_order_relaxed);
+    if (f->live) live_frontends(f->device).fetch_sub(1, std::memory_order_relaxed);
     delete f;
 }
 
@@ -1478,7 +1485,7 @@ int orbhip_frontend_create(orbhip_frontend** out, int device, const orbhip_orb_p
         if (int rc = orbhip_create(&f->ctx[j], device, params)) return rc;
         f->ctx[j]->cone_tile = 10;   // set per push (frontend_cone_tile)
     }
-    g_live_frontends.fetch_add(1, std::memory_order_relaxed);
+    live_frontends(device).fetch_add(1, std::memory_order_relaxed);
     f->live = true;
     const int cap = orbhip_max_keypoints(f->ctx[0], w, h);
     if (cap <= 0) return cap < 0 ? cap : ORBHIP_ERR_UNSUPPORTED;
@@ -1516,8 +1523,8 @@ int orbhip_frontend_push(orbhip_frontend* f, const uint8_t* d_img, int stride, i
     const int S = f->S, ns = f->ns, cap = f->cap;
     const int j = (int)(k % S), cur = (int)(k % ns), prev = (int)((k + ns - 1) % ns);
     orbhip_ctx* c = f->ctx[j];
-    c->cone_tile = frontend_cone_tile();
-    c->fast_nt = frontend_fast_nt();
+    c->cone_tile = frontend_cone_tile(f->device);
+    c->fast_nt = frontend_fast_nt(f->device);
     hipStream_t st = c->stream;
     // slot `cur` was last read as `prev` by the match of frame k - ns + 1 (on another stream when
     // S > 1); its reader as `cur`, frame k - ns, ran on this stream
