@@ -197,6 +197,7 @@ def lib():
     # measurement hooks of the dense Cholesky (HIP events around back-to-back launches)
     L.orbhip_test_cholesky_reg.argtypes = [vp, vp, vp, i32, i32, ctypes.POINTER(f32), vp]
     L.orbhip_test_cholesky_blocked.argtypes = [vp, vp, vp, i32, ctypes.POINTER(f32)]
+    L.orbhip_test_cholesky_dag.argtypes = [vp, vp, vp, i32, i32, i32, ctypes.POINTER(f32), vp]
     _lib = L
     return L
 

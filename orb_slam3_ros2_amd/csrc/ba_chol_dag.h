@@ -1,0 +1,54 @@
+// Persistent tiled-DAG Cholesky solve of the reduced camera system (ba_chol_dag.hip): ONE launch
+// per solve, 32x32 tiles, a chain workgroup on the diagonal critical path and helper workgroups
+// owning the off-diagonal tiles, in-launch hand-offs by flags (a20 / a22: g2o LinearSolverEigen
+// behind OptimizationAlgorithmLevenberg).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <vector>
+
+namespace orbhip {
+
+constexpr int kDagTile = 32;
+constexpr int kDagMaxN = 4096;
+constexpr int kDagMaxHelpers = 255;   // helper workgroups (+ the chain workgroup: one per CU)
+
+// host plan of one problem: the helper tasks (tile (R, C) as R << 16 | C) of each helper
+// workgroup, in the order the workgroup runs them (dependency key order, deadlock-free)
+struct DagPlan {
+    int NT = 0, G = 0;
+    std::vector<int> toff;    // G + 1 offsets into tasks
+    std::vector<int> tasks;
+};
+void dag_plan(const int* row_first, int n, int max_helpers, DagPlan& p);
+int dag_max_helpers();   // min(kDagMaxHelpers, CUs - 1): the whole grid resident, one workgroup per CU
+
+// device storage of one problem: doubles (L tiles NT x NT, the two partial-tile rows, the
+// diagonal inverses, y, the right-hand-side partials) and ints (4 control words + flags; zero
+// before the first solve, never reset between solves: every solve counts its own epoch)
+size_t dag_doubles(int n);
+size_t dag_ints(int n);
+
+struct DagDev {
+    double* buf;         // dag_doubles(n)
+    int* ints;           // dag_ints(n), zeroed once
+    const int* toff;     // plan, on the device
+    const int* tasks;
+    int G;
+};
+
+// S (n x n row-major, lower triangle read, never written), row_first (ceil(n/32): first 32-col
+// tile with a structural non-zero per 32-row tile), bs -> x; flag[0] = 1 ok, 0 on a non-positive
+// pivot (x = 0). gate (optional): returns unless *gate == kPhTrial. dbg (optional, >= 8 + NT
+// u64): the chain's shader-clock phase cycles.
+hipError_t chol_dag_solve(const double* S, int n, const int* row_first, const double* bs, double* x, int* flag,
+                          const DagDev& d, hipStream_t st, const int* gate = nullptr,
+                          unsigned long long* dbg = nullptr);
+
+// test hook: A dense SPD (its structure -> row_first), reps timed solves; ms = device ms per solve;
+// dbg as above (optional); returns 0, -4 on a failed pivot, -5 on a hand-off timeout
+int chol_dag_test(const double* A, const double* b, double* x, int n, int reps, int max_helpers, float* ms,
+                  unsigned long long* dbg);
+
+}  // namespace orbhip

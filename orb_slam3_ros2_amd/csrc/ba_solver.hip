@@ -39,6 +39,7 @@
 #include "orbhip_ba.h"
 #include "ba_chol.h"
 #include "ba_chol_blocked.h"
+#include "ba_chol_dag.h"
 #include "ba_args.h"
 #include "ba_chol_reg.h"
 #include "ba_se3.h"
@@ -926,8 +927,12 @@ struct Prep {
     std::vector<int> cb_tiles, cb_off;   // blocked Cholesky: envelope tiles per panel (cb_envelope_tiles)
     std::vector<int> items, fin;  // Schur work items {k0, k1, blk, slot} and finisher blocks {blk, slot0, n}
     int nslot = 0;
+    bool use_dag = false;         // the persistent tiled-DAG Cholesky (ba_chol_dag.hip)
+    DagPlan dag;                  // its helper task lists
+    size_t dag_task_cap = 0;      // ints reserved for the lists (RCCL shards: planned after the union envelope)
+    size_t o_dag = 0, o_dagi = 0;
     // offsets (elements) into the packed buffers; see the segment map in ba_solve_batch
-    size_t o_chi2, o_state, o_obs, o_scr, o_lin, o_S, o_L, o_part, o_int;
+    size_t o_chi2 = 0, o_state = 0, o_obs = 0, o_scr = 0, o_lin = 0, o_S = 0, o_L = 0, o_part = 0, o_int = 0;
 };
 
 inline void se3_from_float(const float* q, const float* t, double* out) {
@@ -1182,12 +1187,31 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 pp[0].row_first[R] = std::min(pp[0].row_first[R], pp[b].row_first[R]);
         for (int b = 1; b < B; b++) pp[b].row_first = pp[0].row_first;
     }
-    // the blocked solver's per-panel tile lists (not for RCCL shards: their envelope is the union
-    // over the ranks, known on the device only)
-    if (shard_mode != kShardRccl)
-        parallel_for(B, nth, [&](int b) {
-            if (pp[b].n > kCholSmallN) cb_envelope_tiles(pp[b].row_first.data(), pp[b].n, pp[b].cb_tiles, pp[b].cb_off);
-        });
+    // Cholesky per problem: the persistent DAG solver for the GBA sizes and for a problem solved
+    // alone (one LBA), the register / LDS single-workgroup solvers for batches of small problems;
+    // ORBHIP_CHOL_BLOCKED=1 restores the one-launch-per-panel blocked solver for the large ones,
+    // ORBHIP_CHOL_DAG_MIN sets the smallest n a lone problem takes the DAG solver at (default 128)
+    static const bool force_blocked = std::getenv("ORBHIP_CHOL_BLOCKED") != nullptr;
+    static const int dag_min = std::getenv("ORBHIP_CHOL_DAG_MIN") ? std::atoi(std::getenv("ORBHIP_CHOL_DAG_MIN")) : 128;
+    const int dag_helpers = dag_max_helpers();
+    for (int b = 0; b < B; b++)
+        pp[b].use_dag = !force_blocked && pp[b].n > 0 && (pp[b].n > kCholSmallN || (B == 1 && pp[b].n >= dag_min));
+    // the per-panel tile lists / the DAG plans (RCCL shards: the envelope is the union over the
+    // ranks, known after a collective; their DAG plan is made then, into reserved space)
+    parallel_for(B, nth, [&](int b) {
+        Prep& p = pp[b];
+        if (p.use_dag) {
+            if (shard_mode == kShardRccl) {
+                const size_t NT = (p.n + kDagTile - 1) / kDagTile;
+                p.dag_task_cap = (size_t)dag_helpers + 1 + NT * (NT + 1) / 2;
+            } else {
+                dag_plan(p.row_first.data(), p.n, dag_helpers, p.dag);
+                p.dag_task_cap = p.dag.toff.size() + p.dag.tasks.size();
+            }
+        } else if (p.n > kCholSmallN && shard_mode != kShardRccl) {
+            cb_envelope_tiles(p.row_first.data(), p.n, p.cb_tiles, p.cb_off);
+        }
+    });
     const double t_prep = now();
     // ---- packed layout: fp64 segments, each contiguous over all problems ----
     //   C  e_chi2 (E)                 downloaded with A in one transfer
@@ -1213,11 +1237,16 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         p.o_L = nR; nR += 1024 * ((n + 31) / 32);
         nR = (nR + 1) & ~size_t(1);
         p.o_part = nR; nR += 36 * (size_t)p.nslot;
+        if (p.use_dag) {   // 128-byte aligned
+            nR = (nR + 15) & ~size_t(15);
+            p.o_dag = nR; nR += dag_doubles(p.n);
+        }
         p.o_int = ni;
         ni += (P + 4) + 2 * E + (M + 1) + E + (np_ + 1) + p.ps_edges.size() + 3 * p.nblk + 1 + p.blk_pairs.size() +
-              p.row_first.size() + p.items.size() + p.fin.size() + p.cb_tiles.size() + 8;
+              p.row_first.size() + p.items.size() + p.fin.size() + p.cb_tiles.size() + 8 +
+              (p.use_dag ? dag_ints(p.n) + p.dag_task_cap + 4 : 0);
     }
-    const size_t sC = 0, sA = nC, sU = sA + nA, sR = (sU + nU + 3) & ~size_t(3);
+    const size_t sC = 0, sA = nC, sU = sA + nA, sR = (sU + nU + 15) & ~size_t(15);
     const size_t nd = sR + nR;
     BAOK(ws->dbl.ensure(nd));
     BAOK(ws->ints.ensure(ni));
@@ -1247,6 +1276,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     double* hd = ws->hdbl.p;
     int* hi = ws->hint.p;
     BaArgs* ha = ws->hargs.p;
+    std::vector<DagDev> dd(B, DagDev{nullptr, nullptr, nullptr, nullptr, 0});
     parallel_for(B, nth, [&](int b) {
         const Prep& p = pp[b];
         const orbhip_ba_problem* pr = probs[b];
@@ -1287,6 +1317,22 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.nfin = (int)(p.fin.size() / 3);
         a.row_first = dev(put(p.row_first.data(), p.row_first.size()));
         a.cb_tiles = p.cb_tiles.empty() ? nullptr : dev(put(p.cb_tiles.data(), p.cb_tiles.size()));
+        if (p.use_dag) {   // flags + control words (zero), then the plan (or the space reserved for it)
+            while ((q - hi) & 3) q++;
+            dd[b].ints = dev(q);
+            std::memset(q, 0, dag_ints(p.n) * sizeof(int));
+            q += dag_ints(p.n);
+            dd[b].toff = dev(q);
+            if (!p.dag.toff.empty()) {
+                put(p.dag.toff.data(), p.dag.toff.size());
+                dd[b].tasks = dev(q);
+                put(p.dag.tasks.data(), p.dag.tasks.size());
+            } else {
+                dd[b].tasks = dev(q + kDagMaxHelpers + 1);   // RCCL: planned after the union envelope
+                q += p.dag_task_cap;
+            }
+            dd[b].G = p.dag.G;
+        }
         a.nblk = p.nblk;
         a.P = p.P; a.M = p.M; a.E = p.E; a.np = p.np; a.n = p.n;
         a.fx = pr->fx; a.fy = pr->fy; a.cx = pr->cx; a.cy = pr->cy; a.delta = pr->huber_delta;
@@ -1312,6 +1358,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.S = D + sR + p.o_S;
         a.Lsave = D + sR + p.o_L;
         a.Spart = D + sR + p.o_part;
+        if (p.use_dag) dd[b].buf = D + sR + p.o_dag;
         a.lambda = ws->lam.p + b;
         a.lead = shard_mode == kShardLocal ? (b == 0) : (shard_mode == kShardRccl ? (ws->rank == 0) : 1);
         a.ctl = shard_mode == kShardNone ? ws->ctl.p + b : nullptr;
@@ -1328,10 +1375,24 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         if (ncclAllReduce(rf, rf, pp[0].row_first.size(), ncclInt32, ncclMin, ws->comm, st) != ncclSuccess)
             return ORBHIP_ERR_DEVICE;
         const int nt = (int)pp[0].row_first.size(), n = pp[0].n;
-        if (n > kCholSmallN && !std::getenv("ORBHIP_SHARD_FULL_S")) {
         std::vector<int> urf(nt);
-        BAOK(hipMemcpyAsync(urf.data(), rf, nt * sizeof(int), hipMemcpyDeviceToHost, st));
-        BAOK(hipStreamSynchronize(st));
+        if (n > kCholSmallN || pp[0].use_dag) {
+            BAOK(hipMemcpyAsync(urf.data(), rf, nt * sizeof(int), hipMemcpyDeviceToHost, st));
+            BAOK(hipStreamSynchronize(st));
+        }
+        if (pp[0].use_dag) {   // the DAG plan of the union envelope, into the reserved space
+            DagPlan& dp = pp[0].dag;
+            dag_plan(urf.data(), n, dag_helpers, dp);
+            if (dp.toff.size() + dp.tasks.size() > pp[0].dag_task_cap) return ORBHIP_ERR_DEVICE;
+            BAOK(hipMemcpy(const_cast<int*>(dd[0].toff), dp.toff.data(), dp.toff.size() * sizeof(int),
+                           hipMemcpyHostToDevice));
+            dd[0].tasks = dd[0].toff + dp.toff.size();
+            if (!dp.tasks.empty())
+                BAOK(hipMemcpy(const_cast<int*>(dd[0].tasks), dp.tasks.data(), dp.tasks.size() * sizeof(int),
+                               hipMemcpyHostToDevice));
+            dd[0].G = dp.G;
+        }
+        if (n > kCholSmallN && !std::getenv("ORBHIP_SHARD_FULL_S")) {
         std::vector<long long> off(nt + 1, 0);
         for (int R = 0; R < nt; R++)
             off[R + 1] = off[R] + (long long)std::min(32, n - 32 * R) * (std::min(32 * R + 32, n) - 32 * urf[R]);
@@ -1348,17 +1409,30 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         lds_set = true;
     }
     int maxM = 0, maxE = 0, maxP = 0, maxNp = 0, maxBlk = 0, maxN = 0, maxItems = 0, maxFin = 0;
-    bool any_large = false;
-    for (auto& p : pp) {
+    bool any_large = false, s_written = false;
+    // "large": solved on its own (DAG or blocked); the rest share one single-workgroup launch
+    auto large = [&](int b) { return pp[b].use_dag || pp[b].n > kCholSmallN; };
+    for (int b = 0; b < B; b++) {
+        const Prep& p = pp[b];
         maxM = std::max(maxM, p.M); maxE = std::max(maxE, p.E); maxP = std::max(maxP, p.P);
         maxNp = std::max(maxNp, p.np); maxBlk = std::max(maxBlk, p.nblk);
         maxItems = std::max(maxItems, (int)(p.items.size() / 4)); maxFin = std::max(maxFin, (int)(p.fin.size() / 3));
-        if (p.n > kCholSmallN) any_large = true;
+        if (large(b)) any_large = true;
         else maxN = std::max(maxN, p.n);
+        if (!p.use_dag && p.n > kCholRegMaxN) s_written = true;   // the LDS and blocked solvers factor S in place
     }
     const size_t chol_lds = sizeof(double) * chol_lds_doubles(maxN);
-    // every problem on the register-resident Cholesky (reads S, never writes it), no shard sums
-    const bool s_readonly = !any_large && maxN <= kCholRegMaxN && shard_mode == kShardNone;
+    // every problem on a solver that reads S and never writes it (register / DAG), no shard sums
+    const bool s_readonly = !s_written && shard_mode == kShardNone;
+    auto large_solve = [&](int b, const int* gate) -> int {
+        if (pp[b].use_dag) {
+            BAOK(chol_dag_solve(ha[b].S, pp[b].n, ha[b].row_first, ha[b].bs, ha[b].x, ha[b].flag, dd[b], st, gate));
+        } else {
+            chol_blocked_solve(ha[b].S, pp[b].n, ha[b].Lsave, ha[b].bs, ha[b].x, ha[b].flag, ha[b].row_first, st, gate,
+                               ha[b].cb_tiles, pp[b].cb_off.empty() ? nullptr : pp[b].cb_off.data());
+        }
+        return ORBHIP_OK;
+    };
     bool s_clean = false;
     auto gx = [](int n_, int b_) { return (unsigned)std::max(1, (n_ + b_ - 1) / b_); };
     (void)hipGetLastError();
@@ -1439,7 +1513,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         BAOK(hipMemcpyAsync(dctl, ws->hctl.p, B * sizeof(LmCtl), hipMemcpyHostToDevice, st));
         int ns = 0;   // problems on the single-workgroup solvers (act slot 3)
         for (int b = 0; b < B; b++)
-            if (pp[b].n <= kCholSmallN) h_act[2 * B + ns++] = b;
+            if (!large(b)) h_act[2 * B + ns++] = b;
         if (ns) BAOK(hipMemcpyAsync(d_act + 2 * B, h_act + 2 * B, ns * sizeof(int), hipMemcpyHostToDevice, st));
         if (s_readonly) hipLaunchKernelGGL(k_ba_zero_s, dim3(64, B), dim3(256), 0, st, dA, d_act, 1);
         hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), dim3(256), 0, st, dA, d_act, 0);
@@ -1461,10 +1535,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 else hipLaunchKernelGGL(k_ba_cholesky, dim3(ns), dim3(512), chol_lds, st, dA, d_act + 2 * B);
             }
             for (int b = 0; b < B; b++)
-                if (pp[b].n > kCholSmallN)
-                    chol_blocked_solve(ha[b].S, pp[b].n, ha[b].Lsave, ha[b].bs, ha[b].x, ha[b].flag, ha[b].row_first,
-                                       st, &dctl[b].phase, ha[b].cb_tiles,
-                                       pp[b].cb_off.empty() ? nullptr : pp[b].cb_off.data());
+                if (large(b) && large_solve(b, &dctl[b].phase)) return ORBHIP_ERR_DEVICE;
             hipLaunchKernelGGL(k_ba_backsub, dim3(gx(maxM, 256), B), b256, 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_update_poses, dim3(gx(maxP, 256), B), b256, 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 2);
@@ -1600,17 +1671,14 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 // small problems: one workgroup each (act slot 3); large: the blocked solver
                 int ns = 0;
                 for (int b : trial)
-                    if (pp[b].n <= kCholSmallN) h_act[2 * B + ns++] = b;
+                    if (!large(b)) h_act[2 * B + ns++] = b;
                 if (ns) {
                     BAOK(hipMemcpyAsync(d_act + 2 * B, h_act + 2 * B, ns * sizeof(int), hipMemcpyHostToDevice, st));
                     if (maxN <= kCholRegMaxN) BAOK(chol_reg_launch(maxN, ns, dA, d_act + 2 * B, st));
                     else hipLaunchKernelGGL(k_ba_cholesky, dim3(ns), dim3(512), chol_lds, st, dA, d_act + 2 * B);
                 }
                 for (int b : trial)
-                    if (pp[b].n > kCholSmallN)
-                        chol_blocked_solve(ha[b].S, pp[b].n, ha[b].Lsave, ha[b].bs, ha[b].x, ha[b].flag,
-                                           ha[b].row_first, st, nullptr, ha[b].cb_tiles,
-                                           pp[b].cb_off.empty() ? nullptr : pp[b].cb_off.data());
+                    if (large(b) && large_solve(b, nullptr)) return ORBHIP_ERR_DEVICE;
             }
             hipLaunchKernelGGL(k_ba_backsub, dim3(gx(maxM, 256), nt_), dim3(256), 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_update_poses, dim3(gx(maxP, 256), nt_), dim3(256), 0, st, dA, d_act);

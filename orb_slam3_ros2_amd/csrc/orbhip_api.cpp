@@ -28,6 +28,7 @@
 #include "proj.h"
 #include "kfdb.h"
 #include "ba_chol_blocked.h"
+#include "ba_chol_dag.h"
 #include "orbhip_kernels.h"
 #include "orbhip_plan.h"
 #include "graph_cache.h"
@@ -1281,6 +1282,11 @@ int orbhip_test_cholesky_reg(const double* A, const double* b, double* x, int n,
 int orbhip_test_cholesky_blocked(const double* A, const double* b, double* x, int n, float* ms) {
     if (!A || !b || !x || n <= 0 || !ms) return ORBHIP_ERR_ARG;
     return chol_blocked_test(A, b, x, n, ms);
+}
+int orbhip_test_cholesky_dag(const double* A, const double* b, double* x, int n, int reps, int max_helpers, float* ms,
+                             unsigned long long* dbg) {
+    if (!A || !b || !x || n <= 0 || reps < 1) return ORBHIP_ERR_ARG;
+    return chol_dag_test(A, b, x, n, reps, max_helpers, ms, dbg);
 }
 int orbhip_test_sincosf(const float* x, float* cs, float* sn, int64_t n) {
     if (!x || !cs || !sn || n <= 0) return ORBHIP_ERR_ARG;

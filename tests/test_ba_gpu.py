@@ -200,6 +200,60 @@ def test_blocked_cholesky_solves_spd(n, shape):
     assert np.abs(x - ref).max() <= 1e-10 * np.abs(ref).max()
 
 
+@pytest.mark.parametrize("n,shape,helpers", [(31, "dense", 0), (64, "dense", 0), (100, "dense", 3), (294, "dense", 0),
+                                             (294, "dense", 1), (600, "band", 0), (1201, "dense", 0),
+                                             (2394, "loop", 0), (2394, "loop", 7)])
+def test_dag_cholesky_solves_spd(n, shape, helpers):
+    """The persistent tiled-DAG solver (ba_chol_dag.hip: one launch, a chain workgroup on the
+    diagonal path, helper workgroups on the off-diagonal tiles, flag hand-offs) on random SPD
+    systems: dense, banded, and C5's band plus loop-closure corner, with the full helper grid and
+    with few helpers (each helper then runs many tasks in dependency-key order). Against numpy's
+    fp64 solve; three solves in a row reuse the flags through the per-solve epoch."""
+    import ctypes
+    from orb_slam3_ros2_amd._lib import lib
+    L = lib()
+    rng = np.random.default_rng(n + helpers)
+    if shape == "dense":
+        M = rng.normal(size=(n, n))
+        A = M @ M.T + n * np.eye(n)
+    else:
+        bw = 120
+        M = np.zeros((n, n))
+        for i in range(n):
+            lo = max(0, i - bw)
+            M[i, lo:i + 1] = rng.normal(size=i + 1 - lo)
+        if shape == "loop":
+            M[n - 120:, :120] = rng.normal(size=(120, 120)) * 0.3
+        A = M @ M.T + n * np.eye(n)
+    A = 0.5 * (A + A.T)
+    b = rng.normal(size=n)
+    x = np.zeros(n)
+    ms = ctypes.c_float(0)
+    rc = L.orbhip_test_cholesky_dag(A.ctypes.data, b.ctypes.data, x.ctypes.data, n, 3, helpers, ctypes.byref(ms),
+                                    None)
+    assert rc == 0
+    ref = np.linalg.solve(A, b)
+    assert np.abs(x - ref).max() <= 1e-11 * np.abs(ref).max()
+
+
+def test_dag_cholesky_non_spd_rejected():
+    """A matrix that is not positive definite: flag 0 (the LM rejects the trial), x = 0."""
+    import ctypes
+    from orb_slam3_ros2_amd._lib import lib
+    L = lib()
+    n = 200
+    rng = np.random.default_rng(5)
+    M = rng.normal(size=(n, n))
+    A = M @ M.T + n * np.eye(n)
+    A[150, 150] = -1e6
+    b = rng.normal(size=n)
+    x = np.ones(n)
+    ms = ctypes.c_float(0)
+    rc = L.orbhip_test_cholesky_dag(A.ctypes.data, b.ctypes.data, x.ctypes.data, n, 1, 0, ctypes.byref(ms), None)
+    assert rc == -4
+    assert not x.any()
+
+
 def test_device_lm_rejections_and_pops(opt, oracle):
     """Runs past convergence (60 iterations): trials get rejected (rho <= 0: lambda grows, the
     pushed state is popped on the device) and the runs stop on rho == 0 at different iterations;
