@@ -40,8 +40,11 @@ struct DagDev {
 
 // S (n x n row-major, lower triangle read, never written), row_first (ceil(n/32): first 32-col
 // tile with a structural non-zero per 32-row tile), bs -> x; flag[0] = 1 ok, 0 on a non-positive
-// pivot (x = 0). gate (optional): returns unless *gate == kPhTrial. dbg (optional, >= 8 + NT
-// u64): the chain's shader-clock phase cycles.
+// pivot (x = 0). gate (optional): returns unless *gate == kPhTrial. dbg (optional, kDbgWords
+// u64): the chain's shader-clock cycles: [0] prologue, [1] forward, [2] backward, [4] diag32 sum,
+// [5] total, then per interval k < 200 six words at 8 + 6k: the interval, phase 1, phase 2, and in
+// phase 3 wave 0 (diag32), wave 1 (publish + next diagonal partial), waves 2/3 (the next tiles).
+constexpr int kDbgWords = 8 + 6 * 200;
 hipError_t chol_dag_solve(const double* S, int n, const int* row_first, const double* bs, double* x, int* flag,
                           const DagDev& d, hipStream_t st, const int* gate = nullptr,
                           unsigned long long* dbg = nullptr);

@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "ba_args.h"
@@ -43,6 +44,10 @@ constexpr int kT = kDagTile;
 constexpr int kTD = kT * kT;            // doubles per tile
 constexpr unsigned kSpinMax = 1u << 19;
 constexpr size_t kMinLds = 84 * 1024;   // > 80 KB: one workgroup per CU
+#ifndef ORBHIP_DAG_NEWTON
+#define ORBHIP_DAG_NEWTON 1
+#endif
+constexpr int kNewton = ORBHIP_DAG_NEWTON;   // Newton steps after v_rsq_f64 in the pivot blocks
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) int gint;
@@ -61,6 +66,7 @@ struct DagK {
     const int* gate;
     unsigned long long* dbg;
     int n, NT, G;
+    int hsleep;   // helpers' poll back-off (units of s_sleep 1)
 };
 
 __device__ __forceinline__ int ld_flag(const int* p) {
@@ -76,6 +82,13 @@ __device__ __forceinline__ void st_sc1(double* p, double v) {
     __hip_atomic_store((gdbl*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// workgroup barrier ordering LDS only: __syncthreads() is a workgroup fence, which on gfx950 also
+// drains vmcnt, i.e. would wait for every wave's outstanding global loads and stores
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
 
 // one quadrant (256 doubles, 4 per lane) at dbl_off of the DAG buffer, sc1 (16-byte accesses)
 __device__ __forceinline__ double4_t qload(__amdgpu_buffer_rsrc_t rs, int dbl_off) {
@@ -162,7 +175,7 @@ __device__ bool wave_wait_all(const int* f, int epoch, int* ctl) {
 }
 // the number m >= 1 of leading entries i < cnt (<= 64) with fa[i] == fb[i] == fc[i] == epoch
 // (fb / fc optional); 0 on abort / timeout (wave-uniform)
-__device__ int wave_wait_prefix(const int* fa, const int* fb, const int* fc, int cnt, int epoch, int* ctl) {
+__device__ int wave_wait_prefix(const int* fa, const int* fb, const int* fc, int cnt, int epoch, int* ctl, int hsleep) {
     const int lane = threadIdx.x & 63;
     for (unsigned spins = 0;; spins++) {
         bool ok = true;
@@ -182,25 +195,26 @@ __device__ int wave_wait_prefix(const int* fa, const int* fb, const int* fc, int
             }
             return 0;
         }
-        __builtin_amdgcn_s_sleep(2);
+        for (int z = 0; z < hsleep; z++) __builtin_amdgcn_s_sleep(1);   // helpers back off
     }
 }
 
 struct Lay {   // offsets (doubles) into the DAG buffer, flags
     int oL, oP, oLi, oY, oR;
-    int *ctl, *fL, *fP0, *fP1, *fCh;
+    int *ctl, *fL, *fP0, *fP1, *fP2, *fCh;
     __device__ Lay(const DagK& a) {
         const int NT = a.NT;
         oL = 0;
         oP = NT * NT * kTD;
-        oLi = oP + 2 * NT * kTD;
+        oLi = oP + 3 * NT * kTD;
         oY = oLi + NT * kTD;
         oR = oY + NT * kT;
         ctl = a.ints;
         fL = ctl + 4;
         fP0 = fL + NT * NT;
         fP1 = fP0 + NT;
-        fCh = fP1 + NT;
+        fP2 = fP1 + NT;
+        fCh = fP2 + NT;
     }
 };
 
@@ -218,7 +232,7 @@ __device__ void dag_helper(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t r
     int wsel = 0;   // rotating LDS word of the poll results
     auto wg_prefix = [&](const int* fa, const int* fb, const int* fc, int cnt) -> int {
         if (wid == 0) {
-            const int m = wave_wait_prefix(fa, fb, fc, cnt, epoch, L.ctl);
+            const int m = wave_wait_prefix(fa, fb, fc, cnt, epoch, L.ctl, a.hsleep);
             if (lane == 0) word[wsel] = m;
         }
         __syncthreads();
@@ -229,8 +243,11 @@ __device__ void dag_helper(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t r
     for (int t = t0; t < t1; t++) {
         const int code = a.tasks[t];
         const int R = code >> 16, C = code & 0xFFFF;
-        const int type = R == C ? 0 : (R == C + 1 ? 1 : 2);   // diag partial, sub-diag partial, full
-        const int ps = max(a.rf[R], a.rf[C]), pe = type == 2 ? C : C - 2;
+        // by R - C: 0 the diagonal partial (columns <= C-3), 1 the sub-diagonal partial (<= C-3), 2
+        // the second sub-diagonal's partial (<= C-2), >= 3 a full tile (every column, then the TRSM)
+        const int dRC = R - C;
+        const int type = dRC >= 3 ? 2 : (dRC == 0 ? 0 : 1);
+        const int ps = max(a.rf[R], a.rf[C]), pe = dRC >= 3 ? C : (dRC == 2 ? C - 1 : C - 2);
         double4_t acc = s_quad(a.S, a.n, R, C, rq, cq);
         const bool rhs = type == 0 && cq == 0;
         const bool skip = type == 0 && quad == 1;   // the upper quadrant of a diagonal tile: unused
@@ -278,9 +295,9 @@ __device__ void dag_helper(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t r
             qstore(rs, L.oL + (R * NT + C) * kTD + quad * 256, out);
             target = L.fL + R * NT + C;
         } else {
-            qstore(rs, L.oP + (type == 0 ? C : NT + C) * kTD + quad * 256, acc);
+            qstore(rs, L.oP + (dRC * NT + C) * kTD + quad * 256, acc);
             if (rhs && rg == 0) st_sc1(a.buf + L.oR + C * kT + 16 * rq + cc, rv);
-            target = (type == 0 ? L.fP0 : L.fP1) + C;
+            target = (dRC == 0 ? L.fP0 : (dRC == 1 ? L.fP1 : L.fP2)) + C;
         }
         drain_stores();
         __syncthreads();
@@ -294,8 +311,8 @@ __device__ void dag_helper(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t r
 // wave 0: Linv of the diagonal tile in Dx into Lin, y = Linv r into y (32)
 __device__ __forceinline__ bool chain_factor(const double* Dx, double* scr, double* Lin, const double* rvec,
                                              double* y) {
-    const bool ok = diag32_linv([&](int r, int c) { return Dx[qidx(r, c)]; }, scr,
-                                [&](int r, int c, double v) { Lin[qidx(r, c)] = v; });
+    const bool ok = diag32_linv<kNewton>([&](int r, int c) { return Dx[qidx(r, c)]; }, scr,
+                                         [&](int r, int c, double v) { Lin[qidx(r, c)] = v; });
     wave_lds_sync();
     const int lane = threadIdx.x & 63, i = lane >> 1, hh = lane & 1;
     double s = 0.0;
@@ -322,17 +339,21 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, cc = lane & 15, rg = lane >> 4;
     const int rq = wid >> 1, cq = wid & 1, quad = 2 * rq + cq;
     const int NT = a.NT, n = a.n;
-    double* Lin = lds;                  // Linv_k (quadrant layout)
-    double* Lsub = lds + 2048;          // L(k+1, k)
-    double* Tx = lds + 3072;            // the sub-diagonal tile of the next TRSM
-    double* Dx = lds + 4096;            // the diagonal tile to factor
-    double* Dp = lds + 5120;            // the next diagonal tile, all but its last column
-    int* word = (int*)(lds + 6144);     // [0..3] poll results, [4] prep abort, [5] row poll, [8] ok
-    double* scr = lds + 6160;           // diag32 scratch (512)
+    // double buffers by base arithmetic (an array of LDS pointers selected at run time loses the
+    // address space: flat accesses, which wait on vmcnt too)
+    //   lds + 1024 p: Linv_k (p = k & 1); lds + 2048 + 1024 c1: L(k, k-1) / the new L(k+1, k);
+    //   lds + 4096 + 1024 c2: L(k+1, k-1) / the new L(k+2, k)
+    double* Tp = lds + 6144;            // T'_k: tile (k+1, k) with columns <= k-2 applied
+    double* Tx = lds + 7168;            // exchange tile
+    double* Dp = lds + 8192;            // D'_{k+1}: diagonal tile k+1 with columns <= k-2 applied
+    double* Dx = lds + 9216;            // the diagonal tile to factor
+    int* word = (int*)(lds + 10240);    // [0..3] poll results, [4] abort, [5] row polls ok, [8] ok
+    double* scr = lds + 10256;          // diag32 scratch (512)
     double* rvec = scr + 512;           // 32
-    double* rpp = rvec + 32;            // 32: the next rhs, all but its last column
+    double* rpp = rvec + 32;            // 32: rhs of D'
     double* ys = rpp + 32;              // NT x 32: y_k; in the backward the running sums s_k
     double* xs = ys + NT * kT;          // NT x 32
+    int* rfl = (int*)(xs + NT * kT);    // row_first (NT ints)
     unsigned long long* dbg = a.dbg;
     const unsigned long long t_start = dbg ? __builtin_amdgcn_s_memtime() : 0;
     unsigned long long t_fact = 0;
@@ -341,145 +362,210 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         word[4] = 0;
         word[5] = 1;
     }
-    // Prep of interval K (waves 1..3, while wave 0 factors): the sub-diagonal tile (K+1, K) with
-    // columns K-2 and K-1 (T, into Tx), the diagonal tile K+1 with column K-1 (into Dp) and its rhs
-    // (rpp). Each wave polls the flags of the tiles it reads itself. False on abort.
-    auto prep = [&](int K) -> bool {
-        const int K1 = K + 1;
-        const int rfa = a.rf[K1], rfb = a.rf[K];
-        const bool inEnv = rfa <= K;
-        const bool needP1 = inEnv && max(rfa, rfb) <= K - 3;
-        const bool needP0 = rfa <= K - 2;
-        const int pA = K - 2, pB = K - 1;
-        const bool useA = inEnv && pA >= max(rfa, rfb);
-        const bool useBs = inEnv && pB >= max(rfa, rfb);
-        const bool useBd = pB >= rfa;
-        const int* f = nullptr;
-        if (lane == 0 && needP1) f = L.fP1 + K;
-        if (lane == 1 && needP0) f = L.fP0 + K1;
-        if (lane == 2 && useA) f = L.fL + K1 * NT + pA;
-        if (lane == 3 && useA) f = L.fL + K * NT + pA;
-        if (lane == 4 && useBd) f = L.fL + K1 * NT + pB;
-        if (!wave_wait_all(f, epoch, L.ctl)) return false;
-        const int tA1 = L.oL + (K1 * NT + pA) * kTD, tA0 = L.oL + (K * NT + pA) * kTD;
-        const int tB = L.oL + (K1 * NT + pB) * kTD;
-        auto tjob = [&](int qr, int qc) {
-            double4_t T = {0, 0, 0, 0};
-            if (inEnv) {
-                T = needP1 ? qload(rs, L.oP + (NT + K) * kTD + (2 * qr + qc) * 256) : s_quad(a.S, n, K1, K, qr, qc);
-                if (useA) {
-                    mfma_sub(T, qload(rs, tA0 + (2 * qc) * 256), qload(rs, tA1 + (2 * qr) * 256));
-                    mfma_sub(T, qload(rs, tA0 + (2 * qc + 1) * 256), qload(rs, tA1 + (2 * qr + 1) * 256));
-                }
-                if (useBs) {
-                    mfma_sub(T, lq(Lsub + (2 * qc) * 256), qload(rs, tB + (2 * qr) * 256));
-                    mfma_sub(T, lq(Lsub + (2 * qc + 1) * 256), qload(rs, tB + (2 * qr + 1) * 256));
-                }
-            }
-            sq(Tx + (2 * qr + qc) * 256, T);
-        };
-        auto djob = [&](int qr, int qc) {
-            double4_t D = needP0 ? qload(rs, L.oP + K1 * kTD + (2 * qr + qc) * 256) : s_quad(a.S, n, K1, K1, qr, qc);
-            double r = 0.0;
-            if (qc == 0) {
-                const int i = kT * K1 + 16 * qr + cc;
-                r = needP0 ? ld_sc1(a.buf + L.oR + K1 * kT + 16 * qr + cc) : (i < n ? a.bs[i] : 0.0);
-            }
-            if (useBd) {
-                const double4_t l0 = qload(rs, tB + (2 * qr) * 256), l1 = qload(rs, tB + (2 * qr + 1) * 256);
-                mfma_sub(D, qload(rs, tB + (2 * qc) * 256), l0);
-                mfma_sub(D, qload(rs, tB + (2 * qc + 1) * 256), l1);
-                if (qc == 0) r -= lmul_ylds(l0, ys + pB * kT) + lmul_ylds(l1, ys + pB * kT + 16);
-            }
-            sq(Dp + (2 * qr + qc) * 256, D);
-            if (qc == 0 && rg == 0) rpp[16 * qr + cc] = r;
-        };
-        if (wid == 2) {
-            tjob(0, 0);
-            tjob(0, 1);
-            djob(0, 0);
-        } else if (wid == 3) {
-            tjob(1, 0);
-            tjob(1, 1);
-            djob(1, 1);
-        } else {
-            djob(1, 0);
-        }
-        return true;
-    };
-    // ---- prologue: factor the diagonal tile 0 (wave 0) while waves 1..3 prepare interval 0 ----
+    for (int i = tid; i < NT; i += blockDim.x) rfl[i] = a.rf[i];
+    int c1 = 0, c2 = 0;   // current L1 / L2 buffers
+    // ---- prologue: factor tile 0 (wave 0); T'_0 = A(1, 0), D'_1 = A(1, 1), L1 = L2 = 0 ----
     sq(Dx + quad * 256, s_quad(a.S, n, 0, 0, rq, cq));
+    sq(lds + 2048 + quad * 256, double4_t{0, 0, 0, 0});
+    sq(lds + 4096 + quad * 256, double4_t{0, 0, 0, 0});
+    if (NT > 1) {
+        sq(Tp + quad * 256, a.rf[1] <= 0 ? s_quad(a.S, n, 1, 0, rq, cq) : double4_t{0, 0, 0, 0});
+        sq(Dp + quad * 256, s_quad(a.S, n, 1, 1, rq, cq));
+        if (cq == 0 && rg == 0) {
+            const int i = kT + 16 * rq + cc;
+            rpp[16 * rq + cc] = i < n ? a.bs[i] : 0.0;
+        }
+    }
     if (tid < kT) rvec[tid] = tid < n ? a.bs[tid] : 0.0;
     __syncthreads();
-    if (wid == 0) ok = chain_factor(Dx, scr, Lin, rvec, ys);
-    else if (NT > 1 && !prep(0) && lane == 0) word[4] = 1;
+    if (wid == 0) ok = chain_factor(Dx, scr, lds, rvec, ys);
     __syncthreads();
     if (dbg && tid == 0) dbg[0] = __builtin_amdgcn_s_memtime() - t_start;
-    // ---- intervals: TRSM | SYRK | diag32 (wave 0) beside the publish and the next prep ----
+    // ---- interval k: phase 1 L(k+1, k) = (T'_k - L(k+1,k-1) L(k,k-1)^T) Linv_k^T; phase 2 the
+    // diagonal tile k+1's last two columns and its rhs; phase 3 wave 0 factors it, wave 1
+    // publishes and loads D'_{k+2}, waves 2 / 3 form row 0 / 1 of L(k+2, k) and of T'_{k+1} ----
     for (int k = 0; k + 1 < NT; k++) {
         const unsigned long long tk = dbg ? __builtin_amdgcn_s_memtime() : 0;
-        if (word[4]) {
-            aborted = true;
-            break;
+        const int k1 = k + 1, K2 = k + 2;
+        double* Lin = lds + 1024 * (k & 1);
+        double* LinN = lds + 1024 * (k1 & 1);
+        double* L1 = lds + 2048 + 1024 * c1;
+        double* L1n = lds + 2048 + 1024 * (c1 ^ 1);
+        double* L2 = lds + 4096 + 1024 * c2;
+        double* L2n = lds + 4096 + 1024 * (c2 ^ 1);
+        const int rfa = rfl[k1], rfb = rfl[k];
+        const bool inEnv1 = rfa <= k;
+        const bool useT2 = k - 1 >= max(rfa, rfb);
+        const bool useD2 = k - 1 >= rfa;
+        // the flags waves 2 / 3 need in phase 3, loaded now (in flight through phases 1 and 2)
+        const int rfc = K2 < NT ? rfl[K2] : 0;
+        const bool inEnvU = K2 < NT && rfc <= k, inEnvT = K2 < NT && rfc <= k1;
+        const bool needP2 = K2 < NT && max(rfc, rfb) <= k - 2, useU = K2 < NT && k - 1 >= max(rfc, rfb);
+        const bool needP1 = K2 < NT && max(rfc, rfa) <= k - 2, useTp = K2 < NT && k - 1 >= max(rfc, rfa);
+        const bool needP0 = K2 < NT && rfc <= K2 - 3;
+        const int* f3 = nullptr;
+        if (wid >= 2) {
+            if (lane == 0 && needP2) f3 = L.fP2 + k;
+            if (lane == 1 && (useU || useTp)) f3 = L.fL + K2 * NT + k - 1;
+            if (lane == 2 && needP1) f3 = L.fP1 + k1;
+            if (lane == 3 && needP0) f3 = L.fP0 + K2;
         }
-        const int k1 = k + 1;
-        const bool inEnv = a.rf[k1] <= k;
-        // phase 1: wave 1 issues the publish of Linv_k and y_k; every wave one quadrant of
-        // L(k+1, k) = T Linv_k^T
+        const bool need3 = f3 != nullptr;
+        const int fv = ld_flag(need3 ? f3 : L.ctl);   // unconditional: its wait lands at the use in phase 3
+        // wave 1 issues the publish of L(k+1, k-1) and Linv_k, y_k (drained in phase 3)
         if (wid == 1) {
+            if (k >= 1) {
+#pragma unroll
+                for (int qd = 0; qd < 4; qd++) qstore(rs, L.oL + (k1 * NT + k - 1) * kTD + qd * 256, lq(L2 + qd * 256));
+            }
 #pragma unroll
             for (int qd = 0; qd < 4; qd++) qstore(rs, L.oLi + k * kTD + qd * 256, lq(Lin + qd * 256));
             if (lane < kT) st_sc1(a.buf + L.oY + k * kT + lane, ys[k * kT + lane]);
         }
-        double4_t Ln = {0, 0, 0, 0};
-        if (inEnv) {
-            panel_add(Ln, lq(Lin + (2 * cq) * 256), lq(Tx + (2 * rq) * 256));
-            if (cq == 1) panel_add(Ln, lq(Lin + 3 * 256), lq(Tx + (2 * rq + 1) * 256));
+        // phase 1
+        double4_t T = lq(Tp + quad * 256);
+        if (useT2) {   // two independent MFMA chains
+            double4_t T2 = {0, 0, 0, 0};
+            mfma_sub(T, lq(L1 + (2 * cq) * 256), lq(L2 + (2 * rq) * 256));
+            mfma_sub(T2, lq(L1 + (2 * cq + 1) * 256), lq(L2 + (2 * rq + 1) * 256));
+            T += T2;
         }
-        sq(Lsub + quad * 256, Ln);
-        __syncthreads();
-        // phase 2: the diagonal tile's last column (waves 0, 2, 3: the lower quadrants)
+        sq(Tx + quad * 256, T);
+        lds_barrier();
+        double4_t Ln = {0, 0, 0, 0};
+        if (inEnv1) {
+            panel_add(Ln, lq(Lin + (2 * cq) * 256), lq(Tx + (2 * rq) * 256));
+            if (cq == 1) {
+                double4_t L2c = {0, 0, 0, 0};
+                panel_add(L2c, lq(Lin + 3 * 256), lq(Tx + (2 * rq + 1) * 256));
+                Ln += L2c;
+            }
+        }
+        sq(L1n + quad * 256, Ln);
+        lds_barrier();
+        const unsigned long long tp1 = dbg ? __builtin_amdgcn_s_memtime() : 0;
+        // phase 2 (waves 0, 2, 3: the lower quadrants)
         if (wid != 1) {
             double4_t D = lq(Dp + quad * 256);
+            double4_t D1 = {0, 0, 0, 0}, D2 = {0, 0, 0, 0}, D3 = {0, 0, 0, 0};   // independent chains
             double r = cq == 0 ? rpp[16 * rq + cc] : 0.0;
-            if (inEnv) {
-                const double4_t l0 = lq(Lsub + (2 * rq) * 256), l1 = lq(Lsub + (2 * rq + 1) * 256);
-                mfma_sub(D, lq(Lsub + (2 * cq) * 256), l0);
-                mfma_sub(D, lq(Lsub + (2 * cq + 1) * 256), l1);
+            if (useD2) {
+                const double4_t l0 = lq(L2 + (2 * rq) * 256), l1 = lq(L2 + (2 * rq + 1) * 256);
+                mfma_sub(D2, lq(L2 + (2 * cq) * 256), l0);
+                mfma_sub(D3, lq(L2 + (2 * cq + 1) * 256), l1);
+                if (cq == 0) r -= lmul_ylds(l0, ys + (k - 1) * kT) + lmul_ylds(l1, ys + (k - 1) * kT + 16);
+            }
+            if (inEnv1) {
+                const double4_t l0 = lq(L1n + (2 * rq) * 256), l1 = lq(L1n + (2 * rq + 1) * 256);
+                mfma_sub(D, lq(L1n + (2 * cq) * 256), l0);
+                mfma_sub(D1, lq(L1n + (2 * cq + 1) * 256), l1);
                 if (cq == 0) r -= lmul_ylds(l0, ys + k * kT) + lmul_ylds(l1, ys + k * kT + 16);
             }
+            D += (D1 + D2) + D3;
             sq(Dx + quad * 256, D);
             if (cq == 0 && rg == 0) rvec[16 * rq + cc] = r;
-        }
-        __syncthreads();
-        // phase 3: wave 0 factors tile k+1; wave 1 publishes L(k+1, k), then waves 1..3 prepare
-        // interval k+1
-        const unsigned long long tf = dbg ? __builtin_amdgcn_s_memtime() : 0;
-        if (wid == 0) {
-            ok = chain_factor(Dx, scr, Lin, rvec, ys + k1 * kT) && ok;
-            if (dbg) t_fact += __builtin_amdgcn_s_memtime() - tf;
-        } else {
-            if (wid == 1) {   // L(k+1, k); then both publishes are drained and flagged
+        } else {   // wave 1: the publish of L(k+1, k)
 #pragma unroll
-                for (int qd = 0; qd < 4; qd++) qstore(rs, L.oL + (k1 * NT + k) * kTD + qd * 256, lq(Lsub + qd * 256));
-                drain_stores();
-                if (lane == 0) {
-                    st_flag(L.fCh + k, epoch);
-                    st_flag(L.fL + k1 * NT + k, epoch);
-                }
-            }
-            if (k1 + 1 < NT && !prep(k1) && lane == 0) word[4] = 1;
+            for (int qd = 0; qd < 4; qd++) qstore(rs, L.oL + (k1 * NT + k) * kTD + qd * 256, lq(L1n + qd * 256));
         }
-        __syncthreads();
-        if (dbg && tid == 0 && k < 256) dbg[8 + k] = __builtin_amdgcn_s_memtime() - tk;
+        lds_barrier();
+        // phase 3
+        const unsigned long long tf = dbg ? __builtin_amdgcn_s_memtime() : 0;
+        unsigned long long* wts = (unsigned long long*)word + 8;   // per-wave phase-3 cycles (dbg)
+        if (wid == 0) {
+            ok = chain_factor(Dx, scr, LinN, rvec, ys + k1 * kT) && ok;
+            if (dbg) t_fact += __builtin_amdgcn_s_memtime() - tf;
+        } else if (wid == 1) {   // the publishes of this interval complete: drain, then the flags
+            drain_stores();
+            if (lane == 0) {
+                st_flag(L.fCh + k, epoch);
+                st_flag(L.fL + k1 * NT + k, epoch);
+                if (k >= 1) st_flag(L.fL + k1 * NT + k - 1, epoch);
+            }
+        } else if (K2 < NT) {
+            // waves 2 / 3: row h of L(k+2, k) = U Linv_k^T, U = A(k+2, k) - sum_{p <= k-1}
+            // L(k+2,p) L(k,p)^T (the helpers' partial: p <= k-2; here p = k-1), and row h of
+            // T'_{k+1} = A(k+2, k+1) - sum_{p <= k-1} L(k+2,p) L(k+1,p)^T (partial p <= k-2)
+            const int h = wid - 2;
+            if (!__all(!need3 || fv == epoch) && !wave_wait_all(f3, epoch, L.ctl)) {
+                if (lane == 0) word[4] = 1;
+            } else {
+                const int tD = L.oL + (K2 * NT + k - 1) * kTD;
+                double4_t d0 = {0, 0, 0, 0}, d1 = {0, 0, 0, 0};
+                if (useU || useTp) {
+                    d0 = qload(rs, tD + (2 * h) * 256);
+                    d1 = qload(rs, tD + (2 * h + 1) * 256);
+                }
+                // D'_{k+2}: the helpers' partial (columns <= k-1) or A(k+2, k+2), and its rhs; wave 2
+                // the quadrant (0, 0) and rows 0..15, wave 3 (1, 0), (1, 1) and rows 16..31
+#pragma unroll
+                for (int qd = 2 * h; qd <= 2 * h + h; qd++)
+                    if (qd != 1)
+                        sq(Dp + qd * 256, needP0 ? qload(rs, L.oP + K2 * kTD + qd * 256) : s_quad(a.S, n, K2, K2, qd >> 1, qd & 1));
+                if (lane < 16) {
+                    const int i = kT * K2 + 16 * h + lane;
+                    rpp[16 * h + lane] = needP0 ? ld_sc1(a.buf + L.oR + K2 * kT + 16 * h + lane) : (i < n ? a.bs[i] : 0.0);
+                }
+                double4_t u[2], t[2];
+#pragma unroll
+                for (int c = 0; c < 2; c++) {
+                    u[c] = !inEnvU ? double4_t{0, 0, 0, 0}
+                                   : (needP2 ? qload(rs, L.oP + (2 * NT + k) * kTD + (2 * h + c) * 256)
+                                             : s_quad(a.S, n, K2, k, h, c));
+                    t[c] = !inEnvT ? double4_t{0, 0, 0, 0}
+                                   : (needP1 ? qload(rs, L.oP + (NT + k1) * kTD + (2 * h + c) * 256)
+                                             : s_quad(a.S, n, K2, k1, h, c));
+                }
+                double4_t o0 = {0, 0, 0, 0}, o1 = {0, 0, 0, 0};
+                if (inEnvU) {
+                    if (useU) {
+#pragma unroll
+                        for (int c = 0; c < 2; c++) {
+                            mfma_sub(u[c], lq(L1 + (2 * c) * 256), d0);
+                            mfma_sub(u[c], lq(L1 + (2 * c + 1) * 256), d1);
+                        }
+                    }
+                    panel_add(o0, lq(Lin), u[0]);
+                    panel_add(o1, lq(Lin + 2 * 256), u[0]);
+                    panel_add(o1, lq(Lin + 3 * 256), u[1]);
+                }
+                sq(L2n + (2 * h) * 256, o0);
+                sq(L2n + (2 * h + 1) * 256, o1);
+                if (inEnvT && useTp) {
+#pragma unroll
+                    for (int c = 0; c < 2; c++) {
+                        mfma_sub(t[c], lq(L2 + (2 * c) * 256), d0);
+                        mfma_sub(t[c], lq(L2 + (2 * c + 1) * 256), d1);
+                    }
+                }
+                sq(Tp + (2 * h) * 256, t[0]);
+                sq(Tp + (2 * h + 1) * 256, t[1]);
+            }
+        }
+        if (dbg && lane == 0) wts[wid] = __builtin_amdgcn_s_memtime() - tf;
+        lds_barrier();
+        c1 ^= 1;
+        c2 ^= 1;
+        if (dbg && tid == 0 && k < 200) {
+            unsigned long long* dk = dbg + 8 + 6 * k;
+            dk[0] = __builtin_amdgcn_s_memtime() - tk;
+            dk[1] = tp1 - tk;
+            dk[2] = tf - tp1;
+            dk[3] = wts[0];
+            dk[4] = wts[1];
+            dk[5] = std::max(wts[2], wts[3]);
+        }
+        if (word[4]) {
+            aborted = true;
+            break;
+        }
     }
-    if (word[4]) aborted = true;
     const unsigned long long t_fwd = dbg ? __builtin_amdgcn_s_memtime() : 0;
+    double* Lin = lds + 1024 * ((NT - 1) & 1);
     // ---- backward, right-looking by rows: at step R (x_R known) wave 0 forms x_{R-1} from the
     // sub-diagonal tile (R, R-1) and s_{R-1}; waves 1..3 subtract row R's other tiles from the
-    // running sums s_j, j <= R-2. Wave 0's inputs (chain-published) and the first tiles of each
-    // wave's next row are loaded a step ahead; wave 1 polls the helper tiles of row R-2 during
-    // step R. ----
+    // running sums s_j, j <= R-2. The helper tiles' flags are polled once, up front; wave 0's
+    // inputs and the first tiles of each wave's next row are loaded a step ahead. ----
     auto apply_lt = [&](int k) {   // wave 0: xs_k = Linv^T rvec (Linv in Lin)
         const int c = lane >> 1, hh = lane & 1;
         double s = 0.0;
@@ -488,16 +574,18 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         s += dpp64<0xB1>(s);
         if (hh == 0) xs[k * kT + c] = s;
     };
-    auto row_poll = [&](int R) -> bool {   // wave 1: the helper tiles (R, j), j <= R - 2
-        bool good = true;
-        for (int j0 = a.rf[R]; j0 <= R - 2 && good; j0 += 64) {
-            const int j = j0 + lane;
-            good = wave_wait_all(j <= R - 2 ? L.fL + R * NT + j : nullptr, epoch, L.ctl);
+    auto sub_tile = [&](const double4_t* tl, const double* xR, int j) {   // s_j -= L(R, j)^T x_R
+        double t[2][4];
+        tile_lt_x(tl, xR, t);
+        if (cc == 0) {
+#pragma unroll
+            for (int b = 0; b < 2; b++)
+#pragma unroll
+                for (int q = 0; q < 4; q++) ys[j * kT + 16 * b + rg + 4 * q] -= t[b][q];
         }
-        return good;
     };
     double4_t st[4], sn[4], li[4];   // wave 0: tile (R, R-1) now / next, Linv_{R-1}
-    constexpr int kPf = 3;           // waves 1..3: tiles of a row prefetched a step ahead
+    constexpr int kPf = 3;           // waves 1..3: tiles of a row loaded a step ahead
     double4_t pf[kPf][4], pn[kPf][4];
     if (!aborted) {
         if (wid == 0) {
@@ -511,14 +599,43 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                     li[qd] = qload(rs, L.oLi + (NT - 2) * kTD + qd * 256);
                 }
             }
-        } else if (wid == 1 && NT >= 2) {
-            const bool g = row_poll(NT - 1) && (NT < 3 || row_poll(NT - 2));
-            if (lane == 0) word[5] = g ? 1 : 0;
+        } else {
+            // every tile (R, j), j <= R-2, rows 2.. (16 rows of this wave per round: up to 32
+            // flag loads in flight per lane)
+            bool good = true;
+            for (int R0 = 1 + wid; R0 < NT && good; R0 += 48) {
+                for (unsigned spins = 0;; spins++) {
+                    int okl = 1;
+#pragma unroll
+                    for (int u = 0; u < 16; u++) {
+                        const int R = R0 + 3 * u;
+                        if (R < NT) {
+                            const int rfR = rfl[R];
+#pragma unroll
+                            for (int hh = 0; hh < 2; hh++) {
+                                const int j = rfR + 64 * hh + lane;
+                                if (j <= R - 2) okl &= ld_flag(L.fL + R * NT + j) == epoch ? 1 : 0;
+                            }
+                        }
+                    }
+                    if (__all(okl)) break;
+                    if (ld_flag(L.ctl + 2) == epoch || spins >= kSpinMax) {
+                        if (spins >= kSpinMax && lane == 0) {
+                            st_flag(L.ctl + 2, epoch);
+                            __hip_atomic_fetch_add((gint*)(L.ctl + 3), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        }
+                        good = false;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+            if (!good && lane == 0) word[5] = 0;
         }
         __syncthreads();
         if (!word[5]) aborted = true;
         if (wid != 0 && !aborted && NT >= 2) {   // row NT-1's first tiles
-            const int R = NT - 1, jn = a.rf[R] + (wid - 1);
+            const int R = NT - 1, jn = rfl[R] + (wid - 1);
 #pragma unroll
             for (int u = 0; u < kPf; u++)
                 if (jn + 3 * u <= R - 2) {
@@ -544,7 +661,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                         rvec[c] = ys[(R - 1) * kT + c] - t[b][q];
                     }
             }
-            if (R >= 2) {   // prefetch step R-1's inputs
+            if (R >= 2) {   // step R-1's inputs
 #pragma unroll
                 for (int qd = 0; qd < 4; qd++) {
                     sn[qd] = qload(rs, L.oL + ((R - 1) * NT + R - 2) * kTD + qd * 256);
@@ -556,12 +673,11 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
 #pragma unroll
             for (int qd = 0; qd < 4; qd++) st[qd] = sn[qd];
         } else {
-            // row R's helper tiles (R, j), j in [rf[R], R-2], dealt over waves 1..3 (j = rf[R] +
-            // wid - 1 + 3 i); the first kPf of this wave were loaded during the previous step, the
-            // next row's are issued now (their flags were polled two steps ahead)
-            const int j0 = a.rf[R] + (wid - 1);
+            // row R's tiles (R, j), j in [rf[R], R-2], j = rf[R] + wid - 1 + 3 i: the first kPf
+            // came a step ahead, the next row's are issued now, the rest four at a time
+            const int j0 = rfl[R] + (wid - 1);
             if (R >= 2) {
-                const int jn = a.rf[R - 1] + (wid - 1);
+                const int jn = rfl[R - 1] + (wid - 1);
 #pragma unroll
                 for (int u = 0; u < kPf; u++)
                     if (jn + 3 * u <= R - 3) {
@@ -573,39 +689,26 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             for (int u = 0; u < kPf; u++) {
                 const int j = j0 + 3 * u;
                 if (j > R - 2) break;
-                double t[2][4];
-                tile_lt_x(pf[u], xR, t);
-                if (cc == 0) {
-#pragma unroll
-                    for (int b = 0; b < 2; b++)
-#pragma unroll
-                        for (int q = 0; q < 4; q++) ys[j * kT + 16 * b + rg + 4 * q] -= t[b][q];
-                }
+                sub_tile(pf[u], xR, j);
             }
-            for (int j = j0 + 3 * kPf; j <= R - 2; j += 3) {   // long rows: the rest on demand
-                double4_t tl[4];
+            for (int jb = j0 + 3 * kPf; jb <= R - 2; jb += 12) {
+                double4_t tl[4][4];
 #pragma unroll
-                for (int qd = 0; qd < 4; qd++) tl[qd] = qload(rs, L.oL + (R * NT + j) * kTD + qd * 256);
-                double t[2][4];
-                tile_lt_x(tl, xR, t);
-                if (cc == 0) {
+                for (int u = 0; u < 4; u++)
+                    if (jb + 3 * u <= R - 2) {
 #pragma unroll
-                    for (int b = 0; b < 2; b++)
+                        for (int qd = 0; qd < 4; qd++) tl[u][qd] = qload(rs, L.oL + (R * NT + jb + 3 * u) * kTD + qd * 256);
+                    }
 #pragma unroll
-                        for (int q = 0; q < 4; q++) ys[j * kT + 16 * b + rg + 4 * q] -= t[b][q];
-                }
+                for (int u = 0; u < 4; u++)
+                    if (jb + 3 * u <= R - 2) sub_tile(tl[u], xR, jb + 3 * u);
             }
 #pragma unroll
             for (int u = 0; u < kPf; u++)
 #pragma unroll
                 for (int qd = 0; qd < 4; qd++) pf[u][qd] = pn[u][qd];
-            if (wid == 1 && R >= 3) {
-                const bool g = row_poll(R - 2);
-                if (lane == 0) word[5] = g ? 1 : 0;
-            }
         }
-        __syncthreads();
-        if (!word[5]) aborted = true;
+        lds_barrier();   // LDS only: the next step's tiles stay in flight
     }
     if (wid == 0 && lane == 0) word[8] = (ok && !aborted) ? 1 : 0;
     __syncthreads();
@@ -628,7 +731,7 @@ __global__ __launch_bounds__(256) void k_chol_dag(DagK a) {
     const Lay L(a);
     // epoch of this solve: the counter the last workgroup of the previous solve advanced
     const int epoch = ld_flag(L.ctl) + 1;
-    const size_t bytes = ((size_t)a.NT * a.NT + 3 * (size_t)a.NT) * kTD * 8 + (size_t)a.NT * 64 * 8;
+    const size_t bytes = ((size_t)a.NT * a.NT + 4 * (size_t)a.NT) * kTD * 8 + (size_t)a.NT * 64 * 8;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.buf, 0, (int)bytes, 0x00020000);
     if (blockIdx.x == 0) dag_chain(a, L, rs, epoch, lds);
     else dag_helper(a, L, rs, epoch, lds);
@@ -645,7 +748,7 @@ __global__ __launch_bounds__(256) void k_chol_dag(DagK a) {
 }
 
 size_t dag_lds_bytes(int NT) {
-    const size_t need = sizeof(double) * (6160 + 512 + 64 + 2 * (size_t)NT * kT);
+    const size_t need = sizeof(double) * (10256 + 512 + 64 + 2 * (size_t)NT * kT) + sizeof(int) * NT;
     return std::max(need, kMinLds);
 }
 
@@ -665,26 +768,32 @@ int dag_max_helpers() {
 
 size_t dag_doubles(int n) {
     const size_t NT = (n + kT - 1) / kT;
-    return (NT * NT + 3 * NT) * kTD + NT * 64;
+    return (NT * NT + 4 * NT) * kTD + NT * 64;
 }
 size_t dag_ints(int n) {
     const size_t NT = (n + kT - 1) / kT;
-    return (4 + NT * NT + 3 * NT + 3) & ~size_t(3);
+    return (4 + NT * NT + 4 * NT + 3) & ~size_t(3);
 }
 
 void dag_plan(const int* rf, int n, int max_helpers, DagPlan& p) {
     const int NT = (n + kT - 1) / kT;
     p.NT = NT;
+    // dependency keys (x20; the chain's interval k publishes at 20k + 6 and waits for the
+    // helpers at 20k + 8): every task waits only on smaller keys, so each helper running its
+    // tasks in key order with the whole grid resident cannot deadlock
     struct Task { int key, R, C; };
     std::vector<Task> ts;
     for (int R = 0; R < NT; R++)
         for (int C = rf[R]; C <= R; C++) {
-            if (R == C) {
-                if (rf[R] <= C - 3) ts.push_back({10 * C - 29, R, C});             // diagonal partial
-            } else if (R == C + 1) {
-                if (std::max(rf[R], rf[C]) <= C - 3) ts.push_back({10 * C - 29, R, C});   // sub-diagonal partial
+            const int d = R - C;
+            if (d == 0) {
+                if (rf[R] <= C - 3) ts.push_back({20 * C - 50, R, C});                            // diagonal partial
+            } else if (d == 1) {
+                if (std::max(rf[R], rf[C]) <= C - 3) ts.push_back({20 * C - 50, R, C});           // sub-diagonal partial
+            } else if (d == 2) {
+                if (std::max(rf[R], rf[C]) <= C - 2) ts.push_back({20 * C - 10, R, C});           // second sub-diagonal
             } else {
-                ts.push_back({10 * C - 3, R, C});                                 // full tile
+                ts.push_back({20 * C + 7, R, C});                                                  // full tile
             }
         }
     std::sort(ts.begin(), ts.end(), [](const Task& x, const Task& y) {
@@ -715,6 +824,8 @@ hipError_t chol_dag_solve(const double* S, int n, const int* row_first, const do
     a.S = S; a.bs = bs; a.x = x; a.flag = flag; a.rf = row_first;
     a.buf = d.buf; a.ints = d.ints; a.toff = d.toff; a.tasks = d.tasks; a.gate = gate; a.dbg = dbg;
     a.n = n; a.NT = (n + kT - 1) / kT; a.G = d.G;
+    static const int hs = std::getenv("ORBHIP_DAG_SLEEP") ? std::atoi(std::getenv("ORBHIP_DAG_SLEEP")) : 6;
+    a.hsleep = hs;
     hipLaunchKernelGGL(k_chol_dag, dim3((unsigned)(d.G + 1)), dim3(256), dag_lds_bytes(a.NT), st, a);
     return hipGetLastError();
 }
@@ -750,7 +861,7 @@ int chol_dag_test(const double* A, const double* b, double* x, int n, int reps, 
     ok(hipMalloc((void**)&drf, sizeof(int) * nt));
     ok(hipMalloc((void**)&dtoff, sizeof(int) * plan.toff.size()));
     ok(hipMalloc((void**)&dtasks, sizeof(int) * std::max<size_t>(1, plan.tasks.size())));
-    if (dbg) ok(hipMalloc((void**)&ddbg, sizeof(unsigned long long) * (8 + 256)));
+    if (dbg) ok(hipMalloc((void**)&ddbg, sizeof(unsigned long long) * kDbgWords));
     if (rc == 0) {
         ok(hipMemset(dints, 0, sizeof(int) * dag_ints(n)));
         ok(hipMemset(dflag, 0, 4 * sizeof(int)));
@@ -760,7 +871,7 @@ int chol_dag_test(const double* A, const double* b, double* x, int n, int reps, 
         ok(hipMemcpy(dtoff, plan.toff.data(), sizeof(int) * plan.toff.size(), hipMemcpyHostToDevice));
         if (!plan.tasks.empty())
             ok(hipMemcpy(dtasks, plan.tasks.data(), sizeof(int) * plan.tasks.size(), hipMemcpyHostToDevice));
-        if (ddbg) ok(hipMemset(ddbg, 0, sizeof(unsigned long long) * (8 + 256)));
+        if (ddbg) ok(hipMemset(ddbg, 0, sizeof(unsigned long long) * kDbgWords));
         const DagDev d{dbuf, dints, dtoff, dtasks, plan.G};
         ok(chol_dag_solve(dS, n, drf, db, dx, dflag, d, nullptr, nullptr, nullptr));   // warm-up
         ok(hipDeviceSynchronize());
@@ -778,7 +889,7 @@ int chol_dag_test(const double* A, const double* b, double* x, int n, int reps, 
         ok(hipMemcpy(&f, dflag, sizeof(int), hipMemcpyDeviceToHost));
         ok(hipMemcpy(ctl, dints, 4 * sizeof(int), hipMemcpyDeviceToHost));
         ok(hipMemcpy(x, dx, sizeof(double) * n, hipMemcpyDeviceToHost));
-        if (ddbg) ok(hipMemcpy(dbg, ddbg, sizeof(unsigned long long) * (8 + 256), hipMemcpyDeviceToHost));
+        if (ddbg) ok(hipMemcpy(dbg, ddbg, sizeof(unsigned long long) * kDbgWords, hipMemcpyDeviceToHost));
         if (rc == 0 && ctl[3] != 0) rc = -5;
         if (rc == 0 && f == 0) rc = -4;
         (void)hipEventDestroy(e0);

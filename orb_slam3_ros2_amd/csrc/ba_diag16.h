@@ -26,17 +26,18 @@
 
 namespace orbhip {
 
-__device__ __forceinline__ double rsq_nr(double a) {   // 1/sqrt(a): rsq + two Newton steps
+template <int NR = 2>
+__device__ __forceinline__ double rsq_nr(double a) {   // 1/sqrt(a): rsq + NR Newton steps
     double s = __builtin_amdgcn_rsq(a);
-    s = s * fma(-0.5 * a * s, s, 1.5);
-    s = s * fma(-0.5 * a * s, s, 1.5);
+#pragma unroll
+    for (int i = 0; i < NR; i++) s = s * fma(-0.5 * a * s, s, 1.5);
     return s;
 }
 
 // Factor the tile d (C layout, both triangles) of one wave: writes Linv row by row through
 // store(r, c, v) (r = J + rg, c = cc: lane (cc, rg) stores Linv[J + rg][cc] once per pivot step,
 // every lane every step) and returns false in every lane on a non-positive-definite pivot block.
-template <typename Store>
+template <int NR = 2, typename Store>
 __device__ __forceinline__ bool diag16_linv(double4_t d, Store&& store) {
     const int lane = threadIdx.x & 63, cc = lane & 15, rg = lane >> 4;
     double4_t xv;
@@ -58,22 +59,22 @@ __device__ __forceinline__ bool diag16_linv(double4_t d, Store&& store) {
                      b33 = readlane_f64(d[p], J + 51);
         // C = chol(B), r_i = 1 / C_ii
         ok = ok && b00 > 0.0;
-        const double r0 = rsq_nr(b00 > 0.0 ? b00 : 1.0);
+        const double r0 = rsq_nr<NR>(b00 > 0.0 ? b00 : 1.0);
         const double l10 = b10 * r0, l20 = b20 * r0, l30 = b30 * r0;
         const double s11 = fma(-l10, l10, b11);
         ok = ok && s11 > 0.0;
-        const double r1 = rsq_nr(s11 > 0.0 ? s11 : 1.0);
+        const double r1 = rsq_nr<NR>(s11 > 0.0 ? s11 : 1.0);
         const double t21 = fma(-l20, l10, b21), t31 = fma(-l30, l10, b31);
         const double u22 = fma(-l20, l20, b22), u32 = fma(-l30, l20, b32), u33 = fma(-l30, l30, b33);
         const double l21 = t21 * r1, l31 = t31 * r1;
         const double s22 = fma(-l21, l21, u22);
         ok = ok && s22 > 0.0;
-        const double r2 = rsq_nr(s22 > 0.0 ? s22 : 1.0);
+        const double r2 = rsq_nr<NR>(s22 > 0.0 ? s22 : 1.0);
         const double v33 = fma(-l31, l31, u33);
         const double l32 = fma(-l31, l21, u32) * r2;
         const double s33 = fma(-l32, l32, v33);
         ok = ok && s33 > 0.0;
-        const double r3 = rsq_nr(s33 > 0.0 ? s33 : 1.0);
+        const double r3 = rsq_nr<NR>(s33 > 0.0 ? s33 : 1.0);
         // Ci = C^-1 (lower): Ci_ii = r_i, Ci_ij = -r_i sum_{j<=k<i} l_ik Ci_kj
         const double c10 = -r1 * (l10 * r0);
         const double c21 = -r2 * (l21 * r1);
@@ -113,7 +114,7 @@ __device__ __forceinline__ bool diag16_linv(double4_t d, Store&& store) {
 // D21 Linv11^T, D22 -= L21 L21^T, Linv22 = diag16(D22), Linv21 = -Linv22 L21 Linv11 (MFMA).
 // store(r, c, v) receives every entry of Linv once (the zero upper blocks included); scratch: 512
 // doubles of LDS. Returns false on a non-positive-definite pivot block.
-template <typename Elem, typename Store>
+template <int NR = 2, typename Elem, typename Store>
 __device__ __forceinline__ bool diag32_linv(Elem&& elem, double* __restrict__ scratch, Store&& store) {
     const int lane = threadIdx.x & 63, cc = lane & 15, rg = lane >> 4;
     double4_t d11, d21t, d22;
@@ -127,7 +128,7 @@ __device__ __forceinline__ bool diag32_linv(Elem&& elem, double* __restrict__ sc
     double* op11 = scratch;         // Linv11, operand order
     double* op22 = scratch + 256;   // Linv22, operand order
     double4_t lin11;                // Linv11 in the C layout
-    const bool ok1 = diag16_linv(d11, [&](int r, int c, double v) {
+    const bool ok1 = diag16_linv<NR>(d11, [&](int r, int c, double v) {
         op11[(r + 16 * (c & 3)) * 4 + (c >> 2)] = v;
         lin11[r >> 2] = v;
         store(r, c, v);
@@ -141,7 +142,7 @@ __device__ __forceinline__ bool diag32_linv(Elem&& elem, double* __restrict__ sc
     for (int kk = 0; kk < 4; kk++) l21t = __builtin_amdgcn_mfma_f64_16x16x4f64(a11[kk], d21t[kk], l21t, 0, 0, 0);
 #pragma unroll
     for (int kk = 0; kk < 4; kk++) d22 = __builtin_amdgcn_mfma_f64_16x16x4f64(-l21t[kk], l21t[kk], d22, 0, 0, 0);
-    const bool ok2 = diag16_linv(d22, [&](int r, int c, double v) {
+    const bool ok2 = diag16_linv<NR>(d22, [&](int r, int c, double v) {
         op22[(r + 16 * (c & 3)) * 4 + (c >> 2)] = v;
         store(16 + r, 16 + c, v);
     });

@@ -28,6 +28,9 @@ def spd(n, shape, rng):
 
 
 L = lib()
+if os.environ.get("ORBHIP_PROBE_LIB"):   # an alternative build of the library (A/B of a compile-time switch)
+    L = ctypes.CDLL(os.environ["ORBHIP_PROBE_LIB"])
+    L.orbhip_test_cholesky_dag.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 + [ctypes.c_void_p] * 2
 cases = [a.split(":") for a in (sys.argv[1:] or ["31:dense", "100:dense", "294:dense", "600:band", "2394:loop", "2394:dense"])]
 for n_s, shape in cases:
     n = int(n_s)
@@ -37,15 +40,16 @@ for n_s, shape in cases:
     b = rng.normal(size=n)
     x = np.zeros(n)
     ms = ctypes.c_float(0)
-    dbg = np.zeros(8 + 256, np.uint64)
+    dbg = np.zeros(8 + 6 * 200, np.uint64)
     t0 = time.time()
-    rc = L.orbhip_test_cholesky_dag(A.ctypes.data, b.ctypes.data, x.ctypes.data, n, 10, 0, ctypes.byref(ms),
+    rc = L.orbhip_test_cholesky_dag(A.ctypes.data, b.ctypes.data, x.ctypes.data, n, 10, int(os.environ.get('ORBHIP_DAG_HELPERS', '0')), ctypes.byref(ms),
                                     dbg.ctypes.data)
     ref = np.linalg.solve(A, b)
     err = np.abs(x - ref).max() / np.abs(ref).max()
     nt = (n + 31) // 32
-    ks = dbg[8:8 + nt - 1]
+    ki = max(0, min(nt - 1, 200))
+    ph = dbg[8:8 + 6 * ki].reshape(ki, 6).astype(np.int64) if ki else np.zeros((1, 6), np.int64)
+    med = np.median(ph, axis=0).astype(int) if ki else [0] * 6
     print(f"n={n} {shape}: rc={rc} dag {ms.value * 1e3:.1f} us relerr={err:.2e} | cycles prologue={dbg[0]} "
-          f"forward={dbg[1]} backward={dbg[2]} waits={dbg[3]} diag={dbg[4]} total={dbg[5]} | interval "
-          f"min/med/max {ks.min() if len(ks) else 0}/{int(np.median(ks)) if len(ks) else 0}/{ks.max() if len(ks) else 0} "
-          f"({time.time() - t0:.1f}s)", flush=True)
+          f"forward={dbg[1]} backward={dbg[2]} diag={dbg[4]} total={dbg[5]} | interval medians: total {med[0]} "
+          f"ph1 {med[1]} ph2 {med[2]} ph3 w0 {med[3]} w1 {med[4]} w23 {med[5]} ({time.time() - t0:.1f}s)", flush=True)
