@@ -59,6 +59,8 @@ struct BaArgs {
     const int* fin; int nfin;
     double* Spart;
     LmCtl* ctl;        // device-driven solve: this problem's LM state (nullptr: host-driven rounds)
+    double* part;      // workgroup partial sums of a trial: chi2 (npart_e = ceil(E / 256)), then the
+    int npart_e, npart_m;   // landmark scale terms (npart_m = ceil(M / 256))
 };
 
 }  // namespace orbhip

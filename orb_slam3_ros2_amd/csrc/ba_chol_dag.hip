@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <utility>
 #include <vector>
 
 #include "ba_args.h"
@@ -297,7 +298,7 @@ __device__ void dag_helper(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t r
         } else {
             qstore(rs, L.oP + (dRC * NT + C) * kTD + quad * 256, acc);
             if (rhs && rg == 0) st_sc1(a.buf + L.oR + C * kT + 16 * rq + cc, rv);
-            target = (dRC == 0 ? L.fP0 : (dRC == 1 ? L.fP1 : L.fP2)) + C;
+            target = L.fP0 + dRC * NT + C;   // fP0, fP1, fP2 are consecutive rows of NT
         }
         drain_stores();
         __syncthreads();
@@ -335,25 +336,86 @@ __device__ __forceinline__ void tile_lt_x(const double4_t* t, const double* x, d
         for (int q = 0; q < 4; q++) out[b][q] = row16_sum(fma(t[b][q], x0, t[2 + b][q] * x1));
 }
 
+// wave-level helpers of the chain's 32x32 diagonal factorization, split at its two 16x16 pivots
+// (the diag32_linv steps of ba_diag16.h, with the second pivot's inputs handed in by wave 1):
+// part A: Linv11 of D11 (registers, C layout) into quadrant 0 of Lq (and zeros into quadrant 1),
+// returns Linv11 in the C layout (lin11)
+__device__ __forceinline__ bool diag_part_a(const double4_t& d11, double* Lq, double4_t& lin11) {
+    return diag16_linv<kNewton>(d11, [&](int r, int c, double v) {
+        Lq[qidx(r, c)] = v;
+        Lq[qidx(r, 16 + c)] = 0.0;
+        lin11[r >> 2] = v;
+    });
+}
+// part B: from D21^T (quadrant (1, 0) registers) and D22: L21 = D21 Linv11^T (returned as L21^T in
+// the C layout), D22 -= L21 L21^T, Linv22 into quadrant 3, Linv21 = -Linv22 L21 Linv11 into
+// quadrant 2
+__device__ __forceinline__ bool diag_part_b(const double4_t& d21t, double4_t d22, const double4_t& lin11, double* Lq,
+                                            double4_t& l21t) {
+    const int lane = threadIdx.x & 63, cc = lane & 15, rg = lane >> 4;
+    const double* a11 = Lq + lane * 4;   // quadrant 0 in operand order
+    l21t = double4_t{0, 0, 0, 0};
+#pragma unroll
+    for (int kk = 0; kk < 4; kk++) l21t = __builtin_amdgcn_mfma_f64_16x16x4f64(a11[kk], d21t[kk], l21t, 0, 0, 0);
+#pragma unroll
+    for (int kk = 0; kk < 4; kk++) d22 = __builtin_amdgcn_mfma_f64_16x16x4f64(-l21t[kk], l21t[kk], d22, 0, 0, 0);
+    double* op22 = Lq + 3 * 256;
+    const bool ok2 = diag16_linv<kNewton>(d22, [&](int r, int c, double v) { op22[(r + 16 * (c & 3)) * 4 + (c >> 2)] = v; });
+    double4_t w = {0, 0, 0, 0};
+#pragma unroll
+    for (int kk = 0; kk < 4; kk++) w = __builtin_amdgcn_mfma_f64_16x16x4f64(l21t[kk], lin11[kk], w, 0, 0, 0);
+    wave_lds_sync();
+    const double* a22 = op22 + lane * 4;
+    double4_t l21i = {0, 0, 0, 0};
+#pragma unroll
+    for (int kk = 0; kk < 4; kk++) l21i = __builtin_amdgcn_mfma_f64_16x16x4f64(-a22[kk], w[kk], l21i, 0, 0, 0);
+#pragma unroll
+    for (int q = 0; q < 4; q++) Lq[qidx(16 + rg + 4 * q, cc)] = l21i[q];
+    return ok2;
+}
+// y[i] = sum_c Li[i][c] r[c] over one 16x16 quadrant of Lq (rows and columns from 0); every lane
+// returns the value of row lane & 15
+__device__ __forceinline__ double quad_matvec(const double* Lq, int qd, const double* r) {
+    const int lane = threadIdx.x & 63, i = lane & 15, g = lane >> 4;
+    double s = 0.0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int c = 4 * g + j;   // element (i, c) of the quadrant: lane i + 16 (c & 3), component c >> 2
+        s = fma(Lq[qd * 256 + (i + 16 * (c & 3)) * 4 + (c >> 2)], r[c], s);
+    }
+    return col4_sum(s);
+}
+__device__ __forceinline__ void lds_signal(int* w, int v) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_wait(int* w, int v) {
+    while (__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
 __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs, int epoch, double* lds) {
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, cc = lane & 15, rg = lane >> 4;
     const int rq = wid >> 1, cq = wid & 1, quad = 2 * rq + cq;
     const int NT = a.NT, n = a.n;
-    // double buffers by base arithmetic (an array of LDS pointers selected at run time loses the
-    // address space: flat accesses, which wait on vmcnt too)
-    //   lds + 1024 p: Linv_k (p = k & 1); lds + 2048 + 1024 c1: L(k, k-1) / the new L(k+1, k);
-    //   lds + 4096 + 1024 c2: L(k+1, k-1) / the new L(k+2, k)
-    double* Tp = lds + 6144;            // T'_k: tile (k+1, k) with columns <= k-2 applied
-    double* Tx = lds + 7168;            // exchange tile
-    double* Dp = lds + 8192;            // D'_{k+1}: diagonal tile k+1 with columns <= k-2 applied
-    double* Dx = lds + 9216;            // the diagonal tile to factor
-    int* word = (int*)(lds + 10240);    // [0..3] poll results, [4] abort, [5] row polls ok, [8] ok
-    double* scr = lds + 10256;          // diag32 scratch (512)
-    double* rvec = scr + 512;           // 32
-    double* rpp = rvec + 32;            // 32: rhs of D'
-    double* ys = rpp + 32;              // NT x 32: y_k; in the backward the running sums s_k
+    // LDS (doubles), double buffers by base arithmetic (an array of LDS pointers selected at run
+    // time loses the address space: flat accesses, which wait on vmcnt too):
+    //   [0, 2048)      Linv_k by parity p = k & 1
+    //   [2048, 4096)   L1: L(k, k-1) / the new L(k+1, k)        (c1)
+    //   [4096, 6144)   L2: L(k+1, k-1) / the new L(k+2, k)      (c2)
+    //   [6144, 8192)   Tp: T_k, tile (k+1, k) with every column < k applied (parity)
+    //   [8192, 10240)  Dp: D'_{k+1} (quadrants 0, 3: columns <= k-1 applied; 2: <= k-2) (parity)
+    //   [10240, 11264) Dq: D(1,0), D(1,1) of tile k+1, wave 1 -> wave 0 (quadrants 2, 3)
+    int* word = (int*)(lds + 11264);    // [4] abort, [5] row polls ok, [8] ok, [10..12] wave flags
+    double* rvec = lds + 11280;         // 32: r0 (wave 0), r1 (wave 1 -> wave 0)
+    double* rppB = rvec + 32;           // 2 x 32: rhs of D' (parity)
+    double* ys = rppB + 64;             // NT x 32: y_k; in the backward the running sums s_k
     double* xs = ys + NT * kT;          // NT x 32
     int* rfl = (int*)(xs + NT * kT);    // row_first (NT ints)
+    int* F1 = word + 10;                // wave 0: row 0 of L(k+1, k) ready (k + 2)
+    int* F2 = word + 11;                // wave 1: D(1,0), D(1,1), r1 of tile k+1 ready
+    int* F3 = word + 12;                // wave 1: row 1 of L(k+1, k) ready
+    unsigned long long* wts = (unsigned long long*)(lds + 11264 + 8);   // per-wave cycles (dbg)
     unsigned long long* dbg = a.dbg;
     const unsigned long long t_start = dbg ? __builtin_amdgcn_s_memtime() : 0;
     unsigned long long t_fact = 0;
@@ -361,47 +423,69 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     if (tid == 0) {
         word[4] = 0;
         word[5] = 1;
+        *F1 = 0;
+        *F2 = 0;
+        *F3 = 0;
     }
     for (int i = tid; i < NT; i += blockDim.x) rfl[i] = a.rf[i];
-    int c1 = 0, c2 = 0;   // current L1 / L2 buffers
-    // ---- prologue: factor tile 0 (wave 0); T'_0 = A(1, 0), D'_1 = A(1, 1), L1 = L2 = 0 ----
-    sq(Dx + quad * 256, s_quad(a.S, n, 0, 0, rq, cq));
+    int c1 = 0, c2 = 0;
+    // ---- prologue: wave 0 factors tile 0; T_0 = A(1, 0), D'_1 = A(1, 1), L1 = L2 = 0 ----
     sq(lds + 2048 + quad * 256, double4_t{0, 0, 0, 0});
     sq(lds + 4096 + quad * 256, double4_t{0, 0, 0, 0});
     if (NT > 1) {
-        sq(Tp + quad * 256, a.rf[1] <= 0 ? s_quad(a.S, n, 1, 0, rq, cq) : double4_t{0, 0, 0, 0});
-        sq(Dp + quad * 256, s_quad(a.S, n, 1, 1, rq, cq));
+        sq(lds + 6144 + quad * 256, a.rf[1] <= 0 ? s_quad(a.S, n, 1, 0, rq, cq) : double4_t{0, 0, 0, 0});
+        sq(lds + 8192 + quad * 256, s_quad(a.S, n, 1, 1, rq, cq));
         if (cq == 0 && rg == 0) {
             const int i = kT + 16 * rq + cc;
-            rpp[16 * rq + cc] = i < n ? a.bs[i] : 0.0;
+            rppB[16 * rq + cc] = i < n ? a.bs[i] : 0.0;
         }
     }
     if (tid < kT) rvec[tid] = tid < n ? a.bs[tid] : 0.0;
     __syncthreads();
-    if (wid == 0) ok = chain_factor(Dx, scr, lds, rvec, ys);
+    if (wid == 0) {
+        double4_t lin11, l21t;
+        ok = diag_part_a(s_quad(a.S, n, 0, 0, 0, 0), lds, lin11);
+        wave_lds_sync();
+        const double y0 = quad_matvec(lds, 0, rvec);
+        if (rg == 0) ys[cc] = y0;
+        ok = diag_part_b(s_quad(a.S, n, 0, 0, 1, 0), s_quad(a.S, n, 0, 0, 1, 1), lin11, lds, l21t) && ok;
+        wave_lds_sync();
+        const double r1 = rvec[16 + cc] - lmul_ylds(l21t, ys);
+        wave_lds_sync();
+        if (rg == 0) rvec[16 + cc] = r1;
+        wave_lds_sync();
+        const double y1 = quad_matvec(lds, 3, rvec + 16);
+        if (rg == 0) ys[16 + cc] = y1;
+    }
     __syncthreads();
     if (dbg && tid == 0) dbg[0] = __builtin_amdgcn_s_memtime() - t_start;
-    // ---- interval k: phase 1 L(k+1, k) = (T'_k - L(k+1,k-1) L(k,k-1)^T) Linv_k^T; phase 2 the
-    // diagonal tile k+1's last two columns and its rhs; phase 3 wave 0 factors it, wave 1
-    // publishes and loads D'_{k+2}, waves 2 / 3 form row 0 / 1 of L(k+2, k) and of T'_{k+1} ----
+    // ---- interval k: wave 0 the critical path (row 0 of L(k+1, k), D(0,0), its pivot, then D22's
+    // after wave 1's row 1 / D(1,*)); wave 1 row 1 and the publishes; waves 2 / 3 row h of
+    // L(k+2, k), of T_{k+1} and of D'_{k+2} ----
     for (int k = 0; k + 1 < NT; k++) {
         const unsigned long long tk = dbg ? __builtin_amdgcn_s_memtime() : 0;
-        const int k1 = k + 1, K2 = k + 2;
-        double* Lin = lds + 1024 * (k & 1);
-        double* LinN = lds + 1024 * (k1 & 1);
+        const int k1 = k + 1, K2 = k + 2, cur = k & 1, nxt = cur ^ 1;
+        double* Lin = lds + 1024 * cur;
+        double* LinN = lds + 1024 * nxt;
         double* L1 = lds + 2048 + 1024 * c1;
         double* L1n = lds + 2048 + 1024 * (c1 ^ 1);
         double* L2 = lds + 4096 + 1024 * c2;
         double* L2n = lds + 4096 + 1024 * (c2 ^ 1);
+        double* Tp = lds + 6144 + 1024 * cur;
+        double* TpN = lds + 6144 + 1024 * nxt;
+        double* Dp = lds + 8192 + 1024 * cur;
+        double* DpN = lds + 8192 + 1024 * nxt;
+        double* Dq = lds + 10240;
+        double* rp = rppB + 32 * cur;
+        double* rpN = rppB + 32 * nxt;
         const int rfa = rfl[k1], rfb = rfl[k];
         const bool inEnv1 = rfa <= k;
-        const bool useT2 = k - 1 >= max(rfa, rfb);
         const bool useD2 = k - 1 >= rfa;
-        // the flags waves 2 / 3 need in phase 3, loaded now (in flight through phases 1 and 2)
         const int rfc = K2 < NT ? rfl[K2] : 0;
         const bool inEnvU = K2 < NT && rfc <= k, inEnvT = K2 < NT && rfc <= k1;
         const bool needP2 = K2 < NT && max(rfc, rfb) <= k - 2, useU = K2 < NT && k - 1 >= max(rfc, rfb);
         const bool needP1 = K2 < NT && max(rfc, rfa) <= k - 2, useTp = K2 < NT && k - 1 >= max(rfc, rfa);
+        const bool useTk = inEnvU && inEnv1;   // T_{k+1} -= L(k+2, k) L(k+1, k)^T
         const bool needP0 = K2 < NT && rfc <= K2 - 3;
         const int* f3 = nullptr;
         if (wid >= 2) {
@@ -411,9 +495,93 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             if (lane == 3 && needP0) f3 = L.fP0 + K2;
         }
         const bool need3 = f3 != nullptr;
-        const int fv = ld_flag(need3 ? f3 : L.ctl);   // unconditional: its wait lands at the use in phase 3
-        // wave 1 issues the publish of L(k+1, k-1) and Linv_k, y_k (drained in phase 3)
-        if (wid == 1) {
+        const int fv = ld_flag(need3 ? f3 : L.ctl);   // in flight until its use below
+        if (wid == 0) {
+            if (dbg && lane == 0) wts[6] = __builtin_amdgcn_s_memtime() - tk;
+            // row 0 of L(k+1, k) = T Linv_k^T
+            double4_t l0 = {0, 0, 0, 0}, l1 = {0, 0, 0, 0};
+            if (inEnv1) {
+                const double4_t t0 = lq(Tp), t1 = lq(Tp + 256);
+                double4_t l1b = {0, 0, 0, 0};
+                panel_add(l0, lq(Lin), t0);
+                panel_add(l1, lq(Lin + 2 * 256), t0);
+                panel_add(l1b, lq(Lin + 3 * 256), t1);
+                l1 += l1b;
+            }
+            sq(L1n, l0);
+            sq(L1n + 256, l1);
+            lds_signal(F1, k + 2);
+            // D(0,0) and r0 of tile k+1
+            double4_t D = lq(Dp);
+            double r0 = rp[cc];
+            if (inEnv1) {
+                double4_t Db = {0, 0, 0, 0};
+                mfma_sub(D, l0, l0);
+                mfma_sub(Db, l1, l1);
+                D += Db;
+                r0 -= lmul_ylds(l0, ys + k * kT) + lmul_ylds(l1, ys + k * kT + 16);
+            }
+            if (rg == 0) rvec[cc] = r0;
+            const unsigned long long tf = dbg ? __builtin_amdgcn_s_memtime() : 0;
+            if (dbg && lane == 0) wts[7] = tf - tk;
+            double4_t lin11, l21t;
+            ok = diag_part_a(D, LinN, lin11) && ok;
+            wave_lds_sync();
+            const double y0 = quad_matvec(LinN, 0, rvec);
+            if (rg == 0) ys[k1 * kT + cc] = y0;
+            const unsigned long long tw0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
+            lds_wait(F2, k + 2);
+            if (dbg && lane == 0) wts[5] = __builtin_amdgcn_s_memtime() - tw0;
+            ok = diag_part_b(lq(Dq + 2 * 256), lq(Dq + 3 * 256), lin11, LinN, l21t) && ok;
+            wave_lds_sync();
+            const double r1 = rvec[16 + cc] - lmul_ylds(l21t, ys + k1 * kT);
+            wave_lds_sync();
+            if (rg == 0) rvec[16 + cc] = r1;
+            wave_lds_sync();
+            const double y1 = quad_matvec(LinN, 3, rvec + 16);
+            if (rg == 0) ys[k1 * kT + 16 + cc] = y1;
+            if (dbg) t_fact += __builtin_amdgcn_s_memtime() - tf;
+        } else if (wid == 1) {
+            // row 1 of L(k+1, k)
+            double4_t l0 = {0, 0, 0, 0}, l1 = {0, 0, 0, 0};
+            if (inEnv1) {
+                const double4_t t0 = lq(Tp + 2 * 256), t1 = lq(Tp + 3 * 256);
+                double4_t l1b = {0, 0, 0, 0};
+                panel_add(l0, lq(Lin), t0);
+                panel_add(l1, lq(Lin + 2 * 256), t0);
+                panel_add(l1b, lq(Lin + 3 * 256), t1);
+                l1 += l1b;
+            }
+            sq(L1n + 2 * 256, l0);
+            sq(L1n + 3 * 256, l1);
+            lds_signal(F3, k + 2);
+            // D(1,0), D(1,1), r1 of tile k+1
+            double4_t D10 = lq(Dp + 2 * 256), D11 = lq(Dp + 3 * 256);
+            double r1 = rp[16 + cc];
+            lds_wait(F1, k + 2);
+            if (useD2) {   // the column k-1 term of D(1,0) (the other quadrants had theirs applied)
+                double4_t Db = {0, 0, 0, 0};
+                mfma_sub(D10, lq(L2), lq(L2 + 2 * 256));
+                mfma_sub(Db, lq(L2 + 256), lq(L2 + 3 * 256));
+                D10 += Db;
+            }
+            if (inEnv1) {
+                double4_t Db = {0, 0, 0, 0}, Dc = {0, 0, 0, 0};
+                mfma_sub(D10, lq(L1n), l0);
+                mfma_sub(Db, lq(L1n + 256), l1);
+                mfma_sub(D11, l0, l0);
+                mfma_sub(Dc, l1, l1);
+                D10 += Db;
+                D11 += Dc;
+                r1 -= lmul_ylds(l0, ys + k * kT) + lmul_ylds(l1, ys + k * kT + 16);
+            }
+            sq(Dq + 2 * 256, D10);
+            sq(Dq + 3 * 256, D11);
+            if (rg == 0) rvec[16 + cc] = r1;
+            lds_signal(F2, k + 2);
+            // publish L(k+1, k), L(k+1, k-1), Linv_k, y_k
+#pragma unroll
+            for (int qd = 0; qd < 4; qd++) qstore(rs, L.oL + (k1 * NT + k) * kTD + qd * 256, lq(L1n + qd * 256));
             if (k >= 1) {
 #pragma unroll
                 for (int qd = 0; qd < 4; qd++) qstore(rs, L.oL + (k1 * NT + k - 1) * kTD + qd * 256, lq(L2 + qd * 256));
@@ -421,61 +589,6 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
 #pragma unroll
             for (int qd = 0; qd < 4; qd++) qstore(rs, L.oLi + k * kTD + qd * 256, lq(Lin + qd * 256));
             if (lane < kT) st_sc1(a.buf + L.oY + k * kT + lane, ys[k * kT + lane]);
-        }
-        // phase 1
-        double4_t T = lq(Tp + quad * 256);
-        if (useT2) {   // two independent MFMA chains
-            double4_t T2 = {0, 0, 0, 0};
-            mfma_sub(T, lq(L1 + (2 * cq) * 256), lq(L2 + (2 * rq) * 256));
-            mfma_sub(T2, lq(L1 + (2 * cq + 1) * 256), lq(L2 + (2 * rq + 1) * 256));
-            T += T2;
-        }
-        sq(Tx + quad * 256, T);
-        lds_barrier();
-        double4_t Ln = {0, 0, 0, 0};
-        if (inEnv1) {
-            panel_add(Ln, lq(Lin + (2 * cq) * 256), lq(Tx + (2 * rq) * 256));
-            if (cq == 1) {
-                double4_t L2c = {0, 0, 0, 0};
-                panel_add(L2c, lq(Lin + 3 * 256), lq(Tx + (2 * rq + 1) * 256));
-                Ln += L2c;
-            }
-        }
-        sq(L1n + quad * 256, Ln);
-        lds_barrier();
-        const unsigned long long tp1 = dbg ? __builtin_amdgcn_s_memtime() : 0;
-        // phase 2 (waves 0, 2, 3: the lower quadrants)
-        if (wid != 1) {
-            double4_t D = lq(Dp + quad * 256);
-            double4_t D1 = {0, 0, 0, 0}, D2 = {0, 0, 0, 0}, D3 = {0, 0, 0, 0};   // independent chains
-            double r = cq == 0 ? rpp[16 * rq + cc] : 0.0;
-            if (useD2) {
-                const double4_t l0 = lq(L2 + (2 * rq) * 256), l1 = lq(L2 + (2 * rq + 1) * 256);
-                mfma_sub(D2, lq(L2 + (2 * cq) * 256), l0);
-                mfma_sub(D3, lq(L2 + (2 * cq + 1) * 256), l1);
-                if (cq == 0) r -= lmul_ylds(l0, ys + (k - 1) * kT) + lmul_ylds(l1, ys + (k - 1) * kT + 16);
-            }
-            if (inEnv1) {
-                const double4_t l0 = lq(L1n + (2 * rq) * 256), l1 = lq(L1n + (2 * rq + 1) * 256);
-                mfma_sub(D, lq(L1n + (2 * cq) * 256), l0);
-                mfma_sub(D1, lq(L1n + (2 * cq + 1) * 256), l1);
-                if (cq == 0) r -= lmul_ylds(l0, ys + k * kT) + lmul_ylds(l1, ys + k * kT + 16);
-            }
-            D += (D1 + D2) + D3;
-            sq(Dx + quad * 256, D);
-            if (cq == 0 && rg == 0) rvec[16 * rq + cc] = r;
-        } else {   // wave 1: the publish of L(k+1, k)
-#pragma unroll
-            for (int qd = 0; qd < 4; qd++) qstore(rs, L.oL + (k1 * NT + k) * kTD + qd * 256, lq(L1n + qd * 256));
-        }
-        lds_barrier();
-        // phase 3
-        const unsigned long long tf = dbg ? __builtin_amdgcn_s_memtime() : 0;
-        unsigned long long* wts = (unsigned long long*)word + 8;   // per-wave phase-3 cycles (dbg)
-        if (wid == 0) {
-            ok = chain_factor(Dx, scr, LinN, rvec, ys + k1 * kT) && ok;
-            if (dbg) t_fact += __builtin_amdgcn_s_memtime() - tf;
-        } else if (wid == 1) {   // the publishes of this interval complete: drain, then the flags
             drain_stores();
             if (lane == 0) {
                 st_flag(L.fCh + k, epoch);
@@ -483,9 +596,10 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 if (k >= 1) st_flag(L.fL + k1 * NT + k - 1, epoch);
             }
         } else if (K2 < NT) {
-            // waves 2 / 3: row h of L(k+2, k) = U Linv_k^T, U = A(k+2, k) - sum_{p <= k-1}
-            // L(k+2,p) L(k,p)^T (the helpers' partial: p <= k-2; here p = k-1), and row h of
-            // T'_{k+1} = A(k+2, k+1) - sum_{p <= k-1} L(k+2,p) L(k+1,p)^T (partial p <= k-2)
+            // row h of L(k+2, k) = U Linv_k^T, U = A(k+2, k) - sum_{p <= k-1} L(k+2,p) L(k,p)^T (the
+            // helpers' partial: p <= k-2; here p = k-1); row h of T_{k+1} = A(k+2, k+1) - sum_{p <= k}
+            // L(k+2,p) L(k+1,p)^T (partial p <= k-2; p = k-1 and p = k here); D'_{k+2} (partial
+            // p <= k-1; p = k here, quadrant (1,0)'s by wave 1 in the next interval) and its rhs
             const int h = wid - 2;
             if (!__all(!need3 || fv == epoch) && !wave_wait_all(f3, epoch, L.ctl)) {
                 if (lane == 0) word[4] = 1;
@@ -496,17 +610,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                     d0 = qload(rs, tD + (2 * h) * 256);
                     d1 = qload(rs, tD + (2 * h + 1) * 256);
                 }
-                // D'_{k+2}: the helpers' partial (columns <= k-1) or A(k+2, k+2), and its rhs; wave 2
-                // the quadrant (0, 0) and rows 0..15, wave 3 (1, 0), (1, 1) and rows 16..31
-#pragma unroll
-                for (int qd = 2 * h; qd <= 2 * h + h; qd++)
-                    if (qd != 1)
-                        sq(Dp + qd * 256, needP0 ? qload(rs, L.oP + K2 * kTD + qd * 256) : s_quad(a.S, n, K2, K2, qd >> 1, qd & 1));
-                if (lane < 16) {
-                    const int i = kT * K2 + 16 * h + lane;
-                    rpp[16 * h + lane] = needP0 ? ld_sc1(a.buf + L.oR + K2 * kT + 16 * h + lane) : (i < n ? a.bs[i] : 0.0);
-                }
-                double4_t u[2], t[2];
+                double4_t u[2], t[2], dd[2];
 #pragma unroll
                 for (int c = 0; c < 2; c++) {
                     u[c] = !inEnvU ? double4_t{0, 0, 0, 0}
@@ -515,45 +619,84 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                     t[c] = !inEnvT ? double4_t{0, 0, 0, 0}
                                    : (needP1 ? qload(rs, L.oP + (NT + k1) * kTD + (2 * h + c) * 256)
                                              : s_quad(a.S, n, K2, k1, h, c));
+                    const int qd = 2 * h + c;   // D' quadrants: wave 2 q0, wave 3 q2 and q3
+                    dd[c] = (h == 0 && c == 1) ? double4_t{0, 0, 0, 0}
+                                               : (needP0 ? qload(rs, L.oP + K2 * kTD + qd * 256)
+                                                         : s_quad(a.S, n, K2, K2, qd >> 1, qd & 1));
+                }
+                double rr = 0.0;
+                {
+                    const int i = kT * K2 + 16 * h + cc;
+                    rr = needP0 ? ld_sc1(a.buf + L.oR + K2 * kT + 16 * h + cc) : (i < n ? a.bs[i] : 0.0);
                 }
                 double4_t o0 = {0, 0, 0, 0}, o1 = {0, 0, 0, 0};
                 if (inEnvU) {
                     if (useU) {
 #pragma unroll
                         for (int c = 0; c < 2; c++) {
+                            double4_t ub = {0, 0, 0, 0};
                             mfma_sub(u[c], lq(L1 + (2 * c) * 256), d0);
-                            mfma_sub(u[c], lq(L1 + (2 * c + 1) * 256), d1);
+                            mfma_sub(ub, lq(L1 + (2 * c + 1) * 256), d1);
+                            u[c] += ub;
                         }
                     }
+                    double4_t o1b = {0, 0, 0, 0};
                     panel_add(o0, lq(Lin), u[0]);
                     panel_add(o1, lq(Lin + 2 * 256), u[0]);
-                    panel_add(o1, lq(Lin + 3 * 256), u[1]);
+                    panel_add(o1b, lq(Lin + 3 * 256), u[1]);
+                    o1 += o1b;
                 }
                 sq(L2n + (2 * h) * 256, o0);
                 sq(L2n + (2 * h + 1) * 256, o1);
                 if (inEnvT && useTp) {
 #pragma unroll
                     for (int c = 0; c < 2; c++) {
+                        double4_t tb = {0, 0, 0, 0};
                         mfma_sub(t[c], lq(L2 + (2 * c) * 256), d0);
-                        mfma_sub(t[c], lq(L2 + (2 * c + 1) * 256), d1);
+                        mfma_sub(tb, lq(L2 + (2 * c + 1) * 256), d1);
+                        t[c] += tb;
                     }
                 }
-                sq(Tp + (2 * h) * 256, t[0]);
-                sq(Tp + (2 * h + 1) * 256, t[1]);
+                if (inEnvU) {   // D'_{k+2} -= L(k+2,k)_h L(k+2,k)_h^T (the diagonal quadrant of row h)
+                    const int c = h;   // wave 2: q0 (c = 0); wave 3: q3 (c = 1)
+                    double4_t db = {0, 0, 0, 0};
+                    mfma_sub(dd[c], o0, o0);
+                    mfma_sub(db, o1, o1);
+                    dd[c] += db;
+                    rr -= lmul_ylds(o0, ys + k * kT) + lmul_ylds(o1, ys + k * kT + 16);
+                }
+                if (h == 0) {
+                    sq(DpN, dd[0]);
+                } else {
+                    sq(DpN + 2 * 256, dd[0]);
+                    sq(DpN + 3 * 256, dd[1]);
+                }
+                if (rg == 0) rpN[16 * h + cc] = rr;
+                // the column k term of T_{k+1} needs both rows of L(k+1, k)
+                lds_wait(F1, k + 2);
+                lds_wait(F3, k + 2);
+                if (useTk) {
+#pragma unroll
+                    for (int c = 0; c < 2; c++) {
+                        double4_t tb = {0, 0, 0, 0};
+                        mfma_sub(t[c], lq(L1n + (2 * c) * 256), o0);
+                        mfma_sub(tb, lq(L1n + (2 * c + 1) * 256), o1);
+                        t[c] += tb;
+                    }
+                }
+                sq(TpN + (2 * h) * 256, t[0]);
+                sq(TpN + (2 * h + 1) * 256, t[1]);
             }
         }
-        if (dbg && lane == 0) wts[wid] = __builtin_amdgcn_s_memtime() - tf;
+        if (dbg && lane == 0) wts[wid] = __builtin_amdgcn_s_memtime() - tk;
         lds_barrier();
         c1 ^= 1;
         c2 ^= 1;
         if (dbg && tid == 0 && k < 200) {
             unsigned long long* dk = dbg + 8 + 6 * k;
             dk[0] = __builtin_amdgcn_s_memtime() - tk;
-            dk[1] = tp1 - tk;
-            dk[2] = tf - tp1;
-            dk[3] = wts[0];
-            dk[4] = wts[1];
-            dk[5] = std::max(wts[2], wts[3]);
+            for (int w = 0; w < 4; w++) dk[1 + w] = wts[w];
+            dk[5] = wts[6] | (wts[7] << 32);
         }
         if (word[4]) {
             aborted = true;
@@ -564,8 +707,8 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     double* Lin = lds + 1024 * ((NT - 1) & 1);
     // ---- backward, right-looking by rows: at step R (x_R known) wave 0 forms x_{R-1} from the
     // sub-diagonal tile (R, R-1) and s_{R-1}; waves 1..3 subtract row R's other tiles from the
-    // running sums s_j, j <= R-2. The helper tiles' flags are polled once, up front; wave 0's
-    // inputs and the first tiles of each wave's next row are loaded a step ahead. ----
+    // running sums s_j, j <= R-2. The helper tiles' flags are polled once, up front; the tiles
+    // are loaded two steps ahead. ----
     auto apply_lt = [&](int k) {   // wave 0: xs_k = Linv^T rvec (Linv in Lin)
         const int c = lane >> 1, hh = lane & 1;
         double s = 0.0;
@@ -584,74 +727,64 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 for (int q = 0; q < 4; q++) ys[j * kT + 16 * b + rg + 4 * q] -= t[b][q];
         }
     };
-    double4_t st[4], sn[4], li[4];   // wave 0: tile (R, R-1) now / next, Linv_{R-1}
-    constexpr int kPf = 3;           // waves 1..3: tiles of a row loaded a step ahead
-    double4_t pf[kPf][4], pn[kPf][4];
-    if (!aborted) {
-        if (wid == 0) {
-            if (lane < kT) rvec[lane] = ys[(NT - 1) * kT + lane];
-            wave_lds_sync();
-            apply_lt(NT - 1);
-            if (NT >= 2) {
+    // prefetch rings two steps deep (register sets by step parity: each role's loop is unrolled by
+    // two, so the set index is a compile-time constant, and the two roles' rings have disjoint live
+    // ranges): wave 0 tile (R, R-1) and Linv_{R-1}; waves 1..3 the first kPf tiles of their share of
+    // row R, longer rows stream the rest a tile at a time. Both roles pass the same barriers.
+    constexpr int kPf = 3;
+    if (!aborted && wid != 0) {
+        // every tile (R, j), j <= R-2, rows 2.. (16 rows of this wave per round: up to 32 flag
+        // loads in flight per lane)
+        bool good = true;
+        for (int R0 = 1 + wid; R0 < NT && good; R0 += 48) {
+            for (unsigned spins = 0;; spins++) {
+                int okl = 1;
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    const int R = R0 + 3 * u;
+                    if (R < NT) {
+                        const int rfR = rfl[R];
+#pragma unroll
+                        for (int hh = 0; hh < 2; hh++) {
+                            const int j = rfR + 64 * hh + lane;
+                            if (j <= R - 2) okl &= ld_flag(L.fL + R * NT + j) == epoch ? 1 : 0;
+                        }
+                    }
+                }
+                if (__all(okl)) break;
+                if (ld_flag(L.ctl + 2) == epoch || spins >= kSpinMax) {
+                    if (spins >= kSpinMax && lane == 0) {
+                        st_flag(L.ctl + 2, epoch);
+                        __hip_atomic_fetch_add((gint*)(L.ctl + 3), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    good = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        if (!good && lane == 0) word[5] = 0;
+    }
+    __syncthreads();
+    if (!word[5]) aborted = true;
+    if (!aborted && wid == 0) {
+        double4_t st[2][4], li[2][4];
+        auto load = [&](auto setc, int R) {   // inputs of step R
+            constexpr int S = decltype(setc)::value;
+            if (R >= 1) {
 #pragma unroll
                 for (int qd = 0; qd < 4; qd++) {
-                    st[qd] = qload(rs, L.oL + ((NT - 1) * NT + NT - 2) * kTD + qd * 256);
-                    li[qd] = qload(rs, L.oLi + (NT - 2) * kTD + qd * 256);
+                    st[S][qd] = qload(rs, L.oL + (R * NT + R - 1) * kTD + qd * 256);
+                    li[S][qd] = qload(rs, L.oLi + (R - 1) * kTD + qd * 256);
                 }
             }
-        } else {
-            // every tile (R, j), j <= R-2, rows 2.. (16 rows of this wave per round: up to 32
-            // flag loads in flight per lane)
-            bool good = true;
-            for (int R0 = 1 + wid; R0 < NT && good; R0 += 48) {
-                for (unsigned spins = 0;; spins++) {
-                    int okl = 1;
+        };
+        auto step = [&](auto setc, int R) {   // x_{R-1} = Linv_{R-1}^T (s_{R-1} - L(R, R-1)^T x_R)
+            constexpr int S = decltype(setc)::value;
 #pragma unroll
-                    for (int u = 0; u < 16; u++) {
-                        const int R = R0 + 3 * u;
-                        if (R < NT) {
-                            const int rfR = rfl[R];
-#pragma unroll
-                            for (int hh = 0; hh < 2; hh++) {
-                                const int j = rfR + 64 * hh + lane;
-                                if (j <= R - 2) okl &= ld_flag(L.fL + R * NT + j) == epoch ? 1 : 0;
-                            }
-                        }
-                    }
-                    if (__all(okl)) break;
-                    if (ld_flag(L.ctl + 2) == epoch || spins >= kSpinMax) {
-                        if (spins >= kSpinMax && lane == 0) {
-                            st_flag(L.ctl + 2, epoch);
-                            __hip_atomic_fetch_add((gint*)(L.ctl + 3), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        }
-                        good = false;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(2);
-                }
-            }
-            if (!good && lane == 0) word[5] = 0;
-        }
-        __syncthreads();
-        if (!word[5]) aborted = true;
-        if (wid != 0 && !aborted && NT >= 2) {   // row NT-1's first tiles
-            const int R = NT - 1, jn = rfl[R] + (wid - 1);
-#pragma unroll
-            for (int u = 0; u < kPf; u++)
-                if (jn + 3 * u <= R - 2) {
-#pragma unroll
-                    for (int qd = 0; qd < 4; qd++) pf[u][qd] = qload(rs, L.oL + (R * NT + jn + 3 * u) * kTD + qd * 256);
-                }
-        }
-    }
-    for (int R = NT - 1; R >= 1 && !aborted; R--) {
-        const double* xR = xs + R * kT;
-        if (wid == 0) {
-            // x_{R-1} = Linv_{R-1}^T (s_{R-1} - L(R, R-1)^T x_R)
-#pragma unroll
-            for (int qd = 0; qd < 4; qd++) sq(Lin + qd * 256, li[qd]);
+            for (int qd = 0; qd < 4; qd++) sq(Lin + qd * 256, li[S][qd]);
             double t[2][4];
-            tile_lt_x(st, xR, t);
+            tile_lt_x(st[S], xs + R * kT, t);
             if (cc == 0) {
 #pragma unroll
                 for (int b = 0; b < 2; b++)
@@ -661,54 +794,63 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                         rvec[c] = ys[(R - 1) * kT + c] - t[b][q];
                     }
             }
-            if (R >= 2) {   // step R-1's inputs
-#pragma unroll
-                for (int qd = 0; qd < 4; qd++) {
-                    sn[qd] = qload(rs, L.oL + ((R - 1) * NT + R - 2) * kTD + qd * 256);
-                    li[qd] = qload(rs, L.oLi + (R - 2) * kTD + qd * 256);
-                }
-            }
+            load(setc, R - 2);   // step R-2's inputs into this set
             wave_lds_sync();
             apply_lt(R - 1);
-#pragma unroll
-            for (int qd = 0; qd < 4; qd++) st[qd] = sn[qd];
-        } else {
-            // row R's tiles (R, j), j in [rf[R], R-2], j = rf[R] + wid - 1 + 3 i: the first kPf
-            // came a step ahead, the next row's are issued now, the rest four at a time
-            const int j0 = rfl[R] + (wid - 1);
+            lds_barrier();
+        };
+        if (lane < kT) rvec[lane] = ys[(NT - 1) * kT + lane];
+        wave_lds_sync();
+        apply_lt(NT - 1);
+        load(std::integral_constant<int, 0>{}, NT - 1);
+        load(std::integral_constant<int, 1>{}, NT - 2);
+        lds_barrier();
+        for (int R = NT - 1; R >= 1; R -= 2) {
+            step(std::integral_constant<int, 0>{}, R);
+            if (R - 1 >= 1) step(std::integral_constant<int, 1>{}, R - 1);
+        }
+    } else if (!aborted) {
+        double4_t pf[2][kPf][4];
+        auto load = [&](auto setc, int R) {   // the first tiles of this wave's share of row R
+            constexpr int S = decltype(setc)::value;
             if (R >= 2) {
-                const int jn = rfl[R - 1] + (wid - 1);
+                const int j0 = rfl[R] + (wid - 1);
 #pragma unroll
                 for (int u = 0; u < kPf; u++)
-                    if (jn + 3 * u <= R - 3) {
+                    if (j0 + 3 * u <= R - 2) {
 #pragma unroll
-                        for (int qd = 0; qd < 4; qd++) pn[u][qd] = qload(rs, L.oL + ((R - 1) * NT + jn + 3 * u) * kTD + qd * 256);
+                        for (int qd = 0; qd < 4; qd++) pf[S][u][qd] = qload(rs, L.oL + (R * NT + j0 + 3 * u) * kTD + qd * 256);
                     }
             }
+        };
+        auto step = [&](auto setc, int R) {   // s_j -= L(R, j)^T x_R over this wave's share of row R
+            constexpr int S = decltype(setc)::value;
+            const double* xR = xs + R * kT;
+            if (R >= 2) {
+                const int j0 = rfl[R] + (wid - 1);
 #pragma unroll
-            for (int u = 0; u < kPf; u++) {
-                const int j = j0 + 3 * u;
-                if (j > R - 2) break;
-                sub_tile(pf[u], xR, j);
+                for (int u = 0; u < kPf; u++) {
+                    const int j = j0 + 3 * u;
+                    if (j > R - 2) break;
+                    sub_tile(pf[S][u], xR, j);
+                }
+                for (int jb = j0 + 3 * kPf; jb <= R - 2; jb += 3) {
+                    double4_t tl[4];
+#pragma unroll
+                    for (int qd = 0; qd < 4; qd++) tl[qd] = qload(rs, L.oL + (R * NT + jb) * kTD + qd * 256);
+                    sub_tile(tl, xR, jb);
+                }
             }
-            for (int jb = j0 + 3 * kPf; jb <= R - 2; jb += 12) {
-                double4_t tl[4][4];
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    if (jb + 3 * u <= R - 2) {
-#pragma unroll
-                        for (int qd = 0; qd < 4; qd++) tl[u][qd] = qload(rs, L.oL + (R * NT + jb + 3 * u) * kTD + qd * 256);
-                    }
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    if (jb + 3 * u <= R - 2) sub_tile(tl[u], xR, jb + 3 * u);
-            }
-#pragma unroll
-            for (int u = 0; u < kPf; u++)
-#pragma unroll
-                for (int qd = 0; qd < 4; qd++) pf[u][qd] = pn[u][qd];
+            load(setc, R - 2);   // row R-2's first tiles into this set
+            lds_barrier();
+        };
+        load(std::integral_constant<int, 0>{}, NT - 1);
+        load(std::integral_constant<int, 1>{}, NT - 2);
+        lds_barrier();
+        for (int R = NT - 1; R >= 1; R -= 2) {
+            step(std::integral_constant<int, 0>{}, R);
+            if (R - 1 >= 1) step(std::integral_constant<int, 1>{}, R - 1);
         }
-        lds_barrier();   // LDS only: the next step's tiles stay in flight
     }
     if (wid == 0 && lane == 0) word[8] = (ok && !aborted) ? 1 : 0;
     __syncthreads();
@@ -748,7 +890,7 @@ __global__ __launch_bounds__(256) void k_chol_dag(DagK a) {
 }
 
 size_t dag_lds_bytes(int NT) {
-    const size_t need = sizeof(double) * (10256 + 512 + 64 + 2 * (size_t)NT * kT) + sizeof(int) * NT;
+    const size_t need = sizeof(double) * (11280 + 32 + 64 + 2 * (size_t)NT * kT) + sizeof(int) * NT;
     return std::max(need, kMinLds);
 }
 

@@ -80,16 +80,26 @@ __device__ __forceinline__ bool in_phase(const BaArgs& a, int ph) { return !a.ct
 #define BA_PHASE(ph) \
     if (!in_phase(a, ph)) return;
 
+// sum over the workgroup, the same value in every thread (fixed order)
+__device__ double block_sum(double v, double* sh) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    __syncthreads();
+    if (lane == 0) sh[wid] = v;
+    __syncthreads();
+    double s = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); i++) s += sh[i];
+    return s;
+}
+
 // ---------------------------------------------------------------------------
-// errors (when: 0 always, 1 the build's stale-error refresh, 2 a trial's new state)
+// errors (when: 0 always, 1 the build's stale-error refresh, 2 a trial's new state); a trial also
+// writes each workgroup's sum of the robust chi2 terms to part[bx] (k_ba_ctl_end adds them)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_ba_errors(const BaArgs* __restrict__ args, const int* __restrict__ act,
-                                                   int when) {
-    BA_PROLOGUE
-    if (when == 1 && !(in_phase(a, kPhBuild) && (!a.ctl || !a.ctl->errors_valid))) return;
-    if (when == 2 && !in_phase(a, kPhTrial)) return;
-    const int e = bx_ * blockDim.x + threadIdx.x;
-    if (e >= a.E) return;
+// one edge: error, chi2, robust rho (EdgeSE3ProjectXYZ::computeError + RobustKernelHuber::robustify);
+// returns rho0
+__device__ __forceinline__ double edge_error(const BaArgs& a, int e) {
     const double* T = a.pose + 8 * a.e_pose[e];
     const double* X = a.pts + 3 * a.e_pt[e];
     double cx, cy, cz;
@@ -112,6 +122,22 @@ __global__ __launch_bounds__(256) void k_ba_errors(const BaArgs* __restrict__ ar
     a.e_chi2[e] = chi2;
     a.e_rho0[e] = r0;
     a.e_rho1[e] = r1;
+    return r0;
+}
+
+__global__ __launch_bounds__(256) void k_ba_errors(const BaArgs* __restrict__ args, const int* __restrict__ act,
+                                                   int when) {
+    BA_PROLOGUE
+    if (when == 1 && !(in_phase(a, kPhBuild) && (!a.ctl || !a.ctl->errors_valid))) return;
+    if (when == 2 && !in_phase(a, kPhTrial)) return;
+    if (bx_ * (int)blockDim.x >= a.E) return;   // uniform
+    const int e = bx_ * blockDim.x + threadIdx.x;
+    const double r0 = e < a.E ? edge_error(a, e) : 0.0;
+    if (when == 2) {   // uniform: every thread reaches the workgroup sum's barriers once
+        __shared__ double sh[4];
+        const double t = block_sum(r0, sh);
+        if (threadIdx.x == 0) a.part[bx_] = t;
+    }
 }
 
 // Jacobians of EdgeSE3ProjectXYZ at the camera-frame point (x, y, z) of a pose with rotation R
@@ -649,11 +675,8 @@ __global__ __launch_bounds__(512) void k_chol_test(double* S, const double* bs, 
 // ---------------------------------------------------------------------------
 // back-substitution + updates (push saves the old state)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_ba_backsub(const BaArgs* __restrict__ args, const int* __restrict__ act) {
-    BA_PROLOGUE
-    BA_PHASE(kPhTrial)
-    const int m = bx_ * blockDim.x + threadIdx.x;
-    if (m >= a.M) return;
+// landmark m: xl = Dinv (b_l - Hpl^T xp), X += xl (old X saved); returns xl (lambda xl + b_l)
+__device__ __forceinline__ double backsub_point(const BaArgs& a, int m) {
     const double* bl = a.b + a.n + 3 * m;
     double c[3] = {bl[0], bl[1], bl[2]};
     for (int k = a.pt_ptr[m]; k < a.pt_ptr[m + 1]; k++) {
@@ -672,13 +695,29 @@ __global__ __launch_bounds__(256) void k_ba_backsub(const BaArgs* __restrict__ a
     }
     const double* Di = a.Dinv + 9 * m;
     double* X = a.pts + 3 * m;
+    const double lambda = *a.lambda;
+    double sc = 0.0;
 #pragma unroll
     for (int r = 0; r < 3; r++) {
         const double xl = Di[3 * r] * c[0] + Di[3 * r + 1] * c[1] + Di[3 * r + 2] * c[2];
         a.x[a.n + 3 * m + r] = xl;
         a.pts_bak[3 * m + r] = X[r];
         X[r] += xl;
+        sc += xl * (lambda * xl + bl[r]);
     }
+    return sc;
+}
+
+__global__ __launch_bounds__(256) void k_ba_backsub(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    BA_PROLOGUE
+    BA_PHASE(kPhTrial)
+    if (bx_ * (int)blockDim.x >= a.M) return;   // uniform
+    const int m = bx_ * blockDim.x + threadIdx.x;
+    // the landmark part of computeScale, sum of xl (lambda xl + b_l), per workgroup (uniform: every
+    // thread reaches the workgroup sum's barriers once)
+    __shared__ double sh[4];
+    const double t = block_sum(m < a.M ? backsub_point(a, m) : 0.0, sh);
+    if (threadIdx.x == 0) a.part[a.npart_e + bx_] = t;
 }
 
 __global__ __launch_bounds__(256) void k_ba_update_poses(const BaArgs* __restrict__ args, const int* __restrict__ act) {
@@ -717,18 +756,6 @@ __global__ void k_ba_gather_red(const BaArgs* __restrict__ args, const int* __re
 // ---------------------------------------------------------------------------
 // reductions (one workgroup per problem, fixed order): [0] sum rho0, [1] scale, [2] max diag
 // ---------------------------------------------------------------------------
-__device__ double block_sum(double v, double* sh) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    __syncthreads();
-    if (lane == 0) sh[wid] = v;
-    __syncthreads();
-    double s = 0;
-    for (int i = 0; i < (int)(blockDim.x >> 6); i++) s += sh[i];
-    return s;
-}
-
 // In-batch model of the sharded solve: problems 0..B-1 are shards of one problem (same poses,
 // disjoint landmarks); every shard's field[off .. off+count) becomes the sum (op 0) or max
 // (op 1) over the shards, in shard order (deterministic). field: 0 Hpp, 1 S, 2 bs, 3 red.
@@ -869,7 +896,18 @@ __global__ __launch_bounds__(1024) void k_ba_ctl_end(const BaArgs* __restrict__ 
     const BaArgs& a = args[act[blockIdx.x]];
     LmCtl& c = *a.ctl;
     if (c.phase != kPhTrial) return;   // uniform
-    ba_reduce_body(a, 3, sh);
+    {   // chi2 and the scale from the trial kernels' workgroup partials (k_ba_errors, k_ba_backsub)
+        double v = 0.0;
+        for (int i = threadIdx.x; i < a.npart_e; i += blockDim.x) v += a.part[i];
+        v = block_sum(v, sh);
+        if (threadIdx.x == 0) a.red[0] = v;
+        const double lambda = *a.lambda, lam_pose = a.lead ? lambda : 0.0;
+        v = 0.0;
+        for (int j = threadIdx.x; j < a.n; j += blockDim.x) v += a.x[j] * (lam_pose * a.x[j] + a.b[j]);
+        for (int i = threadIdx.x; i < a.npart_m; i += blockDim.x) v += a.part[a.npart_e + i];
+        v = block_sum(v, sh);
+        if (threadIdx.x == 0) a.red[1] = v;
+    }
     if (threadIdx.x != 0) return;
     double* lambda = const_cast<double*>(a.lambda);
     const bool ok2 = a.flag[0] != 0;
@@ -931,6 +969,7 @@ struct Prep {
     DagPlan dag;                  // its helper task lists
     size_t dag_task_cap = 0;      // ints reserved for the lists (RCCL shards: planned after the union envelope)
     size_t o_dag = 0, o_dagi = 0;
+    size_t o_red2 = 0;            // workgroup partials of a trial's chi2 / scale (BaArgs::part)
     // offsets (elements) into the packed buffers; see the segment map in ba_solve_batch
     size_t o_chi2 = 0, o_state = 0, o_obs = 0, o_scr = 0, o_lin = 0, o_S = 0, o_L = 0, o_part = 0, o_int = 0;
 };
@@ -1237,6 +1276,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         p.o_L = nR; nR += 1024 * ((n + 31) / 32);
         nR = (nR + 1) & ~size_t(1);
         p.o_part = nR; nR += 36 * (size_t)p.nslot;
+        p.o_red2 = nR; nR += (E + 255) / 256 + (M + 255) / 256 + 2;
         if (p.use_dag) {   // 128-byte aligned
             nR = (nR + 15) & ~size_t(15);
             p.o_dag = nR; nR += dag_doubles(p.n);
@@ -1358,6 +1398,9 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.S = D + sR + p.o_S;
         a.Lsave = D + sR + p.o_L;
         a.Spart = D + sR + p.o_part;
+        a.part = D + sR + p.o_red2;
+        a.npart_e = (int)((E + 255) / 256);
+        a.npart_m = (int)((M + 255) / 256);
         if (p.use_dag) dd[b].buf = D + sR + p.o_dag;
         a.lambda = ws->lam.p + b;
         a.lead = shard_mode == kShardLocal ? (b == 0) : (shard_mode == kShardRccl ? (ws->rank == 0) : 1);

@@ -52,4 +52,5 @@ for n_s, shape in cases:
     med = np.median(ph, axis=0).astype(int) if ki else [0] * 6
     print(f"n={n} {shape}: rc={rc} dag {ms.value * 1e3:.1f} us relerr={err:.2e} | cycles prologue={dbg[0]} "
           f"forward={dbg[1]} backward={dbg[2]} diag={dbg[4]} total={dbg[5]} | interval medians: total {med[0]} "
-          f"ph1 {med[1]} ph2 {med[2]} ph3 w0 {med[3]} w1 {med[4]} w23 {med[5]} ({time.time() - t0:.1f}s)", flush=True)
+          f"| wave ends {med[1]} {med[2]} {med[3]} {med[4]} w0 start {int(np.median(ph[:, 5] & 0xFFFFFFFF)) if ki else 0} "
+          f"pre-diag {int(np.median(ph[:, 5] >> 32)) if ki else 0} ({time.time() - t0:.1f}s)", flush=True)
