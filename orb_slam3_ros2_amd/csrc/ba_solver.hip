@@ -18,7 +18,7 @@
 //   k_ba_cholesky      dense LL^T + solves, one workgroup per problem; trailing update on
 //                      v_mfma_f64_16x16x4f64
 //   k_ba_backsub       xl = Dinv (b_l - Hpl^T xp), X += xl (push: old X saved)
-//   k_ba_update_poses  T <- exp(xp) * T (SE3Quat::exp, operator*)   (push: old T saved)
+//                      and T <- exp(xp) * T (SE3Quat::exp, operator*)   (push: old T saved)
 //   k_ba_reduce        activeRobustChi2, computeScale, max diag; fixed-order reductions
 //   k_ba_pop           restore the pushed state of problems whose trial was rejected
 #include <hip/hip_runtime.h>
@@ -125,10 +125,26 @@ __device__ __forceinline__ double edge_error(const BaArgs& a, int e) {
     return r0;
 }
 
+// when == 1 also opens the device-driven slot (the former k_ba_ctl_pre): workgroup 0 of each
+// problem clears the pop request of the previous slot and, at an iteration start, ends the solve
+// on the iteration budget or the (host-relayed) stop flag (done[b], host-mapped: the host stops
+// queueing slots once every problem is done). Every workgroup derives the same effective phase
+// from the controller's fields, so none depends on that transition's store.
 __global__ __launch_bounds__(256) void k_ba_errors(const BaArgs* __restrict__ args, const int* __restrict__ act,
-                                                   int when) {
+                                                   int when, int* done) {
     BA_PROLOGUE
-    if (when == 1 && !(in_phase(a, kPhBuild) && (!a.ctl || !a.ctl->errors_valid))) return;
+    if (when == 1) {
+        LmCtl* c = a.ctl;
+        const bool ends = c && c->phase == kPhBuild && (c->stop || c->it >= c->iterations);
+        if (c && bx_ == 0 && threadIdx.x == 0) {
+            c->pop = 0;
+            if (ends) {
+                c->phase = kPhDone;
+                if (done) __hip_atomic_store(done + act[by_], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        if (ends || !(in_phase(a, kPhBuild) && (!c || !c->errors_valid))) return;
+    }
     if (when == 2 && !in_phase(a, kPhTrial)) return;
     if (bx_ * (int)blockDim.x >= a.E) return;   // uniform
     const int e = bx_ * blockDim.x + threadIdx.x;
@@ -429,7 +445,16 @@ __global__ __launch_bounds__(256) void k_ba_schur_fin(const BaArgs* __restrict__
     const int i = a.blk_i[blk], j = a.blk_j[blk];
     const int rr = lane / 6, cc = lane - 6 * rr;
     double s = (i == j && a.lead) ? a.Hpp[36 * i + 6 * rr + cc] + (rr == cc ? *a.lambda : 0.0) : 0.0;
-    for (int c = 0; c < nch; c++) s += a.Spart[36 * (size_t)(slot0 + c) + lane];
+    const double* sp = a.Spart + 36 * (size_t)slot0 + lane;
+    int c = 0;
+    for (; c + 8 <= nch; c += 8) {   // eight loads in flight, summed in order
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = sp[36 * (c + u)];
+#pragma unroll
+        for (int u = 0; u < 8; u++) s += v[u];
+    }
+    for (; c < nch; c++) s += sp[36 * c];
     a.S[(size_t)(6 * i + rr) * a.n + 6 * j + cc] = s;
     if (i != j) a.S[(size_t)(6 * j + cc) * a.n + 6 * i + rr] = s;
 }
@@ -708,29 +733,26 @@ __device__ __forceinline__ double backsub_point(const BaArgs& a, int m) {
     return sc;
 }
 
+// one thread per landmark (back-substitution) and, in the first workgroups, one per pose
+// (T <- exp(xp) T, the former k_ba_update_poses: it reads xp and writes the poses, which the
+// landmarks' back-substitution does not touch)
 __global__ __launch_bounds__(256) void k_ba_backsub(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
     BA_PHASE(kPhTrial)
-    if (bx_ * (int)blockDim.x >= a.M) return;   // uniform
+    if (bx_ * (int)blockDim.x >= max(a.M, a.P)) return;   // uniform
     const int m = bx_ * blockDim.x + threadIdx.x;
+    if (m < a.P) {
+        double* T = a.pose + 8 * m;
+#pragma unroll
+        for (int k = 0; k < 8; k++) a.pose_bak[8 * m + k] = T[k];
+        const int oi = a.opt[m];
+        if (oi >= 0) se3_update(a.x + 6 * oi, T);
+    }
     // the landmark part of computeScale, sum of xl (lambda xl + b_l), per workgroup (uniform: every
     // thread reaches the workgroup sum's barriers once)
     __shared__ double sh[4];
     const double t = block_sum(m < a.M ? backsub_point(a, m) : 0.0, sh);
     if (threadIdx.x == 0) a.part[a.npart_e + bx_] = t;
-}
-
-__global__ __launch_bounds__(256) void k_ba_update_poses(const BaArgs* __restrict__ args, const int* __restrict__ act) {
-    BA_PROLOGUE
-    BA_PHASE(kPhTrial)
-    const int p = bx_ * blockDim.x + threadIdx.x;
-    if (p >= a.P) return;
-    double* T = a.pose + 8 * p;
-#pragma unroll
-    for (int k = 0; k < 8; k++) a.pose_bak[8 * p + k] = T[k];
-    const int oi = a.opt[p];
-    if (oi < 0) return;
-    se3_update(a.x + 6 * oi, T);
 }
 
 // restore the pushed state: host-driven rounds list the rejected problems in act[]; device-driven
@@ -849,21 +871,6 @@ __global__ __launch_bounds__(1024) void k_ba_ctl_init(const BaArgs* __restrict__
     }
 }
 
-// start of a slot: clear the pop request of the previous slot; at an iteration start, stop on the
-// iteration budget or the (host-relayed) stop flag
-// done[b] (host-mapped, optional): set when problem b reaches kPhDone, so the host stops queueing
-// slots once every problem has finished
-__global__ void k_ba_ctl_pre(LmCtl* __restrict__ ctl, int B, int* done) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
-    LmCtl& c = ctl[b];
-    c.pop = 0;
-    if (c.phase == kPhBuild && (c.stop || c.it >= c.iterations)) {
-        c.phase = kPhDone;
-        if (done) __hip_atomic_store(done + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-
 __global__ void k_ba_ctl_stop(LmCtl* __restrict__ ctl, int B) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b < B) ctl[b].stop = 1;
@@ -937,7 +944,7 @@ __global__ __launch_bounds__(1024) void k_ba_ctl_end(const BaArgs* __restrict__ 
     c.errors_valid = rho > 0;   // rejected: the device errors belong to the popped trial
     bool done = (c.qmax == 10 || rho == 0);
     if (c.early_stop && c.nBad >= 3) done = true;
-    if (c.it >= c.iterations) done = true;   // the budget (checked by ctl_pre too), no idle slot
+    if (c.it >= c.iterations) done = true;   // the budget (checked by k_ba_errors(1) too), no idle slot
     c.phase = done ? kPhDone : kPhBuild;
     if (done && done_flags) __hip_atomic_store(done_flags + act[blockIdx.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1559,12 +1566,11 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             if (!large(b)) h_act[2 * B + ns++] = b;
         if (ns) BAOK(hipMemcpyAsync(d_act + 2 * B, h_act + 2 * B, ns * sizeof(int), hipMemcpyHostToDevice, st));
         if (s_readonly) hipLaunchKernelGGL(k_ba_zero_s, dim3(64, B), dim3(256), 0, st, dA, d_act, 1);
-        hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), dim3(256), 0, st, dA, d_act, 0);
+        hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), dim3(256), 0, st, dA, d_act, 0, nullptr);
         hipLaunchKernelGGL(k_ba_ctl_init, dim3(B), dim3(1024), 0, st, dA, d_act);
         const dim3 gB((unsigned)((B + 255) / 256)), b256(256);
         auto slot = [&]() -> int {
-            hipLaunchKernelGGL(k_ba_ctl_pre, gB, b256, 0, st, dctl, B, ws->d_done);
-            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 1);
+            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 1, ws->d_done);
             hipLaunchKernelGGL(k_ba_lin_points, dim3(gx(maxM, 256), B), b256, 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_lin_poses, dim3(gx(maxNp, 4), B), b256, 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_ctl_begin, dim3(B), dim3(1024), 0, st, dA, d_act);
@@ -1579,9 +1585,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             }
             for (int b = 0; b < B; b++)
                 if (large(b) && large_solve(b, &dctl[b].phase)) return ORBHIP_ERR_DEVICE;
-            hipLaunchKernelGGL(k_ba_backsub, dim3(gx(maxM, 256), B), b256, 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_update_poses, dim3(gx(maxP, 256), B), b256, 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 2);
+            hipLaunchKernelGGL(k_ba_backsub, dim3(gx(std::max(maxM, maxP), 256), B), b256, 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 2, nullptr);
             hipLaunchKernelGGL(k_ba_ctl_end, dim3(B), dim3(1024), 0, st, dA, d_act, ws->d_done);
             int maxPM = 0;
             for (auto& p : pp) maxPM = std::max(maxPM, std::max(8 * p.P, 3 * p.M));
@@ -1652,7 +1657,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     } else {
     // ---- host-driven rounds (sharded solves: collectives and the stop-flag consensus) ----
     // ---- initial errors and chi2 ----
-    hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), dim3(256), 0, st, dA, d_act, 0);
+    hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), dim3(256), 0, st, dA, d_act, 0, nullptr);
     hipLaunchKernelGGL(k_ba_reduce, dim3(B), dim3(1024), 0, st, dA, d_act, 1);
     if (coll(3, 0, 1, 0)) return ORBHIP_ERR_DEVICE;
     BAOK(hipGetLastError());
@@ -1677,7 +1682,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             if (!L[b].errors_valid) stale.push_back(b);
         if (!stale.empty()) {
             if (upload_act(stale)) return ORBHIP_ERR_DEVICE;
-            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), (unsigned)stale.size()), dim3(256), 0, st, dA, d_act, 0);
+            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), (unsigned)stale.size()), dim3(256), 0, st, dA, d_act, 0, nullptr);
         }
         if (upload_act(act)) return ORBHIP_ERR_DEVICE;
         hipLaunchKernelGGL(k_ba_lin_points, dim3(gx(maxM, 256), na), dim3(256), 0, st, dA, d_act);
@@ -1723,9 +1728,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 for (int b : trial)
                     if (large(b) && large_solve(b, nullptr)) return ORBHIP_ERR_DEVICE;
             }
-            hipLaunchKernelGGL(k_ba_backsub, dim3(gx(maxM, 256), nt_), dim3(256), 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_update_poses, dim3(gx(maxP, 256), nt_), dim3(256), 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), nt_), dim3(256), 0, st, dA, d_act, 0);
+            hipLaunchKernelGGL(k_ba_backsub, dim3(gx(std::max(maxM, maxP), 256), nt_), dim3(256), 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), nt_), dim3(256), 0, st, dA, d_act, 0, nullptr);
             hipLaunchKernelGGL(k_ba_reduce, dim3(nt_), dim3(1024), 0, st, dA, d_act, 3);
             if (coll(3, 0, 2, 0)) return ORBHIP_ERR_DEVICE;
             BAOK(hipGetLastError());
