@@ -239,15 +239,28 @@ __global__ __launch_bounds__(256) void k_ba_lin_points(const BaArgs* __restrict_
 
 // one wave per optimised pose: 21 upper Hpp terms + 6 b terms, lanes over the pose's edges; lane 0
 // keeps the pose's rotation at the linearisation (R_lin)
+// one halving step of a transpose-reduce: a lane with bit m clear keeps values [0, H), set keeps
+// [H, 2H); each adds its partner's copy of the values it keeps; the kept values end in [0, H)
+template <int H>
+__device__ __forceinline__ void reduce_half(double* acc, int lane, int m) {
+    const bool up = (lane & m) != 0;
+#pragma unroll
+    for (int i = 0; i < H; i++) {
+        const double send = up ? acc[i] : acc[i + H];
+        const double keep = up ? acc[i + H] : acc[i];
+        acc[i] = keep + __shfl_xor(send, m, 64);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_ba_lin_poses(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
     BA_PHASE(kPhBuild)
     const int i = bx_ * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (i >= a.np) return;
-    double acc[27];
+    double acc[32];   // 27 sums (21 of the upper Hpp triangle, 6 of b_p), padded to 32
 #pragma unroll
-    for (int k = 0; k < 27; k++) acc[k] = 0;
+    for (int k = 0; k < 32; k++) acc[k] = 0;
     for (int k = a.ps_ptr[i] + lane; k < a.ps_ptr[i + 1]; k += 64) {
         const int e = a.ps_edges[k];
         double x, y, z, R[9], j[4], A[6], B[12];
@@ -265,19 +278,28 @@ __global__ __launch_bounds__(256) void k_ba_lin_poses(const BaArgs* __restrict__
 #pragma unroll
         for (int r = 0; r < 6; r++) acc[21 + r] += B[r] * om0 + B[6 + r] * om1;
     }
-#pragma unroll
-    for (int k = 0; k < 27; k++) {
-        double v = acc[k];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        acc[k] = v;
-    }
-    if (lane == 0) {
-        int t = 0;
+    // transpose-reduce over the 64 lanes: at each step a lane keeps half of its values and adds
+    // its partner's copy of them (16 + 8 + 4 + 2 + 1 shuffles, then one for the last pair instead
+    // of 27 x 6); lane 2k ends with sum k (k = the lane's bits 5..1, most significant first)
+    reduce_half<16>(acc, lane, 32);
+    reduce_half<8>(acc, lane, 16);
+    reduce_half<4>(acc, lane, 8);
+    reduce_half<2>(acc, lane, 4);
+    reduce_half<1>(acc, lane, 2);
+    const double tot = acc[0] + __shfl_xor(acc[0], 1, 64);
+    const int k = ((lane >> 5) & 1) << 4 | ((lane >> 4) & 1) << 3 | ((lane >> 3) & 1) << 2 | ((lane >> 2) & 1) << 1 |
+                  ((lane >> 1) & 1);
+    if ((lane & 1) == 0 && k < 27) {
         double* H = a.Hpp + 36 * i;
-        for (int r = 0; r < 6; r++)
-            for (int c = r; c < 6; c++) { H[6 * r + c] = acc[t]; H[6 * c + r] = acc[t]; t++; }
-        for (int r = 0; r < 6; r++) a.b[6 * i + r] = acc[21 + r];
+        if (k < 21) {   // k-th entry of the upper triangle, row-major
+            int r = 0, t = k;
+            while (t >= 6 - r) { t -= 6 - r; r++; }
+            const int c = r + t;
+            H[6 * r + c] = tot;
+            H[6 * c + r] = tot;
+        } else {
+            a.b[6 * i + k - 21] = tot;
+        }
     }
     if (lane < 9 && a.ps_ptr[i] < a.ps_ptr[i + 1]) {   // the pose's rotation, as its edges used it
         {
