@@ -290,13 +290,17 @@ class FrontendC2:
 
 
 def stage_bytes(ext, w, h, n_kp, frames):
-    """Algorithmic HBM bytes per launch of each stage: resize reads level l-1 and
-    writes level l (all 7 launches summed), FAST reads every level once, octree reads its packed
-    candidates (8 B) and writes kept keypoints (8 B), desc reads a 43x43 patch + writes kp/desc
-    (56 B), match reads query+train descriptors and writes 3 ints per query, rot filter 12 B/kp."""
+    """Algorithmic HBM bytes per launch of each stage. Pyramid: at batch <= 4 the
+    one-launch cone (k_pyr_cone) reads level 0 once and writes levels 1..7 (A0 + sum_{l>=1} A_l;
+    its halo recompute stays on chip), the 7-launch k_resize cascade of bigger batches reads level
+    l-1 and writes level l (sum A[:-1] + sum A[1:], all 7 launches). FAST reads every level once,
+    octree reads its packed candidates (8 B) and writes kept keypoints (8 B), desc reads a 43x43
+    patch + writes kp/desc (56 B), match reads query+train descriptors and writes 3 ints per
+    query, rot filter 12 B/kp."""
     info = ext.level_info(w, h)
     A = (info["w"].astype(np.int64) * info["h"]).tolist()
-    per = {1: sum(A[:-1]) + sum(A[1:]), 2: sum(A), 3: 8.0 * 4500 + 8 * n_kp, 4: n_kp * (43 * 43 + 56),
+    pyr = sum(A) if frames <= 4 else sum(A[:-1]) + sum(A[1:])
+    per = {1: pyr, 2: sum(A), 3: 8.0 * 4500 + 8 * n_kp, 4: n_kp * (43 * 43 + 56),
            5: 2 * n_kp * 32 + n_kp * 12, 6: n_kp * 12}
     return {k: v * frames for k, v in per.items()}
 
@@ -496,6 +500,24 @@ def c5_gba(ws, rank, iters):
             "c5_problem": "400 KF loop / 20000 pts / 80000 obs, n = 2394"}
 
 
+def cpu_gba(iters_sample=3, iters=10):
+    """C5 on one core: the oracle GBA (same problem as c5_gba) for the first `iters_sample` LM
+    iterations (one trial each on this problem), scaled to the GPU run's `iters` (a full 10-iteration
+    oracle solve takes ~22 s on one core)."""
+    from oracle import pyoracle as O
+    from orb_slam3_ros2_amd.synthetic import synthetic_ba_problem
+    prob, _ = synthetic_ba_problem(n_kf=400, n_pts=20000, layout="loop", window=20, seed=11)
+    prob.iterations, prob.huber_delta = iters_sample, float(np.sqrt(5.99))
+    t0 = time.perf_counter()
+    r = O.ba_solve(prob)
+    t = time.perf_counter() - t0
+    per = t / max(1, int(r["iterations_done"]))
+    return {"c5_gba_single_core_ms": round(1e3 * per * iters, 1),
+            "c5_gba_single_core_ms_per_iteration": round(1e3 * per, 1),
+            "c5_sample": f"oracle GBA (ba_oracle.cpp), C5 problem, first {int(r['iterations_done'])} LM iterations "
+                         f"({int(r['lm_trials'])} trials) on one core in {t:.1f}s, scaled to {iters} iterations"}
+
+
 def _f8_inputs():
     from orb_slam3_ros2_amd.matcher import ProjFrame
     from orb_slam3_ros2_amd.synthetic import synthetic_init_pair, synthetic_pose_problem, synthetic_projection_scene
@@ -636,30 +658,20 @@ class Watchdog:
 
 
 def c2_headline(args, ws, rank):
-    """C2 camera streams: K timed steps of one frame per camera, the dominant stage bracketed by
-    HIP events on its launch stream; then the strict batch-1 figure (one camera, one frame at a
-    time) and one camera with 8 frames in flight."""
+    """C2 camera streams: K timed steps of one frame per camera; then a stage replay of the same
+    16-camera stream, untimed, in which camera c's contexts time stage (c mod 5) + 1 with the
+    stage timer (execution-only: the kernels carry the events, StageTimer in orbhip_kernels.h),
+    so every stage's average kernel duration comes from launches under the timed region's own
+    concurrency and the dominant kernel is the one rocprofv3's kernel trace of this C2 section
+    ranks first; then the strict batch-1 figure (one camera, one frame at a time) and one camera
+    with 8 frames in flight."""
     import torch
     K, W = args.steps, args.warmup
     c2 = FrontendC2(rank, args.inflight, args.cameras)
-    prof = Profiler(c2.ctx0)   # the stage timers of camera 0's context 0
     seq = FrontendC2(rank, 1, 1)
-    # ---- the dominant kernel of the step (short calibration on the one-frame stream, where an
-    # event pair around a kernel holds that kernel only; untimed) ----
-    prof_s = Profiler(seq.ctx0)
-    stage_ms = {}
-    for st in (1, 2, 3, 4, 5, 6):
-        prof_s.select(st)
-        for _ in range(30):
-            seq.step()
-        ms, n = prof_s.collect()
-        stage_ms[st] = ms / max(n, 1)
-    prof_s.select(0)
-    dom = max(stage_ms, key=stage_ms.get)
-    # ---- timed region ----
+    # ---- timed region (no stage timer open: the frames replay as launch graphs) ----
     for _ in range(W):
         c2.step()
-    prof.select(dom)
     _barrier(ws)
     t0 = time.perf_counter()
     for _ in range(K):
@@ -668,12 +680,31 @@ def c2_headline(args, ws, rank):
     torch.cuda.synchronize()
     _barrier(ws)
     elapsed = _max_over_ranks(ws, time.perf_counter() - t0)
-    dom_ms_if, dom_n_if = prof.collect()
-    prof.select(0)
     frames_total = _sum_over_ranks(ws, float(K * c2.frames_per_step))
+    # ---- stage replay: K more steps of the same stream, every stage timed on its own cameras ----
+    profs = []
+    for c, fs in enumerate(c2.fss):
+        st = 1 + c % 5   # stages 1..5 (k_match_finish runs only with the unfused matcher)
+        for j in range(c2.S):
+            p = Profiler(fs.context(j))
+            p.select(st)
+            profs.append((st, p))
+    for _ in range(K):
+        c2.step()
+    torch.cuda.synchronize()
+    acc = {}
+    for st, p in profs:
+        ms, n = p.collect()
+        p.select(0)
+        a = acc.setdefault(st, [0.0, 0])
+        a[0] += ms
+        a[1] += n
+    stage_ms = {st: a[0] / a[1] for st, a in sorted(acc.items()) if a[1]}
+    dom = max(stage_ms, key=stage_ms.get)
     r = {"value": frames_total / elapsed, "elapsed": elapsed, "frames_per_step": c2.frames_per_step,
          "cameras": c2.C, "inflight": c2.S, "host_submit_ms_per_frame": 1e3 * t_enq / (K * c2.frames_per_step),
-         "keypoints": c2.mean_keypoints(), "nmatch": c2.last_matches(), "stage_ms": stage_ms, "dom": dom}
+         "keypoints": c2.mean_keypoints(), "nmatch": c2.last_matches(), "stage_ms": stage_ms, "dom": dom,
+         "dom_avg_ms": stage_ms[dom], "dom_n": acc[dom][1]}
     r["dom_bytes"] = c2.stage_bytes()[dom]
     r["frames_np"] = c2.frames_np
     r["ctx"] = c2.ext.ctx
@@ -690,6 +721,17 @@ def c2_headline(args, ws, rank):
         seq.step()
     torch.cuda.synchronize()
     r["batch1_ms"] = 1e3 * (time.perf_counter() - t1) / K1
+    # per-stage kernel durations of the one-frame stream (informational)
+    prof_s = Profiler(seq.ctx0)
+    one_ms = {}
+    for st in (1, 2, 3, 4, 5):
+        prof_s.select(st)
+        for _ in range(20):
+            seq.step()
+        ms, n = prof_s.collect()
+        one_ms[st] = ms / max(n, 1)
+    prof_s.select(0)
+    r["stage_ms_one_frame"] = one_ms
     # ---- one camera, 8 frames in flight (event hand-offs between its contexts) ----
     one = FrontendC2(rank, 8, 1)
     for _ in range(max(W, 16)):
@@ -701,18 +743,43 @@ def c2_headline(args, ws, rank):
     torch.cuda.synchronize()
     r["one_camera_inflight_fps"] = K1 / (time.perf_counter() - t2)
     del one
-    # ---- the dominant kernel's duration on the one-frame stream (what rocprofv3's kernel trace
-    # reports); with frames in flight an event pair also holds the wait for a dispatch slot ----
-    prof_s.select(dom)
-    for _ in range(300):
-        seq.step()
-    torch.cuda.synchronize()
-    dom_ms, dom_n = prof_s.collect()
-    prof_s.select(0)
-    r["dom_avg_ms"] = dom_ms / max(dom_n, 1)
-    r["dom_n"] = dom_n
-    r["dom_avg_ms_in_flight"] = dom_ms_if / max(dom_n_if, 1)
     return r
+
+
+SIMDS, CUS = 1024, 256   # MI355X: 256 CUs x 4 SIMDs
+
+
+def issue_roofline(kernel, regime, alg_bytes, avg_ms):
+    """Roofline of an extractor kernel against the resource that binds it. HBM: algorithmic bytes
+    / the live average duration. Issue: the kernel's wave64 VALU and LDS instruction counts per
+    launch (profiles/counters.json, rocprofv3 --pmc of the same workload) over the live duration,
+    against the chip's issue rate at the clock those counters saw (busy cycles / duration): a
+    wave64 VALU op holds a SIMD for 2 cycles (1024 SIMDs), one LDS instruction per CU per cycle.
+    `bound` = the resource with the highest fraction; the other fractions ride along."""
+    ach = alg_bytes / (avg_ms * 1e-3) / 1e9
+    hbm = {"achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5)}
+    out = {"kernel": kernel, "bound": "hbm", **hbm, "traffic": load_traffic(kernel, regime),
+           "algorithmic_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(avg_ms, 4)}
+    cn = load_counters(kernel, regime)
+    out["counters"] = cn
+    if cn and cn.get("busy_cycles") and cn.get("duration_us"):
+        clk = cn["busy_cycles"] / (cn["duration_us"] * 1e-6)   # Hz
+        sec = avg_ms * 1e-3
+        valu = cn.get("SQ_INSTS_VALU", 0.0) / sec / 1e9
+        lds = cn.get("SQ_INSTS_LDS", 0.0) / sec / 1e9
+        vpk, lpk = SIMDS / 2 * clk / 1e9, CUS * clk / 1e9
+        fr = {"hbm": ach / HBM_PEAK_GBS, "valu issue": valu / vpk, "lds issue": lds / lpk}
+        out["issue"] = {"clock_ghz": round(clk / 1e9, 3),
+                        "valu": {"achieved": round(valu, 2), "peak": round(vpk, 1), "unit": "G wave-instr/s",
+                                 "frac": round(valu / vpk, 4)},
+                        "lds": {"achieved": round(lds, 2), "peak": round(lpk, 1), "unit": "G wave-instr/s",
+                                "frac": round(lds / lpk, 4)}}
+        b = max(fr, key=fr.get)
+        if b != "hbm":
+            src = out["issue"]["valu" if b == "valu issue" else "lds"]
+            out.update({"bound": b, "achieved": src["achieved"],
+                        "peak": src["peak"], "unit": src["unit"], "frac": src["frac"], "hbm": hbm})
+    return out
 
 
 def c3_batch(args, ws, rank):
@@ -739,15 +806,12 @@ def c3_batch(args, ws, rank):
         p3.select(0)
         d3 = max(c3_ms, key=c3_ms.get)
         b3 = stage_bytes(c3.ext, c3.W, c3.H, float(c3.n.float().mean().item()) or 1000.0, c3.nb)
-        a3 = b3[d3] / (c3_ms[d3] * 1e-3) / 1e9
         ks = kernel_symbol(d3, c3.nb)
-        out["c3_roofline"] = {"kernel": ks, "bound": "hbm", "achieved": round(a3, 2), "peak": HBM_PEAK_GBS,
-                              "unit": "GB/s", "frac": round(a3 / HBM_PEAK_GBS, 5),
-                              "traffic": load_traffic(ks, "c3"), "counters": load_counters(ks, "c3"),
-                              "algorithmic_bytes_per_launch": int(b3[d3]), "avg_launch_ms": round(c3_ms[d3], 4),
-                              "stage_avg_ms": {STAGES[k]: round(v, 4) for k, v in c3_ms.items()}}
+        out["c3_roofline"] = issue_roofline(ks, "c3", b3[d3], c3_ms[d3])
+        out["c3_roofline"]["stage_avg_ms"] = {STAGES[k]: round(v, 4) for k, v in c3_ms.items()}
         # the extractor's streaming stage against the HBM roof: the 7-level k_resize cascade
-        # (level l-1 read, level l written, per frame), timed as one stage (launch gaps included)
+        # (level l-1 read, level l written, per frame), timed as one stage (first kernel's start to
+        # the last kernel's end: the launch gaps between the 7 kernels are included)
         ah = b3[1] / (c3_ms[1] * 1e-3) / 1e9
         out["c3_hbm_stage"] = {"kernel": kernel_symbol(1, c3.nb), "bound": "hbm", "achieved": round(ah, 1),
                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ah / HBM_PEAK_GBS, 4),
@@ -758,10 +822,12 @@ def c3_batch(args, ws, rank):
 FP64_MFMA_PEAK_TFS = 78.6   # MI355X FP64 matrix peak (AMD spec; the guide lists no fp64 row)
 
 
-def ba_cholesky_roofline(n, blocked):
+def ba_cholesky_roofline(n, regime):
     """Live fp64 MFMA roofline of the dense Cholesky solve (n^3/3 + 2n^2 flops per LM
-    trial): a C4 / C5-sized SPD reduced camera system factored and solved by the same kernels the
-    LM loop launches, timed with HIP events around back-to-back launches."""
+    trial): a C4 / C5-sized SPD reduced camera system factored and solved by the persistent DAG
+    kernel the LM loop launches (k_chol_dag: one launch per solve, ba_chol_dag.hip), timed with HIP
+    events around 20 back-to-back launches. Counters: the same workload's rocprofv3 --pmc passes
+    (tools/pmc_workload.py c4 / c5)."""
     from orb_slam3_ros2_amd._lib import lib
     rng = np.random.default_rng(3)
     A = rng.standard_normal((n, n))
@@ -769,22 +835,16 @@ def ba_cholesky_roofline(n, blocked):
     b = rng.standard_normal(n)
     x = np.zeros(n)
     ms = ctypes.c_float(0)
-    L = lib()
-    if blocked:
-        rc = L.orbhip_test_cholesky_blocked(S.ctypes.data, b.ctypes.data, x.ctypes.data, n, ctypes.byref(ms))
-        kern = "k_cb_diag + k_cb_update + k_cb_back (dense S)"
-    else:
-        rc = L.orbhip_test_cholesky_reg(S.ctypes.data, b.ctypes.data, x.ctypes.data, n, 20, ctypes.byref(ms), None)
-        kern = "k_ba_chol_reg"
+    rc = lib().orbhip_test_cholesky_dag(S.ctypes.data, b.ctypes.data, x.ctypes.data, n, 20, 0, ctypes.byref(ms),
+                                        None)
     if rc != 0:
         return {"error": rc}
     err = float(np.abs(S @ x - b).max() / np.abs(b).max())
     flops = n ** 3 / 3 + 2 * n * n
     ach = flops / (ms.value * 1e-3) / 1e12
-    return {"kernel": kern, "bound": "mfma", "achieved": round(ach, 4), "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
-            "frac": round(ach / FP64_MFMA_PEAK_TFS, 6), "n": n, "flops_per_launch": int(flops),
-            "avg_launch_ms": round(ms.value, 4), "residual": err,
-            "counters": load_counters(kern.split()[0], "c5" if blocked else "c4")}
+    return {"kernel": "k_chol_dag", "bound": "mfma", "achieved": round(ach, 4), "peak": FP64_MFMA_PEAK_TFS,
+            "unit": "TFLOP/s", "frac": round(ach / FP64_MFMA_PEAK_TFS, 6), "n": n, "flops_per_launch": int(flops),
+            "avg_launch_ms": round(ms.value, 4), "residual": err, "counters": load_counters("k_chol_dag", regime)}
 
 
 def c4_lba(args, ws, rank, ctx):
@@ -818,8 +878,8 @@ def c4_lba(args, ws, rank, ctx):
     out["c4_lba_batch_per_gpu"] = len(probs)
     out["c4_lba_batched_trials_mean"] = round(float(np.mean([x.lm_trials for x in rs])), 2)
     if rank == 0:
-        out["c4_roofline"] = ba_cholesky_roofline(294, blocked=False)
-        out["c5_roofline"] = ba_cholesky_roofline(2394, blocked=True)
+        out["c4_roofline"] = ba_cholesky_roofline(294, "c4")
+        out["c5_roofline"] = ba_cholesky_roofline(2394, "c5")
     return out
 
 
@@ -865,8 +925,13 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                      "traffic": load_traffic(ks, "c2"), "counters": load_counters(ks, "c2"),
                      "algorithmic_bytes_per_launch": int(r["dom_bytes"]), "avg_launch_ms": round(r["dom_avg_ms"], 5),
-                     "launches_timed": r["dom_n"], "avg_launch_ms_in_flight": round(r["dom_avg_ms_in_flight"], 5),
-                     "stage_avg_ms_calibration": {STAGES[k]: round(v, 5) for k, v in r["stage_ms"].items()}},
+                     "launches_timed": r["dom_n"],
+                     "timing": "kernel execution (hipExtLaunchKernelGGL events) over a replay of the timed "
+                               "16-camera stream; rocprofv3 --kernel-trace of this C2 section: "
+                               "profiles/r03_c2_kernel_stats.md",
+                     "stage_avg_ms": {STAGES[k]: round(v, 5) for k, v in r["stage_ms"].items()},
+                     "stage_avg_ms_one_frame_stream": {STAGES[k]: round(v, 5)
+                                                       for k, v in r["stage_ms_one_frame"].items()}},
     }
     if not args.no_extra:
         wd = Watchdog(out, rank, args.extra_timeout)
@@ -899,6 +964,7 @@ def main():
             out["cpu_baseline"]["c4_lba_single_core_kf_per_s"] = round(cl["single"], 2)
             out["cpu_baseline"]["c4_lba_sample"] = f"{cl['solves']} oracle LBA solves, {cl['cores']} threads"
             out["cpu_baseline"].update(cpu_f8_tracking())
+            out["cpu_baseline"].update(cpu_gba(iters=args.gba_iters))
             # C3's workload on the CPU: 1280x720 frames of the same generator, each extracted and
             # matched to the previous one, one frame stream per thread (bounded sample)
             c3f = make_stream_frames(16, BatchC3.W, BatchC3.H, 5000)

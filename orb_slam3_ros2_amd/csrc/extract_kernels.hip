@@ -1919,7 +1919,7 @@ void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs
     const LevelGeom& D = hP.lv[l];
     dim3 blk(64, 4, 1);
     dim3 grd((D.h + 4 * kRzRows - 1) / (4 * kRzRows), (D.w + 255) / 256, B);
-    hipLaunchKernelGGL(k_resize, grd, blk, 0, st, dP, fb, l, xofs, xalpha, yofs, ybeta);
+    ORBHIP_LAUNCH(k_resize, grd, blk, 0, st, dP, fb, l, xofs, xalpha, yofs, ybeta);
 }
 
 void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameBufs& fb, int B, const ConeRect* rects,
@@ -1929,7 +1929,7 @@ void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameB
         (void)hipFuncSetAttribute((const void*)k_pyr_cone, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
         attr = true;
     }
-    hipLaunchKernelGGL(k_pyr_cone, dim3(ntiles, B), dim3(1024), lds, st, dP, fb, rects, ctab, tab_stride,
+    ORBHIP_LAUNCH(k_pyr_cone, dim3(ntiles, B), dim3(1024), lds, st, dP, fb, rects, ctab, tab_stride,
                        xcd_run_for(B));
 }
 
@@ -1948,7 +1948,7 @@ void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* c
     const int xr = xcd_run_for(B);
     const bool compact = hP.fast_win_rows <= 56 && hP.fast_win_cols + 3 <= 64;   // window dwords (sh <= 3) fit a row
 #define ORBHIP_FAST_LAUNCH(NTV, WRV) \
-    hipLaunchKernelGGL((k_fast_cells<NTV, WRV>), grd, dim3(NTV), 0, st, dP, cells, fb, cand, cand_cnt, err, xr)
+    ORBHIP_LAUNCH((k_fast_cells<NTV, WRV>), grd, dim3(NTV), 0, st, dP, cells, fb, cand, cand_cnt, err, xr)
     if (nt == 1024 && compact)
         ORBHIP_FAST_LAUNCH(1024, 56);
     else if (nt == 1024)
@@ -1991,7 +1991,7 @@ void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom*
                    int* lvl_nlap, const OctreeCfg& cfg, int* err, int B, hipStream_t st) {
     const size_t lds = octree_lds_bytes(hP, cfg);
     dim3 grd(B, hP.n_levels, 1);
-    hipLaunchKernelGGL(k_octree, grd, dim3(1024), lds, st, dP, cells, otab, cand, cand_cnt, kscratch, nscratch, lvl_kp,
+    ORBHIP_LAUNCH(k_octree, grd, dim3(1024), lds, st, dP, cells, otab, cand, cand_cnt, kscratch, nscratch, lvl_kp,
                        lvl_cnt, lvl_nlap, cfg, err);
 }
 
@@ -2005,12 +2005,12 @@ void launch_desc(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& 
     static const int mode = getenv("ORBHIP_DESC_MODE") ? atoi(getenv("ORBHIP_DESC_MODE")) : -1;
     const bool per_wg = mode >= 0 ? mode == 1 : B * hP.kp_slots_total <= kDescKpMaxSlots;
     if (per_wg) {
-        hipLaunchKernelGGL(k_desc_kp, dim3(hP.kp_slots_total, B, 1), dim3(256), 0, st, dP, fb, lvl_kp, lvl_cnt,
+        ORBHIP_LAUNCH(k_desc_kp, dim3(hP.kp_slots_total, B, 1), dim3(256), 0, st, dP, fb, lvl_kp, lvl_cnt,
                            lvl_nlap, disc, out_kps, out_desc, cap, n_out, mono_out, xcd_run_for(B));
         return;
     }
     dim3 grd((hP.kp_slots_total + 3) / 4, B, 1);
-    hipLaunchKernelGGL(k_desc, grd, dim3(256), 0, st, dP, fb, lvl_kp, lvl_cnt, lvl_nlap, disc, out_kps, out_desc,
+    ORBHIP_LAUNCH(k_desc, grd, dim3(256), 0, st, dP, fb, lvl_kp, lvl_cnt, lvl_nlap, disc, out_kps, out_desc,
                        cap, n_out, mono_out, xcd_run_for(B));
 }
 

@@ -444,7 +444,7 @@ static void run_match(const MatchView& v, int npairs, int max_q, int max_t, int 
     const char* unf = std::getenv("ORBHIP_MATCH_UNFUSED");   // A/B switch (read per call: tests flip it)
     if (sync && npairs <= kFusedMaxPairs && !(unf && unf[0] && unf[0] != '0')) {
         if (timer) timer->begin(5, st);
-        hipLaunchKernelGGL(k_match_fused, dim3((unsigned)std::max(1, (max_q + kFQ - 1) / kFQ), npairs), dim3(1024),
+        ORBHIP_LAUNCH(k_match_fused, dim3((unsigned)std::max(1, (max_q + kFQ - 1) / kFQ), npairs), dim3(1024),
                            0, st, v, th_low, ratio, check_orientation, match, best, second, nmatch, sync);
         if (timer) timer->end(5, st);
         return;
@@ -457,13 +457,13 @@ static void run_match(const MatchView& v, int npairs, int max_q, int max_t, int 
     if (timer) timer->begin(5, st);
     if (qblocks > 0 && max_t > 0) {
         if (small)
-            hipLaunchKernelGGL(k_match_top2<kTCSmall>, dim3(qblocks, nch, npairs), dim3(256), 0, st, v, part, nch,
+            ORBHIP_LAUNCH(k_match_top2<kTCSmall>, dim3(qblocks, nch, npairs), dim3(256), 0, st, v, part, nch,
                                max_q);
         else
-            hipLaunchKernelGGL(k_match_top2<kTC>, dim3(qblocks, nch, npairs), dim3(256), 0, st, v, part, nch, max_q);
+            ORBHIP_LAUNCH(k_match_top2<kTC>, dim3(qblocks, nch, npairs), dim3(256), 0, st, v, part, nch, max_q);
     }
     if (timer) { timer->end(5, st); timer->begin(6, st); }
-    hipLaunchKernelGGL(k_match_finish, dim3(npairs), dim3(1024), 0, st, v, part, nch, max_q, tc, th_low, ratio,
+    ORBHIP_LAUNCH(k_match_finish, dim3(npairs), dim3(1024), 0, st, v, part, nch, max_q, tc, th_low, ratio,
                        check_orientation, match, best, second, nmatch);
     if (timer) timer->end(6, st);
 }

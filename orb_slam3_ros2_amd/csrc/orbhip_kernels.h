@@ -1,5 +1,6 @@
 // Host-visible launchers of the gfx950 kernels (one TU per kernel family, no RDC).
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -25,16 +26,40 @@ struct OctreeCfg {
     int max_dh;            // deepest pyramid level allowed (<= 6; tests lower it to force the fallback)
 };
 
-// Live timing of one pipeline stage with hipEvents on the launch stream.
+// Live timing of one pipeline stage. The kernels launched between begin() and end() carry the
+// timer's event pair (hipExtLaunchKernelGGL: the first launch the start event, every launch the
+// stop event), so a pair spans the first kernel's start to the last kernel's end on the device:
+// the execution-only duration rocprofv3's kernel trace reports, without the dispatch latency an
+// event pair recorded on the stream around the launches would add.
+struct StageTimer;
+inline thread_local StageTimer* g_stage_timer = nullptr;   // the timer whose stage is open on this thread
 struct StageTimer {
     int stage = 0;                    // selected stage id (0 = off)
     int n = 0;                        // recorded pairs
     static constexpr int kCap = 8192;
     hipEvent_t ev[2 * kCap];
     bool created = false;
-    void begin(int s, hipStream_t st) { if (s == stage && n < kCap) (void)hipEventRecord(ev[2 * n], st); }
-    void end(int s, hipStream_t st) { if (s == stage && n < kCap) { (void)hipEventRecord(ev[2 * n + 1], st); n++; } }
+    bool used = false;                // a kernel of the open stage carries this pair
+    void begin(int s, hipStream_t) {
+        if (s == stage && n < kCap) { used = false; g_stage_timer = this; }
+    }
+    void end(int s, hipStream_t) {
+        if (s == stage && g_stage_timer == this) { g_stage_timer = nullptr; if (used) n++; }
+    }
 };
+
+// every pipeline-stage kernel launches through this (the stage timer's events when one is open)
+#define ORBHIP_LAUNCH(kern, grid, block, shm, st, ...)                                                          \
+    do {                                                                                                      \
+        ::orbhip::StageTimer* t_ = ::orbhip::g_stage_timer;                                                   \
+        if (t_) {                                                                                             \
+            hipExtLaunchKernelGGL(kern, grid, block, (uint32_t)(shm), st, t_->used ? nullptr : t_->ev[2 * t_->n], \
+                                  t_->ev[2 * t_->n + 1], 0u, __VA_ARGS__);                                    \
+            t_->used = true;                                                                                  \
+        } else {                                                                                              \
+            hipLaunchKernelGGL(kern, grid, block, shm, st, __VA_ARGS__);                                      \
+        }                                                                                                     \
+    } while (0)
 
 // ---- extraction ----
 void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameBufs& fb, int B, const ConeRect* rects,

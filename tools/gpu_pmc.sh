@@ -9,6 +9,13 @@ mkdir -p gpurun_out/pmc
 P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE"
 P2="SQ_LDS_BANK_CONFLICT SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE"
 for regime in ${REGIMES:-c2 c3 c4 c5}; do
+  # plain kernel trace of the same workload (the durations the bench's live timing is checked against)
+  timeout -s KILL 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pmc/${regime}_stats -o run \
+      -- python3 tools/pmc_workload.py $regime > gpurun_out/pmc/${regime}_stats.log 2>&1
+  rc=$?; echo "$regime stats rc=$rc"
+  if [ $rc -ne 0 ]; then tail -5 gpurun_out/pmc/${regime}_stats.log; exit $rc; fi
+  python3 tools/prof_summary.py stats "$(ls gpurun_out/pmc/${regime}_stats/*kernel_stats.csv | head -1)" \
+      gpurun_out/pmc/${PFX:-r03}_${regime}_kernel_stats.md "tools/pmc_workload.py $regime" || exit 1
   for pass in p1 p2 fetch write; do
     case $pass in
       p1) ctr="$P1";; p2) ctr="$P2";; fetch) ctr="FETCH_SIZE";; write) ctr="WRITE_SIZE";;

@@ -2,10 +2,12 @@
 """Short fixed workloads for the rocprofv3 --pmc passes (tools/gpu_pmc.sh), one regime each so a
 kernel's counters are not mixed across regimes:
 
-  c2  the bench's C2 one-frame stream (640x480, extract + match to the previous frame), 200 frames
-  c3  the bench's C3 batch (1280x720, B=64, extract + 63 pair matches), 4 batches
-  c4  C4 LocalBundleAdjustment (50 KF / 2000 pts / 8000 obs, 10 LM iterations), 3 solves
-  c5  the C5 reduced camera system's blocked Cholesky (dense n = 2394), 3 solves
+  c2    the bench's C2 stream: 16 cameras (640x480, extract + match to the camera's previous
+        frame), 40 steps of one frame per camera, as in the bench's timed region
+  c3    the bench's C3 batch (1280x720, B=64, extract + 63 pair matches), 4 batches
+  c4    the C4-sized dense reduced camera system (n = 294) solved by k_chol_dag, 2 x 21 solves
+  c4lba C4 LocalBundleAdjustment (50 KF / 2000 pts / 8000 obs, 10 LM iterations), 3 solves
+  c5    the C5-sized dense reduced camera system (n = 2394) solved by k_chol_dag, 2 x 21 solves
 """
 import ctypes
 import os
@@ -19,14 +21,17 @@ import bench  # noqa: E402
 
 mode = sys.argv[1]
 if mode == "c2":
-    s = bench.FrontendC2(0, 1, 1)
-    for _ in range(200):
+    s = bench.FrontendC2(0, 1, 16)
+    for _ in range(40):
         s.step()
 elif mode == "c3":
     c3 = bench.BatchC3(0, 1)
     for _ in range(4):
         c3.step()
 elif mode == "c4":
+    for _ in range(2):
+        bench.ba_cholesky_roofline(294, "c4")
+elif mode == "c4lba":
     from orb_slam3_ros2_amd import Optimizer
     from orb_slam3_ros2_amd.synthetic import synthetic_ba_problem
     prob, _ = synthetic_ba_problem()
@@ -34,8 +39,8 @@ elif mode == "c4":
     for _ in range(3):
         opt.LocalBundleAdjustment(prob)
 elif mode == "c5":
-    for _ in range(3):
-        bench.ba_cholesky_roofline(2394, blocked=True)
+    for _ in range(2):
+        bench.ba_cholesky_roofline(2394, "c5")
 else:
     raise SystemExit(f"unknown mode {mode}")
 torch.cuda.synchronize()
