@@ -17,6 +17,7 @@ from collections import defaultdict
 
 
 def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "")
     m = re.match(r"(?:void )?(?:[\w:]+::)?(\w+)(?:<.*)?\(", name)
     return m.group(1) if m else name[:60]
 
