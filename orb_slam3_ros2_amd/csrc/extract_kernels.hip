@@ -208,7 +208,7 @@ __global__ __launch_bounds__(256) void k_resize(const ExtractPlan* __restrict__ 
 __device__ __forceinline__ int small_div(int i, float inv_d) { return (int)(((float)i + 0.5f) * inv_d); }
 
 // ---------------------------------------------------------------------------
-// k_pyr_cone: the whole cascade (levels 1..L-1) in ONE launch. Each workgroup owns a tile of
+// k_pyr_cone: the whole cascade (levels 1..L-1, or s0+1..L-1 behind s0 k_resize levels) in ONE launch. Each workgroup owns a tile of
 // the last level and the matching slice of every level (a partition per level); it recomputes
 // in LDS the cone of each level its slices need (bit-exact: the same per-pixel INTER_LINEAR as
 // k_resize, from the level below held in LDS, level 0 staged from the frame) and writes only its
@@ -222,31 +222,32 @@ __device__ __forceinline__ void wait_vm_all() { asm volatile("s_waitcnt vmcnt(0)
 
 __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P, const FrameBufs& fb,
                                               const ConeRect* __restrict__ rects, const int* __restrict__ ctab,
-                                              int tab_stride, uint8_t* __restrict__ cone, int tile, int f) {
+                                              int tab_stride, uint8_t* __restrict__ cone, int tile, int f, int s0) {
     TR_BEGIN()
     const int L = P->n_levels, tid = threadIdx.x, nt = blockDim.x;
     const ConeRect* R = rects + (size_t)tile * kMaxLevels;
     int boff[kMaxLevels], toff[kMaxLevels];
     int tot = 0;
-    // level 0 is staged as aligned dwords: rows of P0 = round_up(width + 3, 4) bytes, the region
-    // starting at byte sh0 of its row (sh0: the frame address misalignment, 0 on the byte path)
-    const int P0 = (R[0].nx1 - R[0].nx0 + 6) & ~3;
-    for (int l = 0; l < L; l++) {
+    // the source level s0 (0: the frame; s0 >= 1: a pyramid level written by k_resize) is staged
+    // as aligned dwords: rows of P0 = round_up(width + 3, 4) bytes, the region starting at byte
+    // sh0 of its row (sh0: the address misalignment, 0 on the byte path)
+    const int P0 = (R[s0].nx1 - R[s0].nx0 + 6) & ~3;
+    for (int l = s0; l < L; l++) {
         boff[l] = tot;
-        tot += ((l == 0 ? P0 : (R[l].nx1 - R[l].nx0)) * (R[l].ny1 - R[l].ny0) + 15) & ~15;
+        tot += ((l == s0 ? P0 : (R[l].nx1 - R[l].nx0)) * (R[l].ny1 - R[l].ny0) + 15) & ~15;
     }
     int sh0 = 0;
     int* tab = (int*)(cone + tot);
     int ttot = 0;
-    for (int l = 1; l < L; l++) {
+    for (int l = s0 + 1; l < L; l++) {
         toff[l] = ttot;
         ttot += 2 * (R[l].nx1 - R[l].nx0) + 3 * (R[l].ny1 - R[l].ny0);
     }
     // ---- one round trip: the tile's tables of every level (prebuilt by the host in LDS layout)
     // and its level-0 cone, all loads issued before any store ----
     {
-        const ImgRef in0 = level_img(P, fb, f, 0);
-        const ConeRect r = R[0];
+        const ImgRef in0 = level_img(P, fb, f, s0);
+        const ConeRect r = R[s0];
         const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0;
         const uint8_t* src0 = in0.p + (int64_t)r.ny0 * in0.pitch + r.nx0;
         const int* gt = ctab + (size_t)tile * tab_stride;
@@ -255,7 +256,7 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
         const int nwd = dw ? (nw + sh0 + 3) >> 2 : 0;   // dwords per row (<= P0 / 4)
         const int tot0 = dw ? nwd * nh : nw * nh;
         const float inv_n = 1.0f / (float)(dw ? nwd : nw);
-        uint8_t* lv0 = cone + boff[0];
+        uint8_t* lv0 = cone + boff[s0];
         if (dw && tot0 <= 1024 && ttot <= 2 * 1024 && nt == 1024) {
             const uint32_t* s4 = (const uint32_t*)(src0 - sh0);
             const int p4 = in0.pitch >> 2;
@@ -270,12 +271,32 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
                 if (tid + 1024 * u < ttot) tab[tid + 1024 * u] = tv[u];
             if (tid < tot0) ((uint32_t*)lv0)[y * (P0 >> 2) + x] = v;
         } else if (dw) {
+            // 8 loads per thread in flight before their stores (a load-store loop waits out one
+            // global round trip per step)
             const uint32_t* s4 = (const uint32_t*)(src0 - sh0);
             const int p4 = in0.pitch >> 2;
-            for (int i = tid; i < ttot; i += nt) tab[i] = gt[i];
-            for (int i = tid; i < tot0; i += nt) {
-                const int y = small_div(i, inv_n), x = i - y * nwd;
-                ((uint32_t*)lv0)[y * (P0 >> 2) + x] = s4[(int64_t)y * p4 + x];
+            constexpr int U = 8;
+            for (int i0 = tid; i0 < ttot; i0 += U * nt) {
+                int v[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) v[u] = gt[min(i0 + u * nt, ttot - 1)];
+#pragma unroll
+                for (int u = 0; u < U; u++)
+                    if (i0 + u * nt < ttot) tab[i0 + u * nt] = v[u];
+            }
+            for (int i0 = tid; i0 < tot0; i0 += U * nt) {
+                uint32_t v[U];
+                int o[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int i = min(i0 + u * nt, tot0 - 1);
+                    const int y = small_div(i, inv_n), x = i - y * nwd;
+                    v[u] = s4[(int64_t)y * p4 + x];
+                    o[u] = y * (P0 >> 2) + x;
+                }
+#pragma unroll
+                for (int u = 0; u < U; u++)
+                    if (i0 + u * nt < tot0) ((uint32_t*)lv0)[o[u]] = v[u];
             }
         } else {
             for (int i = tid; i < ttot; i += nt) tab[i] = gt[i];
@@ -287,12 +308,12 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
     }
     __syncthreads();
     TR_PHASE(0, 0)
-    for (int l = 1; l < L; l++) {
+    for (int l = s0 + 1; l < L; l++) {
         const LevelGeom& D = P->lv[l];
         const ConeRect r = R[l], rp = R[l - 1];
-        const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0, nwp = l == 1 ? P0 : rp.nx1 - rp.nx0;
+        const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0, nwp = l == s0 + 1 ? P0 : rp.nx1 - rp.nx0;
         const int* t = tab + toff[l];
-        const uint8_t* src = cone + boff[l - 1] + (l == 1 ? sh0 : 0);
+        const uint8_t* src = cone + boff[l - 1] + (l == s0 + 1 ? sh0 : 0);
         uint8_t* dst = fb.pyr + (int64_t)f * P->pyr_bytes + D.pyr_off;
         const float inv_nw = 1.0f / (float)nw;
         const bool noclamp = D.rz_noclamp != 0;
@@ -338,10 +359,10 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
 
 __global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict__ P, FrameBufs fb,
                                                    const ConeRect* __restrict__ rects, const int* __restrict__ ctab,
-                                                   int tab_stride, int xrun) {
+                                                   int tab_stride, int xrun, int s0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t cone[];
     const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
-    pyr_cone_body(P, fb, rects, ctab, tab_stride, cone, lg % X, lg / X);
+    pyr_cone_body(P, fb, rects, ctab, tab_stride, cone, lg % X, lg / X, s0);
 }
 
 // ---------------------------------------------------------------------------
@@ -1923,14 +1944,14 @@ void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs
 }
 
 void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameBufs& fb, int B, const ConeRect* rects,
-                     const int* ctab, int tab_stride, hipStream_t st) {
+                     const int* ctab, int tab_stride, hipStream_t st, int s0, int nthreads) {
     static bool attr = false;
     if (!attr) {
         (void)hipFuncSetAttribute((const void*)k_pyr_cone, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
         attr = true;
     }
-    ORBHIP_LAUNCH(k_pyr_cone, dim3(ntiles, B), dim3(1024), lds, st, dP, fb, rects, ctab, tab_stride,
-                       xcd_run_for(B));
+    ORBHIP_LAUNCH(k_pyr_cone, dim3(ntiles, B), dim3(nthreads), lds, st, dP, fb, rects, ctab, tab_stride,
+                  xcd_run_for(B), s0);
 }
 
 void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,

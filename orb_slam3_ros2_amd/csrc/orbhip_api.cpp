@@ -66,6 +66,13 @@ struct DevBuf {
     }
 };
 
+constexpr int kConeHiStart = 2;        // batches: k_resize for levels 1..2, one cone launch for the rest
+// threads per batch-cone tile: ORBHIP_CONE_HI_THREADS (256 / 512 / 1024), else 256
+static int cone_hi_threads() {
+    static const int t = std::getenv("ORBHIP_CONE_HI_THREADS") ? std::atoi(std::getenv("ORBHIP_CONE_HI_THREADS")) : 256;
+    return (t == 512 || t == 1024) ? t : 256;
+}
+
 struct Plan {
     ExtractPlan h{};
     std::vector<CellGeom> cells;
@@ -77,6 +84,14 @@ struct Plan {
     size_t cone_lds = 0;
     DevBuf<ConeRect> d_cone;
     DevBuf<int> d_cone_tab;
+    // the same for batches: levels kConeHiStart+1..L-1 in one launch behind the first
+    // kConeHiStart k_resize levels (empty: all levels by k_resize)
+    std::vector<ConeRect> cone_hi;
+    std::vector<int> cone_hi_tab;
+    int cone_hi_tab_stride = 0, cone_hi_tiles = 0;
+    size_t cone_hi_lds = 0;
+    DevBuf<ConeRect> d_cone_hi;
+    DevBuf<int> d_cone_hi_tab;
     OctreeCfg oct{};
     int kp_cap_frame = 0;   // sum of level caps = max keypoints per frame
     DevBuf<ExtractPlan> d_plan;
@@ -88,6 +103,18 @@ struct Plan {
 
 }  // namespace
 
+// A plan depends only on the device, the frame size, the ORBextractor parameters, the cone tile
+// and the test switches read while building it, never on a context's buffers: contexts with the
+// same key (e.g. the 16 camera streams of the C2 bench) share one, so its tables (the cone's
+// per-tile resize tables are ~0.5 MB at 640x480) stay L2-resident once instead of once per
+// context. The cache holds weak references: a plan dies with the last context using it.
+struct PlanKey {
+    int device, w, h, nfeat, nlev, ini, mn, cone_tile, clist_cap, fast_nt, cone_hi_tile;
+    float scale;
+    bool operator<(const PlanKey& o) const {
+        return std::memcmp(this, &o, sizeof(PlanKey)) < 0;
+    }
+};
 struct orbhip_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -96,7 +123,7 @@ struct orbhip_ctx {
     std::vector<float> scale, inv_scale;
     std::vector<int> feat, umax;
     int blurk[7] = {0};
-    std::map<std::tuple<int, int, int, int, int>, std::shared_ptr<Plan>> plans;   // (w, h, cone tile, FAST clist cap, FAST threads); shared with other contexts (plan_cache)
+    std::map<PlanKey, std::shared_ptr<Plan>> plans;   // shared with other contexts (plan_cache)
     // per-batch scratch (grown on demand)
     DevBuf<uint8_t> d_in, d_pyr;
     DevBuf<uint32_t> d_cand, d_kscratch;
@@ -176,18 +203,6 @@ static void build_orb_tables(orbhip_ctx* c) {
 // ---------------------------------------------------------------------------
 // per-size plan
 // ---------------------------------------------------------------------------
-// A plan depends only on the device, the frame size, the ORBextractor parameters, the cone tile
-// and the test switches read while building it, never on a context's buffers: contexts with the
-// same key (e.g. the 16 camera streams of the C2 bench) share one, so its tables (the cone's
-// per-tile resize tables are ~0.5 MB at 640x480) stay L2-resident once instead of once per
-// context. The cache holds weak references: a plan dies with the last context using it.
-struct PlanKey {
-    int device, w, h, nfeat, nlev, ini, mn, cone_tile, clist_cap, fast_nt;
-    float scale;
-    bool operator<(const PlanKey& o) const {
-        return std::memcmp(this, &o, sizeof(PlanKey)) < 0;
-    }
-};
 static std::mutex g_plan_m;
 static std::map<PlanKey, std::weak_ptr<Plan>>& plan_cache() {
     static auto* m = new std::map<PlanKey, std::weak_ptr<Plan>>();   // never destroyed (exit order)
@@ -203,24 +218,118 @@ static int cone_tile_of(const orbhip_ctx* c) {
     return ts_env > 0 ? ts_env : (c->cone_tile > 0 ? c->cone_tile : 10);
 }
 
+// the batch cone's tile edge (last-level pixels): ORBHIP_CONE_HI_TILE (read per plan lookup), else 32
+static int cone_hi_tile_of() {
+    const char* e = std::getenv("ORBHIP_CONE_HI_TILE");
+    return e ? std::max(4, std::atoi(e)) : 32;
+}
+
+// k_pyr_cone tables from source level s0 (0: the frame): tiles of ts x ts pixels of the last
+// level, every level l > s0 cut into the same tile grid (an even partition, the tile's owned
+// pixels) plus the halo its level l+1 need reads (the need), the source level's need staged.
+// Returns the tile count; rects (kMaxLevels per tile), the per-tile resize tables in the kernel's
+// LDS layout (row indices clamped to the source), their stride, and the LDS bytes of the largest.
+static int cone_tables(const ExtractPlan& P, const Plan& pl, int s0, int ts, std::vector<ConeRect>& rects,
+                       std::vector<int>& ctab, size_t& tab_stride, size_t& lds_max) {
+    const int L = P.n_levels;
+    const LevelGeom& T = P.lv[L - 1];
+    const int ntx = (T.w + ts - 1) / ts, nty = (T.h + ts - 1) / ts;
+    lds_max = 0;
+    rects.assign((size_t)ntx * nty * kMaxLevels, ConeRect{});
+    // the source rectangle of level l's need [nx0, nx1) x [ny0, ny1) on level l - 1
+    auto source_of = [&](int l, int nx0, int nx1, int ny0, int ny1, int* a0, int* a1, int* b0, int* b1) {
+        const LevelGeom& U = P.lv[l];
+        const LevelGeom& G = P.lv[l - 1];
+        *a0 = pl.xofs[U.xtab_off + nx0];
+        *a1 = pl.xofs[U.xtab_off + nx1 - 1] + ((nx1 - 1) < U.xmax ? 1 : 0) + 1;
+        auto clampr = [&](int r) { return r < 0 ? 0 : (r < G.h ? r : G.h - 1); };
+        *b0 = clampr(pl.yofs[U.ytab_off + ny0]);
+        *b1 = clampr(pl.yofs[U.ytab_off + ny1 - 1] + 1) + 1;
+    };
+    for (int ti = 0; ti < nty; ti++)
+        for (int tj = 0; tj < ntx; tj++) {
+            ConeRect* R = &rects[((size_t)ti * ntx + tj) * kMaxLevels];
+            int nx0 = 0, nx1 = 0, ny0 = 0, ny1 = 0;   // need of the level above (l + 1)
+            for (int l = L - 1; l > s0; l--) {
+                const LevelGeom& G = P.lv[l];
+                const int ox0 = (int)((int64_t)tj * G.w / ntx), ox1 = (int)((int64_t)(tj + 1) * G.w / ntx);
+                const int oy0 = (int)((int64_t)ti * G.h / nty), oy1 = (int)((int64_t)(ti + 1) * G.h / nty);
+                int a0 = ox0, a1 = ox1, b0 = oy0, b1 = oy1;
+                if (l < L - 1 && nx1 > nx0 && ny1 > ny0) {   // inputs of the level-(l+1) need
+                    int lo, hi, r0, r1;
+                    source_of(l + 1, nx0, nx1, ny0, ny1, &lo, &hi, &r0, &r1);
+                    a0 = std::min(a0, lo); a1 = std::max(a1, hi);
+                    b0 = std::min(b0, r0); b1 = std::max(b1, r1);
+                    if (ox1 <= ox0 || oy1 <= oy0) { a0 = lo; a1 = hi; b0 = r0; b1 = r1; }
+                }
+                R[l] = ConeRect{(int16_t)a0, (int16_t)a1, (int16_t)b0, (int16_t)b1,
+                                (int16_t)ox0, (int16_t)ox1, (int16_t)oy0, (int16_t)oy1};
+                nx0 = a0; nx1 = a1; ny0 = b0; ny1 = b1;
+            }
+            {   // source-level inputs of the level-(s0+1) need (staged in LDS)
+                int lo, hi, r0, r1;
+                source_of(s0 + 1, nx0, nx1, ny0, ny1, &lo, &hi, &r0, &r1);
+                R[s0] = ConeRect{(int16_t)lo, (int16_t)hi, (int16_t)r0, (int16_t)r1, 0, 0, 0, 0};
+            }
+            size_t tot = 0, ttot = 0;
+            for (int l = s0; l < L; l++) {   // source: rows of round_up(width + 3, 4) (dword staging)
+                const size_t wl = l == s0 ? (size_t)((R[s0].nx1 - R[s0].nx0 + 6) & ~3) : (size_t)(R[l].nx1 - R[l].nx0);
+                tot += (wl * (R[l].ny1 - R[l].ny0) + 15) & ~size_t(15);
+            }
+            for (int l = s0 + 1; l < L; l++)
+                ttot += 4 * (2 * (size_t)(R[l].nx1 - R[l].nx0) + 3 * (size_t)(R[l].ny1 - R[l].ny0));
+            lds_max = std::max(lds_max, tot + ttot);
+        }
+    tab_stride = 0;
+    for (int t = 0; t < ntx * nty; t++) {
+        size_t tt = 0;
+        for (int l = s0 + 1; l < L; l++) {
+            const ConeRect& r = rects[(size_t)t * kMaxLevels + l];
+            tt += 2 * (size_t)(r.nx1 - r.nx0) + 3 * (size_t)(r.ny1 - r.ny0);
+        }
+        tab_stride = std::max(tab_stride, tt);
+    }
+    ctab.assign((size_t)ntx * nty * tab_stride, 0);
+    for (int t = 0; t < ntx * nty; t++) {
+        int* o = ctab.data() + (size_t)t * tab_stride;
+        for (int l = s0 + 1; l < L; l++) {
+            const LevelGeom& D = P.lv[l];
+            const LevelGeom& S = P.lv[l - 1];
+            const ConeRect r = rects[(size_t)t * kMaxLevels + l];
+            const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0;
+            for (int i = 0; i < nw; i++) {
+                o[i] = pl.xofs[D.xtab_off + r.nx0 + i];
+                o[nw + i] = pl.xalpha[D.xtab_off + r.nx0 + i];
+            }
+            auto clampr = [&](int v) { return v < 0 ? 0 : (v < S.h ? v : S.h - 1); };
+            for (int j = 0; j < nh; j++) {
+                const int sy = pl.yofs[D.ytab_off + r.ny0 + j];
+                o[2 * nw + 3 * j] = clampr(sy);
+                o[2 * nw + 3 * j + 1] = clampr(sy + 1);
+                o[2 * nw + 3 * j + 2] = pl.ybeta[D.ytab_off + r.ny0 + j];
+            }
+            o += 2 * nw + 3 * nh;
+        }
+    }
+    return ntx * nty;
+}
+
 static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
-    const int ts = cone_tile_of(c);
-    // every setting the shared PlanKey holds is part of the context's key too, so an env switch
-    // (ORBHIP_FAST_CLIST_CAP / ORBHIP_FAST_NT) takes effect on an existing context
+    // the context's cache is keyed by the full PlanKey, so an env switch read here
+    // (ORBHIP_CONE_TILE / ORBHIP_CONE_HI_TILE / ORBHIP_FAST_CLIST_CAP / ORBHIP_FAST_NT) takes
+    // effect on an existing context too
     const char* cap_env = getenv("ORBHIP_FAST_CLIST_CAP");
-    const int clist_cap = cap_env ? atoi(cap_env) : -1;
     const char* nt_env = getenv("ORBHIP_FAST_NT");
-    const int fast_nt = nt_env ? atoi(nt_env) : -1;
-    auto key = std::make_tuple(w, h, ts, clist_cap, fast_nt);
-    auto it = c->plans.find(key);
-    if (it != c->plans.end()) { *out = it->second.get(); return ORBHIP_OK; }
     PlanKey k;
     std::memset(&k, 0, sizeof(k));
     k.device = c->device; k.w = w; k.h = h; k.nfeat = c->prm.n_features; k.nlev = c->prm.n_levels;
     k.ini = c->prm.ini_th_fast; k.mn = c->prm.min_th_fast; k.scale = c->prm.scale_factor;
-    k.cone_tile = ts;
-    k.clist_cap = clist_cap;
-    k.fast_nt = fast_nt;
+    k.cone_tile = cone_tile_of(c);
+    k.clist_cap = cap_env ? atoi(cap_env) : -1;
+    k.fast_nt = nt_env ? atoi(nt_env) : -1;
+    k.cone_hi_tile = cone_hi_tile_of();
+    auto it = c->plans.find(k);
+    if (it != c->plans.end()) { *out = it->second.get(); return ORBHIP_OK; }
     std::lock_guard<std::mutex> g(g_plan_m);
     std::shared_ptr<Plan> sp = plan_cache()[k].lock();
     if (!sp) {
@@ -228,7 +337,7 @@ static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
         plan_cache()[k] = sp;
     }
     *out = sp.get();
-    c->plans[key] = sp;
+    c->plans[k] = sp;
     return ORBHIP_OK;
 }
 
@@ -405,92 +514,31 @@ static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& ou
     P.fast_win_rows = hc_max;   // k_fast_cells' LDS variant
     P.fast_win_cols = wc_max;
     // cone pyramid tables: tiles of ~10x10 on the last level (252 at 640x480: the per-tile cascade
-    // is latency bound, so smaller cones finish sooner), an even partition of every level
+    // is latency bound, so smaller cones finish sooner), an even partition of every level; for
+    // batches a second set from level kConeHiStart with bigger tiles (the small levels' launches
+    // are latency bound there, the big levels' k_resize launches stream)
     if (L > 1) {
-        const LevelGeom& T = P.lv[L - 1];
+        std::vector<ConeRect> rects;
+        std::vector<int> ctab;
+        size_t stride = 0, lds = 0;
         const int ts = cone_tile_of(c);
-        const int ntx = (T.w + ts - 1) / ts, nty = (T.h + ts - 1) / ts;
-        size_t lds_max = 0;
-        std::vector<ConeRect> rects((size_t)ntx * nty * kMaxLevels);
-        for (int ti = 0; ti < nty; ti++)
-            for (int tj = 0; tj < ntx; tj++) {
-                ConeRect* R = &rects[((size_t)ti * ntx + tj) * kMaxLevels];
-                int nx0 = 0, nx1 = 0, ny0 = 0, ny1 = 0;   // need of the level above (l + 1)
-                for (int l = L - 1; l >= 1; l--) {
-                    const LevelGeom& G = P.lv[l];
-                    const int ox0 = (int)((int64_t)tj * G.w / ntx), ox1 = (int)((int64_t)(tj + 1) * G.w / ntx);
-                    const int oy0 = (int)((int64_t)ti * G.h / nty), oy1 = (int)((int64_t)(ti + 1) * G.h / nty);
-                    int a0 = ox0, a1 = ox1, b0 = oy0, b1 = oy1;
-                    if (l < L - 1 && nx1 > nx0 && ny1 > ny0) {   // inputs of the level-(l+1) need
-                        const LevelGeom& U = P.lv[l + 1];
-                        const int lo = pl->xofs[U.xtab_off + nx0];
-                        const int hi = pl->xofs[U.xtab_off + nx1 - 1] + ((nx1 - 1) < U.xmax ? 1 : 0);
-                        auto clampr = [&](int r) { return r < 0 ? 0 : (r < G.h ? r : G.h - 1); };
-                        const int r0 = clampr(pl->yofs[U.ytab_off + ny0]), r1 = clampr(pl->yofs[U.ytab_off + ny1 - 1] + 1);
-                        a0 = std::min(a0, lo); a1 = std::max(a1, hi + 1);
-                        b0 = std::min(b0, r0); b1 = std::max(b1, r1 + 1);
-                        if (ox1 <= ox0 || oy1 <= oy0) { a0 = lo; a1 = hi + 1; b0 = r0; b1 = r1 + 1; }
-                    }
-                    R[l] = ConeRect{(int16_t)a0, (int16_t)a1, (int16_t)b0, (int16_t)b1,
-                                    (int16_t)ox0, (int16_t)ox1, (int16_t)oy0, (int16_t)oy1};
-                    nx0 = a0; nx1 = a1; ny0 = b0; ny1 = b1;
-                }
-                {   // level-0 inputs of the level-1 need (staged in LDS)
-                    const LevelGeom& U = P.lv[1];
-                    const LevelGeom& G = P.lv[0];
-                    const int lo = pl->xofs[U.xtab_off + nx0];
-                    const int hi = pl->xofs[U.xtab_off + nx1 - 1] + ((nx1 - 1) < U.xmax ? 1 : 0);
-                    auto clampr = [&](int r) { return r < 0 ? 0 : (r < G.h ? r : G.h - 1); };
-                    const int r0 = clampr(pl->yofs[U.ytab_off + ny0]), r1 = clampr(pl->yofs[U.ytab_off + ny1 - 1] + 1);
-                    R[0] = ConeRect{(int16_t)lo, (int16_t)(hi + 1), (int16_t)r0, (int16_t)(r1 + 1), 0, 0, 0, 0};
-                }
-                size_t tot = 0, ttot = 0;
-                for (int l = 0; l < L; l++) {   // level 0: rows of round_up(width + 3, 4) (k_pyr_cone dword staging)
-                    const size_t wl = l == 0 ? (size_t)((R[0].nx1 - R[0].nx0 + 6) & ~3) : (size_t)(R[l].nx1 - R[l].nx0);
-                    tot += (wl * (R[l].ny1 - R[l].ny0) + 15) & ~size_t(15);
-                }
-                for (int l = 1; l < L; l++)
-                    ttot += 4 * (2 * (size_t)(R[l].nx1 - R[l].nx0) + 3 * (size_t)(R[l].ny1 - R[l].ny0));
-                tot += ttot;
-                lds_max = std::max(lds_max, tot);
-            }
-        // the tables of each tile, in the kernel's LDS layout (row indices clamped to the source)
-        size_t tab_max = 0;
-        for (int t = 0; t < ntx * nty; t++) {
-            size_t tt = 0;
-            for (int l = 1; l < L; l++)
-                tt += 2 * (size_t)(rects[(size_t)t * kMaxLevels + l].nx1 - rects[(size_t)t * kMaxLevels + l].nx0) +
-                      3 * (size_t)(rects[(size_t)t * kMaxLevels + l].ny1 - rects[(size_t)t * kMaxLevels + l].ny0);
-            tab_max = std::max(tab_max, tt);
-        }
-        std::vector<int> ctab((size_t)ntx * nty * tab_max, 0);
-        for (int t = 0; t < ntx * nty; t++) {
-            int* o = ctab.data() + (size_t)t * tab_max;
-            for (int l = 1; l < L; l++) {
-                const LevelGeom& D = P.lv[l];
-                const LevelGeom& S = P.lv[l - 1];
-                const ConeRect r = rects[(size_t)t * kMaxLevels + l];
-                const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0;
-                for (int i = 0; i < nw; i++) {
-                    o[i] = pl->xofs[D.xtab_off + r.nx0 + i];
-                    o[nw + i] = pl->xalpha[D.xtab_off + r.nx0 + i];
-                }
-                auto clampr = [&](int v) { return v < 0 ? 0 : (v < S.h ? v : S.h - 1); };
-                for (int j = 0; j < nh; j++) {
-                    const int sy = pl->yofs[D.ytab_off + r.ny0 + j];
-                    o[2 * nw + 3 * j] = clampr(sy);
-                    o[2 * nw + 3 * j + 1] = clampr(sy + 1);
-                    o[2 * nw + 3 * j + 2] = pl->ybeta[D.ytab_off + r.ny0 + j];
-                }
-                o += 2 * nw + 3 * nh;
-            }
-        }
-        if (lds_max <= 60 * 1024) {
+        int tiles = cone_tables(P, *pl, 0, ts, rects, ctab, stride, lds);
+        if (lds <= 60 * 1024) {
             pl->cone_tab.swap(ctab);
-            pl->cone_tab_stride = (int)tab_max;
+            pl->cone_tab_stride = (int)stride;
             pl->cone.swap(rects);
-            pl->cone_tiles = ntx * nty;
-            pl->cone_lds = lds_max;
+            pl->cone_tiles = tiles;
+            pl->cone_lds = lds;
+        }
+        if (L > kConeHiStart + 1) {
+            tiles = cone_tables(P, *pl, kConeHiStart, cone_hi_tile_of(), rects, ctab, stride, lds);
+            if (lds <= 60 * 1024) {
+                pl->cone_hi_tab.swap(ctab);
+                pl->cone_hi_tab_stride = (int)stride;
+                pl->cone_hi.swap(rects);
+                pl->cone_hi_tiles = tiles;
+                pl->cone_hi_lds = lds;
+            }
         }
     }
     // IC_Angle disc offsets (u, v) packed as int16 pairs
@@ -531,6 +579,12 @@ static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& ou
     HIPOK(up(pl->d_disc, pl->disc));
     HIPOK(pl->d_otab.ensure(pl->otab.size()));
     HIPOK(hipMemcpy(pl->d_otab.p, pl->otab.data(), pl->otab.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    if (!pl->cone_hi.empty()) {
+        HIPOK(pl->d_cone_hi.ensure(pl->cone_hi.size()));
+        HIPOK(hipMemcpy(pl->d_cone_hi.p, pl->cone_hi.data(), pl->cone_hi.size() * sizeof(ConeRect),
+                        hipMemcpyHostToDevice));
+        HIPOK(up(pl->d_cone_hi_tab, pl->cone_hi_tab));
+    }
     if (!pl->cone.empty()) {
         HIPOK(pl->d_cone.ensure(pl->cone.size()));
         HIPOK(hipMemcpy(pl->d_cone.p, pl->cone.data(), pl->cone.size() * sizeof(ConeRect), hipMemcpyHostToDevice));
@@ -570,8 +624,10 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
     const int oct_max_dh = e_dh ? std::max(1, std::min(6, std::atoi(e_dh))) : 6;
     // pyramid engine, also per call: ORBHIP_NO_CONE=1 forces the k_resize cascade
     const bool no_cone = std::getenv("ORBHIP_NO_CONE") != nullptr;
+    // ORBHIP_NO_CONE_HI=1: batches run every level by k_resize
+    const bool no_cone_hi = std::getenv("ORBHIP_NO_CONE_HI") != nullptr;
     GraphKey key;
-    key.add(1).add((uint64_t)oct_fast).add((uint64_t)oct_max_dh).add((uint64_t)no_cone).add((uint64_t)c->fast_nt).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
+    key.add(1).add((uint64_t)oct_fast).add((uint64_t)oct_max_dh).add((uint64_t)no_cone).add((uint64_t)no_cone_hi).add((uint64_t)c->fast_nt).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
         .add((uint64_t)lap1).ptr(d_kps).ptr(d_desc).add((uint64_t)cap).ptr(d_n).ptr(d_mono).ptr(st).ptr(c->d_pyr.p)
         .ptr(c->d_cand.p).ptr(c->d_kscratch.p).ptr(c->d_nscratch.p).ptr(c->d_cand_cnt.p).ptr(c->d_lvl_kp.p)
         .ptr(c->d_lvl_cnt.p).ptr(c->d_lvl_nlap.p).ptr(c->d_err.p);
@@ -586,13 +642,18 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
                                            ? (size_t)std::atol(std::getenv("ORBHIP_CONE_MAX_WG"))
                                            : (size_t)1024;
         const bool cone_path = pl->cone_tiles && !no_cone && (size_t)B * pl->cone_tiles <= cone_max;
-        if (cone_path)
+        const bool cone_hi = !cone_path && pl->cone_hi_tiles && !no_cone_hi;
+        if (cone_path) {
             launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_cone_tab.p,
                             pl->cone_tab_stride, st);
-        else
-            for (int l = 1; l < P.n_levels; l++)
+        } else {
+            for (int l = 1; l < (cone_hi ? kConeHiStart + 1 : P.n_levels); l++)
                 launch_resize(pl->d_plan.p, P, fb, B, l, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p, pl->d_ybeta.p,
                               st);
+            if (cone_hi)
+                launch_pyr_cone(pl->d_plan.p, pl->cone_hi_tiles, pl->cone_hi_lds, fb, B, pl->d_cone_hi.p,
+                                pl->d_cone_hi_tab.p, pl->cone_hi_tab_stride, st, kConeHiStart, cone_hi_threads());
+        }
         tm.end(1, st);
         tm.begin(2, st);
         launch_fast(pl->d_plan.p, P, pl->d_cells.p, fb, B, c->d_cand.p, c->d_cand_cnt.p, c->d_err.p, st, c->fast_nt);

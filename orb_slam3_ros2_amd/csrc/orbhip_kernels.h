@@ -62,8 +62,10 @@ struct StageTimer {
     } while (0)
 
 // ---- extraction ----
+// s0 = 0: levels 1..L-1 from the frame (1024 threads per tile); s0 >= 1: levels s0+1..L-1 from
+// pyramid level s0 (written by k_resize before), `nthreads` per tile
 void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameBufs& fb, int B, const ConeRect* rects,
-                     const int* ctab, int tab_stride, hipStream_t st);
+                     const int* ctab, int tab_stride, hipStream_t st, int s0 = 0, int nthreads = 1024);
 void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, int B, int l,
                    const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st);
 void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,

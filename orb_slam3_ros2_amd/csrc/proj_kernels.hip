@@ -69,12 +69,15 @@ __global__ void k_proj_cells(ProjFrame f, const orbhip_kp* __restrict__ kps, int
 
 // SearchByProjection(CurrentFrame, LastFrame, th, bMono): window th * scale[lastOctave], levels
 // lastOctave - 1 .. lastOctave + 1
-__global__ void k_proj_prep_last(ProjFrame f, int nq, const float* __restrict__ pts, const int* __restrict__ oct,
-                                 const float* __restrict__ scale, float th, Query* __restrict__ qs) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nq) return;
+struct PrepLast {
+    const float* pts;
+    const int* oct;
+    const float* scale;
+    float th;
+};
+__device__ __forceinline__ Query prep_last(const ProjFrame& f, const PrepLast& a, int i) {
     Query Q{0, 0, 0, 0, 0, 0};
-    const float P[3] = {pts[3 * i], pts[3 * i + 1], pts[3 * i + 2]};
+    const float P[3] = {a.pts[3 * i], a.pts[3 * i + 1], a.pts[3 * i + 2]};
     float Xc[3];
     qrotf(f.q, P, Xc);
     Xc[0] += f.t[0]; Xc[1] += f.t[1]; Xc[2] += f.t[2];
@@ -82,27 +85,36 @@ __global__ void k_proj_prep_last(ProjFrame f, int nq, const float* __restrict__ 
     if (!(invzc < 0)) {
         const float u = f.fx * Xc[0] / Xc[2] + f.cx, v = f.fy * Xc[1] / Xc[2] + f.cy;
         if (!(u < f.minx || u > f.maxx || v < f.miny || v > f.maxy)) {
-            const int lo = oct[i];
-            Q = Query{u, v, th * scale[lo], lo - 1, lo + 1, 1};
+            const int lo = a.oct[i];
+            Q = Query{u, v, a.th * a.scale[lo], lo - 1, lo + 1, 1};
         }
     }
-    qs[i] = Q;
+    return Q;
+}
+__global__ void k_proj_prep_last(ProjFrame f, int nq, PrepLast a, Query* __restrict__ qs) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nq) return;
+    qs[i] = prep_last(f, a, i);
 }
 
 // Frame::isInFrustum(pMP, viewCosLimit) + the window of SearchByProjection(F, vpMapPoints, ...)
-__global__ void k_proj_prep_local(ProjFrame f, int nq, const float* __restrict__ pts, const float* __restrict__ nrm,
-                                  const float* __restrict__ mind, const float* __restrict__ maxd,
-                                  const uint8_t* __restrict__ skip, const float* __restrict__ scale, int n_levels,
-                                  float log_sf, float view_cos_limit, float th, int far_points, float th_far,
-                                  Query* __restrict__ qs, uint8_t* __restrict__ in_view, int* __restrict__ level) {
-    const int m = blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= nq) return;
+struct PrepLocal {
+    const float *pts, *nrm, *mind, *maxd;
+    const uint8_t* skip;
+    const float* scale;
+    int n_levels;
+    float log_sf, view_cos_limit, th;
+    int far_points;
+    float th_far;
+};
+__device__ __forceinline__ Query prep_local(const ProjFrame& f, const PrepLocal& a, int m, uint8_t* iv_out,
+                                            int* lvl_out) {
     Query Q{0, 0, 0, 0, 0, 0};
     uint8_t iv = 0;
     int lvl = -1;
     do {
-        if (skip && skip[m]) break;
-        const float* P = pts + 3 * m;
+        if (a.skip && a.skip[m]) break;
+        const float* P = a.pts + 3 * m;
         const float* R = f.R;
         const float Pc[3] = {R[0] * P[0] + R[1] * P[1] + R[2] * P[2] + f.t[0],
                              R[3] * P[0] + R[4] * P[1] + R[5] * P[2] + f.t[1],
@@ -114,23 +126,33 @@ __global__ void k_proj_prep_local(ProjFrame f, int nq, const float* __restrict__
         if (v < f.miny || v > f.maxy) break;
         const float PO[3] = {P[0] - f.Ow[0], P[1] - f.Ow[1], P[2] - f.Ow[2]};
         const float dist = sqrtf(PO[0] * PO[0] + PO[1] * PO[1] + PO[2] * PO[2]);
-        const float maxDistance = 1.2f * maxd[m], minDistance = 0.8f * mind[m];
+        const float maxDistance = 1.2f * a.maxd[m], minDistance = 0.8f * a.mind[m];
         if (dist < minDistance || dist > maxDistance) break;
-        const float* Pn = nrm + 3 * m;
+        const float* Pn = a.nrm + 3 * m;
         const float viewCos = (PO[0] * Pn[0] + PO[1] * Pn[1] + PO[2] * Pn[2]) / dist;
-        if (viewCos < view_cos_limit) break;
-        const float ratio = maxd[m] / dist;
-        int nScale = (int)ceilf(logf(ratio) / log_sf);   // MapPoint::PredictScale
+        if (viewCos < a.view_cos_limit) break;
+        const float ratio = a.maxd[m] / dist;
+        int nScale = (int)ceilf(logf(ratio) / a.log_sf);   // MapPoint::PredictScale
         if (nScale < 0) nScale = 0;
-        else if (nScale >= n_levels) nScale = n_levels - 1;
+        else if (nScale >= a.n_levels) nScale = a.n_levels - 1;
         iv = 1;
         lvl = nScale;
-        if (far_points && Pc_dist > th_far) break;
+        if (a.far_points && Pc_dist > a.th_far) break;
         float r = viewCos > 0.998 ? 2.5f : 4.0f;   // RadiusByViewingCos
-        if (th != 1.0f) r *= th;
-        Q = Query{u, v, r * scale[nScale], nScale - 1, nScale, 1};
+        if (a.th != 1.0f) r *= a.th;
+        Q = Query{u, v, r * a.scale[nScale], nScale - 1, nScale, 1};
     } while (false);
-    qs[m] = Q;
+    *iv_out = iv;
+    *lvl_out = lvl;
+    return Q;
+}
+__global__ void k_proj_prep_local(ProjFrame f, int nq, PrepLocal a, Query* __restrict__ qs,
+                                  uint8_t* __restrict__ in_view, int* __restrict__ level) {
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= nq) return;
+    uint8_t iv;
+    int lvl;
+    qs[m] = prep_local(f, a, m, &iv, &lvl);
     in_view[m] = iv;
     level[m] = lvl;
 }
@@ -271,6 +293,256 @@ __global__ __launch_bounds__(1024) void k_proj_finish(int nq, int check_orientat
     if (threadIdx.x == 0) *nmatch = cnt;
 }
 
+
+// ---------------------------------------------------------------------------
+// Two-launch form (the default while every candidate list fits kProjCap entries):
+//   k_proj_lists    one wave per query: the query's window (prep_last / prep_local), then the
+//                   round kernel's tests (cell rectangle, levels, |dx|,|dy| < r, pre-claimed
+//                   keypoints, distance < 256) over the frame's keypoints ONCE, the passing
+//                   keypoints appended by ballot as (dist << 32 | key << 4 | octave), key =
+//                   cell << 16 | index: a u64 compare is the (dist, key) walk order
+//   k_proj_resolve  ONE work-group: the fixed point of k_proj_round over the lists (owner tables
+//                   in LDS, one barrier per round: a round walks a few list entries per query
+//                   instead of scanning the frame), then k_proj_finish's rotation filter / count
+// so the search is one upload, two launches and one download. A longer list (status word) sends
+// the search to the round kernels with the inputs already on the device.
+// ---------------------------------------------------------------------------
+constexpr int kProjCap = 128;     // list entries per query
+constexpr int kProjMaxN = 8192;   // frame keypoints: staged in LDS (16 B each), 3 owner tables of n ints
+constexpr int kProjMaxQ = 8192;   // queries: list offsets in LDS
+constexpr int kListWaves = 16;    // queries per k_proj_lists work-group (one per wave)
+
+__device__ __forceinline__ int proj_decide(const Top2& t, int mode, float nnratio) {
+    if (t.d1 > kThHigh) return -1;
+    if (mode == 0) return t.k1 & 0xFFFF;
+    const bool same = t.l1 == t.l2;
+    const bool reject = same && (float)t.d1 > nnratio * (float)t.d2;
+    return (!reject && (!same || (float)t.d1 <= nnratio * (float)t.d2)) ? (t.k1 & 0xFFFF) : -1;
+}
+
+// the frame's keypoints are staged once per work-group in LDS as (x, y, cell << 16 | claimed << 8 |
+// octave, 0): PosInGrid computed as k_proj_cells does, a 16-byte read per lane and keypoint. The
+// query's window is computed first, so its loads overlap the staging. A list entry is written for
+// every keypoint passing the window tests (distance 256 included, skipped by the rounds): the
+// ballot does not wait on the descriptor load, so the loads of all the scan's steps overlap.
+// Round 0 of the fixed point (no exclusions) is the wave's own top-2: pick0[i].
+template <int MODE>
+__global__ __launch_bounds__(1024) void k_proj_lists(ProjFrame f, int nq, PrepLast pl, PrepLocal pc, int cap,
+                                                     float nnratio, const orbhip_kp* __restrict__ kps,
+                                                     const uint8_t* __restrict__ kdesc,
+                                                     const uint8_t* __restrict__ claimed,
+                                                     const uint8_t* __restrict__ qdesc,
+                                                     uint64_t* __restrict__ lists, int* __restrict__ lcnt,
+                                                     int* __restrict__ pick0, uint8_t* __restrict__ in_view,
+                                                     int* __restrict__ level) {
+    extern __shared__ uint4 kl[];
+    const int n = f.n;
+    const int i = blockIdx.x * kListWaves + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    Query Q{0, 0, 0, 0, 0, 0};
+    uint4 qa{0u, 0u, 0u, 0u}, qb{0u, 0u, 0u, 0u};
+    if (i < nq) {
+        if constexpr (MODE == 0) {
+            Q = prep_last(f, pl, i);
+        } else {
+            uint8_t iv;
+            int lvl;
+            Q = prep_local(f, pc, i, &iv, &lvl);
+            if (lane == 0) { in_view[i] = iv; level[i] = lvl; }
+        }
+        const uint4* qd4 = (const uint4*)(qdesc + 32 * (size_t)i);
+        qa = qd4[0];
+        qb = qd4[1];
+    }
+    for (int k = threadIdx.x; k < n; k += blockDim.x) {
+        const orbhip_kp kp = kps[k];
+        const int px = (int)roundf((kp.x - f.minx) * f.invw);
+        const int py = (int)roundf((kp.y - f.miny) * f.invh);
+        const int c = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? 0xFFFF : px * kGridRows + py;
+        const uint32_t cl = (claimed && claimed[k]) ? 1u : 0u;
+        kl[k] = uint4{__float_as_uint(kp.x), __float_as_uint(kp.y), ((uint32_t)c << 16) | (cl << 8) |
+                      (uint32_t)(kp.octave & 0xFF), 0u};
+    }
+    __syncthreads();
+    if (i >= nq) return;
+    int cnt = 0;
+    Top2 t{256, INT_MAX, -1, 256, INT_MAX, -1};
+    if (Q.valid) {
+        const int nMinCellX = max(0, (int)floorf((Q.u - f.minx - Q.r) * f.invw));
+        const int nMaxCellX = min(kGridCols - 1, (int)ceilf((Q.u - f.minx + Q.r) * f.invw));
+        const int nMinCellY = max(0, (int)floorf((Q.v - f.miny - Q.r) * f.invh));
+        const int nMaxCellY = min(kGridRows - 1, (int)ceilf((Q.v - f.miny + Q.r) * f.invh));
+        const bool any = nMinCellX < kGridCols && nMaxCellX >= 0 && nMinCellY < kGridRows && nMaxCellY >= 0;
+        const bool bCheckLevels = (Q.minL > 0) || (Q.maxL >= 0);
+        uint64_t* out = lists + (size_t)i * cap;
+        for (int k0 = 0; any && k0 < n; k0 += 64) {
+            const int k = k0 + lane;
+            bool ok = false;
+            uint32_t key = 0, oct = 0;
+            if (k < n) {
+                const uint4 e = kl[k];
+                const int c = (int)(e.z >> 16);
+                const int px = c / kGridRows, py = c - px * kGridRows;   // c = 0xFFFF: px = 1365, out
+                oct = e.z & 0xFF;
+                const float x = __uint_as_float(e.x), y = __uint_as_float(e.y);
+                ok = px >= nMinCellX && px <= nMaxCellX && py >= nMinCellY && py <= nMaxCellY;
+                if (ok && bCheckLevels) ok = (int)oct >= Q.minL && !(Q.maxL >= 0 && (int)oct > Q.maxL);
+                ok = ok && fabsf(x - Q.u) < Q.r && fabsf(y - Q.v) < Q.r && !((e.z >> 8) & 1u);
+                key = ((uint32_t)c << 16) | (uint32_t)k;
+            }
+            const uint64_t m = __ballot(ok);
+            if (ok) {
+                const uint4* kd4 = (const uint4*)(kdesc + 32 * (size_t)k);
+                const uint4 ka = kd4[0], kb = kd4[1];
+                const int d = __popc(qa.x ^ ka.x) + __popc(qa.y ^ ka.y) + __popc(qa.z ^ ka.z) +
+                              __popc(qa.w ^ ka.w) + __popc(qb.x ^ kb.x) + __popc(qb.y ^ kb.y) +
+                              __popc(qb.z ^ kb.z) + __popc(qb.w ^ kb.w);
+                const int pos = cnt + __popcll(m & ((1ull << lane) - 1ull));
+                if (pos < cap) out[pos] = ((uint64_t)d << 32) | (uint64_t)((key << 4) | (oct & 15u));
+                if (d != 256) top2_add(t, d, (int)key, (int)(oct & 15u));
+            }
+            cnt += __popcll(m);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int d1 = __shfl_xor(t.d1, o, 64), k1 = __shfl_xor(t.k1, o, 64), l1 = __shfl_xor(t.l1, o, 64);
+        const int d2 = __shfl_xor(t.d2, o, 64), k2 = __shfl_xor(t.k2, o, 64), l2 = __shfl_xor(t.l2, o, 64);
+        top2_add(t, d1, k1, l1);
+        top2_add(t, d2, k2, l2);
+    }
+    if (lane == 0) {
+        lcnt[i] = cnt;
+        pick0[i] = proj_decide(t, MODE, nnratio);
+    }
+}
+
+// res[0] = matches, res[1] = status (1: a list overflowed, nothing else written), res[2] = rounds.
+// Dynamic LDS: 3 owner tables (n ints), the list offsets (nq ints), then the lists themselves when
+// they fit the rest (`ent_cap` entries; else the rounds read them from global memory).
+template <int MODE>
+__global__ __launch_bounds__(1024) void k_proj_resolve(int n, int nq, float nnratio, int check_orientation, int cap,
+                                                       int ent_cap, const float* __restrict__ qangle,
+                                                       const orbhip_kp* __restrict__ kps,
+                                                       const uint64_t* __restrict__ lists,
+                                                       const int* __restrict__ lcnt, const int* __restrict__ pick0,
+                                                       int* __restrict__ pick,
+                                                       int* __restrict__ match, int* __restrict__ res) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
+    int* own = (int*)rsm;                        // 3 x n
+    int* qoff = own + 3 * n;                     // nq
+    uint64_t* ent = (uint64_t*)(rsm + (((size_t)(3 * n + nq) * 4 + 15) & ~size_t(15)));
+    __shared__ int flag[4], hist[32], keep[3], cnt, scan[16];
+    const int tid = threadIdx.x, nt = blockDim.x;
+    if (tid < 4) flag[tid] = 0;
+    if (tid < 32) hist[tid] = 0;
+    if (tid == 0) cnt = 0;
+    for (int k = tid; k < 3 * n; k += nt) own[k] = INT_MAX;
+    // list offsets (block scan of the counts, nt queries at a time)
+    int over = 0, run = 0;
+    for (int i0 = 0; i0 < nq; i0 += nt) {
+        const int i = i0 + tid;
+        const int c = i < nq ? lcnt[i] : 0;
+        over |= c > cap;
+        int tot;
+        const int ex = block_excl_scan(c, scan, &tot);
+        if (i < nq) { qoff[i] = run + ex; pick[i] = pick0[i]; }
+        run += tot;
+    }
+    if (over) flag[3] = 1;
+    __syncthreads();
+    if (flag[3]) {
+        if (tid == 0) res[1] = 1;
+        return;
+    }
+    const bool in_lds = run <= ent_cap;
+    // round 0 was k_proj_lists' (pick0): its claims build own[1]
+    for (int i = tid; i < nq; i += nt) {
+        const int p = pick[i];
+        if (p >= 0) atomicMin(&own[n + p], i);
+        if (in_lds) {
+            const int c = lcnt[i], o = qoff[i];
+            const uint64_t* L = lists + (size_t)i * cap;
+            for (int j = 0; j < c; j++) ent[o + j] = L[j];
+        }
+    }
+    __syncthreads();
+    // round r >= 1: reads own[r % 3], builds own[(r+1) % 3], clears own[(r+2) % 3]; flag[r % 3] =
+    // some pick changed, and flag[(r+1) % 3] (last read before round r-1's barrier) is reset here
+    int r = 1;
+    for (; r < nq + 2; r++) {
+        const int* owner = own + (r % 3) * n;
+        int* own_next = own + ((r + 1) % 3) * n;
+        int* own_clear = own + ((r + 2) % 3) * n;
+        for (int k = tid; k < n; k += nt) own_clear[k] = INT_MAX;
+        if (tid == 0) flag[(r + 1) % 3] = 0;
+        int ch = 0;
+        for (int i = tid; i < nq; i += nt) {
+            const int c = lcnt[i];
+            const uint64_t* L = in_lds ? ent + qoff[i] : lists + (size_t)i * cap;
+            Top2 t{256, INT_MAX, -1, 256, INT_MAX, -1};
+            for (int j = 0; j < c; j++) {
+                const uint64_t e = L[j];
+                const uint32_t lo = (uint32_t)e;
+                const int d = (int)(e >> 32);
+                if (d == 256 || owner[(lo >> 4) & 0xFFFF] < i) continue;
+                top2_add(t, d, (int)(lo >> 4), (int)(lo & 15));
+            }
+            const int p = proj_decide(t, MODE, nnratio);
+            ch |= p != pick[i];
+            pick[i] = p;
+            if (p >= 0) atomicMin(&own_next[p], i);
+        }
+        if (ch) flag[r % 3] = 1;
+        __syncthreads();
+        if (!flag[r % 3]) break;
+    }
+    // ---- the rotation filter of SearchByProjection(CurrentFrame, LastFrame), the count ----
+    const float factor = 1.0f / kHisto;
+    auto bin_of = [&](int i, int k) {
+        float rot = qangle[i] - kps[k].angle;
+        if (rot < 0.0) rot += 360.0f;
+        int b = (int)roundf(rot * factor);
+        if (b == kHisto) b = 0;
+        return b;
+    };
+    const bool rot = MODE == 0 && check_orientation;
+    if (rot) {
+        for (int i = tid; i < nq; i += nt)
+            if (pick[i] >= 0) atomicAdd(&hist[bin_of(i, pick[i])], 1);
+        __syncthreads();
+        if (tid == 0) {   // ComputeThreeMaxima
+            int m1 = 0, m2 = 0, m3 = 0, i1 = -1, i2 = -1, i3 = -1;
+            for (int b = 0; b < kHisto; b++) {
+                const int v = hist[b];
+                if (v > m1) { m3 = m2; m2 = m1; m1 = v; i3 = i2; i2 = i1; i1 = b; }
+                else if (v > m2) { m3 = m2; m2 = v; i3 = i2; i2 = b; }
+                else if (v > m3) { m3 = v; i3 = b; }
+            }
+            if (m2 < 0.1f * (float)m1) { i2 = -1; i3 = -1; }
+            else if (m3 < 0.1f * (float)m1) { i3 = -1; }
+            keep[0] = i1; keep[1] = i2; keep[2] = i3;
+        }
+        __syncthreads();
+    }
+    int c = 0;
+    for (int i = tid; i < nq; i += nt) {
+        int k = pick[i];
+        if (k >= 0 && rot) {
+            const int b = bin_of(i, k);
+            if (b != keep[0] && b != keep[1] && b != keep[2]) k = -1;
+        }
+        match[i] = k;
+        c += k >= 0;
+    }
+    atomicAdd(&cnt, c);
+    __syncthreads();
+    if (tid == 0) {
+        res[0] = cnt;
+        res[1] = 0;
+        res[2] = r + 1;
+    }
+}
 
 // ---------------------------------------------------------------------------
 // SearchForInitialization(F1, F2, vbPrevMatched, vnMatches12, windowSize)
@@ -925,6 +1197,51 @@ int run_rounds(ProjWorkspace* ws, const ProjFrame& f, int nq, int mode, float nn
 
 }  // namespace
 
+namespace {
+
+// the two-launch form applies: every octave fits the list entry's 4 bits, the owner tables fit LDS
+bool onepass_ok(const orbhip_frame* F, int nq) {
+    const char* e = std::getenv("ORBHIP_PROJ_ROUNDS");   // A/B switch (read per call: tests flip it)
+    if ((e && e[0] == '1') || F->n > kProjMaxN || nq > kProjMaxQ) return false;
+    for (int k = 0; k < F->n; k++)
+        if (F->kps[k].octave < 0 || F->kps[k].octave > 15) return false;
+    return true;
+}
+constexpr size_t kResolveLds = 150 * 1024;   // k_proj_resolve's dynamic LDS
+hipError_t proj_lds_attr() {   // beyond the default 64 KiB of dynamic LDS
+    static const hipError_t e[4] = {
+        hipFuncSetAttribute((const void*)k_proj_resolve<0>, hipFuncAttributeMaxDynamicSharedMemorySize, kResolveLds),
+        hipFuncSetAttribute((const void*)k_proj_resolve<1>, hipFuncAttributeMaxDynamicSharedMemorySize, kResolveLds),
+        hipFuncSetAttribute((const void*)k_proj_lists<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 16 * kProjMaxN),
+        hipFuncSetAttribute((const void*)k_proj_lists<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 16 * kProjMaxN)};
+    for (hipError_t x : e)
+        if (x != hipSuccess) return x;
+    return hipSuccess;
+}
+// list entries the resolve kernel holds in LDS next to its owner tables and list offsets
+int resolve_ent_cap(int n, int nq) {
+    const size_t head = ((size_t)(3 * n + nq) * 4 + 15) & ~size_t(15);
+    return head >= kResolveLds ? 0 : (int)((kResolveLds - head) / 8);
+}
+int proj_cap() {
+    const char* e = std::getenv("ORBHIP_PROJ_CAP");   // tests shrink it to force the round path
+    return e ? std::max(1, std::min(kProjCap, std::atoi(e))) : kProjCap;
+}
+
+// outputs in one block (one download): match (nq ints), level (nq ints), in_view (nq bytes), res
+struct OutBlock {
+    size_t match, lvl, iv, res, bytes;
+    explicit OutBlock(int nq) {
+        match = 0;
+        lvl = 4 * (size_t)nq;
+        iv = 8 * (size_t)nq;
+        res = (iv + (size_t)nq + 15) & ~size_t(15);
+        bytes = res + 16;
+    }
+};
+
+}  // namespace
+
 int proj_search_last(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_proj_last* L, float th,
                      int check_orientation, int32_t* match, int* rounds_out, hipStream_t st) {
     if (!ws || !F || !L || !match || F->n < 0 || L->n < 0 || F->n > 65535 || !F->scale_factors ||
@@ -934,6 +1251,10 @@ int proj_search_last(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_proj
         if (L->octave[i] < 0 || L->octave[i] >= F->n_levels) return ORBHIP_ERR_ARG;
     const int n = F->n, nq = L->n;
     if (nq == 0) return 0;
+    const bool onepass = onepass_ok(F, nq);
+    const int cap = proj_cap();
+    if (onepass) PJOK(proj_lds_attr());
+    const OutBlock ob(nq);
     Layout lay;
     const size_t o_kps = lay.add(sizeof(orbhip_kp) * n), o_kd = lay.add(32 * (size_t)n), o_cl = lay.add(n);
     const size_t o_scale = lay.add(sizeof(float) * F->n_levels);
@@ -941,7 +1262,9 @@ int proj_search_last(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_proj
     const size_t o_ang = lay.add(4 * (size_t)nq), o_in_end = lay.off;
     const size_t o_cell = lay.add(4 * (size_t)n), o_own = lay.add(12 * (size_t)std::max(n, 1));
     const size_t o_q = lay.add(sizeof(Query) * nq), o_chg = lay.add(4 * ((size_t)nq + 2));
-    const size_t o_pick = lay.add(4 * (size_t)nq), o_match = lay.add(4 * (size_t)nq), o_flag = lay.add(8);
+    const size_t o_pick = lay.add(4 * (size_t)nq), o_out = lay.add(ob.bytes);
+    const size_t o_list = onepass ? lay.add(8 * (size_t)nq * cap) : 0, o_lcnt = lay.add(4 * (size_t)nq);
+    const size_t o_pick0 = lay.add(4 * (size_t)nq);
     if (int rc = ensure(ws, lay.off)) return rc;
     char* H = (char*)ws->h;
     char* D = (char*)ws->d;
@@ -954,28 +1277,46 @@ int proj_search_last(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_proj
     std::memcpy(H + o_oct, L->octave, 4 * (size_t)nq);
     std::memcpy(H + o_ang, L->angle, 4 * (size_t)nq);
     PJOK(hipMemcpyAsync(D, H, o_in_end, hipMemcpyHostToDevice, st));
-    PJOK(hipMemsetAsync(D + o_pick, 0xFF, 4 * (size_t)nq, st));   // -1: the first round always "changes"
     const ProjFrame f = make_frame(F);
+    const PrepLast pl{(const float*)(D + o_pts), (const int*)(D + o_oct), (const float*)(D + o_scale), th};
+    const uint8_t* dcl = F->claimed ? (const uint8_t*)(D + o_cl) : nullptr;
+    int* hres = (int*)(H + o_out + ob.res);
+    if (onepass) {
+        hipLaunchKernelGGL(k_proj_lists<0>, dim3((unsigned)((nq + kListWaves - 1) / kListWaves)), dim3(1024),
+                           16 * (size_t)n, st, f, nq, pl, PrepLocal{}, cap, 0.f, (const orbhip_kp*)(D + o_kps),
+                           (const uint8_t*)(D + o_kd), dcl, (const uint8_t*)(D + o_qd), (uint64_t*)(D + o_list),
+                           (int*)(D + o_lcnt), (int*)(D + o_pick0), nullptr, nullptr);
+        hipLaunchKernelGGL(k_proj_resolve<0>, dim3(1), dim3(1024), kResolveLds, st, n, nq, 0.f, check_orientation,
+                           cap, resolve_ent_cap(n, nq), (const float*)(D + o_ang), (const orbhip_kp*)(D + o_kps),
+                           (const uint64_t*)(D + o_list), (const int*)(D + o_lcnt), (const int*)(D + o_pick0),
+                           (int*)(D + o_pick), (int*)(D + o_out + ob.match), (int*)(D + o_out + ob.res));
+        PJOK(hipGetLastError());
+        PJOK(hipMemcpyAsync(H + o_out, D + o_out, ob.bytes, hipMemcpyDeviceToHost, st));
+        PJOK(hipStreamSynchronize(st));
+        if (hres[1] == 0) {
+            std::memcpy(match, H + o_out + ob.match, 4 * (size_t)nq);
+            if (rounds_out) *rounds_out = hres[2];
+            return hres[0];
+        }
+    }
+    PJOK(hipMemsetAsync(D + o_pick, 0xFF, 4 * (size_t)nq, st));   // -1: the first round always "changes"
     if (n) hipLaunchKernelGGL(k_proj_cells, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, f,
                               (const orbhip_kp*)(D + o_kps), (int*)(D + o_cell));
-    hipLaunchKernelGGL(k_proj_prep_last, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, f, nq,
-                       (const float*)(D + o_pts), (const int*)(D + o_oct), (const float*)(D + o_scale), th,
+    hipLaunchKernelGGL(k_proj_prep_last, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, f, nq, pl,
                        (Query*)(D + o_q));
     auto tail = [&]() -> int {
         hipLaunchKernelGGL(k_proj_finish, dim3(1), dim3(1024), 0, st, nq, check_orientation,
                            (const float*)(D + o_ang), (const orbhip_kp*)(D + o_kps), (const int*)(D + o_pick),
-                           (int*)(D + o_match), (int*)(D + o_flag));
-        PJOK(hipMemcpyAsync(H + o_match, D + o_match, 4 * (size_t)nq, hipMemcpyDeviceToHost, st));
-        PJOK(hipMemcpyAsync(H + o_flag, D + o_flag, 4, hipMemcpyDeviceToHost, st));
+                           (int*)(D + o_out + ob.match), (int*)(D + o_out + ob.res));
+        PJOK(hipMemcpyAsync(H + o_out, D + o_out, ob.bytes, hipMemcpyDeviceToHost, st));
         return 0;
     };
-    const int rounds = run_rounds(ws, f, nq, 0, 0.f, D, o_q, o_kps, o_kd, o_cell,
-                                  F->claimed ? (const uint8_t*)(D + o_cl) : nullptr, o_own, o_qd, o_pick, o_chg, H,
+    const int rounds = run_rounds(ws, f, nq, 0, 0.f, D, o_q, o_kps, o_kd, o_cell, dcl, o_own, o_qd, o_pick, o_chg, H,
                                   st, tail);
     if (rounds < 0) return rounds;
-    std::memcpy(match, H + o_match, 4 * (size_t)nq);
+    std::memcpy(match, H + o_out + ob.match, 4 * (size_t)nq);
     if (rounds_out) *rounds_out = rounds;
-    return *(int*)(H + o_flag);
+    return hres[0];
 }
 
 int proj_search_local(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_local_points* M, float view_cos_limit,
@@ -987,6 +1328,10 @@ int proj_search_local(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_loc
         return ORBHIP_ERR_ARG;
     const int n = F->n, nq = M->n;
     if (nq == 0) return 0;
+    const bool onepass = onepass_ok(F, nq);
+    const int cap = proj_cap();
+    if (onepass) PJOK(proj_lds_attr());
+    const OutBlock ob(nq);
     Layout lay;
     const size_t o_kps = lay.add(sizeof(orbhip_kp) * n), o_kd = lay.add(32 * (size_t)n), o_cl = lay.add(n);
     const size_t o_scale = lay.add(sizeof(float) * F->n_levels);
@@ -995,8 +1340,9 @@ int proj_search_local(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_loc
     const size_t o_in_end = lay.off;
     const size_t o_cell = lay.add(4 * (size_t)n), o_own = lay.add(12 * (size_t)std::max(n, 1));
     const size_t o_q = lay.add(sizeof(Query) * nq), o_chg = lay.add(4 * ((size_t)nq + 2));
-    const size_t o_pick = lay.add(4 * (size_t)nq), o_lvl = lay.add(4 * (size_t)nq), o_iv = lay.add(nq);
-    const size_t o_match = lay.add(4 * (size_t)nq), o_flag = lay.add(8);
+    const size_t o_pick = lay.add(4 * (size_t)nq), o_out = lay.add(ob.bytes);
+    const size_t o_list = onepass ? lay.add(8 * (size_t)nq * cap) : 0, o_lcnt = lay.add(4 * (size_t)nq);
+    const size_t o_pick0 = lay.add(4 * (size_t)nq);
     if (int rc = ensure(ws, lay.off)) return rc;
     char* H = (char*)ws->h;
     char* D = (char*)ws->d;
@@ -1011,34 +1357,56 @@ int proj_search_local(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_loc
     std::memcpy(H + o_qd, M->desc, 32 * (size_t)nq);
     if (M->skip) std::memcpy(H + o_skip, M->skip, nq);
     PJOK(hipMemcpyAsync(D, H, o_in_end, hipMemcpyHostToDevice, st));
-    PJOK(hipMemsetAsync(D + o_pick, 0xFF, 4 * (size_t)nq, st));
     const ProjFrame f = make_frame(F);
-    if (n) hipLaunchKernelGGL(k_proj_cells, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, f,
-                              (const orbhip_kp*)(D + o_kps), (int*)(D + o_cell));
-    hipLaunchKernelGGL(k_proj_prep_local, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, f, nq,
-                       (const float*)(D + o_pts), (const float*)(D + o_nrm), (const float*)(D + o_mind),
+    const PrepLocal pc{(const float*)(D + o_pts), (const float*)(D + o_nrm), (const float*)(D + o_mind),
                        (const float*)(D + o_maxd), M->skip ? (const uint8_t*)(D + o_skip) : nullptr,
                        (const float*)(D + o_scale), F->n_levels, F->log_scale_factor, view_cos_limit, th, far_points,
-                       th_far, (Query*)(D + o_q), (uint8_t*)(D + o_iv), (int*)(D + o_lvl));
+                       th_far};
+    const uint8_t* dcl = F->claimed ? (const uint8_t*)(D + o_cl) : nullptr;
+    uint8_t* d_iv = (uint8_t*)(D + o_out + ob.iv);
+    int* d_lvl = (int*)(D + o_out + ob.lvl);
+    int* hres = (int*)(H + o_out + ob.res);
+    auto outputs = [&]() {
+        std::memcpy(match, H + o_out + ob.match, 4 * (size_t)nq);
+        std::memcpy(level, H + o_out + ob.lvl, 4 * (size_t)nq);
+        std::memcpy(in_view, H + o_out + ob.iv, nq);
+    };
+    if (onepass) {
+        hipLaunchKernelGGL(k_proj_lists<1>, dim3((unsigned)((nq + kListWaves - 1) / kListWaves)), dim3(1024),
+                           16 * (size_t)n, st, f, nq, PrepLast{}, pc, cap, nnratio, (const orbhip_kp*)(D + o_kps),
+                           (const uint8_t*)(D + o_kd), dcl, (const uint8_t*)(D + o_qd), (uint64_t*)(D + o_list),
+                           (int*)(D + o_lcnt), (int*)(D + o_pick0), d_iv, d_lvl);
+        hipLaunchKernelGGL(k_proj_resolve<1>, dim3(1), dim3(1024), kResolveLds, st, n, nq, nnratio, 0, cap,
+                           resolve_ent_cap(n, nq), (const float*)nullptr, (const orbhip_kp*)(D + o_kps),
+                           (const uint64_t*)(D + o_list), (const int*)(D + o_lcnt), (const int*)(D + o_pick0),
+                           (int*)(D + o_pick), (int*)(D + o_out + ob.match), (int*)(D + o_out + ob.res));
+        PJOK(hipGetLastError());
+        PJOK(hipMemcpyAsync(H + o_out, D + o_out, ob.bytes, hipMemcpyDeviceToHost, st));
+        PJOK(hipStreamSynchronize(st));
+        if (hres[1] == 0) {
+            outputs();
+            if (rounds_out) *rounds_out = hres[2];
+            return hres[0];
+        }
+    }
+    PJOK(hipMemsetAsync(D + o_pick, 0xFF, 4 * (size_t)nq, st));
+    if (n) hipLaunchKernelGGL(k_proj_cells, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, f,
+                              (const orbhip_kp*)(D + o_kps), (int*)(D + o_cell));
+    hipLaunchKernelGGL(k_proj_prep_local, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, f, nq, pc,
+                       (Query*)(D + o_q), d_iv, d_lvl);
     auto tail = [&]() -> int {
         hipLaunchKernelGGL(k_proj_finish, dim3(1), dim3(1024), 0, st, nq, 0, (const float*)nullptr,
-                           (const orbhip_kp*)(D + o_kps), (const int*)(D + o_pick), (int*)(D + o_match),
-                           (int*)(D + o_flag));
-        PJOK(hipMemcpyAsync(H + o_match, D + o_match, 4 * (size_t)nq, hipMemcpyDeviceToHost, st));
-        PJOK(hipMemcpyAsync(H + o_lvl, D + o_lvl, 4 * (size_t)nq, hipMemcpyDeviceToHost, st));
-        PJOK(hipMemcpyAsync(H + o_iv, D + o_iv, nq, hipMemcpyDeviceToHost, st));
-        PJOK(hipMemcpyAsync(H + o_flag, D + o_flag, 4, hipMemcpyDeviceToHost, st));
+                           (const orbhip_kp*)(D + o_kps), (const int*)(D + o_pick), (int*)(D + o_out + ob.match),
+                           (int*)(D + o_out + ob.res));
+        PJOK(hipMemcpyAsync(H + o_out, D + o_out, ob.bytes, hipMemcpyDeviceToHost, st));
         return 0;
     };
-    const int rounds = run_rounds(ws, f, nq, 1, nnratio, D, o_q, o_kps, o_kd, o_cell,
-                                  F->claimed ? (const uint8_t*)(D + o_cl) : nullptr, o_own, o_qd, o_pick, o_chg, H,
-                                  st, tail);
+    const int rounds = run_rounds(ws, f, nq, 1, nnratio, D, o_q, o_kps, o_kd, o_cell, dcl, o_own, o_qd, o_pick, o_chg,
+                                  H, st, tail);
     if (rounds < 0) return rounds;
-    std::memcpy(match, H + o_match, 4 * (size_t)nq);
-    std::memcpy(level, H + o_lvl, 4 * (size_t)nq);
-    std::memcpy(in_view, H + o_iv, nq);
+    outputs();
     if (rounds_out) *rounds_out = rounds;
-    return *(int*)(H + o_flag);
+    return hres[0];
 }
 
 int init_search(ProjWorkspace* ws, const orbhip_init_frame* F1, const orbhip_init_frame* F2, float* prev_matched,

@@ -105,7 +105,7 @@ class ORBmatcher:
         d = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
         oc = np.ascontiguousarray(last_octave, np.int32)
         an = np.ascontiguousarray(last_angle, np.float32)
-        match = np.full(pts.shape[0], -1, np.int32)
+        match = np.empty(pts.shape[0], np.int32)   # written in full by the call
         fc = frame.to_c()
         lc = ProjLastC(pts.shape[0], ptr(pts), ptr(d), ptr(oc), ptr(an))
         n = check(lib().orbhip_search_by_projection_last(self.ctx.handle, ctypes.byref(fc), ctypes.byref(lc),
@@ -125,9 +125,9 @@ class ORBmatcher:
         d = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
         sk = None if skip is None else np.ascontiguousarray(skip, np.uint8)
         m = pts.shape[0]
-        match = np.full(m, -1, np.int32)
-        in_view = np.zeros(m, np.uint8)
-        level = np.full(m, -1, np.int32)
+        match = np.empty(m, np.int32)      # written in full by the call (m > 0)
+        in_view = np.empty(m, np.uint8)
+        level = np.empty(m, np.int32)
         fc = frame.to_c()
         lc = LocalPointsC(m, ptr(pts), ptr(nrm), ptr(mn), ptr(mx), ptr(d), ptr(sk))
         n = check(lib().orbhip_search_local_points(self.ctx.handle, ctypes.byref(fc), ctypes.byref(lc),
@@ -158,8 +158,13 @@ class ProjFrame:
             sf[i] = np.float32(np.float64(sf[i - 1]) * np.float64(np.float32(scale_factor)))
         self.scale_factors = sf
         self.log_scale_factor = float(np.log(np.float32(scale_factor)).astype(np.float32))
+        self._c = None
 
     def to_c(self) -> FrameC:
+        """The C view (built once: a ProjFrame is not modified after construction; it holds the
+        arrays the view points into)."""
+        if self._c is not None:
+            return self._c
         c = FrameC()
         c.n = self.kps.shape[0]
         c.kps, c.desc, c.claimed = ptr(self.kps), ptr(self.desc), ptr(self.claimed)
@@ -169,4 +174,5 @@ class ProjFrame:
         c.fx, c.fy, c.cx, c.cy = self.fx, self.fy, self.cx, self.cy
         c.pose_q[:] = [float(v) for v in self.pose_q]
         c.pose_t[:] = [float(v) for v in self.pose_t]
+        self._c = c
         return c

@@ -117,6 +117,28 @@ def covisibility_system(part: Partition, n_landmarks: int, seed: int = 0, dampin
     return Ss, bs
 
 
+def split_assembled(S, b, part: Partition):
+    """Per-rank partial systems of an ASSEMBLED system with the partition's structure (every
+    rank holds the sum, e.g. the separator system after the all-reduce): rank r keeps its
+    interior's rows and columns and the diagonal block of its own separator Z_r, so the ranks'
+    parts sum to S again. Used for a second dissection level on the separator system
+    (Partition(ranks, ranks // 2, 2, dof = sep * 6): odd separators become the interiors)."""
+    n = S.shape[0]
+    Ss, bs = [], []
+    for r in range(part.ranks):
+        I, Zr = part.interior(r), part.vars_of(part.separator_kf(r))
+        A = np.zeros((n, n))
+        A[I, :] = S[I, :]
+        A[:, I] = S[:, I]
+        A[np.ix_(Zr, Zr)] = S[np.ix_(Zr, Zr)]
+        bb = np.zeros(n)
+        bb[I] = b[I]
+        bb[Zr] = b[Zr]
+        Ss.append(A)
+        bs.append(bb)
+    return Ss, bs
+
+
 def dd_local(S_r, b_r, part: Partition, rank: int):
     """Step 1 on rank `rank` (torch float64): factor the interior, eliminate it. Returns
     (state, Sz, bz): this rank's contribution to the separator system, scattered to its size."""

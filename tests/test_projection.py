@@ -3,8 +3,8 @@ and Tracking::SearchLocalPoints (Frame::isInFrustum + SearchByProjection(F, vpMa
 
 Oracle KATs on the CPU (definitional: a MapPoint projected exactly onto its own keypoint with its
 own descriptor matches it; claimed keypoints are never matched; skipped points are not in view),
-and the device path (one wavefront per query + greedy fixed point) against the oracle on the
-GPU, bit-exact (match indices, in-view flags, predicted levels). Parity unpinned by the reference
+and the device path (one wavefront per query + greedy fixed point; the list/resolve form, its
+overflow into the round kernels, and the round kernels alone) against the oracle on the GPU, bit-exact (match indices, in-view flags, predicted levels). Parity unpinned by the reference
 (no fixtures upstream).
 """
 import numpy as np
@@ -12,6 +12,18 @@ import pytest
 
 from orb_slam3_ros2_amd.matcher import ProjFrame
 from orb_slam3_ros2_amd.synthetic import synthetic_projection_scene
+
+
+# the device forms: the two-launch list/resolve path (default), the list path overflowing into the
+# round kernels (list capacity 2), and the round kernels alone
+PROJ_MODES = {"lists": {}, "overflow": {"ORBHIP_PROJ_CAP": "2"}, "rounds": {"ORBHIP_PROJ_ROUNDS": "1"}}
+
+
+@pytest.fixture(params=list(PROJ_MODES))
+def proj_mode(request, monkeypatch):
+    for k, v in PROJ_MODES[request.param].items():
+        monkeypatch.setenv(k, v)
+    return request.param
 
 
 def _frame(s, claimed=True):
@@ -46,7 +58,7 @@ def test_oracle_claimed_never_matched_and_skip(oracle):
 
 
 @pytest.mark.gpu
-def test_search_by_projection_last_matches_oracle(oracle):
+def test_search_by_projection_last_matches_oracle(oracle, proj_mode):
     from orb_slam3_ros2_amd import ORBmatcher
     mt = ORBmatcher(0.9, True)
     for seed in range(5):
@@ -57,11 +69,11 @@ def test_search_by_projection_last_matches_oracle(oracle):
             n, m = mt.SearchByProjectionLastFrame(f, s["points"], s["mp_desc"], s["last_octave"], s["last_angle"], th)
             on, om = oracle.search_by_projection_last(f, s["points"], s["mp_desc"], s["last_octave"], s["last_angle"],
                                                       th, ori)
-            assert n == on and np.array_equal(m, om), (seed, th, ori)
+            assert n == on and np.array_equal(m, om), (seed, th, ori, proj_mode)
 
 
 @pytest.mark.gpu
-def test_search_local_points_matches_oracle(oracle):
+def test_search_local_points_matches_oracle(oracle, proj_mode):
     from orb_slam3_ros2_amd import ORBmatcher
     for seed in range(5):
         s = synthetic_projection_scene(seed=20 + seed)
@@ -72,13 +84,13 @@ def test_search_local_points_matches_oracle(oracle):
                                      s["skip"], th=th, far_points=far, th_far=5.0)
             o = oracle.search_local_points(f, s["points"], s["normals"], s["min_dist"], s["max_dist"], s["mp_desc"],
                                            s["skip"], th=th, nnratio=ratio, far_points=far, th_far=5.0)
-            assert r[0] == o[0], (seed, th)
+            assert r[0] == o[0], (seed, th, proj_mode)
             for a, b in zip(r[1:], o[1:]):
-                assert np.array_equal(a, b), (seed, th)
+                assert np.array_equal(a, b), (seed, th, proj_mode)
 
 
 @pytest.mark.gpu
-def test_projection_edge_cases(oracle):
+def test_projection_edge_cases(oracle, proj_mode):
     from orb_slam3_ros2_amd import ORBmatcher
     mt = ORBmatcher(0.9, True)
     s = synthetic_projection_scene(n_kp=100, n_mp=50, seed=30)

@@ -72,6 +72,29 @@ def test_dd_solve_c5_shape_in_process():
     assert part.n_sep == 912 and part.interior(0).size == 186
 
 
+def test_two_level_dissection_of_the_separator_system():
+    """The separator system after the all-reduce is cyclic block-tridiagonal (8 separators of
+    19 keyframes): a second dissection level (odd separators as interiors, 4 ranks) solves it
+    exactly too (the model of DESIGN.md §C5 sharding prices both levels)."""
+    import torch
+    from orb_slam3_ros2_amd.schur_dd import (Partition, covisibility_system, dd_local, dd_solve_local,
+                                             split_assembled)
+    part = Partition(400, 8, 20)
+    Ss, bs = covisibility_system(part, 6000, seed=4)
+    loc = [dd_local(torch.from_numpy(S), torch.from_numpy(b), part, r) for r, (S, b) in enumerate(zip(Ss, bs))]
+    Sz = sum(l[1] for l in loc).numpy()
+    bz = sum(l[2] for l in loc).numpy()
+    p2 = Partition(8, 4, 2, dof=part.sep * part.dof)
+    # block-tridiagonal cyclic: separators two apart are uncoupled
+    m = part.sep * part.dof
+    assert not np.any(Sz[:m, 2 * m:3 * m]) and not np.any(Sz[:m, 4 * m:5 * m])
+    S2, b2 = split_assembled(Sz, bz, p2)
+    assert np.allclose(sum(S2), Sz, rtol=0, atol=0) and np.allclose(sum(b2), bz, rtol=0, atol=0)
+    xz = dd_solve_local(S2, b2, p2).numpy()
+    xr = np.linalg.solve(Sz, bz)
+    assert np.abs(xz - xr).max() / np.abs(xr).max() < 1e-10
+
+
 def test_c5_landmarks_fit_one_window():
     """Premise of the partition on the bench's C5 problem: every landmark is observed by keyframes
     within one cyclic 20-keyframe window, so it touches at most one segment interior."""

@@ -16,7 +16,7 @@ from orb_slam3_ros2_amd._lib import lib  # noqa: E402
 import bench  # noqa: E402
 
 STRIDE, NK = 16384, 8
-NAMES = {0: "k_resize(l=1)", 1: "k_fast_cells", 2: "k_octree", 3: "k_desc", 4: "k_match_top2", 5: "k_match_finish"}
+NAMES = {0: "k_pyr_cone|k_resize(l=1)", 1: "k_fast_cells", 2: "k_octree", 3: "k_desc", 4: "k_match_top2", 5: "k_match_finish"}
 
 
 def main():
@@ -47,6 +47,9 @@ def main():
         print(f"{NAMES[k]:14s} wgs={len(st):5d} span={(en.max() - st.min()) / 100:8.2f}us "
               f"start@{(st.min() - t_min) / 100:8.2f}us  wg dur min/med/max={dur.min():.2f}/{np.median(dur):.2f}/"
               f"{dur.max():.2f}us  start skew={(st.max() - st.min()) / 100:.2f}us")
+        if len(st) <= 16:
+            print("     per-wg start/dur (us): " + ", ".join(f"{(a - t_min) / 100:.1f}/{(b - a) / 100:.1f}"
+                                                    for a, b in zip(st, en)))
         ph = buf[k * STRIDE + 8192: k * STRIDE + 8192 + 64].astype(np.int64)
         nz = np.nonzero(ph)[0]
         if len(nz):
