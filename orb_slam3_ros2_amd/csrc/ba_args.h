@@ -11,7 +11,8 @@ struct LmCtl {
     double ni, currentChi, rho, initChi;
     int phase, it, trials, qmax;
     int nBad, errors_valid, pop, stop;
-    int iterations, early_stop, pad0, pad1;
+    int iterations, early_stop;
+    int arrive_b, arrive_t;   // last-arriver counters of k_ba_lin (build) and k_ba_errors(2) (trial), 0 between launches
 };
 
 struct BaArgs {
@@ -60,7 +61,8 @@ struct BaArgs {
     double* Spart;
     LmCtl* ctl;        // device-driven solve: this problem's LM state (nullptr: host-driven rounds)
     double* part;      // workgroup partial sums of a trial: chi2 (npart_e = ceil(E / 256)), then the
-    int npart_e, npart_m;   // landmark scale terms (npart_m = ceil(M / 256))
+    int npart_e, npart_m;   // landmark scale terms (npart_m = ceil(M / 256)); in the build phase
+                            // k_ba_lin's per-workgroup max diagonal (ceil(M / 256) + ceil(np / 4))
 };
 
 }  // namespace orbhip

@@ -93,6 +93,34 @@ __device__ double block_sum(double v, double* sh) {
     return s;
 }
 
+// Last-arriver hand-off inside one launch (MI355X_MICROARCH.md visibility table, row 1): each
+// workgroup of a problem's row stores its partial with an agent-scope (sc1) store, drains it, and
+// bumps the problem's counter; the workgroup that arrives last reads every partial with sc1 loads
+// and runs the controller step that used to be its own launch. Nobody waits for anybody.
+typedef __attribute__((address_space(1))) int ba_gint;
+typedef __attribute__((address_space(1))) double ba_gdbl;
+__device__ __forceinline__ void st_agent(double* p, double v) {
+    __hip_atomic_store((ba_gdbl*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_agent(const double* p) {
+    return __hip_atomic_load((ba_gdbl*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// every workgroup of the row calls it once, after thread 0's partial store; true (uniform) in the
+// last one, which also resets the counter for the next launch
+__device__ __forceinline__ bool last_arrival(int* counter, int total, int* sh_flag) {
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int old = __hip_atomic_fetch_add((ba_gint*)counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == total - 1;
+        if (last) __hip_atomic_store((ba_gint*)counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *sh_flag = last;
+    }
+    __syncthreads();
+    return *sh_flag != 0;
+}
+__device__ void ctl_end_body(const BaArgs& a, int prob, int* done_flags, double* sh);
+__device__ void ctl_begin_body(const BaArgs& a, int nlin);
+
 // ---------------------------------------------------------------------------
 // errors (when: 0 always, 1 the build's stale-error refresh, 2 a trial's new state); a trial also
 // writes each workgroup's sum of the robust chi2 terms to part[bx] (k_ba_ctl_end adds them)
@@ -125,6 +153,8 @@ __device__ __forceinline__ double edge_error(const BaArgs& a, int e) {
     return r0;
 }
 
+// when == 2 (a trial) ends in the trial's controller step, run by the last workgroup of each
+// problem to finish (ctl_end_body; done: the host-mapped done flags).
 // when == 1 also opens the device-driven slot (the former k_ba_ctl_pre): workgroup 0 of each
 // problem clears the pop request of the previous slot and, at an iteration start, ends the solve
 // on the iteration budget or the (host-relayed) stop flag (done[b], host-mapped: the host stops
@@ -146,13 +176,17 @@ __global__ __launch_bounds__(256) void k_ba_errors(const BaArgs* __restrict__ ar
         if (ends || !(in_phase(a, kPhBuild) && (!c || !c->errors_valid))) return;
     }
     if (when == 2 && !in_phase(a, kPhTrial)) return;
-    if (bx_ * (int)blockDim.x >= a.E) return;   // uniform
+    const bool has = bx_ * (int)blockDim.x < a.E;   // uniform
+    if (when != 2 && !has) return;
     const int e = bx_ * blockDim.x + threadIdx.x;
-    const double r0 = e < a.E ? edge_error(a, e) : 0.0;
+    const double r0 = (has && e < a.E) ? edge_error(a, e) : 0.0;
     if (when == 2) {   // uniform: every thread reaches the workgroup sum's barriers once
         __shared__ double sh[4];
+        __shared__ int lastf;
         const double t = block_sum(r0, sh);
-        if (threadIdx.x == 0) a.part[bx_] = t;
+        if (threadIdx.x == 0 && has) st_agent(a.part + bx_, t);
+        // the row's last workgroup runs the trial's controller step (the former k_ba_ctl_end)
+        if (a.ctl && last_arrival(&a.ctl->arrive_t, gridDim.x, &lastf)) ctl_end_body(a, act[by_], done, sh);
     }
 }
 
@@ -208,11 +242,9 @@ __device__ __forceinline__ double lin_ab(const BaArgs& a, int e, int oi, double 
 // buildSystem
 // ---------------------------------------------------------------------------
 // one thread per landmark: Hll, b_l over all its edges; stores each edge's linearisation (Pc, w)
-__global__ __launch_bounds__(256) void k_ba_lin_points(const BaArgs* __restrict__ args, const int* __restrict__ act) {
-    BA_PROLOGUE
-    BA_PHASE(kPhBuild)
-    const int m = bx_ * blockDim.x + threadIdx.x;
-    if (m >= a.M) return;
+// returns the largest |diagonal| of Hll (0 for m >= M)
+__device__ __forceinline__ double lin_point(const BaArgs& a, int m) {
+    if (m >= a.M) return 0.0;
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};
     for (int k = a.pt_ptr[m]; k < a.pt_ptr[m + 1]; k++) {
         const int e = a.pt_edges[k];
@@ -235,6 +267,12 @@ __global__ __launch_bounds__(256) void k_ba_lin_points(const BaArgs* __restrict_
     for (int i = 0; i < 9; i++) a.Hll[9 * m + i] = H[i];
 #pragma unroll
     for (int r = 0; r < 3; r++) a.b[a.n + 3 * m + r] = bl[r];
+    return fmax(fmax(fabs(H[0]), fabs(H[4])), fabs(H[8]));
+}
+__global__ __launch_bounds__(256) void k_ba_lin_points(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    BA_PROLOGUE
+    BA_PHASE(kPhBuild)
+    (void)lin_point(a, bx_ * blockDim.x + threadIdx.x);
 }
 
 // one wave per optimised pose: 21 upper Hpp terms + 6 b terms, lanes over the pose's edges; lane 0
@@ -252,12 +290,9 @@ __device__ __forceinline__ void reduce_half(double* acc, int lane, int m) {
     }
 }
 
-__global__ __launch_bounds__(256) void k_ba_lin_poses(const BaArgs* __restrict__ args, const int* __restrict__ act) {
-    BA_PROLOGUE
-    BA_PHASE(kPhBuild)
-    const int i = bx_ * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (i >= a.np) return;
+// one wave per pose i; returns (in every lane) the largest |diagonal| of the pose's Hpp block
+__device__ __forceinline__ double lin_pose(const BaArgs& a, int i, int lane) {
+    if (i >= a.np) return 0.0;   // wave-uniform
     double acc[32];   // 27 sums (21 of the upper Hpp triangle, 6 of b_p), padded to 32
 #pragma unroll
     for (int k = 0; k < 32; k++) acc[k] = 0;
@@ -289,6 +324,7 @@ __global__ __launch_bounds__(256) void k_ba_lin_poses(const BaArgs* __restrict__
     const double tot = acc[0] + __shfl_xor(acc[0], 1, 64);
     const int k = ((lane >> 5) & 1) << 4 | ((lane >> 4) & 1) << 3 | ((lane >> 3) & 1) << 2 | ((lane >> 2) & 1) << 1 |
                   ((lane >> 1) & 1);
+    double dmax = 0.0;
     if ((lane & 1) == 0 && k < 27) {
         double* H = a.Hpp + 36 * i;
         if (k < 21) {   // k-th entry of the upper triangle, row-major
@@ -297,10 +333,13 @@ __global__ __launch_bounds__(256) void k_ba_lin_poses(const BaArgs* __restrict__
             const int c = r + t;
             H[6 * r + c] = tot;
             H[6 * c + r] = tot;
+            if (r == c) dmax = fabs(tot);
         } else {
             a.b[6 * i + k - 21] = tot;
         }
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) dmax = fmax(dmax, __shfl_xor(dmax, o, 64));
     if (lane < 9 && a.ps_ptr[i] < a.ps_ptr[i + 1]) {   // the pose's rotation, as its edges used it
         {
             const int p = a.e_pose[a.ps_edges[a.ps_ptr[i]]];
@@ -312,6 +351,46 @@ __global__ __launch_bounds__(256) void k_ba_lin_poses(const BaArgs* __restrict__
             a.R_lin[9 * i + lane] = r;
         }
     }
+    return dmax;
+}
+__global__ __launch_bounds__(256) void k_ba_lin_poses(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    BA_PROLOGUE
+    BA_PHASE(kPhBuild)
+    (void)lin_pose(a, bx_ * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
+}
+
+// the device-driven build in one launch: workgroups [0, nbp) linearise landmarks (one per
+// thread), the rest poses (one per wave); each stores its largest |diagonal| (sc1), and the
+// problem's last workgroup runs the controller's trial start (ctl_begin_body: lambda from the
+// maxima on the first iteration)
+__global__ __launch_bounds__(256) void k_ba_lin(const BaArgs* __restrict__ args, const int* __restrict__ act,
+                                               int nbp) {
+    BA_PROLOGUE
+    BA_PHASE(kPhBuild)
+    __shared__ double sh[4];
+    __shared__ int lastf;
+    const int mP = (a.M + 255) / 256, nP = (a.np + 3) / 4;
+    double d;
+    int slot;
+    if (bx_ < nbp) {
+        d = lin_point(a, bx_ * blockDim.x + threadIdx.x);
+        slot = bx_ < mP ? bx_ : -1;
+    } else {
+        const int q = bx_ - nbp;
+        d = lin_pose(a, q * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
+        slot = q < nP ? mP + q : -1;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) d = fmax(d, __shfl_xor(d, o, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = d;
+    __syncthreads();
+    if (threadIdx.x == 0 && slot >= 0) {
+        double m = 0.0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); w++) m = fmax(m, sh[w]);
+        st_agent(a.part + slot, m);
+    }
+    if (last_arrival(&a.ctl->arrive_b, gridDim.x, &lastf)) ctl_begin_body(a, mP + nP);
 }
 
 // ---------------------------------------------------------------------------
@@ -368,9 +447,17 @@ __global__ __launch_bounds__(256) void k_ba_zero_s(const BaArgs* __restrict__ ar
 //   W_a Hpl_b^T = Hpl_a Dinv_m Hpl_b^T = w_a w_b B_a^T (A_a Dinv_m A_b^T) B_b
 // with A, B rebuilt from the edges' stored (Pc, w) and the poses' R_lin: 17 doubles read per pair
 // (edge records + Dinv) instead of the 36 of stored W / Hpl blocks, and no W written per trial.
-__global__ __launch_bounds__(256) void k_ba_schur_items(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+__device__ __forceinline__ void schur_b_pose(const BaArgs& a, int i, int lane);
+// work-groups [nbi, gridDim.x) run k_ba_schur_b's poses instead (it reads only k_ba_schur_points'
+// db and the linearisation: no dependence on the items, one launch less per trial)
+__global__ __launch_bounds__(256) void k_ba_schur_items(const BaArgs* __restrict__ args, const int* __restrict__ act,
+                                                        int nbi) {
     BA_PROLOGUE
     BA_PHASE(kPhTrial)
+    if (bx_ >= nbi) {
+        schur_b_pose(a, (bx_ - nbi) * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
+        return;
+    }
     const int gt = bx_ * blockDim.x + threadIdx.x;
     const int it = gt >> 1, h = gt & 1;
     if (it >= a.nitems) return;
@@ -482,11 +569,7 @@ __global__ __launch_bounds__(256) void k_ba_schur_fin(const BaArgs* __restrict__
 }
 
 // one wave per optimised pose: b_schur = b_p - sum_e Hpl_e db, Hpl_e db = w B^T (A db)
-__global__ __launch_bounds__(256) void k_ba_schur_b(const BaArgs* __restrict__ args, const int* __restrict__ act) {
-    BA_PROLOGUE
-    BA_PHASE(kPhTrial)
-    const int i = bx_ * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
+__device__ __forceinline__ void schur_b_pose(const BaArgs& a, int i, int lane) {
     if (i >= a.np) return;
     double acc[6] = {0, 0, 0, 0, 0, 0};
     for (int k = a.ps_ptr[i] + lane; k < a.ps_ptr[i + 1]; k += 64) {
@@ -506,6 +589,11 @@ __global__ __launch_bounds__(256) void k_ba_schur_b(const BaArgs* __restrict__ a
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
         if (lane == 0) a.bs[6 * i + r] = a.b[6 * i + r] - v;
     }
+}
+__global__ __launch_bounds__(256) void k_ba_schur_b(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    BA_PROLOGUE
+    BA_PHASE(kPhTrial)
+    schur_b_pose(a, bx_ * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
 }
 
 // ---------------------------------------------------------------------------
@@ -898,42 +986,37 @@ __global__ void k_ba_ctl_stop(LmCtl* __restrict__ ctl, int B) {
     if (b < B) ctl[b].stop = 1;
 }
 
-// after the build: lambda initialisation on the first iteration (1e-5 max diagonal), then trials
-__global__ __launch_bounds__(1024) void k_ba_ctl_begin(const BaArgs* __restrict__ args, const int* __restrict__ act) {
-    __shared__ double sh[16];
-    const BaArgs& a = args[act[blockIdx.x]];
+// after the build: lambda initialisation on the first iteration (1e-5 max diagonal, from k_ba_lin's
+// per-workgroup maxima: sc1 loads), then trials. Run by the last workgroup of k_ba_lin.
+__device__ void ctl_begin_body(const BaArgs& a, int nlin) {
+    if (threadIdx.x != 0) return;
     LmCtl& c = *a.ctl;
-    if (c.phase != kPhBuild) return;   // uniform
-    if (c.it == 0) ba_reduce_body(a, 4, sh);
-    if (threadIdx.x == 0) {
-        if (c.it == 0) {
-            *const_cast<double*>(a.lambda) = 1e-5 * a.red[2];
-            c.ni = 2;
-            c.nBad = 0;
-        }
-        c.qmax = 0;
-        c.rho = 0;
-        c.phase = kPhTrial;
+    if (c.it == 0) {
+        double m = 0.0;
+        for (int i = 0; i < nlin; i++) m = fmax(m, ld_agent(a.part + i));
+        *const_cast<double*>(a.lambda) = 1e-5 * m;
+        c.ni = 2;
+        c.nBad = 0;
     }
+    c.qmax = 0;
+    c.rho = 0;
+    c.phase = kPhTrial;
 }
 
 // after a trial: chi2 and scale, rho, accept (lambda shrink) or reject (lambda *= ni, pop), and
-// the end-of-iteration rules
-__global__ __launch_bounds__(1024) void k_ba_ctl_end(const BaArgs* __restrict__ args, const int* __restrict__ act,
-                                                     int* done_flags) {
-    __shared__ double sh[16];
-    const BaArgs& a = args[act[blockIdx.x]];
+// the end-of-iteration rules. Run by the last workgroup of k_ba_errors(2) of the problem: the chi2
+// partials are that launch's (sc1 loads), the scale partials k_ba_backsub's.
+__device__ void ctl_end_body(const BaArgs& a, int prob, int* done_flags, double* sh) {
     LmCtl& c = *a.ctl;
-    if (c.phase != kPhTrial) return;   // uniform
     {   // chi2 and the scale from the trial kernels' workgroup partials (k_ba_errors, k_ba_backsub)
         double v = 0.0;
-        for (int i = threadIdx.x; i < a.npart_e; i += blockDim.x) v += a.part[i];
+        for (int i = threadIdx.x; i < a.npart_e; i += blockDim.x) v += ld_agent(a.part + i);
         v = block_sum(v, sh);
         if (threadIdx.x == 0) a.red[0] = v;
         const double lambda = *a.lambda, lam_pose = a.lead ? lambda : 0.0;
         v = 0.0;
         for (int j = threadIdx.x; j < a.n; j += blockDim.x) v += a.x[j] * (lam_pose * a.x[j] + a.b[j]);
-        for (int i = threadIdx.x; i < a.npart_m; i += blockDim.x) v += a.part[a.npart_e + i];
+        for (int i = threadIdx.x; i < a.npart_m; i += blockDim.x) v += ld_agent(a.part + a.npart_e + i);
         v = block_sum(v, sh);
         if (threadIdx.x == 0) a.red[1] = v;
     }
@@ -968,7 +1051,7 @@ __global__ __launch_bounds__(1024) void k_ba_ctl_end(const BaArgs* __restrict__ 
     if (c.early_stop && c.nBad >= 3) done = true;
     if (c.it >= c.iterations) done = true;   // the budget (checked by k_ba_errors(1) too), no idle slot
     c.phase = done ? kPhDone : kPhBuild;
-    if (done && done_flags) __hip_atomic_store(done_flags + act[blockIdx.x], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (done && done_flags) __hip_atomic_store(done_flags + prob, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------
@@ -1305,7 +1388,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         p.o_L = nR; nR += 1024 * ((n + 31) / 32);
         nR = (nR + 1) & ~size_t(1);
         p.o_part = nR; nR += 36 * (size_t)p.nslot;
-        p.o_red2 = nR; nR += (E + 255) / 256 + (M + 255) / 256 + 2;
+        p.o_red2 = nR;
+        nR += std::max((E + 255) / 256 + (std::max(M, P) + 255) / 256, (M + 255) / 256 + (np_ + 3) / 4) + 2;
         if (p.use_dag) {   // 128-byte aligned
             nR = (nR + 15) & ~size_t(15);
             p.o_dag = nR; nR += dag_doubles(p.n);
@@ -1593,14 +1677,13 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         const dim3 gB((unsigned)((B + 255) / 256)), b256(256);
         auto slot = [&]() -> int {
             hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 1, ws->d_done);
-            hipLaunchKernelGGL(k_ba_lin_points, dim3(gx(maxM, 256), B), b256, 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_lin_poses, dim3(gx(maxNp, 4), B), b256, 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_ctl_begin, dim3(B), dim3(1024), 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_lin, dim3(gx(maxM, 256) + gx(maxNp, 4), B), b256, 0, st, dA, d_act,
+                               (int)gx(maxM, 256));
             if (!s_readonly) hipLaunchKernelGGL(k_ba_zero_s, dim3(64, B), b256, 0, st, dA, d_act, 0);
             hipLaunchKernelGGL(k_ba_schur_points, dim3(gx(maxM, 256), B), b256, 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_schur_items, dim3(gx(2 * maxItems, 256), B), b256, 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_schur_items, dim3(gx(2 * maxItems, 256) + gx(maxNp, 4), B), b256, 0, st, dA, d_act,
+                               (int)gx(2 * maxItems, 256));
             hipLaunchKernelGGL(k_ba_schur_fin, dim3(gx(maxFin, 4), B), b256, 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_schur_b, dim3(gx(maxNp, 4), B), b256, 0, st, dA, d_act);
             if (ns) {
                 if (maxN <= kCholRegMaxN) BAOK(chol_reg_launch(maxN, ns, dA, d_act + 2 * B, st));
                 else hipLaunchKernelGGL(k_ba_cholesky, dim3(ns), dim3(512), chol_lds, st, dA, d_act + 2 * B);
@@ -1608,8 +1691,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             for (int b = 0; b < B; b++)
                 if (large(b) && large_solve(b, &dctl[b].phase)) return ORBHIP_ERR_DEVICE;
             hipLaunchKernelGGL(k_ba_backsub, dim3(gx(std::max(maxM, maxP), 256), B), b256, 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 2, nullptr);
-            hipLaunchKernelGGL(k_ba_ctl_end, dim3(B), dim3(1024), 0, st, dA, d_act, ws->d_done);
+            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 2, ws->d_done);
             int maxPM = 0;
             for (auto& p : pp) maxPM = std::max(maxPM, std::max(8 * p.P, 3 * p.M));
             hipLaunchKernelGGL(k_ba_pop, dim3(gx(maxPM, 256), B), b256, 0, st, dA, d_act);
@@ -1728,7 +1810,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             if (!s_clean) hipLaunchKernelGGL(k_ba_zero_s, dim3(64, nt_), dim3(256), 0, st, dA, d_act, 1);
             s_clean = s_readonly;
             hipLaunchKernelGGL(k_ba_schur_points, dim3(gx(maxM, 256), nt_), dim3(256), 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_schur_items, dim3(gx(2 * maxItems, 256), nt_), dim3(256), 0, st, dA, d_act);
+            hipLaunchKernelGGL(k_ba_schur_items, dim3(gx(2 * maxItems, 256), nt_), dim3(256), 0, st, dA, d_act,
+                               (int)gx(2 * maxItems, 256));
             hipLaunchKernelGGL(k_ba_schur_fin, dim3(gx(maxFin, 4), nt_), dim3(256), 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_schur_b, dim3(gx(maxNp, 4), nt_), dim3(256), 0, st, dA, d_act);
             if (shard_mode) {   // reduced camera system of all shards
