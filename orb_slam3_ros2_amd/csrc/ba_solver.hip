@@ -2,24 +2,25 @@
 // BundleAdjustment (U:src/Optimizer.cc) solved with the Levenberg-Marquardt schedule of
 // OptimizationAlgorithmLevenberg and the Schur complement of BlockSolver<6,3>.
 //
-// Batched: every kernel runs over grid.y = the ACTIVE problems of a round (problem index from
-// act[]), so B independent problems (SURVEY.md §8e "replicas": concurrent maps / agents, or a
-// batch of local windows) share each launch. The host runs each problem's exact g2o control
-// flow (iterations, trials, lambda schedule, push/pop, termination) with ONE device->host read
-// per trial ROUND (all problems' chi2, scale, solve flag). fp64 throughout:
-//   k_ba_errors        EdgeSE3ProjectXYZ::computeError + RobustKernelHuber::robustify
-//   k_ba_lin_points    linearizeOplus + constructQuadraticForm, landmark side (Hll, b_l, Hpl)
-//   k_ba_lin_poses     the pose side (Hpp, b_p), one wave per pose, deterministic tree
-//   k_ba_schur_points  setLambda on Hll, Dinv (Eigen 3x3 cofactor inverse), db, W = Hpl Dinv
-//   k_ba_schur_items   S_ij = [i==j](Hpp_i + lambda I) - sum W_a Hpl_b^T over shared landmarks:
-//   k_ba_schur_fin     one lane per chunk of a block's (host-built) pair list, chunk partials summed
-//                      in order by the finisher (deterministic gather, no atomics)
-//   k_ba_schur_b       b_schur = b_p - sum Hpl db
-//   k_ba_cholesky      dense LL^T + solves, one workgroup per problem; trailing update on
-//                      v_mfma_f64_16x16x4f64
+// Batched: every kernel runs over grid.y = the problems (problem index from act[]), so B
+// independent problems (SURVEY.md §8e "replicas": concurrent maps / agents, or a batch of local
+// windows) share each launch. The device-driven solve advances every problem by one LM trial per
+// slot with no host round trip (the g2o control flow on the device, LmCtl); the host-driven
+// rounds of r01 remain for the sharded solves. fp64 throughout:
+//   k_ba_errors        EdgeSE3ProjectXYZ::computeError + RobustKernelHuber::robustify; in a trial
+//                      its last workgroup per problem runs the LM controller step (ctl_end_body)
+//   k_ba_lin           linearizeOplus + constructQuadraticForm: landmark side (Hll, b_l, the
+//                      edge records) and pose side (Hpp, b_p, one wave per pose) in one launch;
+//                      its last workgroup per problem starts the trial (ctl_begin_body)
+//                      (k_ba_lin_points / k_ba_lin_poses: the same bodies for host-driven rounds)
+//   k_ba_schur_points  setLambda on Hll, Dinv (Eigen 3x3 cofactor inverse), db
+//   k_ba_schur_items   S_ij = [i==j](Hpp_i + lambda I) - sum W_a Hpl_b^T over shared landmarks,
+//                      matrix-free; its trailing workgroups compute b_schur = b_p - sum Hpl db
+//   k_ba_schur_fin     the blocks' chunk partials summed in order (deterministic, no atomics)
+//   k_chol_dag / k_ba_chol_reg / k_ba_cholesky / k_cb_*   the reduced camera system (ba_chol_*)
 //   k_ba_backsub       xl = Dinv (b_l - Hpl^T xp), X += xl (push: old X saved)
 //                      and T <- exp(xp) * T (SE3Quat::exp, operator*)   (push: old T saved)
-//   k_ba_reduce        activeRobustChi2, computeScale, max diag; fixed-order reductions
+//   k_ba_reduce        activeRobustChi2, computeScale, max diag (host-driven rounds)
 //   k_ba_pop           restore the pushed state of problems whose trial was rejected
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>

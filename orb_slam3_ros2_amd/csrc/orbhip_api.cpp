@@ -624,10 +624,13 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
     const int oct_max_dh = e_dh ? std::max(1, std::min(6, std::atoi(e_dh))) : 6;
     // pyramid engine, also per call: ORBHIP_NO_CONE=1 forces the k_resize cascade
     const bool no_cone = std::getenv("ORBHIP_NO_CONE") != nullptr;
-    // ORBHIP_NO_CONE_HI=1: batches run every level by k_resize
-    const bool no_cone_hi = std::getenv("ORBHIP_NO_CONE_HI") != nullptr;
+    // ORBHIP_CONE_HI=1: batches run levels 3.. as one cone launch behind two k_resize levels.
+    // Off by default: at C3 (B = 64, 1280x720) that launch took 255-320 us against the 89 us of
+    // the five k_resize launches it replaces (tools/c3_pyr_sweep.sh, tiles 16-48)
+    const char* e_hi = std::getenv("ORBHIP_CONE_HI");
+    const bool cone_hi_on = e_hi && e_hi[0] == '1';
     GraphKey key;
-    key.add(1).add((uint64_t)oct_fast).add((uint64_t)oct_max_dh).add((uint64_t)no_cone).add((uint64_t)no_cone_hi).add((uint64_t)c->fast_nt).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
+    key.add(1).add((uint64_t)oct_fast).add((uint64_t)oct_max_dh).add((uint64_t)no_cone).add((uint64_t)cone_hi_on).add((uint64_t)c->fast_nt).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
         .add((uint64_t)lap1).ptr(d_kps).ptr(d_desc).add((uint64_t)cap).ptr(d_n).ptr(d_mono).ptr(st).ptr(c->d_pyr.p)
         .ptr(c->d_cand.p).ptr(c->d_kscratch.p).ptr(c->d_nscratch.p).ptr(c->d_cand_cnt.p).ptr(c->d_lvl_kp.p)
         .ptr(c->d_lvl_cnt.p).ptr(c->d_lvl_nlap.p).ptr(c->d_err.p);
@@ -642,7 +645,7 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
                                            ? (size_t)std::atol(std::getenv("ORBHIP_CONE_MAX_WG"))
                                            : (size_t)1024;
         const bool cone_path = pl->cone_tiles && !no_cone && (size_t)B * pl->cone_tiles <= cone_max;
-        const bool cone_hi = !cone_path && pl->cone_hi_tiles && !no_cone_hi;
+        const bool cone_hi = !cone_path && pl->cone_hi_tiles && cone_hi_on;
         if (cone_path) {
             launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_cone_tab.p,
                             pl->cone_tab_stride, st);

@@ -1082,6 +1082,7 @@ struct ProjWorkspace {
     void* d = nullptr;
     size_t dcap = 0;
     void* h = nullptr;
+    void* hd = nullptr;   // h as the device addresses it (kernels write results there: no download)
     size_t hcap = 0;
     int ahead = 4;   // rounds launched per host sync (adapts to the last search)
     int init_ahead = 6;   // the same for SearchForInitialization's rounds
@@ -1153,6 +1154,7 @@ int ensure(ProjWorkspace* ws, size_t total) {
         ws->hcap = 0;
         PJOK(hipHostMalloc(&ws->h, total + total / 4, hipHostMallocDefault));
         ws->hcap = total + total / 4;
+        PJOK(hipHostGetDevicePointer(&ws->hd, ws->h, 0));
     }
     return ORBHIP_OK;
 }
@@ -1267,6 +1269,7 @@ int proj_search_last(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_proj
     const size_t o_pick0 = lay.add(4 * (size_t)nq);
     if (int rc = ensure(ws, lay.off)) return rc;
     char* H = (char*)ws->h;
+    char* HD = (char*)ws->hd;   // the two-launch form writes its results straight into H
     char* D = (char*)ws->d;
     std::memcpy(H + o_kps, F->kps, sizeof(orbhip_kp) * n);
     std::memcpy(H + o_kd, F->desc, 32 * (size_t)n);
@@ -1289,9 +1292,8 @@ int proj_search_last(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_proj
         hipLaunchKernelGGL(k_proj_resolve<0>, dim3(1), dim3(1024), kResolveLds, st, n, nq, 0.f, check_orientation,
                            cap, resolve_ent_cap(n, nq), (const float*)(D + o_ang), (const orbhip_kp*)(D + o_kps),
                            (const uint64_t*)(D + o_list), (const int*)(D + o_lcnt), (const int*)(D + o_pick0),
-                           (int*)(D + o_pick), (int*)(D + o_out + ob.match), (int*)(D + o_out + ob.res));
+                           (int*)(D + o_pick), (int*)(HD + o_out + ob.match), (int*)(HD + o_out + ob.res));
         PJOK(hipGetLastError());
-        PJOK(hipMemcpyAsync(H + o_out, D + o_out, ob.bytes, hipMemcpyDeviceToHost, st));
         PJOK(hipStreamSynchronize(st));
         if (hres[1] == 0) {
             std::memcpy(match, H + o_out + ob.match, 4 * (size_t)nq);
@@ -1345,6 +1347,7 @@ int proj_search_local(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_loc
     const size_t o_pick0 = lay.add(4 * (size_t)nq);
     if (int rc = ensure(ws, lay.off)) return rc;
     char* H = (char*)ws->h;
+    char* HD = (char*)ws->hd;   // the two-launch form writes its results straight into H
     char* D = (char*)ws->d;
     std::memcpy(H + o_kps, F->kps, sizeof(orbhip_kp) * n);
     std::memcpy(H + o_kd, F->desc, 32 * (size_t)n);
@@ -1375,13 +1378,13 @@ int proj_search_local(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_loc
         hipLaunchKernelGGL(k_proj_lists<1>, dim3((unsigned)((nq + kListWaves - 1) / kListWaves)), dim3(1024),
                            16 * (size_t)n, st, f, nq, PrepLast{}, pc, cap, nnratio, (const orbhip_kp*)(D + o_kps),
                            (const uint8_t*)(D + o_kd), dcl, (const uint8_t*)(D + o_qd), (uint64_t*)(D + o_list),
-                           (int*)(D + o_lcnt), (int*)(D + o_pick0), d_iv, d_lvl);
+                           (int*)(D + o_lcnt), (int*)(D + o_pick0), (uint8_t*)(HD + o_out + ob.iv),
+                           (int*)(HD + o_out + ob.lvl));
         hipLaunchKernelGGL(k_proj_resolve<1>, dim3(1), dim3(1024), kResolveLds, st, n, nq, nnratio, 0, cap,
                            resolve_ent_cap(n, nq), (const float*)nullptr, (const orbhip_kp*)(D + o_kps),
                            (const uint64_t*)(D + o_list), (const int*)(D + o_lcnt), (const int*)(D + o_pick0),
-                           (int*)(D + o_pick), (int*)(D + o_out + ob.match), (int*)(D + o_out + ob.res));
+                           (int*)(D + o_pick), (int*)(HD + o_out + ob.match), (int*)(HD + o_out + ob.res));
         PJOK(hipGetLastError());
-        PJOK(hipMemcpyAsync(H + o_out, D + o_out, ob.bytes, hipMemcpyDeviceToHost, st));
         PJOK(hipStreamSynchronize(st));
         if (hres[1] == 0) {
             outputs();

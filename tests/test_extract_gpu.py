@@ -46,24 +46,26 @@ def test_sizes_bit_exact(ext1000, oracle, w, h, seed):
                                                  (1001, 751, 2.5, 3, 34)])
 @pytest.mark.parametrize("hi", ["cone", "resize"])
 def test_resize_cascade_bit_exact(oracle, monkeypatch, w, h, scale, nlev, seed, hi):
-    """The batch engine forced on single frames: k_resize for levels 1-2, then the batch cone
-    (levels 3.. in one launch from level 2) or k_resize for every level. Odd sizes take the edge
+    """The batch engine forced on single frames: k_resize for every level (the default), or
+    k_resize for levels 1-2 and the opt-in batch cone (ORBHIP_CONE_HI=1: levels 3.. in one
+    launch from level 2). Odd sizes take the edge
     lanes, scale factors above 1.2 k_resize's per-row path (a 4-row group reads more than 6
     source rows), all bit-exact against the oracle's cv::resize restatement."""
     from orb_slam3_ros2_amd import ORBextractor
     monkeypatch.setenv("ORBHIP_NO_CONE", "1")
-    if hi == "resize":
-        monkeypatch.setenv("ORBHIP_NO_CONE_HI", "1")
+    if hi == "cone":
+        monkeypatch.setenv("ORBHIP_CONE_HI", "1")
     ext = ORBextractor(1000, scale, nlev, 20, 7)
     _check(ext, oracle, synthetic_frame(seed, w, h), scale=scale, nlevels=nlev)
 
 
 @pytest.mark.parametrize("tile", [5, 17, 48])
 def test_batch_cone_tiles_bit_exact(oracle, monkeypatch, tile):
-    """The batch cone (levels 3.. from level 2, ORBHIP_CONE_HI_TILE per plan lookup) at tile
-    edges other than its default 32: every tiling writes the same pyramid."""
+    """The opt-in batch cone (levels 3.. from level 2, ORBHIP_CONE_HI_TILE per plan lookup) at
+    tile edges other than its default 32: every tiling writes the same pyramid."""
     from orb_slam3_ros2_amd import ORBextractor
     monkeypatch.setenv("ORBHIP_NO_CONE", "1")
+    monkeypatch.setenv("ORBHIP_CONE_HI", "1")
     monkeypatch.setenv("ORBHIP_CONE_HI_TILE", str(tile))
     ext = ORBextractor(1000, 1.2, 8, 20, 7)
     _check(ext, oracle, synthetic_frame(70 + tile, 1280, 720))

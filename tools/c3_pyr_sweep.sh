@@ -6,9 +6,9 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out/c3sweep
 for cfg in ${CFGS:-t16 t32 t64 w64_1024 w48_512 resize}; do
   case $cfg in
-    resize) envs="ORBHIP_NO_CONE_HI=1";;
-    w*) t=${cfg#w}; envs="ORBHIP_CONE_HI_TILE=${t%_*} ORBHIP_CONE_HI_THREADS=${t#*_}";;
-    t*) envs="ORBHIP_CONE_HI_TILE=${cfg#t}";;
+    resize) envs="ORBHIP_CONE_HI=0";;
+    w*) t=${cfg#w}; envs="ORBHIP_CONE_HI=1 ORBHIP_CONE_HI_TILE=${t%_*} ORBHIP_CONE_HI_THREADS=${t#*_}";;
+    t*) envs="ORBHIP_CONE_HI=1 ORBHIP_CONE_HI_TILE=${cfg#t}";;
   esac
   env $envs timeout -k 10 100 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/c3sweep/$cfg -o c3 \
       -- python3 tools/pmc_workload.py c3 > gpurun_out/c3sweep/$cfg.log 2>&1 || { tail -5 gpurun_out/c3sweep/$cfg.log; exit 1; }
