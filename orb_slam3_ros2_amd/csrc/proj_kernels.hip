@@ -354,14 +354,26 @@ __global__ __launch_bounds__(1024) void k_proj_lists(ProjFrame f, int nq, PrepLa
         qa = qd4[0];
         qb = qd4[1];
     }
-    for (int k = threadIdx.x; k < n; k += blockDim.x) {
-        const orbhip_kp kp = kps[k];
-        const int px = (int)roundf((kp.x - f.minx) * f.invw);
-        const int py = (int)roundf((kp.y - f.miny) * f.invh);
-        const int c = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? 0xFFFF : px * kGridRows + py;
-        const uint32_t cl = (claimed && claimed[k]) ? 1u : 0u;
-        kl[k] = uint4{__float_as_uint(kp.x), __float_as_uint(kp.y), ((uint32_t)c << 16) | (cl << 8) |
-                      (uint32_t)(kp.octave & 0xFF), 0u};
+    // two keypoints per thread in flight (1250 keypoints: one round trip)
+    for (int k0 = threadIdx.x; k0 < n; k0 += 2 * blockDim.x) {
+        orbhip_kp kp[2];
+        uint32_t cl[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int k = min(k0 + u * (int)blockDim.x, n - 1);
+            kp[u] = kps[k];
+            cl[u] = (claimed && claimed[k]) ? 1u : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int k = k0 + u * (int)blockDim.x;
+            if (k >= n) break;
+            const int px = (int)roundf((kp[u].x - f.minx) * f.invw);
+            const int py = (int)roundf((kp[u].y - f.miny) * f.invh);
+            const int c = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? 0xFFFF : px * kGridRows + py;
+            kl[k] = uint4{__float_as_uint(kp[u].x), __float_as_uint(kp[u].y), ((uint32_t)c << 16) | (cl[u] << 8) |
+                          (uint32_t)(kp[u].octave & 0xFF), 0u};
+        }
     }
     __syncthreads();
     if (i >= nq) return;
@@ -460,10 +472,17 @@ __global__ __launch_bounds__(1024) void k_proj_resolve(int n, int nq, float nnra
     for (int i = tid; i < nq; i += nt) {
         const int p = pick[i];
         if (p >= 0) atomicMin(&own[n + p], i);
-        if (in_lds) {
+        if (in_lds) {   // 8 loads in flight before their stores (one round trip per 8 entries)
             const int c = lcnt[i], o = qoff[i];
             const uint64_t* L = lists + (size_t)i * cap;
-            for (int j = 0; j < c; j++) ent[o + j] = L[j];
+            for (int j0 = 0; j0 < c; j0 += 8) {
+                uint64_t v[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) v[u] = j0 + u < c ? L[j0 + u] : 0ull;
+#pragma unroll
+                for (int u = 0; u < 8; u++)
+                    if (j0 + u < c) ent[o + j0 + u] = v[u];
+            }
         }
     }
     __syncthreads();

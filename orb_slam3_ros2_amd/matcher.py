@@ -25,6 +25,7 @@ class ORBmatcher:
         self.mfNNratio = float(nnratio)
         self.mbCheckOrientation = bool(checkOri)
         self.ctx = ctx or Context(device)
+        self._lp_cache = None   # SearchLocalPoints: the C view of the last call's map-point arrays
 
     @staticmethod
     def DescriptorDistance(a, b) -> int:
@@ -118,18 +119,30 @@ class ORBmatcher:
                           th_far: float = 0.0):
         """Tracking::SearchLocalPoints: Frame::isInFrustum + SearchByProjection(F, vpMapPoints, th,
         bFarPoints, thFarPoints) with this matcher's nnratio. Returns (nmatches, match, in_view, level)."""
-        pts = np.ascontiguousarray(points, np.float32).reshape(-1, 3)
-        nrm = np.ascontiguousarray(normals, np.float32).reshape(-1, 3)
-        mn = np.ascontiguousarray(min_dist, np.float32)
-        mx = np.ascontiguousarray(max_dist, np.float32)
-        d = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
-        sk = None if skip is None else np.ascontiguousarray(skip, np.uint8)
-        m = pts.shape[0]
+        key = (id(points), id(normals), id(min_dist), id(max_dist), id(mp_desc), id(skip))
+        hit = self._lp_cache
+        if hit is not None and hit[0] == key and all(a is b for a, b in zip(hit[1], (points, normals, min_dist,
+                                                                                      max_dist, mp_desc, skip))):
+            lc, m = hit[2], hit[3]   # the same arrays as the last call: their C view is still valid
+        else:
+            pts = np.ascontiguousarray(points, np.float32).reshape(-1, 3)
+            nrm = np.ascontiguousarray(normals, np.float32).reshape(-1, 3)
+            mn = np.ascontiguousarray(min_dist, np.float32)
+            mx = np.ascontiguousarray(max_dist, np.float32)
+            d = np.ascontiguousarray(mp_desc, np.uint8).reshape(-1, 32)
+            sk = None if skip is None else np.ascontiguousarray(skip, np.uint8)
+            m = pts.shape[0]
+            lc = LocalPointsC(m, ptr(pts), ptr(nrm), ptr(mn), ptr(mx), ptr(d), ptr(sk))
+            # cached only when no conversion copied an input (the view then reads the caller's
+            # memory, so in-place updates are seen); the inputs live with it, so their ids stay theirs
+            srcs = (points, normals, min_dist, max_dist, mp_desc, skip)
+            views = (pts, nrm, mn, mx, d, sk)
+            zero_copy = all(v is o or (v is not None and v.base is o) for v, o in zip(views, srcs))
+            self._lp_cache = (key, srcs, lc, m, views) if zero_copy else None
         match = np.empty(m, np.int32)      # written in full by the call (m > 0)
         in_view = np.empty(m, np.uint8)
         level = np.empty(m, np.int32)
         fc = frame.to_c()
-        lc = LocalPointsC(m, ptr(pts), ptr(nrm), ptr(mn), ptr(mx), ptr(d), ptr(sk))
         n = check(lib().orbhip_search_local_points(self.ctx.handle, ctypes.byref(fc), ctypes.byref(lc),
                                                    float(view_cos_limit), float(th), float(self.mfNNratio),
                                                    int(far_points), float(th_far), ptr(in_view), ptr(level),
