@@ -74,27 +74,23 @@ __device__ __forceinline__ int rz_px(int p00, int p01, int p10, int p11, int aa,
     return v < 0 ? 0 : (v > 255 ? 255 : v);
 }
 
-__global__ __launch_bounds__(256) void k_resize(const ExtractPlan* __restrict__ P, FrameBufs fb, int l,
-                                                const int* __restrict__ xofs, const int* __restrict__ xalpha,
-                                                const int* __restrict__ yofs, const int* __restrict__ ybeta) {
-    TR_BEGIN()
+// one lane's 4 columns x kRzRows rows of level l of frame f: output rows [dyb, min(dyb + kRzRows,
+// row_end)) (dyb wave-uniform), columns dx0..dx0+3 (dx0 < the level's width)
+__device__ __forceinline__ void resize_tile(const ExtractPlan* __restrict__ P, const FrameBufs& fb, int f, int l,
+                                            int dyb, int dx0, int row_end, const int* __restrict__ xofs,
+                                            const int* __restrict__ xalpha, const int* __restrict__ yofs,
+                                            const int* __restrict__ ybeta) {
     // geometry copied to registers (the byte stores below may alias the plan for the compiler)
-    const int Dw = P->lv[l].w, Dh = P->lv[l].h, Dpitch = P->lv[l].pitch;
+    const int Dw = P->lv[l].w, Dpitch = P->lv[l].pitch;
     const int xmax = P->lv[l].xmax, vend = P->lv[l].vend;
     const int xtab = P->lv[l].xtab_off, ytab = P->lv[l].ytab_off;
     const int Sw = P->lv[l - 1].w, Sh = P->lv[l - 1].h;
-    const int f = blockIdx.z;
-    // row groups on blockIdx.x: consecutive work-groups (dealt round-robin to the XCDs) walk down
-    // a column strip, so every XCD gets the same share of the light right-edge strip
-    const int dyb = (blockIdx.x * 4 + threadIdx.y) * kRzRows;   // wave-uniform
-    const int dx0 = (blockIdx.y * 64 + threadIdx.x) * 4;
-    if (dyb >= Dh || dx0 >= Dw) return;
     const ImgRef src = level_img(P, fb, f, l - 1);
     uint8_t* const dst0 = fb.pyr + (int64_t)f * P->pyr_bytes + P->lv[l].pyr_off;
     // the 4 columns' tables as one int4 each (16-byte aligned per level), the rows' tables
     const int4 xo4 = *(const int4*)(xofs + xtab + dx0);
     const int4 xa4 = *(const int4*)(xalpha + xtab + dx0);
-    const int nrow = min(kRzRows, Dh - dyb);
+    const int nrow = min(kRzRows, row_end - dyb);
     int sy[kRzRows], bbv[kRzRows];
 #pragma unroll
     for (int j = 0; j < kRzRows; j++) {
@@ -200,7 +196,48 @@ __global__ __launch_bounds__(256) void k_resize(const ExtractPlan* __restrict__ 
             }
         }
     }
+}
+
+__global__ __launch_bounds__(256) void k_resize(const ExtractPlan* __restrict__ P, FrameBufs fb, int l,
+                                                const int* __restrict__ xofs, const int* __restrict__ xalpha,
+                                                const int* __restrict__ yofs, const int* __restrict__ ybeta) {
+    TR_BEGIN()
+    const int Dw = P->lv[l].w, Dh = P->lv[l].h;
+    // row groups on blockIdx.x: consecutive work-groups (dealt round-robin to the XCDs) walk down
+    // a column strip, so every XCD gets the same share of the light right-edge strip
+    const int dyb = (blockIdx.x * 4 + threadIdx.y) * kRzRows;   // wave-uniform
+    const int dx0 = (blockIdx.y * 64 + threadIdx.x) * 4;
+    if (dyb >= Dh || dx0 >= Dw) return;
+    resize_tile(P, fb, blockIdx.z, l, dyb, dx0, Dh, xofs, xalpha, yofs, ybeta);
     if (l == 1) { TR_END(0) }
+}
+
+// Levels s0+1 .. L-1 of every frame in ONE launch (batches: the small levels' k_resize launches
+// are latency-bound, ~13-25 us each at C3 whatever their size). Work-group (band, frame) computes,
+// level by level, the full-width output rows rows[band][l] = its band of level l plus the halo
+// rows the next level's band rows read, from the level below in global memory (its own rows of
+// the step before; level s0 from k_resize), and writes them to the pyramid. A halo row is
+// computed by both neighbouring bands with identical bytes. Waves take (4-row group, 256-column
+// strip) tiles in turn; one workgroup barrier per level; no work-group waits for another.
+__global__ __launch_bounds__(1024) void k_resize_bands(const ExtractPlan* __restrict__ P, FrameBufs fb, int s0,
+                                                       const int2* __restrict__ rows, const int* __restrict__ xofs,
+                                                       const int* __restrict__ xalpha,
+                                                       const int* __restrict__ yofs,
+                                                       const int* __restrict__ ybeta) {
+    const int band = blockIdx.x, f = blockIdx.y;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    const int L = P->n_levels;
+    for (int l = s0 + 1; l < L; l++) {
+        const int2 rr = rows[band * kMaxLevels + l];
+        const int Dw = P->lv[l].w;
+        const int ng = (rr.y - rr.x + kRzRows - 1) / kRzRows, ns = (Dw + 255) / 256;
+        for (int t = wave; t < ng * ns; t += nw) {   // wave-uniform
+            const int g = t / ns, sidx = t - g * ns;
+            const int dx0 = sidx * 256 + lane * 4;
+            if (dx0 < Dw) resize_tile(P, fb, f, l, rr.x + g * kRzRows, dx0, rr.y, xofs, xalpha, yofs, ybeta);
+        }
+        __syncthreads();   // the level's rows (this work-group's global stores) before the next level reads them
+    }
 }
 
 // quotient of i / d for 0 <= i < 2^16, d >= 1: the float reciprocal's error stays below the
@@ -1941,6 +1978,11 @@ void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs
     dim3 blk(64, 4, 1);
     dim3 grd((D.h + 4 * kRzRows - 1) / (4 * kRzRows), (D.w + 255) / 256, B);
     ORBHIP_LAUNCH(k_resize, grd, blk, 0, st, dP, fb, l, xofs, xalpha, yofs, ybeta);
+}
+
+void launch_resize_bands(const ExtractPlan* dP, int nbands, const FrameBufs& fb, int B, int s0, const int2* rows,
+                         const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st) {
+    ORBHIP_LAUNCH(k_resize_bands, dim3(nbands, B), dim3(1024), 0, st, dP, fb, s0, rows, xofs, xalpha, yofs, ybeta);
 }
 
 void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameBufs& fb, int B, const ConeRect* rects,

@@ -73,6 +73,13 @@ static int cone_hi_threads() {
     return (t == 512 || t == 1024) ? t : 256;
 }
 
+constexpr int kBandStart = 2;   // batches: k_resize for levels 1..2, k_resize_bands for the rest
+// row bands per frame of k_resize_bands: ORBHIP_RZ_BANDS (0: every level by k_resize), else 16
+static int rz_bands() {   // read per plan lookup (tests switch it)
+    const char* e = std::getenv("ORBHIP_RZ_BANDS");
+    return e ? std::max(0, std::atoi(e)) : 16;
+}
+
 struct Plan {
     ExtractPlan h{};
     std::vector<CellGeom> cells;
@@ -92,6 +99,10 @@ struct Plan {
     size_t cone_hi_lds = 0;
     DevBuf<ConeRect> d_cone_hi;
     DevBuf<int> d_cone_hi_tab;
+    // batches: levels kBandStart+1..L-1 by k_resize_bands, the output rows of each (band, level)
+    std::vector<int> bands;   // [nbands][kMaxLevels] (r0, r1) pairs
+    int nbands = 0;
+    DevBuf<int> d_bands;
     OctreeCfg oct{};
     int kp_cap_frame = 0;   // sum of level caps = max keypoints per frame
     DevBuf<ExtractPlan> d_plan;
@@ -109,7 +120,7 @@ struct Plan {
 // per-tile resize tables are ~0.5 MB at 640x480) stay L2-resident once instead of once per
 // context. The cache holds weak references: a plan dies with the last context using it.
 struct PlanKey {
-    int device, w, h, nfeat, nlev, ini, mn, cone_tile, clist_cap, fast_nt, cone_hi_tile;
+    int device, w, h, nfeat, nlev, ini, mn, cone_tile, clist_cap, fast_nt, cone_hi_tile, rz_bands;
     float scale;
     bool operator<(const PlanKey& o) const {
         return std::memcmp(this, &o, sizeof(PlanKey)) < 0;
@@ -328,6 +339,7 @@ static int build_plan(orbhip_ctx* c, int w, int h, Plan** out) {
     k.clist_cap = cap_env ? atoi(cap_env) : -1;
     k.fast_nt = nt_env ? atoi(nt_env) : -1;
     k.cone_hi_tile = cone_hi_tile_of();
+    k.rz_bands = rz_bands();
     auto it = c->plans.find(k);
     if (it != c->plans.end()) { *out = it->second.get(); return ORBHIP_OK; }
     std::lock_guard<std::mutex> g(g_plan_m);
@@ -541,6 +553,33 @@ static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& ou
             }
         }
     }
+    // k_resize_bands rows: per band, from the last level down, its own rows of the level plus the
+    // rows the next level's band rows read (the source rows of k_resize's row tables, clamped)
+    {
+        const int nb = std::min(rz_bands(), L > 0 ? P.lv[L - 1].h : 0);
+        if (L > kBandStart + 1 && nb > 0) {
+            pl->bands.assign((size_t)nb * kMaxLevels * 2, 0);
+            for (int b = 0; b < nb; b++) {
+                int n0 = 0, n1 = 0;   // the rows of level l + 1 this band computes
+                for (int l = L - 1; l > kBandStart; l--) {
+                    const LevelGeom& G = P.lv[l];
+                    int r0 = (int)((int64_t)b * G.h / nb), r1 = (int)((int64_t)(b + 1) * G.h / nb);
+                    if (l < L - 1 && n1 > n0) {
+                        const LevelGeom& U = P.lv[l + 1];
+                        auto clampr = [&](int r) { return r < 0 ? 0 : (r < G.h ? r : G.h - 1); };
+                        const int s0r = clampr(pl->yofs[U.ytab_off + n0]);
+                        const int s1r = clampr(pl->yofs[U.ytab_off + n1 - 1] + 1) + 1;
+                        if (r1 > r0) { r0 = std::min(r0, s0r); r1 = std::max(r1, s1r); }
+                        else { r0 = s0r; r1 = s1r; }
+                    }
+                    pl->bands[((size_t)b * kMaxLevels + l) * 2] = r0;
+                    pl->bands[((size_t)b * kMaxLevels + l) * 2 + 1] = r1;
+                    n0 = r0; n1 = r1;
+                }
+            }
+            pl->nbands = nb;
+        }
+    }
     // IC_Angle disc offsets (u, v) packed as int16 pairs
     for (int v = -15; v <= 15; v++) {
         const int d = c->umax[std::abs(v)];
@@ -579,6 +618,7 @@ static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& ou
     HIPOK(up(pl->d_disc, pl->disc));
     HIPOK(pl->d_otab.ensure(pl->otab.size()));
     HIPOK(hipMemcpy(pl->d_otab.p, pl->otab.data(), pl->otab.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+    if (pl->nbands) HIPOK(up(pl->d_bands, pl->bands));
     if (!pl->cone_hi.empty()) {
         HIPOK(pl->d_cone_hi.ensure(pl->cone_hi.size()));
         HIPOK(hipMemcpy(pl->d_cone_hi.p, pl->cone_hi.data(), pl->cone_hi.size() * sizeof(ConeRect),
@@ -650,12 +690,17 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
             launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_cone_tab.p,
                             pl->cone_tab_stride, st);
         } else {
-            for (int l = 1; l < (cone_hi ? kConeHiStart + 1 : P.n_levels); l++)
+            const bool bands = !cone_hi && pl->nbands > 0;
+            const int lr = cone_hi ? kConeHiStart + 1 : (bands ? kBandStart + 1 : P.n_levels);
+            for (int l = 1; l < lr; l++)
                 launch_resize(pl->d_plan.p, P, fb, B, l, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p, pl->d_ybeta.p,
                               st);
             if (cone_hi)
                 launch_pyr_cone(pl->d_plan.p, pl->cone_hi_tiles, pl->cone_hi_lds, fb, B, pl->d_cone_hi.p,
                                 pl->d_cone_hi_tab.p, pl->cone_hi_tab_stride, st, kConeHiStart, cone_hi_threads());
+            if (bands)
+                launch_resize_bands(pl->d_plan.p, pl->nbands, fb, B, kBandStart, (const int2*)pl->d_bands.p,
+                                    pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p, pl->d_ybeta.p, st);
         }
         tm.end(1, st);
         tm.begin(2, st);

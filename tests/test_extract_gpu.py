@@ -44,17 +44,21 @@ def test_sizes_bit_exact(ext1000, oracle, w, h, seed):
 @pytest.mark.parametrize("w,h,scale,nlev,seed", [(1280, 720, 1.2, 8, 30), (641, 479, 1.2, 8, 31),
                                                  (641, 481, 1.5, 5, 32), (801, 601, 1.9, 4, 33),
                                                  (1001, 751, 2.5, 3, 34)])
-@pytest.mark.parametrize("hi", ["cone", "resize"])
+@pytest.mark.parametrize("hi", ["bands", "bands5", "resize", "cone"])
 def test_resize_cascade_bit_exact(oracle, monkeypatch, w, h, scale, nlev, seed, hi):
-    """The batch engine forced on single frames: k_resize for every level (the default), or
-    k_resize for levels 1-2 and the opt-in batch cone (ORBHIP_CONE_HI=1: levels 3.. in one
-    launch from level 2). Odd sizes take the edge
+    """The batch engine forced on single frames: k_resize for levels 1-2, then levels 3.. by
+    k_resize_bands (16 row bands per frame, the default; 5 bands), by k_resize alone
+    (ORBHIP_RZ_BANDS=0) or by the opt-in batch cone (ORBHIP_CONE_HI=1). Odd sizes take the edge
     lanes, scale factors above 1.2 k_resize's per-row path (a 4-row group reads more than 6
     source rows), all bit-exact against the oracle's cv::resize restatement."""
     from orb_slam3_ros2_amd import ORBextractor
     monkeypatch.setenv("ORBHIP_NO_CONE", "1")
     if hi == "cone":
         monkeypatch.setenv("ORBHIP_CONE_HI", "1")
+    elif hi == "resize":
+        monkeypatch.setenv("ORBHIP_RZ_BANDS", "0")
+    elif hi == "bands5":
+        monkeypatch.setenv("ORBHIP_RZ_BANDS", "5")
     ext = ORBextractor(1000, scale, nlev, 20, 7)
     _check(ext, oracle, synthetic_frame(seed, w, h), scale=scale, nlevels=nlev)
 
