@@ -312,6 +312,21 @@ constexpr int kProjMaxN = 8192;   // frame keypoints: staged in LDS (16 B each),
 constexpr int kProjMaxQ = 8192;   // queries: list offsets in LDS
 constexpr int kListWaves = 16;    // queries per k_proj_lists work-group (one per wave)
 
+typedef __attribute__((address_space(1))) int pj_gint;
+typedef __attribute__((address_space(1))) unsigned long long pj_gull;
+__device__ __forceinline__ void st_ag(uint64_t* p, uint64_t v) {
+    __hip_atomic_store((pj_gull*)p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_ag(const uint64_t* p) {
+    return __hip_atomic_load((pj_gull*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_ag(int* p, int v) {
+    __hip_atomic_store((pj_gint*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_ag(const int* p) {
+    return __hip_atomic_load((pj_gint*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ int proj_decide(const Top2& t, int mode, float nnratio) {
     if (t.d1 > kThHigh) return -1;
     if (mode == 0) return t.k1 & 0xFFFF;
@@ -319,6 +334,23 @@ __device__ __forceinline__ int proj_decide(const Top2& t, int mode, float nnrati
     const bool reject = same && (float)t.d1 > nnratio * (float)t.d2;
     return (!reject && (!same || (float)t.d1 <= nnratio * (float)t.d2)) ? (t.k1 & 0xFFFF) : -1;
 }
+
+// the one-launch form: the last work-group of k_proj_lists runs resolve_body (arrive: a counter,
+// 0 between launches; fuse 0: the resolve runs as its own launch)
+struct ResolveArgs {
+    int fuse, check_orientation, ent_cap;
+    const float* qangle;
+    int* pick;
+    int* match;
+    int* res;
+    int* arrive;
+};
+template <int MODE>
+__device__ void resolve_body(unsigned char* rsm, int n, int nq, float nnratio, int check_orientation, int cap,
+                             int ent_cap, const float* __restrict__ qangle, const orbhip_kp* __restrict__ kps,
+                             const uint64_t* __restrict__ lists, const int* __restrict__ lcnt,
+                             const int* __restrict__ pick0, int* __restrict__ pick, int* __restrict__ match,
+                             int* __restrict__ res);
 
 // the frame's keypoints are staged once per work-group in LDS as (x, y, cell << 16 | claimed << 8 |
 // octave, 0): PosInGrid computed as k_proj_cells does, a 16-byte read per lane and keypoint. The
@@ -334,7 +366,7 @@ __global__ __launch_bounds__(1024) void k_proj_lists(ProjFrame f, int nq, PrepLa
                                                      const uint8_t* __restrict__ qdesc,
                                                      uint64_t* __restrict__ lists, int* __restrict__ lcnt,
                                                      int* __restrict__ pick0, uint8_t* __restrict__ in_view,
-                                                     int* __restrict__ level) {
+                                                     int* __restrict__ level, ResolveArgs ra) {
     extern __shared__ uint4 kl[];
     const int n = f.n;
     const int i = blockIdx.x * kListWaves + (threadIdx.x >> 6);
@@ -376,10 +408,9 @@ __global__ __launch_bounds__(1024) void k_proj_lists(ProjFrame f, int nq, PrepLa
         }
     }
     __syncthreads();
-    if (i >= nq) return;
     int cnt = 0;
     Top2 t{256, INT_MAX, -1, 256, INT_MAX, -1};
-    if (Q.valid) {
+    if (i < nq && Q.valid) {
         const int nMinCellX = max(0, (int)floorf((Q.u - f.minx - Q.r) * f.invw));
         const int nMaxCellX = min(kGridCols - 1, (int)ceilf((Q.u - f.minx + Q.r) * f.invw));
         const int nMinCellY = max(0, (int)floorf((Q.v - f.miny - Q.r) * f.invh));
@@ -410,7 +441,7 @@ __global__ __launch_bounds__(1024) void k_proj_lists(ProjFrame f, int nq, PrepLa
                               __popc(qa.w ^ ka.w) + __popc(qb.x ^ kb.x) + __popc(qb.y ^ kb.y) +
                               __popc(qb.z ^ kb.z) + __popc(qb.w ^ kb.w);
                 const int pos = cnt + __popcll(m & ((1ull << lane) - 1ull));
-                if (pos < cap) out[pos] = ((uint64_t)d << 32) | (uint64_t)((key << 4) | (oct & 15u));
+                if (pos < cap) st_ag(out + pos, ((uint64_t)d << 32) | (uint64_t)((key << 4) | (oct & 15u)));
                 if (d != 256) top2_add(t, d, (int)key, (int)(oct & 15u));
             }
             cnt += __popcll(m);
@@ -423,24 +454,37 @@ __global__ __launch_bounds__(1024) void k_proj_lists(ProjFrame f, int nq, PrepLa
         top2_add(t, d1, k1, l1);
         top2_add(t, d2, k2, l2);
     }
-    if (lane == 0) {
-        lcnt[i] = cnt;
-        pick0[i] = proj_decide(t, MODE, nnratio);
+    if (lane == 0 && i < nq) {
+        st_ag(lcnt + i, cnt);
+        st_ag(pick0 + i, proj_decide(t, MODE, nnratio));
     }
+    if (!ra.fuse) return;   // uniform
+    // one launch: every wave's list stores drained, then the last work-group to arrive resolves
+    __shared__ int lastf;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int old = __hip_atomic_fetch_add((pj_gint*)ra.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lastf = old == (int)gridDim.x - 1;
+        if (lastf) __hip_atomic_store((pj_gint*)ra.arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (lastf)
+        resolve_body<MODE>((unsigned char*)kl, n, nq, nnratio, ra.check_orientation, cap, ra.ent_cap, ra.qangle, kps,
+                           lists, lcnt, pick0, ra.pick, ra.match, ra.res);
 }
 
 // res[0] = matches, res[1] = status (1: a list overflowed, nothing else written), res[2] = rounds.
-// Dynamic LDS: 3 owner tables (n ints), the list offsets (nq ints), then the lists themselves when
-// they fit the rest (`ent_cap` entries; else the rounds read them from global memory).
+// LDS rsm: 3 owner tables (n ints), the list offsets (nq ints), then the lists themselves when
+// they fit the rest (`ent_cap` entries; else the rounds read them from global memory). The lists,
+// their counts and pick0 are read with agent-scope (sc1) loads: in the one-launch form they were
+// written by the other work-groups of the same launch.
 template <int MODE>
-__global__ __launch_bounds__(1024) void k_proj_resolve(int n, int nq, float nnratio, int check_orientation, int cap,
-                                                       int ent_cap, const float* __restrict__ qangle,
-                                                       const orbhip_kp* __restrict__ kps,
-                                                       const uint64_t* __restrict__ lists,
-                                                       const int* __restrict__ lcnt, const int* __restrict__ pick0,
-                                                       int* __restrict__ pick,
-                                                       int* __restrict__ match, int* __restrict__ res) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char rsm[];
+__device__ void resolve_body(unsigned char* rsm, int n, int nq, float nnratio, int check_orientation, int cap,
+                             int ent_cap, const float* __restrict__ qangle, const orbhip_kp* __restrict__ kps,
+                             const uint64_t* __restrict__ lists, const int* __restrict__ lcnt,
+                             const int* __restrict__ pick0, int* __restrict__ pick, int* __restrict__ match,
+                             int* __restrict__ res) {
     int* own = (int*)rsm;                        // 3 x n
     int* qoff = own + 3 * n;                     // nq
     uint64_t* ent = (uint64_t*)(rsm + (((size_t)(3 * n + nq) * 4 + 15) & ~size_t(15)));
@@ -454,11 +498,11 @@ __global__ __launch_bounds__(1024) void k_proj_resolve(int n, int nq, float nnra
     int over = 0, run = 0;
     for (int i0 = 0; i0 < nq; i0 += nt) {
         const int i = i0 + tid;
-        const int c = i < nq ? lcnt[i] : 0;
+        const int c = i < nq ? ld_ag(lcnt + i) : 0;
         over |= c > cap;
         int tot;
         const int ex = block_excl_scan(c, scan, &tot);
-        if (i < nq) { qoff[i] = run + ex; pick[i] = pick0[i]; }
+        if (i < nq) { qoff[i] = run + ex; pick[i] = ld_ag(pick0 + i); }
         run += tot;
     }
     if (over) flag[3] = 1;
@@ -473,12 +517,12 @@ __global__ __launch_bounds__(1024) void k_proj_resolve(int n, int nq, float nnra
         const int p = pick[i];
         if (p >= 0) atomicMin(&own[n + p], i);
         if (in_lds) {   // 8 loads in flight before their stores (one round trip per 8 entries)
-            const int c = lcnt[i], o = qoff[i];
+            const int c = ld_ag(lcnt + i), o = qoff[i];
             const uint64_t* L = lists + (size_t)i * cap;
             for (int j0 = 0; j0 < c; j0 += 8) {
                 uint64_t v[8];
 #pragma unroll
-                for (int u = 0; u < 8; u++) v[u] = j0 + u < c ? L[j0 + u] : 0ull;
+                for (int u = 0; u < 8; u++) v[u] = j0 + u < c ? ld_ag(L + j0 + u) : 0ull;
 #pragma unroll
                 for (int u = 0; u < 8; u++)
                     if (j0 + u < c) ent[o + j0 + u] = v[u];
@@ -497,11 +541,11 @@ __global__ __launch_bounds__(1024) void k_proj_resolve(int n, int nq, float nnra
         if (tid == 0) flag[(r + 1) % 3] = 0;
         int ch = 0;
         for (int i = tid; i < nq; i += nt) {
-            const int c = lcnt[i];
+            const int c = ld_ag(lcnt + i);
             const uint64_t* L = in_lds ? ent + qoff[i] : lists + (size_t)i * cap;
             Top2 t{256, INT_MAX, -1, 256, INT_MAX, -1};
             for (int j = 0; j < c; j++) {
-                const uint64_t e = L[j];
+                const uint64_t e = in_lds ? L[j] : ld_ag(L + j);
                 const uint32_t lo = (uint32_t)e;
                 const int d = (int)(e >> 32);
                 if (d == 256 || owner[(lo >> 4) & 0xFFFF] < i) continue;
@@ -561,6 +605,19 @@ __global__ __launch_bounds__(1024) void k_proj_resolve(int n, int nq, float nnra
         res[1] = 0;
         res[2] = r + 1;
     }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(1024) void k_proj_resolve(int n, int nq, float nnratio, int check_orientation, int cap,
+                                                       int ent_cap, const float* __restrict__ qangle,
+                                                       const orbhip_kp* __restrict__ kps,
+                                                       const uint64_t* __restrict__ lists,
+                                                       const int* __restrict__ lcnt, const int* __restrict__ pick0,
+                                                       int* __restrict__ pick, int* __restrict__ match,
+                                                       int* __restrict__ res) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char rsm_[];
+    resolve_body<MODE>(rsm_, n, nq, nnratio, check_orientation, cap, ent_cap, qangle, kps, lists, lcnt, pick0, pick,
+                       match, res);
 }
 
 // ---------------------------------------------------------------------------
@@ -1102,10 +1159,12 @@ struct ProjWorkspace {
     size_t dcap = 0;
     void* h = nullptr;
     void* hd = nullptr;   // h as the device addresses it (kernels write results there: no download)
+    int* arrive = nullptr;   // the one-launch search's arrival counter (0 between launches)
     size_t hcap = 0;
     int ahead = 4;   // rounds launched per host sync (adapts to the last search)
     int init_ahead = 6;   // the same for SearchForInitialization's rounds
     ~ProjWorkspace() {
+        if (arrive) (void)hipFree(arrive);
         if (d) (void)hipFree(d);
         if (h) (void)hipHostFree(h);
     }
@@ -1160,6 +1219,10 @@ ProjFrame make_frame(const orbhip_frame* F) {
 }
 
 int ensure(ProjWorkspace* ws, size_t total) {
+    if (!ws->arrive) {
+        PJOK(hipMalloc((void**)&ws->arrive, sizeof(int)));
+        PJOK(hipMemset(ws->arrive, 0, sizeof(int)));
+    }
     if (ws->dcap < total) {
         if (ws->d) (void)hipFree(ws->d);
         ws->d = nullptr;
@@ -1233,8 +1296,8 @@ hipError_t proj_lds_attr() {   // beyond the default 64 KiB of dynamic LDS
     static const hipError_t e[4] = {
         hipFuncSetAttribute((const void*)k_proj_resolve<0>, hipFuncAttributeMaxDynamicSharedMemorySize, kResolveLds),
         hipFuncSetAttribute((const void*)k_proj_resolve<1>, hipFuncAttributeMaxDynamicSharedMemorySize, kResolveLds),
-        hipFuncSetAttribute((const void*)k_proj_lists<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 16 * kProjMaxN),
-        hipFuncSetAttribute((const void*)k_proj_lists<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 16 * kProjMaxN)};
+        hipFuncSetAttribute((const void*)k_proj_lists<0>, hipFuncAttributeMaxDynamicSharedMemorySize, kResolveLds),
+        hipFuncSetAttribute((const void*)k_proj_lists<1>, hipFuncAttributeMaxDynamicSharedMemorySize, kResolveLds)};
     for (hipError_t x : e)
         if (x != hipSuccess) return x;
     return hipSuccess;
@@ -1243,6 +1306,11 @@ hipError_t proj_lds_attr() {   // beyond the default 64 KiB of dynamic LDS
 int resolve_ent_cap(int n, int nq) {
     const size_t head = ((size_t)(3 * n + nq) * 4 + 15) & ~size_t(15);
     return head >= kResolveLds ? 0 : (int)((kResolveLds - head) / 8);
+}
+// one launch (the list kernel's last work-group resolves) unless ORBHIP_PROJ_TWO=1 (read per call)
+bool proj_fused() {
+    const char* e = std::getenv("ORBHIP_PROJ_TWO");
+    return !(e && e[0] == '1');
 }
 int proj_cap() {
     const char* e = std::getenv("ORBHIP_PROJ_CAP");   // tests shrink it to force the round path
@@ -1304,14 +1372,18 @@ int proj_search_last(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_proj
     const uint8_t* dcl = F->claimed ? (const uint8_t*)(D + o_cl) : nullptr;
     int* hres = (int*)(H + o_out + ob.res);
     if (onepass) {
+        const bool fused = proj_fused();
+        const ResolveArgs ra{fused ? 1 : 0, check_orientation, resolve_ent_cap(n, nq), (const float*)(D + o_ang),
+                             (int*)(D + o_pick), (int*)(HD + o_out + ob.match), (int*)(HD + o_out + ob.res),
+                             ws->arrive};
         hipLaunchKernelGGL(k_proj_lists<0>, dim3((unsigned)((nq + kListWaves - 1) / kListWaves)), dim3(1024),
-                           16 * (size_t)n, st, f, nq, pl, PrepLocal{}, cap, 0.f, (const orbhip_kp*)(D + o_kps),
-                           (const uint8_t*)(D + o_kd), dcl, (const uint8_t*)(D + o_qd), (uint64_t*)(D + o_list),
-                           (int*)(D + o_lcnt), (int*)(D + o_pick0), nullptr, nullptr);
-        hipLaunchKernelGGL(k_proj_resolve<0>, dim3(1), dim3(1024), kResolveLds, st, n, nq, 0.f, check_orientation,
-                           cap, resolve_ent_cap(n, nq), (const float*)(D + o_ang), (const orbhip_kp*)(D + o_kps),
-                           (const uint64_t*)(D + o_list), (const int*)(D + o_lcnt), (const int*)(D + o_pick0),
-                           (int*)(D + o_pick), (int*)(HD + o_out + ob.match), (int*)(HD + o_out + ob.res));
+                           fused ? kResolveLds : 16 * (size_t)n, st, f, nq, pl, PrepLocal{}, cap, 0.f,
+                           (const orbhip_kp*)(D + o_kps), (const uint8_t*)(D + o_kd), dcl, (const uint8_t*)(D + o_qd),
+                           (uint64_t*)(D + o_list), (int*)(D + o_lcnt), (int*)(D + o_pick0), nullptr, nullptr, ra);
+        if (!fused)
+            hipLaunchKernelGGL(k_proj_resolve<0>, dim3(1), dim3(1024), kResolveLds, st, n, nq, 0.f, check_orientation,
+                               cap, ra.ent_cap, ra.qangle, (const orbhip_kp*)(D + o_kps), (const uint64_t*)(D + o_list),
+                               (const int*)(D + o_lcnt), (const int*)(D + o_pick0), ra.pick, ra.match, ra.res);
         PJOK(hipGetLastError());
         PJOK(hipStreamSynchronize(st));
         if (hres[1] == 0) {
@@ -1394,15 +1466,19 @@ int proj_search_local(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_loc
         std::memcpy(in_view, H + o_out + ob.iv, nq);
     };
     if (onepass) {
+        const bool fused = proj_fused();
+        const ResolveArgs ra{fused ? 1 : 0, 0, resolve_ent_cap(n, nq), nullptr, (int*)(D + o_pick),
+                             (int*)(HD + o_out + ob.match), (int*)(HD + o_out + ob.res), ws->arrive};
         hipLaunchKernelGGL(k_proj_lists<1>, dim3((unsigned)((nq + kListWaves - 1) / kListWaves)), dim3(1024),
-                           16 * (size_t)n, st, f, nq, PrepLast{}, pc, cap, nnratio, (const orbhip_kp*)(D + o_kps),
-                           (const uint8_t*)(D + o_kd), dcl, (const uint8_t*)(D + o_qd), (uint64_t*)(D + o_list),
-                           (int*)(D + o_lcnt), (int*)(D + o_pick0), (uint8_t*)(HD + o_out + ob.iv),
-                           (int*)(HD + o_out + ob.lvl));
-        hipLaunchKernelGGL(k_proj_resolve<1>, dim3(1), dim3(1024), kResolveLds, st, n, nq, nnratio, 0, cap,
-                           resolve_ent_cap(n, nq), (const float*)nullptr, (const orbhip_kp*)(D + o_kps),
-                           (const uint64_t*)(D + o_list), (const int*)(D + o_lcnt), (const int*)(D + o_pick0),
-                           (int*)(D + o_pick), (int*)(HD + o_out + ob.match), (int*)(HD + o_out + ob.res));
+                           fused ? kResolveLds : 16 * (size_t)n, st, f, nq, PrepLast{}, pc, cap, nnratio,
+                           (const orbhip_kp*)(D + o_kps), (const uint8_t*)(D + o_kd), dcl, (const uint8_t*)(D + o_qd),
+                           (uint64_t*)(D + o_list), (int*)(D + o_lcnt), (int*)(D + o_pick0),
+                           (uint8_t*)(HD + o_out + ob.iv), (int*)(HD + o_out + ob.lvl), ra);
+        if (!fused)
+            hipLaunchKernelGGL(k_proj_resolve<1>, dim3(1), dim3(1024), kResolveLds, st, n, nq, nnratio, 0, cap,
+                               ra.ent_cap, (const float*)nullptr, (const orbhip_kp*)(D + o_kps),
+                               (const uint64_t*)(D + o_list), (const int*)(D + o_lcnt), (const int*)(D + o_pick0),
+                               ra.pick, ra.match, ra.res);
         PJOK(hipGetLastError());
         PJOK(hipStreamSynchronize(st));
         if (hres[1] == 0) {

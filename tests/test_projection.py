@@ -14,9 +14,10 @@ from orb_slam3_ros2_amd.matcher import ProjFrame
 from orb_slam3_ros2_amd.synthetic import synthetic_projection_scene
 
 
-# the device forms: the two-launch list/resolve path (default), the list path overflowing into the
-# round kernels (list capacity 2), and the round kernels alone
-PROJ_MODES = {"lists": {}, "overflow": {"ORBHIP_PROJ_CAP": "2"}, "rounds": {"ORBHIP_PROJ_ROUNDS": "1"}}
+# the device forms: the one-launch list/resolve path (default), the same as two launches, the list
+# path overflowing into the round kernels (list capacity 2), and the round kernels alone
+PROJ_MODES = {"lists": {}, "two": {"ORBHIP_PROJ_TWO": "1"}, "overflow": {"ORBHIP_PROJ_CAP": "2"},
+              "rounds": {"ORBHIP_PROJ_ROUNDS": "1"}}
 
 
 @pytest.fixture(params=list(PROJ_MODES))
