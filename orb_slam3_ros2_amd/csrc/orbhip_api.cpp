@@ -74,10 +74,12 @@ static int cone_hi_threads() {
 }
 
 constexpr int kBandStart = 2;   // batches: k_resize for levels 1..2, k_resize_bands for the rest
-// row bands per frame of k_resize_bands: ORBHIP_RZ_BANDS (0: every level by k_resize), else 16
-static int rz_bands() {   // read per plan lookup (tests switch it)
+// row bands per frame of k_resize_bands: ORBHIP_RZ_BANDS (read per plan lookup), default 0 =
+// every level by k_resize. Opt-in: at C3 the band launch measured 400-1200 us for 8-64 bands
+// against the 95 us of the five k_resize launches it replaces (tools/c3_pyr_sweep.sh)
+static int rz_bands() {
     const char* e = std::getenv("ORBHIP_RZ_BANDS");
-    return e ? std::max(0, std::atoi(e)) : 16;
+    return e ? std::max(0, std::atoi(e)) : 0;
 }
 
 struct Plan {

@@ -46,17 +46,17 @@ def test_sizes_bit_exact(ext1000, oracle, w, h, seed):
                                                  (1001, 751, 2.5, 3, 34)])
 @pytest.mark.parametrize("hi", ["bands", "bands5", "resize", "cone"])
 def test_resize_cascade_bit_exact(oracle, monkeypatch, w, h, scale, nlev, seed, hi):
-    """The batch engine forced on single frames: k_resize for levels 1-2, then levels 3.. by
-    k_resize_bands (16 row bands per frame, the default; 5 bands), by k_resize alone
-    (ORBHIP_RZ_BANDS=0) or by the opt-in batch cone (ORBHIP_CONE_HI=1). Odd sizes take the edge
+    """The batch engine forced on single frames: k_resize for every level (the default), or
+    k_resize for levels 1-2 and then levels 3.. by the opt-in k_resize_bands (ORBHIP_RZ_BANDS=16
+    or 5 row bands per frame) or the opt-in batch cone (ORBHIP_CONE_HI=1). Odd sizes take the edge
     lanes, scale factors above 1.2 k_resize's per-row path (a 4-row group reads more than 6
     source rows), all bit-exact against the oracle's cv::resize restatement."""
     from orb_slam3_ros2_amd import ORBextractor
     monkeypatch.setenv("ORBHIP_NO_CONE", "1")
     if hi == "cone":
         monkeypatch.setenv("ORBHIP_CONE_HI", "1")
-    elif hi == "resize":
-        monkeypatch.setenv("ORBHIP_RZ_BANDS", "0")
+    elif hi == "bands":
+        monkeypatch.setenv("ORBHIP_RZ_BANDS", "16")
     elif hi == "bands5":
         monkeypatch.setenv("ORBHIP_RZ_BANDS", "5")
     ext = ORBextractor(1000, scale, nlev, 20, 7)
