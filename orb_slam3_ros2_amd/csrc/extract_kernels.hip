@@ -219,11 +219,12 @@ __global__ __launch_bounds__(256) void k_resize(const ExtractPlan* __restrict__ 
 // the step before; level s0 from k_resize), and writes them to the pyramid. A halo row is
 // computed by both neighbouring bands with identical bytes. Waves take (4-row group, 256-column
 // strip) tiles in turn; one workgroup barrier per level; no work-group waits for another.
-__global__ __launch_bounds__(1024) void k_resize_bands(const ExtractPlan* __restrict__ P, FrameBufs fb, int s0,
+__global__ __launch_bounds__(256) void k_resize_bands(const ExtractPlan* __restrict__ P, FrameBufs fb, int s0,
                                                        const int2* __restrict__ rows, const int* __restrict__ xofs,
                                                        const int* __restrict__ xalpha,
                                                        const int* __restrict__ yofs,
                                                        const int* __restrict__ ybeta) {
+    TR_BEGIN()
     const int band = blockIdx.x, f = blockIdx.y;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
     const int L = P->n_levels;
@@ -237,7 +238,9 @@ __global__ __launch_bounds__(1024) void k_resize_bands(const ExtractPlan* __rest
             if (dx0 < Dw) resize_tile(P, fb, f, l, rr.x + g * kRzRows, dx0, rr.y, xofs, xalpha, yofs, ybeta);
         }
         __syncthreads();   // the level's rows (this work-group's global stores) before the next level reads them
+        TR_PHASE(6, l)
     }
+    TR_END(6)
 }
 
 // quotient of i / d for 0 <= i < 2^16, d >= 1: the float reciprocal's error stays below the
@@ -1982,7 +1985,7 @@ void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs
 
 void launch_resize_bands(const ExtractPlan* dP, int nbands, const FrameBufs& fb, int B, int s0, const int2* rows,
                          const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st) {
-    ORBHIP_LAUNCH(k_resize_bands, dim3(nbands, B), dim3(1024), 0, st, dP, fb, s0, rows, xofs, xalpha, yofs, ybeta);
+    ORBHIP_LAUNCH(k_resize_bands, dim3(nbands, B), dim3(256), 0, st, dP, fb, s0, rows, xofs, xalpha, yofs, ybeta);
 }
 
 void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameBufs& fb, int B, const ConeRect* rects,
