@@ -18,6 +18,7 @@ constexpr int kDagMaxHelpers = 255;   // helper workgroups (+ the chain workgrou
 // workgroup, in the order the workgroup runs them (dependency key order, deadlock-free)
 struct DagPlan {
     int NT = 0, G = 0;
+    int pb = 0;               // backward substitution over the helpers (long rows) or in the chain
     std::vector<int> toff;    // G + 1 offsets into tasks
     std::vector<int> tasks;
 };
@@ -36,6 +37,7 @@ struct DagDev {
     const int* toff;     // plan, on the device
     const int* tasks;
     int G;
+    int pb;              // DagPlan::pb
 };
 
 // S (n x n row-major, lower triangle read, never written), row_first (ceil(n/32): first 32-col

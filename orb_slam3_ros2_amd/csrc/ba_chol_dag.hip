@@ -67,6 +67,7 @@ struct DagK {
     const int* gate;
     unsigned long long* dbg;
     int n, NT, G;
+    int pb;       // backward over the helpers (dag_helper_backward) or in the chain alone
     int hsleep;   // helpers' poll back-off (units of s_sleep 1)
 };
 
@@ -201,8 +202,8 @@ __device__ int wave_wait_prefix(const int* fa, const int* fb, const int* fc, int
 }
 
 struct Lay {   // offsets (doubles) into the DAG buffer, flags
-    int oL, oP, oLi, oY, oR;
-    int *ctl, *fL, *fP0, *fP1, *fP2, *fCh;
+    int oL, oP, oLi, oY, oR, oX, oS;
+    int *ctl, *fL, *fP0, *fP1, *fP2, *fCh, *fX, *fS;
     __device__ Lay(const DagK& a) {
         const int NT = a.NT;
         oL = 0;
@@ -210,14 +211,73 @@ struct Lay {   // offsets (doubles) into the DAG buffer, flags
         oLi = oP + 3 * NT * kTD;
         oY = oLi + NT * kTD;
         oR = oY + NT * kT;
+        oX = oR + NT * kT;   // backward: x_R published by the chain
+        oS = oX + NT * kT;   // backward: the helpers' sums s_j = y_j - sum_{R >= j+2} L(R, j)^T x_R
         ctl = a.ints;
         fL = ctl + 4;
         fP0 = fL + NT * NT;
         fP1 = fP0 + NT;
         fP2 = fP1 + NT;
         fCh = fP2 + NT;
+        fX = fCh + NT;
+        fS = fX + NT;
     }
 };
+
+// ---------------------------------------------------------------------------------------------
+// helper backward: helper h owns the columns j = h, h + G, ... <= NT - 3, spread over its 4
+// waves. A wave accumulates s_j = y_j - sum_{R >= j+2} L(R, j)^T x_R (in LDS) as the chain
+// publishes x_R (sc1 data, flag fX[R]), from R = NT - 1 down, and publishes s_j (oS, fS[j]) once
+// R = j + 2 is in; the chain adds the sub-diagonal term L(j+1, j)^T x_{j+1} itself. L is final
+// once x_{NT-1} exists (the chain's forward is over), so a wave loads its tiles without flags.
+// An aborted solve (ctl[2]) ends every wait.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void tile_lt_x(const double4_t* t, const double* x, double (&out)[2][4]);
+__device__ void dag_helper_backward(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs, int epoch, double* lds,
+                                    int h) {
+    const int NT = a.NT, G = a.G;
+    const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63, cc = lane & 15, rg = lane >> 4;
+    if (G <= 0 || !a.pb) return;
+    // this wave's columns: j = h + G * (wid + 4 i)
+    const int j_first = h + G * wid;
+    if (j_first > NT - 3) return;
+    double* acc = lds;                  // NT x 32 (a column's running sum, owned by one wave)
+    double* xw = lds + 4096 + 64 * wid; // this wave's copy of x_R
+    for (int R = NT - 1; R >= j_first + 2; R--) {
+        if (!wave_wait_all(lane == 0 ? L.fX + R : nullptr, epoch, L.ctl)) return;
+        if (R == NT - 1) {   // the forward is over (x_{NT-1} exists): every y_j is published
+            for (int j = j_first; j <= NT - 3; j += 4 * G)
+                if (lane < kT) acc[j * kT + lane] = ld_sc1(a.buf + L.oY + j * kT + lane);
+        }
+        if (lane < kT) xw[lane] = ld_sc1(a.buf + L.oX + R * kT + lane);
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const int rfR = a.rf[R];
+        for (int j = j_first; j <= R - 2; j += 4 * G) {
+            if (j >= rfR) {
+                double4_t tl[4];
+#pragma unroll
+                for (int qd = 0; qd < 4; qd++) tl[qd] = qload(rs, L.oL + (R * NT + j) * kTD + qd * 256);
+                double t[2][4];
+                tile_lt_x(tl, xw, t);
+                if (cc == 0) {
+#pragma unroll
+                    for (int b = 0; b < 2; b++)
+#pragma unroll
+                        for (int q = 0; q < 4; q++) acc[j * kT + 16 * b + rg + 4 * q] -= t[b][q];
+                }
+            }
+            if (j == R - 2) {   // s_j complete: publish
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (lane < kT) st_sc1(a.buf + L.oS + j * kT + lane, acc[j * kT + lane]);
+                drain_stores();
+                if (lane == 0) st_flag(L.fS + j, epoch);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
 
 // ---------------------------------------------------------------------------------------------
 // helper workgroup: its tasks in order
@@ -304,6 +364,7 @@ __device__ void dag_helper(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t r
         __syncthreads();
         if (tid == 0) st_flag(target, epoch);
     }
+    dag_helper_backward(a, L, rs, epoch, lds, h);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -732,6 +793,59 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     // ranges): wave 0 tile (R, R-1) and Linv_{R-1}; waves 1..3 the first kPf tiles of their share of
     // row R, longer rows stream the rest a tile at a time. Both roles pass the same barriers.
     constexpr int kPf = 3;
+    if (a.G > 0 && a.pb) {
+        // with helpers: they accumulate s_j for j <= NT-3 (dag_helper_backward) from the x_R this
+        // wave publishes; wave 0 alone walks the chain: x_{R-1} = Linv_{R-1}^T (s_{R-1} -
+        // L(R, R-1)^T x_R), s_{R-1} from the helpers (fS) or, for R-1 = NT-2, y itself
+        if (!aborted && wid == 0) {
+            auto publish = [&](int k) {   // x_k to oX (sc1), then its flag
+                wave_lds_sync();
+                if (lane < kT) st_sc1(a.buf + L.oX + k * kT + lane, xs[k * kT + lane]);
+                drain_stores();
+                if (lane == 0) st_flag(L.fX + k, epoch);
+            };
+            if (lane < kT) rvec[lane] = ys[(NT - 1) * kT + lane];
+            wave_lds_sync();
+            apply_lt(NT - 1);
+            publish(NT - 1);
+            double4_t st[4], li[4];
+            for (int R = NT - 1; R >= 1 && !aborted; R--) {
+#pragma unroll
+                for (int qd = 0; qd < 4; qd++) {
+                    st[qd] = qload(rs, L.oL + (R * NT + R - 1) * kTD + qd * 256);
+                    li[qd] = qload(rs, L.oLi + (R - 1) * kTD + qd * 256);
+                }
+                double sv = 0.0;
+                if (R - 1 <= NT - 3) {
+                    if (!wave_wait_all(lane == 0 ? L.fS + R - 1 : nullptr, epoch, L.ctl)) {
+                        aborted = true;
+                        break;
+                    }
+                    if (lane < kT) sv = ld_sc1(a.buf + L.oS + (R - 1) * kT + lane);
+                } else if (lane < kT) {
+                    sv = ys[(R - 1) * kT + lane];
+                }
+                if (lane < kT) rvec[lane] = sv;
+#pragma unroll
+                for (int qd = 0; qd < 4; qd++) sq(Lin + qd * 256, li[qd]);
+                wave_lds_sync();
+                double t[2][4];
+                tile_lt_x(st, xs + R * kT, t);
+                if (cc == 0) {
+#pragma unroll
+                    for (int b = 0; b < 2; b++)
+#pragma unroll
+                        for (int q = 0; q < 4; q++) rvec[16 * b + rg + 4 * q] -= t[b][q];
+                }
+                wave_lds_sync();
+                apply_lt(R - 1);
+                if (R - 1 >= 2) publish(R - 1);
+            }
+            if (aborted && lane == 0) word[5] = 0;
+        }
+        __syncthreads();
+        if (!word[5]) aborted = true;
+    } else {   // short rows (or no helpers): the chain work-group alone
     if (!aborted && wid != 0) {
         // every tile (R, j), j <= R-2, rows 2.. (16 rows of this wave per round: up to 32 flag
         // loads in flight per lane)
@@ -852,6 +966,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             if (R - 1 >= 1) step(std::integral_constant<int, 1>{}, R - 1);
         }
     }
+    }
     if (wid == 0 && lane == 0) word[8] = (ok && !aborted) ? 1 : 0;
     __syncthreads();
     const bool good = word[8] != 0;
@@ -873,7 +988,7 @@ __global__ __launch_bounds__(256) void k_chol_dag(DagK a) {
     const Lay L(a);
     // epoch of this solve: the counter the last workgroup of the previous solve advanced
     const int epoch = ld_flag(L.ctl) + 1;
-    const size_t bytes = ((size_t)a.NT * a.NT + 4 * (size_t)a.NT) * kTD * 8 + (size_t)a.NT * 64 * 8;
+    const size_t bytes = ((size_t)a.NT * a.NT + 4 * (size_t)a.NT) * kTD * 8 + (size_t)a.NT * 4 * kT * 8;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.buf, 0, (int)bytes, 0x00020000);
     if (blockIdx.x == 0) dag_chain(a, L, rs, epoch, lds);
     else dag_helper(a, L, rs, epoch, lds);
@@ -910,11 +1025,11 @@ int dag_max_helpers() {
 
 size_t dag_doubles(int n) {
     const size_t NT = (n + kT - 1) / kT;
-    return (NT * NT + 4 * NT) * kTD + NT * 64;
+    return (NT * NT + 4 * NT) * kTD + NT * 4 * kT;
 }
 size_t dag_ints(int n) {
     const size_t NT = (n + kT - 1) / kT;
-    return (4 + NT * NT + 4 * NT + 3) & ~size_t(3);
+    return (4 + NT * NT + 6 * NT + 3) & ~size_t(3);
 }
 
 void dag_plan(const int* rf, int n, int max_helpers, DagPlan& p) {
@@ -943,6 +1058,16 @@ void dag_plan(const int* rf, int n, int max_helpers, DagPlan& p) {
     });
     const int G = std::min<int>(std::max(1, max_helpers), (int)ts.size());
     p.G = G;
+    // backward substitution: over the helpers when the rows are long (the chain's own waves would
+    // stream every tile of L through one CU: dense n = 2394 1.24 -> 0.69 ms), in the chain when
+    // they are short (a band: the helpers' hand-off per step costs more than the tiles; the C5
+    // loop and C4 systems). ORBHIP_DAG_PBACK=0/1 forces it.
+    {
+        long long off = 0;   // tiles the backward reads beyond the sub-diagonal
+        for (int R = 0; R < NT; R++) off += std::max(0, R - 1 - rf[R]);
+        const char* e = std::getenv("ORBHIP_DAG_PBACK");
+        p.pb = e ? (e[0] == '1' ? 1 : 0) : (off >= 10LL * NT ? 1 : 0);
+    }
     p.toff.assign(G + 1, 0);
     p.tasks.resize(ts.size());
     std::vector<int> cnt(G, 0);
@@ -965,7 +1090,7 @@ hipError_t chol_dag_solve(const double* S, int n, const int* row_first, const do
     DagK a;
     a.S = S; a.bs = bs; a.x = x; a.flag = flag; a.rf = row_first;
     a.buf = d.buf; a.ints = d.ints; a.toff = d.toff; a.tasks = d.tasks; a.gate = gate; a.dbg = dbg;
-    a.n = n; a.NT = (n + kT - 1) / kT; a.G = d.G;
+    a.n = n; a.NT = (n + kT - 1) / kT; a.G = d.G; a.pb = d.pb;
     static const int hs = std::getenv("ORBHIP_DAG_SLEEP") ? std::atoi(std::getenv("ORBHIP_DAG_SLEEP")) : 6;
     a.hsleep = hs;
     hipLaunchKernelGGL(k_chol_dag, dim3((unsigned)(d.G + 1)), dim3(256), dag_lds_bytes(a.NT), st, a);
@@ -1014,7 +1139,7 @@ int chol_dag_test(const double* A, const double* b, double* x, int n, int reps, 
         if (!plan.tasks.empty())
             ok(hipMemcpy(dtasks, plan.tasks.data(), sizeof(int) * plan.tasks.size(), hipMemcpyHostToDevice));
         if (ddbg) ok(hipMemset(ddbg, 0, sizeof(unsigned long long) * kDbgWords));
-        const DagDev d{dbuf, dints, dtoff, dtasks, plan.G};
+        const DagDev d{dbuf, dints, dtoff, dtasks, plan.G, plan.pb};
         ok(chol_dag_solve(dS, n, drf, db, dx, dflag, d, nullptr, nullptr, nullptr));   // warm-up
         ok(hipDeviceSynchronize());
         hipEvent_t e0, e1;

@@ -1430,7 +1430,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     double* hd = ws->hdbl.p;
     int* hi = ws->hint.p;
     BaArgs* ha = ws->hargs.p;
-    std::vector<DagDev> dd(B, DagDev{nullptr, nullptr, nullptr, nullptr, 0});
+    std::vector<DagDev> dd(B, DagDev{nullptr, nullptr, nullptr, nullptr, 0, 0});
     parallel_for(B, nth, [&](int b) {
         const Prep& p = pp[b];
         const orbhip_ba_problem* pr = probs[b];
@@ -1486,6 +1486,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 q += p.dag_task_cap;
             }
             dd[b].G = p.dag.G;
+            dd[b].pb = p.dag.pb;
         }
         a.nblk = p.nblk;
         a.P = p.P; a.M = p.M; a.E = p.E; a.np = p.np; a.n = p.n;
@@ -1548,6 +1549,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 BAOK(hipMemcpy(const_cast<int*>(dd[0].tasks), dp.tasks.data(), dp.tasks.size() * sizeof(int),
                                hipMemcpyHostToDevice));
             dd[0].G = dp.G;
+            dd[0].pb = dp.pb;
         }
         if (n > kCholSmallN && !std::getenv("ORBHIP_SHARD_FULL_S")) {
         std::vector<long long> off(nt + 1, 0);

@@ -200,17 +200,26 @@ def test_blocked_cholesky_solves_spd(n, shape):
     assert np.abs(x - ref).max() <= 1e-10 * np.abs(ref).max()
 
 
-@pytest.mark.parametrize("n,shape,helpers", [(31, "dense", 0), (64, "dense", 0), (100, "dense", 3), (294, "dense", 0),
-                                             (294, "dense", 1), (600, "band", 0), (1201, "dense", 0),
-                                             (2394, "loop", 0), (2394, "loop", 7)])
-def test_dag_cholesky_solves_spd(n, shape, helpers):
+@pytest.mark.parametrize("n,shape,helpers,pback", [(31, "dense", 0, None), (64, "dense", 0, None),
+                                                   (100, "dense", 3, None), (294, "dense", 0, None),
+                                                   (294, "dense", 1, None), (294, "dense", 0, "1"),
+                                                   (294, "dense", 1, "1"), (600, "band", 0, None),
+                                                   (600, "band", 0, "1"), (1201, "dense", 0, None),
+                                                   (1201, "dense", 5, None), (1201, "dense", 0, "0"),
+                                                   (2394, "loop", 0, None), (2394, "loop", 7, None),
+                                                   (2394, "loop", 0, "1"), (2394, "dense", 0, None)])
+def test_dag_cholesky_solves_spd(n, shape, helpers, pback, monkeypatch):
     """The persistent tiled-DAG solver (ba_chol_dag.hip: one launch, a chain workgroup on the
     diagonal path, helper workgroups on the off-diagonal tiles, flag hand-offs) on random SPD
     systems: dense, banded, and C5's band plus loop-closure corner, with the full helper grid and
-    with few helpers (each helper then runs many tasks in dependency-key order). Against numpy's
-    fp64 solve; three solves in a row reuse the flags through the per-solve epoch."""
+    with few helpers (each helper then runs many tasks in dependency-key order), the backward
+    substitution in the chain or over the helpers (ORBHIP_DAG_PBACK forces either; by default long
+    rows go to the helpers). Against numpy's fp64 solve; three solves in a row reuse the flags
+    through the per-solve epoch."""
     import ctypes
     from orb_slam3_ros2_amd._lib import lib
+    if pback is not None:
+        monkeypatch.setenv("ORBHIP_DAG_PBACK", pback)
     L = lib()
     rng = np.random.default_rng(n + helpers)
     if shape == "dense":
