@@ -1490,12 +1490,14 @@ int orbhip_test_trace(int on, unsigned long long* out) {
         HIPOK(hipMemset(buf, 0, n * sizeof(unsigned long long)));
         trace_set_extract(buf);
         trace_set_match(buf);
+        trace_set_proj(buf);
         return ORBHIP_OK;
     }
     HIPOK(hipDeviceSynchronize());
     if (buf && out) HIPOK(hipMemcpy(out, buf, n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     trace_set_extract(nullptr);
     trace_set_match(nullptr);
+    trace_set_proj(nullptr);
     return ORBHIP_OK;
 }
 

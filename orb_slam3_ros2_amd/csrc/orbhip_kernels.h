@@ -143,6 +143,7 @@ constexpr int kTraceStride = 16384;   // u64 per kernel id in the timing trace (
 constexpr int kTraceKernels = 8;
 void trace_set_extract(unsigned long long* p);
 void trace_set_match(unsigned long long* p);
+void trace_set_proj(unsigned long long* p);
 void launch_sincos_probe(const float* x, float* c, float* s, int64_t n, hipStream_t st);
 void launch_sincos_sweep(uint32_t lo_bits, uint32_t hi_bits, const float* ref_c, const float* ref_s,
                          unsigned long long* mismatches, hipStream_t st);

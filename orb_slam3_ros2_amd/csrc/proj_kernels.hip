@@ -29,9 +29,12 @@
 
 #include "../../include/orbhip.h"
 #include "orbhip_device.h"
+#include "orbhip_kernels.h"
 #include "proj.h"
 
 namespace orbhip {
+
+ORBHIP_TRACE_UNIT(proj)   // kernel id 7: k_proj_lists (phases 1-3), its resolving work-group (16-20)
 
 namespace {
 
@@ -310,7 +313,15 @@ __global__ __launch_bounds__(1024) void k_proj_finish(int nq, int check_orientat
 constexpr int kProjCap = 128;     // list entries per query
 constexpr int kProjMaxN = 8192;   // frame keypoints: staged in LDS (16 B each), 3 owner tables of n ints
 constexpr int kProjMaxQ = 8192;   // queries: list offsets in LDS
-constexpr int kListWaves = 16;    // queries per k_proj_lists work-group (one per wave)
+// queries per k_proj_lists work-group (one per wave of its first kListQ waves; the other waves
+// only help stage the frame): one query wave per SIMD, so the scans do not share issue slots
+constexpr int kListQ = 4;
+// resolve_body's LDS head: 3 owner tables (n), list offsets (nq + 1), picks (nq); the lists follow
+__host__ __device__ inline size_t resolve_head_bytes(int n, int nq) {
+    return ((size_t)(3 * n + 2 * nq + 1) * 4 + 15) & ~size_t(15);
+}
+constexpr int kRectCap = 512;   // keypoints in a query's cell rectangle listed per wave (more: every keypoint)
+constexpr size_t kListIdxBytes = kListQ * (kProjCap + kRectCap) * 2;   // k_proj_lists' per-wave index lists (LDS)
 
 typedef __attribute__((address_space(1))) int pj_gint;
 typedef __attribute__((address_space(1))) unsigned long long pj_gull;
@@ -340,7 +351,6 @@ __device__ __forceinline__ int proj_decide(const Top2& t, int mode, float nnrati
 struct ResolveArgs {
     int fuse, check_orientation, ent_cap;
     const float* qangle;
-    int* pick;
     int* match;
     int* res;
     int* arrive;
@@ -349,8 +359,8 @@ template <int MODE>
 __device__ void resolve_body(unsigned char* rsm, int n, int nq, float nnratio, int check_orientation, int cap,
                              int ent_cap, const float* __restrict__ qangle, const orbhip_kp* __restrict__ kps,
                              const uint64_t* __restrict__ lists, const int* __restrict__ lcnt,
-                             const int* __restrict__ pick0, int* __restrict__ pick, int* __restrict__ match,
-                             int* __restrict__ res);
+                             const int* __restrict__ pick0, int* __restrict__ match, int* __restrict__ res,
+                             unsigned long long* tr = nullptr);
 
 // the frame's keypoints are staged once per work-group in LDS as (x, y, cell << 16 | claimed << 8 |
 // octave, 0): PosInGrid computed as k_proj_cells does, a 16-byte read per lane and keypoint. The
@@ -368,46 +378,53 @@ __global__ __launch_bounds__(1024) void k_proj_lists(ProjFrame f, int nq, PrepLa
                                                      int* __restrict__ pick0, uint8_t* __restrict__ in_view,
                                                      int* __restrict__ level, ResolveArgs ra) {
     extern __shared__ uint4 kl[];
-    const int n = f.n;
-    const int i = blockIdx.x * kListWaves + (threadIdx.x >> 6);
+    TR_BEGIN()
+    const int n = f.n, nt = blockDim.x;
+    const int w = threadIdx.x >> 6;
+    const int i = w < kListQ ? blockIdx.x * kListQ + w : nq;   // nq: no query
     const int lane = threadIdx.x & 63;
+    // LDS (list_lds_bytes): kl[n] | kc[n256] cells (u16, 0xFFFF past n) | per-wave index lists
+    const int n256 = (n + 255) & ~255;
+    uint16_t* kc = (uint16_t*)(kl + n);
+    uint16_t* wl = kc + n256 + min(w, kListQ - 1) * kProjCap;
+    uint16_t* wr = kc + n256 + kListQ * kProjCap + min(w, kListQ - 1) * kRectCap;
     Query Q{0, 0, 0, 0, 0, 0};
     uint4 qa{0u, 0u, 0u, 0u}, qb{0u, 0u, 0u, 0u};
+    uint8_t iv = 0;
+    int lvl = 0;
     if (i < nq) {
-        if constexpr (MODE == 0) {
-            Q = prep_last(f, pl, i);
-        } else {
-            uint8_t iv;
-            int lvl;
-            Q = prep_local(f, pc, i, &iv, &lvl);
-            if (lane == 0) { in_view[i] = iv; level[i] = lvl; }
-        }
+        if constexpr (MODE == 0) Q = prep_last(f, pl, i);
+        else Q = prep_local(f, pc, i, &iv, &lvl);
         const uint4* qd4 = (const uint4*)(qdesc + 32 * (size_t)i);
         qa = qd4[0];
         qb = qd4[1];
     }
-    // two keypoints per thread in flight (1250 keypoints: one round trip)
-    for (int k0 = threadIdx.x; k0 < n; k0 += 2 * blockDim.x) {
+    // staging: two keypoints per thread with their loads in flight together (1250 keypoints: one
+    // round trip); the cell of each keypoint also into kc
+    for (int k0 = threadIdx.x; k0 < n; k0 += 2 * nt) {
         orbhip_kp kp[2];
         uint32_t cl[2];
 #pragma unroll
         for (int u = 0; u < 2; u++) {
-            const int k = min(k0 + u * (int)blockDim.x, n - 1);
+            const int k = min(k0 + u * nt, n - 1);
             kp[u] = kps[k];
             cl[u] = (claimed && claimed[k]) ? 1u : 0u;
         }
 #pragma unroll
         for (int u = 0; u < 2; u++) {
-            const int k = k0 + u * (int)blockDim.x;
+            const int k = k0 + u * nt;
             if (k >= n) break;
             const int px = (int)roundf((kp[u].x - f.minx) * f.invw);
             const int py = (int)roundf((kp[u].y - f.miny) * f.invh);
             const int c = (px < 0 || px >= kGridCols || py < 0 || py >= kGridRows) ? 0xFFFF : px * kGridRows + py;
             kl[k] = uint4{__float_as_uint(kp[u].x), __float_as_uint(kp[u].y), ((uint32_t)c << 16) | (cl[u] << 8) |
                           (uint32_t)(kp[u].octave & 0xFF), 0u};
+            kc[k] = (uint16_t)c;
         }
     }
+    for (int k = n + threadIdx.x; k < n256; k += nt) kc[k] = 0xFFFF;
     __syncthreads();
+    TR_PHASE(7, 1)
     int cnt = 0;
     Top2 t{256, INT_MAX, -1, 256, INT_MAX, -1};
     if (i < nq && Q.valid) {
@@ -418,33 +435,83 @@ __global__ __launch_bounds__(1024) void k_proj_lists(ProjFrame f, int nq, PrepLa
         const bool any = nMinCellX < kGridCols && nMaxCellX >= 0 && nMinCellY < kGridRows && nMaxCellY >= 0;
         const bool bCheckLevels = (Q.minL > 0) || (Q.maxL >= 0);
         uint64_t* out = lists + (size_t)i * cap;
-        for (int k0 = 0; any && k0 < n; k0 += 64) {
-            const int k = k0 + lane;
+        // pass 1, LDS only: the indices of the keypoints passing the window tests into the wave's
+        // slice of the index buffer (the first `cap`; the count goes on). Four keypoints per lane
+        // and step: their cells are one 8-byte read, and only the few inside the cell rectangle
+        // read their 16-byte record for the level / radius / claimed tests
+        const uint64_t* kc8 = (const uint64_t*)kc;
+        const uint64_t lt = (1ull << lane) - 1ull;
+        TR_PHASE(7, 5)
+        auto in_rect = [&](int c) {
+            const int px = c / kGridRows, py = c - px * kGridRows;   // c = 0xFFFF: px = 1365, out
+            return px >= nMinCellX && px <= nMaxCellX && py >= nMinCellY && py <= nMaxCellY;
+        };
+        // 1a: the cell rectangle alone, four cells per lane from one 8-byte read (short code: this
+        // runs once per wave, from a cold instruction cache)
+        int nr = 0;
+        for (int s0 = 0; any && s0 < n; s0 += 256) {
+            const uint64_t v = kc8[(s0 >> 2) + lane];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const bool r = in_rect((int)((v >> (16 * u)) & 0xFFFF));
+                const uint64_t m = __ballot(r);
+                const int pos = nr + __popcll(m & lt);
+                if (r && pos < kRectCap) wr[pos] = (uint16_t)(s0 + 4 * lane + u);
+                nr += __popcll(m);
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        // 1b: the level / radius / claimed tests on the rectangle's keypoints (every keypoint when
+        // the rectangle held more than kRectCap), compacted into wl
+        const bool all = nr > kRectCap;
+        const int nb = all ? n : nr;
+        for (int j0 = 0; any && j0 < nb; j0 += 64) {
+            const int j = j0 + lane;
             bool ok = false;
-            uint32_t key = 0, oct = 0;
-            if (k < n) {
+            int k = 0;
+            if (j < nb) {
+                k = all ? j : (int)wr[j];
                 const uint4 e = kl[k];
-                const int c = (int)(e.z >> 16);
-                const int px = c / kGridRows, py = c - px * kGridRows;   // c = 0xFFFF: px = 1365, out
-                oct = e.z & 0xFF;
+                const uint32_t oct = e.z & 0xFF;
                 const float x = __uint_as_float(e.x), y = __uint_as_float(e.y);
-                ok = px >= nMinCellX && px <= nMaxCellX && py >= nMinCellY && py <= nMaxCellY;
+                ok = !all || in_rect((int)(e.z >> 16));
                 if (ok && bCheckLevels) ok = (int)oct >= Q.minL && !(Q.maxL >= 0 && (int)oct > Q.maxL);
                 ok = ok && fabsf(x - Q.u) < Q.r && fabsf(y - Q.v) < Q.r && !((e.z >> 8) & 1u);
-                key = ((uint32_t)c << 16) | (uint32_t)k;
             }
             const uint64_t m = __ballot(ok);
-            if (ok) {
-                const uint4* kd4 = (const uint4*)(kdesc + 32 * (size_t)k);
-                const uint4 ka = kd4[0], kb = kd4[1];
-                const int d = __popc(qa.x ^ ka.x) + __popc(qa.y ^ ka.y) + __popc(qa.z ^ ka.z) +
-                              __popc(qa.w ^ ka.w) + __popc(qb.x ^ kb.x) + __popc(qb.y ^ kb.y) +
-                              __popc(qb.z ^ kb.z) + __popc(qb.w ^ kb.w);
-                const int pos = cnt + __popcll(m & ((1ull << lane) - 1ull));
-                if (pos < cap) st_ag(out + pos, ((uint64_t)d << 32) | (uint64_t)((key << 4) | (oct & 15u)));
-                if (d != 256) top2_add(t, d, (int)key, (int)(oct & 15u));
-            }
+            const int pos = cnt + __popcll(m & lt);
+            if (ok && pos < cap) wl[pos] = (uint16_t)k;
             cnt += __popcll(m);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        TR_PHASE(7, 2)
+        // pass 2: the descriptor loads of every listed keypoint in flight at once (one round trip
+        // instead of one per 64-keypoint step that had a passing lane)
+        const int nl = min(cnt, cap);
+        int kk[kProjCap / 64];
+        uint4 ka[kProjCap / 64], kb[kProjCap / 64];
+#pragma unroll
+        for (int u = 0; u < kProjCap / 64; u++) {
+            const int j = lane + 64 * u;
+            kk[u] = j < nl ? (int)wl[j] : -1;
+            if (kk[u] >= 0) {
+                const uint4* kd4 = (const uint4*)(kdesc + 32 * (size_t)kk[u]);
+                ka[u] = kd4[0];
+                kb[u] = kd4[1];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kProjCap / 64; u++) {
+            if (kk[u] < 0) continue;
+            const int k = kk[u];
+            const uint32_t z = kl[k].z, oct = z & 0xFF, key = ((z >> 16) << 16) | (uint32_t)k;
+            const int d = __popc(qa.x ^ ka[u].x) + __popc(qa.y ^ ka[u].y) + __popc(qa.z ^ ka[u].z) +
+                          __popc(qa.w ^ ka[u].w) + __popc(qb.x ^ kb[u].x) + __popc(qb.y ^ kb[u].y) +
+                          __popc(qb.z ^ kb[u].z) + __popc(qb.w ^ kb[u].w);
+            st_ag(out + lane + 64 * u, ((uint64_t)d << 32) | (uint64_t)((key << 4) | (oct & 15u)));
+            if (d != 256) top2_add(t, d, (int)key, (int)(oct & 15u));
         }
     }
 #pragma unroll
@@ -458,7 +525,14 @@ __global__ __launch_bounds__(1024) void k_proj_lists(ProjFrame f, int nq, PrepLa
         st_ag(lcnt + i, cnt);
         st_ag(pick0 + i, proj_decide(t, MODE, nnratio));
     }
-    if (!ra.fuse) return;   // uniform
+    TR_PHASE(7, 3)
+    // the in_view / level outputs live in host memory: stored after the arrival's vmcnt drain (and
+    // after the resolve in the resolving work-group, whose barriers drain stores), not before it
+    auto host_outputs = [&]() {
+        if constexpr (MODE == 1)
+            if (lane == 0 && i < nq) { in_view[i] = iv; level[i] = lvl; }
+    };
+    if (!ra.fuse) { host_outputs(); TR_END(7) return; }   // uniform
     // one launch: every wave's list stores drained, then the last work-group to arrive resolves
     __shared__ int lastf;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -469,9 +543,13 @@ __global__ __launch_bounds__(1024) void k_proj_lists(ProjFrame f, int nq, PrepLa
         if (lastf) __hip_atomic_store((pj_gint*)ra.arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
+    TR_PHASE(7, 4)
     if (lastf)
         resolve_body<MODE>((unsigned char*)kl, n, nq, nnratio, ra.check_orientation, cap, ra.ent_cap, ra.qangle, kps,
-                           lists, lcnt, pick0, ra.pick, ra.match, ra.res);
+                           lists, lcnt, pick0, ra.match, ra.res,
+                           tr_buf ? tr_buf + 7 * kTraceStride + 8192 + 16 : nullptr);
+    host_outputs();
+    TR_END(7)
 }
 
 // res[0] = matches, res[1] = status (1: a list overflowed, nothing else written), res[2] = rounds.
@@ -483,11 +561,21 @@ template <int MODE>
 __device__ void resolve_body(unsigned char* rsm, int n, int nq, float nnratio, int check_orientation, int cap,
                              int ent_cap, const float* __restrict__ qangle, const orbhip_kp* __restrict__ kps,
                              const uint64_t* __restrict__ lists, const int* __restrict__ lcnt,
-                             const int* __restrict__ pick0, int* __restrict__ pick, int* __restrict__ match,
-                             int* __restrict__ res) {
+                             const int* __restrict__ pick0, int* __restrict__ match, int* __restrict__ res,
+                             unsigned long long* tr) {
+    // tr (diagnostics): s_memtime cycles of the resolve's phases, written by thread 0
+    unsigned long long tr_p = tr && threadIdx.x == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
+    auto mark = [&](int ph) {
+        if (tr && threadIdx.x == 0) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            tr[ph] = t - tr_p;
+            tr_p = t;
+        }
+    };
     int* own = (int*)rsm;                        // 3 x n
-    int* qoff = own + 3 * n;                     // nq
-    uint64_t* ent = (uint64_t*)(rsm + (((size_t)(3 * n + nq) * 4 + 15) & ~size_t(15)));
+    int* qoff = own + 3 * n;                     // nq + 1: list i = entries [qoff[i], qoff[i + 1])
+    int* pk = qoff + nq + 1;                     // nq: the current picks
+    uint64_t* ent = (uint64_t*)(rsm + resolve_head_bytes(n, nq));
     __shared__ int flag[4], hist[32], keep[3], cnt, scan[16];
     const int tid = threadIdx.x, nt = blockDim.x;
     if (tid < 4) flag[tid] = 0;
@@ -499,14 +587,17 @@ __device__ void resolve_body(unsigned char* rsm, int n, int nq, float nnratio, i
     for (int i0 = 0; i0 < nq; i0 += nt) {
         const int i = i0 + tid;
         const int c = i < nq ? ld_ag(lcnt + i) : 0;
+        const int p0 = i < nq ? ld_ag(pick0 + i) : 0;
         over |= c > cap;
         int tot;
         const int ex = block_excl_scan(c, scan, &tot);
-        if (i < nq) { qoff[i] = run + ex; pick[i] = ld_ag(pick0 + i); }
+        if (i < nq) { qoff[i] = run + ex; pk[i] = p0; }
         run += tot;
     }
+    if (tid == 0) qoff[nq] = run;
     if (over) flag[3] = 1;
     __syncthreads();
+    mark(0);
     if (flag[3]) {
         if (tid == 0) res[1] = 1;
         return;
@@ -514,10 +605,10 @@ __device__ void resolve_body(unsigned char* rsm, int n, int nq, float nnratio, i
     const bool in_lds = run <= ent_cap;
     // round 0 was k_proj_lists' (pick0): its claims build own[1]
     for (int i = tid; i < nq; i += nt) {
-        const int p = pick[i];
+        const int p = pk[i];
         if (p >= 0) atomicMin(&own[n + p], i);
         if (in_lds) {   // 8 loads in flight before their stores (one round trip per 8 entries)
-            const int c = ld_ag(lcnt + i), o = qoff[i];
+            const int o = qoff[i], c = qoff[i + 1] - o;
             const uint64_t* L = lists + (size_t)i * cap;
             for (int j0 = 0; j0 < c; j0 += 8) {
                 uint64_t v[8];
@@ -530,6 +621,7 @@ __device__ void resolve_body(unsigned char* rsm, int n, int nq, float nnratio, i
         }
     }
     __syncthreads();
+    mark(1);
     // round r >= 1: reads own[r % 3], builds own[(r+1) % 3], clears own[(r+2) % 3]; flag[r % 3] =
     // some pick changed, and flag[(r+1) % 3] (last read before round r-1's barrier) is reset here
     int r = 1;
@@ -541,8 +633,8 @@ __device__ void resolve_body(unsigned char* rsm, int n, int nq, float nnratio, i
         if (tid == 0) flag[(r + 1) % 3] = 0;
         int ch = 0;
         for (int i = tid; i < nq; i += nt) {
-            const int c = ld_ag(lcnt + i);
-            const uint64_t* L = in_lds ? ent + qoff[i] : lists + (size_t)i * cap;
+            const int o = qoff[i], c = qoff[i + 1] - o;
+            const uint64_t* L = in_lds ? ent + o : lists + (size_t)i * cap;
             Top2 t{256, INT_MAX, -1, 256, INT_MAX, -1};
             for (int j = 0; j < c; j++) {
                 const uint64_t e = in_lds ? L[j] : ld_ag(L + j);
@@ -552,14 +644,15 @@ __device__ void resolve_body(unsigned char* rsm, int n, int nq, float nnratio, i
                 top2_add(t, d, (int)(lo >> 4), (int)(lo & 15));
             }
             const int p = proj_decide(t, MODE, nnratio);
-            ch |= p != pick[i];
-            pick[i] = p;
+            ch |= p != pk[i];
+            pk[i] = p;
             if (p >= 0) atomicMin(&own_next[p], i);
         }
         if (ch) flag[r % 3] = 1;
         __syncthreads();
         if (!flag[r % 3]) break;
     }
+    mark(2);
     // ---- the rotation filter of SearchByProjection(CurrentFrame, LastFrame), the count ----
     const float factor = 1.0f / kHisto;
     auto bin_of = [&](int i, int k) {
@@ -572,7 +665,7 @@ __device__ void resolve_body(unsigned char* rsm, int n, int nq, float nnratio, i
     const bool rot = MODE == 0 && check_orientation;
     if (rot) {
         for (int i = tid; i < nq; i += nt)
-            if (pick[i] >= 0) atomicAdd(&hist[bin_of(i, pick[i])], 1);
+            if (pk[i] >= 0) atomicAdd(&hist[bin_of(i, pk[i])], 1);
         __syncthreads();
         if (tid == 0) {   // ComputeThreeMaxima
             int m1 = 0, m2 = 0, m3 = 0, i1 = -1, i2 = -1, i3 = -1;
@@ -587,24 +680,26 @@ __device__ void resolve_body(unsigned char* rsm, int n, int nq, float nnratio, i
             keep[0] = i1; keep[1] = i2; keep[2] = i3;
         }
         __syncthreads();
+        for (int i = tid; i < nq; i += nt)   // each thread rewrites only its own queries
+            if (pk[i] >= 0) {
+                const int b = bin_of(i, pk[i]);
+                if (b != keep[0] && b != keep[1] && b != keep[2]) pk[i] = -1;
+            }
     }
+    // the count first, then the stores (match / res may be host memory: no barrier waits on them)
     int c = 0;
-    for (int i = tid; i < nq; i += nt) {
-        int k = pick[i];
-        if (k >= 0 && rot) {
-            const int b = bin_of(i, k);
-            if (b != keep[0] && b != keep[1] && b != keep[2]) k = -1;
-        }
-        match[i] = k;
-        c += k >= 0;
-    }
-    atomicAdd(&cnt, c);
+    for (int i = tid; i < nq; i += nt) c += pk[i] >= 0;
+    c = wave_sum_i32(c);   // one LDS atomic per wave: 1024 same-address atomics serialise
+    if ((tid & 63) == 0) atomicAdd(&cnt, c);
     __syncthreads();
+    mark(4);
+    for (int i = tid; i < nq; i += nt) match[i] = pk[i];
     if (tid == 0) {
         res[0] = cnt;
         res[1] = 0;
         res[2] = r + 1;
     }
+    mark(5);
 }
 
 template <int MODE>
@@ -613,11 +708,10 @@ __global__ __launch_bounds__(1024) void k_proj_resolve(int n, int nq, float nnra
                                                        const orbhip_kp* __restrict__ kps,
                                                        const uint64_t* __restrict__ lists,
                                                        const int* __restrict__ lcnt, const int* __restrict__ pick0,
-                                                       int* __restrict__ pick, int* __restrict__ match,
-                                                       int* __restrict__ res) {
+                                                       int* __restrict__ match, int* __restrict__ res) {
     extern __shared__ __attribute__((aligned(16))) unsigned char rsm_[];
-    resolve_body<MODE>(rsm_, n, nq, nnratio, check_orientation, cap, ent_cap, qangle, kps, lists, lcnt, pick0, pick,
-                       match, res);
+    resolve_body<MODE>(rsm_, n, nq, nnratio, check_orientation, cap, ent_cap, qangle, kps, lists, lcnt, pick0, match,
+                       res);
 }
 
 // ---------------------------------------------------------------------------
@@ -1218,6 +1312,27 @@ ProjFrame make_frame(const orbhip_frame* F) {
     return f;
 }
 
+// The staged inputs to device memory by the shader: every lane reads two 16-byte pieces of the
+// pinned staging block over the bus (~140 KB per search: a few us) instead of a DMA-engine copy,
+// whose start-up and ~15 GB/s rate cost ~12 us per call (rocprofv3 memory-copy trace, r03).
+// ORBHIP_PROJ_DMA=1 restores hipMemcpyAsync (A/B, read per call).
+__global__ __launch_bounds__(256) void k_upload(const uint4* __restrict__ src, uint4* __restrict__ dst, int n16) {
+    const int i = blockIdx.x * 512 + threadIdx.x;
+    uint4 a{}, b{};
+    if (i < n16) a = src[i];
+    if (i + 256 < n16) b = src[i + 256];
+    if (i < n16) dst[i] = a;
+    if (i + 256 < n16) dst[i + 256] = b;
+}
+hipError_t upload_inputs(const void* hd, void* d, const void* h, size_t bytes, hipStream_t st) {
+    const char* e = std::getenv("ORBHIP_PROJ_DMA");
+    if (e && e[0] == '1') return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st);
+    const int n16 = (int)((bytes + 15) / 16);   // bytes: a multiple of 256 (Layout)
+    hipLaunchKernelGGL(k_upload, dim3((unsigned)((n16 + 511) / 512)), dim3(256), 0, st, (const uint4*)hd, (uint4*)d,
+                       n16);
+    return hipGetLastError();
+}
+
 int ensure(ProjWorkspace* ws, size_t total) {
     if (!ws->arrive) {
         PJOK(hipMalloc((void**)&ws->arrive, sizeof(int)));
@@ -1284,14 +1399,18 @@ int run_rounds(ProjWorkspace* ws, const ProjFrame& f, int nq, int mode, float nn
 namespace {
 
 // the two-launch form applies: every octave fits the list entry's 4 bits, the owner tables fit LDS
+constexpr size_t kResolveLds = 150 * 1024;   // k_proj_resolve's dynamic LDS
 bool onepass_ok(const orbhip_frame* F, int nq) {
     const char* e = std::getenv("ORBHIP_PROJ_ROUNDS");   // A/B switch (read per call: tests flip it)
-    if ((e && e[0] == '1') || F->n > kProjMaxN || nq > kProjMaxQ) return false;
+    if ((e && e[0] == '1') || F->n > kProjMaxN || nq > kProjMaxQ || resolve_head_bytes(F->n, nq) > kResolveLds)
+        return false;
     for (int k = 0; k < F->n; k++)
         if (F->kps[k].octave < 0 || F->kps[k].octave > 15) return false;
     return true;
 }
-constexpr size_t kResolveLds = 150 * 1024;   // k_proj_resolve's dynamic LDS
+// k_proj_lists' LDS: keypoint records, cells (padded to 256), the waves' index lists
+size_t list_lds_bytes(int n) { return 16 * (size_t)n + 2 * (size_t)((n + 255) & ~255) + kListIdxBytes; }
+static_assert(18 * (size_t)kProjMaxN + kListIdxBytes <= kResolveLds, "k_proj_lists' staging exceeds its LDS");
 hipError_t proj_lds_attr() {   // beyond the default 64 KiB of dynamic LDS
     static const hipError_t e[4] = {
         hipFuncSetAttribute((const void*)k_proj_resolve<0>, hipFuncAttributeMaxDynamicSharedMemorySize, kResolveLds),
@@ -1304,7 +1423,7 @@ hipError_t proj_lds_attr() {   // beyond the default 64 KiB of dynamic LDS
 }
 // list entries the resolve kernel holds in LDS next to its owner tables and list offsets
 int resolve_ent_cap(int n, int nq) {
-    const size_t head = ((size_t)(3 * n + nq) * 4 + 15) & ~size_t(15);
+    const size_t head = resolve_head_bytes(n, nq);
     return head >= kResolveLds ? 0 : (int)((kResolveLds - head) / 8);
 }
 // one launch (the list kernel's last work-group resolves) unless ORBHIP_PROJ_TWO=1 (read per call)
@@ -1366,7 +1485,7 @@ int proj_search_last(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_proj
     std::memcpy(H + o_qd, L->desc, 32 * (size_t)nq);
     std::memcpy(H + o_oct, L->octave, 4 * (size_t)nq);
     std::memcpy(H + o_ang, L->angle, 4 * (size_t)nq);
-    PJOK(hipMemcpyAsync(D, H, o_in_end, hipMemcpyHostToDevice, st));
+    PJOK(upload_inputs(ws->hd, D, H, o_in_end, st));
     const ProjFrame f = make_frame(F);
     const PrepLast pl{(const float*)(D + o_pts), (const int*)(D + o_oct), (const float*)(D + o_scale), th};
     const uint8_t* dcl = F->claimed ? (const uint8_t*)(D + o_cl) : nullptr;
@@ -1374,16 +1493,16 @@ int proj_search_last(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_proj
     if (onepass) {
         const bool fused = proj_fused();
         const ResolveArgs ra{fused ? 1 : 0, check_orientation, resolve_ent_cap(n, nq), (const float*)(D + o_ang),
-                             (int*)(D + o_pick), (int*)(HD + o_out + ob.match), (int*)(HD + o_out + ob.res),
+                             (int*)(HD + o_out + ob.match), (int*)(HD + o_out + ob.res),
                              ws->arrive};
-        hipLaunchKernelGGL(k_proj_lists<0>, dim3((unsigned)((nq + kListWaves - 1) / kListWaves)), dim3(1024),
-                           fused ? kResolveLds : 16 * (size_t)n, st, f, nq, pl, PrepLocal{}, cap, 0.f,
+        hipLaunchKernelGGL(k_proj_lists<0>, dim3((unsigned)((nq + kListQ - 1) / kListQ)), dim3(1024),
+                           fused ? kResolveLds : list_lds_bytes(n), st, f, nq, pl, PrepLocal{}, cap, 0.f,
                            (const orbhip_kp*)(D + o_kps), (const uint8_t*)(D + o_kd), dcl, (const uint8_t*)(D + o_qd),
                            (uint64_t*)(D + o_list), (int*)(D + o_lcnt), (int*)(D + o_pick0), nullptr, nullptr, ra);
         if (!fused)
             hipLaunchKernelGGL(k_proj_resolve<0>, dim3(1), dim3(1024), kResolveLds, st, n, nq, 0.f, check_orientation,
                                cap, ra.ent_cap, ra.qangle, (const orbhip_kp*)(D + o_kps), (const uint64_t*)(D + o_list),
-                               (const int*)(D + o_lcnt), (const int*)(D + o_pick0), ra.pick, ra.match, ra.res);
+                               (const int*)(D + o_lcnt), (const int*)(D + o_pick0), ra.match, ra.res);
         PJOK(hipGetLastError());
         PJOK(hipStreamSynchronize(st));
         if (hres[1] == 0) {
@@ -1450,7 +1569,7 @@ int proj_search_local(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_loc
     std::memcpy(H + o_maxd, M->max_dist, 4 * (size_t)nq);
     std::memcpy(H + o_qd, M->desc, 32 * (size_t)nq);
     if (M->skip) std::memcpy(H + o_skip, M->skip, nq);
-    PJOK(hipMemcpyAsync(D, H, o_in_end, hipMemcpyHostToDevice, st));
+    PJOK(upload_inputs(ws->hd, D, H, o_in_end, st));
     const ProjFrame f = make_frame(F);
     const PrepLocal pc{(const float*)(D + o_pts), (const float*)(D + o_nrm), (const float*)(D + o_mind),
                        (const float*)(D + o_maxd), M->skip ? (const uint8_t*)(D + o_skip) : nullptr,
@@ -1467,10 +1586,10 @@ int proj_search_local(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_loc
     };
     if (onepass) {
         const bool fused = proj_fused();
-        const ResolveArgs ra{fused ? 1 : 0, 0, resolve_ent_cap(n, nq), nullptr, (int*)(D + o_pick),
+        const ResolveArgs ra{fused ? 1 : 0, 0, resolve_ent_cap(n, nq), nullptr,
                              (int*)(HD + o_out + ob.match), (int*)(HD + o_out + ob.res), ws->arrive};
-        hipLaunchKernelGGL(k_proj_lists<1>, dim3((unsigned)((nq + kListWaves - 1) / kListWaves)), dim3(1024),
-                           fused ? kResolveLds : 16 * (size_t)n, st, f, nq, PrepLast{}, pc, cap, nnratio,
+        hipLaunchKernelGGL(k_proj_lists<1>, dim3((unsigned)((nq + kListQ - 1) / kListQ)), dim3(1024),
+                           fused ? kResolveLds : list_lds_bytes(n), st, f, nq, PrepLast{}, pc, cap, nnratio,
                            (const orbhip_kp*)(D + o_kps), (const uint8_t*)(D + o_kd), dcl, (const uint8_t*)(D + o_qd),
                            (uint64_t*)(D + o_list), (int*)(D + o_lcnt), (int*)(D + o_pick0),
                            (uint8_t*)(HD + o_out + ob.iv), (int*)(HD + o_out + ob.lvl), ra);
@@ -1478,7 +1597,7 @@ int proj_search_local(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_loc
             hipLaunchKernelGGL(k_proj_resolve<1>, dim3(1), dim3(1024), kResolveLds, st, n, nq, nnratio, 0, cap,
                                ra.ent_cap, (const float*)nullptr, (const orbhip_kp*)(D + o_kps),
                                (const uint64_t*)(D + o_list), (const int*)(D + o_lcnt), (const int*)(D + o_pick0),
-                               ra.pick, ra.match, ra.res);
+                               ra.match, ra.res);
         PJOK(hipGetLastError());
         PJOK(hipStreamSynchronize(st));
         if (hres[1] == 0) {
@@ -1560,7 +1679,7 @@ int init_search(ProjWorkspace* ws, const orbhip_init_frame* F1, const orbhip_ini
         std::memcpy(H + o_d2, F2->desc, 32 * (size_t)n2);
     }
     std::memcpy(H + o_prev, prev_matched, 8 * (size_t)n1);
-    PJOK(hipMemcpyAsync(D, H, o_in_end, hipMemcpyHostToDevice, st));
+    PJOK(upload_inputs(ws->hd, D, H, o_in_end, st));
     InitGeom g{};
     g.n1 = n1; g.n2 = n2;
     g.minx = F2->min_x; g.maxx = F2->max_x; g.miny = F2->min_y; g.maxy = F2->max_y;
