@@ -25,6 +25,7 @@
 #include "../../include/orbhip.h"
 #include "ba_se3.h"
 #include "pose_opt.h"
+#include "proj.h"
 #include "wave_f64.h"
 
 namespace orbhip {
@@ -301,7 +302,8 @@ __device__ void pose_optimize(FrameGroup<W>& g, double* T, const PoseHdr& h, con
 template <int W>
 __global__ __launch_bounds__(256) void k_pose_opt(const PoseHdr* __restrict__ hdr, const PoseEdgeIn* __restrict__ edges,
                                                    uint8_t* __restrict__ level, uint8_t* __restrict__ outlier,
-                                                   double* __restrict__ chi2_last, PoseOut* __restrict__ out, int B) {
+                                                   double* __restrict__ chi2_last, PoseOut* __restrict__ out,
+                                                   uint8_t* __restrict__ outlier_copy, int B) {
     constexpr int FPB = 4 / W, NT = FrameGroup<W>::T;
     __shared__ double sm[FPB * FrameGroup<W>::kDoubles];
     const int grp = threadIdx.x / NT;
@@ -342,6 +344,8 @@ __global__ __launch_bounds__(256) void k_pose_opt(const PoseHdr* __restrict__ hd
             if (h.n < 10) break;              // optimizer.edges().size() < 10
         }
     }
+    if (outlier_copy)   // zero-copy result: the flags also into the caller-visible block
+        for (int e = tid; e < h.n; e += NT) outlier_copy[h.off + e] = ol[e];
     if (tid == 0) {
         PoseOut& o = out[f];
 #pragma unroll
@@ -358,6 +362,7 @@ struct PoseWorkspace {
     void* d = nullptr;
     size_t dcap = 0;
     void* h = nullptr;
+    void* hd = nullptr;   // device alias of h
     size_t hcap = 0;
     ~PoseWorkspace() {
         if (d) (void)hipFree(d);
@@ -407,6 +412,7 @@ int pose_opt_batch(PoseWorkspace* ws, const orbhip_pose_problem* probs, int B, o
         ws->hcap = 0;
         PSOK(hipHostMalloc(&ws->h, total + total / 4, hipHostMallocDefault));
         ws->hcap = total + total / 4;
+        PSOK(hipHostGetDevicePointer(&ws->hd, ws->h, 0));
     }
     char* H = (char*)ws->h;
     char* D = (char*)ws->d;
@@ -433,7 +439,12 @@ int pose_opt_batch(PoseWorkspace* ws, const orbhip_pose_problem* probs, int B, o
         }
         off += p.n;
     }
-    PSOK(hipMemcpyAsync(D, H, o_edge + sizeof(PoseEdgeIn) * E, hipMemcpyHostToDevice, st));
+    // small batches (one tracking frame): a shader upload and results written straight into the
+    // pinned block (no DMA-engine copies); large batches: DMA both ways
+    const size_t in_bytes = o_edge + sizeof(PoseEdgeIn) * E;
+    const bool small = in_bytes <= ((size_t)1 << 20);
+    if (small) PSOK(upload_inputs(ws->hd, D, H, in_bytes, st));
+    else PSOK(hipMemcpyAsync(D, H, in_bytes, hipMemcpyHostToDevice, st));
     // W = 4 wavefronts per frame while that still fills the chip's SIMDs twice over, else one
     int W = B <= 512 ? 4 : 1;
     if (const char* s = std::getenv("ORBHIP_POSE_WAVES")) W = std::atoi(s) == 1 ? 1 : 4;
@@ -442,14 +453,15 @@ int pose_opt_batch(PoseWorkspace* ws, const orbhip_pose_problem* probs, int B, o
     uint8_t* dlv = (uint8_t*)(D + o_lv);
     uint8_t* dol = (uint8_t*)(D + o_ol);
     double* dc2 = (double*)(D + o_c2);
-    PoseOut* dout = (PoseOut*)(D + o_out);
+    PoseOut* dout = (PoseOut*)((small ? (char*)ws->hd : D) + o_out);
+    uint8_t* olc = small ? (uint8_t*)ws->hd + o_ol : nullptr;
     if (W == 4)
-        hipLaunchKernelGGL(k_pose_opt<4>, dim3((unsigned)B), dim3(256), 0, st, dh, de, dlv, dol, dc2, dout, B);
+        hipLaunchKernelGGL(k_pose_opt<4>, dim3((unsigned)B), dim3(256), 0, st, dh, de, dlv, dol, dc2, dout, olc, B);
     else
         hipLaunchKernelGGL(k_pose_opt<1>, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, dh, de, dlv, dol, dc2,
-                           dout, B);
+                           dout, olc, B);
     PSOK(hipGetLastError());
-    PSOK(hipMemcpyAsync(H + o_out, D + o_out, o_ol - o_out + E, hipMemcpyDeviceToHost, st));
+    if (!small) PSOK(hipMemcpyAsync(H + o_out, D + o_out, o_ol - o_out + E, hipMemcpyDeviceToHost, st));
     PSOK(hipStreamSynchronize(st));
     const PoseOut* ho = (const PoseOut*)(H + o_out);
     const uint8_t* hol = (const uint8_t*)(H + o_ol);

@@ -15,4 +15,7 @@ int proj_search_local(ProjWorkspace* ws, const orbhip_frame* F, const orbhip_loc
                       int32_t* match, int* rounds_out, hipStream_t st);
 int init_search(ProjWorkspace* ws, const orbhip_init_frame* F1, const orbhip_init_frame* F2, float* prev_matched,
                 int window_size, float nnratio, int check_orientation, int32_t* matches12, hipStream_t st);
+// Staged host inputs (pinned block h, its device alias hd) to device memory d by a shader copy
+// (small blocks: no DMA-engine start-up); ORBHIP_PROJ_DMA=1 uses hipMemcpyAsync.
+hipError_t upload_inputs(const void* hd, void* d, const void* h, size_t bytes, hipStream_t st);
 }  // namespace orbhip

@@ -1315,7 +1315,7 @@ ProjFrame make_frame(const orbhip_frame* F) {
 // The staged inputs to device memory by the shader: every lane reads two 16-byte pieces of the
 // pinned staging block over the bus (~140 KB per search: a few us) instead of a DMA-engine copy,
 // whose start-up and ~15 GB/s rate cost ~12 us per call (rocprofv3 memory-copy trace, r03).
-// ORBHIP_PROJ_DMA=1 restores hipMemcpyAsync (A/B, read per call).
+// ORBHIP_PROJ_DMA=1 restores hipMemcpyAsync (A/B, read per call). Also the pose solver's upload.
 __global__ __launch_bounds__(256) void k_upload(const uint4* __restrict__ src, uint4* __restrict__ dst, int n16) {
     const int i = blockIdx.x * 512 + threadIdx.x;
     uint4 a{}, b{};
@@ -1324,6 +1324,8 @@ __global__ __launch_bounds__(256) void k_upload(const uint4* __restrict__ src, u
     if (i < n16) dst[i] = a;
     if (i + 256 < n16) dst[i + 256] = b;
 }
+}  // namespace
+
 hipError_t upload_inputs(const void* hd, void* d, const void* h, size_t bytes, hipStream_t st) {
     const char* e = std::getenv("ORBHIP_PROJ_DMA");
     if (e && e[0] == '1') return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st);
@@ -1332,6 +1334,8 @@ hipError_t upload_inputs(const void* hd, void* d, const void* h, size_t bytes, h
                        n16);
     return hipGetLastError();
 }
+
+namespace {
 
 int ensure(ProjWorkspace* ws, size_t total) {
     if (!ws->arrive) {
