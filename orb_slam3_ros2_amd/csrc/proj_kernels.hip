@@ -446,8 +446,7 @@ __global__ __launch_bounds__(1024) void k_proj_lists(ProjFrame f, int nq, PrepLa
             const int px = c / kGridRows, py = c - px * kGridRows;   // c = 0xFFFF: px = 1365, out
             return px >= nMinCellX && px <= nMaxCellX && py >= nMinCellY && py <= nMaxCellY;
         };
-        // 1a: the cell rectangle alone, four cells per lane from one 8-byte read (short code: this
-        // runs once per wave, from a cold instruction cache)
+        // 1a: the cell rectangle alone, four cells per lane from one 8-byte read
         int nr = 0;
         for (int s0 = 0; any && s0 < n; s0 += 256) {
             const uint64_t v = kc8[(s0 >> 2) + lane];
