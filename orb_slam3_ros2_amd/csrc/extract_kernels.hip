@@ -477,7 +477,7 @@ template <int NT, int WP>
 __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P, const CellGeom* __restrict__ cells,
                                                const FrameBufs& fb, uint32_t* __restrict__ cand,
                                                int* __restrict__ cand_cnt, int* __restrict__ err, int cell, int f,
-                                               const FastLds& LS) {
+                                               const FastLds& LS, const CandPack& cp) {
     uint8_t* const win = LS.win;
     uint8_t* const mv = LS.mv;
     unsigned long long* const bm0 = LS.bmask;
@@ -496,7 +496,10 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     // the error words of the extraction: cleared here, set by the octree (next launch)
     if (cell == 0 && f == 0 && tid < 4) __hip_atomic_store(&err[tid], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (wc <= 6 || hc <= 6) {
-        if (tid == 0) *cnt_out = 0;
+        if (tid == 0) {
+            *cnt_out = 0;
+            if (cp.off) cp.off[(int64_t)f * P->n_cells_total + cell] = 0;
+        }
         return;
     }
     const LevelGeom& G = P->lv[cg.level];
@@ -727,7 +730,28 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     }
     __syncthreads();
     const int sel = wsel;
-    uint32_t* out = cand + (int64_t)f * P->n_slots_total + cg.slot_off;
+    int slot = cg.slot_off;
+    if (cp.off) {
+        // packed candidates (batches): the cell's run goes to the next free range of its level's
+        // region (one atomic per cell), so the octree's reads cover whole lines instead of a line
+        // per sparse cell; the run's frame offset goes to cp.off. ncand is free again here
+        if (tid == 0) {
+            int b = wtot ? atomicAdd(&cp.fill[f * kMaxLevels + cg.level], wtot) : 0;
+            if (b + wtot > G.n_slots) {   // never expected (a level's cells cannot exceed its slots)
+                atomicOr(err, 4);
+                b = -1;
+            }
+            ncand = b;
+            cp.off[(int64_t)f * P->n_cells_total + cell] = b < 0 ? 0 : G.slot_base + b;
+        }
+        __syncthreads();
+        if (ncand < 0) {
+            if (tid == 0) *cnt_out = 0;
+            return;
+        }
+        slot = G.slot_base + ncand;
+    }
+    uint32_t* out = cand + (int64_t)f * P->n_slots_total + slot;
     for (int w = wid; w < nwd; w += NW) {
         const uint64_t mk = (sel ? bm1 : bm0)[w];
         const int p = 64 * w + lane;
@@ -746,7 +770,7 @@ template <int NT, int WR>
 __global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict__ P,
                                                     const CellGeom* __restrict__ cells, FrameBufs fb,
                                                     uint32_t* __restrict__ cand, int* __restrict__ cand_cnt,
-                                                    int* __restrict__ err, int xrun) {
+                                                    int* __restrict__ err, int xrun, CandPack cp) {
     using SH = FastShape<WR>;
     __shared__ __attribute__((aligned(16))) uint8_t win[WR * SH::wp];
     __shared__ uint8_t mv[WR * SH::wp];
@@ -757,7 +781,7 @@ __global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict
     __shared__ int ncand;
     const FastLds LS{win, mv, bmask, SH::nw, woff, &wsel, &wtot, clist, &ncand, min(P->clist_cap, SH::cap)};
     const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
-    fast_cell_body<NT, SH::wp>(P, cells, fb, cand, cand_cnt, err, lg % X, lg / X, LS);
+    fast_cell_body<NT, SH::wp>(P, cells, fb, cand, cand_cnt, err, lg % X, lg / X, LS, cp);
 }
 
 // ---------------------------------------------------------------------------
@@ -935,6 +959,7 @@ constexpr int kOctMaxDh = 6;
 
 __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__ P, const CellGeom* __restrict__ cells,
                                                  const uint16_t* __restrict__ otab, const uint32_t* __restrict__ cand, const int* __restrict__ cand_cnt,
+                                                 const int* __restrict__ cand_off,
                                                  uint32_t* __restrict__ kscratch, uint16_t* __restrict__ nscratch,
                                                  LevelKp* __restrict__ lvl_kp, int* __restrict__ lvl_cnt,
                                                  int* __restrict__ lvl_nlap, OctreeCfg cfg, int* __restrict__ err) {
@@ -1025,7 +1050,8 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
     if (ncell <= nt) {
         // one cell per thread: every count / slot load in flight at once, one block scan
         const int c = tid < ncell ? cc[tid] : 0;
-        const int so = tid < ncell ? cells[G.cell_base + tid].slot_off : 0;
+        const int so = tid >= ncell ? 0 : (cand_off ? cand_off[(int64_t)f * P->n_cells_total + G.cell_base + tid]
+                                                   : cells[G.cell_base + tid].slot_off);
         const uint32_t t0 = tid < ntab ? otl[tid] : 0u, t1 = tid + nt < ntab ? otl[tid + nt] : 0u;
         zero_pyramid();
         if (tid < ncell) S.cslot[tid] = so;
@@ -1040,7 +1066,8 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
     } else if (w0) {
         for (int i = lane; i < ncell; i += 64) {
             S.cellstart[i] = cc[i];
-            S.cslot[i] = cells[G.cell_base + i].slot_off;
+            S.cslot[i] = cand_off ? cand_off[(int64_t)f * P->n_cells_total + G.cell_base + i]
+                                  : cells[G.cell_base + i].slot_off;
         }
         wave_lds_fence();
         const int M0 = wave_scan_lds(S.cellstart, ncell);
@@ -2000,7 +2027,7 @@ void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameB
 }
 
 void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,
-                 uint32_t* cand, int* cand_cnt, int* err, hipStream_t st, int nt_hint) {
+                 uint32_t* cand, int* cand_cnt, int* err, hipStream_t st, int nt_hint, CandPack cp) {
     // more threads per cell while the cells alone cannot fill the chip (one frame: ~600 cells on
     // 256 CUs), as many as keep every work-group resident at once (8192 wave slots); 256 once
     // the batch fills the chip; 128 for big batches (C3: 127k cells), where fewer waves per cell
@@ -2014,7 +2041,7 @@ void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* c
     const int xr = xcd_run_for(B);
     const bool compact = hP.fast_win_rows <= 56 && hP.fast_win_cols + 3 <= 64;   // window dwords (sh <= 3) fit a row
 #define ORBHIP_FAST_LAUNCH(NTV, WRV) \
-    ORBHIP_LAUNCH((k_fast_cells<NTV, WRV>), grd, dim3(NTV), 0, st, dP, cells, fb, cand, cand_cnt, err, xr)
+    ORBHIP_LAUNCH((k_fast_cells<NTV, WRV>), grd, dim3(NTV), 0, st, dP, cells, fb, cand, cand_cnt, err, xr, cp)
     if (nt == 1024 && compact)
         ORBHIP_FAST_LAUNCH(1024, 56);
     else if (nt == 1024)
@@ -2053,12 +2080,12 @@ size_t octree_lds_bytes(const ExtractPlan& hP, const OctreeCfg& cfg) {
 
 void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const uint16_t* otab,
                    const uint32_t* cand,
-                   const int* cand_cnt, uint32_t* kscratch, uint16_t* nscratch, LevelKp* lvl_kp, int* lvl_cnt,
-                   int* lvl_nlap, const OctreeCfg& cfg, int* err, int B, hipStream_t st) {
+                   const int* cand_cnt, const int* cand_off, uint32_t* kscratch, uint16_t* nscratch, LevelKp* lvl_kp,
+                   int* lvl_cnt, int* lvl_nlap, const OctreeCfg& cfg, int* err, int B, hipStream_t st) {
     const size_t lds = octree_lds_bytes(hP, cfg);
     dim3 grd(B, hP.n_levels, 1);
-    ORBHIP_LAUNCH(k_octree, grd, dim3(1024), lds, st, dP, cells, otab, cand, cand_cnt, kscratch, nscratch, lvl_kp,
-                       lvl_cnt, lvl_nlap, cfg, err);
+    ORBHIP_LAUNCH(k_octree, grd, dim3(1024), lds, st, dP, cells, otab, cand, cand_cnt, cand_off, kscratch, nscratch,
+                  lvl_kp, lvl_cnt, lvl_nlap, cfg, err);
 }
 
 constexpr int kDescKpMaxSlots = 16384;

@@ -142,6 +142,7 @@ struct orbhip_ctx {
     DevBuf<uint32_t> d_cand, d_kscratch;
     DevBuf<uint16_t> d_nscratch;
     DevBuf<int> d_cand_cnt, d_lvl_cnt, d_lvl_nlap, d_err;
+    DevBuf<int> d_cand_off, d_cand_fill;   // packed FAST candidates (batches, CandPack)
     DevBuf<uint64_t> d_mpart;   // matcher chunk partials (match_part_entries)
     DevBuf<int> d_msync;        // one-launch matcher counters (zeroed once, reset by every launch)
     DevBuf<double> d_bw;        // bag-of-words weights (host transform)
@@ -643,6 +644,8 @@ static int ensure_batch(orbhip_ctx* c, const Plan* pl, int B) {
     HIPOK(c->d_kscratch.ensure((size_t)B * P.n_slots_total));
     HIPOK(c->d_nscratch.ensure((size_t)B * P.n_slots_total));
     HIPOK(c->d_cand_cnt.ensure((size_t)B * P.n_cells_total));
+    HIPOK(c->d_cand_off.ensure((size_t)B * P.n_cells_total));
+    HIPOK(c->d_cand_fill.ensure((size_t)B * kMaxLevels));
     HIPOK(c->d_lvl_kp.ensure((size_t)B * P.kp_slots_total));
     HIPOK(c->d_lvl_cnt.ensure((size_t)B * P.n_levels));
     HIPOK(c->d_lvl_nlap.ensure((size_t)B * P.n_levels));
@@ -671,11 +674,16 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
     // the five k_resize launches it replaces (tools/c3_pyr_sweep.sh, tiles 16-48)
     const char* e_hi = std::getenv("ORBHIP_CONE_HI");
     const bool cone_hi_on = e_hi && e_hi[0] == '1';
+    // ORBHIP_CAND_PACK=1 (read per call): packed FAST candidates, the octree then reads whole
+    // lines. Off: at C3 it cut k_octree's traffic 21.8 -> 6.4 MB per launch (PMC), but the atomic
+    // each FAST cell waits on held its work-group slot ~1 us longer: k_fast_cells 525 -> 568 us
+    const char* e_pk = std::getenv("ORBHIP_CAND_PACK");
+    const bool pack = e_pk && e_pk[0] == '1';
     GraphKey key;
-    key.add(1).add((uint64_t)oct_fast).add((uint64_t)oct_max_dh).add((uint64_t)no_cone).add((uint64_t)cone_hi_on).add((uint64_t)c->fast_nt).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
+    key.add(1).add((uint64_t)oct_fast).add((uint64_t)oct_max_dh).add((uint64_t)no_cone).add((uint64_t)cone_hi_on).add((uint64_t)pack).add((uint64_t)c->fast_nt).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
         .add((uint64_t)lap1).ptr(d_kps).ptr(d_desc).add((uint64_t)cap).ptr(d_n).ptr(d_mono).ptr(st).ptr(c->d_pyr.p)
         .ptr(c->d_cand.p).ptr(c->d_kscratch.p).ptr(c->d_nscratch.p).ptr(c->d_cand_cnt.p).ptr(c->d_lvl_kp.p)
-        .ptr(c->d_lvl_cnt.p).ptr(c->d_lvl_nlap.p).ptr(c->d_err.p);
+        .ptr(c->d_lvl_cnt.p).ptr(c->d_lvl_nlap.p).ptr(c->d_err.p).ptr(c->d_cand_off.p).ptr(c->d_cand_fill.p);
     return c->graphs.run(key, st, c->timer.stage != 0, [&](hipStream_t st) -> int {
         FrameBufs fb;
         fb.in = d_imgs; fb.in_stride = stride; fb.in_fstride = fstride; fb.pyr = c->d_pyr.p;
@@ -706,15 +714,23 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
         }
         tm.end(1, st);
         tm.begin(2, st);
-        launch_fast(pl->d_plan.p, P, pl->d_cells.p, fb, B, c->d_cand.p, c->d_cand_cnt.p, c->d_err.p, st, c->fast_nt);
+        CandPack cp;
+        if (pack) {
+            HIPOK(hipMemsetAsync(c->d_cand_fill.p, 0, sizeof(int) * (size_t)B * kMaxLevels, st));
+            cp.fill = c->d_cand_fill.p;
+            cp.off = c->d_cand_off.p;
+        }
+        launch_fast(pl->d_plan.p, P, pl->d_cells.p, fb, B, c->d_cand.p, c->d_cand_cnt.p, c->d_err.p, st, c->fast_nt,
+                    cp);
         tm.end(2, st);
         OctreeCfg oc = pl->oct;
         oc.lap0 = lap0; oc.lap1 = lap1;
         oc.fast = oct_fast;
         oc.max_dh = oct_max_dh;
         tm.begin(3, st);
-        launch_octree(pl->d_plan.p, P, pl->d_cells.p, pl->d_otab.p, c->d_cand.p, c->d_cand_cnt.p, c->d_kscratch.p, c->d_nscratch.p,
-                      c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, oc, c->d_err.p, B, st);
+        launch_octree(pl->d_plan.p, P, pl->d_cells.p, pl->d_otab.p, c->d_cand.p, c->d_cand_cnt.p, cp.off,
+                      c->d_kscratch.p, c->d_nscratch.p, c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, oc, c->d_err.p, B,
+                      st);
         tm.end(3, st);
         tm.begin(4, st);
         launch_desc(pl->d_plan.p, P, fb, c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, pl->d_disc.p, d_kps, d_desc,

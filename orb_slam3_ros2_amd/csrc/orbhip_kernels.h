@@ -71,14 +71,20 @@ void launch_resize_bands(const ExtractPlan* dP, int nbands, const FrameBufs& fb,
                          const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st);
 void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, int B, int l,
                    const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st);
+// Packed FAST candidates (batches): per (frame, level) fill counters, zeroed before the launch, and
+// each cell's run offset (per frame); off == nullptr keeps each cell's fixed slot range
+struct CandPack {
+    int* fill = nullptr;   // B x kMaxLevels
+    int* off = nullptr;    // B x n_cells_total
+};
 void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,
-                 uint32_t* cand, int* cand_cnt, int* err, hipStream_t st, int nt_hint = 0);
+                 uint32_t* cand, int* cand_cnt, int* err, hipStream_t st, int nt_hint = 0, CandPack cp = {});
 size_t octree_lds_bytes(const ExtractPlan& hP, const OctreeCfg& cfg);
 bool octree_set_lds_limit(size_t bytes);
 void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const uint16_t* otab,
                    const uint32_t* cand,
-                   const int* cand_cnt, uint32_t* kscratch, uint16_t* nscratch, LevelKp* lvl_kp, int* lvl_cnt,
-                   int* lvl_nlap, const OctreeCfg& cfg, int* err, int B, hipStream_t st);
+                   const int* cand_cnt, const int* cand_off, uint32_t* kscratch, uint16_t* nscratch, LevelKp* lvl_kp,
+                   int* lvl_cnt, int* lvl_nlap, const OctreeCfg& cfg, int* err, int B, hipStream_t st);
 void launch_desc(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, const LevelKp* lvl_kp,
                  const int* lvl_cnt, const int* lvl_nlap, const int* disc, orbhip_kp* out_kps, uint8_t* out_desc,
                  int cap, int* n_out, int* mono_out, int B, hipStream_t st);

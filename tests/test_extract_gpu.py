@@ -63,6 +63,20 @@ def test_resize_cascade_bit_exact(oracle, monkeypatch, w, h, scale, nlev, seed, 
     _check(ext, oracle, synthetic_frame(seed, w, h), scale=scale, nlevels=nlev)
 
 
+@pytest.mark.parametrize("pack", ["1", "0"])
+def test_packed_candidates_bit_exact(oracle, monkeypatch, pack):
+    """FAST's packed candidate layout (one atomic per cell into its level's region, the octree
+    reading each cell's run through the offset table; opt-in, ORBHIP_CAND_PACK=1) and the fixed
+    slot ranges: the keypoints and descriptors are the oracle's either way (the octree's key order
+    is cell-major through the table in both)."""
+    from orb_slam3_ros2_amd import ORBextractor
+    monkeypatch.setenv("ORBHIP_CAND_PACK", pack)
+    ext = ORBextractor(1000, 1.2, 8, 20, 7)
+    _check(ext, oracle, synthetic_frame(81, 640, 480))
+    _check(ext, oracle, synthetic_frame(82, 1280, 720))
+    _check(ext, oracle, synthetic_frame(83, 641, 479))
+
+
 @pytest.mark.parametrize("tile", [5, 17, 48])
 def test_batch_cone_tiles_bit_exact(oracle, monkeypatch, tile):
     """The opt-in batch cone (levels 3.. from level 2, ORBHIP_CONE_HI_TILE per plan lookup) at
