@@ -1329,6 +1329,7 @@ hipError_t upload_inputs(const void* hd, void* d, const void* h, size_t bytes, h
     const char* e = std::getenv("ORBHIP_PROJ_DMA");
     if (e && e[0] == '1') return hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st);
     const int n16 = (int)((bytes + 15) / 16);   // bytes: a multiple of 256 (Layout)
+    if (n16 == 0) return hipSuccess;
     hipLaunchKernelGGL(k_upload, dim3((unsigned)((n16 + 511) / 512)), dim3(256), 0, st, (const uint4*)hd, (uint4*)d,
                        n16);
     return hipGetLastError();
