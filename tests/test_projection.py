@@ -102,3 +102,26 @@ def test_projection_edge_cases(oracle, proj_mode):
     s = synthetic_projection_scene(n_kp=300, n_mp=0, seed=31)
     n, m = mt.SearchByProjectionLastFrame(_frame(s), s["points"], s["mp_desc"], s["last_octave"], s["last_angle"])
     assert n == 0 and m.size == 0
+
+
+@pytest.mark.gpu
+def test_projection_ragged_sizes(oracle, proj_mode):
+    """Frame keypoint counts off the list kernel's 256-key scan step and map-point counts off its
+    4-query work-groups (the last work-group part-filled), both searches against the oracle."""
+    from orb_slam3_ros2_amd import ORBmatcher
+    for n_kp, n_mp, seed in [(777, 333, 40), (257, 5, 41), (1, 3, 42)]:
+        s = synthetic_projection_scene(n_kp=n_kp, n_mp=n_mp, seed=seed)
+        f = _frame(s)
+        mt = ORBmatcher(0.9, True)
+        n, m = mt.SearchByProjectionLastFrame(f, s["points"], s["mp_desc"], s["last_octave"], s["last_angle"], 15.0)
+        on, om = oracle.search_by_projection_last(f, s["points"], s["mp_desc"], s["last_octave"], s["last_angle"],
+                                                  15.0, True)
+        assert n == on and np.array_equal(m, om), (n_kp, n_mp, proj_mode)
+        ml = ORBmatcher(0.8, False)
+        r = ml.SearchLocalPoints(f, s["points"], s["normals"], s["min_dist"], s["max_dist"], s["mp_desc"], s["skip"],
+                                 th=3.0)
+        o = oracle.search_local_points(f, s["points"], s["normals"], s["min_dist"], s["max_dist"], s["mp_desc"],
+                                       s["skip"], th=3.0, nnratio=0.8)
+        assert r[0] == o[0], (n_kp, n_mp, proj_mode)
+        for a, b in zip(r[1:], o[1:]):
+            assert np.array_equal(a, b), (n_kp, n_mp, proj_mode)
