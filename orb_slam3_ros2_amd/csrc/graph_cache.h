@@ -24,7 +24,7 @@
 namespace orbhip {
 
 struct GraphKey {
-    static constexpr int kWords = 32;
+    static constexpr int kWords = 48;
     uint64_t w[kWords] = {};
     int n = 0;
     GraphKey& add(uint64_t v) {
