@@ -259,6 +259,14 @@ __device__ __forceinline__ int small_div(int i, float inv_d) { return (int)(((fl
 // (xofs, xalpha) of its need columns and the row table (clamped r0, r1, ybeta) of its rows: one
 // global round trip loads every table entry and the level-0 cone, then the levels follow from LDS.
 __device__ __forceinline__ void wait_vm_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// work-group barrier that orders LDS only: __syncthreads() also waits for every outstanding global
+// access (s_waitcnt vmcnt(0)), so a level's byte stores to the pyramid would hold the barrier for
+// their write acknowledgements although nothing in the work-group reads them back
+__device__ __forceinline__ void lds_only_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
 
 __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P, const FrameBufs& fb,
                                               const ConeRect* __restrict__ rects, const int* __restrict__ ctab,
@@ -391,7 +399,7 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
             cone[boff[l] + i] = u;
             if (x >= r.ox0 && x < r.ox1 && y >= r.oy0 && y < r.oy1) dst[(int64_t)y * D.pitch + x] = u;
         }
-        __syncthreads();
+        lds_only_barrier();   // the next level reads this one's LDS cone; the stores stay in flight
         TR_PHASE(0, l)
     }
     TR_END(0)

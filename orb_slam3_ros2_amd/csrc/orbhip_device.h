@@ -187,13 +187,16 @@ __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int* total) 
 #define TR_BEGIN()                                                                          \
     unsigned long long tr_t0 = 0, tr_tp = 0;                                                \
     unsigned long long* const tr_buf = g_trace;                                             \
-    (void)tr_tp;                                                                            \
+    /* the traced block is read once here: read inside TR_PHASE, the compiler hoisted the */ \
+    /* load above the branch and every phase then waited on vmcnt(0), stores included */     \
+    const int tr_blk = __builtin_amdgcn_readfirstlane(tr_buf ? g_trace_blk : -1);          \
+    (void)tr_tp; (void)tr_blk;                                                              \
     if (tr_buf && threadIdx.x == 0) {                                                       \
         tr_t0 = __builtin_amdgcn_s_memrealtime();                                           \
         tr_tp = __builtin_amdgcn_s_memtime();                                               \
     }
 #define TR_PHASE(kid, ph)                                                                   \
-    if (tr_buf && threadIdx.x == 0 && blockIdx.x == g_trace_blk && blockIdx.y == 0 && blockIdx.z == 0) { \
+    if (tr_buf && threadIdx.x == 0 && (int)blockIdx.x == tr_blk && blockIdx.y == 0 && blockIdx.z == 0) { \
         const unsigned long long tr_t = __builtin_amdgcn_s_memtime();                       \
         tr_buf[(kid) * kTraceStride + 8192 + (ph)] = tr_t - tr_tp;                          \
         tr_tp = tr_t;                                                                       \
