@@ -2,6 +2,7 @@
 """Summarise rocprofv3 CSV output into the committed files under profiles/.
 
   python tools/prof_summary.py stats  <kernel_stats.csv> <out.md> [title]
+  python tools/prof_summary.py sections <kernel_trace.csv> <out.md> <warmup> <steps>
   python tools/prof_summary.py traffic <fetch counter_collection.csv> <write counter_collection.csv> <out.json>
 
 `traffic` follows MI355X_MICROARCH.md (HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE come from
@@ -61,6 +62,42 @@ def durations(trace_csv):
     for r in csv.DictReader(open(trace_csv)):
         acc[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9)
     return acc
+
+
+def sections(trace_csv, dst, warmup, steps):
+    """Append to `dst` the C2 section's per-kernel averages split by bench phase.
+
+    The camera streams are the streams with warmup + 2 * steps launches of a kernel (bench.py
+    c2_headline: W warmup frames, K timed frames, K stage-replay frames per camera); their
+    launches are split in issue order. Everything else (the one-camera figures) is one row."""
+    per = defaultdict(lambda: defaultdict(list))
+    for r in csv.DictReader(open(trace_csv)):
+        per[r["Stream_Id"]][short(r["Kernel_Name"])].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+    n_cam = warmup + 2 * steps
+    cams = [s for s, ks in per.items() if any(len(v) == n_cam for v in ks.values())]
+    acc = defaultdict(lambda: defaultdict(list))
+    for s, ks in per.items():
+        for k, v in ks.items():
+            v.sort()
+            d = [(e - b) / 1e3 for b, e in v]
+            if s in cams and len(v) >= n_cam - 1:
+                acc[k]["timed"] += d[warmup:warmup + steps]
+                acc[k]["replay"] += d[warmup + steps:]
+            else:
+                acc[k]["other"] += d
+    with open(dst, "a") as f:
+        f.write(f"\n## By bench phase ({len(cams)} camera streams; W = {warmup}, K = {steps} frames per camera)\n\n"
+                "From the kernel trace (`*_kernel_trace.csv`, End - Start per dispatch). `timed` = the K frames "
+                "of the timed region, `replay` = the K frames of the stage replay whose stage timer gives the "
+                "bench's `avg_launch_ms`, `other` = the one-camera figures after the camera streams close.\n\n"
+                "| kernel | timed n | timed avg us | replay n | replay avg us | other n | other avg us |\n"
+                "|---|---:|---:|---:|---:|---:|---:|\n")
+        for k in sorted(acc, key=lambda k: -sum(acc[k]["timed"])):
+            cells = []
+            for ph in ("timed", "replay", "other"):
+                v = acc[k][ph]
+                cells += [str(len(v)), f"{sum(v) / len(v):.2f}" if v else "-"]
+            f.write(f"| {k} | " + " | ".join(cells) + " |\n")
 
 
 SIMDS, CUS = 1024, 256
@@ -132,6 +169,8 @@ def counters(pmc_dir, dst, regimes):
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3], *(sys.argv[4:5] or ["kernel stats"]))
+    elif sys.argv[1] == "sections":
+        sections(sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5]))
     elif sys.argv[1] == "counters":
         counters(sys.argv[2], sys.argv[3], sys.argv[4:])
     else:
