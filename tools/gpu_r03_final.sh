@@ -19,6 +19,8 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
     -- python3 -u bench.py --no-extra --no-cpu > gpurun_out/r03_c2prof.log 2>&1 || { tail -20 gpurun_out/r03_c2prof.log; exit 1; }
 python3 tools/prof_summary.py stats "$(ls gpurun_out/r03_c2prof/*kernel_stats.csv | head -1)" \
     gpurun_out/r03_c2_kernel_stats.md "bench.py --no-extra --no-cpu (the C2 section)" || exit 1
+python3 tools/prof_summary.py sections "$(ls gpurun_out/r03_c2prof/*kernel_trace.csv | head -1)" \
+    gpurun_out/r03_c2_kernel_stats.md 20 200 || exit 1
 grep -v amdgpu.ids gpurun_out/r03_c2prof.log | tail -1 > gpurun_out/r03_c2prof_bench.json
 head -10 gpurun_out/r03_c2_kernel_stats.md
 python3 -c "
