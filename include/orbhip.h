@@ -41,7 +41,8 @@ typedef enum {
     ORBHIP_ERR_DEVICE = -3,       /* HIP runtime failure / no device */
     ORBHIP_ERR_NOT_PD = -4,       /* reduced camera system not positive definite */
     ORBHIP_ERR_UNSUPPORTED = -5,  /* configuration outside the supported envelope */
-    ORBHIP_ERR_EMPTY = -6         /* empty image: ORBextractor::operator() returns -1 */
+    ORBHIP_ERR_EMPTY = -6,        /* empty image: ORBextractor::operator() returns -1 */
+    ORBHIP_ERR_TIMEOUT = -7       /* a persistent-solver hand-off timed out (ORBHIP_DAG_RERUN=0) */
 } orbhip_status;
 
 typedef struct orbhip_ctx orbhip_ctx;
@@ -247,6 +248,18 @@ typedef struct {
  * setForceStopFlag). May be NULL. */
 int orbhip_ba_solve(orbhip_ctx* ctx, const orbhip_ba_problem* prob, orbhip_ba_result* res,
                     const volatile int* stop_flag);
+
+/* Concurrency: LocalMapping's LBA and LoopClosing's GBA (R:src/imu_mono_realsense.cpp:99-100
+ * spawns both threads) may solve at the same time on two contexts. The persistent Cholesky
+ * (one launch owning every CU) is serialised per device across contexts and streams, so two
+ * solves never hold parts of the chip at once. A hand-off that still times out (its bounded spin,
+ * ORBHIP_DAG_SPIN_MAX polls, runs out) never becomes a silently rejected LM trial: the solve is run
+ * again on the non-persistent solvers (same g2o schedule), or, with ORBHIP_DAG_RERUN=0 in the
+ * environment, returns ORBHIP_ERR_TIMEOUT.
+ * orbhip_ba_stats: out[0] persistent solves launched on the context's device (every context),
+ * out[1] of them launched after waiting for another stream's solve, out[2] hand-off timeouts this
+ * context saw, out[3] solves it re-ran. */
+int orbhip_ba_stats(orbhip_ctx* ctx, int64_t out[4]);
 
 /* B independent problems solved together (SURVEY.md §8e replicas: concurrent maps / agents,
  * or a batch of local windows). Each problem follows its own exact LM schedule; all share the

@@ -13,7 +13,7 @@ _lib = None
 
 class OrbHipError(RuntimeError):
     CODES = {-1: "ORBHIP_ERR_ARG", -2: "ORBHIP_ERR_CAPACITY", -3: "ORBHIP_ERR_DEVICE", -4: "ORBHIP_ERR_NOT_PD",
-             -5: "ORBHIP_ERR_UNSUPPORTED", -6: "ORBHIP_ERR_EMPTY"}
+             -5: "ORBHIP_ERR_UNSUPPORTED", -6: "ORBHIP_ERR_EMPTY", -7: "ORBHIP_ERR_TIMEOUT"}
 
     def __init__(self, code: int, what: str = ""):
         self.code = code
@@ -107,7 +107,7 @@ class LocalPointsC(ctypes.Structure):
 EXPORTED = ["orbhip_abi_version", "orbhip_create", "orbhip_destroy", "orbhip_level_info", "orbhip_max_keypoints",
             "orbhip_extract", "orbhip_extract_batch_device", "orbhip_descriptor_distance", "orbhip_match_bf",
             "orbhip_match_pairs_device", "orbhip_match_frames_device", "orbhip_profile_stage",
-            "orbhip_profile_collect", "orbhip_launch_graphs", "orbhip_ba_solve", "orbhip_ba_solve_batch", "orbhip_bgr_to_gray_device",
+            "orbhip_profile_collect", "orbhip_launch_graphs", "orbhip_ba_solve", "orbhip_ba_solve_batch", "orbhip_ba_stats", "orbhip_bgr_to_gray_device",
             "orbhip_comm_unique_id", "orbhip_comm_init", "orbhip_ba_solve_sharded", "orbhip_ba_solve_shards_local",
             "orbhip_vocab_create", "orbhip_vocab_load_text", "orbhip_vocab_destroy", "orbhip_vocab_info",
             "orbhip_bow_transform", "orbhip_bow_transform_device", "orbhip_search_bow",
@@ -167,6 +167,7 @@ def lib():
     L.orbhip_launch_graphs.argtypes = [vp]
     L.orbhip_ba_solve.argtypes = [vp, ctypes.POINTER(BAProblemC), ctypes.POINTER(BAResultC), vp]
     L.orbhip_ba_solve_batch.argtypes = [vp, ctypes.POINTER(BAProblemC), i32, ctypes.POINTER(BAResultC), vp]
+    L.orbhip_ba_stats.argtypes = [vp, vp]
     L.orbhip_pose_optimization.argtypes = [vp, ctypes.POINTER(PoseProblemC), ctypes.POINTER(PoseResultC)]
     L.orbhip_pose_optimization_batch.argtypes = [vp, ctypes.POINTER(PoseProblemC), i32, ctypes.POINTER(PoseResultC)]
     L.orbhip_search_by_projection_last.argtypes = [vp, ctypes.POINTER(FrameC), ctypes.POINTER(ProjLastC), f32, i32,

@@ -23,7 +23,14 @@ struct DagPlan {
     std::vector<int> tasks;
 };
 void dag_plan(const int* row_first, int n, int max_helpers, DagPlan& p);
-int dag_max_helpers();   // min(kDagMaxHelpers, CUs - 1): the whole grid resident, one workgroup per CU
+int dag_max_helpers();   // min(kDagMaxHelpers, CUs - 1) of the current device: the whole grid resident
+// a stream about to be destroyed: no later solve of another stream may record an event on it
+void dag_stream_retired(hipStream_t st);
+// solves launched on the current device, and how many of them first waited for another stream's
+void dag_device_stats(long long* launches, long long* handoffs);
+// polls before a hand-off wait gives up (ORBHIP_DAG_SPIN_MAX, default 2^19); a timeout counts in the
+// problem's control word 3 (DagDev::ints[3]) and fails the solve (flag 0)
+unsigned dag_spin_max();
 
 // device storage of one problem: doubles (L tiles NT x NT, the two partial-tile rows, the
 // diagonal inverses, y, the right-hand-side partials) and ints (4 control words + flags; zero
@@ -33,7 +40,7 @@ size_t dag_ints(int n);
 
 struct DagDev {
     double* buf;         // dag_doubles(n)
-    int* ints;           // dag_ints(n), zeroed once
+    int* ints;           // dag_ints(n), zeroed once; [3] counts hand-off timeouts
     const int* toff;     // plan, on the device
     const int* tasks;
     int G;

@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <mutex>
 #include <utility>
 #include <vector>
 
@@ -43,7 +44,7 @@ namespace {
 
 constexpr int kT = kDagTile;
 constexpr int kTD = kT * kT;            // doubles per tile
-constexpr unsigned kSpinMax = 1u << 19;
+constexpr unsigned kSpinMax = 1u << 19;   // default poll bound (ORBHIP_DAG_SPIN_MAX overrides)
 constexpr size_t kMinLds = 84 * 1024;   // > 80 KB: one workgroup per CU
 #ifndef ORBHIP_DAG_NEWTON
 #define ORBHIP_DAG_NEWTON 1
@@ -69,6 +70,7 @@ struct DagK {
     int n, NT, G;
     int pb;       // backward over the helpers (dag_helper_backward) or in the chain alone
     int hsleep;   // helpers' poll back-off (units of s_sleep 1)
+    unsigned smax;   // polls before a wait gives up (timeout: ctl[2] abort, ctl[3] counted)
 };
 
 __device__ __forceinline__ int ld_flag(const int* p) {
@@ -160,12 +162,12 @@ __device__ __forceinline__ double lmul_ylds(const double4_t& l, const double* y)
 }
 
 // every lane's flag (nullptr: none) equal to epoch; false on abort / timeout (wave-uniform)
-__device__ bool wave_wait_all(const int* f, int epoch, int* ctl) {
+__device__ bool wave_wait_all(const int* f, int epoch, int* ctl, unsigned smax) {
     for (unsigned spins = 0;; spins++) {
         const bool ok = !f || ld_flag(f) == epoch;
         if (__all(ok)) return true;
         if (ld_flag(ctl + 2) == epoch) return false;
-        if (spins >= kSpinMax) {
+        if (spins >= smax) {
             if ((threadIdx.x & 63) == 0) {
                 st_flag(ctl + 2, epoch);
                 __hip_atomic_fetch_add((gint*)(ctl + 3), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -177,7 +179,8 @@ __device__ bool wave_wait_all(const int* f, int epoch, int* ctl) {
 }
 // the number m >= 1 of leading entries i < cnt (<= 64) with fa[i] == fb[i] == fc[i] == epoch
 // (fb / fc optional); 0 on abort / timeout (wave-uniform)
-__device__ int wave_wait_prefix(const int* fa, const int* fb, const int* fc, int cnt, int epoch, int* ctl, int hsleep) {
+__device__ int wave_wait_prefix(const int* fa, const int* fb, const int* fc, int cnt, int epoch, int* ctl, int hsleep,
+                                 unsigned smax) {
     const int lane = threadIdx.x & 63;
     for (unsigned spins = 0;; spins++) {
         bool ok = true;
@@ -190,7 +193,7 @@ __device__ int wave_wait_prefix(const int* fa, const int* fb, const int* fc, int
         const int m = bad ? __builtin_ctzll(bad) : cnt;
         if (m > 0) return m;
         if (ld_flag(ctl + 2) == epoch) return 0;
-        if (spins >= kSpinMax) {
+        if (spins >= smax) {
             if (lane == 0) {
                 st_flag(ctl + 2, epoch);
                 __hip_atomic_fetch_add((gint*)(ctl + 3), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -244,7 +247,7 @@ __device__ void dag_helper_backward(const DagK& a, const Lay& L, __amdgpu_buffer
     double* acc = lds;                  // NT x 32 (a column's running sum, owned by one wave)
     double* xw = lds + 4096 + 64 * wid; // this wave's copy of x_R
     for (int R = NT - 1; R >= j_first + 2; R--) {
-        if (!wave_wait_all(lane == 0 ? L.fX + R : nullptr, epoch, L.ctl)) return;
+        if (!wave_wait_all(lane == 0 ? L.fX + R : nullptr, epoch, L.ctl, a.smax)) return;
         if (R == NT - 1) {   // the forward is over (x_{NT-1} exists): every y_j is published
             for (int j = j_first; j <= NT - 3; j += 4 * G)
                 if (lane < kT) acc[j * kT + lane] = ld_sc1(a.buf + L.oY + j * kT + lane);
@@ -293,7 +296,7 @@ __device__ void dag_helper(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t r
     int wsel = 0;   // rotating LDS word of the poll results
     auto wg_prefix = [&](const int* fa, const int* fb, const int* fc, int cnt) -> int {
         if (wid == 0) {
-            const int m = wave_wait_prefix(fa, fb, fc, cnt, epoch, L.ctl, a.hsleep);
+            const int m = wave_wait_prefix(fa, fb, fc, cnt, epoch, L.ctl, a.hsleep, a.smax);
             if (lane == 0) word[wsel] = m;
         }
         __syncthreads();
@@ -662,7 +665,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             // L(k+2,p) L(k+1,p)^T (partial p <= k-2; p = k-1 and p = k here); D'_{k+2} (partial
             // p <= k-1; p = k here, quadrant (1,0)'s by wave 1 in the next interval) and its rhs
             const int h = wid - 2;
-            if (!__all(!need3 || fv == epoch) && !wave_wait_all(f3, epoch, L.ctl)) {
+            if (!__all(!need3 || fv == epoch) && !wave_wait_all(f3, epoch, L.ctl, a.smax)) {
                 if (lane == 0) word[4] = 1;
             } else {
                 const int tD = L.oL + (K2 * NT + k - 1) * kTD;
@@ -817,7 +820,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 }
                 double sv = 0.0;
                 if (R - 1 <= NT - 3) {
-                    if (!wave_wait_all(lane == 0 ? L.fS + R - 1 : nullptr, epoch, L.ctl)) {
+                    if (!wave_wait_all(lane == 0 ? L.fS + R - 1 : nullptr, epoch, L.ctl, a.smax)) {
                         aborted = true;
                         break;
                     }
@@ -866,8 +869,8 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                     }
                 }
                 if (__all(okl)) break;
-                if (ld_flag(L.ctl + 2) == epoch || spins >= kSpinMax) {
-                    if (spins >= kSpinMax && lane == 0) {
+                if (ld_flag(L.ctl + 2) == epoch || spins >= a.smax) {
+                    if (spins >= a.smax && lane == 0) {
                         st_flag(L.ctl + 2, epoch);
                         __hip_atomic_fetch_add((gint*)(L.ctl + 3), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
@@ -1009,18 +1012,71 @@ size_t dag_lds_bytes(int NT) {
     return std::max(need, kMinLds);
 }
 
+// Per-device state of the persistent solver. Every k_chol_dag launch of a device, from any
+// context / stream / host thread, goes through chol_dag_solve under its mutex:
+//  - the grid size (CUs - 1 helpers + the chain) is the device's own (partitioned GPUs may differ);
+//  - the LDS attribute is set once per device;
+//  - launches are SERIALISED on the device: a launch on a stream other than the previous one first
+//    waits (hipStreamWaitEvent) for an event recorded at the tail of that stream. Two solves whose
+//    grids each assume the whole chip (LocalMapping's LBA and LoopClosing's GBA, on two contexts:
+//    R:src/imu_mono_realsense.cpp:99-100 spawns both threads) then never hold parts of it at once,
+//    which is the residency the no-deadlock argument rests on. One stream pays nothing.
+struct DagDevState {
+    std::mutex m;
+    int helpers = -1;
+    bool attr = false;
+    bool has_last = false;          // `last` launched the device's most recent solve
+    hipStream_t last = nullptr;
+    hipEvent_t ev = nullptr;        // recorded at the tail of `last` when another stream launches
+    long long launches = 0, handoffs = 0;
+};
+constexpr int kMaxDagDevices = 64;
+DagDevState& dag_dev(int dev) {
+    static DagDevState s[kMaxDagDevices];
+    return s[dev];
+}
+int dag_cur_dev() {
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= kMaxDagDevices) d = 0;
+    return d;
+}
+int helpers_locked(DagDevState& ds, int dev) {
+    if (ds.helpers < 0) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 2) cus = 64;
+        ds.helpers = std::min(kDagMaxHelpers, cus - 1);   // every workgroup of the launch resident: one per CU
+    }
+    return ds.helpers;
+}
+
 }  // namespace
 
 int dag_max_helpers() {
-    static int g = -1;
-    if (g < 0) {
-        int dev = 0, cus = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                    hipSuccess || cus < 2)
-            cus = 64;
-        g = std::min(kDagMaxHelpers, cus - 1);   // every workgroup of the launch resident: one per CU
+    const int dev = dag_cur_dev();
+    DagDevState& ds = dag_dev(dev);
+    std::lock_guard<std::mutex> g(ds.m);
+    return helpers_locked(ds, dev);
+}
+
+void dag_stream_retired(hipStream_t st) {
+    for (int d = 0; d < kMaxDagDevices; d++) {
+        DagDevState& ds = dag_dev(d);
+        std::lock_guard<std::mutex> g(ds.m);
+        if (ds.has_last && ds.last == st) ds.has_last = false;
     }
-    return g;
+}
+
+void dag_device_stats(long long* launches, long long* handoffs) {
+    DagDevState& ds = dag_dev(dag_cur_dev());
+    std::lock_guard<std::mutex> g(ds.m);
+    if (launches) *launches = ds.launches;
+    if (handoffs) *handoffs = ds.handoffs;
+}
+
+unsigned dag_spin_max() {
+    const char* e = std::getenv("ORBHIP_DAG_SPIN_MAX");   // read per call: tests force a timeout with it
+    const long v = e ? std::atol(e) : 0;
+    return v > 0 ? (unsigned)v : kSpinMax;
 }
 
 size_t dag_doubles(int n) {
@@ -1080,21 +1136,41 @@ void dag_plan(const int* rf, int n, int max_helpers, DagPlan& p) {
 hipError_t chol_dag_solve(const double* S, int n, const int* row_first, const double* bs, double* x, int* flag,
                           const DagDev& d, hipStream_t st, const int* gate, unsigned long long* dbg) {
     if (n <= 0 || n > kDagMaxN) return hipErrorInvalidValue;
-    static bool attr = false;
-    if (!attr) {
-        const hipError_t e = hipFuncSetAttribute((const void*)k_chol_dag, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 160 * 1024);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
     DagK a;
     a.S = S; a.bs = bs; a.x = x; a.flag = flag; a.rf = row_first;
     a.buf = d.buf; a.ints = d.ints; a.toff = d.toff; a.tasks = d.tasks; a.gate = gate; a.dbg = dbg;
     a.n = n; a.NT = (n + kT - 1) / kT; a.G = d.G; a.pb = d.pb;
     static const int hs = std::getenv("ORBHIP_DAG_SLEEP") ? std::atoi(std::getenv("ORBHIP_DAG_SLEEP")) : 6;
     a.hsleep = hs;
+    a.smax = dag_spin_max();
+    const int dev = dag_cur_dev();
+    DagDevState& ds = dag_dev(dev);
+    std::lock_guard<std::mutex> g(ds.m);
+    if (d.G > helpers_locked(ds, dev)) return hipErrorInvalidValue;   // a plan made for a larger device
+    if (!ds.attr) {
+        const hipError_t e = hipFuncSetAttribute((const void*)k_chol_dag, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 160 * 1024);
+        if (e != hipSuccess) return e;
+        ds.attr = true;
+    }
+    if (ds.has_last && ds.last != st) {   // device-wide order: after the other stream's solve
+        if (!ds.ev) {
+            const hipError_t e = hipEventCreateWithFlags(&ds.ev, hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        hipError_t e = hipEventRecord(ds.ev, ds.last);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, ds.ev, 0);
+        if (e != hipSuccess) return e;
+        ds.handoffs++;
+    }
     hipLaunchKernelGGL(k_chol_dag, dim3((unsigned)(d.G + 1)), dim3(256), dag_lds_bytes(a.NT), st, a);
-    return hipGetLastError();
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess) {
+        ds.has_last = true;
+        ds.last = st;
+        ds.launches++;
+    }
+    return e;
 }
 
 int chol_dag_test(const double* A, const double* b, double* x, int n, int reps, int max_helpers, float* ms,

@@ -956,6 +956,7 @@ __device__ void ba_reduce_body(const BaArgs& a, int what, double* sh) {
             a.red[2] = m;
         }
     }
+    if ((what & 8) && threadIdx.x == 0) a.red[3] = a.flag[0] ? 0.0 : 1.0;   // the solve failed (summed over ranks)
 }
 
 __global__ __launch_bounds__(1024) void k_ba_reduce(const BaArgs* __restrict__ args, const int* __restrict__ act,
@@ -1291,6 +1292,8 @@ struct BaWorkspace {
     int* h_done = nullptr;     // pinned, mapped: per problem, set by the device when its LM run ends
     int* d_done = nullptr;     // its device address
     size_t done_cap = 0;
+    HBuf<int> hto;             // pinned: the persistent solver's hand-off timeout count per problem
+    long long dag_timeouts = 0, dag_reruns = 0;
 };
 
 BaWorkspace* ba_create() { return new BaWorkspace(); }
@@ -1314,7 +1317,7 @@ struct LmState {
 };
 
 int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B, orbhip_ba_result* const* res,
-                   const volatile int* stop, hipStream_t st, int shard_mode) {
+                   const volatile int* stop, hipStream_t st, int shard_mode, bool no_dag) {
     if (B <= 0 || !probs || !res) return ORBHIP_ERR_ARG;
     if (shard_mode == kShardRccl && (B != 1 || !ws->comm)) return ORBHIP_ERR_ARG;
     for (int b = 0; b < B; b++)
@@ -1347,7 +1350,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     static const int dag_min = std::getenv("ORBHIP_CHOL_DAG_MIN") ? std::atoi(std::getenv("ORBHIP_CHOL_DAG_MIN")) : 128;
     const int dag_helpers = dag_max_helpers();
     for (int b = 0; b < B; b++)
-        pp[b].use_dag = !force_blocked && pp[b].n > 0 && (pp[b].n > kCholSmallN || (B == 1 && pp[b].n >= dag_min));
+        pp[b].use_dag = !no_dag && !force_blocked && pp[b].n > 0 && (pp[b].n > kCholSmallN || (B == 1 && pp[b].n >= dag_min));
     // the per-panel tile lists / the DAG plans (RCCL shards: the envelope is the union over the
     // ranks, known after a collective; their DAG plan is made then, into reserved space)
     parallel_for(B, nth, [&](int b) {
@@ -1838,14 +1841,20 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             }
             hipLaunchKernelGGL(k_ba_backsub, dim3(gx(std::max(maxM, maxP), 256), nt_), dim3(256), 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), nt_), dim3(256), 0, st, dA, d_act, 0, nullptr);
-            hipLaunchKernelGGL(k_ba_reduce, dim3(nt_), dim3(1024), 0, st, dA, d_act, 3);
+            hipLaunchKernelGGL(k_ba_reduce, dim3(nt_), dim3(1024), 0, st, dA, d_act, 3 | 8);
             if (coll(3, 0, 2, 0)) return ORBHIP_ERR_DEVICE;
+            // every shard's solve must agree on success, or the ranks' LM schedules (and so their
+            // collective sequences) diverge: RCCL sums the failure flags, the local model ANDs them
+            if (shard_mode == kShardRccl && coll(3, 3, 1, 0)) return ORBHIP_ERR_DEVICE;
             BAOK(hipGetLastError());
             if (read_red(trial)) return ORBHIP_ERR_DEVICE;
+            bool all_ok = true;
+            for (int b : trial) all_ok = all_ok && ws->h_red[5 * b + 4] != 0.0 && ws->h_red[5 * b + 3] == 0.0;
             std::vector<int> pop, next;
             for (int b : trial) {
                 LmState& s = L[b];
-                const bool ok2 = ws->h_red[5 * b + 4] != 0.0;   // gathered as a double
+                const bool ok2 = shard_mode == kShardNone ? ws->h_red[5 * b + 4] != 0.0   // gathered as a double
+                                                          : all_ok;
                 double tempChi = ok2 ? ws->h_red[5 * b] : dmax;
                 double rho = s.currentChi - tempChi;
                 rho /= (ws->h_red[5 * b + 1] + 1e-3);
@@ -1890,9 +1899,41 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     }
     }   // host-driven rounds
     const double t_solve = now();
+    // ---- hand-off timeouts of the persistent solver: a timed-out solve fails its trial (flag 0),
+    // which must never pass for a g2o rejection. Counted per problem (control word 3), read with
+    // the outputs (no extra synchronisation), agreed over the ranks of a sharded solve. ----
+    int ndag = 0;
+    for (int b = 0; b < B; b++) ndag += pp[b].use_dag ? 1 : 0;
+    if (ndag) {
+        BAOK(ws->hto.ensure(B));
+        for (int b = 0, i = 0; b < B; b++)
+            if (pp[b].use_dag) BAOK(hipMemcpyAsync(ws->hto.p + i++, dd[b].ints + 3, sizeof(int), hipMemcpyDeviceToHost, st));
+    }
     // ---- outputs: e_chi2 of every problem + optimised poses/points, one transfer ----
     BAOK(hipMemcpyAsync(hd, D, sizeof(double) * (nC + nA), hipMemcpyDeviceToHost, st));
     BAOK(hipStreamSynchronize(st));
+    {
+        int timeouts = 0;
+        for (int i = 0; i < ndag; i++) timeouts += ws->hto.p[i];
+        if (shard_mode == kShardRccl) {   // one decision for every rank
+            *ws->h_stop = timeouts;
+            if (hipMemcpyAsync(ws->dstop.p, ws->h_stop, sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
+                ncclAllReduce(ws->dstop.p, ws->dstop.p, 1, ncclInt32, ncclMax, ws->comm, st) != ncclSuccess ||
+                hipMemcpyAsync(ws->h_stop, ws->dstop.p, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
+                return ORBHIP_ERR_DEVICE;
+            timeouts = *ws->h_stop;
+        }
+        if (timeouts > 0) {
+            ws->dag_timeouts += timeouts;
+            // default: solve again on the non-persistent solvers (blocked / single-workgroup), which
+            // reproduce the schedule g2o would have run; ORBHIP_DAG_RERUN=0 reports the timeout
+            const char* e = std::getenv("ORBHIP_DAG_RERUN");
+            if (no_dag || (e && e[0] == '0')) return ORBHIP_ERR_TIMEOUT;
+            ws->dag_reruns++;
+            return ba_solve_batch(ws, probs, B, res, stop, st, shard_mode, true);
+        }
+    }
     parallel_for(B, nth, [&](int b) {
         const Prep& p = pp[b];
         const orbhip_ba_problem* pr = probs[b];
@@ -1933,6 +1974,11 @@ int ba_solve(BaWorkspace* ws, const orbhip_ba_problem* prob, orbhip_ba_result* r
     const orbhip_ba_problem* pp[1] = {prob};
     orbhip_ba_result* rr[1] = {res};
     return ba_solve_batch(ws, pp, 1, rr, stop, st, kShardNone);
+}
+
+void ba_stats(BaWorkspace* ws, long long* timeouts, long long* reruns) {
+    *timeouts = ws ? ws->dag_timeouts : 0;
+    *reruns = ws ? ws->dag_reruns : 0;
 }
 
 int ba_comm_init(BaWorkspace* ws, int nranks, int rank, const void* id) {

@@ -27,8 +27,10 @@ struct GraphKey {
     static constexpr int kWords = 48;
     uint64_t w[kWords] = {};
     int n = 0;
+    bool overflow = false;   // more words than kWords: the key is not exact, never replay it
     GraphKey& add(uint64_t v) {
         if (n < kWords) w[n++] = v;
+        else overflow = true;
         return *this;
     }
     GraphKey& ptr(const void* p) { return add((uint64_t)(uintptr_t)p); }
@@ -37,7 +39,9 @@ struct GraphKey {
         std::memcpy(&u, &f, 4);
         return add(u);
     }
-    bool operator==(const GraphKey& o) const { return n == o.n && std::memcmp(w, o.w, sizeof(uint64_t) * n) == 0; }
+    bool operator==(const GraphKey& o) const {
+        return !overflow && !o.overflow && n == o.n && std::memcmp(w, o.w, sizeof(uint64_t) * n) == 0;
+    }
 };
 
 struct GraphKeyHash {
@@ -70,7 +74,7 @@ public:
     template <class F>
     int run(const GraphKey& key, hipStream_t st, bool direct, F&& fn) {
         const char* on = std::getenv("ORBHIP_GRAPH");
-        if (!on || !on[0] || on[0] == '0' || direct || st == nullptr || key.n >= GraphKey::kWords) return fn(st);
+        if (!on || !on[0] || on[0] == '0' || direct || st == nullptr || key.overflow) return fn(st);
         hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
         if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return fn(st);
         auto it = map_.find(key);

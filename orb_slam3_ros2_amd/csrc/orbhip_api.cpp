@@ -688,6 +688,7 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
         FrameBufs fb;
         fb.in = d_imgs; fb.in_stride = stride; fb.in_fstride = fstride; fb.pyr = c->d_pyr.p;
         StageTimer& tm = c->timer;
+        const StageScope scope(tm);
         tm.begin(1, st);
         // the cone recomputes each tile's halo on every level: it pays only while the per-level
         // cascade is launch-latency bound (a few work-groups per CU); big batches keep the cascade
@@ -842,6 +843,7 @@ int orbhip_destroy(orbhip_ctx* c) {
     if (c->timer.created)
         for (int i = 0; i < 2 * StageTimer::kCap; i++) (void)hipEventDestroy(c->timer.ev[i]);
     ba_destroy(c->ba);
+    if (c->stream) dag_stream_retired(c->stream);   // before the stream goes: no solve may wait on it
     pose_ws_destroy(c->pose);
     proj_ws_destroy(c->proj);
     c->plans.clear();
@@ -1070,6 +1072,16 @@ int orbhip_ba_solve(orbhip_ctx* c, const orbhip_ba_problem* prob, orbhip_ba_resu
     if (!c->ba) c->ba = ba_create();
     if (!c->ba) return ORBHIP_ERR_DEVICE;
     return ba_solve(c->ba, prob, res, stop, c->stream);
+}
+
+int orbhip_ba_stats(orbhip_ctx* c, int64_t out[4]) {
+    if (!c || !out) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    long long l = 0, h = 0, t = 0, r = 0;
+    dag_device_stats(&l, &h);
+    ba_stats(c->ba, &t, &r);
+    out[0] = l; out[1] = h; out[2] = t; out[3] = r;
+    return ORBHIP_OK;
 }
 
 int orbhip_ba_solve_batch(orbhip_ctx* c, const orbhip_ba_problem* probs, int B, orbhip_ba_result* res,

@@ -47,6 +47,15 @@ struct StageTimer {
         if (s == stage && g_stage_timer == this) { g_stage_timer = nullptr; if (used) n++; }
     }
 };
+// closes whatever stage of `t` is still open when the scope ends (an early error return between
+// begin() and end() must not leave g_stage_timer pointing at a timer that may be destroyed later)
+struct StageScope {
+    StageTimer& t;
+    explicit StageScope(StageTimer& tm) : t(tm) {}
+    ~StageScope() {
+        if (g_stage_timer == &t) g_stage_timer = nullptr;
+    }
+};
 
 // every pipeline-stage kernel launches through this (the stage timer's events when one is open)
 #define ORBHIP_LAUNCH(kern, grid, block, shm, st, ...)                                                          \

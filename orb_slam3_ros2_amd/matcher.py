@@ -174,18 +174,31 @@ class ProjFrame:
         self._c = None
 
     def to_c(self) -> FrameC:
-        """The C view (built once: a ProjFrame is not modified after construction; it holds the
-        arrays the view points into)."""
-        if self._c is not None:
-            return self._c
-        c = FrameC()
-        c.n = self.kps.shape[0]
-        c.kps, c.desc, c.claimed = ptr(self.kps), ptr(self.desc), ptr(self.claimed)
-        c.min_x, c.max_x, c.min_y, c.max_y = self.bounds
-        c.scale_factors, c.n_levels, c.log_scale_factor = ptr(self.scale_factors), len(self.scale_factors), \
-            self.log_scale_factor
-        c.fx, c.fy, c.cx, c.cy = self.fx, self.fy, self.cx, self.cy
-        c.pose_q[:] = [float(v) for v in self.pose_q]
-        c.pose_t[:] = [float(v) for v in self.pose_t]
-        self._c = c
+        """The C view. The pointer fields are cached while kps / desc / claimed / scale_factors are
+        the same array objects (Tracking keeps them between SearchByProjection and
+        SearchLocalPoints); a reassigned array is converted again and its pointer refreshed. The
+        scalars (pose, bounds, intrinsics) are re-filled on every call: Tcw changes in place after
+        PoseOptimization."""
+        arrs = (self.kps, self.desc, self.claimed, self.scale_factors)
+        hit = self._c
+        if hit is None or any(a is not b for a, b in zip(hit[0], arrs)):
+            self.kps = np.ascontiguousarray(self.kps, KP_DTYPE)
+            self.desc = np.ascontiguousarray(self.desc, np.uint8).reshape(-1, 32)
+            if self.claimed is not None:
+                self.claimed = np.ascontiguousarray(self.claimed, np.uint8)
+            self.scale_factors = np.ascontiguousarray(self.scale_factors, np.float32)
+            c = FrameC()
+            c.n = self.kps.shape[0]
+            c.kps, c.desc, c.claimed = ptr(self.kps), ptr(self.desc), ptr(self.claimed)
+            c.scale_factors, c.n_levels = ptr(self.scale_factors), len(self.scale_factors)
+            # the view keeps the arrays it points into alive
+            self._c = hit = ((self.kps, self.desc, self.claimed, self.scale_factors), c)
+        c = hit[1]
+        if self.claimed is not None and self.claimed.shape[0] < c.n:
+            raise ValueError("ProjFrame.claimed shorter than kps")
+        c.min_x, c.max_x, c.min_y, c.max_y = (float(b) for b in self.bounds)
+        c.log_scale_factor = float(self.log_scale_factor)
+        c.fx, c.fy, c.cx, c.cy = float(self.fx), float(self.fy), float(self.cx), float(self.cy)
+        c.pose_q[:] = [float(v) for v in np.asarray(self.pose_q, np.float32).reshape(4)]
+        c.pose_t[:] = [float(v) for v in np.asarray(self.pose_t, np.float32).reshape(3)]
         return c

@@ -202,6 +202,14 @@ class Optimizer:
         check(lib().orbhip_ba_solve_sharded(self.ctx.handle, ctypes.byref(pc), cres, sf), "orbhip_ba_solve_sharded")
         return self._fill(outs, cres)[0]
 
+    def stats(self) -> dict:
+        """orbhip_ba_stats: persistent-Cholesky launches on this device (all contexts), those that
+        first waited for another stream's solve, the hand-off timeouts this context saw and the
+        solves it re-ran on the non-persistent solvers."""
+        out = (ctypes.c_int64 * 4)()
+        check(lib().orbhip_ba_stats(self.ctx.handle, out), "orbhip_ba_stats")
+        return dict(dag_launches=out[0], dag_handoffs=out[1], dag_timeouts=out[2], dag_reruns=out[3])
+
     def LocalBundleAdjustment(self, prob: BAProblem, stop_flag=None) -> BAResult:
         return self.solve(prob, stop_flag)
 

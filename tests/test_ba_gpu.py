@@ -114,17 +114,6 @@ def test_gba_blocked_cholesky_parity(opt, oracle, n_kf, n_pts, window):
     assert g.final_chi2 < 0.2 * g.initial_chi2
 
 
-@pytest.fixture(scope="module")
-def c5_case(oracle):
-    """C5 at its full size (BASELINE configs[4]): 400 KF loop / 20k points / 80k obs, 20-KF
-    co-visibility window, n = 2394, BundleAdjustment(nIterations=10, bRobust=true); the oracle
-    solve (~20 s on one core) is shared by the tests below."""
-    from orb_slam3_ros2_amd.optimizer import BAProblem
-    prob, _ = synthetic_ba_problem(n_kf=400, n_pts=20000, layout="loop", window=20, seed=11)
-    p = BAProblem(**{**prob.__dict__, "iterations": 10, "huber_delta": float(np.sqrt(5.99))})
-    return prob, p, oracle.ba_solve(p)
-
-
 def test_gba_c5_full_size_parity(opt, c5_case):
     prob, p, o = c5_case
     g = opt.BundleAdjustment(prob, nIterations=10, bRobust=True)

@@ -125,3 +125,44 @@ def test_projection_ragged_sizes(oracle, proj_mode):
         assert r[0] == o[0], (n_kp, n_mp, proj_mode)
         for a, b in zip(r[1:], o[1:]):
             assert np.array_equal(a, b), (n_kp, n_mp, proj_mode)
+
+
+def test_proj_frame_view_tracks_pose_and_arrays():
+    """ProjFrame.to_c(): the pose / bounds / intrinsics are re-read on every call (Tracking updates
+    Tcw in place after PoseOptimization), reassigned arrays get fresh pointers, unchanged arrays
+    keep theirs (no conversion per call)."""
+    s = synthetic_projection_scene(n_kp=50, n_mp=10, seed=5)
+    f = _frame(s)
+    c0 = f.to_c()
+    kp_ptr, cl_ptr = c0.kps, c0.claimed
+    f.pose_q[:] = [0.0, 0.0, 0.0, 1.0]
+    f.pose_t[:] = [0.5, -0.25, 2.0]
+    c1 = f.to_c()
+    assert list(c1.pose_q) == [0.0, 0.0, 0.0, 1.0] and list(c1.pose_t) == [0.5, -0.25, 2.0]
+    assert c1.kps == kp_ptr and c1.claimed == cl_ptr
+    f.claimed = np.zeros(50, np.uint8)
+    f.fx = 123.0
+    c2 = f.to_c()
+    assert c2.claimed == f.claimed.ctypes.data and c2.claimed != cl_ptr and c2.fx == 123.0
+    assert c2.kps == kp_ptr
+
+
+@pytest.mark.gpu
+def test_pose_change_between_searches(oracle):
+    """The same ProjFrame searched, its Tcw changed in place (PoseOptimization), searched again:
+    the second search uses the new pose (oracle on the same frame)."""
+    from orb_slam3_ros2_amd import ORBmatcher
+    s = synthetic_projection_scene(seed=50)
+    f = _frame(s)
+    mt = ORBmatcher(0.9, True)
+    for step in range(3):
+        n, m = mt.SearchByProjectionLastFrame(f, s["points"], s["mp_desc"], s["last_octave"], s["last_angle"], 15.0)
+        on, om = oracle.search_by_projection_last(f, s["points"], s["mp_desc"], s["last_octave"], s["last_angle"],
+                                                  15.0, True)
+        assert n == on and np.array_equal(m, om), step
+        r = ORBmatcher(0.8, False).SearchLocalPoints(f, s["points"], s["normals"], s["min_dist"], s["max_dist"],
+                                                     s["mp_desc"], s["skip"], th=3.0)
+        o = oracle.search_local_points(f, s["points"], s["normals"], s["min_dist"], s["max_dist"], s["mp_desc"],
+                                       s["skip"], th=3.0, nnratio=0.8)
+        assert r[0] == o[0] and all(np.array_equal(a, b) for a, b in zip(r[1:], o[1:])), step
+        f.pose_t[:] = f.pose_t + np.float32([0.02, -0.01, 0.03])   # in place, as Tracking does
