@@ -18,11 +18,12 @@ constexpr int kDagMaxHelpers = 255;   // helper workgroups (+ the chain workgrou
 // workgroup, in the order the workgroup runs them (dependency key order, deadlock-free)
 struct DagPlan {
     int NT = 0, G = 0;
+    int nti = 0;              // partial solve: tiles [0, nti) factored, the trailing block update-only
     int pb = 0;               // backward substitution over the helpers (long rows) or in the chain
     std::vector<int> toff;    // G + 1 offsets into tasks
     std::vector<int> tasks;
 };
-void dag_plan(const int* row_first, int n, int max_helpers, DagPlan& p);
+void dag_plan(const int* row_first, int n, int max_helpers, DagPlan& p, int nti = 0);
 int dag_max_helpers();   // min(kDagMaxHelpers, CUs - 1) of the current device: the whole grid resident
 // a stream about to be destroyed: no later solve of another stream may record an event on it
 void dag_stream_retired(hipStream_t st);
@@ -57,6 +58,35 @@ constexpr int kDbgWords = 8 + 6 * 200;
 hipError_t chol_dag_solve(const double* S, int n, const int* row_first, const double* bs, double* x, int* flag,
                           const DagDev& d, hipStream_t st, const int* gate = nullptr,
                           unsigned long long* dbg = nullptr);
+
+// One problem of a multi-problem launch (the interiors of a nested dissection, ba_nd.hip): the
+// solved matrix is S (row stride ld) through perm (row / column i = S's perm[i], -1 = padding:
+// identity), n x n. nti > 0: partial solve (n > 32 nti): tiles [0, nti) are factored (L, Linv, y
+// in d.buf as a full solve leaves them), and each trailing tile (R, C >= nti) inside the envelope
+// receives -sum_{p < nti} L_Rp L_Cp^T (stored where its L tile would be, the trailing rows' rhs
+// -sum L_Rp y_p at the rhs-partial slot R); flag[0] = the factored block's pivots were positive.
+struct DagProb {
+    const double* S;
+    int ld;
+    const int* perm;
+    int n, nti;
+    const int* rf;
+    const double* bs;
+    double* x;
+    int* flag;
+    DagDev d;
+};
+size_t dag_k_bytes();   // bytes of one problem's launch record
+// fills np launch records (host_ks: np * dag_k_bytes()) and host_wgoff (np + 1): returns the grid
+int dag_multi_fill(const DagProb* probs, int np, void* host_ks, int* host_wgoff, const int* gate, size_t* lds);
+// the records / offsets uploaded to the device: one launch, every problem's chain and helpers
+hipError_t chol_dag_multi_launch(const void* d_ks, const int* d_wgoff, int np, int grid, size_t lds, hipStream_t st);
+// offsets (doubles) of a problem's DAG buffer: tile (R, C) of L (quadrant layout), the rhs partial of
+// tile row R, y of tile row R
+__host__ __device__ inline size_t dag_off_L(int NT, int R, int C) { return ((size_t)R * NT + C) * kDagTile * kDagTile; }
+__host__ __device__ inline size_t dag_off_Linv(int NT, int k) { return ((size_t)NT * NT + 3 * (size_t)NT + k) * kDagTile * kDagTile; }
+__host__ __device__ inline size_t dag_off_y(int NT, int k) { return ((size_t)NT * NT + 4 * (size_t)NT) * kDagTile * kDagTile + (size_t)k * kDagTile; }
+__host__ __device__ inline size_t dag_off_R(int NT, int k) { return dag_off_y(NT, 0) + ((size_t)NT + k) * kDagTile; }
 
 // test hook: A dense SPD (its structure -> row_first), reps timed solves; ms = device ms per solve;
 // dbg as above (optional); returns 0, -4 on a failed pivot, -5 on a hand-off timeout

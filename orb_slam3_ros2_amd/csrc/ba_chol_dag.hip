@@ -71,6 +71,10 @@ struct DagK {
     int pb;       // backward over the helpers (dag_helper_backward) or in the chain alone
     int hsleep;   // helpers' poll back-off (units of s_sleep 1)
     unsigned smax;   // polls before a wait gives up (timeout: ctl[2] abort, ctl[3] counted)
+    int ld;          // row stride of S
+    const int* perm; // nullptr: S itself; else row / column i of the solved matrix is S's perm[i] (-1: padding)
+    int nti;         // partial mode (> 0): tiles [0, nti) are factored; every tile (R, C >= nti) only receives
+                     // the updates of columns < nti (A = 0 there: the eliminated block's Schur contribution)
 };
 
 __device__ __forceinline__ int ld_flag(const int* p) {
@@ -121,20 +125,36 @@ __device__ __forceinline__ void sq(double* base, const double4_t& v) {
 __device__ __forceinline__ int qidx(int r, int c) {
     return (((r >> 4) * 2 + (c >> 4)) * 256) + (((r & 15) + 16 * (c & 3)) * 4) + ((c & 15) >> 2);
 }
-// quadrant (a, b) of tile (R, C) of S (plain loads: written by earlier kernels only); the lower
-// triangle is read (mirrored above the diagonal), identity outside the matrix
-__device__ __forceinline__ double4_t s_quad(const double* __restrict__ S, int n, int R, int C, int a, int b) {
+// element (r, c) of the solved matrix (plain loads: S is written by earlier kernels only): the
+// lower triangle of S is read (mirrored above the diagonal); identity outside the matrix and on
+// padding rows of a permuted matrix; zero in the trailing block of a partial solve
+__device__ __forceinline__ double s_elem(const DagK& k, int r, int c) {
+    const bool in = r < k.n && c < k.n;
+    int pr = r, pc = c;
+    bool z = !in;
+    if (k.perm && in) {
+        pr = k.perm[r];
+        pc = k.perm[c];
+        z = pr < 0 || pc < 0;
+    }
+    if (k.nti && r >= kT * k.nti && c >= kT * k.nti) z = true;   // the separator block: contributions only
+    const size_t off = z ? 0 : (pr >= pc ? (size_t)pr * k.ld + pc : (size_t)pc * k.ld + pr);
+    const double s = k.S[off];
+    return z ? (r == c && (!in || r < kT * k.nti || !k.nti) ? 1.0 : 0.0) : s;
+}
+// right-hand side entry i (zero on padding and in the trailing block of a partial solve)
+__device__ __forceinline__ double s_rhs(const DagK& k, int i) {
+    if (i >= k.n || (k.nti && i >= kT * k.nti)) return 0.0;
+    const int pi = k.perm ? k.perm[i] : i;
+    return pi < 0 ? 0.0 : k.bs[pi];
+}
+// quadrant (a, b) of tile (R, C) of the solved matrix, in the quadrant layout
+__device__ __forceinline__ double4_t s_quad(const DagK& k, int R, int C, int a, int b) {
     const int lane = threadIdx.x & 63;
     const int r = kT * R + 16 * a + (lane & 15);
     double4_t v;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int c = kT * C + 16 * b + (lane >> 4) + 4 * q;
-        const bool in = r < n && c < n;
-        const size_t off = !in ? 0 : (r >= c ? (size_t)r * n + c : (size_t)c * n + r);
-        const double s = S[off];
-        v[q] = in ? s : (r == c ? 1.0 : 0.0);
-    }
+    for (int q = 0; q < 4; q++) v[q] = s_elem(k, r, kT * C + 16 * b + (lane >> 4) + 4 * q);
     return v;
 }
 // c4 -= A B^T in the transposed C layout (a: L_Jk quadrant, b: L_Ik quadrant -> C_IJ^T)
@@ -285,13 +305,12 @@ __device__ void dag_helper_backward(const DagK& a, const Lay& L, __amdgpu_buffer
 // ---------------------------------------------------------------------------------------------
 // helper workgroup: its tasks in order
 // ---------------------------------------------------------------------------------------------
-__device__ void dag_helper(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs, int epoch, double* lds) {
+__device__ void dag_helper(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs, int epoch, double* lds, int h) {
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, cc = lane & 15, rg = lane >> 4;
     const int rq = wid >> 1, cq = wid & 1, quad = 2 * rq + cq;
     const int NT = a.NT;
     double* Tx = lds + 2048;
     int* word = (int*)(lds + 4096);
-    const int h = blockIdx.x - 1;
     const int t0 = a.toff[h], t1 = a.toff[h + 1];
     int wsel = 0;   // rotating LDS word of the poll results
     auto wg_prefix = [&](const int* fa, const int* fb, const int* fc, int cnt) -> int {
@@ -308,23 +327,26 @@ __device__ void dag_helper(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t r
         const int code = a.tasks[t];
         const int R = code >> 16, C = code & 0xFFFF;
         // by R - C: 0 the diagonal partial (columns <= C-3), 1 the sub-diagonal partial (<= C-3), 2
-        // the second sub-diagonal's partial (<= C-2), >= 3 a full tile (every column, then the TRSM)
+        // the second sub-diagonal's partial (<= C-2), >= 3 a full tile (every column, then the TRSM);
+        // 3: a tile of a partial solve's trailing block (C >= nti): every column < nti, no TRSM
         const int dRC = R - C;
-        const int type = dRC >= 3 ? 2 : (dRC == 0 ? 0 : 1);
-        const int ps = max(a.rf[R], a.rf[C]), pe = dRC >= 3 ? C : (dRC == 2 ? C - 1 : C - 2);
-        double4_t acc = s_quad(a.S, a.n, R, C, rq, cq);
-        const bool rhs = type == 0 && cq == 0;
-        const bool skip = type == 0 && quad == 1;   // the upper quadrant of a diagonal tile: unused
+        const bool upd = a.nti && C >= a.nti;
+        const int type = upd ? 3 : (dRC >= 3 ? 2 : (dRC == 0 ? 0 : 1));
+        const int ps = max(a.rf[R], a.rf[C]), pe = upd ? a.nti : (dRC >= 3 ? C : (dRC == 2 ? C - 1 : C - 2));
+        double4_t acc = s_quad(a, R, C, rq, cq);
+        const bool dg = type == 0 || (upd && dRC == 0);   // a diagonal tile: with its right-hand side
+        const bool rhs = dg && cq == 0;
+        const bool skip = dg && quad == 1;   // the upper quadrant of a diagonal tile: unused
         double rv = 0.0;
         if (rhs) {
             const int i = kT * R + 16 * rq + cc;
-            rv = i < a.n ? a.bs[i] : 0.0;
+            rv = s_rhs(a, i);
         }
         bool fail = false;
         for (int p = ps; p < pe && !fail;) {
             const int cnt = min(64, pe - p);
             const int m = wg_prefix(L.fL + R * NT + p, R != C ? L.fL + C * NT + p : nullptr,
-                                    type == 0 ? L.fCh + p : nullptr, cnt);
+                                    dg ? L.fCh + p : nullptr, cnt);
             if (m == 0) {
                 fail = true;
                 break;
@@ -357,6 +379,10 @@ __device__ void dag_helper(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t r
             panel_add(out, qload(rs, li + (2 * cq) * 256), lq(Tx + (2 * rq) * 256));
             if (cq == 1) panel_add(out, qload(rs, li + 3 * 256), lq(Tx + (2 * rq + 1) * 256));
             qstore(rs, L.oL + (R * NT + C) * kTD + quad * 256, out);
+            target = L.fL + R * NT + C;
+        } else if (type == 3) {   // the trailing block's contribution, where its L tile would be
+            qstore(rs, L.oL + (R * NT + C) * kTD + quad * 256, acc);
+            if (rhs && rg == 0) st_sc1(a.buf + L.oR + R * kT + 16 * rq + cc, rv);
             target = L.fL + R * NT + C;
         } else {
             qstore(rs, L.oP + (dRC * NT + C) * kTD + quad * 256, acc);
@@ -497,22 +523,22 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     sq(lds + 2048 + quad * 256, double4_t{0, 0, 0, 0});
     sq(lds + 4096 + quad * 256, double4_t{0, 0, 0, 0});
     if (NT > 1) {
-        sq(lds + 6144 + quad * 256, a.rf[1] <= 0 ? s_quad(a.S, n, 1, 0, rq, cq) : double4_t{0, 0, 0, 0});
-        sq(lds + 8192 + quad * 256, s_quad(a.S, n, 1, 1, rq, cq));
+        sq(lds + 6144 + quad * 256, a.rf[1] <= 0 ? s_quad(a, 1, 0, rq, cq) : double4_t{0, 0, 0, 0});
+        sq(lds + 8192 + quad * 256, s_quad(a, 1, 1, rq, cq));
         if (cq == 0 && rg == 0) {
             const int i = kT + 16 * rq + cc;
-            rppB[16 * rq + cc] = i < n ? a.bs[i] : 0.0;
+            rppB[16 * rq + cc] = s_rhs(a, i);
         }
     }
-    if (tid < kT) rvec[tid] = tid < n ? a.bs[tid] : 0.0;
+    if (tid < kT) rvec[tid] = s_rhs(a, tid);
     __syncthreads();
     if (wid == 0) {
         double4_t lin11, l21t;
-        ok = diag_part_a(s_quad(a.S, n, 0, 0, 0, 0), lds, lin11);
+        ok = diag_part_a(s_quad(a, 0, 0, 0, 0), lds, lin11);
         wave_lds_sync();
         const double y0 = quad_matvec(lds, 0, rvec);
         if (rg == 0) ys[cc] = y0;
-        ok = diag_part_b(s_quad(a.S, n, 0, 0, 1, 0), s_quad(a.S, n, 0, 0, 1, 1), lin11, lds, l21t) && ok;
+        ok = diag_part_b(s_quad(a, 0, 0, 1, 0), s_quad(a, 0, 0, 1, 1), lin11, lds, l21t) && ok;
         wave_lds_sync();
         const double r1 = rvec[16 + cc] - lmul_ylds(l21t, ys);
         wave_lds_sync();
@@ -526,9 +552,14 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     // ---- interval k: wave 0 the critical path (row 0 of L(k+1, k), D(0,0), its pivot, then D22's
     // after wave 1's row 1 / D(1,*)); wave 1 row 1 and the publishes; waves 2 / 3 row h of
     // L(k+2, k), of T_{k+1} and of D'_{k+2} ----
-    for (int k = 0; k + 1 < NT; k++) {
+    // a partial solve (nti > 0) runs intervals 0 .. nti-1: the last one forms the trailing block's
+    // first tiles of L (rows of L(nti, nti-1) and L(nti+1, nti-1)) but factors no diagonal tile
+    const int kEnd = a.nti ? a.nti : NT - 1;
+    for (int k = 0; k < kEnd; k++) {
         const unsigned long long tk = dbg ? __builtin_amdgcn_s_memtime() : 0;
         const int k1 = k + 1, K2 = k + 2, cur = k & 1, nxt = cur ^ 1;
+        const bool last = a.nti && k1 >= a.nti;         // tile k+1 is in the trailing block: not factored
+        const bool zT = last, zD = a.nti && K2 >= a.nti;   // T_{k+1} / D'_{k+2} are trailing-block tiles
         double* Lin = lds + 1024 * cur;
         double* LinN = lds + 1024 * nxt;
         double* L1 = lds + 2048 + 1024 * c1;
@@ -548,9 +579,9 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         const int rfc = K2 < NT ? rfl[K2] : 0;
         const bool inEnvU = K2 < NT && rfc <= k, inEnvT = K2 < NT && rfc <= k1;
         const bool needP2 = K2 < NT && max(rfc, rfb) <= k - 2, useU = K2 < NT && k - 1 >= max(rfc, rfb);
-        const bool needP1 = K2 < NT && max(rfc, rfa) <= k - 2, useTp = K2 < NT && k - 1 >= max(rfc, rfa);
-        const bool useTk = inEnvU && inEnv1;   // T_{k+1} -= L(k+2, k) L(k+1, k)^T
-        const bool needP0 = K2 < NT && rfc <= K2 - 3;
+        const bool needP1 = !zT && K2 < NT && max(rfc, rfa) <= k - 2, useTp = !zT && K2 < NT && k - 1 >= max(rfc, rfa);
+        const bool useTk = !zT && inEnvU && inEnv1;   // T_{k+1} -= L(k+2, k) L(k+1, k)^T
+        const bool needP0 = !zD && K2 < NT && rfc <= K2 - 3;
         const int* f3 = nullptr;
         if (wid >= 2) {
             if (lane == 0 && needP2) f3 = L.fP2 + k;
@@ -575,6 +606,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             sq(L1n, l0);
             sq(L1n + 256, l1);
             lds_signal(F1, k + 2);
+            if (!last) {
             // D(0,0) and r0 of tile k+1
             double4_t D = lq(Dp);
             double r0 = rp[cc];
@@ -605,6 +637,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             const double y1 = quad_matvec(LinN, 3, rvec + 16);
             if (rg == 0) ys[k1 * kT + 16 + cc] = y1;
             if (dbg) t_fact += __builtin_amdgcn_s_memtime() - tf;
+            }   // !last
         } else if (wid == 1) {
             // row 1 of L(k+1, k)
             double4_t l0 = {0, 0, 0, 0}, l1 = {0, 0, 0, 0};
@@ -679,19 +712,19 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 for (int c = 0; c < 2; c++) {
                     u[c] = !inEnvU ? double4_t{0, 0, 0, 0}
                                    : (needP2 ? qload(rs, L.oP + (2 * NT + k) * kTD + (2 * h + c) * 256)
-                                             : s_quad(a.S, n, K2, k, h, c));
+                                             : s_quad(a, K2, k, h, c));
                     t[c] = !inEnvT ? double4_t{0, 0, 0, 0}
                                    : (needP1 ? qload(rs, L.oP + (NT + k1) * kTD + (2 * h + c) * 256)
-                                             : s_quad(a.S, n, K2, k1, h, c));
+                                             : s_quad(a, K2, k1, h, c));
                     const int qd = 2 * h + c;   // D' quadrants: wave 2 q0, wave 3 q2 and q3
                     dd[c] = (h == 0 && c == 1) ? double4_t{0, 0, 0, 0}
                                                : (needP0 ? qload(rs, L.oP + K2 * kTD + qd * 256)
-                                                         : s_quad(a.S, n, K2, K2, qd >> 1, qd & 1));
+                                                         : s_quad(a, K2, K2, qd >> 1, qd & 1));
                 }
                 double rr = 0.0;
                 {
                     const int i = kT * K2 + 16 * h + cc;
-                    rr = needP0 ? ld_sc1(a.buf + L.oR + K2 * kT + 16 * h + cc) : (i < n ? a.bs[i] : 0.0);
+                    rr = needP0 ? ld_sc1(a.buf + L.oR + K2 * kT + 16 * h + cc) : s_rhs(a, i);
                 }
                 double4_t o0 = {0, 0, 0, 0}, o1 = {0, 0, 0, 0};
                 if (inEnvU) {
@@ -766,6 +799,20 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             aborted = true;
             break;
         }
+    }
+    if (a.nti) {   // partial solve: L(nti+1, nti-1) (formed by waves 2/3 in the last interval), then done
+        const int R = a.nti + 1, C = a.nti - 1;
+        if (wid == 1 && R < NT && !aborted) {
+            const double* L2c = lds + 4096 + 1024 * c2;
+#pragma unroll
+            for (int qd = 0; qd < 4; qd++) qstore(rs, L.oL + (R * NT + C) * kTD + qd * 256, lq(L2c + qd * 256));
+            drain_stores();
+            if (lane == 0) st_flag(L.fL + R * NT + C, epoch);
+        }
+        if (wid == 0 && lane == 0) word[8] = (ok && !aborted) ? 1 : 0;
+        __syncthreads();
+        if (tid == 0) a.flag[0] = word[8] != 0 ? 1 : 0;
+        return;
     }
     const unsigned long long t_fwd = dbg ? __builtin_amdgcn_s_memtime() : 0;
     double* Lin = lds + 1024 * ((NT - 1) & 1);
@@ -985,26 +1032,42 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     }
 }
 
-__global__ __launch_bounds__(256) void k_chol_dag(DagK a) {
-    if (a.gate && *a.gate != kPhTrial) return;   // device-driven LM: not in a trial (uniform)
+// one problem's workgroup: role 0 the chain, role h + 1 helper h
+__device__ __forceinline__ void dag_run(const DagK& a, int role) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const Lay L(a);
     // epoch of this solve: the counter the last workgroup of the previous solve advanced
     const int epoch = ld_flag(L.ctl) + 1;
     const size_t bytes = ((size_t)a.NT * a.NT + 4 * (size_t)a.NT) * kTD * 8 + (size_t)a.NT * 4 * kT * 8;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.buf, 0, (int)bytes, 0x00020000);
-    if (blockIdx.x == 0) dag_chain(a, L, rs, epoch, lds);
-    else dag_helper(a, L, rs, epoch, lds);
-    // the last workgroup out advances the epoch counter
+    if (role == 0) dag_chain(a, L, rs, epoch, lds);
+    else dag_helper(a, L, rs, epoch, lds, role - 1);
+    // the last workgroup of the problem out advances the epoch counter
     drain_stores();
     __syncthreads();
     if (threadIdx.x == 0) {
         const int old = __hip_atomic_fetch_add((gint*)(L.ctl + 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == (int)gridDim.x - 1) {
+        if (old == a.G) {
             st_flag(L.ctl + 1, 0);
             st_flag(L.ctl, epoch);
         }
     }
+}
+
+__global__ __launch_bounds__(256) void k_chol_dag(DagK a) {
+    if (a.gate && *a.gate != kPhTrial) return;   // device-driven LM: not in a trial (uniform)
+    dag_run(a, blockIdx.x);
+}
+
+// several independent problems in one launch (the interiors of a nested dissection): problem p
+// owns workgroups [wg_off[p], wg_off[p + 1]); the whole grid is resident (one workgroup per CU)
+__global__ __launch_bounds__(256) void k_chol_dag_multi(const DagK* __restrict__ ks, const int* __restrict__ wg_off,
+                                                        int np) {
+    int p = 0;
+    while (p + 1 < np && (int)blockIdx.x >= wg_off[p + 1]) p++;
+    const DagK a = ks[p];
+    if (a.gate && *a.gate != kPhTrial) return;
+    dag_run(a, blockIdx.x - wg_off[p]);
 }
 
 size_t dag_lds_bytes(int NT) {
@@ -1024,7 +1087,7 @@ size_t dag_lds_bytes(int NT) {
 struct DagDevState {
     std::mutex m;
     int helpers = -1;
-    bool attr = false;
+    bool attr = false, attr_multi = false;
     bool has_last = false;          // `last` launched the device's most recent solve
     hipStream_t last = nullptr;
     hipEvent_t ev = nullptr;        // recorded at the tail of `last` when another stream launches
@@ -1088,9 +1151,10 @@ size_t dag_ints(int n) {
     return (4 + NT * NT + 6 * NT + 3) & ~size_t(3);
 }
 
-void dag_plan(const int* rf, int n, int max_helpers, DagPlan& p) {
+void dag_plan(const int* rf, int n, int max_helpers, DagPlan& p, int nti) {
     const int NT = (n + kT - 1) / kT;
     p.NT = NT;
+    p.nti = nti;
     // dependency keys (x20; the chain's interval k publishes at 20k + 6 and waits for the
     // helpers at 20k + 8): every task waits only on smaller keys, so each helper running its
     // tasks in key order with the whole grid resident cannot deadlock
@@ -1099,7 +1163,9 @@ void dag_plan(const int* rf, int n, int max_helpers, DagPlan& p) {
     for (int R = 0; R < NT; R++)
         for (int C = rf[R]; C <= R; C++) {
             const int d = R - C;
-            if (d == 0) {
+            if (nti && C >= nti) {   // partial solve: the trailing block, after every column < nti
+                ts.push_back({20 * nti + 7, R, C});
+            } else if (d == 0) {
                 if (rf[R] <= C - 3) ts.push_back({20 * C - 50, R, C});                            // diagonal partial
             } else if (d == 1) {
                 if (std::max(rf[R], rf[C]) <= C - 3) ts.push_back({20 * C - 50, R, C});           // sub-diagonal partial
@@ -1123,6 +1189,7 @@ void dag_plan(const int* rf, int n, int max_helpers, DagPlan& p) {
         for (int R = 0; R < NT; R++) off += std::max(0, R - 1 - rf[R]);
         const char* e = std::getenv("ORBHIP_DAG_PBACK");
         p.pb = e ? (e[0] == '1' ? 1 : 0) : (off >= 10LL * NT ? 1 : 0);
+        if (nti) p.pb = 0;   // a partial solve has no backward substitution
     }
     p.toff.assign(G + 1, 0);
     p.tasks.resize(ts.size());
@@ -1143,6 +1210,7 @@ hipError_t chol_dag_solve(const double* S, int n, const int* row_first, const do
     static const int hs = std::getenv("ORBHIP_DAG_SLEEP") ? std::atoi(std::getenv("ORBHIP_DAG_SLEEP")) : 6;
     a.hsleep = hs;
     a.smax = dag_spin_max();
+    a.ld = n; a.perm = nullptr; a.nti = 0;
     const int dev = dag_cur_dev();
     DagDevState& ds = dag_dev(dev);
     std::lock_guard<std::mutex> g(ds.m);
@@ -1164,6 +1232,64 @@ hipError_t chol_dag_solve(const double* S, int n, const int* row_first, const do
         ds.handoffs++;
     }
     hipLaunchKernelGGL(k_chol_dag, dim3((unsigned)(d.G + 1)), dim3(256), dag_lds_bytes(a.NT), st, a);
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess) {
+        ds.has_last = true;
+        ds.last = st;
+        ds.launches++;
+    }
+    return e;
+}
+
+size_t dag_k_bytes() { return sizeof(DagK); }
+
+int dag_multi_fill(const DagProb* probs, int np, void* host_ks, int* host_wgoff, const int* gate, size_t* lds) {
+    DagK* ks = static_cast<DagK*>(host_ks);
+    int g = 0;
+    size_t l = 0;
+    const unsigned smax = dag_spin_max();
+    static const int hs = std::getenv("ORBHIP_DAG_SLEEP") ? std::atoi(std::getenv("ORBHIP_DAG_SLEEP")) : 6;
+    for (int i = 0; i < np; i++) {
+        const DagProb& q = probs[i];
+        DagK& a = ks[i];
+        a = DagK{};
+        a.S = q.S; a.bs = q.bs; a.x = q.x; a.flag = q.flag; a.rf = q.rf;
+        a.buf = q.d.buf; a.ints = q.d.ints; a.toff = q.d.toff; a.tasks = q.d.tasks; a.gate = gate; a.dbg = nullptr;
+        a.n = q.n; a.NT = (q.n + kT - 1) / kT; a.G = q.d.G; a.pb = q.d.pb;
+        a.hsleep = hs; a.smax = smax;
+        a.ld = q.ld; a.perm = q.perm; a.nti = q.nti;
+        host_wgoff[i] = g;
+        g += q.d.G + 1;
+        l = std::max(l, dag_lds_bytes(a.NT));
+    }
+    host_wgoff[np] = g;
+    if (lds) *lds = l;
+    return g;
+}
+
+hipError_t chol_dag_multi_launch(const void* d_ks, const int* d_wgoff, int np, int grid, size_t lds, hipStream_t st) {
+    if (np <= 0 || grid <= 0) return hipErrorInvalidValue;
+    const int dev = dag_cur_dev();
+    DagDevState& ds = dag_dev(dev);
+    std::lock_guard<std::mutex> g(ds.m);
+    if (grid > helpers_locked(ds, dev) + 1) return hipErrorInvalidValue;   // one workgroup per CU
+    if (!ds.attr_multi) {
+        const hipError_t e = hipFuncSetAttribute((const void*)k_chol_dag_multi,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return e;
+        ds.attr_multi = true;
+    }
+    if (ds.has_last && ds.last != st) {
+        if (!ds.ev) {
+            const hipError_t e = hipEventCreateWithFlags(&ds.ev, hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        hipError_t e = hipEventRecord(ds.ev, ds.last);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, ds.ev, 0);
+        if (e != hipSuccess) return e;
+        ds.handoffs++;
+    }
+    hipLaunchKernelGGL(k_chol_dag_multi, dim3((unsigned)grid), dim3(256), lds, st, (const DagK*)d_ks, d_wgoff, np);
     const hipError_t e = hipGetLastError();
     if (e == hipSuccess) {
         ds.has_last = true;

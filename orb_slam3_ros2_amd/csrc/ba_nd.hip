@@ -1,0 +1,501 @@
+// Nested dissection of the reduced camera system (ba_nd.h): the plan, the separator assembly and
+// the interiors' back-substitution; the factorizations themselves are the persistent tiled-DAG
+// Cholesky (ba_chol_dag.hip) in its multi-problem partial form and its plain form.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "ba_args.h"
+#include "ba_chol_dag.h"
+#include "ba_nd.h"
+
+namespace orbhip {
+
+namespace {
+
+constexpr int kT = kDagTile;
+
+// element (r, c) of a 32x32 tile in the DAG buffer's quadrant layout (ba_chol_dag.hip qidx)
+__device__ __forceinline__ int tq(int r, int c) {
+    return (((r >> 4) * 2 + (c >> 4)) * 256) + (((r & 15) + 16 * (c & 3)) * 4) + ((c & 15) >> 2);
+}
+
+struct NdSegDev {
+    const double* buf;   // the segment's DAG buffer (L, Linv, y, the trailing block's contributions)
+    const int* rf;       // its tile envelope
+    const int* flag;     // [0]: its interior factored
+    const int* perm;     // local row -> S row (-1 padding)
+    const int* zmap;     // local row nip + j -> separator index
+    int n, NT, nti, nip;
+    int own0, own1;      // local rows of the segment's own separator (written back by this segment)
+};
+
+struct NdDev {
+    const double* S;
+    const double* bs;
+    double* x;
+    int* flag;
+    const int* gate;
+    int ld, K, nZ;
+    const NdSegDev* segs;
+    const int* zg;       // separator index -> S row
+    const int* zsa;      // separator index -> first segment holding it (-1 none), local row zla
+    const int* zla;
+    const int* zsb;      // -> second segment (-1 none), local row zlb
+    const int* zlb;
+    const int* rfZ;
+    double* SZ;
+    double* bZ;
+    const double* xZ;
+    const int* flagZ;
+};
+
+// a segment's trailing-block contribution at local rows (li, lj) (symmetric; zero outside its envelope)
+__device__ __forceinline__ double seg_contrib(const NdSegDev& s, int li, int lj) {
+    if (li < lj) { const int t = li; li = lj; lj = t; }
+    const int R = li / kT, C = lj / kT;
+    if (C < s.rf[R]) return 0.0;
+    return s.buf[dag_off_L(s.NT, R, C) + tq(li % kT, lj % kT)];
+}
+
+// S_Z row i (lower triangle inside its envelope) and bZ[i]: S's entries plus the contributions of
+// the (at most two) segments whose trailing block holds both separator variables
+__global__ __launch_bounds__(256) void k_nd_assemble(NdDev d) {
+    if (d.gate && *d.gate != kPhTrial) return;
+    const int i = blockIdx.x;
+    const int gi = d.zg[i];
+    const int sa = d.zsa[i], sb = d.zsb[i], la = d.zla[i], lb = d.zlb[i];
+    const int c0 = kT * d.rfZ[i / kT];
+    for (int j = c0 + (int)threadIdx.x; j <= i; j += blockDim.x) {
+        const int gj = d.zg[j];
+        double v = gi >= gj ? d.S[(size_t)gi * d.ld + gj] : d.S[(size_t)gj * d.ld + gi];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int sg = h ? sb : sa, li = h ? lb : la;
+            if (sg < 0) continue;
+            const int lj = d.zsa[j] == sg ? d.zla[j] : (d.zsb[j] == sg ? d.zlb[j] : -1);
+            if (lj >= 0) v += seg_contrib(d.segs[sg], li, lj);
+        }
+        d.SZ[(size_t)i * d.nZ + j] = v;
+    }
+    if (threadIdx.x == 0) {
+        double b = d.bs[gi];
+        if (sa >= 0) b += d.segs[sa].buf[dag_off_R(d.segs[sa].NT, la / kT) + la % kT];
+        if (sb >= 0) b += d.segs[sb].buf[dag_off_R(d.segs[sb].NT, lb / kT) + lb % kT];
+        d.bZ[i] = b;
+    }
+}
+
+// one workgroup per segment: x of its separator rows from x_Z, then L_II^T x_I = y_I - L_ZI^T x_Z
+// tile by tile (tile column R: every tile (R', R), R' > R, of the envelope), then the scatter to S's
+// order. A failed factorization anywhere (a segment or the separator system) zeroes x and flag.
+__global__ __launch_bounds__(256) void k_nd_backsolve(NdDev d) {
+    if (d.gate && *d.gate != kPhTrial) return;
+    extern __shared__ double xs[];   // NT x 32, then 8 x 32 partials, 32 s
+    const NdSegDev s = d.segs[blockIdx.x];
+    double* part = xs + s.NT * kT;
+    double* sv = part + 8 * kT;
+    __shared__ int okw;
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        int ok = d.flagZ[0] != 0;
+        for (int r = 0; r < d.K; r++) ok = ok && d.segs[r].flag[0] != 0;
+        okw = ok;
+        if (blockIdx.x == 0) d.flag[0] = ok;
+    }
+    for (int i = tid; i < s.NT * kT; i += blockDim.x) {
+        double v = 0.0;
+        if (i >= s.nip && i < s.n) v = d.xZ[s.zmap[i - s.nip]];
+        xs[i] = v;
+    }
+    __syncthreads();
+    const bool ok = okw != 0;
+    const int c = tid & 31, g = tid >> 5;
+    for (int R = s.nti - 1; R >= 0 && ok; R--) {
+        double acc = 0.0;
+        for (int Rp = R + 1 + g; Rp < s.NT; Rp += 8) {
+            if (R < s.rf[Rp]) continue;
+            const double* t = s.buf + dag_off_L(s.NT, Rp, R);
+            const double* xr = xs + Rp * kT;
+#pragma unroll 8
+            for (int r = 0; r < kT; r++) acc = fma(t[tq(r, c)], xr[r], acc);
+        }
+        part[g * kT + c] = acc;
+        __syncthreads();
+        if (tid < kT) {
+            double v = s.buf[dag_off_y(s.NT, R) + tid];
+            for (int q = 0; q < 8; q++) v -= part[q * kT + tid];
+            sv[tid] = v;
+        }
+        __syncthreads();
+        if (tid < kT) {   // x_R = Linv_R^T s
+            const double* li = s.buf + dag_off_Linv(s.NT, R);
+            double v = 0.0;
+            for (int q = 0; q < kT; q++) v = fma(li[tq(q, tid)], sv[q], v);
+            xs[R * kT + tid] = v;
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < s.nip; i += blockDim.x) {
+        const int p = s.perm[i];
+        if (p >= 0) d.x[p] = ok ? xs[i] : 0.0;
+    }
+    for (int i = s.own0 + tid; i < s.own1; i += blockDim.x) d.x[s.perm[i]] = ok ? xs[i] : 0.0;
+}
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    hipError_t ensure(size_t c) {
+        if (p && c <= n) return hipSuccess;
+        if (p) { (void)hipFree(p); p = nullptr; n = 0; }
+        const hipError_t e = hipMalloc((void**)&p, std::max<size_t>(c, 1) * sizeof(T));
+        if (e == hipSuccess) n = c;
+        return e;
+    }
+};
+template <typename T>
+struct PinBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    ~PinBuf() { if (p) (void)hipHostFree(p); }
+    hipError_t ensure(size_t c) {
+        if (p && c <= n) return hipSuccess;
+        if (p) { (void)hipHostFree(p); p = nullptr; n = 0; }
+        c = std::max<size_t>(c + c / 4, 64);
+        const hipError_t e = hipHostMalloc((void**)&p, c * sizeof(T), hipHostMallocDefault);
+        if (e == hipSuccess) n = c;
+        return e;
+    }
+};
+
+}  // namespace
+
+struct NdWorkspace {
+    DevBuf<double> dbl;
+    DevBuf<int> ints;
+    DevBuf<unsigned char> rec;
+    PinBuf<int> hint;
+    PinBuf<unsigned char> hrec;
+    // launch state of the last nd_setup
+    int K = 0, grid = 0;
+    size_t lds = 0, bs_lds = 0;
+    const void* d_ks = nullptr;
+    const int* d_wgoff = nullptr;
+    NdDev dev{};
+    DagDev dZ{};
+    int* rfZ = nullptr;
+    int* flagZ = nullptr;
+    std::vector<const int*> tw;
+};
+
+NdWorkspace* nd_create() { return new NdWorkspace(); }
+void nd_destroy(NdWorkspace* w) { delete w; }
+
+void nd_timeout_words(const NdWorkspace* w, std::vector<const int*>& out) {
+    out.insert(out.end(), w->tw.begin(), w->tw.end());
+}
+
+bool nd_plan(int np, const int* bi, const int* bj, int nblk, int K, NdPlan& p) {
+    p = NdPlan{};
+    if (np < 8) return false;
+    int wl = 0, wc = 0;
+    for (int b = 0; b < nblk; b++) {
+        const int d = std::abs(bj[b] - bi[b]);
+        wl = std::max(wl, d);
+        wc = std::max(wc, std::min(d, np - d));
+    }
+    const bool cyc = wl > wc;
+    const int w = std::max(1, cyc ? wc : wl);
+    auto tiles = [](int vars) { return (vars + kT - 1) / kT; };
+    p.full_intervals = tiles(6 * np);
+    auto cost = [&](int k, std::vector<int>& seg) {
+        seg.assign(k + 1, 0);
+        for (int r = 0; r <= k; r++) seg[r] = (int)((long long)r * np / k);
+        const int nsep = cyc ? k : k - 1;
+        int mi = 0;
+        for (int r = 0; r < k; r++) {
+            const bool own = cyc || r < k - 1;
+            const int ni = seg[r + 1] - seg[r] - (own ? w : 0);
+            if (ni < w) return -1;   // interiors at least as wide as the band: a block-tridiagonal separator system
+            mi = std::max(mi, tiles(6 * ni));
+        }
+        return mi + tiles(6 * w * nsep) + 3;   // + the assembly / back-substitution / launches
+    };
+    std::vector<int> seg, best_seg;
+    int best = -1, bestK = 0;
+    const int k0 = K > 0 ? K : 2, k1 = K > 0 ? K : std::min(32, np / std::max(1, 2 * w));
+    for (int k = k0; k <= k1; k++) {
+        const int c = cost(k, seg);
+        if (c > 0 && (best < 0 || c < best)) { best = c; bestK = k; best_seg = seg; }
+    }
+    if (best < 0) return false;
+    p.np = np; p.K = bestK; p.w = w; p.cyclic = cyc; p.seg = best_seg; p.est_intervals = best;
+    // a forced K always plans; the automatic choice only when it pays
+    return K > 0 || best * 10 <= p.full_intervals * 7;
+}
+
+int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int nblk, const double* S,
+             const double* bs, double* x, int* flag, const int* gate, hipStream_t st) {
+    const int np = P.np, K = P.K, w = P.w, n = 6 * np;
+    const bool cyc = P.cyclic;
+    const int nsep = cyc ? K : K - 1;
+    const int nZ = 6 * w * nsep;
+    if (K < 2 || nZ <= 0 || nZ > kDagMaxN) return -5;
+    // pose adjacency (both directions, itself included)
+    std::vector<std::vector<int>> adj(np);
+    for (int i = 0; i < np; i++) adj[i].push_back(i);
+    for (int b = 0; b < nblk; b++)
+        if (bi[b] != bj[b]) { adj[bi[b]].push_back(bj[b]); adj[bj[b]].push_back(bi[b]); }
+    // separators: Z_t = poses [seg[t+1] - w, seg[t+1]), separator index 6 w t + ...
+    auto sep_first = [&](int t) { return P.seg[t + 1] - w; };
+    std::vector<int> sep_of(np, -1);
+    for (int t = 0; t < nsep; t++)
+        for (int q = sep_first(t); q < sep_first(t) + w; q++) sep_of[q] = t;
+    struct Seg {
+        int prev, own, i0, i1, nip, n, NT, nti;
+        std::vector<int> perm, rf, zmap;
+        DagPlan plan;
+    };
+    std::vector<Seg> sg(K);
+    const int helpers = dag_max_helpers();
+    const int share = std::max(2, (helpers + 1) / K);   // workgroups per segment (chain + helpers)
+    for (int r = 0; r < K; r++) {
+        Seg& s = sg[r];
+        s.own = (cyc || r < K - 1) ? r : -1;
+        s.prev = (cyc || r > 0) ? (r - 1 + K) % K : -1;
+        s.i0 = P.seg[r];
+        s.i1 = s.own >= 0 ? P.seg[r + 1] - w : P.seg[r + 1];
+        const int ni = 6 * (s.i1 - s.i0);
+        s.nip = (ni + kT - 1) / kT * kT;
+        s.nti = s.nip / kT;
+        s.n = s.nip + (s.prev >= 0 ? 6 * w : 0) + (s.own >= 0 ? 6 * w : 0);
+        s.NT = (s.n + kT - 1) / kT;
+        s.perm.assign(s.n, -1);
+        std::vector<int> pos(np, -1);   // pose -> local row of its first variable
+        for (int q = s.i0; q < s.i1; q++) {
+            pos[q] = 6 * (q - s.i0);
+            for (int c = 0; c < 6; c++) s.perm[6 * (q - s.i0) + c] = 6 * q + c;
+        }
+        int at = s.nip;
+        for (int t : {s.prev, s.own}) {
+            if (t < 0) continue;
+            for (int q = sep_first(t); q < sep_first(t) + w; q++) {
+                pos[q] = at;
+                for (int c = 0; c < 6; c++) {
+                    s.perm[at + c] = 6 * q + c;
+                    s.zmap.push_back(6 * w * t + 6 * (q - sep_first(t)) + c);
+                }
+                at += 6;
+            }
+        }
+        // tile envelope: first coupled local column of every row (padding rows: themselves)
+        s.rf.assign(s.NT, 0);
+        for (int R = 0; R < s.NT; R++) {
+            int f = R;
+            for (int i = kT * R; i < std::min(s.n, kT * R + kT); i++) {
+                int first = i;
+                const int pi = s.perm[i];
+                if (pi >= 0)
+                    for (int q : adj[pi / 6])
+                        if (pos[q] >= 0) first = std::min(first, pos[q]);
+                f = std::min(f, first / kT);
+            }
+            s.rf[R] = f;
+        }
+        dag_plan(s.rf.data(), s.n, share - 1, s.plan, s.nti);
+    }
+    // separator system: envelope from direct couplings and the fill of each segment's elimination
+    std::vector<int> rfZ((nZ + kT - 1) / kT);
+    {
+        std::vector<int> firstZ(nsep);   // first separator index coupled to separator t
+        for (int t = 0; t < nsep; t++) firstZ[t] = 6 * w * t;
+        for (int r = 0; r < K; r++)
+            if (sg[r].prev >= 0 && sg[r].own >= 0) {
+                const int a = sg[r].prev, b = sg[r].own;
+                firstZ[a] = std::min(firstZ[a], 6 * w * b);
+                firstZ[b] = std::min(firstZ[b], 6 * w * a);
+            }
+        for (int q = 0; q < np; q++)
+            if (sep_of[q] >= 0)
+                for (int o : adj[q])
+                    if (sep_of[o] >= 0) firstZ[sep_of[q]] = std::min(firstZ[sep_of[q]], 6 * w * sep_of[o]);
+        for (size_t R = 0; R < rfZ.size(); R++) {
+            int f = (int)R;
+            for (int i = kT * (int)R; i < std::min(nZ, kT * (int)R + kT); i++) f = std::min(f, firstZ[i / (6 * w)] / kT);
+            rfZ[R] = f;
+        }
+    }
+    DagPlan pZ;
+    dag_plan(rfZ.data(), nZ, helpers, pZ);
+    // separator index -> (segment, local row), twice
+    std::vector<int> zg(nZ), zsa(nZ, -1), zla(nZ, -1), zsb(nZ, -1), zlb(nZ, -1);
+    for (int t = 0; t < nsep; t++)
+        for (int j = 0; j < 6 * w; j++) zg[6 * w * t + j] = 6 * sep_first(t) + j;
+    for (int r = 0; r < K; r++) {
+        const Seg& s = sg[r];
+        for (size_t j = 0; j < s.zmap.size(); j++) {
+            const int z = s.zmap[j], l = s.nip + (int)j;
+            if (zsa[z] < 0) { zsa[z] = r; zla[z] = l; }
+            else { zsb[z] = r; zlb[z] = l; }
+        }
+    }
+    // ---- sizes: doubles (128-byte aligned DAG buffers), ints, records ----
+    auto al16 = [](size_t v) { return (v + 15) & ~size_t(15); };
+    size_t nd = 0;
+    std::vector<size_t> o_buf(K);
+    for (int r = 0; r < K; r++) { o_buf[r] = nd; nd = al16(nd + dag_doubles(sg[r].n)); }
+    const size_t o_bufZ = nd; nd = al16(nd + dag_doubles(nZ));
+    const size_t o_SZ = nd; nd = al16(nd + (size_t)nZ * nZ);
+    const size_t o_bZ = nd; nd = al16(nd + nZ);
+    const size_t o_xZ = nd; nd = al16(nd + nZ);
+    size_t ni = 0;
+    auto ai4 = [](size_t v) { return (v + 3) & ~size_t(3); };
+    struct SegOff { size_t perm, rf, ints, toff, tasks, flag, zmap; };
+    std::vector<SegOff> so(K);
+    for (int r = 0; r < K; r++) {
+        const Seg& s = sg[r];
+        so[r].ints = ni; ni = ai4(ni + dag_ints(s.n));
+        so[r].perm = ni; ni = ai4(ni + s.n);
+        so[r].rf = ni; ni = ai4(ni + s.NT);
+        so[r].toff = ni; ni = ai4(ni + s.plan.toff.size());
+        so[r].tasks = ni; ni = ai4(ni + s.plan.tasks.size());
+        so[r].flag = ni; ni = ai4(ni + 4);
+        so[r].zmap = ni; ni = ai4(ni + s.zmap.size());
+    }
+    const size_t oZ_ints = ni; ni = ai4(ni + dag_ints(nZ));
+    const size_t oZ_rf = ni; ni = ai4(ni + rfZ.size());
+    const size_t oZ_toff = ni; ni = ai4(ni + pZ.toff.size());
+    const size_t oZ_tasks = ni; ni = ai4(ni + pZ.tasks.size());
+    const size_t oZ_flag = ni; ni = ai4(ni + 4);
+    const size_t o_zt = ni; ni = ai4(ni + 5 * (size_t)nZ);
+    const size_t o_wg = ni; ni = ai4(ni + K + 1);
+    const size_t kb = (dag_k_bytes() + 15) & ~size_t(15);
+    const size_t rb_ks = 0, rb_segs = K * kb, rb = rb_segs + K * sizeof(NdSegDev);
+    if (W->dbl.ensure(nd) != hipSuccess || W->ints.ensure(ni) != hipSuccess || W->rec.ensure(rb) != hipSuccess ||
+        W->hint.ensure(ni) != hipSuccess || W->hrec.ensure(rb) != hipSuccess)
+        return -3;
+    double* D = W->dbl.p;
+    int* I = W->ints.p;
+    int* H = W->hint.p;
+    std::memset(H, 0, ni * sizeof(int));
+    auto put = [&](size_t off, const std::vector<int>& v) { if (!v.empty()) std::memcpy(H + off, v.data(), v.size() * sizeof(int)); };
+    std::vector<DagProb> probs(K);
+    std::vector<NdSegDev> segs(K);
+    W->tw.clear();
+    for (int r = 0; r < K; r++) {
+        const Seg& s = sg[r];
+        put(so[r].perm, s.perm); put(so[r].rf, s.rf); put(so[r].toff, s.plan.toff); put(so[r].tasks, s.plan.tasks);
+        put(so[r].zmap, s.zmap);
+        DagProb& q = probs[r];
+        q.S = S; q.ld = n; q.perm = I + so[r].perm; q.n = s.n; q.nti = s.nti; q.rf = I + so[r].rf; q.bs = bs;
+        q.x = nullptr; q.flag = I + so[r].flag;
+        q.d = DagDev{D + o_buf[r], I + so[r].ints, I + so[r].toff, I + so[r].tasks, s.plan.G, s.plan.pb};
+        NdSegDev& g = segs[r];
+        g.buf = D + o_buf[r]; g.rf = I + so[r].rf; g.flag = I + so[r].flag; g.perm = I + so[r].perm;
+        g.zmap = I + so[r].zmap; g.n = s.n; g.NT = s.NT; g.nti = s.nti; g.nip = s.nip;
+        g.own0 = g.own1 = 0;
+        if (s.own >= 0) { g.own1 = s.n; g.own0 = s.n - 6 * w; }
+        W->tw.push_back(I + so[r].ints + 3);
+    }
+    put(oZ_rf, rfZ); put(oZ_toff, pZ.toff); put(oZ_tasks, pZ.tasks);
+    {
+        std::vector<int> zt;
+        zt.reserve(5 * (size_t)nZ);
+        for (auto* v : {&zg, &zsa, &zla, &zsb, &zlb}) zt.insert(zt.end(), v->begin(), v->end());
+        put(o_zt, zt);
+    }
+    W->tw.push_back(I + oZ_ints + 3);
+    size_t lds = 0;
+    const int grid = dag_multi_fill(probs.data(), K, W->hrec.p + rb_ks, H + o_wg, gate, &lds);
+    std::memcpy(W->hrec.p + rb_segs, segs.data(), K * sizeof(NdSegDev));
+    if (hipMemcpyAsync(I, H, ni * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(W->rec.p, W->hrec.p, rb, hipMemcpyHostToDevice, st) != hipSuccess)
+        return -3;
+    W->K = K; W->grid = grid; W->lds = lds;
+    W->d_ks = W->rec.p + rb_ks;
+    W->d_wgoff = I + o_wg;
+    NdDev& d = W->dev;
+    d.S = S; d.bs = bs; d.x = x; d.flag = flag; d.gate = gate; d.ld = n; d.K = K; d.nZ = nZ;
+    d.segs = (const NdSegDev*)(W->rec.p + rb_segs);
+    d.zg = I + o_zt; d.zsa = d.zg + nZ; d.zla = d.zsa + nZ; d.zsb = d.zla + nZ; d.zlb = d.zsb + nZ;
+    d.rfZ = I + oZ_rf;
+    d.SZ = D + o_SZ; d.bZ = D + o_bZ; d.xZ = D + o_xZ; d.flagZ = I + oZ_flag;
+    W->dZ = DagDev{D + o_bufZ, I + oZ_ints, I + oZ_toff, I + oZ_tasks, pZ.G, pZ.pb};
+    W->rfZ = I + oZ_rf;
+    W->flagZ = I + oZ_flag;
+    int maxNT = 0;
+    for (const Seg& s : sg) maxNT = std::max(maxNT, s.NT);
+    W->bs_lds = sizeof(double) * ((size_t)maxNT * kT + 9 * kT);
+    return 0;
+}
+
+hipError_t nd_solve(NdWorkspace* W, hipStream_t st) {
+    hipError_t e = chol_dag_multi_launch(W->d_ks, W->d_wgoff, W->K, W->grid, W->lds, st);
+    if (e != hipSuccess) return e;
+    const NdDev& d = W->dev;
+    hipLaunchKernelGGL(k_nd_assemble, dim3((unsigned)d.nZ), dim3(256), 0, st, d);
+    e = chol_dag_solve(d.SZ, d.nZ, W->rfZ, d.bZ, const_cast<double*>(d.xZ), W->flagZ, W->dZ, st, d.gate);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_nd_backsolve, dim3((unsigned)W->K), dim3(256), W->bs_lds, st, d);
+    return hipGetLastError();
+}
+
+int nd_test(const double* A, const double* b, double* x, int np, const int* bi, const int* bj, int nblk, int K,
+            int reps, float* ms, int* K_used) {
+    NdPlan P;
+    if (!nd_plan(np, bi, bj, nblk, K, P)) return -5;
+    if (K_used) *K_used = P.K;
+    const int n = 6 * np;
+    double *dA = nullptr, *db = nullptr, *dx = nullptr;
+    int* dflag = nullptr;
+    int rc = 0;
+    auto ok = [&](hipError_t e) { if (e != hipSuccess && rc == 0) rc = -3; return e == hipSuccess; };
+    ok(hipMalloc((void**)&dA, sizeof(double) * n * n));
+    ok(hipMalloc((void**)&db, sizeof(double) * n));
+    ok(hipMalloc((void**)&dx, sizeof(double) * n));
+    ok(hipMalloc((void**)&dflag, 4 * sizeof(int)));
+    NdWorkspace* W = nd_create();
+    if (rc == 0) {
+        ok(hipMemcpy(dA, A, sizeof(double) * n * n, hipMemcpyHostToDevice));
+        ok(hipMemcpy(db, b, sizeof(double) * n, hipMemcpyHostToDevice));
+        ok(hipMemset(dflag, 0, 4 * sizeof(int)));
+        if (rc == 0 && nd_setup(W, P, bi, bj, nblk, dA, db, dx, dflag, nullptr, nullptr) != 0) rc = -3;
+        if (rc == 0) ok(nd_solve(W, nullptr));   // warm-up
+        ok(hipDeviceSynchronize());
+        hipEvent_t e0, e1;
+        ok(hipEventCreate(&e0));
+        ok(hipEventCreate(&e1));
+        ok(hipEventRecord(e0, nullptr));
+        for (int r = 0; r < reps && rc == 0; r++) ok(nd_solve(W, nullptr));
+        ok(hipEventRecord(e1, nullptr));
+        ok(hipDeviceSynchronize());
+        float t = 0;
+        ok(hipEventElapsedTime(&t, e0, e1));
+        if (ms) *ms = t / std::max(1, reps);
+        int f = 0;
+        ok(hipMemcpy(&f, dflag, sizeof(int), hipMemcpyDeviceToHost));
+        ok(hipMemcpy(x, dx, sizeof(double) * n, hipMemcpyDeviceToHost));
+        std::vector<const int*> tw;
+        nd_timeout_words(W, tw);
+        for (const int* p : tw) {
+            int v = 0;
+            ok(hipMemcpy(&v, p, sizeof(int), hipMemcpyDeviceToHost));
+            if (rc == 0 && v) rc = -7;
+        }
+        if (rc == 0 && !f) rc = -4;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    }
+    nd_destroy(W);
+    (void)hipFree(dA); (void)hipFree(db); (void)hipFree(dx); (void)hipFree(dflag);
+    return rc;
+}
+
+}  // namespace orbhip

@@ -41,6 +41,7 @@
 #include "ba_chol.h"
 #include "ba_chol_blocked.h"
 #include "ba_chol_dag.h"
+#include "ba_nd.h"
 #include "ba_args.h"
 #include "ba_chol_reg.h"
 #include "ba_se3.h"
@@ -1081,6 +1082,8 @@ struct Prep {
     int nslot = 0;
     bool use_dag = false;         // the persistent tiled-DAG Cholesky (ba_chol_dag.hip)
     DagPlan dag;                  // its helper task lists
+    bool use_nd = false;          // nested dissection over the DAG solver (ba_nd.hip): a lone banded GBA
+    NdPlan nd;
     size_t dag_task_cap = 0;      // ints reserved for the lists (RCCL shards: planned after the union envelope)
     size_t o_dag = 0, o_dagi = 0;
     size_t o_red2 = 0;            // workgroup partials of a trial's chi2 / scale (BaArgs::part)
@@ -1294,6 +1297,7 @@ struct BaWorkspace {
     size_t done_cap = 0;
     HBuf<int> hto;             // pinned: the persistent solver's hand-off timeout count per problem
     long long dag_timeouts = 0, dag_reruns = 0;
+    NdWorkspace* nd = nullptr; // nested-dissection solves (created on first use)
 };
 
 BaWorkspace* ba_create() { return new BaWorkspace(); }
@@ -1301,6 +1305,7 @@ BaWorkspace* ba_create() { return new BaWorkspace(); }
 void ba_destroy(BaWorkspace* w) {
     if (!w) return;
     if (w->comm) (void)ncclCommDestroy(w->comm);
+    if (w->nd) nd_destroy(w->nd);
     if (w->h_stop) (void)hipHostFree(w->h_stop);
     if (w->h_done) (void)hipHostFree(w->h_done);
     if (w->h_lam) (void)hipHostFree(w->h_lam);
@@ -1351,11 +1356,29 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     const int dag_helpers = dag_max_helpers();
     for (int b = 0; b < B; b++)
         pp[b].use_dag = !no_dag && !force_blocked && pp[b].n > 0 && (pp[b].n > kCholSmallN || (B == 1 && pp[b].n >= dag_min));
+    // a lone large problem whose S is a narrow (cyclic) block band (a GBA's keyframe loop): nested
+    // dissection, when the plan's chain is shorter (ORBHIP_ND=0 disables it, ORBHIP_ND_K=k forces k
+    // segments, ORBHIP_ND_MIN sets the smallest n considered)
+    {
+        const char* e_nd = std::getenv("ORBHIP_ND");
+        const char* e_k = std::getenv("ORBHIP_ND_K");
+        const char* e_min = std::getenv("ORBHIP_ND_MIN");
+        const int nd_min = e_min ? std::atoi(e_min) : 960;
+        if (shard_mode == kShardNone && B == 1 && pp[0].use_dag && pp[0].n >= nd_min && !(e_nd && e_nd[0] == '0')) {
+            Prep& p = pp[0];
+            if (nd_plan(p.np, p.blk_i.data(), p.blk_j.data(), p.nblk, e_k ? std::atoi(e_k) : 0, p.nd)) {
+                p.use_nd = true;
+                p.use_dag = false;
+            }
+        }
+    }
     // the per-panel tile lists / the DAG plans (RCCL shards: the envelope is the union over the
     // ranks, known after a collective; their DAG plan is made then, into reserved space)
     parallel_for(B, nth, [&](int b) {
         Prep& p = pp[b];
-        if (p.use_dag) {
+        if (p.use_nd) {
+            // planned above; its device data is set up with the problem's buffers (nd_setup)
+        } else if (p.use_dag) {
             if (shard_mode == kShardRccl) {
                 const size_t NT = (p.n + kDagTile - 1) / kDagTile;
                 p.dag_task_cap = (size_t)dag_helpers + 1 + NT * (NT + 1) / 2;
@@ -1573,7 +1596,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     int maxM = 0, maxE = 0, maxP = 0, maxNp = 0, maxBlk = 0, maxN = 0, maxItems = 0, maxFin = 0;
     bool any_large = false, s_written = false;
     // "large": solved on its own (DAG or blocked); the rest share one single-workgroup launch
-    auto large = [&](int b) { return pp[b].use_dag || pp[b].n > kCholSmallN; };
+    auto large = [&](int b) { return pp[b].use_nd || pp[b].use_dag || pp[b].n > kCholSmallN; };
     for (int b = 0; b < B; b++) {
         const Prep& p = pp[b];
         maxM = std::max(maxM, p.M); maxE = std::max(maxE, p.E); maxP = std::max(maxP, p.P);
@@ -1581,13 +1604,16 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         maxItems = std::max(maxItems, (int)(p.items.size() / 4)); maxFin = std::max(maxFin, (int)(p.fin.size() / 3));
         if (large(b)) any_large = true;
         else maxN = std::max(maxN, p.n);
-        if (!p.use_dag && p.n > kCholRegMaxN) s_written = true;   // the LDS and blocked solvers factor S in place
+        if (!p.use_dag && !p.use_nd && p.n > kCholRegMaxN) s_written = true;   // the LDS and blocked solvers factor S in place
     }
     const size_t chol_lds = sizeof(double) * chol_lds_doubles(maxN);
     // every problem on a solver that reads S and never writes it (register / DAG), no shard sums
     const bool s_readonly = !s_written && shard_mode == kShardNone;
     auto large_solve = [&](int b, const int* gate) -> int {
-        if (pp[b].use_dag) {
+        if (pp[b].use_nd) {
+            (void)gate;   // set at nd_setup
+            BAOK(nd_solve(ws->nd, st));
+        } else if (pp[b].use_dag) {
             BAOK(chol_dag_solve(ha[b].S, pp[b].n, ha[b].row_first, ha[b].bs, ha[b].x, ha[b].flag, dd[b], st, gate));
         } else {
             chol_blocked_solve(ha[b].S, pp[b].n, ha[b].Lsave, ha[b].bs, ha[b].x, ha[b].flag, ha[b].row_first, st, gate,
@@ -1673,6 +1699,13 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             c.early_stop = probs[b]->early_stop;
         }
         BAOK(hipMemcpyAsync(dctl, ws->hctl.p, B * sizeof(LmCtl), hipMemcpyHostToDevice, st));
+        for (int b = 0; b < B; b++)
+            if (pp[b].use_nd) {
+                if (!ws->nd) ws->nd = nd_create();
+                if (nd_setup(ws->nd, pp[b].nd, pp[b].blk_i.data(), pp[b].blk_j.data(), pp[b].nblk, ha[b].S, ha[b].bs,
+                             ha[b].x, ha[b].flag, &dctl[b].phase, st) != 0)
+                    return ORBHIP_ERR_DEVICE;
+            }
         int ns = 0;   // problems on the single-workgroup solvers (act slot 3)
         for (int b = 0; b < B; b++)
             if (!large(b)) h_act[2 * B + ns++] = b;
@@ -1902,12 +1935,15 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     // ---- hand-off timeouts of the persistent solver: a timed-out solve fails its trial (flag 0),
     // which must never pass for a g2o rejection. Counted per problem (control word 3), read with
     // the outputs (no extra synchronisation), agreed over the ranks of a sharded solve. ----
-    int ndag = 0;
-    for (int b = 0; b < B; b++) ndag += pp[b].use_dag ? 1 : 0;
+    std::vector<const int*> tw;   // the timeout words of every persistent solve of this call
+    for (int b = 0; b < B; b++) {
+        if (pp[b].use_dag) tw.push_back(dd[b].ints + 3);
+        if (pp[b].use_nd) nd_timeout_words(ws->nd, tw);
+    }
+    const int ndag = (int)tw.size();
     if (ndag) {
-        BAOK(ws->hto.ensure(B));
-        for (int b = 0, i = 0; b < B; b++)
-            if (pp[b].use_dag) BAOK(hipMemcpyAsync(ws->hto.p + i++, dd[b].ints + 3, sizeof(int), hipMemcpyDeviceToHost, st));
+        BAOK(ws->hto.ensure(ndag));
+        for (int i = 0; i < ndag; i++) BAOK(hipMemcpyAsync(ws->hto.p + i, tw[i], sizeof(int), hipMemcpyDeviceToHost, st));
     }
     // ---- outputs: e_chi2 of every problem + optimised poses/points, one transfer ----
     BAOK(hipMemcpyAsync(hd, D, sizeof(double) * (nC + nA), hipMemcpyDeviceToHost, st));

@@ -29,6 +29,7 @@
 #include "kfdb.h"
 #include "ba_chol_blocked.h"
 #include "ba_chol_dag.h"
+#include "ba_nd.h"
 #include "orbhip_kernels.h"
 #include "orbhip_plan.h"
 #include "graph_cache.h"
@@ -1427,6 +1428,13 @@ int orbhip_test_cholesky_dag(const double* A, const double* b, double* x, int n,
     if (!A || !b || !x || n <= 0 || reps < 1) return ORBHIP_ERR_ARG;
     return chol_dag_test(A, b, x, n, reps, max_helpers, ms, dbg);
 }
+// nested-dissection solve of a pose-structured SPD system (ba_nd.hip): K segments (0 = planned)
+int orbhip_test_nd_solve(const double* A, const double* b, double* x, int np, const int* bi, const int* bj, int nblk,
+                         int K, int reps, float* ms, int* K_used) {
+    if (!A || !b || !x || np <= 0 || !bi || !bj || nblk <= 0 || reps < 1) return ORBHIP_ERR_ARG;
+    return nd_test(A, b, x, np, bi, bj, nblk, K, reps, ms, K_used);
+}
+
 int orbhip_test_sincosf(const float* x, float* cs, float* sn, int64_t n) {
     if (!x || !cs || !sn || n <= 0) return ORBHIP_ERR_ARG;
     float *dx = nullptr, *dc = nullptr, *ds = nullptr;

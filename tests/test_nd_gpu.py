@@ -1,0 +1,92 @@
+"""Nested dissection of the reduced camera system (ba_nd.hip; a20 / a22): K partial
+factorizations of the segment interiors in one k_chol_dag_multi launch, the separator system's
+assembly and solve, the interiors' back-substitution.
+
+The solver is checked against numpy's fp64 solve on pose-structured SPD systems built the way a
+GBA's reduced camera system is (a sum of landmark terms over windows of consecutive keyframes, on
+a loop or a line), and through GlobalBundleAdjustment against the oracle LM at the C5 size with the
+dissection on (the default for a lone banded GBA), forced to other segment counts, and off. The
+solver restates the same LL^T in another elimination order: equal to rounding (north_star: 1e-4 on
+the BA; here 1e-9 on the linear solve). Parity unpinned by the reference (oracle/ba_oracle.cpp)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def banded_system(n_pose, w, cyclic, seed, n_land=None):
+    """S = sum of landmark terms v v^T, each over the 6-vectors of a window of <= w + 1 consecutive
+    poses (cyclic: windows wrap around), + a small diagonal; pose blocks (i <= j) of its structure."""
+    rng = np.random.default_rng(seed)
+    n = 6 * n_pose
+    A = np.zeros((n, n))
+    blocks = set()
+    for _ in range(n_land or 6 * n_pose):
+        s = int(rng.integers(0, n_pose if cyclic else n_pose - w))
+        ln = int(rng.integers(2, w + 2))
+        poses = [(s + k) % n_pose for k in range(ln) if cyclic or s + k < n_pose]
+        idx = np.concatenate([np.arange(6 * p, 6 * p + 6) for p in poses])
+        v = rng.normal(size=idx.size)
+        A[np.ix_(idx, idx)] += np.outer(v, v)
+        for a in poses:
+            for b in poses:
+                blocks.add((min(a, b), max(a, b)))
+    for p in range(n_pose):
+        blocks.add((p, p))
+    A += np.eye(n) * 0.5
+    bi = np.array([b[0] for b in sorted(blocks)], np.int32)
+    bj = np.array([b[1] for b in sorted(blocks)], np.int32)
+    return A, rng.normal(size=n), bi, bj
+
+
+def nd_solve(A, b, n_pose, bi, bj, K=0, reps=1):
+    from orb_slam3_ros2_amd._lib import lib
+    L = lib()
+    f = L.orbhip_test_nd_solve
+    f.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_int] * 3 + \
+        [ctypes.c_void_p] * 2
+    x = np.zeros(A.shape[0])
+    ms = ctypes.c_float(0)
+    ku = ctypes.c_int(0)
+    A = np.ascontiguousarray(A)
+    rc = f(A.ctypes.data, b.ctypes.data, x.ctypes.data, n_pose, bi.ctypes.data, bj.ctypes.data, bi.size, K, reps,
+           ctypes.byref(ms), ctypes.byref(ku))
+    return rc, x, ms.value, ku.value
+
+
+@pytest.mark.parametrize("n_pose,w,cyclic,K", [(120, 7, True, 0), (120, 7, True, 2), (120, 7, True, 5),
+                                                (96, 5, False, 3), (96, 5, False, 0), (399, 19, True, 0),
+                                                (399, 19, True, 8), (200, 3, True, 16)])
+def test_nd_solve_matches_numpy(n_pose, w, cyclic, K):
+    A, b, bi, bj = banded_system(n_pose, w, cyclic, seed=n_pose + w + K)
+    rc, x, ms, ku = nd_solve(A, b, n_pose, bi, bj, K)
+    assert rc == 0, rc
+    assert K == 0 or ku == K
+    ref = np.linalg.solve(A, b)
+    err = np.abs(x - ref).max() / np.abs(ref).max()
+    assert err < 1e-9, (err, ku)
+
+
+def test_nd_not_planned_for_a_dense_system():
+    A, b, bi, bj = banded_system(60, 40, False, seed=3)
+    rc, _, _, _ = nd_solve(A, b, 60, bi, bj, 0)
+    assert rc == -5   # ORBHIP_ERR_UNSUPPORTED: the plain solve is the better one
+
+
+@pytest.mark.parametrize("env", [{}, {"ORBHIP_ND_K": "2"}, {"ORBHIP_ND_K": "8"}, {"ORBHIP_ND": "0"}])
+def test_gba_c5_dissection_parity(c5_case, env, monkeypatch):
+    """GlobalBundleAdjustment at the C5 size (n = 2394) with the dissection's default plan, 2 and 8
+    segments, and the plain DAG solve: each equal to the oracle LM (schedule identical, 1e-4)."""
+    from orb_slam3_ros2_amd import Optimizer
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    prob, p, o = c5_case
+    g = Optimizer().BundleAdjustment(prob, nIterations=10, bRobust=True)
+    assert g.iterations_done == o["iterations_done"] and g.lm_trials == o["lm_trials"]
+    assert abs(g.final_chi2 - o["final_chi2"]) <= 1e-4 * abs(o["final_chi2"])
+    q = lambda a: a.astype(np.float64) * np.where(a[:, 3:4] < 0, -1.0, 1.0)   # noqa: E731
+    assert np.abs(q(g.pose_q) - q(o["pose_q"])).max() < 1e-4
+    assert np.abs(g.pose_t.astype(np.float64) - o["pose_t"]).max() / max(1.0, np.abs(o["pose_t"]).max()) < 1e-4
+    assert np.abs(g.points.astype(np.float64) - o["points"]).max() / max(1.0, np.abs(o["points"]).max()) < 1e-4

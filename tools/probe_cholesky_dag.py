@@ -50,6 +50,8 @@ for n_s, shape in cases:
     ki = max(0, min(nt - 1, 200))
     ph = dbg[8:8 + 6 * ki].reshape(ki, 6).astype(np.int64) if ki else np.zeros((1, 6), np.int64)
     med = np.median(ph, axis=0).astype(int) if ki else [0] * 6
+    if os.environ.get("ORBHIP_PROBE_SAVE"):   # raw per-interval words for offline analysis
+        np.save(os.path.join(os.environ["ORBHIP_PROBE_SAVE"], f"dag_{n}_{shape}.npy"), dbg)
     print(f"n={n} {shape}: rc={rc} dag {ms.value * 1e3:.1f} us relerr={err:.2e} | cycles prologue={dbg[0]} "
           f"forward={dbg[1]} backward={dbg[2]} diag={dbg[4]} total={dbg[5]} | interval medians: total {med[0]} "
           f"| wave ends {med[1]} {med[2]} {med[3]} {med[4]} w0 start {int(np.median(ph[:, 5] & 0xFFFFFFFF)) if ki else 0} "
