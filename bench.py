@@ -280,7 +280,9 @@ class FrontendC2:
         return float(np.mean(ns)) if ns else 0.0
 
     def stage_bytes(self):
-        return stage_bytes(self.ext, self.W, self.H, self.mean_keypoints() or 1000.0, 1)
+        torch_sync()
+        self.n_cand = measured_candidates(self.ctx0, self.W, self.H, 1)
+        return stage_bytes(self.ext, self.W, self.H, self.mean_keypoints() or 1000.0, 1, self.n_cand)
 
     def close(self):
         """End the camera streams (the level-table extractor stays)."""
@@ -289,18 +291,37 @@ class FrontendC2:
         self.fss, self.pushes = [], []
 
 
-def stage_bytes(ext, w, h, n_kp, frames):
+def measured_candidates(ctx, w, h, frames=1):
+    """Mean FAST candidates per frame of the context's last extraction (the octree's input,
+    orbhip_test_candidates), None if unavailable."""
+    from orb_slam3_ros2_amd._lib import lib
+    L = lib()
+    try:
+        f = L.orbhip_test_candidates
+    except AttributeError:
+        return None
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    tot, n = 0, ctypes.c_int64(0)
+    for i in range(frames):
+        if f(ctx.handle, w, h, i, ctypes.byref(n)) != 0:
+            return None
+        tot += n.value
+    return tot / max(1, frames)
+
+
+def stage_bytes(ext, w, h, n_kp, frames, n_cand=None):
     """Algorithmic HBM bytes per launch of each stage. Pyramid: at batch <= 4 the
     one-launch cone (k_pyr_cone) reads level 0 once and writes levels 1..7 (A0 + sum_{l>=1} A_l;
     its halo recompute stays on chip), the 7-launch k_resize cascade of bigger batches reads level
     l-1 and writes level l (sum A[:-1] + sum A[1:], all 7 launches). FAST reads every level once,
-    octree reads its packed candidates (8 B) and writes kept keypoints (8 B), desc reads a 43x43
+    octree reads its candidates (8 B each, the measured count n_cand of FAST's output) and writes
+    kept keypoints (8 B), desc reads a 43x43
     patch + writes kp/desc (56 B), match reads query+train descriptors and writes 3 ints per
     query, rot filter 12 B/kp."""
     info = ext.level_info(w, h)
     A = (info["w"].astype(np.int64) * info["h"]).tolist()
     pyr = sum(A) if frames <= 4 else sum(A[:-1]) + sum(A[1:])
-    per = {1: pyr, 2: sum(A), 3: 8.0 * 4500 + 8 * n_kp, 4: n_kp * (43 * 43 + 56),
+    per = {1: pyr, 2: sum(A), 3: 8.0 * (n_cand if n_cand else 4500) + 8 * n_kp, 4: n_kp * (43 * 43 + 56),
            5: 2 * n_kp * 32 + n_kp * 12, 6: n_kp * 12}
     return {k: v * frames for k, v in per.items()}
 
@@ -374,6 +395,11 @@ class PipelinedC3:
     def step(self):
         self.slots[self.k % len(self.slots)].step()
         self.k += 1
+
+
+def torch_sync():
+    import torch
+    torch.cuda.synchronize()
 
 
 def timed(ws, fn, steps, warmup):
@@ -467,23 +493,33 @@ def cpu_lba(prob, budget_s=8.0):
 
 def c5_gba(ws, rank, iters):
     """C5 GlobalBundleAdjustment (400 KF loop, 20k points, 80k obs, 20-KF co-visibility window).
-    With N > 1: landmark shards over the ranks, the reduced camera system summed with an RCCL
-    all-reduce per LM trial (orbhip_ba_solve_sharded); ORBHIP_C5_SHARDED=0 runs
-    replicas instead (every rank the whole problem). Time = max over ranks of one solve."""
+    One GPU: the nested-dissection solve of the reduced camera system (csrc/ba_nd.hip). With N > 1:
+    the keyframe loop cut into N segments, rank r holding segment r's landmarks
+    (sharding.shard_problem_nd): each rank factors its interior, the separator system and the pose
+    update are all-reduced over RCCL inside the device-driven LM (orbhip_ba_solve_sharded, SURVEY.md
+    §8e). ORBHIP_C5_SHARDED=0 runs replicas instead (every rank the whole problem); a segment plan
+    that does not fit (too many ranks for the loop) falls back to contiguous landmark shards with
+    the summed reduced camera system. Time = max over ranks of one solve."""
     import torch
     from orb_slam3_ros2_amd import Optimizer
-    from orb_slam3_ros2_amd.sharding import shard_problem
+    from orb_slam3_ros2_amd.sharding import nd_segments, pose_blocks, shard_problem, shard_problem_nd
     from orb_slam3_ros2_amd.synthetic import synthetic_ba_problem
     prob, _ = synthetic_ba_problem(n_kf=400, n_pts=20000, layout="loop", window=20, seed=11)
     prob.iterations, prob.huber_delta = iters, float(np.sqrt(5.99))   # BundleAdjustment(bRobust)
     opt = Optimizer()
     sharded = ws > 1 and os.environ.get("ORBHIP_C5_SHARDED", "1") != "0"
+    mode = f"replicas x{ws} (one GPU per solve, nested dissection)"
     if sharded:
         import torch.distributed as dist
         uid = [Optimizer.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         opt.comm_init(ws, rank, uid[0])
-        shard = shard_problem(prob, rank, ws)[0]
+        if nd_segments(*pose_blocks(prob), ws) is not None:
+            shard = shard_problem_nd(prob, rank, ws)[0]
+            mode = f"rccl segments x{ws} (interiors per rank, separator system all-reduced)"
+        else:
+            shard = shard_problem(prob, rank, ws)[0]
+            mode = f"rccl landmark shards x{ws} (reduced camera system all-reduced, replicated solve)"
         solve = lambda: opt.solve_sharded(shard)  # noqa: E731
     else:
         solve = lambda: opt.solve(prob)  # noqa: E731
@@ -496,7 +532,7 @@ def c5_gba(ws, rank, iters):
     t = _max_over_ranks(ws, time.perf_counter() - t0)
     return {"c5_gba_ms": round(1e3 * t, 2), "c5_gba_iterations": r.iterations_done, "c5_gba_trials": r.lm_trials,
             "c5_gba_chi2": [round(r.initial_chi2, 1), round(r.final_chi2, 1)],
-            "c5_gba_mode": f"rccl shards x{ws}" if sharded else f"replicas x{ws} (one GPU per solve)",
+            "c5_gba_mode": mode,
             "c5_problem": "400 KF loop / 20000 pts / 80000 obs, n = 2394"}
 
 
@@ -706,6 +742,7 @@ def c2_headline(args, ws, rank):
          "keypoints": c2.mean_keypoints(), "nmatch": c2.last_matches(), "stage_ms": stage_ms, "dom": dom,
          "dom_avg_ms": stage_ms[dom], "dom_n": acc[dom][1]}
     r["dom_bytes"] = c2.stage_bytes()[dom]
+    r["octree_candidates_per_frame"] = c2.n_cand
     r["frames_np"] = c2.frames_np
     r["ctx"] = c2.ext.ctx
     # the camera streams end here, so that the one-camera figures below run with one camera in the
@@ -747,6 +784,19 @@ def c2_headline(args, ws, rank):
 
 
 SIMDS, CUS = 1024, 256   # MI355X: 256 CUs x 4 SIMDs
+
+
+def headline_bound(kernel):
+    """What bounds the headline kernel, read off its committed counters (profiles/counters.json,
+    c2 regime): "latency" when its waves mostly wait and neither VALU nor LDS issue is busy (the
+    HBM fraction is still reported as the line's frac), else the busiest issue resource."""
+    cn = load_counters(kernel, "c2")
+    if not cn:
+        return "latency"
+    valu, lds = cn.get("valu_issue_frac") or 0.0, cn.get("lds_issue_frac") or 0.0
+    if max(valu, lds) >= 0.5:
+        return "valu issue" if valu >= lds else "lds issue"
+    return "latency"
 
 
 def issue_roofline(kernel, regime, alg_bytes, avg_ms):
@@ -805,7 +855,10 @@ def c3_batch(args, ws, rank):
             c3_ms[st] = ms / max(n, 1)
         p3.select(0)
         d3 = max(c3_ms, key=c3_ms.get)
-        b3 = stage_bytes(c3.ext, c3.W, c3.H, float(c3.n.float().mean().item()) or 1000.0, c3.nb)
+        torch_sync()
+        cand3 = measured_candidates(c3.ext.ctx, c3.W, c3.H, c3.nb)
+        b3 = stage_bytes(c3.ext, c3.W, c3.H, float(c3.n.float().mean().item()) or 1000.0, c3.nb, cand3)
+        out["c3_octree_candidates_per_frame"] = cand3
         ks = kernel_symbol(d3, c3.nb)
         out["c3_roofline"] = issue_roofline(ks, "c3", b3[d3], c3_ms[d3])
         out["c3_roofline"]["stage_avg_ms"] = {STAGES[k]: round(v, 4) for k, v in c3_ms.items()}
@@ -921,14 +974,16 @@ def main():
                    "one_camera_8_in_flight_frames_per_s": round(r["one_camera_inflight_fps"], 1),
                    "host_submit_ms_per_frame": round(r["host_submit_ms_per_frame"], 4),
                    "keypoints_per_frame": round(r["keypoints"], 1), "matches_last_pair": r["nmatch"]},
-        "roofline": {"kernel": ks, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+        "roofline": {"kernel": ks, "bound": headline_bound(ks), "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                      "traffic": load_traffic(ks, "c2"), "counters": load_counters(ks, "c2"),
                      "algorithmic_bytes_per_launch": int(r["dom_bytes"]), "avg_launch_ms": round(r["dom_avg_ms"], 5),
                      "launches_timed": r["dom_n"],
-                     "timing": "kernel execution (hipExtLaunchKernelGGL events) over a replay of the timed "
-                               "16-camera stream; rocprofv3 --kernel-trace of this C2 section: "
-                               "profiles/r03_c2_kernel_stats.md",
+                     "timing": "kernel execution span from device timestamps (k_pyr_cone: first workgroup "
+                               "start -> last workgroup end, s_memrealtime; the other stages: "
+                               "hipExtLaunchKernelGGL events) over a replay of the timed 16-camera stream; "
+                               "rocprofv3 --kernel-trace of this C2 section: profiles/r04_c2_kernel_stats.md",
+                     "octree_candidates_per_frame": r.get("octree_candidates_per_frame"),
                      "stage_avg_ms": {STAGES[k]: round(v, 5) for k, v in r["stage_ms"].items()},
                      "stage_avg_ms_one_frame_stream": {STAGES[k]: round(v, 5)
                                                        for k, v in r["stage_ms_one_frame"].items()}},

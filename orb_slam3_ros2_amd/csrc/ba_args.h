@@ -51,7 +51,15 @@ struct BaArgs {
     double* Lsave;     // ceil(n/32) x 1024: L11^{-1} of every Cholesky panel
     const int* row_first;   // ceil(n/32): envelope of S in 32x32 tiles (blocked solver)
     const int* cb_tiles;    // blocked solver: each panel's trailing-update tiles inside the envelope
-    int lead;          // sharded solve: this shard adds the pose-side Hpp + lambda terms (once)
+    int lead;          // sharded solve: this shard adds lambda x_p^2 to the scale (once), and the
+                       // pose-side Hpp + lambda terms to S when `own` is null
+    const unsigned char* own;   // sharded solve by segments: 1 for the poses whose pose-side terms this shard adds
+    const double* Hpp_g;        // the pose Hessians summed over the shards (== Hpp unsharded)
+    int small;         // unsharded, small enough for the trial's last workgroup to restore a rejected state
+                       // and refresh its stale errors itself (no k_ba_pop / k_ba_errors(1) launch per slot)
+    int sync;          // sharded device-driven rounds: the controller's reductions and decisions run as their
+                       // own launches (a collective between them), not in the last workgroup of k_ba_lin /
+                       // k_ba_errors(2)
     // Schur work items (k_ba_schur_items): {k0, k1, blk, slot} over blk_pairs, at most kSchurChunk
     // pairs each; slot -1 = the block's only item (written to S directly), else its partial sum
     // goes to Spart[36 slot] and k_ba_schur_fin adds the block's partials (+ Hpp + lambda on the

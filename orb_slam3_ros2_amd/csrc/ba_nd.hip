@@ -52,6 +52,9 @@ struct NdDev {
     double* bZ;
     const double* xZ;
     const int* flagZ;
+    double* x_loc;       // shard of a distributed solve: its interior + own separator, [n] failure
+    const double* xg;    // the shards' sum of x_loc
+    int n;
 };
 
 // a segment's trailing-block contribution at local rows (li, lj) (symmetric; zero outside its envelope)
@@ -101,11 +104,15 @@ __global__ __launch_bounds__(256) void k_nd_backsolve(NdDev d) {
     double* sv = part + 8 * kT;
     __shared__ int okw;
     const int tid = threadIdx.x;
+    double* xo = d.x_loc ? d.x_loc : d.x;
     if (tid == 0) {
         int ok = d.flagZ[0] != 0;
         for (int r = 0; r < d.K; r++) ok = ok && d.segs[r].flag[0] != 0;
         okw = ok;
-        if (blockIdx.x == 0) d.flag[0] = ok;
+        if (blockIdx.x == 0) {
+            if (d.x_loc) d.x_loc[d.n] = ok ? 0.0 : 1.0;
+            else d.flag[0] = ok;
+        }
     }
     for (int i = tid; i < s.NT * kT; i += blockDim.x) {
         double v = 0.0;
@@ -142,9 +149,34 @@ __global__ __launch_bounds__(256) void k_nd_backsolve(NdDev d) {
     }
     for (int i = tid; i < s.nip; i += blockDim.x) {
         const int p = s.perm[i];
-        if (p >= 0) d.x[p] = ok ? xs[i] : 0.0;
+        if (p >= 0) xo[p] = ok ? xs[i] : 0.0;
     }
-    for (int i = s.own0 + tid; i < s.own1; i += blockDim.x) d.x[s.perm[i]] = ok ? xs[i] : 0.0;
+    for (int i = s.own0 + tid; i < s.own1; i += blockDim.x) xo[s.perm[i]] = ok ? xs[i] : 0.0;
+}
+
+// a shard's last step: the summed x, and the solve's flag (every shard's factorization and the
+// separator system's)
+__global__ __launch_bounds__(256) void k_nd_finish(NdDev d) {
+    if (d.gate && *d.gate != kPhTrial) return;
+    const bool ok = d.xg[d.n] == 0.0 && d.flagZ[0] != 0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < d.n; i += gridDim.x * blockDim.x) d.x[i] = ok ? d.xg[i] : 0.0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) d.flag[0] = ok ? 1 : 0;
+}
+
+// the separator system's lower envelope <-> a packed buffer (tile row R: columns [32 rf[R], 32R + 32))
+__global__ __launch_bounds__(256) void k_nd_env_pack(NdDev d, const long long* __restrict__ toff, double* __restrict__ buf,
+                                                     int dir) {
+    if (d.gate && *d.gate != kPhTrial) return;
+    const int R = blockIdx.y, n = d.nZ;
+    const int c0 = kT * d.rfZ[R], c1 = min(kT * R + kT, n), w = c1 - c0;
+    const int rows = min(kT, n - kT * R);
+    double* tb = buf + toff[R];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < rows * w; i += gridDim.x * blockDim.x) {
+        const int r = i / w, c = i - r * w;
+        double* e = d.SZ + (size_t)(kT * R + r) * n + c0 + c;
+        if (dir == 0) tb[i] = *e;
+        else *e = tb[i];
+    }
 }
 
 template <typename T>
@@ -193,6 +225,10 @@ struct NdWorkspace {
     int* rfZ = nullptr;
     int* flagZ = nullptr;
     std::vector<const int*> tw;
+    DevBuf<long long> envoff;   // packed separator envelope: per tile row offsets
+    DevBuf<double> pack, xl;    // the packed envelope; x_loc and xg (n + 1 each)
+    size_t pack_n = 0;
+    int nZt = 0;                // tile rows of the separator system
 };
 
 NdWorkspace* nd_create() { return new NdWorkspace(); }
@@ -202,47 +238,81 @@ void nd_timeout_words(const NdWorkspace* w, std::vector<const int*>& out) {
     out.insert(out.end(), w->tw.begin(), w->tw.end());
 }
 
-bool nd_plan(int np, const int* bi, const int* bj, int nblk, int K, NdPlan& p) {
-    p = NdPlan{};
-    if (np < 8) return false;
-    int wl = 0, wc = 0;
+void nd_bandwidth(int np, const int* bi, const int* bj, int nblk, int& wl, int& wc) {
+    wl = 0;
+    wc = 0;
     for (int b = 0; b < nblk; b++) {
         const int d = std::abs(bj[b] - bi[b]);
         wl = std::max(wl, d);
         wc = std::max(wc, std::min(d, np - d));
     }
+}
+
+namespace {
+int plan_cost(int np, int w, bool cyc, int k, std::vector<int>& seg) {
+    auto tiles = [](int vars) { return (vars + kT - 1) / kT; };
+    seg.assign(k + 1, 0);
+    for (int r = 0; r <= k; r++) seg[r] = (int)((long long)r * np / k);
+    const int nsep = cyc ? k : k - 1;
+    int mi = 0;
+    for (int r = 0; r < k; r++) {
+        const bool own = cyc || r < k - 1;
+        const int ni = seg[r + 1] - seg[r] - (own ? w : 0);
+        if (ni < w) return -1;   // interiors at least as wide as the band: a block-tridiagonal separator system
+        mi = std::max(mi, tiles(6 * ni));
+    }
+    return mi + tiles(6 * w * nsep) + 3;   // + the assembly / back-substitution / launches
+}
+}  // namespace
+
+bool nd_plan_band(int np, int wl, int wc, int K, NdPlan& p) {
+    p = NdPlan{};
     const bool cyc = wl > wc;
     const int w = std::max(1, cyc ? wc : wl);
-    auto tiles = [](int vars) { return (vars + kT - 1) / kT; };
-    p.full_intervals = tiles(6 * np);
-    auto cost = [&](int k, std::vector<int>& seg) {
-        seg.assign(k + 1, 0);
-        for (int r = 0; r <= k; r++) seg[r] = (int)((long long)r * np / k);
-        const int nsep = cyc ? k : k - 1;
-        int mi = 0;
-        for (int r = 0; r < k; r++) {
-            const bool own = cyc || r < k - 1;
-            const int ni = seg[r + 1] - seg[r] - (own ? w : 0);
-            if (ni < w) return -1;   // interiors at least as wide as the band: a block-tridiagonal separator system
-            mi = std::max(mi, tiles(6 * ni));
-        }
-        return mi + tiles(6 * w * nsep) + 3;   // + the assembly / back-substitution / launches
-    };
-    std::vector<int> seg, best_seg;
+    std::vector<int> seg;
+    const int c = K >= 2 ? plan_cost(np, w, cyc, K, seg) : -1;
+    if (c < 0) return false;
+    p.np = np; p.K = K; p.w = w; p.cyclic = cyc; p.seg = seg; p.est_intervals = c;
+    p.full_intervals = (6 * np + kT - 1) / kT;
+    return true;
+}
+
+bool nd_plan(int np, const int* bi, const int* bj, int nblk, int K, NdPlan& p) {
+    p = NdPlan{};
+    if (np < 8) return false;
+    int wl = 0, wc = 0;
+    nd_bandwidth(np, bi, bj, nblk, wl, wc);
+    const bool cyc = wl > wc;
+    const int w = std::max(1, cyc ? wc : wl);
+    std::vector<int> seg;
     int best = -1, bestK = 0;
     const int k0 = K > 0 ? K : 2, k1 = K > 0 ? K : std::min(32, np / std::max(1, 2 * w));
     for (int k = k0; k <= k1; k++) {
-        const int c = cost(k, seg);
-        if (c > 0 && (best < 0 || c < best)) { best = c; bestK = k; best_seg = seg; }
+        const int c = plan_cost(np, w, cyc, k, seg);
+        if (c > 0 && (best < 0 || c < best)) { best = c; bestK = k; }
     }
-    if (best < 0) return false;
-    p.np = np; p.K = bestK; p.w = w; p.cyclic = cyc; p.seg = best_seg; p.est_intervals = best;
+    if (best < 0 || !nd_plan_band(np, wl, wc, bestK, p)) return false;
     // a forced K always plans; the automatic choice only when it pays
     return K > 0 || best * 10 <= p.full_intervals * 7;
 }
 
+bool nd_blocks_fit(const NdPlan& p, int r, const int* bi, const int* bj, int nblk) {
+    const int K = p.K, w = p.w;
+    const bool own = p.cyclic || r < K - 1, prev = p.cyclic || r > 0;
+    auto in = [&](int q) {
+        if (q >= p.seg[r] && q < p.seg[r + 1]) return true;   // the interior and the own separator
+        if (!prev) return false;
+        const int t = (r - 1 + K) % K, z0 = p.seg[t + 1] - w;
+        return q >= z0 && q < z0 + w;
+    };
+    (void)own;
+    for (int b = 0; b < nblk; b++)
+        if (!in(bi[b]) || !in(bj[b])) return false;
+    return true;
+}
+
 int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int nblk, const double* S,
-             const double* bs, double* x, int* flag, const int* gate, hipStream_t st) {
+             const double* bs, double* x, int* flag, const int* gate, hipStream_t st, int seg_sel) {
     const int np = P.np, K = P.K, w = P.w, n = 6 * np;
     const bool cyc = P.cyclic;
     const int nsep = cyc ? K : K - 1;
@@ -255,9 +325,6 @@ int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int 
         if (bi[b] != bj[b]) { adj[bi[b]].push_back(bj[b]); adj[bj[b]].push_back(bi[b]); }
     // separators: Z_t = poses [seg[t+1] - w, seg[t+1]), separator index 6 w t + ...
     auto sep_first = [&](int t) { return P.seg[t + 1] - w; };
-    std::vector<int> sep_of(np, -1);
-    for (int t = 0; t < nsep; t++)
-        for (int q = sep_first(t); q < sep_first(t) + w; q++) sep_of[q] = t;
     struct Seg {
         int prev, own, i0, i1, nip, n, NT, nti;
         std::vector<int> perm, rf, zmap;
@@ -265,7 +332,8 @@ int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int 
     };
     std::vector<Seg> sg(K);
     const int helpers = dag_max_helpers();
-    const int share = std::max(2, (helpers + 1) / K);   // workgroups per segment (chain + helpers)
+    const int KL = seg_sel >= 0 ? 1 : K;   // segments factored here
+    const int share = std::max(2, (helpers + 1) / KL);   // workgroups per segment (chain + helpers)
     for (int r = 0; r < K; r++) {
         Seg& s = sg[r];
         s.own = (cyc || r < K - 1) ? r : -1;
@@ -309,8 +377,11 @@ int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int 
             }
             s.rf[R] = f;
         }
-        dag_plan(s.rf.data(), s.n, share - 1, s.plan, s.nti);
+        if (seg_sel < 0 || seg_sel == r) dag_plan(s.rf.data(), s.n, share - 1, s.plan, s.nti);
     }
+    std::vector<int> loc(K, -1);   // segment -> its index among the ones factored here
+    for (int r = 0, i = 0; r < K; r++)
+        if (seg_sel < 0 || seg_sel == r) loc[r] = i++;
     // separator system: envelope from direct couplings and the fill of each segment's elimination
     std::vector<int> rfZ((nZ + kT - 1) / kT);
     {
@@ -322,10 +393,8 @@ int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int 
                 firstZ[a] = std::min(firstZ[a], 6 * w * b);
                 firstZ[b] = std::min(firstZ[b], 6 * w * a);
             }
-        for (int q = 0; q < np; q++)
-            if (sep_of[q] >= 0)
-                for (int o : adj[q])
-                    if (sep_of[o] >= 0) firstZ[sep_of[q]] = std::min(firstZ[sep_of[q]], 6 * w * sep_of[o]);
+        // (no direct coupling between two separators: the interior between them is >= w poses wide, so
+        // the envelope is the same on every shard of a distributed solve)
         for (size_t R = 0; R < rfZ.size(); R++) {
             int f = (int)R;
             for (int i = kT * (int)R; i < std::min(nZ, kT * (int)R + kT); i++) f = std::min(f, firstZ[i / (6 * w)] / kT);
@@ -340,17 +409,19 @@ int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int 
         for (int j = 0; j < 6 * w; j++) zg[6 * w * t + j] = 6 * sep_first(t) + j;
     for (int r = 0; r < K; r++) {
         const Seg& s = sg[r];
+        if (loc[r] < 0) continue;   // another shard's segment: its contributions are summed in there
         for (size_t j = 0; j < s.zmap.size(); j++) {
             const int z = s.zmap[j], l = s.nip + (int)j;
-            if (zsa[z] < 0) { zsa[z] = r; zla[z] = l; }
-            else { zsb[z] = r; zlb[z] = l; }
+            if (zsa[z] < 0) { zsa[z] = loc[r]; zla[z] = l; }
+            else { zsb[z] = loc[r]; zlb[z] = l; }
         }
     }
     // ---- sizes: doubles (128-byte aligned DAG buffers), ints, records ----
     auto al16 = [](size_t v) { return (v + 15) & ~size_t(15); };
     size_t nd = 0;
     std::vector<size_t> o_buf(K);
-    for (int r = 0; r < K; r++) { o_buf[r] = nd; nd = al16(nd + dag_doubles(sg[r].n)); }
+    for (int r = 0; r < K; r++)
+        if (loc[r] >= 0) { o_buf[r] = nd; nd = al16(nd + dag_doubles(sg[r].n)); }
     const size_t o_bufZ = nd; nd = al16(nd + dag_doubles(nZ));
     const size_t o_SZ = nd; nd = al16(nd + (size_t)nZ * nZ);
     const size_t o_bZ = nd; nd = al16(nd + nZ);
@@ -361,6 +432,7 @@ int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int 
     std::vector<SegOff> so(K);
     for (int r = 0; r < K; r++) {
         const Seg& s = sg[r];
+        if (loc[r] < 0) continue;
         so[r].ints = ni; ni = ai4(ni + dag_ints(s.n));
         so[r].perm = ni; ni = ai4(ni + s.n);
         so[r].rf = ni; ni = ai4(ni + s.NT);
@@ -375,9 +447,9 @@ int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int 
     const size_t oZ_tasks = ni; ni = ai4(ni + pZ.tasks.size());
     const size_t oZ_flag = ni; ni = ai4(ni + 4);
     const size_t o_zt = ni; ni = ai4(ni + 5 * (size_t)nZ);
-    const size_t o_wg = ni; ni = ai4(ni + K + 1);
+    const size_t o_wg = ni; ni = ai4(ni + KL + 1);
     const size_t kb = (dag_k_bytes() + 15) & ~size_t(15);
-    const size_t rb_ks = 0, rb_segs = K * kb, rb = rb_segs + K * sizeof(NdSegDev);
+    const size_t rb_ks = 0, rb_segs = KL * kb, rb = rb_segs + KL * sizeof(NdSegDev);
     if (W->dbl.ensure(nd) != hipSuccess || W->ints.ensure(ni) != hipSuccess || W->rec.ensure(rb) != hipSuccess ||
         W->hint.ensure(ni) != hipSuccess || W->hrec.ensure(rb) != hipSuccess)
         return -3;
@@ -386,18 +458,19 @@ int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int 
     int* H = W->hint.p;
     std::memset(H, 0, ni * sizeof(int));
     auto put = [&](size_t off, const std::vector<int>& v) { if (!v.empty()) std::memcpy(H + off, v.data(), v.size() * sizeof(int)); };
-    std::vector<DagProb> probs(K);
-    std::vector<NdSegDev> segs(K);
+    std::vector<DagProb> probs(KL);
+    std::vector<NdSegDev> segs(KL);
     W->tw.clear();
     for (int r = 0; r < K; r++) {
         const Seg& s = sg[r];
+        if (loc[r] < 0) continue;
         put(so[r].perm, s.perm); put(so[r].rf, s.rf); put(so[r].toff, s.plan.toff); put(so[r].tasks, s.plan.tasks);
         put(so[r].zmap, s.zmap);
-        DagProb& q = probs[r];
+        DagProb& q = probs[loc[r]];
         q.S = S; q.ld = n; q.perm = I + so[r].perm; q.n = s.n; q.nti = s.nti; q.rf = I + so[r].rf; q.bs = bs;
         q.x = nullptr; q.flag = I + so[r].flag;
         q.d = DagDev{D + o_buf[r], I + so[r].ints, I + so[r].toff, I + so[r].tasks, s.plan.G, s.plan.pb};
-        NdSegDev& g = segs[r];
+        NdSegDev& g = segs[loc[r]];
         g.buf = D + o_buf[r]; g.rf = I + so[r].rf; g.flag = I + so[r].flag; g.perm = I + so[r].perm;
         g.zmap = I + so[r].zmap; g.n = s.n; g.NT = s.NT; g.nti = s.nti; g.nip = s.nip;
         g.own0 = g.own1 = 0;
@@ -413,16 +486,16 @@ int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int 
     }
     W->tw.push_back(I + oZ_ints + 3);
     size_t lds = 0;
-    const int grid = dag_multi_fill(probs.data(), K, W->hrec.p + rb_ks, H + o_wg, gate, &lds);
-    std::memcpy(W->hrec.p + rb_segs, segs.data(), K * sizeof(NdSegDev));
+    const int grid = dag_multi_fill(probs.data(), KL, W->hrec.p + rb_ks, H + o_wg, gate, &lds);
+    std::memcpy(W->hrec.p + rb_segs, segs.data(), KL * sizeof(NdSegDev));
     if (hipMemcpyAsync(I, H, ni * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
         hipMemcpyAsync(W->rec.p, W->hrec.p, rb, hipMemcpyHostToDevice, st) != hipSuccess)
         return -3;
-    W->K = K; W->grid = grid; W->lds = lds;
+    W->K = KL; W->grid = grid; W->lds = lds;
     W->d_ks = W->rec.p + rb_ks;
     W->d_wgoff = I + o_wg;
     NdDev& d = W->dev;
-    d.S = S; d.bs = bs; d.x = x; d.flag = flag; d.gate = gate; d.ld = n; d.K = K; d.nZ = nZ;
+    d.S = S; d.bs = bs; d.x = x; d.flag = flag; d.gate = gate; d.ld = n; d.K = KL; d.nZ = nZ; d.n = n;
     d.segs = (const NdSegDev*)(W->rec.p + rb_segs);
     d.zg = I + o_zt; d.zsa = d.zg + nZ; d.zla = d.zsa + nZ; d.zsb = d.zla + nZ; d.zlb = d.zsb + nZ;
     d.rfZ = I + oZ_rf;
@@ -431,20 +504,69 @@ int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int 
     W->rfZ = I + oZ_rf;
     W->flagZ = I + oZ_flag;
     int maxNT = 0;
-    for (const Seg& s : sg) maxNT = std::max(maxNT, s.NT);
+    for (int r = 0; r < K; r++)
+        if (loc[r] >= 0) maxNT = std::max(maxNT, sg[r].NT);
     W->bs_lds = sizeof(double) * ((size_t)maxNT * kT + 9 * kT);
+    // shard of a distributed solve: the packed separator envelope and the x buffers
+    d.x_loc = nullptr;
+    d.xg = nullptr;
+    W->nZt = (int)rfZ.size();
+    if (seg_sel >= 0) {
+        std::vector<long long> off(rfZ.size() + 1, 0);
+        for (size_t R = 0; R < rfZ.size(); R++)
+            off[R + 1] = off[R] + (long long)std::min(kT, nZ - kT * (int)R) *
+                                      (std::min(kT * (int)R + kT, nZ) - kT * rfZ[R]);
+        W->pack_n = (size_t)off.back();
+        if (W->envoff.ensure(off.size()) != hipSuccess || W->pack.ensure(W->pack_n) != hipSuccess ||
+            W->xl.ensure(2 * (size_t)(n + 1)) != hipSuccess)
+            return -3;
+        if (hipMemcpy(W->envoff.p, off.data(), off.size() * sizeof(long long), hipMemcpyHostToDevice) != hipSuccess)
+            return -3;
+        d.x_loc = W->xl.p;
+        d.xg = W->xl.p + n + 1;
+    }
     return 0;
 }
 
-hipError_t nd_solve(NdWorkspace* W, hipStream_t st) {
-    hipError_t e = chol_dag_multi_launch(W->d_ks, W->d_wgoff, W->K, W->grid, W->lds, st);
+hipError_t nd_factor_assemble(NdWorkspace* W, hipStream_t st) {
+    const hipError_t e = chol_dag_multi_launch(W->d_ks, W->d_wgoff, W->K, W->grid, W->lds, st);
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_nd_assemble, dim3((unsigned)W->dev.nZ), dim3(256), 0, st, W->dev);
+    return hipGetLastError();
+}
+
+hipError_t nd_separator_backsolve(NdWorkspace* W, hipStream_t st) {
     const NdDev& d = W->dev;
-    hipLaunchKernelGGL(k_nd_assemble, dim3((unsigned)d.nZ), dim3(256), 0, st, d);
-    e = chol_dag_solve(d.SZ, d.nZ, W->rfZ, d.bZ, const_cast<double*>(d.xZ), W->flagZ, W->dZ, st, d.gate);
+    hipError_t e = chol_dag_solve(d.SZ, d.nZ, W->rfZ, d.bZ, const_cast<double*>(d.xZ), W->flagZ, W->dZ, st, d.gate);
     if (e != hipSuccess) return e;
+    if (d.x_loc && (e = hipMemsetAsync(d.x_loc, 0, sizeof(double) * (d.n + 1), st)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_nd_backsolve, dim3((unsigned)W->K), dim3(256), W->bs_lds, st, d);
     return hipGetLastError();
+}
+
+hipError_t nd_sep_pack(NdWorkspace* W, int dir, hipStream_t st) {
+    hipLaunchKernelGGL(k_nd_env_pack, dim3(8, (unsigned)W->nZt), dim3(256), 0, st, W->dev, W->envoff.p, W->pack.p, dir);
+    return hipGetLastError();
+}
+
+NdSepBufs nd_sep_bufs(NdWorkspace* W) {
+    NdSepBufs b;
+    b.pack = W->pack.p; b.pack_n = W->pack_n;
+    b.bZ = W->dev.bZ; b.nZ = W->dev.nZ;
+    b.x_loc = W->dev.x_loc; b.xg = const_cast<double*>(W->dev.xg);
+    b.n = W->dev.n;
+    return b;
+}
+
+hipError_t nd_finish(NdWorkspace* W, hipStream_t st) {
+    hipLaunchKernelGGL(k_nd_finish, dim3((unsigned)std::max(1, std::min(64, (W->dev.n + 255) / 256))), dim3(256), 0, st,
+                       W->dev);
+    return hipGetLastError();
+}
+
+hipError_t nd_solve(NdWorkspace* W, hipStream_t st) {
+    const hipError_t e = nd_factor_assemble(W, st);
+    return e != hipSuccess ? e : nd_separator_backsolve(W, st);
 }
 
 int nd_test(const double* A, const double* b, double* x, int np, const int* bi, const int* bj, int nblk, int K,

@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256) void k_ba_errors(const BaArgs* __restrict__ ar
         const double t = block_sum(r0, sh);
         if (threadIdx.x == 0 && has) st_agent(a.part + bx_, t);
         // the row's last workgroup runs the trial's controller step (the former k_ba_ctl_end)
-        if (a.ctl && last_arrival(&a.ctl->arrive_t, gridDim.x, &lastf)) ctl_end_body(a, act[by_], done, sh);
+        if (a.ctl && !a.sync && last_arrival(&a.ctl->arrive_t, gridDim.x, &lastf)) ctl_end_body(a, act[by_], done, sh);
     }
 }
 
@@ -392,7 +392,7 @@ __global__ __launch_bounds__(256) void k_ba_lin(const BaArgs* __restrict__ args,
         for (int w = 0; w < (int)(blockDim.x >> 6); w++) m = fmax(m, sh[w]);
         st_agent(a.part + slot, m);
     }
-    if (last_arrival(&a.ctl->arrive_b, gridDim.x, &lastf)) ctl_begin_body(a, mP + nP);
+    if (!a.sync && last_arrival(&a.ctl->arrive_b, gridDim.x, &lastf)) ctl_begin_body(a, mP + nP);
 }
 
 // ---------------------------------------------------------------------------
@@ -555,7 +555,8 @@ __global__ __launch_bounds__(256) void k_ba_schur_fin(const BaArgs* __restrict__
     const int blk = a.fin[3 * f], slot0 = a.fin[3 * f + 1], nch = a.fin[3 * f + 2];
     const int i = a.blk_i[blk], j = a.blk_j[blk];
     const int rr = lane / 6, cc = lane - 6 * rr;
-    double s = (i == j && a.lead) ? a.Hpp[36 * i + 6 * rr + cc] + (rr == cc ? *a.lambda : 0.0) : 0.0;
+    const bool pose_side = i == j && (a.own ? a.own[i] != 0 : a.lead != 0);
+    double s = pose_side ? a.Hpp_g[36 * i + 6 * rr + cc] + (rr == cc ? *a.lambda : 0.0) : 0.0;
     const double* sp = a.Spart + 36 * (size_t)slot0 + lane;
     int c = 0;
     for (; c + 8 <= nch; c += 8) {   // eight loads in flight, summed in order
@@ -984,20 +985,24 @@ __global__ __launch_bounds__(1024) void k_ba_ctl_init(const BaArgs* __restrict__
     }
 }
 
-__global__ void k_ba_ctl_stop(LmCtl* __restrict__ ctl, int B) {
+// the host's stop request (LocalMapping mbAbortBA): a problem between iterations ends now, one in a
+// trial at the end of its iteration (ctl_end_decide)
+__global__ void k_ba_ctl_stop(LmCtl* __restrict__ ctl, int B, int* done) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b < B) ctl[b].stop = 1;
+    if (b >= B) return;
+    ctl[b].stop = 1;
+    if (ctl[b].phase == kPhBuild) {
+        ctl[b].phase = kPhDone;
+        if (done) __hip_atomic_store(done + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // after the build: lambda initialisation on the first iteration (1e-5 max diagonal, from k_ba_lin's
 // per-workgroup maxima: sc1 loads), then trials. Run by the last workgroup of k_ba_lin.
-__device__ void ctl_begin_body(const BaArgs& a, int nlin) {
-    if (threadIdx.x != 0) return;
+__device__ void ctl_begin_apply(const BaArgs& a, double maxdiag) {
     LmCtl& c = *a.ctl;
     if (c.it == 0) {
-        double m = 0.0;
-        for (int i = 0; i < nlin; i++) m = fmax(m, ld_agent(a.part + i));
-        *const_cast<double*>(a.lambda) = 1e-5 * m;
+        *const_cast<double*>(a.lambda) = 1e-5 * maxdiag;
         c.ni = 2;
         c.nBad = 0;
     }
@@ -1005,12 +1010,18 @@ __device__ void ctl_begin_body(const BaArgs& a, int nlin) {
     c.rho = 0;
     c.phase = kPhTrial;
 }
+__device__ void ctl_begin_body(const BaArgs& a, int nlin) {
+    if (threadIdx.x != 0) return;
+    double m = 0.0;
+    if (a.ctl->it == 0)
+        for (int i = 0; i < nlin; i++) m = fmax(m, ld_agent(a.part + i));
+    ctl_begin_apply(a, m);
+}
 
 // after a trial: chi2 and scale, rho, accept (lambda shrink) or reject (lambda *= ni, pop), and
 // the end-of-iteration rules. Run by the last workgroup of k_ba_errors(2) of the problem: the chi2
 // partials are that launch's (sc1 loads), the scale partials k_ba_backsub's.
-__device__ void ctl_end_body(const BaArgs& a, int prob, int* done_flags, double* sh) {
-    LmCtl& c = *a.ctl;
+__device__ void ctl_end_sums(const BaArgs& a, double* sh) {
     {   // chi2 and the scale from the trial kernels' workgroup partials (k_ba_errors, k_ba_backsub)
         double v = 0.0;
         for (int i = threadIdx.x; i < a.npart_e; i += blockDim.x) v += ld_agent(a.part + i);
@@ -1023,7 +1034,10 @@ __device__ void ctl_end_body(const BaArgs& a, int prob, int* done_flags, double*
         v = block_sum(v, sh);
         if (threadIdx.x == 0) a.red[1] = v;
     }
-    if (threadIdx.x != 0) return;
+}
+// thread 0: the g2o rules on red[0] (chi2) and red[1] (scale)
+__device__ void ctl_end_decide(const BaArgs& a, int prob, int* done_flags) {
+    LmCtl& c = *a.ctl;
     double* lambda = const_cast<double*>(a.lambda);
     const bool ok2 = a.flag[0] != 0;
     const double tempChi = ok2 ? a.red[0] : DBL_MAX;
@@ -1039,6 +1053,7 @@ __device__ void ctl_end_body(const BaArgs& a, int prob, int* done_flags, double*
             else c.nBad = 0;
         }
         c.currentChi = tempChi;
+        c.pop = 0;
     } else {
         *lambda *= c.ni;
         c.ni *= 2;
@@ -1050,11 +1065,76 @@ __device__ void ctl_end_body(const BaArgs& a, int prob, int* done_flags, double*
     if (rho < 0 && c.qmax < 10 && !c.stop) return;   // another trial of this iteration
     c.it++;
     c.errors_valid = rho > 0;   // rejected: the device errors belong to the popped trial
-    bool done = (c.qmax == 10 || rho == 0);
+    bool done = (c.qmax == 10 || rho == 0) || c.stop;   // stop: SparseOptimizer's force-stop, at the iteration end
     if (c.early_stop && c.nBad >= 3) done = true;
     if (c.it >= c.iterations) done = true;   // the budget (checked by k_ba_errors(1) too), no idle slot
     c.phase = done ? kPhDone : kPhBuild;
     if (done && done_flags) __hip_atomic_store(done_flags + prob, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ void ctl_end_body(const BaArgs& a, int prob, int* done_flags, double* sh) {
+    ctl_end_sums(a, sh);
+    if (threadIdx.x == 0) ctl_end_decide(a, prob, done_flags);
+    if (!a.small) return;
+    // a small problem: this workgroup restores a rejected trial's state (k_ba_pop) and, when the
+    // iteration ended on it, recomputes the errors of the restored state (k_ba_errors(1): g2o's
+    // computeActiveErrors at the next iteration's start), so neither needs a launch of its own
+    __syncthreads();
+    const LmCtl& c = *a.ctl;
+    if (!c.pop) return;
+    for (int i = threadIdx.x; i < 8 * a.P; i += blockDim.x) a.pose[i] = a.pose_bak[i];
+    for (int i = threadIdx.x; i < 3 * a.M; i += blockDim.x) a.pts[i] = a.pts_bak[i];
+    if (c.phase != kPhBuild || c.errors_valid) return;
+    __syncthreads();
+    for (int e = threadIdx.x; e < a.E; e += blockDim.x) (void)edge_error(a, e);
+}
+
+// ---- sharded device-driven rounds (BaArgs::sync): the controller's reductions, a collective
+// over the shards, then its decisions, each a launch of one workgroup per problem ----
+// build: red[2] = the largest |diagonal| (landmarks: k_ba_lin's workgroup maxima; poses: the
+// summed Hpp_g, since a shard's own Hpp holds only its edges' terms)
+__global__ __launch_bounds__(256) void k_ba_sh_maxdiag(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    const BaArgs& a = args[act[blockIdx.x]];
+    if (!in_phase(a, kPhBuild)) return;
+    const int mP = (a.M + 255) / 256;
+    double m = 0.0;
+    for (int i = threadIdx.x; i < mP; i += blockDim.x) m = fmax(m, ld_agent(a.part + i));
+    for (int i = threadIdx.x; i < 6 * a.np; i += blockDim.x) m = fmax(m, fabs(a.Hpp_g[36 * (i / 6) + 7 * (i % 6)]));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    __shared__ double sh[4];
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) a.red[2] = fmax(fmax(sh[0], sh[1]), fmax(sh[2], sh[3]));
+}
+__global__ void k_ba_sh_init(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    const BaArgs& a = args[act[blockIdx.x]];
+    if (threadIdx.x == 0) { a.ctl->currentChi = a.red[0]; a.ctl->initChi = a.red[0]; }
+}
+__global__ void k_ba_sh_begin(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    const BaArgs& a = args[act[blockIdx.x]];
+    if (threadIdx.x == 0 && in_phase(a, kPhBuild)) ctl_begin_apply(a, a.red[2]);
+}
+__global__ __launch_bounds__(1024) void k_ba_sh_sums(const BaArgs* __restrict__ args, const int* __restrict__ act) {
+    __shared__ double sh[16];
+    const BaArgs& a = args[act[blockIdx.x]];
+    if (in_phase(a, kPhTrial)) ctl_end_sums(a, sh);
+}
+__global__ void k_ba_sh_end(const BaArgs* __restrict__ args, const int* __restrict__ act, int* done) {
+    const BaArgs& a = args[act[blockIdx.x]];
+    if (threadIdx.x == 0 && in_phase(a, kPhTrial)) ctl_end_decide(a, act[blockIdx.x], done);
+}
+// the in-process form of a collective over B shards: dst[s][i] = sum (op 0) / max (op 1) over the
+// shards of src[s'][i], in shard order (deterministic); dst may alias src
+__global__ __launch_bounds__(256) void k_ba_multi_reduce(const double* const* __restrict__ src, double* const* __restrict__ dst,
+                                                         int B, size_t count, int op) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x) {
+        double acc = op ? -1.0e300 : 0.0;
+        for (int b = 0; b < B; b++) {
+            const double v = src[b][i];
+            acc = op ? fmax(acc, v) : acc + v;
+        }
+        for (int b = 0; b < B; b++) dst[b][i] = acc;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1084,6 +1164,8 @@ struct Prep {
     DagPlan dag;                  // its helper task lists
     bool use_nd = false;          // nested dissection over the DAG solver (ba_nd.hip): a lone banded GBA
     NdPlan nd;
+    bool use_nd_sh = false;       // a shard of a sharded solve by keyframe segments (segment = shard)
+    std::vector<unsigned char> own;   // ... the poses whose pose-side terms it adds
     size_t dag_task_cap = 0;      // ints reserved for the lists (RCCL shards: planned after the union envelope)
     size_t o_dag = 0, o_dagi = 0;
     size_t o_red2 = 0;            // workgroup partials of a trial's chi2 / scale (BaArgs::part)
@@ -1298,6 +1380,10 @@ struct BaWorkspace {
     HBuf<int> hto;             // pinned: the persistent solver's hand-off timeout count per problem
     long long dag_timeouts = 0, dag_reruns = 0;
     NdWorkspace* nd = nullptr; // nested-dissection solves (created on first use)
+    std::vector<NdWorkspace*> nds;   // sharded solves by segments: one per shard of this process
+    DBuf<double*> ptab;        // in-process shards: the collectives' pointer tables
+    DBuf<int> dint4;           // RCCL: small consensus all-reduces (plan, stop)
+    int* h_int4 = nullptr;     // pinned
 };
 
 BaWorkspace* ba_create() { return new BaWorkspace(); }
@@ -1306,6 +1392,8 @@ void ba_destroy(BaWorkspace* w) {
     if (!w) return;
     if (w->comm) (void)ncclCommDestroy(w->comm);
     if (w->nd) nd_destroy(w->nd);
+    for (NdWorkspace* q : w->nds) nd_destroy(q);
+    if (w->h_int4) (void)hipHostFree(w->h_int4);
     if (w->h_stop) (void)hipHostFree(w->h_stop);
     if (w->h_done) (void)hipHostFree(w->h_done);
     if (w->h_lam) (void)hipHostFree(w->h_lam);
@@ -1372,11 +1460,66 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             }
         }
     }
+    // sharded solves by keyframe segments (the distributed form of the dissection):
+    // shard r is segment r when every shard's landmarks lie inside its segment's matrix
+    // (sharding.shard_problem_nd); then each shard eliminates its interior, the separator system is
+    // summed over the shards, every shard solves it, and the shards' x are summed. Otherwise the
+    // shards sum S itself and every shard solves it (replicated). The decision is agreed over the
+    // ranks; ORBHIP_SHARD_ND=0 forces the replicated form.
+    const int seg0 = shard_mode == kShardRccl ? ws->rank : 0;   // segment of problem 0
+    NdPlan ndp;
+    bool nd_sh = false;
+    if (shard_mode != kShardNone) {
+        const char* e_snd = std::getenv("ORBHIP_SHARD_ND");
+        const char* e_min = std::getenv("ORBHIP_ND_MIN");
+        const int nd_min = e_min ? std::atoi(e_min) : 960;
+        const int K = shard_mode == kShardLocal ? B : ws->nranks;
+        int wl = 0, wc = 0;
+        for (int b = 0; b < B; b++) {
+            int l = 0, c = 0;
+            nd_bandwidth(pp[b].np, pp[b].blk_i.data(), pp[b].blk_j.data(), pp[b].nblk, l, c);
+            wl = std::max(wl, l);
+            wc = std::max(wc, c);
+        }
+        int ok = (!no_dag && !force_blocked && !(e_snd && e_snd[0] == '0') && pp[0].n >= nd_min) ? 1 : 0;
+        if (shard_mode == kShardRccl) {   // the band over every rank's landmarks
+            ws->h_int4[0] = wl; ws->h_int4[1] = wc; ws->h_int4[2] = -ok;
+            if (hipMemcpyAsync(ws->dint4.p, ws->h_int4, 3 * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
+                ncclAllReduce(ws->dint4.p, ws->dint4.p, 3, ncclInt32, ncclMax, ws->comm, st) != ncclSuccess ||
+                hipMemcpyAsync(ws->h_int4, ws->dint4.p, 3 * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
+                return ORBHIP_ERR_DEVICE;
+            wl = ws->h_int4[0]; wc = ws->h_int4[1]; ok = -ws->h_int4[2];
+        }
+        ok = ok && nd_plan_band(pp[0].np, wl, wc, K, ndp);
+        for (int b = 0; b < B && ok; b++)
+            ok = nd_blocks_fit(ndp, seg0 + b, pp[b].blk_i.data(), pp[b].blk_j.data(), pp[b].nblk);
+        if (shard_mode == kShardRccl) {   // every rank's landmarks fit its segment
+            ws->h_int4[0] = ok ? 0 : 1;
+            if (hipMemcpyAsync(ws->dint4.p, ws->h_int4, sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
+                ncclAllReduce(ws->dint4.p, ws->dint4.p, 1, ncclInt32, ncclMax, ws->comm, st) != ncclSuccess ||
+                hipMemcpyAsync(ws->h_int4, ws->dint4.p, sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
+                return ORBHIP_ERR_DEVICE;
+            ok = ws->h_int4[0] == 0;
+        }
+        nd_sh = ok != 0;
+        if (nd_sh)
+            for (int b = 0; b < B; b++) {
+                Prep& p = pp[b];
+                p.use_nd_sh = true;
+                p.use_dag = false;
+                const int r = seg0 + b;
+                p.own.assign(p.np, 0);
+                for (int q = ndp.seg[r]; q < ndp.seg[r + 1]; q++) p.own[q] = 1;   // interior + own separator
+            }
+    }
+    const bool sharded = shard_mode != kShardNone;
     // the per-panel tile lists / the DAG plans (RCCL shards: the envelope is the union over the
     // ranks, known after a collective; their DAG plan is made then, into reserved space)
     parallel_for(B, nth, [&](int b) {
         Prep& p = pp[b];
-        if (p.use_nd) {
+        if (p.use_nd || p.use_nd_sh) {
             // planned above; its device data is set up with the problem's buffers (nd_setup)
         } else if (p.use_dag) {
             if (shard_mode == kShardRccl) {
@@ -1407,6 +1550,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         nR += 8 * P + 3 * M                          // pose_bak, pts_bak
               + 2 * E + 3 * E                        // e_err, e_rho0, e_rho1 (+ pad)
               + 36 * np_ + 9 * np_ + 18 * M + 3 * M  // Hpp, R_lin, Hll, Dinv, db
+              + (sharded ? 36 * np_ : 0)             // Hpp_g: Hpp summed over the shards
               + 2 * (n + 3 * M) + n + 4;             // b, x, bs, red
         nR = (nR + 3) & ~size_t(3);
         p.o_lin = nR; nR += 4 * E;
@@ -1424,7 +1568,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         p.o_int = ni;
         ni += (P + 4) + 2 * E + (M + 1) + E + (np_ + 1) + p.ps_edges.size() + 3 * p.nblk + 1 + p.blk_pairs.size() +
               p.row_first.size() + p.items.size() + p.fin.size() + p.cb_tiles.size() + 8 +
-              (p.use_dag ? dag_ints(p.n) + p.dag_task_cap + 4 : 0);
+              (p.use_dag ? dag_ints(p.n) + p.dag_task_cap + 4 : 0) + (p.own.size() + 3) / 4 + 1;
     }
     const size_t sC = 0, sA = nC, sU = sA + nA, sR = (sU + nU + 15) & ~size_t(15);
     const size_t nd = sR + nR;
@@ -1497,6 +1641,12 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.nfin = (int)(p.fin.size() / 3);
         a.row_first = dev(put(p.row_first.data(), p.row_first.size()));
         a.cb_tiles = p.cb_tiles.empty() ? nullptr : dev(put(p.cb_tiles.data(), p.cb_tiles.size()));
+        a.own = nullptr;
+        if (!p.own.empty()) {   // bytes, in the int staging
+            std::memcpy(q, p.own.data(), p.own.size());
+            a.own = reinterpret_cast<const unsigned char*>(dev(q));
+            q += (p.own.size() + 3) / 4;
+        }
         if (p.use_dag) {   // flags + control words (zero), then the plan (or the space reserved for it)
             while ((q - hi) & 3) q++;
             dd[b].ints = dev(q);
@@ -1532,6 +1682,10 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.Hll = r; r += 9 * M;
         a.Dinv = r; r += 9 * M;
         a.db = r; r += 3 * M;
+        a.Hpp_g = a.Hpp;
+        if (sharded) { a.Hpp_g = r; r += 36 * (size_t)p.np; }
+        a.sync = sharded ? 1 : 0;
+        a.small = (!sharded && 8 * P + 3 * M <= 32768 && E <= 65536) ? 1 : 0;
         a.b = r; r += p.n + 3 * M;
         a.x = r; r += p.n + 3 * M;
         a.bs = r; r += p.n;
@@ -1545,7 +1699,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         if (p.use_dag) dd[b].buf = D + sR + p.o_dag;
         a.lambda = ws->lam.p + b;
         a.lead = shard_mode == kShardLocal ? (b == 0) : (shard_mode == kShardRccl ? (ws->rank == 0) : 1);
-        a.ctl = shard_mode == kShardNone ? ws->ctl.p + b : nullptr;
+        a.ctl = ws->ctl.p + b;
     });
     BAOK(hipMemcpyAsync(D + sA, hd + sA, sizeof(double) * (nA + nU), hipMemcpyHostToDevice, st));
     BAOK(hipMemcpyAsync(I, hi, ni * sizeof(int), hipMemcpyHostToDevice, st));
@@ -1554,7 +1708,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     // envelope; the one-workgroup solvers also read the mirrored upper triangle) all-reduce S
     // over its union envelope only: ~5 MB instead of n^2 doubles (46 MB) at C5
     size_t env_total = 0;
-    if (shard_mode == kShardRccl && !pp[0].row_first.empty()) {   // union envelope over the ranks
+    if (shard_mode == kShardRccl && !nd_sh && !pp[0].row_first.empty()) {   // union envelope over the ranks
         int* rf = const_cast<int*>(ha[0].row_first);
         if (ncclAllReduce(rf, rf, pp[0].row_first.size(), ncclInt32, ncclMin, ws->comm, st) != ncclSuccess)
             return ORBHIP_ERR_DEVICE;
@@ -1594,17 +1748,16 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         lds_set = true;
     }
     int maxM = 0, maxE = 0, maxP = 0, maxNp = 0, maxBlk = 0, maxN = 0, maxItems = 0, maxFin = 0;
-    bool any_large = false, s_written = false;
+    bool s_written = false;
     // "large": solved on its own (DAG or blocked); the rest share one single-workgroup launch
-    auto large = [&](int b) { return pp[b].use_nd || pp[b].use_dag || pp[b].n > kCholSmallN; };
+    auto large = [&](int b) { return pp[b].use_nd || pp[b].use_nd_sh || pp[b].use_dag || pp[b].n > kCholSmallN; };
     for (int b = 0; b < B; b++) {
         const Prep& p = pp[b];
         maxM = std::max(maxM, p.M); maxE = std::max(maxE, p.E); maxP = std::max(maxP, p.P);
         maxNp = std::max(maxNp, p.np); maxBlk = std::max(maxBlk, p.nblk);
         maxItems = std::max(maxItems, (int)(p.items.size() / 4)); maxFin = std::max(maxFin, (int)(p.fin.size() / 3));
-        if (large(b)) any_large = true;
-        else maxN = std::max(maxN, p.n);
-        if (!p.use_dag && !p.use_nd && p.n > kCholRegMaxN) s_written = true;   // the LDS and blocked solvers factor S in place
+        if (!large(b)) maxN = std::max(maxN, p.n);
+        if (!p.use_dag && !p.use_nd && !p.use_nd_sh && p.n > kCholRegMaxN) s_written = true;   // the LDS and blocked solvers factor S in place
     }
     const size_t chol_lds = sizeof(double) * chol_lds_doubles(maxN);
     // every problem on a solver that reads S and never writes it (register / DAG), no shard sums
@@ -1621,7 +1774,6 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         }
         return ORBHIP_OK;
     };
-    bool s_clean = false;
     auto gx = [](int n_, int b_) { return (unsigned)std::max(1, (n_ + b_ - 1) / b_); };
     (void)hipGetLastError();
     int* d_act = ws->act.p;
@@ -1632,43 +1784,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         return ORBHIP_OK;
     };
     const BaArgs* dA = ws->args.p;
-    // per-round readback: the act list currently on the device (same order as v) is gathered
-    // into one contiguous buffer and copied with ONE transfer; h_red is indexed by problem.
-    auto read_red = [&](const std::vector<int>& v) -> int {
-        hipLaunchKernelGGL(k_ba_gather_red, dim3((unsigned)((v.size() + 63) / 64)), dim3(64), 0, st, dA, d_act,
-                           (int)v.size(), ws->gath.p);
-        BAOK(hipMemcpyAsync(ws->h_gath, ws->gath.p, 5 * v.size() * sizeof(double), hipMemcpyDeviceToHost, st));
-        BAOK(hipStreamSynchronize(st));
-        for (size_t i = 0; i < v.size(); i++)
-            for (int k = 0; k < 5; k++) ws->h_red[5 * v[i] + k] = ws->h_gath[5 * i + k];
-        return ORBHIP_OK;
-    };
-    // ---- sharded solve: the collective steps (no-ops for independent problems) ----
-    // field: 0 Hpp, 1 S, 2 bs, 3 red; op 0 sum, 1 max
-    auto coll = [&](int field, int off, size_t count, int op) -> int {
-        if (shard_mode == kShardLocal) {
-            hipLaunchKernelGGL(k_ba_shard_reduce, dim3((unsigned)std::min<size_t>(1024, (count + 255) / 256)),
-                               dim3(256), 0, st, dA, B, field, off, count, op);
-        } else if (shard_mode == kShardRccl) {
-            const BaArgs& a0 = ha[0];
-            if (field == 1 && off == 0 && env_total) {   // S: its union envelope, packed
-                const int nt = (int)pp[0].row_first.size();
-                const dim3 g(8, (unsigned)nt);
-                hipLaunchKernelGGL(k_ba_env_pack, g, dim3(256), 0, st, a0.S, a0.n, a0.row_first, ws->envoff.p,
-                                   ws->envbuf.p, 0);
-                if (ncclAllReduce(ws->envbuf.p, ws->envbuf.p, env_total, ncclDouble, ncclSum, ws->comm, st) != ncclSuccess)
-                    return ORBHIP_ERR_DEVICE;
-                hipLaunchKernelGGL(k_ba_env_pack, g, dim3(256), 0, st, a0.S, a0.n, a0.row_first, ws->envoff.p,
-                                   ws->envbuf.p, 1);
-                return ORBHIP_OK;
-            }
-            double* p = (field == 0 ? a0.Hpp : field == 1 ? a0.S : field == 2 ? a0.bs : a0.red) + off;
-            if (ncclAllReduce(p, p, count, ncclDouble, op ? ncclMax : ncclSum, ws->comm, st) != ncclSuccess)
-                return ORBHIP_ERR_DEVICE;
-        }
-        return ORBHIP_OK;
-    };
-    // stop flag: one consistent decision across ranks (all-reduce max) at each iteration
+    // stop flag: one consistent decision across ranks (all-reduce max) per batch of slots
     auto stop_now = [&]() -> bool {
         const bool local = stop && *stop;
         if (shard_mode != kShardRccl) return local;
@@ -1683,11 +1799,15 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     std::vector<int> all(B);
     for (int b = 0; b < B; b++) all[b] = b;
     if (upload_act(all)) return ORBHIP_ERR_DEVICE;
-    if (shard_mode == kShardNone) {
+    {
         // ---- device-driven rounds: each slot advances every problem by one LM trial (with the
         // iteration's linearisation in front when it starts one); the k_ba_ctl_* kernels apply
         // the g2o rules per problem, so the host only enqueues slots and reads the state back once
-        // per batch of slots ----
+        // per batch of slots. Sharded solves run the same slots with their collectives on the
+        // stream between the kernels (RCCL across ranks, k_ba_multi_reduce across the shards of
+        // this process) and the controller's reductions split from its decisions (BaArgs::sync):
+        // every shard sees the same sums, so every shard takes the same decisions, and the host
+        // decides nothing per trial. ----
         LmCtl* dctl = ws->ctl.p;
         for (int b = 0; b < B; b++) {
             LmCtl& c = ws->hctl.p[b];
@@ -1706,34 +1826,133 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                              ha[b].x, ha[b].flag, &dctl[b].phase, st) != 0)
                     return ORBHIP_ERR_DEVICE;
             }
+        if (nd_sh) {   // one segment per shard
+            while (ws->nds.size() < (size_t)B) ws->nds.push_back(nd_create());
+            for (int b = 0; b < B; b++)
+                if (nd_setup(ws->nds[b], ndp, pp[b].blk_i.data(), pp[b].blk_j.data(), pp[b].nblk, ha[b].S, ha[b].bs,
+                             ha[b].x, ha[b].flag, &dctl[b].phase, st, seg0 + b) != 0)
+                    return ORBHIP_ERR_DEVICE;
+        }
+        // ---- the collectives of a sharded slot: site s sums (or maxes) src[b] into dst[b] over the
+        // shards; RCCL: one all-reduce of this rank's buffers ----
+        enum { kHpp, kRed0, kRed2, kRed01, kRepS, kRepBs, kNdPack, kNdBz, kNdX, kSites };
+        struct Site { std::vector<double*> src, dst; size_t count = 0; int op = 0; size_t tab = 0; };
+        std::vector<Site> sites(sharded ? kSites : 0);
+        if (sharded) {
+            auto site = [&](int id, size_t count, int op, auto src, auto dst) {
+                Site& t = sites[id];
+                t.count = count; t.op = op;
+                for (int b = 0; b < B; b++) { t.src.push_back(src(b)); t.dst.push_back(dst(b)); }
+            };
+            site(kHpp, 36 * (size_t)maxNp, 0, [&](int b) { return ha[b].Hpp; }, [&](int b) { return const_cast<double*>(ha[b].Hpp_g); });
+            site(kRed0, 1, 0, [&](int b) { return ha[b].red; }, [&](int b) { return ha[b].red; });
+            site(kRed2, 1, 1, [&](int b) { return ha[b].red + 2; }, [&](int b) { return ha[b].red + 2; });
+            site(kRed01, 2, 0, [&](int b) { return ha[b].red; }, [&](int b) { return ha[b].red; });
+            if (!nd_sh) {
+                site(kRepS, (size_t)pp[0].n * pp[0].n, 0, [&](int b) { return ha[b].S; }, [&](int b) { return ha[b].S; });
+                site(kRepBs, (size_t)pp[0].n, 0, [&](int b) { return ha[b].bs; }, [&](int b) { return ha[b].bs; });
+            } else {
+                const NdSepBufs q0 = nd_sep_bufs(ws->nds[0]);
+                site(kNdPack, q0.pack_n, 0, [&](int b) { return nd_sep_bufs(ws->nds[b]).pack; },
+                     [&](int b) { return nd_sep_bufs(ws->nds[b]).pack; });
+                site(kNdBz, (size_t)q0.nZ, 0, [&](int b) { return nd_sep_bufs(ws->nds[b]).bZ; },
+                     [&](int b) { return nd_sep_bufs(ws->nds[b]).bZ; });
+                site(kNdX, (size_t)q0.n + 1, 0, [&](int b) { return nd_sep_bufs(ws->nds[b]).x_loc; },
+                     [&](int b) { return nd_sep_bufs(ws->nds[b]).xg; });
+            }
+            if (shard_mode == kShardLocal) {   // the pointer tables, on the device once
+                std::vector<double*> tab;
+                for (Site& t : sites) {
+                    t.tab = tab.size();
+                    tab.insert(tab.end(), t.src.begin(), t.src.end());
+                    tab.insert(tab.end(), t.dst.begin(), t.dst.end());
+                }
+                BAOK(ws->ptab.ensure(tab.size()));
+                BAOK(hipMemcpy(ws->ptab.p, tab.data(), tab.size() * sizeof(double*), hipMemcpyHostToDevice));
+            }
+        }
+        auto coll = [&](int id) -> int {
+            const Site& t = sites[id];
+            if (t.count == 0) return ORBHIP_OK;
+            if (shard_mode == kShardLocal) {
+                hipLaunchKernelGGL(k_ba_multi_reduce, dim3((unsigned)std::min<size_t>(1024, (t.count + 255) / 256)),
+                                   dim3(256), 0, st, (const double* const*)(ws->ptab.p + t.tab),
+                                   (double* const*)(ws->ptab.p + t.tab + B), B, t.count, t.op);
+                return ORBHIP_OK;
+            }
+            if (id == kRepS && env_total) {   // RCCL, replicated: S over its union envelope, packed
+                const BaArgs& a0 = ha[0];
+                const dim3 g(8, (unsigned)pp[0].row_first.size());
+                hipLaunchKernelGGL(k_ba_env_pack, g, dim3(256), 0, st, a0.S, a0.n, a0.row_first, ws->envoff.p,
+                                   ws->envbuf.p, 0);
+                if (ncclAllReduce(ws->envbuf.p, ws->envbuf.p, env_total, ncclDouble, ncclSum, ws->comm, st) != ncclSuccess)
+                    return ORBHIP_ERR_DEVICE;
+                hipLaunchKernelGGL(k_ba_env_pack, g, dim3(256), 0, st, a0.S, a0.n, a0.row_first, ws->envoff.p,
+                                   ws->envbuf.p, 1);
+                return ORBHIP_OK;
+            }
+            if (ncclAllReduce(t.src[0], t.dst[0], t.count, ncclDouble, t.op ? ncclMax : ncclSum, ws->comm, st) != ncclSuccess)
+                return ORBHIP_ERR_DEVICE;
+            return ORBHIP_OK;
+        };
         int ns = 0;   // problems on the single-workgroup solvers (act slot 3)
         for (int b = 0; b < B; b++)
             if (!large(b)) h_act[2 * B + ns++] = b;
         if (ns) BAOK(hipMemcpyAsync(d_act + 2 * B, h_act + 2 * B, ns * sizeof(int), hipMemcpyHostToDevice, st));
         if (s_readonly) hipLaunchKernelGGL(k_ba_zero_s, dim3(64, B), dim3(256), 0, st, dA, d_act, 1);
         hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), dim3(256), 0, st, dA, d_act, 0, nullptr);
-        hipLaunchKernelGGL(k_ba_ctl_init, dim3(B), dim3(1024), 0, st, dA, d_act);
+        if (!sharded) {
+            hipLaunchKernelGGL(k_ba_ctl_init, dim3(B), dim3(1024), 0, st, dA, d_act);
+        } else {   // the initial chi2 over every shard's edges
+            hipLaunchKernelGGL(k_ba_reduce, dim3(B), dim3(1024), 0, st, dA, d_act, 1);
+            if (coll(kRed0)) return ORBHIP_ERR_DEVICE;
+            hipLaunchKernelGGL(k_ba_sh_init, dim3(B), dim3(64), 0, st, dA, d_act);
+        }
         const dim3 gB((unsigned)((B + 255) / 256)), b256(256);
+        bool all_small = true;   // every problem restores / refreshes in its trial's last workgroup
+        for (int b = 0; b < B; b++) all_small = all_small && ha[b].small;
         auto slot = [&]() -> int {
-            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 1, ws->d_done);
+            if (!all_small) hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 1, ws->d_done);
             hipLaunchKernelGGL(k_ba_lin, dim3(gx(maxM, 256) + gx(maxNp, 4), B), b256, 0, st, dA, d_act,
                                (int)gx(maxM, 256));
+            if (sharded) {   // the trial start on the shards' sums: Hpp, then the largest diagonal
+                if (coll(kHpp)) return ORBHIP_ERR_DEVICE;
+                hipLaunchKernelGGL(k_ba_sh_maxdiag, dim3(B), b256, 0, st, dA, d_act);
+                if (coll(kRed2)) return ORBHIP_ERR_DEVICE;
+                hipLaunchKernelGGL(k_ba_sh_begin, dim3(B), dim3(64), 0, st, dA, d_act);
+            }
             if (!s_readonly) hipLaunchKernelGGL(k_ba_zero_s, dim3(64, B), b256, 0, st, dA, d_act, 0);
             hipLaunchKernelGGL(k_ba_schur_points, dim3(gx(maxM, 256), B), b256, 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_schur_items, dim3(gx(2 * maxItems, 256) + gx(maxNp, 4), B), b256, 0, st, dA, d_act,
                                (int)gx(2 * maxItems, 256));
             hipLaunchKernelGGL(k_ba_schur_fin, dim3(gx(maxFin, 4), B), b256, 0, st, dA, d_act);
-            if (ns) {
-                if (maxN <= kCholRegMaxN) BAOK(chol_reg_launch(maxN, ns, dA, d_act + 2 * B, st));
-                else hipLaunchKernelGGL(k_ba_cholesky, dim3(ns), dim3(512), chol_lds, st, dA, d_act + 2 * B);
+            if (nd_sh) {   // each shard its segment; the separator system and x summed over the shards
+                for (int b = 0; b < B; b++) BAOK(nd_factor_assemble(ws->nds[b], st));
+                for (int b = 0; b < B; b++) BAOK(nd_sep_pack(ws->nds[b], 0, st));
+                if (coll(kNdPack) || coll(kNdBz)) return ORBHIP_ERR_DEVICE;
+                for (int b = 0; b < B; b++) BAOK(nd_sep_pack(ws->nds[b], 1, st));
+                for (int b = 0; b < B; b++) BAOK(nd_separator_backsolve(ws->nds[b], st));
+                if (coll(kNdX)) return ORBHIP_ERR_DEVICE;
+                for (int b = 0; b < B; b++) BAOK(nd_finish(ws->nds[b], st));
+            } else {
+                if (sharded && (coll(kRepS) || coll(kRepBs))) return ORBHIP_ERR_DEVICE;   // replicated solves
+                if (ns) {
+                    if (maxN <= kCholRegMaxN) BAOK(chol_reg_launch(maxN, ns, dA, d_act + 2 * B, st));
+                    else hipLaunchKernelGGL(k_ba_cholesky, dim3(ns), dim3(512), chol_lds, st, dA, d_act + 2 * B);
+                }
+                for (int b = 0; b < B; b++)
+                    if (large(b) && large_solve(b, &dctl[b].phase)) return ORBHIP_ERR_DEVICE;
             }
-            for (int b = 0; b < B; b++)
-                if (large(b) && large_solve(b, &dctl[b].phase)) return ORBHIP_ERR_DEVICE;
             hipLaunchKernelGGL(k_ba_backsub, dim3(gx(std::max(maxM, maxP), 256), B), b256, 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 2, ws->d_done);
+            if (sharded) {   // the trial's end on the shards' sums of chi2 and the scale
+                hipLaunchKernelGGL(k_ba_sh_sums, dim3(B), dim3(1024), 0, st, dA, d_act);
+                if (coll(kRed01)) return ORBHIP_ERR_DEVICE;
+                hipLaunchKernelGGL(k_ba_sh_end, dim3(B), dim3(64), 0, st, dA, d_act, ws->d_done);
+            }
             int maxPM = 0;
             for (auto& p : pp) maxPM = std::max(maxPM, std::max(8 * p.P, 3 * p.M));
-            hipLaunchKernelGGL(k_ba_pop, dim3(gx(maxPM, 256), B), b256, 0, st, dA, d_act);
+            if (!all_small) hipLaunchKernelGGL(k_ba_pop, dim3(gx(maxPM, 256), B), b256, 0, st, dA, d_act);
             BAOK(hipGetLastError());
             return ORBHIP_OK;
         };
@@ -1762,17 +1981,26 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         int remaining = 0;   // slots every unfinished problem still needs at least
         for (int b = 0; b < B; b++) remaining = std::max(remaining, probs[b]->iterations);
         int nslot = 0;
+        // ranks of an RCCL solve must enqueue the same slots (their collectives pair up): they look
+        // at the stop flag only between batches, agreed by an all-reduce, and never end a batch on
+        // the asynchronous done flags; the batch length comes from the LM state read back, which
+        // every rank holds identically
+        const bool rccl = shard_mode == kShardRccl;
         while (remaining > 0 && rc == ORBHIP_OK) {
+            if (rccl && !stop_sent && stop_now()) {
+                hipLaunchKernelGGL(k_ba_ctl_stop, gB, b256, 0, st, dctl, B, ws->d_done);
+                stop_sent = true;
+            }
             for (int k = 0; k < remaining && rc == ORBHIP_OK; k++, nslot++) {
-                if (!stop_sent && stop && *stop) {
-                    hipLaunchKernelGGL(k_ba_ctl_stop, gB, b256, 0, st, dctl, B);
+                if (!rccl && !stop_sent && stop && *stop) {
+                    hipLaunchKernelGGL(k_ba_ctl_stop, gB, b256, 0, st, dctl, B, ws->d_done);
                     stop_sent = true;
                 }
                 rc = slot();
                 if (rc == ORBHIP_OK && hipEventRecord(ev[nslot & 1], st) != hipSuccess) rc = ORBHIP_ERR_DEVICE;
                 if (rc == ORBHIP_OK && nslot >= 1 && hipEventSynchronize(ev[(nslot - 1) & 1]) != hipSuccess)
                     rc = ORBHIP_ERR_DEVICE;
-                if (rc == ORBHIP_OK && nslot >= 1 && all_done()) { nslot++; break; }
+                if (rc == ORBHIP_OK && !rccl && nslot >= 1 && all_done()) { nslot++; break; }
             }
             if (rc != ORBHIP_OK) break;
             if (hipMemcpyAsync(ws->hctl.p, dctl, B * sizeof(LmCtl), hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -1797,140 +2025,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             L[b].trials = c.trials;
             res[b]->initial_chi2 = c.initChi;
         }
-    } else {
-    // ---- host-driven rounds (sharded solves: collectives and the stop-flag consensus) ----
-    // ---- initial errors and chi2 ----
-    hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), dim3(256), 0, st, dA, d_act, 0, nullptr);
-    hipLaunchKernelGGL(k_ba_reduce, dim3(B), dim3(1024), 0, st, dA, d_act, 1);
-    if (coll(3, 0, 1, 0)) return ORBHIP_ERR_DEVICE;
-    BAOK(hipGetLastError());
-    if (read_red(all)) return ORBHIP_ERR_DEVICE;
-    for (int b = 0; b < B; b++) {
-        L[b].currentChi = ws->h_red[5 * b];
-        res[b]->initial_chi2 = L[b].currentChi;
     }
-    const int maxIt = [&] { int m = 0; for (int b = 0; b < B; b++) m = std::max(m, probs[b]->iterations); return m; }();
-    const double dmax = std::numeric_limits<double>::max();
-    for (int it = 0; it < maxIt; it++) {
-        std::vector<int> act;
-        const bool stop_it = stop_now();
-        for (int b = 0; b < B; b++)
-            if (!L[b].done && it < probs[b]->iterations && !stop_it) act.push_back(b);
-            else L[b].done = true;
-        if (act.empty()) break;
-        const unsigned na = (unsigned)act.size();
-        // computeActiveErrors (only where the device copy is stale) + buildSystem
-        std::vector<int> stale;
-        for (int b : act)
-            if (!L[b].errors_valid) stale.push_back(b);
-        if (!stale.empty()) {
-            if (upload_act(stale)) return ORBHIP_ERR_DEVICE;
-            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), (unsigned)stale.size()), dim3(256), 0, st, dA, d_act, 0, nullptr);
-        }
-        if (upload_act(act)) return ORBHIP_ERR_DEVICE;
-        hipLaunchKernelGGL(k_ba_lin_points, dim3(gx(maxM, 256), na), dim3(256), 0, st, dA, d_act);
-        hipLaunchKernelGGL(k_ba_lin_poses, dim3(gx(maxNp, 4), na), dim3(256), 0, st, dA, d_act);
-        if (coll(0, 0, (size_t)36 * maxNp, 0)) return ORBHIP_ERR_DEVICE;   // global Hpp on every shard
-        if (it == 0) {
-            hipLaunchKernelGGL(k_ba_reduce, dim3(na), dim3(1024), 0, st, dA, d_act, 4);
-            if (coll(3, 2, 1, 1)) return ORBHIP_ERR_DEVICE;
-            if (read_red(act)) return ORBHIP_ERR_DEVICE;
-            for (int b : act) { L[b].lambda = 1e-5 * ws->h_red[5 * b + 2]; L[b].ni = 2; L[b].nBad = 0; }
-        }
-        for (int b : act) { L[b].qmax = 0; L[b].rho = 0; }
-        std::vector<int> trial = act;
-        while (!trial.empty()) {
-            const unsigned nt_ = (unsigned)trial.size();
-            for (int b : trial) ws->h_lam[b] = L[b].lambda;
-            BAOK(hipMemcpyAsync(ws->lam.p, ws->h_lam, B * sizeof(double), hipMemcpyHostToDevice, st));
-            if (upload_act(trial)) return ORBHIP_ERR_DEVICE;
-            // S outside the block structure stays zero; it only needs clearing again when a solver
-            // factors S in place (or the shards' sums overwrite it)
-            if (!s_clean) hipLaunchKernelGGL(k_ba_zero_s, dim3(64, nt_), dim3(256), 0, st, dA, d_act, 1);
-            s_clean = s_readonly;
-            hipLaunchKernelGGL(k_ba_schur_points, dim3(gx(maxM, 256), nt_), dim3(256), 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_schur_items, dim3(gx(2 * maxItems, 256), nt_), dim3(256), 0, st, dA, d_act,
-                               (int)gx(2 * maxItems, 256));
-            hipLaunchKernelGGL(k_ba_schur_fin, dim3(gx(maxFin, 4), nt_), dim3(256), 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_schur_b, dim3(gx(maxNp, 4), nt_), dim3(256), 0, st, dA, d_act);
-            if (shard_mode) {   // reduced camera system of all shards
-                if (coll(1, 0, (size_t)pp[0].n * pp[0].n, 0) || coll(2, 0, (size_t)pp[0].n, 0)) return ORBHIP_ERR_DEVICE;
-            }
-            if (!any_large) {
-                if (maxN <= kCholRegMaxN) BAOK(chol_reg_launch(maxN, (int)nt_, dA, d_act, st));
-                else hipLaunchKernelGGL(k_ba_cholesky, dim3(nt_), dim3(512), chol_lds, st, dA, d_act);
-            } else {
-                // small problems: one workgroup each (act slot 3); large: the blocked solver
-                int ns = 0;
-                for (int b : trial)
-                    if (!large(b)) h_act[2 * B + ns++] = b;
-                if (ns) {
-                    BAOK(hipMemcpyAsync(d_act + 2 * B, h_act + 2 * B, ns * sizeof(int), hipMemcpyHostToDevice, st));
-                    if (maxN <= kCholRegMaxN) BAOK(chol_reg_launch(maxN, ns, dA, d_act + 2 * B, st));
-                    else hipLaunchKernelGGL(k_ba_cholesky, dim3(ns), dim3(512), chol_lds, st, dA, d_act + 2 * B);
-                }
-                for (int b : trial)
-                    if (large(b) && large_solve(b, nullptr)) return ORBHIP_ERR_DEVICE;
-            }
-            hipLaunchKernelGGL(k_ba_backsub, dim3(gx(std::max(maxM, maxP), 256), nt_), dim3(256), 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), nt_), dim3(256), 0, st, dA, d_act, 0, nullptr);
-            hipLaunchKernelGGL(k_ba_reduce, dim3(nt_), dim3(1024), 0, st, dA, d_act, 3 | 8);
-            if (coll(3, 0, 2, 0)) return ORBHIP_ERR_DEVICE;
-            // every shard's solve must agree on success, or the ranks' LM schedules (and so their
-            // collective sequences) diverge: RCCL sums the failure flags, the local model ANDs them
-            if (shard_mode == kShardRccl && coll(3, 3, 1, 0)) return ORBHIP_ERR_DEVICE;
-            BAOK(hipGetLastError());
-            if (read_red(trial)) return ORBHIP_ERR_DEVICE;
-            bool all_ok = true;
-            for (int b : trial) all_ok = all_ok && ws->h_red[5 * b + 4] != 0.0 && ws->h_red[5 * b + 3] == 0.0;
-            std::vector<int> pop, next;
-            for (int b : trial) {
-                LmState& s = L[b];
-                const bool ok2 = shard_mode == kShardNone ? ws->h_red[5 * b + 4] != 0.0   // gathered as a double
-                                                          : all_ok;
-                double tempChi = ok2 ? ws->h_red[5 * b] : dmax;
-                double rho = s.currentChi - tempChi;
-                rho /= (ws->h_red[5 * b + 1] + 1e-3);
-                if (rho > 0 && std::isfinite(tempChi)) {
-                    double alpha = 1. - std::pow((2 * rho - 1), 3);
-                    alpha = std::min(alpha, 2. / 3.);
-                    s.lambda *= std::max(1. / 3., alpha);
-                    s.ni = 2;
-                    if (probs[b]->early_stop) {
-                        if ((s.currentChi - tempChi) < 1e-3 * s.currentChi) s.nBad++;
-                        else s.nBad = 0;
-                    }
-                    s.currentChi = tempChi;
-                } else {
-                    s.lambda *= s.ni;
-                    s.ni *= 2;
-                    pop.push_back(b);
-                }
-                s.rho = rho;
-                s.qmax++;
-                s.trials++;
-                if (rho < 0 && s.qmax < 10 && !(shard_mode != kShardRccl && stop && *stop)) next.push_back(b);
-            }
-            if (!pop.empty()) {
-                // act slot 2 keeps the pop list away from the next round's upload
-                for (size_t i = 0; i < pop.size(); i++) h_act[B + i] = pop[i];
-                BAOK(hipMemcpyAsync(d_act + B, h_act + B, pop.size() * sizeof(int), hipMemcpyHostToDevice, st));
-                int maxPM = 0;
-                for (int b : pop) maxPM = std::max(maxPM, std::max(8 * pp[b].P, 3 * pp[b].M));
-                hipLaunchKernelGGL(k_ba_pop, dim3(gx(maxPM, 256), (unsigned)pop.size()), dim3(256), 0, st, dA,
-                                   d_act + B);
-            }
-            trial.swap(next);
-        }
-        for (int b : act) {
-            LmState& s = L[b];
-            s.it = it + 1;
-            s.errors_valid = s.rho > 0;   // rejected: device errors belong to the popped trial (g2o keeps them stale)
-            if (s.qmax == 10 || s.rho == 0) s.done = true;
-            if (probs[b]->early_stop && s.nBad >= 3) s.done = true;
-        }
-    }
-    }   // host-driven rounds
     const double t_solve = now();
     // ---- hand-off timeouts of the persistent solver: a timed-out solve fails its trial (flag 0),
     // which must never pass for a g2o rejection. Counted per problem (control word 3), read with
@@ -1939,6 +2034,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     for (int b = 0; b < B; b++) {
         if (pp[b].use_dag) tw.push_back(dd[b].ints + 3);
         if (pp[b].use_nd) nd_timeout_words(ws->nd, tw);
+        if (pp[b].use_nd_sh) nd_timeout_words(ws->nds[b], tw);
     }
     const int ndag = (int)tw.size();
     if (ndag) {
@@ -2026,6 +2122,8 @@ int ba_comm_init(BaWorkspace* ws, int nranks, int rank, const void* id) {
     ws->nranks = nranks;
     ws->rank = rank;
     BAOK(ws->dstop.ensure(1));
+    BAOK(ws->dint4.ensure(4));
+    if (!ws->h_int4) BAOK(hipHostMalloc((void**)&ws->h_int4, 4 * sizeof(int), hipHostMallocDefault));
     if (!ws->h_stop) BAOK(hipHostMalloc((void**)&ws->h_stop, sizeof(int), hipHostMallocDefault));
     return ORBHIP_OK;
 }

@@ -409,8 +409,13 @@ __global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict
                                                    const ConeRect* __restrict__ rects, const int* __restrict__ ctab,
                                                    int tab_stride, int xrun, int s0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t cone[];
+    if (fb.stamp && threadIdx.x == 0) atomicMin(fb.stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
     pyr_cone_body(P, fb, rects, ctab, tab_stride, cone, lg % X, lg / X, s0);
+    if (fb.stamp) {   // the workgroup's end: every wave's stores drained (the barrier waits on them)
+        __syncthreads();
+        if (threadIdx.x == 0) atomicMax(fb.stamp + kStampStride, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
 }
 
 // ---------------------------------------------------------------------------

@@ -698,6 +698,8 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
                                            : (size_t)1024;
         const bool cone_path = pl->cone_tiles && !no_cone && (size_t)B * pl->cone_tiles <= cone_max;
         const bool cone_hi = !cone_path && pl->cone_hi_tiles && cone_hi_on;
+        // the one-launch pyramid stamps its own execution span for the stage timer
+        fb.stamp = (cone_path && tm.stage == 1 && tm.dstamp && tm.n < StageTimer::kCap) ? tm.dstamp + tm.n : nullptr;
         if (cone_path) {
             launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_cone_tab.p,
                             pl->cone_tab_stride, st);
@@ -841,8 +843,10 @@ int orbhip_destroy(orbhip_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->graphs.graphs()) (void)hipDeviceSynchronize();   // replays may run on caller streams
     c->graphs.clear();
-    if (c->timer.created)
+    if (c->timer.created) {
         for (int i = 0; i < 2 * StageTimer::kCap; i++) (void)hipEventDestroy(c->timer.ev[i]);
+        if (c->timer.dstamp) (void)hipFree(c->timer.dstamp);
+    }
     ba_destroy(c->ba);
     if (c->stream) dag_stream_retired(c->stream);   // before the stream goes: no solve may wait on it
     pose_ws_destroy(c->pose);
@@ -1042,9 +1046,12 @@ int orbhip_profile_stage(orbhip_ctx* c, int stage) {
     StageTimer& t = c->timer;
     if (!t.created) {
         for (int i = 0; i < 2 * StageTimer::kCap; i++) HIPOK(hipEventCreate(&t.ev[i]));
+        HIPOK(hipMalloc((void**)&t.dstamp, 2 * StageTimer::kCap * sizeof(unsigned long long)));
         t.created = true;
     }
     HIPOK(hipDeviceSynchronize());
+    HIPOK(hipMemset(t.dstamp, 0xFF, StageTimer::kCap * sizeof(unsigned long long)));   // minima: ~0
+    HIPOK(hipMemset(t.dstamp + StageTimer::kCap, 0, StageTimer::kCap * sizeof(unsigned long long)));
     t.stage = stage;
     t.n = 0;
     return ORBHIP_OK;
@@ -1060,6 +1067,26 @@ int orbhip_profile_collect(orbhip_ctx* c, double* total_ms, int32_t* count) {
         float ms = 0;
         HIPOK(hipEventElapsedTime(&ms, t.ev[2 * i], t.ev[2 * i + 1]));
         s += ms;
+    }
+    // the pyramid's k_pyr_cone also stamps its execution span from the device (first workgroup
+    // start -> last workgroup end, as rocprofv3's kernel trace counts it): used when every timed
+    // launch stamped (the k_resize cascade of batches does not)
+    if (t.stage == 1 && t.n > 0 && t.dstamp) {
+        std::vector<unsigned long long> h(2 * (size_t)t.n);
+        HIPOK(hipMemcpy(h.data(), t.dstamp, t.n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        HIPOK(hipMemcpy(h.data() + t.n, t.dstamp + StageTimer::kCap, t.n * sizeof(unsigned long long),
+                        hipMemcpyDeviceToHost));
+        int rate_khz = 0;
+        HIPOK(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, c->device));
+        bool all = rate_khz > 0;
+        double d = 0;
+        for (int i = 0; i < t.n && all; i++) {
+            all = h[t.n + i] != 0 && h[i] != ~0ull && h[t.n + i] >= h[i];
+            d += (double)(h[t.n + i] - h[i]);
+        }
+        if (all) s = d / rate_khz;   // ticks / kHz = ms
+        HIPOK(hipMemset(t.dstamp, 0xFF, t.n * sizeof(unsigned long long)));
+        HIPOK(hipMemset(t.dstamp + StageTimer::kCap, 0, t.n * sizeof(unsigned long long)));
     }
     *total_ms = s;
     *count = t.n;
@@ -1534,6 +1561,26 @@ int orbhip_test_trace(int on, unsigned long long* out) {
     trace_set_extract(nullptr);
     trace_set_match(nullptr);
     trace_set_proj(nullptr);
+    return ORBHIP_OK;
+}
+
+// FAST candidates of frame `frame` of the context's last extraction at w x h (sum over its cells):
+// the octree's input size, for the bench's algorithmic bytes of k_octree
+int orbhip_test_candidates(orbhip_ctx* c, int w, int h, int frame, int64_t* n) {
+    if (!c || !n || frame < 0) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    Plan* pl = nullptr;
+    const int rc = build_plan(c, w, h, &pl);
+    if (rc) return rc;
+    const size_t nc = (size_t)pl->h.n_cells_total;
+    if (!c->d_cand_cnt.p || c->d_cand_cnt.n < (frame + 1) * nc) return ORBHIP_ERR_ARG;
+    std::vector<int> cnt(nc);
+    HIPOK(hipStreamSynchronize(c->stream));
+    HIPOK(hipDeviceSynchronize());
+    HIPOK(hipMemcpy(cnt.data(), c->d_cand_cnt.p + frame * nc, nc * sizeof(int), hipMemcpyDeviceToHost));
+    int64_t s = 0;
+    for (int v : cnt) s += v;
+    *n = s;
     return ORBHIP_OK;
 }
 

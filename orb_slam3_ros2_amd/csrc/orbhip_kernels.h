@@ -15,7 +15,12 @@ struct FrameBufs {
     int in_stride;
     int64_t in_fstride;
     uint8_t* pyr;          // levels >= 1
+    // live timing of the launch (stage timer, pyramid stage): the earliest workgroup start is
+    // atomic-min'ed into stamp[0], the latest end (after its stores drained) max'ed into
+    // stamp[kStampStride], both s_memrealtime; null: not timed
+    unsigned long long* stamp = nullptr;
 };
+constexpr int kStampStride = 8192;   // == StageTimer::kCap
 
 struct OctreeCfg {
     int node_cap;          // LDS node capacity (>= max list size of any level)
@@ -40,6 +45,7 @@ struct StageTimer {
     hipEvent_t ev[2 * kCap];
     bool created = false;
     bool used = false;                // a kernel of the open stage carries this pair
+    unsigned long long* dstamp = nullptr;   // device: kCap start minima, then kCap end maxima (FrameBufs::stamp)
     void begin(int s, hipStream_t) {
         if (s == stage && n < kCap) { used = false; g_stage_timer = this; }
     }
