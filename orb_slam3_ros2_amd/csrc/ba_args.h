@@ -57,6 +57,8 @@ struct BaArgs {
     const double* Hpp_g;        // the pose Hessians summed over the shards (== Hpp unsharded)
     int small;         // unsharded, small enough for the trial's last workgroup to restore a rejected state
                        // and refresh its stale errors itself (no k_ba_pop / k_ba_errors(1) launch per slot)
+    int fused;         // small and unsharded: the back-substitution computes the trial's errors too
+                       // (k_ba_backsub_errs): the trial's poses go to pose_bak until the controller commits
     int sync;          // sharded device-driven rounds: the controller's reductions and decisions run as their
                        // own launches (a collective between them), not in the last workgroup of k_ba_lin /
                        // k_ba_errors(2)

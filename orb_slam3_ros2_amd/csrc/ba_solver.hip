@@ -129,9 +129,7 @@ __device__ void ctl_begin_body(const BaArgs& a, int nlin);
 // ---------------------------------------------------------------------------
 // one edge: error, chi2, robust rho (EdgeSE3ProjectXYZ::computeError + RobustKernelHuber::robustify);
 // returns rho0
-__device__ __forceinline__ double edge_error(const BaArgs& a, int e) {
-    const double* T = a.pose + 8 * a.e_pose[e];
-    const double* X = a.pts + 3 * a.e_pt[e];
+__device__ __forceinline__ double edge_error_at(const BaArgs& a, int e, const double* T, const double* X) {
     double cx, cy, cz;
     qrot(load_q(T), X[0], X[1], X[2], cx, cy, cz);
     cx += T[4]; cy += T[5]; cz += T[6];
@@ -153,6 +151,9 @@ __device__ __forceinline__ double edge_error(const BaArgs& a, int e) {
     a.e_rho0[e] = r0;
     a.e_rho1[e] = r1;
     return r0;
+}
+__device__ __forceinline__ double edge_error(const BaArgs& a, int e) {
+    return edge_error_at(a, e, a.pose + 8 * a.e_pose[e], a.pts + 3 * a.e_pt[e]);
 }
 
 // when == 2 (a trial) ends in the trial's controller step, run by the last workgroup of each
@@ -868,6 +869,55 @@ __global__ __launch_bounds__(256) void k_ba_backsub(const BaArgs* __restrict__ a
     if (threadIdx.x == 0) a.part[a.npart_e + bx_] = t;
 }
 
+// small problems (BaArgs::fused): the back-substitution and the trial's errors in ONE launch, no
+// k_ba_errors(2) after it. The trial's poses go to pose_bak (pose keeps the accepted state until
+// the controller commits), so the thread of landmark m takes each of its edges' pose update on the
+// fly (se3_update of the unmoved pose) and its own new point; chi2 and the landmark scale terms
+// leave as workgroup partials and the problem's last workgroup runs the controller step
+// (ctl_end_body: commit or take the points back)
+__global__ __launch_bounds__(256) void k_ba_backsub_errs(const BaArgs* __restrict__ args, const int* __restrict__ act,
+                                                         int* done) {
+    BA_PROLOGUE
+    BA_PHASE(kPhTrial)
+    const int m = bx_ * blockDim.x + threadIdx.x;
+    const int nwg = (max(a.M, a.P) + 255) / 256;   // this problem's partial slots (<= npart_e: host-checked)
+    if (m < a.P) {
+        double T[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) T[k] = a.pose[8 * m + k];
+        const int oi = a.opt[m];
+        if (oi >= 0) se3_update(a.x + 6 * oi, T);
+#pragma unroll
+        for (int k = 0; k < 8; k++) a.pose_bak[8 * m + k] = T[k];
+    }
+    double sc = 0.0, chi = 0.0;
+    if (m < a.M) {
+        sc = backsub_point(a, m);
+        const double* X = a.pts + 3 * m;
+        for (int k = a.pt_ptr[m]; k < a.pt_ptr[m + 1]; k++) {
+            const int e = a.pt_edges[k];
+            const int p = a.e_pose[e];
+            double T[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) T[q] = a.pose[8 * p + q];
+            const int oi = a.opt[p];
+            if (oi >= 0) se3_update(a.x + 6 * oi, T);
+            chi += edge_error_at(a, e, T, X);
+        }
+    }
+    __shared__ double sh[4];
+    __shared__ int lastf;
+    const double tc = block_sum(chi, sh);
+    const double ts = block_sum(sc, sh);
+    if (threadIdx.x == 0 && bx_ < nwg) {
+        st_agent(a.part + bx_, tc);
+        st_agent(a.part + a.npart_e + bx_, ts);
+    }
+    if (bx_ == 0)   // the chi2 slots past this problem's workgroups
+        for (int i = nwg + (int)threadIdx.x; i < a.npart_e; i += blockDim.x) st_agent(a.part + i, 0.0);
+    if (last_arrival(&a.ctl->arrive_t, gridDim.x, &lastf)) ctl_end_body(a, act[by_], done, sh);
+}
+
 // restore the pushed state: host-driven rounds list the rejected problems in act[]; device-driven
 // rounds restore every problem whose controller flagged its trial rejected (ctl->pop)
 __global__ __launch_bounds__(256) void k_ba_pop(const BaArgs* __restrict__ args, const int* __restrict__ act) {
@@ -1077,11 +1127,20 @@ __device__ void ctl_end_body(const BaArgs& a, int prob, int* done_flags, double*
     if (!a.small) return;
     // a small problem: this workgroup restores a rejected trial's state (k_ba_pop) and, when the
     // iteration ended on it, recomputes the errors of the restored state (k_ba_errors(1): g2o's
-    // computeActiveErrors at the next iteration's start), so neither needs a launch of its own
+    // computeActiveErrors at the next iteration's start), so neither needs a launch of its own.
+    // Fused trials (k_ba_backsub_errs) left the poses unmoved and the new ones in pose_bak: an
+    // accepted trial commits them, a rejected one only takes the points back
     __syncthreads();
     const LmCtl& c = *a.ctl;
-    if (!c.pop) return;
-    for (int i = threadIdx.x; i < 8 * a.P; i += blockDim.x) a.pose[i] = a.pose_bak[i];
+    if (a.fused) {
+        if (!c.pop) {
+            for (int i = threadIdx.x; i < 8 * a.P; i += blockDim.x) a.pose[i] = a.pose_bak[i];
+            return;
+        }
+    } else {
+        if (!c.pop) return;
+        for (int i = threadIdx.x; i < 8 * a.P; i += blockDim.x) a.pose[i] = a.pose_bak[i];
+    }
     for (int i = threadIdx.x; i < 3 * a.M; i += blockDim.x) a.pts[i] = a.pts_bak[i];
     if (c.phase != kPhBuild || c.errors_valid) return;
     __syncthreads();
@@ -1686,6 +1745,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         if (sharded) { a.Hpp_g = r; r += 36 * (size_t)p.np; }
         a.sync = sharded ? 1 : 0;
         a.small = (!sharded && 8 * P + 3 * M <= 32768 && E <= 65536) ? 1 : 0;
+        a.fused = 0;   // set below once the batch's launch width is known
         a.b = r; r += p.n + 3 * M;
         a.x = r; r += p.n + 3 * M;
         a.bs = r; r += p.n;
@@ -1911,6 +1971,16 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         const dim3 gB((unsigned)((B + 255) / 256)), b256(256);
         bool all_small = true;   // every problem restores / refreshes in its trial's last workgroup
         for (int b = 0; b < B; b++) all_small = all_small && ha[b].small;
+        // ... and takes its errors inside the back-substitution when its partial slots hold the
+        // fused kernel's workgroups (ORBHIP_BA_FUSED=0 keeps the separate k_ba_errors(2))
+        const unsigned gbs = gx(std::max(maxM, maxP), 256);
+        static const bool fuse_env = !(std::getenv("ORBHIP_BA_FUSED") && std::getenv("ORBHIP_BA_FUSED")[0] == '0');
+        bool fused = all_small && fuse_env;
+        for (int b = 0; b < B && fused; b++) fused = (int)gbs <= ha[b].npart_e;
+        if (fused) {
+            for (int b = 0; b < B; b++) ha[b].fused = 1;
+            BAOK(hipMemcpyAsync(ws->args.p, ha, B * sizeof(BaArgs), hipMemcpyHostToDevice, st));
+        }
         auto slot = [&]() -> int {
             if (!all_small) hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 1, ws->d_done);
             hipLaunchKernelGGL(k_ba_lin, dim3(gx(maxM, 256) + gx(maxNp, 4), B), b256, 0, st, dA, d_act,
@@ -1943,8 +2013,12 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 for (int b = 0; b < B; b++)
                     if (large(b) && large_solve(b, &dctl[b].phase)) return ORBHIP_ERR_DEVICE;
             }
-            hipLaunchKernelGGL(k_ba_backsub, dim3(gx(std::max(maxM, maxP), 256), B), b256, 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 2, ws->d_done);
+            if (fused) {
+                hipLaunchKernelGGL(k_ba_backsub_errs, dim3(gbs, B), b256, 0, st, dA, d_act, ws->d_done);
+            } else {
+                hipLaunchKernelGGL(k_ba_backsub, dim3(gx(std::max(maxM, maxP), 256), B), b256, 0, st, dA, d_act);
+                hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 2, ws->d_done);
+            }
             if (sharded) {   // the trial's end on the shards' sums of chi2 and the scale
                 hipLaunchKernelGGL(k_ba_sh_sums, dim3(B), dim3(1024), 0, st, dA, d_act);
                 if (coll(kRed01)) return ORBHIP_ERR_DEVICE;

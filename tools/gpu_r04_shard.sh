@@ -16,3 +16,5 @@ grep -v amdgpu.ids gpurun_out/r04_shard/bench.log | tail -1 | python3 -c "
 import json,sys; d=json.loads(sys.stdin.read()); r=d['roofline']
 print('value', d['value'], 'batch1', d['batch1_latency_ms'], r['kernel'], r['bound'], r['avg_launch_ms'], r['frac'], r.get('octree_candidates_per_frame'))
 print(r['stage_avg_ms'])"
+timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r04_shard/prof_nd -o nd -- python3 -u tools/time_shard_nd.py 8 > gpurun_out/r04_shard/prof_nd.log 2>&1 || { tail -5 gpurun_out/r04_shard/prof_nd.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/r04_shard/prof_nd.log | tail -3
