@@ -128,8 +128,11 @@ __global__ __launch_bounds__(256) void k_nd_backsolve(NdDev d) {
             if (R < s.rf[Rp]) continue;
             const double* t = s.buf + dag_off_L(s.NT, Rp, R);
             const double* xr = xs + Rp * kT;
-#pragma unroll 8
-            for (int r = 0; r < kT; r++) acc = fma(t[tq(r, c)], xr[r], acc);
+            double v[kT];   // the tile column's 32 loads in flight together
+#pragma unroll
+            for (int r = 0; r < kT; r++) v[r] = t[tq(r, c)];
+#pragma unroll
+            for (int r = 0; r < kT; r++) acc = fma(v[r], xr[r], acc);
         }
         part[g * kT + c] = acc;
         __syncthreads();
@@ -141,8 +144,12 @@ __global__ __launch_bounds__(256) void k_nd_backsolve(NdDev d) {
         __syncthreads();
         if (tid < kT) {   // x_R = Linv_R^T s
             const double* li = s.buf + dag_off_Linv(s.NT, R);
+            double lv[kT];
+#pragma unroll
+            for (int q = 0; q < kT; q++) lv[q] = li[tq(q, tid)];
             double v = 0.0;
-            for (int q = 0; q < kT; q++) v = fma(li[tq(q, tid)], sv[q], v);
+#pragma unroll
+            for (int q = 0; q < kT; q++) v = fma(lv[q], sv[q], v);
             xs[R * kT + tid] = v;
         }
         __syncthreads();
@@ -306,8 +313,8 @@ bool nd_blocks_fit(const NdPlan& p, int r, const int* bi, const int* bj, int nbl
         return q >= z0 && q < z0 + w;
     };
     (void)own;
-    for (int b = 0; b < nblk; b++)
-        if (!in(bi[b]) || !in(bj[b])) return false;
+    for (int b = 0; b < nblk; b++)   // a pose's own block may be empty here (the solver lists every diagonal)
+        if (bi[b] != bj[b] && (!in(bi[b]) || !in(bj[b]))) return false;
     return true;
 }
 

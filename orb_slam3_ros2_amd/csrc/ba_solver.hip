@@ -414,7 +414,17 @@ __device__ __forceinline__ void inv3(const double m[9], double r[9]) {
     r[8] = (m[0] * m[4] - m[1] * m[3]) * id;
 }
 
-// one thread per landmark: setLambda on Hll, Dinv (Eigen 3x3 cofactor inverse), db = Dinv b_l
+// Dinv of landmark m = (Hll + lambda I)^-1 (Eigen 3x3 cofactor inverse)
+__device__ __forceinline__ void dinv_of(const BaArgs& a, int m, double Di[9]) {
+    const double lambda = *a.lambda;
+    double D[9];
+#pragma unroll
+    for (int k = 0; k < 9; k++) D[k] = a.Hll[9 * m + k] + (k % 4 == 0 ? lambda : 0.0);
+    inv3(D, Di);
+}
+
+// one thread per landmark: setLambda on Hll, Dinv (Eigen 3x3 cofactor inverse), db = Dinv b_l.
+// Fused trials (BaArgs::fused) skip this launch: every consumer forms Dinv (the same bits) itself
 __global__ __launch_bounds__(256) void k_ba_schur_points(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
     BA_PHASE(kPhTrial)
@@ -476,7 +486,13 @@ __global__ __launch_bounds__(256) void k_ba_schur_items(const BaArgs* __restrict
     for (int k = wi.x; k < wi.y; k++) {
         const int2 pr = ((const int2*)a.blk_pairs)[k];
         const double4 la = ((const double4*)a.e_lin)[pr.x], lb = ((const double4*)a.e_lin)[pr.y];
-        const double* Di = a.Dinv + 9 * a.e_pt[pr.x];
+        double Di[9];   // in registers either way (a pointer choice would put a local copy in scratch)
+        if (a.fused) {
+            dinv_of(a, a.e_pt[pr.x], Di);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 9; k++) Di[k] = a.Dinv[9 * a.e_pt[pr.x] + k];
+        }
         // the projection Jacobians of both edges (proj_jac); A and B are used through their structure
         double ja[4], jb[4];
         proj_jac(fx, fy, la.x, la.y, la.z, ja);
@@ -580,8 +596,19 @@ __device__ __forceinline__ void schur_b_pose(const BaArgs& a, int i, int lane) {
         const int e = a.ps_edges[k];
         double A[6], B[12];
         const double w = lin_ab(a, e, i, A, B);
-        const double* d = a.db + 3 * a.e_pt[e];
-        const double d0 = d[0], d1 = d[1], d2 = d[2];
+        double d0, d1, d2;
+        if (a.fused) {   // db = Dinv b_l, formed here
+            const int m = a.e_pt[e];
+            double Di[9];
+            dinv_of(a, m, Di);
+            const double* bl = a.b + a.n + 3 * m;
+            d0 = Di[0] * bl[0] + Di[1] * bl[1] + Di[2] * bl[2];
+            d1 = Di[3] * bl[0] + Di[4] * bl[1] + Di[5] * bl[2];
+            d2 = Di[6] * bl[0] + Di[7] * bl[1] + Di[8] * bl[2];
+        } else {
+            const double* d = a.db + 3 * a.e_pt[e];
+            d0 = d[0]; d1 = d[1]; d2 = d[2];
+        }
         const double v0 = w * (A[0] * d0 + A[1] * d1 + A[2] * d2), v1 = w * (A[3] * d0 + A[4] * d1 + A[5] * d2);
 #pragma unroll
         for (int r = 0; r < 6; r++) acc[r] += B[r] * v0 + B[6 + r] * v1;
@@ -832,7 +859,13 @@ __device__ __forceinline__ double backsub_point(const BaArgs& a, int m) {
 #pragma unroll
         for (int cc = 0; cc < 3; cc++) c[cc] -= A[cc] * u0 + A[3 + cc] * u1;
     }
-    const double* Di = a.Dinv + 9 * m;
+    double Di[9];
+    if (a.fused) {
+        dinv_of(a, m, Di);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 9; k++) Di[k] = a.Dinv[9 * m + k];
+    }
     double* X = a.pts + 3 * m;
     const double lambda = *a.lambda;
     double sc = 0.0;
@@ -871,42 +904,50 @@ __global__ __launch_bounds__(256) void k_ba_backsub(const BaArgs* __restrict__ a
 
 // small problems (BaArgs::fused): the back-substitution and the trial's errors in ONE launch, no
 // k_ba_errors(2) after it. The trial's poses go to pose_bak (pose keeps the accepted state until
-// the controller commits), so the thread of landmark m takes each of its edges' pose update on the
-// fly (se3_update of the unmoved pose) and its own new point; chi2 and the landmark scale terms
+// the controller commits). Every workgroup forms all P new poses in LDS (P <= kFusedMaxP: a few
+// se3 updates per thread), back-substitutes its 256 landmarks (new points in LDS too), then takes
+// the errors of those landmarks' edges, spread over its threads. chi2 and the landmark scale terms
 // leave as workgroup partials and the problem's last workgroup runs the controller step
-// (ctl_end_body: commit or take the points back)
+// (ctl_end_body: commit the poses or take the points back)
+constexpr int kFusedMaxP = 512;
 __global__ __launch_bounds__(256) void k_ba_backsub_errs(const BaArgs* __restrict__ args, const int* __restrict__ act,
                                                          int* done) {
     BA_PROLOGUE
     BA_PHASE(kPhTrial)
-    const int m = bx_ * blockDim.x + threadIdx.x;
-    const int nwg = (max(a.M, a.P) + 255) / 256;   // this problem's partial slots (<= npart_e: host-checked)
-    if (m < a.P) {
-        double T[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) T[k] = a.pose[8 * m + k];
-        const int oi = a.opt[m];
-        if (oi >= 0) se3_update(a.x + 6 * oi, T);
-#pragma unroll
-        for (int k = 0; k < 8; k++) a.pose_bak[8 * m + k] = T[k];
-    }
-    double sc = 0.0, chi = 0.0;
-    if (m < a.M) {
-        sc = backsub_point(a, m);
-        const double* X = a.pts + 3 * m;
-        for (int k = a.pt_ptr[m]; k < a.pt_ptr[m + 1]; k++) {
-            const int e = a.pt_edges[k];
-            const int p = a.e_pose[e];
-            double T[8];
-#pragma unroll
-            for (int q = 0; q < 8; q++) T[q] = a.pose[8 * p + q];
-            const int oi = a.opt[p];
-            if (oi >= 0) se3_update(a.x + 6 * oi, T);
-            chi += edge_error_at(a, e, T, X);
-        }
-    }
+    __shared__ double Tn[8 * kFusedMaxP];   // the trial's poses
+    __shared__ double Xn[3 * 256];          // this workgroup's new points
     __shared__ double sh[4];
     __shared__ int lastf;
+    const int nwg = (max(a.M, a.P) + 255) / 256;   // this problem's partial slots (<= npart_e: host-checked)
+    for (int p = threadIdx.x; p < a.P; p += blockDim.x) {
+        double T[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) T[k] = a.pose[8 * p + k];
+        const int oi = a.opt[p];
+        if (oi >= 0) se3_update(a.x + 6 * oi, T);
+#pragma unroll
+        for (int k = 0; k < 8; k++) Tn[8 * p + k] = T[k];
+        if (bx_ == 0) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) a.pose_bak[8 * p + k] = T[k];
+        }
+    }
+    const int m0 = bx_ * 256, m = m0 + threadIdx.x;
+    double sc = 0.0;
+    if (m < a.M) {
+        sc = backsub_point(a, m);
+#pragma unroll
+        for (int r = 0; r < 3; r++) Xn[3 * threadIdx.x + r] = a.pts[3 * m + r];
+    }
+    __syncthreads();
+    double chi = 0.0;
+    if (m0 < a.M) {
+        const int k0 = a.pt_ptr[m0], k1 = a.pt_ptr[min(m0 + 256, a.M)];
+        for (int k = k0 + (int)threadIdx.x; k < k1; k += blockDim.x) {
+            const int e = a.pt_edges[k];
+            chi += edge_error_at(a, e, Tn + 8 * a.e_pose[e], Xn + 3 * (a.e_pt[e] - m0));
+        }
+    }
     const double tc = block_sum(chi, sh);
     const double ts = block_sum(sc, sh);
     if (threadIdx.x == 0 && bx_ < nwg) {
@@ -1873,7 +1914,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             LmCtl& c = ws->hctl.p[b];
             c = LmCtl{};
             c.ni = 2;
-            c.phase = kPhBuild;
+            c.phase = probs[b]->iterations > 0 ? kPhBuild : kPhDone;   // optimize(0): nothing to run
             c.errors_valid = 1;
             c.iterations = probs[b]->iterations;
             c.early_stop = probs[b]->early_stop;
@@ -1976,7 +2017,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         const unsigned gbs = gx(std::max(maxM, maxP), 256);
         static const bool fuse_env = !(std::getenv("ORBHIP_BA_FUSED") && std::getenv("ORBHIP_BA_FUSED")[0] == '0');
         bool fused = all_small && fuse_env;
-        for (int b = 0; b < B && fused; b++) fused = (int)gbs <= ha[b].npart_e;
+        for (int b = 0; b < B && fused; b++) fused = (int)gbs <= ha[b].npart_e && pp[b].P <= kFusedMaxP;
         if (fused) {
             for (int b = 0; b < B; b++) ha[b].fused = 1;
             BAOK(hipMemcpyAsync(ws->args.p, ha, B * sizeof(BaArgs), hipMemcpyHostToDevice, st));
@@ -1992,7 +2033,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 hipLaunchKernelGGL(k_ba_sh_begin, dim3(B), dim3(64), 0, st, dA, d_act);
             }
             if (!s_readonly) hipLaunchKernelGGL(k_ba_zero_s, dim3(64, B), b256, 0, st, dA, d_act, 0);
-            hipLaunchKernelGGL(k_ba_schur_points, dim3(gx(maxM, 256), B), b256, 0, st, dA, d_act);
+            if (!fused) hipLaunchKernelGGL(k_ba_schur_points, dim3(gx(maxM, 256), B), b256, 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_schur_items, dim3(gx(2 * maxItems, 256) + gx(maxNp, 4), B), b256, 0, st, dA, d_act,
                                (int)gx(2 * maxItems, 256));
             hipLaunchKernelGGL(k_ba_schur_fin, dim3(gx(maxFin, 4), B), b256, 0, st, dA, d_act);
@@ -2046,7 +2087,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             BAOK(hipHostGetDevicePointer((void**)&ws->d_done, ws->h_done, 0));
             ws->done_cap = B;
         }
-        for (int b = 0; b < B; b++) __atomic_store_n(ws->h_done + b, 0, __ATOMIC_RELAXED);
+        for (int b = 0; b < B; b++) __atomic_store_n(ws->h_done + b, probs[b]->iterations > 0 ? 0 : 1, __ATOMIC_RELAXED);
         auto all_done = [&] {
             for (int b = 0; b < B; b++)
                 if (!__atomic_load_n(ws->h_done + b, __ATOMIC_RELAXED)) return false;

@@ -25,10 +25,15 @@ def _close(g, o):
     assert np.abs(g.points.astype(np.float64) - o["points"]).max() / max(1.0, np.abs(o["points"]).max()) < REL
 
 
-def _solve_segments(opt, p, K):
+def _solve_segments(opt, p, K, dissected=True):
     from orb_slam3_ros2_amd.sharding import merge_results_nd, shard_problem_nd
     parts = [shard_problem_nd(p, r, K) for r in range(K)]
+    l0 = opt.stats()["dag_launches"]
     res = opt.solve_shards_local([q[0] for q in parts])
+    # the dissected form launches two persistent solves per shard and trial (its segment's partial
+    # factorization, the separator system), the replicated form one (the summed S)
+    per = (opt.stats()["dag_launches"] - l0) / (K * res[0].lm_trials)
+    assert per >= 2 if dissected else per < 2, per
     for r in res[1:]:
         assert np.array_equal(r.pose_t, res[0].pose_t)   # every shard applies the same pose update
     return merge_results_nd(p, res, [q[1] for q in parts], [q[2] for q in parts])
@@ -56,4 +61,4 @@ def test_segment_shards_replicated_fallback(c5_case, monkeypatch):
     from orb_slam3_ros2_amd import Optimizer
     monkeypatch.setenv("ORBHIP_SHARD_ND", "0")
     _, p, o = c5_case
-    _close(_solve_segments(Optimizer(), p, 4), o)
+    _close(_solve_segments(Optimizer(), p, 4, dissected=False), o)
