@@ -198,7 +198,10 @@ int orbhip_frontend_context(orbhip_frontend* fe, int j, orbhip_ctx** out);
  * orbhip_profile_stage selects ONE stage whose launches are bracketed by hipEvents on the
  * stream they run on (0 off, 1 pyramid resize, 2 FAST cells, 3 octree, 4 orientation +
  * descriptor, 5 Hamming top-2, 6 rotation filter). orbhip_profile_collect synchronises and
- * returns the summed duration (ms) and the number of bracketed launches, then resets. */
+ * returns the summed duration (ms) and the number of bracketed launches, then resets. The one-launch
+ * pyramid (k_pyr_cone) and the octree also time themselves on the device (first workgroup start to
+ * last workgroup end, s_memrealtime: the span rocprofv3's kernel trace reports); their stages
+ * return that span when every launch recorded it, the event pairs otherwise. */
 int orbhip_profile_stage(orbhip_ctx* ctx, int stage);
 int orbhip_profile_collect(orbhip_ctx* ctx, double* total_ms, int32_t* count);
 

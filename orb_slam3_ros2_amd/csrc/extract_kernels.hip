@@ -975,9 +975,17 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                                                  const int* __restrict__ cand_off,
                                                  uint32_t* __restrict__ kscratch, uint16_t* __restrict__ nscratch,
                                                  LevelKp* __restrict__ lvl_kp, int* __restrict__ lvl_cnt,
-                                                 int* __restrict__ lvl_nlap, OctreeCfg cfg, int* __restrict__ err) {
+                                                 int* __restrict__ lvl_nlap, OctreeCfg cfg, int* __restrict__ err,
+                                                 unsigned long long* __restrict__ stamp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     TR_BEGIN()
+    // live timing (stage timer): the earliest workgroup start, the latest end (FrameBufs::stamp)
+    if (stamp && threadIdx.x == 0) atomicMin(stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    auto stamp_end = [&]() {
+        if (!stamp) return;
+        __syncthreads();   // every wave's stores drained
+        if (threadIdx.x == 0) atomicMax(stamp + kStampStride, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    };
     // grid (frame, level): the level-0 work-groups (the longest) of every frame dispatch first
     const int f = blockIdx.x, l = blockIdx.y;
     const LevelGeom& G = P->lv[l];
@@ -1587,6 +1595,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
         if (run(std::true_type{})) {
             TR_PHASE(2, 63)
             TR_END(2)
+            stamp_end();
             return;
         }
         // a node too deep for the pyramid: the sweep path from the gather on
@@ -1596,6 +1605,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
     run(std::false_type{});
     TR_PHASE(2, 63)
     TR_END(2)
+    stamp_end();
 }
 
 // ---------------------------------------------------------------------------
@@ -2094,11 +2104,12 @@ size_t octree_lds_bytes(const ExtractPlan& hP, const OctreeCfg& cfg) {
 void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const uint16_t* otab,
                    const uint32_t* cand,
                    const int* cand_cnt, const int* cand_off, uint32_t* kscratch, uint16_t* nscratch, LevelKp* lvl_kp,
-                   int* lvl_cnt, int* lvl_nlap, const OctreeCfg& cfg, int* err, int B, hipStream_t st) {
+                   int* lvl_cnt, int* lvl_nlap, const OctreeCfg& cfg, int* err, int B, hipStream_t st,
+                   unsigned long long* stamp) {
     const size_t lds = octree_lds_bytes(hP, cfg);
     dim3 grd(B, hP.n_levels, 1);
     ORBHIP_LAUNCH(k_octree, grd, dim3(1024), lds, st, dP, cells, otab, cand, cand_cnt, cand_off, kscratch, nscratch,
-                  lvl_kp, lvl_cnt, lvl_nlap, cfg, err);
+                  lvl_kp, lvl_cnt, lvl_nlap, cfg, err, stamp);
 }
 
 constexpr int kDescKpMaxSlots = 16384;

@@ -52,16 +52,20 @@ __device__ __forceinline__ void top2_merge(int& b, int& i, int& s, int b2, int i
 // train chunk broadcast from LDS; wave w scans its quarter of the chunk in index order (strict <:
 // the first index wins), the 4 waves merge in index order. part[(pair, chunk, q)] =
 // {best | second << 16, index}.
+// xrun > 0 (batches): the dispatch order is remapped (xcd_runs) so that each XCD receives whole
+// pairs: a pair's train chunk and query blocks are then read by ONE L2, not by all eight.
 template <int TC>
 __global__ __launch_bounds__(256) void k_match_top2(MatchView v, uint2* __restrict__ part, int nchunk_cap,
-                                                     int part_stride) {
+                                                     int part_stride, int xrun) {
     __shared__ __attribute__((aligned(16))) uint4 tile[TC * 2];
     __shared__ int mb[3][64], mi[3][64], ms[3][64];
     TR_BEGIN()
-    const int p = blockIdx.z;
+    const int X = gridDim.x, XY = gridDim.x * gridDim.y;
+    const int lg = xcd_runs(blockIdx.x + X * (blockIdx.y + gridDim.y * blockIdx.z), XY * gridDim.z, xrun);
+    const int p = lg / XY, bx = lg % X, by = (lg % XY) / X;
     const int nq = v.nq_arr ? v.nq_arr[p] : v.nq;
     const int nt = v.nt_arr ? v.nt_arr[p] : v.nt;
-    const int q0 = blockIdx.x * 64, t0 = blockIdx.y * TC;
+    const int q0 = bx * 64, t0 = by * TC;
     if (q0 >= nq || t0 >= nt) return;   // workgroup-uniform
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
     const int tn = min(TC, nt - t0);
@@ -90,7 +94,7 @@ __global__ __launch_bounds__(256) void k_match_top2(MatchView v, uint2* __restri
     if (wid == 0 && q < nq) {
 #pragma unroll
         for (int w = 0; w < 3; w++) top2_merge(b, bi, s, mb[w][lane], mi[w][lane], ms[w][lane]);
-        part[((int64_t)p * nchunk_cap + blockIdx.y) * part_stride + q] = make_uint2((uint32_t)b | ((uint32_t)s << 16),
+        part[((int64_t)p * nchunk_cap + by) * part_stride + q] = make_uint2((uint32_t)b | ((uint32_t)s << 16),
                                                                                   (uint32_t)bi);
     }
     TR_END(4)
@@ -437,6 +441,11 @@ size_t match_part_entries(int npairs, int max_q, int max_t) {
     return (size_t)std::max(npairs, 1) * nch * std::max(max_q, 1);
 }
 
+static bool match_xcd_on() {
+    const char* e = std::getenv("ORBHIP_MATCH_XCD");
+    return !(e && e[0] == '0');
+}
+
 static void run_match(const MatchView& v, int npairs, int max_q, int max_t, int th_low, float ratio,
                       int check_orientation, int32_t* match, int32_t* best, int32_t* second, int32_t* nmatch,
                       uint2* part, hipStream_t st, StageTimer* timer = nullptr, int* sync = nullptr) {
@@ -458,9 +467,10 @@ static void run_match(const MatchView& v, int npairs, int max_q, int max_t, int 
     if (qblocks > 0 && max_t > 0) {
         if (small)
             ORBHIP_LAUNCH(k_match_top2<kTCSmall>, dim3(qblocks, nch, npairs), dim3(256), 0, st, v, part, nch,
-                               max_q);
-        else
-            ORBHIP_LAUNCH(k_match_top2<kTC>, dim3(qblocks, nch, npairs), dim3(256), 0, st, v, part, nch, max_q);
+                               max_q, 0);
+        else   // batches: whole pairs per XCD (ORBHIP_MATCH_XCD=0: the plain round-robin order)
+            ORBHIP_LAUNCH(k_match_top2<kTC>, dim3(qblocks, nch, npairs), dim3(256), 0, st, v, part, nch, max_q,
+                          match_xcd_on() && npairs >= 8 ? qblocks * nch : 0);
     }
     if (timer) { timer->end(5, st); timer->begin(6, st); }
     ORBHIP_LAUNCH(k_match_finish, dim3(npairs), dim3(1024), 0, st, v, part, nch, max_q, tc, th_low, ratio,

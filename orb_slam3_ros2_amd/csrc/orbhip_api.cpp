@@ -734,7 +734,7 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
         tm.begin(3, st);
         launch_octree(pl->d_plan.p, P, pl->d_cells.p, pl->d_otab.p, c->d_cand.p, c->d_cand_cnt.p, cp.off,
                       c->d_kscratch.p, c->d_nscratch.p, c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, oc, c->d_err.p, B,
-                      st);
+                      st, (tm.stage == 3 && tm.dstamp && tm.n < StageTimer::kCap) ? tm.dstamp + tm.n : nullptr);
         tm.end(3, st);
         tm.begin(4, st);
         launch_desc(pl->d_plan.p, P, fb, c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, pl->d_disc.p, d_kps, d_desc,
@@ -1068,10 +1068,10 @@ int orbhip_profile_collect(orbhip_ctx* c, double* total_ms, int32_t* count) {
         HIPOK(hipEventElapsedTime(&ms, t.ev[2 * i], t.ev[2 * i + 1]));
         s += ms;
     }
-    // the pyramid's k_pyr_cone also stamps its execution span from the device (first workgroup
-    // start -> last workgroup end, as rocprofv3's kernel trace counts it): used when every timed
-    // launch stamped (the k_resize cascade of batches does not)
-    if (t.stage == 1 && t.n > 0 && t.dstamp) {
+    // the pyramid's k_pyr_cone and k_octree also stamp their execution span from the device (first
+    // workgroup start -> last workgroup end, as rocprofv3's kernel trace counts it): used when every
+    // timed launch stamped (the k_resize cascade of batches does not)
+    if ((t.stage == 1 || t.stage == 3) && t.n > 0 && t.dstamp) {
         std::vector<unsigned long long> h(2 * (size_t)t.n);
         HIPOK(hipMemcpy(h.data(), t.dstamp, t.n * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         HIPOK(hipMemcpy(h.data() + t.n, t.dstamp + StageTimer::kCap, t.n * sizeof(unsigned long long),

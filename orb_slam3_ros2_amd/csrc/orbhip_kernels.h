@@ -99,7 +99,8 @@ bool octree_set_lds_limit(size_t bytes);
 void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const uint16_t* otab,
                    const uint32_t* cand,
                    const int* cand_cnt, const int* cand_off, uint32_t* kscratch, uint16_t* nscratch, LevelKp* lvl_kp,
-                   int* lvl_cnt, int* lvl_nlap, const OctreeCfg& cfg, int* err, int B, hipStream_t st);
+                   int* lvl_cnt, int* lvl_nlap, const OctreeCfg& cfg, int* err, int B, hipStream_t st,
+                   unsigned long long* stamp = nullptr);
 void launch_desc(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, const LevelKp* lvl_kp,
                  const int* lvl_cnt, const int* lvl_nlap, const int* disc, orbhip_kp* out_kps, uint8_t* out_desc,
                  int cap, int* n_out, int* mono_out, int B, hipStream_t st);
