@@ -423,59 +423,50 @@ __global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict
 // FAST strength m = max(A, B, 0): A = max over the 16 9-arcs of min(v - p), B the same for
 // (p - v). cornerScore<16> == m - 1 for every detected corner and a pixel is a corner at
 // threshold t iff m > t (derivation in DESIGN.md), so one map serves both thresholds.
+//
+// The window sits in LDS as a "pair window" of f16 pairs: dword (r, c) holds 1024 + the pixel of
+// window row r (low half) and of row r + R (high half), R = ceil(dr / 2) the pixel rows of the
+// cell's top half. One ds_read_b32 at a circle offset then gives the circle value of a top-half
+// pixel and of the pixel R rows below it, already packed for the v_pk_*_f16 ops; the 3-input
+// v_pk_minimum3 / v_pk_maximum3 halve the arc networks. 1024 + v (v = 0..255, sums with t up to
+// 1534) is an exact f16 integer, so every min / max / difference is exact.
 // ---------------------------------------------------------------------------
 constexpr int kWinMax = 80;
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));   // two pixels, one per 16-bit half
-constexpr int kWinP = kWinMax;   // LDS row pitch of the FAST window and strength maps
-static_assert(kWinP % 4 == 0, "dword window rows");
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));   // two pixels, one per 16-bit half
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+constexpr uint32_t kPwBias = 0x64006400u;                   // f16(1024) in both halves
 
-// m = max(A, B, 0) from the 16 differences d[k] = v - circle[k]. The 9-arcs are folded from
-// 4-arcs (pairs of neighbouring pair-minima, built one arc start at a time) instead of holding
-// all 16 pair minima and maxima live: 32 fewer VGPRs, so k_fast_cells keeps 8 waves per SIMD.
-__device__ __forceinline__ int fast_strength_d(const int* d) {
-    int A = -256, Bm = 256;
-#pragma unroll
-    for (int k = 0; k < 16; k++) {
-        // arc k .. k+8: min / max over 9 consecutive d
-        const int m4a = min(min(d[k], d[(k + 1) & 15]), min(d[(k + 2) & 15], d[(k + 3) & 15]));
-        const int m4b = min(min(d[(k + 4) & 15], d[(k + 5) & 15]), min(d[(k + 6) & 15], d[(k + 7) & 15]));
-        const int x4a = max(max(d[k], d[(k + 1) & 15]), max(d[(k + 2) & 15], d[(k + 3) & 15]));
-        const int x4b = max(max(d[(k + 4) & 15], d[(k + 5) & 15]), max(d[(k + 6) & 15], d[(k + 7) & 15]));
-        A = max(A, min(min(m4a, m4b), d[(k + 8) & 15]));
-        Bm = min(Bm, max(max(x4a, x4b), d[(k + 8) & 15]));
-    }
-    int m = max(A, -Bm);
-    return m < 0 ? 0 : m;
-}
+__device__ __forceinline__ h2 as_h2(uint32_t u) { return __builtin_bit_cast(h2, u); }
+__device__ __forceinline__ h2 hmin(h2 a, h2 b) { return __builtin_elementwise_minimum(a, b); }
+__device__ __forceinline__ h2 hmax(h2 a, h2 b) { return __builtin_elementwise_maximum(a, b); }
 
+// circle offsets (dwords) from the circle's top-left corner (the pixel at (-3, -3)), row pitch P:
+// the 16 points of OpenCV's pattern in its order, then the centre
+template <int P>
+struct Circle {
+    static constexpr int o[17] = {6 * P + 3, 6 * P + 4, 5 * P + 5, 4 * P + 6, 3 * P + 6, 2 * P + 6,
+                                  P + 5,     4,         3,         2,         P + 1,     2 * P,
+                                  3 * P,     4 * P,     5 * P + 1, 6 * P + 2, 3 * P + 3};
+};
 
-// Is the pixel a FAST corner candidate at threshold t? Necessary condition of a 9-arc: every
-// opposite pair (k, k+8) has at least one member beyond v +- t on the arc's side, i.e.
-// max_k min(d[k], d[k+8]) < -t (bright circle) or min_k max(d[k], d[k+8]) > t (dark). As
-// min/max chains (v_min3/v_max3) instead of 32 compares and their boolean reduction.
-__device__ __forceinline__ bool fast_pair_test(const int* d, int t) {
-    int bright = -256, dark = 256;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        bright = max(bright, min(d[k], d[k + 8]));
-        dark = min(dark, max(d[k], d[k + 8]));
-    }
-    return (bright < -t) | (dark > t);
-}
-
-// LDS of one FAST cell: static arrays in k_fast_cells, sized for windows of up to WR rows (80:
-// any cell; 56: the compact variant, rows of 64 bytes, ~9.6 KB, which keeps 16 work-groups of
-// 128 threads per CU)
+// LDS of one FAST cell, sized for windows of up to WR rows. Compact variant (WR 50): windows of
+// <= 50 rows and <= 45 columns (every level of 640x480 and 1280x720), ~9.7 KB, 16 work-groups
+// of 128 threads per CU. Full variant: any cell (windows up to 80 x 80).
 template <int WR>
 struct FastShape {
     static constexpr bool full = WR >= kWinMax;
-    static constexpr int wp = full ? kWinP : 64;                     // window / map row pitch
-    static constexpr int nw = ((WR - 6) * (wp - 6) + 63) / 64;       // mask words of the largest cell
-    static constexpr int cap = full ? kClistCap : 768;               // survivor list entries
+    static constexpr int wmax = full ? kWinMax : 45;        // window columns
+    static constexpr int pwp = ((wmax + 3 + 3) / 4) * 4;     // pair-window row pitch (dwords): 48 / 84
+    static constexpr int pwr = (WR - 6 + 1) / 2 + 6;         // pair-window rows: 28 / 43
+    static constexpr int mp = full ? 80 : 48;                // strength map row pitch (bytes) >= dc + 2
+    static constexpr int mr = WR - 4;                        // strength map rows dr + 2
+    static constexpr int nw = ((WR - 6) * (wmax - 6) + 63) / 64;   // mask words of the largest cell
+    static constexpr int cap = full ? kClistCap : 768;       // survivor list entries
+    static_assert(mp % 4 == 0 && mp >= wmax - 4, "strength map rows");
 };
 struct FastLds {
-    uint8_t* win;                   // window, rows of kWinP bytes
-    uint8_t* mv;                    // strength map, rows of kWinP bytes
+    uint32_t* pw;                   // pair window
+    uint8_t* mv;                    // strength map (zero border)
     unsigned long long* bmask;      // [2][nw] NMS survivors per threshold, raster order
     int nw;
     int* woff;                      // [nw] output offset of each 64-px word
@@ -486,12 +477,12 @@ struct FastLds {
     int cap;                        // clist entries in use: min(plan's clist_cap, the variant's)
 };
 
-template <int NT, int WP>
+template <int NT, int PWP, int MP>
 __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P, const CellGeom* __restrict__ cells,
                                                const FrameBufs& fb, uint32_t* __restrict__ cand,
                                                int* __restrict__ cand_cnt, int* __restrict__ err, int cell, int f,
                                                const FastLds& LS, const CandPack& cp) {
-    uint8_t* const win = LS.win;
+    uint32_t* const pw = LS.pw;
     uint8_t* const mv = LS.mv;
     unsigned long long* const bm0 = LS.bmask;
     unsigned long long* const bm1 = LS.bmask + LS.nw;
@@ -518,47 +509,72 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     const LevelGeom& G = P->lv[cg.level];
     ImgRef im = level_img(P, fb, f, cg.level);
     const uint8_t* base = im.p + (int64_t)cg.y0 * im.pitch + cg.x0;
-    // ---- window -> LDS: all loads of a thread issued back to back. When the rows are 4-byte
-    // aligned (pyramid levels always; the caller's frame when its pointer and stride are), the
-    // window moves as aligned dwords into LDS rows of WP bytes, shifted by sh = base & 3 ----
+    const int dc = wc - 6, dr = hc - 6, np = dc * dr;
+    const int R = (dr + 1) >> 1;   // top-half pixel rows; pair-window rows R + 6
+    const int RW = R + 6;
+    // ---- window -> pair window: all loads of a thread issued back to back. When the rows are
+    // 4-byte aligned (pyramid levels always; the caller's frame when its pointer and stride are),
+    // a task moves one aligned dword of window rows r and r + R (4 pixels each) into 4 pair-window
+    // dwords (one ds_write_b128), columns shifted by sh = base & 3 ----
     int sh = 0;
     {
         const bool dw = ((im.pitch & 3) == 0) && ((((uintptr_t)im.p) & 3) == 0);
         if (dw) {
             sh = (int)(((uintptr_t)base) & 3);
             const uint32_t* b4 = (const uint32_t*)(base - sh);
-            const int nwd = (wc + sh + 3) >> 2;   // <= WP / 4
-            const int tot = nwd * hc, p4 = im.pitch >> 2;
+            const int nwd = (wc + sh + 3) >> 2;   // <= PWP / 4
+            const int tot = nwd * RW, p4 = im.pitch >> 2;
             const float inv_n = 1.0f / (float)nwd;
-            uint32_t* w4 = (uint32_t*)win;
-            constexpr int NU = (NT >= 512) ? 1 : 512 / NT;   // a 44 x 43 window (473 dwords) in one round
+            auto put = [&](int r, int j, uint32_t a, uint32_t b) {
+                uint4 o;
+                o.x = __builtin_amdgcn_perm(b, a, 0x0C040C00u) | kPwBias;
+                o.y = __builtin_amdgcn_perm(b, a, 0x0C050C01u) | kPwBias;
+                o.z = __builtin_amdgcn_perm(b, a, 0x0C060C02u) | kPwBias;
+                o.w = __builtin_amdgcn_perm(b, a, 0x0C070C03u) | kPwBias;
+                *(uint4*)(pw + r * PWP + 4 * j) = o;
+            };
+            constexpr int NU = (NT >= 512) ? 1 : 512 / NT;
             if (tot <= NU * NT) {
-                uint32_t v[NU];
-                int li[NU];
+                uint32_t va[NU], vb[NU];
 #pragma unroll
                 for (int u = 0; u < NU; u++) {
                     const int i = min(tid + NT * u, tot - 1);
-                    const int yy = small_div(i, inv_n), xx = i - yy * nwd;
-                    v[u] = b4[(int64_t)yy * p4 + xx];
-                    li[u] = yy * (WP / 4) + xx;
+                    const int r = small_div(i, inv_n), j = i - r * nwd;
+                    va[u] = b4[(int64_t)r * p4 + j];
+                    vb[u] = r + R < hc ? b4[(int64_t)(r + R) * p4 + j] : 0u;
                 }
 #pragma unroll
-                for (int u = 0; u < NU; u++)
-                    if (tid + NT * u < tot) w4[li[u]] = v[u];
+                for (int u = 0; u < NU; u++) {
+                    const int i = tid + NT * u;
+                    if (i < tot) {
+                        const int r = small_div(i, inv_n);
+                        put(r, i - r * nwd, va[u], vb[u]);
+                    }
+                }
             } else {
                 for (int i = tid; i < tot; i += NT) {
-                    const int yy = small_div(i, inv_n), xx = i - yy * nwd;
-                    w4[yy * (WP / 4) + xx] = b4[(int64_t)yy * p4 + xx];
+                    const int r = small_div(i, inv_n), j = i - r * nwd;
+                    const uint32_t a = b4[(int64_t)r * p4 + j];
+                    const uint32_t b = r + R < hc ? b4[(int64_t)(r + R) * p4 + j] : 0u;
+                    put(r, j, a, b);
                 }
             }
         } else {
-            const int tot = wc * hc;
+            const int tot = wc * RW;
             const float inv_wc = 1.0f / (float)wc;
             for (int i = tid; i < tot; i += NT) {
-                const int yy = small_div(i, inv_wc), xx = i - yy * wc;
-                win[yy * WP + xx] = base[(int64_t)yy * im.pitch + xx];
+                const int r = small_div(i, inv_wc), c = i - r * wc;
+                const uint32_t a = base[(int64_t)r * im.pitch + c];
+                const uint32_t b = r + R < hc ? base[(int64_t)(r + R) * im.pitch + c] : 0u;
+                pw[r * PWP + c] = kPwBias | a | (b << 16);
             }
         }
+    }
+    // the strength map starts all zero (border, and every pixel the pair test rejects)
+    {
+        uint32_t* m4 = (uint32_t*)mv;
+        const int n4 = (dr + 2) * (MP / 4);
+        for (int i = tid; i < n4; i += NT) m4[i] = 0u;
     }
     if (tid == 0) ncand = 0;
     for (int i = tid; i < 2 * LS.nw; i += NT) LS.bmask[i] = 0ull;
@@ -566,139 +582,90 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     TR_PHASE(1, 0)
     const int t_ini = P->ini_th, t_min = P->min_th;
     const int t_lo = min(t_ini, t_min);
-    const int dc = wc - 6, dr = hc - 6, np = dc * dr;
     const float inv_dc = 1.0f / (float)dc;
-    // ---- strength map: m if m > t_lo (a corner at some threshold in use), else 0; stored with
-    // a zero border (row pitch W2 = dc + 2) so the NMS reads its 3x3 without bounds checks ----
-    // both LDS maps use the fixed pitch WP: every neighbour offset is an immediate
-    constexpr int W2 = WP;
-    const int Wz = dc + 2;   // zero border: rows 0 and dr + 1, columns 0 and dc + 1
-    for (int i = tid; i < 2 * Wz + 2 * dr; i += NT) {
-        const int idx = i < Wz ? i : (i < 2 * Wz ? (dr + 1) * W2 + (i - Wz) : (1 + (i - 2 * Wz) / 2) * W2 + ((i & 1) ? Wz - 1 : 0));
-        mv[idx] = 0;
-    }
-    // every pixel runs the cheap opposite-pair test; the ~5-10% that pass are compacted into
-    // clist, and the strength (the expensive part) runs on the dense list, so no wave spends its
-    // issue slots on masked-off lanes
-    auto diffs = [&](int p, int* d) {
-        const int py = small_div(p, inv_dc), px = p - py * dc;
-        const uint8_t* c = &win[(py + 3) * WP + px + 3 + sh];
-        constexpr int P = WP;
-        constexpr int o[16] = {3 * P,      3 * P + 1,  2 * P + 2,  P + 3,      3,      -P + 3, -2 * P + 2, -3 * P + 1,
-                               -3 * P,     -3 * P - 1, -2 * P - 2, -P - 3,     -3,     P - 3,  2 * P - 2,  3 * P - 1};
-        const int vv = c[0];
-#pragma unroll
-        for (int k = 0; k < 16; k++) d[k] = vv - (int)c[o[k]];
-        return (py + 1) * W2 + px + 1;
-    };
+    // a threshold >= 255 passes no pixel, as 255 does (|v - c| <= 255); keeps every sum exact
+    const _Float16 th = (_Float16)max(min(t_lo, 255), -255);
+    const h2 tv = {th, th};
+    constexpr int MPc = MP;
+    using C = Circle<PWP>;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int clist_cap = LS.cap;
-    // the pair test runs on two pixels per lane (q and q + half) as 16-bit halves: the circle
-    // bytes land in the halves straight from LDS (d16 / d16_hi loads), and the min / max chains
-    // and threshold compares are packed ops. In circle values c (d = v - c): bright iff
-    // min_k max(c_k, c_k+8) > v + t, dark iff v > max_k min(c_k, c_k+8) + t.
-    const int half = (np + 1) >> 1;
-    const u16x2 tv = {(unsigned short)t_lo, (unsigned short)t_lo};
-    for (int q0 = 0; q0 < half; q0 += NT) {
+    // every pixel pair (q: top half, q + R dc: the pixel R rows below) runs the cheap
+    // opposite-pair test; the ~5-10% that pass are compacted into clist, and the strength (the
+    // expensive part) runs on the dense list, so no wave spends its issue slots on masked-off
+    // lanes. In circle values c: bright iff min_k max(c_k, c_k+8) > v + t, dark iff
+    // v > max_k min(c_k, c_k+8) + t.
+    const int nq = R * dc, qb = R * dc;
+    for (int q0 = 0; q0 < nq; q0 += NT) {
         const int q = q0 + tid;
         bool pass0 = false, pass1 = false;
-        if (q < half) {
-            const bool two = q + half < np;
-            const int pa = q, pb = two ? q + half : q;
-            const int ya = small_div(pa, inv_dc), xa = pa - ya * dc;
-            const int yb = small_div(pb, inv_dc), xb = pb - yb * dc;
-            const uint8_t* ca = &win[(ya + 3) * WP + xa + 3 + sh];
-            const uint8_t* cb = &win[(yb + 3) * WP + xb + 3 + sh];
-            constexpr int P = WP;
-            constexpr int o[16] = {3 * P,      3 * P + 1,  2 * P + 2,  P + 3,      3,      -P + 3, -2 * P + 2, -3 * P + 1,
-                                   -3 * P,     -3 * P - 1, -2 * P - 2, -P - 3,     -3,     P - 3,  2 * P - 2,  3 * P - 1};
-            u16x2 c[16];
+        if (q < nq) {
+            const int y = small_div(q, inv_dc), x = q - y * dc;
+            const uint32_t* c = pw + y * PWP + x + sh;
+            h2 cc[16];
 #pragma unroll
-            for (int k = 0; k < 16; k++) c[k] = u16x2{(unsigned short)ca[o[k]], (unsigned short)cb[o[k]]};
-            const u16x2 v = {(unsigned short)ca[0], (unsigned short)cb[0]};
-            u16x2 M1 = __builtin_elementwise_max(c[0], c[8]), M2 = __builtin_elementwise_min(c[0], c[8]);
+            for (int k = 0; k < 16; k++) cc[k] = as_h2(c[C::o[k]]);
+            const h2 v = as_h2(c[C::o[16]]);
+            h2 M1 = hmax(cc[0], cc[8]), M2 = hmin(cc[0], cc[8]);
 #pragma unroll
             for (int k = 1; k < 8; k++) {
-                M1 = __builtin_elementwise_min(M1, __builtin_elementwise_max(c[k], c[k + 8]));
-                M2 = __builtin_elementwise_max(M2, __builtin_elementwise_min(c[k], c[k + 8]));
+                M1 = hmin(M1, hmax(cc[k], cc[k + 8]));
+                M2 = hmax(M2, hmin(cc[k], cc[k + 8]));
             }
-            const u16x2 X = v + tv, Y = M2 + tv;
-            pass0 = (M1.x > X.x) | (v.x > Y.x);
-            pass1 = two & ((M1.y > X.y) | (v.y > Y.y));
-            mv[(ya + 1) * W2 + xa + 1] = 0;
-            mv[(yb + 1) * W2 + xb + 1] = 0;
+            const h2 s = hmax(M1 - (v + tv), v - (M2 + tv));   // > 0: passes (exact integers)
+            pass0 = s.x > (_Float16)0;
+            pass1 = (y + R < dr) & (s.y > (_Float16)0);
         }
         const uint64_t b0 = __ballot(pass0), b1 = __ballot(pass1);
-        int base = 0;
-        if (lane == 0 && (b0 | b1)) base = atomicAdd(&ncand, __popcll(b0) + __popcll(b1));
-        base = __shfl(base, 0, 64);
-        const int ci0 = base + __popcll(b0 & lt), ci1 = base + __popcll(b0) + __popcll(b1 & lt);
+        int base_i = 0;
+        if (lane == 0 && (b0 | b1)) base_i = atomicAdd(&ncand, __popcll(b0) + __popcll(b1));
+        base_i = __shfl(base_i, 0, 64);
+        const int ci0 = base_i + __popcll(b0 & lt), ci1 = base_i + __popcll(b0) + __popcll(b1 & lt);
         if (pass0 && ci0 < clist_cap) clist[ci0] = (uint16_t)q;
-        if (pass1 && ci1 < clist_cap) clist[ci1] = (uint16_t)(q + half);
+        if (pass1 && ci1 < clist_cap) clist[ci1] = (uint16_t)(q + qb);
     }
     __syncthreads();
-    // dense: the list overflowed, so the strength and NMS passes walk every pixel instead (the
-    // pair test repeated; pixels that failed it hold m = 0 and are skipped by the NMS)
+    // dense: the list overflowed, so the strength runs on every pixel instead (m <= t_lo for
+    // every pixel the pair test rejects, so the map is the same) and the NMS walks every pixel
     const bool dense = ncand > clist_cap;
     const int nc = dense ? np : ncand;
-    if (dense) {
-        for (int i = tid; i < nc; i += NT) {
-            int d[16];
-            const int mi = diffs(i, d);
-            if (!fast_pair_test(d, t_lo)) continue;
-            int m = fast_strength_d(d);
-            if (m <= t_lo) m = 0;
-            mv[mi] = (uint8_t)m;
-        }
-    } else {
-        // listed survivors two per lane (i and i + hn) as 16-bit halves, in circle values:
+    {
+        // two pixels per lane (i and i + hn) as the halves of one f16 pair, each read from its
+        // pair-window half and joined by one v_perm per circle point:
         // m = max(v - min over 9-arcs of the arc max, max over 9-arcs of the arc min - v, 0), the
-        // arc extrema built by doubling (2-, 4-, 8-arcs, then the 9th value)
+        // 9-arc extrema as 3-input ops over 3-arcs
         const int hn = (nc + 1) >> 1;
         for (int i = tid; i < hn; i += NT) {
             const bool two = i + hn < nc;
-            const int pa = clist[i], pb = two ? clist[i + hn] : pa;
+            const int pa = dense ? i : clist[i];
+            const int pb = two ? (dense ? i + hn : clist[i + hn]) : pa;
             const int ya = small_div(pa, inv_dc), xa = pa - ya * dc;
             const int yb = small_div(pb, inv_dc), xb = pb - yb * dc;
-            const uint8_t* ca = &win[(ya + 3) * WP + xa + 3 + sh];
-            const uint8_t* cb = &win[(yb + 3) * WP + xb + 3 + sh];
-            constexpr int P = WP;
-            constexpr int o[16] = {3 * P,      3 * P + 1,  2 * P + 2,  P + 3,      3,      -P + 3, -2 * P + 2, -3 * P + 1,
-                                   -3 * P,     -3 * P - 1, -2 * P - 2, -P - 3,     -3,     P - 3,  2 * P - 2,  3 * P - 1};
-            u16x2 c[16];
+            const bool ha = ya >= R, hb = yb >= R;
+            const uint32_t* ca = pw + (ha ? ya - R : ya) * PWP + xa + sh;
+            const uint32_t* cb = pw + (hb ? yb - R : yb) * PWP + xb + sh;
+            const uint32_t sel = (ha ? 0x0302u : 0x0100u) | ((hb ? 0x0706u : 0x0504u) << 16);
+            h2 c[16];
 #pragma unroll
-            for (int k = 0; k < 16; k++) c[k] = u16x2{(unsigned short)ca[o[k]], (unsigned short)cb[o[k]]};
-            const u16x2 v = {(unsigned short)ca[0], (unsigned short)cb[0]};
-            // one network at a time (mins, then maxes): 16 arc registers live instead of 32
-            auto arc9 = [&](auto op, auto fold, u16x2 init) {
-                u16x2 t[16];
+            for (int k = 0; k < 16; k++) c[k] = as_h2(__builtin_amdgcn_perm(cb[C::o[k]], ca[C::o[k]], sel));
+            const h2 v = as_h2(__builtin_amdgcn_perm(cb[C::o[16]], ca[C::o[16]], sel));
+            // one network at a time (mins, then maxes): 16 3-arc registers live
+            auto arc9 = [&](auto op, auto fold) {
+                h2 u[16];
 #pragma unroll
-                for (int k = 0; k < 16; k++) t[k] = op(c[k], c[(k + 1) & 15]);   // 2-arcs k, k+1
+                for (int k = 0; k < 16; k++) u[k] = op(op(c[k], c[(k + 1) & 15]), c[(k + 2) & 15]);   // 3-arcs
+                h2 r = op(op(u[0], u[3]), u[6]);
 #pragma unroll
-                for (int sp = 2; sp <= 4; sp *= 2) {   // 4-arcs, then 8-arcs
-                    u16x2 h[4];
-#pragma unroll
-                    for (int k = 0; k < 4; k++) h[k] = t[k];
-#pragma unroll
-                    for (int k = 0; k < 16; k++) {
-                        const int j = (k + sp) & 15;
-                        t[k] = op(t[k], j < 4 ? h[j] : t[j]);
-                    }
-                }
-                u16x2 r = init;
-#pragma unroll
-                for (int k = 0; k < 16; k++) r = fold(r, op(t[k], c[(k + 8) & 15]));   // 9-arcs k .. k+8
+                for (int k = 1; k < 16; k++) r = fold(r, op(op(u[k], u[(k + 3) & 15]), u[(k + 6) & 15]));   // 9-arcs
                 return r;
             };
-            auto vmin = [](u16x2 p, u16x2 q) { return __builtin_elementwise_min(p, q); };
-            auto vmax = [](u16x2 p, u16x2 q) { return __builtin_elementwise_max(p, q); };
-            const u16x2 Mm = arc9(vmin, vmax, u16x2{0, 0});       // max over arcs of the arc min
-            const u16x2 MM = arc9(vmax, vmin, u16x2{255, 255});   // min over arcs of the arc max
-            const u16x2 m2 = __builtin_elementwise_max(__builtin_elementwise_sub_sat(v, MM),
-                                                       __builtin_elementwise_sub_sat(Mm, v));
-            const int ma = m2.x > t_lo ? (int)m2.x : 0, mb = m2.y > t_lo ? (int)m2.y : 0;
-            mv[(ya + 1) * W2 + xa + 1] = (uint8_t)ma;
-            if (two) mv[(yb + 1) * W2 + xb + 1] = (uint8_t)mb;
+            const h2 Mm = arc9(hmin, hmax);   // max over arcs of the arc min
+            const h2 MM = arc9(hmax, hmin);   // min over arcs of the arc max
+            const h2 zero = {(_Float16)0, (_Float16)0};
+            const h2 m2 = hmax(hmax(v - MM, Mm - v), zero);
+            const int ma = (int)m2.x, mb = (int)m2.y;
+            mv[(ya + 1) * MPc + xa + 1] = (uint8_t)(ma > t_lo ? ma : 0);
+            if (two) mv[(yb + 1) * MPc + xb + 1] = (uint8_t)(mb > t_lo ? mb : 0);
         }
     }
     __syncthreads();
@@ -708,10 +675,10 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     for (int i = tid; i < nc; i += NT) {
         const int p = dense ? i : clist[i];
         const int py = small_div(p, inv_dc), px = p - py * dc;
-        const uint8_t* c = &mv[(py + 1) * W2 + px + 1];
+        const uint8_t* c = &mv[(py + 1) * MPc + px + 1];
         const int m = c[0];
         if (m == 0) continue;
-        const int nb[8] = {c[-W2 - 1], c[-W2], c[-W2 + 1], c[-1], c[1], c[W2 - 1], c[W2], c[W2 + 1]};
+        const int nb[8] = {c[-MPc - 1], c[-MPc], c[-MPc + 1], c[-1], c[1], c[MPc - 1], c[MPc], c[MPc + 1]};
         bool k_ini = m > t_ini, k_min = m > t_min;
 #pragma unroll
         for (int k = 0; k < 8; k++) {
@@ -771,7 +738,7 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
         if ((mk >> lane) & 1ull) {
             const int py = small_div(p, inv_dc), px = p - py * dc;
             const int x = cg.x0 + 3 + px - G.min_bx, y = cg.y0 + 3 + py - G.min_by;
-            out[woff[w] + __popcll(mk & lt)] = pack_cand(x, y, (int)mv[(py + 1) * W2 + px + 1] - 1);
+            out[woff[w] + __popcll(mk & lt)] = pack_cand(x, y, (int)mv[(py + 1) * MPc + px + 1] - 1);
         }
     }
     if (tid == 0) *cnt_out = wtot;
@@ -785,16 +752,16 @@ __global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict
                                                     uint32_t* __restrict__ cand, int* __restrict__ cand_cnt,
                                                     int* __restrict__ err, int xrun, CandPack cp) {
     using SH = FastShape<WR>;
-    __shared__ __attribute__((aligned(16))) uint8_t win[WR * SH::wp];
-    __shared__ uint8_t mv[WR * SH::wp];
+    __shared__ __attribute__((aligned(16))) uint32_t pw[SH::pwr * SH::pwp];
+    __shared__ __attribute__((aligned(16))) uint8_t mv[SH::mr * SH::mp];
     __shared__ unsigned long long bmask[2 * SH::nw];
     __shared__ int woff[SH::nw];
     __shared__ int wsel, wtot;
     __shared__ uint16_t clist[SH::cap];
     __shared__ int ncand;
-    const FastLds LS{win, mv, bmask, SH::nw, woff, &wsel, &wtot, clist, &ncand, min(P->clist_cap, SH::cap)};
+    const FastLds LS{pw, mv, bmask, SH::nw, woff, &wsel, &wtot, clist, &ncand, min(P->clist_cap, SH::cap)};
     const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
-    fast_cell_body<NT, SH::wp>(P, cells, fb, cand, cand_cnt, err, lg % X, lg / X, LS, cp);
+    fast_cell_body<NT, SH::pwp, SH::mp>(P, cells, fb, cand, cand_cnt, err, lg % X, lg / X, LS, cp);
 }
 
 // ---------------------------------------------------------------------------
@@ -2062,23 +2029,23 @@ void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* c
                                          : (ncell <= 512 ? 1024 : (ncell <= 1024 ? 512 : (ncell <= 32768 ? 256 : 128))));
     dim3 grd(hP.n_cells_total, B, 1);
     const int xr = xcd_run_for(B);
-    const bool compact = hP.fast_win_rows <= 56 && hP.fast_win_cols + 3 <= 64;   // window dwords (sh <= 3) fit a row
+    const bool compact = hP.fast_win_rows <= 50 && hP.fast_win_cols <= 45;   // FastShape<50>
 #define ORBHIP_FAST_LAUNCH(NTV, WRV) \
     ORBHIP_LAUNCH((k_fast_cells<NTV, WRV>), grd, dim3(NTV), 0, st, dP, cells, fb, cand, cand_cnt, err, xr, cp)
     if (nt == 1024 && compact)
-        ORBHIP_FAST_LAUNCH(1024, 56);
+        ORBHIP_FAST_LAUNCH(1024, 50);
     else if (nt == 1024)
         ORBHIP_FAST_LAUNCH(1024, kWinMax);
     else if (nt == 512 && compact)
-        ORBHIP_FAST_LAUNCH(512, 56);
+        ORBHIP_FAST_LAUNCH(512, 50);
     else if (nt == 512)
         ORBHIP_FAST_LAUNCH(512, kWinMax);
     else if (nt == 128 && compact)
-        ORBHIP_FAST_LAUNCH(128, 56);
+        ORBHIP_FAST_LAUNCH(128, 50);
     else if (nt == 128)
         ORBHIP_FAST_LAUNCH(128, kWinMax);
     else if (compact)
-        ORBHIP_FAST_LAUNCH(256, 56);
+        ORBHIP_FAST_LAUNCH(256, 50);
     else
         ORBHIP_FAST_LAUNCH(256, kWinMax);
 #undef ORBHIP_FAST_LAUNCH

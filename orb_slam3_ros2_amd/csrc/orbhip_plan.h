@@ -53,7 +53,7 @@ struct ExtractPlan {
     int max_cells_level;                // max cells of any level (octree LDS carve)
     int clist_cap;                      // FAST survivors listed per cell (<= kClistCap; more -> dense pass)
     int fast_nt;                        // k_fast_cells threads per cell: 0 = by batch size, else 128/256/512/1024
-    int fast_win_rows, fast_win_cols;   // largest FAST cell window (<= 56 rows, <= 61 columns: the compact LDS variant)
+    int fast_win_rows, fast_win_cols;   // largest FAST cell window (<= 50 rows, <= 45 columns: the compact LDS variant)
     LevelGeom lv[kMaxLevels];
 };
 
