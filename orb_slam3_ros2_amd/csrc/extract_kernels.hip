@@ -491,7 +491,6 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     int& wtot = *LS.wtot;
     uint16_t* const clist = LS.clist;
     int& ncand = *LS.ncand;
-    constexpr int NW = NT / 64;
     TR_BEGIN()
     const CellGeom cg = cells[cell];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -732,13 +731,17 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
         slot = G.slot_base + ncand;
     }
     uint32_t* out = cand + (int64_t)f * P->n_slots_total + slot;
-    for (int w = wid; w < nwd; w += NW) {
-        const uint64_t mk = (sel ? bm1 : bm0)[w];
-        const int p = 64 * w + lane;
-        if ((mk >> lane) & 1ull) {
+    // one lane per mask word walks its set bits (a cell keeps a few corners: ~1 per word), in
+    // raster order from the word's scanned offset
+    for (int w = tid; w < nwd; w += NT) {
+        uint64_t mk = (sel ? bm1 : bm0)[w];
+        int o = woff[w];
+        while (mk) {
+            const int p = 64 * w + __builtin_ctzll(mk);
+            mk &= mk - 1;
             const int py = small_div(p, inv_dc), px = p - py * dc;
             const int x = cg.x0 + 3 + px - G.min_bx, y = cg.y0 + 3 + py - G.min_by;
-            out[woff[w] + __popcll(mk & lt)] = pack_cand(x, y, (int)mv[(py + 1) * MPc + px + 1] - 1);
+            out[o++] = pack_cand(x, y, (int)mv[(py + 1) * MPc + px + 1] - 1);
         }
     }
     if (tid == 0) *cnt_out = wtot;
@@ -1680,7 +1683,7 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
             }
         }
     }
-    __syncthreads();
+    wave_lds_fence();   // each wave works on its own keypoint's LDS only
     TR_PHASE(3, 0)
     // ---- IC_Angle: m10 = sum u*I, m01 = sum v*I over the umax disc (unblurred level) ----
     float angle = 0.f;
@@ -1719,7 +1722,7 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
             }
         }
     }
-    __syncthreads();
+    wave_lds_fence();   // each wave works on its own keypoint's LDS only
     if (active) {
         // ---- column pass: bl[r][c] = (sum_j k_j hr[r + j][c] + 2^15) >> 16, 4 rows per task:
         // rows r0 .. r0+9 of column c as 5 dwords of row pairs, 4 v_dot2_u32_u16 per output
@@ -1745,7 +1748,7 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
             }
         }
     }
-    __syncthreads();
+    wave_lds_fence();   // each wave works on its own keypoint's LDS only
     TR_PHASE(3, 1)
     if (!active) {
         TR_END(3)
