@@ -493,13 +493,14 @@ def cpu_lba(prob, budget_s=8.0):
 
 def c5_gba(ws, rank, iters):
     """C5 GlobalBundleAdjustment (400 KF loop, 20k points, 80k obs, 20-KF co-visibility window).
-    One GPU: the nested-dissection solve of the reduced camera system (csrc/ba_nd.hip). With N > 1:
-    the keyframe loop cut into N segments, rank r holding segment r's landmarks
-    (sharding.shard_problem_nd): each rank factors its interior, the separator system and the pose
-    update are all-reduced over RCCL inside the device-driven LM (orbhip_ba_solve_sharded, SURVEY.md
-    §8e). ORBHIP_C5_SHARDED=0 runs replicas instead (every rank the whole problem); a segment plan
-    that does not fit (too many ranks for the loop) falls back to contiguous landmark shards with
-    the summed reduced camera system. Time = max over ranks of one solve."""
+    One GPU: the nested-dissection solve of the reduced camera system (csrc/ba_nd.hip). With N > 1
+    the default is replicas (every rank its own GBA: the modelled 8-rank segment-sharded trial is
+    slower than one GPU). ORBHIP_C5_SHARDED=1: the keyframe loop cut into N segments,
+    rank r holding segment r's landmarks (sharding.shard_problem_nd): each rank factors its
+    interior, the separator system and the pose update are all-reduced over RCCL inside the
+    device-driven LM (orbhip_ba_solve_sharded); a segment plan that does not fit
+    (too many ranks for the loop) falls back to contiguous landmark shards with the summed reduced
+    camera system. Time = max over ranks of one solve."""
     import torch
     from orb_slam3_ros2_amd import Optimizer
     from orb_slam3_ros2_amd.sharding import nd_segments, pose_blocks, shard_problem, shard_problem_nd
@@ -507,7 +508,7 @@ def c5_gba(ws, rank, iters):
     prob, _ = synthetic_ba_problem(n_kf=400, n_pts=20000, layout="loop", window=20, seed=11)
     prob.iterations, prob.huber_delta = iters, float(np.sqrt(5.99))   # BundleAdjustment(bRobust)
     opt = Optimizer()
-    sharded = ws > 1 and os.environ.get("ORBHIP_C5_SHARDED", "1") != "0"
+    sharded = ws > 1 and os.environ.get("ORBHIP_C5_SHARDED", "0") == "1"
     mode = f"replicas x{ws} (one GPU per solve, nested dissection)"
     if sharded:
         import torch.distributed as dist

@@ -93,72 +93,132 @@ __global__ __launch_bounds__(256) void k_nd_assemble(NdDev d) {
     }
 }
 
+// workgroup barrier ordering LDS only (__syncthreads() on gfx950 also drains vmcnt, i.e. would
+// wait for the next step's prefetched tile loads)
+__device__ __forceinline__ void lds_only_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
 // one workgroup per segment: x of its separator rows from x_Z, then L_II^T x_I = y_I - L_ZI^T x_Z
 // tile by tile (tile column R: every tile (R', R), R' > R, of the envelope), then the scatter to S's
 // order. A failed factorization anywhere (a segment or the separator system) zeroes x and flag.
+// The step's operands do not depend on x: each group's first two tiles of column R - 1, the
+// Linv_{R-1} column and y_{R-1} are loaded while step R runs, and the envelope sits in LDS, so a
+// step waits on LDS and barriers only (a column deeper than 16 tiles loads the rest in the step).
+// the segment buffers are reached through pointers loaded from memory (NdSegDev), which the
+// compiler cannot place in an address space: without these casts every load is a flat load,
+// counted in lgkmcnt too, so each LDS wait of a step would also wait for the prefetched tiles
+template <typename T>
+__device__ __forceinline__ const __attribute__((address_space(1))) T* gp(const T* p) {
+    return (const __attribute__((address_space(1))) T*)p;
+}
+
 __global__ __launch_bounds__(256) void k_nd_backsolve(NdDev d) {
     if (d.gate && *d.gate != kPhTrial) return;
-    extern __shared__ double xs[];   // NT x 32, then 8 x 32 partials, 32 s
+    extern __shared__ double xs[];   // NT x 32, then 8 x 32 partials, 32 s, then NT ints (envelope)
     const NdSegDev s = d.segs[blockIdx.x];
     double* part = xs + s.NT * kT;
     double* sv = part + 8 * kT;
+    int* rfs = (int*)(sv + kT);
     __shared__ int okw;
     const int tid = threadIdx.x;
     double* xo = d.x_loc ? d.x_loc : d.x;
-    if (tid == 0) {
-        int ok = d.flagZ[0] != 0;
-        for (int r = 0; r < d.K; r++) ok = ok && d.segs[r].flag[0] != 0;
-        okw = ok;
-        if (blockIdx.x == 0) {
-            if (d.x_loc) d.x_loc[d.n] = ok ? 0.0 : 1.0;
-            else d.flag[0] = ok;
-        }
-    }
+    if (tid == 0) okw = d.flagZ[0] != 0;
+    for (int i = tid; i < s.NT; i += blockDim.x) rfs[i] = gp(s.rf)[i];
     for (int i = tid; i < s.NT * kT; i += blockDim.x) {
         double v = 0.0;
-        if (i >= s.nip && i < s.n) v = d.xZ[s.zmap[i - s.nip]];
+        if (i >= s.nip && i < s.n) v = gp(d.xZ)[gp(s.zmap)[i - s.nip]];
         xs[i] = v;
     }
     __syncthreads();
+    if (tid < d.K && gp(d.segs[tid].flag)[0] == 0) okw = 0;   // every segment factored (all in parallel)
+    __syncthreads();
     const bool ok = okw != 0;
+    if (blockIdx.x == 0 && tid == 0) {
+        if (d.x_loc) d.x_loc[d.n] = ok ? 0.0 : 1.0;
+        else d.flag[0] = ok;
+    }
     const int c = tid & 31, g = tid >> 5;
-    for (int R = s.nti - 1; R >= 0 && ok; R--) {
-        double acc = 0.0;
-        for (int Rp = R + 1 + g; Rp < s.NT; Rp += 8) {
-            if (R < s.rf[Rp]) continue;
-            const double* t = s.buf + dag_off_L(s.NT, Rp, R);
-            const double* xr = xs + Rp * kT;
-            double v[kT];   // the tile column's 32 loads in flight together
+    // group g's tiles of column R: rows R + 1 + g, + 8, ... inside the envelope
+    auto next_row = [&](int R, int Rp) {
+        for (; Rp < s.NT; Rp += 8)
+            if (R >= rfs[Rp]) return Rp;
+        return -1;
+    };
+    double vn0[kT], vn1[kT], lvn[kT], yn = 0.0;
+    int rpn0 = -1, rpn1 = -1;
+    auto prefetch = [&](int R) {
+        rpn0 = next_row(R, R + 1 + g);
+        rpn1 = rpn0 >= 0 ? next_row(R, rpn0 + 8) : -1;
+        if (rpn0 >= 0) {
+            const auto t = gp(s.buf) + dag_off_L(s.NT, rpn0, R);
 #pragma unroll
-            for (int r = 0; r < kT; r++) v[r] = t[tq(r, c)];
-#pragma unroll
-            for (int r = 0; r < kT; r++) acc = fma(v[r], xr[r], acc);
+            for (int r = 0; r < kT; r++) vn0[r] = t[tq(r, c)];
         }
-        part[g * kT + c] = acc;
-        __syncthreads();
+        if (rpn1 >= 0) {
+            const auto t = gp(s.buf) + dag_off_L(s.NT, rpn1, R);
+#pragma unroll
+            for (int r = 0; r < kT; r++) vn1[r] = t[tq(r, c)];
+        }
         if (tid < kT) {
-            double v = s.buf[dag_off_y(s.NT, R) + tid];
-            for (int q = 0; q < 8; q++) v -= part[q * kT + tid];
-            sv[tid] = v;
+            const auto li = gp(s.buf) + dag_off_Linv(s.NT, R);
+#pragma unroll
+            for (int q = 0; q < kT; q++) lvn[q] = li[tq(q, tid)];
+            yn = gp(s.buf)[dag_off_y(s.NT, R) + tid];
         }
-        __syncthreads();
+    };
+    if (ok && s.nti > 0) prefetch(s.nti - 1);
+    for (int R = s.nti - 1; R >= 0 && ok; R--) {
+        double v0[kT], v1[kT], lv[kT];
+#pragma unroll
+        for (int r = 0; r < kT; r++) { v0[r] = vn0[r]; v1[r] = vn1[r]; lv[r] = lvn[r]; }
+        const int rp0 = rpn0, rp1 = rpn1;
+        const double yR = yn;
+        if (R > 0) prefetch(R - 1);
+        double a4[4] = {0.0, 0.0, 0.0, 0.0};
+        if (rp0 >= 0) {
+            const double* xr = xs + rp0 * kT;
+#pragma unroll
+            for (int r = 0; r < kT; r++) a4[r & 3] = fma(v0[r], xr[r], a4[r & 3]);
+        }
+        if (rp1 >= 0) {
+            const double* xr = xs + rp1 * kT;
+#pragma unroll
+            for (int r = 0; r < kT; r++) a4[r & 3] = fma(v1[r], xr[r], a4[r & 3]);
+            // further tiles of this group (a column deeper than 16 tiles): loaded here
+            for (int Rp = next_row(R, rp1 + 8); Rp >= 0; Rp = next_row(R, Rp + 8)) {
+                const auto t = gp(s.buf) + dag_off_L(s.NT, Rp, R);
+                const double* xq = xs + Rp * kT;
+                double w[kT];
+#pragma unroll
+                for (int r = 0; r < kT; r++) w[r] = t[tq(r, c)];
+#pragma unroll
+                for (int r = 0; r < kT; r++) a4[r & 3] = fma(w[r], xq[r], a4[r & 3]);
+            }
+        }
+        part[g * kT + c] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+        lds_only_barrier();
+        if (tid < kT) {
+            double y = yR;
+            for (int q = 0; q < 8; q++) y -= part[q * kT + tid];
+            sv[tid] = y;
+        }
+        lds_only_barrier();
         if (tid < kT) {   // x_R = Linv_R^T s
-            const double* li = s.buf + dag_off_Linv(s.NT, R);
-            double lv[kT];
+            double b4[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int q = 0; q < kT; q++) lv[q] = li[tq(q, tid)];
-            double v = 0.0;
-#pragma unroll
-            for (int q = 0; q < kT; q++) v = fma(lv[q], sv[q], v);
-            xs[R * kT + tid] = v;
+            for (int q = 0; q < kT; q++) b4[q & 3] = fma(lv[q], sv[q], b4[q & 3]);
+            xs[R * kT + tid] = (b4[0] + b4[1]) + (b4[2] + b4[3]);
         }
-        __syncthreads();
+        lds_only_barrier();
     }
     for (int i = tid; i < s.nip; i += blockDim.x) {
-        const int p = s.perm[i];
+        const int p = gp(s.perm)[i];
         if (p >= 0) xo[p] = ok ? xs[i] : 0.0;
     }
-    for (int i = s.own0 + tid; i < s.own1; i += blockDim.x) xo[s.perm[i]] = ok ? xs[i] : 0.0;
+    for (int i = s.own0 + tid; i < s.own1; i += blockDim.x) xo[gp(s.perm)[i]] = ok ? xs[i] : 0.0;
 }
 
 // a shard's last step: the summed x, and the solve's flag (every shard's factorization and the
@@ -513,7 +573,7 @@ int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int 
     int maxNT = 0;
     for (int r = 0; r < K; r++)
         if (loc[r] >= 0) maxNT = std::max(maxNT, sg[r].NT);
-    W->bs_lds = sizeof(double) * ((size_t)maxNT * kT + 9 * kT);
+    W->bs_lds = sizeof(double) * ((size_t)maxNT * kT + 9 * kT) + sizeof(int) * (size_t)maxNT;
     // shard of a distributed solve: the packed separator envelope and the x buffers
     d.x_loc = nullptr;
     d.xg = nullptr;

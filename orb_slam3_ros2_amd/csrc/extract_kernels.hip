@@ -40,6 +40,18 @@ __device__ __forceinline__ ImgRef level_img(const ExtractPlan* __restrict__ P, c
     return ImgRef{fb.pyr + (int64_t)f * P->pyr_bytes + P->lv[l].pyr_off, P->lv[l].pitch};
 }
 
+// a wave's own LDS writes visible to its later LDS reads (no workgroup barrier)
+// LDS-only form: waits for the wave's LDS operations alone (a seq_cst fence also waits vmcnt(0),
+// i.e. for every outstanding global store)
+__device__ __forceinline__ void wave_lds_only() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 // ---------------------------------------------------------------------------
 // k_resize: OCV resizeGeneric_ 8UC1 INTER_LINEAR; block (64,4), 4 output px x kRzRows output rows
 // per thread. Latency-bound at one round trip per dependent load, so each thread keeps
@@ -74,12 +86,24 @@ __device__ __forceinline__ int rz_px(int p00, int p01, int p10, int p11, int aa,
     return v < 0 ? 0 : (v > 255 ? 255 : v);
 }
 
+typedef __attribute__((address_space(1))) int ex_gint;
+// the one-launch batch pyramid (k_pyr_flow) reads the levels it writes itself: 4-byte sc1 buffer
+// loads (L2-served, never a stale L1 line; MI355X_MICROARCH.md visibility table, row 1)
+__device__ __forceinline__ uint32_t pyr_ld4_sc1(__amdgpu_buffer_rsrc_t rs, const uint8_t* p, const uint8_t* pyr) {
+    return __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(p - pyr), 0, 16);
+}
+
 // one lane's 4 columns x kRzRows rows of level l of frame f: output rows [dyb, min(dyb + kRzRows,
-// row_end)) (dyb wave-uniform), columns dx0..dx0+3 (dx0 < the level's width)
-__device__ __forceinline__ void resize_tile(const ExtractPlan* __restrict__ P, const FrameBufs& fb, int f, int l,
-                                            int dyb, int dx0, int row_end, const int* __restrict__ xofs,
-                                            const int* __restrict__ xalpha, const int* __restrict__ yofs,
-                                            const int* __restrict__ ybeta) {
+// row_end)) (dyb wave-uniform), columns dx0..dx0+3 (dx0 < the level's width).
+// FLOW (k_pyr_flow): the outputs go to the wave's LDS stage (row j at dwords [64 j, 64 j + 64), this
+// lane's 4 bytes at dword lane) instead of the pyramid, and a source level >= 1 is read with sc1 loads.
+template <bool FLOW>
+__device__ __forceinline__ void resize_tile_g(const ExtractPlan* __restrict__ P, const FrameBufs& fb, int f, int l,
+                                              int dyb, int dx0, int row_end, const int* __restrict__ xofs,
+                                              const int* __restrict__ xalpha, const int* __restrict__ yofs,
+                                              const int* __restrict__ ybeta, __amdgpu_buffer_rsrc_t prs,
+                                              uint32_t* stage) {
+    const bool sc1 = FLOW && l >= 2;   // wave-uniform
     // geometry copied to registers (the byte stores below may alias the plan for the compiler)
     const int Dw = P->lv[l].w, Dpitch = P->lv[l].pitch;
     const int xmax = P->lv[l].xmax, vend = P->lv[l].vend;
@@ -112,8 +136,15 @@ __device__ __forceinline__ void resize_tile(const ExtractPlan* __restrict__ P, c
         uint32_t W[kRzSrc][3];
 #pragma unroll
         for (int i = 0; i < kRzSrc; i++) {
-            const uint32_t* p = (const uint32_t*)(src.p + (int64_t)min(rbase + i, Sh - 1) * src.pitch + base);
-            W[i][0] = p[0]; W[i][1] = p[1]; W[i][2] = p[2];
+            const uint8_t* pb = src.p + (int64_t)min(rbase + i, Sh - 1) * src.pitch + base;
+            if (sc1) {   // one 16-byte sc1 load (4-byte aligned) for the 12-byte span
+                typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+                const u32x4v q = __builtin_amdgcn_raw_buffer_load_b128(prs, (int)(pb - fb.pyr), 0, 16);
+                W[i][0] = q.x; W[i][1] = q.y; W[i][2] = q.z;
+            } else {
+                const uint32_t* p = (const uint32_t*)pb;
+                W[i][0] = p[0]; W[i][1] = p[1]; W[i][2] = p[2];
+            }
         }
         // horizontal pass once per source row: bytes o, o + 1 (o = sx - base <= 10) of the 12-byte
         // span picked by one v_perm from the dword pair (w1:w0) (o <= 6) or (w2:w1) into 16-bit
@@ -154,7 +185,11 @@ __device__ __forceinline__ void resize_tile(const ExtractPlan* __restrict__ P, c
         const bool noclamp = P->lv[l].rz_noclamp != 0;
 #pragma unroll
         for (int j = 0; j < kRzRows; j++) {
-            const int i0 = clampr(sy[j]) - rbase, i1 = clampr(sy[j] + 1) - rbase;   // wave-uniform
+            // wave-uniform; readfirstlane'd so the H[k][i] selects stay SGPR-indexed (s_set_gpr_idx)
+            // in every caller: left in VGPRs (k_resize_bands, k_pyr_flow) they were lowered to
+            // readlane / writelane loops, ~25k cycles per 4-row tile
+            const int i0 = __builtin_amdgcn_readfirstlane(clampr(sy[j]) - rbase);
+            const int i1 = __builtin_amdgcn_readfirstlane(clampr(sy[j] + 1) - rbase);
             const int b0 = (int)(short)(bbv[j] & 0xFFFF), b1 = (int)(short)(bbv[j] >> 16);
             uint32_t packed = 0;
             if (noclamp) {
@@ -175,9 +210,15 @@ __device__ __forceinline__ void resize_tile(const ExtractPlan* __restrict__ P, c
                     packed |= (uint32_t)v << (8 * k);
                 }
             }
-            *(uint32_t*)(dst0 + (int64_t)(dyb + j) * Dpitch + dx0) = packed;
+            if (FLOW) stage[j * 64 + (threadIdx.x & 63)] = packed;
+            else *(uint32_t*)(dst0 + (int64_t)(dyb + j) * Dpitch + dx0) = packed;
         }
     } else {
+        auto ld1 = [&](const uint8_t* q) -> int {
+            if (!sc1) return *q;
+            const uintptr_t a = (uintptr_t)q;
+            return (int)((pyr_ld4_sc1(prs, (const uint8_t*)(a & ~(uintptr_t)3), fb.pyr) >> (8 * (a & 3))) & 0xFFu);
+        };
         for (int j = 0; j < nrow; j++) {
             const int dy = dyb + j;
             uint8_t* dst = dst0 + (int64_t)dy * Dpitch;
@@ -190,12 +231,22 @@ __device__ __forceinline__ void resize_tile(const ExtractPlan* __restrict__ P, c
                 if (dx >= Dw) break;
                 const int sx = sxa[k];
                 const bool inx = dx < xmax;
-                const int p00 = S0[sx], p10 = S1[sx];
-                const int p01 = inx ? S0[sx + 1] : 0, p11 = inx ? S1[sx + 1] : 0;
-                dst[dx] = (uint8_t)rz_px(p00, p01, p10, p11, axa[k], b0, b1, inx, dx < vend);
+                const int p00 = ld1(S0 + sx), p10 = ld1(S1 + sx);
+                const int p01 = inx ? ld1(S0 + sx + 1) : 0, p11 = inx ? ld1(S1 + sx + 1) : 0;
+                const uint8_t v = (uint8_t)rz_px(p00, p01, p10, p11, axa[k], b0, b1, inx, dx < vend);
+                if (FLOW) ((uint8_t*)stage)[j * 256 + (threadIdx.x & 63) * 4 + k] = v;
+                else dst[dx] = v;
             }
         }
     }
+}
+
+__device__ __forceinline__ void resize_tile(const ExtractPlan* __restrict__ P, const FrameBufs& fb, int f, int l,
+                                            int dyb, int dx0, int row_end, const int* __restrict__ xofs,
+                                            const int* __restrict__ xalpha, const int* __restrict__ yofs,
+                                            const int* __restrict__ ybeta) {
+    resize_tile_g<false>(P, fb, f, l, dyb, dx0, row_end, xofs, xalpha, yofs, ybeta,
+                         __builtin_amdgcn_make_buffer_rsrc(fb.pyr, 0, 0, 0x00020000), nullptr);
 }
 
 __global__ __launch_bounds__(256) void k_resize(const ExtractPlan* __restrict__ P, FrameBufs fb, int l,
@@ -241,6 +292,111 @@ __global__ __launch_bounds__(256) void k_resize_bands(const ExtractPlan* __restr
         TR_PHASE(6, l)
     }
     TR_END(6)
+}
+
+// k_pyr_flow: the whole batch cascade (levels 1..L-1 of every frame) in ONE launch, as a dataflow
+// over row bands. A task = (level l, frame f, band b): output rows [16 b, 16 b + 16) of level l,
+// full width; wave w computes rows 16 b + 4 w .. + 3 with k_resize's per-pixel code
+// (resize_tile), strip by strip (256 columns), staged in LDS and written as 16-byte sc1 stores.
+// The frames are dealt to kFlowQ queues (frame f to queue f mod kFlowQ, work-group g serves queue
+// g mod kFlowQ); a queue's tasks are numbered level-major, frame-major, and taken kFlowChunk
+// tickets at a time from the queue's counter. A task of level l >= 2 first waits (wave 0, bounded
+// sc1 polls) for the flags of the level l-1 bands of its frame that its source rows lie in: tasks
+// of the same queue with lower tickets, and a ticket is only taken by a running work-group that
+// runs its tickets in order, so the launch cannot deadlock whatever the grid size, residency or
+// dispatch order. Visibility (MI355X_MICROARCH.md, visibility table row 1): the payload is stored
+// sc1, each wave drains vmcnt, the work-group barriers, one lane stores the band's flag (agent
+// scope); the consumer polls the flag with sc1 loads and reads the bytes with sc1 loads only
+// (16-byte). Flags hold the launch's generation (advanced with the ticket reset by the last
+// work-group out), so nothing is cleared between launches. A spin that runs out counts in
+// ctl[kFlowQ + 2] (never expected: the waits cannot deadlock) and the band proceeds.
+// ---------------------------------------------------------------------------
+constexpr int kFlowRows = 16;         // output rows per task (4 waves x kRzRows)
+constexpr int kFlowSpin = 1 << 22;    // polls before a wait gives up (~0.5 s)
+
+__global__ __launch_bounds__(256) void k_pyr_flow(const ExtractPlan* __restrict__ P, FrameBufs fb,
+                                                   const int* __restrict__ xofs, const int* __restrict__ xalpha,
+                                                   const int* __restrict__ yofs, const int* __restrict__ ybeta,
+                                                   PyrFlow a) {
+    __shared__ __attribute__((aligned(16))) uint32_t stage[4][kRzRows * 64];
+    __shared__ int s_t;
+    TR_BEGIN()
+    int tr_k = 0;   // tasks run by this work-group (trace phases of work-group 0: wait, then compute)
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int L = P->n_levels;
+    int* const ctl = a.ctl;
+    const int gen = __hip_atomic_load((ex_gint*)(ctl + kFlowQ + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(fb.pyr, 0, a.pyr_limit, 0x00020000);
+    const int q = blockIdx.x % kFlowQ;
+    const int nfq = q < a.B ? (a.B - q + kFlowQ - 1) / kFlowQ : 0;   // frames q, q + Q, ...
+    const int ntask = nfq * a.boff[L];
+    for (;;) {
+        if (tid == 0) s_t = atomicAdd(ctl + q, kFlowChunk);
+        __syncthreads();
+        const int t0 = s_t;
+        if (t0 >= ntask) break;
+        const int t1 = min(t0 + kFlowChunk, ntask);
+        for (int t = t0; t < t1; t++) {
+            int l = 1;
+            while (l + 1 < L && nfq * a.boff[l + 1] <= t) l++;
+            const int nb = a.boff[l + 1] - a.boff[l];
+            const int loc = t - nfq * a.boff[l], fi = loc / nb, b = loc - fi * nb;
+            const int f = q + kFlowQ * fi;
+            int* const fl = a.flags + (int64_t)f * a.nbt;
+            if (l >= 2 && wave == 0) {
+                const int2 d = a.dep[a.boff[l] + b];   // level l-1 bands holding this band's source rows
+                const int* w = fl + a.boff[l - 1];
+                for (int it = 0;; it++) {
+                    const bool mine = d.x + lane > d.y ||
+                                      __hip_atomic_load((ex_gint*)(w + d.x + lane), __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT) == gen + 1;
+                    if (__ballot(!mine) == 0ull) break;
+                    if (it >= kFlowSpin) {
+                        if (lane == 0) atomicAdd(ctl + kFlowQ + 2, 1);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            __syncthreads();
+            if (tr_k < 32) { TR_PHASE(7, 2 * tr_k) }
+            const int Dh = P->lv[l].h, Dw = P->lv[l].w, pitch = P->lv[l].pitch;
+            const int row_end = min(b * kFlowRows + kFlowRows, Dh);
+            const int dyb = b * kFlowRows + wave * kRzRows;   // wave-uniform
+            if (dyb < row_end) {
+                const int obase = (int)((int64_t)f * P->pyr_bytes + P->lv[l].pyr_off);
+                for (int s0 = 0; s0 < Dw; s0 += 256) {
+                    const int dx0 = s0 + lane * 4;
+                    if (dx0 < Dw)
+                        resize_tile_g<true>(P, fb, f, l, dyb, dx0, row_end, xofs, xalpha, yofs, ybeta, prs,
+                                            stage[wave]);
+                    wave_lds_only();   // the stage's LDS writes, not the strip's stores (no vmcnt wait)
+                    const int r = lane >> 4, c = s0 + (lane & 15) * 16;
+                    if (dyb + r < row_end && c < Dw) {
+                        const uint4 v = *(const uint4*)&stage[wave][r * 64 + (lane & 15) * 4];
+                        typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+                        const u32x4v u = {v.x, v.y, v.z, v.w};
+                        __builtin_amdgcn_raw_buffer_store_b128(u, prs, obase + (dyb + r) * pitch + c, 0, 16);
+                    }
+                    wave_lds_only();
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (tid == 0)
+                __hip_atomic_store((ex_gint*)(fl + a.boff[l] + b), gen + 1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            if (tr_k < 32) { TR_PHASE(7, 2 * tr_k + 1) }
+            tr_k++;
+        }
+    }
+    TR_END(7)
+    // the last work-group out resets the tickets and advances the generation for the next launch
+    if (tid == 0 && atomicAdd(ctl + kFlowQ, 1) == (int)gridDim.x - 1) {
+        for (int i = 0; i <= kFlowQ; i++)
+            __hip_atomic_store((ex_gint*)(ctl + i), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((ex_gint*)(ctl + kFlowQ + 1), gen + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // quotient of i / d for 0 <= i < 2^16, d >= 1: the float reciprocal's error stays below the
@@ -472,8 +628,9 @@ struct FastLds {
     int* woff;                      // [nw] output offset of each 64-px word
     int* wsel;
     int* wtot;
-    uint16_t* clist;                // pair-test survivors (strength to compute)
+    uint16_t* clist;                // pair-test survivors (strength to compute), one region per wave
     int* ncand;
+    int* ncw;                       // [NT / 64] survivors listed by each wave
     int cap;                        // clist entries in use: min(plan's clist_cap, the variant's)
 };
 
@@ -575,7 +732,6 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
         const int n4 = (dr + 2) * (MP / 4);
         for (int i = tid; i < n4; i += NT) m4[i] = 0u;
     }
-    if (tid == 0) ncand = 0;
     for (int i = tid; i < 2 * LS.nw; i += NT) LS.bmask[i] = 0ull;
     __syncthreads();
     TR_PHASE(1, 0)
@@ -594,12 +750,20 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     // expensive part) runs on the dense list, so no wave spends its issue slots on masked-off
     // lanes. In circle values c: bright iff min_k max(c_k, c_k+8) > v + t, dark iff
     // v > max_k min(c_k, c_k+8) + t.
+    // Each wave lists its survivors in its own region of clist (capw entries) with a running
+    // count, so no list position waits on an LDS atomic. q advances by NT per round: (y, x) are
+    // stepped, not divided.
+    constexpr int NW = NT / 64;
+    const int capw = clist_cap / NW;
+    uint16_t* const wlist = clist + wid * capw;
+    int wcnt = 0;   // wave-uniform
     const int nq = R * dc, qb = R * dc;
+    const int ystep = NT / dc, xstep = NT - ystep * dc;
+    int y = small_div(tid, inv_dc), x = tid - y * dc;
     for (int q0 = 0; q0 < nq; q0 += NT) {
         const int q = q0 + tid;
         bool pass0 = false, pass1 = false;
         if (q < nq) {
-            const int y = small_div(q, inv_dc), x = q - y * dc;
             const uint32_t* c = pw + y * PWP + x + sh;
             h2 cc[16];
 #pragma unroll
@@ -616,18 +780,38 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
             pass1 = (y + R < dr) & (s.y > (_Float16)0);
         }
         const uint64_t b0 = __ballot(pass0), b1 = __ballot(pass1);
-        int base_i = 0;
-        if (lane == 0 && (b0 | b1)) base_i = atomicAdd(&ncand, __popcll(b0) + __popcll(b1));
-        base_i = __shfl(base_i, 0, 64);
-        const int ci0 = base_i + __popcll(b0 & lt), ci1 = base_i + __popcll(b0) + __popcll(b1 & lt);
-        if (pass0 && ci0 < clist_cap) clist[ci0] = (uint16_t)q;
-        if (pass1 && ci1 < clist_cap) clist[ci1] = (uint16_t)(q + qb);
+        const int ci0 = wcnt + __popcll(b0 & lt), ci1 = wcnt + __popcll(b0) + __popcll(b1 & lt);
+        if (pass0 && ci0 < capw) wlist[ci0] = (uint16_t)q;
+        if (pass1 && ci1 < capw) wlist[ci1] = (uint16_t)(q + qb);
+        wcnt += __popcll(b0) + __popcll(b1);
+        x += xstep;
+        y += ystep;
+        if (x >= dc) { x -= dc; y++; }
     }
+    if (lane == 0) LS.ncw[wid] = wcnt;
     __syncthreads();
-    // dense: the list overflowed, so the strength runs on every pixel instead (m <= t_lo for
-    // every pixel the pair test rejects, so the map is the same) and the NMS walks every pixel
-    const bool dense = ncand > clist_cap;
-    const int nc = dense ? np : ncand;
+    // dense: a wave's list overflowed, so the strength runs on every pixel instead (m <= t_lo for
+    // every pixel the pair test rejects, so the map is the same) and the NMS walks every pixel.
+    // Otherwise survivor i (in wave order) sits at i + the unused tails of the regions before it.
+    int pre[NW], gap[NW];
+    bool dense = false;
+    int nc = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        const int cw = LS.ncw[w];
+        pre[w] = nc;
+        gap[w] = capw - cw;
+        dense |= cw > capw;
+        nc += cw;
+    }
+    if (dense) nc = np;
+    auto surv = [&](int i) -> int {
+        if (dense) return i;
+        int o = i;
+#pragma unroll
+        for (int w = 1; w < NW; w++) o += i >= pre[w] ? gap[w - 1] : 0;
+        return clist[o];
+    };
     {
         // two pixels per lane (i and i + hn) as the halves of one f16 pair, each read from its
         // pair-window half and joined by one v_perm per circle point:
@@ -636,8 +820,8 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
         const int hn = (nc + 1) >> 1;
         for (int i = tid; i < hn; i += NT) {
             const bool two = i + hn < nc;
-            const int pa = dense ? i : clist[i];
-            const int pb = two ? (dense ? i + hn : clist[i + hn]) : pa;
+            const int pa = surv(i);
+            const int pb = two ? surv(i + hn) : pa;
             const int ya = small_div(pa, inv_dc), xa = pa - ya * dc;
             const int yb = small_div(pb, inv_dc), xb = pb - yb * dc;
             const bool ha = ya >= R, hb = yb >= R;
@@ -672,7 +856,7 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     // ---- window-local strict 3x3 NMS at both thresholds, on the surviving pixels only; the
     // results are bits of a raster-order mask per threshold ----
     for (int i = tid; i < nc; i += NT) {
-        const int p = dense ? i : clist[i];
+        const int p = surv(i);
         const int py = small_div(p, inv_dc), px = p - py * dc;
         const uint8_t* c = &mv[(py + 1) * MPc + px + 1];
         const int m = c[0];
@@ -762,7 +946,8 @@ __global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict
     __shared__ int wsel, wtot;
     __shared__ uint16_t clist[SH::cap];
     __shared__ int ncand;
-    const FastLds LS{pw, mv, bmask, SH::nw, woff, &wsel, &wtot, clist, &ncand, min(P->clist_cap, SH::cap)};
+    __shared__ int ncw[NT / 64];
+    const FastLds LS{pw, mv, bmask, SH::nw, woff, &wsel, &wtot, clist, &ncand, ncw, min(P->clist_cap, SH::cap)};
     const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
     fast_cell_body<NT, SH::pwp, SH::mp>(P, cells, fb, cand, cand_cnt, err, lg % X, lg / X, LS, cp);
 }
@@ -901,10 +1086,6 @@ __device__ __forceinline__ void wave_aggregate_count(uint32_t tgt, uint32_t* cnt
 
 constexpr int kOctKR = 8;    // keys per thread kept in registers through the division (M <= 8 x 1024)
 
-__device__ __forceinline__ void wave_lds_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-}
 
 // In-place exclusive scan of arr[0..n) in LDS by ONE wave (a contiguous range per lane, DPP wave
 // scan of the range sums). Returns the total (uniform). No block barrier.
@@ -1630,6 +1811,16 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
     static_assert(kBlW * kBlW <= kPatchW * kDpP, "blurred region fits the patch");
     int cx = 0, cy = 0, sh = 0;
     LevelKp kp{};
+    // the IC_Angle disc offsets (n_disc <= 31 x 31 < 16 x 64), loaded with the keypoint so that
+    // they arrive with the patch instead of one dependent load per disc round; entries past
+    // n_disc are (0, 0) and add nothing
+    constexpr int kDiscU = 16;
+    int dv[kDiscU];
+    if (active) {
+        const int nd = P->n_disc;
+#pragma unroll
+        for (int u = 0; u < kDiscU; u++) dv[u] = lane + 64 * u < nd ? disc[lane + 64 * u] : 0;
+    }
     if (active) {
         const LevelGeom& G = P->lv[l];
         ImgRef im = level_img(P, fb, f, l);
@@ -1689,8 +1880,9 @@ __global__ __launch_bounds__(256) void k_desc(const ExtractPlan* __restrict__ P,
     float angle = 0.f;
     if (active) {
         int m10 = 0, m01 = 0;
-        for (int i = lane; i < P->n_disc; i += 64) {
-            const int uv = disc[i];
+#pragma unroll
+        for (int k = 0; k < kDiscU; k++) {
+            const int uv = dv[k];
             const int u = (int)(int16_t)(uv & 0xFFFF), vv = (int)(int16_t)(uv >> 16);
             const int val = pt[(kPatchR + vv) * kDpP + sh + kPatchR + u];
             m10 += u * val;
@@ -2001,6 +2193,15 @@ void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs
     dim3 blk(64, 4, 1);
     dim3 grd((D.h + 4 * kRzRows - 1) / (4 * kRzRows), (D.w + 255) / 256, B);
     ORBHIP_LAUNCH(k_resize, grd, blk, 0, st, dP, fb, l, xofs, xalpha, yofs, ybeta);
+}
+
+void launch_pyr_flow(const ExtractPlan* dP, const FrameBufs& fb, const int* xofs, const int* xalpha, const int* yofs,
+                     const int* ybeta, const PyrFlow& a, hipStream_t st) {
+    // persistent work-groups (4 per CU): any grid is deadlock-free (tickets), this one keeps the
+    // dispatch short and every CU busy
+    const int ntask = a.B * a.boff[kMaxLevels];
+    const int grid = std::max(kFlowQ, std::min((ntask + kFlowChunk - 1) / kFlowChunk, 1024));
+    ORBHIP_LAUNCH(k_pyr_flow, dim3(grid), dim3(256), 0, st, dP, fb, xofs, xalpha, yofs, ybeta, a);
 }
 
 void launch_resize_bands(const ExtractPlan* dP, int nbands, const FrameBufs& fb, int B, int s0, const int2* rows,

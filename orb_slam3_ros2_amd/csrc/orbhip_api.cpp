@@ -106,6 +106,12 @@ struct Plan {
     std::vector<int> bands;   // [nbands][kMaxLevels] (r0, r1) pairs
     int nbands = 0;
     DevBuf<int> d_bands;
+    // batches: k_pyr_flow's 16-row bands (level 1 first), the level l-1 bands each band's source
+    // rows lie in
+    int flow_boff[kMaxLevels + 1] = {0};
+    int flow_nbt = 0;
+    std::vector<int> flow_dep;   // (b0, b1) per band
+    DevBuf<int> d_flow_dep;
     OctreeCfg oct{};
     int kp_cap_frame = 0;   // sum of level caps = max keypoints per frame
     DevBuf<ExtractPlan> d_plan;
@@ -144,6 +150,7 @@ struct orbhip_ctx {
     DevBuf<uint16_t> d_nscratch;
     DevBuf<int> d_cand_cnt, d_lvl_cnt, d_lvl_nlap, d_err;
     DevBuf<int> d_cand_off, d_cand_fill;   // packed FAST candidates (batches, CandPack)
+    DevBuf<int> d_flow;         // k_pyr_flow: kFlowCtl control words + B x nbt band flags, zeroed when (re)allocated
     DevBuf<uint64_t> d_mpart;   // matcher chunk partials (match_part_entries)
     DevBuf<int> d_msync;        // one-launch matcher counters (zeroed once, reset by every launch)
     DevBuf<double> d_bw;        // bag-of-words weights (host transform)
@@ -584,6 +591,40 @@ static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& ou
             pl->nbands = nb;
         }
     }
+    // k_pyr_flow bands: task (l, b) = output rows [16 b, 16 b + 16) of level l; its source rows are
+    // what resize_tile reads for each 4-row group (the interior path loads kRzSrc = 6 rows from the
+    // group's first clamped source row, the per-row path rows sy and sy + 1), clamped
+    if (L > 1) {
+        constexpr int kFR = 16, kGroup = 4, kSrcRows = 6;
+        int nbt = 0;
+        for (int l = 1; l < L; l++) {
+            pl->flow_boff[l] = nbt;
+            nbt += (P.lv[l].h + kFR - 1) / kFR;
+        }
+        for (int l = L; l <= kMaxLevels; l++) pl->flow_boff[l] = nbt;
+        pl->flow_nbt = nbt;
+        pl->flow_dep.assign((size_t)nbt * 2, 0);
+        for (int l = 2; l < L; l++) {
+            const LevelGeom& G = P.lv[l];
+            const int Sh = P.lv[l - 1].h;
+            auto clampr = [&](int r) { return r < 0 ? 0 : (r < Sh ? r : Sh - 1); };
+            for (int b = 0; b * kFR < G.h; b++) {
+                const int r0 = b * kFR, r1 = std::min(r0 + kFR, G.h);
+                int lo = Sh, hi = 0;
+                for (int g = r0; g < r1; g += kGroup) {
+                    const int rb = clampr(pl->yofs[G.ytab_off + g]);
+                    lo = std::min(lo, rb);
+                    hi = std::max(hi, std::min(rb + kSrcRows - 1, Sh - 1));
+                    for (int dy = g; dy < std::min(g + kGroup, r1); dy++) {
+                        lo = std::min(lo, clampr(pl->yofs[G.ytab_off + dy]));
+                        hi = std::max(hi, clampr(pl->yofs[G.ytab_off + dy] + 1));
+                    }
+                }
+                pl->flow_dep[(size_t)(pl->flow_boff[l] + b) * 2] = lo / kFR;
+                pl->flow_dep[(size_t)(pl->flow_boff[l] + b) * 2 + 1] = hi / kFR;
+            }
+        }
+    }
     // IC_Angle disc offsets (u, v) packed as int16 pairs
     for (int v = -15; v <= 15; v++) {
         const int d = c->umax[std::abs(v)];
@@ -623,6 +664,7 @@ static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& ou
     HIPOK(pl->d_otab.ensure(pl->otab.size()));
     HIPOK(hipMemcpy(pl->d_otab.p, pl->otab.data(), pl->otab.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
     if (pl->nbands) HIPOK(up(pl->d_bands, pl->bands));
+    if (pl->flow_nbt) HIPOK(up(pl->d_flow_dep, pl->flow_dep));
     if (!pl->cone_hi.empty()) {
         HIPOK(pl->d_cone_hi.ensure(pl->cone_hi.size()));
         HIPOK(hipMemcpy(pl->d_cone_hi.p, pl->cone_hi.data(), pl->cone_hi.size() * sizeof(ConeRect),
@@ -647,6 +689,11 @@ static int ensure_batch(orbhip_ctx* c, const Plan* pl, int B) {
     HIPOK(c->d_cand_cnt.ensure((size_t)B * P.n_cells_total));
     HIPOK(c->d_cand_off.ensure((size_t)B * P.n_cells_total));
     HIPOK(c->d_cand_fill.ensure((size_t)B * kMaxLevels));
+    if (pl->flow_nbt) {
+        int* const was = c->d_flow.p;
+        HIPOK(c->d_flow.ensure(kFlowCtl + (size_t)B * pl->flow_nbt));
+        if (c->d_flow.p != was) HIPOK(hipMemset(c->d_flow.p, 0, c->d_flow.n * sizeof(int)));
+    }
     HIPOK(c->d_lvl_kp.ensure((size_t)B * P.kp_slots_total));
     HIPOK(c->d_lvl_cnt.ensure((size_t)B * P.n_levels));
     HIPOK(c->d_lvl_nlap.ensure((size_t)B * P.n_levels));
@@ -680,8 +727,11 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
     // each FAST cell waits on held its work-group slot ~1 us longer: k_fast_cells 525 -> 568 us
     const char* e_pk = std::getenv("ORBHIP_CAND_PACK");
     const bool pack = e_pk && e_pk[0] == '1';
+    // ORBHIP_RZ_FLOW=1 (read per call): batches build levels 1..L-1 in one k_pyr_flow launch
+    const char* e_fl = std::getenv("ORBHIP_RZ_FLOW");
+    const bool flow_on = e_fl && e_fl[0] == '1' && pl->flow_nbt > 0 && (int64_t)B * P.pyr_bytes < (1ll << 31);
     GraphKey key;
-    key.add(1).add((uint64_t)oct_fast).add((uint64_t)oct_max_dh).add((uint64_t)no_cone).add((uint64_t)cone_hi_on).add((uint64_t)pack).add((uint64_t)c->fast_nt).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
+    key.add(1).add((uint64_t)oct_fast).add((uint64_t)oct_max_dh).add((uint64_t)no_cone).add((uint64_t)cone_hi_on).add((uint64_t)flow_on).add((uint64_t)pack).add((uint64_t)c->fast_nt).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
         .add((uint64_t)lap1).ptr(d_kps).ptr(d_desc).add((uint64_t)cap).ptr(d_n).ptr(d_mono).ptr(st).ptr(c->d_pyr.p)
         .ptr(c->d_cand.p).ptr(c->d_kscratch.p).ptr(c->d_nscratch.p).ptr(c->d_cand_cnt.p).ptr(c->d_lvl_kp.p)
         .ptr(c->d_lvl_cnt.p).ptr(c->d_lvl_nlap.p).ptr(c->d_err.p).ptr(c->d_cand_off.p).ptr(c->d_cand_fill.p);
@@ -703,6 +753,16 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
         if (cone_path) {
             launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_cone_tab.p,
                             pl->cone_tab_stride, st);
+        } else if (flow_on) {
+            PyrFlow fa{};
+            fa.ctl = c->d_flow.p;
+            fa.flags = c->d_flow.p + kFlowCtl;
+            fa.dep = (const int2*)pl->d_flow_dep.p;
+            for (int l = 0; l <= kMaxLevels; l++) fa.boff[l] = pl->flow_boff[l];
+            fa.B = B;
+            fa.nbt = pl->flow_nbt;
+            fa.pyr_limit = (int)((int64_t)B * P.pyr_bytes);
+            launch_pyr_flow(pl->d_plan.p, fb, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p, pl->d_ybeta.p, fa, st);
         } else {
             const bool bands = !cone_hi && pl->nbands > 0;
             const int lr = cone_hi ? kConeHiStart + 1 : (bands ? kBandStart + 1 : P.n_levels);

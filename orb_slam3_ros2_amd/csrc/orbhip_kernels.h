@@ -86,6 +86,21 @@ void launch_resize_bands(const ExtractPlan* dP, int nbands, const FrameBufs& fb,
                          const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st);
 void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, int B, int l,
                    const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st);
+// k_pyr_flow (batches): levels 1..L-1 of every frame in one launch, a dataflow over 16-row bands
+constexpr int kFlowQ = 8;         // task queues (frame f in queue f mod kFlowQ)
+constexpr int kFlowChunk = 1;     // tickets taken per counter add
+constexpr int kFlowCtl = 16;      // control ints ahead of the flags
+struct PyrFlow {
+    int* ctl;                     // [0, Q) queue tickets, [Q] work-groups out, [Q+1] generation, [Q+2] timed-out waits
+    int* flags;                   // B x nbt band flags (zeroed once with ctl)
+    const int2* dep;              // per (level >= 2, band): the level l-1 bands its source rows lie in
+    int boff[kMaxLevels + 1];     // first band of each level (level 1 at 0), boff[l >= L] = nbt
+    int B;
+    int nbt;
+    int pyr_limit;                // bytes of the batch's pyramid block (buffer resource range)
+};
+void launch_pyr_flow(const ExtractPlan* dP, const FrameBufs& fb, const int* xofs, const int* xalpha, const int* yofs,
+                     const int* ybeta, const PyrFlow& a, hipStream_t st);
 // Packed FAST candidates (batches): per (frame, level) fill counters, zeroed before the launch, and
 // each cell's run offset (per frame); off == nullptr keeps each cell's fixed slot range
 struct CandPack {

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 W, H, B = 1280, 720, 64
 
 
-def _run(frames_np):
+def _run(frames_np, reps=1):
     import torch
     from orb_slam3_ros2_amd import ORBextractor, ORBmatcher
     ext = ORBextractor(1000, 1.2, 8, 20, 7)
@@ -27,7 +27,9 @@ def _run(frames_np):
     desc = torch.zeros((nb, cap, 32), dtype=torch.uint8, device=dev)
     n = torch.zeros(nb, dtype=torch.int32, device=dev)
     mono = torch.zeros(nb, dtype=torch.int32, device=dev)
-    ext.extract_batch_device(torch.from_numpy(np.ascontiguousarray(frames_np)).to(dev), kps, desc, n, mono)
+    fr = torch.from_numpy(np.ascontiguousarray(frames_np)).to(dev)
+    for _ in range(reps):   # reps > 1: the same context's launches back to back (k_pyr_flow generations)
+        ext.extract_batch_device(fr, kps, desc, n, mono)
     mm = torch.full((3, max(nb - 1, 1), cap), -7, dtype=torch.int32, device=dev)
     nm = torch.zeros(max(nb - 1, 1), dtype=torch.int32, device=dev)
     if nb > 1:
@@ -60,6 +62,18 @@ def test_c3_batch_vs_oracle(c3, oracle):
                                        True)
         assert nm[p] == on and np.array_equal(mm[0, p, :n[p]], om), p
         assert on > 200
+
+
+def test_c3_flow_pyramid_reproduces_batch(c3, monkeypatch):
+    """The batch pyramid as one dataflow launch (ORBHIP_RZ_FLOW=1, k_pyr_flow: 16-row band tasks
+    from a ticket counter, each waiting on the flags of the bands its source rows lie in) gives the
+    oracle-checked batch bit for bit, over three launches on one context (the band flags carry the
+    launch generation, nothing is reset between launches)."""
+    monkeypatch.setenv("ORBHIP_RZ_FLOW", "1")
+    frames, ref = c3
+    got = _run(frames, reps=3)
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)
 
 
 @pytest.mark.parametrize("N", [2, 3, 8])

@@ -44,9 +44,10 @@ def test_sizes_bit_exact(ext1000, oracle, w, h, seed):
 @pytest.mark.parametrize("w,h,scale,nlev,seed", [(1280, 720, 1.2, 8, 30), (641, 479, 1.2, 8, 31),
                                                  (641, 481, 1.5, 5, 32), (801, 601, 1.9, 4, 33),
                                                  (1001, 751, 2.5, 3, 34)])
-@pytest.mark.parametrize("hi", ["bands", "bands5", "resize", "cone"])
+@pytest.mark.parametrize("hi", ["bands", "bands5", "resize", "cone", "flow"])
 def test_resize_cascade_bit_exact(oracle, monkeypatch, w, h, scale, nlev, seed, hi):
-    """The batch engine forced on single frames: k_resize for every level (the default), or
+    """The batch engine forced on single frames: k_resize for every level (the default), the
+    one-launch dataflow pyramid (ORBHIP_RZ_FLOW=1, k_pyr_flow), or
     k_resize for levels 1-2 and then levels 3.. by the opt-in k_resize_bands (ORBHIP_RZ_BANDS=16
     or 5 row bands per frame) or the opt-in batch cone (ORBHIP_CONE_HI=1). Odd sizes take the edge
     lanes, scale factors above 1.2 k_resize's per-row path (a 4-row group reads more than 6
@@ -59,6 +60,8 @@ def test_resize_cascade_bit_exact(oracle, monkeypatch, w, h, scale, nlev, seed, 
         monkeypatch.setenv("ORBHIP_RZ_BANDS", "16")
     elif hi == "bands5":
         monkeypatch.setenv("ORBHIP_RZ_BANDS", "5")
+    elif hi == "flow":
+        monkeypatch.setenv("ORBHIP_RZ_FLOW", "1")
     ext = ORBextractor(1000, scale, nlev, 20, 7)
     _check(ext, oracle, synthetic_frame(seed, w, h), scale=scale, nlevels=nlev)
 

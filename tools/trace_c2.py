@@ -17,7 +17,7 @@ import bench  # noqa: E402
 
 STRIDE, NK = 16384, 8
 NAMES = {0: "k_pyr_cone|k_resize(l=1)", 1: "k_fast_cells", 2: "k_octree", 3: "k_desc", 4: "k_match_top2", 5: "k_match_finish",
-         6: "k_resize_bands"}
+         6: "k_resize_bands", 7: "k_pyr_flow"}
 
 
 def main():
@@ -35,7 +35,7 @@ def main():
     assert L.orbhip_test_trace(0, buf.ctypes.data) == 0
     t_min = None
     rows = []
-    for k in range(7):
+    for k in range(8):
         seg = buf[k * STRIDE: k * STRIDE + 8192].reshape(-1, 2).astype(np.int64)
         ok = seg[:, 1] > 0
         if not ok.any():
