@@ -915,6 +915,9 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
         slot = G.slot_base + ncand;
     }
     uint32_t* out = cand + (int64_t)f * P->n_slots_total + slot;
+    // primary slots (fixed ranges): the cell's first kCandPrim candidates sit next to the other
+    // cells' (16 per cell, cell-major), so the octree reads them as whole lines
+    uint32_t* const prim = (cp.prim && !cp.off) ? cp.prim + ((int64_t)f * P->n_cells_total + cell) * kCandPrim : nullptr;
     // one lane per mask word walks its set bits (a cell keeps a few corners: ~1 per word), in
     // raster order from the word's scanned offset
     for (int w = tid; w < nwd; w += NT) {
@@ -925,7 +928,10 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
             mk &= mk - 1;
             const int py = small_div(p, inv_dc), px = p - py * dc;
             const int x = cg.x0 + 3 + px - G.min_bx, y = cg.y0 + 3 + py - G.min_by;
-            out[o++] = pack_cand(x, y, (int)mv[(py + 1) * MPc + px + 1] - 1);
+            const uint32_t v = pack_cand(x, y, (int)mv[(py + 1) * MPc + px + 1] - 1);
+            if (prim && o < kCandPrim) prim[o] = v;
+            else out[o] = v;
+            o++;
         }
     }
     if (tid == 0) *cnt_out = wtot;
@@ -1122,7 +1128,8 @@ __device__ __forceinline__ int multi4(const uint32_t* c) { return (c[0] > 1) + (
 constexpr int kOctMaxDh = 6;
 
 __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__ P, const CellGeom* __restrict__ cells,
-                                                 const uint16_t* __restrict__ otab, const uint32_t* __restrict__ cand, const int* __restrict__ cand_cnt,
+                                                 const uint16_t* __restrict__ otab, const uint32_t* __restrict__ cand,
+                                                 const uint32_t* __restrict__ cprim, const int* __restrict__ cand_cnt,
                                                  const int* __restrict__ cand_off,
                                                  uint32_t* __restrict__ kscratch, uint16_t* __restrict__ nscratch,
                                                  LevelKp* __restrict__ lvl_kp, int* __restrict__ lvl_cnt,
@@ -1219,6 +1226,12 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
         }
     };
     const uint32_t* cbase = cand + (int64_t)f * P->n_slots_total;
+    // key j of level cell c: its primary slot (j < kCandPrim, fixed ranges) or its slot range
+    const uint32_t* pbase = (cprim && !cand_off) ? cprim + ((int64_t)f * P->n_cells_total + G.cell_base) * kCandPrim
+                                                 : nullptr;
+    auto cand_at = [&](int c, int j) -> uint32_t {
+        return (pbase && j < kCandPrim) ? pbase[c * kCandPrim + j] : cbase[S.cslot[c] + j];
+    };
     if (ncell <= nt) {
         // one cell per thread: every count / slot load in flight at once, one block scan
         const int c = tid < ncell ? cc[tid] : 0;
@@ -1277,7 +1290,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                 }
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++) kv[u] = cbase[S.cslot[lo[u]] + (k[u] - S.cellstart[lo[u]])];
+            for (int u = 0; u < 4; u++) kv[u] = cand_at(lo[u], k[u] - S.cellstart[lo[u]]);
         };
         auto root_of = [&](uint32_t key) { return root_of_x(cand_x(key)); };
         auto root_rect = [&](int r) { return mk_rect((int)(hX * (float)r), 0, (int)(hX * (float)(r + 1)), Hroot); };
@@ -1313,7 +1326,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                     for (int u = 0; u < 4; u++) {
                         const int k = min(k0 + tid + u * nt, M - 1);
                         const int c = cellof[k];
-                        kv[u] = cbase[S.cslot[c] + (k - S.cellstart[c])];
+                        kv[u] = cand_at(c, k - S.cellstart[c]);
                     }
                 } else {
                     gather4(k0, kv);
@@ -2273,14 +2286,14 @@ size_t octree_lds_bytes(const ExtractPlan& hP, const OctreeCfg& cfg) {
 }
 
 void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const uint16_t* otab,
-                   const uint32_t* cand,
+                   const uint32_t* cand, const uint32_t* cprim,
                    const int* cand_cnt, const int* cand_off, uint32_t* kscratch, uint16_t* nscratch, LevelKp* lvl_kp,
                    int* lvl_cnt, int* lvl_nlap, const OctreeCfg& cfg, int* err, int B, hipStream_t st,
                    unsigned long long* stamp) {
     const size_t lds = octree_lds_bytes(hP, cfg);
     dim3 grd(B, hP.n_levels, 1);
-    ORBHIP_LAUNCH(k_octree, grd, dim3(1024), lds, st, dP, cells, otab, cand, cand_cnt, cand_off, kscratch, nscratch,
-                  lvl_kp, lvl_cnt, lvl_nlap, cfg, err, stamp);
+    ORBHIP_LAUNCH(k_octree, grd, dim3(1024), lds, st, dP, cells, otab, cand, cprim, cand_cnt, cand_off, kscratch,
+                  nscratch, lvl_kp, lvl_cnt, lvl_nlap, cfg, err, stamp);
 }
 
 constexpr int kDescKpMaxSlots = 16384;

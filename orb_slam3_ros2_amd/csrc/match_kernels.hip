@@ -41,6 +41,20 @@ constexpr int kTC = 256;     // train descriptors per workgroup chunk (64 per wa
 constexpr int kTCSmall = 64; // 16 per wave: one pair (C2), where 256-chunks leave the chip idle
 constexpr int kFusedMaxPairs = 4;   // k_match_fused up to this many pairs (the sync scratch holds 64 ints each)
 
+// A chunk partial {best | second << 16, index} (8 B), or packed in 4 B while every train index
+// fits 14 bits (pk): best | second << 9 | index << 18 (index 0x3FFF when there is no best), which
+// halves the partials' traffic; unpacked to the 8-byte form on read
+__device__ __forceinline__ void part_store(uint2* part, int64_t i, int pk, int b, int s, int bi) {
+    if (pk) ((uint32_t*)part)[i] = (uint32_t)b | ((uint32_t)s << 9) | ((uint32_t)(b < 256 ? bi : 0x3FFF) << 18);
+    else part[i] = make_uint2((uint32_t)b | ((uint32_t)s << 16), (uint32_t)bi);
+}
+__device__ __forceinline__ uint2 part_load(const uint2* part, int64_t i, int pk) {
+    if (!pk) return part[i];
+    const uint32_t x = ((const uint32_t*)part)[i];
+    const uint32_t b = x & 511u, s = (x >> 9) & 511u;
+    return make_uint2(b | (s << 16), b < 256u ? (x >> 18) : 0x7fffffffu);
+}
+
 __device__ __forceinline__ void top2_merge(int& b, int& i, int& s, int b2, int i2, int s2) {
     const int nb = (b2 < b || (b2 == b && i2 < i)) ? b2 : b;
     const int ni = (b2 < b || (b2 == b && i2 < i)) ? i2 : i;
@@ -56,7 +70,7 @@ __device__ __forceinline__ void top2_merge(int& b, int& i, int& s, int b2, int i
 // pairs: a pair's train chunk and query blocks are then read by ONE L2, not by all eight.
 template <int TC>
 __global__ __launch_bounds__(256) void k_match_top2(MatchView v, uint2* __restrict__ part, int nchunk_cap,
-                                                     int part_stride, int xrun) {
+                                                     int part_stride, int xrun, int pk) {
     __shared__ __attribute__((aligned(16))) uint4 tile[TC * 2];
     __shared__ int mb[3][64], mi[3][64], ms[3][64];
     TR_BEGIN()
@@ -94,8 +108,7 @@ __global__ __launch_bounds__(256) void k_match_top2(MatchView v, uint2* __restri
     if (wid == 0 && q < nq) {
 #pragma unroll
         for (int w = 0; w < 3; w++) top2_merge(b, bi, s, mb[w][lane], mi[w][lane], ms[w][lane]);
-        part[((int64_t)p * nchunk_cap + by) * part_stride + q] = make_uint2((uint32_t)b | ((uint32_t)s << 16),
-                                                                                  (uint32_t)bi);
+        part_store(part, ((int64_t)p * nchunk_cap + by) * part_stride + q, pk, b, s, bi);
     }
     TR_END(4)
 }
@@ -142,7 +155,7 @@ __global__ __launch_bounds__(1024) void k_match_finish(MatchView v, const uint2*
                                                         int part_stride, int tc, int th_low, float ratio,
                                                         int check_orientation, int32_t* __restrict__ match,
                                                         int32_t* __restrict__ best_out, int32_t* __restrict__ second_out,
-                                                        int32_t* __restrict__ nmatch) {
+                                                        int32_t* __restrict__ nmatch, int pk) {
     __shared__ int hist[32];
     __shared__ int keep[3];
     __shared__ int cnt;
@@ -164,7 +177,7 @@ __global__ __launch_bounds__(1024) void k_match_finish(MatchView v, const uint2*
     if (tid < nq) {
 #pragma unroll
         for (int j = 0; j < 16; j++)
-            u0[j] = part[((int64_t)p * nchunk_cap + min(j, max(nch - 1, 0))) * part_stride + tid];
+            u0[j] = part_load(part, ((int64_t)p * nchunk_cap + min(j, max(nch - 1, 0))) * part_stride + tid, pk);
         qa0 = qa[(int64_t)tid * v.angle_stride];
     }
     if (tang_lds)
@@ -188,7 +201,7 @@ __global__ __launch_bounds__(1024) void k_match_finish(MatchView v, const uint2*
             uint2 u[16];
 #pragma unroll
             for (int j = 0; j < 16; j++)
-                u[j] = part[((int64_t)p * nchunk_cap + min(c0 + j, nch - 1)) * part_stride + q];
+                u[j] = part_load(part, ((int64_t)p * nchunk_cap + min(c0 + j, nch - 1)) * part_stride + q, pk);
 #pragma unroll
             for (int j = 0; j < 16; j++)
                 if (c0 + j < nch) top2_merge(b, bi, s, (int)(u[j].x & 0xFFFF), (int)u[j].y, (int)(u[j].x >> 16));
@@ -461,20 +474,31 @@ static void run_match(const MatchView& v, int npairs, int max_q, int max_t, int 
     const int qblocks = (max_q + 63) / 64;
     // 16 trains per wave while 64 per wave would leave most of the chip idle (one pair)
     const bool small = (int64_t)npairs * qblocks * ((max_t + kTC - 1) / kTC) < 512;
-    const int tc = small ? kTCSmall : kTC;
+    // batches: trains per chunk (ORBHIP_MATCH_TC = 256 / 512 / 1024, read per call; A/B): bigger
+    // chunks write fewer (query, chunk) partials
+    const char* e_tc = std::getenv("ORBHIP_MATCH_TC");
+    const int tcb = e_tc ? std::atoi(e_tc) : kTC;
+    const int tc = small ? kTCSmall : (tcb == 512 || tcb == 1024 ? tcb : kTC);
     const int nch = std::max(1, (max_t + tc - 1) / tc);
+    const int pk = max_t <= 0x3FFF ? 1 : 0;   // 4-byte partials while train indices fit 14 bits
     if (timer) timer->begin(5, st);
     if (qblocks > 0 && max_t > 0) {
         if (small)
             ORBHIP_LAUNCH(k_match_top2<kTCSmall>, dim3(qblocks, nch, npairs), dim3(256), 0, st, v, part, nch,
-                               max_q, 0);
-        else   // batches: whole pairs per XCD (ORBHIP_MATCH_XCD=0: the plain round-robin order)
+                               max_q, 0, pk);
+        else if (tc == 1024)   // batches: whole pairs per XCD (ORBHIP_MATCH_XCD=0: the plain round-robin order)
+            ORBHIP_LAUNCH(k_match_top2<1024>, dim3(qblocks, nch, npairs), dim3(256), 0, st, v, part, nch, max_q,
+                          match_xcd_on() && npairs >= 8 ? qblocks * nch : 0, pk);
+        else if (tc == 512)
+            ORBHIP_LAUNCH(k_match_top2<512>, dim3(qblocks, nch, npairs), dim3(256), 0, st, v, part, nch, max_q,
+                          match_xcd_on() && npairs >= 8 ? qblocks * nch : 0, pk);
+        else
             ORBHIP_LAUNCH(k_match_top2<kTC>, dim3(qblocks, nch, npairs), dim3(256), 0, st, v, part, nch, max_q,
-                          match_xcd_on() && npairs >= 8 ? qblocks * nch : 0);
+                          match_xcd_on() && npairs >= 8 ? qblocks * nch : 0, pk);
     }
     if (timer) { timer->end(5, st); timer->begin(6, st); }
     ORBHIP_LAUNCH(k_match_finish, dim3(npairs), dim3(1024), 0, st, v, part, nch, max_q, tc, th_low, ratio,
-                       check_orientation, match, best, second, nmatch);
+                       check_orientation, match, best, second, nmatch, pk);
     if (timer) timer->end(6, st);
 }
 

@@ -147,6 +147,7 @@ struct orbhip_ctx {
     // per-batch scratch (grown on demand)
     DevBuf<uint8_t> d_in, d_pyr;
     DevBuf<uint32_t> d_cand, d_kscratch;
+    DevBuf<uint32_t> d_cprim;   // FAST candidates' primary slots (kCandPrim per cell)
     DevBuf<uint16_t> d_nscratch;
     DevBuf<int> d_cand_cnt, d_lvl_cnt, d_lvl_nlap, d_err;
     DevBuf<int> d_cand_off, d_cand_fill;   // packed FAST candidates (batches, CandPack)
@@ -684,6 +685,7 @@ static int ensure_batch(orbhip_ctx* c, const Plan* pl, int B) {
     const ExtractPlan& P = pl->h;
     HIPOK(c->d_pyr.ensure((size_t)B * P.pyr_bytes));
     HIPOK(c->d_cand.ensure((size_t)B * P.n_slots_total));
+    HIPOK(c->d_cprim.ensure((size_t)B * P.n_cells_total * kCandPrim));
     HIPOK(c->d_kscratch.ensure((size_t)B * P.n_slots_total));
     HIPOK(c->d_nscratch.ensure((size_t)B * P.n_slots_total));
     HIPOK(c->d_cand_cnt.ensure((size_t)B * P.n_cells_total));
@@ -734,7 +736,7 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
     key.add(1).add((uint64_t)oct_fast).add((uint64_t)oct_max_dh).add((uint64_t)no_cone).add((uint64_t)cone_hi_on).add((uint64_t)flow_on).add((uint64_t)pack).add((uint64_t)c->fast_nt).ptr(pl).ptr(d_imgs).add((uint64_t)B).add((uint64_t)stride).add((uint64_t)fstride).add((uint64_t)lap0)
         .add((uint64_t)lap1).ptr(d_kps).ptr(d_desc).add((uint64_t)cap).ptr(d_n).ptr(d_mono).ptr(st).ptr(c->d_pyr.p)
         .ptr(c->d_cand.p).ptr(c->d_kscratch.p).ptr(c->d_nscratch.p).ptr(c->d_cand_cnt.p).ptr(c->d_lvl_kp.p)
-        .ptr(c->d_lvl_cnt.p).ptr(c->d_lvl_nlap.p).ptr(c->d_err.p).ptr(c->d_cand_off.p).ptr(c->d_cand_fill.p);
+        .ptr(c->d_lvl_cnt.p).ptr(c->d_lvl_nlap.p).ptr(c->d_err.p).ptr(c->d_cand_off.p).ptr(c->d_cand_fill.p).ptr(c->d_cprim.p);
     return c->graphs.run(key, st, c->timer.stage != 0, [&](hipStream_t st) -> int {
         FrameBufs fb;
         fb.in = d_imgs; fb.in_stride = stride; fb.in_fstride = fstride; fb.pyr = c->d_pyr.p;
@@ -779,6 +781,7 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
         tm.end(1, st);
         tm.begin(2, st);
         CandPack cp;
+        cp.prim = c->d_cprim.p;
         if (pack) {
             HIPOK(hipMemsetAsync(c->d_cand_fill.p, 0, sizeof(int) * (size_t)B * kMaxLevels, st));
             cp.fill = c->d_cand_fill.p;
@@ -792,7 +795,8 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
         oc.fast = oct_fast;
         oc.max_dh = oct_max_dh;
         tm.begin(3, st);
-        launch_octree(pl->d_plan.p, P, pl->d_cells.p, pl->d_otab.p, c->d_cand.p, c->d_cand_cnt.p, cp.off,
+        launch_octree(pl->d_plan.p, P, pl->d_cells.p, pl->d_otab.p, c->d_cand.p, cp.off ? nullptr : cp.prim,
+                      c->d_cand_cnt.p, cp.off,
                       c->d_kscratch.p, c->d_nscratch.p, c->d_lvl_kp.p, c->d_lvl_cnt.p, c->d_lvl_nlap.p, oc, c->d_err.p, B,
                       st, (tm.stage == 3 && tm.dstamp && tm.n < StageTimer::kCap) ? tm.dstamp + tm.n : nullptr);
         tm.end(3, st);
@@ -1592,6 +1596,13 @@ int orbhip_test_extract_debug(orbhip_ctx* c, const uint8_t* img, int w, int h, i
     }
     HIPOK(hipMemcpy(cand, c->d_cand.p, (size_t)P.n_slots_total * 4, hipMemcpyDeviceToHost));
     HIPOK(hipMemcpy(cand_cnt, c->d_cand_cnt.p, (size_t)P.n_cells_total * 4, hipMemcpyDeviceToHost));
+    {   // each cell's first kCandPrim candidates sit in its primary slots: back into its slot range
+        std::vector<uint32_t> prim((size_t)P.n_cells_total * kCandPrim);
+        HIPOK(hipMemcpy(prim.data(), c->d_cprim.p, prim.size() * 4, hipMemcpyDeviceToHost));
+        for (int ci = 0; ci < P.n_cells_total; ci++)
+            for (int j = 0; j < std::min(cand_cnt[ci], kCandPrim); j++)
+                cand[pl->cells[ci].slot_off + j] = prim[(size_t)ci * kCandPrim + j];
+    }
     HIPOK(hipMemcpy(lvl, c->d_lvl_kp.p, (size_t)P.kp_slots_total * sizeof(LevelKp), hipMemcpyDeviceToHost));
     HIPOK(hipMemcpy(lvl_cnt, c->d_lvl_cnt.p, (size_t)P.n_levels * 4, hipMemcpyDeviceToHost));
     HIPOK(hipMemcpy(lvl_nlap, c->d_lvl_nlap.p, (size_t)P.n_levels * 4, hipMemcpyDeviceToHost));

@@ -106,13 +106,18 @@ void launch_pyr_flow(const ExtractPlan* dP, const FrameBufs& fb, const int* xofs
 struct CandPack {
     int* fill = nullptr;   // B x kMaxLevels
     int* off = nullptr;    // B x n_cells_total
+    // fixed slot ranges (off == nullptr): a cell's first kCandPrim candidates go to its primary
+    // slots prim[(f n_cells_total + cell) kCandPrim ..], the rest to its slot range at the same
+    // index; null: everything in the slot range
+    uint32_t* prim = nullptr;
 };
+constexpr int kCandPrim = 16;
 void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,
                  uint32_t* cand, int* cand_cnt, int* err, hipStream_t st, int nt_hint = 0, CandPack cp = {});
 size_t octree_lds_bytes(const ExtractPlan& hP, const OctreeCfg& cfg);
 bool octree_set_lds_limit(size_t bytes);
 void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const uint16_t* otab,
-                   const uint32_t* cand,
+                   const uint32_t* cand, const uint32_t* cprim,
                    const int* cand_cnt, const int* cand_off, uint32_t* kscratch, uint16_t* nscratch, LevelKp* lvl_kp,
                    int* lvl_cnt, int* lvl_nlap, const OctreeCfg& cfg, int* err, int B, hipStream_t st,
                    unsigned long long* stamp = nullptr);
