@@ -634,7 +634,7 @@ struct FastLds {
     int cap;                        // clist entries in use: min(plan's clist_cap, the variant's)
 };
 
-template <int NT, int PWP, int MP>
+template <int NT, int PWP, int MP, int PWR>
 __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P, const CellGeom* __restrict__ cells,
                                                const FrameBufs& fb, uint32_t* __restrict__ cand,
                                                int* __restrict__ cand_cnt, int* __restrict__ err, int cell, int f,
@@ -679,8 +679,7 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
             sh = (int)(((uintptr_t)base) & 3);
             const uint32_t* b4 = (const uint32_t*)(base - sh);
             const int nwd = (wc + sh + 3) >> 2;   // <= PWP / 4
-            const int tot = nwd * RW, p4 = im.pitch >> 2;
-            const float inv_n = 1.0f / (float)nwd;
+            const int p4 = im.pitch >> 2;
             auto put = [&](int r, int j, uint32_t a, uint32_t b) {
                 uint4 o;
                 o.x = __builtin_amdgcn_perm(b, a, 0x0C040C00u) | kPwBias;
@@ -689,31 +688,24 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
                 o.w = __builtin_amdgcn_perm(b, a, 0x0C070C03u) | kPwBias;
                 *(uint4*)(pw + r * PWP + 4 * j) = o;
             };
-            constexpr int NU = (NT >= 512) ? 1 : 512 / NT;
-            if (tot <= NU * NT) {
-                uint32_t va[NU], vb[NU];
+            // threads on a (row, dword column) grid, no division: JC columns per row (>= the
+            // window's dwords), NT / JC rows per pass, every pass's loads in flight together
+            constexpr int JC = (PWP / 4 <= 16) ? 16 : 32;
+            constexpr int RP = NT / JC;
+            constexpr int NP = (PWR + RP - 1) / RP;
+            const int j = tid % JC, r0 = tid / JC;
+            uint32_t va[NP], vb[NP];
 #pragma unroll
-                for (int u = 0; u < NU; u++) {
-                    const int i = min(tid + NT * u, tot - 1);
-                    const int r = small_div(i, inv_n), j = i - r * nwd;
-                    va[u] = b4[(int64_t)r * p4 + j];
-                    vb[u] = r + R < hc ? b4[(int64_t)(r + R) * p4 + j] : 0u;
-                }
+            for (int u = 0; u < NP; u++) {
+                const int r = r0 + RP * u;
+                const bool ok = r < RW && j < nwd;
+                va[u] = ok ? b4[(int64_t)r * p4 + j] : 0u;
+                vb[u] = ok && r + R < hc ? b4[(int64_t)(r + R) * p4 + j] : 0u;
+            }
 #pragma unroll
-                for (int u = 0; u < NU; u++) {
-                    const int i = tid + NT * u;
-                    if (i < tot) {
-                        const int r = small_div(i, inv_n);
-                        put(r, i - r * nwd, va[u], vb[u]);
-                    }
-                }
-            } else {
-                for (int i = tid; i < tot; i += NT) {
-                    const int r = small_div(i, inv_n), j = i - r * nwd;
-                    const uint32_t a = b4[(int64_t)r * p4 + j];
-                    const uint32_t b = r + R < hc ? b4[(int64_t)(r + R) * p4 + j] : 0u;
-                    put(r, j, a, b);
-                }
+            for (int u = 0; u < NP; u++) {
+                const int r = r0 + RP * u;
+                if (r < RW && j < nwd) put(r, j, va[u], vb[u]);
             }
         } else {
             const int tot = wc * RW;
@@ -955,7 +947,7 @@ __global__ __launch_bounds__(NT) void k_fast_cells(const ExtractPlan* __restrict
     __shared__ int ncw[NT / 64];
     const FastLds LS{pw, mv, bmask, SH::nw, woff, &wsel, &wtot, clist, &ncand, ncw, min(P->clist_cap, SH::cap)};
     const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
-    fast_cell_body<NT, SH::pwp, SH::mp>(P, cells, fb, cand, cand_cnt, err, lg % X, lg / X, LS, cp);
+    fast_cell_body<NT, SH::pwp, SH::mp, SH::pwr>(P, cells, fb, cand, cand_cnt, err, lg % X, lg / X, LS, cp);
 }
 
 // ---------------------------------------------------------------------------
