@@ -104,9 +104,10 @@ __device__ __forceinline__ void lds_only_barrier() {
 // one workgroup per segment: x of its separator rows from x_Z, then L_II^T x_I = y_I - L_ZI^T x_Z
 // tile by tile (tile column R: every tile (R', R), R' > R, of the envelope), then the scatter to S's
 // order. A failed factorization anywhere (a segment or the separator system) zeroes x and flag.
-// The step's operands do not depend on x: each group's first two tiles of column R - 1, the
-// Linv_{R-1} column and y_{R-1} are loaded while step R runs, and the envelope sits in LDS, so a
-// step waits on LDS and barriers only (a column deeper than 16 tiles loads the rest in the step).
+// The step's operands do not depend on x: each thread's first three tiles of column R - 1 (half
+// a tile column each), Linv_{R-1} and y_{R-1} are loaded while step R runs, and the envelope sits
+// in LDS, so a step waits on LDS and barriers only (a column deeper than 12 tiles loads the rest
+// in the step).
 // the segment buffers are reached through pointers loaded from memory (NdSegDev), which the
 // compiler cannot place in an address space: without these casts every load is a flat load,
 // counted in lgkmcnt too, so each LDS wait of a step would also wait for the prefetched tiles
@@ -141,61 +142,70 @@ __global__ __launch_bounds__(256) void k_nd_backsolve(NdDev d) {
         else d.flag[0] = ok;
     }
     const int c = tid & 31, g = tid >> 5;
-    // group g's tiles of column R: rows R + 1 + g, + 8, ... inside the envelope
+    // group g = (tile slot ts, row half): its tiles of column R are rows R + 1 + ts, + 4, ... inside
+    // the envelope, 16 of their 32 rows each
+    const int ts = g >> 1, rh = (g & 1) * 16;
     auto next_row = [&](int R, int Rp) {
-        for (; Rp < s.NT; Rp += 8)
+        for (; Rp < s.NT; Rp += 4)
             if (R >= rfs[Rp]) return Rp;
         return -1;
     };
-    double vn0[kT], vn1[kT], lvn[kT], yn = 0.0;
-    int rpn0 = -1, rpn1 = -1;
+    // per step and thread: the first three of its tiles (16 loads each), 4 entries of Linv_R, y:
+    // 53 loads in flight, under the 63 that vmcnt can count (more would make the step wait for
+    // its own prefetch)
+    constexpr int kPT = 3;
+    double vn[kPT][16], lqn[4], yn = 0.0;
+    int rpn[kPT];
     auto prefetch = [&](int R) {
-        rpn0 = next_row(R, R + 1 + g);
-        rpn1 = rpn0 >= 0 ? next_row(R, rpn0 + 8) : -1;
-        if (rpn0 >= 0) {
-            const auto t = gp(s.buf) + dag_off_L(s.NT, rpn0, R);
+        int Rp = R + 1 + ts;
 #pragma unroll
-            for (int r = 0; r < kT; r++) vn0[r] = t[tq(r, c)];
-        }
-        if (rpn1 >= 0) {
-            const auto t = gp(s.buf) + dag_off_L(s.NT, rpn1, R);
+        for (int k = 0; k < kPT; k++) {
+            Rp = Rp >= 0 ? next_row(R, Rp) : -1;
+            rpn[k] = Rp;
+            if (Rp >= 0) {
+                const auto t = gp(s.buf) + dag_off_L(s.NT, Rp, R);
 #pragma unroll
-            for (int r = 0; r < kT; r++) vn1[r] = t[tq(r, c)];
+                for (int r = 0; r < 16; r++) vn[k][r] = t[tq(rh + r, c)];
+                Rp += 4;
+            }
         }
-        if (tid < kT) {
-            const auto li = gp(s.buf) + dag_off_Linv(s.NT, R);
+        const auto li = gp(s.buf) + dag_off_Linv(s.NT, R);
 #pragma unroll
-            for (int q = 0; q < kT; q++) lvn[q] = li[tq(q, tid)];
-            yn = gp(s.buf)[dag_off_y(s.NT, R) + tid];
-        }
+        for (int k = 0; k < 4; k++) lqn[k] = li[tq(4 * g + k, c)];
+        if (tid < kT) yn = gp(s.buf)[dag_off_y(s.NT, R) + tid];
     };
     if (ok && s.nti > 0) prefetch(s.nti - 1);
     for (int R = s.nti - 1; R >= 0 && ok; R--) {
-        double v0[kT], v1[kT], lv[kT];
+        double v[kPT][16], lq[4];
+        int rp[kPT];
 #pragma unroll
-        for (int r = 0; r < kT; r++) { v0[r] = vn0[r]; v1[r] = vn1[r]; lv[r] = lvn[r]; }
-        const int rp0 = rpn0, rp1 = rpn1;
+        for (int k = 0; k < kPT; k++) {
+            rp[k] = rpn[k];
+#pragma unroll
+            for (int r = 0; r < 16; r++) v[k][r] = vn[k][r];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) lq[k] = lqn[k];
         const double yR = yn;
         if (R > 0) prefetch(R - 1);
         double a4[4] = {0.0, 0.0, 0.0, 0.0};
-        if (rp0 >= 0) {
-            const double* xr = xs + rp0 * kT;
 #pragma unroll
-            for (int r = 0; r < kT; r++) a4[r & 3] = fma(v0[r], xr[r], a4[r & 3]);
+        for (int k = 0; k < kPT; k++) {
+            if (rp[k] < 0) continue;
+            const double* xr = xs + rp[k] * kT + rh;
+#pragma unroll
+            for (int r = 0; r < 16; r++) a4[r & 3] = fma(v[k][r], xr[r], a4[r & 3]);
         }
-        if (rp1 >= 0) {
-            const double* xr = xs + rp1 * kT;
-#pragma unroll
-            for (int r = 0; r < kT; r++) a4[r & 3] = fma(v1[r], xr[r], a4[r & 3]);
-            // further tiles of this group (a column deeper than 16 tiles): loaded here
-            for (int Rp = next_row(R, rp1 + 8); Rp >= 0; Rp = next_row(R, Rp + 8)) {
+        // further tiles of this group (a column deeper than 12 tiles): loaded here
+        if (rp[kPT - 1] >= 0) {
+            for (int Rp = next_row(R, rp[kPT - 1] + 4); Rp >= 0; Rp = next_row(R, Rp + 4)) {
                 const auto t = gp(s.buf) + dag_off_L(s.NT, Rp, R);
-                const double* xq = xs + Rp * kT;
-                double w[kT];
+                const double* xq = xs + Rp * kT + rh;
+                double w[16];
 #pragma unroll
-                for (int r = 0; r < kT; r++) w[r] = t[tq(r, c)];
+                for (int r = 0; r < 16; r++) w[r] = t[tq(rh + r, c)];
 #pragma unroll
-                for (int r = 0; r < kT; r++) a4[r & 3] = fma(w[r], xq[r], a4[r & 3]);
+                for (int r = 0; r < 16; r++) a4[r & 3] = fma(w[r], xq[r], a4[r & 3]);
             }
         }
         part[g * kT + c] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
@@ -206,11 +216,18 @@ __global__ __launch_bounds__(256) void k_nd_backsolve(NdDev d) {
             sv[tid] = y;
         }
         lds_only_barrier();
-        if (tid < kT) {   // x_R = Linv_R^T s
-            double b4[4] = {0.0, 0.0, 0.0, 0.0};
+        // x_R = Linv_R^T s: thread (g, c) sums rows 4g .. 4g+3 of column c, then 8 partials
+        {
+            double p2 = 0.0;
 #pragma unroll
-            for (int q = 0; q < kT; q++) b4[q & 3] = fma(lv[q], sv[q], b4[q & 3]);
-            xs[R * kT + tid] = (b4[0] + b4[1]) + (b4[2] + b4[3]);
+            for (int k = 0; k < 4; k++) p2 = fma(lq[k], sv[4 * g + k], p2);
+            part[g * kT + c] = p2;
+        }
+        lds_only_barrier();
+        if (tid < kT) {
+            double xv = 0.0;
+            for (int q = 0; q < 8; q++) xv += part[q * kT + tid];
+            xs[R * kT + tid] = xv;
         }
         lds_only_barrier();
     }
