@@ -1524,6 +1524,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     // would leave it mostly idle, so their items are cut to 4 pairs (4x the lanes)
     const int chunk = B >= 32 ? kSchurChunk : 4;
     parallel_for(B, nth, [&](int b) { pp[b].rc = prepare(probs[b], pp[b], chunk); });
+    const double t_prepare = now();
     for (int b = 0; b < B; b++)
         if (pp[b].rc) return pp[b].rc;
     if (shard_mode == kShardLocal) {
@@ -2211,8 +2212,10 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         }
     });
     if (timing)
-        std::fprintf(stderr, "orbhip ba timing B=%d: prep %.3f ms, pack+upload %.3f ms, solve %.3f ms, outputs %.3f ms\n",
-                     B, t_prep - t_start, t_pack - t_prep, t_solve - t_pack, now() - t_solve);
+        std::fprintf(stderr,
+                     "orbhip ba timing B=%d: prep %.3f ms (problem structure %.3f), pack+upload %.3f ms, solve %.3f ms, "
+                     "outputs %.3f ms\n",
+                     B, t_prep - t_start, t_prepare - t_start, t_pack - t_prep, t_solve - t_pack, now() - t_solve);
     return ORBHIP_OK;
 }
 
