@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-extra", action="store_true", help="skip the C3 / LBA extra lines")
     ap.add_argument("--c3-steps", type=int, default=10)
-    ap.add_argument("--c3-inflight", type=int, default=4,
+    ap.add_argument("--c3-inflight", type=int, default=8,
                     help="C3 batches in flight (each its own context and stream)")
     ap.add_argument("--lba-steps", type=int, default=20)
     ap.add_argument("--lba-batch", type=int, default=256)
