@@ -121,7 +121,7 @@ __device__ __forceinline__ bool last_arrival(int* counter, int total, int* sh_fl
     return *sh_flag != 0;
 }
 __device__ void ctl_end_body(const BaArgs& a, int prob, int* done_flags, double* sh);
-__device__ void ctl_begin_body(const BaArgs& a, int nlin);
+__device__ void ctl_begin_body(const BaArgs& a, int nlin, int* done_flags, int prob);
 
 // ---------------------------------------------------------------------------
 // errors (when: 0 always, 1 the build's stale-error refresh, 2 a trial's new state); a trial also
@@ -163,9 +163,29 @@ __device__ __forceinline__ double edge_error(const BaArgs& a, int e) {
 // on the iteration budget or the (host-relayed) stop flag (done[b], host-mapped: the host stops
 // queueing slots once every problem is done). Every workgroup derives the same effective phase
 // from the controller's fields, so none depends on that transition's store.
+// host-mapped words of a device-driven solve, reached through a device-resident pointer pair
+// donep = {done, hstop}: done[prob] is set once when the problem's LM run ends (the host stops
+// queueing slots once all are set); *hstop is the caller's stop flag as the host relays it while
+// it waits (null for sharded solves, whose shards must take the same decisions: they get the
+// stop between batches of slots). A store to host memory in every trial put ~5 us in front of
+// the next kernel, so the done words are written once per solve and the stop word only read.
+__device__ __forceinline__ void post_done(int* done, int prob) {
+    if (done) __hip_atomic_store(done + prob, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ int* done_of(int* const* donep) { return donep ? donep[0] : nullptr; }
+// The stop word is read over PCIe (~2 us) by an extra workgroup of k_ba_schur_items, off every
+// critical path (a read in the controller's tail, or early in a working wave, delays the kernel:
+// vmcnt waits in order), and copied into LmCtl::stop, which the controller checks at its trial end
+// (this slot) and at the next iteration's start.
+__device__ __forceinline__ void relay_host_stop(LmCtl* c, int* const* donep) {
+    const int* hstop = donep ? donep[1] : nullptr;
+    if (c && hstop && __hip_atomic_load(hstop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) c->stop = 1;
+}
+
 __global__ __launch_bounds__(256) void k_ba_errors(const BaArgs* __restrict__ args, const int* __restrict__ act,
-                                                   int when, int* done) {
+                                                   int when, int* const* donep) {
     BA_PROLOGUE
+    int* const done = done_of(donep);
     if (when == 1) {
         LmCtl* c = a.ctl;
         const bool ends = c && c->phase == kPhBuild && (c->stop || c->it >= c->iterations);
@@ -173,7 +193,7 @@ __global__ __launch_bounds__(256) void k_ba_errors(const BaArgs* __restrict__ ar
             c->pop = 0;
             if (ends) {
                 c->phase = kPhDone;
-                if (done) __hip_atomic_store(done + act[by_], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                post_done(done, act[by_]);
             }
         }
         if (ends || !(in_phase(a, kPhBuild) && (!c || !c->errors_valid))) return;
@@ -367,7 +387,7 @@ __global__ __launch_bounds__(256) void k_ba_lin_poses(const BaArgs* __restrict__
 // problem's last workgroup runs the controller's trial start (ctl_begin_body: lambda from the
 // maxima on the first iteration)
 __global__ __launch_bounds__(256) void k_ba_lin(const BaArgs* __restrict__ args, const int* __restrict__ act,
-                                               int nbp) {
+                                               int nbp, int* const* donep) {
     BA_PROLOGUE
     BA_PHASE(kPhBuild)
     __shared__ double sh[4];
@@ -393,7 +413,8 @@ __global__ __launch_bounds__(256) void k_ba_lin(const BaArgs* __restrict__ args,
         for (int w = 0; w < (int)(blockDim.x >> 6); w++) m = fmax(m, sh[w]);
         st_agent(a.part + slot, m);
     }
-    if (!a.sync && last_arrival(&a.ctl->arrive_b, gridDim.x, &lastf)) ctl_begin_body(a, mP + nP);
+    if (!a.sync && last_arrival(&a.ctl->arrive_b, gridDim.x, &lastf))
+        ctl_begin_body(a, mP + nP, done_of(donep), act[by_]);
 }
 
 // ---------------------------------------------------------------------------
@@ -464,9 +485,13 @@ __device__ __forceinline__ void schur_b_pose(const BaArgs& a, int i, int lane);
 // work-groups [nbi, gridDim.x) run k_ba_schur_b's poses instead (it reads only k_ba_schur_points'
 // db and the linearisation: no dependence on the items, one launch less per trial)
 __global__ __launch_bounds__(256) void k_ba_schur_items(const BaArgs* __restrict__ args, const int* __restrict__ act,
-                                                        int nbi) {
+                                                        int nbi, int* const* donep) {
     BA_PROLOGUE
     BA_PHASE(kPhTrial)
+    if (donep && bx_ == (int)gridDim.x - 1) {   // the extra workgroup: the relayed stop flag
+        if (threadIdx.x == 0) relay_host_stop(a.ctl, donep);
+        return;
+    }
     if (bx_ >= nbi) {
         schur_b_pose(a, (bx_ - nbi) * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
         return;
@@ -911,8 +936,9 @@ __global__ __launch_bounds__(256) void k_ba_backsub(const BaArgs* __restrict__ a
 // (ctl_end_body: commit the poses or take the points back)
 constexpr int kFusedMaxP = 512;
 __global__ __launch_bounds__(256) void k_ba_backsub_errs(const BaArgs* __restrict__ args, const int* __restrict__ act,
-                                                         int* done) {
+                                                         int* const* donep) {
     BA_PROLOGUE
+    int* const done = done_of(donep);
     BA_PHASE(kPhTrial)
     __shared__ double Tn[8 * kFusedMaxP];   // the trial's poses
     __shared__ double Xn[3 * 256];          // this workgroup's new points
@@ -1078,13 +1104,14 @@ __global__ __launch_bounds__(1024) void k_ba_ctl_init(const BaArgs* __restrict__
 
 // the host's stop request (LocalMapping mbAbortBA): a problem between iterations ends now, one in a
 // trial at the end of its iteration (ctl_end_decide)
-__global__ void k_ba_ctl_stop(LmCtl* __restrict__ ctl, int B, int* done) {
+__global__ void k_ba_ctl_stop(LmCtl* __restrict__ ctl, int B, int* const* donep) {
+    int* const done = done_of(donep);
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     ctl[b].stop = 1;
     if (ctl[b].phase == kPhBuild) {
         ctl[b].phase = kPhDone;
-        if (done) __hip_atomic_store(done + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        post_done(done, b);
     }
 }
 
@@ -1101,8 +1128,14 @@ __device__ void ctl_begin_apply(const BaArgs& a, double maxdiag) {
     c.rho = 0;
     c.phase = kPhTrial;
 }
-__device__ void ctl_begin_body(const BaArgs& a, int nlin) {
+__device__ void ctl_begin_body(const BaArgs& a, int nlin, int* done_flags, int prob) {
     if (threadIdx.x != 0) return;
+    if (a.ctl->stop) {   // a stop relayed before this iteration: g2o's terminate() check, no trial
+        LmCtl& c = *a.ctl;
+        c.phase = kPhDone;
+        post_done(done_flags, prob);
+        return;
+    }
     double m = 0.0;
     if (a.ctl->it == 0)
         for (int i = 0; i < nlin; i++) m = fmax(m, ld_agent(a.part + i));
@@ -1160,7 +1193,7 @@ __device__ void ctl_end_decide(const BaArgs& a, int prob, int* done_flags) {
     if (c.early_stop && c.nBad >= 3) done = true;
     if (c.it >= c.iterations) done = true;   // the budget (checked by k_ba_errors(1) too), no idle slot
     c.phase = done ? kPhDone : kPhBuild;
-    if (done && done_flags) __hip_atomic_store(done_flags + prob, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (done) post_done(done_flags, prob);
 }
 __device__ void ctl_end_body(const BaArgs& a, int prob, int* done_flags, double* sh) {
     ctl_end_sums(a, sh);
@@ -1219,7 +1252,8 @@ __global__ __launch_bounds__(1024) void k_ba_sh_sums(const BaArgs* __restrict__ 
     const BaArgs& a = args[act[blockIdx.x]];
     if (in_phase(a, kPhTrial)) ctl_end_sums(a, sh);
 }
-__global__ void k_ba_sh_end(const BaArgs* __restrict__ args, const int* __restrict__ act, int* done) {
+__global__ void k_ba_sh_end(const BaArgs* __restrict__ args, const int* __restrict__ act, int* const* donep) {
+    int* const done = done_of(donep);
     const BaArgs& a = args[act[blockIdx.x]];
     if (threadIdx.x == 0 && in_phase(a, kPhTrial)) ctl_end_decide(a, act[blockIdx.x], done);
 }
@@ -1311,41 +1345,56 @@ int prepare(const orbhip_ba_problem* pr, Prep& o, int chunk) {
     for (int i = 0; i < np; i++) o.ps_ptr[i + 1] += o.ps_ptr[i];
     o.pt_edges.resize(E);
     o.ps_edges.resize(o.ps_ptr[np]);
+    // scratch kept per host thread across calls (no page faults on the hot path): eopt[k] = the opt
+    // index of the pose of landmark-CSR slot k (one load per pair endpoint below), cnt = the dense
+    // (i, j) pair counts, then the blocks' fill cursors
+    static thread_local std::vector<int> eopt, cnt;
+    eopt.resize(E);
     {
         std::vector<int> fp(o.pt_ptr.begin(), o.pt_ptr.end() - 1), fq(o.ps_ptr.begin(), o.ps_ptr.end() - 1);
         for (int e = 0; e < E; e++) {
-            o.pt_edges[fp[e_pt[e]]++] = e;
             const int oi = o.opt[e_pose[e]];
+            const int k = fp[e_pt[e]]++;
+            o.pt_edges[k] = e;
+            eopt[k] = oi;
             if (oi >= 0) o.ps_edges[fq[oi]++] = e;
         }
     }
     // Schur pairs (a, b) of one landmark with opt(a) <= opt(b), grouped by block (i, j) with a
     // counting sort on the dense block id i*np + j; within a block: landmark order (deterministic).
-    std::vector<int> cnt((size_t)np * np, 0);
+    cnt.assign((size_t)np * np, 0);
     size_t npairs = 0;
-    for (int m = 0; m < M; m++)
-        for (int ka = o.pt_ptr[m]; ka < o.pt_ptr[m + 1]; ka++) {
-            const int ia = o.opt[e_pose[o.pt_edges[ka]]];
+    for (int m = 0; m < M; m++) {
+        const int k0 = o.pt_ptr[m], k1 = o.pt_ptr[m + 1];
+        for (int ka = k0; ka < k1; ka++) {
+            const int ia = eopt[ka];
             if (ia < 0) continue;
-            for (int kb = o.pt_ptr[m]; kb < o.pt_ptr[m + 1]; kb++) {
-                const int ib = o.opt[e_pose[o.pt_edges[kb]]];
-                if (ib < 0 || ib < ia) continue;
-                cnt[(size_t)ia * np + ib]++;
+            int* row = cnt.data() + (size_t)ia * np;
+            for (int kb = k0; kb < k1; kb++) {
+                const int ib = eopt[kb];
+                if (ib < ia) continue;   // also drops the fixed poses (-1)
+                row[ib]++;
                 npairs++;
             }
         }
-    std::vector<int> bid((size_t)np * np, -1);
+    }
     o.blk_ptr.assign(1, 0);
-    for (int i = 0; i < np; i++)
-        for (int j = i; j < np; j++) {
-            const size_t k = (size_t)i * np + j;
-            if (i == j || cnt[k] > 0) {
-                bid[k] = (int)o.blk_i.size();
-                o.blk_i.push_back(i);
-                o.blk_j.push_back(j);
-                o.blk_ptr.push_back(o.blk_ptr.back() + cnt[k]);
+    {
+        int s = 0;
+        for (int i = 0; i < np; i++) {
+            int* row = cnt.data() + (size_t)i * np;
+            for (int j = i; j < np; j++) {
+                const int c = row[j];
+                if (i == j || c > 0) {
+                    o.blk_i.push_back(i);
+                    o.blk_j.push_back(j);
+                    row[j] = s;   // from here on: the block's fill cursor
+                    s += c;
+                    o.blk_ptr.push_back(s);
+                }
             }
         }
+    }
     o.nblk = (int)o.blk_i.size();
     {   // envelope of S: first pose column coupled to each pose row (blocks are stored i <= j)
         std::vector<int> fp(np);
@@ -1375,19 +1424,23 @@ int prepare(const orbhip_ba_problem* pr, Prep& o, int chunk) {
         o.nslot += nch;
     }
     o.blk_pairs.resize(2 * npairs);
-    std::vector<int> fill(o.blk_ptr.begin(), o.blk_ptr.end() - 1);
-    for (int m = 0; m < M; m++)
-        for (int ka = o.pt_ptr[m]; ka < o.pt_ptr[m + 1]; ka++) {
-            const int ea = o.pt_edges[ka], ia = o.opt[e_pose[ea]];
+    int* bp = o.blk_pairs.data();
+    for (int m = 0; m < M; m++) {
+        const int k0 = o.pt_ptr[m], k1 = o.pt_ptr[m + 1];
+        for (int ka = k0; ka < k1; ka++) {
+            const int ia = eopt[ka];
             if (ia < 0) continue;
-            for (int kb = o.pt_ptr[m]; kb < o.pt_ptr[m + 1]; kb++) {
-                const int eb = o.pt_edges[kb], ib = o.opt[e_pose[eb]];
-                if (ib < 0 || ib < ia) continue;
-                const int slot = fill[bid[(size_t)ia * np + ib]]++;
-                o.blk_pairs[2 * slot] = ea;
-                o.blk_pairs[2 * slot + 1] = eb;
+            const int ea = o.pt_edges[ka];
+            int* row = cnt.data() + (size_t)ia * np;
+            for (int kb = k0; kb < k1; kb++) {
+                const int ib = eopt[kb];
+                if (ib < ia) continue;
+                const int slot = row[ib]++;
+                bp[2 * (size_t)slot] = ea;
+                bp[2 * (size_t)slot + 1] = o.pt_edges[kb];
             }
         }
+    }
     return ORBHIP_OK;
 }
 
@@ -1476,6 +1529,7 @@ struct BaWorkspace {
     int* h_stop = nullptr;     // pinned
     int* h_done = nullptr;     // pinned, mapped: per problem, set by the device when its LM run ends
     int* d_done = nullptr;     // its device address
+    DBuf<int*> d_donep;        // ... stored in device memory: what the kernels get
     size_t done_cap = 0;
     HBuf<int> hto;             // pinned: the persistent solver's hand-off timeout count per problem
     long long dag_timeouts = 0, dag_reruns = 0;
@@ -2023,10 +2077,27 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             for (int b = 0; b < B; b++) ha[b].fused = 1;
             BAOK(hipMemcpyAsync(ws->args.p, ha, B * sizeof(BaArgs), hipMemcpyHostToDevice, st));
         }
+        // the host-mapped words (post_done): B done flags, then the relayed stop flag. The kernels
+        // get them through a device-resident pointer pair: {done, stop} for a solve of its own,
+        // {done, null} for a sharded one (its shards agree on the stop between batches)
+        if (ws->done_cap < (size_t)B) {
+            if (ws->h_done) (void)hipHostFree(ws->h_done);
+            ws->h_done = nullptr; ws->d_done = nullptr; ws->done_cap = 0;
+            BAOK(hipHostMalloc((void**)&ws->h_done, sizeof(int) * (B + 1), hipHostMallocMapped | hipHostMallocCoherent));
+            BAOK(hipHostGetDevicePointer((void**)&ws->d_done, ws->h_done, 0));
+            int* const ptrs[4] = {ws->d_done, ws->d_done + B, ws->d_done, nullptr};
+            BAOK(ws->d_donep.ensure(4));
+            BAOK(hipMemcpy(ws->d_donep.p, ptrs, sizeof(ptrs), hipMemcpyHostToDevice));
+            ws->done_cap = B;
+        }
+        int* const* const donep = ws->d_donep.p + (sharded ? 2 : 0);
+        int* const h_stopw = sharded ? nullptr : ws->h_done + ws->done_cap;
+        for (int b = 0; b < B; b++) __atomic_store_n(ws->h_done + b, probs[b]->iterations > 0 ? 0 : 1, __ATOMIC_RELAXED);
+        __atomic_store_n(ws->h_done + ws->done_cap, 0, __ATOMIC_RELAXED);
         auto slot = [&]() -> int {
-            if (!all_small) hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 1, ws->d_done);
+            if (!all_small) hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 1, donep);
             hipLaunchKernelGGL(k_ba_lin, dim3(gx(maxM, 256) + gx(maxNp, 4), B), b256, 0, st, dA, d_act,
-                               (int)gx(maxM, 256));
+                               (int)gx(maxM, 256), donep);
             if (sharded) {   // the trial start on the shards' sums: Hpp, then the largest diagonal
                 if (coll(kHpp)) return ORBHIP_ERR_DEVICE;
                 hipLaunchKernelGGL(k_ba_sh_maxdiag, dim3(B), b256, 0, st, dA, d_act);
@@ -2035,8 +2106,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             }
             if (!s_readonly) hipLaunchKernelGGL(k_ba_zero_s, dim3(64, B), b256, 0, st, dA, d_act, 0);
             if (!fused) hipLaunchKernelGGL(k_ba_schur_points, dim3(gx(maxM, 256), B), b256, 0, st, dA, d_act);
-            hipLaunchKernelGGL(k_ba_schur_items, dim3(gx(2 * maxItems, 256) + gx(maxNp, 4), B), b256, 0, st, dA, d_act,
-                               (int)gx(2 * maxItems, 256));
+            hipLaunchKernelGGL(k_ba_schur_items, dim3(gx(2 * maxItems, 256) + gx(maxNp, 4) + 1, B), b256, 0, st, dA,
+                               d_act, (int)gx(2 * maxItems, 256), donep);
             hipLaunchKernelGGL(k_ba_schur_fin, dim3(gx(maxFin, 4), B), b256, 0, st, dA, d_act);
             if (nd_sh) {   // each shard its segment; the separator system and x summed over the shards
                 for (int b = 0; b < B; b++) BAOK(nd_factor_assemble(ws->nds[b], st));
@@ -2056,15 +2127,15 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                     if (large(b) && large_solve(b, &dctl[b].phase)) return ORBHIP_ERR_DEVICE;
             }
             if (fused) {
-                hipLaunchKernelGGL(k_ba_backsub_errs, dim3(gbs, B), b256, 0, st, dA, d_act, ws->d_done);
+                hipLaunchKernelGGL(k_ba_backsub_errs, dim3(gbs, B), b256, 0, st, dA, d_act, donep);
             } else {
                 hipLaunchKernelGGL(k_ba_backsub, dim3(gx(std::max(maxM, maxP), 256), B), b256, 0, st, dA, d_act);
-                hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 2, ws->d_done);
+                hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 2, donep);
             }
             if (sharded) {   // the trial's end on the shards' sums of chi2 and the scale
                 hipLaunchKernelGGL(k_ba_sh_sums, dim3(B), dim3(1024), 0, st, dA, d_act);
                 if (coll(kRed01)) return ORBHIP_ERR_DEVICE;
-                hipLaunchKernelGGL(k_ba_sh_end, dim3(B), dim3(64), 0, st, dA, d_act, ws->d_done);
+                hipLaunchKernelGGL(k_ba_sh_end, dim3(B), dim3(64), 0, st, dA, d_act, donep);
             }
             int maxPM = 0;
             for (auto& p : pp) maxPM = std::max(maxPM, std::max(8 * p.P, 3 * p.M));
@@ -2072,35 +2143,40 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             BAOK(hipGetLastError());
             return ORBHIP_OK;
         };
-        // Pacing: at most two slots in flight, so a stop request reaches the device within about
-        // two trials (g2o checks its force-stop flag once per iteration). The host reads nothing
-        // through these events (the done flags are system-scope atomics, the LM state comes back
-        // through a copy and a stream synchronisation), so they skip the system-scope release: with
-        // it every slot boundary paid an L2 writeback, a ~6 us bubble before the next k_ba_lin.
+        // Slots go out in chunks of kChunk behind one event each (at most two chunks in flight):
+        // the host checks the done flags once per chunk, and while it waits it relays the caller's
+        // stop flag into the mapped word that every trial's Schur launch copies into the controller
+        // (relay_host_stop; checked at the trial's end and the next iteration's start: g2o's
+        // force-stop checks), so a stop takes effect within a trial or two however many slots are
+        // queued. r04: an event or a store to host memory between every two slots put a
+        // ~5 us bubble in front of every trial (the queue drains for the marker; the kernel that
+        // wrote host memory ends with a system-scope release).
+        constexpr int kChunk = 8;
+        int rc = ORBHIP_OK;
+        bool stop_sent = false;
         hipEvent_t ev[2];
         const unsigned evf = hipEventDisableTiming | hipEventDisableSystemFence;
         BAOK(hipEventCreateWithFlags(&ev[0], evf));
-        BAOK(hipEventCreateWithFlags(&ev[1], evf));
-        int rc = ORBHIP_OK;
-        bool stop_sent = false;
-        // done flags: a problem that ends early (rho == 0, 10 trials, _nBad) leaves the later
-        // slots empty; once every flag is set the host queues no further slot
-        if (ws->done_cap < (size_t)B) {
-            if (ws->h_done) (void)hipHostFree(ws->h_done);
-            ws->h_done = nullptr; ws->d_done = nullptr; ws->done_cap = 0;
-            BAOK(hipHostMalloc((void**)&ws->h_done, sizeof(int) * B, hipHostMallocMapped | hipHostMallocCoherent));
-            BAOK(hipHostGetDevicePointer((void**)&ws->d_done, ws->h_done, 0));
-            ws->done_cap = B;
-        }
-        for (int b = 0; b < B; b++) __atomic_store_n(ws->h_done + b, probs[b]->iterations > 0 ? 0 : 1, __ATOMIC_RELAXED);
+        if (hipEventCreateWithFlags(&ev[1], evf) != hipSuccess) { (void)hipEventDestroy(ev[0]); return ORBHIP_ERR_DEVICE; }
         auto all_done = [&] {
             for (int b = 0; b < B; b++)
                 if (!__atomic_load_n(ws->h_done + b, __ATOMIC_RELAXED)) return false;
             return true;
         };
+        auto relay_stop = [&] {
+            if (h_stopw && stop && *stop) __atomic_store_n(h_stopw, 1, __ATOMIC_RELAXED);
+        };
+        auto wait_ev = [&](hipEvent_t e) -> int {   // polls, relaying the stop flag
+            for (;;) {
+                const hipError_t q = hipEventQuery(e);
+                if (q == hipSuccess) return ORBHIP_OK;
+                if (q != hipErrorNotReady) return ORBHIP_ERR_DEVICE;
+                relay_stop();
+            }
+        };
         int remaining = 0;   // slots every unfinished problem still needs at least
         for (int b = 0; b < B; b++) remaining = std::max(remaining, probs[b]->iterations);
-        int nslot = 0;
+        int nchunk = 0;
         // ranks of an RCCL solve must enqueue the same slots (their collectives pair up): they look
         // at the stop flag only between batches, agreed by an all-reduce, and never end a batch on
         // the asynchronous done flags; the batch length comes from the LM state read back, which
@@ -2108,20 +2184,23 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         const bool rccl = shard_mode == kShardRccl;
         while (remaining > 0 && rc == ORBHIP_OK) {
             if (rccl && !stop_sent && stop_now()) {
-                hipLaunchKernelGGL(k_ba_ctl_stop, gB, b256, 0, st, dctl, B, ws->d_done);
+                hipLaunchKernelGGL(k_ba_ctl_stop, gB, b256, 0, st, dctl, B, donep);
                 stop_sent = true;
             }
-            for (int k = 0; k < remaining && rc == ORBHIP_OK; k++, nslot++) {
+            for (int k = 0; k < remaining && rc == ORBHIP_OK;) {
                 if (!rccl && !stop_sent && stop && *stop) {
-                    hipLaunchKernelGGL(k_ba_ctl_stop, gB, b256, 0, st, dctl, B, ws->d_done);
+                    hipLaunchKernelGGL(k_ba_ctl_stop, gB, b256, 0, st, dctl, B, donep);
                     stop_sent = true;
                 }
-                rc = slot();
-                if (rc == ORBHIP_OK && hipEventRecord(ev[nslot & 1], st) != hipSuccess) rc = ORBHIP_ERR_DEVICE;
-                if (rc == ORBHIP_OK && nslot >= 1 && hipEventSynchronize(ev[(nslot - 1) & 1]) != hipSuccess)
-                    rc = ORBHIP_ERR_DEVICE;
-                if (rc == ORBHIP_OK && !rccl && nslot >= 1 && all_done()) { nslot++; break; }
+                const int n = std::min(kChunk, remaining - k);
+                for (int j = 0; j < n && rc == ORBHIP_OK; j++) rc = slot();
+                k += n;
+                if (rc == ORBHIP_OK && hipEventRecord(ev[nchunk & 1], st) != hipSuccess) rc = ORBHIP_ERR_DEVICE;
+                if (rc != ORBHIP_OK) break;
+                if (nchunk++ >= 1) rc = wait_ev(ev[nchunk & 1]);   // the chunk before this one
+                if (rc == ORBHIP_OK && !rccl && all_done()) break;
             }
+            if (rc == ORBHIP_OK) rc = wait_ev(ev[(nchunk - 1) & 1]);
             if (rc != ORBHIP_OK) break;
             if (hipMemcpyAsync(ws->hctl.p, dctl, B * sizeof(LmCtl), hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess) {

@@ -87,6 +87,28 @@ def test_stop_flag_aborts(opt):
     assert r.iterations_done == 0
 
 
+def test_stop_flag_mid_solve(opt, oracle):
+    """A stop raised while the solve runs (LocalMapping's mbAbortBA): the host relays it into a
+    mapped word that the device controller reads at every iteration start and trial end, so the
+    run ends within a trial although all its slots are queued. The state it leaves is the oracle's
+    after the same number of iterations. C4 run to convergence takes 20 iterations / 38 trials
+    (~5 ms on the GPU); the flag goes up 1 ms in."""
+    import ctypes
+    import threading
+    prob, _ = synthetic_ba_problem()
+    prob.iterations = 400
+    flag = ctypes.c_int(0)
+    opt.solve(prob)   # warm: the timed call's workspace exists
+    timer = threading.Timer(0.001, lambda: setattr(flag, "value", 1))
+    timer.start()
+    g = opt.solve(prob, stop_flag=flag)
+    timer.join()
+    assert 0 < g.iterations_done < 20, g.iterations_done
+    prob.iterations = g.iterations_done
+    o = oracle.ba_solve(prob)
+    _compare(g, o, prob, exact_schedule=g.lm_trials == g.iterations_done)
+
+
 def test_batch_matches_single(opt, oracle):
     """orbhip_ba_solve_batch: 6 independent problems of different sizes; each equals its own
     oracle solve (per-problem LM schedules, shared launches)."""

@@ -214,6 +214,94 @@ static void rowwise(int P, int M, int E, const int* e_pose, const int* e_pt, con
     t[3] += now() - t0;
 }
 
+// serial2: the serial order with one load per pair endpoint (eopt: each pt_edges slot's opt
+// index, filled with the CSR) and the dense count array turned into the blocks' fill cursors
+// (no block-id array); scratch vectors kept across calls (as a workspace would)
+static void serial2(int P, int M, int E, const int* e_pose, const int* e_pt, const unsigned char* fixed, Out& o, double* t) {
+    double t0 = now();
+    static std::vector<int> eopt, cnt, fp;
+    o.opt.assign(P, -1);
+    int np = 0;
+    for (int i = 0; i < P; i++)
+        if (!fixed[i]) o.opt[i] = np++;
+    o.np = np;
+    o.pt_ptr.assign(M + 1, 0);
+    o.ps_ptr.assign(np + 1, 0);
+    for (int e = 0; e < E; e++) {
+        o.pt_ptr[e_pt[e] + 1]++;
+        if (o.opt[e_pose[e]] >= 0) o.ps_ptr[o.opt[e_pose[e]] + 1]++;
+    }
+    for (int m = 0; m < M; m++) o.pt_ptr[m + 1] += o.pt_ptr[m];
+    for (int i = 0; i < np; i++) o.ps_ptr[i + 1] += o.ps_ptr[i];
+    o.pt_edges.resize(E);
+    o.ps_edges.resize(o.ps_ptr[np]);
+    eopt.resize(E);
+    {
+        fp.assign(o.pt_ptr.begin(), o.pt_ptr.end() - 1);
+        std::vector<int> fq(o.ps_ptr.begin(), o.ps_ptr.end() - 1);
+        for (int e = 0; e < E; e++) {
+            const int oi = o.opt[e_pose[e]];
+            const int k = fp[e_pt[e]]++;
+            o.pt_edges[k] = e;
+            eopt[k] = oi;
+            if (oi >= 0) o.ps_edges[fq[oi]++] = e;
+        }
+    }
+    t[0] += now() - t0; t0 = now();
+    cnt.assign((size_t)np * np, 0);
+    size_t npairs = 0;
+    for (int m = 0; m < M; m++) {
+        const int k0 = o.pt_ptr[m], k1 = o.pt_ptr[m + 1];
+        for (int ka = k0; ka < k1; ka++) {
+            const int ia = eopt[ka];
+            if (ia < 0) continue;
+            int* row = cnt.data() + (size_t)ia * np;
+            for (int kb = k0; kb < k1; kb++) {
+                const int ib = eopt[kb];
+                if (ib < ia) continue;
+                row[ib]++;
+                npairs++;
+            }
+        }
+    }
+    t[1] += now() - t0; t0 = now();
+    o.blk_ptr.assign(1, 0);
+    int s = 0;
+    for (int i = 0; i < np; i++) {
+        int* row = cnt.data() + (size_t)i * np;
+        for (int j = i; j < np; j++) {
+            const int c = row[j];
+            if (i == j || c > 0) {
+                o.blk_i.push_back(i);
+                o.blk_j.push_back(j);
+                row[j] = s;   // the block's fill cursor
+                s += c;
+                o.blk_ptr.push_back(s);
+            }
+        }
+    }
+    t[2] += now() - t0; t0 = now();
+    o.blk_pairs.resize(2 * npairs);
+    int* bp = o.blk_pairs.data();
+    for (int m = 0; m < M; m++) {
+        const int k0 = o.pt_ptr[m], k1 = o.pt_ptr[m + 1];
+        for (int ka = k0; ka < k1; ka++) {
+            const int ia = eopt[ka];
+            if (ia < 0) continue;
+            const int ea = o.pt_edges[ka];
+            int* row = cnt.data() + (size_t)ia * np;
+            for (int kb = k0; kb < k1; kb++) {
+                const int ib = eopt[kb];
+                if (ib < ia) continue;
+                const int slot = row[ib]++;
+                bp[2 * slot] = ea;
+                bp[2 * slot + 1] = o.pt_edges[kb];
+            }
+        }
+    }
+    t[3] += now() - t0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 4) return 1;
     auto a = slurp(argv[1]), b = slurp(argv[2]), c = slurp(argv[3]);
@@ -228,6 +316,11 @@ int main(int argc, char** argv) {
     const int R = 20;
     for (int r = 0; r < R; r++) { o1 = Out(); serial(P, M, E, ep, et, (const unsigned char*)c.data(), o1, ts); }
     for (int r = 0; r < R; r++) { o2 = Out(); rowwise(P, M, E, ep, et, (const unsigned char*)c.data(), o2, tt, nth); }
+    Out o3;
+    double t3[4] = {0};
+    for (int r = 0; r < R; r++) { o3.blk_i.clear(); o3.blk_j.clear(); serial2(P, M, E, ep, et, (const unsigned char*)c.data(), o3, t3); }
+    const bool same3 = o1.blk_i == o3.blk_i && o1.blk_j == o3.blk_j && o1.blk_ptr == o3.blk_ptr && o1.blk_pairs == o3.blk_pairs && o1.pt_edges == o3.pt_edges && o1.ps_edges == o3.ps_edges;
+    std::printf("serial2  ms: csr %.3f count %.3f blocks %.3f fill %.3f total %.3f identical=%d\n", t3[0] / R, t3[1] / R, t3[2] / R, t3[3] / R, (t3[0] + t3[1] + t3[2] + t3[3]) / R, same3);
     const bool same = o1.blk_i == o2.blk_i && o1.blk_j == o2.blk_j && o1.blk_ptr == o2.blk_ptr &&
                       o1.blk_pairs == o2.blk_pairs && o1.pt_edges == o2.pt_edges && o1.ps_edges == o2.ps_edges;
     std::printf("P=%d M=%d E=%d blocks=%zu pairs=%zu identical=%d\n", P, M, E, o1.blk_i.size(), o1.blk_pairs.size() / 2, same);
