@@ -1,8 +1,9 @@
 // CPU microbenchmark of the BA host preparation's structure build (ba_solver.hip prepare()):
-// the serial form (the one ba_solver.hip keeps) against a row-wise form (each pose row builds its
-// own blocks and pairs in a few KB), on edge lists dumped from synthetic_ba_problem (C4 / C5).
-// Checks that both produce identical lists. r04: the row-wise form is ~1.8x slower single-threaded
-// (every landmark's edge list walked once per pose row it touches, plus the row lists' build).
+// the r03 serial form, a row-wise form (each pose row builds its own blocks and pairs in a few KB)
+// and serial2 (the form ba_solver.hip now has: one load per pair endpoint, the dense counts turned
+// into fill cursors in place, scratch kept across calls), on edge lists dumped from
+// synthetic_ba_problem (C4 / C5). Checks that all produce identical lists. r04 on this
+// container's CPU: serial 3.1-3.7 ms, row-wise ~1.8x slower, serial2 2.2-2.3 ms at C5.
 //   g++ -O2 -std=c++17 -pthread tools/ubench/ba_prep.cpp -o /tmp/ba_prep && /tmp/ba_prep ep.bin et.bin fx.bin
 #include <algorithm>
 #include <atomic>
