@@ -177,9 +177,15 @@ __device__ __forceinline__ int* done_of(int* const* donep) { return donep ? done
 // critical path (a read in the controller's tail, or early in a working wave, delays the kernel:
 // vmcnt waits in order), and copied into LmCtl::stop, which the controller checks at its trial end
 // (this slot) and at the next iteration's start.
-__device__ __forceinline__ void relay_host_stop(LmCtl* c, int* const* donep) {
+// One read per slot (problem row 0's extra workgroup), fanned out to every problem of the launch:
+// a read per problem put 256 same-address PCIe reads into every batched slot.
+__device__ __forceinline__ void relay_host_stop(const BaArgs* args, const int* act, int* const* donep) {
     const int* hstop = donep ? donep[1] : nullptr;
-    if (c && hstop && __hip_atomic_load(hstop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) c->stop = 1;
+    if (!hstop || __hip_atomic_load(hstop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) return;
+    for (int b = 0; b < (int)gridDim.y; b++) {
+        LmCtl* c = args[act[b]].ctl;
+        if (c) c->stop = 1;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_ba_errors(const BaArgs* __restrict__ args, const int* __restrict__ act,
@@ -487,11 +493,11 @@ __device__ __forceinline__ void schur_b_pose(const BaArgs& a, int i, int lane);
 __global__ __launch_bounds__(256) void k_ba_schur_items(const BaArgs* __restrict__ args, const int* __restrict__ act,
                                                         int nbi, int* const* donep) {
     BA_PROLOGUE
-    BA_PHASE(kPhTrial)
     if (donep && bx_ == (int)gridDim.x - 1) {   // the extra workgroup: the relayed stop flag
-        if (threadIdx.x == 0) relay_host_stop(a.ctl, donep);
+        if (by_ == 0 && threadIdx.x == 0) relay_host_stop(args, act, donep);
         return;
     }
+    BA_PHASE(kPhTrial)
     if (bx_ >= nbi) {
         schur_b_pose(a, (bx_ - nbi) * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
         return;
@@ -2090,8 +2096,9 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             BAOK(hipMemcpy(ws->d_donep.p, ptrs, sizeof(ptrs), hipMemcpyHostToDevice));
             ws->done_cap = B;
         }
-        int* const* const donep = ws->d_donep.p + (sharded ? 2 : 0);
-        int* const h_stopw = sharded ? nullptr : ws->h_done + ws->done_cap;
+        const bool relay = !sharded && stop;   // a caller's stop flag to relay mid-solve
+        int* const* const donep = ws->d_donep.p + (relay ? 0 : 2);
+        int* const h_stopw = relay ? ws->h_done + ws->done_cap : nullptr;
         for (int b = 0; b < B; b++) __atomic_store_n(ws->h_done + b, probs[b]->iterations > 0 ? 0 : 1, __ATOMIC_RELAXED);
         __atomic_store_n(ws->h_done + ws->done_cap, 0, __ATOMIC_RELAXED);
         auto slot = [&]() -> int {
