@@ -2,8 +2,10 @@
 // the r03 serial form, a row-wise form (each pose row builds its own blocks and pairs in a few KB)
 // and serial2 (the form ba_solver.hip now has: one load per pair endpoint, the dense counts turned
 // into fill cursors in place, scratch kept across calls), on edge lists dumped from
-// synthetic_ba_problem (C4 / C5). Checks that all produce identical lists. r04 on this
-// container's CPU: serial 3.1-3.7 ms, row-wise ~1.8x slower, serial2 2.2-2.3 ms at C5.
+// synthetic_ba_problem (C4 / C5), and serial3 (serial2's pair passes over T landmark ranges on
+// T threads). Checks that all produce identical lists. r04 on this container's CPU at C5: serial
+// 3.1-3.7 ms, row-wise ~1.8x slower, serial2 1.9-2.3 ms, serial3 2.4 (T=2) / 2.8 (T=4): the
+// threads' start-up and the T dense count arrays cost more than the split passes save.
 //   g++ -O2 -std=c++17 -pthread tools/ubench/ba_prep.cpp -o /tmp/ba_prep && /tmp/ba_prep ep.bin et.bin fx.bin
 #include <algorithm>
 #include <atomic>
@@ -303,6 +305,120 @@ static void serial2(int P, int M, int E, const int* e_pose, const int* e_pt, con
     t[3] += now() - t0;
 }
 
+// serial3: serial2 with the two pair passes split over T contiguous landmark ranges (T count
+// arrays; a block's pairs from range t follow those of ranges < t, so the lists stay identical)
+static void serial3(int P, int M, int E, const int* e_pose, const int* e_pt, const unsigned char* fixed, Out& o, double* t,
+                    int T) {
+    double t0 = now();
+    static std::vector<int> eopt;
+    static std::vector<std::vector<int>> cnts;
+    o.opt.assign(P, -1);
+    int np = 0;
+    for (int i = 0; i < P; i++)
+        if (!fixed[i]) o.opt[i] = np++;
+    o.np = np;
+    o.pt_ptr.assign(M + 1, 0);
+    o.ps_ptr.assign(np + 1, 0);
+    for (int e = 0; e < E; e++) {
+        o.pt_ptr[e_pt[e] + 1]++;
+        if (o.opt[e_pose[e]] >= 0) o.ps_ptr[o.opt[e_pose[e]] + 1]++;
+    }
+    for (int m = 0; m < M; m++) o.pt_ptr[m + 1] += o.pt_ptr[m];
+    for (int i = 0; i < np; i++) o.ps_ptr[i + 1] += o.ps_ptr[i];
+    o.pt_edges.resize(E);
+    o.ps_edges.resize(o.ps_ptr[np]);
+    eopt.resize(E);
+    {
+        std::vector<int> fp(o.pt_ptr.begin(), o.pt_ptr.end() - 1), fq(o.ps_ptr.begin(), o.ps_ptr.end() - 1);
+        for (int e = 0; e < E; e++) {
+            const int oi = o.opt[e_pose[e]];
+            const int k = fp[e_pt[e]]++;
+            o.pt_edges[k] = e;
+            eopt[k] = oi;
+            if (oi >= 0) o.ps_edges[fq[oi]++] = e;
+        }
+    }
+    t[0] += now() - t0; t0 = now();
+    if ((int)cnts.size() < T) cnts.resize(T);
+    std::vector<size_t> npr(T, 0);
+    auto range = [&](int q) { return std::make_pair((int)((long long)M * q / T), (int)((long long)M * (q + 1) / T)); };
+    auto count = [&](int q) {
+        std::vector<int>& cnt = cnts[q];
+        cnt.assign((size_t)np * np, 0);
+        size_t n = 0;
+        const auto [m0, m1] = range(q);
+        for (int m = m0; m < m1; m++) {
+            const int k0 = o.pt_ptr[m], k1 = o.pt_ptr[m + 1];
+            for (int ka = k0; ka < k1; ka++) {
+                const int ia = eopt[ka];
+                if (ia < 0) continue;
+                int* row = cnt.data() + (size_t)ia * np;
+                for (int kb = k0; kb < k1; kb++) {
+                    const int ib = eopt[kb];
+                    if (ib < ia) continue;
+                    row[ib]++;
+                    n++;
+                }
+            }
+        }
+        npr[q] = n;
+    };
+    {
+        std::vector<std::thread> th;
+        for (int q = 1; q < T; q++) th.emplace_back(count, q);
+        count(0);
+        for (auto& x : th) x.join();
+    }
+    size_t npairs = 0;
+    for (int q = 0; q < T; q++) npairs += npr[q];
+    t[1] += now() - t0; t0 = now();
+    o.blk_ptr.assign(1, 0);
+    int s = 0;
+    for (int i = 0; i < np; i++) {
+        for (int j = i; j < np; j++) {
+            const size_t k = (size_t)i * np + j;
+            int c = 0;
+            for (int q = 0; q < T; q++) c += cnts[q][k];
+            if (i == j || c > 0) {
+                o.blk_i.push_back(i);
+                o.blk_j.push_back(j);
+                for (int q = 0; q < T; q++) { const int v = cnts[q][k]; cnts[q][k] = s; s += v; }
+                o.blk_ptr.push_back(s);
+            }
+        }
+    }
+    t[2] += now() - t0; t0 = now();
+    o.blk_pairs.resize(2 * npairs);
+    int* bp = o.blk_pairs.data();
+    auto fill = [&](int q) {
+        std::vector<int>& cur = cnts[q];
+        const auto [m0, m1] = range(q);
+        for (int m = m0; m < m1; m++) {
+            const int k0 = o.pt_ptr[m], k1 = o.pt_ptr[m + 1];
+            for (int ka = k0; ka < k1; ka++) {
+                const int ia = eopt[ka];
+                if (ia < 0) continue;
+                const int ea = o.pt_edges[ka];
+                int* row = cur.data() + (size_t)ia * np;
+                for (int kb = k0; kb < k1; kb++) {
+                    const int ib = eopt[kb];
+                    if (ib < ia) continue;
+                    const int slot = row[ib]++;
+                    bp[2 * (size_t)slot] = ea;
+                    bp[2 * (size_t)slot + 1] = o.pt_edges[kb];
+                }
+            }
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int q = 1; q < T; q++) th.emplace_back(fill, q);
+        fill(0);
+        for (auto& x : th) x.join();
+    }
+    t[3] += now() - t0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 4) return 1;
     auto a = slurp(argv[1]), b = slurp(argv[2]), c = slurp(argv[3]);
@@ -321,6 +437,13 @@ int main(int argc, char** argv) {
     double t3[4] = {0};
     for (int r = 0; r < R; r++) { o3.blk_i.clear(); o3.blk_j.clear(); serial2(P, M, E, ep, et, (const unsigned char*)c.data(), o3, t3); }
     const bool same3 = o1.blk_i == o3.blk_i && o1.blk_j == o3.blk_j && o1.blk_ptr == o3.blk_ptr && o1.blk_pairs == o3.blk_pairs && o1.pt_edges == o3.pt_edges && o1.ps_edges == o3.ps_edges;
+    for (int T : {2, 4}) {
+        Out o4;
+        double t4[4] = {0};
+        for (int r = 0; r < R; r++) { o4.blk_i.clear(); o4.blk_j.clear(); serial3(P, M, E, ep, et, (const unsigned char*)c.data(), o4, t4, T); }
+        const bool same4 = o1.blk_i == o4.blk_i && o1.blk_j == o4.blk_j && o1.blk_ptr == o4.blk_ptr && o1.blk_pairs == o4.blk_pairs;
+        std::printf("serial3 T=%d ms: csr %.3f count %.3f blocks %.3f fill %.3f total %.3f identical=%d\n", T, t4[0] / R, t4[1] / R, t4[2] / R, t4[3] / R, (t4[0] + t4[1] + t4[2] + t4[3]) / R, same4);
+    }
     std::printf("serial2  ms: csr %.3f count %.3f blocks %.3f fill %.3f total %.3f identical=%d\n", t3[0] / R, t3[1] / R, t3[2] / R, t3[3] / R, (t3[0] + t3[1] + t3[2] + t3[3]) / R, same3);
     const bool same = o1.blk_i == o2.blk_i && o1.blk_j == o2.blk_j && o1.blk_ptr == o2.blk_ptr &&
                       o1.blk_pairs == o2.blk_pairs && o1.pt_edges == o2.pt_edges && o1.ps_edges == o2.ps_edges;
