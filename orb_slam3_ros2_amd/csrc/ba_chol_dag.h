@@ -54,7 +54,13 @@ struct DagDev {
 // u64): the chain's shader-clock cycles: [0] prologue, [1] forward, [2] backward, [4] diag32 sum,
 // [5] total, then per interval k < 200 six words at 8 + 6k: the interval, phase 1, phase 2, and in
 // phase 3 wave 0 (diag32), wave 1 (publish + next diagonal partial), waves 2/3 (the next tiles).
-constexpr int kDbgWords = 8 + 6 * 200;
+// Then, for intervals k < kDbgSubK, 16 sub-phase stamps at kDbgSubOff + 16k (cycles from the
+// interval start): wave 0 [0] diag part A done, [1] wave 1's D(1,*) in, [2] part B done; waves 2/3
+// (h = 0, 1) [4 + 4h] their global loads in, [5 + 4h] L(k+2, k) row formed, [6 + 4h] T / D' updates
+// done, [7 + 4h] rows of L(k+1, k) in.
+constexpr int kDbgSubK = 100;
+constexpr int kDbgSubOff = 8 + 6 * 200;
+constexpr int kDbgWords = kDbgSubOff + 16 * kDbgSubK;
 hipError_t chol_dag_solve(const double* S, int n, const int* row_first, const double* bs, double* x, int* flag,
                           const DagDev& d, hipStream_t st, const int* gate = nullptr,
                           unsigned long long* dbg = nullptr);

@@ -49,7 +49,10 @@ constexpr size_t kMinLds = 84 * 1024;   // > 80 KB: one workgroup per CU
 #ifndef ORBHIP_DAG_NEWTON
 #define ORBHIP_DAG_NEWTON 1
 #endif
-constexpr int kNewton = ORBHIP_DAG_NEWTON;   // Newton steps after v_rsq_f64 in the pivot blocks
+constexpr int kNewton = ORBHIP_DAG_NEWTON;   // Newton steps after v_rsq_f64 / v_rcp_f64 in the pivots
+#ifndef ORBHIP_DAG_DIAG_DPP
+#define ORBHIP_DAG_DIAG_DPP 1   // r05: the 16x16 diagonal factorizations by DPP elimination (diag16_dpp)
+#endif
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) int gint;
@@ -326,13 +329,14 @@ __device__ void dag_helper(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t r
     for (int t = t0; t < t1; t++) {
         const int code = a.tasks[t];
         const int R = code >> 16, C = code & 0xFFFF;
-        // by R - C: 0 the diagonal partial (columns <= C-3), 1 the sub-diagonal partial (<= C-3), 2
+        // by R - C: 0 the diagonal partial (columns <= C-4), 1 the sub-diagonal partial (<= C-3), 2
         // the second sub-diagonal's partial (<= C-2), >= 3 a full tile (every column, then the TRSM);
         // 3: a tile of a partial solve's trailing block (C >= nti): every column < nti, no TRSM
         const int dRC = R - C;
         const bool upd = a.nti && C >= a.nti;
         const int type = upd ? 3 : (dRC >= 3 ? 2 : (dRC == 0 ? 0 : 1));
-        const int ps = max(a.rf[R], a.rf[C]), pe = upd ? a.nti : (dRC >= 3 ? C : (dRC == 2 ? C - 1 : C - 2));
+        const int ps = max(a.rf[R], a.rf[C]),
+                  pe = upd ? a.nti : (dRC >= 3 ? C : (dRC == 2 ? C - 1 : (dRC == 1 ? C - 2 : C - 3)));
         double4_t acc = s_quad(a, R, C, rq, cq);
         const bool dg = type == 0 || (upd && dRC == 0);   // a diagonal tile: with its right-hand side
         const bool rhs = dg && cq == 0;
@@ -430,18 +434,49 @@ __device__ __forceinline__ void tile_lt_x(const double4_t* t, const double* x, d
 // (the diag32_linv steps of ba_diag16.h, with the second pivot's inputs handed in by wave 1):
 // part A: Linv11 of D11 (registers, C layout) into quadrant 0 of Lq (and zeros into quadrant 1),
 // returns Linv11 in the C layout (lin11)
-__device__ __forceinline__ bool diag_part_a(const double4_t& d11, double* Lq, double4_t& lin11) {
+#if ORBHIP_DAG_DIAG_DPP
+// D (C layout) -> v (column lane & 15, rows 0..15) through a padded column-major scratch (stride
+// 18 doubles: the 16 lanes' 16-byte reads start on distinct banks)
+__device__ __forceinline__ void c_to_cols(const double4_t& d, double* scr, double (&v)[16]) {
+    const int lane = threadIdx.x & 63, cc = lane & 15, rg = lane >> 4;
+#pragma unroll
+    for (int q = 0; q < 4; q++) scr[cc * 18 + rg + 4 * q] = d[q];
+    wave_lds_sync();
+    const double* p = scr + cc * 18;
+#pragma unroll
+    for (int i = 0; i < 16; i++) v[i] = p[i];
+    wave_lds_sync();
+}
+#endif
+// part A: Linv11 of D11 (registers, C layout) into quadrant 0 of Lq (and zeros into quadrant 1),
+// returns Linv11 in the C layout (lin11). scr: 288 doubles of wave-private LDS scratch.
+__device__ __forceinline__ bool diag_part_a(const double4_t& d11, double* Lq, double4_t& lin11, double* scr) {
+#if ORBHIP_DAG_DIAG_DPP
+    // DPP column elimination (ba_diag16.h, diag16_dpp), then the quadrant stores
+    const int lane = threadIdx.x & 63, cc = lane & 15, rg = lane >> 4;
+    double v[16];
+    c_to_cols(d11, scr, v);
+    const bool ok = diag16_dpp<kNewton>(v, lin11);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        Lq[qidx(rg + 4 * q, cc)] = lin11[q];
+        Lq[qidx(rg + 4 * q, 16 + cc)] = 0.0;
+    }
+    return ok;
+#else
+    (void)scr;
     return diag16_linv<kNewton>(d11, [&](int r, int c, double v) {
         Lq[qidx(r, c)] = v;
         Lq[qidx(r, 16 + c)] = 0.0;
         lin11[r >> 2] = v;
     });
+#endif
 }
 // part B: from D21^T (quadrant (1, 0) registers) and D22: L21 = D21 Linv11^T (returned as L21^T in
 // the C layout), D22 -= L21 L21^T, Linv22 into quadrant 3, Linv21 = -Linv22 L21 Linv11 into
 // quadrant 2
 __device__ __forceinline__ bool diag_part_b(const double4_t& d21t, double4_t d22, const double4_t& lin11, double* Lq,
-                                            double4_t& l21t) {
+                                            double4_t& l21t, double* scr) {
     const int lane = threadIdx.x & 63, cc = lane & 15, rg = lane >> 4;
     const double* a11 = Lq + lane * 4;   // quadrant 0 in operand order
     l21t = double4_t{0, 0, 0, 0};
@@ -450,7 +485,17 @@ __device__ __forceinline__ bool diag_part_b(const double4_t& d21t, double4_t d22
 #pragma unroll
     for (int kk = 0; kk < 4; kk++) d22 = __builtin_amdgcn_mfma_f64_16x16x4f64(-l21t[kk], l21t[kk], d22, 0, 0, 0);
     double* op22 = Lq + 3 * 256;
+#if ORBHIP_DAG_DIAG_DPP
+    double4_t l22;
+    double v[16];
+    c_to_cols(d22, scr, v);
+    const bool ok2 = diag16_dpp<kNewton>(v, l22);
+#pragma unroll
+    for (int q = 0; q < 4; q++) op22[(rg + 4 * q + 16 * (cc & 3)) * 4 + (cc >> 2)] = l22[q];
+#else
+    (void)scr;
     const bool ok2 = diag16_linv<kNewton>(d22, [&](int r, int c, double v) { op22[(r + 16 * (c & 3)) * 4 + (c >> 2)] = v; });
+#endif
     double4_t w = {0, 0, 0, 0};
 #pragma unroll
     for (int kk = 0; kk < 4; kk++) w = __builtin_amdgcn_mfma_f64_16x16x4f64(l21t[kk], lin11[kk], w, 0, 0, 0);
@@ -495,7 +540,8 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     //   [4096, 6144)   L2: L(k+1, k-1) / the new L(k+2, k)      (c2)
     //   [6144, 8192)   Tp: T_k, tile (k+1, k) with every column < k applied (parity)
     //   [8192, 10240)  Dp: D'_{k+1} (quadrants 0, 3: columns <= k-1 applied; 2: <= k-2) (parity)
-    //   [10240, 11264) Dq: D(1,0), D(1,1) of tile k+1, wave 1 -> wave 0 (quadrants 2, 3)
+    //   [10240, 11264) Dq: D(1,0), D(1,1) of tile k+1, wave 1 -> wave 0 (quadrants 2, 3); its first
+    //                  half: wave 0's transposition scratch [10240, 10528), debug stamps [10560, 10576)
     int* word = (int*)(lds + 11264);    // [4] abort, [5] row polls ok, [8] ok, [10..12] wave flags
     double* rvec = lds + 11280;         // 32: r0 (wave 0), r1 (wave 1 -> wave 0)
     double* rppB = rvec + 32;           // 2 x 32: rhs of D' (parity)
@@ -506,6 +552,8 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     int* F2 = word + 11;                // wave 1: D(1,0), D(1,1), r1 of tile k+1 ready
     int* F3 = word + 12;                // wave 1: row 1 of L(k+1, k) ready
     unsigned long long* wts = (unsigned long long*)(lds + 11264 + 8);   // per-wave cycles (dbg)
+    unsigned long long* stm = (unsigned long long*)(lds + 10560);       // sub-phase stamps (dbg), 16
+#define DAG_STAMP(i) do { if (dbg && lane == 0) stm[i] = __builtin_amdgcn_s_memtime() - tk; } while (0)
     unsigned long long* dbg = a.dbg;
     const unsigned long long t_start = dbg ? __builtin_amdgcn_s_memtime() : 0;
     unsigned long long t_fact = 0;
@@ -534,11 +582,11 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     __syncthreads();
     if (wid == 0) {
         double4_t lin11, l21t;
-        ok = diag_part_a(s_quad(a, 0, 0, 0, 0), lds, lin11);
+        ok = diag_part_a(s_quad(a, 0, 0, 0, 0), lds, lin11, lds + 10240);
         wave_lds_sync();
         const double y0 = quad_matvec(lds, 0, rvec);
         if (rg == 0) ys[cc] = y0;
-        ok = diag_part_b(s_quad(a, 0, 0, 1, 0), s_quad(a, 0, 0, 1, 1), lin11, lds, l21t) && ok;
+        ok = diag_part_b(s_quad(a, 0, 0, 1, 0), s_quad(a, 0, 0, 1, 1), lin11, lds, l21t, lds + 10240) && ok;
         wave_lds_sync();
         const double r1 = rvec[16 + cc] - lmul_ylds(l21t, ys);
         wave_lds_sync();
@@ -581,11 +629,12 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         const bool needP2 = K2 < NT && max(rfc, rfb) <= k - 2, useU = K2 < NT && k - 1 >= max(rfc, rfb);
         const bool needP1 = !zT && K2 < NT && max(rfc, rfa) <= k - 2, useTp = !zT && K2 < NT && k - 1 >= max(rfc, rfa);
         const bool useTk = !zT && inEnvU && inEnv1;   // T_{k+1} -= L(k+2, k) L(k+1, k)^T
-        const bool needP0 = !zD && K2 < NT && rfc <= K2 - 3;
+        const bool needP0 = !zD && K2 < NT && rfc <= K2 - 4;   // the helpers' diagonal partial: columns <= k-2
+        const bool useP0c = !zD && K2 < NT && k - 1 >= rfc;     // column k-1 of D'_{k+2}: applied here
         const int* f3 = nullptr;
         if (wid >= 2) {
             if (lane == 0 && needP2) f3 = L.fP2 + k;
-            if (lane == 1 && (useU || useTp)) f3 = L.fL + K2 * NT + k - 1;
+            if (lane == 1 && (useU || useTp || useP0c)) f3 = L.fL + K2 * NT + k - 1;
             if (lane == 2 && needP1) f3 = L.fP1 + k1;
             if (lane == 3 && needP0) f3 = L.fP0 + K2;
         }
@@ -621,14 +670,17 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             const unsigned long long tf = dbg ? __builtin_amdgcn_s_memtime() : 0;
             if (dbg && lane == 0) wts[7] = tf - tk;
             double4_t lin11, l21t;
-            ok = diag_part_a(D, LinN, lin11) && ok;
+            ok = diag_part_a(D, LinN, lin11, Dq) && ok;
+            DAG_STAMP(0);
             wave_lds_sync();
             const double y0 = quad_matvec(LinN, 0, rvec);
             if (rg == 0) ys[k1 * kT + cc] = y0;
             const unsigned long long tw0 = dbg ? __builtin_amdgcn_s_memtime() : 0;
             lds_wait(F2, k + 2);
             if (dbg && lane == 0) wts[5] = __builtin_amdgcn_s_memtime() - tw0;
-            ok = diag_part_b(lq(Dq + 2 * 256), lq(Dq + 3 * 256), lin11, LinN, l21t) && ok;
+            DAG_STAMP(1);
+            ok = diag_part_b(lq(Dq + 2 * 256), lq(Dq + 3 * 256), lin11, LinN, l21t, Dq) && ok;
+            DAG_STAMP(2);
             wave_lds_sync();
             const double r1 = rvec[16 + cc] - lmul_ylds(l21t, ys + k1 * kT);
             wave_lds_sync();
@@ -696,16 +748,23 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             // row h of L(k+2, k) = U Linv_k^T, U = A(k+2, k) - sum_{p <= k-1} L(k+2,p) L(k,p)^T (the
             // helpers' partial: p <= k-2; here p = k-1); row h of T_{k+1} = A(k+2, k+1) - sum_{p <= k}
             // L(k+2,p) L(k+1,p)^T (partial p <= k-2; p = k-1 and p = k here); D'_{k+2} (partial
-            // p <= k-1; p = k here, quadrant (1,0)'s by wave 1 in the next interval) and its rhs
+            // p <= k-2; p = k-1 and k here, quadrant (1,0)'s column k by wave 1 in the next interval)
+            // and its rhs
             const int h = wid - 2;
-            if (!__all(!need3 || fv == epoch) && !wave_wait_all(f3, epoch, L.ctl, a.smax)) {
+            const bool got = __all(!need3 || fv == epoch) || wave_wait_all(f3, epoch, L.ctl, a.smax);
+            if (dbg && lane == 0 && h == 1) wts[4] = __builtin_amdgcn_s_memtime() - tk;   // helpers' flags in
+            if (!got) {
                 if (lane == 0) word[4] = 1;
             } else {
                 const int tD = L.oL + (K2 * NT + k - 1) * kTD;
-                double4_t d0 = {0, 0, 0, 0}, d1 = {0, 0, 0, 0};
-                if (useU || useTp) {
+                double4_t d0 = {0, 0, 0, 0}, d1 = {0, 0, 0, 0}, e0 = {0, 0, 0, 0}, e1 = {0, 0, 0, 0};
+                if (useU || useTp || useP0c) {
                     d0 = qload(rs, tD + (2 * h) * 256);
                     d1 = qload(rs, tD + (2 * h + 1) * 256);
+                }
+                if (useP0c && h == 1) {   // row half 0 of L(k+2, k-1), for quadrant (1, 0) of D'_{k+2}
+                    e0 = qload(rs, tD);
+                    e1 = qload(rs, tD + 256);
                 }
                 double4_t u[2], t[2], dd[2];
 #pragma unroll
@@ -726,6 +785,10 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                     const int i = kT * K2 + 16 * h + cc;
                     rr = needP0 ? ld_sc1(a.buf + L.oR + K2 * kT + 16 * h + cc) : s_rhs(a, i);
                 }
+                if (dbg) {   // the loads in (diagnostics only)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    DAG_STAMP(4 + 4 * h);
+                }
                 double4_t o0 = {0, 0, 0, 0}, o1 = {0, 0, 0, 0};
                 if (inEnvU) {
                     if (useU) {
@@ -745,6 +808,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 }
                 sq(L2n + (2 * h) * 256, o0);
                 sq(L2n + (2 * h + 1) * 256, o1);
+                DAG_STAMP(5 + 4 * h);
                 if (inEnvT && useTp) {
 #pragma unroll
                     for (int c = 0; c < 2; c++) {
@@ -753,6 +817,19 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                         mfma_sub(tb, lq(L2 + (2 * c + 1) * 256), d1);
                         t[c] += tb;
                     }
+                }
+                if (useP0c) {   // column k-1: D'_{k+2} -= L(k+2,k-1) L(k+2,k-1)^T (this wave's quadrants), rhs
+                    double4_t db = {0, 0, 0, 0};
+                    mfma_sub(dd[h], d0, d0);
+                    mfma_sub(db, d1, d1);
+                    dd[h] += db;
+                    if (h == 1) {   // quadrant (1, 0): row half 1 against row half 0
+                        double4_t dc = {0, 0, 0, 0};
+                        mfma_sub(dd[0], e0, d0);
+                        mfma_sub(dc, e1, d1);
+                        dd[0] += dc;
+                    }
+                    rr -= lmul_ylds(d0, ys + (k - 1) * kT) + lmul_ylds(d1, ys + (k - 1) * kT + 16);
                 }
                 if (inEnvU) {   // D'_{k+2} -= L(k+2,k)_h L(k+2,k)_h^T (the diagonal quadrant of row h)
                     const int c = h;   // wave 2: q0 (c = 0); wave 3: q3 (c = 1)
@@ -769,9 +846,11 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                     sq(DpN + 3 * 256, dd[1]);
                 }
                 if (rg == 0) rpN[16 * h + cc] = rr;
+                DAG_STAMP(6 + 4 * h);
                 // the column k term of T_{k+1} needs both rows of L(k+1, k)
                 lds_wait(F1, k + 2);
                 lds_wait(F3, k + 2);
+                DAG_STAMP(7 + 4 * h);
                 if (useTk) {
 #pragma unroll
                     for (int c = 0; c < 2; c++) {
@@ -793,7 +872,12 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             unsigned long long* dk = dbg + 8 + 6 * k;
             dk[0] = __builtin_amdgcn_s_memtime() - tk;
             for (int w = 0; w < 4; w++) dk[1 + w] = wts[w];
+            dk[2] |= wts[4] << 32;   // wave 3: the helpers' flags arrived
             dk[5] = wts[6] | (wts[7] << 32);
+            if (k < kDbgSubK) {
+                unsigned long long* ds = dbg + kDbgSubOff + 16 * k;
+                for (int i = 0; i < 16; i++) ds[i] = stm[i];
+            }
         }
         if (word[4]) {
             aborted = true;
@@ -1166,7 +1250,9 @@ void dag_plan(const int* rf, int n, int max_helpers, DagPlan& p, int nti) {
             if (nti && C >= nti) {   // partial solve: the trailing block, after every column < nti
                 ts.push_back({20 * nti + 7, R, C});
             } else if (d == 0) {
-                if (rf[R] <= C - 3) ts.push_back({20 * C - 50, R, C});                            // diagonal partial
+                // diagonal partial: columns <= C-4, so that its last full tile L(C, C-4) comes from the
+                // Linv of four intervals back (one helper hop between two more); the chain applies C-3..C-1
+                if (rf[R] <= C - 4) ts.push_back({20 * C - 70, R, C});
             } else if (d == 1) {
                 if (std::max(rf[R], rf[C]) <= C - 3) ts.push_back({20 * C - 50, R, C});           // sub-diagonal partial
             } else if (d == 2) {

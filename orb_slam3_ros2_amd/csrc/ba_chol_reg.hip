@@ -30,6 +30,7 @@
 #include <utility>
 
 #include "ba_args.h"
+#include "dev_attr.h"
 #include "ba_chol.h"
 #include "ba_chol_reg.h"
 #include "ba_diag16.h"
@@ -374,18 +375,16 @@ int chol_reg_maxt(int n) {
 hipError_t chol_reg_launch(int maxN, int nprob, const BaArgs* args, const int* act, hipStream_t st) {
     const int mt = chol_reg_maxt(maxN);
     if (!mt) return hipErrorInvalidValue;
-    static bool attr = false;
-    if (!attr) {
-        for (const void* f : {(const void*)k_ba_chol_reg<4>, (const void*)k_ba_chol_reg<8>,
-                              (const void*)k_ba_chol_reg<12>, (const void*)k_ba_chol_reg<16>,
-                              (const void*)k_ba_chol_reg<20>, (const void*)k_ba_chol_reg<22>, (const void*)k_chol_reg_probe<4>,
-                              (const void*)k_chol_reg_probe<8>, (const void*)k_chol_reg_probe<12>,
-                              (const void*)k_chol_reg_probe<16>, (const void*)k_chol_reg_probe<20>,
-                              (const void*)k_chol_reg_probe<22>}) {
-            hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            if (e != hipSuccess) return e;
-        }
-        attr = true;
+    static LdsAttrOnce attr;   // per device, thread-safe (dev_attr.h)
+    static const void* const fs[] = {(const void*)k_ba_chol_reg<4>, (const void*)k_ba_chol_reg<8>,
+                                     (const void*)k_ba_chol_reg<12>, (const void*)k_ba_chol_reg<16>,
+                                     (const void*)k_ba_chol_reg<20>, (const void*)k_ba_chol_reg<22>,
+                                     (const void*)k_chol_reg_probe<4>, (const void*)k_chol_reg_probe<8>,
+                                     (const void*)k_chol_reg_probe<12>, (const void*)k_chol_reg_probe<16>,
+                                     (const void*)k_chol_reg_probe<20>, (const void*)k_chol_reg_probe<22>};
+    {
+        const hipError_t e = attr.ensure(fs, 12, 160 * 1024);
+        if (e != hipSuccess) return e;
     }
     const size_t lds = chol_reg_lds_bytes(maxN);
     const dim3 g((unsigned)nprob), b(512);

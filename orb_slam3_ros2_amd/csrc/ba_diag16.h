@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include "ba_chol.h"
+#include "ba_dpp16.h"
 
 namespace orbhip {
 
@@ -107,6 +108,67 @@ __device__ __forceinline__ bool diag16_linv(double4_t d, Store&& store) {
         xv = __builtin_amdgcn_mfma_f64_16x16x4f64(mneg, xp, xv, 0, 0, 0);
     }
     return ok;
+}
+
+// ---------------------------------------------------------------------------------------------
+// DPP column elimination (r05): the same Linv of a 16x16 SPD tile with no MFMA and no readlane on
+// its critical path. Lane c (= lane & 15, every 16-lane row holds the same copy) keeps column c
+// of the tile in v[0..15]. Step j eliminates column j from rows j+1..15 (row ops on [D | I], the
+// LDL^T of D): row i -= m_ij row j, m_ij = D[i][j] / d_j, where D[i][j] is lane j's v[i], read by
+// v_fmac_f64_dpp row_newbcast:j as part of the update itself (one instruction per row and step).
+// A lane's column is a column of D until its own step and a column of X = L~^-1 after it: at step
+// j lane j keeps D's column j, which is -d_j times X's column j (X[i][j] = -m_ij, and later row ops
+// act linearly on it), and every lane's multiplier operand is its own row-j entry, so D columns
+// (c > j) and X columns (c < j) take the same update. At the end Linv = Dg^-1/2 X:
+//   Linv[i][c] = -v[i] s_i / d_c (i > c),  s_c (i = c),  0 (i < c),  s_i = 1/sqrt(d_i).
+// Critical path per step: the pivot broadcast, v_rcp_f64 + Newton, one multiply and the update of
+// row j+1; the other rows' updates (rest()) fill the reciprocal's latency.
+// ---------------------------------------------------------------------------------------------
+template <int J>
+__device__ __forceinline__ double bcast16(double v) {   // lane J of this lane's 16-lane row
+    double r;
+    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v), "n"(J));
+    return r;
+}
+template <int NR = 1>
+__device__ __forceinline__ double rcp_nr(double a) {   // 1/a: v_rcp_f64 + NR Newton steps
+    double r = __builtin_amdgcn_rcp(a);
+#pragma unroll
+    for (int i = 0; i < NR; i++) r = fma(r, fma(-a, r, 1.0), r);
+    return r;
+}
+template <int J, int NR>
+__device__ __forceinline__ void dpp16_step(double (&v)[16], double& pown, int c) {
+    if constexpr (J < 16) {
+        const double piv = bcast16<J>(v[J]);
+        const bool me = c == J;
+        const double u = me ? 0.0 : -v[J];
+        const double r = rcp_nr<NR>(piv);
+        pown = me ? piv : pown;   // lane J keeps its pivot
+        const double t = u * r;
+        Dpp16Step<J>::first(v, t);
+        Dpp16Step<J>::rest(v, t);
+        dpp16_step<J + 1, NR>(v, pown, c);
+    }
+}
+// v: column lane & 15 of the tile (rows 0..15, every 16-lane row the same); lv: Linv in the MFMA C
+// layout (lane (c, g), component q: Linv[g + 4q][c]). False in every lane on a non-positive (or
+// NaN) pivot. The per-lane pivot d_c gives 1/d_c and s_c; s_i of the lane's rows comes from lane i.
+template <int NR = 1>
+__device__ __forceinline__ bool diag16_dpp(double (&v)[16], double4_t& lv) {
+    const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+    double pown = 1.0;
+    dpp16_step<0, NR>(v, pown, c);
+    const bool bad = __any(!(pown > 0.0));
+    const double rown = rcp_nr<NR>(pown), sown = rsq_nr<NR>(pown);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const double x = g == 0 ? v[4 * q] : (g == 1 ? v[4 * q + 1] : (g == 2 ? v[4 * q + 2] : v[4 * q + 3]));
+        const int i = g + 4 * q;
+        const double si = __shfl(sown, i, 64);
+        lv[q] = i > c ? -x * rown * si : (i == c ? sown : 0.0);
+    }
+    return !bad;
 }
 
 // One wave: the 32x32 SPD block read by elem(r, c) (r >= c, both < 32; the caller pads) into Linv

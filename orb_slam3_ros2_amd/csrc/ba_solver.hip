@@ -38,6 +38,7 @@
 #include <vector>
 
 #include "orbhip_ba.h"
+#include "dev_attr.h"
 #include "ba_chol.h"
 #include "ba_chol_blocked.h"
 #include "ba_chol_dag.h"
@@ -145,11 +146,14 @@ __device__ __forceinline__ double edge_error_at(const BaArgs& a, int e, const do
             r1 = a.delta / sq;
         }
     }
-    a.e_err[2 * e] = e0;
-    a.e_err[2 * e + 1] = e1;
-    a.e_chi2[e] = chi2;
-    a.e_rho0[e] = r0;
-    a.e_rho1[e] = r1;
+    // agent-scope (sc1, write-through) stores: a small problem's last workgroup may rewrite these
+    // words in the same launch (ctl_end_body's refresh), and a plain store's dirty line in another
+    // XCD's L2 could otherwise be written back over that rewrite at kernel end
+    st_agent(a.e_err + 2 * e, e0);
+    st_agent(a.e_err + 2 * e + 1, e1);
+    st_agent(a.e_chi2 + e, chi2);
+    st_agent(a.e_rho0 + e, r0);
+    st_agent(a.e_rho1 + e, r1);
     return r0;
 }
 __device__ __forceinline__ double edge_error(const BaArgs& a, int e) {
@@ -904,8 +908,11 @@ __device__ __forceinline__ double backsub_point(const BaArgs& a, int m) {
     for (int r = 0; r < 3; r++) {
         const double xl = Di[3 * r] * c[0] + Di[3 * r + 1] * c[1] + Di[3 * r + 2] * c[2];
         a.x[a.n + 3 * m + r] = xl;
-        a.pts_bak[3 * m + r] = X[r];
-        X[r] += xl;
+        // sc1: the problem's last workgroup of a fused trial reads pts_bak and may restore pts in
+        // the same launch (ctl_end_body)
+        const double xo = X[r];
+        st_agent(a.pts_bak + 3 * m + r, xo);
+        st_agent(X + r, xo + xl);
         sc += xl * (lambda * xl + bl[r]);
     }
     return sc;
@@ -959,9 +966,9 @@ __global__ __launch_bounds__(256) void k_ba_backsub_errs(const BaArgs* __restric
         if (oi >= 0) se3_update(a.x + 6 * oi, T);
 #pragma unroll
         for (int k = 0; k < 8; k++) Tn[8 * p + k] = T[k];
-        if (bx_ == 0) {
+        if (bx_ == 0) {   // sc1: read back by the problem's last workgroup in this launch
 #pragma unroll
-            for (int k = 0; k < 8; k++) a.pose_bak[8 * p + k] = T[k];
+            for (int k = 0; k < 8; k++) st_agent(a.pose_bak + 8 * p + k, T[k]);
         }
     }
     const int m0 = bx_ * 256, m = m0 + threadIdx.x;
@@ -1211,20 +1218,32 @@ __device__ void ctl_end_body(const BaArgs& a, int prob, int* done_flags, double*
     // Fused trials (k_ba_backsub_errs) left the poses unmoved and the new ones in pose_bak: an
     // accepted trial commits them, a rejected one only takes the points back
     __syncthreads();
+    // The backups and the trial's points / errors were stored by other workgroups of this launch
+    // (other XCDs) with sc1 stores drained before their arrival: sc1 loads here see them, and the
+    // sc1 stores below are the last writes of those words.
     const LmCtl& c = *a.ctl;
     if (a.fused) {
         if (!c.pop) {
-            for (int i = threadIdx.x; i < 8 * a.P; i += blockDim.x) a.pose[i] = a.pose_bak[i];
+            for (int i = threadIdx.x; i < 8 * a.P; i += blockDim.x) st_agent(a.pose + i, ld_agent(a.pose_bak + i));
             return;
         }
     } else {
         if (!c.pop) return;
-        for (int i = threadIdx.x; i < 8 * a.P; i += blockDim.x) a.pose[i] = a.pose_bak[i];
+        for (int i = threadIdx.x; i < 8 * a.P; i += blockDim.x) st_agent(a.pose + i, ld_agent(a.pose_bak + i));
     }
-    for (int i = threadIdx.x; i < 3 * a.M; i += blockDim.x) a.pts[i] = a.pts_bak[i];
+    for (int i = threadIdx.x; i < 3 * a.M; i += blockDim.x) st_agent(a.pts + i, ld_agent(a.pts_bak + i));
     if (c.phase != kPhBuild || c.errors_valid) return;
     __syncthreads();
-    for (int e = threadIdx.x; e < a.E; e += blockDim.x) (void)edge_error(a, e);
+    for (int e = threadIdx.x; e < a.E; e += blockDim.x) {   // the restored state, read back sc1
+        const double* tp = a.pose + 8 * a.e_pose[e];
+        const double* xp = a.pts + 3 * a.e_pt[e];
+        double T[8], X[3];
+#pragma unroll
+        for (int k = 0; k < 8; k++) T[k] = ld_agent(tp + k);
+#pragma unroll
+        for (int k = 0; k < 3; k++) X[k] = ld_agent(xp + k);
+        (void)edge_error_at(a, e, T, X);
+    }
 }
 
 // ---- sharded device-driven rounds (BaArgs::sync): the controller's reductions, a collective
@@ -1904,11 +1923,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         }
     }
     const double t_pack = now();
-    static bool lds_set = false;
-    if (!lds_set) {
-        BAOK(hipFuncSetAttribute((const void*)k_ba_cholesky, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        lds_set = true;
-    }
+    static LdsAttrOnce chol_attr;   // per device, thread-safe (dev_attr.h)
+    BAOK(chol_attr.ensure((const void*)k_ba_cholesky, 160 * 1024));
     int maxM = 0, maxE = 0, maxP = 0, maxNp = 0, maxBlk = 0, maxN = 0, maxItems = 0, maxFin = 0;
     bool s_written = false;
     // "large": solved on its own (DAG or blocked); the rest share one single-workgroup launch
@@ -2076,7 +2092,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         // ... and takes its errors inside the back-substitution when its partial slots hold the
         // fused kernel's workgroups (ORBHIP_BA_FUSED=0 keeps the separate k_ba_errors(2))
         const unsigned gbs = gx(std::max(maxM, maxP), 256);
-        static const bool fuse_env = !(std::getenv("ORBHIP_BA_FUSED") && std::getenv("ORBHIP_BA_FUSED")[0] == '0');
+        const char* fz = std::getenv("ORBHIP_BA_FUSED");   // per call: the tests compare both forms
+        const bool fuse_env = !(fz && fz[0] == '0');
         bool fused = all_small && fuse_env;
         for (int b = 0; b < B && fused; b++) fused = (int)gbs <= ha[b].npart_e && pp[b].P <= kFusedMaxP;
         if (fused) {

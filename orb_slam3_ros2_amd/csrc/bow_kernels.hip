@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include "orbhip_device.h"
+#include "dev_attr.h"
 #include "orbhip_kernels.h"
 
 namespace orbhip {
@@ -226,9 +227,9 @@ __global__ __launch_bounds__(1024) void k_search_bow(BowSide K, BowSide F, float
 
 size_t search_bow_lds_bytes() { return sizeof(SearchLds); }
 
-bool search_bow_set_lds_limit() {
-    return hipFuncSetAttribute((const void*)k_search_bow, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)sizeof(SearchLds)) == hipSuccess;
+bool search_bow_set_lds_limit() {   // per device, thread-safe (dev_attr.h)
+    static LdsAttrOnce attr;
+    return attr.ensure((const void*)k_search_bow, (int)sizeof(SearchLds)) == hipSuccess;
 }
 
 void launch_search_bow(const BowSide& K, const BowSide& F, float ratio, int check_orientation, int th_low,

@@ -16,6 +16,7 @@
 #include <type_traits>
 
 #include "../../include/orbhip.h"
+#include "dev_attr.h"
 #include "../../include/orbhip_pattern.h"
 #include "orbhip_device.h"
 #include "orbhip_kernels.h"
@@ -2216,11 +2217,8 @@ void launch_resize_bands(const ExtractPlan* dP, int nbands, const FrameBufs& fb,
 
 void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameBufs& fb, int B, const ConeRect* rects,
                      const int* ctab, int tab_stride, hipStream_t st, int s0, int nthreads) {
-    static bool attr = false;
-    if (!attr) {
-        (void)hipFuncSetAttribute((const void*)k_pyr_cone, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
-        attr = true;
-    }
+    static LdsAttrOnce attr;   // per device, thread-safe (dev_attr.h)
+    (void)attr.ensure((const void*)k_pyr_cone, 64 * 1024);
     ORBHIP_LAUNCH(k_pyr_cone, dim3(ntiles, B), dim3(nthreads), lds, st, dP, fb, rects, ctab, tab_stride,
                   xcd_run_for(B), s0);
 }

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/orbhip.h"
+#include "dev_attr.h"
 #include "orbhip_ba.h"
 #include "pose_opt.h"
 #include "proj.h"
@@ -1462,11 +1463,7 @@ int orbhip_search_bow(orbhip_ctx* c, const uint8_t* kf_desc, const float* kf_ang
         return ORBHIP_ERR_ARG;
     HIPOK(hipSetDevice(c->device));
     hipStream_t st = c->stream;
-    static bool lds_ok = false;
-    if (!lds_ok) {
-        if (!search_bow_set_lds_limit()) return ORBHIP_ERR_DEVICE;
-        lds_ok = true;
-    }
+    if (!search_bow_set_lds_limit()) return ORBHIP_ERR_DEVICE;   // once per device (dev_attr.h)
     // one staging block: [kf desc | f desc | kf angle | f angle | kf node | f node | kf w | f w | valid | match, n]
     const size_t bytes = (size_t)(nkf + nf) * 32 + (size_t)(nkf + nf) * (4 + 4 + 8) + nkf + (size_t)nf * 4 + 64;
     HIPOK(c->d_bow_stage.ensure(bytes + 64));

@@ -28,6 +28,7 @@
 #include <vector>
 
 #include "../../include/orbhip.h"
+#include "dev_attr.h"
 #include "orbhip_device.h"
 #include "orbhip_kernels.h"
 #include "proj.h"
@@ -1415,15 +1416,11 @@ bool onepass_ok(const orbhip_frame* F, int nq) {
 // k_proj_lists' LDS: keypoint records, cells (padded to 256), the waves' index lists
 size_t list_lds_bytes(int n) { return 16 * (size_t)n + 2 * (size_t)((n + 255) & ~255) + kListIdxBytes; }
 static_assert(18 * (size_t)kProjMaxN + kListIdxBytes <= kResolveLds, "k_proj_lists' staging exceeds its LDS");
-hipError_t proj_lds_attr() {   // beyond the default 64 KiB of dynamic LDS
-    static const hipError_t e[4] = {
-        hipFuncSetAttribute((const void*)k_proj_resolve<0>, hipFuncAttributeMaxDynamicSharedMemorySize, kResolveLds),
-        hipFuncSetAttribute((const void*)k_proj_resolve<1>, hipFuncAttributeMaxDynamicSharedMemorySize, kResolveLds),
-        hipFuncSetAttribute((const void*)k_proj_lists<0>, hipFuncAttributeMaxDynamicSharedMemorySize, kResolveLds),
-        hipFuncSetAttribute((const void*)k_proj_lists<1>, hipFuncAttributeMaxDynamicSharedMemorySize, kResolveLds)};
-    for (hipError_t x : e)
-        if (x != hipSuccess) return x;
-    return hipSuccess;
+hipError_t proj_lds_attr() {   // beyond the default 64 KiB of dynamic LDS; per device (dev_attr.h)
+    static LdsAttrOnce attr;
+    static const void* const fs[] = {(const void*)k_proj_resolve<0>, (const void*)k_proj_resolve<1>,
+                                     (const void*)k_proj_lists<0>, (const void*)k_proj_lists<1>};
+    return attr.ensure(fs, 4, kResolveLds);
 }
 // list entries the resolve kernel holds in LDS next to its owner tables and list offsets
 int resolve_ent_cap(int n, int nq) {
@@ -1652,12 +1649,9 @@ int init_search(ProjWorkspace* ws, const orbhip_init_frame* F1, const orbhip_ini
     const int list_cap = std::max(64, (nr0 + 63) & ~63);
     if ((size_t)std::max(nq0, 1) * list_cap > ((size_t)1 << 28)) return ORBHIP_ERR_UNSUPPORTED;
     // the kernel's static LDS (histogram) comes on top of the dynamic 150 KiB envelope
-    static const hipError_t attr = hipFuncSetAttribute((const void*)k_init_greedy,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024);
-    PJOK(attr);
-    static const hipError_t attr_f = hipFuncSetAttribute((const void*)k_init_finish,
-                                                         hipFuncAttributeMaxDynamicSharedMemorySize, 152 * 1024);
-    PJOK(attr_f);
+    static LdsAttrOnce attr;   // per device, thread-safe (dev_attr.h)
+    static const void* const fs[] = {(const void*)k_init_greedy, (const void*)k_init_finish};
+    PJOK(attr.ensure(fs, 2, 152 * 1024));
     Layout lay;
     const size_t o_k1 = lay.add(sizeof(orbhip_kp) * n1), o_d1 = lay.add(32 * (size_t)n1);
     const size_t o_k2 = lay.add(sizeof(orbhip_kp) * std::max(n2, 1)), o_d2 = lay.add(32 * (size_t)std::max(n2, 1));

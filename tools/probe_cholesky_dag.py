@@ -40,7 +40,7 @@ for n_s, shape in cases:
     b = rng.normal(size=n)
     x = np.zeros(n)
     ms = ctypes.c_float(0)
-    dbg = np.zeros(8 + 6 * 200, np.uint64)
+    dbg = np.zeros(8 + 6 * 200 + 16 * 100, np.uint64)   # kDbgWords (ba_chol_dag.h)
     t0 = time.time()
     rc = L.orbhip_test_cholesky_dag(A.ctypes.data, b.ctypes.data, x.ctypes.data, n, 10, int(os.environ.get('ORBHIP_DAG_HELPERS', '0')), ctypes.byref(ms),
                                     dbg.ctypes.data)
@@ -54,5 +54,13 @@ for n_s, shape in cases:
         np.save(os.path.join(os.environ["ORBHIP_PROBE_SAVE"], f"dag_{n}_{shape}.npy"), dbg)
     print(f"n={n} {shape}: rc={rc} dag {ms.value * 1e3:.1f} us relerr={err:.2e} | cycles prologue={dbg[0]} "
           f"forward={dbg[1]} backward={dbg[2]} diag={dbg[4]} total={dbg[5]} | interval medians: total {med[0]} "
-          f"| wave ends {med[1]} {med[2]} {med[3]} {med[4]} w0 start {int(np.median(ph[:, 5] & 0xFFFFFFFF)) if ki else 0} "
+          f"| wave ends {med[0 + 1]} {int(np.median(ph[:, 2] & 0xFFFFFFFF)) if ki else 0} {med[3]} {med[4]} "
+          f"w3 flags in {int(np.median(ph[:, 2] >> 32)) if ki else 0} w0 start {int(np.median(ph[:, 5] & 0xFFFFFFFF)) if ki else 0} "
           f"pre-diag {int(np.median(ph[:, 5] >> 32)) if ki else 0} ({time.time() - t0:.1f}s)", flush=True)
+    ks = min(ki, 100)
+    if ks:
+        sub = dbg[8 + 6 * 200:8 + 6 * 200 + 16 * ks].reshape(ks, 16).astype(np.int64)
+        m = np.median(sub, axis=0).astype(int)
+        print(f"    sub-phases (median cycles from the interval start): w0 diagA {m[0]} D(1,*) in {m[1]} diagB {m[2]} | "
+              f"w2 loads {m[4]} L(k+2,k) {m[5]} T/D' {m[6]} L(k+1,k) in {m[7]} | "
+              f"w3 loads {m[8]} L(k+2,k) {m[9]} T/D' {m[10]} L(k+1,k) in {m[11]}", flush=True)

@@ -52,6 +52,37 @@ __global__ __launch_bounds__(64) void k_diag16_loop(const double* __restrict__ A
     for (int q = 0; q < 4; q++) Linv[(rg + 4 * q) * 16 + cc] = lv[q];
 }
 
+// the DPP column elimination (diag16_dpp): lane c holds column c, Linv comes in the C layout
+__global__ __launch_bounds__(64) void k_dpp16(const double* __restrict__ A, double* __restrict__ Linv, int* okf) {
+    const int lane = threadIdx.x, c = lane & 15, rg = lane >> 4;
+    const double* a = A + (size_t)blockIdx.x * 256;
+    double* L = Linv + (size_t)blockIdx.x * 256;
+    double v[16];
+    double4_t lv;
+#pragma unroll
+    for (int i = 0; i < 16; i++) v[i] = a[i * 16 + c];
+    const bool ok = diag16_dpp(v, lv);
+#pragma unroll
+    for (int q = 0; q < 4; q++) L[(rg + 4 * q) * 16 + c] = lv[q];
+    if (lane == 0) okf[blockIdx.x] = ok;
+}
+__global__ __launch_bounds__(64) void k_dpp16_loop(const double* __restrict__ A, double* __restrict__ Linv, int reps) {
+    const int lane = threadIdx.x, c = lane & 15, rg = lane >> 4;
+    double v0[16];
+    double4_t lv = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 16; i++) v0[i] = A[i * 16 + c];
+    for (int r = 0; r < reps; r++) {
+        double v[16];
+        const double z = lv[0] + lv[1] + lv[2] + lv[3];
+#pragma unroll
+        for (int i = 0; i < 16; i++) v[i] = fma(0.0, z, v0[i]);   // a dependency on the previous result
+        diag16_dpp(v, lv);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) Linv[(rg + 4 * q) * 16 + c] = lv[q];
+}
+
 static void ref_linv(const double* A, double* Li) {
     long double L[16][16] = {}, X[16][16] = {};
     for (int j = 0; j < 16; j++) {
@@ -187,5 +218,51 @@ int main() {
         hipEventElapsedTime(&ms2, e0, e1);
         printf("diag16 chain: %.3f us per factorization (1000: %.3f ms, 11000: %.3f ms)\n", (ms2 - ms1) * 1e3 / 10000, ms1, ms2);
     }
+    // the DPP forms: accuracy against the long-double reference and the dependent-chain time
+    auto check = [&](const char* nm, void (*kone)(const double*, double*, int*), void (*kloop)(const double*, double*, int)) -> bool {
+        hipLaunchKernelGGL(kone, dim3(NB), dim3(64), 0, nullptr, dA, dL, dok);
+        hipDeviceSynchronize();
+        hipMemcpy(Lg.data(), dL, sizeof(double) * A.size(), hipMemcpyDeviceToHost);
+        hipMemcpy(ok.data(), dok, sizeof(int) * NB, hipMemcpyDeviceToHost);
+        double w2 = 0;
+        int nok2 = 0;
+        for (int b = 0; b < NB; b++) {
+            double num = 0, den = 0;
+            for (int i = 0; i < 256; i++) {
+                num = std::fmax(num, std::fabs(Lg[b * 256 + i] - Lr[b * 256 + i]));
+                den = std::fmax(den, std::fabs(Lr[b * 256 + i]));
+            }
+            w2 = std::fmax(w2, num / den);
+            nok2 += ok[b];
+            if (b < 12) printf("  %s tile %d (eps 1e-%d): rel err %.3e\n", nm, b, b % 12, num / den);
+        }
+        printf("%s: %d/%d pd, max rel err %.3e\n", nm, nok2, NB, w2);
+        std::vector<double> Bn(A.begin(), A.begin() + 256);
+        Bn[5 * 16 + 5] = -1.0;
+        hipMemcpy(dA, Bn.data(), sizeof(double) * 256, hipMemcpyHostToDevice);
+        hipLaunchKernelGGL(kone, dim3(1), dim3(64), 0, nullptr, dA, dL, dok);
+        int okn = 1;
+        hipMemcpy(&okn, dok, sizeof(int), hipMemcpyDeviceToHost);
+        printf("%s non-PD tile reported: %s\n", nm, okn ? "NO" : "yes");
+        hipMemcpy(dA, A.data(), sizeof(double) * A.size(), hipMemcpyHostToDevice);
+        hipEvent_t e0, e1;
+        hipEventCreate(&e0); hipEventCreate(&e1);
+        hipLaunchKernelGGL(kloop, dim3(1), dim3(64), 0, nullptr, dA, dL, 10);
+        hipEventRecord(e0, nullptr);
+        hipLaunchKernelGGL(kloop, dim3(1), dim3(64), 0, nullptr, dA, dL, 1000);
+        hipEventRecord(e1, nullptr);
+        hipEventSynchronize(e1);
+        float ms1 = 0;
+        hipEventElapsedTime(&ms1, e0, e1);
+        hipEventRecord(e0, nullptr);
+        hipLaunchKernelGGL(kloop, dim3(1), dim3(64), 0, nullptr, dA, dL, 11000);
+        hipEventRecord(e1, nullptr);
+        hipEventSynchronize(e1);
+        float ms2 = 0;
+        hipEventElapsedTime(&ms2, e0, e1);
+        printf("%s chain: %.3f us per factorization\n", nm, (ms2 - ms1) * 1e3 / 10000);
+        return !okn && nok2 == NB && w2 <= 1e-6;
+    };
+    if (!check("dpp16", k_dpp16, k_dpp16_loop)) return 1;
     return worst < 1e-6 && nok == NB ? 0 : 1;
 }
