@@ -901,6 +901,52 @@ def ba_cholesky_roofline(n, regime):
             "avg_launch_ms": round(ms.value, 4), "residual": err, "counters": load_counters("k_chol_dag", regime)}
 
 
+def ba_nd_roofline(reps=20):
+    """Live fp64 MFMA roofline of the solve the C5 GBA actually runs: the nested dissection of the
+    reduced camera system (csrc/ba_nd.hip) on a C5-structured system (399 optimised poses, cyclic
+    co-visibility band w = 19: synthetic.banded_pose_system), with the planner's K. The kernels are
+    k_chol_dag_multi (the K interiors' partial factorizations in one launch), k_nd_assemble, the
+    separator's k_chol_dag and k_nd_backsolve (+ k_nd_finish); the two halves are timed alone as
+    well (HIP events, `reps` solves each). Algorithmic flops of one solve: every
+    interior's banded factorization n_I b^2 with b = 6 w, plus its Schur contribution to its two
+    separators n_I (2b)^2, plus the separator system's dense Cholesky n_Z^3 / 3 + 2 n_Z^2,
+    n_Z = 6 w K. Counters: rocprofv3 --pmc passes of tools/pmc_workload.py c5nd."""
+    from orb_slam3_ros2_amd._lib import lib
+    from orb_slam3_ros2_amd.synthetic import banded_pose_system
+    n_pose, w = 399, 19
+    A, b, bi, bj = banded_pose_system(n_pose, w, True, seed=1)
+    L = lib()
+    f = L.orbhip_test_nd_stages
+    f.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] + [ctypes.c_void_p] * 2 + [ctypes.c_int] * 3 + \
+        [ctypes.c_void_p] * 4
+    x = np.zeros(A.shape[0])
+    ms, ku = ctypes.c_float(0), ctypes.c_int(0)
+    stage = (ctypes.c_float * 2)()
+    seg = (ctypes.c_int * 65)()
+    rc = f(A.ctypes.data, b.ctypes.data, x.ctypes.data, n_pose, bi.ctypes.data, bj.ctypes.data, bi.size, 0, reps,
+           ctypes.byref(ms), ctypes.byref(ku), stage, seg)
+    if rc != 0:
+        return {"error": rc}
+    K = ku.value
+    bw = 6 * w
+    n_int = [6 * (seg[r + 1] - seg[r] - w) for r in range(K)]
+    n_z = 6 * w * K
+    fl_int = sum(ni * bw * bw + ni * (2 * bw) ** 2 for ni in n_int)
+    fl_sep = n_z ** 3 / 3 + 2 * n_z * n_z
+    flops = fl_int + fl_sep
+    err = float(np.abs(A @ x - b).max() / np.abs(b).max())
+    ach = flops / (ms.value * 1e-3) / 1e12
+    out = {"kernels": "k_chol_dag_multi + k_nd_assemble + k_chol_dag (separator) + k_nd_backsolve + k_nd_finish",
+           "bound": "mfma", "achieved": round(ach, 4), "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+           "frac": round(ach / FP64_MFMA_PEAK_TFS, 6), "n": int(A.shape[0]), "segments": K, "band_poses": w,
+           "n_interiors": n_int, "n_separator": n_z, "flops_per_solve": int(flops),
+           "flops_interiors": int(fl_int), "flops_separator": int(fl_sep), "avg_solve_ms": round(ms.value, 4),
+           "interiors_and_assembly_ms": round(stage[0], 4), "separator_and_backsolve_ms": round(stage[1], 4),
+           "residual": err, "counters": {k: load_counters(k, "c5nd") for k in
+                                         ("k_chol_dag_multi", "k_chol_dag", "k_nd_backsolve", "k_nd_assemble")}}
+    return out
+
+
 def c4_lba(args, ws, rank, ctx):
     from orb_slam3_ros2_amd import Optimizer
     from orb_slam3_ros2_amd.synthetic import synthetic_ba_problem
@@ -933,7 +979,10 @@ def c4_lba(args, ws, rank, ctx):
     out["c4_lba_batched_trials_mean"] = round(float(np.mean([x.lm_trials for x in rs])), 2)
     if rank == 0:
         out["c4_roofline"] = ba_cholesky_roofline(294, "c4")
-        out["c5_roofline"] = ba_cholesky_roofline(2394, "c5")
+        # a microbenchmark: the dense n = 2394 solve through the plain DAG kernel (C5-sized); the
+        # C5 GBA itself runs the nested dissection measured by c5_nd_roofline
+        out["c5_dense_solve_microbench"] = ba_cholesky_roofline(2394, "c5")
+        out["c5_nd_roofline"] = ba_nd_roofline()
     return out
 
 

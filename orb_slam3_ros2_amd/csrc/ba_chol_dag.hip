@@ -160,7 +160,9 @@ __device__ __forceinline__ double4_t s_quad(const DagK& k, int R, int C, int a, 
     for (int q = 0; q < 4; q++) v[q] = s_elem(k, r, kT * C + 16 * b + (lane >> 4) + 4 * q);
     return v;
 }
-// c4 -= A B^T in the transposed C layout (a: L_Jk quadrant, b: L_Ik quadrant -> C_IJ^T)
+// c4 -= A B^T in the transposed C layout (a: L_Jk quadrant, b: L_Ik quadrant -> C_IJ^T). (Splitting
+// the 4-deep accumulation over two accumulators measured slower: the extra adds and AGPR moves
+// cost more than the MFMA latency they hide.)
 __device__ __forceinline__ void mfma_sub(double4_t& c4, const double4_t& a, const double4_t& b) {
     c4 = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[0], b[0], c4, 0, 0, 0);
     c4 = __builtin_amdgcn_mfma_f64_16x16x4f64(-a[1], b[1], c4, 0, 0, 0);
@@ -182,6 +184,12 @@ __device__ __forceinline__ double lmul_y4(const double4_t& l, double y0, double 
 __device__ __forceinline__ double lmul_ylds(const double4_t& l, const double* y) {
     const int rg = (threadIdx.x & 63) >> 4;
     return lmul_y4(l, y[rg], y[rg + 4], y[rg + 8], y[rg + 12]);
+}
+// this lane's part of lmul_ylds before the cross-row sum: several quadrants' parts are added
+// first and summed across the row groups once (col4_sum)
+__device__ __forceinline__ double lmul_part(const double4_t& l, const double* y) {
+    const int rg = (threadIdx.x & 63) >> 4;
+    return l[0] * y[rg] + l[1] * y[rg + 4] + l[2] * y[rg + 8] + l[3] * y[rg + 12];
 }
 
 // every lane's flag (nullptr: none) equal to epoch; false on abort / timeout (wave-uniform)
@@ -456,7 +464,7 @@ __device__ __forceinline__ bool diag_part_a(const double4_t& d11, double* Lq, do
     const int lane = threadIdx.x & 63, cc = lane & 15, rg = lane >> 4;
     double v[16];
     c_to_cols(d11, scr, v);
-    const bool ok = diag16_dpp<kNewton>(v, lin11);
+    const bool ok = diag16_dpp<kNewton>(v, scr, lin11);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         Lq[qidx(rg + 4 * q, cc)] = lin11[q];
@@ -480,16 +488,14 @@ __device__ __forceinline__ bool diag_part_b(const double4_t& d21t, double4_t d22
     const int lane = threadIdx.x & 63, cc = lane & 15, rg = lane >> 4;
     const double* a11 = Lq + lane * 4;   // quadrant 0 in operand order
     l21t = double4_t{0, 0, 0, 0};
-#pragma unroll
-    for (int kk = 0; kk < 4; kk++) l21t = __builtin_amdgcn_mfma_f64_16x16x4f64(a11[kk], d21t[kk], l21t, 0, 0, 0);
-#pragma unroll
-    for (int kk = 0; kk < 4; kk++) d22 = __builtin_amdgcn_mfma_f64_16x16x4f64(-l21t[kk], l21t[kk], d22, 0, 0, 0);
+    panel_add(l21t, double4_t{a11[0], a11[1], a11[2], a11[3]}, d21t);
+    mfma_sub(d22, l21t, l21t);
     double* op22 = Lq + 3 * 256;
 #if ORBHIP_DAG_DIAG_DPP
     double4_t l22;
     double v[16];
     c_to_cols(d22, scr, v);
-    const bool ok2 = diag16_dpp<kNewton>(v, l22);
+    const bool ok2 = diag16_dpp<kNewton>(v, scr, l22);
 #pragma unroll
     for (int q = 0; q < 4; q++) op22[(rg + 4 * q + 16 * (cc & 3)) * 4 + (cc >> 2)] = l22[q];
 #else
@@ -497,13 +503,11 @@ __device__ __forceinline__ bool diag_part_b(const double4_t& d21t, double4_t d22
     const bool ok2 = diag16_linv<kNewton>(d22, [&](int r, int c, double v) { op22[(r + 16 * (c & 3)) * 4 + (c >> 2)] = v; });
 #endif
     double4_t w = {0, 0, 0, 0};
-#pragma unroll
-    for (int kk = 0; kk < 4; kk++) w = __builtin_amdgcn_mfma_f64_16x16x4f64(l21t[kk], lin11[kk], w, 0, 0, 0);
+    panel_add(w, l21t, lin11);
     wave_lds_sync();
     const double* a22 = op22 + lane * 4;
     double4_t l21i = {0, 0, 0, 0};
-#pragma unroll
-    for (int kk = 0; kk < 4; kk++) l21i = __builtin_amdgcn_mfma_f64_16x16x4f64(-a22[kk], w[kk], l21i, 0, 0, 0);
+    mfma_sub(l21i, double4_t{a22[0], a22[1], a22[2], a22[3]}, w);
 #pragma unroll
     for (int q = 0; q < 4; q++) Lq[qidx(16 + rg + 4 * q, cc)] = l21i[q];
     return ok2;
@@ -529,6 +533,9 @@ __device__ __forceinline__ void lds_wait(int* w, int v) {
     asm volatile("" ::: "memory");
 }
 
+// DBG: the debug build of the chain (the probe's per-interval cycle words); the product build
+// carries no stamp code (the debug values would otherwise stay live through the whole loop)
+template <bool DBG>
 __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs, int epoch, double* lds) {
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63, cc = lane & 15, rg = lane >> 4;
     const int rq = wid >> 1, cq = wid & 1, quad = 2 * rq + cq;
@@ -554,7 +561,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     unsigned long long* wts = (unsigned long long*)(lds + 11264 + 8);   // per-wave cycles (dbg)
     unsigned long long* stm = (unsigned long long*)(lds + 10560);       // sub-phase stamps (dbg), 16
 #define DAG_STAMP(i) do { if (dbg && lane == 0) stm[i] = __builtin_amdgcn_s_memtime() - tk; } while (0)
-    unsigned long long* dbg = a.dbg;
+    unsigned long long* dbg = DBG ? a.dbg : nullptr;
     const unsigned long long t_start = dbg ? __builtin_amdgcn_s_memtime() : 0;
     unsigned long long t_fact = 0;
     bool ok = true, aborted = false;
@@ -603,43 +610,82 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     // a partial solve (nti > 0) runs intervals 0 .. nti-1: the last one forms the trailing block's
     // first tiles of L (rows of L(nti, nti-1) and L(nti+1, nti-1)) but factors no diagonal tile
     const int kEnd = a.nti ? a.nti : NT - 1;
+    // waves 2/3: the helpers' flag this lane waits for in interval kk (nullptr: none), i.e. the
+    // partials P2[kk], P1[kk+1], P0[kk+2] and the full tile L(kk+2, kk-1) the flags of that interval
+    // (fl) select
+    auto helper_flag = [&](int kk) -> const int* {
+        const int kk1 = kk + 1, kk2 = kk + 2;
+        if (kk2 >= NT || lane > 3) return nullptr;
+        const bool zT = a.nti && kk1 >= a.nti, zD = a.nti && kk2 >= a.nti;
+        const int ra = rfl[kk1], rb = rfl[kk], rc = rfl[kk2];
+        if (lane == 0) return max(rc, rb) <= kk - 2 ? L.fP2 + kk : nullptr;
+        if (lane == 1) {
+            const bool uU = kk - 1 >= max(rc, rb), uT = !zT && kk - 1 >= max(rc, ra), uC = !zD && kk - 1 >= rc;
+            return (uU || uT || uC) ? L.fL + kk2 * NT + kk - 1 : nullptr;
+        }
+        if (lane == 2) return (!zT && max(rc, ra) <= kk - 2) ? L.fP1 + kk1 : nullptr;
+        return (!zD && rc <= kk2 - 4) ? L.fP0 + kk2 : nullptr;
+    };
+    int fvp = 0;   // waves 2/3: the next interval's helper flag, loaded ahead
     for (int k = 0; k < kEnd; k++) {
         const unsigned long long tk = dbg ? __builtin_amdgcn_s_memtime() : 0;
-        const int k1 = k + 1, K2 = k + 2, cur = k & 1, nxt = cur ^ 1;
-        const bool last = a.nti && k1 >= a.nti;         // tile k+1 is in the trailing block: not factored
-        const bool zT = last, zD = a.nti && K2 >= a.nti;   // T_{k+1} / D'_{k+2} are trailing-block tiles
-        double* Lin = lds + 1024 * cur;
-        double* LinN = lds + 1024 * nxt;
-        double* L1 = lds + 2048 + 1024 * c1;
-        double* L1n = lds + 2048 + 1024 * (c1 ^ 1);
-        double* L2 = lds + 4096 + 1024 * c2;
-        double* L2n = lds + 4096 + 1024 * (c2 ^ 1);
-        double* Tp = lds + 6144 + 1024 * cur;
-        double* TpN = lds + 6144 + 1024 * nxt;
-        double* Dp = lds + 8192 + 1024 * cur;
-        double* DpN = lds + 8192 + 1024 * nxt;
-        double* Dq = lds + 10240;
-        double* rp = rppB + 32 * cur;
-        double* rpN = rppB + 32 * nxt;
-        const int rfa = rfl[k1], rfb = rfl[k];
-        const bool inEnv1 = rfa <= k;
-        const bool useD2 = k - 1 >= rfa;
-        const int rfc = K2 < NT ? rfl[K2] : 0;
-        const bool inEnvU = K2 < NT && rfc <= k, inEnvT = K2 < NT && rfc <= k1;
-        const bool needP2 = K2 < NT && max(rfc, rfb) <= k - 2, useU = K2 < NT && k - 1 >= max(rfc, rfb);
-        const bool needP1 = !zT && K2 < NT && max(rfc, rfa) <= k - 2, useTp = !zT && K2 < NT && k - 1 >= max(rfc, rfa);
-        const bool useTk = !zT && inEnvU && inEnv1;   // T_{k+1} -= L(k+2, k) L(k+1, k)^T
-        const bool needP0 = !zD && K2 < NT && rfc <= K2 - 4;   // the helpers' diagonal partial: columns <= k-2
-        const bool useP0c = !zD && K2 < NT && k - 1 >= rfc;     // column k-1 of D'_{k+2}: applied here
-        const int* f3 = nullptr;
-        if (wid >= 2) {
-            if (lane == 0 && needP2) f3 = L.fP2 + k;
-            if (lane == 1 && (useU || useTp || useP0c)) f3 = L.fL + K2 * NT + k - 1;
-            if (lane == 2 && needP1) f3 = L.fP1 + k1;
-            if (lane == 3 && needP0) f3 = L.fP0 + K2;
+        const int k1 = k + 1, K2 = k + 2;
+        // every per-interval flag packed in one word (fl), every LDS buffer pointer derived from
+        // one parity word (par) where it is used: held across the role branches as separate
+        // values they exceeded the SGPR budget and were spilled / reloaded by readlanes
+        unsigned fl;
+        {
+            const bool last = a.nti && k1 >= a.nti;   // tile k+1 is in the trailing block: not factored
+            const bool zT = last, zD = a.nti && K2 >= a.nti;   // T_{k+1} / D'_{k+2}: trailing-block tiles
+            const int rfa = rfl[k1], rfb = rfl[k];
+            const bool inEnv1 = rfa <= k;
+            const bool useD2 = k - 1 >= rfa;
+            const int rfc = K2 < NT ? rfl[K2] : 0;
+            const bool inEnvU = K2 < NT && rfc <= k, inEnvT = K2 < NT && rfc <= k1;
+            const bool needP2 = K2 < NT && max(rfc, rfb) <= k - 2, useU = K2 < NT && k - 1 >= max(rfc, rfb);
+            const bool needP1 = !zT && K2 < NT && max(rfc, rfa) <= k - 2;
+            const bool useTp = !zT && K2 < NT && k - 1 >= max(rfc, rfa);
+            const bool useTk = !zT && inEnvU && inEnv1;   // T_{k+1} -= L(k+2, k) L(k+1, k)^T
+            const bool needP0 = !zD && K2 < NT && rfc <= K2 - 4;   // the helpers' diagonal partial: columns <= k-2
+            const bool useP0c = !zD && K2 < NT && k - 1 >= rfc;     // column k-1 of D'_{k+2}: applied here
+            fl = (unsigned)last | (unsigned)inEnv1 << 1 | (unsigned)useD2 << 2 | (unsigned)inEnvU << 3 |
+                 (unsigned)inEnvT << 4 | (unsigned)needP2 << 5 | (unsigned)useU << 6 | (unsigned)needP1 << 7 |
+                 (unsigned)useTp << 8 | (unsigned)useTk << 9 | (unsigned)needP0 << 10 | (unsigned)useP0c << 11;
         }
+#define DAG_FL(b) (((fl >> (b)) & 1u) != 0u)
+#define last DAG_FL(0)
+#define inEnv1 DAG_FL(1)
+#define useD2 DAG_FL(2)
+#define inEnvU DAG_FL(3)
+#define inEnvT DAG_FL(4)
+#define needP2 DAG_FL(5)
+#define useU DAG_FL(6)
+#define needP1 DAG_FL(7)
+#define useTp DAG_FL(8)
+#define useTk DAG_FL(9)
+#define needP0 DAG_FL(10)
+#define useP0c DAG_FL(11)
+        const int par = (k & 1) | c1 << 1 | c2 << 2;
+#define cur (par & 1)
+#define nxt ((par & 1) ^ 1)
+#define Lin (lds + 1024 * cur)
+#define LinN (lds + 1024 * nxt)
+#define L1 (lds + 2048 + 1024 * ((par >> 1) & 1))
+#define L1n (lds + 2048 + 1024 * (((par >> 1) & 1) ^ 1))
+#define L2 (lds + 4096 + 1024 * ((par >> 2) & 1))
+#define L2n (lds + 4096 + 1024 * (((par >> 2) & 1) ^ 1))
+#define Tp (lds + 6144 + 1024 * cur)
+#define TpN (lds + 6144 + 1024 * nxt)
+#define Dp (lds + 8192 + 1024 * cur)
+#define DpN (lds + 8192 + 1024 * nxt)
+#define rp (rppB + 32 * cur)
+#define rpN (rppB + 32 * nxt)
+        double* Dq = lds + 10240;
+        const int* f3 = wid >= 2 ? helper_flag(k) : nullptr;
         const bool need3 = f3 != nullptr;
-        const int fv = ld_flag(need3 ? f3 : L.ctl);   // in flight until its use below
+        // the flag was loaded at the end of the previous interval (fvp), so its round trip overlaps
+        // the interval barrier; interval 0 loads it here
+        const int fv = k == 0 ? ld_flag(need3 ? f3 : L.ctl) : fvp;
         if (wid == 0) {
             if (dbg && lane == 0) wts[6] = __builtin_amdgcn_s_memtime() - tk;
             // row 0 of L(k+1, k) = T Linv_k^T
@@ -664,7 +710,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 mfma_sub(D, l0, l0);
                 mfma_sub(Db, l1, l1);
                 D += Db;
-                r0 -= lmul_ylds(l0, ys + k * kT) + lmul_ylds(l1, ys + k * kT + 16);
+                r0 -= col4_sum(lmul_part(l0, ys + k * kT) + lmul_part(l1, ys + k * kT + 16));
             }
             if (rg == 0) rvec[cc] = r0;
             const unsigned long long tf = dbg ? __builtin_amdgcn_s_memtime() : 0;
@@ -688,6 +734,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             wave_lds_sync();
             const double y1 = quad_matvec(LinN, 3, rvec + 16);
             if (rg == 0) ys[k1 * kT + 16 + cc] = y1;
+            DAG_STAMP(3);
             if (dbg) t_fact += __builtin_amdgcn_s_memtime() - tf;
             }   // !last
         } else if (wid == 1) {
@@ -722,7 +769,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 mfma_sub(Dc, l1, l1);
                 D10 += Db;
                 D11 += Dc;
-                r1 -= lmul_ylds(l0, ys + k * kT) + lmul_ylds(l1, ys + k * kT + 16);
+                r1 -= col4_sum(lmul_part(l0, ys + k * kT) + lmul_part(l1, ys + k * kT + 16));
             }
             sq(Dq + 2 * 256, D10);
             sq(Dq + 3 * 256, D11);
@@ -789,21 +836,26 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     DAG_STAMP(4 + 4 * h);
                 }
+                // every LDS operand of this wave's MFMA work first (one LDS round trip), the MFMA
+                // chains two deep per product, the rhs terms (LDS + cross-row sums) after the tiles
+                const double4_t l1q[4] = {lq(L1), lq(L1 + 256), lq(L1 + 512), lq(L1 + 768)};
+                const double4_t liq[3] = {lq(Lin), lq(Lin + 512), lq(Lin + 768)};
+                const double4_t l2q[4] = {lq(L2), lq(L2 + 256), lq(L2 + 512), lq(L2 + 768)};
                 double4_t o0 = {0, 0, 0, 0}, o1 = {0, 0, 0, 0};
                 if (inEnvU) {
                     if (useU) {
 #pragma unroll
                         for (int c = 0; c < 2; c++) {
                             double4_t ub = {0, 0, 0, 0};
-                            mfma_sub(u[c], lq(L1 + (2 * c) * 256), d0);
-                            mfma_sub(ub, lq(L1 + (2 * c + 1) * 256), d1);
+                            mfma_sub(u[c], l1q[2 * c], d0);
+                            mfma_sub(ub, l1q[2 * c + 1], d1);
                             u[c] += ub;
                         }
                     }
                     double4_t o1b = {0, 0, 0, 0};
-                    panel_add(o0, lq(Lin), u[0]);
-                    panel_add(o1, lq(Lin + 2 * 256), u[0]);
-                    panel_add(o1b, lq(Lin + 3 * 256), u[1]);
+                    panel_add(o0, liq[0], u[0]);
+                    panel_add(o1, liq[1], u[0]);
+                    panel_add(o1b, liq[2], u[1]);
                     o1 += o1b;
                 }
                 sq(L2n + (2 * h) * 256, o0);
@@ -813,37 +865,47 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
 #pragma unroll
                     for (int c = 0; c < 2; c++) {
                         double4_t tb = {0, 0, 0, 0};
-                        mfma_sub(t[c], lq(L2 + (2 * c) * 256), d0);
-                        mfma_sub(tb, lq(L2 + (2 * c + 1) * 256), d1);
+                        mfma_sub(t[c], l2q[2 * c], d0);
+                        mfma_sub(tb, l2q[2 * c + 1], d1);
                         t[c] += tb;
                     }
                 }
-                if (useP0c) {   // column k-1: D'_{k+2} -= L(k+2,k-1) L(k+2,k-1)^T (this wave's quadrants), rhs
-                    double4_t db = {0, 0, 0, 0};
-                    mfma_sub(dd[h], d0, d0);
-                    mfma_sub(db, d1, d1);
-                    dd[h] += db;
-                    if (h == 1) {   // quadrant (1, 0): row half 1 against row half 0
-                        double4_t dc = {0, 0, 0, 0};
-                        mfma_sub(dd[0], e0, d0);
-                        mfma_sub(dc, e1, d1);
-                        dd[0] += dc;
+                DAG_STAMP(12 + 2 * h);
+                {   // D'_{k+2}: column k-1 (L(k+2, k-1)) and column k (L(k+2, k)) in independent chains
+                    double4_t da = {0, 0, 0, 0}, db = {0, 0, 0, 0}, dc = {0, 0, 0, 0}, de = {0, 0, 0, 0};
+                    if (useP0c) {
+                        mfma_sub(da, d0, d0);
+                        mfma_sub(db, d1, d1);
+                        if (h == 1) {   // quadrant (1, 0): row half 1 against row half 0
+                            mfma_sub(dc, e0, d0);
+                            mfma_sub(de, e1, d1);
+                        }
                     }
-                    rr -= lmul_ylds(d0, ys + (k - 1) * kT) + lmul_ylds(d1, ys + (k - 1) * kT + 16);
-                }
-                if (inEnvU) {   // D'_{k+2} -= L(k+2,k)_h L(k+2,k)_h^T (the diagonal quadrant of row h)
-                    const int c = h;   // wave 2: q0 (c = 0); wave 3: q3 (c = 1)
-                    double4_t db = {0, 0, 0, 0};
-                    mfma_sub(dd[c], o0, o0);
-                    mfma_sub(db, o1, o1);
-                    dd[c] += db;
-                    rr -= lmul_ylds(o0, ys + k * kT) + lmul_ylds(o1, ys + k * kT + 16);
+                    double4_t dg = {0, 0, 0, 0}, dh = {0, 0, 0, 0};
+                    if (inEnvU) {
+                        mfma_sub(dg, o0, o0);
+                        mfma_sub(dh, o1, o1);
+                    }
+                    const double4_t dsum = (da + db) + (dg + dh);
+                    if (h == 0) {   // constant indices only (a runtime index put dd in scratch)
+                        dd[0] += dsum;
+                    } else {
+                        dd[1] += dsum;
+                        dd[0] += dc + de;
+                    }
                 }
                 if (h == 0) {
                     sq(DpN, dd[0]);
                 } else {
                     sq(DpN + 2 * 256, dd[0]);
                     sq(DpN + 3 * 256, dd[1]);
+                }
+                DAG_STAMP(13 + 2 * h);
+                {   // the rhs terms of columns k-1 and k, one cross-row sum
+                    double part = 0.0;
+                    if (useP0c) part += lmul_part(d0, ys + (k - 1) * kT) + lmul_part(d1, ys + (k - 1) * kT + 16);
+                    if (inEnvU) part += lmul_part(o0, ys + k * kT) + lmul_part(o1, ys + k * kT + 16);
+                    rr -= col4_sum(part);
                 }
                 if (rg == 0) rpN[16 * h + cc] = rr;
                 DAG_STAMP(6 + 4 * h);
@@ -864,8 +926,39 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 sq(TpN + (2 * h + 1) * 256, t[1]);
             }
         }
+        if (wid >= 2 && k + 1 < kEnd) {
+            const int* fn = helper_flag(k + 1);
+            fvp = ld_flag(fn ? fn : L.ctl);
+        }
         if (dbg && lane == 0) wts[wid] = __builtin_amdgcn_s_memtime() - tk;
         lds_barrier();
+#undef DAG_FL
+#undef last
+#undef inEnv1
+#undef useD2
+#undef inEnvU
+#undef inEnvT
+#undef needP2
+#undef useU
+#undef needP1
+#undef useTp
+#undef useTk
+#undef needP0
+#undef useP0c
+#undef cur
+#undef nxt
+#undef Lin
+#undef LinN
+#undef L1
+#undef L1n
+#undef L2
+#undef L2n
+#undef Tp
+#undef TpN
+#undef Dp
+#undef DpN
+#undef rp
+#undef rpN
         c1 ^= 1;
         c2 ^= 1;
         if (dbg && tid == 0 && k < 200) {
@@ -1117,6 +1210,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
 }
 
 // one problem's workgroup: role 0 the chain, role h + 1 helper h
+template <bool DBG>
 __device__ __forceinline__ void dag_run(const DagK& a, int role) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const Lay L(a);
@@ -1124,7 +1218,7 @@ __device__ __forceinline__ void dag_run(const DagK& a, int role) {
     const int epoch = ld_flag(L.ctl) + 1;
     const size_t bytes = ((size_t)a.NT * a.NT + 4 * (size_t)a.NT) * kTD * 8 + (size_t)a.NT * 4 * kT * 8;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.buf, 0, (int)bytes, 0x00020000);
-    if (role == 0) dag_chain(a, L, rs, epoch, lds);
+    if (role == 0) dag_chain<DBG>(a, L, rs, epoch, lds);
     else dag_helper(a, L, rs, epoch, lds, role - 1);
     // the last workgroup of the problem out advances the epoch counter
     drain_stores();
@@ -1138,9 +1232,10 @@ __device__ __forceinline__ void dag_run(const DagK& a, int role) {
     }
 }
 
+template <bool DBG>
 __global__ __launch_bounds__(256) void k_chol_dag(DagK a) {
     if (a.gate && *a.gate != kPhTrial) return;   // device-driven LM: not in a trial (uniform)
-    dag_run(a, blockIdx.x);
+    dag_run<DBG>(a, blockIdx.x);
 }
 
 // several independent problems in one launch (the interiors of a nested dissection): problem p
@@ -1151,7 +1246,7 @@ __global__ __launch_bounds__(256) void k_chol_dag_multi(const DagK* __restrict__
     while (p + 1 < np && (int)blockIdx.x >= wg_off[p + 1]) p++;
     const DagK a = ks[p];
     if (a.gate && *a.gate != kPhTrial) return;
-    dag_run(a, blockIdx.x - wg_off[p]);
+    dag_run<false>(a, blockIdx.x - wg_off[p]);
 }
 
 size_t dag_lds_bytes(int NT) {
@@ -1302,9 +1397,10 @@ hipError_t chol_dag_solve(const double* S, int n, const int* row_first, const do
     std::lock_guard<std::mutex> g(ds.m);
     if (d.G > helpers_locked(ds, dev)) return hipErrorInvalidValue;   // a plan made for a larger device
     if (!ds.attr) {
-        const hipError_t e = hipFuncSetAttribute((const void*)k_chol_dag, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 160 * 1024);
-        if (e != hipSuccess) return e;
+        for (const void* f : {(const void*)k_chol_dag<false>, (const void*)k_chol_dag<true>}) {
+            const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            if (e != hipSuccess) return e;
+        }
         ds.attr = true;
     }
     if (ds.has_last && ds.last != st) {   // device-wide order: after the other stream's solve
@@ -1317,7 +1413,8 @@ hipError_t chol_dag_solve(const double* S, int n, const int* row_first, const do
         if (e != hipSuccess) return e;
         ds.handoffs++;
     }
-    hipLaunchKernelGGL(k_chol_dag, dim3((unsigned)(d.G + 1)), dim3(256), dag_lds_bytes(a.NT), st, a);
+    if (dbg) hipLaunchKernelGGL(k_chol_dag<true>, dim3((unsigned)(d.G + 1)), dim3(256), dag_lds_bytes(a.NT), st, a);
+    else hipLaunchKernelGGL(k_chol_dag<false>, dim3((unsigned)(d.G + 1)), dim3(256), dag_lds_bytes(a.NT), st, a);
     const hipError_t e = hipGetLastError();
     if (e == hipSuccess) {
         ds.has_last = true;

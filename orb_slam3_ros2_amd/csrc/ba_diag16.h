@@ -137,15 +137,32 @@ __device__ __forceinline__ double rcp_nr(double a) {   // 1/a: v_rcp_f64 + NR Ne
     for (int i = 0; i < NR; i++) r = fma(r, fma(-a, r, 1.0), r);
     return r;
 }
+// in lane J of each 16-lane row (and only there): t = 0, pown = piv. One opaque asm block per step:
+// as plain selects, the compiler hoisted the 16 loop-invariant lane masks (32 SGPRs) out of the
+// solve loop and spilled them. (Lane J cannot be left out by EXEC instead: it is the DPP source.)
+template <int J>
+__device__ __forceinline__ void lane_j_pick(double& t, double& pown, double piv, int c) {
+    const unsigned long long tb = __builtin_bit_cast(unsigned long long, t), pb = __builtin_bit_cast(unsigned long long, pown),
+                             vb = __builtin_bit_cast(unsigned long long, piv);
+    unsigned tl = (unsigned)tb, th = (unsigned)(tb >> 32), pl = (unsigned)pb, ph = (unsigned)(pb >> 32);
+    unsigned long long m;
+    asm("v_cmp_eq_u32 %[m], %[j], %[c]\n\t"
+        "v_cndmask_b32 %[tl], %[tl], 0, %[m]\n\t"
+        "v_cndmask_b32 %[th], %[th], 0, %[m]\n\t"
+        "v_cndmask_b32 %[pl], %[pl], %[vl], %[m]\n\t"
+        "v_cndmask_b32 %[ph], %[ph], %[vh], %[m]"
+        : [tl] "+v"(tl), [th] "+v"(th), [pl] "+v"(pl), [ph] "+v"(ph), [m] "=&s"(m)
+        : [vl] "v"((unsigned)vb), [vh] "v"((unsigned)(vb >> 32)), [c] "v"(c), [j] "n"(J));
+    t = __builtin_bit_cast(double, (unsigned long long)th << 32 | tl);
+    pown = __builtin_bit_cast(double, (unsigned long long)ph << 32 | pl);
+}
 template <int J, int NR>
 __device__ __forceinline__ void dpp16_step(double (&v)[16], double& pown, int c) {
     if constexpr (J < 16) {
         const double piv = bcast16<J>(v[J]);
-        const bool me = c == J;
-        const double u = me ? 0.0 : -v[J];
         const double r = rcp_nr<NR>(piv);
-        pown = me ? piv : pown;   // lane J keeps its pivot
-        const double t = u * r;
+        double t = -v[J] * r;
+        lane_j_pick<J>(t, pown, piv, c);   // lane J: t = 0 (its column stays), pown = its pivot
         Dpp16Step<J>::first(v, t);
         Dpp16Step<J>::rest(v, t);
         dpp16_step<J + 1, NR>(v, pown, c);
@@ -153,21 +170,35 @@ __device__ __forceinline__ void dpp16_step(double (&v)[16], double& pown, int c)
 }
 // v: column lane & 15 of the tile (rows 0..15, every 16-lane row the same); lv: Linv in the MFMA C
 // layout (lane (c, g), component q: Linv[g + 4q][c]). False in every lane on a non-positive (or
-// NaN) pivot. The per-lane pivot d_c gives 1/d_c and s_c; s_i of the lane's rows comes from lane i.
+// NaN) pivot. The raw columns go through scr (272 doubles of LDS, this wave's) into the C layout,
+// where each lane scales its four rows: selecting register g + 4q per lane in registers made the
+// compiler index the column array, i.e. put it in scratch memory.
 template <int NR = 1>
-__device__ __forceinline__ bool diag16_dpp(double (&v)[16], double4_t& lv) {
+__device__ __forceinline__ bool diag16_dpp(double (&v)[16], double* __restrict__ scr, double4_t& lv) {
     const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
     double pown = 1.0;
     dpp16_step<0, NR>(v, pown, c);
     const bool bad = __any(!(pown > 0.0));
     const double rown = rcp_nr<NR>(pown), sown = rsq_nr<NR>(pown);
+    if (g == 0) {
+#pragma unroll
+        for (int i = 0; i < 16; i++) scr[16 * i + c] = v[i];
+        scr[256 + c] = sown;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const double nr = -rown;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        const double x = g == 0 ? v[4 * q] : (g == 1 ? v[4 * q + 1] : (g == 2 ? v[4 * q + 2] : v[4 * q + 3]));
         const int i = g + 4 * q;
-        const double si = __shfl(sown, i, 64);
-        lv[q] = i > c ? -x * rown * si : (i == c ? sown : 0.0);
+        const double x = scr[16 * i + c], si = scr[256 + i];
+        const double p = x * nr * si;
+        double o = i == c ? sown : 0.0;
+        o = i > c ? p : o;
+        lv[q] = o;
     }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
     return !bad;
 }
 

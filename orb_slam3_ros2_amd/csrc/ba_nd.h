@@ -77,6 +77,6 @@ void nd_timeout_words(const NdWorkspace* w, std::vector<const int*>& out);
 
 // test hook: A (6 np dense SPD, structure given by the pose blocks), b -> x; reps timed solves
 int nd_test(const double* A, const double* b, double* x, int np, const int* bi, const int* bj, int nblk, int K,
-            int reps, float* ms, int* K_used);
+            int reps, float* ms, int* K_used, float* stage_ms = nullptr, int* seg_out = nullptr);
 
 }  // namespace orbhip

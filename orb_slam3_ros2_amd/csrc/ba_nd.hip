@@ -654,10 +654,12 @@ hipError_t nd_solve(NdWorkspace* W, hipStream_t st) {
 }
 
 int nd_test(const double* A, const double* b, double* x, int np, const int* bi, const int* bj, int nblk, int K,
-            int reps, float* ms, int* K_used) {
+            int reps, float* ms, int* K_used, float* stage_ms, int* seg_out) {
     NdPlan P;
     if (!nd_plan(np, bi, bj, nblk, K, P)) return -5;
     if (K_used) *K_used = P.K;
+    if (seg_out)   // segment starts (pose index), K + 1 entries, and the band's half-width last
+        for (int r = 0; r <= P.K; r++) seg_out[r] = (int)((long long)r * np / P.K);
     const int n = 6 * np;
     double *dA = nullptr, *db = nullptr, *dx = nullptr;
     int* dflag = nullptr;
@@ -685,6 +687,20 @@ int nd_test(const double* A, const double* b, double* x, int np, const int* bi, 
         float t = 0;
         ok(hipEventElapsedTime(&t, e0, e1));
         if (ms) *ms = t / std::max(1, reps);
+        if (stage_ms && rc == 0) {   // the two halves alone: interiors + assembly, separator + back-substitution
+            for (int st = 0; st < 2; st++) {
+                ok(hipEventRecord(e0, nullptr));
+                for (int r = 0; r < reps && rc == 0; r++)
+                    ok(st == 0 ? nd_factor_assemble(W, nullptr) : nd_separator_backsolve(W, nullptr));
+                ok(hipEventRecord(e1, nullptr));
+                ok(hipDeviceSynchronize());
+                float ts = 0;
+                ok(hipEventElapsedTime(&ts, e0, e1));
+                stage_ms[st] = ts / std::max(1, reps);
+            }
+            ok(nd_solve(W, nullptr));   // x and the flags of a whole solve again
+            ok(hipDeviceSynchronize());
+        }
         int f = 0;
         ok(hipMemcpy(&f, dflag, sizeof(int), hipMemcpyDeviceToHost));
         ok(hipMemcpy(x, dx, sizeof(double) * n, hipMemcpyDeviceToHost));

@@ -1974,6 +1974,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         return *ws->h_stop != 0;
     };
     std::vector<LmState> L(B);
+    bool ctl_with_outputs = false;   // the final LM state is read back with the outputs
     std::vector<int> all(B);
     for (int b = 0; b < B; b++) all[b] = b;
     if (upload_act(all)) return ORBHIP_ERR_DEVICE;
@@ -2226,6 +2227,10 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             }
             if (rc == ORBHIP_OK) rc = wait_ev(ev[(nchunk - 1) & 1]);
             if (rc != ORBHIP_OK) break;
+            if (!rccl && all_done()) {   // every problem ended: its LM state comes with the outputs
+                ctl_with_outputs = true;
+                break;
+            }
             if (hipMemcpyAsync(ws->hctl.p, dctl, B * sizeof(LmCtl), hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess) {
                 rc = ORBHIP_ERR_DEVICE;
@@ -2241,13 +2246,9 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         (void)hipEventDestroy(ev[0]);
         (void)hipEventDestroy(ev[1]);
         if (rc != ORBHIP_OK) return rc;
-        for (int b = 0; b < B; b++) {
-            const LmCtl& c = ws->hctl.p[b];
-            L[b].currentChi = c.currentChi;
-            L[b].it = c.it;
-            L[b].trials = c.trials;
-            res[b]->initial_chi2 = c.initChi;
-        }
+        // the LM state read back with the outputs below (one synchronisation for all of it: each
+        // read-back + synchronisation of its own cost ~20-30 us of host round trip at C4)
+        if (ctl_with_outputs) BAOK(hipMemcpyAsync(ws->hctl.p, dctl, B * sizeof(LmCtl), hipMemcpyDeviceToHost, st));
     }
     const double t_solve = now();
     // ---- hand-off timeouts of the persistent solver: a timed-out solve fails its trial (flag 0),
@@ -2267,6 +2268,15 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     // ---- outputs: e_chi2 of every problem + optimised poses/points, one transfer ----
     BAOK(hipMemcpyAsync(hd, D, sizeof(double) * (nC + nA), hipMemcpyDeviceToHost, st));
     BAOK(hipStreamSynchronize(st));
+    {   // the LM state of every problem (read back in the loop, or just now with the outputs)
+        for (int b = 0; b < B; b++) {
+            const LmCtl& c = ws->hctl.p[b];
+            L[b].currentChi = c.currentChi;
+            L[b].it = c.it;
+            L[b].trials = c.trials;
+            res[b]->initial_chi2 = c.initChi;
+        }
+    }
     {
         int timeouts = 0;
         for (int i = 0; i < ndag; i++) timeouts += ws->hto.p[i];

@@ -1522,6 +1522,14 @@ int orbhip_test_nd_solve(const double* A, const double* b, double* x, int np, co
     if (!A || !b || !x || np <= 0 || !bi || !bj || nblk <= 0 || reps < 1) return ORBHIP_ERR_ARG;
     return nd_test(A, b, x, np, bi, bj, nblk, K, reps, ms, K_used);
 }
+// the same, with the two halves timed alone (stage_ms[0]: interior factorizations + separator
+// assembly, stage_ms[1]: separator solve + interior back-substitution) and the plan's segment
+// starts (seg_out: K + 1 pose indices; capacity 65)
+int orbhip_test_nd_stages(const double* A, const double* b, double* x, int np, const int* bi, const int* bj, int nblk,
+                          int K, int reps, float* ms, int* K_used, float* stage_ms, int* seg_out) {
+    if (!A || !b || !x || np <= 0 || !bi || !bj || nblk <= 0 || reps < 1 || !stage_ms || !seg_out) return ORBHIP_ERR_ARG;
+    return nd_test(A, b, x, np, bi, bj, nblk, K, reps, ms, K_used, stage_ms, seg_out);
+}
 
 int orbhip_test_sincosf(const float* x, float* cs, float* sn, int64_t n) {
     if (!x || !cs || !sn || n <= 0) return ORBHIP_ERR_ARG;

@@ -390,3 +390,30 @@ def synthetic_query_bow(scene, kf, seed, n_words=20000, keep=0.6, noise=80):
     w = np.unique(np.concatenate(parts + [rng.choice(n_words, noise, replace=False)])).astype(np.int32)
     v = rng.gamma(2.0, 1.0, w.shape[0])
     return w, v / v.sum()
+
+
+def banded_pose_system(n_pose, w, cyclic, seed, n_land=None):
+    """A reduced-camera-system-shaped SPD matrix: S = sum of landmark terms v v^T, each over the
+    6-vectors of a window of <= w + 1 consecutive poses (cyclic: windows wrap around, a keyframe
+    loop), + 0.5 I; and the pose blocks (i <= j) of its structure. (399 poses, w = 19, cyclic: the
+    C5 GBA's system) Returns (S, b, block_i, block_j)."""
+    rng = np.random.default_rng(seed)
+    n = 6 * n_pose
+    A = np.zeros((n, n))
+    blocks = set()
+    for _ in range(n_land or 6 * n_pose):
+        s = int(rng.integers(0, n_pose if cyclic else n_pose - w))
+        ln = int(rng.integers(2, w + 2))
+        poses = [(s + k) % n_pose for k in range(ln) if cyclic or s + k < n_pose]
+        idx = np.concatenate([np.arange(6 * p, 6 * p + 6) for p in poses])
+        v = rng.normal(size=idx.size)
+        A[np.ix_(idx, idx)] += np.outer(v, v)
+        for a in poses:
+            for b in poses:
+                blocks.add((min(a, b), max(a, b)))
+    for p in range(n_pose):
+        blocks.add((p, p))
+    A += np.eye(n) * 0.5
+    bi = np.array([b[0] for b in sorted(blocks)], np.int32)
+    bj = np.array([b[1] for b in sorted(blocks)], np.int32)
+    return A, rng.normal(size=n), bi, bj

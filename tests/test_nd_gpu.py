@@ -17,28 +17,8 @@ pytestmark = pytest.mark.gpu
 
 
 def banded_system(n_pose, w, cyclic, seed, n_land=None):
-    """S = sum of landmark terms v v^T, each over the 6-vectors of a window of <= w + 1 consecutive
-    poses (cyclic: windows wrap around), + a small diagonal; pose blocks (i <= j) of its structure."""
-    rng = np.random.default_rng(seed)
-    n = 6 * n_pose
-    A = np.zeros((n, n))
-    blocks = set()
-    for _ in range(n_land or 6 * n_pose):
-        s = int(rng.integers(0, n_pose if cyclic else n_pose - w))
-        ln = int(rng.integers(2, w + 2))
-        poses = [(s + k) % n_pose for k in range(ln) if cyclic or s + k < n_pose]
-        idx = np.concatenate([np.arange(6 * p, 6 * p + 6) for p in poses])
-        v = rng.normal(size=idx.size)
-        A[np.ix_(idx, idx)] += np.outer(v, v)
-        for a in poses:
-            for b in poses:
-                blocks.add((min(a, b), max(a, b)))
-    for p in range(n_pose):
-        blocks.add((p, p))
-    A += np.eye(n) * 0.5
-    bi = np.array([b[0] for b in sorted(blocks)], np.int32)
-    bj = np.array([b[1] for b in sorted(blocks)], np.int32)
-    return A, rng.normal(size=n), bi, bj
+    from orb_slam3_ros2_amd.synthetic import banded_pose_system
+    return banded_pose_system(n_pose, w, cyclic, seed, n_land)
 
 
 def nd_solve(A, b, n_pose, bi, bj, K=0, reps=1):

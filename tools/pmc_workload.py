@@ -8,6 +8,7 @@ kernel's counters are not mixed across regimes:
   c4    the C4-sized dense reduced camera system (n = 294) solved by k_chol_dag, 2 x 21 solves
   c4lba C4 LocalBundleAdjustment (50 KF / 2000 pts / 8000 obs, 10 LM iterations), 3 solves
   c5    the C5-sized dense reduced camera system (n = 2394) solved by k_chol_dag, 2 x 21 solves
+  c5nd  the nested-dissection solve the C5 GBA runs (399 poses, cyclic band 19), 2 x 61 solves
 """
 import ctypes
 import os
@@ -41,6 +42,9 @@ elif mode == "c4lba":
 elif mode == "c5":
     for _ in range(2):
         bench.ba_cholesky_roofline(2394, "c5")
+elif mode == "c5nd":
+    for _ in range(2):
+        bench.ba_nd_roofline()
 else:
     raise SystemExit(f"unknown mode {mode}")
 torch.cuda.synchronize()

@@ -63,4 +63,5 @@ for n_s, shape in cases:
         m = np.median(sub, axis=0).astype(int)
         print(f"    sub-phases (median cycles from the interval start): w0 diagA {m[0]} D(1,*) in {m[1]} diagB {m[2]} | "
               f"w2 loads {m[4]} L(k+2,k) {m[5]} T/D' {m[6]} L(k+1,k) in {m[7]} | "
-              f"w3 loads {m[8]} L(k+2,k) {m[9]} T/D' {m[10]} L(k+1,k) in {m[11]}", flush=True)
+              f"w3 loads {m[8]} L(k+2,k) {m[9]} T/D' {m[10]} L(k+1,k) in {m[11]} | w0 y {m[3]} "
+              f"| W23 form: w2 T {m[12]} D' {m[13]} w3 T {m[14]} D' {m[15]}", flush=True)

@@ -57,17 +57,19 @@ __global__ __launch_bounds__(64) void k_dpp16(const double* __restrict__ A, doub
     const int lane = threadIdx.x, c = lane & 15, rg = lane >> 4;
     const double* a = A + (size_t)blockIdx.x * 256;
     double* L = Linv + (size_t)blockIdx.x * 256;
+    __shared__ double scr[272];
     double v[16];
     double4_t lv;
 #pragma unroll
     for (int i = 0; i < 16; i++) v[i] = a[i * 16 + c];
-    const bool ok = diag16_dpp(v, lv);
+    const bool ok = diag16_dpp(v, scr, lv);
 #pragma unroll
     for (int q = 0; q < 4; q++) L[(rg + 4 * q) * 16 + c] = lv[q];
     if (lane == 0) okf[blockIdx.x] = ok;
 }
 __global__ __launch_bounds__(64) void k_dpp16_loop(const double* __restrict__ A, double* __restrict__ Linv, int reps) {
     const int lane = threadIdx.x, c = lane & 15, rg = lane >> 4;
+    __shared__ double scr[272];
     double v0[16];
     double4_t lv = {0, 0, 0, 0};
 #pragma unroll
@@ -77,7 +79,7 @@ __global__ __launch_bounds__(64) void k_dpp16_loop(const double* __restrict__ A,
         const double z = lv[0] + lv[1] + lv[2] + lv[3];
 #pragma unroll
         for (int i = 0; i < 16; i++) v[i] = fma(0.0, z, v0[i]);   // a dependency on the previous result
-        diag16_dpp(v, lv);
+        diag16_dpp(v, scr, lv);
     }
 #pragma unroll
     for (int q = 0; q < 4; q++) Linv[(rg + 4 * q) * 16 + c] = lv[q];
