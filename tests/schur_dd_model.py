@@ -1,4 +1,8 @@
-"""Domain decomposition of the C5 reduced camera system over ranks (SURVEY.md §8e, row "GBA
+"""Test-side model (moved out of the product package in r05): the r03 torch restatement of the
+distributed C5 step, superseded on the device by csrc/ba_nd.hip (segment-dissected, device-driven).
+Kept as the arithmetic reference of tests/test_schur_dd_dist.py and tools/model_c5_dd.py.
+
+Domain decomposition of the C5 reduced camera system over ranks (SURVEY.md §8e, row "GBA
 sharded"): the distributed LM step's linear solve.
 
 Why: with landmark shards (sharding.py) every rank builds a partial reduced camera system S and an

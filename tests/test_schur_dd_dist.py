@@ -1,4 +1,4 @@
-"""The distributed C5 step's arithmetic (orb_slam3_ros2_amd/schur_dd.py, DESIGN.md §C5 sharding):
+"""The distributed C5 step's arithmetic (tests/schur_dd_model.py, DESIGN.md §C5 sharding):
 nested dissection of the reduced camera system by keyframe segments. Each rank eliminates its
 interior, one all-reduce sums the separator system, every rank solves it, an all-gather collects
 the interiors; the result equals the full solve. gloo world size 2 on the CPU; the C5 shape (400
@@ -21,7 +21,7 @@ def _worker(rank, port, q):
     import torch
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     try:
-        from orb_slam3_ros2_amd.schur_dd import Partition, covisibility_system, dd_solve
+        from schur_dd_model import Partition, covisibility_system, dd_solve
         part = Partition(40, WORLD, 5)
         Ss, bs = covisibility_system(part, 400, seed=1)   # every rank builds all, keeps its own
         x = dd_solve(torch.from_numpy(Ss[rank]), torch.from_numpy(bs[rank]), part, rank).numpy()
@@ -50,7 +50,7 @@ def test_dd_solve_gloo_matches_full_solve():
 
 
 def test_partial_systems_live_on_their_segment():
-    from orb_slam3_ros2_amd.schur_dd import Partition, covisibility_system
+    from schur_dd_model import Partition, covisibility_system
     part = Partition(48, 4, 6)
     Ss, _ = covisibility_system(part, 600, seed=2)
     for r, S in enumerate(Ss):
@@ -63,7 +63,7 @@ def test_partial_systems_live_on_their_segment():
 
 
 def test_dd_solve_c5_shape_in_process():
-    from orb_slam3_ros2_amd.schur_dd import Partition, covisibility_system, dd_solve_local
+    from schur_dd_model import Partition, covisibility_system, dd_solve_local
     part = Partition(400, 8, 20)
     Ss, bs = covisibility_system(part, 6000, seed=3)
     x = dd_solve_local(Ss, bs, part).numpy()
@@ -77,7 +77,7 @@ def test_two_level_dissection_of_the_separator_system():
     19 keyframes): a second dissection level (odd separators as interiors, 4 ranks) solves it
     exactly too (the model of DESIGN.md §C5 sharding prices both levels)."""
     import torch
-    from orb_slam3_ros2_amd.schur_dd import (Partition, covisibility_system, dd_local, dd_solve_local,
+    from schur_dd_model import (Partition, covisibility_system, dd_local, dd_solve_local,
                                              split_assembled)
     part = Partition(400, 8, 20)
     Ss, bs = covisibility_system(part, 6000, seed=4)
@@ -98,7 +98,7 @@ def test_two_level_dissection_of_the_separator_system():
 def test_c5_landmarks_fit_one_window():
     """Premise of the partition on the bench's C5 problem: every landmark is observed by keyframes
     within one cyclic 20-keyframe window, so it touches at most one segment interior."""
-    from orb_slam3_ros2_amd.schur_dd import Partition
+    from schur_dd_model import Partition
     from orb_slam3_ros2_amd.synthetic import synthetic_ba_problem
     prob, _ = synthetic_ba_problem(n_kf=400, n_pts=20000, layout="loop", window=20, seed=11)
     part = Partition(400, 8, 20)

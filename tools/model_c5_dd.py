@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Measured pieces of the modelled 8-rank C5 step (DESIGN.md §C5 sharding, schur_dd.py): the
+"""Measured pieces of the modelled 8-rank C5 step (DESIGN.md §C5 sharding, tests/schur_dd_model.py): the
 persistent DAG Cholesky (k_chol_dag, the kernel the LM loop launches) on
   - the full C5-structured system (n = 2400, cyclic 20-KF band: the 1-GPU solve),
   - one rank's local system Z_{r-1} + I_r + Z_r (n = 414, interior first: an upper bound of the
@@ -20,7 +20,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402,F401
 
 from orb_slam3_ros2_amd._lib import lib  # noqa: E402
-from orb_slam3_ros2_amd.schur_dd import Partition, covisibility_system, dd_local, split_assembled  # noqa: E402
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+from schur_dd_model import Partition, covisibility_system, dd_local, split_assembled  # noqa: E402
 
 
 def dag_ms(S, reps=20):
