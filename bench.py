@@ -493,14 +493,16 @@ def cpu_lba(prob, budget_s=8.0):
 
 def c5_gba(ws, rank, iters):
     """C5 GlobalBundleAdjustment (400 KF loop, 20k points, 80k obs, 20-KF co-visibility window).
-    One GPU: the nested-dissection solve of the reduced camera system (csrc/ba_nd.hip). With N > 1
-    the default is replicas (every rank its own GBA: the modelled 8-rank segment-sharded trial is
-    slower than one GPU). ORBHIP_C5_SHARDED=1: the keyframe loop cut into N segments,
-    rank r holding segment r's landmarks (sharding.shard_problem_nd): each rank factors its
-    interior, the separator system and the pose update are all-reduced over RCCL inside the
-    device-driven LM (orbhip_ba_solve_sharded); a segment plan that does not fit
-    (too many ranks for the loop) falls back to contiguous landmark shards with the summed reduced
-    camera system. Time = max over ranks of one solve."""
+    One GPU: the nested-dissection solve of the reduced camera system (csrc/ba_nd.hip), and beside it
+    the same solve in its sharded form on one RCCL rank holding all 8 segments
+    (orbhip_ba_solve_sharded_segments: every collective of the sharded slot through RCCL).
+    N > 1: c5_gba_ms is the sharded solve (ORBHIP_C5_SHARDED=0 turns it off): the keyframe loop cut
+    into N segments, rank r holding segment r's landmarks (sharding.shard_problem_nd); each rank
+    factors its interior, the separator system and the pose update are all-reduced over RCCL inside
+    the device-driven LM; a segment plan that does not fit (too many ranks for the
+    loop) falls back to contiguous landmark shards with the summed reduced camera system. Replicas
+    (every rank its own whole GBA) are timed beside it as c5_gba_replica_ms. Time = max over ranks of
+    one solve, after one untimed solve."""
     import torch
     from orb_slam3_ros2_amd import Optimizer
     from orb_slam3_ros2_amd.sharding import nd_segments, pose_blocks, shard_problem, shard_problem_nd
@@ -508,33 +510,50 @@ def c5_gba(ws, rank, iters):
     prob, _ = synthetic_ba_problem(n_kf=400, n_pts=20000, layout="loop", window=20, seed=11)
     prob.iterations, prob.huber_delta = iters, float(np.sqrt(5.99))   # BundleAdjustment(bRobust)
     opt = Optimizer()
-    sharded = ws > 1 and os.environ.get("ORBHIP_C5_SHARDED", "0") == "1"
-    mode = f"replicas x{ws} (one GPU per solve, nested dissection)"
+
+    def run(solve):
+        solve()
+        _barrier(ws)
+        t0 = time.perf_counter()
+        r = solve()
+        torch.cuda.synchronize()
+        _barrier(ws)
+        return r, _max_over_ranks(ws, time.perf_counter() - t0)
+
+    out = {"c5_problem": "400 KF loop / 20000 pts / 80000 obs, n = 2394"}
+    sharded = ws > 1 and os.environ.get("ORBHIP_C5_SHARDED", "1") == "1"
     if sharded:
         import torch.distributed as dist
         uid = [Optimizer.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
-        opt.comm_init(ws, rank, uid[0])
+        sopt = Optimizer()
+        sopt.comm_init(ws, rank, uid[0])
         if nd_segments(*pose_blocks(prob), ws) is not None:
             shard = shard_problem_nd(prob, rank, ws)[0]
             mode = f"rccl segments x{ws} (interiors per rank, separator system all-reduced)"
         else:
             shard = shard_problem(prob, rank, ws)[0]
             mode = f"rccl landmark shards x{ws} (reduced camera system all-reduced, replicated solve)"
-        solve = lambda: opt.solve_sharded(shard)  # noqa: E731
+        r, t = run(lambda: sopt.solve_sharded(shard))
+        rr, tr = run(lambda: opt.solve(prob))
+        out["c5_gba_replica_ms"] = round(1e3 * tr, 2)
+        out["c5_gba_replica_mode"] = f"replicas x{ws} (one GPU per solve, nested dissection)"
+        out["c5_gba_scaling_note"] = ("the sharded N-rank time is the driver's first measurement of it: no multi-GPU "
+                                      "run was available to this build (DESIGN.md, C5 sharding)")
     else:
-        solve = lambda: opt.solve(prob)  # noqa: E731
-    solve()
-    _barrier(ws)
-    t0 = time.perf_counter()
-    r = solve()
-    torch.cuda.synchronize()
-    _barrier(ws)
-    t = _max_over_ranks(ws, time.perf_counter() - t0)
-    return {"c5_gba_ms": round(1e3 * t, 2), "c5_gba_iterations": r.iterations_done, "c5_gba_trials": r.lm_trials,
-            "c5_gba_chi2": [round(r.initial_chi2, 1), round(r.final_chi2, 1)],
-            "c5_gba_mode": mode,
-            "c5_problem": "400 KF loop / 20000 pts / 80000 obs, n = 2394"}
+        mode = f"replicas x{ws} (one GPU per solve, nested dissection)" if ws > 1 else \
+            "one GPU (nested dissection, device-driven LM)"
+        r, t = run(lambda: opt.solve(prob))
+        if ws == 1:   # the sharded form's collectives on one RCCL rank holding all 8 segments
+            sopt = Optimizer()
+            sopt.comm_init(1, 0, Optimizer.comm_unique_id())
+            segs = [shard_problem_nd(prob, q, 8)[0] for q in range(8)]
+            rs, ts = run(lambda: sopt.solve_sharded_segments(segs))
+            out["c5_gba_rccl_1rank_8seg_ms"] = round(1e3 * ts, 2)
+            out["c5_gba_rccl_1rank_8seg_trials"] = rs[0].lm_trials
+    out.update({"c5_gba_ms": round(1e3 * t, 2), "c5_gba_iterations": r.iterations_done, "c5_gba_trials": r.lm_trials,
+                "c5_gba_chi2": [round(r.initial_chi2, 1), round(r.final_chi2, 1)], "c5_gba_mode": mode})
+    return out
 
 
 def cpu_gba(iters_sample=3, iters=10):
@@ -910,7 +929,9 @@ def ba_nd_roofline(reps=20):
     well (HIP events, `reps` solves each). Algorithmic flops of one solve: every
     interior's banded factorization n_I b^2 with b = 6 w, plus its Schur contribution to its two
     separators n_I (2b)^2, plus the separator system's dense Cholesky n_Z^3 / 3 + 2 n_Z^2,
-    n_Z = 6 w K. Counters: rocprofv3 --pmc passes of tools/pmc_workload.py c5nd."""
+    n_Z = 6 w K; with the second level (K >= 6) the separator part is its own interiors (n_I = b or
+    2b, the same banded terms) plus the dense remainder n_Zd = b K / 2. Counters: rocprofv3 --pmc
+    passes of tools/pmc_workload.py c5nd."""
     from orb_slam3_ros2_amd._lib import lib
     from orb_slam3_ros2_amd.synthetic import banded_pose_system
     n_pose, w = 399, 19
@@ -932,14 +953,22 @@ def ba_nd_roofline(reps=20):
     n_int = [6 * (seg[r + 1] - seg[r] - w) for r in range(K)]
     n_z = 6 * w * K
     fl_int = sum(ni * bw * bw + ni * (2 * bw) ** 2 for ni in n_int)
-    fl_sep = n_z ** 3 / 3 + 2 * n_z * n_z
+    # the second level (ba_nd.hip nd_inner_plan; cyclic, K >= 6, ORBHIP_ND_LEVELS != 1): the even
+    # separators are the interiors of the separator system (the last inner segment of an odd K
+    # holds two), the K // 2 odd ones its dense part
+    two = os.environ.get("ORBHIP_ND_LEVELS", "2") != "1" and K >= 6
+    n_int2 = [bw * (2 if (K % 2 and r == K // 2 - 1) else 1) for r in range(K // 2)] if two else []
+    n_zd = bw * (K // 2) if two else n_z
+    fl_int2 = sum(ni * bw * bw + ni * (2 * bw) ** 2 for ni in n_int2)
+    fl_sep = fl_int2 + n_zd ** 3 / 3 + 2 * n_zd * n_zd
     flops = fl_int + fl_sep
     err = float(np.abs(A @ x - b).max() / np.abs(b).max())
     ach = flops / (ms.value * 1e-3) / 1e12
     out = {"kernels": "k_chol_dag_multi + k_nd_assemble + k_chol_dag (separator) + k_nd_backsolve + k_nd_finish",
            "bound": "mfma", "achieved": round(ach, 4), "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
            "frac": round(ach / FP64_MFMA_PEAK_TFS, 6), "n": int(A.shape[0]), "segments": K, "band_poses": w,
-           "n_interiors": n_int, "n_separator": n_z, "flops_per_solve": int(flops),
+           "n_interiors": n_int, "n_separator": n_z, "levels": 2 if two else 1, "n_interiors_level2": n_int2,
+           "n_separator_dense": n_zd, "flops_per_solve": int(flops),
            "flops_interiors": int(fl_int), "flops_separator": int(fl_sep), "avg_solve_ms": round(ms.value, 4),
            "interiors_and_assembly_ms": round(stage[0], 4), "separator_and_backsolve_ms": round(stage[1], 4),
            "residual": err, "counters": {k: load_counters(k, "c5nd") for k in

@@ -451,12 +451,18 @@ int orbhip_search_bow(orbhip_ctx* ctx, const uint8_t* kf_desc, const float* kf_a
  *   orbhip_comm_init       collective over the ranks: creates the context's communicator
  *   orbhip_ba_solve_sharded  collective: this rank's shard (all poses, its landmarks/edges);
  *                            the stop flag is agreed on (max over ranks) at each iteration
+ *   orbhip_ba_solve_sharded_segments  collective: this rank holds nlocal consecutive shards
+ *                            (segments rank*nlocal .. rank*nlocal+nlocal-1 of nranks*nlocal; the
+ *                            same nlocal on every rank, else ORBHIP_ERR_ARG); they are summed on
+ *                            the device, then all-reduced over the ranks
  *   orbhip_ba_solve_shards_local  the same decomposition with all shards in one process on one
  *                            device (the sums run on the device): single-GPU model and test. */
 int orbhip_comm_unique_id(uint8_t* id128);
 int orbhip_comm_init(orbhip_ctx* ctx, int nranks, int rank, const uint8_t* id128);
 int orbhip_ba_solve_sharded(orbhip_ctx* ctx, const orbhip_ba_problem* shard, orbhip_ba_result* res,
                             const volatile int* stop_flag);
+int orbhip_ba_solve_sharded_segments(orbhip_ctx* ctx, const orbhip_ba_problem* shards, int nlocal,
+                                     orbhip_ba_result* res, const volatile int* stop_flag);
 int orbhip_ba_solve_shards_local(orbhip_ctx* ctx, const orbhip_ba_problem* shards, int nshards,
                                  orbhip_ba_result* res, const volatile int* stop_flag);
 

@@ -108,7 +108,8 @@ EXPORTED = ["orbhip_abi_version", "orbhip_create", "orbhip_destroy", "orbhip_lev
             "orbhip_extract", "orbhip_extract_batch_device", "orbhip_descriptor_distance", "orbhip_match_bf",
             "orbhip_match_pairs_device", "orbhip_match_frames_device", "orbhip_profile_stage",
             "orbhip_profile_collect", "orbhip_launch_graphs", "orbhip_ba_solve", "orbhip_ba_solve_batch", "orbhip_ba_stats", "orbhip_bgr_to_gray_device",
-            "orbhip_comm_unique_id", "orbhip_comm_init", "orbhip_ba_solve_sharded", "orbhip_ba_solve_shards_local",
+            "orbhip_comm_unique_id", "orbhip_comm_init", "orbhip_ba_solve_sharded", "orbhip_ba_solve_sharded_segments",
+            "orbhip_ba_solve_shards_local",
             "orbhip_vocab_create", "orbhip_vocab_load_text", "orbhip_vocab_destroy", "orbhip_vocab_info",
             "orbhip_bow_transform", "orbhip_bow_transform_device", "orbhip_search_bow",
             "orbhip_pose_optimization", "orbhip_pose_optimization_batch", "orbhip_search_by_projection_last",
@@ -160,6 +161,7 @@ def lib():
     L.orbhip_comm_unique_id.argtypes = [vp]
     L.orbhip_comm_init.argtypes = [vp, i32, i32, vp]
     L.orbhip_ba_solve_sharded.argtypes = [vp, ctypes.POINTER(BAProblemC), ctypes.POINTER(BAResultC), vp]
+    L.orbhip_ba_solve_sharded_segments.argtypes = [vp, ctypes.POINTER(BAProblemC), i32, ctypes.POINTER(BAResultC), vp]
     L.orbhip_ba_solve_shards_local.argtypes = [vp, ctypes.POINTER(BAProblemC), i32, ctypes.POINTER(BAResultC), vp]
     L.orbhip_bgr_to_gray_device.argtypes = [vp, vp, i32, i32, i32, i32, ctypes.c_int64, vp, i32, ctypes.c_int64, vp]
     L.orbhip_profile_stage.argtypes = [vp, i32]

@@ -60,7 +60,11 @@ struct DagDev {
 // done, [7 + 4h] rows of L(k+1, k) in.
 constexpr int kDbgSubK = 100;
 constexpr int kDbgSubOff = 8 + 6 * 200;
-constexpr int kDbgWords = kDbgSubOff + 16 * kDbgSubK;
+// then the backward steps R (chain-only form, R < kDbgBackR): [3R] wave 0 step start, [3R+1] wave 0
+// x_{R-1} formed, [3R+2] wave 1 row R subtracted (cycles from the backward's start)
+constexpr int kDbgBackR = 128;
+constexpr int kDbgBackOff = kDbgSubOff + 16 * kDbgSubK;
+constexpr int kDbgWords = kDbgBackOff + 3 * kDbgBackR;
 hipError_t chol_dag_solve(const double* S, int n, const int* row_first, const double* bs, double* x, int* flag,
                           const DagDev& d, hipStream_t st, const int* gate = nullptr,
                           unsigned long long* dbg = nullptr);

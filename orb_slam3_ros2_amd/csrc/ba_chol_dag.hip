@@ -53,6 +53,12 @@ constexpr int kNewton = ORBHIP_DAG_NEWTON;   // Newton steps after v_rsq_f64 / v
 #ifndef ORBHIP_DAG_DIAG_DPP
 #define ORBHIP_DAG_DIAG_DPP 1   // r05: the 16x16 diagonal factorizations by DPP elimination (diag16_dpp)
 #endif
+#ifndef ORBHIP_DAG_FLAG_AHEAD
+#define ORBHIP_DAG_FLAG_AHEAD 1   // waves 2/3 load the next interval's helper flag before the barrier
+#endif
+#ifndef ORBHIP_DAG_BACK_COL
+#define ORBHIP_DAG_BACK_COL 1   // r05: the chain-only backward on column-major tile loads (bwd_col_dot)
+#endif
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) int gint;
@@ -427,6 +433,39 @@ __device__ __forceinline__ bool chain_factor(const double* Dx, double* scr, doub
     return ok;
 }
 
+// column c = lane & 31 of a tile, rows 16 hh .. 16 hh + 15 (hh = lane >> 5), from its quadrant
+// layout (sc1 loads): the backward's L^T x then needs 16 lane-local FMAs and one half-wave sum
+// instead of eight 16-lane reductions
+__device__ __forceinline__ void tcol(__amdgpu_buffer_rsrc_t rs, int dbl_off, double (&v)[16]) {
+    const int lane = threadIdx.x & 63, c = lane & 31, hh = lane >> 5;
+    const int base = dbl_off + (2 * hh + (c >> 4)) * 256 + 64 * (c & 3) + ((c & 15) >> 2);
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const auto u = __builtin_amdgcn_raw_buffer_load_b64(rs, (base + 4 * i) * 8, 0, 16);
+        v[i] = mk64(u[0], u[1]);
+    }
+}
+// sum over the two half-waves (lane l and l ^ 32), the same bits in both
+__device__ __forceinline__ double half32_sum(double v) {
+    const auto tl = __builtin_amdgcn_permlane32_swap(lo32(v), lo32(v), false, false);
+    const auto th = __builtin_amdgcn_permlane32_swap(hi32(v), hi32(v), false, false);
+    return mk64(tl[0], th[0]) + mk64(tl[1], th[1]);
+}
+// (T^T x)[c] for a tile column held by tcol and x (32 doubles in LDS): every lane of column c
+// returns it
+__device__ __forceinline__ double bwd_col_dot(const double (&v)[16], const double* x) {
+    const double* xh = x + 16 * ((threadIdx.x & 63) >> 5);
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+#pragma unroll
+    for (int i = 0; i < 16; i += 4) {
+        s0 = fma(v[i], xh[i], s0);
+        s1 = fma(v[i + 1], xh[i + 1], s1);
+        s2 = fma(v[i + 2], xh[i + 2], s2);
+        s3 = fma(v[i + 3], xh[i + 3], s3);
+    }
+    return half32_sum((s0 + s1) + (s2 + s3));
+}
+
 // the contribution L^T x of one tile (4 quadrants q0..q3 of this lane) to the 32 columns: lanes with
 // (lane & 15) == 0 receive column 16b + rg + 4q in out[b][q]
 __device__ __forceinline__ void tile_lt_x(const double4_t* t, const double* x, double (&out)[2][4]) {
@@ -685,7 +724,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         const bool need3 = f3 != nullptr;
         // the flag was loaded at the end of the previous interval (fvp), so its round trip overlaps
         // the interval barrier; interval 0 loads it here
-        const int fv = k == 0 ? ld_flag(need3 ? f3 : L.ctl) : fvp;
+        const int fv = (k == 0 || !ORBHIP_DAG_FLAG_AHEAD) ? ld_flag(need3 ? f3 : L.ctl) : fvp;
         if (wid == 0) {
             if (dbg && lane == 0) wts[6] = __builtin_amdgcn_s_memtime() - tk;
             // row 0 of L(k+1, k) = T Linv_k^T
@@ -926,7 +965,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 sq(TpN + (2 * h + 1) * 256, t[1]);
             }
         }
-        if (wid >= 2 && k + 1 < kEnd) {
+        if (ORBHIP_DAG_FLAG_AHEAD && wid >= 2 && k + 1 < kEnd) {
             const int* fn = helper_flag(k + 1);
             fvp = ld_flag(fn ? fn : L.ctl);
         }
@@ -1005,7 +1044,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         s += dpp64<0xB1>(s);
         if (hh == 0) xs[k * kT + c] = s;
     };
-    auto sub_tile = [&](const double4_t* tl, const double* xR, int j) {   // s_j -= L(R, j)^T x_R
+    [[maybe_unused]] auto sub_tile = [&](const double4_t* tl, const double* xR, int j) {   // s_j -= L(R, j)^T x_R
         double t[2][4];
         tile_lt_x(tl, xR, t);
         if (cc == 0) {
@@ -1073,6 +1112,94 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         __syncthreads();
         if (!word[5]) aborted = true;
     } else {   // short rows (or no helpers): the chain work-group alone
+#if ORBHIP_DAG_BACK_COL
+    // Every tile is final here: the last diagonal tile waited, directly or through the helpers'
+    // partials (which waited on their tiles' flags before publishing), on every tile of L, and
+    // this work-group's own tile stores are drained by the barrier. Wave 0 walks the chain,
+    // x_{R-1} = Linv_{R-1}^T (s_{R-1} - L(R, R-1)^T x_R); waves 1..3 subtract row R's other tiles
+    // from the running sums s_j, j <= R-2. Both read their tiles column-major (tcol), two steps
+    // ahead, and pass one barrier per step.
+    __syncthreads();
+    if (!aborted) {
+        const int c = lane & 31, hh = lane >> 5;
+        if (wid == 0) {
+            double st[2][16], li[2][16];
+            auto load = [&](auto setc, int R) {   // inputs of step R
+                constexpr int S = decltype(setc)::value;
+                if (R >= 1) {
+                    tcol(rs, L.oL + (R * NT + R - 1) * kTD, st[S]);
+                    tcol(rs, L.oLi + (R - 1) * kTD, li[S]);
+                }
+            };
+            auto step = [&](auto setc, int R) {
+                constexpr int S = decltype(setc)::value;
+                if (dbg && lane == 0 && R < kDbgBackR) dbg[kDbgBackOff + 3 * R] = __builtin_amdgcn_s_memtime() - t_fwd;
+                const double p = bwd_col_dot(st[S], xs + R * kT);
+                if (hh == 0) rvec[c] = ys[(R - 1) * kT + c] - p;
+                wave_lds_sync();
+                const double xv = bwd_col_dot(li[S], rvec);
+                load(setc, R - 2);   // step R-2's inputs into this set
+                if (hh == 0) xs[(R - 1) * kT + c] = xv;
+                if (dbg && lane == 0 && R < kDbgBackR) dbg[kDbgBackOff + 3 * R + 1] = __builtin_amdgcn_s_memtime() - t_fwd;
+                lds_barrier();
+            };
+            if (lane < kT) rvec[lane] = ys[(NT - 1) * kT + lane];
+            wave_lds_sync();
+            apply_lt(NT - 1);
+            load(std::integral_constant<int, 0>{}, NT - 1);
+            load(std::integral_constant<int, 1>{}, NT - 2);
+            lds_barrier();
+            for (int R = NT - 1; R >= 1; R -= 2) {
+                step(std::integral_constant<int, 0>{}, R);
+                if (R - 1 >= 1) step(std::integral_constant<int, 1>{}, R - 1);
+            }
+        } else {
+            double pf[2][kPf][16];
+            auto load = [&](auto setc, int R) {   // the first tiles of this wave's share of row R
+                constexpr int S = decltype(setc)::value;
+                if (R >= 2) {
+                    const int j0 = rfl[R] + (wid - 1);
+#pragma unroll
+                    for (int u = 0; u < kPf; u++)
+                        if (j0 + 3 * u <= R - 2) tcol(rs, L.oL + (R * NT + j0 + 3 * u) * kTD, pf[S][u]);
+                }
+            };
+            auto sub = [&](const double (&v)[16], const double* xR, int j) {   // s_j -= L(R, j)^T x_R
+                const double p = bwd_col_dot(v, xR);
+                if (hh == 0) ys[j * kT + c] -= p;
+            };
+            auto step = [&](auto setc, int R) {
+                constexpr int S = decltype(setc)::value;
+                const double* xR = xs + R * kT;
+                if (R >= 2) {
+                    const int j0 = rfl[R] + (wid - 1);
+#pragma unroll
+                    for (int u = 0; u < kPf; u++) {
+                        const int j = j0 + 3 * u;
+                        if (j > R - 2) break;
+                        sub(pf[S][u], xR, j);
+                    }
+                    for (int jb = j0 + 3 * kPf; jb <= R - 2; jb += 3) {
+                        double tl[16];
+                        tcol(rs, L.oL + (R * NT + jb) * kTD, tl);
+                        sub(tl, xR, jb);
+                    }
+                }
+                load(setc, R - 2);   // row R-2's first tiles into this set
+                if (dbg && wid == 1 && lane == 0 && R < kDbgBackR)
+                    dbg[kDbgBackOff + 3 * R + 2] = __builtin_amdgcn_s_memtime() - t_fwd;
+                lds_barrier();
+            };
+            load(std::integral_constant<int, 0>{}, NT - 1);
+            load(std::integral_constant<int, 1>{}, NT - 2);
+            lds_barrier();
+            for (int R = NT - 1; R >= 1; R -= 2) {
+                step(std::integral_constant<int, 0>{}, R);
+                if (R - 1 >= 1) step(std::integral_constant<int, 1>{}, R - 1);
+            }
+        }
+    }
+#else
     if (!aborted && wid != 0) {
         // every tile (R, j), j <= R-2, rows 2.. (16 rows of this wave per round: up to 32 flag
         // loads in flight per lane)
@@ -1122,6 +1249,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         };
         auto step = [&](auto setc, int R) {   // x_{R-1} = Linv_{R-1}^T (s_{R-1} - L(R, R-1)^T x_R)
             constexpr int S = decltype(setc)::value;
+            if (dbg && lane == 0 && R < kDbgBackR) dbg[kDbgBackOff + 3 * R] = __builtin_amdgcn_s_memtime() - t_fwd;
 #pragma unroll
             for (int qd = 0; qd < 4; qd++) sq(Lin + qd * 256, li[S][qd]);
             double t[2][4];
@@ -1138,6 +1266,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             load(setc, R - 2);   // step R-2's inputs into this set
             wave_lds_sync();
             apply_lt(R - 1);
+            if (dbg && lane == 0 && R < kDbgBackR) dbg[kDbgBackOff + 3 * R + 1] = __builtin_amdgcn_s_memtime() - t_fwd;
             lds_barrier();
         };
         if (lane < kT) rvec[lane] = ys[(NT - 1) * kT + lane];
@@ -1183,6 +1312,8 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 }
             }
             load(setc, R - 2);   // row R-2's first tiles into this set
+            if (dbg && wid == 1 && lane == 0 && R < kDbgBackR)
+                dbg[kDbgBackOff + 3 * R + 2] = __builtin_amdgcn_s_memtime() - t_fwd;
             lds_barrier();
         };
         load(std::integral_constant<int, 0>{}, NT - 1);
@@ -1193,6 +1324,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             if (R - 1 >= 1) step(std::integral_constant<int, 1>{}, R - 1);
         }
     }
+#endif
     }
     if (wid == 0 && lane == 0) word[8] = (ok && !aborted) ? 1 : 0;
     __syncthreads();

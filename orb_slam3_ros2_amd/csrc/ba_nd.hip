@@ -313,10 +313,14 @@ struct NdWorkspace {
     DevBuf<double> pack, xl;    // the packed envelope; x_loc and xg (n + 1 each)
     size_t pack_n = 0;
     int nZt = 0;                // tile rows of the separator system
+    NdWorkspace* inner = nullptr;   // the separator system's own dissection (second level), or none
+    bool use_inner = false;
+    ~NdWorkspace();
 };
 
 NdWorkspace* nd_create() { return new NdWorkspace(); }
 void nd_destroy(NdWorkspace* w) { delete w; }
+NdWorkspace::~NdWorkspace() { delete inner; }
 
 void nd_timeout_words(const NdWorkspace* w, std::vector<const int*>& out) {
     out.insert(out.end(), w->tw.begin(), w->tw.end());
@@ -333,6 +337,27 @@ void nd_bandwidth(int np, const int* bi, const int* bj, int nblk, int& wl, int& 
 }
 
 namespace {
+// levels of the dissection: ORBHIP_ND_LEVELS=1 solves the separator system densely; 2 (default)
+// dissects a cyclic separator system of >= 6 separators once more (nd_inner_plan)
+int nd_levels() {
+    const char* e = std::getenv("ORBHIP_ND_LEVELS");
+    return e ? std::max(1, std::atoi(e)) : 2;
+}
+
+// the second level: the K separators of a cyclic dissection, w poses each, as a cyclic chain of
+// K2 = K / 2 segments of two separators (the last one takes a third when K is odd): the even
+// separators become interiors, the odd ones the separators of the separator system
+bool nd_inner_plan(int nsep, int w, NdPlan& p) {
+    if (nsep < 6 || 6 * w <= kT) return false;   // (interiors of one separator: more than one tile)
+    const int K2 = nsep / 2;
+    p = NdPlan{};
+    p.np = nsep * w; p.K = K2; p.w = w; p.cyclic = true;
+    p.seg.assign(K2 + 1, 0);
+    for (int r = 0; r < K2; r++) p.seg[r] = 2 * r * w;
+    p.seg[K2] = nsep * w;
+    return true;
+}
+
 int plan_cost(int np, int w, bool cyc, int k, std::vector<int>& seg) {
     auto tiles = [](int vars) { return (vars + kT - 1) / kT; };
     seg.assign(k + 1, 0);
@@ -342,10 +367,15 @@ int plan_cost(int np, int w, bool cyc, int k, std::vector<int>& seg) {
     for (int r = 0; r < k; r++) {
         const bool own = cyc || r < k - 1;
         const int ni = seg[r + 1] - seg[r] - (own ? w : 0);
-        if (ni < w) return -1;   // interiors at least as wide as the band: a block-tridiagonal separator system
+        // interiors at least as wide as the band (a block-tridiagonal separator system) and longer
+        // than one tile (the partial DAG solve's chain forms two tile rows past its last interval)
+        if (ni < w || 6 * ni <= kT) return -1;
         mi = std::max(mi, tiles(6 * ni));
     }
-    return mi + tiles(6 * w * nsep) + 3;   // + the assembly / back-substitution / launches
+    int sep = tiles(6 * w * nsep);
+    if (cyc && nd_levels() > 1 && nsep >= 6 && 6 * w > kT)   // the separator system dissected once more
+        sep = std::min(sep, tiles(6 * w * (nsep % 2 ? 2 : 1)) + tiles(6 * w * (nsep / 2)) + 3);
+    return mi + sep + 3;   // + the assembly / back-substitution / launches
 }
 }  // namespace
 
@@ -370,7 +400,11 @@ bool nd_plan(int np, const int* bi, const int* bj, int nblk, int K, NdPlan& p) {
     const int w = std::max(1, cyc ? wc : wl);
     std::vector<int> seg;
     int best = -1, bestK = 0;
-    const int k0 = K > 0 ? K : 2, k1 = K > 0 ? K : std::min(32, np / std::max(1, 2 * w));
+    // every segment's factorization needs two workgroups (chain + a helper) resident together: K
+    // is capped by the device's persistent grid (a partitioned or smaller device holds fewer)
+    const int kcap = (dag_max_helpers() + 1) / 2;
+    if (K > kcap) return false;
+    const int k0 = K > 0 ? K : 2, k1 = K > 0 ? K : std::min(std::min(32, kcap), np / std::max(1, 2 * w));
     for (int k = k0; k <= k1; k++) {
         const int c = plan_cost(np, w, cyc, k, seg);
         if (c > 0 && (best < 0 || c < best)) { best = c; bestK = k; }
@@ -609,6 +643,33 @@ int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int 
         d.x_loc = W->xl.p;
         d.xg = W->xl.p + n + 1;
     }
+    // the second level: a cyclic separator system of >= 6 separators is itself dissected (the even
+    // separators eliminated in one more k_chol_dag_multi, the odd ones solved densely), which
+    // replaces the dense solve's chain of nZ / 32 intervals by ~(6w + 6w K/2) / 32 + 3. Every
+    // shard of a distributed solve runs it on the summed system (replicated: the levels' work is
+    // spread over the CUs anyway, a collective per level would only add latency).
+    W->use_inner = false;
+    NdPlan P2;
+    if (cyc && nd_levels() > 1 && nd_inner_plan(nsep, w, P2)) {
+        std::vector<int> b2i, b2j;
+        for (int t = 0; t < nsep; t++)   // every separator's own block
+            for (int p = 0; p < w; p++)
+                for (int q = p; q < w; q++) { b2i.push_back(t * w + p); b2j.push_back(t * w + q); }
+        for (int r = 0; r < K; r++)   // the fill of each segment's elimination: Z_prev x Z_own
+            if (sg[r].prev >= 0 && sg[r].own >= 0)
+                for (int p = 0; p < w; p++)
+                    for (int q = 0; q < w; q++) {
+                        const int a = sg[r].prev * w + p, b = sg[r].own * w + q;
+                        b2i.push_back(std::min(a, b));
+                        b2j.push_back(std::max(a, b));
+                    }
+        if (!W->inner) W->inner = nd_create();
+        const int rc = nd_setup(W->inner, P2, b2i.data(), b2j.data(), (int)b2i.size(), d.SZ, d.bZ,
+                                const_cast<double*>(d.xZ), W->flagZ, gate, st, -1);
+        if (rc != 0) return rc;
+        W->use_inner = true;
+        nd_timeout_words(W->inner, W->tw);
+    }
     return 0;
 }
 
@@ -621,7 +682,9 @@ hipError_t nd_factor_assemble(NdWorkspace* W, hipStream_t st) {
 
 hipError_t nd_separator_backsolve(NdWorkspace* W, hipStream_t st) {
     const NdDev& d = W->dev;
-    hipError_t e = chol_dag_solve(d.SZ, d.nZ, W->rfZ, d.bZ, const_cast<double*>(d.xZ), W->flagZ, W->dZ, st, d.gate);
+    hipError_t e = W->use_inner ? nd_solve(W->inner, st)
+                                : chol_dag_solve(d.SZ, d.nZ, W->rfZ, d.bZ, const_cast<double*>(d.xZ), W->flagZ, W->dZ,
+                                                 st, d.gate);
     if (e != hipSuccess) return e;
     if (d.x_loc && (e = hipMemsetAsync(d.x_loc, 0, sizeof(double) * (d.n + 1), st)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_nd_backsolve, dim3((unsigned)W->K), dim3(256), W->bs_lds, st, d);

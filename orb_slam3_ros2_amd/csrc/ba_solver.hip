@@ -1284,15 +1284,17 @@ __global__ void k_ba_sh_end(const BaArgs* __restrict__ args, const int* __restri
 }
 // the in-process form of a collective over B shards: dst[s][i] = sum (op 0) / max (op 1) over the
 // shards of src[s'][i], in shard order (deterministic); dst may alias src
-__global__ __launch_bounds__(256) void k_ba_multi_reduce(const double* const* __restrict__ src, double* const* __restrict__ dst,
-                                                         int B, size_t count, int op) {
+// sum (op 0) or max (op 1) of nsrc buffers into each of ndst buffers (a destination may alias a
+// source: every element is read before it is written, by the same thread)
+__global__ __launch_bounds__(256) void k_ba_multi_reduce(const double* const* __restrict__ src, int nsrc,
+                                                         double* const* __restrict__ dst, int ndst, size_t count, int op) {
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x) {
         double acc = op ? -1.0e300 : 0.0;
-        for (int b = 0; b < B; b++) {
+        for (int b = 0; b < nsrc; b++) {
             const double v = src[b][i];
             acc = op ? fmax(acc, v) : acc + v;
         }
-        for (int b = 0; b < B; b++) dst[b][i] = acc;
+        for (int b = 0; b < ndst; b++) dst[b][i] = acc;
     }
 }
 
@@ -1591,7 +1593,9 @@ struct LmState {
 int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B, orbhip_ba_result* const* res,
                    const volatile int* stop, hipStream_t st, int shard_mode, bool no_dag) {
     if (B <= 0 || !probs || !res) return ORBHIP_ERR_ARG;
-    if (shard_mode == kShardRccl && (B != 1 || !ws->comm)) return ORBHIP_ERR_ARG;
+    // RCCL: this rank holds B consecutive shards (segments rank*B .. rank*B+B-1 of nranks*B), the
+    // same B on every rank; the shards of one rank are summed on the device before the all-reduce
+    if (shard_mode == kShardRccl && !ws->comm) return ORBHIP_ERR_ARG;
     for (int b = 0; b < B; b++)
         if (!probs[b] || !res[b]) return ORBHIP_ERR_ARG;
     static const bool timing = std::getenv("ORBHIP_BA_TIMING") != nullptr;
@@ -1606,7 +1610,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     const double t_prepare = now();
     for (int b = 0; b < B; b++)
         if (pp[b].rc) return pp[b].rc;
-    if (shard_mode == kShardLocal) {
+    if (shard_mode != kShardNone && B > 1) {
         for (int b = 1; b < B; b++)
             if (pp[b].P != pp[0].P || pp[b].np != pp[0].np) return ORBHIP_ERR_ARG;
         // every shard factors the SUMMED S: the blocked Cholesky needs the union envelope
@@ -1646,14 +1650,14 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     // summed over the shards, every shard solves it, and the shards' x are summed. Otherwise the
     // shards sum S itself and every shard solves it (replicated). The decision is agreed over the
     // ranks; ORBHIP_SHARD_ND=0 forces the replicated form.
-    const int seg0 = shard_mode == kShardRccl ? ws->rank : 0;   // segment of problem 0
+    const int seg0 = shard_mode == kShardRccl ? ws->rank * B : 0;   // segment of problem 0
     NdPlan ndp;
     bool nd_sh = false;
     if (shard_mode != kShardNone) {
         const char* e_snd = std::getenv("ORBHIP_SHARD_ND");
         const char* e_min = std::getenv("ORBHIP_ND_MIN");
         const int nd_min = e_min ? std::atoi(e_min) : 960;
-        const int K = shard_mode == kShardLocal ? B : ws->nranks;
+        const int K = shard_mode == kShardLocal ? B : ws->nranks * B;
         int wl = 0, wc = 0;
         for (int b = 0; b < B; b++) {
             int l = 0, c = 0;
@@ -1662,13 +1666,14 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             wc = std::max(wc, c);
         }
         int ok = (!no_dag && !force_blocked && !(e_snd && e_snd[0] == '0') && pp[0].n >= nd_min) ? 1 : 0;
-        if (shard_mode == kShardRccl) {   // the band over every rank's landmarks
-            ws->h_int4[0] = wl; ws->h_int4[1] = wc; ws->h_int4[2] = -ok;
-            if (hipMemcpyAsync(ws->dint4.p, ws->h_int4, 3 * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
-                ncclAllReduce(ws->dint4.p, ws->dint4.p, 3, ncclInt32, ncclMax, ws->comm, st) != ncclSuccess ||
-                hipMemcpyAsync(ws->h_int4, ws->dint4.p, 3 * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        if (shard_mode == kShardRccl) {   // the band over every rank's landmarks; the same B everywhere
+            ws->h_int4[0] = wl; ws->h_int4[1] = wc; ws->h_int4[2] = -ok; ws->h_int4[3] = B; ws->h_int4[4] = -B;
+            if (hipMemcpyAsync(ws->dint4.p, ws->h_int4, 5 * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
+                ncclAllReduce(ws->dint4.p, ws->dint4.p, 5, ncclInt32, ncclMax, ws->comm, st) != ncclSuccess ||
+                hipMemcpyAsync(ws->h_int4, ws->dint4.p, 5 * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess)
                 return ORBHIP_ERR_DEVICE;
+            if (ws->h_int4[3] != B || -ws->h_int4[4] != B) return ORBHIP_ERR_ARG;
             wl = ws->h_int4[0]; wc = ws->h_int4[1]; ok = -ws->h_int4[2];
         }
         ok = ok && nd_plan_band(pp[0].np, wl, wc, K, ndp);
@@ -1879,7 +1884,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.npart_m = (int)((M + 255) / 256);
         if (p.use_dag) dd[b].buf = D + sR + p.o_dag;
         a.lambda = ws->lam.p + b;
-        a.lead = shard_mode == kShardLocal ? (b == 0) : (shard_mode == kShardRccl ? (ws->rank == 0) : 1);
+        a.lead = shard_mode == kShardLocal ? (b == 0) : (shard_mode == kShardRccl ? (ws->rank == 0 && b == 0) : 1);
         a.ctl = ws->ctl.p + b;
     });
     BAOK(hipMemcpyAsync(D + sA, hd + sA, sizeof(double) * (nA + nU), hipMemcpyHostToDevice, st));
@@ -1899,20 +1904,26 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             BAOK(hipMemcpyAsync(urf.data(), rf, nt * sizeof(int), hipMemcpyDeviceToHost, st));
             BAOK(hipStreamSynchronize(st));
         }
+        for (int b = 1; b < B; b++)   // this rank's other shards: the same envelope
+            BAOK(hipMemcpyAsync(const_cast<int*>(ha[b].row_first), rf, nt * sizeof(int), hipMemcpyDeviceToDevice, st));
         if (pp[0].use_dag) {   // the DAG plan of the union envelope, into the reserved space
             DagPlan& dp = pp[0].dag;
             dag_plan(urf.data(), n, dag_helpers, dp);
-            if (dp.toff.size() + dp.tasks.size() > pp[0].dag_task_cap) return ORBHIP_ERR_DEVICE;
-            BAOK(hipMemcpy(const_cast<int*>(dd[0].toff), dp.toff.data(), dp.toff.size() * sizeof(int),
-                           hipMemcpyHostToDevice));
-            dd[0].tasks = dd[0].toff + dp.toff.size();
-            if (!dp.tasks.empty())
-                BAOK(hipMemcpy(const_cast<int*>(dd[0].tasks), dp.tasks.data(), dp.tasks.size() * sizeof(int),
+            for (int b = 0; b < B; b++) {
+                if (dp.toff.size() + dp.tasks.size() > pp[b].dag_task_cap) return ORBHIP_ERR_DEVICE;
+                BAOK(hipMemcpy(const_cast<int*>(dd[b].toff), dp.toff.data(), dp.toff.size() * sizeof(int),
                                hipMemcpyHostToDevice));
-            dd[0].G = dp.G;
-            dd[0].pb = dp.pb;
+                dd[b].tasks = dd[b].toff + dp.toff.size();
+                if (!dp.tasks.empty())
+                    BAOK(hipMemcpy(const_cast<int*>(dd[b].tasks), dp.tasks.data(), dp.tasks.size() * sizeof(int),
+                                   hipMemcpyHostToDevice));
+                dd[b].G = dp.G;
+                dd[b].pb = dp.pb;
+            }
         }
-        if (n > kCholSmallN && !std::getenv("ORBHIP_SHARD_FULL_S")) {
+        // one shard per rank: S all-reduced over its union envelope, packed; several: the full S
+        // (summed on the device first, then the all-reduce, then copied to the other shards)
+        if (B == 1 && n > kCholSmallN && !std::getenv("ORBHIP_SHARD_FULL_S")) {
         std::vector<long long> off(nt + 1, 0);
         for (int R = 0; R < nt; R++)
             off[R + 1] = off[R] + (long long)std::min(32, n - 32 * R) * (std::min(32 * R + 32, n) - 32 * urf[R]);
@@ -2039,7 +2050,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 site(kNdX, (size_t)q0.n + 1, 0, [&](int b) { return nd_sep_bufs(ws->nds[b]).x_loc; },
                      [&](int b) { return nd_sep_bufs(ws->nds[b]).xg; });
             }
-            if (shard_mode == kShardLocal) {   // the pointer tables, on the device once
+            if (shard_mode == kShardLocal || B > 1) {   // the pointer tables of the in-process sums, on the device once
                 std::vector<double*> tab;
                 for (Site& t : sites) {
                     t.tab = tab.size();
@@ -2053,10 +2064,21 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         auto coll = [&](int id) -> int {
             const Site& t = sites[id];
             if (t.count == 0) return ORBHIP_OK;
+            const dim3 gr((unsigned)std::min<size_t>(1024, (t.count + 255) / 256));
+            double* const* tab = (shard_mode == kShardLocal || B > 1) ? ws->ptab.p + t.tab : nullptr;   // [src | dst]
             if (shard_mode == kShardLocal) {
-                hipLaunchKernelGGL(k_ba_multi_reduce, dim3((unsigned)std::min<size_t>(1024, (t.count + 255) / 256)),
-                                   dim3(256), 0, st, (const double* const*)(ws->ptab.p + t.tab),
-                                   (double* const*)(ws->ptab.p + t.tab + B), B, t.count, t.op);
+                hipLaunchKernelGGL(k_ba_multi_reduce, gr, dim3(256), 0, st, (const double* const*)tab, B, tab + B, B,
+                                   t.count, t.op);
+                return ORBHIP_OK;
+            }
+            if (B > 1) {   // RCCL with several shards per rank: this rank's sum into dst[0] first
+                hipLaunchKernelGGL(k_ba_multi_reduce, gr, dim3(256), 0, st, (const double* const*)tab, B, tab + B, 1,
+                                   t.count, t.op);
+                if (ncclAllReduce(t.dst[0], t.dst[0], t.count, ncclDouble, t.op ? ncclMax : ncclSum, ws->comm, st) !=
+                    ncclSuccess)
+                    return ORBHIP_ERR_DEVICE;
+                hipLaunchKernelGGL(k_ba_multi_reduce, gr, dim3(256), 0, st, (const double* const*)(tab + B), 1,
+                                   tab + B + 1, B - 1, t.count, t.op);
                 return ORBHIP_OK;
             }
             if (id == kRepS && env_total) {   // RCCL, replicated: S over its union envelope, packed
@@ -2191,8 +2213,12 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         auto relay_stop = [&] {
             if (h_stopw && stop && *stop) __atomic_store_n(h_stopw, 1, __ATOMIC_RELAXED);
         };
-        auto wait_ev = [&](hipEvent_t e) -> int {   // polls, relaying the stop flag
+        // with a stop flag to relay: polls, yielding the core between polls (the caller's Tracking
+        // thread may need it); without one: blocks in the runtime
+        auto wait_ev = [&](hipEvent_t e) -> int {
+            if (!h_stopw) return hipEventSynchronize(e) == hipSuccess ? ORBHIP_OK : ORBHIP_ERR_DEVICE;
             for (;;) {
+                std::this_thread::yield();
                 const hipError_t q = hipEventQuery(e);
                 if (q == hipSuccess) return ORBHIP_OK;
                 if (q != hipErrorNotReady) return ORBHIP_ERR_DEVICE;
@@ -2212,12 +2238,14 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 hipLaunchKernelGGL(k_ba_ctl_stop, gB, b256, 0, st, dctl, B, donep);
                 stop_sent = true;
             }
-            for (int k = 0; k < remaining && rc == ORBHIP_OK;) {
+            // RCCL: at most kChunk slots per batch, so the agreed stop is looked at every few trials
+            const int batch = rccl ? std::min(remaining, kChunk) : remaining;
+            for (int k = 0; k < batch && rc == ORBHIP_OK;) {
                 if (!rccl && !stop_sent && stop && *stop) {
                     hipLaunchKernelGGL(k_ba_ctl_stop, gB, b256, 0, st, dctl, B, donep);
                     stop_sent = true;
                 }
-                const int n = std::min(kChunk, remaining - k);
+                const int n = std::min(kChunk, batch - k);
                 for (int j = 0; j < n && rc == ORBHIP_OK; j++) rc = slot();
                 k += n;
                 if (rc == ORBHIP_OK && hipEventRecord(ev[nchunk & 1], st) != hipSuccess) rc = ORBHIP_ERR_DEVICE;
@@ -2357,8 +2385,8 @@ int ba_comm_init(BaWorkspace* ws, int nranks, int rank, const void* id) {
     ws->nranks = nranks;
     ws->rank = rank;
     BAOK(ws->dstop.ensure(1));
-    BAOK(ws->dint4.ensure(4));
-    if (!ws->h_int4) BAOK(hipHostMalloc((void**)&ws->h_int4, 4 * sizeof(int), hipHostMallocDefault));
+    BAOK(ws->dint4.ensure(8));
+    if (!ws->h_int4) BAOK(hipHostMalloc((void**)&ws->h_int4, 8 * sizeof(int), hipHostMallocDefault));
     if (!ws->h_stop) BAOK(hipHostMalloc((void**)&ws->h_stop, sizeof(int), hipHostMallocDefault));
     return ORBHIP_OK;
 }

@@ -1301,6 +1301,16 @@ int orbhip_ba_solve_sharded(orbhip_ctx* c, const orbhip_ba_problem* shard, orbhi
     return ba_solve_batch(c->ba, pp, 1, rr, stop, c->stream, kShardRccl);
 }
 
+int orbhip_ba_solve_sharded_segments(orbhip_ctx* c, const orbhip_ba_problem* shards, int nlocal, orbhip_ba_result* res,
+                                     const volatile int* stop) {
+    if (!c || !shards || !res || nlocal <= 0 || !c->ba) return ORBHIP_ERR_ARG;
+    HIPOK(hipSetDevice(c->device));
+    std::vector<const orbhip_ba_problem*> pp(nlocal);
+    std::vector<orbhip_ba_result*> rr(nlocal);
+    for (int b = 0; b < nlocal; b++) { pp[b] = shards + b; rr[b] = res + b; }
+    return ba_solve_batch(c->ba, pp.data(), nlocal, rr.data(), stop, c->stream, kShardRccl);
+}
+
 int orbhip_ba_solve_shards_local(orbhip_ctx* c, const orbhip_ba_problem* shards, int nshards, orbhip_ba_result* res,
                                  const volatile int* stop) {
     if (!c || !shards || !res || nshards <= 0) return ORBHIP_ERR_ARG;

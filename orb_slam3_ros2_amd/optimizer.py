@@ -202,6 +202,17 @@ class Optimizer:
         check(lib().orbhip_ba_solve_sharded(self.ctx.handle, ctypes.byref(pc), cres, sf), "orbhip_ba_solve_sharded")
         return self._fill(outs, cres)[0]
 
+    def solve_sharded_segments(self, shards, stop_flag: ctypes.c_int | None = None):
+        """This rank's consecutive shards (segments rank*len .. of nranks*len, sharding.shard_problem_nd)
+        solved jointly over RCCL (after comm_init): summed on the device, then all-reduced."""
+        ps = [p.normalized() for p in shards]
+        outs, cres = self._results_for(ps)
+        cprobs = (BAProblemC * len(ps))(*[p.to_c() for p in ps])
+        sf = ctypes.addressof(stop_flag) if stop_flag is not None else None
+        check(lib().orbhip_ba_solve_sharded_segments(self.ctx.handle, cprobs, len(ps), cres, sf),
+              "orbhip_ba_solve_sharded_segments")
+        return self._fill(outs, cres)
+
     def stats(self) -> dict:
         """orbhip_ba_stats: persistent-Cholesky launches on this device (all contexts), those that
         first waited for another stream's solve, the hand-off timeouts this context saw and the

@@ -173,6 +173,14 @@ def dd_finish(state, Sz, bz):
     return xi, xz
 
 
+def dd_finish_given(state, xz):
+    """dd_finish with the separator solution already known (the second level solved it)."""
+    import torch
+    L, W, y, zi = state
+    xi = torch.linalg.solve_triangular(L.T, y - W @ xz[zi].unsqueeze(1), upper=True).squeeze(1)
+    return xi, xz
+
+
 def dd_assemble(xis, xz, part: Partition):
     """The full x from every rank's interior (the all-gather) and the separators."""
     import torch
@@ -209,3 +217,42 @@ def dd_solve_local(Ss, bs, part: Partition):
     bz = sum(l[2] for l in loc)
     fin = [dd_finish(l[0], Sz, bz) for l in loc]
     return dd_assemble([f[0] for f in fin], fin[0][1], part)
+
+
+def dd_solve_separator_two_level(Sz, bz, part: Partition):
+    """The separator system's second dissection level (ba_nd.hip nd_inner_plan, replicated on every
+    rank after the all-reduce): the even separators eliminated as interiors, the odd ones solved
+    densely (Partition(K, K // 2, 2, dof = sep * 6); K even here)."""
+    import torch
+    p2 = Partition(part.ranks, part.ranks // 2, 2, dof=part.sep * part.dof)
+    S2, b2 = split_assembled(Sz.numpy(), bz.numpy(), p2)
+    return dd_solve_local(S2, b2, p2).to(torch.float64)
+
+
+def dd_solve_segments(Ss_loc, bs_loc, part: Partition, rank: int, group=None, levels: int = 1):
+    """Ranks x local segments (the device's orbhip_ba_solve_sharded_segments): this rank holds
+    segments rank*L .. rank*L+L-1 of part.ranks = world*L (Ss_loc / bs_loc: their partial systems).
+    The local separator contributions are summed in-process first, then one all-reduce; every
+    segment finishes its interior, and the pose update is summed over the ranks (each interior once,
+    the separators from rank 0) like the device's kNdX all-reduce. Returns the full x."""
+    import torch
+    import torch.distributed as dist
+    L = len(Ss_loc)
+    loc = [dd_local(torch.as_tensor(S), torch.as_tensor(b), part, rank * L + j) for j, (S, b) in
+           enumerate(zip(Ss_loc, bs_loc))]
+    nz = part.n_sep
+    flat = torch.cat([sum(l[1] for l in loc).reshape(-1), sum(l[2] for l in loc)])
+    dist.all_reduce(flat, group=group)
+    Sz, bz = flat[:nz * nz].reshape(nz, nz), flat[nz * nz:]
+    x = torch.zeros(part.n_kf * part.dof, dtype=torch.float64)
+    m = part.sep * part.dof
+    xz2 = dd_solve_separator_two_level(Sz, bz, part) if levels > 1 else None
+    for j, l in enumerate(loc):
+        r = rank * L + j
+        xi, xz = dd_finish(l[0], Sz, bz) if xz2 is None else dd_finish_given(l[0], xz2)
+        x[torch.as_tensor(part.interior(r))] = xi
+        if rank == 0 and j == 0:
+            for t in range(part.ranks):
+                x[torch.as_tensor(part.vars_of(part.separator_kf(t)))] = xz[t * m:(t + 1) * m]
+    dist.all_reduce(x, group=group)
+    return x

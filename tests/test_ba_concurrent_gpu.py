@@ -100,3 +100,60 @@ def test_forced_dag_timeout_is_reported(oracle, monkeypatch):
     t0 = opt.stats()["dag_timeouts"]
     _close(opt.LocalBundleAdjustment(prob), o)
     assert opt.stats()["dag_timeouts"] == t0
+
+
+_FIRST_CALLS = r"""
+import json, sys, threading
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from orb_slam3_ros2_amd import ORBextractor, Optimizer
+from orb_slam3_ros2_amd.synthetic import synthetic_ba_problem, synthetic_frame
+prob, _ = synthetic_ba_problem(seed=7)
+img = synthetic_frame(3)
+# every context is created before the race; the first solve / extraction of this process (the
+# per-device kernel attributes: LDS sizes of the Cholesky, extraction and DAG kernels) runs in
+# both threads at once
+ctx = [(Optimizer(), ORBextractor(1000)) for _ in range(2)]
+go = threading.Barrier(2)
+out, errs = [None, None], []
+def run(i):
+    try:
+        opt, ext = ctx[i]
+        go.wait()
+        r = opt.LocalBundleAdjustment(prob) if i == 0 else None
+        mono, kps, desc = ext(img)
+        if i == 1:
+            r = opt.LocalBundleAdjustment(prob)
+        out[i] = dict(chi2=r.final_chi2, trials=r.lm_trials, it=r.iterations_done, pose_t=r.pose_t.tolist(),
+                      n=int(kps.shape[0]), desc=desc.tobytes().hex())
+    except Exception as e:
+        errs.append(repr(e))
+th = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+[t.start() for t in th]
+[t.join(120) for t in th]
+print(json.dumps(dict(out=out, errs=errs, alive=any(t.is_alive() for t in th))))
+"""
+
+
+def test_two_thread_first_calls_fresh_process(oracle):
+    """A fresh process whose two threads make their first LBA solve and first extraction at once
+    (each on its own contexts): the per-device kernel attributes (dev_attr.h LdsAttrOnce, DagDevState)
+    are set under a lock, so both calls launch with their LDS size and both results are correct."""
+    import json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", _FIRST_CALLS, repo], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    assert not res["alive"] and not res["errs"], res["errs"]
+    prob, _ = synthetic_ba_problem(seed=7)
+    o = oracle.ba_solve(prob)
+    for r in res["out"]:
+        assert r["it"] == o["iterations_done"] and r["trials"] == o["lm_trials"]
+        assert abs(r["chi2"] - o["final_chi2"]) <= 1e-4 * abs(o["final_chi2"])
+        pt = np.asarray(r["pose_t"])
+        assert np.abs(pt - o["pose_t"]).max() / max(1.0, np.abs(o["pose_t"]).max()) < 1e-4
+    a, b = res["out"]
+    assert a["n"] == b["n"] > 0 and a["desc"] == b["desc"]   # the same frame: identical extraction

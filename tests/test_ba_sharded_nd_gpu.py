@@ -4,7 +4,9 @@ system and the pose update are summed over the shards, every shard solves the se
 the LM runs device-driven with the collectives on the stream, no host round trip per trial).
 
 In-process shards (orbhip_ba_solve_shards_local, sums by k_ba_multi_reduce) stand in for the ranks
-on one GPU; the RCCL form runs the same slot with ncclAllReduce in those places. Each against the
+on one GPU; the RCCL form runs the same slot with ncclAllReduce in those places: a one-rank
+communicator holding all K segments (orbhip_ba_solve_sharded_segments: the rank's segments summed on
+the device, then the all-reduce) runs every collective of the dissected slot through RCCL. Each against the
 oracle LM (schedule identical, 1e-4 on poses / points / chi2) at the full C5 size with 4 and 8
 segments, and on 100- and 150-KF loops with 2 and 3. Parity unpinned by the reference."""
 import numpy as np
@@ -25,11 +27,12 @@ def _close(g, o):
     assert np.abs(g.points.astype(np.float64) - o["points"]).max() / max(1.0, np.abs(o["points"]).max()) < REL
 
 
-def _solve_segments(opt, p, K, dissected=True):
+def _solve_segments(opt, p, K, dissected=True, rccl=False):
     from orb_slam3_ros2_amd.sharding import merge_results_nd, shard_problem_nd
     parts = [shard_problem_nd(p, r, K) for r in range(K)]
     l0 = opt.stats()["dag_launches"]
-    res = opt.solve_shards_local([q[0] for q in parts])
+    shards = [q[0] for q in parts]
+    res = opt.solve_sharded_segments(shards) if rccl else opt.solve_shards_local(shards)
     # the dissected form launches two persistent solves per shard and trial (its segment's partial
     # factorization, the separator system), the replicated form one (the summed S)
     per = (opt.stats()["dag_launches"] - l0) / (K * res[0].lm_trials)
@@ -62,3 +65,26 @@ def test_segment_shards_replicated_fallback(c5_case, monkeypatch):
     monkeypatch.setenv("ORBHIP_SHARD_ND", "0")
     _, p, o = c5_case
     _close(_solve_segments(Optimizer(), p, 4, dissected=False), o)
+
+
+def _rccl_optimizer():
+    from orb_slam3_ros2_amd import Optimizer
+    opt = Optimizer()
+    opt.comm_init(1, 0, Optimizer.comm_unique_id())
+    return opt
+
+
+@pytest.mark.parametrize("K", [4, 8])
+def test_c5_rccl_rank_segments_parity(c5_case, K):
+    """One RCCL rank with K local segments: the kNdPack / kNdBz / kNdX all-reduces, the Hpp / chi2
+    sums and the plan / stop / timeout consensus all go through ncclAllReduce."""
+    _, p, o = c5_case
+    _close(_solve_segments(_rccl_optimizer(), p, K, rccl=True), o)
+
+
+def test_c5_rccl_rank_segments_replicated(c5_case, monkeypatch):
+    """ORBHIP_SHARD_ND=0 over RCCL with 4 local shards: S summed on the device, all-reduced in full,
+    copied to the other shards; every shard solves it on the union envelope's DAG plan."""
+    monkeypatch.setenv("ORBHIP_SHARD_ND", "0")
+    _, p, o = c5_case
+    _close(_solve_segments(_rccl_optimizer(), p, 4, dissected=False, rccl=True), o)

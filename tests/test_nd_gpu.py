@@ -49,13 +49,29 @@ def test_nd_solve_matches_numpy(n_pose, w, cyclic, K):
     assert err < 1e-9, (err, ku)
 
 
+@pytest.mark.parametrize("levels", ["1", "2"])
+@pytest.mark.parametrize("K", [6, 7, 8, 10])
+def test_nd_two_levels_match_numpy(K, levels, monkeypatch):
+    """The second level (a cyclic separator system of >= 6 separators dissected once more: even
+    separators eliminated by one more k_chol_dag_multi, the odd ones solved densely; K odd: the last
+    inner segment holds three separators) against the one-level solve and numpy, at the C5 band."""
+    monkeypatch.setenv("ORBHIP_ND_LEVELS", levels)
+    A, b, bi, bj = banded_system(399, 19, True, seed=40 + K)
+    rc, x, ms, ku = nd_solve(A, b, 399, bi, bj, K)
+    assert rc == 0 and ku == K, (rc, ku)
+    ref = np.linalg.solve(A, b)
+    err = np.abs(x - ref).max() / np.abs(ref).max()
+    assert err < 1e-9, (err, ku)
+
+
 def test_nd_not_planned_for_a_dense_system():
     A, b, bi, bj = banded_system(60, 40, False, seed=3)
     rc, _, _, _ = nd_solve(A, b, 60, bi, bj, 0)
     assert rc == -5   # ORBHIP_ERR_UNSUPPORTED: the plain solve is the better one
 
 
-@pytest.mark.parametrize("env", [{}, {"ORBHIP_ND_K": "2"}, {"ORBHIP_ND_K": "8"}, {"ORBHIP_ND": "0"}])
+@pytest.mark.parametrize("env", [{}, {"ORBHIP_ND_K": "2"}, {"ORBHIP_ND_K": "8"}, {"ORBHIP_ND": "0"},
+                                 {"ORBHIP_ND_K": "8", "ORBHIP_ND_LEVELS": "1"}, {"ORBHIP_ND_K": "7"}])
 def test_gba_c5_dissection_parity(c5_case, env, monkeypatch):
     """GlobalBundleAdjustment at the C5 size (n = 2394) with the dissection's default plan, 2 and 8
     segments, and the plain DAG solve: each equal to the oracle LM (schedule identical, 1e-4)."""

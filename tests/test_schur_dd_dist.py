@@ -31,6 +31,67 @@ def _worker(rank, port, q):
         dist.destroy_process_group()
 
 
+def _worker_segments(rank, port, q):
+    """Two ranks x two local segments each (K = 4): the orbhip_ba_solve_sharded_segments flow."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from schur_dd_model import Partition, covisibility_system, dd_solve_segments
+        part = Partition(48, 2 * WORLD, 5)
+        Ss, bs = covisibility_system(part, 500, seed=5)
+        mine = [2 * rank, 2 * rank + 1]
+        x = dd_solve_segments([Ss[r] for r in mine], [bs[r] for r in mine], part, rank).numpy()
+        xr = np.linalg.solve(sum(Ss), sum(bs))
+        q.put((rank, float(np.abs(x - xr).max() / np.abs(xr).max())))
+    finally:
+        dist.destroy_process_group()
+
+
+def _worker_segments_two_level(rank, port, q):
+    """Two ranks x four local segments (K = 8), the separator system dissected once more on every
+    rank after the all-reduce (the device's second level)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from schur_dd_model import Partition, covisibility_system, dd_solve_segments
+        part = Partition(80, 8, 5)
+        Ss, bs = covisibility_system(part, 800, seed=6)
+        mine = list(range(4 * rank, 4 * rank + 4))
+        x = dd_solve_segments([Ss[r] for r in mine], [bs[r] for r in mine], part, rank, levels=2).numpy()
+        xr = np.linalg.solve(sum(Ss), sum(bs))
+        q.put((rank, float(np.abs(x - xr).max() / np.abs(xr).max())))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_gloo(target):
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return [q.get(timeout=5) for _ in range(WORLD)]
+
+
+def test_dd_solve_segments_gloo_ranks_times_local():
+    for rank, err in _run_gloo(_worker_segments):
+        assert err < 1e-10, (rank, err)
+
+
+def test_dd_solve_segments_gloo_two_levels():
+    for rank, err in _run_gloo(_worker_segments_two_level):
+        assert err < 1e-10, (rank, err)
+
+
 def test_dd_solve_gloo_matches_full_solve():
     import socket
     with socket.socket() as s:

@@ -28,7 +28,7 @@ def spd(n, shape, rng):
 
 
 L = lib()
-if os.environ.get("ORBHIP_PROBE_LIB"):   # an alternative build of the library (A/B of a compile-time switch)
+if os.environ.get("ORBHIP_PROBE_LIB", ""):   # an alternative build of the library (A/B of a compile-time switch)
     L = ctypes.CDLL(os.environ["ORBHIP_PROBE_LIB"])
     L.orbhip_test_cholesky_dag.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int] * 3 + [ctypes.c_void_p] * 2
 cases = [a.split(":") for a in (sys.argv[1:] or ["31:dense", "100:dense", "294:dense", "600:band", "2394:loop", "2394:dense"])]
@@ -40,7 +40,7 @@ for n_s, shape in cases:
     b = rng.normal(size=n)
     x = np.zeros(n)
     ms = ctypes.c_float(0)
-    dbg = np.zeros(8 + 6 * 200 + 16 * 100, np.uint64)   # kDbgWords (ba_chol_dag.h)
+    dbg = np.zeros(8 + 6 * 200 + 16 * 100 + 3 * 128, np.uint64)   # kDbgWords (ba_chol_dag.h)
     t0 = time.time()
     rc = L.orbhip_test_cholesky_dag(A.ctypes.data, b.ctypes.data, x.ctypes.data, n, 10, int(os.environ.get('ORBHIP_DAG_HELPERS', '0')), ctypes.byref(ms),
                                     dbg.ctypes.data)
@@ -65,3 +65,9 @@ for n_s, shape in cases:
               f"w2 loads {m[4]} L(k+2,k) {m[5]} T/D' {m[6]} L(k+1,k) in {m[7]} | "
               f"w3 loads {m[8]} L(k+2,k) {m[9]} T/D' {m[10]} L(k+1,k) in {m[11]} | w0 y {m[3]} "
               f"| W23 form: w2 T {m[12]} D' {m[13]} w3 T {m[14]} D' {m[15]}", flush=True)
+    nb = min(nt, 128)
+    bk = dbg[8 + 6 * 200 + 16 * 100:].reshape(128, 3).astype(np.int64)[:nb]
+    if nb > 1 and bk[1:nb, 0].any():
+        st = bk[1:nb]
+        print("    backward steps R (start, x formed, wave 1 done; cycles from the backward start): " +
+              " ".join(f"{R}:{a}/{b}/{c}" for R, (a, b, c) in zip(range(nb - 1, 0, -1), st[::-1][:12])), flush=True)

@@ -19,7 +19,11 @@ prob, _ = synthetic_ba_problem(n_kf=n_kf, n_pts=n_pts, layout="loop", window=20,
 print(f"problem: {n_kf} KF, {n_pts} pts, {prob.edge_pose.shape[0]} obs ({time.perf_counter() - t:.1f}s to build)")
 opt = Optimizer()
 opt.BundleAdjustment(prob, nIterations=1)
-t = time.perf_counter()
-r = opt.BundleAdjustment(prob, nIterations=iters)
-dt = time.perf_counter() - t
-print(f"GBA {iters} it: {dt*1e3:.1f} ms  trials={r.lm_trials} chi2 {r.initial_chi2:.1f} -> {r.final_chi2:.1f}")
+ts = []
+for _ in range(5):
+    t = time.perf_counter()
+    r = opt.BundleAdjustment(prob, nIterations=iters)
+    ts.append(time.perf_counter() - t)
+print(f"GBA {iters} it: {np.median(ts)*1e3:.2f} ms median of 5 (min {min(ts)*1e3:.2f})  trials={r.lm_trials} "
+      f"chi2 {r.initial_chi2:.1f} -> {r.final_chi2:.1f}  ND_K={os.environ.get('ORBHIP_ND_K', 'auto')} "
+      f"levels={os.environ.get('ORBHIP_ND_LEVELS', '2')}")
