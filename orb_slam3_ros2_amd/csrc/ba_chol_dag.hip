@@ -53,11 +53,15 @@ constexpr int kNewton = ORBHIP_DAG_NEWTON;   // Newton steps after v_rsq_f64 / v
 #ifndef ORBHIP_DAG_DIAG_DPP
 #define ORBHIP_DAG_DIAG_DPP 1   // r05: the 16x16 diagonal factorizations by DPP elimination (diag16_dpp)
 #endif
+// A/B switches measured on MI355X (tools/build_ab.sh + probe_cholesky_dag.py, r05): loading the
+// next interval's helper flag before the barrier made the interval longer (13.2k -> 14.0k cycles
+// at n = 294), and the column-major backward's scattered 8-byte tile loads cost more than the
+// reductions they remove (backward 41.8k -> 59.9k cycles): both off.
 #ifndef ORBHIP_DAG_FLAG_AHEAD
-#define ORBHIP_DAG_FLAG_AHEAD 1   // waves 2/3 load the next interval's helper flag before the barrier
+#define ORBHIP_DAG_FLAG_AHEAD 0   // waves 2/3 load the next interval's helper flag before the barrier
 #endif
 #ifndef ORBHIP_DAG_BACK_COL
-#define ORBHIP_DAG_BACK_COL 1   // r05: the chain-only backward on column-major tile loads (bwd_col_dot)
+#define ORBHIP_DAG_BACK_COL 0   // the chain-only backward on column-major tile loads (bwd_col_dot)
 #endif
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));

@@ -12,6 +12,8 @@
 #include "ba_args.h"
 #include "ba_chol_dag.h"
 #include "ba_nd.h"
+#include "dev_attr.h"
+#include "wave_f64.h"
 
 namespace orbhip {
 
@@ -101,13 +103,17 @@ __device__ __forceinline__ void lds_only_barrier() {
     asm volatile("" ::: "memory");
 }
 
-// one workgroup per segment: x of its separator rows from x_Z, then L_II^T x_I = y_I - L_ZI^T x_Z
-// tile by tile (tile column R: every tile (R', R), R' > R, of the envelope), then the scatter to S's
-// order. A failed factorization anywhere (a segment or the separator system) zeroes x and flag.
-// The step's operands do not depend on x: each thread's first three tiles of column R - 1 (half
-// a tile column each), Linv_{R-1} and y_{R-1} are loaded while step R runs, and the envelope sits
-// in LDS, so a step waits on LDS and barriers only (a column deeper than 12 tiles loads the rest
-// in the step).
+// one workgroup per segment (4 waves): x of its separator rows from x_Z, then
+// L_II^T x_I = y_I - L_ZI^T x_Z in two phases.
+//   1. the separator rows' part of every interior column at once: y_R -= sum over separator tile
+//      rows R' of L(R', R)^T x_R' (no dependency between columns: a stream of tile loads);
+//   2. the banded back-substitution over the interior tiles only: at step R each wave adds the
+//      products of its tiles of column R (rows R + 1 + w, + 4, ...) lane-locally, ONE set of
+//      16-lane reductions per wave, then wave 0 forms x_R = Linv_R^T (y_R - sum) (one more).
+// Tiles are read in their quadrant layout, 16 doubles per lane in four 32-byte loads (coalesced),
+// one step ahead in two register sets. r04's form walked every tile of column R (separator rows
+// included) with 16 scattered 8-byte loads per thread and tile and four barriers per step.
+// A failed factorization anywhere (a segment or the separator system) zeroes x and flag.
 // the segment buffers are reached through pointers loaded from memory (NdSegDev), which the
 // compiler cannot place in an address space: without these casts every load is a flat load,
 // counted in lgkmcnt too, so each LDS wait of a step would also wait for the prefetched tiles
@@ -115,23 +121,61 @@ template <typename T>
 __device__ __forceinline__ const __attribute__((address_space(1))) T* gp(const T* p) {
     return (const __attribute__((address_space(1))) T*)p;
 }
+typedef double dv4 __attribute__((ext_vector_type(4)));
+// this lane's 16 values of a tile: quadrant qd, component q = element
+// (16 (qd >> 1) + (l & 15), 16 (qd & 1) + (l >> 4) + 4 q)
+__device__ __forceinline__ void tile_ld(const double* t, dv4 (&v)[4]) {
+    const auto p = gp((const dv4*)t) + (threadIdx.x & 63);
+#pragma unroll
+    for (int qd = 0; qd < 4; qd++) v[qd] = p[64 * qd];
+}
+// p[b][q] += this lane's part of (tile^T x) for column 16 b + (l >> 4) + 4 q (its two rows)
+__device__ __forceinline__ void tile_acc(const dv4 (&v)[4], const double* x, double (&p)[2][4]) {
+    const int r = threadIdx.x & 15;
+    const double x0 = x[r], x1 = x[16 + r];
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) p[b][q] = fma(v[2 + b][q], x1, fma(v[b][q], x0, p[b][q]));
+}
+// the 16-lane sums: lanes with (l & 15) == 0 store column 16 b + (l >> 4) + 4 q to out
+__device__ __forceinline__ void tile_red_store(double (&p)[2][4], double* out) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int b = 0; b < 2; b++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) p[b][q] = row16_sum(p[b][q]);
+    if ((lane & 15) == 0)
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) out[16 * b + (lane >> 4) + 4 * q] = p[b][q];
+}
+
+constexpr int kBsM = 2;   // tiles per wave and step held in registers (more are loaded in the step)
+constexpr size_t kBsMaxLds = 128 * 1024;   // (below the 160 KB of a CU: the kernel has static LDS too)
 
 __global__ __launch_bounds__(256) void k_nd_backsolve(NdDev d) {
     if (d.gate && *d.gate != kPhTrial) return;
-    extern __shared__ double xs[];   // NT x 32, then 8 x 32 partials, 32 s, then NT ints (envelope)
+    // LDS: xs (NT x 32), ys (NT x 32), part1 (4 x NT x 32), part (4 x 32), sv (32), then NT ints
+    extern __shared__ double xs[];
     const NdSegDev s = d.segs[blockIdx.x];
-    double* part = xs + s.NT * kT;
-    double* sv = part + 8 * kT;
+    const int NT = s.NT, nti = s.nti;
+    double* ys = xs + NT * kT;
+    double* part1 = ys + NT * kT;
+    double* part = part1 + 4 * NT * kT;
+    double* sv = part + 4 * kT;
     int* rfs = (int*)(sv + kT);
     __shared__ int okw;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
     double* xo = d.x_loc ? d.x_loc : d.x;
     if (tid == 0) okw = d.flagZ[0] != 0;
-    for (int i = tid; i < s.NT; i += blockDim.x) rfs[i] = gp(s.rf)[i];
-    for (int i = tid; i < s.NT * kT; i += blockDim.x) {
+    for (int i = tid; i < NT; i += blockDim.x) rfs[i] = gp(s.rf)[i];
+    for (int i = tid; i < NT * kT; i += blockDim.x) {
         double v = 0.0;
         if (i >= s.nip && i < s.n) v = gp(d.xZ)[gp(s.zmap)[i - s.nip]];
         xs[i] = v;
+        ys[i] = i < nti * kT ? gp(s.buf)[dag_off_y(NT, i / kT) + i % kT] : 0.0;
     }
     __syncthreads();
     if (tid < d.K && gp(d.segs[tid].flag)[0] == 0) okw = 0;   // every segment factored (all in parallel)
@@ -141,96 +185,110 @@ __global__ __launch_bounds__(256) void k_nd_backsolve(NdDev d) {
         if (d.x_loc) d.x_loc[d.n] = ok ? 0.0 : 1.0;
         else d.flag[0] = ok;
     }
-    const int c = tid & 31, g = tid >> 5;
-    // group g = (tile slot ts, row half): its tiles of column R are rows R + 1 + ts, + 4, ... inside
-    // the envelope, 16 of their 32 rows each
-    const int ts = g >> 1, rh = (g & 1) * 16;
-    auto next_row = [&](int R, int Rp) {
-        for (; Rp < s.NT; Rp += 4)
-            if (R >= rfs[Rp]) return Rp;
-        return -1;
-    };
-    // per step and thread: the first three of its tiles (16 loads each), 4 entries of Linv_R, y:
-    // 53 loads in flight, under the 63 that vmcnt can count (more would make the step wait for
-    // its own prefetch)
-    constexpr int kPT = 3;
-    double vn[kPT][16], lqn[4], yn = 0.0;
-    int rpn[kPT];
-    auto prefetch = [&](int R) {
-        int Rp = R + 1 + ts;
-#pragma unroll
-        for (int k = 0; k < kPT; k++) {
-            Rp = Rp >= 0 ? next_row(R, Rp) : -1;
-            rpn[k] = Rp;
-            if (Rp >= 0) {
-                const auto t = gp(s.buf) + dag_off_L(s.NT, Rp, R);
-#pragma unroll
-                for (int r = 0; r < 16; r++) vn[k][r] = t[tq(rh + r, c)];
-                Rp += 4;
-            }
-        }
-        const auto li = gp(s.buf) + dag_off_Linv(s.NT, R);
-#pragma unroll
-        for (int k = 0; k < 4; k++) lqn[k] = li[tq(4 * g + k, c)];
-        if (tid < kT) yn = gp(s.buf)[dag_off_y(s.NT, R) + tid];
-    };
-    if (ok && s.nti > 0) prefetch(s.nti - 1);
-    for (int R = s.nti - 1; R >= 0 && ok; R--) {
-        double v[kPT][16], lq[4];
-        int rp[kPT];
-#pragma unroll
-        for (int k = 0; k < kPT; k++) {
-            rp[k] = rpn[k];
-#pragma unroll
-            for (int r = 0; r < 16; r++) v[k][r] = vn[k][r];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++) lq[k] = lqn[k];
-        const double yR = yn;
-        if (R > 0) prefetch(R - 1);
-        double a4[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int k = 0; k < kPT; k++) {
-            if (rp[k] < 0) continue;
-            const double* xr = xs + rp[k] * kT + rh;
-#pragma unroll
-            for (int r = 0; r < 16; r++) a4[r & 3] = fma(v[k][r], xr[r], a4[r & 3]);
-        }
-        // further tiles of this group (a column deeper than 12 tiles): loaded here
-        if (rp[kPT - 1] >= 0) {
-            for (int Rp = next_row(R, rp[kPT - 1] + 4); Rp >= 0; Rp = next_row(R, Rp + 4)) {
-                const auto t = gp(s.buf) + dag_off_L(s.NT, Rp, R);
-                const double* xq = xs + Rp * kT + rh;
-                double w[16];
-#pragma unroll
-                for (int r = 0; r < 16; r++) w[r] = t[tq(rh + r, c)];
-#pragma unroll
-                for (int r = 0; r < 16; r++) a4[r & 3] = fma(w[r], xq[r], a4[r & 3]);
-            }
-        }
-        part[g * kT + c] = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-        lds_only_barrier();
-        if (tid < kT) {
-            double y = yR;
-            for (int q = 0; q < 8; q++) y -= part[q * kT + tid];
-            sv[tid] = y;
-        }
-        lds_only_barrier();
-        // x_R = Linv_R^T s: thread (g, c) sums rows 4g .. 4g+3 of column c, then 8 partials
+    if (ok && nti > 0) {
+        // ---- phase 1: wave w takes separator tile rows nti + w, + 4, ... of every interior column,
+        // the next column's first kBsM tiles loaded while this one's are summed ----
         {
-            double p2 = 0.0;
+            dv4 tv[2][kBsM][4];
+            int rp[2][kBsM];
+            auto load1 = [&](auto setc, int R) {
+                constexpr int S = decltype(setc)::value;
+                int Rp = nti + wid;
 #pragma unroll
-            for (int k = 0; k < 4; k++) p2 = fma(lq[k], sv[4 * g + k], p2);
-            part[g * kT + c] = p2;
+                for (int m = 0; m < kBsM; m++) {
+                    while (Rp < NT && rfs[Rp] > R) Rp += 4;
+                    rp[S][m] = Rp < NT && R < nti ? Rp : -1;
+                    if (rp[S][m] >= 0) {
+                        tile_ld(s.buf + dag_off_L(NT, Rp, R), tv[S][m]);
+                        Rp += 4;
+                    }
+                }
+            };
+            auto col1 = [&](auto setc, int R) {
+                constexpr int S = decltype(setc)::value;
+                double p[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+                int last = -1;
+#pragma unroll
+                for (int m = 0; m < kBsM; m++)
+                    if (rp[S][m] >= 0) { tile_acc(tv[S][m], xs + rp[S][m] * kT, p); last = rp[S][m]; }
+                if (rp[S][kBsM - 1] >= 0)   // more separator tiles in this column: loaded here
+                    for (int Rp = last + 4; Rp < NT; Rp += 4)
+                        if (rfs[Rp] <= R) {
+                            dv4 w4[4];
+                            tile_ld(s.buf + dag_off_L(NT, Rp, R), w4);
+                            tile_acc(w4, xs + Rp * kT, p);
+                        }
+                load1(setc, R + 2);
+                tile_red_store(p, part1 + (wid * NT + R) * kT);
+            };
+            load1(std::integral_constant<int, 0>{}, 0);
+            load1(std::integral_constant<int, 1>{}, 1);
+            for (int R = 0; R < nti; R += 2) {
+                col1(std::integral_constant<int, 0>{}, R);
+                if (R + 1 < nti) col1(std::integral_constant<int, 1>{}, R + 1);
+            }
         }
-        lds_only_barrier();
-        if (tid < kT) {
-            double xv = 0.0;
-            for (int q = 0; q < 8; q++) xv += part[q * kT + tid];
-            xs[R * kT + tid] = xv;
+        __syncthreads();
+        for (int i = tid; i < nti * kT; i += blockDim.x) {
+            const int R = i / kT, c = i % kT;
+            double t = 0.0;
+#pragma unroll
+            for (int w = 0; w < 4; w++) t += part1[(w * NT + R) * kT + c];
+            ys[i] -= t;
         }
-        lds_only_barrier();
+        __syncthreads();
+        // ---- phase 2: the banded back-substitution over the interior tiles ----
+        dv4 tv[2][kBsM][4], li[2][4];
+        int rp[2][kBsM];
+        auto load2 = [&](auto setc, int R) {
+            constexpr int S = decltype(setc)::value;
+            int Rp = R + 1 + wid;
+#pragma unroll
+            for (int m = 0; m < kBsM; m++) {
+                while (Rp < nti && rfs[Rp] > R) Rp += 4;
+                rp[S][m] = Rp < nti && R >= 0 ? Rp : -1;
+                if (rp[S][m] >= 0) {
+                    tile_ld(s.buf + dag_off_L(NT, Rp, R), tv[S][m]);
+                    Rp += 4;
+                }
+            }
+            if (wid == 0 && R >= 0) tile_ld(s.buf + dag_off_Linv(NT, R), li[S]);
+        };
+        auto step = [&](auto setc, int R) {
+            constexpr int S = decltype(setc)::value;
+            double p[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+            int last = -1;
+#pragma unroll
+            for (int m = 0; m < kBsM; m++)
+                if (rp[S][m] >= 0) { tile_acc(tv[S][m], xs + rp[S][m] * kT, p); last = rp[S][m]; }
+            if (rp[S][kBsM - 1] >= 0)
+                for (int Rp = last + 4; Rp < nti; Rp += 4)
+                    if (rfs[Rp] <= R) {
+                        dv4 w4[4];
+                        tile_ld(s.buf + dag_off_L(NT, Rp, R), w4);
+                        tile_acc(w4, xs + Rp * kT, p);
+                    }
+            tile_red_store(p, part + wid * kT);
+            lds_only_barrier();
+            if (wid == 0) {
+                if (lane < kT)
+                    sv[lane] = ys[R * kT + lane] - ((part[lane] + part[kT + lane]) + (part[2 * kT + lane] + part[3 * kT + lane]));
+                wave_lds_sync();
+                double q[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+                tile_acc(li[S], sv, q);
+                tile_red_store(q, xs + R * kT);
+            }
+            load2(setc, R - 2);
+            lds_only_barrier();
+        };
+        load2(std::integral_constant<int, 0>{}, nti - 1);
+        load2(std::integral_constant<int, 1>{}, nti - 2);
+        for (int R = nti - 1; R >= 0; R -= 2) {
+            step(std::integral_constant<int, 0>{}, R);
+            if (R - 1 >= 0) step(std::integral_constant<int, 1>{}, R - 1);
+        }
     }
+    __syncthreads();
     for (int i = tid; i < s.nip; i += blockDim.x) {
         const int p = gp(s.perm)[i];
         if (p >= 0) xo[p] = ok ? xs[i] : 0.0;
@@ -624,7 +682,8 @@ int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int 
     int maxNT = 0;
     for (int r = 0; r < K; r++)
         if (loc[r] >= 0) maxNT = std::max(maxNT, sg[r].NT);
-    W->bs_lds = sizeof(double) * ((size_t)maxNT * kT + 9 * kT) + sizeof(int) * (size_t)maxNT;
+    W->bs_lds = sizeof(double) * ((size_t)6 * maxNT * kT + 5 * kT) + sizeof(int) * (size_t)maxNT;
+    if (W->bs_lds > kBsMaxLds) return -5;   // a segment too long for the back-substitution's LDS
     // shard of a distributed solve: the packed separator envelope and the x buffers
     d.x_loc = nullptr;
     d.xg = nullptr;
@@ -687,6 +746,8 @@ hipError_t nd_separator_backsolve(NdWorkspace* W, hipStream_t st) {
                                                  st, d.gate);
     if (e != hipSuccess) return e;
     if (d.x_loc && (e = hipMemsetAsync(d.x_loc, 0, sizeof(double) * (d.n + 1), st)) != hipSuccess) return e;
+    static LdsAttrOnce bs_attr;   // per device, thread-safe
+    if ((e = bs_attr.ensure((const void*)k_nd_backsolve, (int)kBsMaxLds)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_nd_backsolve, dim3((unsigned)W->K), dim3(256), W->bs_lds, st, d);
     return hipGetLastError();
 }

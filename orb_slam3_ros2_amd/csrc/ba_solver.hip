@@ -28,6 +28,9 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cfloat>
 #include <cmath>
 #include <cstdlib>
@@ -1334,6 +1337,232 @@ struct Prep {
     size_t o_chi2 = 0, o_state = 0, o_obs = 0, o_scr = 0, o_lin = 0, o_S = 0, o_L = 0, o_part = 0, o_int = 0;
 };
 
+// fn(i) for i in [0, n) on up to `threads` host threads (problems are independent)
+template <typename F>
+void parallel_for(int n, int threads, F fn) {
+    threads = std::max(1, std::min(threads, n));
+    if (threads == 1) {
+        for (int i = 0; i < n; i++) fn(i);
+        return;
+    }
+    std::atomic<int> next{0};
+    auto work = [&] {
+        for (int i; (i = next.fetch_add(1)) < n;) fn(i);
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; t++) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+}
+
+int host_threads() {
+    static const int n = [] {
+        const char* s = std::getenv("ORBHIP_BA_THREADS");
+        if (s && std::atoi(s) > 0) return std::atoi(s);
+        const unsigned hw = std::thread::hardware_concurrency();
+        return (int)std::min<unsigned>(16, hw ? hw : 1);
+    }();
+    return n;
+}
+
+constexpr int kPrepParallelE = 20000;   // edges from which one problem's pair lists use host threads
+
+// A persistent host worker pool for the preparation of one large problem: run(n, fn) calls fn(i)
+// for i in [0, n) on the caller and the idle workers (indices claimed dynamically, so it completes
+// on the caller alone if no worker is free), and returns when every call has returned. One run at a
+// time: a concurrent caller (another context's thread) runs its loop alone.
+class HostPool {
+  public:
+    static HostPool& get(int workers) {
+        static HostPool pool(workers);
+        return pool;
+    }
+    template <typename F>
+    void run(int n, F&& fn) {
+        std::unique_lock<std::mutex> busy(run_m_, std::try_to_lock);
+        if (!busy.owns_lock() || workers_.empty()) {
+            for (int i = 0; i < n; i++) fn(i);
+            return;
+        }
+        std::function<void(int)> job(fn);
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &job;
+            n_ = n;
+            next_.store(0, std::memory_order_relaxed);
+            active_ = (int)workers_.size();
+            gen_++;
+        }
+        cv_.notify_all();
+        for (int i; (i = next_.fetch_add(1)) < n;) job(i);
+        std::unique_lock<std::mutex> g(m_);
+        done_cv_.wait(g, [&] { return active_ == 0; });   // every worker has left this job
+        job_ = nullptr;
+    }
+
+  private:
+    explicit HostPool(int workers) {
+        for (int w = 0; w < workers; w++) workers_.emplace_back([this] { loop(); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+            gen_++;
+        }
+        cv_.notify_all();
+        for (auto& t : workers_) t.join();
+    }
+    void loop() {
+        unsigned long long seen = 0;
+        for (;;) {
+            std::function<void(int)>* job;
+            int n;
+            {
+                std::unique_lock<std::mutex> g(m_);
+                cv_.wait(g, [&] { return gen_ != seen; });
+                seen = gen_;
+                if (stop_) return;
+                job = job_;
+                n = n_;
+            }
+            if (job)
+                for (int i; (i = next_.fetch_add(1)) < n;) (*job)(i);
+            std::lock_guard<std::mutex> g(m_);
+            if (--active_ == 0) done_cv_.notify_one();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex run_m_, m_;
+    std::condition_variable cv_, done_cv_;
+    std::function<void(int)>* job_ = nullptr;
+    int n_ = 0, active_ = 0;
+    std::atomic<int> next_{0};
+    unsigned long long gen_ = 0;
+    bool stop_ = false;
+};
+
+// The Schur pair lists of prepare() on host threads, identical to the serial build:
+//   1. landmark chunk t (contiguous): its pairs counted per pose row ia;
+//   2. the same chunk writes its pairs (ib, ea, eb) at its per-row cursors (rows in order, chunks
+//      in order within a row: landmark order within a row);
+//   3. rows in parallel: a stable counting sort by ib gives the row's blocks (j = i always, others
+//      with pairs) and their pairs at the row's offset; then the blocks are listed row by row.
+void schur_pairs_parallel(Prep& o, const int* eopt, int threads) {
+    const int M = o.M, np = o.np;
+    const int T = std::max(1, std::min(threads, M / 512 + 1));
+    // scratch kept per calling thread across calls; the lambdas below run on the pool's threads, so
+    // they must reach it through these references (a thread_local named inside them would be the
+    // worker's own, empty instance)
+    static thread_local std::vector<size_t> rc_s, roff_s;
+    static thread_local std::vector<int> tj_s, tab_s;
+    static thread_local std::vector<std::vector<int>> rb_s;
+    std::vector<size_t>& rc = rc_s;
+    std::vector<size_t>& roff = roff_s;
+    std::vector<int>& tj = tj_s;
+    std::vector<int>& tab = tab_s;
+    std::vector<std::vector<int>>& rb = rb_s;
+    std::vector<int> m0(T + 1);
+    for (int t = 0; t <= T; t++) m0[t] = (int)((long long)M * t / T);
+    rc.assign((size_t)T * np, 0);
+    roff.assign(np + 1, 0);
+    rb.resize(np);
+    for (auto& v : rb) v.clear();
+    HostPool& pool = HostPool::get(host_threads() - 1);
+    pool.run(T, [&](int t) {
+        size_t* c = rc.data() + (size_t)t * np;
+        for (int m = m0[t]; m < m0[t + 1]; m++) {
+            const int k0 = o.pt_ptr[m], k1 = o.pt_ptr[m + 1];
+            for (int ka = k0; ka < k1; ka++) {
+                const int ia = eopt[ka];
+                if (ia < 0) continue;
+                for (int kb = k0; kb < k1; kb++) c[ia] += eopt[kb] >= ia;
+            }
+        }
+    });
+    size_t total = 0;
+    for (int i = 0; i < np; i++) {
+        roff[i] = total;
+        for (int t = 0; t < T; t++) {
+            const size_t v = rc[(size_t)t * np + i];
+            rc[(size_t)t * np + i] = total;
+            total += v;
+        }
+    }
+    roff[np] = total;
+    tj.resize(total);
+    tab.resize(2 * total);
+    o.blk_pairs.resize(2 * total);
+    pool.run(T, [&](int t) {
+        size_t* c = rc.data() + (size_t)t * np;
+        for (int m = m0[t]; m < m0[t + 1]; m++) {
+            const int k0 = o.pt_ptr[m], k1 = o.pt_ptr[m + 1];
+            for (int ka = k0; ka < k1; ka++) {
+                const int ia = eopt[ka];
+                if (ia < 0) continue;
+                const int ea = o.pt_edges[ka];
+                for (int kb = k0; kb < k1; kb++) {
+                    const int ib = eopt[kb];
+                    if (ib < ia) continue;
+                    const size_t slot = c[ia]++;
+                    tj[slot] = ib;
+                    tab[2 * slot] = ea;
+                    tab[2 * slot + 1] = o.pt_edges[kb];
+                }
+            }
+        }
+    });
+    const int RB = 8;   // rows per task
+    pool.run((np + RB - 1) / RB, [&](int task) {
+        static thread_local std::vector<int> cj;
+        cj.assign(np, 0);
+        for (int i = task * RB; i < std::min(np, task * RB + RB); i++) {
+            const size_t a = roff[i], b = roff[i + 1];
+            for (size_t k = a; k < b; k++) cj[tj[k]]++;
+            int s = 0;
+            for (int j = i; j < np; j++) {
+                const int cnt = cj[j];
+                if (j == i || cnt > 0) { rb[i].push_back(j); rb[i].push_back(cnt); }
+                cj[j] = s;   // from here on: the block's cursor within the row
+                s += cnt;
+            }
+            for (size_t k = a; k < b; k++) {
+                const size_t slot = a + (size_t)cj[tj[k]]++;
+                o.blk_pairs[2 * slot] = tab[2 * k];
+                o.blk_pairs[2 * slot + 1] = tab[2 * k + 1];
+            }
+            for (int j = i; j < np; j++) cj[j] = 0;
+        }
+    });
+    o.blk_ptr.assign(1, 0);
+    size_t s = 0;
+    for (int i = 0; i < np; i++)
+        for (size_t q = 0; q < rb[i].size(); q += 2) {
+            o.blk_i.push_back(i);
+            o.blk_j.push_back(rb[i][q]);
+            s += (size_t)rb[i][q + 1];
+            o.blk_ptr.push_back((int)s);
+        }
+}
+
+// a Prep for the next call with its vectors' capacity kept (no allocation / first-touch page
+// faults on the hot path: the C5 lists are a few MB)
+void prep_reset(Prep& o) {
+    o.rc = 0;
+    o.P = o.M = o.E = o.np = o.n = o.nblk = 0;
+    for (auto* v : {&o.opt, &o.pt_ptr, &o.pt_edges, &o.ps_ptr, &o.ps_edges, &o.blk_i, &o.blk_j, &o.blk_ptr,
+                    &o.blk_pairs, &o.row_first, &o.cb_tiles, &o.cb_off, &o.items, &o.fin})
+        v->clear();
+    o.own.clear();
+    o.nslot = 0;
+    o.use_dag = o.use_nd = o.use_nd_sh = false;
+    o.dag = DagPlan{};
+    o.nd = NdPlan{};
+    o.dag_task_cap = 0;
+    o.o_dag = o.o_dagi = o.o_red2 = 0;
+    o.o_chi2 = o.o_state = o.o_obs = o.o_scr = o.o_lin = o.o_S = o.o_L = o.o_part = o.o_int = 0;
+}
+
 inline void se3_from_float(const float* q, const float* t, double* out) {
     double x = q[0], y = q[1], z = q[2], w = q[3];
     if (w < 0) { x = -x; y = -y; z = -z; w = -w; }
@@ -1342,7 +1571,7 @@ inline void se3_from_float(const float* q, const float* t, double* out) {
     out[4] = t[0]; out[5] = t[1]; out[6] = t[2]; out[7] = 0;
 }
 
-int prepare(const orbhip_ba_problem* pr, Prep& o, int chunk) {
+int prepare(const orbhip_ba_problem* pr, Prep& o, int chunk, int threads) {
     const int P = pr->n_poses, M = pr->n_points, E = pr->n_edges;
     if (P < 0 || M < 0 || E < 0 || (P && (!pr->pose_q || !pr->pose_t || !pr->pose_fixed)) || (M && !pr->points) ||
         (E && (!pr->edge_pose || !pr->edge_point || !pr->edge_uv || !pr->edge_octave || !pr->inv_sigma2)))
@@ -1351,6 +1580,9 @@ int prepare(const orbhip_ba_problem* pr, Prep& o, int chunk) {
         if (pr->edge_pose[e] < 0 || pr->edge_pose[e] >= P || pr->edge_point[e] < 0 || pr->edge_point[e] >= M ||
             pr->edge_octave[e] < 0 || pr->edge_octave[e] >= pr->n_octaves)
             return ORBHIP_ERR_ARG;
+    static const bool pdbg = std::getenv("ORBHIP_PREP_DBG") != nullptr;
+    auto tus = [] { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    double tp[8] = {tus()};
     o.P = P; o.M = M; o.E = E;
     o.opt.assign(P, -1);
     int np = 0;
@@ -1387,41 +1619,67 @@ int prepare(const orbhip_ba_problem* pr, Prep& o, int chunk) {
             if (oi >= 0) o.ps_edges[fq[oi]++] = e;
         }
     }
-    // Schur pairs (a, b) of one landmark with opt(a) <= opt(b), grouped by block (i, j) with a
-    // counting sort on the dense block id i*np + j; within a block: landmark order (deterministic).
-    cnt.assign((size_t)np * np, 0);
-    size_t npairs = 0;
-    for (int m = 0; m < M; m++) {
-        const int k0 = o.pt_ptr[m], k1 = o.pt_ptr[m + 1];
-        for (int ka = k0; ka < k1; ka++) {
-            const int ia = eopt[ka];
-            if (ia < 0) continue;
-            int* row = cnt.data() + (size_t)ia * np;
-            for (int kb = k0; kb < k1; kb++) {
-                const int ib = eopt[kb];
-                if (ib < ia) continue;   // also drops the fixed poses (-1)
-                row[ib]++;
-                npairs++;
+    tp[1] = tus();
+    // Schur pairs (a, b) of one landmark with opt(a) <= opt(b), grouped by block (i, j) (row-major
+    // over i <= j, every diagonal block listed); within a block: landmark order (deterministic).
+    // Large problems: schur_pairs_parallel (the same lists, built on host threads)
+    if (threads > 1 && E >= kPrepParallelE) {
+        schur_pairs_parallel(o, eopt.data(), threads);
+    } else {
+        // a counting sort on the dense block id i*np + j
+        cnt.assign((size_t)np * np, 0);
+        size_t npairs = 0;
+        for (int m = 0; m < M; m++) {
+            const int k0 = o.pt_ptr[m], k1 = o.pt_ptr[m + 1];
+            for (int ka = k0; ka < k1; ka++) {
+                const int ia = eopt[ka];
+                if (ia < 0) continue;
+                int* row = cnt.data() + (size_t)ia * np;
+                for (int kb = k0; kb < k1; kb++) {
+                    const int ib = eopt[kb];
+                    if (ib < ia) continue;   // also drops the fixed poses (-1)
+                    row[ib]++;
+                    npairs++;
+                }
             }
         }
-    }
-    o.blk_ptr.assign(1, 0);
-    {
-        int s = 0;
-        for (int i = 0; i < np; i++) {
-            int* row = cnt.data() + (size_t)i * np;
-            for (int j = i; j < np; j++) {
-                const int c = row[j];
-                if (i == j || c > 0) {
-                    o.blk_i.push_back(i);
-                    o.blk_j.push_back(j);
-                    row[j] = s;   // from here on: the block's fill cursor
-                    s += c;
-                    o.blk_ptr.push_back(s);
+        o.blk_ptr.assign(1, 0);
+        {
+            int s = 0;
+            for (int i = 0; i < np; i++) {
+                int* row = cnt.data() + (size_t)i * np;
+                for (int j = i; j < np; j++) {
+                    const int c = row[j];
+                    if (i == j || c > 0) {
+                        o.blk_i.push_back(i);
+                        o.blk_j.push_back(j);
+                        row[j] = s;   // from here on: the block's fill cursor
+                        s += c;
+                        o.blk_ptr.push_back(s);
+                    }
+                }
+            }
+        }
+        o.blk_pairs.resize(2 * npairs);
+        int* bp = o.blk_pairs.data();
+        for (int m = 0; m < M; m++) {
+            const int k0 = o.pt_ptr[m], k1 = o.pt_ptr[m + 1];
+            for (int ka = k0; ka < k1; ka++) {
+                const int ia = eopt[ka];
+                if (ia < 0) continue;
+                const int ea = o.pt_edges[ka];
+                int* row = cnt.data() + (size_t)ia * np;
+                for (int kb = k0; kb < k1; kb++) {
+                    const int ib = eopt[kb];
+                    if (ib < ia) continue;
+                    const int slot = row[ib]++;
+                    bp[2 * (size_t)slot] = ea;
+                    bp[2 * (size_t)slot + 1] = o.pt_edges[kb];
                 }
             }
         }
     }
+    tp[2] = tus();
     o.nblk = (int)o.blk_i.size();
     {   // envelope of S: first pose column coupled to each pose row (blocks are stored i <= j)
         std::vector<int> fp(np);
@@ -1450,24 +1708,8 @@ int prepare(const orbhip_ba_problem* pr, Prep& o, int chunk) {
             o.items.insert(o.items.end(), {k0 + c * chunk, std::min(k1, k0 + (c + 1) * chunk), b, o.nslot + c});
         o.nslot += nch;
     }
-    o.blk_pairs.resize(2 * npairs);
-    int* bp = o.blk_pairs.data();
-    for (int m = 0; m < M; m++) {
-        const int k0 = o.pt_ptr[m], k1 = o.pt_ptr[m + 1];
-        for (int ka = k0; ka < k1; ka++) {
-            const int ia = eopt[ka];
-            if (ia < 0) continue;
-            const int ea = o.pt_edges[ka];
-            int* row = cnt.data() + (size_t)ia * np;
-            for (int kb = k0; kb < k1; kb++) {
-                const int ib = eopt[kb];
-                if (ib < ia) continue;
-                const int slot = row[ib]++;
-                bp[2 * (size_t)slot] = ea;
-                bp[2 * (size_t)slot + 1] = o.pt_edges[kb];
-            }
-        }
-    }
+    tp[3] = tus();
+    if (pdbg) std::fprintf(stderr, "prepare E=%d: csr %.0f us, pairs %.0f us, envelope+items %.0f us\n", E, tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2]);
     return ORBHIP_OK;
 }
 
@@ -1499,34 +1741,6 @@ struct HBuf {   // pinned host staging
         return e;
     }
 };
-
-// fn(i) for i in [0, n) on up to `threads` host threads (problems are independent)
-template <typename F>
-void parallel_for(int n, int threads, F fn) {
-    threads = std::max(1, std::min(threads, n));
-    if (threads == 1) {
-        for (int i = 0; i < n; i++) fn(i);
-        return;
-    }
-    std::atomic<int> next{0};
-    auto work = [&] {
-        for (int i; (i = next.fetch_add(1)) < n;) fn(i);
-    };
-    std::vector<std::thread> pool;
-    for (int t = 1; t < threads; t++) pool.emplace_back(work);
-    work();
-    for (auto& th : pool) th.join();
-}
-
-int host_threads() {
-    static const int n = [] {
-        const char* s = std::getenv("ORBHIP_BA_THREADS");
-        if (s && std::atoi(s) > 0) return std::atoi(s);
-        const unsigned hw = std::thread::hardware_concurrency();
-        return (int)std::min<unsigned>(16, hw ? hw : 1);
-    }();
-    return n;
-}
 
 }  // namespace
 
@@ -1560,6 +1774,7 @@ struct BaWorkspace {
     size_t done_cap = 0;
     HBuf<int> hto;             // pinned: the persistent solver's hand-off timeout count per problem
     long long dag_timeouts = 0, dag_reruns = 0;
+    std::vector<Prep> prep;    // the per-problem host preparations of the last call (capacity reused)
     NdWorkspace* nd = nullptr; // nested-dissection solves (created on first use)
     std::vector<NdWorkspace*> nds;   // sharded solves by segments: one per shard of this process
     DBuf<double*> ptab;        // in-process shards: the collectives' pointer tables
@@ -1602,11 +1817,21 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const double t_start = now();
     const int nth = host_threads();
-    std::vector<Prep> pp(B);
+    // the per-problem preparations, kept in the workspace across calls (their vectors' capacity:
+    // no allocation on the hot path). A DAG-timeout re-run re-enters with the same workspace as a
+    // tail call, after this frame's last use of them.
+    if (ws->prep.size() < (size_t)B) ws->prep.resize(B);
+    std::vector<Prep>& pp = ws->prep;
+    for (int b = 0; b < B; b++) prep_reset(pp[b]);
     // Schur work-item size: a batch fills the chip with 16 pairs per lane; a few problems alone
     // would leave it mostly idle, so their items are cut to 4 pairs (4x the lanes)
     const int chunk = B >= 32 ? kSchurChunk : 4;
-    parallel_for(B, nth, [&](int b) { pp[b].rc = prepare(probs[b], pp[b], chunk); });
+    // one problem: its Schur pair lists on the host threads; a batch: one problem per thread
+    // (ORBHIP_PREP_THREADS=k: one large problem's pair lists on k host threads; off by default: on
+    // the MI355X box's EPYC the C5 build went 0.62 -> 0.55 ms at 16 threads, 0.71 at 4 (its
+    // scattered fill does not scale), and it measured slower on the 8-core container)
+    static const int prep_par = std::getenv("ORBHIP_PREP_THREADS") ? std::atoi(std::getenv("ORBHIP_PREP_THREADS")) : 1;
+    parallel_for(B, nth, [&](int b) { pp[b].rc = prepare(probs[b], pp[b], chunk, B == 1 ? prep_par : 1); });
     const double t_prepare = now();
     for (int b = 0; b < B; b++)
         if (pp[b].rc) return pp[b].rc;
@@ -1726,7 +1951,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     //   R  the rest (scratch), then the edge linearisations e_lin (32-byte aligned), S (n*n) and
     //      the panel inverses Lsave, 16-byte aligned
     size_t nC = 0, nA = 0, nU = 0, nR = 0, ni = 0;
-    for (auto& p : pp) {
+    for (int b = 0; b < B; b++) {
+        Prep& p = pp[b];
         const size_t P = p.P, M = p.M, E = p.E, np_ = p.np, n = p.n;
         p.o_chi2 = nC; nC += E;
         p.o_state = nA; nA += 8 * P + 3 * M;
@@ -2185,7 +2411,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 hipLaunchKernelGGL(k_ba_sh_end, dim3(B), dim3(64), 0, st, dA, d_act, donep);
             }
             int maxPM = 0;
-            for (auto& p : pp) maxPM = std::max(maxPM, std::max(8 * p.P, 3 * p.M));
+            for (int b = 0; b < B; b++) maxPM = std::max(maxPM, std::max(8 * pp[b].P, 3 * pp[b].M));
             if (!all_small) hipLaunchKernelGGL(k_ba_pop, dim3(gx(maxPM, 256), B), b256, 0, st, dA, d_act);
             BAOK(hipGetLastError());
             return ORBHIP_OK;
@@ -2369,6 +2595,43 @@ int ba_solve(BaWorkspace* ws, const orbhip_ba_problem* prob, orbhip_ba_result* r
     const orbhip_ba_problem* pp[1] = {prob};
     orbhip_ba_result* rr[1] = {res};
     return ba_solve_batch(ws, pp, 1, rr, stop, st, kShardNone);
+}
+
+int ba_test_prepare(const orbhip_ba_problem* pr, int threads, double* out4) {
+    Prep a, b;
+    int rc = prepare(pr, a, kSchurChunk, 1);
+    if (rc) return rc;
+    auto ms_since = [](std::chrono::steady_clock::time_point t) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+    };
+    // out4[3]: the threaded build (threads > 1) or the serial build into a reused Prep (threads = 1)
+    if (threads == 1) {
+        prep_reset(a);
+        const auto t1 = std::chrono::steady_clock::now();
+        rc = prepare(pr, a, kSchurChunk, 1);
+        const double ms1 = ms_since(t1);
+        if (rc) return rc;
+        if (out4) out4[3] = ms1;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    rc = prepare(pr, b, kSchurChunk, threads);
+    const double ms = ms_since(t0);
+    if (rc) return rc;
+    if (threads == 1) {
+        if (out4) { out4[0] = b.nblk; out4[1] = (double)(b.blk_pairs.size() / 2); out4[2] = ms; }
+        return a.blk_pairs == b.blk_pairs ? ORBHIP_OK : -1;
+    }
+    const bool same = a.opt == b.opt && a.pt_ptr == b.pt_ptr && a.pt_edges == b.pt_edges && a.ps_ptr == b.ps_ptr &&
+                      a.ps_edges == b.ps_edges && a.blk_i == b.blk_i && a.blk_j == b.blk_j && a.blk_ptr == b.blk_ptr &&
+                      a.blk_pairs == b.blk_pairs && a.row_first == b.row_first && a.items == b.items && a.fin == b.fin &&
+                      a.nslot == b.nslot && a.nblk == b.nblk;
+    if (out4) {
+        out4[0] = b.nblk;
+        out4[1] = (double)(b.blk_pairs.size() / 2);
+        out4[2] = (double)(b.items.size() / 4);
+        out4[3] = ms;
+    }
+    return same ? ORBHIP_OK : -1;
 }
 
 void ba_stats(BaWorkspace* ws, long long* timeouts, long long* reruns) {

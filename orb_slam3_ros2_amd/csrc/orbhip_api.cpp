@@ -1526,6 +1526,11 @@ int orbhip_test_cholesky_dag(const double* A, const double* b, double* x, int n,
     if (!A || !b || !x || n <= 0 || reps < 1) return ORBHIP_ERR_ARG;
     return chol_dag_test(A, b, x, n, reps, max_helpers, ms, dbg);
 }
+// host only (no device): the BA preparation serial vs on host threads (identical lists -> 0)
+int orbhip_test_ba_prepare(const orbhip_ba_problem* prob, int threads, double* out4) {
+    if (!prob || threads < 1) return ORBHIP_ERR_ARG;
+    return ba_test_prepare(prob, threads, out4);
+}
 // nested-dissection solve of a pose-structured SPD system (ba_nd.hip): K segments (0 = planned)
 int orbhip_test_nd_solve(const double* A, const double* b, double* x, int np, const int* bi, const int* bj, int nblk,
                          int K, int reps, float* ms, int* K_used) {

@@ -24,4 +24,7 @@ int ba_comm_unique_id(void* id);
 int ba_test_cholesky_reg(const double* A, const double* b, double* x, int n, int reps, float* ms,
                          unsigned long long* phases5);
 int ba_test_cholesky(const double* A, const double* b, double* x, int n, unsigned long long* phases5, float* ms);
+// host only: the problem preparation serial and on `threads` host threads; 0 when every list is
+// identical (out4: blocks, pairs, Schur items, host ms of the threaded build), -1 otherwise
+int ba_test_prepare(const orbhip_ba_problem* pr, int threads, double* out4);
 }  // namespace orbhip
