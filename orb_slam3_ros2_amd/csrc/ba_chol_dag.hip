@@ -60,6 +60,11 @@ constexpr int kNewton = ORBHIP_DAG_NEWTON;   // Newton steps after v_rsq_f64 / v
 #ifndef ORBHIP_DAG_FLAG_AHEAD
 #define ORBHIP_DAG_FLAG_AHEAD 0   // waves 2/3 load the next interval's helper flag before the barrier
 #endif
+#ifndef ORBHIP_DAG_T_W1
+// r05: wave 1 (idle after its publishes) applies T_{k+1}'s column-k term for waves 2 / 3: the
+// interval 13.55k -> 12.8k cycles at n = 294 (every wave now ends within ~0.6k of the others)
+#define ORBHIP_DAG_T_W1 1
+#endif
 #ifndef ORBHIP_DAG_BACK_COL
 #define ORBHIP_DAG_BACK_COL 0   // the chain-only backward on column-major tile loads (bwd_col_dot)
 #endif
@@ -601,6 +606,8 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     int* F1 = word + 10;                // wave 0: row 0 of L(k+1, k) ready (k + 2)
     int* F2 = word + 11;                // wave 1: D(1,0), D(1,1), r1 of tile k+1 ready
     int* F3 = word + 12;                // wave 1: row 1 of L(k+1, k) ready
+    int* F4 = word + 13;                // wave 2 / 3: their rows of T_{k+1} up to column k-1 in TpN
+    int* F5 = word + 14;
     unsigned long long* wts = (unsigned long long*)(lds + 11264 + 8);   // per-wave cycles (dbg)
     unsigned long long* stm = (unsigned long long*)(lds + 10560);       // sub-phase stamps (dbg), 16
 #define DAG_STAMP(i) do { if (dbg && lane == 0) stm[i] = __builtin_amdgcn_s_memtime() - tk; } while (0)
@@ -614,6 +621,8 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         *F1 = 0;
         *F2 = 0;
         *F3 = 0;
+        *F4 = 0;
+        *F5 = 0;
     }
     for (int i = tid; i < NT; i += blockDim.x) rfl[i] = a.rf[i];
     int c1 = 0, c2 = 0;
@@ -834,6 +843,28 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 st_flag(L.fL + k1 * NT + k, epoch);
                 if (k >= 1) st_flag(L.fL + k1 * NT + k - 1, epoch);
             }
+#if ORBHIP_DAG_T_W1
+            // T_{k+1} -= L(k+2, k) L(k+1, k)^T for both row halves of waves 2 / 3 (their partials
+            // in TpN, their rows of L(k+2, k) in L2n): off their critical path, the same MFMAs
+            // in the same order as theirs
+            if (K2 < NT && useTk) {
+                lds_wait(F4, k + 2);
+                lds_wait(F5, k + 2);
+                if (!word[4]) {
+#pragma unroll
+                    for (int h = 0; h < 2; h++) {
+                        const double4_t o0 = lq(L2n + (2 * h) * 256), o1 = lq(L2n + (2 * h + 1) * 256);
+#pragma unroll
+                        for (int c = 0; c < 2; c++) {
+                            double4_t tc = lq(TpN + (2 * h + c) * 256), tb = {0, 0, 0, 0};
+                            mfma_sub(tc, lq(L1n + (2 * c) * 256), o0);
+                            mfma_sub(tb, lq(L1n + (2 * c + 1) * 256), o1);
+                            sq(TpN + (2 * h + c) * 256, tc + tb);
+                        }
+                    }
+                }
+            }
+#endif
         } else if (K2 < NT) {
             // row h of L(k+2, k) = U Linv_k^T, U = A(k+2, k) - sum_{p <= k-1} L(k+2,p) L(k,p)^T (the
             // helpers' partial: p <= k-2; here p = k-1); row h of T_{k+1} = A(k+2, k+1) - sum_{p <= k}
@@ -845,6 +876,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             if (dbg && lane == 0 && h == 1) wts[4] = __builtin_amdgcn_s_memtime() - tk;   // helpers' flags in
             if (!got) {
                 if (lane == 0) word[4] = 1;
+                if (ORBHIP_DAG_T_W1) lds_signal(h ? F5 : F4, k + 2);
             } else {
                 const int tD = L.oL + (K2 * NT + k - 1) * kTD;
                 double4_t d0 = {0, 0, 0, 0}, d1 = {0, 0, 0, 0}, e0 = {0, 0, 0, 0}, e1 = {0, 0, 0, 0};
@@ -913,6 +945,11 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                         t[c] += tb;
                     }
                 }
+#if ORBHIP_DAG_T_W1
+                sq(TpN + (2 * h) * 256, t[0]);
+                sq(TpN + (2 * h + 1) * 256, t[1]);
+                lds_signal(h ? F5 : F4, k + 2);
+#endif
                 DAG_STAMP(12 + 2 * h);
                 {   // D'_{k+2}: column k-1 (L(k+2, k-1)) and column k (L(k+2, k)) in independent chains
                     double4_t da = {0, 0, 0, 0}, db = {0, 0, 0, 0}, dc = {0, 0, 0, 0}, de = {0, 0, 0, 0};
@@ -952,6 +989,9 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 }
                 if (rg == 0) rpN[16 * h + cc] = rr;
                 DAG_STAMP(6 + 4 * h);
+#if ORBHIP_DAG_T_W1
+                DAG_STAMP(7 + 4 * h);
+#else
                 // the column k term of T_{k+1} needs both rows of L(k+1, k)
                 lds_wait(F1, k + 2);
                 lds_wait(F3, k + 2);
@@ -967,6 +1007,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 }
                 sq(TpN + (2 * h) * 256, t[0]);
                 sq(TpN + (2 * h + 1) * 256, t[1]);
+#endif
             }
         }
         if (ORBHIP_DAG_FLAG_AHEAD && wid >= 2 && k + 1 < kEnd) {
