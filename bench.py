@@ -493,9 +493,7 @@ def cpu_lba(prob, budget_s=8.0):
 
 def c5_gba(ws, rank, iters):
     """C5 GlobalBundleAdjustment (400 KF loop, 20k points, 80k obs, 20-KF co-visibility window).
-    One GPU: the nested-dissection solve of the reduced camera system (csrc/ba_nd.hip), and beside it
-    the same solve in its sharded form on one RCCL rank holding all 8 segments
-    (orbhip_ba_solve_sharded_segments: every collective of the sharded slot through RCCL).
+    One GPU: the nested-dissection solve of the reduced camera system (csrc/ba_nd.hip).
     N > 1: c5_gba_ms is the sharded solve (ORBHIP_C5_SHARDED=0 turns it off): the keyframe loop cut
     into N segments, rank r holding segment r's landmarks (sharding.shard_problem_nd); each rank
     factors its interior, the separator system and the pose update are all-reduced over RCCL inside
@@ -544,13 +542,6 @@ def c5_gba(ws, rank, iters):
         mode = f"replicas x{ws} (one GPU per solve, nested dissection)" if ws > 1 else \
             "one GPU (nested dissection, device-driven LM)"
         r, t = run(lambda: opt.solve(prob))
-        if ws == 1:   # the sharded form's collectives on one RCCL rank holding all 8 segments
-            sopt = Optimizer()
-            sopt.comm_init(1, 0, Optimizer.comm_unique_id())
-            segs = [shard_problem_nd(prob, q, 8)[0] for q in range(8)]
-            rs, ts = run(lambda: sopt.solve_sharded_segments(segs))
-            out["c5_gba_rccl_1rank_8seg_ms"] = round(1e3 * ts, 2)
-            out["c5_gba_rccl_1rank_8seg_trials"] = rs[0].lm_trials
     out.update({"c5_gba_ms": round(1e3 * t, 2), "c5_gba_iterations": r.iterations_done, "c5_gba_trials": r.lm_trials,
                 "c5_gba_chi2": [round(r.initial_chi2, 1), round(r.final_chi2, 1)], "c5_gba_mode": mode})
     return out
