@@ -2175,8 +2175,11 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         if (!p.use_dag && !p.use_nd && !p.use_nd_sh && p.n > kCholRegMaxN) s_written = true;   // the LDS and blocked solvers factor S in place
     }
     const size_t chol_lds = sizeof(double) * chol_lds_doubles(maxN);
-    // every problem on a solver that reads S and never writes it (register / DAG), no shard sums
-    const bool s_readonly = !s_written && shard_mode == kShardNone;
+    // every problem on a solver that reads S and never writes it (register / DAG / dissection) and no
+    // sum of S over the shards (the replicated form all-reduces S in place): S is zeroed once, the
+    // Schur finisher overwrites its blocks every trial (r05: segment shards too, which saved a
+    // 46 MB memset per shard and trial at C5)
+    const bool s_readonly = !s_written && (shard_mode == kShardNone || nd_sh);
     auto large_solve = [&](int b, const int* gate) -> int {
         if (pp[b].use_nd) {
             (void)gate;   // set at nd_setup
