@@ -425,9 +425,21 @@ __device__ __forceinline__ void lds_only_barrier() {
     asm volatile("" ::: "memory");
 }
 
+// the compact resize tables (one per level, shared by every tile: r05) — the same entries the
+// host packs per tile in ctab, read from the plan's per-level tables instead, so a launch's tiles
+// share a ~40 KB working set (the per-tile copies were ~3.5 KB per tile, ~0.9 MB per 640x480 launch,
+// most of k_pyr_cone's fetched bytes)
+struct ConeTabs {
+    const int* xofs;
+    const int* xalpha;
+    const int* yofs;
+    const int* ybeta;
+};
+
 __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P, const FrameBufs& fb,
                                               const ConeRect* __restrict__ rects, const int* __restrict__ ctab,
-                                              int tab_stride, uint8_t* __restrict__ cone, int tile, int f, int s0) {
+                                              int tab_stride, uint8_t* __restrict__ cone, int tile, int f, int s0,
+                                              const ConeTabs& ct) {
     TR_BEGIN()
     const int L = P->n_levels, tid = threadIdx.x, nt = blockDim.x;
     const ConeRect* R = rects + (size_t)tile * kMaxLevels;
@@ -448,14 +460,33 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
         toff[l] = ttot;
         ttot += 2 * (R[l].nx1 - R[l].nx0) + 3 * (R[l].ny1 - R[l].ny0);
     }
-    // ---- one round trip: the tile's tables of every level (prebuilt by the host in LDS layout)
-    // and its level-0 cone, all loads issued before any store ----
+    // staged table entry i (LDS layout: per level l > s0, xofs[nw] | xalpha[nw] | (r0, r1, beta)[nh]):
+    // from the compact per-level tables when the plan has them, else the host's per-tile copy
+    const int* gt = ctab + (size_t)tile * tab_stride;
+    auto tab_at = [&](int i) -> int {
+        if (!ct.xofs) return gt[i];
+        int l = s0 + 1;
+#pragma unroll
+        for (int q = 2; q < kMaxLevels; q++)
+            if (q > s0 + 1 && q < L && i >= toff[q]) l = q;
+        const ConeRect r = R[l];
+        const LevelGeom& D = P->lv[l];
+        const int nw = r.nx1 - r.nx0, j = i - toff[l];
+        if (j < nw) return ct.xofs[D.xtab_off + r.nx0 + j];
+        if (j < 2 * nw) return ct.xalpha[D.xtab_off + r.nx0 + j - nw];
+        const int jj = j - 2 * nw, row = (jj * 21846) >> 16, comp = jj - 3 * row;   // jj / 3 (jj < 2^15)
+        const int y = D.ytab_off + r.ny0 + row;
+        if (comp == 2) return ct.ybeta[y];
+        const int sy = ct.yofs[y] + comp, hs = P->lv[l - 1].h;
+        return sy < 0 ? 0 : (sy < hs ? sy : hs - 1);
+    };
+    // ---- one round trip: the tile's tables of every level and its level-0 cone, all loads issued
+    // before any store ----
     {
         const ImgRef in0 = level_img(P, fb, f, s0);
         const ConeRect r = R[s0];
         const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0;
         const uint8_t* src0 = in0.p + (int64_t)r.ny0 * in0.pitch + r.nx0;
-        const int* gt = ctab + (size_t)tile * tab_stride;
         const bool dw = ((in0.pitch & 3) == 0) && ((((uintptr_t)in0.p) & 3) == 0);
         if (dw) sh0 = (int)(((uintptr_t)src0) & 3);
         const int nwd = dw ? (nw + sh0 + 3) >> 2 : 0;   // dwords per row (<= P0 / 4)
@@ -467,7 +498,7 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
             const int p4 = in0.pitch >> 2;
             int tv[2];
 #pragma unroll
-            for (int u = 0; u < 2; u++) tv[u] = gt[min(tid + 1024 * u, ttot - 1)];
+            for (int u = 0; u < 2; u++) tv[u] = tab_at(min(tid + 1024 * u, ttot - 1));
             const int i = min(tid, tot0 - 1);
             const int y = small_div(i, inv_n), x = i - y * nwd;
             const uint32_t v = s4[(int64_t)y * p4 + x];
@@ -484,7 +515,7 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
             for (int i0 = tid; i0 < ttot; i0 += U * nt) {
                 int v[U];
 #pragma unroll
-                for (int u = 0; u < U; u++) v[u] = gt[min(i0 + u * nt, ttot - 1)];
+                for (int u = 0; u < U; u++) v[u] = tab_at(min(i0 + u * nt, ttot - 1));
 #pragma unroll
                 for (int u = 0; u < U; u++)
                     if (i0 + u * nt < ttot) tab[i0 + u * nt] = v[u];
@@ -504,7 +535,7 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
                     if (i0 + u * nt < tot0) ((uint32_t*)lv0)[o[u]] = v[u];
             }
         } else {
-            for (int i = tid; i < ttot; i += nt) tab[i] = gt[i];
+            for (int i = tid; i < ttot; i += nt) tab[i] = tab_at(i);
             for (int i = tid; i < tot0; i += nt) {
                 const int y = small_div(i, inv_n), x = i - y * nw;
                 lv0[y * P0 + x] = src0[(int64_t)y * in0.pitch + x];
@@ -564,11 +595,11 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
 
 __global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict__ P, FrameBufs fb,
                                                    const ConeRect* __restrict__ rects, const int* __restrict__ ctab,
-                                                   int tab_stride, int xrun, int s0) {
+                                                   int tab_stride, int xrun, int s0, ConeTabs ct) {
     extern __shared__ __attribute__((aligned(16))) uint8_t cone[];
     if (fb.stamp && threadIdx.x == 0) atomicMin(fb.stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
-    pyr_cone_body(P, fb, rects, ctab, tab_stride, cone, lg % X, lg / X, s0);
+    pyr_cone_body(P, fb, rects, ctab, tab_stride, cone, lg % X, lg / X, s0, ct);
     if (fb.stamp) {   // the workgroup's end: every wave's stores drained (the barrier waits on them)
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(fb.stamp + kStampStride, (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -2188,9 +2219,14 @@ __global__ __launch_bounds__(256) void k_desc_kp(const ExtractPlan* __restrict__
 // HBM traffic per launch, against 183 MB algorithmic; the time is unchanged, the kernel is
 // VALU-bound). Smaller batches: runs of 16. One frame: the plain round-robin order (grouping
 // neighbours onto one XCD measured ~1% below it on the 16-camera C2 stream).
+// XCD-grouped work-group order (xcd_runs): whole frames per XCD for big batches, runs of 16 for
+// small ones, runs of 8 at one frame (r05: at one frame the grouped order measured the same
+// 16-camera throughput as round-robin, 38.9k / 38.8k frames/s on one box, and cut the PMC bytes per
+// launch of k_pyr_cone 2.89 -> 2.18 MB, k_fast_cells 4.16 -> 1.69 MB, k_desc_kp 5.24 -> 3.57 MB:
+// neighbouring tiles' shared lines stay in one L2; r02 had measured it ~1% slower)
 static int xcd_run_for(int B) {
     static const int env = getenv("ORBHIP_XCD_RUN") ? atoi(getenv("ORBHIP_XCD_RUN")) : -2;
-    return env >= -1 ? env : (B >= 8 ? -1 : (B > 1 ? 16 : 0));
+    return env >= -1 ? env : (B >= 8 ? -1 : (B > 1 ? 16 : 8));
 }
 
 void launch_resize(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& fb, int B, int l,
@@ -2216,11 +2252,15 @@ void launch_resize_bands(const ExtractPlan* dP, int nbands, const FrameBufs& fb,
 }
 
 void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameBufs& fb, int B, const ConeRect* rects,
-                     const int* ctab, int tab_stride, hipStream_t st, int s0, int nthreads) {
+                     const int* ctab, int tab_stride, hipStream_t st, int s0, int nthreads, const int* xofs,
+                     const int* xalpha, const int* yofs, const int* ybeta) {
     static LdsAttrOnce attr;   // per device, thread-safe (dev_attr.h)
     (void)attr.ensure((const void*)k_pyr_cone, 64 * 1024);
+    // ORBHIP_CONE_TABS=tile keeps the host's per-tile table copies (A/B)
+    static const bool per_tile = getenv("ORBHIP_CONE_TABS") && getenv("ORBHIP_CONE_TABS")[0] == 't';
+    const ConeTabs ct = per_tile ? ConeTabs{nullptr, nullptr, nullptr, nullptr} : ConeTabs{xofs, xalpha, yofs, ybeta};
     ORBHIP_LAUNCH(k_pyr_cone, dim3(ntiles, B), dim3(nthreads), lds, st, dP, fb, rects, ctab, tab_stride,
-                  xcd_run_for(B), s0);
+                  xcd_run_for(B), s0, ct);
 }
 
 void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,

@@ -755,7 +755,8 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
         fb.stamp = (cone_path && tm.stage == 1 && tm.dstamp && tm.n < StageTimer::kCap) ? tm.dstamp + tm.n : nullptr;
         if (cone_path) {
             launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_cone_tab.p,
-                            pl->cone_tab_stride, st);
+                            pl->cone_tab_stride, st, 0, 1024, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p,
+                            pl->d_ybeta.p);
         } else if (flow_on) {
             PyrFlow fa{};
             fa.ctl = c->d_flow.p;
@@ -774,7 +775,8 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
                               st);
             if (cone_hi)
                 launch_pyr_cone(pl->d_plan.p, pl->cone_hi_tiles, pl->cone_hi_lds, fb, B, pl->d_cone_hi.p,
-                                pl->d_cone_hi_tab.p, pl->cone_hi_tab_stride, st, kConeHiStart, cone_hi_threads());
+                                pl->d_cone_hi_tab.p, pl->cone_hi_tab_stride, st, kConeHiStart, cone_hi_threads(),
+                                pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p, pl->d_ybeta.p);
             if (bands)
                 launch_resize_bands(pl->d_plan.p, pl->nbands, fb, B, kBandStart, (const int2*)pl->d_bands.p,
                                     pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p, pl->d_ybeta.p, st);

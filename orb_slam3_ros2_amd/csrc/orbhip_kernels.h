@@ -80,7 +80,9 @@ struct StageScope {
 // s0 = 0: levels 1..L-1 from the frame (1024 threads per tile); s0 >= 1: levels s0+1..L-1 from
 // pyramid level s0 (written by k_resize before), `nthreads` per tile
 void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameBufs& fb, int B, const ConeRect* rects,
-                     const int* ctab, int tab_stride, hipStream_t st, int s0 = 0, int nthreads = 1024);
+                     const int* ctab, int tab_stride, hipStream_t st, int s0 = 0, int nthreads = 1024,
+                     const int* xofs = nullptr, const int* xalpha = nullptr, const int* yofs = nullptr,
+                     const int* ybeta = nullptr);
 // levels s0+1..L-1 in one launch, nbands row bands per frame (rows: [nbands][kMaxLevels] int2)
 void launch_resize_bands(const ExtractPlan* dP, int nbands, const FrameBufs& fb, int B, int s0, const int2* rows,
                          const int* xofs, const int* xalpha, const int* yofs, const int* ybeta, hipStream_t st);
