@@ -21,7 +21,8 @@ class OrbHipError(RuntimeError):
 
 
 def library_path() -> str:
-    return os.path.join(_HERE, _LIB_NAME)
+    # ORBHIP_LIB: an A/B build of the same library (tools/build_ab.sh); default the in-tree build
+    return os.environ.get("ORBHIP_LIB") or os.path.join(_HERE, _LIB_NAME)
 
 
 class KP(ctypes.Structure):

@@ -425,10 +425,9 @@ __device__ __forceinline__ void lds_only_barrier() {
     asm volatile("" ::: "memory");
 }
 
-// the compact resize tables (one per level, shared by every tile: r05) — the same entries the
-// host packs per tile in ctab, read from the plan's per-level tables instead, so a launch's tiles
-// share a ~40 KB working set (the per-tile copies were ~3.5 KB per tile, ~0.9 MB per 640x480 launch,
-// most of k_pyr_cone's fetched bytes)
+// the compact resize tables (one per level, shared by every tile; r05, optional) — the same entries
+// the host packs per tile in ctab, read from the plan's per-level tables instead, so a launch's
+// tiles share a ~40 KB working set instead of ~3.5 KB of copies per tile
 struct ConeTabs {
     const int* xofs;
     const int* xalpha;
@@ -620,6 +619,9 @@ __global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict
 // 1534) is an exact f16 integer, so every min / max / difference is exact.
 // ---------------------------------------------------------------------------
 constexpr int kWinMax = 80;
+#ifndef ORBHIP_FAST_LEAN
+#define ORBHIP_FAST_LEAN 1   // r05: branch-free pair-test round, mbcnt positions (A/B: 0 = r04's form)
+#endif
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));   // two pixels, one per 16-bit half
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 constexpr uint32_t kPwBias = 0x64006400u;                   // f16(1024) in both halves
@@ -784,6 +786,46 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     const int nq = R * dc, qb = R * dc;
     const int ystep = NT / dc, xstep = NT - ystep * dc;
     int y = small_div(tid, inv_dc), x = tid - y * dc;
+#if ORBHIP_FAST_LEAN
+    // r05: the round without a branch (a lane past the last pixel reads a clamped row and passes
+    // nothing), the list positions by mbcnt, the capacity checked once per wave and round
+    (void)lt;
+    for (int q0 = 0; q0 < nq; q0 += NT) {
+        const int q = q0 + tid;
+        const bool in = q < nq;
+        const uint32_t* c = pw + min(y, R - 1) * PWP + x + sh;
+        h2 cc[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) cc[k] = as_h2(c[C::o[k]]);
+        const h2 v = as_h2(c[C::o[16]]);
+        h2 M1 = hmax(cc[0], cc[8]), M2 = hmin(cc[0], cc[8]);
+#pragma unroll
+        for (int k = 1; k < 8; k++) {
+            M1 = hmin(M1, hmax(cc[k], cc[k + 8]));
+            M2 = hmax(M2, hmin(cc[k], cc[k + 8]));
+        }
+        const h2 s = hmax(M1 - (v + tv), v - (M2 + tv));   // > 0: passes (exact integers)
+        const bool pass0 = in & (s.x > (_Float16)0);
+        const bool pass1 = in & (y + R < dr) & (s.y > (_Float16)0);
+        // the compare masks as they are (HIP's __ballot(int) makes a lane value of each and compares
+        // it again)
+        const uint64_t b0 = __builtin_amdgcn_ballot_w64(pass0), b1 = __builtin_amdgcn_ballot_w64(pass1);
+        const int n0 = __popcll(b0), n1 = __popcll(b1);
+        const int ci0 = wcnt + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0, 0u));
+        const int ci1 = wcnt + n0 + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, 0u));
+        if (wcnt + n0 + n1 <= capw) {   // wave-uniform: the round's survivors all fit
+            if (pass0) wlist[ci0] = (uint16_t)q;
+            if (pass1) wlist[ci1] = (uint16_t)(q + qb);
+        } else {
+            if (pass0 && ci0 < capw) wlist[ci0] = (uint16_t)q;
+            if (pass1 && ci1 < capw) wlist[ci1] = (uint16_t)(q + qb);
+        }
+        wcnt += n0 + n1;
+        x += xstep;
+        y += ystep;
+        if (x >= dc) { x -= dc; y++; }
+    }
+#else
     for (int q0 = 0; q0 < nq; q0 += NT) {
         const int q = q0 + tid;
         bool pass0 = false, pass1 = false;
@@ -812,6 +854,7 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
         y += ystep;
         if (x >= dc) { x -= dc; y++; }
     }
+#endif
     if (lane == 0) LS.ncw[wid] = wcnt;
     __syncthreads();
     // dense: a wave's list overflowed, so the strength runs on every pixel instead (m <= t_lo for
@@ -2256,8 +2299,10 @@ void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameB
                      const int* xalpha, const int* yofs, const int* ybeta) {
     static LdsAttrOnce attr;   // per device, thread-safe (dev_attr.h)
     (void)attr.ensure((const void*)k_pyr_cone, 64 * 1024);
-    // ORBHIP_CONE_TABS=tile keeps the host's per-tile table copies (A/B)
-    static const bool per_tile = getenv("ORBHIP_CONE_TABS") && getenv("ORBHIP_CONE_TABS")[0] == 't';
+    // the host's per-tile table copies by default; ORBHIP_CONE_TABS=level reads the compact per-level
+    // tables instead (r05 A/B: 130 KB fewer fetched bytes per 640x480 launch, but every staged entry
+    // then waits on its level's ConeRect before its table load: 20.8 -> 26.9 us per launch)
+    static const bool per_tile = !(getenv("ORBHIP_CONE_TABS") && getenv("ORBHIP_CONE_TABS")[0] == 'l');
     const ConeTabs ct = per_tile ? ConeTabs{nullptr, nullptr, nullptr, nullptr} : ConeTabs{xofs, xalpha, yofs, ybeta};
     ORBHIP_LAUNCH(k_pyr_cone, dim3(ntiles, B), dim3(nthreads), lds, st, dP, fb, rects, ctab, tab_stride,
                   xcd_run_for(B), s0, ct);
