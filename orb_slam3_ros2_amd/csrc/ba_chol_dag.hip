@@ -65,6 +65,11 @@ constexpr int kNewton = ORBHIP_DAG_NEWTON;   // Newton steps after v_rsq_f64 / v
 // interval 13.55k -> 12.8k cycles at n = 294 (every wave now ends within ~0.6k of the others)
 #define ORBHIP_DAG_T_W1 1
 #endif
+#ifndef ORBHIP_DAG_Q10_W2
+// r05: wave 2 computes the column k-1 term of D'_{k+2}'s quadrant (1,0) for wave 3 (which had 6
+// of the 10 D' products), handing it over in LDS (Q10, flag F6)
+#define ORBHIP_DAG_Q10_W2 1
+#endif
 #ifndef ORBHIP_DAG_BACK_COL
 #define ORBHIP_DAG_BACK_COL 0   // the chain-only backward on column-major tile loads (bwd_col_dot)
 #endif
@@ -608,6 +613,8 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     int* F3 = word + 12;                // wave 1: row 1 of L(k+1, k) ready
     int* F4 = word + 13;                // wave 2 / 3: their rows of T_{k+1} up to column k-1 in TpN
     int* F5 = word + 14;
+    int* F6 = word + 15;                // wave 2: Q10 holds quadrant (1,0)'s column k-1 term
+    double* Q10 = (double*)(rfl + NT + (NT & 1));   // 256 doubles after the row_first ints
     unsigned long long* wts = (unsigned long long*)(lds + 11264 + 8);   // per-wave cycles (dbg)
     unsigned long long* stm = (unsigned long long*)(lds + 10560);       // sub-phase stamps (dbg), 16
 #define DAG_STAMP(i) do { if (dbg && lane == 0) stm[i] = __builtin_amdgcn_s_memtime() - tk; } while (0)
@@ -623,6 +630,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         *F3 = 0;
         *F4 = 0;
         *F5 = 0;
+        *F6 = 0;
     }
     for (int i = tid; i < NT; i += blockDim.x) rfl[i] = a.rf[i];
     int c1 = 0, c2 = 0;
@@ -877,6 +885,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             if (!got) {
                 if (lane == 0) word[4] = 1;
                 if (ORBHIP_DAG_T_W1) lds_signal(h ? F5 : F4, k + 2);
+                if (ORBHIP_DAG_Q10_W2 && h == 0) lds_signal(F6, k + 2);
             } else {
                 const int tD = L.oL + (K2 * NT + k - 1) * kTD;
                 double4_t d0 = {0, 0, 0, 0}, d1 = {0, 0, 0, 0}, e0 = {0, 0, 0, 0}, e1 = {0, 0, 0, 0};
@@ -884,9 +893,11 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                     d0 = qload(rs, tD + (2 * h) * 256);
                     d1 = qload(rs, tD + (2 * h + 1) * 256);
                 }
-                if (useP0c && h == 1) {   // row half 0 of L(k+2, k-1), for quadrant (1, 0) of D'_{k+2}
-                    e0 = qload(rs, tD);
-                    e1 = qload(rs, tD + 256);
+                // quadrant (1, 0) of D'_{k+2} needs both row halves of L(k+2, k-1): the other half
+                // is loaded by the wave that forms the term (wave 2 with ORBHIP_DAG_Q10_W2, else 3)
+                if (useP0c && h == (ORBHIP_DAG_Q10_W2 ? 0 : 1)) {
+                    e0 = qload(rs, tD + (ORBHIP_DAG_Q10_W2 ? 2 : 0) * 256);
+                    e1 = qload(rs, tD + (ORBHIP_DAG_Q10_W2 ? 3 : 1) * 256);
                 }
                 double4_t u[2], t[2], dd[2];
 #pragma unroll
@@ -953,13 +964,23 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 DAG_STAMP(12 + 2 * h);
                 {   // D'_{k+2}: column k-1 (L(k+2, k-1)) and column k (L(k+2, k)) in independent chains
                     double4_t da = {0, 0, 0, 0}, db = {0, 0, 0, 0}, dc = {0, 0, 0, 0}, de = {0, 0, 0, 0};
+#if ORBHIP_DAG_Q10_W2
+                    if (useP0c && h == 0) {   // quadrant (1, 0) for wave 3: the same operands as its form
+                        mfma_sub(dc, d0, e0);
+                        mfma_sub(de, d1, e1);
+                        sq(Q10, dc + de);
+                        lds_signal(F6, k + 2);
+                    }
+#endif
                     if (useP0c) {
                         mfma_sub(da, d0, d0);
                         mfma_sub(db, d1, d1);
+#if !ORBHIP_DAG_Q10_W2
                         if (h == 1) {   // quadrant (1, 0): row half 1 against row half 0
                             mfma_sub(dc, e0, d0);
                             mfma_sub(de, e1, d1);
                         }
+#endif
                     }
                     double4_t dg = {0, 0, 0, 0}, dh = {0, 0, 0, 0};
                     if (inEnvU) {
@@ -971,7 +992,14 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                         dd[0] += dsum;
                     } else {
                         dd[1] += dsum;
+#if ORBHIP_DAG_Q10_W2
+                        if (useP0c) {
+                            lds_wait(F6, k + 2);
+                            dd[0] += lq(Q10);
+                        }
+#else
                         dd[0] += dc + de;
+#endif
                     }
                 }
                 if (h == 0) {
@@ -1427,7 +1455,7 @@ __global__ __launch_bounds__(256) void k_chol_dag_multi(const DagK* __restrict__
 }
 
 size_t dag_lds_bytes(int NT) {
-    const size_t need = sizeof(double) * (11280 + 32 + 64 + 2 * (size_t)NT * kT) + sizeof(int) * NT;
+    const size_t need = sizeof(double) * (11280 + 32 + 64 + 2 * (size_t)NT * kT + 256 + 1) + sizeof(int) * NT;
     return std::max(need, kMinLds);
 }
 
