@@ -66,9 +66,10 @@ constexpr int kNewton = ORBHIP_DAG_NEWTON;   // Newton steps after v_rsq_f64 / v
 #define ORBHIP_DAG_T_W1 1
 #endif
 #ifndef ORBHIP_DAG_Q10_W2
-// r05: wave 2 computes the column k-1 term of D'_{k+2}'s quadrant (1,0) for wave 3 (which had 6
-// of the 10 D' products), handing it over in LDS (Q10, flag F6)
-#define ORBHIP_DAG_Q10_W2 1
+// wave 2 computes the column k-1 term of D'_{k+2}'s quadrant (1,0) for wave 3 (which has 6 of the
+// 10 D' products), handing it over in LDS (Q10, flag F6). r05 A/B (two alternating runs): wave 3
+// ended ~0.2k cycles earlier and wave 2 ~0.5k later, the interval unchanged (12.6-12.8k): off
+#define ORBHIP_DAG_Q10_W2 0
 #endif
 #ifndef ORBHIP_DAG_BACK_COL
 #define ORBHIP_DAG_BACK_COL 0   // the chain-only backward on column-major tile loads (bwd_col_dot)

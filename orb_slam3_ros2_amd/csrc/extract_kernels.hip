@@ -2264,8 +2264,8 @@ __global__ __launch_bounds__(256) void k_desc_kp(const ExtractPlan* __restrict__
 // neighbours onto one XCD measured ~1% below it on the 16-camera C2 stream).
 // XCD-grouped work-group order (xcd_runs): whole frames per XCD for big batches, runs of 16 for
 // small ones, runs of 8 at one frame (r05: at one frame the grouped order measured the same
-// 16-camera throughput as round-robin, 38.9k / 38.8k frames/s on one box, and cut the PMC bytes per
-// launch of k_pyr_cone 2.89 -> 2.18 MB, k_fast_cells 4.16 -> 1.69 MB, k_desc_kp 5.24 -> 3.57 MB:
+// 16-camera throughput as round-robin (38.9k / 38.8k frames/s on one box) and cut the PMC bytes
+// per launch of k_pyr_cone by 0.7 MB, k_fast_cells 4.16 -> 1.69 MB, k_desc_kp 5.24 -> 3.57 MB:
 // neighbouring tiles' shared lines stay in one L2; r02 had measured it ~1% slower)
 static int xcd_run_for(int B) {
     static const int env = getenv("ORBHIP_XCD_RUN") ? atoi(getenv("ORBHIP_XCD_RUN")) : -2;
