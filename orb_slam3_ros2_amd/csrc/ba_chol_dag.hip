@@ -615,7 +615,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     int* F4 = word + 13;                // wave 2 / 3: their rows of T_{k+1} up to column k-1 in TpN
     int* F5 = word + 14;
     int* F6 = word + 15;                // wave 2: Q10 holds quadrant (1,0)'s column k-1 term
-    double* Q10 = (double*)(rfl + NT + (NT & 1));   // 256 doubles after the row_first ints
+    [[maybe_unused]] double* Q10 = (double*)(rfl + NT + (NT & 1));   // 256 doubles after the row_first ints
     unsigned long long* wts = (unsigned long long*)(lds + 11264 + 8);   // per-wave cycles (dbg)
     unsigned long long* stm = (unsigned long long*)(lds + 10560);       // sub-phase stamps (dbg), 16
 #define DAG_STAMP(i) do { if (dbg && lane == 0) stm[i] = __builtin_amdgcn_s_memtime() - tk; } while (0)
