@@ -1476,8 +1476,46 @@ struct DagDevState {
     bool has_last = false;          // `last` launched the device's most recent solve
     hipStream_t last = nullptr;
     hipEvent_t ev = nullptr;        // recorded at the tail of `last` when another stream launches
+    // contended (a hand-off in the last kContendWindow launches): every launch records `after`
+    // right behind itself, and the next launch from another stream waits on that instead of the
+    // other stream's tail (which may hold a whole chunk of its queued LM slots). An event between
+    // two slots costs ~5 us of queue drain (r04), so an uncontended solve records none.
+    hipEvent_t after = nullptr;
+    bool after_valid = false;       // `after` was recorded right behind `last`'s latest launch
+    long long contended_until = 0;
     long long launches = 0, handoffs = 0;
 };
+constexpr long long kContendWindow = 64;
+// the hand-off before a launch on st, and the bookkeeping after it (ds.m held)
+hipError_t dag_handoff_before(DagDevState& ds, hipStream_t st) {
+    if (!ds.has_last || ds.last == st) return hipSuccess;
+    static const bool tail_only = std::getenv("ORBHIP_DAG_HANDOFF_TAIL") != nullptr;   // A/B: r04's form
+    hipError_t e = hipSuccess;
+    if (ds.after_valid && !tail_only) {
+        e = hipStreamWaitEvent(st, ds.after, 0);
+    } else {
+        if (!ds.ev && (e = hipEventCreateWithFlags(&ds.ev, hipEventDisableTiming)) != hipSuccess) return e;
+        e = hipEventRecord(ds.ev, ds.last);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, ds.ev, 0);
+    }
+    if (e != hipSuccess) return e;
+    ds.handoffs++;
+    ds.contended_until = ds.launches + kContendWindow;
+    return hipSuccess;
+}
+hipError_t dag_handoff_after(DagDevState& ds, hipStream_t st) {
+    ds.has_last = true;
+    ds.last = st;
+    ds.launches++;
+    ds.after_valid = false;
+    if (ds.launches < ds.contended_until) {
+        hipError_t e = hipSuccess;
+        if (!ds.after && (e = hipEventCreateWithFlags(&ds.after, hipEventDisableTiming)) != hipSuccess) return e;
+        if ((e = hipEventRecord(ds.after, st)) != hipSuccess) return e;
+        ds.after_valid = true;
+    }
+    return hipSuccess;
+}
 constexpr int kMaxDagDevices = 64;
 DagDevState& dag_dev(int dev) {
     static DagDevState s[kMaxDagDevices];
@@ -1510,7 +1548,10 @@ void dag_stream_retired(hipStream_t st) {
     for (int d = 0; d < kMaxDagDevices; d++) {
         DagDevState& ds = dag_dev(d);
         std::lock_guard<std::mutex> g(ds.m);
-        if (ds.has_last && ds.last == st) ds.has_last = false;
+        if (ds.has_last && ds.last == st) {
+            ds.has_last = false;
+            ds.after_valid = false;
+        }
     }
 }
 
@@ -1609,25 +1650,14 @@ hipError_t chol_dag_solve(const double* S, int n, const int* row_first, const do
         }
         ds.attr = true;
     }
-    if (ds.has_last && ds.last != st) {   // device-wide order: after the other stream's solve
-        if (!ds.ev) {
-            const hipError_t e = hipEventCreateWithFlags(&ds.ev, hipEventDisableTiming);
-            if (e != hipSuccess) return e;
-        }
-        hipError_t e = hipEventRecord(ds.ev, ds.last);
-        if (e == hipSuccess) e = hipStreamWaitEvent(st, ds.ev, 0);
+    {   // device-wide order: after the other stream's last solve
+        const hipError_t e = dag_handoff_before(ds, st);
         if (e != hipSuccess) return e;
-        ds.handoffs++;
     }
     if (dbg) hipLaunchKernelGGL(k_chol_dag<true>, dim3((unsigned)(d.G + 1)), dim3(256), dag_lds_bytes(a.NT), st, a);
     else hipLaunchKernelGGL(k_chol_dag<false>, dim3((unsigned)(d.G + 1)), dim3(256), dag_lds_bytes(a.NT), st, a);
     const hipError_t e = hipGetLastError();
-    if (e == hipSuccess) {
-        ds.has_last = true;
-        ds.last = st;
-        ds.launches++;
-    }
-    return e;
+    return e == hipSuccess ? dag_handoff_after(ds, st) : e;
 }
 
 size_t dag_k_bytes() { return sizeof(DagK); }
@@ -1668,24 +1698,13 @@ hipError_t chol_dag_multi_launch(const void* d_ks, const int* d_wgoff, int np, i
         if (e != hipSuccess) return e;
         ds.attr_multi = true;
     }
-    if (ds.has_last && ds.last != st) {
-        if (!ds.ev) {
-            const hipError_t e = hipEventCreateWithFlags(&ds.ev, hipEventDisableTiming);
-            if (e != hipSuccess) return e;
-        }
-        hipError_t e = hipEventRecord(ds.ev, ds.last);
-        if (e == hipSuccess) e = hipStreamWaitEvent(st, ds.ev, 0);
+    {
+        const hipError_t e = dag_handoff_before(ds, st);
         if (e != hipSuccess) return e;
-        ds.handoffs++;
     }
     hipLaunchKernelGGL(k_chol_dag_multi, dim3((unsigned)grid), dim3(256), lds, st, (const DagK*)d_ks, d_wgoff, np);
     const hipError_t e = hipGetLastError();
-    if (e == hipSuccess) {
-        ds.has_last = true;
-        ds.last = st;
-        ds.launches++;
-    }
-    return e;
+    return e == hipSuccess ? dag_handoff_after(ds, st) : e;
 }
 
 int chol_dag_test(const double* A, const double* b, double* x, int n, int reps, int max_helpers, float* ms,
