@@ -1052,7 +1052,7 @@ def main():
                      "timing": "kernel execution span from device timestamps (k_pyr_cone: first workgroup "
                                "start -> last workgroup end, s_memrealtime; the other stages: "
                                "hipExtLaunchKernelGGL events) over a replay of the timed 16-camera stream; "
-                               "rocprofv3 --kernel-trace of this C2 section: profiles/r04_c2_kernel_stats.md",
+                               "rocprofv3 --kernel-trace of this C2 section: profiles/r05_c2_kernel_stats.md",
                      "octree_candidates_per_frame": r.get("octree_candidates_per_frame"),
                      "stage_avg_ms": {STAGES[k]: round(v, 5) for k, v in r["stage_ms"].items()},
                      "stage_avg_ms_one_frame_stream": {STAGES[k]: round(v, 5)
