@@ -442,22 +442,38 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
     TR_BEGIN()
     const int L = P->n_levels, tid = threadIdx.x, nt = blockDim.x;
     const ConeRect* R = rects + (size_t)tile * kMaxLevels;
+    // the tile's level rectangles (kMaxLevels x 16 bytes) as one dword per lane, read back by
+    // readlane (uniform level index): read as int16 fields they compiled to a chain of dependent
+    // global loads, one per level (~5k cycles before the staging loads were issued)
+    static_assert(sizeof(ConeRect) == 16 && kMaxLevels * 4 <= 64 && (kMaxLevels & (kMaxLevels - 1)) == 0, "4 dwords per level");
+    const uint32_t rdw = ((const uint32_t*)R)[threadIdx.x & (4 * kMaxLevels - 1)];
+    auto rect = [&](int l) -> ConeRect {   // l wave-uniform
+        const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)rdw, 4 * l),
+                       d1 = (uint32_t)__builtin_amdgcn_readlane((int)rdw, 4 * l + 1),
+                       d2 = (uint32_t)__builtin_amdgcn_readlane((int)rdw, 4 * l + 2),
+                       d3 = (uint32_t)__builtin_amdgcn_readlane((int)rdw, 4 * l + 3);
+        return ConeRect{(int16_t)(d0 & 0xFFFF), (int16_t)(d0 >> 16), (int16_t)(d1 & 0xFFFF), (int16_t)(d1 >> 16),
+                        (int16_t)(d2 & 0xFFFF), (int16_t)(d2 >> 16), (int16_t)(d3 & 0xFFFF), (int16_t)(d3 >> 16)};
+    };
     int boff[kMaxLevels], toff[kMaxLevels];
     int tot = 0;
     // the source level s0 (0: the frame; s0 >= 1: a pyramid level written by k_resize) is staged
     // as aligned dwords: rows of P0 = round_up(width + 3, 4) bytes, the region starting at byte
     // sh0 of its row (sh0: the address misalignment, 0 on the byte path)
-    const int P0 = (R[s0].nx1 - R[s0].nx0 + 6) & ~3;
+    const ConeRect Rs0 = rect(s0);
+    const int P0 = (Rs0.nx1 - Rs0.nx0 + 6) & ~3;
     for (int l = s0; l < L; l++) {
+        const ConeRect r = rect(l);
         boff[l] = tot;
-        tot += ((l == s0 ? P0 : (R[l].nx1 - R[l].nx0)) * (R[l].ny1 - R[l].ny0) + 15) & ~15;
+        tot += ((l == s0 ? P0 : (r.nx1 - r.nx0)) * (r.ny1 - r.ny0) + 15) & ~15;
     }
     int sh0 = 0;
     int* tab = (int*)(cone + tot);
     int ttot = 0;
     for (int l = s0 + 1; l < L; l++) {
         toff[l] = ttot;
-        ttot += 2 * (R[l].nx1 - R[l].nx0) + 3 * (R[l].ny1 - R[l].ny0);
+        const ConeRect r = rect(l);
+        ttot += 2 * (r.nx1 - r.nx0) + 3 * (r.ny1 - r.ny0);
     }
     // staged table entry i (LDS layout: per level l > s0, xofs[nw] | xalpha[nw] | (r0, r1, beta)[nh]):
     // from the compact per-level tables when the plan has them, else the host's per-tile copy
@@ -479,11 +495,12 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
         const int sy = ct.yofs[y] + comp, hs = P->lv[l - 1].h;
         return sy < 0 ? 0 : (sy < hs ? sy : hs - 1);
     };
+    TR_PHASE(0, 20)
     // ---- one round trip: the tile's tables of every level and its level-0 cone, all loads issued
     // before any store ----
     {
         const ImgRef in0 = level_img(P, fb, f, s0);
-        const ConeRect r = R[s0];
+        const ConeRect r = Rs0;
         const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0;
         const uint8_t* src0 = in0.p + (int64_t)r.ny0 * in0.pitch + r.nx0;
         const bool dw = ((in0.pitch & 3) == 0) && ((((uintptr_t)in0.p) & 3) == 0);
@@ -505,6 +522,7 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
             for (int u = 0; u < 2; u++)
                 if (tid + 1024 * u < ttot) tab[tid + 1024 * u] = tv[u];
             if (tid < tot0) ((uint32_t*)lv0)[y * (P0 >> 2) + x] = v;
+            TR_PHASE(0, 21)
         } else if (dw) {
             // 8 loads per thread in flight before their stores (a load-store loop waits out one
             // global round trip per step)
@@ -545,7 +563,7 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
     TR_PHASE(0, 0)
     for (int l = s0 + 1; l < L; l++) {
         const LevelGeom& D = P->lv[l];
-        const ConeRect r = R[l], rp = R[l - 1];
+        const ConeRect r = rect(l), rp = rect(l - 1);
         const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0, nwp = l == s0 + 1 ? P0 : rp.nx1 - rp.nx0;
         const int* t = tab + toff[l];
         const uint8_t* src = cone + boff[l - 1] + (l == s0 + 1 ? sh0 : 0);
@@ -619,6 +637,9 @@ __global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict
 // 1534) is an exact f16 integer, so every min / max / difference is exact.
 // ---------------------------------------------------------------------------
 constexpr int kWinMax = 80;
+#ifndef ORBHIP_OCT_W0_MAIN
+#define ORBHIP_OCT_W0_MAIN 1   // r05: the octree's MAIN rounds of short lists in wave 0 alone (0: the block loop)
+#endif
 #ifndef ORBHIP_FAST_LEAN
 #define ORBHIP_FAST_LEAN 1   // r05: branch-free pair-test round, mbcnt positions (A/B: 0 = r04's form)
 #endif
@@ -1279,6 +1300,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
     // ---- 1. candidate count per cell -> cell-major key order (wave 0 scans the cells) ----
     const int ncell = G.n_cells;
     const int* cc = cand_cnt + (int64_t)f * P->n_cells_total + G.cell_base;
+    TR_PHASE(2, 51)
     // the pyramid's deepest level starts at zero (16-byte stores while the count loads fly)
     auto zero_pyramid = [&]() {
         if (Dh) {
@@ -1307,6 +1329,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
         const uint32_t t0 = tid < ntab ? otl[tid] : 0u, t1 = tid + nt < ntab ? otl[tid + nt] : 0u;
         zero_pyramid();
         if (tid < ncell) S.cslot[tid] = so;
+        TR_PHASE(2, 52)
         int M0;
         const int ex = block_excl_scan(c, ctl, &M0);
         if (tid < ncell) S.cellstart[tid] = ex;
@@ -1527,7 +1550,86 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
         uint64_t *rectC = S.rectA, *rectO = S.rectB;
         uint32_t *cntC = S.cntA, *serC = S.serA;
         uint32_t *cntO = S.cntB, *serO = S.serB;
-        for (int iter = 0;; iter++) {
+#if ORBHIP_OCT_W0_MAIN
+        if constexpr (FAST) {
+            // MAIN rounds of lists of <= 64 nodes by wave 0 alone, one node per lane in registers and
+            // no block barrier between rounds: the same pass as the loop below (children of the
+            // dividing nodes pushed to the front, later parents first, n4..n1 inside a parent's
+            // block, the undivided nodes behind them in order; serials in division order). The
+            // loop below takes over at the first longer list or FINAL pass (ctl[61]: rounds run).
+            if (w0) {
+                uint64_t *rC = S.rectA, *rO = S.rectB;
+                uint32_t *cC = S.cntA, *sC = S.serA, *cO = S.cntB, *sO = S.serB;
+                int n = ctl[56], serial = ctl[57], rounds = 0;
+                bool deep = false, fin = false, fmode = false;
+                while (n <= 64 && rounds < 64) {
+                    const bool has = lane < n;
+                    const uint64_t cd = has ? rC[lane] : 0ull;
+                    const uint32_t cnt = has ? cC[lane] : 0u, ser = has ? sC[lane] : 0u;
+                    const bool dv = has && cnt > 1;
+                    const int d = (int)(cd >> 32);
+                    if (__ballot(dv && d >= Dh)) {   // a node too deep for the pyramid
+                        deep = true;
+                        break;
+                    }
+                    uint4 c4 = {0u, 0u, 0u, 0u};
+                    if (dv) c4 = *(const uint4*)&pcnt[poff(d + 1) + 4 * (int)(uint32_t)cd];
+                    const uint32_t cq[4] = {c4.x, c4.y, c4.z, c4.w};
+                    const int c = dv ? nonempty4(cq) : 0, e = dv ? multi4(cq) : 0, u = (has && !dv) ? 1 : 0;
+                    const int ic = wave_incl_scan(c), iu = wave_incl_scan(u), ie = wave_incl_scan(e);
+                    const int T = __builtin_amdgcn_readlane(ic, 63), U = __builtin_amdgcn_readlane(iu, 63);
+                    const int E = __builtin_amdgcn_readlane(ie, 63);
+                    const int cb = ic - c;
+                    if (dv) {
+                        const int base = T - cb - c;
+                        int r = 0;
+#pragma unroll
+                        for (int q = 0; q < 4; q++) {
+                            if (cq[q] == 0) continue;
+                            const int pos = base + (c - 1 - r);
+                            rO[pos] = kid(cd, q);
+                            cO[pos] = cq[q];
+                            sO[pos] = (uint32_t)(serial + cb + r);
+                            r++;
+                        }
+                    } else if (has) {
+                        const int pos = T + iu - u;
+                        rO[pos] = cd;
+                        cO[pos] = cnt;
+                        sO[pos] = ser;
+                    }
+                    wave_lds_fence();
+                    const int newSize = T + U;
+                    serial += T;
+                    rounds++;
+                    { uint64_t* t = rC; rC = rO; rO = t; }
+                    { uint32_t* t = cC; cC = cO; cO = t; }
+                    { uint32_t* t = sC; sC = sO; sO = t; }
+                    const int prev = n;
+                    n = newSize;
+                    if (newSize >= N || newSize == prev) { fin = true; break; }
+                    if (newSize + E * 3 > N) { fmode = true; break; }
+                }
+                if (lane == 0) {
+                    ctl[56] = n;
+                    ctl[57] = serial;
+                    ctl[58] = fmode ? 1 : 0;
+                    ctl[59] = fin ? 1 : 0;
+                    ctl[61] = rounds;
+                    ctl[62] = deep ? 1 : 0;
+                }
+            }
+            __syncthreads();
+            TR_PHASE(2, 40)
+            if (ctl[62]) return false;   // every thread, after the barrier: the level goes to the sweep path
+            if (ctl[61] & 1) {
+                { uint64_t* t = rectC; rectC = rectO; rectO = t; }
+                { uint32_t* t = cntC; cntC = cntO; cntO = t; }
+                { uint32_t* t = serC; serC = serO; serO = t; }
+            }
+        }
+#endif
+        for (int iter = 0; !ctl[59]; iter++) {
             // read before the round's barrier: wave 0 rewrites the control words in its node pass
             const int n = ctl[56];
             const int mode = ctl[58];
@@ -1539,15 +1641,55 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                 // ---- children counts of every node to divide, from the pyramid (wave 0) ----
                 if (w0) {
                     bool deep = false;
-                    for (int p = lane; p < n; p += 64) {
-                        if (cntC[p] > 1) {
-                            const uint64_t cd = rectC[p];
-                            const int d = (int)(cd >> 32);
-                            if (d >= Dh) {
-                                deep = true;
-                            } else {
-                                const uint4 c4 = *(const uint4*)&pcnt[poff(d + 1) + 4 * (int)(uint32_t)cd];
-                                *(uint4*)&S.ccount[4 * p] = c4;
+                    if (n <= 256) {
+                        // the list's four 64-node chunks with every load in flight together; a FINAL
+                        // pass also collects its (size, serial, node) keys here (in any order: the
+                        // block sort orders them)
+                        uint32_t cv[4], sv[4];
+                        uint64_t dv[4];
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const int p = lane + 64 * i;
+                            cv[i] = p < n ? cntC[p] : 0u;
+                            dv[i] = p < n ? rectC[p] : 0ull;
+                            sv[i] = (p < n && mode) ? serC[p] : 0u;
+                        }
+                        uint4 c4v[4];
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const int d = (int)(dv[i] >> 32);
+                            const bool dvd = cv[i] > 1;
+                            deep = deep || (dvd && d >= Dh);
+                            c4v[i] = (dvd && d < Dh) ? *(const uint4*)&pcnt[poff(d + 1) + 4 * (int)(uint32_t)dv[i]]
+                                                     : uint4{0u, 0u, 0u, 0u};
+                        }
+                        int kpos = 0;
+#pragma unroll
+                        for (int i = 0; i < 4; i++) {
+                            const int p = lane + 64 * i;
+                            const bool dvd = cv[i] > 1;
+                            if (dvd) *(uint4*)&S.ccount[4 * p] = c4v[i];
+                            if (mode) {
+                                const uint64_t m = __ballot(dvd);
+                                const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                                if (dvd) S.skey2[kpos + below] = ((uint64_t)cv[i] << 40) | ((uint64_t)sv[i] << 16) | (uint64_t)p;
+                                kpos += __popcll(m);
+                            }
+                        }
+                        if (mode && lane == 0) ctl[60] = kpos;
+                        TR_PHASE(2, 43)
+                    } else {
+                        for (int p = lane; p < n; p += 64) {
+                            if (cntC[p] > 1) {
+                                const uint64_t cd = rectC[p];
+                                const int d = (int)(cd >> 32);
+                                if (d >= Dh) {
+                                    deep = true;
+                                } else {
+                                    const uint4 c4 = *(const uint4*)&pcnt[poff(d + 1) + 4 * (int)(uint32_t)cd];
+                                    *(uint4*)&S.ccount[4 * p] = c4;
+                                }
                             }
                         }
                     }
@@ -1656,7 +1798,8 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
             } else {
                 // ---- FINAL phase: divide largest (size, serial) first until >= N ----
                 TR_PHASE(2, 48)
-                if (w0) {
+                const bool short_list = FAST && n <= 256;   // keys collected by the fill above; the register node pass
+                if (w0 && !short_list) {
                     const int per = (n + 63) >> 6;
                     const int b = min(lane * per, n), e = min(b + per, n);
                     int s = 0;
@@ -1674,7 +1817,108 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                 const int K = ctl[60];
                 block_rank_sort_desc(S.skey2, S.skey, K);   // keys unique: (size, serial) order; ends in a barrier
                 TR_PHASE(2, 47)
-                if (w0 && !stop) {
+                if (w0 && !stop && short_list) {
+                    // the pass below with every operand loaded once into registers (K <= n <= 256:
+                    // at most four sorted entries and four list nodes per lane), jstar from one
+                    // ballot (run is non-decreasing in j: every divided node has a child)
+                    const int serial0 = ctl[57];
+                    const int per = (K + 63) >> 6;
+                    const int b = min(lane * per, K), e = min(b + per, K);
+                    int pj[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) pj[u] = b + u < e ? (int)(S.skey[b + u] & 0xFFFF) : 0;
+                    uint4 c4j[4];
+                    uint64_t rj[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        c4j[u] = b + u < e ? *(const uint4*)&S.ccount[4 * pj[u]] : uint4{0u, 0u, 0u, 0u};
+                        rj[u] = b + u < e ? rectC[pj[u]] : 0ull;
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; i++)
+                        if (lane + 64 * i < n) S.tD[lane + 64 * i] = 1;
+                    int cj[4], g = 0;
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const uint32_t q4[4] = {c4j[u].x, c4j[u].y, c4j[u].z, c4j[u].w};
+                        cj[u] = b + u < e ? nonempty4(q4) : 0;
+                        g += b + u < e ? cj[u] - 1 : 0;
+                    }
+                    const int ig = wave_incl_scan(g);
+                    int run = n + ig - g, cand = -1;
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        if (b + u < e && cand < 0) {
+                            run += cj[u] - 1;
+                            if (run >= N) cand = b + u;
+                        }
+                    }
+                    const uint64_t cmask = __ballot(cand >= 0);
+                    const int jstar = cmask ? __builtin_amdgcn_readlane(cand, __ffsll((unsigned long long)cmask) - 1) : K - 1;
+                    int sc = 0;
+#pragma unroll
+                    for (int u = 0; u < 4; u++) sc += (b + u < e && b + u <= jstar) ? cj[u] : 0;
+                    const int ic = wave_incl_scan(sc);
+                    const int Ctot = __builtin_amdgcn_readlane(ic, 63);
+                    int cb = ic - sc;
+                    wave_lds_fence();   // the tD = 1 stores before the divided nodes' zeros
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        if (b + u < e && b + u <= jstar) {
+                            const uint32_t q4[4] = {c4j[u].x, c4j[u].y, c4j[u].z, c4j[u].w};
+                            const int c = cj[u], base = Ctot - cb - c;
+                            int r = 0;
+#pragma unroll
+                            for (int q = 0; q < 4; q++) {
+                                if (q4[q] == 0) continue;
+                                const int ps = base + (c - 1 - r);
+                                rectO[ps] = kid(rj[u], q);
+                                cntO[ps] = q4[q];
+                                serO[ps] = serial0 + cb + r;
+                                r++;
+                            }
+                            S.tD[pj[u]] = 0;
+                            cb += c;
+                        }
+                    }
+                    wave_lds_fence();
+                    // the other nodes keep their order behind the children
+                    const int pn = (n + 63) >> 6;
+                    const int bn = min(lane * pn, n), en = min(bn + pn, n);
+                    int tdv[4];
+                    uint64_t rv[4];
+                    uint32_t cv[4], sv[4];
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        const int p = bn + u;
+                        const bool in = p < en;
+                        tdv[u] = in ? S.tD[p] : 0;
+                        rv[u] = in ? rectC[p] : 0ull;
+                        cv[u] = in ? cntC[p] : 0u;
+                        sv[u] = in ? serC[p] : 0u;
+                    }
+                    const int st = tdv[0] + tdv[1] + tdv[2] + tdv[3];
+                    const int is = wave_incl_scan(st);
+                    int sb = is - st;
+#pragma unroll
+                    for (int u = 0; u < 4; u++) {
+                        if (tdv[u]) {
+                            const int ps = Ctot + sb;
+                            rectO[ps] = rv[u];
+                            cntO[ps] = cv[u];
+                            serO[ps] = sv[u];
+                            sb++;
+                        }
+                    }
+                    const int newSize = Ctot + (n - (jstar + 1));
+                    wave_lds_fence();
+                    if (lane == 0) {
+                        ctl[57] = serial0 + Ctot;
+                        ctl[56] = newSize;
+                        if (newSize >= N || newSize == n) ctl[59] = 1;
+                    }
+                    TR_PHASE(2, 42)
+                } else if (w0 && !stop) {
                     const int serial0 = ctl[57];
                     const int per = (K + 63) >> 6;
                     const int b = min(lane * per, K), e = min(b + per, K);
@@ -2367,7 +2611,14 @@ void launch_octree(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom*
                    unsigned long long* stamp) {
     const size_t lds = octree_lds_bytes(hP, cfg);
     dim3 grd(B, hP.n_levels, 1);
-    ORBHIP_LAUNCH(k_octree, grd, dim3(1024), lds, st, dP, cells, otab, cand, cprim, cand_cnt, cand_off, kscratch,
+    // threads per level: 512 (r05, C2 alternating runs: level-0 work-group 13.3 us at 512 against
+    // 14.0 at 1024 and 13.5 at 256, with the slowest at 15.6; ORBHIP_OCT_NT = 256 / 1024 for A/B)
+    static const int nt = [] {
+        const char* e = std::getenv("ORBHIP_OCT_NT");
+        const int v = e ? std::atoi(e) : 512;
+        return (v == 256 || v == 1024) ? v : 512;
+    }();
+    ORBHIP_LAUNCH(k_octree, grd, dim3(nt), lds, st, dP, cells, otab, cand, cprim, cand_cnt, cand_off, kscratch,
                   nscratch, lvl_kp, lvl_cnt, lvl_nlap, cfg, err, stamp);
 }
 

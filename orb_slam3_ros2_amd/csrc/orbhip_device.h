@@ -175,8 +175,8 @@ __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int* total) 
 // ---------------------------------------------------------------------------
 
 #define ORBHIP_TRACE_UNIT(unit)                                                             \
-    static __device__ unsigned long long* g_trace = nullptr;                               \
-    static __device__ int g_trace_blk = 0;                                                 \
+    static __constant__ unsigned long long* g_trace = nullptr;                             \
+    static __constant__ int g_trace_blk = 0;                                               \
     void trace_set_##unit(unsigned long long* p) {                                         \
         (void)hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &p, sizeof(p));                       \
         const char* e = std::getenv("ORBHIP_TRACE_BLOCK");                                 \
