@@ -640,6 +640,12 @@ constexpr int kWinMax = 80;
 #ifndef ORBHIP_OCT_W0_MAIN
 #define ORBHIP_OCT_W0_MAIN 1   // r05: the octree's MAIN rounds of short lists in wave 0 alone (0: the block loop)
 #endif
+#ifndef ORBHIP_OCT_W0_FINAL
+// r05: the FINAL pass of short lists with its operands loaded once into registers. A/B on C2
+// (tools/gpu_r05_octab.sh, three alternating runs): octree stage 14.4 us with it against 13.8 us
+// with the r04 wave-0 loops, so off
+#define ORBHIP_OCT_W0_FINAL 0
+#endif
 #ifndef ORBHIP_FAST_LEAN
 #define ORBHIP_FAST_LEAN 1   // r05: branch-free pair-test round, mbcnt positions (A/B: 0 = r04's form)
 #endif
@@ -1563,17 +1569,22 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                 int n = ctl[56], serial = ctl[57], rounds = 0;
                 bool deep = false, fin = false, fmode = false;
                 while (n <= 64 && rounds < 64) {
+                    // loads from clamped addresses, no branch around them (a branch per load made
+                    // the compiler wait out each one's round trip in turn)
                     const bool has = lane < n;
-                    const uint64_t cd = has ? rC[lane] : 0ull;
-                    const uint32_t cnt = has ? cC[lane] : 0u, ser = has ? sC[lane] : 0u;
+                    const int pl = has ? lane : 0;
+                    const uint64_t cd0 = rC[pl];
+                    const uint32_t cnt0 = cC[pl], ser0 = sC[pl];
+                    const uint64_t cd = has ? cd0 : 0ull;
+                    const uint32_t cnt = has ? cnt0 : 0u, ser = has ? ser0 : 0u;
                     const bool dv = has && cnt > 1;
                     const int d = (int)(cd >> 32);
                     if (__ballot(dv && d >= Dh)) {   // a node too deep for the pyramid
                         deep = true;
                         break;
                     }
-                    uint4 c4 = {0u, 0u, 0u, 0u};
-                    if (dv) c4 = *(const uint4*)&pcnt[poff(d + 1) + 4 * (int)(uint32_t)cd];
+                    const uint4 c4l = *(const uint4*)&pcnt[dv ? poff(d + 1) + 4 * (int)(uint32_t)cd : 0];
+                    const uint4 c4 = dv ? c4l : uint4{0u, 0u, 0u, 0u};
                     const uint32_t cq[4] = {c4.x, c4.y, c4.z, c4.w};
                     const int c = dv ? nonempty4(cq) : 0, e = dv ? multi4(cq) : 0, u = (has && !dv) ? 1 : 0;
                     const int ic = wave_incl_scan(c), iu = wave_incl_scan(u), ie = wave_incl_scan(e);
@@ -1641,27 +1652,29 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                 // ---- children counts of every node to divide, from the pyramid (wave 0) ----
                 if (w0) {
                     bool deep = false;
-                    if (n <= 256) {
+                    if (ORBHIP_OCT_W0_FINAL && n <= 256) {
                         // the list's four 64-node chunks with every load in flight together; a FINAL
                         // pass also collects its (size, serial, node) keys here (in any order: the
                         // block sort orders them)
                         uint32_t cv[4], sv[4];
                         uint64_t dv[4];
 #pragma unroll
-                        for (int i = 0; i < 4; i++) {
-                            const int p = lane + 64 * i;
-                            cv[i] = p < n ? cntC[p] : 0u;
-                            dv[i] = p < n ? rectC[p] : 0ull;
-                            sv[i] = (p < n && mode) ? serC[p] : 0u;
+                        for (int i = 0; i < 4; i++) {   // clamped addresses, no branch around the loads
+                            const int p = lane + 64 * i, pc = p < n ? p : 0;
+                            const uint32_t c = cntC[pc], sr = serC[pc];
+                            const uint64_t r = rectC[pc];
+                            cv[i] = p < n ? c : 0u;
+                            dv[i] = p < n ? r : 0ull;
+                            sv[i] = p < n ? sr : 0u;
                         }
                         uint4 c4v[4];
 #pragma unroll
                         for (int i = 0; i < 4; i++) {
                             const int d = (int)(dv[i] >> 32);
-                            const bool dvd = cv[i] > 1;
+                            const bool dvd = cv[i] > 1, ok = dvd && d < Dh;
                             deep = deep || (dvd && d >= Dh);
-                            c4v[i] = (dvd && d < Dh) ? *(const uint4*)&pcnt[poff(d + 1) + 4 * (int)(uint32_t)dv[i]]
-                                                     : uint4{0u, 0u, 0u, 0u};
+                            const uint4 c4 = *(const uint4*)&pcnt[ok ? poff(d + 1) + 4 * (int)(uint32_t)dv[i] : 0];
+                            c4v[i] = ok ? c4 : uint4{0u, 0u, 0u, 0u};
                         }
                         int kpos = 0;
 #pragma unroll
@@ -1798,7 +1811,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
             } else {
                 // ---- FINAL phase: divide largest (size, serial) first until >= N ----
                 TR_PHASE(2, 48)
-                const bool short_list = FAST && n <= 256;   // keys collected by the fill above; the register node pass
+                const bool short_list = FAST && ORBHIP_OCT_W0_FINAL && n <= 256;   // keys collected by the fill above; the register node pass
                 if (w0 && !short_list) {
                     const int per = (n + 63) >> 6;
                     const int b = min(lane * per, n), e = min(b + per, n);
@@ -1817,22 +1830,24 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                 const int K = ctl[60];
                 block_rank_sort_desc(S.skey2, S.skey, K);   // keys unique: (size, serial) order; ends in a barrier
                 TR_PHASE(2, 47)
-                if (w0 && !stop && short_list) {
+                if (w0 && !stop && short_list && K > 0) {
                     // the pass below with every operand loaded once into registers (K <= n <= 256:
                     // at most four sorted entries and four list nodes per lane), jstar from one
                     // ballot (run is non-decreasing in j: every divided node has a child)
                     const int serial0 = ctl[57];
                     const int per = (K + 63) >> 6;
                     const int b = min(lane * per, K), e = min(b + per, K);
+                    // clamped addresses, no branch around the loads (K >= 1 here: FINAL had nodes to divide)
                     int pj[4];
 #pragma unroll
-                    for (int u = 0; u < 4; u++) pj[u] = b + u < e ? (int)(S.skey[b + u] & 0xFFFF) : 0;
+                    for (int u = 0; u < 4; u++) pj[u] = (int)(S.skey[min(b + u, K - 1)] & 0xFFFF);
                     uint4 c4j[4];
                     uint64_t rj[4];
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
-                        c4j[u] = b + u < e ? *(const uint4*)&S.ccount[4 * pj[u]] : uint4{0u, 0u, 0u, 0u};
-                        rj[u] = b + u < e ? rectC[pj[u]] : 0ull;
+                        const uint4 c4 = *(const uint4*)&S.ccount[4 * pj[u]];
+                        c4j[u] = b + u < e ? c4 : uint4{0u, 0u, 0u, 0u};
+                        rj[u] = rectC[pj[u]];
                     }
 #pragma unroll
                     for (int i = 0; i < 4; i++)
@@ -1890,12 +1905,13 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                     uint32_t cv[4], sv[4];
 #pragma unroll
                     for (int u = 0; u < 4; u++) {
-                        const int p = bn + u;
+                        const int p = bn + u, pc = min(p, n - 1);
                         const bool in = p < en;
-                        tdv[u] = in ? S.tD[p] : 0;
-                        rv[u] = in ? rectC[p] : 0ull;
-                        cv[u] = in ? cntC[p] : 0u;
-                        sv[u] = in ? serC[p] : 0u;
+                        const int t = S.tD[pc];
+                        rv[u] = rectC[pc];
+                        cv[u] = cntC[pc];
+                        sv[u] = serC[pc];
+                        tdv[u] = in ? t : 0;
                     }
                     const int st = tdv[0] + tdv[1] + tdv[2] + tdv[3];
                     const int is = wave_incl_scan(st);
