@@ -24,7 +24,8 @@
 
 namespace orbhip {
 
-static __constant__ signed char kPattern[256 * 4] = ORBHIP_BIT_PATTERN_31_INIT;
+// external, hidden: a static __constant__ table is addressed through the GOT (a dependent load)
+__constant__ __attribute__((visibility("hidden"))) signed char kPattern[256 * 4] = ORBHIP_BIT_PATTERN_31_INIT;
 
 ORBHIP_TRACE_UNIT(extract)
 

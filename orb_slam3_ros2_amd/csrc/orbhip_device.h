@@ -174,22 +174,27 @@ __device__ __forceinline__ int block_excl_scan(int v, int* scratch, int* total) 
 // workgroup 0 (last launch).
 // ---------------------------------------------------------------------------
 
-#define ORBHIP_TRACE_UNIT(unit)                                                             \
-    static __constant__ unsigned long long* g_trace = nullptr;                             \
-    static __constant__ int g_trace_blk = 0;                                               \
-    void trace_set_##unit(unsigned long long* p) {                                         \
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_trace), &p, sizeof(p));                       \
-        const char* e = std::getenv("ORBHIP_TRACE_BLOCK");                                 \
-        const int b = e ? std::atoi(e) : 0;                                                \
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_trace_blk), &b, sizeof(b));                   \
+// The unit's trace words are external symbols of hidden visibility: an internal-linkage
+// (static) __constant__ variable is addressed through the GOT, i.e. two dependent scalar loads at
+// every kernel start (with cold caches, ~1 us) before the branch on tr_buf could resolve.
+#define ORBHIP_TRACE_UNIT(unit)                                                                 \
+    __constant__ __attribute__((visibility("hidden"))) unsigned long long* g_trace_##unit = nullptr; \
+    __constant__ __attribute__((visibility("hidden"))) int g_trace_blk_##unit = 0;          \
+    static __device__ __forceinline__ unsigned long long* tr_ptr() { return g_trace_##unit; } \
+    static __device__ __forceinline__ int tr_blk_val() { return g_trace_blk_##unit; }       \
+    void trace_set_##unit(unsigned long long* p) {                                          \
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_trace_##unit), &p, sizeof(p));                 \
+        const char* e = std::getenv("ORBHIP_TRACE_BLOCK");                                  \
+        const int b = e ? std::atoi(e) : 0;                                                 \
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_trace_blk_##unit), &b, sizeof(b));             \
     }
 
+// (stamping every wave unconditionally, so that nothing waited on the trace word, cost 5% of the
+// 16-camera C2 stream: the clock reads are not free when every wave of every launch takes them)
 #define TR_BEGIN()                                                                          \
     unsigned long long tr_t0 = 0, tr_tp = 0;                                                \
-    unsigned long long* const tr_buf = g_trace;                                             \
-    /* the traced block is read once here: read inside TR_PHASE, the compiler hoisted the */ \
-    /* load above the branch and every phase then waited on vmcnt(0), stores included */     \
-    const int tr_blk = __builtin_amdgcn_readfirstlane(tr_buf ? g_trace_blk : -1);          \
+    unsigned long long* const tr_buf = tr_ptr();                                            \
+    const int tr_blk = tr_blk_val();                                                        \
     (void)tr_tp; (void)tr_blk;                                                              \
     if (tr_buf && threadIdx.x == 0) {                                                       \
         tr_t0 = __builtin_amdgcn_s_memrealtime();                                           \
