@@ -2336,7 +2336,8 @@ __global__ __launch_bounds__(256) void k_desc_kp(const ExtractPlan* __restrict__
                                                  const LevelKp* __restrict__ lvl_kp, const int* __restrict__ lvl_cnt,
                                                  const int* __restrict__ lvl_nlap, const int* __restrict__ disc,
                                                  orbhip_kp* __restrict__ out_kps, uint8_t* __restrict__ out_desc,
-                                                 int cap, int* __restrict__ n_out, int* __restrict__ mono_out, int xrun) {
+                                                 int cap, int* __restrict__ n_out, int* __restrict__ mono_out, int xrun,
+                                                 int nlev) {
     // the k_desc layouts: patch rows of kDpP bytes offset by sh, row-pass sums transposed, the
     // blurred region over the dead patch
     __shared__ __attribute__((aligned(16))) uint8_t pt[kPatchW * kDpP + 16];
@@ -2347,30 +2348,63 @@ __global__ __launch_bounds__(256) void k_desc_kp(const ExtractPlan* __restrict__
     const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
     const int f = lg / X;
     const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
-    // the IC_Angle disc offsets (n_disc <= 31 x 31 < 4 x 256), loaded first so that they arrive
-    // with the keypoint and the patch; entries past n_disc are (0, 0) and add nothing
+    // Every load that needs only the kernel arguments goes out first, together (one round trip
+    // after the arguments instead of a chain of five): the keypoint record (slot lg % X of the
+    // frame's kp_slots_total = X slots), the IC_Angle disc offsets (zero-padded to 4 x 256 entries
+    // on the host: a (0, 0) entry adds nothing), the level capacities and the frame's counts
+    // (L = nlev, a launch argument, so their addresses wait for nothing)
     constexpr int kDiscU = 4;
+    const int slot0 = lg % X;
+    const LevelKp kp = lvl_kp[(int64_t)f * X + slot0];
     int dv[kDiscU];
 #pragma unroll
-    for (int u = 0; u < kDiscU; u++) dv[u] = tid + 256 * u < P->n_disc ? disc[tid + 256 * u] : 0;
-    int slot = lg % X;
-    const int L = P->n_levels;
-    int total = 0, nlap_tot = 0;
-    for (int l = 0; l < L; l++) { total += lvl_cnt[f * L + l]; nlap_tot += lvl_nlap[f * L + l]; }
-    if (slot == 0 && tid == 0) {
+    for (int u = 0; u < kDiscU; u++) dv[u] = disc[tid + 256 * u];
+    const int L = nlev;
+    int slot = slot0, total = 0, nlap_tot = 0, l = 0, mono_base = 0, lap_base = 0, cnt_l = 0;
+    constexpr int kDescL = 8;   // levels walked from registers (more: the loop below)
+    if (L <= kDescL) {
+        int capv[kDescL], cntv[kDescL], nlv[kDescL];
+#pragma unroll
+        for (int q = 0; q < kDescL; q++) {
+            const int lc = min(q, L - 1);
+            capv[q] = P->lv[lc].kp_cap;
+            cntv[q] = lvl_cnt[f * L + lc];
+            nlv[q] = lvl_nlap[f * L + lc];
+        }
+        bool go = true;
+#pragma unroll
+        for (int q = 0; q < kDescL; q++) {
+            if (q < L) {
+                total += cntv[q];
+                nlap_tot += nlv[q];
+                if (go && slot >= capv[q]) {
+                    slot -= capv[q];
+                    mono_base += cntv[q] - nlv[q];
+                    lap_base += nlv[q];
+                    l = q + 1;
+                } else {
+                    go = false;
+                }
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kDescL; q++) cnt_l = q == l ? cntv[q] : cnt_l;
+    } else {
+        for (int q = 0; q < L; q++) { total += lvl_cnt[f * L + q]; nlap_tot += lvl_nlap[f * L + q]; }
+        while (l < L && slot >= P->lv[l].kp_cap) {
+            slot -= P->lv[l].kp_cap;
+            mono_base += lvl_cnt[f * L + l] - lvl_nlap[f * L + l];
+            lap_base += lvl_nlap[f * L + l];
+            l++;
+        }
+        cnt_l = l < L ? lvl_cnt[f * L + l] : 0;
+    }
+    if (slot0 == 0 && tid == 0) {
         n_out[f] = total;
         mono_out[f] = total - nlap_tot;
     }
-    int l = 0, mono_base = 0, lap_base = 0;
-    while (l < L && slot >= P->lv[l].kp_cap) {
-        slot -= P->lv[l].kp_cap;
-        mono_base += lvl_cnt[f * L + l] - lvl_nlap[f * L + l];
-        lap_base += lvl_nlap[f * L + l];
-        l++;
-    }
-    if (!(l < L && slot < lvl_cnt[f * L + l])) return;   // block-uniform
+    if (!(l < L && slot < cnt_l)) return;   // block-uniform
     const LevelGeom& G = P->lv[l];
-    const LevelKp kp = lvl_kp[(int64_t)f * P->kp_slots_total + G.kp_base + slot];
     const int cx = kp.x, cy = kp.y;
     int sh = 0;
     {
@@ -2650,7 +2684,7 @@ void launch_desc(const ExtractPlan* dP, const ExtractPlan& hP, const FrameBufs& 
     const bool per_wg = mode >= 0 ? mode == 1 : B * hP.kp_slots_total <= kDescKpMaxSlots;
     if (per_wg) {
         ORBHIP_LAUNCH(k_desc_kp, dim3(hP.kp_slots_total, B, 1), dim3(256), 0, st, dP, fb, lvl_kp, lvl_cnt,
-                           lvl_nlap, disc, out_kps, out_desc, cap, n_out, mono_out, xcd_run_for(B));
+                           lvl_nlap, disc, out_kps, out_desc, cap, n_out, mono_out, xcd_run_for(B), hP.n_levels);
         return;
     }
     dim3 grd((hP.kp_slots_total + 3) / 4, B, 1);

@@ -633,6 +633,8 @@ static int build_plan_new(orbhip_ctx* c, int w, int h, std::shared_ptr<Plan>& ou
         for (int u = -d; u <= d; u++) pl->disc.push_back((int)(uint16_t)(int16_t)u | ((int)(int16_t)v << 16));
     }
     P.n_disc = (int)pl->disc.size();   // <= 31 x 31 (k_desc_kp holds 4 entries per thread)
+    if (P.n_disc > 1024) return ORBHIP_ERR_UNSUPPORTED;
+    pl->disc.resize(1024, 0);   // zero-padded: k_desc_kp loads 4 x 256 entries without a bound (a (0, 0) entry adds nothing)
     // octree LDS configuration
     int max_kp_cap = 0;
     for (int l = 0; l < L; l++) max_kp_cap = std::max(max_kp_cap, P.lv[l].kp_cap);
