@@ -133,14 +133,15 @@ __device__ void ctl_begin_body(const BaArgs& a, int nlin, int* done_flags, int p
 // ---------------------------------------------------------------------------
 // one edge: error, chi2, robust rho (EdgeSE3ProjectXYZ::computeError + RobustKernelHuber::robustify);
 // returns rho0
-__device__ __forceinline__ double edge_error_at(const BaArgs& a, int e, const double* T, const double* X) {
-    double cx, cy, cz;
-    qrot(load_q(T), X[0], X[1], X[2], cx, cy, cz);
-    cx += T[4]; cy += T[5]; cz += T[6];
+// the error terms of edge e from its camera-frame point
+__device__ __forceinline__ void edge_terms(const BaArgs& a, int e, double cx, double cy, double cz, double& e0,
+                                           double& e1, double& chi2, double& r0, double& r1) {
     const double u = a.fx * cx / cz + a.cx, v = a.fy * cy / cz + a.cy;
-    const double e0 = a.e_obs[2 * e] - u, e1 = a.e_obs[2 * e + 1] - v;
-    const double chi2 = a.e_info[e] * (e0 * e0 + e1 * e1);
-    double r0 = chi2, r1 = 1.0;
+    e0 = a.e_obs[2 * e] - u;
+    e1 = a.e_obs[2 * e + 1] - v;
+    chi2 = a.e_info[e] * (e0 * e0 + e1 * e1);
+    r0 = chi2;
+    r1 = 1.0;
     if (a.delta > 0) {
         const double dsqr = a.delta * a.delta;
         if (chi2 > dsqr) {
@@ -149,14 +150,25 @@ __device__ __forceinline__ double edge_error_at(const BaArgs& a, int e, const do
             r1 = a.delta / sq;
         }
     }
-    // agent-scope (sc1, write-through) stores: a small problem's last workgroup may rewrite these
-    // words in the same launch (ctl_end_body's refresh), and a plain store's dirty line in another
-    // XCD's L2 could otherwise be written back over that rewrite at kernel end
-    st_agent(a.e_err + 2 * e, e0);
-    st_agent(a.e_err + 2 * e + 1, e1);
-    st_agent(a.e_chi2 + e, chi2);
-    st_agent(a.e_rho0 + e, r0);
-    st_agent(a.e_rho1 + e, r1);
+}
+__device__ __forceinline__ void store_terms(const BaArgs& a, int e, double e0, double e1, double chi2, double r0,
+                                            double r1) {
+    a.e_err[2 * e] = e0;
+    a.e_err[2 * e + 1] = e1;
+    a.e_chi2[e] = chi2;
+    a.e_rho0[e] = r0;
+    a.e_rho1[e] = r1;
+}
+// Plain stores: no launch rewrites these words after another workgroup of the same launch wrote
+// them (a rejected small problem's refresh is done by the next build, k_ba_lin, not by the
+// trial's last workgroup; r05: the agent-scope stores cost ~4 us per C4 trial)
+__device__ __forceinline__ double edge_error_at(const BaArgs& a, int e, const double* T, const double* X) {
+    double cx, cy, cz;
+    qrot(load_q(T), X[0], X[1], X[2], cx, cy, cz);
+    cx += T[4]; cy += T[5]; cz += T[6];
+    double e0, e1, chi2, r0, r1;
+    edge_terms(a, e, cx, cy, cz, e0, e1, chi2, r0, r1);
+    store_terms(a, e, e0, e1, chi2, r0, r1);
     return r0;
 }
 __device__ __forceinline__ double edge_error(const BaArgs& a, int e) {
@@ -279,7 +291,9 @@ __device__ __forceinline__ double lin_ab(const BaArgs& a, int e, int oi, double 
 // ---------------------------------------------------------------------------
 // one thread per landmark: Hll, b_l over all its edges; stores each edge's linearisation (Pc, w)
 // returns the largest |diagonal| of Hll (0 for m >= M)
-__device__ __forceinline__ double lin_point(const BaArgs& a, int m) {
+// fresh: the stored errors belong to a rejected trial (a small problem whose iteration ended on
+// one): each edge's terms are taken from the restored state here, and stored, instead of read
+__device__ __forceinline__ double lin_point(const BaArgs& a, int m, bool fresh = false) {
     if (m >= a.M) return 0.0;
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};
     for (int k = a.pt_ptr[m]; k < a.pt_ptr[m + 1]; k++) {
@@ -288,9 +302,19 @@ __device__ __forceinline__ double lin_point(const BaArgs& a, int m) {
         edge_pc(a, e, x, y, z, R);
         proj_jac(a.fx, a.fy, x, y, z, j);
         jac_ab(j, x, y, z, R, A, B);
-        const double r1 = a.e_rho1[e], info = a.e_info[e];
+        double r1, er0, er1;
+        if (fresh) {   // uniform
+            double chi2, r0;
+            edge_terms(a, e, x, y, z, er0, er1, chi2, r0, r1);
+            store_terms(a, e, er0, er1, chi2, r0, r1);
+        } else {
+            r1 = a.e_rho1[e];
+            er0 = a.e_err[2 * e];
+            er1 = a.e_err[2 * e + 1];
+        }
+        const double info = a.e_info[e];
         const double w = r1 * info;
-        const double om0 = -info * a.e_err[2 * e] * r1, om1 = -info * a.e_err[2 * e + 1] * r1;
+        const double om0 = -info * er0 * r1, om1 = -info * er1 * r1;
 #pragma unroll
         for (int r = 0; r < 3; r++) {
             bl[r] += A[r] * om0 + A[3 + r] * om1;
@@ -327,7 +351,7 @@ __device__ __forceinline__ void reduce_half(double* acc, int lane, int m) {
 }
 
 // one wave per pose i; returns (in every lane) the largest |diagonal| of the pose's Hpp block
-__device__ __forceinline__ double lin_pose(const BaArgs& a, int i, int lane) {
+__device__ __forceinline__ double lin_pose(const BaArgs& a, int i, int lane, bool fresh = false) {
     if (i >= a.np) return 0.0;   // wave-uniform
     double acc[32];   // 27 sums (21 of the upper Hpp triangle, 6 of b_p), padded to 32
 #pragma unroll
@@ -338,9 +362,18 @@ __device__ __forceinline__ double lin_pose(const BaArgs& a, int i, int lane) {
         edge_pc(a, e, x, y, z, R);
         proj_jac(a.fx, a.fy, x, y, z, j);
         jac_ab(j, x, y, z, R, A, B);
-        const double r1 = a.e_rho1[e], info = a.e_info[e];
+        double r1, er0, er1;
+        if (fresh) {   // uniform; the landmark side stores the same values
+            double chi2, r0;
+            edge_terms(a, e, x, y, z, er0, er1, chi2, r0, r1);
+        } else {
+            r1 = a.e_rho1[e];
+            er0 = a.e_err[2 * e];
+            er1 = a.e_err[2 * e + 1];
+        }
+        const double info = a.e_info[e];
         const double w = r1 * info;
-        const double om0 = -info * a.e_err[2 * e] * r1, om1 = -info * a.e_err[2 * e + 1] * r1;
+        const double om0 = -info * er0 * r1, om1 = -info * er1 * r1;
         int t = 0;
 #pragma unroll
         for (int r = 0; r < 6; r++)
@@ -406,14 +439,17 @@ __global__ __launch_bounds__(256) void k_ba_lin(const BaArgs* __restrict__ args,
     __shared__ double sh[4];
     __shared__ int lastf;
     const int mP = (a.M + 255) / 256, nP = (a.np + 3) / 4;
+    // a small problem whose iteration ended on a rejected trial: its stored errors are the trial's,
+    // so this build takes them from the restored state (the larger problems' k_ba_errors(1) did)
+    const bool fresh = a.small && a.ctl && !a.ctl->errors_valid;
     double d;
     int slot;
     if (bx_ < nbp) {
-        d = lin_point(a, bx_ * blockDim.x + threadIdx.x);
+        d = lin_point(a, bx_ * blockDim.x + threadIdx.x, fresh);
         slot = bx_ < mP ? bx_ : -1;
     } else {
         const int q = bx_ - nbp;
-        d = lin_pose(a, q * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
+        d = lin_pose(a, q * 4 + (threadIdx.x >> 6), threadIdx.x & 63, fresh);
         slot = q < nP ? mP + q : -1;
     }
 #pragma unroll
@@ -911,11 +947,16 @@ __device__ __forceinline__ double backsub_point(const BaArgs& a, int m) {
     for (int r = 0; r < 3; r++) {
         const double xl = Di[3 * r] * c[0] + Di[3 * r + 1] * c[1] + Di[3 * r + 2] * c[2];
         a.x[a.n + 3 * m + r] = xl;
-        // sc1: the problem's last workgroup of a fused trial reads pts_bak and may restore pts in
-        // the same launch (ctl_end_body)
         const double xo = X[r];
-        st_agent(a.pts_bak + 3 * m + r, xo);
-        st_agent(X + r, xo + xl);
+        // sc1 for a small problem: its trial's last workgroup may restore pts from pts_bak in
+        // the same launch (ctl_end_body); the others' k_ba_pop runs in a launch of its own
+        if (a.small) {
+            st_agent(a.pts_bak + 3 * m + r, xo);
+            st_agent(X + r, xo + xl);
+        } else {
+            a.pts_bak[3 * m + r] = xo;
+            X[r] = xo + xl;
+        }
         sc += xl * (lambda * xl + bl[r]);
     }
     return sc;
@@ -1142,6 +1183,7 @@ __device__ void ctl_begin_apply(const BaArgs& a, double maxdiag) {
     }
     c.qmax = 0;
     c.rho = 0;
+    c.errors_valid = 1;   // the build just done used the current state's errors
     c.phase = kPhTrial;
 }
 __device__ void ctl_begin_body(const BaArgs& a, int nlin, int* done_flags, int prob) {
@@ -1215,9 +1257,9 @@ __device__ void ctl_end_body(const BaArgs& a, int prob, int* done_flags, double*
     ctl_end_sums(a, sh);
     if (threadIdx.x == 0) ctl_end_decide(a, prob, done_flags);
     if (!a.small) return;
-    // a small problem: this workgroup restores a rejected trial's state (k_ba_pop) and, when the
-    // iteration ended on it, recomputes the errors of the restored state (k_ba_errors(1): g2o's
-    // computeActiveErrors at the next iteration's start), so neither needs a launch of its own.
+    // a small problem: this workgroup restores a rejected trial's state (k_ba_pop), so that needs
+    // no launch of its own (the restored state's errors, g2o's computeActiveErrors at the next
+    // iteration's start, come from the next k_ba_lin).
     // Fused trials (k_ba_backsub_errs) left the poses unmoved and the new ones in pose_bak: an
     // accepted trial commits them, a rejected one only takes the points back
     __syncthreads();
@@ -1235,18 +1277,9 @@ __device__ void ctl_end_body(const BaArgs& a, int prob, int* done_flags, double*
         for (int i = threadIdx.x; i < 8 * a.P; i += blockDim.x) st_agent(a.pose + i, ld_agent(a.pose_bak + i));
     }
     for (int i = threadIdx.x; i < 3 * a.M; i += blockDim.x) st_agent(a.pts + i, ld_agent(a.pts_bak + i));
-    if (c.phase != kPhBuild || c.errors_valid) return;
-    __syncthreads();
-    for (int e = threadIdx.x; e < a.E; e += blockDim.x) {   // the restored state, read back sc1
-        const double* tp = a.pose + 8 * a.e_pose[e];
-        const double* xp = a.pts + 3 * a.e_pt[e];
-        double T[8], X[3];
-#pragma unroll
-        for (int k = 0; k < 8; k++) T[k] = ld_agent(tp + k);
-#pragma unroll
-        for (int k = 0; k < 3; k++) X[k] = ld_agent(xp + k);
-        (void)edge_error_at(a, e, T, X);
-    }
+    // the restored state's errors, when the iteration ended here, are taken by the next build
+    // (k_ba_lin's fresh terms): rewritten here, in this launch, they raced the other workgroups'
+    // plain stores of the trial's errors
 }
 
 // ---- sharded device-driven rounds (BaArgs::sync): the controller's reductions, a collective
