@@ -756,8 +756,13 @@ static int run_extract(orbhip_ctx* c, Plan* pl, const uint8_t* d_imgs, int B, in
         // the one-launch pyramid stamps its own execution span for the stage timer
         fb.stamp = (cone_path && tm.stage == 1 && tm.dstamp && tm.n < StageTimer::kCap) ? tm.dstamp + tm.n : nullptr;
         if (cone_path) {
+            static const int cone_nt = [] {   // threads per tile (A/B: ORBHIP_CONE_NT = 256 / 512)
+                const char* e = std::getenv("ORBHIP_CONE_NT");
+                const int v = e ? std::atoi(e) : 1024;
+                return (v == 256 || v == 512) ? v : 1024;
+            }();
             launch_pyr_cone(pl->d_plan.p, pl->cone_tiles, pl->cone_lds, fb, B, pl->d_cone.p, pl->d_cone_tab.p,
-                            pl->cone_tab_stride, st, 0, 1024, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p,
+                            pl->cone_tab_stride, st, 0, cone_nt, pl->d_xofs.p, pl->d_xalpha.p, pl->d_yofs.p,
                             pl->d_ybeta.p);
         } else if (flow_on) {
             PyrFlow fa{};
