@@ -641,6 +641,13 @@ constexpr int kWinMax = 80;
 #ifndef ORBHIP_OCT_W0_MAIN
 #define ORBHIP_OCT_W0_MAIN 1   // r05: the octree's MAIN rounds of short lists in wave 0 alone (0: the block loop)
 #endif
+#ifndef ORBHIP_OCT_BLK_FINAL
+// r05: FINAL passes of lists of <= threads nodes by the whole block (block scans) instead of wave 0.
+// A/B (profiles/r05_octree_blkfinal_ab.log, three alternating runs): octree stage 13.84-14.08 against
+// 14.01-14.16 us, the stream 43.3-44.2k against 42.8-44.2k frames/s: the block's barriers cost about
+// what wave 0's serial LDS round trips did
+#define ORBHIP_OCT_BLK_FINAL 1
+#endif
 #ifndef ORBHIP_OCT_W0_FINAL
 // r05: the FINAL pass of short lists with its operands loaded once into registers. A/B on C2
 // (tools/gpu_r05_octab.sh, three alternating runs): octree stage 14.4 us with it against 13.8 us
@@ -1649,9 +1656,28 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                 if (tid == 0) atomicOr(err, 1);
                 break;
             }
+            // a FINAL pass of a list the block covers with one node per thread: its fill, key
+            // collection and node pass by the whole block (block scans) instead of wave 0 alone
+            const bool blk_final = FAST && ORBHIP_OCT_BLK_FINAL && mode == 1 && n <= nt;   // block-uniform
             if constexpr (FAST) {
+                if (blk_final) {
+                    // node tid's children counts, and its (size, serial, node) key if it divides
+                    const int p = tid, pc = p < n ? p : 0;
+                    const uint32_t cn = cntC[pc], sr = serC[pc];
+                    const uint64_t cd = rectC[pc];
+                    const bool dvd = p < n && cn > 1;
+                    const int d = (int)(cd >> 32);
+                    const bool okd = dvd && d < Dh;
+                    const uint4 c4 = *(const uint4*)&pcnt[okd ? poff(d + 1) + 4 * (int)(uint32_t)cd : 0];
+                    if (dvd && d >= Dh) ctl[62] = 1;   // every writer stores 1; read after the scan's barriers
+                    if (okd) *(uint4*)&S.ccount[4 * p] = c4;
+                    int K;
+                    const int pos = block_excl_scan(dvd ? 1 : 0, ctl, &K);
+                    if (dvd) S.skey2[pos] = ((uint64_t)cn << 40) | ((uint64_t)sr << 16) | (uint64_t)p;
+                    if (tid == 0) ctl[60] = K;
+                }
                 // ---- children counts of every node to divide, from the pyramid (wave 0) ----
-                if (w0) {
+                if (w0 && !blk_final) {
                     bool deep = false;
                     if (ORBHIP_OCT_W0_FINAL && n <= 256) {
                         // the list's four 64-node chunks with every load in flight together; a FINAL
@@ -1813,7 +1839,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                 // ---- FINAL phase: divide largest (size, serial) first until >= N ----
                 TR_PHASE(2, 48)
                 const bool short_list = FAST && ORBHIP_OCT_W0_FINAL && n <= 256;   // keys collected by the fill above; the register node pass
-                if (w0 && !short_list) {
+                if (w0 && !short_list && !blk_final) {
                     const int per = (n + 63) >> 6;
                     const int b = min(lane * per, n), e = min(b + per, n);
                     int s = 0;
@@ -1831,7 +1857,68 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                 const int K = ctl[60];
                 block_rank_sort_desc(S.skey2, S.skey, K);   // keys unique: (size, serial) order; ends in a barrier
                 TR_PHASE(2, 47)
-                if (w0 && !stop && short_list && K > 0) {
+                if (blk_final) {
+                    if (!ctl[62]) {   // block-uniform (after the sort's barrier)
+                        // thread j: sorted entry j. run_j = n + sum_{i <= j} (c_i - 1) is
+                        // non-decreasing (a divided node has a child), so jstar, the first division
+                        // after which the list holds >= N nodes, is the count of divisions that
+                        // leave it short (or K - 1 when none reaches N)
+                        const int serial0 = ctl[57];
+                        const int j = tid, jc = j < K ? j : 0;
+                        const int pj = (int)(S.skey[jc] & 0xFFFF);
+                        const uint4 c4 = *(const uint4*)&S.ccount[4 * pj];
+                        const uint64_t rj = rectC[pj];
+                        const uint32_t q4[4] = {c4.x, c4.y, c4.z, c4.w};
+                        const int c = j < K ? nonempty4(q4) : 0;
+                        // (counted with an LDS atomic on a control word: __syncthreads_count
+                        // would add static LDS to a kernel whose dynamic LDS fills the CU)
+                        if (tid == 0) ctl[53] = 0;
+                        int gt;
+                        const int gex = block_excl_scan(j < K ? c - 1 : 0, ctl, &gt);   // barriers
+                        if (j < K && n + gex + c - 1 < N) atomicAdd(&ctl[53], 1);
+                        __syncthreads();
+                        const int nb = ctl[53];
+                        const int jstar = min(nb, K - 1);
+                        const bool dvj = j < K && j <= jstar;
+                        int Ctot;
+                        const int cb = block_excl_scan(dvj ? c : 0, ctl, &Ctot);
+                        if (tid < n) S.tD[tid] = 1;
+                        __syncthreads();
+                        if (dvj) {   // children pushed to the front in division order, n4..n1 inside
+                            const int base = Ctot - cb - c;
+                            int r = 0;
+#pragma unroll
+                            for (int q = 0; q < 4; q++) {
+                                if (q4[q] == 0) continue;
+                                const int ps = base + (c - 1 - r);
+                                rectO[ps] = kid(rj, q);
+                                cntO[ps] = q4[q];
+                                serO[ps] = serial0 + cb + r;
+                                r++;
+                            }
+                            S.tD[pj] = 0;
+                        }
+                        __syncthreads();
+                        // the other nodes keep their order behind the children
+                        const int p = tid, pc = p < n ? p : 0;
+                        const int keep = p < n ? S.tD[pc] : 0;
+                        const uint64_t rv = rectC[pc];
+                        const uint32_t cv = cntC[pc], sv = serC[pc];
+                        int nk;
+                        const int ex = block_excl_scan(keep, ctl, &nk);
+                        if (keep) {
+                            rectO[Ctot + ex] = rv;
+                            cntO[Ctot + ex] = cv;
+                            serO[Ctot + ex] = sv;
+                        }
+                        const int newSize = Ctot + (n - (jstar + 1));
+                        if (tid == 0) {
+                            ctl[57] = serial0 + Ctot;
+                            ctl[56] = newSize;
+                            if (newSize >= N || newSize == n) ctl[59] = 1;
+                        }
+                    }
+                } else if (w0 && !stop && short_list && K > 0) {
                     // the pass below with every operand loaded once into registers (K <= n <= 256:
                     // at most four sorted entries and four list nodes per lane), jstar from one
                     // ballot (run is non-decreasing in j: every divided node has a child)

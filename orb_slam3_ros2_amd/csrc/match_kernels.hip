@@ -403,7 +403,12 @@ __global__ __launch_bounds__(1024) void k_match_fused(MatchView v, int th_low, f
             if (ok) atomicAdd(&cnt, 1);
         }
     }
-    __syncthreads();
+    // LDS only (hist, cnt): __syncthreads() would also drain every thread's global stores here,
+    // one write-through round trip before the histogram atomics go out; wait_vm_all() below
+    // orders them all before the done counter
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     TR_PHASE(5, 3)
     if (tid < 30 && hist[tid]) atomicAdd(&ps[1 + tid], hist[tid]);
     if (tid == 0 && cnt) atomicAdd(&ps[31], cnt);
