@@ -426,15 +426,33 @@ __device__ __forceinline__ void lds_only_barrier() {
     asm volatile("" ::: "memory");
 }
 
-// the compact resize tables (one per level, shared by every tile; r05, optional) — the same entries
-// the host packs per tile in ctab, read from the plan's per-level tables instead, so a launch's
-// tiles share a ~40 KB working set instead of ~3.5 KB of copies per tile
+// r05: the tile's resize tables computed in the kernel (dev = 1, ORBHIP_CONE_TABDEV=1: the host's
+// expressions step for step, bit-exact) instead of read from the host-built per-tile copies in ctab
+// (dev = 0, the default: ~3.5 KB per tile, most of the cone's fetched bytes, but faster)
 struct ConeTabs {
-    const int* xofs;
-    const int* xalpha;
-    const int* yofs;
-    const int* ybeta;
+    int dev;
 };
+__device__ __forceinline__ int cone_floor_f(float v) {   // the host's floor_f
+    const int i = (int)v;
+    return i - (i > v ? 1 : 0);
+}
+__device__ __forceinline__ int cone_sat_s16(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
+// resize coefficient of destination coordinate d of a level (dl) from its source level (sl), as the
+// plan builder computes it (orbhip_api.cpp: cv::resize INTER_LINEAR's fixed-point taps): the
+// source index and the packed (1 - f, f) taps
+__device__ __forceinline__ void cone_coef(int d, int dl, int sl, int& s_idx, int& taps, bool clamp_x) {
+    const double scale = 1. / ((double)dl / sl);
+    float f = (float)((d + 0.5) * scale - 0.5);
+    int si = cone_floor_f(f);
+    f -= si;
+    if (clamp_x) {
+        if (si < 0) { f = 0; si = 0; }
+        if (si + 1 >= sl && si >= sl - 1) { f = 0; si = sl - 1; }
+    }
+    const int t0 = cone_sat_s16((int)rintf((1.f - f) * 2048)), t1 = cone_sat_s16((int)rintf(f * 2048));
+    s_idx = si;
+    taps = (int)(uint16_t)t0 | ((int)(uint16_t)t1 << 16);
+}
 
 __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P, const FrameBufs& fb,
                                               const ConeRect* __restrict__ rects, const int* __restrict__ ctab,
@@ -477,25 +495,32 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
         ttot += 2 * (r.nx1 - r.nx0) + 3 * (r.ny1 - r.ny0);
     }
     // staged table entry i (LDS layout: per level l > s0, xofs[nw] | xalpha[nw] | (r0, r1, beta)[nh]):
-    // from the compact per-level tables when the plan has them, else the host's per-tile copy
+    // the host's per-tile copy, or (ct.dev) computed here: a wave's lanes take consecutive entries,
+    // so each level's branch runs only in the one or two waves whose entries it holds
     const int* gt = ctab + (size_t)tile * tab_stride;
-    auto tab_at = [&](int i) -> int {
-        if (!ct.xofs) return gt[i];
-        int l = s0 + 1;
-#pragma unroll
-        for (int q = 2; q < kMaxLevels; q++)
-            if (q > s0 + 1 && q < L && i >= toff[q]) l = q;
-        const ConeRect r = R[l];
-        const LevelGeom& D = P->lv[l];
-        const int nw = r.nx1 - r.nx0, j = i - toff[l];
-        if (j < nw) return ct.xofs[D.xtab_off + r.nx0 + j];
-        if (j < 2 * nw) return ct.xalpha[D.xtab_off + r.nx0 + j - nw];
-        const int jj = j - 2 * nw, row = (jj * 21846) >> 16, comp = jj - 3 * row;   // jj / 3 (jj < 2^15)
-        const int y = D.ytab_off + r.ny0 + row;
-        if (comp == 2) return ct.ybeta[y];
-        const int sy = ct.yofs[y] + comp, hs = P->lv[l - 1].h;
-        return sy < 0 ? 0 : (sy < hs ? sy : hs - 1);
+    auto tab_dev = [&](int i) -> int {
+        int v = 0;
+        for (int q = s0 + 1; q < L; q++) {   // uniform
+            const ConeRect r = rect(q);
+            const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0, j = i - toff[q];
+            if (j >= 0 && j < 2 * nw + 3 * nh) {
+                const LevelGeom& D = P->lv[q];
+                const LevelGeom& Sg = P->lv[q - 1];
+                int si, taps;
+                if (j < 2 * nw) {
+                    cone_coef(r.nx0 + (j < nw ? j : j - nw), D.w, Sg.w, si, taps, true);
+                    v = j < nw ? si : taps;
+                } else {
+                    const int jj = j - 2 * nw, row = (jj * 21846) >> 16, comp = jj - 3 * row;   // jj / 3 (jj < 2^15)
+                    cone_coef(r.ny0 + row, D.h, Sg.h, si, taps, false);
+                    const int sy = si + comp, hs = Sg.h;
+                    v = comp == 2 ? taps : (sy < 0 ? 0 : (sy < hs ? sy : hs - 1));
+                }
+            }
+        }
+        return v;
     };
+    auto tab_at = [&](int i) -> int { return ct.dev ? tab_dev(i) : gt[i]; };
     TR_PHASE(0, 20)
     // ---- one round trip: the tile's tables of every level and its level-0 cone, all loads issued
     // before any store ----
@@ -514,11 +539,17 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
             const uint32_t* s4 = (const uint32_t*)(src0 - sh0);
             const int p4 = in0.pitch >> 2;
             int tv[2];
+            if (!ct.dev) {
 #pragma unroll
-            for (int u = 0; u < 2; u++) tv[u] = tab_at(min(tid + 1024 * u, ttot - 1));
+                for (int u = 0; u < 2; u++) tv[u] = gt[min(tid + 1024 * u, ttot - 1)];
+            }
             const int i = min(tid, tot0 - 1);
             const int y = small_div(i, inv_n), x = i - y * nwd;
             const uint32_t v = s4[(int64_t)y * p4 + x];
+            if (ct.dev) {   // computed while the level-0 load is in flight
+#pragma unroll
+                for (int u = 0; u < 2; u++) tv[u] = tid + 1024 * u < ttot ? tab_dev(tid + 1024 * u) : 0;
+            }
 #pragma unroll
             for (int u = 0; u < 2; u++)
                 if (tid + 1024 * u < ttot) tab[tid + 1024 * u] = tv[u];
@@ -2681,11 +2712,15 @@ void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameB
                      const int* xalpha, const int* yofs, const int* ybeta) {
     static LdsAttrOnce attr;   // per device, thread-safe (dev_attr.h)
     (void)attr.ensure((const void*)k_pyr_cone, 64 * 1024);
-    // the host's per-tile table copies by default; ORBHIP_CONE_TABS=level reads the compact per-level
-    // tables instead (r05 A/B: 130 KB fewer fetched bytes per 640x480 launch, but every staged entry
-    // then waits on its level's ConeRect before its table load: 20.8 -> 26.9 us per launch)
-    static const bool per_tile = !(getenv("ORBHIP_CONE_TABS") && getenv("ORBHIP_CONE_TABS")[0] == 'l');
-    const ConeTabs ct = per_tile ? ConeTabs{nullptr, nullptr, nullptr, nullptr} : ConeTabs{xofs, xalpha, yofs, ybeta};
+    (void)xofs; (void)xalpha; (void)yofs; (void)ybeta;
+    // the host's per-tile table copies by default; ORBHIP_CONE_TABDEV=1 computes the tables in the
+    // kernel (bit-exact; r05 A/B, three alternating runs: the cone's HBM bytes 2.44 -> 1.98 MB per
+    // 640x480 launch, but the launch 21 -> 35 us in the 16-camera stream, 43.6k -> 37.0k frames/s:
+    // the per-level double-precision coefficients cost more than the table round trip). (r05 also
+    // measured the plan's compact per-level tables: 130 KB fewer fetched bytes, but every staged
+    // entry waited on its level's ConeRect before its table load: 20.8 -> 26.9 us; removed.)
+    static const bool dev = getenv("ORBHIP_CONE_TABDEV") && getenv("ORBHIP_CONE_TABDEV")[0] == '1';
+    const ConeTabs ct{dev ? 1 : 0};
     ORBHIP_LAUNCH(k_pyr_cone, dim3(ntiles, B), dim3(nthreads), lds, st, dP, fb, rects, ctab, tab_stride,
                   xcd_run_for(B), s0, ct);
 }
