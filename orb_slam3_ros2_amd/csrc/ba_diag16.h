@@ -24,6 +24,11 @@
 
 #include "ba_chol.h"
 #include "ba_dpp16.h"
+#include "ba_dpp16f.h"
+
+#ifndef ORBHIP_DPP16_FUSED
+#define ORBHIP_DPP16_FUSED 1
+#endif
 
 namespace orbhip {
 
@@ -173,11 +178,36 @@ __device__ __forceinline__ void dpp16_step(double (&v)[16], double& pown, int c)
 // NaN) pivot. The raw columns go through scr (272 doubles of LDS, this wave's) into the C layout,
 // where each lane scales its four rows: selecting register g + 4q per lane in registers made the
 // compiler index the column array, i.e. put it in scratch memory.
+// Fused form (r05, ORBHIP_DPP16_FUSED, one Newton step only): one asm block per step from
+// tools/gen_dpp16.py (ba_dpp16f.h) issues the next pivot's reciprocal, Newton step and multiplier
+// between the current step's row updates instead of after all of them, and broadcasts the pivot
+// inside v_rcp_f64_dpp / v_fmac_f64_dpp; lane p's zero multiplier and own pivot come from bit p
+// of a one-hot column mask. Critical path per step: row update -> rcp -> e -> multiplier.
+template <int J>
+__device__ __forceinline__ void dpp16f_steps(double (&v)[16], double t, double& pown, unsigned oh, unsigned nh) {
+    if constexpr (J < 15) {
+        double tn;
+        Dpp16F<J>::step(v, t, tn, pown, oh, nh);
+        dpp16f_steps<J + 1>(v, tn, pown, oh, nh);
+    }
+}
 template <int NR = 1>
 __device__ __forceinline__ bool diag16_dpp(double (&v)[16], double* __restrict__ scr, double4_t& lv) {
     const int lane = threadIdx.x & 63, c = lane & 15, g = lane >> 4;
+#if ORBHIP_DPP16_FUSED
+    double pown;
+    if constexpr (NR == 1) {
+        pown = 0.0;
+        const unsigned oh = 1u << c;
+        dpp16f_steps<-1>(v, 0.0, pown, oh, ~oh);
+    } else {
+        pown = 1.0;
+        dpp16_step<0, NR>(v, pown, c);
+    }
+#else
     double pown = 1.0;
     dpp16_step<0, NR>(v, pown, c);
+#endif
     const bool bad = __any(!(pown > 0.0));
     const double rown = rcp_nr<NR>(pown), sown = rsq_nr<NR>(pown);
     if (g == 0) {
