@@ -4,7 +4,9 @@ kernel's counters are not mixed across regimes:
 
   c2    the bench's C2 stream: 16 cameras (640x480, extract + match to the camera's previous
         frame), 40 steps of one frame per camera, as in the bench's timed region
-  c3    the bench's C3 batch (1280x720, B=64, extract + 63 pair matches), 4 batches
+  c3    the bench's C3 batch (1280x720, B=64, extract + 63 pair matches), 96 batches
+        (PMC_C3_STEPS): k_fast_cells averages 368 us over the first 16 batches after start, 348
+        over 96, against the bench's warm 345 (profiles/r05_pmc_c3_kernel_stats.md)
   c4    the C4-sized dense reduced camera system (n = 294) solved by k_chol_dag, 2 x 21 solves
   c4lba C4 LocalBundleAdjustment (50 KF / 2000 pts / 8000 obs, 10 LM iterations), 3 solves
   c5    the C5-sized dense reduced camera system (n = 2394) solved by k_chol_dag, 2 x 21 solves
@@ -27,7 +29,7 @@ if mode == "c2":
         s.step()
 elif mode == "c3":
     c3 = bench.BatchC3(0, 1)
-    for _ in range(4):
+    for _ in range(int(os.environ.get("PMC_C3_STEPS", "96"))):
         c3.step()
 elif mode == "c4":
     for _ in range(2):
