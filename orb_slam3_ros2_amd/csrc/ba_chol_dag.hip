@@ -72,6 +72,9 @@ constexpr int kNewton = ORBHIP_DAG_NEWTON;   // Newton steps after v_rsq_f64 / v
 #define ORBHIP_DAG_Q10_W2 0
 #endif
 #ifndef ORBHIP_DAG_BACK_COL
+#ifndef ORBHIP_DAG_W23_EARLY
+#define ORBHIP_DAG_W23_EARLY 0   // r05: waves 2/3 U, T and D column k-1 MFMA chains in one block (dense case): measured slower
+#endif
 #define ORBHIP_DAG_BACK_COL 0   // the chain-only backward on column-major tile loads (bwd_col_dot)
 #endif
 
@@ -929,7 +932,44 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 const double4_t liq[3] = {lq(Lin), lq(Lin + 512), lq(Lin + 768)};
                 const double4_t l2q[4] = {lq(L2), lq(L2 + 256), lq(L2 + 512), lq(L2 + 768)};
                 double4_t o0 = {0, 0, 0, 0}, o1 = {0, 0, 0, 0};
-                if (inEnvU) {
+                // D' column k-1 terms (da, db; dc, de: quadrant (1, 0), wave 3)
+                double4_t da = {0, 0, 0, 0}, db = {0, 0, 0, 0}, dc = {0, 0, 0, 0}, de = {0, 0, 0, 0};
+#if ORBHIP_DAG_W23_EARLY
+                // every term present (the dense case): U's, T's and D''s column k-1 products in one
+                // basic block, so the scheduler interleaves their independent MFMA chains (T and
+                // D' do not depend on L(k+2, k)); the same MFMAs in the same order per accumulator
+                const bool early = inEnvU && useU && inEnvT && useTp && useP0c;
+#else
+                const bool early = false;
+#endif
+                if (early) {
+                    double4_t ub0 = {0, 0, 0, 0}, ub1 = {0, 0, 0, 0}, tb0 = {0, 0, 0, 0}, tb1 = {0, 0, 0, 0};
+                    mfma_sub(u[0], l1q[0], d0);
+                    mfma_sub(ub0, l1q[1], d1);
+                    mfma_sub(u[1], l1q[2], d0);
+                    mfma_sub(ub1, l1q[3], d1);
+                    mfma_sub(t[0], l2q[0], d0);
+                    mfma_sub(tb0, l2q[1], d1);
+                    mfma_sub(t[1], l2q[2], d0);
+                    mfma_sub(tb1, l2q[3], d1);
+                    mfma_sub(da, d0, d0);
+                    mfma_sub(db, d1, d1);
+                    u[0] += ub0;
+                    u[1] += ub1;
+                    t[0] += tb0;
+                    t[1] += tb1;
+                    double4_t o1b = {0, 0, 0, 0};
+                    panel_add(o0, liq[0], u[0]);
+                    panel_add(o1, liq[1], u[0]);
+                    panel_add(o1b, liq[2], u[1]);
+                    o1 += o1b;
+#if !ORBHIP_DAG_Q10_W2
+                    if (h == 1) {   // quadrant (1, 0): row half 1 against row half 0
+                        mfma_sub(dc, e0, d0);
+                        mfma_sub(de, e1, d1);
+                    }
+#endif
+                } else if (inEnvU) {
                     if (useU) {
 #pragma unroll
                         for (int c = 0; c < 2; c++) {
@@ -948,7 +988,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 sq(L2n + (2 * h) * 256, o0);
                 sq(L2n + (2 * h + 1) * 256, o1);
                 DAG_STAMP(5 + 4 * h);
-                if (inEnvT && useTp) {
+                if (!early && inEnvT && useTp) {
 #pragma unroll
                     for (int c = 0; c < 2; c++) {
                         double4_t tb = {0, 0, 0, 0};
@@ -964,7 +1004,6 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
 #endif
                 DAG_STAMP(12 + 2 * h);
                 {   // D'_{k+2}: column k-1 (L(k+2, k-1)) and column k (L(k+2, k)) in independent chains
-                    double4_t da = {0, 0, 0, 0}, db = {0, 0, 0, 0}, dc = {0, 0, 0, 0}, de = {0, 0, 0, 0};
 #if ORBHIP_DAG_Q10_W2
                     if (useP0c && h == 0) {   // quadrant (1, 0) for wave 3: the same operands as its form
                         mfma_sub(dc, d0, e0);
@@ -973,7 +1012,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                         lds_signal(F6, k + 2);
                     }
 #endif
-                    if (useP0c) {
+                    if (!early && useP0c) {
                         mfma_sub(da, d0, d0);
                         mfma_sub(db, d1, d1);
 #if !ORBHIP_DAG_Q10_W2
