@@ -64,6 +64,8 @@ def parse():
                     help="frames in flight per camera (pipelined batch-1 frames; 1 = frame by frame)")
     ap.add_argument("--extra-timeout", type=float, default=240.0,
                     help="seconds for the extras (C3/C4/C5/8f) before the watchdog prints the headline")
+    ap.add_argument("--detail", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="file for the full record (counters, stage tables); '' for none")
     return ap.parse_args()
 
 
@@ -326,6 +328,14 @@ def stage_bytes(ext, w, h, n_kp, frames, n_cand=None):
     return {k: v * frames for k, v in per.items()}
 
 
+def survey_frame_bytes(ext, w, h, n_kp):
+    """SURVEY.md §8(d) algorithmic bytes of one frame: the input level read once, every cascaded
+    level written once and read once, N keypoint records + descriptors (24 + 32 B) written."""
+    info = ext.level_info(w, h)
+    A = (info["w"].astype(np.int64) * info["h"]).tolist()
+    return float(A[0] + 2 * sum(A[1:]) + 56 * n_kp)
+
+
 def load_traffic(kernel_name, regime="c2"):
     """HBM bytes per launch of `kernel_name` from the committed PMC summary of the regime
     (profiles/traffic_<regime>.json: separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of
@@ -527,10 +537,11 @@ def c5_gba(ws, rank, iters):
         sopt = Optimizer()
         sopt.comm_init(ws, rank, uid[0])
         if nd_segments(*pose_blocks(prob), ws) is not None:
-            shard = shard_problem_nd(prob, rank, ws)[0]
+            shard, pts_sel, _ = shard_problem_nd(prob, rank, ws)
             mode = f"rccl segments x{ws} (interiors per rank, separator system all-reduced)"
         else:
-            shard = shard_problem(prob, rank, ws)[0]
+            shard, lo, hi, _ = shard_problem(prob, rank, ws)
+            pts_sel = np.arange(lo, hi)
             mode = f"rccl landmark shards x{ws} (reduced camera system all-reduced, replicated solve)"
         r, t = run(lambda: sopt.solve_sharded(shard))
         rr, tr = run(lambda: opt.solve(prob))
@@ -538,6 +549,11 @@ def c5_gba(ws, rank, iters):
         out["c5_gba_replica_mode"] = f"replicas x{ws} (one GPU per solve, nested dissection)"
         out["c5_gba_scaling_note"] = ("the sharded N-rank time is the driver's first measurement of it: no multi-GPU "
                                       "run was available to this build (DESIGN.md, C5 sharding)")
+        # the first multi-rank run checks itself: this rank's sharded result against the one-GPU
+        # solve of the whole problem (the same LM on the same data: chi2, poses and the rank's
+        # points within the north_star's 1e-4, the LM schedule identical), every rank's verdict
+        # AND-ed over the ranks
+        out.update(c5_sharded_parity(ws, r, rr, pts_sel))
     else:
         mode = f"replicas x{ws} (one GPU per solve, nested dissection)" if ws > 1 else \
             "one GPU (nested dissection, device-driven LM)"
@@ -545,6 +561,24 @@ def c5_gba(ws, rank, iters):
     out.update({"c5_gba_ms": round(1e3 * t, 2), "c5_gba_iterations": r.iterations_done, "c5_gba_trials": r.lm_trials,
                 "c5_gba_chi2": [round(r.initial_chi2, 1), round(r.final_chi2, 1)], "c5_gba_mode": mode})
     return out
+
+
+def c5_sharded_parity(ws, r, rr, pts_sel, tol=1e-4):
+    """Sharded C5 result `r` (this rank's landmarks pts_sel) against the replica `rr` of the whole
+    problem. Relative errors: chi2 and the poses (quaternion + translation, against the largest
+    magnitude of each), the rank's points; `c5_sharded_parity` is True on every rank only if each
+    is within tol and the iteration / trial counts agree."""
+    def rel(a, b):
+        a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+        return float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-30)) if b.size else 0.0
+    errs = {"chi2": rel([r.final_chi2], [rr.final_chi2]), "pose_q": rel(r.pose_q, rr.pose_q),
+            "pose_t": rel(r.pose_t, rr.pose_t), "points": rel(r.points, rr.points[pts_sel])}
+    sched = r.iterations_done == rr.iterations_done and r.lm_trials == rr.lm_trials
+    ok = float(sched and max(errs.values()) <= tol)
+    worst = _max_over_ranks(ws, max(errs.values()))
+    ok_all = _max_over_ranks(ws, 1.0 - ok) == 0.0
+    return {"c5_sharded_parity": bool(ok_all), "c5_sharded_max_rel_err": float(f"{worst:.3g}"),
+            "c5_sharded_schedule_equal": bool(_max_over_ranks(ws, 0.0 if sched else 1.0) == 0.0)}
 
 
 def cpu_gba(iters_sample=3, iters=10):
@@ -684,9 +718,9 @@ class Watchdog:
     collective across ranks, say), the watchdog prints the line measured so far with the stage
     that timed out and ends the process, so the driver never loses the headline."""
 
-    def __init__(self, out, rank, limit_s):
+    def __init__(self, out, rank, limit_s, detail=None):
         import threading
-        self.out, self.rank, self.stage, self.done = out, rank, "", False
+        self.out, self.rank, self.stage, self.done, self.detail = out, rank, "", False, detail
         self.t = threading.Timer(limit_s, self._fire)
         self.t.daemon = True
         self.t.start()
@@ -696,7 +730,7 @@ class Watchdog:
             return
         if self.rank == 0:
             self.out.setdefault("extra", {})["timeout_in"] = self.stage
-            print(json.dumps(self.out), flush=True)
+            print(json.dumps(compact_line(self.out, write_detail(self.out, self.detail))), flush=True)
         os._exit(0)
 
     def disarm(self):
@@ -756,6 +790,7 @@ def c2_headline(args, ws, rank):
     r["octree_candidates_per_frame"] = c2.n_cand
     r["frames_np"] = c2.frames_np
     r["ctx"] = c2.ext.ctx
+    r["ext"] = c2.ext
     # the camera streams end here, so that the one-camera figures below run with one camera in the
     # process (the front-end sizes its cone tiles by the number of live streams)
     c2.close()
@@ -1015,7 +1050,12 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={ws}")
     r = c2_headline(args, ws, rank)
     K, W, dom = args.steps, args.warmup, r["dom"]
-    achieved = r["dom_bytes"] / (r["dom_avg_ms"] * 1e-3) / 1e9
+    # algorithmic bytes per frame = A0 + 2 sum_{l>=1} A_l + N * 56 (1,649,864 B at
+    # 640x480 and N = 1000), one frame per launch of the dominant kernel; the kernel's own bytes
+    # (stage_bytes) ride along as kernel_own_bytes
+    frame_bytes = survey_frame_bytes(r["ext"], StreamC2.W, StreamC2.H, r["keypoints"] or 1000.0)
+    achieved = frame_bytes / (r["dom_avg_ms"] * 1e-3) / 1e9
+    own = r["dom_bytes"] / (r["dom_avg_ms"] * 1e-3) / 1e9
     ks = kernel_symbol(dom, 1)
     host = host_cpus()
     out = {
@@ -1047,7 +1087,11 @@ def main():
         "roofline": {"kernel": ks, "bound": headline_bound(ks), "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                      "traffic": load_traffic(ks, "c2"), "counters": load_counters(ks, "c2"),
-                     "algorithmic_bytes_per_launch": int(r["dom_bytes"]), "avg_launch_ms": round(r["dom_avg_ms"], 5),
+                     "algorithmic_bytes_per_launch": int(frame_bytes),
+                     "bytes_rule": "SURVEY 8(d): A0 + 2*sum(A_l, l>=1) + N*56 per frame, 1 frame per launch",
+                     "kernel_own_bytes": {"bytes": int(r["dom_bytes"]), "achieved": round(own, 3),
+                                          "frac": round(own / HBM_PEAK_GBS, 6)},
+                     "avg_launch_ms": round(r["dom_avg_ms"], 5),
                      "launches_timed": r["dom_n"],
                      "timing": "kernel execution span from device timestamps (k_pyr_cone: first workgroup "
                                "start -> last workgroup end, s_memrealtime; the other stages: "
@@ -1059,7 +1103,7 @@ def main():
                                                        for k, v in r["stage_ms_one_frame"].items()}},
     }
     if not args.no_extra:
-        wd = Watchdog(out, rank, args.extra_timeout)
+        wd = Watchdog(out, rank, args.extra_timeout, args.detail)
         extra = {}
         for name, fn in (("c5", lambda: c5_gba(ws, rank, args.gba_iters)),
                          ("c3", lambda: c3_batch(args, ws, rank)),
@@ -1100,10 +1144,70 @@ def main():
                                                 f"extract + match to the previous frame, {c3c['cores']} threads, "
                                                 f"{c3c['wall']:.1f}s wall")
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        detail = write_detail(out, args.detail)
+        print(json.dumps(compact_line(out, detail)), flush=True)
     if ws > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+
+
+def write_detail(out, path):
+    """The full record (every counter dict, per-stage timings, samples) goes to a file; the
+    printed line keeps the figures (the driver reads only the last ~4 KB of stdout)."""
+    if not path:
+        return None
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+        return os.path.relpath(os.path.abspath(path), ROOT)
+    except OSError:
+        return None
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if isinstance(d, dict) and k in d}
+
+
+def compact_line(out, detail):
+    """The one JSON line rank 0 prints: the contract fields, the headline roofline and CPU
+    baseline, and every extra figure (C3, C4, C5, 8f), without the PMC counter dicts and stage
+    tables (those are in `detail` and profiles/counters.json)."""
+    line = {k: v for k, v in out.items() if k not in ("roofline", "extra", "cpu_baseline", "config")}
+    cfg = out["config"]
+    line["config"] = _pick(cfg, ("workload", "step", "frames_per_step", "parallelism", "cameras",
+                                 "one_camera_8_in_flight_frames_per_s", "keypoints_per_frame"))
+    rf = out["roofline"]
+    line["roofline"] = _pick(rf, ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic",
+                                  "algorithmic_bytes_per_launch", "bytes_rule", "avg_launch_ms", "launches_timed",
+                                  "kernel_own_bytes"))
+    ex = out.get("extra")
+    if ex is not None:
+        e = {}
+        for k, v in ex.items():
+            if not isinstance(v, (dict, list)) and k not in ("c3_partition", "f8_inputs", "c5_problem",
+                                                             "c5_gba_scaling_note", "c3_octree_candidates_per_frame",
+                                                             "c4_lba_batch_per_gpu", "c4_lba_batched_trials_mean",
+                                                             "c5_gba_iterations", "c3_batches_in_flight"):
+                e[k] = v
+        rk = ("kernel", "bound", "frac", "avg_launch_ms")
+        for k in ("c3_roofline", "c3_hbm_stage", "c4_roofline", "c5_dense_solve_microbench"):
+            if isinstance(ex.get(k), dict):
+                e[k] = _pick(ex[k], rk + ("stage_ms",))
+        if isinstance(ex.get("c5_nd_roofline"), dict):
+            e["c5_nd_roofline"] = _pick(ex["c5_nd_roofline"], ("bound", "frac", "avg_solve_ms"))
+        if "c5_gba_chi2" in ex:
+            e["c5_gba_chi2"] = ex["c5_gba_chi2"]
+        line["extra"] = e
+    cb = out.get("cpu_baseline")
+    if cb is not None:
+        c = {k: v for k, v in cb.items() if not isinstance(v, dict) and not k.endswith("_sample")
+             and k != "sample"}
+        c["sample"] = f"oracle/ (g++ -O3), {cb.get('cores')} threads; bounded samples (see detail)"
+        c["host_cpu"] = cb.get("host", {}).get("model", "")
+        line["cpu_baseline"] = c
+    line["detail"] = detail
+    return line
 
 
 if __name__ == "__main__":

@@ -38,6 +38,12 @@ unsigned dag_spin_max();
 // before the first solve, never reset between solves: every solve counts its own epoch)
 size_t dag_doubles(int n);
 size_t dag_ints(int n);
+// dag_doubles for NT tiles per side: L (NT x NT tiles), the three partial rows and the diagonal
+// inverses (4 NT tiles), y / rhs partials / x / s (4 NT x 32), the column-major copies of L and
+// of the inverses (NT x NT + NT tiles) that the chain's backward reads
+__host__ __device__ inline size_t dag_doubles_nt(size_t NT) {
+    return (NT * NT + 4 * NT) * kDagTile * kDagTile + NT * 4 * kDagTile + (NT * NT + NT) * kDagTile * kDagTile;
+}
 
 struct DagDev {
     double* buf;         // dag_doubles(n)

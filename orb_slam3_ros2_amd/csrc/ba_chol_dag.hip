@@ -46,6 +46,7 @@ constexpr int kT = kDagTile;
 constexpr int kTD = kT * kT;            // doubles per tile
 constexpr unsigned kSpinMax = 1u << 19;   // default poll bound (ORBHIP_DAG_SPIN_MAX overrides)
 constexpr size_t kMinLds = 84 * 1024;   // > 80 KB: one workgroup per CU
+constexpr int kCopyTask = 0x7FFF;       // task code kCopyTask << 16 | k: the copies of interval k
 #ifndef ORBHIP_DAG_NEWTON
 #define ORBHIP_DAG_NEWTON 1
 #endif
@@ -53,32 +54,14 @@ constexpr int kNewton = ORBHIP_DAG_NEWTON;   // Newton steps after v_rsq_f64 / v
 #ifndef ORBHIP_DAG_DIAG_DPP
 #define ORBHIP_DAG_DIAG_DPP 1   // r05: the 16x16 diagonal factorizations by DPP elimination (diag16_dpp)
 #endif
-// A/B switches measured on MI355X (tools/build_ab.sh + probe_cholesky_dag.py, r05): loading the
-// next interval's helper flag before the barrier made the interval longer (13.2k -> 14.0k cycles
-// at n = 294), and the column-major backward's scattered 8-byte tile loads cost more than the
-// reductions they remove (backward 41.8k -> 59.9k cycles): both off.
-#ifndef ORBHIP_DAG_FLAG_AHEAD
-#define ORBHIP_DAG_FLAG_AHEAD 0   // waves 2/3 load the next interval's helper flag before the barrier
-#endif
 #ifndef ORBHIP_DAG_T_W1
 // r05: wave 1 (idle after its publishes) applies T_{k+1}'s column-k term for waves 2 / 3: the
 // interval 13.55k -> 12.8k cycles at n = 294 (every wave now ends within ~0.6k of the others)
 #define ORBHIP_DAG_T_W1 1
 #endif
-#ifndef ORBHIP_DAG_Q10_W2
-// wave 2 computes the column k-1 term of D'_{k+2}'s quadrant (1,0) for wave 3 (which has 6 of the
-// 10 D' products), handing it over in LDS (Q10, flag F6). r05 A/B (two alternating runs): wave 3
-// ended ~0.2k cycles earlier and wave 2 ~0.5k later, the interval unchanged (12.6-12.8k): off
-#define ORBHIP_DAG_Q10_W2 0
-#endif
-#ifndef ORBHIP_DAG_BACK_COL
-#ifndef ORBHIP_DAG_W23_EARLY
-#define ORBHIP_DAG_W23_EARLY 0   // r05: waves 2/3 U, T and D column k-1 MFMA chains in one block (dense case): measured slower
-#endif
-#define ORBHIP_DAG_BACK_COL 0   // the chain-only backward on column-major tile loads (bwd_col_dot)
-#endif
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(1))) int gint;
 typedef __attribute__((address_space(1))) double gdbl;
 
@@ -138,6 +121,34 @@ __device__ __forceinline__ void qstore(__amdgpu_buffer_rsrc_t rs, int dbl_off, c
     const u32x4 v = {lo32(d[2]), hi32(d[2]), lo32(d[3]), hi32(d[3])};
     __builtin_amdgcn_raw_buffer_store_b128(u, rs, off, 0, 16);
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, off + 16, 0, 16);
+}
+// Column copies of a tile for the chain's backward: lane L = c + 32 hh (c = L & 31, hh = L >> 5)
+// reads column c, rows 16 hh .. 16 hh + 15, as 8 pairs; pair i of every lane forms one contiguous
+// 1 KB block, so each of a tile's 8 loads is fully coalesced. Element (r, c) sits at double
+// 2 (64 i + L) + e, i = (r & 15) >> 1, e = r & 1, L = c + 32 (r >> 4).
+__device__ __forceinline__ int cm_idx(int r, int c) {
+    return 2 * (64 * ((r & 15) >> 1) + c + 32 * (r >> 4)) + (r & 1);
+}
+// quadrant `quad` (a = quad >> 1, b = quad & 1) of a tile held in the quadrant layout (lane l,
+// component q: element (16 a + (l & 15), 16 b + 4 q + (l >> 4))) stored into its column copy
+__device__ __forceinline__ void cmstore(__amdgpu_buffer_rsrc_t rs, int dbl_off, int quad, const double4_t& d) {
+    const int lane = threadIdx.x & 63, a = quad >> 1, b = quad & 1;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const u32x2 u = {lo32(d[q]), hi32(d[q])};
+        const int i = dbl_off + cm_idx(16 * a + (lane & 15), 16 * b + 4 * q + (lane >> 4));
+        __builtin_amdgcn_raw_buffer_store_b64(u, rs, i * 8, 0, 16);
+    }
+}
+// this lane's column of a column copy (v[j] = element (16 hh + j, c)), sc1
+__device__ __forceinline__ void cmload(__amdgpu_buffer_rsrc_t rs, int dbl_off, double (&v)[16]) {
+    const int off = (dbl_off + 2 * (int)(threadIdx.x & 63)) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 1024 * i, 0, 16);
+        v[2 * i] = mk64(u.x, u.y);
+        v[2 * i + 1] = mk64(u.z, u.w);
+    }
 }
 // a quadrant held in LDS (same layout)
 __device__ __forceinline__ double4_t lq(const double* base) {
@@ -260,8 +271,8 @@ __device__ int wave_wait_prefix(const int* fa, const int* fb, const int* fc, int
 }
 
 struct Lay {   // offsets (doubles) into the DAG buffer, flags
-    int oL, oP, oLi, oY, oR, oX, oS;
-    int *ctl, *fL, *fP0, *fP1, *fP2, *fCh, *fX, *fS;
+    int oL, oP, oLi, oY, oR, oX, oS, oCM, oCI;
+    int *ctl, *fL, *fP0, *fP1, *fP2, *fCh, *fX, *fS, *fCp;
     __device__ Lay(const DagK& a) {
         const int NT = a.NT;
         oL = 0;
@@ -271,6 +282,12 @@ struct Lay {   // offsets (doubles) into the DAG buffer, flags
         oR = oY + NT * kT;
         oX = oR + NT * kT;   // backward: x_R published by the chain
         oS = oX + NT * kT;   // backward: the helpers' sums s_j = y_j - sum_{R >= j+2} L(R, j)^T x_R
+        // the chain's backward (short rows, dag_chain): column-major copies of the L tiles (element
+        // (r, c) at 32 c + r) and of the diagonal inverses, so that a lane's tile column is 16
+        // contiguous doubles (the full tiles' copies by their helper tasks, the chain's own tiles
+        // by the copy tasks, fCp)
+        oCM = oS + NT * kT;
+        oCI = oCM + NT * NT * kTD;
         ctl = a.ints;
         fL = ctl + 4;
         fP0 = fL + NT * NT;
@@ -279,6 +296,7 @@ struct Lay {   // offsets (doubles) into the DAG buffer, flags
         fCh = fP2 + NT;
         fX = fCh + NT;
         fS = fX + NT;
+        fCp = fS + NT;
     }
 };
 
@@ -358,9 +376,27 @@ __device__ void dag_helper(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t r
         wsel = (wsel + 1) & 3;
         return m;
     };
+    const bool copies = !a.pb && !a.nti;   // the chain's backward reads column-major copies
     for (int t = t0; t < t1; t++) {
         const int code = a.tasks[t];
         const int R = code >> 16, C = code & 0xFFFF;
+        if (R == kCopyTask) {
+            // copy task of interval k = C: column-major copies of the tiles the chain published in
+            // it (L(k+1, k), L(k+1, k-1), Linv_k; one flag covers all three), then fCp[k]
+            const int k = C;
+            if (wg_prefix(L.fCh + k, nullptr, nullptr, 1) == 0) break;
+            const int tA = L.oL + ((k + 1) * NT + k) * kTD, tI = L.oLi + k * kTD;
+            const double4_t qa = qload(rs, tA + quad * 256), qi = qload(rs, tI + quad * 256);
+            double4_t qb = {0, 0, 0, 0};
+            if (k >= 1) qb = qload(rs, L.oL + ((k + 1) * NT + k - 1) * kTD + quad * 256);
+            cmstore(rs, L.oCM + ((k + 1) * NT + k) * kTD, quad, qa);
+            cmstore(rs, L.oCI + k * kTD, quad, qi);
+            if (k >= 1) cmstore(rs, L.oCM + ((k + 1) * NT + k - 1) * kTD, quad, qb);
+            drain_stores();
+            __syncthreads();
+            if (tid == 0) st_flag(L.fCp + k, epoch);
+            continue;
+        }
         // by R - C: 0 the diagonal partial (columns <= C-4), 1 the sub-diagonal partial (<= C-3), 2
         // the second sub-diagonal's partial (<= C-2), >= 3 a full tile (every column, then the TRSM);
         // 3: a tile of a partial solve's trailing block (C >= nti): every column < nti, no TRSM
@@ -415,6 +451,7 @@ __device__ void dag_helper(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t r
             panel_add(out, qload(rs, li + (2 * cq) * 256), lq(Tx + (2 * rq) * 256));
             if (cq == 1) panel_add(out, qload(rs, li + 3 * 256), lq(Tx + (2 * rq + 1) * 256));
             qstore(rs, L.oL + (R * NT + C) * kTD + quad * 256, out);
+            if (copies) cmstore(rs, L.oCM + (R * NT + C) * kTD, quad, out);   // covered by the tile's flag
             target = L.fL + R * NT + C;
         } else if (type == 3) {   // the trailing block's contribution, where its L tile would be
             qstore(rs, L.oL + (R * NT + C) * kTD + quad * 256, acc);
@@ -451,25 +488,13 @@ __device__ __forceinline__ bool chain_factor(const double* Dx, double* scr, doub
     return ok;
 }
 
-// column c = lane & 31 of a tile, rows 16 hh .. 16 hh + 15 (hh = lane >> 5), from its quadrant
-// layout (sc1 loads): the backward's L^T x then needs 16 lane-local FMAs and one half-wave sum
-// instead of eight 16-lane reductions
-__device__ __forceinline__ void tcol(__amdgpu_buffer_rsrc_t rs, int dbl_off, double (&v)[16]) {
-    const int lane = threadIdx.x & 63, c = lane & 31, hh = lane >> 5;
-    const int base = dbl_off + (2 * hh + (c >> 4)) * 256 + 64 * (c & 3) + ((c & 15) >> 2);
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-        const auto u = __builtin_amdgcn_raw_buffer_load_b64(rs, (base + 4 * i) * 8, 0, 16);
-        v[i] = mk64(u[0], u[1]);
-    }
-}
 // sum over the two half-waves (lane l and l ^ 32), the same bits in both
 __device__ __forceinline__ double half32_sum(double v) {
     const auto tl = __builtin_amdgcn_permlane32_swap(lo32(v), lo32(v), false, false);
     const auto th = __builtin_amdgcn_permlane32_swap(hi32(v), hi32(v), false, false);
     return mk64(tl[0], th[0]) + mk64(tl[1], th[1]);
 }
-// (T^T x)[c] for a tile column held by tcol and x (32 doubles in LDS): every lane of column c
+// (T^T x)[c] for a tile column held by cmload and x (32 doubles in LDS): every lane of column c
 // returns it
 __device__ __forceinline__ double bwd_col_dot(const double (&v)[16], const double* x) {
     const double* xh = x + 16 * ((threadIdx.x & 63) >> 5);
@@ -617,8 +642,6 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     int* F3 = word + 12;                // wave 1: row 1 of L(k+1, k) ready
     int* F4 = word + 13;                // wave 2 / 3: their rows of T_{k+1} up to column k-1 in TpN
     int* F5 = word + 14;
-    int* F6 = word + 15;                // wave 2: Q10 holds quadrant (1,0)'s column k-1 term
-    [[maybe_unused]] double* Q10 = (double*)(rfl + NT + (NT & 1));   // 256 doubles after the row_first ints
     unsigned long long* wts = (unsigned long long*)(lds + 11264 + 8);   // per-wave cycles (dbg)
     unsigned long long* stm = (unsigned long long*)(lds + 10560);       // sub-phase stamps (dbg), 16
 #define DAG_STAMP(i) do { if (dbg && lane == 0) stm[i] = __builtin_amdgcn_s_memtime() - tk; } while (0)
@@ -634,7 +657,6 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         *F3 = 0;
         *F4 = 0;
         *F5 = 0;
-        *F6 = 0;
     }
     for (int i = tid; i < NT; i += blockDim.x) rfl[i] = a.rf[i];
     int c1 = 0, c2 = 0;
@@ -690,7 +712,6 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         if (lane == 2) return (!zT && max(rc, ra) <= kk - 2) ? L.fP1 + kk1 : nullptr;
         return (!zD && rc <= kk2 - 4) ? L.fP0 + kk2 : nullptr;
     };
-    int fvp = 0;   // waves 2/3: the next interval's helper flag, loaded ahead
     for (int k = 0; k < kEnd; k++) {
         const unsigned long long tk = dbg ? __builtin_amdgcn_s_memtime() : 0;
         const int k1 = k + 1, K2 = k + 2;
@@ -747,9 +768,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         double* Dq = lds + 10240;
         const int* f3 = wid >= 2 ? helper_flag(k) : nullptr;
         const bool need3 = f3 != nullptr;
-        // the flag was loaded at the end of the previous interval (fvp), so its round trip overlaps
-        // the interval barrier; interval 0 loads it here
-        const int fv = (k == 0 || !ORBHIP_DAG_FLAG_AHEAD) ? ld_flag(need3 ? f3 : L.ctl) : fvp;
+        const int fv = ld_flag(need3 ? f3 : L.ctl);
         if (wid == 0) {
             if (dbg && lane == 0) wts[6] = __builtin_amdgcn_s_memtime() - tk;
             // row 0 of L(k+1, k) = T Linv_k^T
@@ -889,7 +908,6 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             if (!got) {
                 if (lane == 0) word[4] = 1;
                 if (ORBHIP_DAG_T_W1) lds_signal(h ? F5 : F4, k + 2);
-                if (ORBHIP_DAG_Q10_W2 && h == 0) lds_signal(F6, k + 2);
             } else {
                 const int tD = L.oL + (K2 * NT + k - 1) * kTD;
                 double4_t d0 = {0, 0, 0, 0}, d1 = {0, 0, 0, 0}, e0 = {0, 0, 0, 0}, e1 = {0, 0, 0, 0};
@@ -897,11 +915,11 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                     d0 = qload(rs, tD + (2 * h) * 256);
                     d1 = qload(rs, tD + (2 * h + 1) * 256);
                 }
-                // quadrant (1, 0) of D'_{k+2} needs both row halves of L(k+2, k-1): the other half
-                // is loaded by the wave that forms the term (wave 2 with ORBHIP_DAG_Q10_W2, else 3)
-                if (useP0c && h == (ORBHIP_DAG_Q10_W2 ? 0 : 1)) {
-                    e0 = qload(rs, tD + (ORBHIP_DAG_Q10_W2 ? 2 : 0) * 256);
-                    e1 = qload(rs, tD + (ORBHIP_DAG_Q10_W2 ? 3 : 1) * 256);
+                // quadrant (1, 0) of D'_{k+2} needs both row halves of L(k+2, k-1): wave 3, which
+                // forms that term, loads the other half
+                if (useP0c && h == 1) {
+                    e0 = qload(rs, tD);
+                    e1 = qload(rs, tD + 256);
                 }
                 double4_t u[2], t[2], dd[2];
 #pragma unroll
@@ -934,42 +952,9 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 double4_t o0 = {0, 0, 0, 0}, o1 = {0, 0, 0, 0};
                 // D' column k-1 terms (da, db; dc, de: quadrant (1, 0), wave 3)
                 double4_t da = {0, 0, 0, 0}, db = {0, 0, 0, 0}, dc = {0, 0, 0, 0}, de = {0, 0, 0, 0};
-#if ORBHIP_DAG_W23_EARLY
-                // every term present (the dense case): U's, T's and D''s column k-1 products in one
-                // basic block, so the scheduler interleaves their independent MFMA chains (T and
-                // D' do not depend on L(k+2, k)); the same MFMAs in the same order per accumulator
-                const bool early = inEnvU && useU && inEnvT && useTp && useP0c;
-#else
-                const bool early = false;
-#endif
-                if (early) {
-                    double4_t ub0 = {0, 0, 0, 0}, ub1 = {0, 0, 0, 0}, tb0 = {0, 0, 0, 0}, tb1 = {0, 0, 0, 0};
-                    mfma_sub(u[0], l1q[0], d0);
-                    mfma_sub(ub0, l1q[1], d1);
-                    mfma_sub(u[1], l1q[2], d0);
-                    mfma_sub(ub1, l1q[3], d1);
-                    mfma_sub(t[0], l2q[0], d0);
-                    mfma_sub(tb0, l2q[1], d1);
-                    mfma_sub(t[1], l2q[2], d0);
-                    mfma_sub(tb1, l2q[3], d1);
-                    mfma_sub(da, d0, d0);
-                    mfma_sub(db, d1, d1);
-                    u[0] += ub0;
-                    u[1] += ub1;
-                    t[0] += tb0;
-                    t[1] += tb1;
-                    double4_t o1b = {0, 0, 0, 0};
-                    panel_add(o0, liq[0], u[0]);
-                    panel_add(o1, liq[1], u[0]);
-                    panel_add(o1b, liq[2], u[1]);
-                    o1 += o1b;
-#if !ORBHIP_DAG_Q10_W2
-                    if (h == 1) {   // quadrant (1, 0): row half 1 against row half 0
-                        mfma_sub(dc, e0, d0);
-                        mfma_sub(de, e1, d1);
-                    }
-#endif
-                } else if (inEnvU) {
+                // (U's, T's and D''s column k-1 chains in one basic block measured slower, r05: L(k+2, k)
+                // is published first, wave 1 waits on it)
+                if (inEnvU) {
                     if (useU) {
 #pragma unroll
                         for (int c = 0; c < 2; c++) {
@@ -988,7 +973,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 sq(L2n + (2 * h) * 256, o0);
                 sq(L2n + (2 * h + 1) * 256, o1);
                 DAG_STAMP(5 + 4 * h);
-                if (!early && inEnvT && useTp) {
+                if (inEnvT && useTp) {
 #pragma unroll
                     for (int c = 0; c < 2; c++) {
                         double4_t tb = {0, 0, 0, 0};
@@ -1004,23 +989,13 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
 #endif
                 DAG_STAMP(12 + 2 * h);
                 {   // D'_{k+2}: column k-1 (L(k+2, k-1)) and column k (L(k+2, k)) in independent chains
-#if ORBHIP_DAG_Q10_W2
-                    if (useP0c && h == 0) {   // quadrant (1, 0) for wave 3: the same operands as its form
-                        mfma_sub(dc, d0, e0);
-                        mfma_sub(de, d1, e1);
-                        sq(Q10, dc + de);
-                        lds_signal(F6, k + 2);
-                    }
-#endif
-                    if (!early && useP0c) {
+                    if (useP0c) {
                         mfma_sub(da, d0, d0);
                         mfma_sub(db, d1, d1);
-#if !ORBHIP_DAG_Q10_W2
                         if (h == 1) {   // quadrant (1, 0): row half 1 against row half 0
                             mfma_sub(dc, e0, d0);
                             mfma_sub(de, e1, d1);
                         }
-#endif
                     }
                     double4_t dg = {0, 0, 0, 0}, dh = {0, 0, 0, 0};
                     if (inEnvU) {
@@ -1032,14 +1007,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                         dd[0] += dsum;
                     } else {
                         dd[1] += dsum;
-#if ORBHIP_DAG_Q10_W2
-                        if (useP0c) {
-                            lds_wait(F6, k + 2);
-                            dd[0] += lq(Q10);
-                        }
-#else
                         dd[0] += dc + de;
-#endif
                     }
                 }
                 if (h == 0) {
@@ -1077,10 +1045,6 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 sq(TpN + (2 * h + 1) * 256, t[1]);
 #endif
             }
-        }
-        if (ORBHIP_DAG_FLAG_AHEAD && wid >= 2 && k + 1 < kEnd) {
-            const int* fn = helper_flag(k + 1);
-            fvp = ld_flag(fn ? fn : L.ctl);
         }
         if (dbg && lane == 0) wts[wid] = __builtin_amdgcn_s_memtime() - tk;
         lds_barrier();
@@ -1157,21 +1121,6 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         s += dpp64<0xB1>(s);
         if (hh == 0) xs[k * kT + c] = s;
     };
-    [[maybe_unused]] auto sub_tile = [&](const double4_t* tl, const double* xR, int j) {   // s_j -= L(R, j)^T x_R
-        double t[2][4];
-        tile_lt_x(tl, xR, t);
-        if (cc == 0) {
-#pragma unroll
-            for (int b = 0; b < 2; b++)
-#pragma unroll
-                for (int q = 0; q < 4; q++) ys[j * kT + 16 * b + rg + 4 * q] -= t[b][q];
-        }
-    };
-    // prefetch rings two steps deep (register sets by step parity: each role's loop is unrolled by
-    // two, so the set index is a compile-time constant, and the two roles' rings have disjoint live
-    // ranges): wave 0 tile (R, R-1) and Linv_{R-1}; waves 1..3 the first kPf tiles of their share of
-    // row R, longer rows stream the rest a tile at a time. Both roles pass the same barriers.
-    constexpr int kPf = 3;
     if (a.G > 0 && a.pb) {
         // with helpers: they accumulate s_j for j <= NT-3 (dag_helper_backward) from the x_R this
         // wave publishes; wave 0 alone walks the chain: x_{R-1} = Linv_{R-1}^T (s_{R-1} -
@@ -1225,219 +1174,189 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         __syncthreads();
         if (!word[5]) aborted = true;
     } else {   // short rows (or no helpers): the chain work-group alone
-#if ORBHIP_DAG_BACK_COL
-    // Every tile is final here: the last diagonal tile waited, directly or through the helpers'
-    // partials (which waited on their tiles' flags before publishing), on every tile of L, and
-    // this work-group's own tile stores are drained by the barrier. Wave 0 walks the chain,
-    // x_{R-1} = Linv_{R-1}^T (s_{R-1} - L(R, R-1)^T x_R); waves 1..3 subtract row R's other tiles
-    // from the running sums s_j, j <= R-2. Both read their tiles column-major (tcol), two steps
-    // ahead, and pass one barrier per step.
-    __syncthreads();
-    if (!aborted) {
+        // Right-looking, no barrier per step (r06). Wave 0 walks the chain: step t forms
+        // x_{t-1} = Linv_{t-1}^T (s_{t-1} - L(t, t-1)^T x_t) (t = NT: Linv_{NT-1}^T s_{NT-1}) from
+        // column-major copies (a lane's column: 16 contiguous doubles, a 16-FMA dot product and one
+        // half-wave sum), its operands prefetched two steps ahead; the last two steps' operands are
+        // still in this work-group's LDS. Waves 1..3 own the columns j = wid - 1 (mod 3) of every
+        // row: as x_R appears (xcnt) they subtract L(R, j)^T x_R from s_j for j <= R - 2, tiles
+        // streamed two ahead, and count each applied row (cnt[j]); step t waits until s_{t-1} has
+        // every row R >= t + 1 of its envelope. LDS flags only (the forward's tile buffers are
+        // free now): cnt at the T / D' buffers, xcnt / the abort word after the forward's flags.
+        int* cnt = (int*)(lds + 6144);
+        int* xcnt = word + 16;
+        int* bab = word + 17;
+        int* cpok = word + 18;   // wave 0 saw every copy task's flag
+        for (int i = tid; i < NT; i += blockDim.x) cnt[i] = 0;
+        if (tid == 0) { *xcnt = 0; *bab = 0; *cpok = 0; }
+        __syncthreads();
         const int c = lane & 31, hh = lane >> 5;
-        if (wid == 0) {
-            double st[2][16], li[2][16];
-            auto load = [&](auto setc, int R) {   // inputs of step R
-                constexpr int S = decltype(setc)::value;
-                if (R >= 1) {
-                    tcol(rs, L.oL + (R * NT + R - 1) * kTD, st[S]);
-                    tcol(rs, L.oLi + (R - 1) * kTD, li[S]);
-                }
-            };
-            auto step = [&](auto setc, int R) {
-                constexpr int S = decltype(setc)::value;
-                if (dbg && lane == 0 && R < kDbgBackR) dbg[kDbgBackOff + 3 * R] = __builtin_amdgcn_s_memtime() - t_fwd;
-                const double p = bwd_col_dot(st[S], xs + R * kT);
-                if (hh == 0) rvec[c] = ys[(R - 1) * kT + c] - p;
-                wave_lds_sync();
-                const double xv = bwd_col_dot(li[S], rvec);
-                load(setc, R - 2);   // step R-2's inputs into this set
-                if (hh == 0) xs[(R - 1) * kT + c] = xv;
-                if (dbg && lane == 0 && R < kDbgBackR) dbg[kDbgBackOff + 3 * R + 1] = __builtin_amdgcn_s_memtime() - t_fwd;
-                lds_barrier();
-            };
-            if (lane < kT) rvec[lane] = ys[(NT - 1) * kT + lane];
-            wave_lds_sync();
-            apply_lt(NT - 1);
-            load(std::integral_constant<int, 0>{}, NT - 1);
-            load(std::integral_constant<int, 1>{}, NT - 2);
-            lds_barrier();
-            for (int R = NT - 1; R >= 1; R -= 2) {
-                step(std::integral_constant<int, 0>{}, R);
-                if (R - 1 >= 1) step(std::integral_constant<int, 1>{}, R - 1);
-            }
-        } else {
-            double pf[2][kPf][16];
-            auto load = [&](auto setc, int R) {   // the first tiles of this wave's share of row R
-                constexpr int S = decltype(setc)::value;
-                if (R >= 2) {
-                    const int j0 = rfl[R] + (wid - 1);
+        // element (16 hh + i, c) of a quadrant-layout tile in LDS, i = 0..15
+        auto lds_col = [&](const double* base, double (&v)[16]) {
 #pragma unroll
-                    for (int u = 0; u < kPf; u++)
-                        if (j0 + 3 * u <= R - 2) tcol(rs, L.oL + (R * NT + j0 + 3 * u) * kTD, pf[S][u]);
-                }
-            };
-            auto sub = [&](const double (&v)[16], const double* xR, int j) {   // s_j -= L(R, j)^T x_R
-                const double p = bwd_col_dot(v, xR);
-                if (hh == 0) ys[j * kT + c] -= p;
-            };
-            auto step = [&](auto setc, int R) {
-                constexpr int S = decltype(setc)::value;
-                const double* xR = xs + R * kT;
-                if (R >= 2) {
-                    const int j0 = rfl[R] + (wid - 1);
-#pragma unroll
-                    for (int u = 0; u < kPf; u++) {
-                        const int j = j0 + 3 * u;
-                        if (j > R - 2) break;
-                        sub(pf[S][u], xR, j);
-                    }
-                    for (int jb = j0 + 3 * kPf; jb <= R - 2; jb += 3) {
-                        double tl[16];
-                        tcol(rs, L.oL + (R * NT + jb) * kTD, tl);
-                        sub(tl, xR, jb);
-                    }
-                }
-                load(setc, R - 2);   // row R-2's first tiles into this set
-                if (dbg && wid == 1 && lane == 0 && R < kDbgBackR)
-                    dbg[kDbgBackOff + 3 * R + 2] = __builtin_amdgcn_s_memtime() - t_fwd;
-                lds_barrier();
-            };
-            load(std::integral_constant<int, 0>{}, NT - 1);
-            load(std::integral_constant<int, 1>{}, NT - 2);
-            lds_barrier();
-            for (int R = NT - 1; R >= 1; R -= 2) {
-                step(std::integral_constant<int, 0>{}, R);
-                if (R - 1 >= 1) step(std::integral_constant<int, 1>{}, R - 1);
-            }
-        }
-    }
-#else
-    if (!aborted && wid != 0) {
-        // every tile (R, j), j <= R-2, rows 2.. (16 rows of this wave per round: up to 32 flag
-        // loads in flight per lane)
-        bool good = true;
-        for (int R0 = 1 + wid; R0 < NT && good; R0 += 48) {
-            for (unsigned spins = 0;; spins++) {
-                int okl = 1;
-#pragma unroll
-                for (int u = 0; u < 16; u++) {
-                    const int R = R0 + 3 * u;
-                    if (R < NT) {
-                        const int rfR = rfl[R];
-#pragma unroll
-                        for (int hh = 0; hh < 2; hh++) {
-                            const int j = rfR + 64 * hh + lane;
-                            if (j <= R - 2) okl &= ld_flag(L.fL + R * NT + j) == epoch ? 1 : 0;
-                        }
-                    }
-                }
-                if (__all(okl)) break;
-                if (ld_flag(L.ctl + 2) == epoch || spins >= a.smax) {
-                    if (spins >= a.smax && lane == 0) {
+            for (int i = 0; i < 16; i++) v[i] = base[qidx(16 * hh + i, c)];
+        };
+        // an LDS count reaching v; false on the abort word or after smax polls (then the solve fails:
+        // the abort word and the problem's timeout count, as a global wait's timeout does)
+        auto lwait = [&](const int* w, int v) -> bool {
+            for (unsigned spins = 0; __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < v; spins++) {
+                if (__hip_atomic_load(bab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+                if (spins >= a.smax) {
+                    if (lane == 0) {
                         st_flag(L.ctl + 2, epoch);
                         __hip_atomic_fetch_add((gint*)(L.ctl + 3), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
-                    good = false;
-                    break;
+                    return false;
                 }
-                __builtin_amdgcn_s_sleep(2);
+                __builtin_amdgcn_s_sleep(1);
             }
-        }
-        if (!good && lane == 0) word[5] = 0;
-    }
-    __syncthreads();
-    if (!word[5]) aborted = true;
-    if (!aborted && wid == 0) {
-        double4_t st[2][4], li[2][4];
-        auto load = [&](auto setc, int R) {   // inputs of step R
-            constexpr int S = decltype(setc)::value;
-            if (R >= 1) {
-#pragma unroll
-                for (int qd = 0; qd < 4; qd++) {
-                    st[S][qd] = qload(rs, L.oL + (R * NT + R - 1) * kTD + qd * 256);
-                    li[S][qd] = qload(rs, L.oLi + (R - 1) * kTD + qd * 256);
-                }
-            }
+            asm volatile("" ::: "memory");
+            return true;
         };
-        auto step = [&](auto setc, int R) {   // x_{R-1} = Linv_{R-1}^T (s_{R-1} - L(R, R-1)^T x_R)
-            constexpr int S = decltype(setc)::value;
-            if (dbg && lane == 0 && R < kDbgBackR) dbg[kDbgBackOff + 3 * R] = __builtin_amdgcn_s_memtime() - t_fwd;
-#pragma unroll
-            for (int qd = 0; qd < 4; qd++) sq(Lin + qd * 256, li[S][qd]);
-            double t[2][4];
-            tile_lt_x(st[S], xs + R * kT, t);
-            if (cc == 0) {
-#pragma unroll
-                for (int b = 0; b < 2; b++)
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        const int c = 16 * b + rg + 4 * q;
-                        rvec[c] = ys[(R - 1) * kT + c] - t[b][q];
+        if (!aborted && wid == 0) {
+            bool good = true;
+            double li[2][16], lt[2][16], liA[16], ltA[16];
+            auto load = [&](auto setc, int t) {   // operands of step t <= NT - 2 (copies)
+                constexpr int S = decltype(setc)::value;
+                if (t >= 1) {
+                    cmload(rs, L.oCI + (t - 1) * kTD, li[S]);
+                    cmload(rs, L.oCM + (t * NT + t - 1) * kTD, lt[S]);
+                }
+            };
+            // x_{t-1} from the step's operands (lv: L(t, t-1) by columns, unused at t = NT; iv: Linv_{t-1})
+            auto xstep = [&](const double (&lv)[16], const double (&iv)[16], int t) -> bool {
+                const int k = t - 1;
+                if (dbg && lane == 0 && t < kDbgBackR) dbg[kDbgBackOff + 3 * t] = __builtin_amdgcn_s_memtime() - t_fwd;
+                double p = 0.0;
+                if (t < NT) p = bwd_col_dot(lv, xs + t * kT);
+                int need = 0;   // rows R >= k + 2 whose envelope reaches column k
+                for (int R0 = k + 2; R0 < NT; R0 += 64)
+                    need += __popcll(__ballot(R0 + lane < NT && rfl[R0 + lane] <= k));
+                if (!lwait(cnt + k, need)) return false;
+                if (dbg && lane == 0 && t < kDbgBackR) dbg[kDbgBackOff + 3 * t + 2] = __builtin_amdgcn_s_memtime() - t_fwd;
+                const double r = ys[k * kT + c] - p;
+                if (hh == 0) rvec[c] = r;
+                wave_lds_sync();
+                const double xv = bwd_col_dot(iv, rvec);
+                if (hh == 0) xs[k * kT + c] = xv;
+                lds_signal(xcnt, NT - k);
+                if (dbg && lane == 0 && t < kDbgBackR) dbg[kDbgBackOff + 3 * t + 1] = __builtin_amdgcn_s_memtime() - t_fwd;
+                return true;
+            };
+            {
+                // the last two steps' operands are in LDS (Linv_{NT-1}; Linv_{NT-2} and L(NT-1, NT-2):
+                // the last interval's buffers), the rest are copies: every copy task's flag
+                // (intervals k <= NT - 3) once, then the first two steps' loads
+                lds_col(lds + 1024 * ((NT - 1) & 1), liA);
+                good = xstep(ltA, liA, NT);
+                if (good && NT >= 2) {
+                    lds_col(lds + 1024 * (NT & 1), liA);
+                    lds_col(lds + 2048 + 1024 * ((NT - 1) & 1), ltA);
+                    good = xstep(ltA, liA, NT - 1);
+                }
+                for (int k0 = 0; k0 <= NT - 3 && good; k0 += 64)
+                    good = wave_wait_all(k0 + lane <= NT - 3 ? L.fCp + k0 + lane : nullptr, epoch, L.ctl, a.smax);
+                if (good && lane == 0) lds_signal(cpok, 1);
+                load(std::integral_constant<int, 0>{}, NT - 2);
+                load(std::integral_constant<int, 1>{}, NT - 3);
+                for (int t = NT - 2; t >= 1 && good; t -= 2) {
+                    good = xstep(lt[0], li[0], t);
+                    load(std::integral_constant<int, 0>{}, t - 2);
+                    if (good && t - 1 >= 1) {
+                        good = xstep(lt[1], li[1], t - 1);
+                        load(std::integral_constant<int, 1>{}, t - 3);
                     }
+                }
             }
-            load(setc, R - 2);   // step R-2's inputs into this set
-            wave_lds_sync();
-            apply_lt(R - 1);
-            if (dbg && lane == 0 && R < kDbgBackR) dbg[kDbgBackOff + 3 * R + 1] = __builtin_amdgcn_s_memtime() - t_fwd;
-            lds_barrier();
-        };
-        if (lane < kT) rvec[lane] = ys[(NT - 1) * kT + lane];
-        wave_lds_sync();
-        apply_lt(NT - 1);
-        load(std::integral_constant<int, 0>{}, NT - 1);
-        load(std::integral_constant<int, 1>{}, NT - 2);
-        lds_barrier();
-        for (int R = NT - 1; R >= 1; R -= 2) {
-            step(std::integral_constant<int, 0>{}, R);
-            if (R - 1 >= 1) step(std::integral_constant<int, 1>{}, R - 1);
-        }
-    } else if (!aborted) {
-        double4_t pf[2][kPf][4];
-        auto load = [&](auto setc, int R) {   // the first tiles of this wave's share of row R
-            constexpr int S = decltype(setc)::value;
-            if (R >= 2) {
-                const int j0 = rfl[R] + (wid - 1);
-#pragma unroll
-                for (int u = 0; u < kPf; u++)
-                    if (j0 + 3 * u <= R - 2) {
-#pragma unroll
-                        for (int qd = 0; qd < 4; qd++) pf[S][u][qd] = qload(rs, L.oL + (R * NT + j0 + 3 * u) * kTD + qd * 256);
+            if (!good && lane == 0) __hip_atomic_store(bab, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if (!aborted) {
+            const int own = wid - 1;
+            // the largest j <= R - 2 of this wave's residue class
+            auto jtop = [&](int R) { const int j = R - 2; return j - ((j - own) % 3 + 3) % 3; };
+            // (R, j) moved to this wave's next tile in processing order: by urgency, i.e. columns
+            // down (s_j is needed at step j + 1), rows down within a column (x_R appears in that
+            // order); j < 0: none left. Tile (NT-1, NT-3) (the last interval's, no copy) is taken
+            // first, from LDS
+            auto norm = [&](int& R, int& j) {
+                for (;;) {
+                    if (j < 0) return;
+                    if (R >= j + 2) {
+                        if (!(R == NT - 1 && j == NT - 3) && rfl[R] <= j) return;
+                        R--;
+                        continue;
                     }
-            }
-        };
-        auto step = [&](auto setc, int R) {   // s_j -= L(R, j)^T x_R over this wave's share of row R
-            constexpr int S = decltype(setc)::value;
-            const double* xR = xs + R * kT;
-            if (R >= 2) {
-                const int j0 = rfl[R] + (wid - 1);
-#pragma unroll
-                for (int u = 0; u < kPf; u++) {
-                    const int j = j0 + 3 * u;
-                    if (j > R - 2) break;
-                    sub_tile(pf[S][u], xR, j);
+                    j -= 3;
+                    R = NT - 1;
                 }
-                for (int jb = j0 + 3 * kPf; jb <= R - 2; jb += 3) {
-                    double4_t tl[4];
+            };
+            // Flags: the full tiles (helpers, copies stored before the tile's flag) were consumed by
+            // the forward, which is over; the special tile (NT-1, NT-3) is read from this
+            // work-group's LDS; the copy tiles (R, R-2), R <= NT-2,
+            // wait for wave 0's poll of the copy tasks' flags (cpok) before their loads are issued.
+            bool good = true;
+            auto applied = [&](int j) {   // one more row in s_j (this wave is its only writer)
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                if (lane == 0)
+                    __hip_atomic_store(cnt + j, cnt[j] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            };
+            if (NT >= 3 && (NT - 3) % 3 == own && rfl[NT - 1] <= NT - 3) {
+                // L(NT-1, NT-3) is still in the last interval's L2 buffer (wave 1 published it from there)
+                const double* L2last = lds + 4096 + 1024 * (NT & 1);
+                const double4_t tl[4] = {lq(L2last), lq(L2last + 256), lq(L2last + 512), lq(L2last + 768)};
+                good = lwait(xcnt, 1);
+                if (good) {
+                    double t[2][4];
+                    tile_lt_x(tl, xs + (NT - 1) * kT, t);
+                    if (cc == 0) {
 #pragma unroll
-                    for (int qd = 0; qd < 4; qd++) tl[qd] = qload(rs, L.oL + (R * NT + jb) * kTD + qd * 256);
-                    sub_tile(tl, xR, jb);
+                        for (int b = 0; b < 2; b++)
+#pragma unroll
+                            for (int q = 0; q < 4; q++) ys[(NT - 3) * kT + 16 * b + rg + 4 * q] -= t[b][q];
+                    }
+                    applied(NT - 3);
                 }
             }
-            load(setc, R - 2);   // row R-2's first tiles into this set
-            if (dbg && wid == 1 && lane == 0 && R < kDbgBackR)
-                dbg[kDbgBackOff + 3 * R + 2] = __builtin_amdgcn_s_memtime() - t_fwd;
-            lds_barrier();
-        };
-        load(std::integral_constant<int, 0>{}, NT - 1);
-        load(std::integral_constant<int, 1>{}, NT - 2);
-        lds_barrier();
-        for (int R = NT - 1; R >= 1; R -= 2) {
-            step(std::integral_constant<int, 0>{}, R);
-            if (R - 1 >= 1) step(std::integral_constant<int, 1>{}, R - 1);
+            if (good) {
+                double v[2][16];
+                int Ra = NT - 1, ja = jtop(NT - 1);
+                norm(Ra, ja);
+                int Rb = Ra - 1, jb = ja;
+                norm(Rb, jb);
+                bool cp = false;   // cpok seen
+                auto load = [&](auto setc, int R, int j) {
+                    constexpr int S = decltype(setc)::value;
+                    if (j < 0) return;
+                    if (j == R - 2 && !cp) cp = good = good && lwait(cpok, 1);
+                    if (good) cmload(rs, L.oCM + (R * NT + j) * kTD, v[S]);
+                };
+                auto apply = [&](auto setc, int R, int j) -> bool {   // s_j -= L(R, j)^T x_R
+                    constexpr int S = decltype(setc)::value;
+                    if (!lwait(xcnt, NT - R)) return false;
+                    const double p = bwd_col_dot(v[S], xs + R * kT);
+                    if (hh == 0) ys[j * kT + c] -= p;
+                    applied(j);
+                    return true;
+                };
+                load(std::integral_constant<int, 0>{}, Ra, ja);
+                load(std::integral_constant<int, 1>{}, Rb, jb);
+                while (ja >= 0 && good) {
+                    int Rn = Rb - 1, jn = jb;
+                    norm(Rn, jn);
+                    good = apply(std::integral_constant<int, 0>{}, Ra, ja);
+                    load(std::integral_constant<int, 0>{}, Rn, jn);
+                    Ra = Rb; ja = jb; Rb = Rn; jb = jn;
+                    if (ja < 0 || !good) break;
+                    Rn = Rb - 1; jn = jb;
+                    norm(Rn, jn);
+                    good = apply(std::integral_constant<int, 1>{}, Ra, ja);
+                    load(std::integral_constant<int, 1>{}, Rn, jn);
+                    Ra = Rb; ja = jb; Rb = Rn; jb = jn;
+                }
+            }
+            if (!good && lane == 0) __hip_atomic_store(bab, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-    }
-#endif
+        __syncthreads();
+        if (*bab) aborted = true;
     }
     if (wid == 0 && lane == 0) word[8] = (ok && !aborted) ? 1 : 0;
     __syncthreads();
@@ -1461,7 +1380,7 @@ __device__ __forceinline__ void dag_run(const DagK& a, int role) {
     const Lay L(a);
     // epoch of this solve: the counter the last workgroup of the previous solve advanced
     const int epoch = ld_flag(L.ctl) + 1;
-    const size_t bytes = ((size_t)a.NT * a.NT + 4 * (size_t)a.NT) * kTD * 8 + (size_t)a.NT * 4 * kT * 8;
+    const size_t bytes = dag_doubles_nt(a.NT) * 8;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.buf, 0, (int)bytes, 0x00020000);
     if (role == 0) dag_chain<DBG>(a, L, rs, epoch, lds);
     else dag_helper(a, L, rs, epoch, lds, role - 1);
@@ -1607,13 +1526,10 @@ unsigned dag_spin_max() {
     return v > 0 ? (unsigned)v : kSpinMax;
 }
 
-size_t dag_doubles(int n) {
-    const size_t NT = (n + kT - 1) / kT;
-    return (NT * NT + 4 * NT) * kTD + NT * 4 * kT;
-}
+size_t dag_doubles(int n) { return dag_doubles_nt((n + kT - 1) / kT); }
 size_t dag_ints(int n) {
     const size_t NT = (n + kT - 1) / kT;
-    return (4 + NT * NT + 6 * NT + 3) & ~size_t(3);
+    return (4 + NT * NT + 7 * NT + 3) & ~size_t(3);
 }
 
 void dag_plan(const int* rf, int n, int max_helpers, DagPlan& p, int nti) {
@@ -1642,11 +1558,6 @@ void dag_plan(const int* rf, int n, int max_helpers, DagPlan& p, int nti) {
                 ts.push_back({20 * C + 7, R, C});                                                  // full tile
             }
         }
-    std::sort(ts.begin(), ts.end(), [](const Task& x, const Task& y) {
-        return x.key != y.key ? x.key < y.key : (x.R != y.R ? x.R < y.R : x.C < y.C);
-    });
-    const int G = std::min<int>(std::max(1, max_helpers), (int)ts.size());
-    p.G = G;
     // backward substitution: over the helpers when the rows are long (the chain's own waves would
     // stream every tile of L through one CU: dense n = 2394 1.24 -> 0.69 ms), in the chain when
     // they are short (a band: the helpers' hand-off per step costs more than the tiles; the C5
@@ -1658,6 +1569,17 @@ void dag_plan(const int* rf, int n, int max_helpers, DagPlan& p, int nti) {
         p.pb = e ? (e[0] == '1' ? 1 : 0) : (off >= 10LL * NT ? 1 : 0);
         if (nti) p.pb = 0;   // a partial solve has no backward substitution
     }
+    // the chain's backward reads column-major copies: the full tiles' helper tasks write theirs, a
+    // copy task per interval k <= NT - 3 those of the chain's own tiles (L(k+1, k), L(k+1, k-1),
+    // Linv_k; the last interval's stay in the chain's LDS / are read in the quadrant layout). Key
+    // 20k + 7: after the interval's publish (20k + 6); nothing but the backward waits on them
+    if (!p.pb && !nti)
+        for (int k = 0; k <= NT - 3; k++) ts.push_back({20 * k + 7, kCopyTask, k});
+    std::sort(ts.begin(), ts.end(), [](const Task& x, const Task& y) {
+        return x.key != y.key ? x.key < y.key : (x.R != y.R ? x.R < y.R : x.C < y.C);
+    });
+    const int G = std::min<int>(std::max(1, max_helpers), (int)ts.size());
+    p.G = G;
     p.toff.assign(G + 1, 0);
     p.tasks.resize(ts.size());
     std::vector<int> cnt(G, 0);

@@ -154,6 +154,11 @@ __device__ __forceinline__ void tile_red_store(double (&p)[2][4], double* out) {
 
 constexpr int kBsM = 2;   // tiles per wave and step held in registers (more are loaded in the step)
 constexpr size_t kBsMaxLds = 128 * 1024;   // (below the 160 KB of a CU: the kernel has static LDS too)
+// dynamic LDS of k_nd_backsolve for segments of at most maxNT tiles (the layout below): the
+// planner keeps every segment within kBsMaxLds (84 tiles), nd_setup checks it again
+constexpr size_t bs_lds_bytes(int maxNT) {
+    return sizeof(double) * ((size_t)6 * maxNT * kDagTile + 5 * kDagTile) + sizeof(int) * (size_t)maxNT;
+}
 
 __global__ __launch_bounds__(256) void k_nd_backsolve(NdDev d) {
     if (d.gate && *d.gate != kPhTrial) return;
@@ -407,6 +412,10 @@ int nd_levels() {
 // separators become interiors, the odd ones the separators of the separator system
 bool nd_inner_plan(int nsep, int w, NdPlan& p) {
     if (nsep < 6 || 6 * w <= kT) return false;   // (interiors of one separator: more than one tile)
+    // its longest segment (three separators' interior when nsep is odd, plus two separators) must
+    // fit the back-substitution's LDS; otherwise the separator system is solved densely
+    if (bs_lds_bytes((kT * ((6 * w * (nsep % 2 ? 2 : 1) + kT - 1) / kT) + 12 * w + kT - 1) / kT) > kBsMaxLds)
+        return false;
     const int K2 = nsep / 2;
     p = NdPlan{};
     p.np = nsep * w; p.K = K2; p.w = w; p.cyclic = true;
@@ -429,7 +438,12 @@ int plan_cost(int np, int w, bool cyc, int k, std::vector<int>& seg) {
         // than one tile (the partial DAG solve's chain forms two tile rows past its last interval)
         if (ni < w || 6 * ni <= kT) return -1;
         mi = std::max(mi, tiles(6 * ni));
+        // the segment's matrix (interior padded to tiles + its two separators) must fit the
+        // back-substitution's LDS (nd_setup: segment tiles NT)
+        const int nseg = kT * tiles(6 * ni) + 6 * w * ((cyc || r > 0 ? 1 : 0) + (own ? 1 : 0));
+        if (bs_lds_bytes(tiles(nseg)) > kBsMaxLds) return -1;
     }
+    if (6 * w * nsep > kDagMaxN) return -1;   // the separator system on one DAG solve (nd_setup)
     int sep = tiles(6 * w * nsep);
     if (cyc && nd_levels() > 1 && nsep >= 6 && 6 * w > kT)   // the separator system dissected once more
         sep = std::min(sep, tiles(6 * w * (nsep % 2 ? 2 : 1)) + tiles(6 * w * (nsep / 2)) + 3);
@@ -682,7 +696,7 @@ int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int 
     int maxNT = 0;
     for (int r = 0; r < K; r++)
         if (loc[r] >= 0) maxNT = std::max(maxNT, sg[r].NT);
-    W->bs_lds = sizeof(double) * ((size_t)6 * maxNT * kT + 5 * kT) + sizeof(int) * (size_t)maxNT;
+    W->bs_lds = bs_lds_bytes(maxNT);
     if (W->bs_lds > kBsMaxLds) return -5;   // a segment too long for the back-substitution's LDS
     // shard of a distributed solve: the packed separator envelope and the x buffers
     d.x_loc = nullptr;
@@ -782,8 +796,10 @@ int nd_test(const double* A, const double* b, double* x, int np, const int* bi, 
     NdPlan P;
     if (!nd_plan(np, bi, bj, nblk, K, P)) return -5;
     if (K_used) *K_used = P.K;
-    if (seg_out)   // segment starts (pose index), K + 1 entries, and the band's half-width last
-        for (int r = 0; r <= P.K; r++) seg_out[r] = (int)((long long)r * np / P.K);
+    if (seg_out) {   // the plan's segment starts (pose index), K + 1 entries, then the band's half-width
+        for (int r = 0; r <= P.K; r++) seg_out[r] = P.seg[r];
+        seg_out[P.K + 1] = P.w;
+    }
     const int n = 6 * np;
     double *dA = nullptr, *db = nullptr, *dx = nullptr;
     int* dflag = nullptr;

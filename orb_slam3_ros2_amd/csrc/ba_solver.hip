@@ -329,6 +329,55 @@ __device__ __forceinline__ double lin_point(const BaArgs& a, int m, bool fresh =
     for (int r = 0; r < 3; r++) a.b[a.n + 3 * m + r] = bl[r];
     return fmax(fmax(fabs(H[0]), fabs(H[4])), fabs(H[8]));
 }
+// the same with four lanes per landmark (k_ba_lin, r06): lane sub takes edges sub, sub + 4, ...
+// of landmark m, the 12 sums are added over the quad (butterfly: the same bits in its lanes) and
+// lane 0 stores them; returns the largest |diagonal| of Hll in every lane of the quad
+constexpr int kLinL = 64;   // landmarks per workgroup of k_ba_lin
+__device__ __forceinline__ double lin_point_quad(const BaArgs& a, int m, int sub, bool fresh) {
+    if (m >= a.M) return 0.0;
+    double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};
+    for (int k = a.pt_ptr[m] + sub; k < a.pt_ptr[m + 1]; k += 4) {
+        const int e = a.pt_edges[k];
+        double x, y, z, R[9], j[4], A[6], B[12];
+        edge_pc(a, e, x, y, z, R);
+        proj_jac(a.fx, a.fy, x, y, z, j);
+        jac_ab(j, x, y, z, R, A, B);
+        double r1, er0, er1;
+        if (fresh) {   // uniform
+            double chi2, r0;
+            edge_terms(a, e, x, y, z, er0, er1, chi2, r0, r1);
+            store_terms(a, e, er0, er1, chi2, r0, r1);
+        } else {
+            r1 = a.e_rho1[e];
+            er0 = a.e_err[2 * e];
+            er1 = a.e_err[2 * e + 1];
+        }
+        const double info = a.e_info[e];
+        const double w = r1 * info;
+        const double om0 = -info * er0 * r1, om1 = -info * er1 * r1;
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            bl[r] += A[r] * om0 + A[3 + r] * om1;
+#pragma unroll
+            for (int c = 0; c < 3; c++) H[3 * r + c] += w * (A[r] * A[c] + A[3 + r] * A[3 + c]);
+        }
+        ((double4*)a.e_lin)[e] = make_double4(x, y, z, w);
+    }
+#pragma unroll
+    for (int o = 1; o <= 2; o <<= 1) {
+#pragma unroll
+        for (int i = 0; i < 9; i++) H[i] += __shfl_xor(H[i], o, 64);
+#pragma unroll
+        for (int r = 0; r < 3; r++) bl[r] += __shfl_xor(bl[r], o, 64);
+    }
+    if (sub == 0) {
+#pragma unroll
+        for (int i = 0; i < 9; i++) a.Hll[9 * m + i] = H[i];
+#pragma unroll
+        for (int r = 0; r < 3; r++) a.b[a.n + 3 * m + r] = bl[r];
+    }
+    return fmax(fmax(fabs(H[0]), fabs(H[4])), fabs(H[8]));
+}
 __global__ __launch_bounds__(256) void k_ba_lin_points(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
     BA_PHASE(kPhBuild)
@@ -428,8 +477,8 @@ __global__ __launch_bounds__(256) void k_ba_lin_poses(const BaArgs* __restrict__
     (void)lin_pose(a, bx_ * 4 + (threadIdx.x >> 6), threadIdx.x & 63);
 }
 
-// the device-driven build in one launch: workgroups [0, nbp) linearise landmarks (one per
-// thread), the rest poses (one per wave); each stores its largest |diagonal| (sc1), and the
+// the device-driven build in one launch: workgroups [0, nbp) linearise landmarks (kLinL each,
+// four lanes per landmark), the rest poses (one per wave); each stores its largest |diagonal| (sc1), and the
 // problem's last workgroup runs the controller's trial start (ctl_begin_body: lambda from the
 // maxima on the first iteration)
 __global__ __launch_bounds__(256) void k_ba_lin(const BaArgs* __restrict__ args, const int* __restrict__ act,
@@ -438,14 +487,14 @@ __global__ __launch_bounds__(256) void k_ba_lin(const BaArgs* __restrict__ args,
     BA_PHASE(kPhBuild)
     __shared__ double sh[4];
     __shared__ int lastf;
-    const int mP = (a.M + 255) / 256, nP = (a.np + 3) / 4;
+    const int mP = (a.M + kLinL - 1) / kLinL, nP = (a.np + 3) / 4;
     // a small problem whose iteration ended on a rejected trial: its stored errors are the trial's,
     // so this build takes them from the restored state (the larger problems' k_ba_errors(1) did)
     const bool fresh = a.small && a.ctl && !a.ctl->errors_valid;
     double d;
     int slot;
     if (bx_ < nbp) {
-        d = lin_point(a, bx_ * blockDim.x + threadIdx.x, fresh);
+        d = lin_point_quad(a, bx_ * kLinL + (threadIdx.x >> 2), threadIdx.x & 3, fresh);
         slot = bx_ < mP ? bx_ : -1;
     } else {
         const int q = bx_ - nbp;
@@ -982,26 +1031,51 @@ __global__ __launch_bounds__(256) void k_ba_backsub(const BaArgs* __restrict__ a
     __shared__ double sh[4];
     const double t = block_sum(m < a.M ? backsub_point(a, m) : 0.0, sh);
     if (threadIdx.x == 0) a.part[a.npart_e + bx_] = t;
+    if (bx_ == 0)   // the scale slots past this launch's workgroups (npart_m counts k_ba_backsub_errs')
+        for (int i = (max(a.M, a.P) + 255) / 256 + (int)threadIdx.x; i < a.npart_m; i += blockDim.x)
+            a.part[a.npart_e + i] = 0.0;
 }
 
 // small problems (BaArgs::fused): the back-substitution and the trial's errors in ONE launch, no
 // k_ba_errors(2) after it. The trial's poses go to pose_bak (pose keeps the accepted state until
 // the controller commits). Every workgroup forms all P new poses in LDS (P <= kFusedMaxP: a few
-// se3 updates per thread), back-substitutes its 256 landmarks (new points in LDS too), then takes
-// the errors of those landmarks' edges, spread over its threads. chi2 and the landmark scale terms
-// leave as workgroup partials and the problem's last workgroup runs the controller step
-// (ctl_end_body: commit the poses or take the points back)
+// se3 updates per thread, overlapping its landmark loads) and takes kBsL landmarks, four lanes per
+// landmark (r06; one thread per landmark and 256 per workgroup before: 8 workgroups at C4): the
+// lanes split the landmark's edges for Hpl^T xp (summed over the quad), each forms the new point
+// (the same bits in all four) and then the errors of its own edges with it. chi2 and the landmark
+// scale terms leave as workgroup partials and the problem's last workgroup runs the controller
+// step (ctl_end_body: commit the poses or take the points back)
 constexpr int kFusedMaxP = 512;
+constexpr int kBsL = 64;   // landmarks per workgroup of k_ba_backsub_errs
 __global__ __launch_bounds__(256) void k_ba_backsub_errs(const BaArgs* __restrict__ args, const int* __restrict__ act,
                                                          int* const* donep) {
     BA_PROLOGUE
     int* const done = done_of(donep);
     BA_PHASE(kPhTrial)
     __shared__ double Tn[8 * kFusedMaxP];   // the trial's poses
-    __shared__ double Xn[3 * 256];          // this workgroup's new points
     __shared__ double sh[4];
     __shared__ int lastf;
-    const int nwg = (max(a.M, a.P) + 255) / 256;   // this problem's partial slots (<= npart_e: host-checked)
+    const int nwg = (max(a.M, a.P) + kBsL - 1) / kBsL;   // this problem's partial slots (<= npart_e, npart_m)
+    const int m = bx_ * kBsL + (threadIdx.x >> 2), sub = threadIdx.x & 3;
+    // this lane's edges of landmark m: its back-substitution terms (their loads go out first)
+    int k0 = 0, k1 = 0;
+    if (m < a.M) { k0 = a.pt_ptr[m]; k1 = a.pt_ptr[m + 1]; }
+    double c0 = 0.0, c1 = 0.0, c2 = 0.0;   // - sum_e Hpl_e^T xp over this lane's edges
+    for (int k = k0 + sub; k < k1; k += 4) {
+        const int e = a.pt_edges[k];
+        const int oi = a.opt[a.e_pose[e]];
+        if (oi < 0) continue;
+        double A[6], B[12];
+        const double w = lin_ab(a, e, oi, A, B);   // Hpl_e^T xp = w A^T (B xp)
+        const double* xp = a.x + 6 * oi;
+        double u0 = 0.0, u1 = 0.0;
+#pragma unroll
+        for (int r = 0; r < 6; r++) { u0 += B[r] * xp[r]; u1 += B[6 + r] * xp[r]; }
+        u0 *= w; u1 *= w;
+        c0 -= A[0] * u0 + A[3] * u1;
+        c1 -= A[1] * u0 + A[4] * u1;
+        c2 -= A[2] * u0 + A[5] * u1;
+    }
     for (int p = threadIdx.x; p < a.P; p += blockDim.x) {
         double T[8];
 #pragma unroll
@@ -1015,21 +1089,37 @@ __global__ __launch_bounds__(256) void k_ba_backsub_errs(const BaArgs* __restric
             for (int k = 0; k < 8; k++) st_agent(a.pose_bak + 8 * p + k, T[k]);
         }
     }
-    const int m0 = bx_ * 256, m = m0 + threadIdx.x;
-    double sc = 0.0;
-    if (m < a.M) {
-        sc = backsub_point(a, m);
+    // the quad's sum (butterfly: the same bits in its four lanes)
+    c0 += __shfl_xor(c0, 1, 64); c1 += __shfl_xor(c1, 1, 64); c2 += __shfl_xor(c2, 1, 64);
+    c0 += __shfl_xor(c0, 2, 64); c1 += __shfl_xor(c1, 2, 64); c2 += __shfl_xor(c2, 2, 64);
+    double sc = 0.0, Xn[3] = {0.0, 0.0, 0.0};
+    if (m < a.M) {   // xl = Dinv (b_l - Hpl^T xp), X += xl (old X saved): every lane of the quad
+        const double* bl = a.b + a.n + 3 * m;
+        const double cv[3] = {bl[0] + c0, bl[1] + c1, bl[2] + c2};
+        double Di[9];
+        dinv_of(a, m, Di);
+        double* X = a.pts + 3 * m;
+        const double lambda = *a.lambda;
 #pragma unroll
-        for (int r = 0; r < 3; r++) Xn[3 * threadIdx.x + r] = a.pts[3 * m + r];
-    }
-    __syncthreads();
-    double chi = 0.0;
-    if (m0 < a.M) {
-        const int k0 = a.pt_ptr[m0], k1 = a.pt_ptr[min(m0 + 256, a.M)];
-        for (int k = k0 + (int)threadIdx.x; k < k1; k += blockDim.x) {
-            const int e = a.pt_edges[k];
-            chi += edge_error_at(a, e, Tn + 8 * a.e_pose[e], Xn + 3 * (a.e_pt[e] - m0));
+        for (int r = 0; r < 3; r++) {
+            const double xl = Di[3 * r] * cv[0] + Di[3 * r + 1] * cv[1] + Di[3 * r + 2] * cv[2];
+            const double xo = X[r];
+            Xn[r] = xo + xl;
+            if (sub == 0) {
+                a.x[a.n + 3 * m + r] = xl;
+                // sc1 for a small problem: its trial's last workgroup may restore pts from pts_bak
+                // in this launch (ctl_end_body)
+                st_agent(a.pts_bak + 3 * m + r, xo);
+                st_agent(X + r, Xn[r]);
+                sc += xl * (lambda * xl + bl[r]);
+            }
         }
+    }
+    __syncthreads();   // the trial's poses in Tn
+    double chi = 0.0;
+    for (int k = k0 + sub; k < k1; k += 4) {
+        const int e = a.pt_edges[k];
+        chi += edge_error_at(a, e, Tn + 8 * a.e_pose[e], Xn);
     }
     const double tc = block_sum(chi, sh);
     const double ts = block_sum(sc, sh);
@@ -1037,8 +1127,10 @@ __global__ __launch_bounds__(256) void k_ba_backsub_errs(const BaArgs* __restric
         st_agent(a.part + bx_, tc);
         st_agent(a.part + a.npart_e + bx_, ts);
     }
-    if (bx_ == 0)   // the chi2 slots past this problem's workgroups
+    if (bx_ == 0) {   // the slots past this problem's workgroups
         for (int i = nwg + (int)threadIdx.x; i < a.npart_e; i += blockDim.x) st_agent(a.part + i, 0.0);
+        for (int i = nwg + (int)threadIdx.x; i < a.npart_m; i += blockDim.x) st_agent(a.part + a.npart_e + i, 0.0);
+    }
     if (last_arrival(&a.ctl->arrive_t, gridDim.x, &lastf)) ctl_end_body(a, act[by_], done, sh);
 }
 
@@ -1289,7 +1381,7 @@ __device__ void ctl_end_body(const BaArgs& a, int prob, int* done_flags, double*
 __global__ __launch_bounds__(256) void k_ba_sh_maxdiag(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     const BaArgs& a = args[act[blockIdx.x]];
     if (!in_phase(a, kPhBuild)) return;
-    const int mP = (a.M + 255) / 256;
+    const int mP = (a.M + kLinL - 1) / kLinL;   // k_ba_lin's landmark workgroups
     double m = 0.0;
     for (int i = threadIdx.x; i < mP; i += blockDim.x) m = fmax(m, ld_agent(a.part + i));
     for (int i = threadIdx.x; i < 6 * a.np; i += blockDim.x) m = fmax(m, fabs(a.Hpp_g[36 * (i / 6) + 7 * (i % 6)]));
@@ -1404,11 +1496,14 @@ constexpr int kPrepParallelE = 20000;   // edges from which one problem's pair l
 // for i in [0, n) on the caller and the idle workers (indices claimed dynamically, so it completes
 // on the caller alone if no worker is free), and returns when every call has returned. One run at a
 // time: a concurrent caller (another context's thread) runs its loop alone.
+// Created lazily, on the first large problem prepared with ORBHIP_PREP_THREADS > 1 (never
+// otherwise), and deliberately leaked with detached workers: no destructor runs at process exit
+// or library unload, so no join can meet a worker inside run() or a destroyed mutex.
 class HostPool {
   public:
     static HostPool& get(int workers) {
-        static HostPool pool(workers);
-        return pool;
+        static HostPool* pool = new HostPool(workers);
+        return *pool;
     }
     template <typename F>
     void run(int n, F&& fn) {
@@ -1435,17 +1530,13 @@ class HostPool {
 
   private:
     explicit HostPool(int workers) {
-        for (int w = 0; w < workers; w++) workers_.emplace_back([this] { loop(); });
-    }
-    ~HostPool() {
-        {
-            std::lock_guard<std::mutex> g(m_);
-            stop_ = true;
-            gen_++;
+        for (int w = 0; w < workers; w++) {
+            std::thread t([this] { loop(); });
+            t.detach();
+            workers_.push_back(w);
         }
-        cv_.notify_all();
-        for (auto& t : workers_) t.join();
     }
+    ~HostPool() = delete;   // leaked (see above)
     void loop() {
         unsigned long long seen = 0;
         for (;;) {
@@ -1455,7 +1546,6 @@ class HostPool {
                 std::unique_lock<std::mutex> g(m_);
                 cv_.wait(g, [&] { return gen_ != seen; });
                 seen = gen_;
-                if (stop_) return;
                 job = job_;
                 n = n_;
             }
@@ -1465,14 +1555,13 @@ class HostPool {
             if (--active_ == 0) done_cv_.notify_one();
         }
     }
-    std::vector<std::thread> workers_;
+    std::vector<int> workers_;   // the detached workers' indices (their count is what run() uses)
     std::mutex run_m_, m_;
     std::condition_variable cv_, done_cv_;
     std::function<void(int)>* job_ = nullptr;
     int n_ = 0, active_ = 0;
     std::atomic<int> next_{0};
     unsigned long long gen_ = 0;
-    bool stop_ = false;
 };
 
 // The Schur pair lists of prepare() on host threads, identical to the serial build:
@@ -1839,7 +1928,7 @@ struct LmState {
 };
 
 int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B, orbhip_ba_result* const* res,
-                   const volatile int* stop, hipStream_t st, int shard_mode, bool no_dag) {
+                   const volatile int* stop, hipStream_t st, int shard_mode, bool no_dag, bool no_nd) {
     if (B <= 0 || !probs || !res) return ORBHIP_ERR_ARG;
     // RCCL: this rank holds B consecutive shards (segments rank*B .. rank*B+B-1 of nranks*B), the
     // same B on every rank; the shards of one rank are summed on the device before the all-reduce
@@ -1866,11 +1955,23 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     static const int prep_par = std::getenv("ORBHIP_PREP_THREADS") ? std::atoi(std::getenv("ORBHIP_PREP_THREADS")) : 1;
     parallel_for(B, nth, [&](int b) { pp[b].rc = prepare(probs[b], pp[b], chunk, B == 1 ? prep_par : 1); });
     const double t_prepare = now();
-    for (int b = 0; b < B; b++)
-        if (pp[b].rc) return pp[b].rc;
-    if (shard_mode != kShardNone && B > 1) {
-        for (int b = 1; b < B; b++)
-            if (pp[b].P != pp[0].P || pp[b].np != pp[0].np) return ORBHIP_ERR_ARG;
+    // RCCL shards: a rank whose shards are invalid must not return before the first collective
+    // (the other ranks would wait in it forever); its verdict travels in that all-reduce and every
+    // rank returns together
+    int local_bad = 0;
+    for (int b = 0; b < B && !local_bad; b++)
+        if (pp[b].rc) {
+            if (shard_mode != kShardRccl) return pp[b].rc;
+            local_bad = pp[b].rc;
+        }
+    if (shard_mode != kShardNone && B > 1 && !local_bad) {
+        for (int b = 1; b < B && !local_bad; b++)
+            if (pp[b].P != pp[0].P || pp[b].np != pp[0].np) {
+                if (shard_mode != kShardRccl) return ORBHIP_ERR_ARG;
+                local_bad = ORBHIP_ERR_ARG;
+            }
+    }
+    if (shard_mode != kShardNone && B > 1 && !local_bad) {
         // every shard factors the SUMMED S: the blocked Cholesky needs the union envelope
         for (int b = 1; b < B; b++)
             for (size_t R = 0; R < pp[0].row_first.size(); R++)
@@ -1894,7 +1995,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         const char* e_k = std::getenv("ORBHIP_ND_K");
         const char* e_min = std::getenv("ORBHIP_ND_MIN");
         const int nd_min = e_min ? std::atoi(e_min) : 960;
-        if (shard_mode == kShardNone && B == 1 && pp[0].use_dag && pp[0].n >= nd_min && !(e_nd && e_nd[0] == '0')) {
+        if (shard_mode == kShardNone && B == 1 && !no_nd && pp[0].use_dag && pp[0].n >= nd_min &&
+            !(e_nd && e_nd[0] == '0')) {
             Prep& p = pp[0];
             if (nd_plan(p.np, p.blk_i.data(), p.blk_j.data(), p.nblk, e_k ? std::atoi(e_k) : 0, p.nd)) {
                 p.use_nd = true;
@@ -1917,7 +2019,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         const int nd_min = e_min ? std::atoi(e_min) : 960;
         const int K = shard_mode == kShardLocal ? B : ws->nranks * B;
         int wl = 0, wc = 0;
-        for (int b = 0; b < B; b++) {
+        for (int b = 0; b < B && !local_bad; b++) {
             int l = 0, c = 0;
             nd_bandwidth(pp[b].np, pp[b].blk_i.data(), pp[b].blk_j.data(), pp[b].nblk, l, c);
             wl = std::max(wl, l);
@@ -1925,13 +2027,16 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         }
         int ok = (!no_dag && !force_blocked && !(e_snd && e_snd[0] == '0') && pp[0].n >= nd_min) ? 1 : 0;
         if (shard_mode == kShardRccl) {   // the band over every rank's landmarks; the same B everywhere
-            ws->h_int4[0] = wl; ws->h_int4[1] = wc; ws->h_int4[2] = -ok; ws->h_int4[3] = B; ws->h_int4[4] = -B;
+            // words 3 / 4: the max of B and of -B agree only when every rank has the same B and
+            // valid shards (an invalid rank sends INT_MAX)
+            ws->h_int4[0] = wl; ws->h_int4[1] = wc; ws->h_int4[2] = -ok;
+            ws->h_int4[3] = local_bad ? std::numeric_limits<int>::max() : B; ws->h_int4[4] = -B;
             if (hipMemcpyAsync(ws->dint4.p, ws->h_int4, 5 * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
                 ncclAllReduce(ws->dint4.p, ws->dint4.p, 5, ncclInt32, ncclMax, ws->comm, st) != ncclSuccess ||
                 hipMemcpyAsync(ws->h_int4, ws->dint4.p, 5 * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess)
                 return ORBHIP_ERR_DEVICE;
-            if (ws->h_int4[3] != B || -ws->h_int4[4] != B) return ORBHIP_ERR_ARG;
+            if (ws->h_int4[3] != B || -ws->h_int4[4] != B) return local_bad ? local_bad : ORBHIP_ERR_ARG;
             wl = ws->h_int4[0]; wc = ws->h_int4[1]; ok = -ws->h_int4[2];
         }
         ok = ok && nd_plan_band(pp[0].np, wl, wc, K, ndp);
@@ -1967,7 +2072,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         } else if (p.use_dag) {
             if (shard_mode == kShardRccl) {
                 const size_t NT = (p.n + kDagTile - 1) / kDagTile;
-                p.dag_task_cap = (size_t)dag_helpers + 1 + NT * (NT + 1) / 2;
+                p.dag_task_cap = (size_t)dag_helpers + 1 + NT * (NT + 1) / 2 + NT;   // + the copy tasks
             } else {
                 dag_plan(p.row_first.data(), p.n, dag_helpers, p.dag);
                 p.dag_task_cap = p.dag.toff.size() + p.dag.tasks.size();
@@ -2004,7 +2109,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         nR = (nR + 1) & ~size_t(1);
         p.o_part = nR; nR += 36 * (size_t)p.nslot;
         p.o_red2 = nR;
-        nR += std::max((E + 255) / 256 + (std::max(M, P) + 255) / 256, (M + 255) / 256 + (np_ + 3) / 4) + 2;
+        nR += std::max((E + 255) / 256 + (std::max(M, P) + kBsL - 1) / kBsL, (M + kLinL - 1) / kLinL + (np_ + 3) / 4) + 2;
         if (p.use_dag) {   // 128-byte aligned
             nR = (nR + 15) & ~size_t(15);
             p.o_dag = nR; nR += dag_doubles(p.n);
@@ -2140,7 +2245,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.Spart = D + sR + p.o_part;
         a.part = D + sR + p.o_red2;
         a.npart_e = (int)((E + 255) / 256);
-        a.npart_m = (int)((M + 255) / 256);
+        a.npart_m = (int)((std::max(M, (size_t)P) + kBsL - 1) / kBsL);   // k_ba_backsub_errs' workgroups
         if (p.use_dag) dd[b].buf = D + sR + p.o_dag;
         a.lambda = ws->lam.p + b;
         a.lead = shard_mode == kShardLocal ? (b == 0) : (shard_mode == kShardRccl ? (ws->rank == 0 && b == 0) : 1);
@@ -2274,9 +2379,16 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         for (int b = 0; b < B; b++)
             if (pp[b].use_nd) {
                 if (!ws->nd) ws->nd = nd_create();
-                if (nd_setup(ws->nd, pp[b].nd, pp[b].blk_i.data(), pp[b].blk_j.data(), pp[b].nblk, ha[b].S, ha[b].bs,
-                             ha[b].x, ha[b].flag, &dctl[b].phase, st) != 0)
-                    return ORBHIP_ERR_DEVICE;
+                const int rc = nd_setup(ws->nd, pp[b].nd, pp[b].blk_i.data(), pp[b].blk_j.data(), pp[b].nblk, ha[b].S,
+                                        ha[b].bs, ha[b].x, ha[b].flag, &dctl[b].phase, st);
+                // a plan the device setup refuses (a segment beyond the back-substitution's LDS, a
+                // separator system beyond the DAG solver; the planner rejects both, so this is a
+                // guard): the same problem again on the plain DAG solve, nothing was run yet
+                if (rc == -5) {
+                    if (hipStreamSynchronize(st) != hipSuccess) return ORBHIP_ERR_DEVICE;
+                    return ba_solve_batch(ws, probs, B, res, stop, st, shard_mode, no_dag, true);
+                }
+                if (rc != 0) return ORBHIP_ERR_DEVICE;
             }
         if (nd_sh) {   // one segment per shard
             while (ws->nds.size() < (size_t)B) ws->nds.push_back(nd_create());
@@ -2376,7 +2488,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         for (int b = 0; b < B; b++) all_small = all_small && ha[b].small;
         // ... and takes its errors inside the back-substitution when its partial slots hold the
         // fused kernel's workgroups (ORBHIP_BA_FUSED=0 keeps the separate k_ba_errors(2))
-        const unsigned gbs = gx(std::max(maxM, maxP), 256);
+        const unsigned gbs = gx(std::max(maxM, maxP), kBsL);
         const char* fz = std::getenv("ORBHIP_BA_FUSED");   // per call: the tests compare both forms
         const bool fuse_env = !(fz && fz[0] == '0');
         bool fused = all_small && fuse_env;
@@ -2405,8 +2517,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         __atomic_store_n(ws->h_done + ws->done_cap, 0, __ATOMIC_RELAXED);
         auto slot = [&]() -> int {
             if (!all_small) hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 1, donep);
-            hipLaunchKernelGGL(k_ba_lin, dim3(gx(maxM, 256) + gx(maxNp, 4), B), b256, 0, st, dA, d_act,
-                               (int)gx(maxM, 256), donep);
+            hipLaunchKernelGGL(k_ba_lin, dim3(gx(maxM, kLinL) + gx(maxNp, 4), B), b256, 0, st, dA, d_act,
+                               (int)gx(maxM, kLinL), donep);
             if (sharded) {   // the trial start on the shards' sums: Hpp, then the largest diagonal
                 if (coll(kHpp)) return ORBHIP_ERR_DEVICE;
                 hipLaunchKernelGGL(k_ba_sh_maxdiag, dim3(B), b256, 0, st, dA, d_act);
@@ -2586,7 +2698,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             const char* e = std::getenv("ORBHIP_DAG_RERUN");
             if (no_dag || (e && e[0] == '0')) return ORBHIP_ERR_TIMEOUT;
             ws->dag_reruns++;
-            return ba_solve_batch(ws, probs, B, res, stop, st, shard_mode, true);
+            return ba_solve_batch(ws, probs, B, res, stop, st, shard_mode, true, no_nd);
         }
     }
     parallel_for(B, nth, [&](int b) {

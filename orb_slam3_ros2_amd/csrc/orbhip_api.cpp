@@ -1548,7 +1548,7 @@ int orbhip_test_nd_solve(const double* A, const double* b, double* x, int np, co
 }
 // the same, with the two halves timed alone (stage_ms[0]: interior factorizations + separator
 // assembly, stage_ms[1]: separator solve + interior back-substitution) and the plan's segment
-// starts (seg_out: K + 1 pose indices; capacity 65)
+// starts (seg_out: the plan's K + 1 pose indices, then the band's half-width; capacity 65)
 int orbhip_test_nd_stages(const double* A, const double* b, double* x, int np, const int* bi, const int* bj, int nblk,
                           int K, int reps, float* ms, int* K_used, float* stage_ms, int* seg_out) {
     if (!A || !b || !x || np <= 0 || !bi || !bj || nblk <= 0 || reps < 1 || !stage_ms || !seg_out) return ORBHIP_ERR_ARG;

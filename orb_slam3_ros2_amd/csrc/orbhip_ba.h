@@ -14,9 +14,11 @@ int ba_solve(BaWorkspace* ws, const orbhip_ba_problem* prob, orbhip_ba_result* r
 // process (device-side sum across the batch); kShardRccl = this rank's shard (B == 1), the
 // sums are RCCL all-reduces over the communicator of ba_comm_init.
 constexpr int kShardNone = 0, kShardLocal = 1, kShardRccl = 2;
-// no_dag: never the persistent DAG Cholesky (the re-run after a DAG hand-off timeout)
+// no_dag: never the persistent DAG Cholesky (the re-run after a DAG hand-off timeout); no_nd: no
+// nested dissection of a lone problem (the re-run when its device setup refuses the plan)
 int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B, orbhip_ba_result* const* res,
-                   const volatile int* stop, hipStream_t st, int shard_mode, bool no_dag = false);
+                   const volatile int* stop, hipStream_t st, int shard_mode, bool no_dag = false,
+                   bool no_nd = false);
 // DAG hand-off timeouts this workspace saw, and the solves it re-ran on the other solvers
 void ba_stats(BaWorkspace* ws, long long* timeouts, long long* reruns);
 int ba_comm_init(BaWorkspace* ws, int nranks, int rank, const void* id);

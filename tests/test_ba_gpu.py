@@ -69,8 +69,11 @@ def test_lba_with_outliers_and_several_fixed(opt, oracle):
 def test_rejected_trials_restore_across_workgroups(opt, oracle, monkeypatch, fused):
     """A single problem spread over many workgroups (3000 landmarks: 12 per launch) with gross
     outliers, so that the LM rejects trials: the problem's last workgroup restores the pushed
-    state and refreshes the errors inside the trial's launch (ctl_end_body), reading the backups
-    the other workgroups (other XCDs) stored in that same launch. Both trial forms (the fused
+    state inside the trial's launch (ctl_end_body), reading the backups the other workgroups
+    (other XCDs) stored in that same launch. When an iteration ends on a rejected trial (only a
+    non-finite trial chi2 does that: a finite rejection retries within the iteration, up to the
+    tenth, which ends the run) the restored state's errors are refreshed by the next build
+    (k_ba_lin's fresh terms), not in the trial's launch. Both trial forms (the fused
     back-substitution + errors, and k_ba_errors(2) after k_ba_backsub) equal the oracle."""
     monkeypatch.setenv("ORBHIP_BA_FUSED", fused)
     # a large initial perturbation: the oracle rejects 2 of 12 trials over optimize(10)

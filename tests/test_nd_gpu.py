@@ -86,3 +86,35 @@ def test_gba_c5_dissection_parity(c5_case, env, monkeypatch):
     assert np.abs(q(g.pose_q) - q(o["pose_q"])).max() < 1e-4
     assert np.abs(g.pose_t.astype(np.float64) - o["pose_t"]).max() / max(1.0, np.abs(o["pose_t"]).max()) < 1e-4
     assert np.abs(g.points.astype(np.float64) - o["points"]).max() / max(1.0, np.abs(o["points"]).max()) < 1e-4
+
+
+def test_nd_plan_respects_backsolve_lds():
+    """A wide cyclic band near the solver's n = 4096 limit (680 poses, half-bandwidth 114): with
+    K = 2 a segment (226-pose interior + two 114-pose separators: 86 tiles) would exceed the
+    back-substitution's 128 KB of LDS (84 tiles), so the forced plan is refused up front
+    (ORBHIP_ERR_UNSUPPORTED, no device error); the automatic plan either fits or is not made."""
+    A, b, bi, bj = banded_system(680, 114, True, seed=7)
+    rc, _, _, _ = nd_solve(A, b, 680, bi, bj, 2)
+    assert rc == -5, rc
+    rc, x, _, ku = nd_solve(A, b, 680, bi, bj, 0)
+    assert rc in (0, -5), rc
+    if rc == 0:
+        ref = np.linalg.solve(A, b)
+        assert np.abs(x - ref).max() / np.abs(ref).max() < 1e-9, ku
+
+
+def test_gba_forced_k2_on_a_wide_band_falls_back(monkeypatch):
+    """The same wide band as a GlobalBundleAdjustment (a 681-keyframe loop with a 115-keyframe
+    co-visibility window, n = 4080) with ORBHIP_ND_K=2 forced: the planner refuses the segment
+    that would not fit the back-substitution's LDS and the solve runs on the plain DAG solver;
+    it equals the solve with the dissection off (same solver, same schedule)."""
+    from orb_slam3_ros2_amd import Optimizer
+    from orb_slam3_ros2_amd.synthetic import synthetic_ba_problem
+    prob, _ = synthetic_ba_problem(n_kf=681, n_pts=6000, layout="loop", window=115, seed=17)
+    monkeypatch.setenv("ORBHIP_ND_K", "2")
+    g = Optimizer().BundleAdjustment(prob, nIterations=3, bRobust=True)
+    monkeypatch.delenv("ORBHIP_ND_K")
+    monkeypatch.setenv("ORBHIP_ND", "0")
+    r = Optimizer().BundleAdjustment(prob, nIterations=3, bRobust=True)
+    assert g.lm_trials == r.lm_trials and g.final_chi2 < g.initial_chi2
+    assert abs(g.final_chi2 - r.final_chi2) <= 1e-9 * abs(r.final_chi2)

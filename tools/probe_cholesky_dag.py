@@ -69,5 +69,5 @@ for n_s, shape in cases:
     bk = dbg[8 + 6 * 200 + 16 * 100:].reshape(128, 3).astype(np.int64)[:nb]
     if nb > 1 and bk[1:nb, 0].any():
         st = bk[1:nb]
-        print("    backward steps R (start, x formed, wave 1 done; cycles from the backward start): " +
+        print("    backward steps t (start, x_{t-1} formed, s_{t-1} complete; cycles from the backward start): " +
               " ".join(f"{R}:{a}/{b}/{c}" for R, (a, b, c) in zip(range(nb - 1, 0, -1), st[::-1][:12])), flush=True)
