@@ -652,6 +652,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     if (tid == 0) {
         word[4] = 0;
         word[5] = 1;
+        word[18] = NT < 3 ? 1 : 0;   // the backward's column copies ready (no copy task below NT = 3)
         *F1 = 0;
         *F2 = 0;
         *F3 = 0;
@@ -659,6 +660,11 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         *F5 = 0;
     }
     for (int i = tid; i < NT; i += blockDim.x) rfl[i] = a.rf[i];
+    // the chain backward's per-column counts (dag_plan: rows R >= k + 2 whose envelope reaches
+    // column k), after the helpers' task list
+    int* need = rfl + NT;
+    if (!a.pb && !a.nti)
+        for (int i = tid; i < NT; i += blockDim.x) need[i] = a.tasks[a.toff[a.G] + i];
     int c1 = 0, c2 = 0;
     // ---- prologue: wave 0 factors tile 0; T_0 = A(1, 0), D'_1 = A(1, 1), L1 = L2 = 0 ----
     sq(lds + 2048 + quad * 256, double4_t{0, 0, 0, 0});
@@ -675,11 +681,14 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     __syncthreads();
     if (wid == 0) {
         double4_t lin11, l21t;
-        ok = diag_part_a(s_quad(a, 0, 0, 0, 0), lds, lin11, lds + 10240);
+        // tile 0's three quadrants in one global round trip (part B's were loaded after part A's
+        // pivots, behind their asm blocks)
+        const double4_t q00 = s_quad(a, 0, 0, 0, 0), q10 = s_quad(a, 0, 0, 1, 0), q11 = s_quad(a, 0, 0, 1, 1);
+        ok = diag_part_a(q00, lds, lin11, lds + 10240);
         wave_lds_sync();
         const double y0 = quad_matvec(lds, 0, rvec);
         if (rg == 0) ys[cc] = y0;
-        ok = diag_part_b(s_quad(a, 0, 0, 1, 0), s_quad(a, 0, 0, 1, 1), lin11, lds, l21t, lds + 10240) && ok;
+        ok = diag_part_b(q10, q11, lin11, lds, l21t, lds + 10240) && ok;
         wave_lds_sync();
         const double r1 = rvec[16 + cc] - lmul_ylds(l21t, ys);
         wave_lds_sync();
@@ -712,31 +721,70 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         if (lane == 2) return (!zT && max(rc, ra) <= kk - 2) ? L.fP1 + kk1 : nullptr;
         return (!zD && rc <= kk2 - 4) ? L.fP0 + kk2 : nullptr;
     };
+    // every per-interval flag of interval k packed in one word (fl), every LDS buffer pointer
+    // derived from one parity word (par) where it is used: held across the role branches as separate
+    // values they exceeded the SGPR budget and were spilled / reloaded by readlanes
+    auto flags_of = [&](int k) -> unsigned {
+        const int k1 = k + 1, K2 = k + 2;
+        const bool last = a.nti && k1 >= a.nti;   // tile k+1 is in the trailing block: not factored
+        const bool zT = last, zD = a.nti && K2 >= a.nti;   // T_{k+1} / D'_{k+2}: trailing-block tiles
+        const int rfa = rfl[k1], rfb = rfl[k];
+        const bool inEnv1 = rfa <= k;
+        const bool useD2 = k - 1 >= rfa;
+        const int rfc = K2 < NT ? rfl[K2] : 0;
+        const bool inEnvU = K2 < NT && rfc <= k, inEnvT = K2 < NT && rfc <= k1;
+        const bool needP2 = K2 < NT && max(rfc, rfb) <= k - 2, useU = K2 < NT && k - 1 >= max(rfc, rfb);
+        const bool needP1 = !zT && K2 < NT && max(rfc, rfa) <= k - 2;
+        const bool useTp = !zT && K2 < NT && k - 1 >= max(rfc, rfa);
+        const bool useTk = !zT && inEnvU && inEnv1;   // T_{k+1} -= L(k+2, k) L(k+1, k)^T
+        const bool needP0 = !zD && K2 < NT && rfc <= K2 - 4;   // the helpers' diagonal partial: columns <= k-2
+        const bool useP0c = !zD && K2 < NT && k - 1 >= rfc;     // column k-1 of D'_{k+2}: applied here
+        return (unsigned)last | (unsigned)inEnv1 << 1 | (unsigned)useD2 << 2 | (unsigned)inEnvU << 3 |
+               (unsigned)inEnvT << 4 | (unsigned)needP2 << 5 | (unsigned)useU << 6 | (unsigned)needP1 << 7 |
+               (unsigned)useTp << 8 | (unsigned)useTk << 9 | (unsigned)needP0 << 10 | (unsigned)useP0c << 11;
+    };
+    // waves 2/3: the global inputs of interval kk (the helpers' partial tiles / S, the full tile
+    // L(kk+2, kk-1), the rhs partial) into the p* registers; issued at the start of interval kk, or
+    // (r06) at the end of interval kk-1 when its helpers' flags are already in (their poll goes out
+    // early in interval kk-1, behind that interval's own loads), so interval kk starts with them
+    double4_t pd0 = {0, 0, 0, 0}, pd1 = {0, 0, 0, 0}, pe0 = {0, 0, 0, 0}, pe1 = {0, 0, 0, 0};
+    double4_t pu[2] = {}, pt[2] = {}, pdd[2] = {};
+    double prr = 0.0;
+    bool pre = false;
+    auto fetch_in = [&](int kk, unsigned flk) {
+        const int h = wid - 2, kk1 = kk + 1, KK2 = kk + 2;
+        auto F = [&](int b) { return ((flk >> b) & 1u) != 0u; };
+        const int tD = L.oL + (KK2 * NT + kk - 1) * kTD;
+        pd0 = pd1 = pe0 = pe1 = double4_t{0, 0, 0, 0};
+        if (F(6) || F(8) || F(11)) {   // useU || useTp || useP0c
+            pd0 = qload(rs, tD + (2 * h) * 256);
+            pd1 = qload(rs, tD + (2 * h + 1) * 256);
+        }
+        // quadrant (1, 0) of D'_{kk+2} needs both row halves of L(kk+2, kk-1): wave 3, which forms
+        // that term, loads the other half
+        if (F(11) && h == 1) {
+            pe0 = qload(rs, tD);
+            pe1 = qload(rs, tD + 256);
+        }
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            pu[c] = !F(3) ? double4_t{0, 0, 0, 0}
+                          : (F(5) ? qload(rs, L.oP + (2 * NT + kk) * kTD + (2 * h + c) * 256) : s_quad(a, KK2, kk, h, c));
+            pt[c] = !F(4) ? double4_t{0, 0, 0, 0}
+                          : (F(7) ? qload(rs, L.oP + (NT + kk1) * kTD + (2 * h + c) * 256) : s_quad(a, KK2, kk1, h, c));
+            const int qd = 2 * h + c;   // D' quadrants: wave 2 q0, wave 3 q2 and q3
+            pdd[c] = (h == 0 && c == 1) ? double4_t{0, 0, 0, 0}
+                                        : (F(10) ? qload(rs, L.oP + KK2 * kTD + qd * 256) : s_quad(a, KK2, KK2, qd >> 1, qd & 1));
+        }
+        prr = F(10) ? ld_sc1(a.buf + L.oR + KK2 * kT + 16 * h + cc) : s_rhs(a, kT * KK2 + 16 * h + cc);
+    };
     for (int k = 0; k < kEnd; k++) {
         const unsigned long long tk = dbg ? __builtin_amdgcn_s_memtime() : 0;
         const int k1 = k + 1, K2 = k + 2;
         // every per-interval flag packed in one word (fl), every LDS buffer pointer derived from
         // one parity word (par) where it is used: held across the role branches as separate
         // values they exceeded the SGPR budget and were spilled / reloaded by readlanes
-        unsigned fl;
-        {
-            const bool last = a.nti && k1 >= a.nti;   // tile k+1 is in the trailing block: not factored
-            const bool zT = last, zD = a.nti && K2 >= a.nti;   // T_{k+1} / D'_{k+2}: trailing-block tiles
-            const int rfa = rfl[k1], rfb = rfl[k];
-            const bool inEnv1 = rfa <= k;
-            const bool useD2 = k - 1 >= rfa;
-            const int rfc = K2 < NT ? rfl[K2] : 0;
-            const bool inEnvU = K2 < NT && rfc <= k, inEnvT = K2 < NT && rfc <= k1;
-            const bool needP2 = K2 < NT && max(rfc, rfb) <= k - 2, useU = K2 < NT && k - 1 >= max(rfc, rfb);
-            const bool needP1 = !zT && K2 < NT && max(rfc, rfa) <= k - 2;
-            const bool useTp = !zT && K2 < NT && k - 1 >= max(rfc, rfa);
-            const bool useTk = !zT && inEnvU && inEnv1;   // T_{k+1} -= L(k+2, k) L(k+1, k)^T
-            const bool needP0 = !zD && K2 < NT && rfc <= K2 - 4;   // the helpers' diagonal partial: columns <= k-2
-            const bool useP0c = !zD && K2 < NT && k - 1 >= rfc;     // column k-1 of D'_{k+2}: applied here
-            fl = (unsigned)last | (unsigned)inEnv1 << 1 | (unsigned)useD2 << 2 | (unsigned)inEnvU << 3 |
-                 (unsigned)inEnvT << 4 | (unsigned)needP2 << 5 | (unsigned)useU << 6 | (unsigned)needP1 << 7 |
-                 (unsigned)useTp << 8 | (unsigned)useTk << 9 | (unsigned)needP0 << 10 | (unsigned)useP0c << 11;
-        }
+        const unsigned fl = flags_of(k);
 #define DAG_FL(b) (((fl >> (b)) & 1u) != 0u)
 #define last DAG_FL(0)
 #define inEnv1 DAG_FL(1)
@@ -766,9 +814,9 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
 #define rp (rppB + 32 * cur)
 #define rpN (rppB + 32 * nxt)
         double* Dq = lds + 10240;
-        const int* f3 = wid >= 2 ? helper_flag(k) : nullptr;
+        const int* f3 = wid >= 2 && !pre ? helper_flag(k) : nullptr;
         const bool need3 = f3 != nullptr;
-        const int fv = ld_flag(need3 ? f3 : L.ctl);
+        const int fv = wid >= 2 && !pre ? ld_flag(need3 ? f3 : L.ctl) : epoch;
         if (wid == 0) {
             if (dbg && lane == 0) wts[6] = __builtin_amdgcn_s_memtime() - tk;
             // row 0 of L(k+1, k) = T Linv_k^T
@@ -903,47 +951,24 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             // p <= k-2; p = k-1 and k here, quadrant (1,0)'s column k by wave 1 in the next interval)
             // and its rhs
             const int h = wid - 2;
-            const bool got = __all(!need3 || fv == epoch) || wave_wait_all(f3, epoch, L.ctl, a.smax);
+            const bool got = pre || __all(!need3 || fv == epoch) || wave_wait_all(f3, epoch, L.ctl, a.smax);
             if (dbg && lane == 0 && h == 1) wts[4] = __builtin_amdgcn_s_memtime() - tk;   // helpers' flags in
+            if (got && !pre) fetch_in(k, fl);
+            if (dbg) {   // the loads in (diagnostics only)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                DAG_STAMP(4 + 4 * h);
+            }
+            // the next interval's helper flag: its poll goes out behind this interval's loads
+            const bool nx = k + 1 < kEnd && K2 + 1 < NT;
+            const int* f3n = nx ? helper_flag(k + 1) : nullptr;
+            const int fvn = ld_flag(f3n ? f3n : L.ctl);
             if (!got) {
                 if (lane == 0) word[4] = 1;
                 if (ORBHIP_DAG_T_W1) lds_signal(h ? F5 : F4, k + 2);
             } else {
-                const int tD = L.oL + (K2 * NT + k - 1) * kTD;
-                double4_t d0 = {0, 0, 0, 0}, d1 = {0, 0, 0, 0}, e0 = {0, 0, 0, 0}, e1 = {0, 0, 0, 0};
-                if (useU || useTp || useP0c) {
-                    d0 = qload(rs, tD + (2 * h) * 256);
-                    d1 = qload(rs, tD + (2 * h + 1) * 256);
-                }
-                // quadrant (1, 0) of D'_{k+2} needs both row halves of L(k+2, k-1): wave 3, which
-                // forms that term, loads the other half
-                if (useP0c && h == 1) {
-                    e0 = qload(rs, tD);
-                    e1 = qload(rs, tD + 256);
-                }
-                double4_t u[2], t[2], dd[2];
-#pragma unroll
-                for (int c = 0; c < 2; c++) {
-                    u[c] = !inEnvU ? double4_t{0, 0, 0, 0}
-                                   : (needP2 ? qload(rs, L.oP + (2 * NT + k) * kTD + (2 * h + c) * 256)
-                                             : s_quad(a, K2, k, h, c));
-                    t[c] = !inEnvT ? double4_t{0, 0, 0, 0}
-                                   : (needP1 ? qload(rs, L.oP + (NT + k1) * kTD + (2 * h + c) * 256)
-                                             : s_quad(a, K2, k1, h, c));
-                    const int qd = 2 * h + c;   // D' quadrants: wave 2 q0, wave 3 q2 and q3
-                    dd[c] = (h == 0 && c == 1) ? double4_t{0, 0, 0, 0}
-                                               : (needP0 ? qload(rs, L.oP + K2 * kTD + qd * 256)
-                                                         : s_quad(a, K2, K2, qd >> 1, qd & 1));
-                }
-                double rr = 0.0;
-                {
-                    const int i = kT * K2 + 16 * h + cc;
-                    rr = needP0 ? ld_sc1(a.buf + L.oR + K2 * kT + 16 * h + cc) : s_rhs(a, i);
-                }
-                if (dbg) {   // the loads in (diagnostics only)
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    DAG_STAMP(4 + 4 * h);
-                }
+                const double4_t d0 = pd0, d1 = pd1, e0 = pe0, e1 = pe1;
+                double4_t u[2] = {pu[0], pu[1]}, t[2] = {pt[0], pt[1]}, dd[2] = {pdd[0], pdd[1]};
+                double rr = prr;
                 // every LDS operand of this wave's MFMA work first (one LDS round trip), the MFMA
                 // chains two deep per product, the rhs terms (LDS + cross-row sums) after the tiles
                 const double4_t l1q[4] = {lq(L1), lq(L1 + 256), lq(L1 + 512), lq(L1 + 768)};
@@ -1044,6 +1069,21 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 sq(TpN + (2 * h) * 256, t[0]);
                 sq(TpN + (2 * h + 1) * 256, t[1]);
 #endif
+            }
+            pre = false;
+            if (got && nx && __all(!f3n || fvn == epoch)) {
+                fetch_in(k + 1, flags_of(k + 1));
+                pre = true;
+            }
+        } else if (wid == 2 && k == kEnd - 1 && !a.pb && !a.nti && NT >= 3) {
+            // the last interval, idle otherwise: every copy task's flag (intervals <= NT - 3) for
+            // the backward (the last one was published one interval ago)
+            bool got = true;
+            for (int k0 = 0; k0 <= NT - 3 && got; k0 += 64)
+                got = wave_wait_all(k0 + lane <= NT - 3 ? L.fCp + k0 + lane : nullptr, epoch, L.ctl, a.smax);
+            if (lane == 0) {
+                if (got) lds_signal(word + 18, 1);
+                else word[4] = 1;
             }
         }
         if (dbg && lane == 0) wts[wid] = __builtin_amdgcn_s_memtime() - tk;
@@ -1186,9 +1226,9 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         int* cnt = (int*)(lds + 6144);
         int* xcnt = word + 16;
         int* bab = word + 17;
-        int* cpok = word + 18;   // wave 0 saw every copy task's flag
+        int* cpok = word + 18;   // every copy task's flag seen (wave 2, in the last interval)
         for (int i = tid; i < NT; i += blockDim.x) cnt[i] = 0;
-        if (tid == 0) { *xcnt = 0; *bab = 0; *cpok = 0; }
+        if (tid == 0) { *xcnt = 0; *bab = 0; }
         __syncthreads();
         const int c = lane & 31, hh = lane >> 5;
         // element (16 hh + i, c) of a quadrant-layout tile in LDS, i = 0..15
@@ -1229,10 +1269,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 if (dbg && lane == 0 && t < kDbgBackR) dbg[kDbgBackOff + 3 * t] = __builtin_amdgcn_s_memtime() - t_fwd;
                 double p = 0.0;
                 if (t < NT) p = bwd_col_dot(lv, xs + t * kT);
-                int need = 0;   // rows R >= k + 2 whose envelope reaches column k
-                for (int R0 = k + 2; R0 < NT; R0 += 64)
-                    need += __popcll(__ballot(R0 + lane < NT && rfl[R0 + lane] <= k));
-                if (!lwait(cnt + k, need)) return false;
+                if (!lwait(cnt + k, need[k])) return false;
                 if (dbg && lane == 0 && t < kDbgBackR) dbg[kDbgBackOff + 3 * t + 2] = __builtin_amdgcn_s_memtime() - t_fwd;
                 const double r = ys[k * kT + c] - p;
                 if (hh == 0) rvec[c] = r;
@@ -1245,20 +1282,20 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             };
             {
                 // the last two steps' operands are in LDS (Linv_{NT-1}; Linv_{NT-2} and L(NT-1, NT-2):
-                // the last interval's buffers), the rest are copies: every copy task's flag
-                // (intervals k <= NT - 3) once, then the first two steps' loads
-                lds_col(lds + 1024 * ((NT - 1) & 1), liA);
-                good = xstep(ltA, liA, NT);
+                // the last interval's buffers), the rest are copies (every copy task's flag was
+                // polled by wave 2 in the last interval): their first two steps' loads go out first
+                good = lwait(cpok, 1);
+                if (good) {
+                    load(std::integral_constant<int, 0>{}, NT - 2);
+                    load(std::integral_constant<int, 1>{}, NT - 3);
+                    lds_col(lds + 1024 * ((NT - 1) & 1), liA);
+                    good = xstep(ltA, liA, NT);
+                }
                 if (good && NT >= 2) {
                     lds_col(lds + 1024 * (NT & 1), liA);
                     lds_col(lds + 2048 + 1024 * ((NT - 1) & 1), ltA);
                     good = xstep(ltA, liA, NT - 1);
                 }
-                for (int k0 = 0; k0 <= NT - 3 && good; k0 += 64)
-                    good = wave_wait_all(k0 + lane <= NT - 3 ? L.fCp + k0 + lane : nullptr, epoch, L.ctl, a.smax);
-                if (good && lane == 0) lds_signal(cpok, 1);
-                load(std::integral_constant<int, 0>{}, NT - 2);
-                load(std::integral_constant<int, 1>{}, NT - 3);
                 for (int t = NT - 2; t >= 1 && good; t -= 2) {
                     good = xstep(lt[0], li[0], t);
                     load(std::integral_constant<int, 0>{}, t - 2);
@@ -1294,11 +1331,6 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             // work-group's LDS; the copy tiles (R, R-2), R <= NT-2,
             // wait for wave 0's poll of the copy tasks' flags (cpok) before their loads are issued.
             bool good = true;
-            auto applied = [&](int j) {   // one more row in s_j (this wave is its only writer)
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                if (lane == 0)
-                    __hip_atomic_store(cnt + j, cnt[j] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            };
             if (NT >= 3 && (NT - 3) % 3 == own && rfl[NT - 1] <= NT - 3) {
                 // L(NT-1, NT-3) is still in the last interval's L2 buffer (wave 1 published it from there)
                 const double* L2last = lds + 4096 + 1024 * (NT & 1);
@@ -1313,45 +1345,64 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
 #pragma unroll
                             for (int q = 0; q < 4; q++) ys[(NT - 3) * kT + 16 * b + rg + 4 * q] -= t[b][q];
                     }
-                    applied(NT - 3);
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (lane == 0) __hip_atomic_store(cnt + NT - 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
             if (good) {
-                double v[2][16];
-                int Ra = NT - 1, ja = jtop(NT - 1);
-                norm(Ra, ja);
-                int Rb = Ra - 1, jb = ja;
-                norm(Rb, jb);
+                // a ring of kOwnAhead tiles in flight (a tile's load ~2k cycles, its product ~0.5k:
+                // two in flight left the owners behind the chain on the C5 loop's corner rows)
+                constexpr int kOwnAhead = 4;
+                double v[kOwnAhead][16];
+                int Rq[kOwnAhead], jq[kOwnAhead];
+                int Rn = NT - 1, jn = jtop(NT - 1);   // the next tile to load
+                norm(Rn, jn);
                 bool cp = false;   // cpok seen
-                auto load = [&](auto setc, int R, int j) {
+                auto fetch = [&](auto setc) {   // the next tile into ring slot S
                     constexpr int S = decltype(setc)::value;
-                    if (j < 0) return;
-                    if (j == R - 2 && !cp) cp = good = good && lwait(cpok, 1);
-                    if (good) cmload(rs, L.oCM + (R * NT + j) * kTD, v[S]);
+                    Rq[S] = Rn;
+                    jq[S] = jn;
+                    if (jn < 0) return;
+                    if (jn == Rn - 2 && !cp) cp = good = good && lwait(cpok, 1);
+                    if (good) cmload(rs, L.oCM + (Rn * NT + jn) * kTD, v[S]);
+                    Rn--;
+                    norm(Rn, jn);
                 };
-                auto apply = [&](auto setc, int R, int j) -> bool {   // s_j -= L(R, j)^T x_R
+                // a column's tiles come one after another: their products are summed in a register
+                // and s_j is updated once, its count set to the column's total (need[j])
+                double acc = 0.0;
+                int jcur = -1, xseen = 0;
+                auto flush = [&]() {
+                    if (jcur < 0) return;
+                    if (hh == 0) ys[jcur * kT + c] -= acc;
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    if (lane == 0) __hip_atomic_store(cnt + jcur, need[jcur], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                };
+                auto stepq = [&](auto setc) -> bool {   // L(R, j)^T x_R of slot S into acc, then refill the slot
                     constexpr int S = decltype(setc)::value;
-                    if (!lwait(xcnt, NT - R)) return false;
-                    const double p = bwd_col_dot(v[S], xs + R * kT);
-                    if (hh == 0) ys[j * kT + c] -= p;
-                    applied(j);
+                    const int R = Rq[S], j = jq[S];
+                    if (j < 0 || !good) return false;
+                    if (j != jcur) {
+                        flush();
+                        jcur = j;
+                        acc = 0.0;
+                    }
+                    if (xseen < NT - R) {   // x_R not seen yet: wait for it (xcnt only grows)
+                        if (!(good = lwait(xcnt, NT - R))) return false;
+                        xseen = __hip_atomic_load(xcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                    acc += bwd_col_dot(v[S], xs + R * kT);
+                    fetch(setc);
                     return true;
                 };
-                load(std::integral_constant<int, 0>{}, Ra, ja);
-                load(std::integral_constant<int, 1>{}, Rb, jb);
-                while (ja >= 0 && good) {
-                    int Rn = Rb - 1, jn = jb;
-                    norm(Rn, jn);
-                    good = apply(std::integral_constant<int, 0>{}, Ra, ja);
-                    load(std::integral_constant<int, 0>{}, Rn, jn);
-                    Ra = Rb; ja = jb; Rb = Rn; jb = jn;
-                    if (ja < 0 || !good) break;
-                    Rn = Rb - 1; jn = jb;
-                    norm(Rn, jn);
-                    good = apply(std::integral_constant<int, 1>{}, Ra, ja);
-                    load(std::integral_constant<int, 1>{}, Rn, jn);
-                    Ra = Rb; ja = jb; Rb = Rn; jb = jn;
+                fetch(std::integral_constant<int, 0>{});
+                fetch(std::integral_constant<int, 1>{});
+                fetch(std::integral_constant<int, 2>{});
+                fetch(std::integral_constant<int, 3>{});
+                while (stepq(std::integral_constant<int, 0>{}) && stepq(std::integral_constant<int, 1>{}) &&
+                       stepq(std::integral_constant<int, 2>{}) && stepq(std::integral_constant<int, 3>{})) {
                 }
+                if (good) flush();
             }
             if (!good && lane == 0) __hip_atomic_store(bab, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -1587,6 +1638,14 @@ void dag_plan(const int* rf, int n, int max_helpers, DagPlan& p, int nti) {
     for (int h = 0; h < G; h++) p.toff[h + 1] = p.toff[h] + cnt[h];
     std::vector<int> at(p.toff.begin(), p.toff.end() - 1);
     for (size_t i = 0; i < ts.size(); i++) p.tasks[at[i % G]++] = ts[i].R << 16 | ts[i].C;
+    // the chain's backward: for each column k, the rows R >= k + 2 whose envelope reaches it (the
+    // tiles its owner wave applies), after the task list (tasks[toff[G] + k])
+    if (!p.pb && !nti)
+        for (int k = 0; k < NT; k++) {
+            int q = 0;
+            for (int R = k + 2; R < NT; R++) q += rf[R] <= k ? 1 : 0;
+            p.tasks.push_back(q);
+        }
 }
 
 hipError_t chol_dag_solve(const double* S, int n, const int* row_first, const double* bs, double* x, int* flag,

@@ -2072,7 +2072,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         } else if (p.use_dag) {
             if (shard_mode == kShardRccl) {
                 const size_t NT = (p.n + kDagTile - 1) / kDagTile;
-                p.dag_task_cap = (size_t)dag_helpers + 1 + NT * (NT + 1) / 2 + NT;   // + the copy tasks
+                p.dag_task_cap = (size_t)dag_helpers + 1 + NT * (NT + 1) / 2 + 2 * NT;   // + the copy tasks, the column counts
             } else {
                 dag_plan(p.row_first.data(), p.n, dag_helpers, p.dag);
                 p.dag_task_cap = p.dag.toff.size() + p.dag.tasks.size();

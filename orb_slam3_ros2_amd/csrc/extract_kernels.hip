@@ -426,38 +426,9 @@ __device__ __forceinline__ void lds_only_barrier() {
     asm volatile("" ::: "memory");
 }
 
-// r05: the tile's resize tables computed in the kernel (dev = 1, ORBHIP_CONE_TABDEV=1: the host's
-// expressions step for step, bit-exact) instead of read from the host-built per-tile copies in ctab
-// (dev = 0, the default: ~3.5 KB per tile, most of the cone's fetched bytes, but faster)
-struct ConeTabs {
-    int dev;
-};
-__device__ __forceinline__ int cone_floor_f(float v) {   // the host's floor_f
-    const int i = (int)v;
-    return i - (i > v ? 1 : 0);
-}
-__device__ __forceinline__ int cone_sat_s16(int v) { return v < -32768 ? -32768 : (v > 32767 ? 32767 : v); }
-// resize coefficient of destination coordinate d of a level (dl) from its source level (sl), as the
-// plan builder computes it (orbhip_api.cpp: cv::resize INTER_LINEAR's fixed-point taps): the
-// source index and the packed (1 - f, f) taps
-__device__ __forceinline__ void cone_coef(int d, int dl, int sl, int& s_idx, int& taps, bool clamp_x) {
-    const double scale = 1. / ((double)dl / sl);
-    float f = (float)((d + 0.5) * scale - 0.5);
-    int si = cone_floor_f(f);
-    f -= si;
-    if (clamp_x) {
-        if (si < 0) { f = 0; si = 0; }
-        if (si + 1 >= sl && si >= sl - 1) { f = 0; si = sl - 1; }
-    }
-    const int t0 = cone_sat_s16((int)rintf((1.f - f) * 2048)), t1 = cone_sat_s16((int)rintf(f * 2048));
-    s_idx = si;
-    taps = (int)(uint16_t)t0 | ((int)(uint16_t)t1 << 16);
-}
-
 __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P, const FrameBufs& fb,
                                               const ConeRect* __restrict__ rects, const int* __restrict__ ctab,
-                                              int tab_stride, uint8_t* __restrict__ cone, int tile, int f, int s0,
-                                              const ConeTabs& ct) {
+                                              int tab_stride, uint8_t* __restrict__ cone, int tile, int f, int s0) {
     TR_BEGIN()
     const int L = P->n_levels, tid = threadIdx.x, nt = blockDim.x;
     const ConeRect* R = rects + (size_t)tile * kMaxLevels;
@@ -495,32 +466,11 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
         ttot += 2 * (r.nx1 - r.nx0) + 3 * (r.ny1 - r.ny0);
     }
     // staged table entry i (LDS layout: per level l > s0, xofs[nw] | xalpha[nw] | (r0, r1, beta)[nh]):
-    // the host's per-tile copy, or (ct.dev) computed here: a wave's lanes take consecutive entries,
-    // so each level's branch runs only in the one or two waves whose entries it holds
+    // the host's per-tile copy (r05: computing the tables in the kernel, bit-exact, cut the cone's
+    // HBM bytes 2.44 -> 1.98 MB per 640x480 launch but took the launch 21 -> 35 us in the 16-camera
+    // stream: the per-level double-precision coefficients cost more than the table round trip)
     const int* gt = ctab + (size_t)tile * tab_stride;
-    auto tab_dev = [&](int i) -> int {
-        int v = 0;
-        for (int q = s0 + 1; q < L; q++) {   // uniform
-            const ConeRect r = rect(q);
-            const int nw = r.nx1 - r.nx0, nh = r.ny1 - r.ny0, j = i - toff[q];
-            if (j >= 0 && j < 2 * nw + 3 * nh) {
-                const LevelGeom& D = P->lv[q];
-                const LevelGeom& Sg = P->lv[q - 1];
-                int si, taps;
-                if (j < 2 * nw) {
-                    cone_coef(r.nx0 + (j < nw ? j : j - nw), D.w, Sg.w, si, taps, true);
-                    v = j < nw ? si : taps;
-                } else {
-                    const int jj = j - 2 * nw, row = (jj * 21846) >> 16, comp = jj - 3 * row;   // jj / 3 (jj < 2^15)
-                    cone_coef(r.ny0 + row, D.h, Sg.h, si, taps, false);
-                    const int sy = si + comp, hs = Sg.h;
-                    v = comp == 2 ? taps : (sy < 0 ? 0 : (sy < hs ? sy : hs - 1));
-                }
-            }
-        }
-        return v;
-    };
-    auto tab_at = [&](int i) -> int { return ct.dev ? tab_dev(i) : gt[i]; };
+    auto tab_at = [&](int i) -> int { return gt[i]; };
     TR_PHASE(0, 20)
     // ---- one round trip: the tile's tables of every level and its level-0 cone, all loads issued
     // before any store ----
@@ -539,17 +489,11 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
             const uint32_t* s4 = (const uint32_t*)(src0 - sh0);
             const int p4 = in0.pitch >> 2;
             int tv[2];
-            if (!ct.dev) {
 #pragma unroll
-                for (int u = 0; u < 2; u++) tv[u] = gt[min(tid + 1024 * u, ttot - 1)];
-            }
+            for (int u = 0; u < 2; u++) tv[u] = gt[min(tid + 1024 * u, ttot - 1)];
             const int i = min(tid, tot0 - 1);
             const int y = small_div(i, inv_n), x = i - y * nwd;
             const uint32_t v = s4[(int64_t)y * p4 + x];
-            if (ct.dev) {   // computed while the level-0 load is in flight
-#pragma unroll
-                for (int u = 0; u < 2; u++) tv[u] = tid + 1024 * u < ttot ? tab_dev(tid + 1024 * u) : 0;
-            }
 #pragma unroll
             for (int u = 0; u < 2; u++)
                 if (tid + 1024 * u < ttot) tab[tid + 1024 * u] = tv[u];
@@ -644,11 +588,11 @@ __device__ __forceinline__ void pyr_cone_body(const ExtractPlan* __restrict__ P,
 
 __global__ __launch_bounds__(1024) void k_pyr_cone(const ExtractPlan* __restrict__ P, FrameBufs fb,
                                                    const ConeRect* __restrict__ rects, const int* __restrict__ ctab,
-                                                   int tab_stride, int xrun, int s0, ConeTabs ct) {
+                                                   int tab_stride, int xrun, int s0) {
     extern __shared__ __attribute__((aligned(16))) uint8_t cone[];
     if (fb.stamp && threadIdx.x == 0) atomicMin(fb.stamp, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     const int X = gridDim.x, lg = xcd_runs(blockIdx.x + X * blockIdx.y, X * gridDim.y, xrun < 0 ? X : xrun);
-    pyr_cone_body(P, fb, rects, ctab, tab_stride, cone, lg % X, lg / X, s0, ct);
+    pyr_cone_body(P, fb, rects, ctab, tab_stride, cone, lg % X, lg / X, s0);
     if (fb.stamp) {   // the workgroup's end: every wave's stores drained (the barrier waits on them)
         __syncthreads();
         if (threadIdx.x == 0) atomicMax(fb.stamp + kStampStride, (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -678,12 +622,6 @@ constexpr int kWinMax = 80;
 // 14.01-14.16 us, the stream 43.3-44.2k against 42.8-44.2k frames/s: the block's barriers cost about
 // what wave 0's serial LDS round trips did
 #define ORBHIP_OCT_BLK_FINAL 1
-#endif
-#ifndef ORBHIP_OCT_W0_FINAL
-// r05: the FINAL pass of short lists with its operands loaded once into registers. A/B on C2
-// (tools/gpu_r05_octab.sh, three alternating runs): octree stage 14.4 us with it against 13.8 us
-// with the r04 wave-0 loops, so off
-#define ORBHIP_OCT_W0_FINAL 0
 #endif
 #ifndef ORBHIP_FAST_LEAN
 #define ORBHIP_FAST_LEAN 1   // r05: branch-free pair-test round, mbcnt positions (A/B: 0 = r04's form)
@@ -1710,60 +1648,19 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                 // ---- children counts of every node to divide, from the pyramid (wave 0) ----
                 if (w0 && !blk_final) {
                     bool deep = false;
-                    if (ORBHIP_OCT_W0_FINAL && n <= 256) {
-                        // the list's four 64-node chunks with every load in flight together; a FINAL
-                        // pass also collects its (size, serial, node) keys here (in any order: the
-                        // block sort orders them)
-                        uint32_t cv[4], sv[4];
-                        uint64_t dv[4];
-#pragma unroll
-                        for (int i = 0; i < 4; i++) {   // clamped addresses, no branch around the loads
-                            const int p = lane + 64 * i, pc = p < n ? p : 0;
-                            const uint32_t c = cntC[pc], sr = serC[pc];
-                            const uint64_t r = rectC[pc];
-                            cv[i] = p < n ? c : 0u;
-                            dv[i] = p < n ? r : 0ull;
-                            sv[i] = p < n ? sr : 0u;
-                        }
-                        uint4 c4v[4];
-#pragma unroll
-                        for (int i = 0; i < 4; i++) {
-                            const int d = (int)(dv[i] >> 32);
-                            const bool dvd = cv[i] > 1, ok = dvd && d < Dh;
-                            deep = deep || (dvd && d >= Dh);
-                            const uint4 c4 = *(const uint4*)&pcnt[ok ? poff(d + 1) + 4 * (int)(uint32_t)dv[i] : 0];
-                            c4v[i] = ok ? c4 : uint4{0u, 0u, 0u, 0u};
-                        }
-                        int kpos = 0;
-#pragma unroll
-                        for (int i = 0; i < 4; i++) {
-                            const int p = lane + 64 * i;
-                            const bool dvd = cv[i] > 1;
-                            if (dvd) *(uint4*)&S.ccount[4 * p] = c4v[i];
-                            if (mode) {
-                                const uint64_t m = __ballot(dvd);
-                                const int below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                                if (dvd) S.skey2[kpos + below] = ((uint64_t)cv[i] << 40) | ((uint64_t)sv[i] << 16) | (uint64_t)p;
-                                kpos += __popcll(m);
-                            }
-                        }
-                        if (mode && lane == 0) ctl[60] = kpos;
-                        TR_PHASE(2, 43)
-                    } else {
-                        for (int p = lane; p < n; p += 64) {
-                            if (cntC[p] > 1) {
-                                const uint64_t cd = rectC[p];
-                                const int d = (int)(cd >> 32);
-                                if (d >= Dh) {
-                                    deep = true;
-                                } else {
-                                    const uint4 c4 = *(const uint4*)&pcnt[poff(d + 1) + 4 * (int)(uint32_t)cd];
-                                    *(uint4*)&S.ccount[4 * p] = c4;
-                                }
+                    for (int p = lane; p < n; p += 64) {
+                        if (cntC[p] > 1) {
+                            const uint64_t cd = rectC[p];
+                            const int d = (int)(cd >> 32);
+                            if (d >= Dh) {
+                                deep = true;
+                            } else {
+                                const uint4 c4 = *(const uint4*)&pcnt[poff(d + 1) + 4 * (int)(uint32_t)cd];
+                                *(uint4*)&S.ccount[4 * p] = c4;
                             }
                         }
                     }
+                
                     if (__ballot(deep) && lane == 0) ctl[62] = 1;
                     wave_lds_fence();
                 }
@@ -1869,8 +1766,7 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
             } else {
                 // ---- FINAL phase: divide largest (size, serial) first until >= N ----
                 TR_PHASE(2, 48)
-                const bool short_list = FAST && ORBHIP_OCT_W0_FINAL && n <= 256;   // keys collected by the fill above; the register node pass
-                if (w0 && !short_list && !blk_final) {
+                if (w0 && !blk_final) {
                     const int per = (n + 63) >> 6;
                     const int b = min(lane * per, n), e = min(b + per, n);
                     int s = 0;
@@ -1949,110 +1845,6 @@ __global__ __launch_bounds__(1024) void k_octree(const ExtractPlan* __restrict__
                             if (newSize >= N || newSize == n) ctl[59] = 1;
                         }
                     }
-                } else if (w0 && !stop && short_list && K > 0) {
-                    // the pass below with every operand loaded once into registers (K <= n <= 256:
-                    // at most four sorted entries and four list nodes per lane), jstar from one
-                    // ballot (run is non-decreasing in j: every divided node has a child)
-                    const int serial0 = ctl[57];
-                    const int per = (K + 63) >> 6;
-                    const int b = min(lane * per, K), e = min(b + per, K);
-                    // clamped addresses, no branch around the loads (K >= 1 here: FINAL had nodes to divide)
-                    int pj[4];
-#pragma unroll
-                    for (int u = 0; u < 4; u++) pj[u] = (int)(S.skey[min(b + u, K - 1)] & 0xFFFF);
-                    uint4 c4j[4];
-                    uint64_t rj[4];
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const uint4 c4 = *(const uint4*)&S.ccount[4 * pj[u]];
-                        c4j[u] = b + u < e ? c4 : uint4{0u, 0u, 0u, 0u};
-                        rj[u] = rectC[pj[u]];
-                    }
-#pragma unroll
-                    for (int i = 0; i < 4; i++)
-                        if (lane + 64 * i < n) S.tD[lane + 64 * i] = 1;
-                    int cj[4], g = 0;
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const uint32_t q4[4] = {c4j[u].x, c4j[u].y, c4j[u].z, c4j[u].w};
-                        cj[u] = b + u < e ? nonempty4(q4) : 0;
-                        g += b + u < e ? cj[u] - 1 : 0;
-                    }
-                    const int ig = wave_incl_scan(g);
-                    int run = n + ig - g, cand = -1;
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        if (b + u < e && cand < 0) {
-                            run += cj[u] - 1;
-                            if (run >= N) cand = b + u;
-                        }
-                    }
-                    const uint64_t cmask = __ballot(cand >= 0);
-                    const int jstar = cmask ? __builtin_amdgcn_readlane(cand, __ffsll((unsigned long long)cmask) - 1) : K - 1;
-                    int sc = 0;
-#pragma unroll
-                    for (int u = 0; u < 4; u++) sc += (b + u < e && b + u <= jstar) ? cj[u] : 0;
-                    const int ic = wave_incl_scan(sc);
-                    const int Ctot = __builtin_amdgcn_readlane(ic, 63);
-                    int cb = ic - sc;
-                    wave_lds_fence();   // the tD = 1 stores before the divided nodes' zeros
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        if (b + u < e && b + u <= jstar) {
-                            const uint32_t q4[4] = {c4j[u].x, c4j[u].y, c4j[u].z, c4j[u].w};
-                            const int c = cj[u], base = Ctot - cb - c;
-                            int r = 0;
-#pragma unroll
-                            for (int q = 0; q < 4; q++) {
-                                if (q4[q] == 0) continue;
-                                const int ps = base + (c - 1 - r);
-                                rectO[ps] = kid(rj[u], q);
-                                cntO[ps] = q4[q];
-                                serO[ps] = serial0 + cb + r;
-                                r++;
-                            }
-                            S.tD[pj[u]] = 0;
-                            cb += c;
-                        }
-                    }
-                    wave_lds_fence();
-                    // the other nodes keep their order behind the children
-                    const int pn = (n + 63) >> 6;
-                    const int bn = min(lane * pn, n), en = min(bn + pn, n);
-                    int tdv[4];
-                    uint64_t rv[4];
-                    uint32_t cv[4], sv[4];
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        const int p = bn + u, pc = min(p, n - 1);
-                        const bool in = p < en;
-                        const int t = S.tD[pc];
-                        rv[u] = rectC[pc];
-                        cv[u] = cntC[pc];
-                        sv[u] = serC[pc];
-                        tdv[u] = in ? t : 0;
-                    }
-                    const int st = tdv[0] + tdv[1] + tdv[2] + tdv[3];
-                    const int is = wave_incl_scan(st);
-                    int sb = is - st;
-#pragma unroll
-                    for (int u = 0; u < 4; u++) {
-                        if (tdv[u]) {
-                            const int ps = Ctot + sb;
-                            rectO[ps] = rv[u];
-                            cntO[ps] = cv[u];
-                            serO[ps] = sv[u];
-                            sb++;
-                        }
-                    }
-                    const int newSize = Ctot + (n - (jstar + 1));
-                    wave_lds_fence();
-                    if (lane == 0) {
-                        ctl[57] = serial0 + Ctot;
-                        ctl[56] = newSize;
-                        if (newSize >= N || newSize == n) ctl[59] = 1;
-                    }
-                    TR_PHASE(2, 42)
                 } else if (w0 && !stop) {
                     const int serial0 = ctl[57];
                     const int per = (K + 63) >> 6;
@@ -2713,16 +2505,11 @@ void launch_pyr_cone(const ExtractPlan* dP, int ntiles, size_t lds, const FrameB
     static LdsAttrOnce attr;   // per device, thread-safe (dev_attr.h)
     (void)attr.ensure((const void*)k_pyr_cone, 64 * 1024);
     (void)xofs; (void)xalpha; (void)yofs; (void)ybeta;
-    // the host's per-tile table copies by default; ORBHIP_CONE_TABDEV=1 computes the tables in the
-    // kernel (bit-exact; r05 A/B, three alternating runs: the cone's HBM bytes 2.44 -> 1.98 MB per
-    // 640x480 launch, but the launch 21 -> 35 us in the 16-camera stream, 43.6k -> 37.0k frames/s:
-    // the per-level double-precision coefficients cost more than the table round trip). (r05 also
-    // measured the plan's compact per-level tables: 130 KB fewer fetched bytes, but every staged
-    // entry waited on its level's ConeRect before its table load: 20.8 -> 26.9 us; removed.)
-    static const bool dev = getenv("ORBHIP_CONE_TABDEV") && getenv("ORBHIP_CONE_TABDEV")[0] == '1';
-    const ConeTabs ct{dev ? 1 : 0};
+    // the host's per-tile table copies (r05 also measured the plan's compact per-level tables: 130
+    // KB fewer fetched bytes, but every staged entry waited on its level's ConeRect before its
+    // table load: 20.8 -> 26.9 us; and in-kernel tables, see pyr_cone_body)
     ORBHIP_LAUNCH(k_pyr_cone, dim3(ntiles, B), dim3(nthreads), lds, st, dP, fb, rects, ctab, tab_stride,
-                  xcd_run_for(B), s0, ct);
+                  xcd_run_for(B), s0);
 }
 
 void launch_fast(const ExtractPlan* dP, const ExtractPlan& hP, const CellGeom* cells, const FrameBufs& fb, int B,

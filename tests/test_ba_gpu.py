@@ -243,7 +243,9 @@ def test_blocked_cholesky_solves_spd(n, shape):
 
 
 @pytest.mark.parametrize("n,shape,helpers,pback", [(31, "dense", 0, None), (64, "dense", 0, None),
+                                                   (70, "dense", 0, None), (96, "dense", 1, None),
                                                    (100, "dense", 3, None), (294, "dense", 0, None),
+                                                   (300, "band", 2, None), (330, "loop", 0, None),
                                                    (294, "dense", 1, None), (294, "dense", 0, "1"),
                                                    (294, "dense", 1, "1"), (600, "band", 0, None),
                                                    (600, "band", 0, "1"), (1201, "dense", 0, None),
@@ -256,8 +258,10 @@ def test_dag_cholesky_solves_spd(n, shape, helpers, pback, monkeypatch):
     systems: dense, banded, and C5's band plus loop-closure corner, with the full helper grid and
     with few helpers (each helper then runs many tasks in dependency-key order), the backward
     substitution in the chain or over the helpers (ORBHIP_DAG_PBACK forces either; by default long
-    rows go to the helpers). Against numpy's fp64 solve; three solves in a row reuse the flags
-    through the per-solve epoch."""
+    rows go to the helpers). The chain's backward (r06: column copies written by the helpers' tasks,
+    the last interval's operands from LDS, owner waves per column residue) at NT = 3 (the first
+    copy task), with few helpers, and on band / loop envelopes whose rows skip columns. Against
+    numpy's fp64 solve; three solves in a row reuse the flags through the per-solve epoch."""
     import ctypes
     from orb_slam3_ros2_amd._lib import lib
     if pback is not None:
