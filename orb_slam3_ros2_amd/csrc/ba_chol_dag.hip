@@ -667,6 +667,15 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         for (int i = tid; i < NT; i += blockDim.x) need[i] = a.tasks[a.toff[a.G] + i];
     int c1 = 0, c2 = 0;
     // ---- prologue: wave 0 factors tile 0; T_0 = A(1, 0), D'_1 = A(1, 1), L1 = L2 = 0 ----
+    // wave 0's tile-0 quadrants go out first, with every other prologue load (one global round
+    // trip); it reads only its own LDS stores (rvec: tid < 32) before the interval barrier, so it
+    // passes no barrier here
+    double4_t q00 = {0, 0, 0, 0}, q10 = {0, 0, 0, 0}, q11 = {0, 0, 0, 0};
+    if (wid == 0) {
+        q00 = s_quad(a, 0, 0, 0, 0);
+        q10 = s_quad(a, 0, 0, 1, 0);
+        q11 = s_quad(a, 0, 0, 1, 1);
+    }
     sq(lds + 2048 + quad * 256, double4_t{0, 0, 0, 0});
     sq(lds + 4096 + quad * 256, double4_t{0, 0, 0, 0});
     if (NT > 1) {
@@ -678,12 +687,9 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         }
     }
     if (tid < kT) rvec[tid] = s_rhs(a, tid);
-    __syncthreads();
     if (wid == 0) {
         double4_t lin11, l21t;
-        // tile 0's three quadrants in one global round trip (part B's were loaded after part A's
-        // pivots, behind their asm blocks)
-        const double4_t q00 = s_quad(a, 0, 0, 0, 0), q10 = s_quad(a, 0, 0, 1, 0), q11 = s_quad(a, 0, 0, 1, 1);
+        wave_lds_sync();   // rvec
         ok = diag_part_a(q00, lds, lin11, lds + 10240);
         wave_lds_sync();
         const double y0 = quad_matvec(lds, 0, rvec);
@@ -744,13 +750,14 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                (unsigned)useTp << 8 | (unsigned)useTk << 9 | (unsigned)needP0 << 10 | (unsigned)useP0c << 11;
     };
     // waves 2/3: the global inputs of interval kk (the helpers' partial tiles / S, the full tile
-    // L(kk+2, kk-1), the rhs partial) into the p* registers; issued at the start of interval kk, or
-    // (r06) at the end of interval kk-1 when its helpers' flags are already in (their poll goes out
-    // early in interval kk-1, behind that interval's own loads), so interval kk starts with them
+    // L(kk+2, kk-1), the rhs partial) into the p* registers, issued once the interval's helper flags
+    // are in. (r06: issuing them at the end of interval kk-1 whenever its flags were already in,
+    // behind an early poll, took the n = 294 interval 12.5k -> 15.6k cycles on one box, two alternating
+    // runs each: reverted)
     double4_t pd0 = {0, 0, 0, 0}, pd1 = {0, 0, 0, 0}, pe0 = {0, 0, 0, 0}, pe1 = {0, 0, 0, 0};
     double4_t pu[2] = {}, pt[2] = {}, pdd[2] = {};
     double prr = 0.0;
-    bool pre = false;
+    const bool pre = false;
     auto fetch_in = [&](int kk, unsigned flk) {
         const int h = wid - 2, kk1 = kk + 1, KK2 = kk + 2;
         auto F = [&](int b) { return ((flk >> b) & 1u) != 0u; };
@@ -958,10 +965,6 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 DAG_STAMP(4 + 4 * h);
             }
-            // the next interval's helper flag: its poll goes out behind this interval's loads
-            const bool nx = k + 1 < kEnd && K2 + 1 < NT;
-            const int* f3n = nx ? helper_flag(k + 1) : nullptr;
-            const int fvn = ld_flag(f3n ? f3n : L.ctl);
             if (!got) {
                 if (lane == 0) word[4] = 1;
                 if (ORBHIP_DAG_T_W1) lds_signal(h ? F5 : F4, k + 2);
@@ -1069,11 +1072,6 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 sq(TpN + (2 * h) * 256, t[0]);
                 sq(TpN + (2 * h + 1) * 256, t[1]);
 #endif
-            }
-            pre = false;
-            if (got && nx && __all(!f3n || fvn == epoch)) {
-                fetch_in(k + 1, flags_of(k + 1));
-                pre = true;
             }
         } else if (wid == 2 && k == kEnd - 1 && !a.pb && !a.nti && NT >= 3) {
             // the last interval, idle otherwise: every copy task's flag (intervals <= NT - 3) for

@@ -623,9 +623,6 @@ constexpr int kWinMax = 80;
 // what wave 0's serial LDS round trips did
 #define ORBHIP_OCT_BLK_FINAL 1
 #endif
-#ifndef ORBHIP_FAST_LEAN
-#define ORBHIP_FAST_LEAN 1   // r05: branch-free pair-test round, mbcnt positions (A/B: 0 = r04's form)
-#endif
 typedef _Float16 h2 __attribute__((ext_vector_type(2)));   // two pixels, one per 16-bit half
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 constexpr uint32_t kPwBias = 0x64006400u;                   // f16(1024) in both halves
@@ -790,7 +787,6 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
     const int nq = R * dc, qb = R * dc;
     const int ystep = NT / dc, xstep = NT - ystep * dc;
     int y = small_div(tid, inv_dc), x = tid - y * dc;
-#if ORBHIP_FAST_LEAN
     // r05: the round without a branch (a lane past the last pixel reads a clamped row and passes
     // nothing), the list positions by mbcnt, the capacity checked once per wave and round
     (void)lt;
@@ -829,36 +825,6 @@ __device__ __forceinline__ void fast_cell_body(const ExtractPlan* __restrict__ P
         y += ystep;
         if (x >= dc) { x -= dc; y++; }
     }
-#else
-    for (int q0 = 0; q0 < nq; q0 += NT) {
-        const int q = q0 + tid;
-        bool pass0 = false, pass1 = false;
-        if (q < nq) {
-            const uint32_t* c = pw + y * PWP + x + sh;
-            h2 cc[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) cc[k] = as_h2(c[C::o[k]]);
-            const h2 v = as_h2(c[C::o[16]]);
-            h2 M1 = hmax(cc[0], cc[8]), M2 = hmin(cc[0], cc[8]);
-#pragma unroll
-            for (int k = 1; k < 8; k++) {
-                M1 = hmin(M1, hmax(cc[k], cc[k + 8]));
-                M2 = hmax(M2, hmin(cc[k], cc[k + 8]));
-            }
-            const h2 s = hmax(M1 - (v + tv), v - (M2 + tv));   // > 0: passes (exact integers)
-            pass0 = s.x > (_Float16)0;
-            pass1 = (y + R < dr) & (s.y > (_Float16)0);
-        }
-        const uint64_t b0 = __ballot(pass0), b1 = __ballot(pass1);
-        const int ci0 = wcnt + __popcll(b0 & lt), ci1 = wcnt + __popcll(b0) + __popcll(b1 & lt);
-        if (pass0 && ci0 < capw) wlist[ci0] = (uint16_t)q;
-        if (pass1 && ci1 < capw) wlist[ci1] = (uint16_t)(q + qb);
-        wcnt += __popcll(b0) + __popcll(b1);
-        x += xstep;
-        y += ystep;
-        if (x >= dc) { x -= dc; y++; }
-    }
-#endif
     if (lane == 0) LS.ncw[wid] = wcnt;
     __syncthreads();
     // dense: a wave's list overflowed, so the strength runs on every pixel instead (m <= t_lo for
