@@ -667,15 +667,6 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         for (int i = tid; i < NT; i += blockDim.x) need[i] = a.tasks[a.toff[a.G] + i];
     int c1 = 0, c2 = 0;
     // ---- prologue: wave 0 factors tile 0; T_0 = A(1, 0), D'_1 = A(1, 1), L1 = L2 = 0 ----
-    // wave 0's tile-0 quadrants go out first, with every other prologue load (one global round
-    // trip); it reads only its own LDS stores (rvec: tid < 32) before the interval barrier, so it
-    // passes no barrier here
-    double4_t q00 = {0, 0, 0, 0}, q10 = {0, 0, 0, 0}, q11 = {0, 0, 0, 0};
-    if (wid == 0) {
-        q00 = s_quad(a, 0, 0, 0, 0);
-        q10 = s_quad(a, 0, 0, 1, 0);
-        q11 = s_quad(a, 0, 0, 1, 1);
-    }
     sq(lds + 2048 + quad * 256, double4_t{0, 0, 0, 0});
     sq(lds + 4096 + quad * 256, double4_t{0, 0, 0, 0});
     if (NT > 1) {
@@ -687,9 +678,13 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         }
     }
     if (tid < kT) rvec[tid] = s_rhs(a, tid);
+    __syncthreads();
     if (wid == 0) {
         double4_t lin11, l21t;
-        wave_lds_sync();   // rvec
+        // tile 0's three quadrants in one global round trip (part B's were loaded after part A's
+        // pivots, behind their asm blocks). (r06: issuing them before the prologue's barrier, with
+        // wave 0 skipping it, measured the same: 81.2-82.1 against 80.7-81.1 us at n = 294)
+        const double4_t q00 = s_quad(a, 0, 0, 0, 0), q10 = s_quad(a, 0, 0, 1, 0), q11 = s_quad(a, 0, 0, 1, 1);
         ok = diag_part_a(q00, lds, lin11, lds + 10240);
         wave_lds_sync();
         const double y0 = quad_matvec(lds, 0, rvec);
