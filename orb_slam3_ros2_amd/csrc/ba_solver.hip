@@ -471,6 +471,81 @@ __device__ __forceinline__ double lin_pose(const BaArgs& a, int i, int lane, boo
     }
     return dmax;
 }
+// the same with the whole work-group on pose i (r06, k_ba_lin with one pose per work-group): its
+// four waves take edges lane, lane + 256, ... of the pose, each reduces its 27 sums as above, and
+// wave 0 adds the four in wave order; returns the largest |diagonal| in wave 0 (0 in the others)
+__device__ __forceinline__ double lin_pose_wg(const BaArgs& a, int i, bool fresh, double* sh27) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (i >= a.np) return 0.0;   // work-group-uniform
+    double acc[32];
+#pragma unroll
+    for (int k = 0; k < 32; k++) acc[k] = 0;
+    for (int k = a.ps_ptr[i] + (int)threadIdx.x; k < a.ps_ptr[i + 1]; k += blockDim.x) {
+        const int e = a.ps_edges[k];
+        double x, y, z, R[9], j[4], A[6], B[12];
+        edge_pc(a, e, x, y, z, R);
+        proj_jac(a.fx, a.fy, x, y, z, j);
+        jac_ab(j, x, y, z, R, A, B);
+        double r1, er0, er1;
+        if (fresh) {
+            double chi2, r0;
+            edge_terms(a, e, x, y, z, er0, er1, chi2, r0, r1);
+        } else {
+            r1 = a.e_rho1[e];
+            er0 = a.e_err[2 * e];
+            er1 = a.e_err[2 * e + 1];
+        }
+        const double info = a.e_info[e];
+        const double w = r1 * info;
+        const double om0 = -info * er0 * r1, om1 = -info * er1 * r1;
+        int t = 0;
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int c = r; c < 6; c++) acc[t++] += w * (B[r] * B[c] + B[6 + r] * B[6 + c]);
+#pragma unroll
+        for (int r = 0; r < 6; r++) acc[21 + r] += B[r] * om0 + B[6 + r] * om1;
+    }
+    reduce_half<16>(acc, lane, 32);
+    reduce_half<8>(acc, lane, 16);
+    reduce_half<4>(acc, lane, 8);
+    reduce_half<2>(acc, lane, 4);
+    reduce_half<1>(acc, lane, 2);
+    const double tot = acc[0] + __shfl_xor(acc[0], 1, 64);
+    const int k = ((lane >> 5) & 1) << 4 | ((lane >> 4) & 1) << 3 | ((lane >> 3) & 1) << 2 | ((lane >> 2) & 1) << 1 |
+                  ((lane >> 1) & 1);
+    if ((lane & 1) == 0 && k < 27) sh27[27 * wid + k] = tot;
+    __syncthreads();
+    double dmax = 0.0;
+    if (wid == 0) {
+        if (lane < 27) {
+            const double v = (sh27[lane] + sh27[27 + lane]) + (sh27[54 + lane] + sh27[81 + lane]);
+            double* H = a.Hpp + 36 * i;
+            if (lane < 21) {   // lane-th entry of the upper triangle, row-major
+                int r = 0, t = lane;
+                while (t >= 6 - r) { t -= 6 - r; r++; }
+                const int c = r + t;
+                H[6 * r + c] = v;
+                H[6 * c + r] = v;
+                if (r == c) dmax = fabs(v);
+            } else {
+                a.b[6 * i + lane - 21] = v;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) dmax = fmax(dmax, __shfl_xor(dmax, o, 64));
+        if (lane < 9 && a.ps_ptr[i] < a.ps_ptr[i + 1]) {   // the pose's rotation, as its edges used it
+            const int p = a.e_pose[a.ps_edges[a.ps_ptr[i]]];
+            double R[9];
+            qtomat(load_q(a.pose + 8 * p), R);
+            double r = R[0];
+#pragma unroll
+            for (int kk = 1; kk < 9; kk++) r = lane == kk ? R[kk] : r;
+            a.R_lin[9 * i + lane] = r;
+        }
+    }
+    return dmax;
+}
 __global__ __launch_bounds__(256) void k_ba_lin_poses(const BaArgs* __restrict__ args, const int* __restrict__ act) {
     BA_PROLOGUE
     BA_PHASE(kPhBuild)
@@ -481,13 +556,15 @@ __global__ __launch_bounds__(256) void k_ba_lin_poses(const BaArgs* __restrict__
 // four lanes per landmark), the rest poses (one per wave); each stores its largest |diagonal| (sc1), and the
 // problem's last workgroup runs the controller's trial start (ctl_begin_body: lambda from the
 // maxima on the first iteration)
+// ppw: poses per pose work-group, 4 (a wave each) or 1 (the whole work-group, lin_pose_wg)
 __global__ __launch_bounds__(256) void k_ba_lin(const BaArgs* __restrict__ args, const int* __restrict__ act,
-                                               int nbp, int* const* donep) {
+                                               int nbp, int ppw, int* const* donep) {
     BA_PROLOGUE
     BA_PHASE(kPhBuild)
     __shared__ double sh[4];
+    __shared__ double sh27[4 * 27];
     __shared__ int lastf;
-    const int mP = (a.M + kLinL - 1) / kLinL, nP = (a.np + 3) / 4;
+    const int mP = (a.M + kLinL - 1) / kLinL, nP = (a.np + ppw - 1) / ppw;
     // a small problem whose iteration ended on a rejected trial: its stored errors are the trial's,
     // so this build takes them from the restored state (the larger problems' k_ba_errors(1) did)
     const bool fresh = a.small && a.ctl && !a.ctl->errors_valid;
@@ -498,7 +575,7 @@ __global__ __launch_bounds__(256) void k_ba_lin(const BaArgs* __restrict__ args,
         slot = bx_ < mP ? bx_ : -1;
     } else {
         const int q = bx_ - nbp;
-        d = lin_pose(a, q * 4 + (threadIdx.x >> 6), threadIdx.x & 63, fresh);
+        d = ppw == 1 ? lin_pose_wg(a, q, fresh, sh27) : lin_pose(a, q * 4 + (threadIdx.x >> 6), threadIdx.x & 63, fresh);
         slot = q < nP ? mP + q : -1;
     }
 #pragma unroll
@@ -1947,7 +2024,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     for (int b = 0; b < B; b++) prep_reset(pp[b]);
     // Schur work-item size: a batch fills the chip with 16 pairs per lane; a few problems alone
     // would leave it mostly idle, so their items are cut to 4 pairs (4x the lanes)
-    const int chunk = B >= 32 ? kSchurChunk : 4;
+    static const int chunk_env = std::getenv("ORBHIP_SCHUR_CHUNK") ? std::atoi(std::getenv("ORBHIP_SCHUR_CHUNK")) : 0;
+    const int chunk = chunk_env > 0 ? chunk_env : (B >= 32 ? kSchurChunk : 4);
     // one problem: its Schur pair lists on the host threads; a batch: one problem per thread
     // (ORBHIP_PREP_THREADS=k: one large problem's pair lists on k host threads; off by default: on
     // the MI355X box's EPYC the C5 build went 0.62 -> 0.55 ms at 16 threads, 0.71 at 4 (its
@@ -2109,7 +2187,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         nR = (nR + 1) & ~size_t(1);
         p.o_part = nR; nR += 36 * (size_t)p.nslot;
         p.o_red2 = nR;
-        nR += std::max((E + 255) / 256 + (std::max(M, P) + kBsL - 1) / kBsL, (M + kLinL - 1) / kLinL + (np_ + 3) / 4) + 2;
+        nR += std::max((E + 255) / 256 + (std::max(M, P) + kBsL - 1) / kBsL, (M + kLinL - 1) / kLinL + np_) + 2;
         if (p.use_dag) {   // 128-byte aligned
             nR = (nR + 15) & ~size_t(15);
             p.o_dag = nR; nR += dag_doubles(p.n);
@@ -2489,6 +2567,10 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         // ... and takes its errors inside the back-substitution when its partial slots hold the
         // fused kernel's workgroups (ORBHIP_BA_FUSED=0 keeps the separate k_ba_errors(2))
         const unsigned gbs = gx(std::max(maxM, maxP), kBsL);
+        // k_ba_lin's pose work-groups: one pose per work-group (its four waves on its edges) for a
+        // lone problem, four (a wave each) for batches; ORBHIP_LIN_PPW=1/4 forces one
+        const char* e_ppw = std::getenv("ORBHIP_LIN_PPW");
+        const int lin_ppw = e_ppw ? (std::atoi(e_ppw) == 1 ? 1 : 4) : (B == 1 ? 1 : 4);
         const char* fz = std::getenv("ORBHIP_BA_FUSED");   // per call: the tests compare both forms
         const bool fuse_env = !(fz && fz[0] == '0');
         bool fused = all_small && fuse_env;
@@ -2517,8 +2599,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         __atomic_store_n(ws->h_done + ws->done_cap, 0, __ATOMIC_RELAXED);
         auto slot = [&]() -> int {
             if (!all_small) hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 1, donep);
-            hipLaunchKernelGGL(k_ba_lin, dim3(gx(maxM, kLinL) + gx(maxNp, 4), B), b256, 0, st, dA, d_act,
-                               (int)gx(maxM, kLinL), donep);
+            hipLaunchKernelGGL(k_ba_lin, dim3(gx(maxM, kLinL) + gx(maxNp, lin_ppw), B), b256, 0, st, dA, d_act,
+                               (int)gx(maxM, kLinL), lin_ppw, donep);
             if (sharded) {   // the trial start on the shards' sums: Hpp, then the largest diagonal
                 if (coll(kHpp)) return ORBHIP_ERR_DEVICE;
                 hipLaunchKernelGGL(k_ba_sh_maxdiag, dim3(B), b256, 0, st, dA, d_act);
