@@ -125,7 +125,7 @@ __device__ __forceinline__ bool last_arrival(int* counter, int total, int* sh_fl
     return *sh_flag != 0;
 }
 __device__ void ctl_end_body(const BaArgs& a, int prob, int* done_flags, double* sh);
-__device__ void ctl_begin_body(const BaArgs& a, int nlin, int* done_flags, int prob);
+__device__ void ctl_begin_body(const BaArgs& a, int nlin, int* done_flags, int prob, double* sh);
 
 // ---------------------------------------------------------------------------
 // errors (when: 0 always, 1 the build's stale-error refresh, 2 a trial's new state); a trial also
@@ -589,7 +589,7 @@ __global__ __launch_bounds__(256) void k_ba_lin(const BaArgs* __restrict__ args,
         st_agent(a.part + slot, m);
     }
     if (!a.sync && last_arrival(&a.ctl->arrive_b, gridDim.x, &lastf))
-        ctl_begin_body(a, mP + nP, done_of(donep), act[by_]);
+        ctl_begin_body(a, mP + nP, done_of(donep), act[by_], sh);
 }
 
 // ---------------------------------------------------------------------------
@@ -1113,7 +1113,8 @@ __global__ __launch_bounds__(256) void k_ba_backsub(const BaArgs* __restrict__ a
             a.part[a.npart_e + i] = 0.0;
 }
 
-// small problems (BaArgs::fused): the back-substitution and the trial's errors in ONE launch, no
+// the fused trial (BaArgs::fused; every unsharded problem since r06, small ones only before): the
+// back-substitution and the trial's errors in ONE launch, no k_ba_schur_points before it and no
 // k_ba_errors(2) after it. The trial's poses go to pose_bak (pose keeps the accepted state until
 // the controller commits). Every workgroup forms all P new poses in LDS (P <= kFusedMaxP: a few
 // se3 updates per thread, overlapping its landmark loads) and takes kBsL landmarks, four lanes per
@@ -1217,7 +1218,8 @@ __global__ __launch_bounds__(256) void k_ba_pop(const BaArgs* __restrict__ args,
     BA_PROLOGUE
     if (a.ctl && !a.ctl->pop) return;
     const int i = bx_ * blockDim.x + threadIdx.x;
-    if (i < 8 * a.P) a.pose[i] = a.pose_bak[i];
+    // (a fused trial left the poses unmoved: pose_bak holds the rejected trial's)
+    if (i < 8 * a.P && !a.fused) a.pose[i] = a.pose_bak[i];
     if (i < 3 * a.M) a.pts[i] = a.pts_bak[i];
 }
 
@@ -1355,7 +1357,20 @@ __device__ void ctl_begin_apply(const BaArgs& a, double maxdiag) {
     c.errors_valid = 1;   // the build just done used the current state's errors
     c.phase = kPhTrial;
 }
-__device__ void ctl_begin_body(const BaArgs& a, int nlin, int* done_flags, int prob) {
+// every thread of the work-group calls it: on the first iteration the largest diagonal over the
+// build's nlin work-group maxima is a block reduction (r06: thread 0 alone read them one after
+// another, 94 us of the first C5 build for its 712 partials)
+__device__ void ctl_begin_body(const BaArgs& a, int nlin, int* done_flags, int prob, double* sh) {
+    double m = 0.0;
+    if (a.ctl->it == 0) {   // block-uniform: written by an earlier launch
+        for (int i = threadIdx.x; i < nlin; i += blockDim.x) m = fmax(m, ld_agent(a.part + i));
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = m;
+        __syncthreads();
+        for (int w = 0; w < (int)(blockDim.x >> 6); w++) m = fmax(m, sh[w]);
+    }
     if (threadIdx.x != 0) return;
     if (a.ctl->stop) {   // a stop relayed before this iteration: g2o's terminate() check, no trial
         LmCtl& c = *a.ctl;
@@ -1363,9 +1378,6 @@ __device__ void ctl_begin_body(const BaArgs& a, int nlin, int* done_flags, int p
         post_done(done_flags, prob);
         return;
     }
-    double m = 0.0;
-    if (a.ctl->it == 0)
-        for (int i = 0; i < nlin; i++) m = fmax(m, ld_agent(a.part + i));
     ctl_begin_apply(a, m);
 }
 
@@ -1425,7 +1437,7 @@ __device__ void ctl_end_decide(const BaArgs& a, int prob, int* done_flags) {
 __device__ void ctl_end_body(const BaArgs& a, int prob, int* done_flags, double* sh) {
     ctl_end_sums(a, sh);
     if (threadIdx.x == 0) ctl_end_decide(a, prob, done_flags);
-    if (!a.small) return;
+    if (!a.small && !a.fused) return;
     // a small problem: this workgroup restores a rejected trial's state (k_ba_pop), so that needs
     // no launch of its own (the restored state's errors, g2o's computeActiveErrors at the next
     // iteration's start, come from the next k_ba_lin).
@@ -1441,6 +1453,9 @@ __device__ void ctl_end_body(const BaArgs& a, int prob, int* done_flags, double*
             for (int i = threadIdx.x; i < 8 * a.P; i += blockDim.x) st_agent(a.pose + i, ld_agent(a.pose_bak + i));
             return;
         }
+        // r06: larger problems take the fused trial too; their points come back in k_ba_pop (3M
+        // words are too many for this one work-group)
+        if (!a.small) return;
     } else {
         if (!c.pop) return;
         for (int i = threadIdx.x; i < 8 * a.P; i += blockDim.x) st_agent(a.pose + i, ld_agent(a.pose_bak + i));
@@ -2013,6 +2028,11 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     for (int b = 0; b < B; b++)
         if (!probs[b] || !res[b]) return ORBHIP_ERR_ARG;
     static const bool timing = std::getenv("ORBHIP_BA_TIMING") != nullptr;
+    // the state words (8 P + 3 M) up to which the trial's last work-group restores a rejected
+    // trial itself ("small"); larger problems restore in k_ba_pop. ORBHIP_BA_SMALL_WORDS (read per
+    // call) lowers it: the tests run the large-problem path on problems that reject trials
+    const char* e_sw = std::getenv("ORBHIP_BA_SMALL_WORDS");
+    const long small_words = e_sw ? std::atol(e_sw) : 32768;
     auto now = [] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const double t_start = now();
     const int nth = host_threads();
@@ -2312,7 +2332,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.Hpp_g = a.Hpp;
         if (sharded) { a.Hpp_g = r; r += 36 * (size_t)p.np; }
         a.sync = sharded ? 1 : 0;
-        a.small = (!sharded && 8 * P + 3 * M <= 32768 && E <= 65536) ? 1 : 0;
+        a.small = (!sharded && 8 * P + 3 * M <= (size_t)small_words && E <= 65536) ? 1 : 0;
         a.fused = 0;   // set below once the batch's launch width is known
         a.b = r; r += p.n + 3 * M;
         a.x = r; r += p.n + 3 * M;
@@ -2573,7 +2593,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         const int lin_ppw = e_ppw ? (std::atoi(e_ppw) == 1 ? 1 : 4) : (B == 1 ? 1 : 4);
         const char* fz = std::getenv("ORBHIP_BA_FUSED");   // per call: the tests compare both forms
         const bool fuse_env = !(fz && fz[0] == '0');
-        bool fused = all_small && fuse_env;
+        // (r06: every unsharded problem, small or not; a sharded trial ends in the split controller)
+        bool fused = !sharded && fuse_env;
         for (int b = 0; b < B && fused; b++) fused = (int)gbs <= ha[b].npart_e && pp[b].P <= kFusedMaxP;
         if (fused) {
             for (int b = 0; b < B; b++) ha[b].fused = 1;

@@ -94,6 +94,30 @@ def test_rejected_trials_restore_across_workgroups(opt, oracle, monkeypatch, fus
     assert dp < 1e-3, dp
 
 
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_rejected_trials_large_problem_path(opt, oracle, monkeypatch, fused):
+    """The path of problems too large for the trial's last work-group to restore (8 P + 3 M above
+    ORBHIP_BA_SMALL_WORDS, 32768 by default; forced to 0 here on the problem above that rejects
+    trials): since r06 their trials are fused too (back-substitution + errors in one launch, the new
+    poses committed by the controller's work-group), a rejected trial's points restored by k_ba_pop
+    and its errors refreshed by the next build's k_ba_errors. Both trial forms equal the oracle."""
+    monkeypatch.setenv("ORBHIP_BA_FUSED", fused)
+    monkeypatch.setenv("ORBHIP_BA_SMALL_WORDS", "0")
+    prob, _ = synthetic_ba_problem(n_kf=50, n_pts=3000, seed=31, rot_noise=0.1, trans_noise=0.2, pt_noise=0.5)
+    prob.pose_fixed[:2] = 1
+    prob.iterations = 10
+    g = opt.solve(prob)
+    o = oracle.ba_solve(prob)
+    assert o["lm_trials"] > o["iterations_done"]   # rejected trials happened
+    assert g.iterations_done == o["iterations_done"] and g.lm_trials == o["lm_trials"]
+    assert abs(g.final_chi2 - o["final_chi2"]) <= REL * abs(o["final_chi2"])
+    dq = np.abs(_qsign(g.pose_q) - _qsign(o["pose_q"])).max()
+    dt = np.abs(g.pose_t.astype(np.float64) - o["pose_t"]).max() / max(1.0, np.abs(o["pose_t"]).max())
+    assert dq < REL and dt < REL, (dq, dt)
+    dp = np.abs(g.points.astype(np.float64) - o["points"]).max() / max(1.0, np.abs(o["points"]).max())
+    assert dp < 1e-3, dp
+
+
 def test_gba_no_robust_kernel(opt, oracle):
     prob, _ = synthetic_ba_problem(n_kf=25, n_pts=800, seed=10)
     prob.huber_delta = 0.0           # BundleAdjustment(bRobust=false)
