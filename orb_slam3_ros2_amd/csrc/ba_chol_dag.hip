@@ -667,11 +667,21 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         for (int i = tid; i < NT; i += blockDim.x) need[i] = a.tasks[a.toff[a.G] + i];
     int c1 = 0, c2 = 0;
     // ---- prologue: wave 0 factors tile 0; T_0 = A(1, 0), D'_1 = A(1, 1), L1 = L2 = 0 ----
+    // every prologue load in one round trip: wave 0's tile-0 quadrants with the others, and tile
+    // (1, 0) loaded whatever row_first says (a load chosen by a.rf[1] waited for that load first:
+    // r06, ~5.3k cycles to the prologue's barrier at n = 294)
+    double4_t q00 = {0, 0, 0, 0}, q10 = {0, 0, 0, 0}, q11 = {0, 0, 0, 0};
+    if (wid == 0) {
+        q00 = s_quad(a, 0, 0, 0, 0);
+        q10 = s_quad(a, 0, 0, 1, 0);
+        q11 = s_quad(a, 0, 0, 1, 1);
+    }
     sq(lds + 2048 + quad * 256, double4_t{0, 0, 0, 0});
     sq(lds + 4096 + quad * 256, double4_t{0, 0, 0, 0});
     if (NT > 1) {
-        sq(lds + 6144 + quad * 256, a.rf[1] <= 0 ? s_quad(a, 1, 0, rq, cq) : double4_t{0, 0, 0, 0});
-        sq(lds + 8192 + quad * 256, s_quad(a, 1, 1, rq, cq));
+        const double4_t t10 = s_quad(a, 1, 0, rq, cq), t11 = s_quad(a, 1, 1, rq, cq);
+        sq(lds + 6144 + quad * 256, a.rf[1] <= 0 ? t10 : double4_t{0, 0, 0, 0});
+        sq(lds + 8192 + quad * 256, t11);
         if (cq == 0 && rg == 0) {
             const int i = kT + 16 * rq + cc;
             rppB[16 * rq + cc] = s_rhs(a, i);
@@ -679,13 +689,11 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     }
     if (tid < kT) rvec[tid] = s_rhs(a, tid);
     __syncthreads();
+    if (dbg && tid == 0) dbg[6] = __builtin_amdgcn_s_memtime() - t_start;
     if (wid == 0) {
         double4_t lin11, l21t;
-        // tile 0's three quadrants in one global round trip (part B's were loaded after part A's
-        // pivots, behind their asm blocks). (r06: issuing them before the prologue's barrier, with
-        // wave 0 skipping it, measured the same: 81.2-82.1 against 80.7-81.1 us at n = 294)
-        const double4_t q00 = s_quad(a, 0, 0, 0, 0), q10 = s_quad(a, 0, 0, 1, 0), q11 = s_quad(a, 0, 0, 1, 1);
         ok = diag_part_a(q00, lds, lin11, lds + 10240);
+        if (dbg && lane == 0) dbg[7] = __builtin_amdgcn_s_memtime() - t_start;
         wave_lds_sync();
         const double y0 = quad_matvec(lds, 0, rvec);
         if (rg == 0) ys[cc] = y0;

@@ -647,7 +647,10 @@ template <int WR>
 struct FastShape {
     static constexpr bool full = WR >= kWinMax;
     static constexpr int wmax = full ? kWinMax : 45;        // window columns
-    static constexpr int pwp = ((wmax + 3 + 3) / 4) * 4;     // pair-window row pitch (dwords): 48 / 84
+    // pair-window row pitch (dwords): 48 / 84. (r06 A/B: 68, which is the cells' dc = 36 mod 32, so
+    // that each half-wave of the pair test reads 32 consecutive banks, took k_fast_cells at C3 0.353
+    // -> 0.41 ms: the larger window costs work-groups per CU)
+    static constexpr int pwp = ((wmax + 3 + 3) / 4) * 4;
     static constexpr int pwr = (WR - 6 + 1) / 2 + 6;         // pair-window rows: 28 / 43
     static constexpr int mp = full ? 80 : 48;                // strength map row pitch (bytes) >= dc + 2
     static constexpr int mr = WR - 4;                        // strength map rows dr + 2

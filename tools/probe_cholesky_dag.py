@@ -53,7 +53,7 @@ for n_s, shape in cases:
     if os.environ.get("ORBHIP_PROBE_SAVE"):   # raw per-interval words for offline analysis
         np.save(os.path.join(os.environ["ORBHIP_PROBE_SAVE"], f"dag_{n}_{shape}.npy"), dbg)
     print(f"n={n} {shape}: rc={rc} dag {ms.value * 1e3:.1f} us relerr={err:.2e} | cycles prologue={dbg[0]} "
-          f"forward={dbg[1]} backward={dbg[2]} diag={dbg[4]} total={dbg[5]} | interval medians: total {med[0]} "
+          f"forward={dbg[1]} backward={dbg[2]} diag={dbg[4]} total={dbg[5]} (prologue: barrier {dbg[6]}, part A {dbg[7]}) | interval medians: total {med[0]} "
           f"| wave ends {med[0 + 1]} {int(np.median(ph[:, 2] & 0xFFFFFFFF)) if ki else 0} {med[3]} {med[4]} "
           f"w3 flags in {int(np.median(ph[:, 2] >> 32)) if ki else 0} w0 start {int(np.median(ph[:, 5] & 0xFFFFFFFF)) if ki else 0} "
           f"pre-diag {int(np.median(ph[:, 5] >> 32)) if ki else 0} ({time.time() - t0:.1f}s)", flush=True)
