@@ -62,13 +62,14 @@ struct BaArgs {
     int sync;          // sharded device-driven rounds: the controller's reductions and decisions run as their
                        // own launches (a collective between them), not in the last workgroup of k_ba_lin /
                        // k_ba_errors(2)
-    // Schur work items (k_ba_schur_items): {k0, k1, blk, slot} over blk_pairs, at most kSchurChunk
-    // pairs each; slot -1 = the block's only item (written to S directly), else its partial sum
-    // goes to Spart[36 slot] and k_ba_schur_fin adds the block's partials (+ Hpp + lambda on the
-    // diagonal) in order. fin: {blk, first slot, count} per such block.
+    // Schur work items (k_ba_schur_items): {k0, k1, blk, slot} over blk_pairs; slot -1 = the
+    // block's only item (written to S directly), else the block's chunk `slot` (the chunks of a
+    // block sit in one work-group of 128 items and are summed there, + Hpp + lambda on the
+    // diagonal; blk -1 = padding). fin: {blk, first slot, count} per such block; ifin: each item's
+    // fin entry (-1: none)
     const int* items; int nitems;
     const int* fin; int nfin;
-    double* Spart;
+    const int* ifin;
     LmCtl* ctl;        // device-driven solve: this problem's LM state (nullptr: host-driven rounds)
     double* part;      // workgroup partial sums of a trial: chi2 (npart_e = ceil(E / 256)), then the
     int npart_e, npart_m;   // landmark scale terms (npart_m = ceil(M / 256)); in the build phase

@@ -16,7 +16,7 @@
 //   k_ba_schur_points  setLambda on Hll, Dinv (Eigen 3x3 cofactor inverse), db
 //   k_ba_schur_items   S_ij = [i==j](Hpp_i + lambda I) - sum W_a Hpl_b^T over shared landmarks,
 //                      matrix-free; its trailing workgroups compute b_schur = b_p - sum Hpl db
-//   k_ba_schur_fin     the blocks' chunk partials summed in order (deterministic, no atomics)
+//                      (a block of several items: its last item adds their partials in order)
 //   k_chol_dag / k_ba_chol_reg / k_ba_cholesky / k_cb_*   the reduced camera system (ba_chol_*)
 //   k_ba_backsub       xl = Dinv (b_l - Hpl^T xp), X += xl (push: old X saved)
 //                      and T <- exp(xp) * T (SE3Quat::exp, operator*)   (push: old T saved)
@@ -656,6 +656,7 @@ __global__ __launch_bounds__(256) void k_ba_zero_s(const BaArgs* __restrict__ ar
 //   W_a Hpl_b^T = Hpl_a Dinv_m Hpl_b^T = w_a w_b B_a^T (A_a Dinv_m A_b^T) B_b
 // with A, B rebuilt from the edges' stored (Pc, w) and the poses' R_lin: 17 doubles read per pair
 // (edge records + Dinv) instead of the 36 of stored W / Hpl blocks, and no W written per trial.
+constexpr int kItemsWg = 128;   // Schur work items per k_ba_schur_items work-group (two lanes each)
 __device__ __forceinline__ void schur_b_pose(const BaArgs& a, int i, int lane);
 // work-groups [nbi, gridDim.x) run k_ba_schur_b's poses instead (it reads only k_ba_schur_points'
 // db and the linearisation: no dependence on the items, one launch less per trial)
@@ -673,9 +674,10 @@ __global__ __launch_bounds__(256) void k_ba_schur_items(const BaArgs* __restrict
     }
     const int gt = bx_ * blockDim.x + threadIdx.x;
     const int it = gt >> 1, h = gt & 1;
-    if (it >= a.nitems) return;
-    const int4 wi = ((const int4*)a.items)[it];
-    const int bi = a.blk_i[wi.z], bj = a.blk_j[wi.z];
+    const int lane = threadIdx.x & 63;
+    const bool valid = it < a.nitems;   // no early exit: the whole wave meets at the ballot below
+    const int4 wi = valid ? ((const int4*)a.items)[it] : make_int4(0, 0, 0, -1);
+    const int bi = valid && wi.z >= 0 ? a.blk_i[wi.z] : 0, bj = valid && wi.z >= 0 ? a.blk_j[wi.z] : 0;
     double Ri[9], Rj[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) { Ri[k] = a.R_lin[9 * bi + k]; Rj[k] = a.R_lin[9 * bj + k]; }
@@ -744,48 +746,58 @@ __global__ __launch_bounds__(256) void k_ba_schur_items(const BaArgs* __restrict
 #pragma unroll
             for (int cc = 0; cc < 6; cc++) s[6 * rr + cc] -= u0[rr] * CB0[cc] + u1[rr] * CB1[cc];
     }
-    if (wi.w < 0) {   // the block's only item: straight into S (both triangles)
+    // r06: a block's chunks (consecutive items, all in this work-group: prepare pads) are summed
+    // here, not by a finisher launch. Per wave run of one block a segmented shuffle tree (fixed
+    // order: deterministic) leaves the run's sum in its head pair, which puts it in LDS at its item
+    // position; after the barrier the block's first pair adds its later runs (they start at wave
+    // boundaries) and writes S. (r06 first tries handed the partials over through global memory
+    // to the block's last arrival: agent-scope stores, an atomic count and loads, 11 + 6 us
+    // (items + finisher) -> 26-43 us per C4 trial.)
+    const int myf = valid && wi.w >= 0 ? a.ifin[it] : -1;
+    const int prevf = __shfl(myf, (lane + 62) & 63, 64), nextf = __shfl(myf, (lane + 2) & 63, 64);
+    const unsigned long long ends = __ballot(h == 0 && myf >= 0 && (lane >= 62 || nextf != myf));
+    const int endl = myf >= 0 ? __ffsll((long long)(ends >> (lane & ~1))) - 1 + (lane & ~1) + h : 0;
 #pragma unroll
-        for (int r = 0; r < 3; r++) {
-            const int rr = 3 * h + r;
+    for (int off = 2; off < 64; off <<= 1) {
+        const bool take = myf >= 0 && lane + off <= endl;
 #pragma unroll
-            for (int cc = 0; cc < 6; cc++) {
-                a.S[(size_t)(6 * bi + rr) * a.n + 6 * bj + cc] = s[6 * r + cc];
-                a.S[(size_t)(6 * bj + cc) * a.n + 6 * bi + rr] = s[6 * r + cc];
+        for (int k = 0; k < 18; k++) {
+            const double o = __shfl(s[k], (lane + off) & 63, 64);
+            if (take) s[k] += o;
+        }
+    }
+    __shared__ double runs[kItemsWg * 36];   // a run's sum at its head item's position
+    const int li = it & (kItemsWg - 1);
+    if (myf >= 0 && (lane < 2 || prevf != myf))
+#pragma unroll
+        for (int k = 0; k < 18; k++) runs[36 * li + 18 * h + k] = s[k];
+    __syncthreads();
+    if (myf >= 0 && wi.w == a.fin[3 * myf + 1]) {   // the block's first chunk (a run head)
+        const int nch = a.fin[3 * myf + 2];
+        for (int c = 32 - (li & 31); c < nch; c += 32)   // the runs after the first: wave starts
+#pragma unroll
+            for (int k = 0; k < 18; k++) s[k] += runs[36 * (li + c) + 18 * h + k];
+        if (bi == bj && (a.own ? a.own[bi] != 0 : a.lead != 0)) {   // pose side: Hpp + lambda
+            const double lambda = *a.lambda;
+#pragma unroll
+            for (int k = 0; k < 18; k++) {
+                const int rr = 3 * h + k / 6, cc = k % 6;
+                s[k] += a.Hpp_g[36 * bi + 6 * rr + cc] + (rr == cc ? lambda : 0.0);
             }
         }
-    } else {
-        double2* dst = (double2*)(a.Spart + 36 * (size_t)wi.w + 18 * h);
-#pragma unroll
-        for (int k = 0; k < 9; k++) dst[k] = make_double2(s[2 * k], s[2 * k + 1]);
+    } else if (!(valid && myf < 0 && wi.z >= 0)) {
+        return;   // not a block's writer (a later chunk, padding, past the items)
     }
-}
-
-// one wave per block with several items or on the diagonal: [i==j](Hpp_i + lambda I) + its partial
-// sums in item order (fixed order: deterministic)
-__global__ __launch_bounds__(256) void k_ba_schur_fin(const BaArgs* __restrict__ args, const int* __restrict__ act) {
-    BA_PROLOGUE
-    BA_PHASE(kPhTrial)
-    const int f = bx_ * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (f >= a.nfin || lane >= 36) return;
-    const int blk = a.fin[3 * f], slot0 = a.fin[3 * f + 1], nch = a.fin[3 * f + 2];
-    const int i = a.blk_i[blk], j = a.blk_j[blk];
-    const int rr = lane / 6, cc = lane - 6 * rr;
-    const bool pose_side = i == j && (a.own ? a.own[i] != 0 : a.lead != 0);
-    double s = pose_side ? a.Hpp_g[36 * i + 6 * rr + cc] + (rr == cc ? *a.lambda : 0.0) : 0.0;
-    const double* sp = a.Spart + 36 * (size_t)slot0 + lane;
-    int c = 0;
-    for (; c + 8 <= nch; c += 8) {   // eight loads in flight, summed in order
-        double v[8];
+    // straight into S (both triangles)
 #pragma unroll
-        for (int u = 0; u < 8; u++) v[u] = sp[36 * (c + u)];
+    for (int r = 0; r < 3; r++) {
+        const int rr = 3 * h + r;
 #pragma unroll
-        for (int u = 0; u < 8; u++) s += v[u];
+        for (int cc = 0; cc < 6; cc++) {
+            a.S[(size_t)(6 * bi + rr) * a.n + 6 * bj + cc] = s[6 * r + cc];
+            a.S[(size_t)(6 * bj + cc) * a.n + 6 * bi + rr] = s[6 * r + cc];
+        }
     }
-    for (; c < nch; c++) s += sp[36 * c];
-    a.S[(size_t)(6 * i + rr) * a.n + 6 * j + cc] = s;
-    if (i != j) a.S[(size_t)(6 * j + cc) * a.n + 6 * i + rr] = s;
 }
 
 // one wave per optimised pose: b_schur = b_p - sum_e Hpl_e db, Hpl_e db = w B^T (A db)
@@ -1540,6 +1552,7 @@ struct Prep {
     std::vector<int> row_first;   // blocked Cholesky structure: first 32-col tile per 32-row tile
     std::vector<int> cb_tiles, cb_off;   // blocked Cholesky: envelope tiles per panel (cb_envelope_tiles)
     std::vector<int> items, fin;  // Schur work items {k0, k1, blk, slot} and finisher blocks {blk, slot0, n}
+    std::vector<int> ifin;        // each item's finisher entry (-1: the block's only item)
     int nslot = 0;
     bool use_dag = false;         // the persistent tiled-DAG Cholesky (ba_chol_dag.hip)
     DagPlan dag;                  // its helper task lists
@@ -1551,7 +1564,7 @@ struct Prep {
     size_t o_dag = 0, o_dagi = 0;
     size_t o_red2 = 0;            // workgroup partials of a trial's chi2 / scale (BaArgs::part)
     // offsets (elements) into the packed buffers; see the segment map in ba_solve_batch
-    size_t o_chi2 = 0, o_state = 0, o_obs = 0, o_scr = 0, o_lin = 0, o_S = 0, o_L = 0, o_part = 0, o_int = 0;
+    size_t o_chi2 = 0, o_state = 0, o_obs = 0, o_scr = 0, o_lin = 0, o_S = 0, o_L = 0, o_int = 0;
 };
 
 // fn(i) for i in [0, n) on up to `threads` host threads (problems are independent)
@@ -1765,7 +1778,7 @@ void prep_reset(Prep& o) {
     o.rc = 0;
     o.P = o.M = o.E = o.np = o.n = o.nblk = 0;
     for (auto* v : {&o.opt, &o.pt_ptr, &o.pt_edges, &o.ps_ptr, &o.ps_edges, &o.blk_i, &o.blk_j, &o.blk_ptr,
-                    &o.blk_pairs, &o.row_first, &o.cb_tiles, &o.cb_off, &o.items, &o.fin})
+                    &o.blk_pairs, &o.row_first, &o.cb_tiles, &o.cb_off, &o.items, &o.fin, &o.ifin})
         v->clear();
     o.own.clear();
     o.nslot = 0;
@@ -1774,7 +1787,7 @@ void prep_reset(Prep& o) {
     o.nd = NdPlan{};
     o.dag_task_cap = 0;
     o.o_dag = o.o_dagi = o.o_red2 = 0;
-    o.o_chi2 = o.o_state = o.o_obs = o.o_scr = o.o_lin = o.o_S = o.o_L = o.o_part = o.o_int = 0;
+    o.o_chi2 = o.o_state = o.o_obs = o.o_scr = o.o_lin = o.o_S = o.o_L = o.o_int = 0;
 }
 
 inline void se3_from_float(const float* q, const float* t, double* out) {
@@ -1907,19 +1920,33 @@ int prepare(const orbhip_ba_problem* pr, Prep& o, int chunk, int threads) {
             o.row_first[R] = f;
         }
     }
-    // Schur work items: chunks of at most kSchurChunk pairs; a block with one off-diagonal chunk
-    // is written by its item, the others (and every diagonal block) through the finisher
+    // Schur work items: chunks of at most `chunk` pairs; a block with one off-diagonal chunk is
+    // written by its item, the others (and every diagonal block) are summed inside one work-group
+    // of k_ba_schur_items (r06): at most kItemsWg chunks per block (a longer block takes longer
+    // chunks), and a block that would straddle a work-group boundary starts the next work-group
+    // (empty items, blk -1, pad the one before)
     for (int b = 0; b < o.nblk; b++) {
         const int k0 = o.blk_ptr[b], k1 = o.blk_ptr[b + 1];
         const bool diag = o.blk_i[b] == o.blk_j[b];
         if (!diag && k1 - k0 <= chunk) {
             o.items.insert(o.items.end(), {k0, k1, b, -1});
+            o.ifin.push_back(-1);
             continue;
         }
-        const int nch = std::max(1, (k1 - k0 + chunk - 1) / chunk);
+        const int cb = std::max(chunk, (k1 - k0 + kItemsWg - 1) / kItemsWg);
+        const int nch = std::max(1, (k1 - k0 + cb - 1) / cb);
+        const int at = (int)(o.ifin.size() % kItemsWg);
+        if (at + nch > kItemsWg)
+            for (int q = at; q < kItemsWg; q++) {
+                o.items.insert(o.items.end(), {0, 0, -1, -1});
+                o.ifin.push_back(-1);
+            }
+        const int f = (int)(o.fin.size() / 3);
         o.fin.insert(o.fin.end(), {b, o.nslot, nch});
-        for (int c = 0; c < nch; c++)
-            o.items.insert(o.items.end(), {k0 + c * chunk, std::min(k1, k0 + (c + 1) * chunk), b, o.nslot + c});
+        for (int c = 0; c < nch; c++) {
+            o.items.insert(o.items.end(), {k0 + c * cb, std::min(k1, k0 + (c + 1) * cb), b, o.nslot + c});
+            o.ifin.push_back(f);
+        }
         o.nslot += nch;
     }
     tp[3] = tus();
@@ -1993,6 +2020,7 @@ struct BaWorkspace {
     std::vector<NdWorkspace*> nds;   // sharded solves by segments: one per shard of this process
     DBuf<double*> ptab;        // in-process shards: the collectives' pointer tables
     DBuf<int> dint4;           // RCCL: small consensus all-reduces (plan, stop)
+    DBuf<unsigned char> uadj;  // RCCL, replicated form: the union pose adjacency (all-reduce max)
     int* h_int4 = nullptr;     // pinned
 };
 
@@ -2111,6 +2139,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     const int seg0 = shard_mode == kShardRccl ? ws->rank * B : 0;   // segment of problem 0
     NdPlan ndp;
     bool nd_sh = false;
+    std::vector<int> ubi, ubj;   // the replicated form's union block structure (when dissected)
     if (shard_mode != kShardNone) {
         const char* e_snd = std::getenv("ORBHIP_SHARD_ND");
         const char* e_min = std::getenv("ORBHIP_ND_MIN");
@@ -2123,7 +2152,8 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             wl = std::max(wl, l);
             wc = std::max(wc, c);
         }
-        int ok = (!no_dag && !force_blocked && !(e_snd && e_snd[0] == '0') && pp[0].n >= nd_min) ? 1 : 0;
+        const bool ok_base = !no_dag && !force_blocked && pp[0].n >= nd_min;
+        int ok = (ok_base && !(e_snd && e_snd[0] == '0')) ? 1 : 0;
         if (shard_mode == kShardRccl) {   // the band over every rank's landmarks; the same B everywhere
             // words 3 / 4: the max of B and of -B agree only when every rank has the same B and
             // valid shards (an invalid rank sends INT_MAX)
@@ -2159,6 +2189,40 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 p.own.assign(p.np, 0);
                 for (int q = ndp.seg[r]; q < ndp.seg[r + 1]; q++) p.own[q] = 1;   // interior + own separator
             }
+        // r06: the replicated form (landmark shards, or segments whose landmarks cross) solves the
+        // summed S by nested dissection too when that pays, planned on the union of the shards'
+        // pose adjacencies (every rank derives the same plan from the same union); ORBHIP_ND=0
+        // keeps the plain DAG solve on the union envelope
+        const char* e_nd = std::getenv("ORBHIP_ND");
+        if (!nd_sh && ok_base && !no_nd && !(e_nd && e_nd[0] == '0')) {
+            const int np = pp[0].np;
+            std::vector<unsigned char> adj((size_t)np * np, 0);   // [max(i, j)][min(i, j)]
+            for (int b = 0; b < B; b++)
+                for (int k = 0; k < pp[b].nblk; k++) {
+                    const int i = pp[b].blk_i[k], j = pp[b].blk_j[k];
+                    adj[(size_t)std::max(i, j) * np + std::min(i, j)] = 1;
+                }
+            if (shard_mode == kShardRccl) {
+                BAOK(ws->uadj.ensure(adj.size()));
+                if (hipMemcpyAsync(ws->uadj.p, adj.data(), adj.size(), hipMemcpyHostToDevice, st) != hipSuccess ||
+                    ncclAllReduce(ws->uadj.p, ws->uadj.p, adj.size(), ncclUint8, ncclMax, ws->comm, st) != ncclSuccess ||
+                    hipMemcpyAsync(adj.data(), ws->uadj.p, adj.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                    hipStreamSynchronize(st) != hipSuccess)
+                    return ORBHIP_ERR_DEVICE;
+            }
+            for (int i = 0; i < np; i++)
+                for (int j = 0; j <= i; j++)
+                    if (adj[(size_t)i * np + j]) { ubi.push_back(j); ubj.push_back(i); }
+            NdPlan up;
+            if (nd_plan(np, ubi.data(), ubj.data(), (int)ubi.size(), 0, up))
+                for (int b = 0; b < B; b++) {
+                    pp[b].nd = up;
+                    pp[b].use_nd = true;
+                    pp[b].use_dag = false;
+                }
+            else
+                ubi.clear(), ubj.clear();
+        }
     }
     const bool sharded = shard_mode != kShardNone;
     // the per-panel tile lists / the DAG plans (RCCL shards: the envelope is the union over the
@@ -2205,7 +2269,6 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         nR = (nR + 1) & ~size_t(1);
         p.o_L = nR; nR += 1024 * ((n + 31) / 32);
         nR = (nR + 1) & ~size_t(1);
-        p.o_part = nR; nR += 36 * (size_t)p.nslot;
         p.o_red2 = nR;
         nR += std::max((E + 255) / 256 + (std::max(M, P) + kBsL - 1) / kBsL, (M + kLinL - 1) / kLinL + np_) + 2;
         if (p.use_dag) {   // 128-byte aligned
@@ -2214,7 +2277,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         }
         p.o_int = ni;
         ni += (P + 4) + 2 * E + (M + 1) + E + (np_ + 1) + p.ps_edges.size() + 3 * p.nblk + 1 + p.blk_pairs.size() +
-              p.row_first.size() + p.items.size() + p.fin.size() + p.cb_tiles.size() + 8 +
+              p.row_first.size() + p.items.size() + p.fin.size() + p.ifin.size() + p.cb_tiles.size() + 8 +
               (p.use_dag ? dag_ints(p.n) + p.dag_task_cap + 4 : 0) + (p.own.size() + 3) / 4 + 1;
     }
     const size_t sC = 0, sA = nC, sU = sA + nA, sR = (sU + nU + 15) & ~size_t(15);
@@ -2286,6 +2349,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.nitems = (int)(p.items.size() / 4);
         a.fin = dev(put(p.fin.data(), p.fin.size()));
         a.nfin = (int)(p.fin.size() / 3);
+        a.ifin = dev(put(p.ifin.data(), p.ifin.size()));
         a.row_first = dev(put(p.row_first.data(), p.row_first.size()));
         a.cb_tiles = p.cb_tiles.empty() ? nullptr : dev(put(p.cb_tiles.data(), p.cb_tiles.size()));
         a.own = nullptr;
@@ -2340,7 +2404,6 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.red = r;
         a.S = D + sR + p.o_S;
         a.Lsave = D + sR + p.o_L;
-        a.Spart = D + sR + p.o_part;
         a.part = D + sR + p.o_red2;
         a.npart_e = (int)((E + 255) / 256);
         a.npart_m = (int)((std::max(M, (size_t)P) + kBsL - 1) / kBsL);   // k_ba_backsub_errs' workgroups
@@ -2398,7 +2461,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     const double t_pack = now();
     static LdsAttrOnce chol_attr;   // per device, thread-safe (dev_attr.h)
     BAOK(chol_attr.ensure((const void*)k_ba_cholesky, 160 * 1024));
-    int maxM = 0, maxE = 0, maxP = 0, maxNp = 0, maxBlk = 0, maxN = 0, maxItems = 0, maxFin = 0;
+    int maxM = 0, maxE = 0, maxP = 0, maxNp = 0, maxBlk = 0, maxN = 0, maxItems = 0;
     bool s_written = false;
     // "large": solved on its own (DAG or blocked); the rest share one single-workgroup launch
     auto large = [&](int b) { return pp[b].use_nd || pp[b].use_nd_sh || pp[b].use_dag || pp[b].n > kCholSmallN; };
@@ -2406,7 +2469,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         const Prep& p = pp[b];
         maxM = std::max(maxM, p.M); maxE = std::max(maxE, p.E); maxP = std::max(maxP, p.P);
         maxNp = std::max(maxNp, p.np); maxBlk = std::max(maxBlk, p.nblk);
-        maxItems = std::max(maxItems, (int)(p.items.size() / 4)); maxFin = std::max(maxFin, (int)(p.fin.size() / 3));
+        maxItems = std::max(maxItems, (int)(p.items.size() / 4));
         if (!large(b)) maxN = std::max(maxN, p.n);
         if (!p.use_dag && !p.use_nd && !p.use_nd_sh && p.n > kCholRegMaxN) s_written = true;   // the LDS and blocked solvers factor S in place
     }
@@ -2419,7 +2482,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     auto large_solve = [&](int b, const int* gate) -> int {
         if (pp[b].use_nd) {
             (void)gate;   // set at nd_setup
-            BAOK(nd_solve(ws->nd, st));
+            BAOK(nd_solve(B == 1 ? ws->nd : ws->nds[b], st));
         } else if (pp[b].use_dag) {
             BAOK(chol_dag_solve(ha[b].S, pp[b].n, ha[b].row_first, ha[b].bs, ha[b].x, ha[b].flag, dd[b], st, gate));
         } else {
@@ -2474,11 +2537,15 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             c.early_stop = probs[b]->early_stop;
         }
         BAOK(hipMemcpyAsync(dctl, ws->hctl.p, B * sizeof(LmCtl), hipMemcpyHostToDevice, st));
+        if (B > 1)   // shards of the replicated form: each solves the summed S in its own workspace
+            while (ws->nds.size() < (size_t)B) ws->nds.push_back(nd_create());
         for (int b = 0; b < B; b++)
             if (pp[b].use_nd) {
                 if (!ws->nd) ws->nd = nd_create();
-                const int rc = nd_setup(ws->nd, pp[b].nd, pp[b].blk_i.data(), pp[b].blk_j.data(), pp[b].nblk, ha[b].S,
-                                        ha[b].bs, ha[b].x, ha[b].flag, &dctl[b].phase, st);
+                const bool uni = !ubi.empty();
+                const int rc = nd_setup(B == 1 ? ws->nd : ws->nds[b], pp[b].nd, uni ? ubi.data() : pp[b].blk_i.data(),
+                                        uni ? ubj.data() : pp[b].blk_j.data(), uni ? (int)ubi.size() : pp[b].nblk,
+                                        ha[b].S, ha[b].bs, ha[b].x, ha[b].flag, &dctl[b].phase, st);
                 // a plan the device setup refuses (a segment beyond the back-substitution's LDS, a
                 // separator system beyond the DAG solver; the planner rejects both, so this is a
                 // guard): the same problem again on the plain DAG solve, nothing was run yet
@@ -2632,7 +2699,6 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             if (!fused) hipLaunchKernelGGL(k_ba_schur_points, dim3(gx(maxM, 256), B), b256, 0, st, dA, d_act);
             hipLaunchKernelGGL(k_ba_schur_items, dim3(gx(2 * maxItems, 256) + gx(maxNp, 4) + 1, B), b256, 0, st, dA,
                                d_act, (int)gx(2 * maxItems, 256), donep);
-            hipLaunchKernelGGL(k_ba_schur_fin, dim3(gx(maxFin, 4), B), b256, 0, st, dA, d_act);
             if (nd_sh) {   // each shard its segment; the separator system and x summed over the shards
                 for (int b = 0; b < B; b++) BAOK(nd_factor_assemble(ws->nds[b], st));
                 for (int b = 0; b < B; b++) BAOK(nd_sep_pack(ws->nds[b], 0, st));
@@ -2762,7 +2828,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     std::vector<const int*> tw;   // the timeout words of every persistent solve of this call
     for (int b = 0; b < B; b++) {
         if (pp[b].use_dag) tw.push_back(dd[b].ints + 3);
-        if (pp[b].use_nd) nd_timeout_words(ws->nd, tw);
+        if (pp[b].use_nd) nd_timeout_words(B == 1 ? ws->nd : ws->nds[b], tw);
         if (pp[b].use_nd_sh) nd_timeout_words(ws->nds[b], tw);
     }
     const int ndag = (int)tw.size();

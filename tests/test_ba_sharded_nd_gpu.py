@@ -27,16 +27,17 @@ def _close(g, o):
     assert np.abs(g.points.astype(np.float64) - o["points"]).max() / max(1.0, np.abs(o["points"]).max()) < REL
 
 
-def _solve_segments(opt, p, K, dissected=True, rccl=False):
+def _solve_segments(opt, p, K, per2=True, rccl=False):
     from orb_slam3_ros2_amd.sharding import merge_results_nd, shard_problem_nd
     parts = [shard_problem_nd(p, r, K) for r in range(K)]
     l0 = opt.stats()["dag_launches"]
     shards = [q[0] for q in parts]
     res = opt.solve_sharded_segments(shards) if rccl else opt.solve_shards_local(shards)
     # the dissected form launches two persistent solves per shard and trial (its segment's partial
-    # factorization, the separator system), the replicated form one (the summed S)
+    # factorization, the separator system), so does the replicated form when it dissects the summed
+    # S (r06, its union adjacency); on the plain DAG solve (ORBHIP_ND=0) it launches one
     per = (opt.stats()["dag_launches"] - l0) / (K * res[0].lm_trials)
-    assert per >= 2 if dissected else per < 2, per
+    assert per >= 2 if per2 else per < 2, per
     for r in res[1:]:
         assert np.array_equal(r.pose_t, res[0].pose_t)   # every shard applies the same pose update
     return merge_results_nd(p, res, [q[1] for q in parts], [q[2] for q in parts])
@@ -59,12 +60,17 @@ def test_loop_segment_shards_parity(oracle, n_kf, K, monkeypatch):
     _close(_solve_segments(Optimizer(), p, K), oracle.ba_solve(p))
 
 
-def test_segment_shards_replicated_fallback(c5_case, monkeypatch):
-    """ORBHIP_SHARD_ND=0: the same shards sum S itself and every shard solves it (replicated)."""
+@pytest.mark.parametrize("nd", [1, 0])
+def test_segment_shards_replicated_fallback(c5_case, monkeypatch, nd):
+    """ORBHIP_SHARD_ND=0: the same shards sum S itself and every shard solves it (replicated), by
+    nested dissection of the summed S planned on the shards' union adjacency (nd=1), or on the
+    plain DAG solve over the union envelope (ORBHIP_ND=0)."""
     from orb_slam3_ros2_amd import Optimizer
     monkeypatch.setenv("ORBHIP_SHARD_ND", "0")
+    if not nd:
+        monkeypatch.setenv("ORBHIP_ND", "0")
     _, p, o = c5_case
-    _close(_solve_segments(Optimizer(), p, 4, dissected=False), o)
+    _close(_solve_segments(Optimizer(), p, 4, per2=bool(nd)), o)
 
 
 def _rccl_optimizer():
@@ -82,9 +88,29 @@ def test_c5_rccl_rank_segments_parity(c5_case, K):
     _close(_solve_segments(_rccl_optimizer(), p, K, rccl=True), o)
 
 
-def test_c5_rccl_rank_segments_replicated(c5_case, monkeypatch):
+@pytest.mark.parametrize("nd", [1, 0])
+def test_c5_rccl_rank_segments_replicated(c5_case, monkeypatch, nd):
     """ORBHIP_SHARD_ND=0 over RCCL with 4 local shards: S summed on the device, all-reduced in full,
-    copied to the other shards; every shard solves it on the union envelope's DAG plan."""
+    copied to the other shards; every shard solves it by the dissection planned on the union
+    adjacency (all-reduced, nd=1) or on the union envelope's DAG plan (ORBHIP_ND=0)."""
     monkeypatch.setenv("ORBHIP_SHARD_ND", "0")
+    if not nd:
+        monkeypatch.setenv("ORBHIP_ND", "0")
     _, p, o = c5_case
-    _close(_solve_segments(_rccl_optimizer(), p, 4, dissected=False, rccl=True), o)
+    _close(_solve_segments(_rccl_optimizer(), p, 4, per2=bool(nd), rccl=True), o)
+
+
+@pytest.mark.parametrize("nd", [1, 0])
+def test_c5_rccl_landmark_shard_dissected(c5_case, monkeypatch, nd):
+    """The landmark-shard form on one RCCL rank (orbhip_ba_solve_sharded: S all-reduced over its
+    union envelope, packed): the summed S solved by the dissection planned on the all-reduced
+    union adjacency (two persistent solves per trial), or by the plain DAG solve (ORBHIP_ND=0)."""
+    if not nd:
+        monkeypatch.setenv("ORBHIP_ND", "0")
+    _, p, o = c5_case
+    opt = _rccl_optimizer()
+    l0 = opt.stats()["dag_launches"]
+    g = opt.solve_sharded(p)
+    per = (opt.stats()["dag_launches"] - l0) / g.lm_trials
+    assert per >= 2 if nd else per < 2, per
+    _close(g, o)

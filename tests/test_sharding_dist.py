@@ -1,7 +1,10 @@
 """N > 1 path on the CPU (gloo, world size 2): landmark shards partition the problem, and the
 shards' partial reduced camera systems sum (all_reduce) to the full system — the identity the
 RCCL all-reduce of orbhip_ba_solve_sharded relies on — also when only their
-union envelope is packed and summed (the blocked-solver sizes)."""
+union envelope is packed and summed (the blocked-solver sizes) — and (r06) the replicated form's
+nested dissection: the shards' pose adjacencies all-reduced (max) give the summed system's block
+structure, and the dissection planned on it (interiors eliminated, the separator system solved,
+back-substitution) solves the summed system."""
 import os
 
 import numpy as np
@@ -68,10 +71,61 @@ def _worker(rank, port, q):
         env = lower & (cols >= 32 * rf[rows // 32])
         assert not np.any(Sf[lower & ~env]), "a non-zero of the summed S outside the union envelope"
         d_env = float(np.abs(Senv - Sf)[env].max() / scale)
+        # 4. the replicated form's dissection (ba_solve_batch: union adjacency, nd_plan, nd_setup)
+        d_nd = _nd_union_check(rank, dist, torch)
         q.put((rank, max(float(np.abs(St.numpy() - Sf).max() / scale), d_env),
-               float(np.abs(bt.numpy() - bf).max() / np.abs(bf).max())))
+               float(np.abs(bt.numpy() - bf).max() / np.abs(bf).max()), d_nd))
     finally:
         dist.destroy_process_group()
+
+
+def _nd_union_check(rank, dist, torch):
+    """A 24-keyframe loop (window 4) in landmark shards: each rank's pose adjacency as a byte map,
+    all-reduced with MAX (the ncclUint8 all-reduce of the replicated form), must equal the summed
+    system's block structure; the two-segment cyclic dissection planned on it (nd_plan_band:
+    w = the cyclic half-bandwidth, segment r = interior [seg_r, seg_r+1 - w) + separator
+    [seg_r+1 - w, seg_r+1)) solves S + lambda I by interior elimination, the separator system and
+    back-substitution. Returns the relative difference to the dense solve."""
+    from orb_slam3_ros2_amd.sharding import shard_problem
+    from orb_slam3_ros2_amd.synthetic import synthetic_ba_problem
+    from tests.ba_numpy import reduced_system
+    prob, _ = synthetic_ba_problem(n_kf=24, n_pts=480, layout="loop", window=4, seed=4)
+    sh = shard_problem(prob, rank, WORLD)[0]
+    S, bs = reduced_system(sh)
+    n = S.shape[0]
+    npz = n // 6
+    blk = np.abs(S).reshape(npz, 6, npz, 6).max(axis=(1, 3)) > 0
+    adj = torch.from_numpy(np.tril(blk).astype(np.uint8))
+    dist.all_reduce(adj, op=dist.ReduceOp.MAX)
+    St, bt = torch.from_numpy(S.copy()), torch.from_numpy(bs.copy())
+    dist.all_reduce(St)
+    dist.all_reduce(bt)
+    Sf, bf = St.numpy() + 1e-3 * np.abs(St.numpy()).max() * np.eye(n), bt.numpy()
+    full = np.abs(Sf).reshape(npz, 6, npz, 6).max(axis=(1, 3)) > 0
+    assert np.array_equal(np.tril(full), adj.numpy().astype(bool)), "union adjacency != summed structure"
+    i, j = np.nonzero(adj.numpy())
+    d = np.abs(i - j)
+    wl, wc = int(d.max()), int(np.minimum(d, npz - d).max())
+    assert wl > wc   # cyclic
+    K, w = 2, wc
+    seg = [r * npz // K for r in range(K + 1)]
+    inter = [np.arange(seg[r], seg[r + 1] - w) for r in range(K)]
+    seps = [np.arange(seg[r + 1] - w, seg[r + 1]) for r in range(K)]
+    var = lambda poses: (6 * poses[:, None] + np.arange(6)).ravel()   # noqa: E731
+    I = [var(x) for x in inter]
+    Z = np.concatenate([var(x) for x in seps])
+    assert not np.any(Sf[np.ix_(I[0], I[1])]), "two interiors couple"
+    SZ, bZ = Sf[np.ix_(Z, Z)].copy(), bf[Z].copy()
+    for Ir in I:   # each interior eliminated (the partial factorizations), its fill on the separators
+        A, C = Sf[np.ix_(Ir, Ir)], Sf[np.ix_(Z, Ir)]
+        SZ -= C @ np.linalg.solve(A, C.T)
+        bZ -= C @ np.linalg.solve(A, bf[Ir])
+    x = np.zeros(n)
+    x[Z] = np.linalg.solve(SZ, bZ)
+    for Ir in I:   # back-substitution of the interiors
+        x[Ir] = np.linalg.solve(Sf[np.ix_(Ir, Ir)], bf[Ir] - Sf[np.ix_(Ir, Z)] @ x[Z])
+    xd = np.linalg.solve(Sf, bf)
+    return float(np.abs(x - xd).max() / np.abs(xd).max())
 
 
 def test_shards_sum_to_full_system_gloo():
@@ -88,8 +142,8 @@ def test_shards_sum_to_full_system_gloo():
         p.join(120)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     res = [q.get(timeout=5) for _ in range(WORLD)]
-    for rank, dS, db in res:
-        assert dS < 1e-12 and db < 1e-12, (rank, dS, db)
+    for rank, dS, db, dnd in res:
+        assert dS < 1e-12 and db < 1e-12 and dnd < 1e-9, (rank, dS, db, dnd)
 
 
 def test_shard_bounds_balance_edges():
