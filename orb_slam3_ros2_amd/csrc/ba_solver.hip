@@ -1150,10 +1150,27 @@ __global__ __launch_bounds__(256) void k_ba_backsub_errs(const BaArgs* __restric
     // this lane's edges of landmark m: its back-substitution terms (their loads go out first)
     int k0 = 0, k1 = 0;
     if (m < a.M) { k0 = a.pt_ptr[m]; k1 = a.pt_ptr[m + 1]; }
+    // r06: the landmark's own words and this lane's first two edges' observation words are loaded
+    // here, with the first loop's: after the barrier below everything would be loaded again, two
+    // dependent round trips (edge list -> edge words) in front of the errors
+    double Hm[9] = {}, blv[3] = {}, Xo[3] = {};
+    if (m < a.M) {
+#pragma unroll
+        for (int k = 0; k < 9; k++) Hm[k] = a.Hll[9 * m + k];
+#pragma unroll
+        for (int r = 0; r < 3; r++) { blv[r] = a.b[a.n + 3 * m + r]; Xo[r] = a.pts[3 * m + r]; }
+    }
+    int ce[2] = {-1, -1}, cp[2] = {0, 0};
+    double co0[2] = {0, 0}, co1[2] = {0, 0}, ci[2] = {0, 0};
     double c0 = 0.0, c1 = 0.0, c2 = 0.0;   // - sum_e Hpl_e^T xp over this lane's edges
-    for (int k = k0 + sub; k < k1; k += 4) {
+    for (int k = k0 + sub, j = 0; k < k1; k += 4, j++) {
         const int e = a.pt_edges[k];
-        const int oi = a.opt[a.e_pose[e]];
+        const int pe = a.e_pose[e];
+        if (j < 2) {
+            ce[j] = e; cp[j] = pe;
+            co0[j] = a.e_obs[2 * e]; co1[j] = a.e_obs[2 * e + 1]; ci[j] = a.e_info[e];
+        }
+        const int oi = a.opt[pe];
         if (oi < 0) continue;
         double A[6], B[12];
         const double w = lin_ab(a, e, oi, A, B);   // Hpl_e^T xp = w A^T (B xp)
@@ -1184,16 +1201,17 @@ __global__ __launch_bounds__(256) void k_ba_backsub_errs(const BaArgs* __restric
     c0 += __shfl_xor(c0, 2, 64); c1 += __shfl_xor(c1, 2, 64); c2 += __shfl_xor(c2, 2, 64);
     double sc = 0.0, Xn[3] = {0.0, 0.0, 0.0};
     if (m < a.M) {   // xl = Dinv (b_l - Hpl^T xp), X += xl (old X saved): every lane of the quad
-        const double* bl = a.b + a.n + 3 * m;
-        const double cv[3] = {bl[0] + c0, bl[1] + c1, bl[2] + c2};
-        double Di[9];
-        dinv_of(a, m, Di);
-        double* X = a.pts + 3 * m;
+        const double cv[3] = {blv[0] + c0, blv[1] + c1, blv[2] + c2};
         const double lambda = *a.lambda;
+        double D[9], Di[9];   // dinv_of's expressions on the preloaded Hll
+#pragma unroll
+        for (int k = 0; k < 9; k++) D[k] = Hm[k] + (k % 4 == 0 ? lambda : 0.0);
+        inv3(D, Di);
+        double* X = a.pts + 3 * m;
 #pragma unroll
         for (int r = 0; r < 3; r++) {
             const double xl = Di[3 * r] * cv[0] + Di[3 * r + 1] * cv[1] + Di[3 * r + 2] * cv[2];
-            const double xo = X[r];
+            const double xo = Xo[r];
             Xn[r] = xo + xl;
             if (sub == 0) {
                 a.x[a.n + 3 * m + r] = xl;
@@ -1201,15 +1219,37 @@ __global__ __launch_bounds__(256) void k_ba_backsub_errs(const BaArgs* __restric
                 // in this launch (ctl_end_body)
                 st_agent(a.pts_bak + 3 * m + r, xo);
                 st_agent(X + r, Xn[r]);
-                sc += xl * (lambda * xl + bl[r]);
+                sc += xl * (lambda * xl + blv[r]);
             }
         }
     }
     __syncthreads();   // the trial's poses in Tn
     double chi = 0.0;
-    for (int k = k0 + sub; k < k1; k += 4) {
-        const int e = a.pt_edges[k];
-        chi += edge_error_at(a, e, Tn + 8 * a.e_pose[e], Xn);
+    for (int k = k0 + sub, j = 0; k < k1; k += 4, j++) {
+        if (j < 2) {   // from the preloaded words (edge_error_at's expressions)
+            const int e = ce[j];
+            const double* T = Tn + 8 * cp[j];
+            double cx, cy, cz;
+            qrot(load_q(T), Xn[0], Xn[1], Xn[2], cx, cy, cz);
+            cx += T[4]; cy += T[5]; cz += T[6];
+            const double u = a.fx * cx / cz + a.cx, v = a.fy * cy / cz + a.cy;
+            const double e0 = co0[j] - u, e1 = co1[j] - v;
+            const double chi2 = ci[j] * (e0 * e0 + e1 * e1);
+            double r0 = chi2, r1 = 1.0;
+            if (a.delta > 0) {
+                const double dsqr = a.delta * a.delta;
+                if (chi2 > dsqr) {
+                    const double sq = sqrt(chi2);
+                    r0 = 2 * sq * a.delta - dsqr;
+                    r1 = a.delta / sq;
+                }
+            }
+            store_terms(a, e, e0, e1, chi2, r0, r1);
+            chi += r0;
+        } else {
+            const int e = a.pt_edges[k];
+            chi += edge_error_at(a, e, Tn + 8 * a.e_pose[e], Xn);
+        }
     }
     const double tc = block_sum(chi, sh);
     const double ts = block_sum(sc, sh);
