@@ -747,56 +747,53 @@ __global__ __launch_bounds__(256) void k_ba_schur_items(const BaArgs* __restrict
             for (int cc = 0; cc < 6; cc++) s[6 * rr + cc] -= u0[rr] * CB0[cc] + u1[rr] * CB1[cc];
     }
     // r06: a block's chunks (consecutive items, all in this work-group: prepare pads) are summed
-    // here, not by a finisher launch. Per wave run of one block a segmented shuffle tree (fixed
-    // order: deterministic) leaves the run's sum in its head pair, which puts it in LDS at its item
-    // position; after the barrier the block's first pair adds its later runs (they start at wave
-    // boundaries) and writes S. (r06 first tries handed the partials over through global memory
-    // to the block's last arrival: agent-scope stores, an atomic count and loads, 11 + 6 us
-    // (items + finisher) -> 26-43 us per C4 trial.)
+    // here, not by a finisher launch: every chunk's 36 values go to LDS at its item position and
+    // the pair holding a block's first chunk lists the block (per wave, 32 slots); after the
+    // barrier the work-group's threads take the listed blocks' entries, one (block, entry) each:
+    // Hpp + lambda (diagonal, pose side), then the chunks in order (the r05 finisher's order),
+    // into S. (r06 first tries: the partials handed over through global memory to the block's last
+    // arrival, agent-scope stores, an atomic count and loads: 11 + 6 us (items + finisher) ->
+    // 26-43 us per C4 trial; a segmented shuffle tree per wave run before an LDS hand-off: 16.5 us,
+    // 3.5 of them the tree; each wave summing its own blocks, 36 lanes per block: 15.5 us.)
+    __shared__ double parts[kItemsWg * 36];   // partial sums by item position in the work-group
+    __shared__ int4 blist[4 * 32];            // per wave: {first item position, chunks, i, j}
+    __shared__ int bcnt[4];
+    const int li = it & (kItemsWg - 1), wv = threadIdx.x >> 6;
     const int myf = valid && wi.w >= 0 ? a.ifin[it] : -1;
-    const int prevf = __shfl(myf, (lane + 62) & 63, 64), nextf = __shfl(myf, (lane + 2) & 63, 64);
-    const unsigned long long ends = __ballot(h == 0 && myf >= 0 && (lane >= 62 || nextf != myf));
-    const int endl = myf >= 0 ? __ffsll((long long)(ends >> (lane & ~1))) - 1 + (lane & ~1) + h : 0;
+    const bool first = myf >= 0 && h == 0 && wi.w == a.fin[3 * myf + 1];
+    const int nch0 = first ? a.fin[3 * myf + 2] : 0;
+    if (myf >= 0)
 #pragma unroll
-    for (int off = 2; off < 64; off <<= 1) {
-        const bool take = myf >= 0 && lane + off <= endl;
-#pragma unroll
-        for (int k = 0; k < 18; k++) {
-            const double o = __shfl(s[k], (lane + off) & 63, 64);
-            if (take) s[k] += o;
-        }
-    }
-    __shared__ double runs[kItemsWg * 36];   // a run's sum at its head item's position
-    const int li = it & (kItemsWg - 1);
-    if (myf >= 0 && (lane < 2 || prevf != myf))
-#pragma unroll
-        for (int k = 0; k < 18; k++) runs[36 * li + 18 * h + k] = s[k];
+        for (int k = 0; k < 18; k++) parts[36 * li + 18 * h + k] = s[k];
+    const unsigned long long om = __ballot(first);
+    if (first) blist[32 * wv + __popcll(om & ((1ull << lane) - 1))] = make_int4(li, nch0, bi, bj);
+    if (lane == 0) bcnt[wv] = __popcll(om);
     __syncthreads();
-    if (myf >= 0 && wi.w == a.fin[3 * myf + 1]) {   // the block's first chunk (a run head)
-        const int nch = a.fin[3 * myf + 2];
-        for (int c = 32 - (li & 31); c < nch; c += 32)   // the runs after the first: wave starts
+    if (valid && myf < 0 && wi.z >= 0) {   // a block of one chunk: straight into S (both triangles)
 #pragma unroll
-            for (int k = 0; k < 18; k++) s[k] += runs[36 * (li + c) + 18 * h + k];
-        if (bi == bj && (a.own ? a.own[bi] != 0 : a.lead != 0)) {   // pose side: Hpp + lambda
-            const double lambda = *a.lambda;
+        for (int r = 0; r < 3; r++) {
+            const int rr = 3 * h + r;
 #pragma unroll
-            for (int k = 0; k < 18; k++) {
-                const int rr = 3 * h + k / 6, cc = k % 6;
-                s[k] += a.Hpp_g[36 * bi + 6 * rr + cc] + (rr == cc ? lambda : 0.0);
+            for (int cc = 0; cc < 6; cc++) {
+                a.S[(size_t)(6 * bi + rr) * a.n + 6 * bj + cc] = s[6 * r + cc];
+                a.S[(size_t)(6 * bj + cc) * a.n + 6 * bi + rr] = s[6 * r + cc];
             }
         }
-    } else if (!(valid && myf < 0 && wi.z >= 0)) {
-        return;   // not a block's writer (a later chunk, padding, past the items)
     }
-    // straight into S (both triangles)
-#pragma unroll
-    for (int r = 0; r < 3; r++) {
-        const int rr = 3 * h + r;
-#pragma unroll
-        for (int cc = 0; cc < 6; cc++) {
-            a.S[(size_t)(6 * bi + rr) * a.n + 6 * bj + cc] = s[6 * r + cc];
-            a.S[(size_t)(6 * bj + cc) * a.n + 6 * bi + rr] = s[6 * r + cc];
-        }
+    const int n0 = bcnt[0], n1 = n0 + bcnt[1], n2 = n1 + bcnt[2], nb = n2 + bcnt[3];
+    if (nb == 0) return;
+    const double lambda = *a.lambda;
+    for (int q = threadIdx.x; q < 36 * nb; q += blockDim.x) {
+        const int g = q / 36, e = q - 36 * g;   // block g of the work-group's list, entry e
+        const int w = (g >= n0) + (g >= n1) + (g >= n2);
+        const int4 B = blist[32 * w + g - (w == 0 ? 0 : w == 1 ? n0 : w == 2 ? n1 : n2)];
+        const int i = B.z, j = B.w, rr = e / 6, cc = e - 6 * rr;
+        double acc = i == j && (a.own ? a.own[i] != 0 : a.lead != 0)
+                         ? a.Hpp_g[36 * i + 6 * rr + cc] + (rr == cc ? lambda : 0.0) : 0.0;
+        const double* pp = parts + 36 * B.x + e;
+        for (int c = 0; c < B.y; c++) acc += pp[36 * c];
+        a.S[(size_t)(6 * i + rr) * a.n + 6 * j + cc] = acc;
+        if (i != j) a.S[(size_t)(6 * j + cc) * a.n + 6 * i + rr] = acc;
     }
 }
 
