@@ -2549,6 +2549,20 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         if (hipStreamSynchronize(st) != hipSuccess) return true;
         return *ws->h_stop != 0;
     };
+    // ---- hand-off timeouts of the persistent solver: a timed-out solve fails its trial (flag 0),
+    // which must never pass for a g2o rejection. Counted per problem (control word 3), read with
+    // the outputs (no extra synchronisation), agreed over the ranks of a sharded solve. ----
+    std::vector<const int*> tw;   // the timeout words of every persistent solve of this call
+    int ndag = 0;
+    // the outputs: the timeout words, e_chi2 of every problem + optimised poses/points (one
+    // transfer); r06: enqueued behind the slots that may be the last ones, so a solve that ended
+    // there needs no further host round trip (a wasted copy of ~115 KB at C4 otherwise)
+    auto out_copies = [&]() -> int {
+        for (int i = 0; i < ndag; i++) BAOK(hipMemcpyAsync(ws->hto.p + i, tw[i], sizeof(int), hipMemcpyDeviceToHost, st));
+        BAOK(hipMemcpyAsync(hd, D, sizeof(double) * (nC + nA), hipMemcpyDeviceToHost, st));
+        return ORBHIP_OK;
+    };
+    bool outputs_in = false;
     std::vector<LmState> L(B);
     bool ctl_with_outputs = false;   // the final LM state is read back with the outputs
     std::vector<int> all(B);
@@ -2599,6 +2613,13 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                              ha[b].x, ha[b].flag, &dctl[b].phase, st, seg0 + b) != 0)
                     return ORBHIP_ERR_DEVICE;
         }
+        for (int b = 0; b < B; b++) {
+            if (pp[b].use_dag) tw.push_back(dd[b].ints + 3);
+            if (pp[b].use_nd) nd_timeout_words(B == 1 ? ws->nd : ws->nds[b], tw);
+            if (pp[b].use_nd_sh) nd_timeout_words(ws->nds[b], tw);
+        }
+        ndag = (int)tw.size();
+        if (ndag) BAOK(ws->hto.ensure(ndag));
         // ---- the collectives of a sharded slot: site s sums (or maxes) src[b] into dst[b] over the
         // shards; RCCL: one all-reduce of this rank's buffers ----
         enum { kHpp, kRed0, kRed2, kRed01, kRepS, kRepBs, kNdPack, kNdBz, kNdX, kSites };
@@ -2813,6 +2834,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         // the asynchronous done flags; the batch length comes from the LM state read back, which
         // every rank holds identically
         const bool rccl = shard_mode == kShardRccl;
+        bool last_ev_spec = false;   // the last event recorded follows the speculative copies
         while (remaining > 0 && rc == ORBHIP_OK) {
             if (rccl && !stop_sent && stop_now()) {
                 hipLaunchKernelGGL(k_ba_ctl_stop, gB, b256, 0, st, dctl, B, donep);
@@ -2828,15 +2850,25 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 const int n = std::min(kChunk, batch - k);
                 for (int j = 0; j < n && rc == ORBHIP_OK; j++) rc = slot();
                 k += n;
+                bool spec = false;   // this batch's last slots: the LM state and outputs behind them
+                if (rc == ORBHIP_OK && !rccl && k == batch) {
+                    spec = true;
+                    if (hipMemcpyAsync(ws->hctl.p, dctl, B * sizeof(LmCtl), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                        out_copies() != ORBHIP_OK)
+                        rc = ORBHIP_ERR_DEVICE;
+                }
                 if (rc == ORBHIP_OK && hipEventRecord(ev[nchunk & 1], st) != hipSuccess) rc = ORBHIP_ERR_DEVICE;
                 if (rc != ORBHIP_OK) break;
+                last_ev_spec = spec;
                 if (nchunk++ >= 1) rc = wait_ev(ev[nchunk & 1]);   // the chunk before this one
                 if (rc == ORBHIP_OK && !rccl && all_done()) break;
             }
             if (rc == ORBHIP_OK) rc = wait_ev(ev[(nchunk - 1) & 1]);
             if (rc != ORBHIP_OK) break;
             if (!rccl && all_done()) {   // every problem ended: its LM state comes with the outputs
-                ctl_with_outputs = true;
+                // (already in when the last event followed the speculative copies)
+                outputs_in = !rccl && last_ev_spec;
+                ctl_with_outputs = !outputs_in;
                 break;
             }
             if (hipMemcpyAsync(ws->hctl.p, dctl, B * sizeof(LmCtl), hipMemcpyDeviceToHost, st) != hipSuccess ||
@@ -2859,23 +2891,10 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         if (ctl_with_outputs) BAOK(hipMemcpyAsync(ws->hctl.p, dctl, B * sizeof(LmCtl), hipMemcpyDeviceToHost, st));
     }
     const double t_solve = now();
-    // ---- hand-off timeouts of the persistent solver: a timed-out solve fails its trial (flag 0),
-    // which must never pass for a g2o rejection. Counted per problem (control word 3), read with
-    // the outputs (no extra synchronisation), agreed over the ranks of a sharded solve. ----
-    std::vector<const int*> tw;   // the timeout words of every persistent solve of this call
-    for (int b = 0; b < B; b++) {
-        if (pp[b].use_dag) tw.push_back(dd[b].ints + 3);
-        if (pp[b].use_nd) nd_timeout_words(B == 1 ? ws->nd : ws->nds[b], tw);
-        if (pp[b].use_nd_sh) nd_timeout_words(ws->nds[b], tw);
+    if (!outputs_in) {   // (else the speculative copies below the last slots brought them)
+        if (out_copies() != ORBHIP_OK) return ORBHIP_ERR_DEVICE;
+        BAOK(hipStreamSynchronize(st));
     }
-    const int ndag = (int)tw.size();
-    if (ndag) {
-        BAOK(ws->hto.ensure(ndag));
-        for (int i = 0; i < ndag; i++) BAOK(hipMemcpyAsync(ws->hto.p + i, tw[i], sizeof(int), hipMemcpyDeviceToHost, st));
-    }
-    // ---- outputs: e_chi2 of every problem + optimised poses/points, one transfer ----
-    BAOK(hipMemcpyAsync(hd, D, sizeof(double) * (nC + nA), hipMemcpyDeviceToHost, st));
-    BAOK(hipStreamSynchronize(st));
     {   // the LM state of every problem (read back in the loop, or just now with the outputs)
         for (int b = 0; b < B; b++) {
             const LmCtl& c = ws->hctl.p[b];
