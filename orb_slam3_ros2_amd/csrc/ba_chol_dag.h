@@ -52,6 +52,7 @@ struct DagDev {
     const int* tasks;
     int G;
     int pb;              // DagPlan::pb
+    int need_off;        // toff[G]: the chain backward's column counts follow the tasks there
 };
 
 // S (n x n row-major, lower triangle read, never written), row_first (ceil(n/32): first 32-col

@@ -75,6 +75,7 @@ struct DagK {
     int* ints;
     const int* toff;
     const int* tasks;
+    int need_off;        // tasks[need_off ...]: the chain backward's column counts (DagDev::need_off)
     const int* gate;
     unsigned long long* dbg;
     int n, NT, G;
@@ -664,7 +665,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     // column k), after the helpers' task list
     int* need = rfl + NT;
     if (!a.pb && !a.nti)
-        for (int i = tid; i < NT; i += blockDim.x) need[i] = a.tasks[a.toff[a.G] + i];
+        for (int i = tid; i < NT; i += blockDim.x) need[i] = a.tasks[a.need_off + i];   // (r06: not behind a load of toff[G])
     int c1 = 0, c2 = 0;
     // ---- prologue: wave 0 factors tile 0; T_0 = A(1, 0), D'_1 = A(1, 1), L1 = L2 = 0 ----
     // every prologue load in one round trip: wave 0's tile-0 quadrants with the others, and tile
@@ -690,27 +691,6 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     if (tid < kT) rvec[tid] = s_rhs(a, tid);
     __syncthreads();
     if (dbg && tid == 0) dbg[6] = __builtin_amdgcn_s_memtime() - t_start;
-    if (wid == 0) {
-        double4_t lin11, l21t;
-        ok = diag_part_a(q00, lds, lin11, lds + 10240);
-        if (dbg && lane == 0) dbg[7] = __builtin_amdgcn_s_memtime() - t_start;
-        wave_lds_sync();
-        const double y0 = quad_matvec(lds, 0, rvec);
-        if (rg == 0) ys[cc] = y0;
-        ok = diag_part_b(q10, q11, lin11, lds, l21t, lds + 10240) && ok;
-        wave_lds_sync();
-        const double r1 = rvec[16 + cc] - lmul_ylds(l21t, ys);
-        wave_lds_sync();
-        if (rg == 0) rvec[16 + cc] = r1;
-        wave_lds_sync();
-        const double y1 = quad_matvec(lds, 3, rvec + 16);
-        if (rg == 0) ys[16 + cc] = y1;
-    }
-    __syncthreads();
-    if (dbg && tid == 0) dbg[0] = __builtin_amdgcn_s_memtime() - t_start;
-    // ---- interval k: wave 0 the critical path (row 0 of L(k+1, k), D(0,0), its pivot, then D22's
-    // after wave 1's row 1 / D(1,*)); wave 1 row 1 and the publishes; waves 2 / 3 row h of
-    // L(k+2, k), of T_{k+1} and of D'_{k+2} ----
     // a partial solve (nti > 0) runs intervals 0 .. nti-1: the last one forms the trailing block's
     // first tiles of L (rows of L(nti, nti-1) and L(nti+1, nti-1)) but factors no diagonal tile
     const int kEnd = a.nti ? a.nti : NT - 1;
@@ -760,34 +740,83 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     double4_t pd0 = {0, 0, 0, 0}, pd1 = {0, 0, 0, 0}, pe0 = {0, 0, 0, 0}, pe1 = {0, 0, 0, 0};
     double4_t pu[2] = {}, pt[2] = {}, pdd[2] = {};
     double prr = 0.0;
-    const bool pre = false;
-    auto fetch_in = [&](int kk, unsigned flk) {
+    // part: 1 the inputs read from S itself (no helper flag), 2 the helpers' tiles, 3 both. r06: the
+    // S part of interval kk goes out in interval kk-1 (the first touch of S costs ~5-7k cycles: the
+    // first two intervals took 17.8k / 19.7k cycles against ~12.6k at n = 294); its loads are old
+    // by the next interval's flag poll, which waits for them in the in-order vmcnt queue
+    auto fetch_in = [&](int kk, unsigned flk, int part) {
         const int h = wid - 2, kk1 = kk + 1, KK2 = kk + 2;
         auto F = [&](int b) { return ((flk >> b) & 1u) != 0u; };
-        const int tD = L.oL + (KK2 * NT + kk - 1) * kTD;
-        pd0 = pd1 = pe0 = pe1 = double4_t{0, 0, 0, 0};
-        if (F(6) || F(8) || F(11)) {   // useU || useTp || useP0c
-            pd0 = qload(rs, tD + (2 * h) * 256);
-            pd1 = qload(rs, tD + (2 * h + 1) * 256);
-        }
-        // quadrant (1, 0) of D'_{kk+2} needs both row halves of L(kk+2, kk-1): wave 3, which forms
-        // that term, loads the other half
-        if (F(11) && h == 1) {
-            pe0 = qload(rs, tD);
-            pe1 = qload(rs, tD + 256);
+        const bool ps = part & 1, ph = part & 2;
+        if (ph) {
+            const int tD = L.oL + (KK2 * NT + kk - 1) * kTD;
+            pd0 = pd1 = pe0 = pe1 = double4_t{0, 0, 0, 0};
+            if (F(6) || F(8) || F(11)) {   // useU || useTp || useP0c
+                pd0 = qload(rs, tD + (2 * h) * 256);
+                pd1 = qload(rs, tD + (2 * h + 1) * 256);
+            }
+            // quadrant (1, 0) of D'_{kk+2} needs both row halves of L(kk+2, kk-1): wave 3, which forms
+            // that term, loads the other half
+            if (F(11) && h == 1) {
+                pe0 = qload(rs, tD);
+                pe1 = qload(rs, tD + 256);
+            }
         }
 #pragma unroll
         for (int c = 0; c < 2; c++) {
-            pu[c] = !F(3) ? double4_t{0, 0, 0, 0}
-                          : (F(5) ? qload(rs, L.oP + (2 * NT + kk) * kTD + (2 * h + c) * 256) : s_quad(a, KK2, kk, h, c));
-            pt[c] = !F(4) ? double4_t{0, 0, 0, 0}
-                          : (F(7) ? qload(rs, L.oP + (NT + kk1) * kTD + (2 * h + c) * 256) : s_quad(a, KK2, kk1, h, c));
+            if (!F(3)) {
+                if (ps) pu[c] = double4_t{0, 0, 0, 0};
+            } else if (F(5)) {
+                if (ph) pu[c] = qload(rs, L.oP + (2 * NT + kk) * kTD + (2 * h + c) * 256);
+            } else if (ps) {
+                pu[c] = s_quad(a, KK2, kk, h, c);
+            }
+            if (!F(4)) {
+                if (ps) pt[c] = double4_t{0, 0, 0, 0};
+            } else if (F(7)) {
+                if (ph) pt[c] = qload(rs, L.oP + (NT + kk1) * kTD + (2 * h + c) * 256);
+            } else if (ps) {
+                pt[c] = s_quad(a, KK2, kk1, h, c);
+            }
             const int qd = 2 * h + c;   // D' quadrants: wave 2 q0, wave 3 q2 and q3
-            pdd[c] = (h == 0 && c == 1) ? double4_t{0, 0, 0, 0}
-                                        : (F(10) ? qload(rs, L.oP + KK2 * kTD + qd * 256) : s_quad(a, KK2, KK2, qd >> 1, qd & 1));
+            if (h == 0 && c == 1) {
+                if (ps) pdd[c] = double4_t{0, 0, 0, 0};
+            } else if (F(10)) {
+                if (ph) pdd[c] = qload(rs, L.oP + KK2 * kTD + qd * 256);
+            } else if (ps) {
+                pdd[c] = s_quad(a, KK2, KK2, qd >> 1, qd & 1);
+            }
         }
-        prr = F(10) ? ld_sc1(a.buf + L.oR + KK2 * kT + 16 * h + cc) : s_rhs(a, kT * KK2 + 16 * h + cc);
+        if (F(10)) {
+            if (ph) prr = ld_sc1(a.buf + L.oR + KK2 * kT + 16 * h + cc);
+        } else if (ps) {
+            prr = s_rhs(a, kT * KK2 + 16 * h + cc);
+        }
     };
+    // interval 0's inputs (all from S: no helper tile exists yet) go out now, under the prologue's
+    // factorization of tile 0
+    if (wid >= 2 && kEnd > 0 && 2 < NT) fetch_in(0, flags_of(0), 3);
+    if (wid == 0) {
+        double4_t lin11, l21t;
+        ok = diag_part_a(q00, lds, lin11, lds + 10240);
+        if (dbg && lane == 0) dbg[7] = __builtin_amdgcn_s_memtime() - t_start;
+        wave_lds_sync();
+        const double y0 = quad_matvec(lds, 0, rvec);
+        if (rg == 0) ys[cc] = y0;
+        ok = diag_part_b(q10, q11, lin11, lds, l21t, lds + 10240) && ok;
+        wave_lds_sync();
+        const double r1 = rvec[16 + cc] - lmul_ylds(l21t, ys);
+        wave_lds_sync();
+        if (rg == 0) rvec[16 + cc] = r1;
+        wave_lds_sync();
+        const double y1 = quad_matvec(lds, 3, rvec + 16);
+        if (rg == 0) ys[16 + cc] = y1;
+    }
+    __syncthreads();
+    if (dbg && tid == 0) dbg[0] = __builtin_amdgcn_s_memtime() - t_start;
+    // ---- interval k: wave 0 the critical path (row 0 of L(k+1, k), D(0,0), its pivot, then D22's
+    // after wave 1's row 1 / D(1,*)); wave 1 row 1 and the publishes; waves 2 / 3 row h of
+    // L(k+2, k), of T_{k+1} and of D'_{k+2} ----
     for (int k = 0; k < kEnd; k++) {
         const unsigned long long tk = dbg ? __builtin_amdgcn_s_memtime() : 0;
         const int k1 = k + 1, K2 = k + 2;
@@ -824,9 +853,9 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
 #define rp (rppB + 32 * cur)
 #define rpN (rppB + 32 * nxt)
         double* Dq = lds + 10240;
-        const int* f3 = wid >= 2 && !pre ? helper_flag(k) : nullptr;
+        const int* f3 = wid >= 2 ? helper_flag(k) : nullptr;
         const bool need3 = f3 != nullptr;
-        const int fv = wid >= 2 && !pre ? ld_flag(need3 ? f3 : L.ctl) : epoch;
+        const int fv = wid >= 2 ? ld_flag(need3 ? f3 : L.ctl) : epoch;
         if (wid == 0) {
             if (dbg && lane == 0) wts[6] = __builtin_amdgcn_s_memtime() - tk;
             // row 0 of L(k+1, k) = T Linv_k^T
@@ -961,9 +990,9 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
             // p <= k-2; p = k-1 and k here, quadrant (1,0)'s column k by wave 1 in the next interval)
             // and its rhs
             const int h = wid - 2;
-            const bool got = pre || __all(!need3 || fv == epoch) || wave_wait_all(f3, epoch, L.ctl, a.smax);
+            const bool got = __all(!need3 || fv == epoch) || wave_wait_all(f3, epoch, L.ctl, a.smax);
             if (dbg && lane == 0 && h == 1) wts[4] = __builtin_amdgcn_s_memtime() - tk;   // helpers' flags in
-            if (got && !pre) fetch_in(k, fl);
+            if (got) fetch_in(k, fl, 2);   // (the S part went out in the interval before / the prologue)
             if (dbg) {   // the loads in (diagnostics only)
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 DAG_STAMP(4 + 4 * h);
@@ -975,6 +1004,7 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 const double4_t d0 = pd0, d1 = pd1, e0 = pe0, e1 = pe1;
                 double4_t u[2] = {pu[0], pu[1]}, t[2] = {pt[0], pt[1]}, dd[2] = {pdd[0], pdd[1]};
                 double rr = prr;
+                if (k + 1 < kEnd && k + 3 < NT) fetch_in(k + 1, flags_of(k + 1), 1);   // the next interval's S part
                 // every LDS operand of this wave's MFMA work first (one LDS round trip), the MFMA
                 // chains two deep per product, the rhs terms (LDS + cross-row sums) after the tiles
                 const double4_t l1q[4] = {lq(L1), lq(L1 + 256), lq(L1 + 512), lq(L1 + 768)};
@@ -1425,13 +1455,14 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
     }
 }
 
-// one problem's workgroup: role 0 the chain, role h + 1 helper h
+// one problem's workgroup: role 0 the chain, role h + 1 helper h. ep: the epoch counter (read by
+// the kernel together with the gate word: r06, one dependent round trip less at kernel start)
 template <bool DBG>
-__device__ __forceinline__ void dag_run(const DagK& a, int role) {
+__device__ __forceinline__ void dag_run(const DagK& a, int role, int ep) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const Lay L(a);
     // epoch of this solve: the counter the last workgroup of the previous solve advanced
-    const int epoch = ld_flag(L.ctl) + 1;
+    const int epoch = ep + 1;
     const size_t bytes = dag_doubles_nt(a.NT) * 8;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.buf, 0, (int)bytes, 0x00020000);
     if (role == 0) dag_chain<DBG>(a, L, rs, epoch, lds);
@@ -1450,8 +1481,11 @@ __device__ __forceinline__ void dag_run(const DagK& a, int role) {
 
 template <bool DBG>
 __global__ __launch_bounds__(256) void k_chol_dag(DagK a) {
+    // the epoch load goes out with the gate's (the previous solve of this workspace is over: stream
+    // order; unused when the gate returns)
+    const int ep = ld_flag(Lay(a).ctl);
     if (a.gate && *a.gate != kPhTrial) return;   // device-driven LM: not in a trial (uniform)
-    dag_run<DBG>(a, blockIdx.x);
+    dag_run<DBG>(a, blockIdx.x, ep);
 }
 
 // several independent problems in one launch (the interiors of a nested dissection): problem p
@@ -1461,8 +1495,9 @@ __global__ __launch_bounds__(256) void k_chol_dag_multi(const DagK* __restrict__
     int p = 0;
     while (p + 1 < np && (int)blockIdx.x >= wg_off[p + 1]) p++;
     const DagK a = ks[p];
+    const int ep = ld_flag(Lay(a).ctl);
     if (a.gate && *a.gate != kPhTrial) return;
-    dag_run<false>(a, blockIdx.x - wg_off[p]);
+    dag_run<false>(a, blockIdx.x - wg_off[p], ep);
 }
 
 size_t dag_lds_bytes(int NT) {
@@ -1654,7 +1689,7 @@ hipError_t chol_dag_solve(const double* S, int n, const int* row_first, const do
     if (n <= 0 || n > kDagMaxN) return hipErrorInvalidValue;
     DagK a;
     a.S = S; a.bs = bs; a.x = x; a.flag = flag; a.rf = row_first;
-    a.buf = d.buf; a.ints = d.ints; a.toff = d.toff; a.tasks = d.tasks; a.gate = gate; a.dbg = dbg;
+    a.buf = d.buf; a.ints = d.ints; a.toff = d.toff; a.tasks = d.tasks; a.need_off = d.need_off; a.gate = gate; a.dbg = dbg;
     a.n = n; a.NT = (n + kT - 1) / kT; a.G = d.G; a.pb = d.pb;
     static const int hs = std::getenv("ORBHIP_DAG_SLEEP") ? std::atoi(std::getenv("ORBHIP_DAG_SLEEP")) : 6;
     a.hsleep = hs;
@@ -1694,7 +1729,8 @@ int dag_multi_fill(const DagProb* probs, int np, void* host_ks, int* host_wgoff,
         DagK& a = ks[i];
         a = DagK{};
         a.S = q.S; a.bs = q.bs; a.x = q.x; a.flag = q.flag; a.rf = q.rf;
-        a.buf = q.d.buf; a.ints = q.d.ints; a.toff = q.d.toff; a.tasks = q.d.tasks; a.gate = gate; a.dbg = nullptr;
+        a.buf = q.d.buf; a.ints = q.d.ints; a.toff = q.d.toff; a.tasks = q.d.tasks; a.need_off = q.d.need_off;
+        a.gate = gate; a.dbg = nullptr;
         a.n = q.n; a.NT = (q.n + kT - 1) / kT; a.G = q.d.G; a.pb = q.d.pb;
         a.hsleep = hs; a.smax = smax;
         a.ld = q.ld; a.perm = q.perm; a.nti = q.nti;
@@ -1770,7 +1806,7 @@ int chol_dag_test(const double* A, const double* b, double* x, int n, int reps, 
         if (!plan.tasks.empty())
             ok(hipMemcpy(dtasks, plan.tasks.data(), sizeof(int) * plan.tasks.size(), hipMemcpyHostToDevice));
         if (ddbg) ok(hipMemset(ddbg, 0, sizeof(unsigned long long) * kDbgWords));
-        const DagDev d{dbuf, dints, dtoff, dtasks, plan.G, plan.pb};
+        const DagDev d{dbuf, dints, dtoff, dtasks, plan.G, plan.pb, plan.toff[plan.G]};
         ok(chol_dag_solve(dS, n, drf, db, dx, dflag, d, nullptr, nullptr, nullptr));   // warm-up
         ok(hipDeviceSynchronize());
         hipEvent_t e0, e1;

@@ -659,7 +659,8 @@ int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int 
         DagProb& q = probs[loc[r]];
         q.S = S; q.ld = n; q.perm = I + so[r].perm; q.n = s.n; q.nti = s.nti; q.rf = I + so[r].rf; q.bs = bs;
         q.x = nullptr; q.flag = I + so[r].flag;
-        q.d = DagDev{D + o_buf[r], I + so[r].ints, I + so[r].toff, I + so[r].tasks, s.plan.G, s.plan.pb};
+        q.d = DagDev{D + o_buf[r], I + so[r].ints, I + so[r].toff, I + so[r].tasks, s.plan.G, s.plan.pb,
+                     s.plan.toff.empty() ? 0 : s.plan.toff[s.plan.G]};
         NdSegDev& g = segs[loc[r]];
         g.buf = D + o_buf[r]; g.rf = I + so[r].rf; g.flag = I + so[r].flag; g.perm = I + so[r].perm;
         g.zmap = I + so[r].zmap; g.n = s.n; g.NT = s.NT; g.nti = s.nti; g.nip = s.nip;
@@ -690,7 +691,7 @@ int nd_setup(NdWorkspace* W, const NdPlan& P, const int* bi, const int* bj, int 
     d.zg = I + o_zt; d.zsa = d.zg + nZ; d.zla = d.zsa + nZ; d.zsb = d.zla + nZ; d.zlb = d.zsb + nZ;
     d.rfZ = I + oZ_rf;
     d.SZ = D + o_SZ; d.bZ = D + o_bZ; d.xZ = D + o_xZ; d.flagZ = I + oZ_flag;
-    W->dZ = DagDev{D + o_bufZ, I + oZ_ints, I + oZ_toff, I + oZ_tasks, pZ.G, pZ.pb};
+    W->dZ = DagDev{D + o_bufZ, I + oZ_ints, I + oZ_toff, I + oZ_tasks, pZ.G, pZ.pb, pZ.toff.empty() ? 0 : pZ.toff[pZ.G]};
     W->rfZ = I + oZ_rf;
     W->flagZ = I + oZ_flag;
     int maxNT = 0;

@@ -2347,7 +2347,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     double* hd = ws->hdbl.p;
     int* hi = ws->hint.p;
     BaArgs* ha = ws->hargs.p;
-    std::vector<DagDev> dd(B, DagDev{nullptr, nullptr, nullptr, nullptr, 0, 0});
+    std::vector<DagDev> dd(B, DagDev{nullptr, nullptr, nullptr, nullptr, 0, 0, 0});
     parallel_for(B, nth, [&](int b) {
         const Prep& p = pp[b];
         const orbhip_ba_problem* pr = probs[b];
@@ -2411,6 +2411,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             }
             dd[b].G = p.dag.G;
             dd[b].pb = p.dag.pb;
+            dd[b].need_off = p.dag.toff.empty() ? 0 : p.dag.toff[p.dag.G];
         }
         a.nblk = p.nblk;
         a.P = p.P; a.M = p.M; a.E = p.E; a.np = p.np; a.n = p.n;
@@ -2481,6 +2482,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                                    hipMemcpyHostToDevice));
                 dd[b].G = dp.G;
                 dd[b].pb = dp.pb;
+                dd[b].need_off = dp.toff[dp.G];
             }
         }
         // one shard per rank: S all-reduced over its union envelope, packed; several: the full S

@@ -57,6 +57,8 @@ for n_s, shape in cases:
           f"| wave ends {med[0 + 1]} {int(np.median(ph[:, 2] & 0xFFFFFFFF)) if ki else 0} {med[3]} {med[4]} "
           f"w3 flags in {int(np.median(ph[:, 2] >> 32)) if ki else 0} w0 start {int(np.median(ph[:, 5] & 0xFFFFFFFF)) if ki else 0} "
           f"pre-diag {int(np.median(ph[:, 5] >> 32)) if ki else 0} ({time.time() - t0:.1f}s)", flush=True)
+    if ki and n <= 600:   # per interval: total cycles and wave 3's wait for the helpers' flags
+        print("    intervals (total/flags-in): " + " ".join(f"{int(r[0])}/{int(r[2]) >> 32}" for r in ph), flush=True)
     ks = min(ki, 100)
     if ks:
         sub = dbg[8 + 6 * 200:8 + 6 * 200 + 16 * ks].reshape(ks, 16).astype(np.int64)
