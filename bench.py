@@ -508,7 +508,8 @@ def c5_gba(ws, rank, iters):
     into N segments, rank r holding segment r's landmarks (sharding.shard_problem_nd); each rank
     factors its interior, the separator system and the pose update are all-reduced over RCCL inside
     the device-driven LM; a segment plan that does not fit (too many ranks for the
-    loop) falls back to contiguous landmark shards with the summed reduced camera system. Replicas
+    loop) falls back to contiguous landmark shards with the summed reduced camera system (every rank
+    solving it by the dissection planned on the ranks' union adjacency, r06). Replicas
     (every rank its own whole GBA) are timed beside it as c5_gba_replica_ms. Time = max over ranks of
     one solve, after one untimed solve."""
     import torch
@@ -542,7 +543,7 @@ def c5_gba(ws, rank, iters):
         else:
             shard, lo, hi, _ = shard_problem(prob, rank, ws)
             pts_sel = np.arange(lo, hi)
-            mode = f"rccl landmark shards x{ws} (reduced camera system all-reduced, replicated solve)"
+            mode = f"rccl landmark shards x{ws} (reduced camera system all-reduced, replicated dissected solve)"
         r, t = run(lambda: sopt.solve_sharded(shard))
         rr, tr = run(lambda: opt.solve(prob))
         out["c5_gba_replica_ms"] = round(1e3 * tr, 2)

@@ -1,10 +1,10 @@
-# final tree of a round (R=r05 default): the whole -m gpu suite, smoke, the default bench line, and a rocprofv3 kernel
+# final tree of a round (R=r06 default): the whole -m gpu suite, smoke, the default bench line, and a rocprofv3 kernel
 # trace of the bench's C2 section (the headline roofline's reproduction); logs under gpurun_out/
 # for profiles/. Stops at the first failure.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-R=${R:-r05}
+R=${R:-r06}
 mkdir -p gpurun_out
 echo "[1/4] pytest -m gpu"
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread > gpurun_out/${R}_pytest_gpu.log 2>&1
