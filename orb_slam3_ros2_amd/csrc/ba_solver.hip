@@ -2108,9 +2108,13 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     std::vector<Prep>& pp = ws->prep;
     for (int b = 0; b < B; b++) prep_reset(pp[b]);
     // Schur work-item size: a batch fills the chip with 16 pairs per lane; a few problems alone
-    // would leave it mostly idle, so their items are cut to 4 pairs (4x the lanes)
+    // would leave it mostly idle, so their items are cut to 4 pairs (4x the lanes), 3 for the
+    // LBA sizes (r06, alternating runs: C4 1.323 -> 1.309 ms with 3, 1.31-1.33 with 2, 1.34-1.35
+    // with 1; the C5 GBA 5.18 -> 5.58 ms with 2)
     static const int chunk_env = std::getenv("ORBHIP_SCHUR_CHUNK") ? std::atoi(std::getenv("ORBHIP_SCHUR_CHUNK")) : 0;
-    const int chunk = chunk_env > 0 ? chunk_env : (B >= 32 ? kSchurChunk : 4);
+    int maxE_in = 0;
+    for (int b = 0; b < B; b++) maxE_in = std::max(maxE_in, probs[b]->n_edges);
+    const int chunk = chunk_env > 0 ? chunk_env : (B >= 32 ? kSchurChunk : (maxE_in <= 32768 ? 3 : 4));
     // one problem: its Schur pair lists on the host threads; a batch: one problem per thread
     // (ORBHIP_PREP_THREADS=k: one large problem's pair lists on k host threads; off by default: on
     // the MI355X box's EPYC the C5 build went 0.62 -> 0.55 ms at 16 threads, 0.71 at 4 (its

@@ -124,8 +124,9 @@ class Optimizer:
     def solve(self, prob: BAProblem, stop_flag: ctypes.c_int | None = None) -> BAResult:
         p = prob.normalized()
         P, M, E = p.pose_q.shape[0], p.points.shape[0], p.edge_pose.shape[0]
-        out = BAResult(np.zeros((P, 4), np.float32), np.zeros((P, 3), np.float32), np.zeros((M, 3), np.float32),
-                       np.zeros(E, np.float32), np.zeros(E, np.uint8), 0.0, 0.0, 0, 0)
+        # (every output word is written by the solve: no zero fill)
+        out = BAResult(np.empty((P, 4), np.float32), np.empty((P, 3), np.float32), np.empty((M, 3), np.float32),
+                       np.empty(E, np.float32), np.empty(E, np.uint8), 0.0, 0.0, 0, 0)
         rc = BAResultC(ptr(out.pose_q), ptr(out.pose_t), ptr(out.points), ptr(out.edge_chi2),
                        ptr(out.edge_depth_ok), 0.0, 0.0, 0, 0)
         pc = p.to_c()
