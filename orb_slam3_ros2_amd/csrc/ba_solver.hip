@@ -2024,16 +2024,12 @@ struct HBuf {   // pinned host staging
 
 struct BaWorkspace {
     DBuf<double> dbl;      // all fp64 per-problem arrays, packed (segment map in ba_solve_batch)
-    DBuf<int> ints;        // all int per-problem arrays, packed
-    DBuf<BaArgs> args;
     DBuf<int> act;         // active problem lists (several slots)
     DBuf<double> lam;      // per-problem lambda
     DBuf<double> gath;     // gathered red/flag of the active problems
     DBuf<LmCtl> ctl;       // device-driven rounds: per-problem LM state
     HBuf<LmCtl> hctl;      // its pinned staging (initial state up, final state down)
-    HBuf<double> hdbl;     // staging: [e_chi2 | pose,pts | obs,info] of every problem
-    HBuf<int> hint;
-    HBuf<BaArgs> hargs;
+    HBuf<double> hdbl;     // staging: [e_chi2 | pose,pts | obs,info | the int arrays | BaArgs] of every problem
     double* h_gath = nullptr;  // pinned
     double* h_lam = nullptr;   // pinned
     double* h_red = nullptr;   // pinned: per problem red[4] + flag
@@ -2321,19 +2317,20 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
               p.row_first.size() + p.items.size() + p.fin.size() + p.ifin.size() + p.cb_tiles.size() + 8 +
               (p.use_dag ? dag_ints(p.n) + p.dag_task_cap + 4 : 0) + (p.own.size() + 3) / 4 + 1;
     }
-    const size_t sC = 0, sA = nC, sU = sA + nA, sR = (sU + nU + 15) & ~size_t(15);
+    // r06: the int arrays and the BaArgs follow the uploaded doubles in the same device / pinned
+    // buffers, so that ONE copy uploads all of it (three blit launches of ~4.4 us each before)
+    const size_t sC = 0, sA = nC, sU = sA + nA;
+    const size_t sI = (sU + nU + 1) & ~size_t(1);                            // 16-byte aligned
+    const size_t sG = (sI + (ni * sizeof(int) + 7) / 8 + 1) & ~size_t(1);  // the BaArgs
+    const size_t sR = (sG + (B * sizeof(BaArgs) + 7) / 8 + 15) & ~size_t(15);
     const size_t nd = sR + nR;
     BAOK(ws->dbl.ensure(nd));
-    BAOK(ws->ints.ensure(ni));
-    BAOK(ws->args.ensure(B));
     BAOK(ws->act.ensure(3 * (size_t)B));
     BAOK(ws->lam.ensure(B));
     BAOK(ws->gath.ensure(5 * (size_t)B));
     BAOK(ws->ctl.ensure(B));
     BAOK(ws->hctl.ensure(B));
-    BAOK(ws->hdbl.ensure(sU + nU));
-    BAOK(ws->hint.ensure(ni));
-    BAOK(ws->hargs.ensure(B));
+    BAOK(ws->hdbl.ensure(sR));
     if (ws->h_cap < (size_t)B) {
         if (ws->h_lam) (void)hipHostFree(ws->h_lam);
         if (ws->h_red) (void)hipHostFree(ws->h_red);
@@ -2347,10 +2344,11 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         ws->h_cap = B;
     }
     double* D = ws->dbl.p;
-    int* I = ws->ints.p;
+    int* I = reinterpret_cast<int*>(D + sI);
     double* hd = ws->hdbl.p;
-    int* hi = ws->hint.p;
-    BaArgs* ha = ws->hargs.p;
+    int* hi = reinterpret_cast<int*>(hd + sI);
+    BaArgs* ha = reinterpret_cast<BaArgs*>(hd + sG);
+    BaArgs* const dArgs = reinterpret_cast<BaArgs*>(D + sG);
     std::vector<DagDev> dd(B, DagDev{nullptr, nullptr, nullptr, nullptr, 0, 0, 0});
     parallel_for(B, nth, [&](int b) {
         const Prep& p = pp[b];
@@ -2454,9 +2452,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.lead = shard_mode == kShardLocal ? (b == 0) : (shard_mode == kShardRccl ? (ws->rank == 0 && b == 0) : 1);
         a.ctl = ws->ctl.p + b;
     });
-    BAOK(hipMemcpyAsync(D + sA, hd + sA, sizeof(double) * (nA + nU), hipMemcpyHostToDevice, st));
-    BAOK(hipMemcpyAsync(I, hi, ni * sizeof(int), hipMemcpyHostToDevice, st));
-    BAOK(hipMemcpyAsync(ws->args.p, ha, B * sizeof(BaArgs), hipMemcpyHostToDevice, st));
+    BAOK(hipMemcpyAsync(D + sA, hd + sA, sizeof(double) * (sR - sA), hipMemcpyHostToDevice, st));
     // RCCL shards solved by the blocked Cholesky (which reads only the lower triangle inside the
     // envelope; the one-workgroup solvers also read the mirrored upper triangle) all-reduce S
     // over its union envelope only: ~5 MB instead of n^2 doubles (46 MB) at C5
@@ -2543,7 +2539,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         BAOK(hipMemcpyAsync(d_act, h_act, v.size() * sizeof(int), hipMemcpyHostToDevice, st));
         return ORBHIP_OK;
     };
-    const BaArgs* dA = ws->args.p;
+    const BaArgs* dA = dArgs;
     // stop flag: one consistent decision across ranks (all-reduce max) per batch of slots
     auto stop_now = [&]() -> bool {
         const bool local = stop && *stop;
@@ -2729,7 +2725,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         for (int b = 0; b < B && fused; b++) fused = (int)gbs <= ha[b].npart_e && pp[b].P <= kFusedMaxP;
         if (fused) {
             for (int b = 0; b < B; b++) ha[b].fused = 1;
-            BAOK(hipMemcpyAsync(ws->args.p, ha, B * sizeof(BaArgs), hipMemcpyHostToDevice, st));
+            BAOK(hipMemcpyAsync(dArgs, ha, B * sizeof(BaArgs), hipMemcpyHostToDevice, st));
         }
         // the host-mapped words (post_done): B done flags, then the relayed stop flag. The kernels
         // get them through a device-resident pointer pair: {done, stop} for a solve of its own,
