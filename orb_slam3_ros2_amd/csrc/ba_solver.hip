@@ -2105,7 +2105,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     for (int b = 0; b < B; b++) prep_reset(pp[b]);
     // Schur work-item size: a batch fills the chip with 16 pairs per lane; a few problems alone
     // would leave it mostly idle, so their items are cut to 4 pairs (4x the lanes), 3 for the
-    // LBA sizes (r06, alternating runs: C4 1.323 -> 1.309 ms with 3, 1.31-1.33 with 2, 1.34-1.35
+    // LBA sizes (r06, alternating runs, tools/r06/gpu_chunk.sh: C4 1.323 -> 1.309 ms with 3, 1.31-1.33 with 2, 1.34-1.35
     // with 1; the C5 GBA 5.18 -> 5.58 ms with 2)
     static const int chunk_env = std::getenv("ORBHIP_SCHUR_CHUNK") ? std::atoi(std::getenv("ORBHIP_SCHUR_CHUNK")) : 0;
     int maxE_in = 0;
