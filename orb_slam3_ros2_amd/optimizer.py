@@ -136,6 +136,19 @@ class Optimizer:
         out.iterations_done, out.lm_trials = rc.iterations_done, rc.lm_trials
         return out
 
+    def prepare_single(self, prob: BAProblem) -> "BABatch":
+        """The C-ABI view of one problem (orbhip_ba_problem / orbhip_ba_result over the problem's
+        own arrays and fresh outputs), as LocalMapping's C++ adapter holds it:
+        run_single is the orbhip_ba_solve call alone, without solve()'s per-call marshalling."""
+        p = prob.normalized()
+        outs, cres = self._results_for([p])
+        return BABatch([p], outs, p.to_c(), cres)
+
+    def run_single(self, single: "BABatch", stop_flag: ctypes.c_int | None = None) -> BAResult:
+        sf = ctypes.addressof(stop_flag) if stop_flag is not None else None
+        check(lib().orbhip_ba_solve(self.ctx.handle, ctypes.byref(single.cprobs), single.cres, sf), "orbhip_ba_solve")
+        return self._fill(single.outs, single.cres)[0]
+
     def solve_batch(self, probs, stop_flag: ctypes.c_int | None = None):
         """B independent problems in one batched solve (replicas); returns a list of BAResult."""
         return self.run_batch(self.prepare_batch(probs), stop_flag)
