@@ -1706,6 +1706,17 @@ class HostPool {
     unsigned long long gen_ = 0;
 };
 
+// r06 (late): one large problem (E >= kPrepParallelE, a GBA) writes its outputs on the pool (C5
+// 0.146 -> 0.05 ms; its pair lists and packing measured slower there, tools/r06/gpu_hostpool_ab.sh);
+// ORBHIP_HOST_POOL=0 keeps every host loop on the calling thread
+bool host_pool_on() {
+    static const bool on = [] {
+        const char* s = std::getenv("ORBHIP_HOST_POOL");
+        return !(s && s[0] == '0') && host_threads() > 1;
+    }();
+    return on;
+}
+
 // The Schur pair lists of prepare() on host threads, identical to the serial build:
 //   1. landmark chunk t (contiguous): its pairs counted per pose row ia;
 //   2. the same chunk writes its pairs (ib, ea, eb) at its per-row cursors (rows in order, chunks
@@ -2138,9 +2149,11 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
     const int chunk = chunk_env > 0 ? chunk_env : (B >= 32 ? kSchurChunk : (maxE_in <= 32768 ? 3 : 4));
     // one problem: its Schur pair lists on the host threads; a batch: one problem per thread
     // (ORBHIP_PREP_THREADS=k: one large problem's pair lists on k host threads; off by default: on
-    // the MI355X box's EPYC the C5 build went 0.62 -> 0.55 ms at 16 threads, 0.71 at 4 (its
-    // scattered fill does not scale), and it measured slower on the 8-core container)
-    static const int prep_par = std::getenv("ORBHIP_PREP_THREADS") ? std::atoi(std::getenv("ORBHIP_PREP_THREADS")) : 1;
+    // the MI355X box's EPYC the C5 build went 0.62 -> 0.55 ms at 16 threads, 0.71 at 4 in r05, and
+    // 0.63 -> 1.09-1.26 ms on the r06 tree (tools/r06/gpu_hostpool_ab.sh): its scattered fill does
+    // not scale)
+    static const int prep_par = std::getenv("ORBHIP_PREP_THREADS") ? std::atoi(std::getenv("ORBHIP_PREP_THREADS"))
+                                                                   : 1;
     parallel_for(B, nth, [&](int b) { pp[b].rc = prepare(probs[b], pp[b], chunk, B == 1 ? prep_par : 1); });
     const double t_prepare = now();
     // RCCL shards: a rank whose shards are invalid must not return before the first collective
@@ -2383,6 +2396,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         for (size_t i = 0; i < P; i++) se3_from_float(pr->pose_q + 4 * i, pr->pose_t + 3 * i, st_ + 8 * i);
         for (size_t k = 0; k < 3 * M; k++) st_[8 * P + k] = pr->points[k];
         double* ob = hd + sU + p.o_obs;
+        // (on the host pool this loop measured slower: C5 pack + upload 0.11 -> 0.21 ms, r06 A/B)
         for (size_t e = 0; e < E; e++) {
             ob[2 * e] = pr->edge_uv[2 * e];
             ob[2 * e + 1] = pr->edge_uv[2 * e + 1];
@@ -2953,22 +2967,25 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             return ba_solve_batch(ws, probs, B, res, stop, st, shard_mode, true, no_nd);
         }
     }
-    parallel_for(B, nth, [&](int b) {
+    // the outputs of problem b, edges [e0, e1) (the poses, points and LM words with the first range)
+    auto outputs = [&](int b, int e0, int e1) {
         const Prep& p = pp[b];
         const orbhip_ba_problem* pr = probs[b];
         orbhip_ba_result* r = res[b];
-        r->final_chi2 = L[b].currentChi;
-        r->iterations_done = L[b].it;
-        r->lm_trials = L[b].trials;
         const double* pose_o = hd + sA + p.o_state;
         const double* pts_o = pose_o + 8 * (size_t)p.P;
         const double* chi2_o = hd + sC + p.o_chi2;
-        for (int i = 0; i < p.P; i++) {
-            if (r->pose_q) for (int k = 0; k < 4; k++) r->pose_q[4 * i + k] = (float)pose_o[8 * i + k];
-            if (r->pose_t) for (int k = 0; k < 3; k++) r->pose_t[3 * i + k] = (float)pose_o[8 * i + 4 + k];
+        if (e0 == 0) {
+            r->final_chi2 = L[b].currentChi;
+            r->iterations_done = L[b].it;
+            r->lm_trials = L[b].trials;
+            for (int i = 0; i < p.P; i++) {
+                if (r->pose_q) for (int k = 0; k < 4; k++) r->pose_q[4 * i + k] = (float)pose_o[8 * i + k];
+                if (r->pose_t) for (int k = 0; k < 3; k++) r->pose_t[3 * i + k] = (float)pose_o[8 * i + 4 + k];
+            }
+            if (r->points) for (int k = 0; k < 3 * p.M; k++) r->points[k] = (float)pts_o[k];
         }
-        if (r->points) for (int k = 0; k < 3 * p.M; k++) r->points[k] = (float)pts_o[k];
-        for (int e = 0; e < p.E; e++) {
+        for (int e = e0; e < e1; e++) {
             if (r->edge_chi2) r->edge_chi2[e] = (float)chi2_o[e];
             if (r->edge_depth_ok) {   // isDepthPositive: (T.map(X)).z > 0
                 const double* T = &pose_o[8 * pr->edge_pose[e]];
@@ -2981,7 +2998,15 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
                 r->edge_depth_ok[e] = z > 0.0 ? 1 : 0;
             }
         }
-    });
+    };
+    if (B == 1 && pp[0].E >= kPrepParallelE && host_pool_on()) {
+        // one large problem (a GBA): its edges in chunks on the host pool (r06, late: the C5 loop's
+        // 80k depth tests and conversions took ~0.2 ms on one core)
+        const int E = pp[0].E, T = std::min(host_threads(), E / 4096 + 1);
+        HostPool::get(host_threads() - 1).run(T, [&](int t) { outputs(0, (int)((long long)E * t / T), (int)((long long)E * (t + 1) / T)); });
+    } else {
+        parallel_for(B, nth, [&](int b) { outputs(b, 0, pp[b].E); });
+    }
     if (timing)
         std::fprintf(stderr,
                      "orbhip ba timing B=%d: prep %.3f ms (problem structure %.3f), pack+upload %.3f ms, solve %.3f ms, "
