@@ -510,8 +510,8 @@ def c5_gba(ws, rank, iters):
     the device-driven LM; a segment plan that does not fit (too many ranks for the
     loop) falls back to contiguous landmark shards with the summed reduced camera system (every rank
     solving it by the dissection planned on the ranks' union adjacency, r06). Replicas
-    (every rank its own whole GBA) are timed beside it as c5_gba_replica_ms. Time = max over ranks of
-    one solve, after one untimed solve."""
+    (every rank its own whole GBA) are timed beside it as c5_gba_replica_ms. Time = the median of
+    three solves, each the max over the ranks, after one untimed solve."""
     import torch
     from orb_slam3_ros2_amd import Optimizer
     from orb_slam3_ros2_amd.sharding import nd_segments, pose_blocks, shard_problem, shard_problem_nd
@@ -520,14 +520,18 @@ def c5_gba(ws, rank, iters):
     prob.iterations, prob.huber_delta = iters, float(np.sqrt(5.99))   # BundleAdjustment(bRobust)
     opt = Optimizer()
 
-    def run(solve):
+    def run(solve, reps=3):
+        # one untimed solve, then the median of `reps` timed ones (each the max over the ranks)
         solve()
-        _barrier(ws)
-        t0 = time.perf_counter()
-        r = solve()
-        torch.cuda.synchronize()
-        _barrier(ws)
-        return r, _max_over_ranks(ws, time.perf_counter() - t0)
+        ts = []
+        for _ in range(reps):
+            _barrier(ws)
+            t0 = time.perf_counter()
+            r = solve()
+            torch.cuda.synchronize()
+            _barrier(ws)
+            ts.append(_max_over_ranks(ws, time.perf_counter() - t0))
+        return r, float(np.median(ts))
 
     out = {"c5_problem": "400 KF loop / 20000 pts / 80000 obs, n = 2394"}
     sharded = ws > 1 and os.environ.get("ORBHIP_C5_SHARDED", "1") == "1"

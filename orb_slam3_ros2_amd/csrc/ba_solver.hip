@@ -291,8 +291,8 @@ __device__ __forceinline__ double lin_ab(const BaArgs& a, int e, int oi, double 
 // ---------------------------------------------------------------------------
 // one thread per landmark: Hll, b_l over all its edges; stores each edge's linearisation (Pc, w)
 // returns the largest |diagonal| of Hll (0 for m >= M)
-// fresh: the stored errors belong to a rejected trial (a small problem whose iteration ended on
-// one): each edge's terms are taken from the restored state here, and stored, instead of read
+// fresh: the stored errors belong to a rejected trial (an unsharded problem whose iteration ended
+// on one): each edge's terms are taken from the restored state here, and stored, instead of read
 __device__ __forceinline__ double lin_point(const BaArgs& a, int m, bool fresh = false) {
     if (m >= a.M) return 0.0;
     double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bl[3] = {0, 0, 0};
@@ -565,9 +565,11 @@ __global__ __launch_bounds__(256) void k_ba_lin(const BaArgs* __restrict__ args,
     __shared__ double sh27[4 * 27];
     __shared__ int lastf;
     const int mP = (a.M + kLinL - 1) / kLinL, nP = (a.np + ppw - 1) / ppw;
-    // a small problem whose iteration ended on a rejected trial: its stored errors are the trial's,
-    // so this build takes them from the restored state (the larger problems' k_ba_errors(1) did)
-    const bool fresh = a.small && a.ctl && !a.ctl->errors_valid;
+    // a problem whose iteration ended on a rejected trial: its stored errors are the trial's, so this
+    // build takes them from the restored state (a small problem's restored in the trial's launch, a
+    // larger one's by k_ba_pop). r06 (late): every unsharded problem, so the larger ones' slots lost
+    // their k_ba_errors(1) launch (C5: one launch less per trial); the shards keep it
+    const bool fresh = (a.small || !a.sync) && a.ctl && !a.ctl->errors_valid;
     double d;
     int slot;
     if (bx_ < nbp) {
@@ -1479,7 +1481,7 @@ __device__ void ctl_end_decide(const BaArgs& a, int prob, int* done_flags) {
     c.errors_valid = rho > 0;   // rejected: the device errors belong to the popped trial
     bool done = (c.qmax == 10 || rho == 0) || c.stop;   // stop: SparseOptimizer's force-stop, at the iteration end
     if (c.early_stop && c.nBad >= 3) done = true;
-    if (c.it >= c.iterations) done = true;   // the budget (checked by k_ba_errors(1) too), no idle slot
+    if (c.it >= c.iterations) done = true;   // the budget (a sharded slot's k_ba_errors(1) checks it too), no idle slot
     c.phase = done ? kPhDone : kPhBuild;
     if (done) post_done(done_flags, prob);
 }
@@ -2785,7 +2787,10 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         for (int b = 0; b < B; b++) __atomic_store_n(ws->h_done + b, probs[b]->iterations > 0 ? 0 : 1, __ATOMIC_RELAXED);
         __atomic_store_n(ws->h_done + ws->done_cap, 0, __ATOMIC_RELAXED);
         auto slot = [&]() -> int {
-            if (!all_small) hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 1, donep);
+            // the sharded slots' error refresh and budget check; an unsharded problem's iteration
+            // ends in its controller (ctl_end_decide) and its stale errors are refreshed by k_ba_lin
+            if (!all_small && sharded)
+                hipLaunchKernelGGL(k_ba_errors, dim3(gx(maxE, 256), B), b256, 0, st, dA, d_act, 1, donep);
             hipLaunchKernelGGL(k_ba_lin, dim3(gx(maxM, kLinL) + gx(maxNp, lin_ppw), B), b256, 0, st, dA, d_act,
                                (int)gx(maxM, kLinL), lin_ppw, donep);
             if (sharded) {   // the trial start on the shards' sums: Hpp, then the largest diagonal

@@ -100,7 +100,8 @@ def test_rejected_trials_large_problem_path(opt, oracle, monkeypatch, fused):
     ORBHIP_BA_SMALL_WORDS, 32768 by default; forced to 0 here on the problem above that rejects
     trials): since r06 their trials are fused too (back-substitution + errors in one launch, the new
     poses committed by the controller's work-group), a rejected trial's points restored by k_ba_pop
-    and its errors refreshed by the next build's k_ba_errors. Both trial forms equal the oracle."""
+    and, when the iteration ended there, its errors refreshed by the next build (k_ba_lin's fresh
+    terms; r06 late: no k_ba_errors(1) launch per slot). Both trial forms equal the oracle."""
     monkeypatch.setenv("ORBHIP_BA_FUSED", fused)
     monkeypatch.setenv("ORBHIP_BA_SMALL_WORDS", "0")
     prob, _ = synthetic_ba_problem(n_kf=50, n_pts=3000, seed=31, rot_noise=0.1, trans_noise=0.2, pt_noise=0.5)
