@@ -141,12 +141,17 @@ __device__ __forceinline__ void cmstore(__amdgpu_buffer_rsrc_t rs, int dbl_off, 
         __builtin_amdgcn_raw_buffer_store_b64(u, rs, i * 8, 0, 16);
     }
 }
-// this lane's column of a column copy (v[j] = element (16 hh + j, c)), sc1
+// this lane's column of a column copy (v[j] = element (16 hh + j, c)), sc1. The lane's part of the
+// address is a VGPR that never changes, the tile's (wave-uniform) part and the block's go in the
+// scalar offset: no VGPR is written per load. (r06, late: with the whole address per load in VGPRs
+// the allocator took the other prefetch set's destination registers as address temporaries, so
+// the backward waited for that set's loads, vmcnt(1) / vmcnt(0), at every step)
 __device__ __forceinline__ void cmload(__amdgpu_buffer_rsrc_t rs, int dbl_off, double (&v)[16]) {
-    const int off = (dbl_off + 2 * (int)(threadIdx.x & 63)) * 8;
+    const int voff = 16 * (int)(threadIdx.x & 63);
+    const int soff = __builtin_amdgcn_readfirstlane(dbl_off * 8);
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-        const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 1024 * i, 0, 16);
+        const u32x4 u = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff + 1024 * i, 16);
         v[2 * i] = mk64(u.x, u.y);
         v[2 * i + 1] = mk64(u.z, u.w);
     }
@@ -1287,12 +1292,16 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
         if (!aborted && wid == 0) {
             bool good = true;
             double li[2][16], lt[2][16], liA[16], ltA[16];
-            auto load = [&](auto setc, int t) {   // operands of step t <= NT - 2 (copies)
+            // operands of step t <= NT - 2 (copies). r06 (late): issued on every path, t < 1 (and
+            // NT < 2) reading step 1's (an unused reload, in range of the buffer): with the loads
+            // behind a branch, the waitcnt pass merged the paths that skip them and made each
+            // step's dot wait for the loads issued just before it (vmcnt(7) .. vmcnt(0) after the
+            // next step's 16 loads), so no step had its operands two steps ahead
+            auto load = [&](auto setc, int t) {
                 constexpr int S = decltype(setc)::value;
-                if (t >= 1) {
-                    cmload(rs, L.oCI + (t - 1) * kTD, li[S]);
-                    cmload(rs, L.oCM + (t * NT + t - 1) * kTD, lt[S]);
-                }
+                const int tt = NT >= 2 ? max(t, 1) : 0;
+                cmload(rs, L.oCI + max(tt - 1, 0) * kTD, li[S]);
+                cmload(rs, L.oCM + (tt * NT + max(tt - 1, 0)) * kTD, lt[S]);
             };
             // x_{t-1} from the step's operands (lv: L(t, t-1) by columns, unused at t = NT; iv: Linv_{t-1})
             auto xstep = [&](const double (&lv)[16], const double (&iv)[16], int t) -> bool {
@@ -1316,9 +1325,11 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 // the last interval's buffers), the rest are copies (every copy task's flag was
                 // polled by wave 2 in the last interval): their first two steps' loads go out first
                 good = lwait(cpok, 1);
+                // (every load below issues whatever `good` says: a failed wait fails the solve and
+                // its loads go unused; the steps themselves are skipped)
+                load(std::integral_constant<int, 0>{}, NT - 2);
+                load(std::integral_constant<int, 1>{}, NT - 3);
                 if (good) {
-                    load(std::integral_constant<int, 0>{}, NT - 2);
-                    load(std::integral_constant<int, 1>{}, NT - 3);
                     lds_col(lds + 1024 * ((NT - 1) & 1), liA);
                     good = xstep(ltA, liA, NT);
                 }
@@ -1327,13 +1338,11 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                     lds_col(lds + 2048 + 1024 * ((NT - 1) & 1), ltA);
                     good = xstep(ltA, liA, NT - 1);
                 }
-                for (int t = NT - 2; t >= 1 && good; t -= 2) {
-                    good = xstep(lt[0], li[0], t);
+                for (int t = NT - 2; t >= 1; t -= 2) {
+                    if (good) good = xstep(lt[0], li[0], t);
                     load(std::integral_constant<int, 0>{}, t - 2);
-                    if (good && t - 1 >= 1) {
-                        good = xstep(lt[1], li[1], t - 1);
-                        load(std::integral_constant<int, 1>{}, t - 3);
-                    }
+                    if (good && t - 1 >= 1) good = xstep(lt[1], li[1], t - 1);
+                    load(std::integral_constant<int, 1>{}, t - 3);
                 }
             }
             if (!good && lane == 0) __hip_atomic_store(bab, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1389,15 +1398,21 @@ __device__ void dag_chain(const DagK& a, const Lay& L, __amdgpu_buffer_rsrc_t rs
                 int Rn = NT - 1, jn = jtop(NT - 1);   // the next tile to load
                 norm(Rn, jn);
                 bool cp = false;   // cpok seen
-                auto fetch = [&](auto setc) {   // the next tile into ring slot S
+                // the next tile into ring slot S. r06 (late): its load issues on every path (an
+                // exhausted ring, or a failed wait, reloads tile 0's copy, unused), so the waitcnt
+                // pass counts the ring exactly: behind a branch, every slot's product waited for
+                // the three loads fetched after it (vmcnt(7) .. vmcnt(0))
+                auto fetch = [&](auto setc) {
                     constexpr int S = decltype(setc)::value;
                     Rq[S] = Rn;
                     jq[S] = jn;
-                    if (jn < 0) return;
-                    if (jn == Rn - 2 && !cp) cp = good = good && lwait(cpok, 1);
-                    if (good) cmload(rs, L.oCM + (Rn * NT + jn) * kTD, v[S]);
-                    Rn--;
-                    norm(Rn, jn);
+                    const bool has = jn >= 0;
+                    if (has && jn == Rn - 2 && !cp) cp = good = good && lwait(cpok, 1);
+                    cmload(rs, L.oCM + (has && good ? Rn * NT + jn : 0) * kTD, v[S]);
+                    if (has) {
+                        Rn--;
+                        norm(Rn, jn);
+                    }
                 };
                 // a column's tiles come one after another: their products are summed in a register
                 // and s_j is updated once, its count set to the column's total (need[j])
