@@ -68,7 +68,8 @@ typedef struct {
 
 /* ---- context ------------------------------------------------------------------- */
 int orbhip_abi_version(void);
-/* device: HIP ordinal. params may be NULL -> ORB_SLAM3 defaults (1000, 1.2, 8, 20, 7). */
+/* device: HIP ordinal, or < 0 for the calling thread's current device (hipGetDevice: one process
+   per GPU). params may be NULL -> ORB_SLAM3 defaults (1000, 1.2, 8, 20, 7). */
 int orbhip_create(orbhip_ctx** out, int device, const orbhip_orb_params* params);
 int orbhip_destroy(orbhip_ctx* ctx);
 /* Per-level tables of the ORBextractor ctor: mvScaleFactor, mnFeaturesPerLevel. */

@@ -234,9 +234,10 @@ def ptr(a) -> int | None:
 
 
 class Context:
-    """Owns one orbhip_ctx (device memory, pinned staging, one HIP stream)."""
+    """Owns one orbhip_ctx (device memory, pinned staging, one HIP stream). device < 0 (the default):
+    the calling thread's current HIP device, i.e. the rank's GPU after torch.cuda.set_device."""
 
-    def __init__(self, device: int = 0, n_features=1000, scale_factor=1.2, n_levels=8, ini_th_fast=20,
+    def __init__(self, device: int = -1, n_features=1000, scale_factor=1.2, n_levels=8, ini_th_fast=20,
                  min_th_fast=7):
         self._h = ctypes.c_void_p()
         prm = OrbParams(int(n_features), float(scale_factor), int(n_levels), int(ini_th_fast), int(min_th_fast))

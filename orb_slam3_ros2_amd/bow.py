@@ -12,7 +12,7 @@ from .vocabulary import Vocabulary, bow_vector, feature_vector
 
 
 class ORBVocabulary:
-    def __init__(self, vocab: Vocabulary | str, device: int = 0, ctx: Context | None = None):
+    def __init__(self, vocab: Vocabulary | str, device: int = -1, ctx: Context | None = None):
         self.ctx = ctx or Context(device)
         self._h = ctypes.c_void_p()
         if isinstance(vocab, str):

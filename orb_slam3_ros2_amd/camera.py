@@ -17,7 +17,7 @@ MILKV = dict(fx=342.67, fy=342.67, cx=203.0, cy=132.67, k1=-0.35952, k2=0.080321
 
 class PinholeCamera:
     def __init__(self, fx, fy, cx, cy, k1=0.0, k2=0.0, p1=0.0, p2=0.0, k3=0.0, width=640, height=480,
-                 device: int = 0, ctx: Context | None = None):
+                 device: int = -1, ctx: Context | None = None):
         self.c = PinholeC(fx, fy, cx, cy, k1, k2, p1, p2, k3)
         self.width, self.height = int(width), int(height)
         self.ctx = ctx or Context(device)

@@ -899,7 +899,11 @@ int orbhip_create(orbhip_ctx** out, int device, const orbhip_orb_params* params)
     if (p.n_features < 0 || p.n_levels < 1 || p.n_levels > kMaxLevels || !(p.scale_factor >= 1.0f))
         return ORBHIP_ERR_ARG;
     int ndev = 0;
-    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) return ORBHIP_ERR_DEVICE;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return ORBHIP_ERR_DEVICE;
+    // device < 0: the calling thread's current HIP device (the rank's GPU after torch.cuda.set_device
+    // / hipSetDevice in a one-process-per-GPU job)
+    if (device < 0 && hipGetDevice(&device) != hipSuccess) return ORBHIP_ERR_DEVICE;
+    if (device < 0 || device >= ndev) return ORBHIP_ERR_DEVICE;
     std::unique_ptr<orbhip_ctx> c(new orbhip_ctx());
     c->device = device;
     c->prm = p;
@@ -1777,6 +1781,7 @@ int orbhip_frontend_create(orbhip_frontend** out, int device, const orbhip_orb_p
                            int frames_in_flight, int th_low, float ratio, int check_orientation) {
     if (!out || w <= 0 || h <= 0 || frames_in_flight < 1 || frames_in_flight > 32) return ORBHIP_ERR_ARG;
     *out = nullptr;
+    if (device < 0 && hipGetDevice(&device) != hipSuccess) return ORBHIP_ERR_DEVICE;   // as orbhip_create
     std::unique_ptr<orbhip_frontend, void (*)(orbhip_frontend*)> f(new orbhip_frontend(), frontend_free);
     f->device = device; f->w = w; f->h = h;
     f->S = frames_in_flight;

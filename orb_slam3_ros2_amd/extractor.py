@@ -45,7 +45,7 @@ class ORBextractor:
     """U:src/ORBextractor.cc::ORBextractor — the constructor builds the per-level tables,
     ``__call__`` is ``operator()``."""
 
-    def __init__(self, nfeatures=1000, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7, device=0):
+    def __init__(self, nfeatures=1000, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7, device=-1):
         self.nfeatures, self.scaleFactor, self.nlevels = int(nfeatures), float(scaleFactor), int(nlevels)
         self.iniThFAST, self.minThFAST = int(iniThFAST), int(minThFAST)
         self.ctx = Context(device, nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST)

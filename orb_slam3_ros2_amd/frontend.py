@@ -37,7 +37,7 @@ class _CtxRef:
 class FrameStream:
     def __init__(self, w: int, h: int, frames_in_flight: int = 8, nfeatures=1000, scaleFactor=1.2, nlevels=8,
                  iniThFAST=20, minThFAST=7, th_low: int = 50, nnratio: float = 0.9, checkOri: bool = True,
-                 device: int = 0):
+                 device: int = -1):
         self.w, self.h, self.S = int(w), int(h), int(frames_in_flight)
         self._h = ctypes.c_void_p()
         prm = OrbParams(int(nfeatures), float(scaleFactor), int(nlevels), int(iniThFAST), int(minThFAST))

@@ -45,12 +45,12 @@ class MonoIngest:
     (kps [cap, 6] float32, desc [cap, 32] uint8, n, monoIndex), ready for the matcher."""
 
     def __init__(self, width, height, nfeatures=1000, scaleFactor=1.2, nlevels=8, iniThFAST=20, minThFAST=7,
-                 device=0):
+                 device=-1):
         import torch
         self.torch = torch
         self.ext = ORBextractor(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, device)
         self.w, self.h = int(width), int(height)
-        dev = torch.device("cuda", device)
+        dev = torch.device("cuda", device) if device >= 0 else torch.device("cuda", torch.cuda.current_device())
         self.cap = self.ext.max_keypoints(self.w, self.h)
         self.bgr = torch.empty((self.h, self.w, 3), dtype=torch.uint8, device=dev)
         self.gray = torch.empty((1, self.h, self.w), dtype=torch.uint8, device=dev)

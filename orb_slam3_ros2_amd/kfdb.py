@@ -19,7 +19,7 @@ def _bow(bow):
 class KeyFrameDatabase:
     COVIS = 10
 
-    def __init__(self, max_kf: int, device: int = 0, ctx: Context | None = None):
+    def __init__(self, max_kf: int, device: int = -1, ctx: Context | None = None):
         self.ctx = ctx or Context(device)
         self.max_kf = int(max_kf)
         self._h = ctypes.c_void_p()

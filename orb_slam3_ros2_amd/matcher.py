@@ -21,7 +21,7 @@ class ORBmatcher:
     TH_LOW = 50
     HISTO_LENGTH = 30
 
-    def __init__(self, nnratio: float = 0.6, checkOri: bool = True, device: int = 0, ctx: Context | None = None):
+    def __init__(self, nnratio: float = 0.6, checkOri: bool = True, device: int = -1, ctx: Context | None = None):
         self.mfNNratio = float(nnratio)
         self.mbCheckOrientation = bool(checkOri)
         self.ctx = ctx or Context(device)

@@ -118,7 +118,7 @@ class BABatch:
 
 
 class Optimizer:
-    def __init__(self, device: int = 0, ctx: Context | None = None):
+    def __init__(self, device: int = -1, ctx: Context | None = None):
         self.ctx = ctx or Context(device)
 
     def solve(self, prob: BAProblem, stop_flag: ctypes.c_int | None = None) -> BAResult:

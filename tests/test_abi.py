@@ -60,3 +60,20 @@ def test_create_fails_loudly_without_device():
     assert rc == -3 and not h.value
     with pytest.raises(_lib.OrbHipError):
         _lib.Context(0)
+    with pytest.raises(_lib.OrbHipError):
+        _lib.Context()   # device < 0: the current device, none here either
+
+
+@pytest.mark.gpu
+def test_context_on_the_current_device():
+    """device < 0 (the Python default) resolves to the calling thread's current HIP device, so a
+    rank of a one-process-per-GPU job (torch.cuda.set_device(LOCAL_RANK)) computes on its own GPU;
+    an ordinal past the last device fails loudly."""
+    import torch
+    from orb_slam3_ros2_amd import _lib
+    torch.cuda.set_device(torch.cuda.device_count() - 1)
+    h = ctypes.c_void_p()
+    assert _lib.lib().orbhip_create(ctypes.byref(h), -1, None) == 0 and h.value
+    assert _lib.lib().orbhip_destroy(h) == 0
+    assert _lib.lib().orbhip_create(ctypes.byref(h), torch.cuda.device_count(), None) == -3
+    torch.cuda.set_device(0)
