@@ -69,6 +69,13 @@ def parse():
     return ap.parse_args()
 
 
+# ORBHIP_BENCH_REHEARSAL=1: the N-rank flow on fewer GPUs than ranks (ranks share GPUs by LOCAL_RANK
+# modulo the device count; the bench's own collectives over gloo on the host; the C5 solve as
+# replicas, since RCCL refuses two ranks on one GPU). A rehearsal of the multi-rank code paths on a
+# one-GPU box, never a measurement.
+REHEARSAL = os.environ.get("ORBHIP_BENCH_REHEARSAL", "0") == "1"
+
+
 def _dist_setup(args):
     import torch
     ws = int(os.environ.get("WORLD_SIZE", "1"))
@@ -76,8 +83,13 @@ def _dist_setup(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if ws > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if REHEARSAL:
+            local %= torch.cuda.device_count()
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     return ws, rank, local
@@ -91,24 +103,26 @@ def _barrier(ws):
     torch.cuda.synchronize()
 
 
+def _all_reduce_value(v: float, op) -> float:
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64, device="cpu" if REHEARSAL else "cuda")
+    dist.all_reduce(t, op=op)
+    return float(t.item())
+
+
 def _max_over_ranks(ws, v: float) -> float:
     if ws == 1:
         return v
-    import torch
     import torch.distributed as dist
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    return _all_reduce_value(v, dist.ReduceOp.MAX)
 
 
 def _sum_over_ranks(ws, v: float) -> float:
     if ws == 1:
         return v
-    import torch
     import torch.distributed as dist
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return float(t.item())
+    return _all_reduce_value(v, dist.ReduceOp.SUM)
 
 
 def make_stream_frames(n, w, h, seed0):
@@ -534,7 +548,7 @@ def c5_gba(ws, rank, iters):
         return r, float(np.median(ts))
 
     out = {"c5_problem": "400 KF loop / 20000 pts / 80000 obs, n = 2394"}
-    sharded = ws > 1 and os.environ.get("ORBHIP_C5_SHARDED", "1") == "1"
+    sharded = ws > 1 and os.environ.get("ORBHIP_C5_SHARDED", "1") == "1" and not REHEARSAL
     if sharded:
         import torch.distributed as dist
         uid = [Optimizer.comm_unique_id() if rank == 0 else None]
