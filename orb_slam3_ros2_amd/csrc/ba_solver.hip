@@ -678,9 +678,8 @@ __global__ __launch_bounds__(256) void k_ba_schur_items(const BaArgs* __restrict
     const int it = gt >> 1, h = gt & 1;
     const int lane = threadIdx.x & 63;
     const bool valid = it < a.nitems;   // no early exit: the whole wave meets at the ballot below
-    const int4 wi = valid ? ((const int4*)a.items)[it] : make_int4(0, 0, -1, -1);
-    // (the device form: block (i, j) as i << 16 | j, -1 for a padding item)
-    const int bi = valid && wi.z >= 0 ? (wi.z >> 16) : 0, bj = valid && wi.z >= 0 ? (wi.z & 0xFFFF) : 0;
+    const int4 wi = valid ? ((const int4*)a.items)[it] : make_int4(0, 0, 0, -1);
+    const int bi = valid && wi.z >= 0 ? a.blk_i[wi.z] : 0, bj = valid && wi.z >= 0 ? a.blk_j[wi.z] : 0;
     double Ri[9], Rj[9];
 #pragma unroll
     for (int k = 0; k < 9; k++) { Ri[k] = a.R_lin[9 * bi + k]; Rj[k] = a.R_lin[9 * bj + k]; }
@@ -689,14 +688,14 @@ __global__ __launch_bounds__(256) void k_ba_schur_items(const BaArgs* __restrict
     for (int k = 0; k < 18; k++) s[k] = 0.0;
     const double fx = a.fx, fy = a.fy;
     for (int k = wi.x; k < wi.y; k++) {
-        const int4 pr = ((const int4*)a.blk_pairs)[k];   // {ea, eb, the landmark, 0}
+        const int2 pr = ((const int2*)a.blk_pairs)[k];
         const double4 la = ((const double4*)a.e_lin)[pr.x], lb = ((const double4*)a.e_lin)[pr.y];
         double Di[9];   // in registers either way (a pointer choice would put a local copy in scratch)
         if (a.fused) {
-            dinv_of(a, pr.z, Di);
+            dinv_of(a, a.e_pt[pr.x], Di);
         } else {
 #pragma unroll
-            for (int k = 0; k < 9; k++) Di[k] = a.Dinv[9 * pr.z + k];
+            for (int k = 0; k < 9; k++) Di[k] = a.Dinv[9 * a.e_pt[pr.x] + k];
         }
         // the projection Jacobians of both edges (proj_jac); A and B are used through their structure
         double ja[4], jb[4];
@@ -2354,7 +2353,7 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
             p.o_dag = nR; nR += dag_doubles(p.n);
         }
         p.o_int = ni;
-        ni += (P + 4) + 2 * E + (M + 1) + E + (np_ + 1) + p.ps_edges.size() + 3 * p.nblk + 1 + 2 * p.blk_pairs.size() + 3 +
+        ni += (P + 4) + 2 * E + (M + 1) + E + (np_ + 1) + p.ps_edges.size() + 3 * p.nblk + 1 + p.blk_pairs.size() +
               p.row_first.size() + p.items.size() + p.fin.size() + p.ifin.size() + p.cb_tiles.size() + 8 +
               (p.use_dag ? dag_ints(p.n) + p.dag_task_cap + 4 : 0) + (p.own.size() + 3) / 4 + 1;
     }
@@ -2423,27 +2422,10 @@ int ba_solve_batch(BaWorkspace* ws, const orbhip_ba_problem* const* probs, int B
         a.blk_i = dev(put(p.blk_i.data(), p.nblk));
         a.blk_j = dev(put(p.blk_j.data(), p.nblk));
         a.blk_ptr = dev(put(p.blk_ptr.data(), p.nblk + 1));
-        // r06 (late): the device forms of the pair list and the items carry what k_ba_schur_items
-        // would otherwise fetch one dependent round later: each pair as {ea, eb, landmark, 0} (no
-        // load of e_pt[ea]), each item's block as (i << 16 | j) (no loads of blk_i / blk_j)
-        while ((q - hi) & 3) q++;   // int4 alignment of the pair list
-        {
-            const size_t npr = p.blk_pairs.size() / 2;
-            int* d = q;
-            for (size_t k = 0; k < npr; k++) {
-                const int ea = p.blk_pairs[2 * k], eb = p.blk_pairs[2 * k + 1];
-                d[4 * k] = ea; d[4 * k + 1] = eb; d[4 * k + 2] = pr->edge_point[ea]; d[4 * k + 3] = 0;
-            }
-            a.blk_pairs = dev(d);
-            q += 4 * npr;
-        }
-        a.items = dev(q);   // int4-aligned: the pair list is 4 ints per entry
-        for (size_t k = 0; k < p.items.size(); k += 4) {
-            const int blk = p.items[k + 2];
-            q[k] = p.items[k]; q[k + 1] = p.items[k + 1]; q[k + 3] = p.items[k + 3];
-            q[k + 2] = blk < 0 ? -1 : (p.blk_i[blk] << 16 | p.blk_j[blk]);
-        }
-        q += p.items.size();
+        if ((q - hi) & 1) q++;   // int2 alignment of the pair list
+        a.blk_pairs = dev(put(p.blk_pairs.data(), p.blk_pairs.size()));
+        while ((q - hi) & 3) q++;   // int4 alignment of the items
+        a.items = dev(put(p.items.data(), p.items.size()));
         a.nitems = (int)(p.items.size() / 4);
         a.fin = dev(put(p.fin.data(), p.fin.size()));
         a.nfin = (int)(p.fin.size() / 3);
